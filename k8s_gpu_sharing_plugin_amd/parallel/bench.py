@@ -1,0 +1,189 @@
+"""Multi-rank pod-churn benchmark of the device plugin.
+
+One process per GPU (torchrun). Rank 0 starts the native stub kubelet and the
+real ``amdgpu-device-plugin`` daemon serving exactly the N GPUs of the job
+(``--devices 0..N-1``; real libamd_smi on a GPU box, the amdsmi mock with an
+N x MI355X node model elsewhere). Every rank then plays kubelet for its own
+GPU's devices: each "pod" is GetPreferredAllocation(free, 1) + Allocate(chosen)
+on one persistent gRPC connection, retiring the oldest pod when its share of
+the node is full. One step = ``pods_per_step`` pods per rank. The K timed steps
+run between barrier + device-synchronize brackets; the job reports the max
+over ranks.
+
+After the timed region each rank runs the HIP probe on its GPU (real hardware
+only) to show the allocated device is usable and has the advertised shape.
+"""
+
+import json
+import os
+import time
+
+METRIC = "allocatable amd.com/gpu count + Allocate() p50 latency at 1/2/4/8 MI355X"
+
+# name -> (partition strategy, resource config, description)
+CONFIGS = {
+    "spx-none": ("none", "", "{n}xMI355X SPX, partitionStrategy=none, one amd.com/gpu:1 pod per GPU"),
+    "timeslice4": ("none", "gpu:gpu:4", "{n}xMI355X SPX, time-slice sharing 4 replicas/GPU ({p} concurrent pods)"),
+    "auto-mem": ("none", "gpu:gpu-mem-gb:-1", "{n}xMI355X SPX, auto memory replicas (gpu-mem-gb)"),
+    "cpx-single": ("single", "", "{n}xMI355X CPX, partitionStrategy=single, 8 partitions/GPU"),
+}
+
+
+def _env_int(name, default):
+    try:
+        return int(os.environ.get(name, default))
+    except ValueError:
+        return default
+
+
+def _sync(torch_mod):
+    if torch_mod is not None and torch_mod.cuda.is_available():
+        torch_mod.cuda.synchronize()
+
+
+def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_mock=False,
+        probe=True, log=print):
+    try:
+        import torch
+        import torch.distributed as dist
+    except ImportError:  # pragma: no cover - torch is part of the image
+        torch, dist = None, None
+    from ..models import fixtures
+    from ..utils import harness, native
+
+    rank = _env_int("RANK", 0)
+    world = _env_int("WORLD_SIZE", 1)
+    local_rank = _env_int("LOCAL_RANK", 0)
+    if world != gpus:
+        raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={world}")
+    have_gpu = torch is not None and torch.cuda.is_available()
+    real = have_gpu and not force_mock
+    if world > 1:
+        backend = "nccl" if have_gpu else "gloo"
+        if have_gpu:
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend=backend)
+
+    strategy, rc, desc = CONFIGS[config]
+    daemon = kub = None
+    info = {}
+    try:
+        if rank == 0:
+            d = harness.scratch_dir("adpbench")
+            kub = harness.NativeKubelet(os.path.join(d, "kubelet.sock")).start()
+            args = ["--partition-strategy", strategy, "--devices", ",".join(str(i) for i in range(gpus))]
+            if rc:
+                args += ["--resource-config", rc]
+            mode = "CPX" if config == "cpx-single" else "SPX"
+            fx = None if real else fixtures.node(gpus, mode, memory="NPS2" if mode == "CPX" else "NPS1")
+            daemon = harness.Daemon(d, fx, args=args, real_smi=real,
+                                    env={"DP_HEALTH_POLL_MS": "0", "ADP_LOG_LEVEL": "warn"}).start()
+            reg = kub.wait(lambda e: e.get("event") == "register", 20)
+            devs = kub.wait(lambda e: e.get("event") == "devices", 20)
+            info = {"socket": os.path.join(d, reg["endpoint"]), "resource": reg["resource"],
+                    "allocatable": devs["healthy"], "advertised": devs["total"], "scratch": d}
+        if world > 1:
+            box = [info]
+            dist.broadcast_object_list(box, src=0)
+            info = box[0]
+
+        client = native.ChurnClient(info["socket"], pod_size=1, rank=rank, world=world)
+        client.run(max(1, warmup) * pods_per_step, record=False)
+        client.reset()
+
+        if world > 1:
+            dist.barrier()
+        _sync(torch)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            client.run(pods_per_step, record=True)
+        _sync(torch)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        stats = client.stats()
+        stats["elapsed_s"] = elapsed
+        client.close()
+
+        if real and probe:
+            from ..ops import probe as hip_probe
+            try:
+                stats["probe"] = hip_probe.run(local_rank, 256 << 20, 5)
+            except Exception as e:  # reported, not fatal for the latency metric
+                stats["probe"] = {"error": str(e)}
+
+        everyone = [stats]
+        if world > 1:
+            everyone = [None] * world
+            dist.all_gather_object(everyone, stats)
+        if rank == 0:
+            ms_per_step = max(s["elapsed_s"] for s in everyone) / steps * 1e3
+            p50 = max(s["allocate"]["p50_us"] for s in everyone)
+            total_pods = sum(s["pods"] for s in everyone)
+            result = {
+                "metric": METRIC,
+                "value": round(p50, 2),
+                "unit": "us",
+                "n_gpus": gpus,
+                "steps": steps,
+                "warmup": warmup,
+                "ms_per_step": round(ms_per_step, 4),
+                "higher_is_better": False,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "n/a",
+                "data": ("synthetic pod churn; real libamd_smi on MI355X" if real
+                         else "synthetic pod churn; amdsmi mock node model (no GPU)"),
+                "config": {
+                    "model": desc.format(n=gpus, p=info.get("advertised")),
+                    "global_batch": pods_per_step * world,
+                    "seq_len": None,
+                    "parallelism": f"ranks{world} (one kubelet client per GPU)",
+                    "partition_strategy": strategy,
+                    "resource_config": rc,
+                },
+                "allocatable": info["allocatable"],
+                "advertised": info["advertised"],
+                "resource": info["resource"],
+                "allocate_p99_us": round(max(s["allocate"]["p99_us"] for s in everyone), 2),
+                "preferred_p50_us": round(max(s["preferred"]["p50_us"] for s in everyone), 2),
+                "pod_p50_us": round(max(s["pod"]["p50_us"] for s in everyone), 2),
+                "pods_per_s": round(total_pods / (max(s["elapsed_s"] for s in everyone)), 1),
+                "per_rank": [{k: s[k] for k in ("rank", "rank_devices", "pods", "allocate", "preferred")}
+                             for s in everyone],
+            }
+            probes = [s.get("probe") for s in everyone if s.get("probe")]
+            if probes:
+                result["probe"] = probes
+            return result
+        return None
+    finally:
+        if rank == 0:
+            if daemon is not None:
+                code = daemon.stop()
+                if code not in (0, None):
+                    log(f"daemon exited with {code}:\n{daemon.log()[-3000:]}")
+            if kub is not None:
+                kub.stop()
+        if world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def main(argv=None):
+    import argparse
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pods-per-step", type=int, default=100)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="spx-none")
+    ap.add_argument("--mock", action="store_true", help="use the amdsmi mock even on a GPU box")
+    ap.add_argument("--no-probe", action="store_true")
+    a = ap.parse_args(argv)
+    res = run(a.gpus, a.steps, a.warmup, a.pods_per_step, a.config, a.mock, not a.no_probe)
+    if res is not None:
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,78 @@
+"""Build the native tree (CMake + Ninja) and the HIP probe (hipcc, gfx950).
+
+Everything is built in-tree under ``build/`` so the artefacts travel with the
+repository snapshot to the GPU box.
+"""
+
+import os
+import shutil
+import subprocess
+import sys
+
+from .. import BUILD_DIR, PROBE_DIR, PROBE_LIB, REPO_ROOT
+
+NATIVE_SRC = os.path.join(REPO_ROOT, "native")
+PROBE_SRC = os.path.join(NATIVE_SRC, "probe", "visibility_probe.hip")
+PROTO_SRC = os.path.join(REPO_ROOT, "proto", "deviceplugin", "v1beta1", "api.proto")
+DESCRIPTOR = os.path.join(REPO_ROOT, "build", "api_descriptor.pb")
+
+
+def _run(cmd, **kw):
+    res = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, **kw)
+    if res.returncode != 0:
+        sys.stderr.write(res.stdout[-8000:])
+        raise RuntimeError(f"command failed ({res.returncode}): {' '.join(cmd)}")
+    return res.stdout
+
+
+def build_native(jobs: int = 8, build_type: str = "Release", build_dir: str = BUILD_DIR,
+                 extra_cmake=None) -> str:
+    """Configure (once) and build every native target. Returns the build dir."""
+    generator = ["-G", "Ninja"] if shutil.which("ninja") else []
+    if not os.path.exists(os.path.join(build_dir, "CMakeCache.txt")):
+        os.makedirs(build_dir, exist_ok=True)
+        _run(["cmake", "-S", NATIVE_SRC, "-B", build_dir, f"-DCMAKE_BUILD_TYPE={build_type}",
+              *generator, *(extra_cmake or [])])
+    _run(["cmake", "--build", build_dir, "--", f"-j{jobs}"])
+    return build_dir
+
+
+def build_probe(arch: str = "gfx950") -> str:
+    """Compile the HIP visibility probe into build/probe/libadp_probe.so."""
+    os.makedirs(PROBE_DIR, exist_ok=True)
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    src_mtime = os.path.getmtime(PROBE_SRC)
+    if os.path.exists(PROBE_LIB) and os.path.getmtime(PROBE_LIB) >= src_mtime:
+        return PROBE_LIB
+    _run([hipcc, f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-shared",
+          "-Wall", "-o", PROBE_LIB, PROBE_SRC])
+    return PROBE_LIB
+
+
+def build_descriptor() -> str:
+    """protoc --descriptor_set_out for the kubelet API (used by the grpcio stub)."""
+    if os.path.exists(DESCRIPTOR) and os.path.getmtime(DESCRIPTOR) >= os.path.getmtime(PROTO_SRC):
+        return DESCRIPTOR
+    protoc = shutil.which("protoc")
+    if protoc is None:
+        import torch  # the image ships protoc next to torch's binaries
+        cand = os.path.join(os.path.dirname(torch.__file__), "bin", "protoc")
+        protoc = cand if os.path.exists(cand) else None
+    if protoc is None:
+        raise RuntimeError("protoc not found")
+    os.makedirs(os.path.dirname(DESCRIPTOR), exist_ok=True)
+    _run([protoc, f"--proto_path={os.path.join(REPO_ROOT, 'proto')}",
+          f"--descriptor_set_out={DESCRIPTOR}", "deviceplugin/v1beta1/api.proto"])
+    return DESCRIPTOR
+
+
+def build_all(probe: bool = True) -> None:
+    build_native()
+    build_descriptor()
+    if probe:
+        build_probe()
+
+
+if __name__ == "__main__":
+    build_all(probe="--no-probe" not in sys.argv)
+    print("built:", BUILD_DIR, PROBE_LIB)

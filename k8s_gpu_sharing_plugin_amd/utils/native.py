@@ -1,0 +1,150 @@
+"""ctypes binding to libadp_capi.so: the daemon's own C++ core, called in-process.
+
+Used by the tests to pin the reference's test vectors against the exact code the
+daemon runs, and by the GPU tests to enumerate real hardware through libamd_smi.
+Fails loudly if the library has not been built.
+"""
+
+import ctypes
+import json
+import os
+from functools import lru_cache
+
+from .. import CAPI_LIB
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+@lru_cache(maxsize=1)
+def lib() -> ctypes.CDLL:
+    if not os.path.exists(CAPI_LIB):
+        raise NativeError(f"{CAPI_LIB} not built; run `python -m k8s_gpu_sharing_plugin_amd.utils.build`")
+    so = ctypes.CDLL(CAPI_LIB)
+    for name in ("adp_prioritize", "adp_strip_replicas", "adp_parse_additional_ids",
+                 "adp_parse_resource_config", "adp_best_effort", "adp_snapshot", "adp_plugin_specs"):
+        fn = getattr(so, name)
+        fn.argtypes = [ctypes.c_char_p]
+        fn.restype = ctypes.c_void_p
+    so.adp_health_config.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    so.adp_health_config.restype = ctypes.c_void_p
+    so.adp_proto_roundtrip.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+    so.adp_proto_roundtrip.restype = ctypes.c_void_p
+    so.adp_free.argtypes = [ctypes.c_void_p]
+    so.adp_version.restype = ctypes.c_char_p
+    return so
+
+
+def _take(ptr) -> object:
+    so = lib()
+    try:
+        text = ctypes.string_at(ptr).decode()
+    finally:
+        so.adp_free(ptr)
+    return json.loads(text)
+
+
+def _call(name: str, payload) -> object:
+    arg = payload if isinstance(payload, str) else json.dumps(payload)
+    return _take(getattr(lib(), name)(arg.encode()))
+
+
+def _check(res):
+    if isinstance(res, dict) and "error" in res:
+        raise NativeError(res["error"])
+    return res
+
+
+def version() -> str:
+    return lib().adp_version().decode()
+
+
+def prioritize(available, must_include, size, policy="spread"):
+    """Returns (ids, non_unique) or raises NativeError with the reference's message."""
+    res = _check(_call("adp_prioritize", {"available": list(available), "must_include": list(must_include),
+                                           "size": size, "policy": policy}))
+    return res["ids"], res["non_unique"]
+
+
+def strip_replicas(ids):
+    return _call("adp_strip_replicas", list(ids))
+
+
+def parse_additional_ids(text: str):
+    return _call("adp_parse_additional_ids", text)
+
+
+def health_config(disable_value: str = "", poll_ms: str = ""):
+    return _take(lib().adp_health_config(disable_value.encode(), poll_ms.encode()))
+
+
+def parse_resource_config(text: str):
+    return _check(_call("adp_parse_resource_config", text))
+
+
+def best_effort(parent, scores, available, required, size):
+    return _call("adp_best_effort", {"parent": parent, "scores": scores, "available": available,
+                                      "required": required, "size": size})
+
+
+def snapshot(lib_path: str = "", devices=None, include_card_nodes=False):
+    req = {"lib": lib_path, "include_card_nodes": include_card_nodes}
+    if devices is not None:
+        req["devices"] = list(devices)
+    return _check(_call("adp_snapshot", req))
+
+
+def plugin_specs(lib_path: str = "", strategy="none", resource_config="", devices=None,
+                 auto_unit_mib=1000, id_strategy="uuid"):
+    req = {"lib": lib_path, "strategy": strategy, "resource_config": resource_config,
+           "auto_unit_mib": auto_unit_mib, "id_strategy": id_strategy}
+    if devices is not None:
+        req["devices"] = list(devices)
+    return _check(_call("adp_plugin_specs", req))
+
+
+class ChurnClient:
+    """In-process pod-churn client (native/src/bench/churn.cc) on one plugin socket."""
+
+    def __init__(self, socket_path: str, pod_size=1, rank=0, world=1, preferred=True):
+        so = lib()
+        so.adp_bench_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+        so.adp_bench_open.restype = ctypes.c_void_p
+        so.adp_bench_run.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        so.adp_bench_run.restype = ctypes.c_void_p
+        so.adp_bench_stats.argtypes = [ctypes.c_void_p]
+        so.adp_bench_stats.restype = ctypes.c_void_p
+        so.adp_bench_reset.argtypes = [ctypes.c_void_p]
+        so.adp_bench_close.argtypes = [ctypes.c_void_p]
+        err = ctypes.c_void_p()
+        cfg = json.dumps({"socket": socket_path, "pod_size": pod_size, "rank": rank, "world": world,
+                          "preferred": preferred}).encode()
+        self._h = so.adp_bench_open(cfg, ctypes.byref(err))
+        if not self._h:
+            msg = ctypes.string_at(err.value).decode() if err.value else "unknown error"
+            so.adp_free(err.value)
+            raise NativeError(msg)
+
+    def run(self, pods: int, record: bool = True) -> None:
+        err = lib().adp_bench_run(self._h, pods, 1 if record else 0)
+        if err:
+            msg = ctypes.string_at(err).decode()
+            lib().adp_free(err)
+            raise NativeError(msg)
+
+    def stats(self) -> dict:
+        return _take(lib().adp_bench_stats(self._h))
+
+    def reset(self) -> None:
+        lib().adp_bench_reset(self._h)
+
+    def close(self) -> None:
+        if self._h:
+            lib().adp_bench_close(self._h)
+            self._h = None
+
+
+def proto_roundtrip(msg_type: str, data: bytes) -> bytes:
+    res = _check(_take(lib().adp_proto_roundtrip(msg_type.encode(), data, len(data))))
+    return bytes.fromhex(res["hex"])

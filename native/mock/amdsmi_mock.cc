@@ -1,0 +1,506 @@
+// libamdsmi_mock.so -- a stand-in for libamd_smi.so driven by a JSON fixture.
+//
+// It exports the subset of the amdsmi C ABI that native/src/smi/smi.cc resolves,
+// compiled against the real /opt/rocm/include/amd_smi/amdsmi.h so the struct
+// layouts match. It lets every plugin path (partition strategies on SPX/DPX/QPX/
+// CPX x NPS nodes, 1..8 GPU xGMI meshes, health events, RAS errors, init failure)
+// run on a machine without a GPU -- the reference has no device mock at all
+// (SURVEY §4.1), so this is the backbone of the CPU test matrix.
+//
+// Fixture: $AMDSMI_MOCK_FIXTURE (JSON). Schema (all keys optional except gpus):
+//   { "init_status": 0, "events_supported": true, "lib_version": [26,2,1],
+//     "event_fifo": "<path>", "state_dir": "<path>", "topology": "xgmi"|"pcie",
+//     "numa_bw_penalty": false,
+//     "gpus": [ { "uuid": "...", "bdf": "0000:0c:00.0", "numa": 0, "vram_mib": 294896,
+//                 "num_cu": 256, "xcd": 8, "market_name": "...",
+//                 "compute_partition": "SPX"|"DPX"|"QPX"|"CPX", "memory_partition": "NPS1",
+//                 "partitions": N, "partition_uuids": "distinct"|"shared",
+//                 "render_minor": 128, "card_minor": 0, "xgmi_links_down": 0 } ] }
+// Runtime injection:
+//   event FIFO lines: "<gpu>[:<partition>] <event-type> [message]"
+//   state_dir files:  gpu<i>.ecc (uncorrectable count), gpu<i>.dead (device gone)
+#include <amd_smi/amdsmi.h>
+#include <fcntl.h>
+#include <poll.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <json.hpp>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+namespace {
+
+using nlohmann::json;
+
+struct MockProc {
+  int gpu = 0;
+  int part = 0;
+  std::string uuid;
+  uint64_t bdf = 0;
+  uint32_t render = 0;
+  uint32_t card = 0;
+  int numa = -1;
+  uint64_t vram_mib = 0;
+  uint32_t num_cu = 0;
+  uint16_t xcd = 0;
+  std::string market;
+  std::string cmode, mmode;
+  int links_down = 0;
+  bool evt_init = false;
+  uint64_t evt_mask = 0;
+};
+
+struct MockGpu {
+  std::vector<MockProc*> procs;
+};
+
+struct State {
+  bool loaded = false;
+  int init_status = 0;
+  bool events_supported = true;
+  uint32_t ver[3] = {26, 2, 1};
+  std::string topology = "xgmi";
+  std::string event_fifo, state_dir;
+  int fifo_fd = -1;
+  std::string fifo_buf;
+  std::vector<std::unique_ptr<MockProc>> procs;
+  std::vector<MockGpu> gpus;
+};
+
+State* g = nullptr;
+std::mutex g_mu;
+
+uint64_t ParseBdf(const std::string& s) {
+  unsigned dom = 0, bus = 0, dev = 0, fn = 0;
+  sscanf(s.c_str(), "%x:%x:%x.%x", &dom, &bus, &dev, &fn);
+  amdsmi_bdf_t b;
+  b.as_uint = 0;
+  b.domain_number = dom;
+  b.bus_number = bus;
+  b.device_number = dev;
+  b.function_number = fn;
+  return b.as_uint;
+}
+
+int DefaultPartitions(const std::string& mode) {
+  if (mode == "DPX") return 2;
+  if (mode == "TPX") return 3;
+  if (mode == "QPX") return 4;
+  if (mode == "CPX") return 8;
+  return 1;
+}
+
+bool Load() {
+  if (g && g->loaded) return true;
+  if (!g) g = new State();
+  const char* path = getenv("AMDSMI_MOCK_FIXTURE");
+  if (!path) {
+    fprintf(stderr, "amdsmi_mock: AMDSMI_MOCK_FIXTURE not set\n");
+    return false;
+  }
+  std::ifstream in(path);
+  if (!in) {
+    fprintf(stderr, "amdsmi_mock: cannot open %s\n", path);
+    return false;
+  }
+  json j;
+  try {
+    in >> j;
+  } catch (const std::exception& e) {
+    fprintf(stderr, "amdsmi_mock: bad fixture %s: %s\n", path, e.what());
+    return false;
+  }
+  g->init_status = j.value("init_status", 0);
+  g->events_supported = j.value("events_supported", true);
+  g->topology = j.value("topology", std::string("xgmi"));
+  g->event_fifo = j.value("event_fifo", std::string());
+  g->state_dir = j.value("state_dir", std::string());
+  if (const char* e = getenv("AMDSMI_MOCK_EVENT_FIFO")) g->event_fifo = e;
+  if (const char* e = getenv("AMDSMI_MOCK_STATE_DIR")) g->state_dir = e;
+  if (j.count("lib_version")) {
+    for (int i = 0; i < 3; ++i) g->ver[i] = j["lib_version"][i].get<uint32_t>();
+  }
+  int gi = 0;
+  for (const auto& jg : j["gpus"]) {
+    MockGpu mg;
+    std::string cmode = jg.value("compute_partition", std::string("SPX"));
+    std::string mmode = jg.value("memory_partition", std::string("NPS1"));
+    int nparts = jg.value("partitions", DefaultPartitions(cmode));
+    if (nparts < 1) nparts = 1;
+    char defuuid[64];
+    snprintf(defuuid, sizeof(defuuid), "%08x-0000-1000-80c0-%012llx", 0x75a30000u + gi,
+             static_cast<unsigned long long>(0xbf9907890000ull + gi));
+    std::string uuid = jg.value("uuid", std::string(defuuid));
+    char defbdf[32];
+    snprintf(defbdf, sizeof(defbdf), "0000:%02x:00.0", 0x0c + 0x20 * gi);
+    uint64_t bdf = ParseBdf(jg.value("bdf", std::string(defbdf)));
+    uint32_t render = jg.value("render_minor", 128u + 8u * gi);
+    uint32_t card = jg.value("card_minor", 8u * gi);
+    uint64_t vram = jg.value("vram_mib", static_cast<uint64_t>(294896));
+    uint32_t ncu = jg.value("num_cu", 256u);
+    uint16_t xcd = static_cast<uint16_t>(jg.value("xcd", 8));
+    bool shared = jg.value("partition_uuids", std::string("distinct")) == "shared";
+    for (int p = 0; p < nparts; ++p) {
+      auto mp = std::make_unique<MockProc>();
+      mp->gpu = gi;
+      mp->part = p;
+      mp->uuid = uuid;
+      if (p > 0 && !shared) {
+        // Distinct per-partition UUID: encode the partition in the 3rd group.
+        char buf[16];
+        snprintf(buf, sizeof(buf), "%x", p);
+        if (mp->uuid.size() > 15) mp->uuid[15] = buf[0];
+      }
+      amdsmi_bdf_t b;
+      b.as_uint = bdf;
+      b.function_number = p & 7;
+      mp->bdf = b.as_uint;
+      mp->render = render + p;
+      mp->card = card + p;
+      mp->numa = jg.value("numa", gi < 4 ? 0 : 1);
+      // In a partitioned mode amdsmi reports each partition's share of the pool.
+      mp->vram_mib = nparts > 1 ? vram / nparts : vram;
+      mp->num_cu = nparts > 1 ? ncu / nparts : ncu;
+      mp->xcd = nparts > 1 ? static_cast<uint16_t>(xcd / nparts ? xcd / nparts : 1) : xcd;
+      mp->market = jg.value("market_name", std::string("AMD Instinct MI355X"));
+      mp->cmode = cmode;
+      mp->mmode = mmode;
+      mp->links_down = jg.value("xgmi_links_down", 0);
+      mg.procs.push_back(mp.get());
+      g->procs.push_back(std::move(mp));
+    }
+    g->gpus.push_back(mg);
+    ++gi;
+  }
+  g->loaded = true;
+  return true;
+}
+
+MockProc* P(amdsmi_processor_handle h) {
+  if (!g) return nullptr;
+  for (auto& p : g->procs)
+    if (p.get() == h) return p.get();
+  return nullptr;
+}
+
+bool Dead(const MockProc* p) {
+  if (!g || g->state_dir.empty()) return false;
+  struct stat st;
+  std::string f = g->state_dir + "/gpu" + std::to_string(p->gpu) + ".dead";
+  return stat(f.c_str(), &st) == 0;
+}
+
+#define GET_PROC(h)                                   \
+  std::lock_guard<std::mutex> lk(g_mu);               \
+  MockProc* p = P(h);                                 \
+  if (!p) return AMDSMI_STATUS_INVAL;                 \
+  if (Dead(p)) return AMDSMI_STATUS_NOT_FOUND;
+
+void CopyStr(char* dst, size_t len, const std::string& s) {
+  if (!len) return;
+  size_t n = s.size() < len - 1 ? s.size() : len - 1;
+  memcpy(dst, s.data(), n);
+  dst[n] = 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+amdsmi_status_t amdsmi_init(uint64_t) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!Load()) return AMDSMI_STATUS_INIT_ERROR;
+  return static_cast<amdsmi_status_t>(g->init_status);
+}
+
+amdsmi_status_t amdsmi_shut_down(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g) {
+    if (g->fifo_fd >= 0) close(g->fifo_fd);
+    delete g;
+    g = nullptr;
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_lib_version(amdsmi_version_t* v) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g || !v) return AMDSMI_STATUS_INVAL;
+  v->major = g->ver[0];
+  v->minor = g->ver[1];
+  v->release = g->ver[2];
+  v->build = "mock";
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_status_code_to_string(amdsmi_status_t status, const char** s) {
+  static thread_local char buf[64];
+  snprintf(buf, sizeof(buf), "AMDSMI_MOCK_STATUS_%d", static_cast<int>(status));
+  *s = buf;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_socket_handles(uint32_t* count, amdsmi_socket_handle* out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g || !count) return AMDSMI_STATUS_INVAL;
+  uint32_t n = static_cast<uint32_t>(g->gpus.size());
+  if (!out) { *count = n; return AMDSMI_STATUS_SUCCESS; }
+  uint32_t m = *count < n ? *count : n;
+  for (uint32_t i = 0; i < m; ++i) out[i] = &g->gpus[i];
+  *count = m;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle sock, uint32_t* count,
+                                             amdsmi_processor_handle* out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g || !count) return AMDSMI_STATUS_INVAL;
+  MockGpu* mg = static_cast<MockGpu*>(sock);
+  uint32_t n = static_cast<uint32_t>(mg->procs.size());
+  if (!out) { *count = n; return AMDSMI_STATUS_SUCCESS; }
+  uint32_t m = *count < n ? *count : n;
+  for (uint32_t i = 0; i < m; ++i) out[i] = mg->procs[i];
+  *count = m;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_processor_type(amdsmi_processor_handle h, processor_type_t* t) {
+  GET_PROC(h);
+  *t = AMDSMI_PROCESSOR_TYPE_AMD_GPU;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_device_uuid(amdsmi_processor_handle h, unsigned int* len,
+                                           char* uuid) {
+  GET_PROC(h);
+  if (*len < p->uuid.size() + 1) return AMDSMI_STATUS_INSUFFICIENT_SIZE;
+  CopyStr(uuid, *len, p->uuid);
+  *len = static_cast<unsigned>(p->uuid.size());
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_device_bdf(amdsmi_processor_handle h, amdsmi_bdf_t* bdf) {
+  GET_PROC(h);
+  bdf->as_uint = p->bdf;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_enumeration_info(amdsmi_processor_handle h,
+                                                amdsmi_enumeration_info_t* info) {
+  GET_PROC(h);
+  memset(info, 0, sizeof(*info));
+  info->drm_render = p->render;
+  info->drm_card = p->card;
+  uint32_t idx = 0;
+  for (auto& q : g->procs) {
+    if (q.get() == p) break;
+    ++idx;
+  }
+  info->hsa_id = idx + 1;
+  info->hip_id = idx;
+  CopyStr(info->hip_uuid, sizeof(info->hip_uuid), "GPU-" + p->uuid);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_topo_numa_affinity(amdsmi_processor_handle h, int32_t* numa) {
+  GET_PROC(h);
+  *numa = p->numa;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_vram_info(amdsmi_processor_handle h, amdsmi_vram_info_t* info) {
+  GET_PROC(h);
+  memset(info, 0, sizeof(*info));
+  info->vram_type = AMDSMI_VRAM_TYPE_HBM3E;
+  CopyStr(info->vram_vendor, sizeof(info->vram_vendor), "MOCK");
+  info->vram_size = p->vram_mib;
+  info->vram_bit_width = 8192;
+  info->vram_max_bandwidth = 8192;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_memory_total(amdsmi_processor_handle h, amdsmi_memory_type_t,
+                                            uint64_t* total) {
+  GET_PROC(h);
+  *total = p->vram_mib << 20;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_compute_partition(amdsmi_processor_handle h, char* buf,
+                                                 uint32_t len) {
+  GET_PROC(h);
+  CopyStr(buf, len, p->cmode);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_memory_partition(amdsmi_processor_handle h, char* buf,
+                                                uint32_t len) {
+  GET_PROC(h);
+  CopyStr(buf, len, p->mmode);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_kfd_info(amdsmi_processor_handle h, amdsmi_kfd_info_t* info) {
+  GET_PROC(h);
+  memset(info, 0, sizeof(*info));
+  info->kfd_id = 1000 + p->gpu * 16 + p->part;
+  info->node_id = 2 + p->gpu * 8 + p->part;
+  info->current_partition_id = p->part;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_asic_info(amdsmi_processor_handle h, amdsmi_asic_info_t* info) {
+  GET_PROC(h);
+  memset(info, 0, sizeof(*info));
+  CopyStr(info->market_name, sizeof(info->market_name), p->market);
+  info->vendor_id = 0x1002;
+  info->device_id = 0x75a3;
+  info->num_of_compute_units = p->num_cu;
+  info->oam_id = p->gpu;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_xcd_counter(amdsmi_processor_handle h, uint16_t* xcd) {
+  GET_PROC(h);
+  *xcd = p->xcd;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_topo_get_link_type(amdsmi_processor_handle a, amdsmi_processor_handle b,
+                                          uint64_t* hops, amdsmi_link_type_t* type) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  MockProc* pa = P(a);
+  MockProc* pb = P(b);
+  if (!pa || !pb) return AMDSMI_STATUS_INVAL;
+  if (pa->gpu == pb->gpu) {
+    *hops = 0;
+    *type = AMDSMI_LINK_TYPE_INTERNAL;
+  } else if (g->topology == "pcie") {
+    *hops = pa->numa == pb->numa ? 2 : 3;
+    *type = AMDSMI_LINK_TYPE_PCIE;
+  } else {
+    *hops = 1;
+    *type = AMDSMI_LINK_TYPE_XGMI;
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_topo_get_link_weight(amdsmi_processor_handle a, amdsmi_processor_handle b,
+                                            uint64_t* w) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  MockProc* pa = P(a);
+  MockProc* pb = P(b);
+  if (!pa || !pb) return AMDSMI_STATUS_INVAL;
+  if (pa->gpu == pb->gpu) *w = 0;
+  else if (g->topology == "pcie") *w = pa->numa == pb->numa ? 20 : 40;
+  else *w = 15;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_xgmi_link_status(amdsmi_processor_handle h,
+                                                amdsmi_xgmi_link_status_t* s) {
+  GET_PROC(h);
+  memset(s, 0, sizeof(*s));
+  s->total_links = 8;
+  for (int i = 0; i < 8; ++i)
+    s->status[i] = i < p->links_down ? AMDSMI_XGMI_LINK_DOWN : AMDSMI_XGMI_LINK_UP;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_total_ecc_count(amdsmi_processor_handle h,
+                                               amdsmi_error_count_t* ec) {
+  GET_PROC(h);
+  memset(ec, 0, sizeof(*ec));
+  if (!g->state_dir.empty()) {
+    std::ifstream f(g->state_dir + "/gpu" + std::to_string(p->gpu) + ".ecc");
+    uint64_t v = 0;
+    if (f >> v) ec->uncorrectable_count = v;
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_init_gpu_event_notification(amdsmi_processor_handle h) {
+  GET_PROC(h);
+  if (!g->events_supported) return AMDSMI_STATUS_NOT_SUPPORTED;
+  p->evt_init = true;
+  if (g->fifo_fd < 0 && !g->event_fifo.empty()) {
+    // O_RDWR keeps a writer open so poll() blocks instead of reporting HUP.
+    g->fifo_fd = open(g->event_fifo.c_str(), O_RDWR | O_NONBLOCK | O_CLOEXEC);
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_set_gpu_event_notification_mask(amdsmi_processor_handle h, uint64_t mask) {
+  GET_PROC(h);
+  if (!p->evt_init) return AMDSMI_STATUS_INIT_ERROR;
+  p->evt_mask = mask;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_stop_gpu_event_notification(amdsmi_processor_handle h) {
+  GET_PROC(h);
+  p->evt_init = false;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_event_notification(int timeout_ms, uint32_t* num,
+                                                  amdsmi_evt_notification_data_t* data) {
+  int fd;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g) return AMDSMI_STATUS_INIT_ERROR;
+    fd = g->fifo_fd;
+  }
+  if (fd < 0) {
+    if (timeout_ms > 0) usleep(static_cast<useconds_t>(timeout_ms) * 1000);
+    *num = 0;
+    return AMDSMI_STATUS_NO_DATA;
+  }
+  pollfd pfd{fd, POLLIN, 0};
+  int r = poll(&pfd, 1, timeout_ms);
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g) return AMDSMI_STATUS_INIT_ERROR;
+  if (r > 0) {
+    char buf[4096];
+    ssize_t n;
+    while ((n = read(fd, buf, sizeof(buf))) > 0) g->fifo_buf.append(buf, n);
+  }
+  uint32_t cap = *num, got = 0;
+  size_t nl;
+  while (got < cap && (nl = g->fifo_buf.find('\n')) != std::string::npos) {
+    std::string line = g->fifo_buf.substr(0, nl);
+    g->fifo_buf.erase(0, nl + 1);
+    std::istringstream ls(line);
+    std::string target;
+    int type = 0;
+    if (!(ls >> target >> type)) continue;
+    std::string msg;
+    std::getline(ls, msg);
+    int gpu = atoi(target.c_str());
+    int part = 0;
+    size_t colon = target.find(':');
+    if (colon != std::string::npos) part = atoi(target.c_str() + colon + 1);
+    MockProc* hit = nullptr;
+    for (auto& p : g->procs)
+      if (p->gpu == gpu && p->part == part) hit = p.get();
+    if (!hit || !hit->evt_init) continue;
+    if (!(hit->evt_mask & AMDSMI_EVENT_MASK_FROM_INDEX(type))) continue;
+    memset(&data[got], 0, sizeof(data[got]));
+    data[got].processor_handle = hit;
+    data[got].event = static_cast<amdsmi_evt_notification_type_t>(type);
+    CopyStr(data[got].message, sizeof(data[got].message), msg.empty() ? "mock event" : msg);
+    ++got;
+  }
+  *num = got;
+  return got ? AMDSMI_STATUS_SUCCESS : AMDSMI_STATUS_NO_DATA;
+}
+
+}  // extern "C"

@@ -1,0 +1,210 @@
+// HIP visibility / partition probe for gfx950 (MI355X).
+//
+// Run inside (or on behalf of) a container after Allocate() to prove that the
+// device nodes the plugin handed out give a working GPU with the shape the
+// plugin advertised -- the MI355X analogue of the reference's PyTorch smoke pod
+// (examples/pods/pod1-shared-pytorch.yml) and SHARED_GPU_TUTORIAL.md's manual
+// `nvidia-smi -L` check.
+//
+// What it measures, per HIP device:
+//   * census: a launch of 8 workgroups per CU records each workgroup's
+//     hardware placement -- XCC id (s_getreg HW_REG_XCC_ID) and SE/SH/CU id
+//     (HW_REG_HW_ID) -- so the host counts the XCDs and CUs that actually run
+//     work. SPX must show 8 XCDs / 256 CUs; a CPX partition 1 XCD / 32 CUs.
+//   * HBM bandwidth: a 16-byte-per-lane streaming copy (grid-stride, 8
+//     workgroups x 256 threads per CU, dwordx4 loads/stores) timed with events;
+//     a partition should see its share of the ~6.3 TB/s a full MI355X sustains.
+//   * correctness: the copied buffer is checksummed on the device (wave64
+//     shuffle reduction + one 64-bit atomic per workgroup) against the closed
+//     form, so a broken mapping cannot pass silently.
+//
+// C ABI (loaded with ctypes by k8s_gpu_sharing_plugin_amd/ops/probe.py):
+//   int adp_probe_device_count(void);
+//   int adp_probe_list(char* out, int len);                       // JSON array
+//   int adp_probe_run(int device, unsigned long long bytes, int iters, char* out, int len);
+// Return 0 on success, a hipError_t (>0) on failure; `out` holds JSON either way.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <set>
+#include <string>
+#include <vector>
+
+namespace {
+
+__device__ __forceinline__ uint32_t ReadXccId() {
+  uint32_t v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 0xf;
+}
+
+__device__ __forceinline__ uint32_t ReadHwId() {
+  uint32_t v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
+  return v;
+}
+
+// One record per workgroup: xcc[3:0] << 16 | se/sh/cu bits of HW_ID [15:8].
+__global__ void __launch_bounds__(64) CensusKernel(uint32_t* out) {
+  if (threadIdx.x == 0) {
+    uint32_t xcc = ReadXccId();
+    uint32_t hw = ReadHwId();
+    out[blockIdx.x] = (xcc << 16) | ((hw >> 8) & 0xff);
+  }
+}
+
+__global__ void __launch_bounds__(256) FillKernel(uint4* p, size_t n) {
+  size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint32_t b = static_cast<uint32_t>(i * 4);
+    p[i] = make_uint4(b, b + 1, b + 2, b + 3);
+  }
+}
+
+__global__ void __launch_bounds__(256) CopyKernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                  size_t n) {
+  size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  // Two independent 16-byte loads in flight per lane per iteration.
+  for (; i + stride < n; i += 2 * stride) {
+    uint4 a = src[i];
+    uint4 b = src[i + stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+  }
+  if (i < n) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(256) SumKernel(const uint4* __restrict__ p, size_t n,
+                                                 unsigned long long* total) {
+  size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  unsigned long long acc = 0;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint4 v = p[i];
+    acc += static_cast<unsigned long long>(v.x) + v.y + v.z + v.w;
+  }
+  // wave64 reduction
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+  __shared__ unsigned long long partial[4];
+  int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) partial[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long s = partial[0] + partial[1] + partial[2] + partial[3];
+    atomicAdd(total, s);
+  }
+}
+
+int Fail(char* out, int len, hipError_t e, const char* where) {
+  snprintf(out, len, "{\"error\": \"%s: %s\"}", where, hipGetErrorString(e));
+  return static_cast<int>(e) ? static_cast<int>(e) : 1;
+}
+
+#define HIP_TRY(expr)                                   \
+  do {                                                  \
+    hipError_t _e = (expr);                             \
+    if (_e != hipSuccess) return Fail(out, len, _e, #expr); \
+  } while (0)
+
+}  // namespace
+
+extern "C" int adp_probe_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return -1;
+  return n;
+}
+
+extern "C" int adp_probe_list(char* out, int len) {
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  std::string s = "[";
+  for (int d = 0; d < n; ++d) {
+    hipDeviceProp_t p;
+    HIP_TRY(hipGetDeviceProperties(&p, d));
+    char buf[512];
+    snprintf(buf, sizeof(buf),
+             "%s{\"device\": %d, \"name\": \"%s\", \"arch\": \"%s\", \"pci\": \"%04x:%02x:%02x.0\", "
+             "\"cus\": %d, \"total_mem_mib\": %zu}",
+             d ? ", " : "", d, p.name, p.gcnArchName, p.pciDomainID, p.pciBusID, p.pciDeviceID,
+             p.multiProcessorCount, static_cast<size_t>(p.totalGlobalMem >> 20));
+    s += buf;
+  }
+  s += "]";
+  snprintf(out, len, "%s", s.c_str());
+  return 0;
+}
+
+extern "C" int adp_probe_run(int device, unsigned long long bytes, int iters, char* out, int len) {
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  const int cus = prop.multiProcessorCount;
+
+  // --- census ---
+  const int census_blocks = cus * 8;
+  uint32_t* d_census = nullptr;
+  HIP_TRY(hipMalloc(&d_census, census_blocks * sizeof(uint32_t)));
+  hipLaunchKernelGGL(CensusKernel, dim3(census_blocks), dim3(64), 0, 0, d_census);
+  HIP_TRY(hipGetLastError());
+  std::vector<uint32_t> census(census_blocks);
+  HIP_TRY(hipMemcpy(census.data(), d_census, census_blocks * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipFree(d_census));
+  std::set<uint32_t> xccs, cu_keys;
+  for (uint32_t r : census) {
+    xccs.insert(r >> 16);
+    cu_keys.insert(r);
+  }
+
+  // --- bandwidth + checksum ---
+  size_t n = bytes / sizeof(uint4);
+  if (n < 1024) n = 1024;
+  if (iters < 1) iters = 1;
+  uint4 *src = nullptr, *dst = nullptr;
+  unsigned long long* d_sum = nullptr;
+  HIP_TRY(hipMalloc(&src, n * sizeof(uint4)));
+  HIP_TRY(hipMalloc(&dst, n * sizeof(uint4)));
+  HIP_TRY(hipMalloc(&d_sum, sizeof(unsigned long long)));
+  const int blocks = cus * 8;
+  hipLaunchKernelGGL(FillKernel, dim3(blocks), dim3(256), 0, 0, src, n);
+  hipLaunchKernelGGL(CopyKernel, dim3(blocks), dim3(256), 0, 0, src, dst, n);  // warm-up
+  HIP_TRY(hipGetLastError());
+  hipEvent_t e0, e1;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i)
+    hipLaunchKernelGGL(CopyKernel, dim3(blocks), dim3(256), 0, 0, src, dst, n);
+  HIP_TRY(hipEventRecord(e1, 0));
+  HIP_TRY(hipEventSynchronize(e1));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  HIP_TRY(hipMemset(d_sum, 0, sizeof(unsigned long long)));
+  hipLaunchKernelGGL(SumKernel, dim3(blocks), dim3(256), 0, 0, dst, n, d_sum);
+  HIP_TRY(hipGetLastError());
+  unsigned long long got = 0;
+  HIP_TRY(hipMemcpy(&got, d_sum, sizeof(got), hipMemcpyDeviceToHost));
+  // sum of the uint32 sequence 0..4n-1, each term taken mod 2^32
+  unsigned long long want = 0;
+  {
+    unsigned long long m = 4ull * n;
+    // terms are < 2^32 as long as 4n <= 2^32 (bytes <= 16 GiB); closed form otherwise too large
+    want = (m % 2 == 0) ? (m / 2) * (m - 1) : m * ((m - 1) / 2);
+  }
+  HIP_TRY(hipEventDestroy(e0));
+  HIP_TRY(hipEventDestroy(e1));
+  HIP_TRY(hipFree(src));
+  HIP_TRY(hipFree(dst));
+  HIP_TRY(hipFree(d_sum));
+  double gbps = ms > 0 ? (2.0 * n * sizeof(uint4) * iters) / (ms * 1e-3) / 1e9 : 0.0;
+  snprintf(out, len,
+           "{\"device\": %d, \"name\": \"%s\", \"arch\": \"%s\", \"pci\": \"%04x:%02x:%02x.0\", "
+           "\"cus\": %d, \"total_mem_mib\": %zu, \"xccs_seen\": %zu, \"cus_seen\": %zu, "
+           "\"copy_bytes\": %zu, \"copy_iters\": %d, \"copy_ms\": %.4f, \"hbm_copy_gbps\": %.1f, "
+           "\"checksum_ok\": %s}",
+           device, prop.name, prop.gcnArchName, prop.pciDomainID, prop.pciBusID, prop.pciDeviceID, cus,
+           static_cast<size_t>(prop.totalGlobalMem >> 20), xccs.size(), cu_keys.size(),
+           n * sizeof(uint4), iters, ms, gbps, got == want ? "true" : "false");
+  return got == want ? 0 : 2;
+}

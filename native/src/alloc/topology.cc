@@ -1,0 +1,215 @@
+#include "alloc/topology.h"
+
+#include <algorithm>
+#include <climits>
+#include <functional>
+#include <map>
+#include <set>
+
+namespace adp::alloc {
+
+using inventory::LinkClass;
+
+int PairScore(const inventory::Snapshot& snap, int a, int b) {
+  if (a == b) return 1000;
+  const auto& ga = snap.gpus[a];
+  const auto& gb = snap.gpus[b];
+  int score = (ga.numa >= 0 && ga.numa == gb.numa) ? 20 : 10;
+  switch (snap.Link(a, b)) {
+    case LinkClass::kSame: return 1000;
+    case LinkClass::kXgmi: {
+      uint64_t hops = std::max<uint64_t>(1, snap.Hops(a, b));
+      score += static_cast<int>(100 / hops);
+      break;
+    }
+    case LinkClass::kPcieSameNuma:
+    case LinkClass::kPcieCrossNuma:
+    case LinkClass::kUnknown:
+      break;
+  }
+  score -= 10 * (ga.xgmi_links_down + gb.xgmi_links_down);
+  return score;
+}
+
+DeviceGraph::DeviceGraph(const inventory::Snapshot& snap, const std::vector<DeviceRef>& devices)
+    : n_(static_cast<int>(devices.size())), parent_(devices.size()), score_(devices.size() * devices.size()) {
+  for (int i = 0; i < n_; ++i) parent_[i] = devices[i].gpu;
+  for (int i = 0; i < n_; ++i)
+    for (int j = 0; j < n_; ++j)
+      score_[i * n_ + j] = (i == j) ? 0 : PairScore(snap, devices[i].gpu, devices[j].gpu);
+}
+
+DeviceGraph::DeviceGraph(std::vector<int> parent, std::vector<int> scores)
+    : n_(static_cast<int>(parent.size())), parent_(std::move(parent)), score_(std::move(scores)) {}
+
+namespace {
+
+// Calls fn(mask) for every subset of `bits` (list of bit positions) of size s.
+void ForEachCombination(const std::vector<int>& bits, int s, const std::function<void(uint32_t)>& fn) {
+  int n = static_cast<int>(bits.size());
+  if (s < 0 || s > n) return;
+  if (s == 0) { fn(0); return; }
+  std::vector<int> idx(s);
+  for (int i = 0; i < s; ++i) idx[i] = i;
+  while (true) {
+    uint32_t m = 0;
+    for (int i : idx) m |= 1u << bits[i];
+    fn(m);
+    int i = s - 1;
+    while (i >= 0 && idx[i] == n - s + i) --i;
+    if (i < 0) return;
+    ++idx[i];
+    for (int j = i + 1; j < s; ++j) idx[j] = idx[j - 1] + 1;
+  }
+}
+
+std::vector<int> Bits(uint32_t mask) {
+  std::vector<int> out;
+  for (int i = 0; mask; ++i, mask >>= 1)
+    if (mask & 1) out.push_back(i);
+  return out;
+}
+
+std::vector<int> ExactSearch(const DeviceGraph& g, const std::vector<int>& avail,
+                             const std::vector<int>& required, int k) {
+  int m = static_cast<int>(avail.size());
+  int r = m % k;
+  auto set_score = [&](uint32_t mask) {
+    auto b = Bits(mask);
+    int s = 0;
+    for (size_t i = 0; i < b.size(); ++i)
+      for (size_t j = i + 1; j < b.size(); ++j) s += g.Score(avail[b[i]], avail[b[j]]);
+    return s;
+  };
+  std::vector<int> memo(1u << m, INT_MIN);
+  std::function<int(uint32_t)> f = [&](uint32_t mask) -> int {
+    if (!mask) return 0;
+    if (memo[mask] != INT_MIN) return memo[mask];
+    int low = __builtin_ctz(mask);
+    uint32_t rest = mask & ~(1u << low);
+    int cnt = __builtin_popcount(mask);
+    int best = INT_MIN / 2;
+    std::vector<int> sizes;
+    if (cnt >= k) sizes.push_back(k);
+    if (r > 0 && cnt % k == r) sizes.push_back(r);
+    auto rb = Bits(rest);
+    for (int sz : sizes) {
+      ForEachCombination(rb, sz - 1, [&](uint32_t sub) {
+        uint32_t grp = sub | (1u << low);
+        int v = set_score(grp) + f(mask & ~grp);
+        if (v > best) best = v;
+      });
+    }
+    memo[mask] = best;
+    return best;
+  };
+
+  uint32_t full = (m == 32) ? 0xffffffffu : ((1u << m) - 1);
+  uint32_t req = 0;
+  for (int d : required)
+    for (int i = 0; i < m; ++i)
+      if (avail[i] == d) req |= 1u << i;
+  auto free_bits = Bits(full & ~req);
+  int need = k - __builtin_popcount(req);
+  uint32_t best_grp = 0;
+  int best_total = INT_MIN, best_set = INT_MIN;
+  ForEachCombination(free_bits, need, [&](uint32_t sub) {
+    uint32_t grp = sub | req;
+    int s = set_score(grp);
+    int total = s + f(full & ~grp);
+    if (total > best_total || (total == best_total && s > best_set)) {
+      best_total = total;
+      best_set = s;
+      best_grp = grp;
+    }
+  });
+  std::vector<int> out;
+  for (int i : Bits(best_grp)) out.push_back(avail[i]);
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+std::vector<int> Hierarchical(const DeviceGraph& g, const std::vector<int>& avail,
+                              const std::vector<int>& required, int size) {
+  std::set<int> chosen(required.begin(), required.end());
+  std::map<int, std::vector<int>> remaining;  // parent -> unchosen available devices
+  std::map<int, int> rep;                     // parent -> representative device
+  for (int d : avail) {
+    rep.emplace(g.parent(d), d);
+    if (!chosen.count(d)) remaining[g.parent(d)].push_back(d);
+  }
+  std::set<int> parents;
+  for (int d : required) parents.insert(g.parent(d));
+  int need = size - static_cast<int>(chosen.size());
+
+  auto take = [&](int p) {
+    auto& v = remaining[p];
+    while (need > 0 && !v.empty()) {
+      chosen.insert(v.front());
+      v.erase(v.begin());
+      --need;
+    }
+    parents.insert(p);
+  };
+
+  // 1. Finish on the GPUs the required devices already occupy (most room first).
+  std::vector<int> req_parents(parents.begin(), parents.end());
+  std::stable_sort(req_parents.begin(), req_parents.end(),
+                   [&](int a, int b) { return remaining[a].size() > remaining[b].size(); });
+  for (int p : req_parents) take(p);
+
+  // 2. Grow: affinity to the GPUs already chosen, then best fit, then index.
+  while (need > 0) {
+    int best = -1;
+    long best_aff = LONG_MIN;
+    bool best_fits = false;
+    size_t best_room = 0;
+    for (auto& [p, v] : remaining) {
+      if (v.empty() || parents.count(p)) continue;
+      long aff = 0;
+      for (int q : parents) aff += g.Score(rep[p], rep[q]);
+      bool fits = v.size() >= static_cast<size_t>(need);
+      bool better;
+      if (best < 0) better = true;
+      else if (aff != best_aff) better = aff > best_aff;
+      else if (fits != best_fits) better = fits;
+      else if (fits) better = v.size() < best_room;   // best fit: tightest hole
+      else better = v.size() > best_room;             // else: biggest chunk first
+      if (better) {
+        best = p;
+        best_aff = aff;
+        best_fits = fits;
+        best_room = v.size();
+      }
+    }
+    if (best < 0) return {};
+    take(best);
+  }
+  return std::vector<int>(chosen.begin(), chosen.end());
+}
+
+}  // namespace
+
+std::vector<int> BestEffortAllocate(const DeviceGraph& g, const std::vector<int>& available,
+                                    const std::vector<int>& required, int size) {
+  if (size <= 0) return {};
+  std::vector<int> avail(available);
+  std::sort(avail.begin(), avail.end());
+  avail.erase(std::unique(avail.begin(), avail.end()), avail.end());
+  std::vector<int> req(required);
+  std::sort(req.begin(), req.end());
+  req.erase(std::unique(req.begin(), req.end()), req.end());
+  if (static_cast<int>(avail.size()) < size || static_cast<int>(req.size()) > size) return {};
+  for (int d : req)
+    if (!std::binary_search(avail.begin(), avail.end(), d)) return {};
+  for (int d : avail)
+    if (d < 0 || d >= g.size()) return {};
+
+  std::set<int> parents;
+  for (int d : avail) parents.insert(g.parent(d));
+  bool distinct = parents.size() == avail.size();
+  if (distinct && avail.size() <= 12) return ExactSearch(g, avail, req, size);
+  return Hierarchical(g, avail, req, size);
+}
+
+}  // namespace adp::alloc

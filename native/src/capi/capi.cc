@@ -1,0 +1,256 @@
+// C ABI over the native core, for the Python test-suite and benchmark harness
+// (loaded with ctypes from k8s_gpu_sharing_plugin_amd/native.py). Every function
+// takes and returns JSON strings; returned strings are freed with adp_free().
+// This is a test/tooling surface -- the daemon itself never goes through it.
+#include <cstdlib>
+#include <cstring>
+#include <json.hpp>
+#include <string>
+
+#include "alloc/replicas.h"
+#include "alloc/topology.h"
+#include "health/health.h"
+#include "inventory/inventory.h"
+#include "plugin/plugin.h"
+#include "proto/messages.h"
+#include "smi/smi.h"
+#include "strategy/strategy.h"
+
+using nlohmann::json;
+
+namespace {
+
+char* Dup(const std::string& s) {
+  char* p = static_cast<char*>(malloc(s.size() + 1));
+  memcpy(p, s.data(), s.size());
+  p[s.size()] = 0;
+  return p;
+}
+
+char* Err(const std::string& msg) { return Dup(json{{"error", msg}}.dump()); }
+
+template <typename Fn>
+char* Guard(Fn fn) {
+  try {
+    return fn();
+  } catch (const std::exception& e) {
+    return Err(std::string("exception: ") + e.what());
+  }
+}
+
+json SnapshotJson(const adp::inventory::Snapshot& s) {
+  json gpus = json::array();
+  for (const auto& g : s.gpus) {
+    json parts = json::array();
+    for (const auto& p : g.partitions) {
+      parts.push_back({{"uuid", p.uuid}, {"partition_id", p.partition_id}, {"render", p.render_path},
+                       {"card", p.card_path}, {"numa", p.numa}, {"vram_mib", p.vram_mib},
+                       {"xcds", p.xcds}, {"cus", p.cus}});
+    }
+    gpus.push_back({{"index", g.index}, {"node_index", g.node_index}, {"uuid", g.uuid}, {"bdf", g.bdf},
+                    {"numa", g.numa}, {"vram_mib", g.vram_mib}, {"xcds", g.xcds}, {"cus", g.cus},
+                    {"compute_mode", g.compute_mode}, {"memory_mode", g.memory_mode},
+                    {"market_name", g.market_name}, {"profile", g.PartitionProfile()},
+                    {"partitioned", g.partitioned()}, {"xgmi_links_down", g.xgmi_links_down},
+                    {"partitions", parts}});
+  }
+  json links = json::array();
+  for (size_t a = 0; a < s.gpus.size(); ++a) {
+    json row = json::array();
+    for (size_t b = 0; b < s.gpus.size(); ++b) row.push_back(static_cast<int>(s.Link(a, b)));
+    links.push_back(row);
+  }
+  return {{"gpus", gpus}, {"links", links}, {"smi_path", s.smi_path}, {"smi_version", s.smi_version}};
+}
+
+}  // namespace
+
+extern "C" {
+
+void adp_free(char* p) { free(p); }
+
+const char* adp_version() { return ADP_VERSION; }
+
+// {"available": [...], "must_include": [...], "size": n, "policy": "spread"|"pack"}
+char* adp_prioritize(const char* in) {
+  return Guard([&] {
+    json j = json::parse(in);
+    adp::alloc::ReplicaPolicy pol = adp::alloc::ReplicaPolicy::kSpread;
+    if (j.count("policy")) adp::alloc::ParseReplicaPolicy(j["policy"].get<std::string>(), &pol);
+    auto r = adp::alloc::PrioritizeDevices(j["available"].get<std::vector<std::string>>(),
+                                           j["must_include"].get<std::vector<std::string>>(),
+                                           j["size"].get<int>(), pol);
+    if (!r.ok()) return Err(r.status().message());
+    return Dup(json{{"ids", r->ids}, {"non_unique", r->non_unique}}.dump());
+  });
+}
+
+char* adp_strip_replicas(const char* in) {
+  return Guard([&] {
+    json j = json::parse(in);
+    return Dup(json(adp::alloc::StripReplicas(j.get<std::vector<std::string>>())).dump());
+  });
+}
+
+char* adp_parse_additional_ids(const char* in) {
+  return Guard([&] { return Dup(json(adp::health::ParseAdditionalIds(in)).dump()); });
+}
+
+// Health config from (DP_DISABLE_HEALTHCHECKS, DP_HEALTH_POLL_MS) + event classification table.
+char* adp_health_config(const char* disable_value, const char* poll_value) {
+  return Guard([&] {
+    auto c = adp::health::HealthConfig::FromValues(disable_value, poll_value);
+    json verdicts = json::object();
+    for (uint32_t t = 1; t <= 13; ++t)
+      verdicts[std::to_string(t)] = adp::health::Monitor::Classify(c, t);
+    return Dup(json{{"disabled", c.disabled}, {"ignored", c.ignored}, {"poll_ms", c.poll_interval_ms},
+                    {"verdicts", verdicts}}
+                   .dump());
+  });
+}
+
+char* adp_parse_resource_config(const char* in) {
+  return Guard([&] {
+    auto rc = adp::strategy::ResourceConfig::Parse(in);
+    if (!rc.ok()) return Err(rc.status().message());
+    json out = json::object();
+    for (const auto& [k, v] : rc->entries())
+      out[k] = {{"name", v.name}, {"replicas", v.replicas}, {"auto", v.auto_replicas}};
+    return Dup(out.dump());
+  });
+}
+
+// {"parent": [...], "scores": [n*n], "available": [...], "required": [...], "size": k}
+char* adp_best_effort(const char* in) {
+  return Guard([&] {
+    json j = json::parse(in);
+    adp::alloc::DeviceGraph g(j["parent"].get<std::vector<int>>(), j["scores"].get<std::vector<int>>());
+    auto r = adp::alloc::BestEffortAllocate(g, j["available"].get<std::vector<int>>(),
+                                            j["required"].get<std::vector<int>>(), j["size"].get<int>());
+    return Dup(json(r).dump());
+  });
+}
+
+// Loads libamd_smi (path "" = default search), enumerates, returns the snapshot.
+// {"lib": "...", "devices": [0,1]}
+char* adp_snapshot(const char* in) {
+  return Guard([&] {
+    json j = json::parse(in);
+    auto lib = adp::smi::Library::Open(j.value("lib", std::string()));
+    if (!lib.ok()) return Err(lib.status().ToString());
+    adp::inventory::BuildOptions opt;
+    if (j.count("devices")) opt.only_gpus = j["devices"].get<std::vector<int>>();
+    opt.include_card_nodes = j.value("include_card_nodes", false);
+    auto snap = adp::inventory::BuildSnapshot(lib->get(), opt);
+    if (!snap.ok()) return Err(snap.status().ToString());
+    return Dup(SnapshotJson(**snap).dump());
+  });
+}
+
+// Plugin set for a strategy: {"lib", "strategy", "resource_config", "devices",
+//  "auto_unit_mib", "id_strategy"} -> [{resource, socket, original, devices:[{id,index,paths,replicas,vram_mib,numa}], advertised}]
+char* adp_plugin_specs(const char* in) {
+  return Guard([&] {
+    json j = json::parse(in);
+    auto lib = adp::smi::Library::Open(j.value("lib", std::string()));
+    if (!lib.ok()) return Err(lib.status().ToString());
+    adp::inventory::BuildOptions opt;
+    if (j.count("devices")) opt.only_gpus = j["devices"].get<std::vector<int>>();
+    auto snap = adp::inventory::BuildSnapshot(lib->get(), opt);
+    if (!snap.ok()) return Err(snap.status().ToString());
+    adp::strategy::PartitionStrategy ps;
+    if (!adp::strategy::ParsePartitionStrategy(j.value("strategy", std::string("none")), &ps))
+      return Err("bad strategy");
+    auto rc = adp::strategy::ResourceConfig::Parse(j.value("resource_config", std::string()));
+    if (!rc.ok()) return Err(rc.status().message());
+    auto specs = adp::strategy::BuildPluginSpecs(**snap, ps, *rc);
+    if (!specs.ok()) return Err(specs.status().message());
+    adp::plugin::PluginOptions po;
+    po.auto_replica_unit_mib = j.value("auto_unit_mib", 1000);
+    if (j.count("id_strategy"))
+      adp::plugin::ParseDeviceIdStrategy(j["id_strategy"].get<std::string>(), &po.id_strategy);
+    json out = json::array();
+    for (const auto& s : *specs) {
+      adp::plugin::Plugin p(*snap, s, po);
+      json devs = json::array();
+      for (const auto& u : p.units())
+        devs.push_back({{"id", u.id}, {"index", u.index}, {"paths", u.paths}, {"replicas", u.replicas},
+                        {"vram_mib", u.vram_mib}, {"numa", u.numa}, {"gpu", u.gpu}});
+      out.push_back({{"resource", s.resource_name}, {"socket", s.socket_name}, {"original", s.original},
+                     {"devices", devs}, {"advertised", p.advertised_count()},
+                     {"advertised_ids", p.advertised_ids()}, {"replicated", p.replicated()}});
+    }
+    return Dup(out.dump());
+  });
+}
+
+// Proto codec round trip: decode `len` bytes as message `type` with the native
+// codec, re-encode, return hex. Types: allocate_request, allocate_response,
+// preferred_request, preferred_response, law_response, register_request, options.
+char* adp_proto_roundtrip(const char* type, const unsigned char* bytes, size_t len) {
+  return Guard([&] {
+    std::string_view in(reinterpret_cast<const char*>(bytes), len);
+    std::string out;
+    adp::Status st;
+    std::string t = type;
+    auto rt = [&](auto msg) {
+      st = adp::pb::Decode(in, &msg);
+      if (st.ok()) adp::pb::Encode(msg, &out);
+    };
+    if (t == "allocate_request") rt(adp::pb::AllocateRequest{});
+    else if (t == "allocate_response") rt(adp::pb::AllocateResponse{});
+    else if (t == "preferred_request") rt(adp::pb::PreferredAllocationRequest{});
+    else if (t == "preferred_response") rt(adp::pb::PreferredAllocationResponse{});
+    else if (t == "law_response") rt(adp::pb::ListAndWatchResponse{});
+    else if (t == "register_request") rt(adp::pb::RegisterRequest{});
+    else if (t == "options") rt(adp::pb::DevicePluginOptions{});
+    else if (t == "prestart_request") rt(adp::pb::PreStartContainerRequest{});
+    else return Err("unknown type");
+    if (!st.ok()) return Err(st.message());
+    static const char* hx = "0123456789abcdef";
+    std::string h;
+    for (unsigned char c : out) { h += hx[c >> 4]; h += hx[c & 15]; }
+    return Dup(json{{"hex", h}}.dump());
+  });
+}
+
+}  // extern "C"
+
+// ---- in-process churn benchmark client (bench.py times exactly the K steps) ----
+#include "bench/churn.h"
+
+extern "C" {
+
+// {"socket": "...", "pod_size": 1, "rank": 0, "world": 1, "preferred": true} -> handle or null
+void* adp_bench_open(const char* in, char** err) {
+  try {
+    json j = json::parse(in);
+    adp::bench::ChurnOptions o;
+    o.pod_size = j.value("pod_size", 1);
+    o.rank = j.value("rank", 0);
+    o.world = j.value("world", 1);
+    o.preferred = j.value("preferred", true);
+    auto c = adp::bench::ChurnClient::Open(j["socket"].get<std::string>(), o);
+    if (!c.ok()) {
+      *err = Dup(c.status().ToString());
+      return nullptr;
+    }
+    return c->release();
+  } catch (const std::exception& e) {
+    *err = Dup(e.what());
+    return nullptr;
+  }
+}
+
+// Runs `pods` admissions; returns null on success or an error string.
+char* adp_bench_run(void* h, int pods, int record) {
+  auto* c = static_cast<adp::bench::ChurnClient*>(h);
+  adp::Status st = c->Run(pods, record != 0);
+  return st.ok() ? nullptr : Dup(st.ToString());
+}
+
+char* adp_bench_stats(void* h) { return Dup(static_cast<adp::bench::ChurnClient*>(h)->StatsJson()); }
+void adp_bench_reset(void* h) { static_cast<adp::bench::ChurnClient*>(h)->ResetStats(); }
+void adp_bench_close(void* h) { delete static_cast<adp::bench::ChurnClient*>(h); }
+
+}  // extern "C"

@@ -1,0 +1,84 @@
+#include "common/log.h"
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <mutex>
+#include <sys/time.h>
+
+#include "common/status.h"
+
+namespace adp {
+namespace {
+
+LogLevel InitialLevel() {
+  const char* e = std::getenv("ADP_LOG_LEVEL");
+  if (!e) return LogLevel::kInfo;
+  if (!strcasecmp(e, "debug")) return LogLevel::kDebug;
+  if (!strcasecmp(e, "warn") || !strcasecmp(e, "warning")) return LogLevel::kWarn;
+  if (!strcasecmp(e, "error")) return LogLevel::kError;
+  return LogLevel::kInfo;
+}
+
+std::atomic<int> g_level{static_cast<int>(InitialLevel())};
+std::mutex g_mu;
+
+const char* LevelName(LogLevel l) {
+  switch (l) {
+    case LogLevel::kDebug: return "D";
+    case LogLevel::kInfo: return "I";
+    case LogLevel::kWarn: return "W";
+    case LogLevel::kError: return "E";
+  }
+  return "?";
+}
+
+}  // namespace
+
+void SetLogLevel(LogLevel l) { g_level.store(static_cast<int>(l)); }
+LogLevel GetLogLevel() { return static_cast<LogLevel>(g_level.load()); }
+bool LogEnabled(LogLevel l) { return static_cast<int>(l) >= g_level.load(std::memory_order_relaxed); }
+
+void Logf(LogLevel l, const char* component, const char* fmt, ...) {
+  char msg[4096];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(msg, sizeof(msg), fmt, ap);
+  va_end(ap);
+  struct timeval tv;
+  gettimeofday(&tv, nullptr);
+  struct tm tm;
+  gmtime_r(&tv.tv_sec, &tm);
+  char ts[32];
+  strftime(ts, sizeof(ts), "%Y-%m-%dT%H:%M:%S", &tm);
+  std::lock_guard<std::mutex> lk(g_mu);
+  fprintf(stderr, "%s.%06ldZ %s %s: %s\n", ts, static_cast<long>(tv.tv_usec), LevelName(l),
+          component, msg);
+  fflush(stderr);
+}
+
+const char* CodeName(Code c) {
+  switch (c) {
+    case Code::kOk: return "OK";
+    case Code::kInvalidArgument: return "INVALID_ARGUMENT";
+    case Code::kNotFound: return "NOT_FOUND";
+    case Code::kAlreadyExists: return "ALREADY_EXISTS";
+    case Code::kFailedPrecondition: return "FAILED_PRECONDITION";
+    case Code::kUnavailable: return "UNAVAILABLE";
+    case Code::kUnimplemented: return "UNIMPLEMENTED";
+    case Code::kInternal: return "INTERNAL";
+    case Code::kDeadlineExceeded: return "DEADLINE_EXCEEDED";
+    case Code::kNotSupported: return "NOT_SUPPORTED";
+    case Code::kPermissionDenied: return "PERMISSION_DENIED";
+  }
+  return "UNKNOWN";
+}
+
+std::string Status::ToString() const {
+  if (ok()) return "OK";
+  return std::string(CodeName(code_)) + ": " + msg_;
+}
+
+}  // namespace adp

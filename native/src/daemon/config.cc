@@ -1,0 +1,319 @@
+#include "daemon/config.h"
+
+#include <cctype>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <json.hpp>
+#include <sstream>
+
+#include "common/strings.h"
+
+extern char** environ;
+
+namespace adp::daemon {
+namespace {
+
+enum class Kind { kString, kBool, kUint };
+
+struct FlagDef {
+  const char* name;      // command line, without "--"
+  const char* env;       // environment variable ("" = none)
+  const char* file_key;  // key under `flags:` in the config file ("" = none)
+  Kind kind;
+  const char* help;
+  std::function<void*(Flags&)> field;
+};
+
+const std::vector<FlagDef>& Table() {
+  static const std::vector<FlagDef> t = {
+      {"partition-strategy", "PARTITION_STRATEGY", "partitionStrategy", Kind::kString,
+       "strategy for exposing compute partitions (SPX/DPX/QPX/CPX): [none | single | mixed]",
+       [](Flags& f) -> void* { return &f.partition_strategy; }},
+      {"fail-on-init-error", "FAIL_ON_INIT_ERROR", "failOnInitError", Kind::kBool,
+       "fail the plugin if an error is encountered during initialization, otherwise block "
+       "indefinitely",
+       [](Flags& f) -> void* { return &f.fail_on_init_error; }},
+      {"pass-device-specs", "PASS_DEVICE_SPECS", "passDeviceSpecs", Kind::kBool,
+       "pass /dev/kfd and the render nodes as DeviceSpecs on Allocate()",
+       [](Flags& f) -> void* { return &f.pass_device_specs; }},
+      {"device-list-strategy", "DEVICE_LIST_STRATEGY", "deviceListStrategy", Kind::kString,
+       "how the device list is also passed to the runtime: [envvar | volume-mounts | "
+       "cdi-annotations | cdi-cri]",
+       [](Flags& f) -> void* { return &f.device_list_strategy; }},
+      {"device-id-strategy", "DEVICE_ID_STRATEGY", "deviceIDStrategy", Kind::kString,
+       "how device IDs are passed to the runtime: [uuid | index]",
+       [](Flags& f) -> void* { return &f.device_id_strategy; }},
+      {"driver-root", "DRIVER_ROOT", "driverRoot", Kind::kString,
+       "root path of the host driver installation (device nodes are <driver-root>/dev/...)",
+       [](Flags& f) -> void* { return &f.driver_root; }},
+      {"resource-config", "RESOURCE_CONFIG", "resourceConfig", Kind::kString,
+       "rename/replicate resources: <original>:<new>:<replicas>,... e.g. "
+       "'gpu:sharedgpu:4,cpx-1xcd.36gb:small:2'; replicas -1 = one per 1000 MiB of VRAM",
+       [](Flags& f) -> void* { return &f.resource_config; }},
+      {"replica-policy", "REPLICA_POLICY", "replicaPolicy", Kind::kString,
+       "preferred allocation over replicas: [spread | pack] (pack suits memory-unit resources)",
+       [](Flags& f) -> void* { return &f.replica_policy; }},
+      {"device-plugin-path", "DP_PLUGIN_DIR", "devicePluginPath", Kind::kString,
+       "kubelet device-plugin directory",
+       [](Flags& f) -> void* { return &f.plugin_dir; }},
+      {"kubelet-socket", "DP_KUBELET_SOCKET", "kubeletSocket", Kind::kString,
+       "kubelet registration socket (default <device-plugin-path>/kubelet.sock)",
+       [](Flags& f) -> void* { return &f.kubelet_socket; }},
+      {"amdsmi-lib", "AMD_SMI_LIB", "amdsmiLib", Kind::kString,
+       "path of libamd_smi.so to load (default: search the loader path and /opt/rocm/lib)",
+       [](Flags& f) -> void* { return &f.amdsmi_lib; }},
+      {"devices", "AMD_DP_DEVICES", "devices", Kind::kString,
+       "only serve these node GPU indices, comma separated (default: all)",
+       [](Flags& f) -> void* { return &f.devices; }},
+      {"auto-replica-unit-mib", "AUTO_REPLICA_UNIT_MIB", "autoReplicaUnitMiB", Kind::kUint,
+       "MiB of VRAM per replica when replicas=-1",
+       [](Flags& f) -> void* { return &f.auto_replica_unit_mib; }},
+      {"resource-prefix", "RESOURCE_PREFIX", "resourcePrefix", Kind::kString,
+       "extended-resource domain", [](Flags& f) -> void* { return &f.resource_prefix; }},
+      {"include-card-nodes", "INCLUDE_CARD_NODES", "includeCardNodes", Kind::kBool,
+       "also pass /dev/dri/card<N> nodes (not needed for compute)",
+       [](Flags& f) -> void* { return &f.include_card_nodes; }},
+  };
+  return t;
+}
+
+Status Assign(const FlagDef& d, Flags& f, const std::string& value, const std::string& origin) {
+  void* p = d.field(f);
+  switch (d.kind) {
+    case Kind::kString:
+      *static_cast<std::string*>(p) = value;
+      return Status::Ok();
+    case Kind::kBool: {
+      auto b = ParseBool(value);
+      if (!b) return InvalidArgument("invalid boolean '" + value + "' for " + d.name + " (" + origin + ")");
+      *static_cast<bool*>(p) = *b;
+      return Status::Ok();
+    }
+    case Kind::kUint: {
+      auto u = ParseUint(Trim(value));
+      if (!u || *u == 0) return InvalidArgument("invalid value '" + value + "' for " + d.name + " (" + origin + ")");
+      *static_cast<uint64_t*>(p) = *u;
+      return Status::Ok();
+    }
+  }
+  return Internal("bad flag kind");
+}
+
+std::string ValueOf(const FlagDef& d, Flags& f) {
+  void* p = d.field(f);
+  switch (d.kind) {
+    case Kind::kString: return "\"" + JsonEscape(*static_cast<std::string*>(p)) + "\"";
+    case Kind::kBool: return *static_cast<bool*>(p) ? "true" : "false";
+    case Kind::kUint: return std::to_string(*static_cast<uint64_t*>(p));
+  }
+  return "null";
+}
+
+}  // namespace
+
+namespace {
+
+// Flattens a JSON object into dotted keys with scalar string values.
+Status FlattenJson(const nlohmann::json& j, const std::string& prefix,
+                   std::map<std::string, std::string>* out) {
+  for (auto it = j.begin(); it != j.end(); ++it) {
+    std::string key = prefix.empty() ? it.key() : prefix + "." + it.key();
+    const auto& v = it.value();
+    if (v.is_object()) {
+      ADP_RETURN_IF_ERROR(FlattenJson(v, key, out));
+    } else if (v.is_string()) {
+      (*out)[key] = v.get<std::string>();
+    } else if (v.is_boolean()) {
+      (*out)[key] = v.get<bool>() ? "true" : "false";
+    } else if (v.is_number_integer()) {
+      (*out)[key] = std::to_string(v.get<long long>());
+    } else if (v.is_number_unsigned()) {
+      (*out)[key] = std::to_string(v.get<unsigned long long>());
+    } else if (v.is_null()) {
+      (*out)[key] = "";
+    } else {
+      return InvalidArgument("unmarshal error: unsupported value for " + key);
+    }
+  }
+  return Status::Ok();
+}
+
+std::string Unquote(const std::string& v) {
+  if (v.size() >= 2 && ((v.front() == '"' && v.back() == '"') || (v.front() == '\'' && v.back() == '\'')))
+    return v.substr(1, v.size() - 2);
+  return v;
+}
+
+// Block-style YAML subset: nested mappings by indentation, scalar values,
+// '#' comments, single/double quotes. (The config schema has nothing else.)
+Status ParseYamlBlock(const std::string& body, std::map<std::string, std::string>* out) {
+  std::vector<std::pair<int, std::string>> stack;  // (indent, key) of open mappings
+  std::istringstream in(body);
+  std::string line;
+  int lineno = 0;
+  while (std::getline(in, line)) {
+    ++lineno;
+    // Strip comments outside quotes.
+    char quote = 0;
+    for (size_t i = 0; i < line.size(); ++i) {
+      char c = line[i];
+      if (quote) { if (c == quote) quote = 0; continue; }
+      if (c == '"' || c == '\'') quote = c;
+      else if (c == '#' && (i == 0 || isspace(static_cast<unsigned char>(line[i - 1])))) { line.resize(i); break; }
+    }
+    std::string t = Trim(line);
+    if (t.empty() || t == "---" || t == "...") continue;
+    if (t[0] == '-') return InvalidArgument("unmarshal error: sequences are not valid (line " + std::to_string(lineno) + ")");
+    int indent = 0;
+    while (indent < static_cast<int>(line.size()) && line[indent] == ' ') ++indent;
+    size_t colon = std::string::npos;
+    quote = 0;
+    for (size_t i = 0; i < t.size(); ++i) {
+      char c = t[i];
+      if (quote) { if (c == quote) quote = 0; continue; }
+      if (c == '"' || c == '\'') quote = c;
+      else if (c == ':' && (i + 1 == t.size() || t[i + 1] == ' ')) { colon = i; break; }
+    }
+    if (colon == std::string::npos)
+      return InvalidArgument("unmarshal error: expected 'key: value' at line " + std::to_string(lineno));
+    std::string key = Unquote(Trim(t.substr(0, colon)));
+    std::string val = Trim(t.substr(colon + 1));
+    while (!stack.empty() && stack.back().first >= indent) stack.pop_back();
+    std::string full;
+    for (const auto& [_, k] : stack) full += k + ".";
+    full += key;
+    if (val.empty()) {
+      stack.emplace_back(indent, key);
+    } else {
+      (*out)[full] = Unquote(val);
+    }
+  }
+  return Status::Ok();
+}
+
+}  // namespace
+
+Result<std::map<std::string, std::string>> ParseConfigFile(const std::string& body) {
+  std::map<std::string, std::string> out;
+  std::string t = Trim(body);
+  if (!t.empty() && t[0] == '{') {
+    nlohmann::json j;
+    try {
+      j = nlohmann::json::parse(t);
+    } catch (const std::exception& e) {
+      return InvalidArgument(std::string("unmarshal error: ") + e.what());
+    }
+    if (!j.is_object()) return InvalidArgument("unmarshal error: top level must be an object");
+    ADP_RETURN_IF_ERROR(FlattenJson(j, "", &out));
+  } else {
+    ADP_RETURN_IF_ERROR(ParseYamlBlock(body, &out));
+  }
+  if (!out.count("version") || out["version"].empty()) return InvalidArgument("missing version field");
+  if (out["version"] != "v1") return InvalidArgument("unknown version: " + out["version"]);
+  return out;
+}
+
+Result<Config> LoadConfig(int argc, const char* const* argv,
+                          const std::map<std::string, std::string>* env_in) {
+  std::map<std::string, std::string> env;
+  if (env_in) {
+    env = *env_in;
+  } else {
+    for (char** e = environ; e && *e; ++e) {
+      const char* eq = strchr(*e, '=');
+      if (eq) env[std::string(*e, eq - *e)] = eq + 1;
+    }
+  }
+  Config cfg;
+  std::map<std::string, std::string> cli;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    if (a == "--help" || a == "-h") { cfg.show_help = true; continue; }
+    if (a == "--version" || a == "-v") { cfg.show_version = true; continue; }
+    if (!StartsWith(a, "--")) return InvalidArgument("unexpected argument: " + a);
+    std::string name = a.substr(2), value;
+    bool has_value = false;
+    size_t eq = name.find('=');
+    if (eq != std::string::npos) {
+      value = name.substr(eq + 1);
+      name = name.substr(0, eq);
+      has_value = true;
+    }
+    if (name == "config-file") {
+      if (!has_value) {
+        if (i + 1 >= argc) return InvalidArgument("flag needs an argument: --config-file");
+        value = argv[++i];
+      }
+      cfg.config_file = value;
+      continue;
+    }
+    const FlagDef* def = nullptr;
+    for (const auto& d : Table())
+      if (name == d.name) def = &d;
+    if (!def) return InvalidArgument("flag provided but not defined: --" + name);
+    if (!has_value) {
+      if (def->kind == Kind::kBool) {
+        value = "true";
+      } else {
+        if (i + 1 >= argc) return InvalidArgument("flag needs an argument: --" + name);
+        value = argv[++i];
+      }
+    }
+    cli[name] = value;
+  }
+  if (cfg.config_file.empty() && env.count("CONFIG_FILE")) cfg.config_file = env["CONFIG_FILE"];
+
+  std::map<std::string, std::string> file;
+  if (!cfg.config_file.empty()) {
+    std::ifstream in(cfg.config_file);
+    if (!in) return InvalidArgument("unable to parse config file: error opening config file: " + cfg.config_file);
+    std::stringstream ss;
+    ss << in.rdbuf();
+    auto parsed = ParseConfigFile(ss.str());
+    if (!parsed.ok())
+      return InvalidArgument("unable to parse config file: error parsing config file: " +
+                             parsed.status().message());
+    file = std::move(*parsed);
+  }
+
+  // Precedence: command line > environment > config file > default.
+  for (const auto& d : Table()) {
+    Status st;
+    if (cli.count(d.name)) st = Assign(d, cfg.flags, cli[d.name], std::string("--") + d.name);
+    else if (*d.env && env.count(d.env)) st = Assign(d, cfg.flags, env[d.env], d.env);
+    else if (*d.file_key && file.count(std::string("flags.") + d.file_key))
+      st = Assign(d, cfg.flags, file[std::string("flags.") + d.file_key], cfg.config_file);
+    if (!st.ok()) return st;
+  }
+  return cfg;
+}
+
+std::string Config::ToJson() const {
+  Flags f = flags;
+  std::string out = "{\n  \"version\": \"" + version + "\",\n  \"flags\": {";
+  bool first = true;
+  for (const auto& d : Table()) {
+    out += first ? "\n" : ",\n";
+    first = false;
+    out += "    \"" + std::string(*d.file_key ? d.file_key : d.name) + "\": " + ValueOf(d, f);
+  }
+  return out + "\n  }\n}";
+}
+
+std::string UsageText() {
+  std::string s =
+      "amdgpu-device-plugin: Kubernetes device plugin for AMD Instinct MI355X GPUs\n\n"
+      "Usage: amdgpu-device-plugin [flags]\n\nFlags:\n";
+  Flags defaults;
+  for (const auto& d : Table()) {
+    s += "  --" + std::string(d.name) + "  (env " + d.env + ", default " + ValueOf(d, defaults) +
+         ")\n      " + d.help + "\n";
+  }
+  s += "  --config-file  (env CONFIG_FILE)\n      versioned YAML/JSON config (version: v1, flags: {...})\n";
+  s += "  --version, --help\n";
+  return s;
+}
+
+}  // namespace adp::daemon

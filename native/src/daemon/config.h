@@ -1,0 +1,65 @@
+// Daemon configuration: command-line flags, environment variables and an
+// optional versioned config file (YAML or JSON).
+//
+// Parity: reference cmd/nvidia-device-plugin/main.go:62-130 (flag table with env
+// mirrors), main.go:140-169 (validation), api/config/v1/config.go:30-144 (versioned
+// file, `version: v1`, precedence CLI > env > file).
+//
+// Renames for MI355X: --mig-strategy -> --partition-strategy (PARTITION_STRATEGY),
+// --nvidia-driver-root -> --driver-root (DRIVER_ROOT), NVIDIA_DRIVER_RESOURCE_CONFIG
+// -> RESOURCE_CONFIG. Kept as-is: FAIL_ON_INIT_ERROR, PASS_DEVICE_SPECS,
+// DEVICE_LIST_STRATEGY, DEVICE_ID_STRATEGY, CONFIG_FILE.
+//
+// Fixes: boolean values from the file can be false (B7); resourceConfig can come
+// from the file (B8). --pass-device-specs defaults to true: on AMD the device
+// nodes are the only thing that makes a GPU usable inside a container (there is
+// no runtime hook reading an env var).
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "common/status.h"
+
+namespace adp::daemon {
+
+struct Flags {
+  std::string partition_strategy = "none";
+  bool fail_on_init_error = true;
+  bool pass_device_specs = true;
+  std::string device_list_strategy = "envvar";
+  std::string device_id_strategy = "uuid";
+  std::string driver_root = "/";
+  std::string resource_config;
+  std::string replica_policy = "spread";
+  std::string plugin_dir = "/var/lib/kubelet/device-plugins/";
+  std::string kubelet_socket;  // default: <plugin_dir>/kubelet.sock
+  std::string amdsmi_lib;
+  std::string devices;         // GPU index filter, e.g. "0,1,2,3" (empty = all)
+  uint64_t auto_replica_unit_mib = 1000;
+  std::string resource_prefix = "amd.com";
+  bool include_card_nodes = false;
+};
+
+struct Config {
+  std::string version = "v1";
+  Flags flags;
+  std::string config_file;
+  bool show_version = false;
+  bool show_help = false;
+  std::string ToJson() const;
+};
+
+// Parses argv + environment (+ the config file they name). `env` lets tests
+// inject an environment; nullptr means the process environment.
+Result<Config> LoadConfig(int argc, const char* const* argv,
+                          const std::map<std::string, std::string>* env = nullptr);
+
+// Parses a versioned config file body into (camelCase key -> scalar value).
+Result<std::map<std::string, std::string>> ParseConfigFile(const std::string& body);
+
+std::string UsageText();
+
+}  // namespace adp::daemon

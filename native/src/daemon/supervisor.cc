@@ -1,0 +1,267 @@
+#include "daemon/supervisor.h"
+
+#include <errno.h>
+#include <poll.h>
+#include <signal.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/inotify.h>
+#include <sys/signalfd.h>
+#include <sys/timerfd.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "alloc/replicas.h"
+#include "common/log.h"
+#include "common/strings.h"
+#include "health/health.h"
+#include "inventory/inventory.h"
+#include "plugin/plugin.h"
+#include "smi/smi.h"
+#include "strategy/strategy.h"
+
+namespace adp::daemon {
+namespace {
+
+constexpr const char* kComp = "daemon";
+constexpr int kMaxBackoffMs = 30000;
+
+struct Validated {
+  strategy::PartitionStrategy partition;
+  plugin::PluginOptions popts;
+  strategy::ResourceConfig rc;
+  inventory::BuildOptions bopts;
+};
+
+Result<Validated> Validate(const Config& cfg) {
+  Validated v;
+  const Flags& f = cfg.flags;
+  if (!strategy::ParsePartitionStrategy(f.partition_strategy, &v.partition))
+    return InvalidArgument("invalid --partition-strategy option: " + f.partition_strategy);
+  if (!plugin::ParseDeviceListStrategy(f.device_list_strategy, &v.popts.list_strategy))
+    return InvalidArgument("invalid --device-list-strategy option: " + f.device_list_strategy);
+  if (!plugin::ParseDeviceIdStrategy(f.device_id_strategy, &v.popts.id_strategy))
+    return InvalidArgument("invalid --device-id-strategy option: " + f.device_id_strategy);
+  if (!alloc::ParseReplicaPolicy(f.replica_policy, &v.popts.replica_policy))
+    return InvalidArgument("invalid --replica-policy option: " + f.replica_policy);
+  auto rc = strategy::ResourceConfig::Parse(f.resource_config);
+  if (!rc.ok())
+    return InvalidArgument("invalid --resource-config option: '" + f.resource_config + "' " +
+                           rc.status().message());
+  v.rc = std::move(*rc);
+  v.popts.plugin_dir = f.plugin_dir;
+  v.popts.kubelet_socket = f.kubelet_socket;
+  v.popts.pass_device_specs = f.pass_device_specs;
+  v.popts.driver_root = f.driver_root;
+  v.popts.auto_replica_unit_mib = f.auto_replica_unit_mib;
+  v.bopts.driver_root = f.driver_root;
+  v.bopts.include_card_nodes = f.include_card_nodes;
+  std::string devs = Trim(f.devices);
+  if (!devs.empty() && devs != "all") {
+    for (const auto& d : Split(devs, ',')) {
+      auto n = ParseUint(Trim(d));
+      if (!n) return InvalidArgument("invalid --devices entry: '" + d + "'");
+      v.bopts.only_gpus.push_back(static_cast<int>(*n));
+    }
+  }
+  return v;
+}
+
+void ArmTimer(int tfd, int ms) {
+  itimerspec its{};
+  its.it_value.tv_sec = ms / 1000;
+  its.it_value.tv_nsec = (ms % 1000) * 1000000L;
+  timerfd_settime(tfd, 0, &its, nullptr);
+}
+
+}  // namespace
+
+int RunDaemon(const Config& cfg) {
+  auto validated = Validate(cfg);
+  if (!validated.ok()) {
+    LOG_ERROR(kComp, "unable to validate flags: %s", validated.status().message().c_str());
+    return 1;
+  }
+  Validated v = std::move(*validated);
+  LOG_INFO(kComp, "running with config:\n%s", cfg.ToJson().c_str());
+  LOG_INFO(kComp, "running with resource config: %s", v.rc.ToJson().c_str());
+
+  // Signals are consumed through a signalfd; block them before any thread starts.
+  sigset_t sigs;
+  sigemptyset(&sigs);
+  for (int s : {SIGHUP, SIGINT, SIGTERM, SIGQUIT, SIGUSR1}) sigaddset(&sigs, s);
+  pthread_sigmask(SIG_BLOCK, &sigs, nullptr);
+  int sfd = signalfd(-1, &sigs, SFD_CLOEXEC | SFD_NONBLOCK);
+
+  LOG_INFO(kComp, "loading amdsmi");
+  auto lib = smi::Library::Open(cfg.flags.amdsmi_lib);
+  if (!lib.ok()) {
+    LOG_ERROR(kComp, "failed to initialize amdsmi: %s", lib.status().message().c_str());
+    LOG_ERROR(kComp, "if this is a GPU node, check that the amdgpu driver is loaded and ROCm's "
+                     "libamd_smi.so is available (or pass --amdsmi-lib)");
+    LOG_ERROR(kComp, "if this is not a GPU node, use a nodeSelector or toleration so the plugin "
+                     "only runs on GPU nodes");
+    if (cfg.flags.fail_on_init_error) return 1;
+    LOG_INFO(kComp, "failOnInitError=false: blocking until terminated");
+    while (true) {
+      signalfd_siginfo si;
+      pollfd p{sfd, POLLIN, 0};
+      poll(&p, 1, -1);
+      if (read(sfd, &si, sizeof(si)) == sizeof(si) && si.ssi_signo != SIGHUP && si.ssi_signo != SIGUSR1)
+        return 0;
+    }
+  }
+  LOG_INFO(kComp, "amdsmi %s loaded from %s", (*lib)->Version().c_str(), (*lib)->path().c_str());
+
+  std::string kubelet_sock =
+      v.popts.kubelet_socket.empty() ? PathJoin(v.popts.plugin_dir, "kubelet.sock") : v.popts.kubelet_socket;
+  std::string watch_dir = kubelet_sock.substr(0, kubelet_sock.rfind('/'));
+  if (watch_dir.empty()) watch_dir = "/";
+  std::string kubelet_name = BaseName(kubelet_sock);
+  LOG_INFO(kComp, "starting FS watcher on %s", watch_dir.c_str());
+  int ifd = inotify_init1(IN_NONBLOCK | IN_CLOEXEC);
+  if (ifd < 0 || inotify_add_watch(ifd, watch_dir.c_str(), IN_CREATE | IN_MOVED_TO) < 0) {
+    LOG_ERROR(kComp, "failed to create FS watcher on %s: %s", watch_dir.c_str(), strerror(errno));
+    return 1;
+  }
+  int tfd = timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC | TFD_NONBLOCK);
+  int efd = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  int ep = epoll_create1(EPOLL_CLOEXEC);
+  for (int fd : {sfd, ifd, tfd, efd}) {
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.fd = fd;
+    epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev);
+  }
+
+  std::vector<std::unique_ptr<plugin::Plugin>> plugins;
+  std::unique_ptr<health::Monitor> monitor;
+  int backoff_ms = 1000;
+  int exit_code = 0;
+  bool quit = false;
+
+  auto stop_all = [&] {
+    if (monitor) monitor->Stop();
+    monitor.reset();
+    for (auto& p : plugins) p->Stop();
+    plugins.clear();
+  };
+
+  auto schedule_retry = [&](const char* why) {
+    LOG_WARN(kComp, "%s; retrying in %d ms", why, backoff_ms);
+    ArmTimer(tfd, backoff_ms);
+    backoff_ms = std::min(kMaxBackoffMs, backoff_ms * 2);
+  };
+
+  auto restart = [&] {
+    stop_all();
+    ArmTimer(tfd, 0);  // disarm
+    LOG_INFO(kComp, "retrieving plugins");
+    auto snap = inventory::BuildSnapshot(lib->get(), v.bopts);
+    if (!snap.ok()) {
+      LOG_ERROR(kComp, "device enumeration failed: %s", snap.status().ToString().c_str());
+      schedule_retry("enumeration failed");
+      return;
+    }
+    auto specs = strategy::BuildPluginSpecs(**snap, v.partition, v.rc, cfg.flags.resource_prefix);
+    if (!specs.ok()) {
+      LOG_ERROR(kComp, "error creating partition strategy: %s", specs.status().message().c_str());
+      exit_code = 1;
+      quit = true;
+      return;
+    }
+    for (auto& s : *specs) plugins.push_back(std::make_unique<plugin::Plugin>(*snap, s, v.popts));
+    int started = 0;
+    for (auto& p : plugins) {
+      if (p->device_count() == 0) continue;
+      Status st = p->Start([efd] {
+        uint64_t one = 1;
+        ssize_t w = write(efd, &one, sizeof(one));
+        (void)w;
+      });
+      if (!st.ok()) {
+        LOG_ERROR(kComp, "could not contact kubelet, retrying (is the device-plugin feature "
+                         "enabled and is %s present?)", kubelet_sock.c_str());
+        schedule_retry("plugin start failed");
+        return;
+      }
+      ++started;
+    }
+    backoff_ms = 1000;
+    if (started == 0) LOG_INFO(kComp, "no devices found; waiting indefinitely");
+    monitor = std::make_unique<health::Monitor>(lib->get(), *snap, health::HealthConfig::FromEnv());
+    for (auto& p : plugins) {
+      plugin::Plugin* raw = p.get();
+      monitor->AddListener([raw](int gpu, bool ok, const std::string& why) { raw->SetGpuHealth(gpu, ok, why); });
+    }
+    Status hs = monitor->Start();
+    if (!hs.ok()) LOG_WARN(kComp, "health monitor: %s", hs.ToString().c_str());
+  };
+
+  restart();
+  while (!quit) {
+    epoll_event events[8];
+    int n = epoll_wait(ep, events, 8, -1);
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      LOG_ERROR(kComp, "epoll_wait: %s", strerror(errno));
+      exit_code = 1;
+      break;
+    }
+    bool do_restart = false;
+    for (int i = 0; i < n && !quit; ++i) {
+      int fd = events[i].data.fd;
+      if (fd == tfd) {
+        uint64_t exp;
+        ssize_t r = read(tfd, &exp, sizeof(exp));
+        (void)r;
+        do_restart = true;
+      } else if (fd == efd) {
+        uint64_t x;
+        ssize_t r = read(efd, &x, sizeof(x));
+        (void)r;
+        LOG_ERROR(kComp, "a gRPC server exhausted its crash budget; exiting");
+        exit_code = 1;
+        quit = true;
+      } else if (fd == ifd) {
+        char buf[4096] __attribute__((aligned(__alignof__(inotify_event))));
+        ssize_t len;
+        while ((len = read(ifd, buf, sizeof(buf))) > 0) {
+          for (char* p = buf; p < buf + len;) {
+            auto* e = reinterpret_cast<inotify_event*>(p);
+            if (e->len && kubelet_name == e->name && (e->mask & (IN_CREATE | IN_MOVED_TO))) {
+              LOG_INFO(kComp, "inotify: %s created, restarting", kubelet_sock.c_str());
+              backoff_ms = 1000;
+              do_restart = true;
+            }
+            p += sizeof(inotify_event) + e->len;
+          }
+        }
+      } else if (fd == sfd) {
+        signalfd_siginfo si;
+        while (read(sfd, &si, sizeof(si)) == sizeof(si)) {
+          if (si.ssi_signo == SIGHUP) {
+            LOG_INFO(kComp, "received SIGHUP, restarting");
+            do_restart = true;
+          } else if (si.ssi_signo == SIGUSR1) {
+            for (auto& p : plugins) LOG_INFO(kComp, "stats: %s", p->StatsJson().c_str());
+          } else {
+            LOG_INFO(kComp, "received signal %s, shutting down", strsignal(static_cast<int>(si.ssi_signo)));
+            quit = true;
+          }
+        }
+      }
+    }
+    if (do_restart && !quit) restart();
+  }
+  stop_all();
+  for (int fd : {ep, sfd, ifd, tfd, efd}) close(fd);
+  LOG_INFO(kComp, "shutdown complete (exit %d)", exit_code);
+  return exit_code;
+}
+
+}  // namespace adp::daemon

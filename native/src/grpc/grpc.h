@@ -1,0 +1,182 @@
+// gRPC over HTTP/2 cleartext (h2c) on Unix-domain sockets, built on nghttp2.
+//
+// The kubelet talks to device plugins with gRPC over UDS (reference
+// cmd/nvidia-device-plugin/server.go:113-240, grpc-go v1.29 vendored). There is
+// no grpc++ in this toolchain, and a full gRPC stack is not needed: the plugin
+// serves five unary/server-streaming methods and makes one unary call. This
+// module implements exactly the gRPC-over-HTTP/2 protocol subset they use:
+//   * 5-byte length-prefixed messages (uncompressed),
+//   * `content-type: application/grpc`, `te: trailers`,
+//   * status in trailers (`grpc-status`, percent-encoded `grpc-message`),
+//     trailers-only responses for errors,
+//   * unary and server-streaming calls (ListAndWatch stays open for the life of
+//     the plugin and pushes a new device list on every health transition).
+// nghttp2 provides HPACK, flow control, SETTINGS/PING/GOAWAY handling.
+//
+// Threading: each Server runs one epoll loop thread. Handlers execute on that
+// thread (they are O(k) in-memory work, so an inline call is cheaper than any
+// hand-off); other threads inject work with Post().
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <vector>
+
+#include "common/status.h"
+
+namespace adp::grpc {
+
+// gRPC status codes (https://grpc.github.io/grpc/core/md_doc_statuscodes.html).
+enum GrpcCode : int {
+  kGrpcOk = 0,
+  kGrpcCancelled = 1,
+  kGrpcUnknown = 2,
+  kGrpcInvalidArgument = 3,
+  kGrpcDeadlineExceeded = 4,
+  kGrpcNotFound = 5,
+  kGrpcAlreadyExists = 6,
+  kGrpcPermissionDenied = 7,
+  kGrpcResourceExhausted = 8,
+  kGrpcFailedPrecondition = 9,
+  kGrpcAborted = 10,
+  kGrpcOutOfRange = 11,
+  kGrpcUnimplemented = 12,
+  kGrpcInternal = 13,
+  kGrpcUnavailable = 14,
+};
+int ToGrpcCode(Code c);
+Code FromGrpcCode(int g);
+
+// 5-byte gRPC message framing.
+void FrameMessage(std::string_view msg, std::string* out);
+std::string PercentEncode(std::string_view s);
+std::string PercentDecode(std::string_view s);
+
+class ServerConn;
+
+// A server-streaming call that the handler keeps open. All methods must be
+// called on the server's loop thread (use Server::Post from elsewhere).
+class ServerStream {
+ public:
+  // Queues one message. Returns false once the peer has gone away.
+  bool Send(std::string_view message);
+  // Ends the call with trailers carrying `st`.
+  void Finish(const Status& st);
+  bool closed() const { return closed_; }
+  uint64_t id() const { return id_; }
+
+ private:
+  friend class Server;
+  friend class ServerConn;
+  ServerConn* conn_ = nullptr;
+  int32_t stream_id_ = 0;
+  uint64_t id_ = 0;
+  bool closed_ = false;
+};
+
+using UnaryHandler = std::function<Status(std::string_view request, std::string* response)>;
+using StreamHandler =
+    std::function<Status(std::string_view request, std::shared_ptr<ServerStream> stream)>;
+
+struct ServerStats {
+  std::atomic<uint64_t> connections{0};
+  std::atomic<uint64_t> calls{0};
+  std::atomic<uint64_t> errors{0};
+};
+
+class Server {
+ public:
+  explicit Server(std::string name);
+  ~Server();
+  Server(const Server&) = delete;
+  Server& operator=(const Server&) = delete;
+
+  void AddUnary(const std::string& path, UnaryHandler h);
+  void AddServerStream(const std::string& path, StreamHandler h);
+
+  // Removes a stale socket file, binds and listens.
+  Status Listen(const std::string& socket_path);
+  // Starts the loop thread. `on_fatal` runs (on the loop thread) if the loop
+  // fails more than 5 times with less than an hour between failures -- the
+  // reference's crash budget (server.go:177-205).
+  Status Start(std::function<void()> on_fatal = nullptr);
+  // Closes every connection and the listener, joins the thread. Idempotent.
+  void Stop();
+  // Runs `fn` on the loop thread. Safe from any thread; dropped after Stop().
+  void Post(std::function<void()> fn);
+  bool OnLoopThread() const;
+  const std::string& socket_path() const { return socket_path_; }
+  const ServerStats& stats() const { return stats_; }
+
+  // Test hook: make the next loop iteration fail as if epoll_wait errored.
+  void InjectLoopFailureForTest() { inject_failure_.store(true); }
+
+ private:
+  friend class ServerConn;
+  friend class ServerStream;
+  Status RunLoop();
+  void LoopMain();
+  void AcceptAll();
+  void CloseConn(int fd);
+  void DrainPosted();
+
+  std::string name_;
+  std::string socket_path_;
+  std::map<std::string, UnaryHandler> unary_;
+  std::map<std::string, StreamHandler> streams_;
+  int listen_fd_ = -1;
+  int epoll_fd_ = -1;
+  int event_fd_ = -1;
+  std::thread thread_;
+  std::thread::id loop_tid_;
+  std::atomic<bool> stopping_{false};
+  std::atomic<bool> inject_failure_{false};
+  std::function<void()> on_fatal_;
+  std::mutex post_mu_;
+  std::vector<std::function<void()>> posted_;
+  std::map<int, std::unique_ptr<ServerConn>> conns_;
+  uint64_t next_stream_id_ = 1;
+  ServerStats stats_;
+};
+
+// Blocking client (one HTTP/2 connection). Used for kubelet registration, the
+// self-dial readiness probe, and the native benchmark/stub-kubelet tools.
+class Channel {
+ public:
+  ~Channel();
+  static Result<std::unique_ptr<Channel>> Dial(const std::string& uds_path, int timeout_ms);
+
+  Status Unary(const std::string& path, std::string_view request, std::string* response,
+               int timeout_ms);
+  // Opens a server-streaming call; returns the stream id.
+  Result<int32_t> StartStream(const std::string& path, std::string_view request);
+  // Next message of a stream. Returns NotFound("end of stream") after a clean end,
+  // DeadlineExceeded on timeout, or the call's error status.
+  Status Recv(int32_t stream_id, std::string* message, int timeout_ms);
+  // Processes pending input without blocking (or up to timeout_ms).
+  Status Pump(int timeout_ms);
+  bool alive() const;
+
+ private:
+  struct CallState;
+  Channel() = default;
+  Status Flush();
+  Status WaitFor(const std::function<bool()>& done, int timeout_ms);
+  Result<int32_t> Submit(const std::string& path, std::string_view request);
+
+  int fd_ = -1;
+  void* session_ = nullptr;  // nghttp2_session*
+  bool dead_ = false;
+  bool got_settings_ = false;
+  std::map<int32_t, std::unique_ptr<CallState>> calls_;
+  friend struct ChannelCallbacks;
+};
+
+}  // namespace adp::grpc

@@ -1,0 +1,563 @@
+// gRPC h2c server on a Unix-domain socket (see grpc.h for the protocol subset).
+//
+// Parity: reference cmd/nvidia-device-plugin/server.go:168-215 (Serve: remove stale
+// socket, listen on unix:<socket>, register the service, restart the serve loop on
+// failure with a crash budget of 5 failures within an hour each).
+#include <errno.h>
+#include <fcntl.h>
+#include <nghttp2/nghttp2.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+
+#include "common/log.h"
+#include "grpc/grpc.h"
+
+namespace adp::grpc {
+namespace {
+
+constexpr size_t kMaxRequestBytes = 16u << 20;  // 16 MiB, >> any kubelet request
+constexpr const char* kComp = "grpc-server";
+
+bool StartsWithGrpc(const std::string& ct) { return ct.rfind("application/grpc", 0) == 0; }
+
+nghttp2_nv MakeNv(const char* name, const std::string& value) {
+  nghttp2_nv nv;
+  nv.name = reinterpret_cast<uint8_t*>(const_cast<char*>(name));
+  nv.namelen = strlen(name);
+  nv.value = reinterpret_cast<uint8_t*>(const_cast<char*>(value.data()));
+  nv.valuelen = value.size();
+  nv.flags = NGHTTP2_NV_FLAG_NONE;
+  return nv;
+}
+
+}  // namespace
+
+struct StreamState {
+  std::string path;
+  std::string content_type;
+  std::string body;
+  bool dispatched = false;
+  std::string out;       // framed response bytes not yet handed to nghttp2
+  size_t out_off = 0;
+  bool finishing = false;  // send trailers once `out` drains
+  bool deferred = false;
+  int grpc_status = 0;
+  std::string grpc_message;
+  std::shared_ptr<ServerStream> stream;
+};
+
+class ServerConn {
+ public:
+  ServerConn(Server* srv, int fd) : srv_(srv), fd_(fd) {}
+  ~ServerConn() {
+    for (auto& [_, st] : streams_) {
+      if (st.stream) { st.stream->closed_ = true; st.stream->conn_ = nullptr; }
+    }
+    if (session_) nghttp2_session_del(session_);
+    if (fd_ >= 0) close(fd_);
+  }
+
+  bool Init();
+  bool OnReadable();
+  bool Flush();
+  bool Done() const {
+    return !nghttp2_session_want_read(session_) && !nghttp2_session_want_write(session_) &&
+           wbuf_.size() == woff_;
+  }
+  bool want_epollout() const { return wbuf_.size() > woff_; }
+  int fd() const { return fd_; }
+
+  // --- called from nghttp2 callbacks ---
+  StreamState* Find(int32_t sid) {
+    auto it = streams_.find(sid);
+    return it == streams_.end() ? nullptr : &it->second;
+  }
+  void Dispatch(int32_t sid);
+  void OnStreamClose(int32_t sid) {
+    auto it = streams_.find(sid);
+    if (it == streams_.end()) return;
+    if (it->second.stream) { it->second.stream->closed_ = true; it->second.stream->conn_ = nullptr; }
+    streams_.erase(it);
+  }
+  ssize_t ReadData(int32_t sid, uint8_t* buf, size_t len, uint32_t* flags);
+
+  // --- used by ServerStream ---
+  bool QueueMessage(int32_t sid, std::string_view msg);
+  void Finish(int32_t sid, const Status& st);
+
+  Server* srv_;
+  std::map<int32_t, StreamState> streams_;
+
+ private:
+  void SubmitTrailersOnly(int32_t sid, int code, const std::string& msg);
+  void SubmitResponse(int32_t sid);
+  void SubmitTrailers(int32_t sid, StreamState* st);
+
+  int fd_;
+  nghttp2_session* session_ = nullptr;
+  std::string wbuf_;
+  size_t woff_ = 0;
+};
+
+// ------------------------- nghttp2 callbacks -------------------------
+
+static int OnBeginHeaders(nghttp2_session*, const nghttp2_frame* frame, void* ud) {
+  auto* c = static_cast<ServerConn*>(ud);
+  if (frame->hd.type == NGHTTP2_HEADERS && frame->headers.cat == NGHTTP2_HCAT_REQUEST) {
+    c->streams_[frame->hd.stream_id];
+  }
+  return 0;
+}
+
+static int OnHeader(nghttp2_session*, const nghttp2_frame* frame, const uint8_t* name,
+                    size_t namelen, const uint8_t* value, size_t valuelen, uint8_t, void* ud) {
+  auto* c = static_cast<ServerConn*>(ud);
+  if (frame->hd.type != NGHTTP2_HEADERS) return 0;
+  StreamState* st = c->Find(frame->hd.stream_id);
+  if (!st) return 0;
+  std::string_view n(reinterpret_cast<const char*>(name), namelen);
+  std::string_view v(reinterpret_cast<const char*>(value), valuelen);
+  if (n == ":path") st->path.assign(v);
+  else if (n == "content-type") st->content_type.assign(v);
+  return 0;
+}
+
+static int OnDataChunk(nghttp2_session* s, uint8_t, int32_t sid, const uint8_t* data, size_t len,
+                       void* ud) {
+  auto* c = static_cast<ServerConn*>(ud);
+  StreamState* st = c->Find(sid);
+  if (!st) return 0;
+  if (st->body.size() + len > kMaxRequestBytes) {
+    nghttp2_submit_rst_stream(s, NGHTTP2_FLAG_NONE, sid, NGHTTP2_REFUSED_STREAM);
+    return 0;
+  }
+  st->body.append(reinterpret_cast<const char*>(data), len);
+  return 0;
+}
+
+static int OnFrameRecv(nghttp2_session*, const nghttp2_frame* frame, void* ud) {
+  auto* c = static_cast<ServerConn*>(ud);
+  if ((frame->hd.type == NGHTTP2_DATA || frame->hd.type == NGHTTP2_HEADERS) &&
+      (frame->hd.flags & NGHTTP2_FLAG_END_STREAM)) {
+    c->Dispatch(frame->hd.stream_id);
+  }
+  return 0;
+}
+
+static int OnStreamCloseCb(nghttp2_session*, int32_t sid, uint32_t, void* ud) {
+  static_cast<ServerConn*>(ud)->OnStreamClose(sid);
+  return 0;
+}
+
+static ssize_t ReadCallback(nghttp2_session*, int32_t sid, uint8_t* buf, size_t length,
+                            uint32_t* data_flags, nghttp2_data_source*, void* ud) {
+  return static_cast<ServerConn*>(ud)->ReadData(sid, buf, length, data_flags);
+}
+
+// ------------------------- ServerConn -------------------------
+
+bool ServerConn::Init() {
+  nghttp2_session_callbacks* cbs;
+  nghttp2_session_callbacks_new(&cbs);
+  nghttp2_session_callbacks_set_on_begin_headers_callback(cbs, OnBeginHeaders);
+  nghttp2_session_callbacks_set_on_header_callback(cbs, OnHeader);
+  nghttp2_session_callbacks_set_on_data_chunk_recv_callback(cbs, OnDataChunk);
+  nghttp2_session_callbacks_set_on_frame_recv_callback(cbs, OnFrameRecv);
+  nghttp2_session_callbacks_set_on_stream_close_callback(cbs, OnStreamCloseCb);
+  int rv = nghttp2_session_server_new(&session_, cbs, this);
+  nghttp2_session_callbacks_del(cbs);
+  if (rv != 0) return false;
+  nghttp2_settings_entry iv[] = {
+      {NGHTTP2_SETTINGS_MAX_CONCURRENT_STREAMS, 1024},
+      {NGHTTP2_SETTINGS_INITIAL_WINDOW_SIZE, 1u << 20},
+      {NGHTTP2_SETTINGS_MAX_FRAME_SIZE, 1u << 16},
+  };
+  if (nghttp2_submit_settings(session_, NGHTTP2_FLAG_NONE, iv, sizeof(iv) / sizeof(iv[0])) != 0)
+    return false;
+  nghttp2_session_set_local_window_size(session_, NGHTTP2_FLAG_NONE, 0, 8 << 20);
+  return Flush();
+}
+
+bool ServerConn::OnReadable() {
+  char buf[64 * 1024];
+  while (true) {
+    ssize_t n = read(fd_, buf, sizeof(buf));
+    if (n > 0) {
+      ssize_t rv = nghttp2_session_mem_recv(session_, reinterpret_cast<uint8_t*>(buf), n);
+      if (rv < 0) {
+        LOG_DEBUG(kComp, "nghttp2 recv error: %s", nghttp2_strerror(static_cast<int>(rv)));
+        return false;
+      }
+      if (static_cast<size_t>(n) < sizeof(buf)) break;
+      continue;
+    }
+    if (n == 0) return false;  // peer closed
+    if (errno == EINTR) continue;
+    if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+    return false;
+  }
+  return Flush();
+}
+
+bool ServerConn::Flush() {
+  // Pull frames out of nghttp2 until it has nothing more (flow control bounds
+  // how much it produces), then write as much as the socket takes.
+  while (true) {
+    const uint8_t* data;
+    ssize_t n = nghttp2_session_mem_send(session_, &data);
+    if (n < 0) return false;
+    if (n == 0) break;
+    if (woff_ == wbuf_.size()) { wbuf_.clear(); woff_ = 0; }
+    wbuf_.append(reinterpret_cast<const char*>(data), n);
+  }
+  while (woff_ < wbuf_.size()) {
+    ssize_t n = send(fd_, wbuf_.data() + woff_, wbuf_.size() - woff_, MSG_NOSIGNAL);
+    if (n > 0) { woff_ += n; continue; }
+    if (n < 0 && errno == EINTR) continue;
+    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+    return false;
+  }
+  if (woff_ == wbuf_.size()) { wbuf_.clear(); woff_ = 0; }
+  return true;
+}
+
+ssize_t ServerConn::ReadData(int32_t sid, uint8_t* buf, size_t len, uint32_t* flags) {
+  StreamState* st = Find(sid);
+  if (!st) return NGHTTP2_ERR_TEMPORAL_CALLBACK_FAILURE;
+  size_t avail = st->out.size() - st->out_off;
+  size_t n = avail < len ? avail : len;
+  if (n) {
+    memcpy(buf, st->out.data() + st->out_off, n);
+    st->out_off += n;
+    if (st->out_off == st->out.size()) { st->out.clear(); st->out_off = 0; }
+  }
+  if (st->out.size() == st->out_off) {
+    if (st->finishing) {
+      *flags |= NGHTTP2_DATA_FLAG_EOF | NGHTTP2_DATA_FLAG_NO_END_STREAM;
+      SubmitTrailers(sid, st);
+      return static_cast<ssize_t>(n);
+    }
+    if (n == 0) {
+      st->deferred = true;
+      return NGHTTP2_ERR_DEFERRED;
+    }
+  }
+  return static_cast<ssize_t>(n);
+}
+
+void ServerConn::SubmitTrailers(int32_t sid, StreamState* st) {
+  std::string code = std::to_string(st->grpc_status);
+  std::string msg = PercentEncode(st->grpc_message);
+  nghttp2_nv nva[2] = {MakeNv("grpc-status", code), MakeNv("grpc-message", msg)};
+  nghttp2_submit_trailer(session_, sid, nva, msg.empty() ? 1 : 2);
+}
+
+void ServerConn::SubmitTrailersOnly(int32_t sid, int code, const std::string& msg) {
+  std::string status = "200", ct = "application/grpc", c = std::to_string(code);
+  std::string m = PercentEncode(msg);
+  nghttp2_nv nva[4] = {MakeNv(":status", status), MakeNv("content-type", ct),
+                       MakeNv("grpc-status", c), MakeNv("grpc-message", m)};
+  nghttp2_submit_response(session_, sid, nva, m.empty() ? 3 : 4, nullptr);
+  srv_->stats_.errors.fetch_add(1, std::memory_order_relaxed);
+}
+
+void ServerConn::SubmitResponse(int32_t sid) {
+  std::string status = "200", ct = "application/grpc";
+  nghttp2_nv nva[2] = {MakeNv(":status", status), MakeNv("content-type", ct)};
+  nghttp2_data_provider prd;
+  prd.source.ptr = nullptr;
+  prd.read_callback = ReadCallback;
+  nghttp2_submit_response(session_, sid, nva, 2, &prd);
+}
+
+void ServerConn::Dispatch(int32_t sid) {
+  StreamState* st = Find(sid);
+  if (!st || st->dispatched) return;
+  st->dispatched = true;
+  srv_->stats_.calls.fetch_add(1, std::memory_order_relaxed);
+
+  if (!StartsWithGrpc(st->content_type)) {
+    SubmitTrailersOnly(sid, kGrpcInternal, "invalid content-type: " + st->content_type);
+    return;
+  }
+  // Exactly one length-prefixed message (an empty body is treated as an empty message).
+  std::string_view req;
+  if (!st->body.empty()) {
+    if (st->body.size() < 5) {
+      SubmitTrailersOnly(sid, kGrpcInternal, "truncated gRPC message header");
+      return;
+    }
+    const auto* b = reinterpret_cast<const uint8_t*>(st->body.data());
+    if (b[0] != 0) {
+      SubmitTrailersOnly(sid, kGrpcUnimplemented, "compressed messages are not supported");
+      return;
+    }
+    uint32_t n = (uint32_t(b[1]) << 24) | (uint32_t(b[2]) << 16) | (uint32_t(b[3]) << 8) | b[4];
+    if (st->body.size() != 5 + static_cast<size_t>(n)) {
+      SubmitTrailersOnly(sid, kGrpcInternal, "gRPC message length mismatch");
+      return;
+    }
+    req = std::string_view(st->body).substr(5);
+  }
+
+  auto u = srv_->unary_.find(st->path);
+  if (u != srv_->unary_.end()) {
+    std::string resp;
+    Status s = u->second(req, &resp);
+    st = Find(sid);  // handler cannot erase streams, but be defensive
+    if (!st) return;
+    if (!s.ok()) {
+      SubmitTrailersOnly(sid, ToGrpcCode(s.code()), s.message());
+      return;
+    }
+    FrameMessage(resp, &st->out);
+    st->finishing = true;
+    SubmitResponse(sid);
+    return;
+  }
+  auto ss = srv_->streams_.find(st->path);
+  if (ss != srv_->streams_.end()) {
+    auto stream = std::make_shared<ServerStream>();
+    stream->conn_ = this;
+    stream->stream_id_ = sid;
+    stream->id_ = srv_->next_stream_id_++;
+    st->stream = stream;
+    SubmitResponse(sid);
+    Status s = ss->second(req, stream);
+    if (!s.ok() && !stream->closed_) stream->Finish(s);
+    return;
+  }
+  SubmitTrailersOnly(sid, kGrpcUnimplemented, "unknown method " + st->path);
+}
+
+bool ServerConn::QueueMessage(int32_t sid, std::string_view msg) {
+  StreamState* st = Find(sid);
+  if (!st || st->finishing) return false;
+  FrameMessage(msg, &st->out);
+  if (st->deferred) {
+    st->deferred = false;
+    nghttp2_session_resume_data(session_, sid);
+  }
+  return true;
+}
+
+void ServerConn::Finish(int32_t sid, const Status& s) {
+  StreamState* st = Find(sid);
+  if (!st || st->finishing) return;
+  st->finishing = true;
+  st->grpc_status = ToGrpcCode(s.code());
+  st->grpc_message = s.ok() ? "" : s.message();
+  if (st->deferred) {
+    st->deferred = false;
+    nghttp2_session_resume_data(session_, sid);
+  }
+}
+
+// ------------------------- ServerStream -------------------------
+
+// Send/Finish only queue: they may run inside an nghttp2 callback (a handler
+// sending its first message), where nghttp2_session_mem_send must not be
+// re-entered. The loop flushes every connection after each iteration.
+bool ServerStream::Send(std::string_view message) {
+  if (closed_ || !conn_) return false;
+  return conn_->QueueMessage(stream_id_, message);
+}
+
+void ServerStream::Finish(const Status& st) {
+  if (closed_ || !conn_) return;
+  conn_->Finish(stream_id_, st);
+  closed_ = true;
+}
+
+// ------------------------- Server -------------------------
+
+Server::Server(std::string name) : name_(std::move(name)) {}
+
+Server::~Server() { Stop(); }
+
+void Server::AddUnary(const std::string& path, UnaryHandler h) { unary_[path] = std::move(h); }
+void Server::AddServerStream(const std::string& path, StreamHandler h) {
+  streams_[path] = std::move(h);
+}
+
+Status Server::Listen(const std::string& socket_path) {
+  socket_path_ = socket_path;
+  struct sockaddr_un addr;
+  if (socket_path.size() >= sizeof(addr.sun_path))
+    return InvalidArgument("socket path too long: " + socket_path);
+  unlink(socket_path.c_str());  // stale socket from a previous run (server.go:169)
+  listen_fd_ = socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  if (listen_fd_ < 0) return Internal(std::string("socket: ") + strerror(errno));
+  memset(&addr, 0, sizeof(addr));
+  addr.sun_family = AF_UNIX;
+  memcpy(addr.sun_path, socket_path.c_str(), socket_path.size());
+  if (bind(listen_fd_, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0) {
+    Status s = Unavailable("bind " + socket_path + ": " + strerror(errno));
+    close(listen_fd_);
+    listen_fd_ = -1;
+    return s;
+  }
+  if (listen(listen_fd_, 128) != 0) {
+    Status s = Unavailable("listen " + socket_path + ": " + strerror(errno));
+    close(listen_fd_);
+    listen_fd_ = -1;
+    return s;
+  }
+  return Status::Ok();
+}
+
+Status Server::Start(std::function<void()> on_fatal) {
+  if (listen_fd_ < 0) return FailedPrecondition("Start() before Listen()");
+  on_fatal_ = std::move(on_fatal);
+  epoll_fd_ = epoll_create1(EPOLL_CLOEXEC);
+  event_fd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  if (epoll_fd_ < 0 || event_fd_ < 0) return Internal("epoll/eventfd setup failed");
+  epoll_event ev{};
+  ev.events = EPOLLIN;
+  ev.data.fd = listen_fd_;
+  epoll_ctl(epoll_fd_, EPOLL_CTL_ADD, listen_fd_, &ev);
+  ev.data.fd = event_fd_;
+  epoll_ctl(epoll_fd_, EPOLL_CTL_ADD, event_fd_, &ev);
+  stopping_.store(false);
+  thread_ = std::thread([this] { LoopMain(); });
+  return Status::Ok();
+}
+
+void Server::Stop() {
+  if (thread_.joinable()) {
+    stopping_.store(true);
+    uint64_t one = 1;
+    ssize_t w = write(event_fd_, &one, sizeof(one));
+    (void)w;
+    thread_.join();
+  }
+  conns_.clear();  // loop is gone; safe to tear down here
+  {
+    std::lock_guard<std::mutex> lk(post_mu_);
+    posted_.clear();
+  }
+  if (listen_fd_ >= 0) {
+    close(listen_fd_);
+    listen_fd_ = -1;
+    if (!socket_path_.empty()) unlink(socket_path_.c_str());
+  }
+  if (epoll_fd_ >= 0) { close(epoll_fd_); epoll_fd_ = -1; }
+  if (event_fd_ >= 0) { close(event_fd_); event_fd_ = -1; }
+}
+
+void Server::Post(std::function<void()> fn) {
+  if (stopping_.load() || event_fd_ < 0) return;
+  {
+    std::lock_guard<std::mutex> lk(post_mu_);
+    posted_.push_back(std::move(fn));
+  }
+  uint64_t one = 1;
+  ssize_t w = write(event_fd_, &one, sizeof(one));
+  (void)w;
+}
+
+bool Server::OnLoopThread() const { return std::this_thread::get_id() == loop_tid_; }
+
+void Server::DrainPosted() {
+  uint64_t v;
+  ssize_t r = read(event_fd_, &v, sizeof(v));
+  (void)r;
+  std::vector<std::function<void()>> work;
+  {
+    std::lock_guard<std::mutex> lk(post_mu_);
+    work.swap(posted_);
+  }
+  for (auto& fn : work) fn();
+}
+
+void Server::AcceptAll() {
+  while (true) {
+    int fd = accept4(listen_fd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+    if (fd < 0) {
+      if (errno == EINTR) continue;
+      return;  // EAGAIN or transient (EMFILE...): retry on next readiness
+    }
+    auto conn = std::make_unique<ServerConn>(this, fd);
+    if (!conn->Init()) continue;
+    epoll_event ev{};
+    ev.events = EPOLLIN | (conn->want_epollout() ? static_cast<uint32_t>(EPOLLOUT) : 0u);
+    ev.data.fd = fd;
+    epoll_ctl(epoll_fd_, EPOLL_CTL_ADD, fd, &ev);
+    stats_.connections.fetch_add(1, std::memory_order_relaxed);
+    conns_[fd] = std::move(conn);
+  }
+}
+
+void Server::CloseConn(int fd) {
+  auto it = conns_.find(fd);
+  if (it == conns_.end()) return;
+  epoll_ctl(epoll_fd_, EPOLL_CTL_DEL, fd, nullptr);
+  conns_.erase(it);
+}
+
+Status Server::RunLoop() {
+  epoll_event events[64];
+  while (!stopping_.load()) {
+    int n = epoll_wait(epoll_fd_, events, 64, -1);
+    if (inject_failure_.exchange(false)) return Internal("injected loop failure");
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      return Internal(std::string("epoll_wait: ") + strerror(errno));
+    }
+    for (int i = 0; i < n; ++i) {
+      int fd = events[i].data.fd;
+      if (fd == listen_fd_) { AcceptAll(); continue; }
+      if (fd == event_fd_) { DrainPosted(); continue; }
+      auto it = conns_.find(fd);
+      if (it == conns_.end()) continue;
+      ServerConn* c = it->second.get();
+      bool ok = true;
+      if (events[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) ok = c->OnReadable();
+      else if (events[i].events & EPOLLOUT) ok = c->Flush();
+      if (!ok || c->Done()) { CloseConn(fd); continue; }
+    }
+    // Flush every connection (handlers and posted work may have queued data on
+    // any of them) and refresh EPOLLOUT interest.
+    std::vector<int> dead;
+    for (auto& [fd, c] : conns_) {
+      if (!c->Flush() || c->Done()) { dead.push_back(fd); continue; }
+      epoll_event ev{};
+      ev.events = EPOLLIN | (c->want_epollout() ? static_cast<uint32_t>(EPOLLOUT) : 0u);
+      ev.data.fd = fd;
+      epoll_ctl(epoll_fd_, EPOLL_CTL_MOD, fd, &ev);
+    }
+    for (int fd : dead) CloseConn(fd);
+  }
+  return Status::Ok();
+}
+
+void Server::LoopMain() {
+  loop_tid_ = std::this_thread::get_id();
+  using Clock = std::chrono::steady_clock;
+  auto last_crash = Clock::now();
+  int restarts = 0;
+  while (!stopping_.load()) {
+    LOG_DEBUG(kComp, "starting gRPC loop for '%s'", name_.c_str());
+    Status st = RunLoop();
+    if (st.ok() || stopping_.load()) break;
+    LOG_ERROR(kComp, "gRPC server for '%s' crashed: %s", name_.c_str(), st.ToString().c_str());
+    if (restarts > 5) {
+      LOG_ERROR(kComp, "gRPC server for '%s' has repeatedly crashed recently; giving up",
+                name_.c_str());
+      if (on_fatal_) on_fatal_();
+      break;
+    }
+    double since = std::chrono::duration<double>(Clock::now() - last_crash).count();
+    last_crash = Clock::now();
+    restarts = since > 3600 ? 1 : restarts + 1;
+  }
+}
+
+}  // namespace adp::grpc

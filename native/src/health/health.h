@@ -1,0 +1,93 @@
+// Device health: amdsmi event pump + RAS polling, with recovery.
+//
+// Parity: reference cmd/nvidia-device-plugin/nvidia.go:181-294 (checkHealth):
+//  * DP_DISABLE_HEALTHCHECKS: "all" or anything containing "xids" disables health
+//    checking; otherwise a comma-separated list of extra IDs to ignore
+//    (getAdditionalXids, nvidia.go:274-294 -- its 10 test vectors are pinned).
+//  * Application errors are ignored by default (Xids 13,31,43,45,68, nvidia.go:193-199).
+//  * Event wait with a 5000 ms timeout (nvidia.go:235).
+//
+// MI355X-native mapping (amdsmi_evt_notification_type_t):
+//  * GPU_PRE_RESET (3)  -> every device of that GPU goes Unhealthy.
+//  * GPU_POST_RESET (4) -> the GPU's devices go Healthy again. The reference has
+//    no recovery path at all (FIXME at server.go:259, defect B15).
+//  * VMFAULT (1) and THERMAL_THROTTLE (2) are application/environment events,
+//    the analogue of Xid 31/43 -> ignored by default.
+//  * The extra IDs in DP_DISABLE_HEALTHCHECKS are amdsmi event type numbers.
+//  * If event notification is unavailable (e.g. missing permissions) the device
+//    is NOT marked unhealthy (the reference does, nvidia.go:218-223, because on
+//    NVIDIA that meant an ancient GPU); health falls back to polling only.
+//  * Polling (every DP_HEALTH_POLL_MS, default 5000, 0 = off): a GPU that stops
+//    answering amdsmi or whose uncorrectable ECC count rises goes Unhealthy; an
+//    unresponsive GPU that answers again recovers.
+// One Monitor per daemon generation serves all plugins (amdsmi event delivery
+// is process-wide, so per-plugin pumps as in the reference would steal each
+// other's events).
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <vector>
+
+#include "inventory/inventory.h"
+#include "smi/smi.h"
+
+namespace adp::health {
+
+// getAdditionalXids semantics: split on ',', trim, keep valid unsigned values in order.
+std::vector<uint64_t> ParseAdditionalIds(std::string_view input);
+
+struct HealthConfig {
+  bool disabled = false;
+  std::set<uint32_t> ignored{smi::kEvtVmFault, smi::kEvtThermalThrottle};
+  int wait_ms = 5000;
+  int poll_interval_ms = 5000;
+  static HealthConfig FromEnv();
+  static HealthConfig FromValues(const char* disable_value, const char* poll_ms_value);
+};
+
+using Listener = std::function<void(int gpu, bool healthy, const std::string& reason)>;
+
+class Monitor {
+ public:
+  Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> snap, HealthConfig cfg);
+  ~Monitor();
+  void AddListener(Listener l);
+  Status Start();
+  void Stop();
+  bool events_enabled() const { return events_ok_; }
+
+  // Decision function, exposed for tests: how an event changes a GPU's health.
+  // Returns +1 (healthy), -1 (unhealthy), 0 (no change).
+  static int Classify(const HealthConfig& cfg, uint32_t event_type);
+
+ private:
+  void Run();
+  void Notify(int gpu, bool healthy, const std::string& reason);
+  void PollOnce();
+
+  smi::Library* lib_;
+  std::shared_ptr<const inventory::Snapshot> snap_;
+  HealthConfig cfg_;
+  std::vector<Listener> listeners_;
+  std::vector<void*> handles_;
+  bool events_ok_ = false;
+  std::thread thread_;
+  std::atomic<bool> stop_{false};
+  std::mutex mu_;
+  std::condition_variable cv_;
+  // Per-GPU polling state.
+  std::vector<uint64_t> ecc_baseline_;
+  std::vector<uint8_t> unresponsive_;
+  std::vector<uint8_t> ecc_failed_;
+};
+
+}  // namespace adp::health

@@ -1,0 +1,184 @@
+#include "inventory/inventory.h"
+
+#include <algorithm>
+#include <map>
+#include <set>
+#include <sys/stat.h>
+
+#include "common/log.h"
+#include "common/strings.h"
+
+namespace adp::inventory {
+namespace {
+
+constexpr const char* kComp = "inventory";
+
+std::string Upper(std::string s) {
+  for (auto& c : s) c = static_cast<char>(toupper(static_cast<unsigned char>(c)));
+  return s;
+}
+
+std::string ModeForCount(size_t n) {
+  switch (n) {
+    case 1: return "SPX";
+    case 2: return "DPX";
+    case 3: return "TPX";
+    case 4: return "QPX";
+    default: return "CPX";
+  }
+}
+
+// MI355X: 32 CUs per XCD. Used only when amdsmi cannot report XCD counts.
+constexpr uint32_t kCusPerXcd = 32;
+
+}  // namespace
+
+std::string RenderPath(uint32_t minor) { return "/dev/dri/renderD" + std::to_string(minor); }
+std::string CardPath(uint32_t minor) { return "/dev/dri/card" + std::to_string(minor); }
+uint64_t GbCeil(uint64_t mib) { return (mib + 1023) / 1024; }
+
+std::string PhysicalGpu::PartitionProfile() const {
+  if (compute_mode == "SPX" || partitions.empty()) return "";
+  const Partition& p = partitions.front();
+  uint32_t x = p.xcds;
+  if (!x && xcds && !partitions.empty()) x = xcds / static_cast<uint32_t>(partitions.size());
+  if (!x && p.cus) x = std::max<uint32_t>(1, p.cus / kCusPerXcd);
+  if (!x) x = 1;
+  return ToLower(compute_mode) + "-" + std::to_string(x) + "xcd." + std::to_string(GbCeil(p.vram_mib)) +
+         "gb";
+}
+
+std::vector<int> Snapshot::HandlesOf(int gpu) const {
+  std::vector<int> out;
+  for (const auto& p : gpus[gpu].partitions) out.push_back(p.handle);
+  return out;
+}
+
+int Snapshot::GpuOfHandle(int h) const {
+  for (const auto& g : gpus)
+    for (const auto& p : g.partitions)
+      if (p.handle == h) return g.index;
+  return -1;
+}
+
+Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo> procs,
+                                                  const BuildOptions& opt) {
+  auto snap = std::make_shared<Snapshot>();
+  snap->procs = std::move(procs);
+  // Group handles into physical GPUs by PCI domain:bus:device (partitions differ
+  // only in the function number); fall back to the UUID when no BDF is known.
+  std::vector<std::string> order;
+  std::map<std::string, std::vector<int>> groups;
+  for (size_t i = 0; i < snap->procs.size(); ++i) {
+    const auto& p = snap->procs[i];
+    std::string key = p.bdf_id ? "bdf:" + std::to_string(p.bdf_id & ~uint64_t{7}) : "uuid:" + p.uuid;
+    if (!groups.count(key)) order.push_back(key);
+    groups[key].push_back(static_cast<int>(i));
+  }
+
+  std::set<int> only(opt.only_gpus.begin(), opt.only_gpus.end());
+  int index = 0;
+  for (size_t gi = 0; gi < order.size(); ++gi) {
+    auto& handles = groups[order[gi]];
+    std::sort(handles.begin(), handles.end(), [&](int a, int b) {
+      return snap->procs[a].partition_id < snap->procs[b].partition_id;
+    });
+    if (!only.empty() && !only.count(static_cast<int>(gi))) continue;
+    const auto& first = snap->procs[handles.front()];
+    PhysicalGpu g;
+    g.index = index++;
+    g.node_index = static_cast<int>(gi);
+    g.uuid = first.uuid;
+    g.bdf = smi::FormatBdf(first.bdf_id & ~uint64_t{7});
+    g.numa = first.numa_node;
+    g.market_name = first.market_name;
+    g.compute_mode = Upper(first.compute_partition);
+    if (g.compute_mode.empty()) g.compute_mode = ModeForCount(handles.size());
+    g.memory_mode = Upper(first.memory_partition);
+
+    // Partition IDs must be unique and stable across restarts: the handle UUID
+    // when amdsmi reports distinct ones, else "<uuid>-p<partition>".
+    std::set<std::string> seen;
+    bool unique = true;
+    for (int h : handles)
+      if (!seen.insert(snap->procs[h].uuid).second) unique = false;
+    for (int h : handles) {
+      const auto& p = snap->procs[h];
+      Partition part;
+      part.handle = h;
+      part.partition_id = p.partition_id;
+      part.uuid = (unique || handles.size() == 1) ? p.uuid
+                                                   : p.uuid + "-p" + std::to_string(p.partition_id);
+      part.render_path = p.render_minor ? RenderPath(p.render_minor) : "";
+      if (opt.include_card_nodes && p.card_minor != 0xffffffffu) part.card_path = CardPath(p.card_minor);
+      part.numa = p.numa_node;
+      part.vram_mib = p.vram_mib;
+      part.xcds = p.xcd_count;
+      part.cus = p.num_cu;
+      g.vram_mib += p.vram_mib;
+      g.xcds += p.xcd_count;
+      g.cus += p.num_cu;
+      g.partitions.push_back(std::move(part));
+    }
+    (void)opt;
+    if (g.compute_mode == "SPX" && handles.size() > 1) {
+      LOG_WARN(kComp, "GPU %s reports SPX but has %zu handles; treating as %s", g.bdf.c_str(),
+               handles.size(), ModeForCount(handles.size()).c_str());
+      g.compute_mode = ModeForCount(handles.size());
+    }
+    snap->gpus.push_back(std::move(g));
+  }
+  size_t n = snap->gpus.size();
+  snap->gpu_links.assign(n * n, LinkClass::kUnknown);
+  snap->gpu_hops.assign(n * n, 0);
+  for (size_t a = 0; a < n; ++a) snap->gpu_links[a * n + a] = LinkClass::kSame;
+  return snap;
+}
+
+Result<std::shared_ptr<const Snapshot>> BuildSnapshot(smi::Library* lib, const BuildOptions& opt) {
+  auto procs = lib->Enumerate();
+  if (!procs.ok()) return procs.status();
+  auto grouped = GroupProcessors(std::move(*procs), opt);
+  if (!grouped.ok()) return grouped.status();
+  std::shared_ptr<Snapshot> snap = std::move(*grouped);
+  snap->smi_path = lib->path();
+  snap->smi_version = lib->Version();
+  size_t n = snap->gpus.size();
+  for (size_t a = 0; a < n; ++a) {
+    auto& ga = snap->gpus[a];
+    void* ha = snap->procs[ga.partitions.front().handle].handle;
+    ga.xgmi_links_down = lib->XgmiLinksDown(ha);
+    for (size_t b = 0; b < n; ++b) {
+      if (a == b) continue;
+      void* hb = snap->procs[snap->gpus[b].partitions.front().handle].handle;
+      smi::Link l = lib->GetLink(ha, hb);
+      LinkClass c = LinkClass::kUnknown;
+      if (l.valid) {
+        if (l.type == smi::LinkType::kXgmi) c = LinkClass::kXgmi;
+        else if (l.type == smi::LinkType::kInternal) c = LinkClass::kSame;
+        else if (l.type == smi::LinkType::kPcie)
+          c = (ga.numa >= 0 && ga.numa == snap->gpus[b].numa) ? LinkClass::kPcieSameNuma
+                                                               : LinkClass::kPcieCrossNuma;
+      }
+      snap->gpu_links[a * n + b] = c;
+      snap->gpu_hops[a * n + b] = l.hops;
+    }
+  }
+  struct stat st;
+  std::string kfd = PathJoin(opt.driver_root, "/dev/kfd");
+  if (stat(kfd.c_str(), &st) != 0)
+    LOG_WARN(kComp, "%s is not visible to the plugin; it is still passed to containers", kfd.c_str());
+  for (const auto& g : snap->gpus) {
+    LOG_INFO(kComp,
+             "GPU %d: %s bdf=%s numa=%d vram=%llu MiB mode=%s/%s partitions=%zu profile=%s "
+             "render=%s",
+             g.index, g.uuid.c_str(), g.bdf.c_str(), g.numa,
+             static_cast<unsigned long long>(g.vram_mib), g.compute_mode.c_str(),
+             g.memory_mode.empty() ? "?" : g.memory_mode.c_str(), g.partitions.size(),
+             g.PartitionProfile().empty() ? "-" : g.PartitionProfile().c_str(),
+             g.partitions.front().render_path.c_str());
+  }
+  return std::shared_ptr<const Snapshot>(snap);
+}
+
+}  // namespace adp::inventory

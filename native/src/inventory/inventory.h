@@ -1,0 +1,108 @@
+// Immutable node inventory: physical GPUs, their compute partitions, device
+// nodes, NUMA affinity, VRAM and the device-to-device link matrix.
+//
+// Parity (what the reference enumerates, and where):
+//  * Device{ID, Health, Topology(NUMA), Paths, Index, TotalMemory}:
+//    cmd/nvidia-device-plugin/nvidia.go:40-46, buildDevice nvidia.go:162-179.
+//  * Full GPUs: GpuDeviceManager.Devices nvidia.go:87-111 (index "i").
+//  * MIG slices: MigDeviceManager.Devices nvidia.go:114-150 (index "i:j"),
+//    capability-device resolution mig.go:121-226.
+//  * gpuallocator device graph: vendor/github.com/NVIDIA/go-gpuallocator/gpuallocator/device.go:15-95.
+//
+// MI355X-native design:
+//  * A physical GPU in SPX mode is one amdsmi processor handle with one render
+//    node. In DPX/QPX/CPX mode amdsmi reports one handle per compute partition,
+//    each with its own /dev/dri/renderD<N> and its own share of HBM3E. There are
+//    no capability files: a partition is handed to a container purely by its
+//    render node plus the shared /dev/kfd.
+//  * Partitions of one GPU share the PCI bus/device (function differs), which is
+//    how they are grouped back into a physical GPU.
+//  * The snapshot is built once per (re)start with cheap queries only and never
+//    touched again on the RPC path (the reference re-enumerates NVML on every
+//    GetPreferredAllocation call, defect B5).
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common/status.h"
+#include "smi/smi.h"
+
+namespace adp::inventory {
+
+struct Partition {
+  int handle = -1;            // index into Snapshot::procs
+  uint32_t partition_id = 0;  // amdsmi kfd current_partition_id
+  std::string uuid;           // stable device ID for this partition
+  std::string render_path;    // /dev/dri/renderD<N>
+  std::string card_path;      // /dev/dri/card<N> ("" if unknown)
+  int numa = -1;
+  uint64_t vram_mib = 0;      // this partition's share of HBM
+  uint32_t xcds = 0;
+  uint32_t cus = 0;
+};
+
+struct PhysicalGpu {
+  int index = 0;                  // position in Snapshot::gpus
+  int node_index = 0;             // node-local GPU index in amdsmi order (what "index" IDs use)
+  std::string uuid;               // ID of the whole GPU
+  std::string bdf;                // function-0 BDF
+  int numa = -1;
+  uint64_t vram_mib = 0;          // total HBM of the GPU
+  uint32_t xcds = 0;
+  uint32_t cus = 0;
+  std::string compute_mode;       // SPX / DPX / TPX / QPX / CPX ("SPX" if unknown)
+  std::string memory_mode;        // NPS1 / NPS2 / ... ("" if unknown)
+  std::string market_name;
+  std::vector<Partition> partitions;  // one per amdsmi handle; sorted by partition_id
+  int xgmi_links_down = 0;
+
+  bool partitioned() const { return compute_mode != "SPX"; }
+  // Resource name of this GPU's partitions, e.g. "cpx-1xcd.36gb" (empty if SPX).
+  std::string PartitionProfile() const;
+};
+
+// Link classification between two physical GPUs, the analogue of NVML's P2P
+// level + NVLink count (vendor/.../nvml/nvml.go:132-154,592-658).
+enum class LinkClass { kSame = 0, kXgmi = 1, kPcieSameNuma = 2, kPcieCrossNuma = 3, kUnknown = 4 };
+
+struct Snapshot {
+  std::vector<smi::ProcessorInfo> procs;   // raw amdsmi handles
+  std::vector<PhysicalGpu> gpus;
+  // gpu_links[a * gpus.size() + b]
+  std::vector<LinkClass> gpu_links;
+  std::vector<uint64_t> gpu_hops;
+  std::string smi_path;
+  std::string smi_version;
+
+  LinkClass Link(int a, int b) const { return gpu_links[a * gpus.size() + b]; }
+  uint64_t Hops(int a, int b) const { return gpu_hops[a * gpus.size() + b]; }
+  // amdsmi handle indices belonging to physical GPU `gpu`.
+  std::vector<int> HandlesOf(int gpu) const;
+  // Physical GPU that owns amdsmi handle index `h` (-1 if none).
+  int GpuOfHandle(int h) const;
+};
+
+struct BuildOptions {
+  std::string driver_root = "/";
+  // Restrict to these physical GPU indices (empty = all). Used by the benchmark
+  // to serve exactly N GPUs of a node, and by operators to carve a node.
+  std::vector<int> only_gpus;
+  bool include_card_nodes = false;
+};
+
+// Builds a snapshot from the loaded library (one enumeration + link queries).
+Result<std::shared_ptr<const Snapshot>> BuildSnapshot(smi::Library* lib, const BuildOptions& opt);
+
+// Exposed for tests: grouping + profile naming on raw processor records.
+Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo> procs,
+                                                  const BuildOptions& opt);
+
+std::string RenderPath(uint32_t minor);
+std::string CardPath(uint32_t minor);
+// ceil(mib / 1024): the reference's GB rounding for MIG names (mig-strategy.go:185).
+uint64_t GbCeil(uint64_t mib);
+
+}  // namespace adp::inventory

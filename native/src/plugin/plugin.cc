@@ -1,0 +1,415 @@
+#include "plugin/plugin.h"
+
+#include <algorithm>
+#include <chrono>
+#include <future>
+
+#include "common/log.h"
+#include "common/strings.h"
+#include "proto/messages.h"
+#include "proto/wire.h"
+
+namespace adp::plugin {
+namespace {
+
+constexpr const char* kComp = "plugin";
+constexpr const char* kSvc = "/v1beta1.DevicePlugin/";
+
+uint64_t NowNs() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+}  // namespace
+
+bool ParseDeviceListStrategy(std::string_view s, DeviceListStrategy* out) {
+  if (s == "envvar") { *out = DeviceListStrategy::kEnvvar; return true; }
+  if (s == "volume-mounts") { *out = DeviceListStrategy::kVolumeMounts; return true; }
+  if (s == "cdi-annotations") { *out = DeviceListStrategy::kCdiAnnotations; return true; }
+  if (s == "cdi-cri") { *out = DeviceListStrategy::kCdiCri; return true; }
+  return false;
+}
+
+bool ParseDeviceIdStrategy(std::string_view s, DeviceIdStrategy* out) {
+  if (s == "uuid") { *out = DeviceIdStrategy::kUuid; return true; }
+  if (s == "index") { *out = DeviceIdStrategy::kIndex; return true; }
+  return false;
+}
+
+const char* DeviceListStrategyName(DeviceListStrategy s) {
+  switch (s) {
+    case DeviceListStrategy::kEnvvar: return "envvar";
+    case DeviceListStrategy::kVolumeMounts: return "volume-mounts";
+    case DeviceListStrategy::kCdiAnnotations: return "cdi-annotations";
+    case DeviceListStrategy::kCdiCri: return "cdi-cri";
+  }
+  return "?";
+}
+
+const char* DeviceIdStrategyName(DeviceIdStrategy s) {
+  return s == DeviceIdStrategy::kIndex ? "index" : "uuid";
+}
+
+Plugin::Plugin(std::shared_ptr<const inventory::Snapshot> snap, strategy::PluginSpec spec,
+               PluginOptions opts)
+    : snap_(std::move(snap)), spec_(std::move(spec)), opts_(std::move(opts)) {
+  if (opts_.kubelet_socket.empty()) opts_.kubelet_socket = PathJoin(opts_.plugin_dir, "kubelet.sock");
+  BuildUnits();
+}
+
+Plugin::~Plugin() { Stop(); }
+
+std::string Plugin::socket_path() const { return PathJoin(opts_.plugin_dir, spec_.socket_name); }
+
+void Plugin::BuildUnits() {
+  const auto& v = spec_.variant;
+  replicated_ = v.replicas > 1 || v.auto_replicas;
+  for (const auto& ref : spec_.devices) {
+    const auto& g = snap_->gpus[ref.gpu];
+    Unit u;
+    u.gpu = ref.gpu;
+    if (ref.partition < 0) {
+      u.id = g.uuid;
+      u.index = std::to_string(g.node_index);
+      u.numa = g.numa;
+      u.vram_mib = g.vram_mib;
+      for (const auto& p : g.partitions) {
+        if (!p.render_path.empty()) u.paths.push_back(p.render_path);
+        if (!p.card_path.empty()) u.paths.push_back(p.card_path);
+        u.handles.push_back(p.handle);
+      }
+    } else {
+      const auto& p = g.partitions[ref.partition];
+      u.id = p.uuid;
+      u.index = std::to_string(g.node_index) + ":" + std::to_string(ref.partition);
+      u.numa = p.numa >= 0 ? p.numa : g.numa;
+      u.vram_mib = p.vram_mib;
+      if (!p.render_path.empty()) u.paths.push_back(p.render_path);
+      if (!p.card_path.empty()) u.paths.push_back(p.card_path);
+      u.handles.push_back(p.handle);
+    }
+    // Auto replicas: one per `auto_replica_unit_mib` of this device's own memory
+    // (server.go:100-103; per-partition memory fixes B4). At least one.
+    u.replicas = v.auto_replicas
+                     ? static_cast<unsigned>(std::max<uint64_t>(1, u.vram_mib / opts_.auto_replica_unit_mib))
+                     : std::max(1u, v.replicas);
+    u.visible_id = opts_.id_strategy == DeviceIdStrategy::kIndex ? u.index : u.id;
+    for (const auto& path : u.paths) {
+      pb::DeviceSpec ds{path, PathJoin(opts_.driver_root, path), "rw"};
+      std::string b;
+      pb::Encode(ds, &b);
+      pb::PutLen(&u.spec_bytes, 3, b);
+    }
+    pb::Mount m{PathJoin(kVolumeMountRoot, u.visible_id), kVolumeMountHostPath, false};
+    std::string mb;
+    pb::Encode(m, &mb);
+    pb::PutLen(&u.mount_bytes, 2, mb);
+    units_.push_back(std::move(u));
+  }
+  for (size_t i = 0; i < units_.size(); ++i) {
+    const auto& u = units_[i];
+    unit_by_id_[u.id] = static_cast<int>(i);
+    if (replicated_) {
+      LOG_INFO(kComp, "replicating device %s (%s, %llu MiB) %u times", u.id.c_str(), u.index.c_str(),
+               static_cast<unsigned long long>(u.vram_mib), u.replicas);
+      for (unsigned r = 0; r < u.replicas; ++r) {
+        advertised_.push_back(alloc::ReplicaId(u.id, r));
+        advertised_unit_.push_back(static_cast<int>(i));
+      }
+    } else {
+      advertised_.push_back(u.id);
+      advertised_unit_.push_back(static_cast<int>(i));
+    }
+  }
+  advertised_index_.reserve(advertised_.size() * 2);
+  for (size_t i = 0; i < advertised_.size(); ++i) {
+    if (advertised_[i].size() > 63)
+      LOG_WARN(kComp, "device ID '%s' exceeds 63 characters", advertised_[i].c_str());
+    advertised_index_[advertised_[i]] = advertised_unit_[i];
+  }
+  pb::DeviceSpec kfd{"/dev/kfd", PathJoin(opts_.driver_root, "/dev/kfd"), "rw"};
+  std::string kb;
+  pb::Encode(kfd, &kb);
+  pb::PutLen(&kfd_spec_bytes_, 3, kb);
+  graph_ = alloc::DeviceGraph(*snap_, spec_.devices);
+  healthy_.assign(units_.size(), 1);
+  RebuildListAndWatch();
+}
+
+void Plugin::RebuildListAndWatch() {
+  // Encode every advertised ID once per health transition; sends reuse the bytes.
+  std::string out;
+  out.reserve(advertised_.size() * 72);
+  std::string dev;
+  for (size_t i = 0; i < advertised_.size(); ++i) {
+    const Unit& u = units_[advertised_unit_[i]];
+    pb::Device d;
+    d.id = advertised_[i];
+    d.health = healthy_[advertised_unit_[i]] ? pb::kHealthy : pb::kUnhealthy;
+    if (u.numa >= 0) {
+      d.has_topology = true;
+      d.numa_nodes.push_back(u.numa);
+    }
+    dev.clear();
+    pb::Encode(d, &dev);
+    pb::PutLen(&out, 1, dev);
+  }
+  law_bytes_ = std::move(out);
+}
+
+Status Plugin::HandleGetOptions(std::string_view, std::string* resp) {
+  // Preferred allocation is always offered: replicas use the prioritizer, whole
+  // GPUs and partitions use the topology policy (server.go:243-248 offered it
+  // only with a policy or replicas).
+  pb::DevicePluginOptions o;
+  o.pre_start_required = false;
+  o.get_preferred_allocation_available = true;
+  pb::Encode(o, resp);
+  return Status::Ok();
+}
+
+Status Plugin::HandlePreStart(std::string_view req, std::string*) {
+  pb::PreStartContainerRequest r;
+  return pb::Decode(req, &r);
+}
+
+Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
+  uint64_t t0 = NowNs();
+  pb::AllocateRequest r;
+  ADP_RETURN_IF_ERROR(pb::Decode(req, &r));
+  std::vector<int> us;
+  std::string c, joined;
+  for (const auto& ids : r.container_requests) {
+    us.clear();
+    for (const auto& id : ids) {
+      auto it = advertised_index_.find(id);
+      if (it == advertised_index_.end())
+        return InvalidArgument("invalid allocation request for '" + spec_.resource_name +
+                               "': unknown device: " + id);
+      us.push_back(it->second);
+    }
+    // Unique physical devices. uuid strategy: sorted by ID (stripReplicas order,
+    // server.go:325); index strategy: enumeration order (server.go:406-411).
+    std::sort(us.begin(), us.end());
+    us.erase(std::unique(us.begin(), us.end()), us.end());
+    if (opts_.id_strategy == DeviceIdStrategy::kUuid)
+      std::sort(us.begin(), us.end(), [&](int a, int b) { return units_[a].id < units_[b].id; });
+
+    c.clear();
+    joined.clear();
+    for (size_t i = 0; i < us.size(); ++i) {
+      if (i) joined += ',';
+      joined += units_[us[i]].visible_id;
+    }
+    switch (opts_.list_strategy) {
+      case DeviceListStrategy::kEnvvar:
+        pb::PutMapEntry(&c, 1, opts_.envvar, joined);
+        break;
+      case DeviceListStrategy::kVolumeMounts:
+        pb::PutMapEntry(&c, 1, opts_.envvar, kVolumeMountRoot);
+        for (int u : us) c += units_[u].mount_bytes;
+        break;
+      case DeviceListStrategy::kCdiAnnotations: {
+        if (us.empty()) break;
+        std::string names;
+        for (size_t i = 0; i < us.size(); ++i) {
+          if (i) names += ',';
+          names += std::string(kCdiVendorClass) + "=" + units_[us[i]].visible_id;
+        }
+        pb::PutMapEntry(&c, 4, "cdi.k8s.io/amd-gpu-device-plugin_" + units_[us[0]].visible_id, names);
+        break;
+      }
+      case DeviceListStrategy::kCdiCri:
+        for (int u : us) {
+          std::string n;
+          pb::PutStr(&n, 1, std::string(kCdiVendorClass) + "=" + units_[u].visible_id);
+          pb::PutLen(&c, 5, n);
+        }
+        break;
+    }
+    if (opts_.pass_device_specs) {
+      c += kfd_spec_bytes_;
+      for (int u : us) c += units_[u].spec_bytes;
+    }
+    pb::PutLen(resp, 1, c);
+    LOG_DEBUG(kComp, "allocate '%s': %zu IDs -> [%s]", spec_.resource_name.c_str(), ids.size(),
+              joined.c_str());
+  }
+  uint64_t dt = NowNs() - t0;
+  stats_.allocate_calls.fetch_add(1, std::memory_order_relaxed);
+  stats_.allocate_ns_total.fetch_add(dt, std::memory_order_relaxed);
+  uint64_t prev = stats_.allocate_ns_max.load(std::memory_order_relaxed);
+  while (dt > prev && !stats_.allocate_ns_max.compare_exchange_weak(prev, dt)) {}
+  return Status::Ok();
+}
+
+Status Plugin::HandlePreferred(std::string_view req, std::string* resp) {
+  pb::PreferredAllocationRequest r;
+  ADP_RETURN_IF_ERROR(pb::Decode(req, &r));
+  pb::PreferredAllocationResponse out;
+  stats_.preferred_calls.fetch_add(1, std::memory_order_relaxed);
+  for (const auto& cr : r.container_requests) {
+    if (replicated_) {
+      auto res = alloc::PrioritizeDevices(cr.available, cr.must_include, cr.allocation_size,
+                                          opts_.replica_policy);
+      if (!res.ok()) return res.status();
+      if (res->non_unique) LOG_DEBUG(kComp, "ignoring: %s", alloc::kNonUniqueMessage);
+      out.container_responses.push_back(std::move(res->ids));
+      continue;
+    }
+    std::vector<int> avail, must;
+    for (const auto& id : cr.available) {
+      auto it = advertised_index_.find(id);
+      if (it == advertised_index_.end())
+        return InvalidArgument("unable to retrieve list of available devices: unknown device " + id);
+      avail.push_back(it->second);
+    }
+    for (const auto& id : cr.must_include) {
+      auto it = advertised_index_.find(id);
+      if (it == advertised_index_.end())
+        return InvalidArgument("unable to retrieve list of required devices: unknown device " + id);
+      must.push_back(it->second);
+    }
+    std::vector<std::string> ids;
+    for (int u : alloc::BestEffortAllocate(graph_, avail, must, cr.allocation_size))
+      ids.push_back(units_[u].id);  // advertised ID (no replica suffix here), fixes B6
+    out.container_responses.push_back(std::move(ids));
+  }
+  pb::Encode(out, resp);
+  return Status::Ok();
+}
+
+Status Plugin::Register() {
+  auto ch = grpc::Channel::Dial(opts_.kubelet_socket, opts_.dial_timeout_ms);
+  if (!ch.ok()) return ch.status();
+  pb::RegisterRequest rr;
+  rr.version = pb::kApiVersion;
+  rr.endpoint = BaseName(socket_path());
+  rr.resource_name = spec_.resource_name;
+  rr.has_options = true;
+  rr.options.get_preferred_allocation_available = true;
+  std::string resp;
+  return (*ch)->Unary("/v1beta1.Registration/Register", pb::Encode(rr), &resp,
+                      opts_.dial_timeout_ms);
+}
+
+Status Plugin::Start(std::function<void()> on_fatal) {
+  if (server_) return FailedPrecondition("plugin already started");
+  server_ = std::make_unique<grpc::Server>(spec_.resource_name);
+  server_->AddUnary(std::string(kSvc) + "GetDevicePluginOptions",
+                    [this](std::string_view q, std::string* r) { return HandleGetOptions(q, r); });
+  server_->AddUnary(std::string(kSvc) + "Allocate",
+                    [this](std::string_view q, std::string* r) { return HandleAllocate(q, r); });
+  server_->AddUnary(std::string(kSvc) + "GetPreferredAllocation",
+                    [this](std::string_view q, std::string* r) { return HandlePreferred(q, r); });
+  server_->AddUnary(std::string(kSvc) + "PreStartContainer",
+                    [this](std::string_view q, std::string* r) { return HandlePreStart(q, r); });
+  server_->AddServerStream(std::string(kSvc) + "ListAndWatch",
+                           [this](std::string_view, std::shared_ptr<grpc::ServerStream> s) {
+                             law_streams_.push_back(s);
+                             s->Send(law_bytes_);
+                             stats_.law_sends.fetch_add(1, std::memory_order_relaxed);
+                             return Status::Ok();
+                           });
+  Status st = server_->Listen(socket_path());
+  if (st.ok()) st = server_->Start(std::move(on_fatal));
+  if (st.ok()) {
+    // Block until the server answers, like the reference's self-dial (server.go:207-213).
+    auto probe = grpc::Channel::Dial(socket_path(), opts_.dial_timeout_ms);
+    if (!probe.ok()) st = probe.status();
+  }
+  if (!st.ok()) {
+    LOG_ERROR(kComp, "could not start device plugin for '%s': %s", spec_.resource_name.c_str(),
+              st.ToString().c_str());
+    server_->Stop();
+    server_.reset();
+    return st;
+  }
+  LOG_INFO(kComp, "serving '%s' on %s (%zu devices, %zu advertised)", spec_.resource_name.c_str(),
+           socket_path().c_str(), units_.size(), advertised_.size());
+  if (opts_.register_with_kubelet) {
+    st = Register();
+    if (!st.ok()) {
+      LOG_ERROR(kComp, "could not register device plugin '%s' with kubelet at %s: %s",
+                spec_.resource_name.c_str(), opts_.kubelet_socket.c_str(), st.ToString().c_str());
+      Stop();
+      return st;
+    }
+    LOG_INFO(kComp, "registered device plugin for '%s' with kubelet", spec_.resource_name.c_str());
+  }
+  return Status::Ok();
+}
+
+void Plugin::Stop() {
+  if (!server_) return;
+  LOG_INFO(kComp, "stopping '%s' on %s", spec_.resource_name.c_str(), socket_path().c_str());
+  // End open ListAndWatch streams cleanly (the reference returns nil on stop).
+  auto done = std::make_shared<std::promise<void>>();
+  auto fut = done->get_future();
+  server_->Post([this, done] {
+    for (auto& s : law_streams_) s->Finish(Status::Ok());
+    law_streams_.clear();
+    done->set_value();
+  });
+  fut.wait_for(std::chrono::milliseconds(500));
+  server_->Stop();
+  server_.reset();
+  law_streams_.clear();
+}
+
+void Plugin::ApplyHealth(const std::vector<int>& us, bool healthy, const std::string& reason) {
+  bool changed = false;
+  for (int u : us) {
+    if (static_cast<bool>(healthy_[u]) == healthy) continue;
+    healthy_[u] = healthy ? 1 : 0;
+    changed = true;
+    LOG_INFO(kComp, "'%s' device %s marked %s: %s", spec_.resource_name.c_str(), units_[u].id.c_str(),
+             healthy ? "healthy" : "unhealthy", reason.c_str());
+  }
+  if (!changed) return;
+  RebuildListAndWatch();
+  std::vector<std::shared_ptr<grpc::ServerStream>> live;
+  for (auto& s : law_streams_) {
+    if (s->closed()) continue;
+    if (s->Send(law_bytes_)) stats_.law_sends.fetch_add(1, std::memory_order_relaxed);
+    live.push_back(s);
+  }
+  law_streams_.swap(live);
+}
+
+void Plugin::SetHandleHealth(int handle, bool healthy, const std::string& reason) {
+  std::vector<int> us;
+  for (size_t i = 0; i < units_.size(); ++i)
+    for (int h : units_[i].handles)
+      if (h == handle) us.push_back(static_cast<int>(i));
+  if (us.empty()) return;
+  if (server_) server_->Post([this, us, healthy, reason] { ApplyHealth(us, healthy, reason); });
+  else ApplyHealth(us, healthy, reason);
+}
+
+void Plugin::SetGpuHealth(int gpu, bool healthy, const std::string& reason) {
+  std::vector<int> us;
+  for (size_t i = 0; i < units_.size(); ++i)
+    if (units_[i].gpu == gpu) us.push_back(static_cast<int>(i));
+  if (us.empty()) return;
+  if (server_) server_->Post([this, us, healthy, reason] { ApplyHealth(us, healthy, reason); });
+  else ApplyHealth(us, healthy, reason);
+}
+
+std::string Plugin::StatsJson() const {
+  uint64_t n = stats_.allocate_calls.load();
+  double avg = n ? stats_.allocate_ns_total.load() / 1e3 / n : 0.0;
+  char buf[512];
+  snprintf(buf, sizeof(buf),
+           "{\"resource\": \"%s\", \"devices\": %zu, \"advertised\": %zu, \"allocate_calls\": %llu, "
+           "\"allocate_handler_avg_us\": %.3f, \"allocate_handler_max_us\": %.3f, "
+           "\"preferred_calls\": %llu, \"law_sends\": %llu}",
+           JsonEscape(spec_.resource_name).c_str(), units_.size(), advertised_.size(),
+           static_cast<unsigned long long>(n), avg, stats_.allocate_ns_max.load() / 1e3,
+           static_cast<unsigned long long>(stats_.preferred_calls.load()),
+           static_cast<unsigned long long>(stats_.law_sends.load()));
+  return buf;
+}
+
+}  // namespace adp::plugin

@@ -1,0 +1,156 @@
+// One kubelet device plugin: a resource name, its devices (+ time-slice replicas)
+// and the v1beta1 DevicePlugin gRPC service on its own Unix socket.
+//
+// Parity: reference cmd/nvidia-device-plugin/server.go
+//   NvidiaDevicePlugin fields :56-71, initialize/replicas :95-116, Start :129-151,
+//   Stop :154-165, Register :218-240, GetDevicePluginOptions :243-248,
+//   ListAndWatch :251-265, GetPreferredAllocation :268-313, Allocate :316-353,
+//   PreStartContainer :356-358, device-list/ID strategies :37-53,397-441,
+//   DeviceSpecs :443-480.
+//
+// MI355X-native design:
+//  * Containers get GPUs as device nodes: /dev/kfd (shared compute interface)
+//    plus each allocated GPU's/partition's /dev/dri/renderD<N>. There is no
+//    container-runtime hook, so DeviceSpecs are the primary mechanism; the
+//    AMD_VISIBLE_DEVICES env / volume-mount list is kept for deviceListStrategy
+//    compatibility (and the AMD container toolkit).
+//  * Everything the RPCs need is precomputed at Start(): replica-ID -> device
+//    hash map, pre-encoded DeviceSpec / Mount protobuf fragments per device, the
+//    encoded ListAndWatch response, the topology graph. Allocate is O(k) hash
+//    lookups plus byte concatenation with zero SMI calls (reference: linear
+//    scans over all replicas, server.go:377-394, and os.Stat per call :453-462).
+//  * Mutable state (health, open ListAndWatch streams) lives on the gRPC loop
+//    thread; other threads reach it through Server::Post, so there are no locks
+//    on the RPC path and no data races (reference defects B13/B14).
+//  * Health propagates to every replica of a device and recovers (B1, B15).
+#pragma once
+
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "alloc/replicas.h"
+#include "alloc/topology.h"
+#include "grpc/grpc.h"
+#include "inventory/inventory.h"
+#include "strategy/strategy.h"
+
+namespace adp::plugin {
+
+enum class DeviceListStrategy { kEnvvar, kVolumeMounts, kCdiAnnotations, kCdiCri };
+enum class DeviceIdStrategy { kUuid, kIndex };
+bool ParseDeviceListStrategy(std::string_view s, DeviceListStrategy* out);
+bool ParseDeviceIdStrategy(std::string_view s, DeviceIdStrategy* out);
+const char* DeviceListStrategyName(DeviceListStrategy s);
+const char* DeviceIdStrategyName(DeviceIdStrategy s);
+
+inline constexpr const char* kDefaultPluginDir = "/var/lib/kubelet/device-plugins/";
+inline constexpr const char* kVisibleDevicesEnv = "AMD_VISIBLE_DEVICES";
+inline constexpr const char* kVolumeMountHostPath = "/dev/null";
+inline constexpr const char* kVolumeMountRoot = "/var/run/amd-container-devices";
+inline constexpr const char* kCdiVendorClass = "amd.com/gpu";
+
+struct PluginOptions {
+  std::string plugin_dir = kDefaultPluginDir;
+  std::string kubelet_socket;  // "" -> plugin_dir + "kubelet.sock"
+  DeviceListStrategy list_strategy = DeviceListStrategy::kEnvvar;
+  DeviceIdStrategy id_strategy = DeviceIdStrategy::kUuid;
+  bool pass_device_specs = true;
+  std::string driver_root = "/";
+  std::string envvar = kVisibleDevicesEnv;
+  alloc::ReplicaPolicy replica_policy = alloc::ReplicaPolicy::kSpread;
+  uint64_t auto_replica_unit_mib = 1000;  // reference: TotalMemory / 1000 (server.go:102)
+  int dial_timeout_ms = 5000;             // server.go:208,219
+  bool register_with_kubelet = true;
+};
+
+// One allocatable device (whole GPU or partition) after snapshot resolution.
+struct Unit {
+  std::string id;          // advertised physical ID
+  std::string index;       // "<gpu>" or "<gpu>:<partition>"
+  int numa = -1;
+  uint64_t vram_mib = 0;
+  std::vector<std::string> paths;  // device nodes inside the container
+  std::vector<int> handles;        // amdsmi handle indices (health routing)
+  int gpu = 0;
+  std::string visible_id;          // id or index, per DeviceIdStrategy
+  std::string spec_bytes;          // pre-encoded ContainerAllocateResponse.devices entries
+  std::string mount_bytes;         // pre-encoded ContainerAllocateResponse.mounts entry
+  unsigned replicas = 1;
+};
+
+struct RpcStats {
+  std::atomic<uint64_t> allocate_calls{0};
+  std::atomic<uint64_t> allocate_ns_total{0};
+  std::atomic<uint64_t> allocate_ns_max{0};
+  std::atomic<uint64_t> preferred_calls{0};
+  std::atomic<uint64_t> law_sends{0};
+};
+
+class Plugin {
+ public:
+  Plugin(std::shared_ptr<const inventory::Snapshot> snap, strategy::PluginSpec spec,
+         PluginOptions opts);
+  ~Plugin();
+  Plugin(const Plugin&) = delete;
+  Plugin& operator=(const Plugin&) = delete;
+
+  const std::string& resource_name() const { return spec_.resource_name; }
+  std::string socket_path() const;
+  size_t device_count() const { return units_.size(); }
+  size_t advertised_count() const { return advertised_.size(); }
+  bool replicated() const { return replicated_; }
+  const std::vector<Unit>& units() const { return units_; }
+  const std::vector<std::string>& advertised_ids() const { return advertised_; }
+
+  // Serve -> self-dial -> Register. On failure everything is torn down again.
+  Status Start(std::function<void()> on_fatal = nullptr);
+  void Stop();
+  bool running() const { return server_ != nullptr; }
+
+  // Thread-safe. Marks every device that contains amdsmi handle `handle`.
+  void SetHandleHealth(int handle, bool healthy, const std::string& reason);
+  // Thread-safe. Marks every device of physical GPU `gpu`.
+  void SetGpuHealth(int gpu, bool healthy, const std::string& reason);
+
+  const RpcStats& stats() const { return stats_; }
+  std::string StatsJson() const;
+
+  // Handlers (public for in-process tests and benchmarks; loop thread only when serving).
+  Status HandleGetOptions(std::string_view req, std::string* resp);
+  Status HandleAllocate(std::string_view req, std::string* resp);
+  Status HandlePreferred(std::string_view req, std::string* resp);
+  Status HandlePreStart(std::string_view req, std::string* resp);
+
+ private:
+  void BuildUnits();
+  void RebuildListAndWatch();
+  void ApplyHealth(const std::vector<int>& units, bool healthy, const std::string& reason);
+  Status Register();
+
+  std::shared_ptr<const inventory::Snapshot> snap_;
+  strategy::PluginSpec spec_;
+  PluginOptions opts_;
+  bool replicated_ = false;
+
+  std::vector<Unit> units_;
+  std::unordered_map<std::string, int> unit_by_id_;
+  std::vector<std::string> advertised_;       // advertised IDs (replicas or plain)
+  std::vector<int> advertised_unit_;
+  std::unordered_map<std::string, int> advertised_index_;  // advertised ID -> unit
+  std::string kfd_spec_bytes_;
+  alloc::DeviceGraph graph_;
+
+  // Loop-thread state.
+  std::vector<uint8_t> healthy_;
+  std::string law_bytes_;
+  std::vector<std::shared_ptr<grpc::ServerStream>> law_streams_;
+
+  std::unique_ptr<grpc::Server> server_;
+  RpcStats stats_;
+};
+
+}  // namespace adp::plugin

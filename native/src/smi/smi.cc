@@ -1,0 +1,315 @@
+#include "smi/smi.h"
+
+#include <amd_smi/amdsmi.h>
+#include <dlfcn.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "common/log.h"
+
+namespace adp::smi {
+
+namespace {
+constexpr const char* kComp = "smi";
+}
+
+// Function table resolved with dlsym. Required entries fail Open(); optional ones
+// degrade a feature (e.g. no topology -> flat link matrix).
+struct Library::Fns {
+  decltype(&amdsmi_init) init = nullptr;
+  decltype(&amdsmi_shut_down) shut_down = nullptr;
+  decltype(&amdsmi_get_socket_handles) socket_handles = nullptr;
+  decltype(&amdsmi_get_processor_handles) processor_handles = nullptr;
+  decltype(&amdsmi_get_processor_type) processor_type = nullptr;
+  decltype(&amdsmi_get_gpu_device_uuid) uuid = nullptr;
+  decltype(&amdsmi_get_gpu_device_bdf) bdf = nullptr;
+  decltype(&amdsmi_get_gpu_enumeration_info) enum_info = nullptr;
+  decltype(&amdsmi_get_gpu_topo_numa_affinity) numa = nullptr;
+  decltype(&amdsmi_get_gpu_vram_info) vram_info = nullptr;
+  decltype(&amdsmi_get_gpu_memory_total) memory_total = nullptr;
+  decltype(&amdsmi_get_gpu_compute_partition) compute_partition = nullptr;
+  decltype(&amdsmi_get_gpu_memory_partition) memory_partition = nullptr;
+  decltype(&amdsmi_get_gpu_kfd_info) kfd_info = nullptr;
+  decltype(&amdsmi_get_gpu_asic_info) asic_info = nullptr;
+  decltype(&amdsmi_get_gpu_xcd_counter) xcd_counter = nullptr;
+  decltype(&amdsmi_topo_get_link_type) link_type = nullptr;
+  decltype(&amdsmi_topo_get_link_weight) link_weight = nullptr;
+  decltype(&amdsmi_get_gpu_xgmi_link_status) xgmi_link_status = nullptr;
+  decltype(&amdsmi_init_gpu_event_notification) evt_init = nullptr;
+  decltype(&amdsmi_set_gpu_event_notification_mask) evt_mask = nullptr;
+  decltype(&amdsmi_get_gpu_event_notification) evt_get = nullptr;
+  decltype(&amdsmi_stop_gpu_event_notification) evt_stop = nullptr;
+  decltype(&amdsmi_get_gpu_total_ecc_count) ecc_total = nullptr;
+  decltype(&amdsmi_status_code_to_string) status_string = nullptr;
+  decltype(&amdsmi_get_lib_version) lib_version = nullptr;
+};
+
+namespace {
+
+template <typename T>
+void Resolve(void* dl, const char* name, T* out) {
+  *out = reinterpret_cast<T>(dlsym(dl, name));
+}
+
+}  // namespace
+
+std::string FormatBdf(uint64_t bdf_id) {
+  amdsmi_bdf_t b;
+  b.as_uint = bdf_id;
+  char buf[32];
+  snprintf(buf, sizeof(buf), "%04llx:%02x:%02x.%x",
+           static_cast<unsigned long long>(b.domain_number), static_cast<unsigned>(b.bus_number),
+           static_cast<unsigned>(b.device_number), static_cast<unsigned>(b.function_number));
+  return buf;
+}
+
+uint64_t EventMask(uint32_t event_type) { return AMDSMI_EVENT_MASK_FROM_INDEX(event_type); }
+
+Library::~Library() {
+  if (initialized_ && f_ && f_->shut_down) f_->shut_down();
+  if (dl_) dlclose(dl_);
+}
+
+Result<std::unique_ptr<Library>> Library::Open(const std::string& path,
+                                               const std::string& rocm_root) {
+  std::vector<std::string> candidates;
+  if (!path.empty()) {
+    candidates.push_back(path);
+  } else {
+    if (const char* e = std::getenv("AMD_SMI_LIB"); e && *e) candidates.push_back(e);
+    candidates.push_back("libamd_smi.so");
+    candidates.push_back("libamd_smi.so.26");
+    candidates.push_back(rocm_root + "/lib/libamd_smi.so");
+  }
+  std::unique_ptr<Library> lib(new Library());
+  std::string errors;
+  for (const auto& c : candidates) {
+    lib->dl_ = dlopen(c.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (lib->dl_) { lib->path_ = c; break; }
+    const char* e = dlerror();
+    errors += (errors.empty() ? "" : "; ") + std::string(e ? e : c);
+    if (!path.empty()) break;
+  }
+  if (!lib->dl_) return Unavailable("cannot load libamd_smi: " + errors);
+
+  auto f = std::make_unique<Fns>();
+  void* dl = lib->dl_;
+  Resolve(dl, "amdsmi_init", &f->init);
+  Resolve(dl, "amdsmi_shut_down", &f->shut_down);
+  Resolve(dl, "amdsmi_get_socket_handles", &f->socket_handles);
+  Resolve(dl, "amdsmi_get_processor_handles", &f->processor_handles);
+  Resolve(dl, "amdsmi_get_processor_type", &f->processor_type);
+  Resolve(dl, "amdsmi_get_gpu_device_uuid", &f->uuid);
+  Resolve(dl, "amdsmi_get_gpu_device_bdf", &f->bdf);
+  Resolve(dl, "amdsmi_get_gpu_enumeration_info", &f->enum_info);
+  Resolve(dl, "amdsmi_get_gpu_topo_numa_affinity", &f->numa);
+  Resolve(dl, "amdsmi_get_gpu_vram_info", &f->vram_info);
+  Resolve(dl, "amdsmi_get_gpu_memory_total", &f->memory_total);
+  Resolve(dl, "amdsmi_get_gpu_compute_partition", &f->compute_partition);
+  Resolve(dl, "amdsmi_get_gpu_memory_partition", &f->memory_partition);
+  Resolve(dl, "amdsmi_get_gpu_kfd_info", &f->kfd_info);
+  Resolve(dl, "amdsmi_get_gpu_asic_info", &f->asic_info);
+  Resolve(dl, "amdsmi_get_gpu_xcd_counter", &f->xcd_counter);
+  Resolve(dl, "amdsmi_topo_get_link_type", &f->link_type);
+  Resolve(dl, "amdsmi_topo_get_link_weight", &f->link_weight);
+  Resolve(dl, "amdsmi_get_gpu_xgmi_link_status", &f->xgmi_link_status);
+  Resolve(dl, "amdsmi_init_gpu_event_notification", &f->evt_init);
+  Resolve(dl, "amdsmi_set_gpu_event_notification_mask", &f->evt_mask);
+  Resolve(dl, "amdsmi_get_gpu_event_notification", &f->evt_get);
+  Resolve(dl, "amdsmi_stop_gpu_event_notification", &f->evt_stop);
+  Resolve(dl, "amdsmi_get_gpu_total_ecc_count", &f->ecc_total);
+  Resolve(dl, "amdsmi_status_code_to_string", &f->status_string);
+  Resolve(dl, "amdsmi_get_lib_version", &f->lib_version);
+  if (!f->init || !f->shut_down || !f->socket_handles || !f->processor_handles || !f->uuid ||
+      !f->bdf) {
+    return Unavailable(lib->path_ + " lacks required amdsmi symbols");
+  }
+  lib->f_ = std::move(f);
+  amdsmi_status_t st = lib->f_->init(AMDSMI_INIT_AMD_GPUS);
+  if (st != AMDSMI_STATUS_SUCCESS) {
+    const char* s = nullptr;
+    if (lib->f_->status_string) lib->f_->status_string(st, &s);
+    return Unavailable("amdsmi_init failed: " + std::string(s ? s : std::to_string(st)));
+  }
+  lib->initialized_ = true;
+  return lib;
+}
+
+std::string Library::Version() const {
+  if (!f_->lib_version) return "unknown";
+  amdsmi_version_t v{};
+  if (f_->lib_version(&v) != AMDSMI_STATUS_SUCCESS) return "unknown";
+  char buf[64];
+  snprintf(buf, sizeof(buf), "%u.%u.%u", v.major, v.minor, v.release);
+  return buf;
+}
+
+Result<std::vector<ProcessorInfo>> Library::Enumerate() {
+  uint32_t nsock = 0;
+  if (f_->socket_handles(&nsock, nullptr) != AMDSMI_STATUS_SUCCESS)
+    return Unavailable("amdsmi_get_socket_handles(count) failed");
+  std::vector<amdsmi_socket_handle> sockets(nsock);
+  if (nsock && f_->socket_handles(&nsock, sockets.data()) != AMDSMI_STATUS_SUCCESS)
+    return Unavailable("amdsmi_get_socket_handles failed");
+  sockets.resize(nsock);
+
+  std::vector<ProcessorInfo> out;
+  for (auto sock : sockets) {
+    uint32_t np = 0;
+    if (f_->processor_handles(sock, &np, nullptr) != AMDSMI_STATUS_SUCCESS) continue;
+    std::vector<amdsmi_processor_handle> procs(np);
+    if (np && f_->processor_handles(sock, &np, procs.data()) != AMDSMI_STATUS_SUCCESS) continue;
+    procs.resize(np);
+    for (auto h : procs) {
+      if (f_->processor_type) {
+        processor_type_t t = AMDSMI_PROCESSOR_TYPE_UNKNOWN;
+        if (f_->processor_type(h, &t) == AMDSMI_STATUS_SUCCESS && t != AMDSMI_PROCESSOR_TYPE_AMD_GPU)
+          continue;
+      }
+      ProcessorInfo p;
+      p.handle = h;
+      char uuid[AMDSMI_GPU_UUID_SIZE + 16] = {0};
+      unsigned int ulen = sizeof(uuid);
+      if (f_->uuid(h, &ulen, uuid) != AMDSMI_STATUS_SUCCESS) {
+        LOG_WARN(kComp, "skipping processor: uuid query failed");
+        continue;
+      }
+      p.uuid = uuid;
+      amdsmi_bdf_t bdf{};
+      if (f_->bdf(h, &bdf) == AMDSMI_STATUS_SUCCESS) {
+        p.bdf_id = bdf.as_uint;
+        p.bdf = FormatBdf(bdf.as_uint);
+      }
+      if (f_->enum_info) {
+        amdsmi_enumeration_info_t ei{};
+        if (f_->enum_info(h, &ei) == AMDSMI_STATUS_SUCCESS) {
+          p.render_minor = ei.drm_render;
+          p.card_minor = ei.drm_card;
+          p.hip_id = ei.hip_id;
+        }
+      }
+      if (f_->numa) {
+        int32_t n = -1;
+        if (f_->numa(h, &n) == AMDSMI_STATUS_SUCCESS) p.numa_node = n;
+      }
+      if (f_->vram_info) {
+        amdsmi_vram_info_t vi{};
+        if (f_->vram_info(h, &vi) == AMDSMI_STATUS_SUCCESS) p.vram_mib = vi.vram_size;
+      }
+      if (!p.vram_mib && f_->memory_total) {
+        uint64_t total = 0;
+        if (f_->memory_total(h, AMDSMI_MEM_TYPE_VRAM, &total) == AMDSMI_STATUS_SUCCESS)
+          p.vram_mib = total >> 20;
+      }
+      if (f_->compute_partition) {
+        char buf[64] = {0};
+        if (f_->compute_partition(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS)
+          p.compute_partition = buf;
+      }
+      if (f_->memory_partition) {
+        char buf[64] = {0};
+        if (f_->memory_partition(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS)
+          p.memory_partition = buf;
+      }
+      if (f_->kfd_info) {
+        amdsmi_kfd_info_t ki{};
+        if (f_->kfd_info(h, &ki) == AMDSMI_STATUS_SUCCESS && ki.current_partition_id != 0xffffffffu)
+          p.partition_id = ki.current_partition_id;
+      }
+      if (f_->asic_info) {
+        amdsmi_asic_info_t ai{};
+        if (f_->asic_info(h, &ai) == AMDSMI_STATUS_SUCCESS) {
+          p.market_name = ai.market_name;
+          if (ai.num_of_compute_units != 0xffffffffu) p.num_cu = ai.num_of_compute_units;
+        }
+      }
+      if (f_->xcd_counter) {
+        uint16_t x = 0;
+        if (f_->xcd_counter(h, &x) == AMDSMI_STATUS_SUCCESS) p.xcd_count = x;
+      }
+      out.push_back(std::move(p));
+    }
+  }
+  return out;
+}
+
+Link Library::GetLink(void* src, void* dst) {
+  Link l;
+  if (!f_->link_type) return l;
+  uint64_t hops = 0;
+  amdsmi_link_type_t t = AMDSMI_LINK_TYPE_UNKNOWN;
+  if (f_->link_type(src, dst, &hops, &t) != AMDSMI_STATUS_SUCCESS) return l;
+  l.valid = true;
+  l.hops = hops;
+  l.type = static_cast<LinkType>(t);
+  if (f_->link_weight) {
+    uint64_t w = 0;
+    if (f_->link_weight(src, dst, &w) == AMDSMI_STATUS_SUCCESS) l.weight = w;
+  }
+  return l;
+}
+
+int Library::XgmiLinksDown(void* h) {
+  if (!f_->xgmi_link_status) return 0;
+  amdsmi_xgmi_link_status_t s{};
+  if (f_->xgmi_link_status(h, &s) != AMDSMI_STATUS_SUCCESS) return 0;
+  int down = 0;
+  for (uint32_t i = 0; i < s.total_links && i < AMDSMI_MAX_NUM_XGMI_LINKS; ++i)
+    if (s.status[i] == AMDSMI_XGMI_LINK_DOWN) ++down;
+  return down;
+}
+
+Status Library::EventsInit(const std::vector<void*>& handles, uint64_t mask) {
+  if (!f_->evt_init || !f_->evt_mask || !f_->evt_get)
+    return NotSupported("event notification API not present");
+  for (void* h : handles) {
+    amdsmi_status_t st = f_->evt_init(h);
+    if (st != AMDSMI_STATUS_SUCCESS)
+      return Status(st == AMDSMI_STATUS_NOT_SUPPORTED ? Code::kNotSupported : Code::kUnavailable,
+                    "amdsmi_init_gpu_event_notification failed (" + std::to_string(st) + ")");
+    st = f_->evt_mask(h, mask);
+    if (st != AMDSMI_STATUS_SUCCESS)
+      return Unavailable("amdsmi_set_gpu_event_notification_mask failed (" + std::to_string(st) + ")");
+  }
+  return Status::Ok();
+}
+
+Status Library::EventsWait(int timeout_ms, std::vector<Event>* out) {
+  amdsmi_evt_notification_data_t data[16];
+  uint32_t n = 16;
+  amdsmi_status_t st = f_->evt_get(timeout_ms, &n, data);
+  if (st == AMDSMI_STATUS_NO_DATA) return Status::Ok();
+  if (st != AMDSMI_STATUS_SUCCESS)
+    return Unavailable("amdsmi_get_gpu_event_notification failed (" + std::to_string(st) + ")");
+  for (uint32_t i = 0; i < n && i < 16; ++i) {
+    Event e;
+    e.handle = data[i].processor_handle;
+    e.type = static_cast<uint32_t>(data[i].event);
+    e.message.assign(data[i].message, strnlen(data[i].message, sizeof(data[i].message)));
+    out->push_back(std::move(e));
+  }
+  return Status::Ok();
+}
+
+void Library::EventsStop(const std::vector<void*>& handles) {
+  if (!f_->evt_stop) return;
+  for (void* h : handles) f_->evt_stop(h);
+}
+
+Result<uint64_t> Library::UncorrectableErrors(void* h) {
+  if (!f_->ecc_total) return NotSupported("ecc query not present");
+  amdsmi_error_count_t ec{};
+  amdsmi_status_t st = f_->ecc_total(h, &ec);
+  if (st != AMDSMI_STATUS_SUCCESS) return Unavailable("ecc query failed (" + std::to_string(st) + ")");
+  return static_cast<uint64_t>(ec.uncorrectable_count);
+}
+
+bool Library::Responsive(void* h) {
+  char uuid[AMDSMI_GPU_UUID_SIZE + 16] = {0};
+  unsigned int ulen = sizeof(uuid);
+  return f_->uuid(h, &ulen, uuid) == AMDSMI_STATUS_SUCCESS;
+}
+
+}  // namespace adp::smi

@@ -1,0 +1,110 @@
+// libamd_smi, loaded at run time with dlopen, wrapped in typed calls.
+//
+// Parity: the reference's NVML layer -- dlopen("libnvidia-ml.so.1") + nvmlInit_v2
+// (vendor/.../gpu-monitoring-tools/bindings/go/nvml/nvml_dl.go:29-36), thin C
+// wrappers (bindings.go:94-859) and the high-level Device (nvml.go:294-822).
+// MI355X-native replacement: amdsmi (/opt/rocm/include/amd_smi/amdsmi.h), only the
+// cheap queries the plugin needs. The reference calls ~14 NVML
+// queries per GPU via Status() just to read total memory (nvidia.go:96-98); here
+// enumeration is uuid + bdf + enumeration info (render/card minors) + NUMA +
+// VRAM + partition mode, once per snapshot.
+//
+// The library path is overridable (AMD_SMI_LIB / --amdsmi-lib) so tests load
+// native/mock/libamdsmi_mock.so, which exports the same C symbols driven by a
+// JSON fixture. Every call returns a Status; nothing
+// panics (reference defect B16).
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common/status.h"
+
+namespace adp::smi {
+
+// One amdsmi processor handle: a whole GPU (SPX) or one compute partition.
+struct ProcessorInfo {
+  void* handle = nullptr;
+  std::string uuid;
+  std::string bdf;           // "dddd:bb:dd.f"
+  uint64_t bdf_id = 0;       // amdsmi_bdf_t.as_uint
+  uint32_t render_minor = 0; // /dev/dri/renderD<minor>; 0 = unknown
+  uint32_t card_minor = 0xffffffff;
+  uint32_t hip_id = 0xffffffff;
+  int32_t numa_node = -1;
+  uint64_t vram_mib = 0;
+  std::string compute_partition;  // "SPX", "DPX", "TPX", "QPX", "CPX" or "" if unknown
+  std::string memory_partition;   // "NPS1", "NPS2", ... or ""
+  uint32_t partition_id = 0;      // kfd current_partition_id (0 when not reported)
+  uint32_t num_cu = 0;
+  uint32_t xcd_count = 0;         // 0 = unknown
+  std::string market_name;
+};
+
+enum class LinkType { kInternal = 0, kPcie = 1, kXgmi = 2, kNotApplicable = 3, kUnknown = 4 };
+
+struct Link {
+  bool valid = false;
+  LinkType type = LinkType::kUnknown;
+  uint64_t hops = 0;
+  uint64_t weight = 0;
+};
+
+enum EventType : uint32_t {  // amdsmi_evt_notification_type_t values
+  kEvtVmFault = 1,
+  kEvtThermalThrottle = 2,
+  kEvtGpuPreReset = 3,
+  kEvtGpuPostReset = 4,
+};
+
+struct Event {
+  void* handle = nullptr;
+  uint32_t type = 0;
+  std::string message;
+};
+
+class Library {
+ public:
+  ~Library();
+  Library(const Library&) = delete;
+  Library& operator=(const Library&) = delete;
+
+  // dlopen(path or default) + resolve + amdsmi_init(AMD_GPUS). `path` empty ->
+  // $AMD_SMI_LIB, then libamd_smi.so on the loader path, then
+  // <rocm_root>/lib/libamd_smi.so.
+  static Result<std::unique_ptr<Library>> Open(const std::string& path,
+                                               const std::string& rocm_root = "/opt/rocm");
+
+  const std::string& path() const { return path_; }
+  std::string Version() const;
+
+  Result<std::vector<ProcessorInfo>> Enumerate();
+  Link GetLink(void* src, void* dst);
+  // Number of xGMI links reported down (0 when unsupported).
+  int XgmiLinksDown(void* h);
+
+  // Event notification (health). Init registers `mask` on each handle.
+  Status EventsInit(const std::vector<void*>& handles, uint64_t mask);
+  // Waits up to timeout_ms; appends received events.
+  Status EventsWait(int timeout_ms, std::vector<Event>* out);
+  void EventsStop(const std::vector<void*>& handles);
+
+  // RAS polling (fallback health when events are unavailable).
+  Result<uint64_t> UncorrectableErrors(void* h);
+  bool Responsive(void* h);
+
+ private:
+  Library() = default;
+  struct Fns;
+  void* dl_ = nullptr;
+  std::unique_ptr<Fns> f_;
+  std::string path_;
+  bool initialized_ = false;
+};
+
+std::string FormatBdf(uint64_t bdf_id);
+uint64_t EventMask(uint32_t event_type);
+
+}  // namespace adp::smi

@@ -1,0 +1,299 @@
+// Native unit tests (no GPU, no kubelet). Run: build/native/adp_unit_tests
+// Pins the reference's test vectors:
+//   cmd/nvidia-device-plugin/replica_test.go:37-96   (15 prioritizeDevices cases)
+//   cmd/nvidia-device-plugin/replica_test.go:120-122 (3 stripReplicas cases)
+//   cmd/nvidia-device-plugin/nvidia_test.go:31-64    (10 getAdditionalXids cases)
+// plus codec, config, resource-config, topology and gRPC loopback tests.
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "alloc/replicas.h"
+#include "alloc/topology.h"
+#include "common/strings.h"
+#include "daemon/config.h"
+#include "grpc/grpc.h"
+#include "health/health.h"
+#include "proto/messages.h"
+#include "strategy/strategy.h"
+
+using namespace adp;
+using V = std::vector<std::string>;
+
+static int g_failed = 0, g_checks = 0;
+static std::string g_case;
+
+#define CHECK(cond)                                                                \
+  do {                                                                             \
+    ++g_checks;                                                                    \
+    if (!(cond)) {                                                                 \
+      ++g_failed;                                                                  \
+      fprintf(stderr, "FAIL [%s] %s:%d: %s\n", g_case.c_str(), __FILE__, __LINE__, #cond); \
+    }                                                                              \
+  } while (0)
+
+static std::string Str(const V& v) { return "[" + Join(v, ",") + "]"; }
+
+static void TestPrioritize() {
+  struct Case {
+    const char* name;
+    V avail, must;
+    int size;
+    bool ok;
+    V want;
+    bool non_unique;
+    std::string err;
+  };
+  const std::string missing = "in mustIncludeDeviceIDs is missing from availableDeviceIDs";
+  std::vector<Case> cases = {
+      {"Basic", {"a-replica-0", "a-replica-1", "b-replica-1"}, {}, 1, true, {"a-replica-0"}, false, ""},
+      {"Multiple Unique", {"a-replica-0", "a-replica-1", "b-replica-1"}, {}, 2, true, {"a-replica-0", "b-replica-1"}, false, ""},
+      {"NonuniqueError", {"a-replica-0", "a-replica-1", "a-replica-2", "b-replica-1"}, {}, 3, true,
+       {"a-replica-0", "a-replica-1", "b-replica-1"}, true, ""},
+      {"Must Include Greater Utilized", {"a-replica-0", "a-replica-1", "b-replica-1"}, {"b-replica-1"}, 1, true, {"b-replica-1"}, false, ""},
+      {"Must Include Least Utilized", {"a-replica-0", "a-replica-1", "b-replica-1"}, {"a-replica-1"}, 1, true, {"a-replica-1"}, false, ""},
+      {"Must Include Two", {"a-replica-0", "a-replica-1", "b-replica-1"}, {"a-replica-1"}, 2, true, {"a-replica-1", "b-replica-1"}, false, ""},
+      {"NonuniqueError Must Include", {"a-replica-0", "a-replica-1", "a-replica-2", "b-replica-2", "b-replica-1"}, {"a-replica-2"}, 3, true,
+       {"a-replica-0", "a-replica-2", "b-replica-1"}, true, ""},
+      {"Must Include", {"a-replica-0", "a-replica-1", "a-replica-2", "b-replica-1", "c-replica-0"}, {"a-replica-2"}, 3, true,
+       {"a-replica-2", "b-replica-1", "c-replica-0"}, false, ""},
+      {"Must Include Entire Allocated", {"a-replica-0", "a-replica-1", "a-replica-2", "b-replica-1"},
+       {"a-replica-2", "b-replica-1", "a-replica-1"}, 3, true, {"a-replica-1", "a-replica-2", "b-replica-1"}, true, ""},
+      {"Deterministic", {"a-replica-1", "b-replica-1", "c-replica-1", "d-replica-1", "e-replica-1", "f-replica-1", "g-replica-1", "h-replica-1"},
+       {}, 1, true, {"a-replica-1"}, false, ""},
+      {"OversizedRequest", {"a-replica-0", "a-replica-1", "a-replica-2", "b-replica-1"}, {}, 5, false, {}, false, "no devices left to allocate"},
+      {"Undersized", {"a-replica-0", "a-replica-1", "a-replica-2", "b-replica-1"}, {}, 0, true, {}, false, ""},
+      {"NoneAvailable", {}, {}, 1, false, {}, false, "no devices left to allocate"},
+      {"SubsetSame", {"a-replica-0", "a-replica-1"}, {"a-replica-2"}, 1, false, {}, false, "device 'a-replica-2' " + missing},
+      {"SubsetDifferent", {"a-replica-0", "a-replica-1"}, {"b-replica-2"}, 1, false, {}, false, "device 'b-replica-2' " + missing},
+  };
+  for (const auto& c : cases) {
+    g_case = std::string("prioritize/") + c.name;
+    auto r = alloc::PrioritizeDevices(c.avail, c.must, c.size);
+    CHECK(r.ok() == c.ok);
+    if (c.ok && r.ok()) {
+      if (r->ids != c.want) fprintf(stderr, "  got %s want %s\n", Str(r->ids).c_str(), Str(c.want).c_str());
+      CHECK(r->ids == c.want);
+      CHECK(r->non_unique == c.non_unique);
+    }
+    if (!c.ok && !r.ok()) CHECK(r.status().message() == c.err);
+  }
+  g_case = "prioritize/B12-must-exceeds-size";
+  CHECK(!alloc::PrioritizeDevices({"a-replica-0", "b-replica-0"}, {"a-replica-0", "b-replica-0"}, 1).ok());
+
+  g_case = "prioritize/pack";
+  auto p = alloc::PrioritizeDevices({"a-replica-0", "a-replica-1", "a-replica-2", "b-replica-0", "b-replica-1",
+                                     "c-replica-0", "c-replica-1", "c-replica-2", "c-replica-3"},
+                                    {}, 2, alloc::ReplicaPolicy::kPack);
+  CHECK(p.ok());
+  if (p.ok()) CHECK(p->ids == V({"b-replica-0", "b-replica-1"}));  // best fit: tightest GPU
+  auto p2 = alloc::PrioritizeDevices({"a-replica-0", "a-replica-1", "b-replica-0", "b-replica-1", "b-replica-2"},
+                                     {"a-replica-1"}, 3, alloc::ReplicaPolicy::kPack);
+  CHECK(p2.ok());
+  if (p2.ok()) CHECK(p2->ids == V({"a-replica-0", "a-replica-1", "b-replica-0"}));
+}
+
+static void TestStrip() {
+  g_case = "strip";
+  CHECK(alloc::StripReplicas({"b-replica-5", "a-replica-1", "a-replica-0"}) == V({"a", "b"}));
+  CHECK(alloc::StripReplicas({"b-replica-0", "a-replica-1", "a-replica-2", "c-replica-2"}) == V({"a", "b", "c"}));
+  CHECK(alloc::StripReplicas({}).empty());
+  CHECK(alloc::StripReplica("plain-uuid") == "plain-uuid");
+  CHECK(alloc::ReplicaId("u", 7) == "u-replica-7");
+}
+
+static void TestAdditionalIds() {
+  g_case = "additional-ids";
+  using U = std::vector<uint64_t>;
+  CHECK(health::ParseAdditionalIds("") == U{});
+  CHECK(health::ParseAdditionalIds(",") == U{});
+  CHECK(health::ParseAdditionalIds("not-an-int") == U{});
+  CHECK(health::ParseAdditionalIds("68") == U{68});
+  CHECK(health::ParseAdditionalIds("-68") == U{});
+  CHECK(health::ParseAdditionalIds("68  ") == U{68});
+  CHECK(health::ParseAdditionalIds("68,") == U{68});
+  CHECK(health::ParseAdditionalIds(",68") == U{68});
+  CHECK(health::ParseAdditionalIds("68,67") == (U{68, 67}));
+  CHECK(health::ParseAdditionalIds("68,not-an-int,67") == (U{68, 67}));
+
+  g_case = "health-config";
+  auto c = health::HealthConfig::FromValues("all", nullptr);
+  CHECK(c.disabled);
+  c = health::HealthConfig::FromValues("XIDS", nullptr);
+  CHECK(c.disabled);
+  c = health::HealthConfig::FromValues("3", "0");
+  CHECK(!c.disabled && c.ignored.count(3) && c.poll_interval_ms == 0);
+  CHECK(health::Monitor::Classify(c, 3) == 0);
+  c = health::HealthConfig::FromValues("", nullptr);
+  CHECK(health::Monitor::Classify(c, 3) == -1);
+  CHECK(health::Monitor::Classify(c, 4) == +1);
+  CHECK(health::Monitor::Classify(c, 1) == 0);
+}
+
+static void TestResourceConfig() {
+  g_case = "resource-config";
+  auto rc = strategy::ResourceConfig::Parse("gpu:sharedgpu:4, cpx-1xcd.36gb:small:2,,");
+  CHECK(rc.ok());
+  if (rc.ok()) {
+    CHECK(rc->Get("gpu").name == "sharedgpu" && rc->Get("gpu").replicas == 4);
+    CHECK(rc->Get("cpx-1xcd.36gb").name == "small");
+    CHECK(rc->Get("other").name == "other" && rc->Get("other").replicas == 1);  // B2 fixed
+  }
+  auto a = strategy::ResourceConfig::Parse("gpu:gpu-mem-gb:-1");
+  CHECK(a.ok() && a->Get("gpu").auto_replicas && a->Get("gpu").replicas == 1);
+  CHECK(!strategy::ResourceConfig::Parse("gpu:x").ok());
+  CHECK(strategy::ResourceConfig::Parse("gpu:x").status().message().find("colon") != std::string::npos);
+  CHECK(!strategy::ResourceConfig::Parse("gpu:x:-2").ok());  // B11
+  CHECK(!strategy::ResourceConfig::Parse("gpu:x:0").ok());
+  CHECK(!strategy::ResourceConfig::Parse("gpu:x:abc").ok());
+  CHECK(!strategy::ResourceConfig::Parse("gpu:bad name:2").ok());
+  CHECK(strategy::ResourceConfig::Parse("").ok());
+}
+
+static void TestProto() {
+  g_case = "proto";
+  pb::AllocateResponse r;
+  r.container_responses.emplace_back();
+  auto& c = r.container_responses[0];
+  c.envs = {{"AMD_VISIBLE_DEVICES", "u1,u2"}};
+  c.mounts.push_back({"/var/run/amd-container-devices/u1", "/dev/null", true});
+  c.devices.push_back({"/dev/kfd", "/dev/kfd", "rw"});
+  c.devices.push_back({"/dev/dri/renderD128", "/dev/dri/renderD128", "rw"});
+  c.annotations = {{"k", ""}};
+  c.cdi_devices = {"amd.com/gpu=u1"};
+  std::string b = pb::Encode(r);
+  pb::AllocateResponse d;
+  CHECK(pb::Decode(b, &d).ok());
+  CHECK(d.container_responses.size() == 1);
+  const auto& e = d.container_responses[0];
+  CHECK(e.envs == c.envs && e.annotations == c.annotations && e.cdi_devices == c.cdi_devices);
+  CHECK(e.mounts.size() == 1 && e.mounts[0].read_only && e.mounts[0].host_path == "/dev/null");
+  CHECK(e.devices.size() == 2 && e.devices[1].container_path == "/dev/dri/renderD128");
+  CHECK(pb::Encode(d) == b);
+
+  pb::ListAndWatchResponse law;
+  law.devices.push_back({"id0", pb::kHealthy, true, {1}});
+  law.devices.push_back({"id1", pb::kUnhealthy, false, {}});
+  pb::ListAndWatchResponse law2;
+  CHECK(pb::Decode(pb::Encode(law), &law2).ok());
+  CHECK(law2.devices.size() == 2 && law2.devices[0].numa_nodes == std::vector<int64_t>{1} &&
+        !law2.devices[1].has_topology && law2.devices[1].health == pb::kUnhealthy);
+
+  pb::PreferredAllocationRequest pr;
+  pr.container_requests.push_back({{"a", "b"}, {"a"}, -1});
+  pb::PreferredAllocationRequest pr2;
+  CHECK(pb::Decode(pb::Encode(pr), &pr2).ok());
+  CHECK(pr2.container_requests[0].allocation_size == -1 && pr2.container_requests[0].must_include == V({"a"}));
+
+  pb::AllocateRequest bad;
+  CHECK(!pb::Decode(std::string("\x0a\x05\x0a\x09", 4), &bad).ok());  // truncated
+}
+
+static void TestTopology() {
+  g_case = "topology";
+  // 4 GPUs: 0,1 on NUMA 0 and 2,3 on NUMA 1, full xGMI. Scores: same NUMA 120, cross 110.
+  std::vector<int> parent = {0, 1, 2, 3};
+  auto score = [](int a, int b) { return (a / 2 == b / 2) ? 120 : 110; };
+  std::vector<int> s(16);
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) s[a * 4 + b] = a == b ? 0 : score(a, b);
+  alloc::DeviceGraph g(parent, s);
+  CHECK(alloc::BestEffortAllocate(g, {0, 1, 2, 3}, {}, 2) == std::vector<int>({0, 1}));
+  CHECK(alloc::BestEffortAllocate(g, {0, 1, 2, 3}, {2}, 2) == std::vector<int>({2, 3}));
+  CHECK(alloc::BestEffortAllocate(g, {0, 2, 3}, {}, 2) == std::vector<int>({2, 3}));
+  CHECK(alloc::BestEffortAllocate(g, {0, 1}, {}, 3).empty());
+  CHECK(alloc::BestEffortAllocate(g, {0, 1, 2, 3}, {}, 0).empty());
+  CHECK(alloc::BestEffortAllocate(g, {0, 1, 2, 3}, {0, 1, 2}, 2).empty());
+  // Partitions: 2 GPUs x 4 partitions; GPU 0 has 1 free, GPU 1 has 4 free.
+  std::vector<int> pp = {0, 1, 1, 1, 1};
+  std::vector<int> ps(25);
+  for (int a = 0; a < 5; ++a)
+    for (int b = 0; b < 5; ++b) ps[a * 5 + b] = a == b ? 0 : (pp[a] == pp[b] ? 1000 : 110);
+  alloc::DeviceGraph pg(pp, ps);
+  CHECK(alloc::BestEffortAllocate(pg, {0, 1, 2, 3, 4}, {}, 1) == std::vector<int>({0}));   // best fit
+  CHECK(alloc::BestEffortAllocate(pg, {0, 1, 2, 3, 4}, {}, 2) == std::vector<int>({1, 2})); // one die
+  CHECK(alloc::BestEffortAllocate(pg, {0, 1, 2, 3, 4}, {0}, 2).size() == 2);
+}
+
+static void TestConfig() {
+  g_case = "config";
+  std::map<std::string, std::string> env = {{"FAIL_ON_INIT_ERROR", "false"}, {"DEVICE_ID_STRATEGY", "index"}};
+  const char* argv[] = {"x", "--device-id-strategy=uuid", "--pass-device-specs", "--partition-strategy", "mixed"};
+  auto c = daemon::LoadConfig(5, argv, &env);
+  CHECK(c.ok());
+  if (c.ok()) {
+    CHECK(!c->flags.fail_on_init_error);
+    CHECK(c->flags.device_id_strategy == "uuid");
+    CHECK(c->flags.partition_strategy == "mixed");
+  }
+  auto f = daemon::ParseConfigFile("version: v1\nflags:\n  failOnInitError: false # comment\n  resourceConfig: 'gpu:g:2'\n");
+  CHECK(f.ok());
+  if (f.ok()) {
+    CHECK((*f)["flags.failOnInitError"] == "false");
+    CHECK((*f)["flags.resourceConfig"] == "gpu:g:2");
+  }
+  CHECK(!daemon::ParseConfigFile("flags:\n  a: b\n").ok());
+  CHECK(!daemon::ParseConfigFile("version: v2\n").ok());
+  auto j = daemon::ParseConfigFile("{\"version\": \"v1\", \"flags\": {\"passDeviceSpecs\": false}}");
+  CHECK(j.ok() && (*j)["flags.passDeviceSpecs"] == "false");
+  const char* bad[] = {"x", "--no-such-flag"};
+  CHECK(!daemon::LoadConfig(2, bad, &env).ok());
+}
+
+static void TestGrpcLoopback() {
+  g_case = "grpc";
+  std::string dir = "/tmp/adp-unit-" + std::to_string(getpid());
+  mkdir(dir.c_str(), 0755);
+  std::string sock = dir + "/t.sock";
+  grpc::Server srv("test");
+  srv.AddUnary("/t.S/Echo", [](std::string_view q, std::string* r) {
+    r->assign(q);
+    return Status::Ok();
+  });
+  srv.AddUnary("/t.S/Fail", [](std::string_view, std::string*) { return InvalidArgument("bad thing: 100%"); });
+  std::shared_ptr<grpc::ServerStream> keep;
+  srv.AddServerStream("/t.S/Watch", [&](std::string_view, std::shared_ptr<grpc::ServerStream> s) {
+    keep = s;
+    s->Send("first");
+    return Status::Ok();
+  });
+  CHECK(srv.Listen(sock).ok());
+  CHECK(srv.Start().ok());
+  auto ch = grpc::Channel::Dial(sock, 2000);
+  CHECK(ch.ok());
+  if (ch.ok()) {
+    std::string resp;
+    std::string big(300000, 'x');
+    CHECK((*ch)->Unary("/t.S/Echo", big, &resp, 2000).ok() && resp == big);
+    Status st = (*ch)->Unary("/t.S/Fail", "", &resp, 2000);
+    CHECK(st.code() == Code::kInvalidArgument && st.message() == "bad thing: 100%");
+    CHECK((*ch)->Unary("/t.S/Nope", "", &resp, 2000).code() == Code::kUnimplemented);
+    auto sid = (*ch)->StartStream("/t.S/Watch", "");
+    CHECK(sid.ok());
+    std::string m;
+    CHECK((*ch)->Recv(*sid, &m, 2000).ok() && m == "first");
+    srv.Post([&] { keep->Send(std::string(100000, 'y')); keep->Finish(Status::Ok()); });
+    CHECK((*ch)->Recv(*sid, &m, 2000).ok() && m.size() == 100000);
+    CHECK((*ch)->Recv(*sid, &m, 2000).code() == Code::kNotFound);
+  }
+  srv.Stop();
+  unlink(sock.c_str());
+  rmdir(dir.c_str());
+}
+
+int main() {
+  TestPrioritize();
+  TestStrip();
+  TestAdditionalIds();
+  TestResourceConfig();
+  TestProto();
+  TestTopology();
+  TestConfig();
+  TestGrpcLoopback();
+  printf("%d checks, %d failed\n", g_checks, g_failed);
+  return g_failed ? 1 : 0;
+}

@@ -1,0 +1,108 @@
+"""End-to-end: the real daemon binary + grpcio stub kubelet + amdsmi mock (BASELINE config 1).
+
+kubelet receives Register(amd.com/gpu), opens ListAndWatch, sees 2 Healthy
+devices, Allocate(1) returns DeviceSpecs [/dev/kfd, /dev/dri/renderD128].
+"""
+
+import os
+
+import grpc
+import pytest
+
+from k8s_gpu_sharing_plugin_amd.models import fixtures
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
+
+
+@pytest.fixture
+def running(scratch):
+    started = []
+
+    def start(fixture=None, args=(), env=None, **kw):
+        k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+        d = harness.Daemon(scratch, fixture or fixtures.node(2), args=args, env=env, **kw).start()
+        started.append((d, k))
+        return d, k
+    yield start
+    for d, k in started:
+        d.stop()
+        k.stop()
+
+
+def test_minimum_slice(running, scratch):
+    d, k = running()
+    reg = k.wait_registration()
+    assert reg.version == "v1beta1"
+    assert reg.endpoint == "amd-gpu.sock"
+    assert reg.resource_name == "amd.com/gpu"
+    assert reg.options.get_preferred_allocation_available
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    opts = c.options()
+    assert not opts.pre_start_required and opts.get_preferred_allocation_available
+    q, call = c.watch()
+    law = q.get(timeout=5)
+    assert len(law.devices) == 2
+    assert all(x.health == "Healthy" for x in law.devices)
+    assert [n.ID for n in law.devices[0].topology.nodes] == [0]
+    r = c.allocate([law.devices[0].ID])
+    cr = r.container_responses[0]
+    assert [(s.container_path, s.host_path, s.permissions) for s in cr.devices] == [
+        ("/dev/kfd", "/dev/kfd", "rw"), ("/dev/dri/renderD128", "/dev/dri/renderD128", "rw")]
+    assert dict(cr.envs) == {"AMD_VISIBLE_DEVICES": law.devices[0].ID}
+    assert c.prestart([law.devices[0].ID]) is not None
+    call.cancel()
+    c.close()
+
+
+def test_allocate_unknown_device_is_invalid_argument(running, scratch):
+    d, k = running()
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    with pytest.raises(grpc.RpcError) as e:
+        c.allocate(["no-such-device"])
+    assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+    assert "unknown device: no-such-device" in e.value.details()
+    c.close()
+
+
+def test_multi_container_allocate_and_index_strategy(running, scratch):
+    d, k = running(fixtures.node(4), args=["--device-id-strategy", "index", "--device-list-strategy",
+                                           "volume-mounts"])
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    law = c.watch()[0].get(timeout=5)
+    ids = [x.ID for x in law.devices]
+    r = c.allocate([ids[2], ids[0]], [ids[3]])
+    a, b = r.container_responses
+    assert dict(a.envs) == {"AMD_VISIBLE_DEVICES": "/var/run/amd-container-devices"}
+    assert [m.container_path for m in a.mounts] == ["/var/run/amd-container-devices/0",
+                                                    "/var/run/amd-container-devices/2"]
+    assert all(m.host_path == "/dev/null" for m in a.mounts)
+    assert [s.container_path for s in a.devices] == ["/dev/kfd", "/dev/dri/renderD128", "/dev/dri/renderD144"]
+    assert [s.container_path for s in b.devices] == ["/dev/kfd", "/dev/dri/renderD152"]
+    c.close()
+
+
+def test_driver_root_prefixes_host_paths(running, scratch):
+    d, k = running(args=["--driver-root", "/run/amd/driver"])
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    law = c.watch()[0].get(timeout=5)
+    r = c.allocate([law.devices[1].ID])
+    assert [(s.container_path, s.host_path) for s in r.container_responses[0].devices] == [
+        ("/dev/kfd", "/run/amd/driver/dev/kfd"), ("/dev/dri/renderD136", "/run/amd/driver/dev/dri/renderD136")]
+    c.close()
+
+
+def test_native_stub_kubelet_sees_devices(scratch):
+    """Same flow through the native stub kubelet (amdgpu-dp-kubelet serve)."""
+    k = harness.NativeKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(8)).start()
+    try:
+        reg = k.wait(lambda e: e.get("event") == "register")
+        assert reg["resource"] == "amd.com/gpu" and reg["preferred"]
+        dev = k.wait(lambda e: e.get("event") == "devices")
+        assert dev["total"] == 8 and dev["healthy"] == 8
+        assert dev["numa"] == {"0": 4, "1": 4}
+    finally:
+        assert d.stop() == 0
+        k.stop()

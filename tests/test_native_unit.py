@@ -1,0 +1,11 @@
+"""Runs the C++ unit-test binary (codec, config, prioritizer, topology, gRPC loopback)."""
+
+import subprocess
+
+from k8s_gpu_sharing_plugin_amd import UNIT_TESTS
+
+
+def test_native_unit_tests_pass():
+    res = subprocess.run([UNIT_TESTS], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=120)
+    assert res.returncode == 0, res.stdout
+    assert ", 0 failed" in res.stdout
