@@ -1,0 +1,174 @@
+"""Health pipeline: amdsmi events / RAS polling -> ListAndWatch updates, with recovery.
+
+Parity: reference nvidia.go:181-294 (checkHealth, DP_DISABLE_HEALTHCHECKS,
+application-error ignore list), server.go:251-265 (ListAndWatch resend).
+Fault injection goes through the amdsmi mock's event FIFO and state directory.
+Fixes pinned here: B1 (health reaches every replica), B15 (recovery).
+"""
+
+import os
+import time
+
+import pytest
+
+from k8s_gpu_sharing_plugin_amd.models import fixtures
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet, native
+
+# nvidia_test.go:31-64 TestGetAdditionalXids, same semantics for amdsmi event IDs.
+XID_CASES = [("", []), (",", []), ("not-an-int", []), ("68", [68]), ("-68", []), ("68  ", [68]),
+             ("68,", [68]), (",68", [68]), ("68,67", [68, 67]), ("68,not-an-int,67", [68, 67])]
+
+
+@pytest.mark.parametrize("text,want", XID_CASES)
+def test_additional_ids_reference_vectors(text, want):
+    assert native.parse_additional_ids(text) == want
+
+
+def test_event_classification():
+    c = native.health_config("", "")
+    assert not c["disabled"]
+    v = c["verdicts"]
+    assert v["3"] == -1  # GPU_PRE_RESET -> unhealthy
+    assert v["4"] == +1  # GPU_POST_RESET -> healthy (recovery)
+    assert v["1"] == 0 and v["2"] == 0  # VMFAULT / THERMAL_THROTTLE: application events, ignored
+    assert native.health_config("all", "")["disabled"]
+    assert native.health_config("xids", "")["disabled"]
+    assert native.health_config("foo,XIDS", "")["disabled"]
+    c = native.health_config("3", "0")
+    assert c["verdicts"]["3"] == 0 and c["poll_ms"] == 0
+
+
+class Node:
+    def __init__(self, scratch, fx, env=None, args=()):
+        self.fifo = os.path.join(scratch + ".fixture", "events")
+        self.state = os.path.join(scratch + ".fixture", "state")
+        os.makedirs(self.state, exist_ok=True)
+        os.mkfifo(self.fifo)
+        self.k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+        self.d = harness.Daemon(scratch, fx, args=args, env=env, event_fifo=self.fifo,
+                                state_dir=self.state).start()
+        reg = self.k.wait_registration()
+        self.c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        self.q, self.call = self.c.watch()
+        self.first = self.q.get(timeout=5)
+
+    def inject(self, line):
+        try:
+            fd = os.open(self.fifo, os.O_WRONLY | os.O_NONBLOCK)
+        except OSError as e:
+            if e.errno == 6:  # ENXIO: nobody reads events (health checks disabled)
+                return
+            raise
+        os.write(fd, (line + "\n").encode())
+        os.close(fd)
+
+    def next(self, timeout=5):
+        return self.q.get(timeout=timeout)
+
+    def health(self, resp):
+        return {x.ID: x.health for x in resp.devices}
+
+    def close(self):
+        self.call.cancel()
+        self.c.close()
+        code = self.d.stop()
+        self.k.stop()
+        return code
+
+
+@pytest.fixture
+def node(scratch):
+    nodes = []
+
+    def make(fx=None, **kw):
+        n = Node(scratch, fx or fixtures.node(2), **kw)
+        nodes.append(n)
+        return n
+    yield make
+    for n in nodes:
+        n.close()
+
+
+def test_reset_marks_unhealthy_then_recovers(node):
+    n = node()
+    ids = [x.ID for x in n.first.devices]
+    n.inject("0 3 pre-reset")
+    h = n.health(n.next())
+    assert h == {ids[0]: "Unhealthy", ids[1]: "Healthy"}
+    n.inject("0 4 post-reset")
+    h = n.health(n.next())
+    assert h == {ids[0]: "Healthy", ids[1]: "Healthy"}
+
+
+def test_application_events_are_ignored(node):
+    n = node()
+    n.inject("1 1 vm fault")
+    n.inject("1 2 thermal")
+    time.sleep(0.8)
+    assert n.q.empty()
+    assert "(ignored)" in n.d.log()
+
+
+def test_health_reaches_every_replica(node):
+    # Reference defect B1: Unhealthy was set on the raw device, never the advertised replicas.
+    n = node(args=["--resource-config", "gpu:sharedgpu:3"])
+    assert len(n.first.devices) == 6
+    n.inject("1 3")
+    h = n.next()
+    bad = sorted(x.ID for x in h.devices if x.health == "Unhealthy")
+    assert len(bad) == 3 and all("-replica-" in i for i in bad)
+    assert len({i.split("-replica-")[0] for i in bad}) == 1
+
+
+def test_partition_reset_takes_down_the_whole_gpu(node):
+    n = node(fixtures.node(2, "CPX", memory="NPS2"), args=["--partition-strategy", "single"])
+    assert len(n.first.devices) == 16
+    n.inject("1:5 3")  # reset seen on partition 5 of GPU 1
+    h = n.next()
+    assert sum(x.health == "Unhealthy" for x in h.devices) == 8
+
+
+def test_disable_healthchecks_ignores_configured_ids(node):
+    n = node(env={"DP_DISABLE_HEALTHCHECKS": "3"})
+    n.inject("0 3")
+    time.sleep(0.8)
+    assert n.q.empty()
+
+
+def test_disable_all(node):
+    n = node(env={"DP_DISABLE_HEALTHCHECKS": "all"})
+    n.inject("0 3")
+    time.sleep(0.8)
+    assert n.q.empty()
+    assert "health checks disabled" in n.d.log()
+
+
+def test_ecc_polling(node):
+    n = node(env={"DP_HEALTH_POLL_MS": "100"})
+    ids = [x.ID for x in n.first.devices]
+    with open(os.path.join(n.state, "gpu1.ecc"), "w") as f:
+        f.write("7\n")
+    h = n.health(n.next())
+    assert h[ids[1]] == "Unhealthy" and h[ids[0]] == "Healthy"
+    n.inject("1 4")  # a completed reset clears it
+    assert n.health(n.next())[ids[1]] == "Healthy"
+
+
+def test_unresponsive_device_recovers(node):
+    n = node(env={"DP_HEALTH_POLL_MS": "100"})
+    ids = [x.ID for x in n.first.devices]
+    dead = os.path.join(n.state, "gpu0.dead")
+    open(dead, "w").close()
+    assert n.health(n.next())[ids[0]] == "Unhealthy"
+    os.unlink(dead)
+    assert n.health(n.next())[ids[0]] == "Healthy"
+
+
+def test_events_unsupported_falls_back_to_polling(node):
+    fx = fixtures.node(2)
+    fx["events_supported"] = False
+    n = node(fx, env={"DP_HEALTH_POLL_MS": "100"})
+    assert all(x.health == "Healthy" for x in n.first.devices)  # not marked unhealthy
+    assert "using polling only" in n.d.log()
+    open(os.path.join(n.state, "gpu0.dead"), "w").close()
+    assert "Unhealthy" in n.health(n.next()).values()
