@@ -145,7 +145,10 @@ Result<std::unique_ptr<Channel>> Channel::Dial(const std::string& uds_path, int 
     }
     close(ch->fd_);
     ch->fd_ = -1;
-    if (NowMs() >= deadline)
+    // No socket file at all: nobody will bind it within a dial timeout (kubelet
+    // re-creating kubelet.sock is picked up by the daemon's inotify watch), so
+    // fail fast instead of blocking signal handling for the whole timeout.
+    if (err == ENOENT || NowMs() >= deadline)
       return Unavailable("connect " + uds_path + ": " + strerror(err));
     usleep(20 * 1000);
   }

@@ -1,0 +1,56 @@
+"""bench.py contract on CPU: single process and a 2-rank torchrun (gloo) job on the mock."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _last_json(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_single_process_contract():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--mock"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = _last_json(r.stdout)
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in res
+    assert res["n_gpus"] == 1 and res["steps"] == 3 and res["warmup"] == 1
+    assert res["higher_is_better"] is False and res["unit"] == "us"
+    assert res["allocatable"] == 1
+    assert 0 < res["value"] < 5000
+    assert res["per_rank"][0]["allocate"]["n"] == 300
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_gloo():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29561", "bench.py", "--gpus", "2",
+                        "--steps", "2", "--warmup", "1", "--mock"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = _last_json(r.stdout)
+    assert res["n_gpus"] == 2 and res["allocatable"] == 2
+    assert sorted(p["rank"] for p in res["per_rank"]) == [0, 1]
+    assert all(p["rank_devices"] == 1 for p in res["per_rank"])
+
+
+@pytest.mark.parametrize("config,advertised", [("timeslice4", 4), ("cpx-single", 8), ("auto-mem", 294)])
+def test_bench_configs_on_mock(config, advertised, monkeypatch):
+    sys.path.insert(0, ROOT)
+    from k8s_gpu_sharing_plugin_amd.parallel import bench
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    res = bench.run(gpus=1, steps=1, warmup=1, pods_per_step=50, config=config, force_mock=True, probe=False)
+    assert res["advertised"] == advertised
+    assert res["allocatable"] == advertised
+    assert res["per_rank"][0]["allocate"]["n"] == 50

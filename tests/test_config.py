@@ -1,0 +1,116 @@
+"""Flags / env / versioned config file precedence.
+
+Parity: api/config/v1/config.go:30-144 (version v1, CLI > env > file) and
+main.go:62-130 (flags + env). Fixes pinned: B7 (false booleans from the file
+are honoured), B8 (resourceConfig can come from the file).
+"""
+
+import json
+import os
+
+import pytest
+
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
+
+
+def effective_config(scratch, args=(), env=None, file_body=None, expect_exit=None):
+    if file_body is not None:
+        path = os.path.join(scratch, "config.yaml")
+        with open(path, "w") as f:
+            f.write(file_body)
+        args = ["--config-file", path, *args]
+    d = harness.Daemon(scratch, args=args, env=env).start()
+    if expect_exit is not None:
+        assert d.proc.wait(10) == expect_exit
+        return d.log()
+    text = d.wait_log("running with resource config")
+    d.stop()
+    start = text.index("running with config:\n") + len("running with config:\n")
+    end = text.index("\n}\n", start) + 2
+    return json.loads(text[start:end])["flags"]
+
+
+def test_defaults(scratch):
+    f = effective_config(scratch)
+    assert f["partitionStrategy"] == "none"
+    assert f["failOnInitError"] is True
+    assert f["passDeviceSpecs"] is True
+    assert f["deviceListStrategy"] == "envvar"
+    assert f["deviceIDStrategy"] == "uuid"
+    assert f["driverRoot"] == "/"
+    assert f["resourceConfig"] == ""
+
+
+def test_file_values_apply(scratch):
+    body = """
+version: v1
+flags:
+  partitionStrategy: mixed
+  failOnInitError: false      # B7: false from the file is honoured
+  passDeviceSpecs: false
+  deviceListStrategy: volume-mounts
+  deviceIDStrategy: index
+  driverRoot: /run/amd/driver
+  resourceConfig: "gpu:sharedgpu:4"   # B8: resourceConfig from the file
+"""
+    f = effective_config(scratch, file_body=body)
+    assert f["partitionStrategy"] == "mixed"
+    assert f["failOnInitError"] is False
+    assert f["passDeviceSpecs"] is False
+    assert f["deviceListStrategy"] == "volume-mounts"
+    assert f["deviceIDStrategy"] == "index"
+    assert f["driverRoot"] == "/run/amd/driver"
+    assert f["resourceConfig"] == "gpu:sharedgpu:4"
+
+
+def test_precedence_cli_over_env_over_file(scratch):
+    body = "version: v1\nflags:\n  deviceIDStrategy: index\n  deviceListStrategy: volume-mounts\n  driverRoot: /file\n"
+    f = effective_config(scratch, args=["--device-id-strategy", "uuid"],
+                         env={"DEVICE_LIST_STRATEGY": "envvar", "DEVICE_ID_STRATEGY": "index"},
+                         file_body=body)
+    assert f["deviceIDStrategy"] == "uuid"          # CLI beats env and file
+    assert f["deviceListStrategy"] == "envvar"      # env beats file
+    assert f["driverRoot"] == "/file"               # file beats default
+
+
+def test_json_config_file(scratch):
+    body = json.dumps({"version": "v1", "flags": {"passDeviceSpecs": False, "resourceConfig": "gpu:g:2"}})
+    f = effective_config(scratch, file_body=body)
+    assert f["passDeviceSpecs"] is False and f["resourceConfig"] == "gpu:g:2"
+
+
+def test_config_file_from_env(scratch):
+    path = os.path.join(scratch, "c.yaml")
+    with open(path, "w") as fh:
+        fh.write("version: v1\nflags:\n  deviceIDStrategy: index\n")
+    f = effective_config(scratch, env={"CONFIG_FILE": path})
+    assert f["deviceIDStrategy"] == "index"
+
+
+@pytest.mark.parametrize("body,msg", [
+    ("flags:\n  deviceIDStrategy: index\n", "missing version field"),
+    ("version: v2\n", "unknown version: v2"),
+    ("version: v1\nflags:\n  failOnInitError: maybe\n", "invalid boolean 'maybe'"),
+    ("version: v1\nflags:\n  - a\n", "sequences are not valid"),
+])
+def test_bad_config_files(scratch, body, msg):
+    log = effective_config(scratch, file_body=body, expect_exit=1)
+    assert msg in log
+
+
+def test_missing_config_file(scratch):
+    d = harness.Daemon(scratch, args=["--config-file", "/nonexistent.yaml"]).start()
+    assert d.proc.wait(10) == 1
+    assert "error opening config file" in d.log()
+
+
+def test_resource_config_env_renames_resource(scratch):
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, env={"RESOURCE_CONFIG": "gpu:sharedgpu:3"}).start()
+    reg = k.wait_registration()
+    assert reg.resource_name == "amd.com/sharedgpu"
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    assert len(c.watch()[0].get(timeout=5).devices) == 6
+    c.close()
+    d.stop()
+    k.stop()

@@ -1,0 +1,184 @@
+"""Daemon lifecycle: restart triggers, signals, init-failure policy, retries.
+
+Parity: reference main.go:205-326 -- failOnInitError (block forever when false),
+restart on kubelet.sock re-creation (inotify) and SIGHUP, stop + exit on
+SIGINT/SIGTERM/SIGQUIT, restart loop when a plugin fails to start (here with
+backoff, fixing B17), and main.go:140-157 flag validation.
+"""
+
+import os
+import signal
+import subprocess
+import time
+
+import pytest
+
+from k8s_gpu_sharing_plugin_amd import DAEMON, MOCK_LIB
+from k8s_gpu_sharing_plugin_amd.models import fixtures
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
+
+
+def sock(scratch):
+    return os.path.join(scratch, "kubelet.sock")
+
+
+def test_sigterm_stops_and_removes_socket(scratch):
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch).start()
+    k.wait_registration()
+    assert os.path.exists(os.path.join(scratch, "amd-gpu.sock"))
+    assert d.stop() == 0
+    assert not os.path.exists(os.path.join(scratch, "amd-gpu.sock"))
+    assert "shutting down" in d.log()
+    k.stop()
+
+
+@pytest.mark.parametrize("sig", [signal.SIGINT, signal.SIGQUIT])
+def test_other_terminating_signals(scratch, sig):
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch).start()
+    k.wait_registration()
+    d.signal(sig)
+    assert d.proc.wait(10) == 0
+    k.stop()
+
+
+def test_sighup_restarts_and_reregisters(scratch):
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch).start()
+    k.wait_registration()
+    d.signal(signal.SIGHUP)
+    reg = k.wait_registration()
+    assert reg.resource_name == "amd.com/gpu"
+    assert "received SIGHUP, restarting" in d.log()
+    assert d.stop() == 0
+    k.stop()
+
+
+def test_kubelet_restart_is_detected(scratch):
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch).start()
+    k.wait_registration()
+    k.stop()
+    if os.path.exists(sock(scratch)):
+        os.unlink(sock(scratch))
+    k2 = kubelet.StubKubelet(sock(scratch)).start()  # re-creates kubelet.sock -> inotify
+    reg = k2.wait_registration(15)
+    assert reg.endpoint == "amd-gpu.sock"
+    d.wait_log("kubelet.sock created, restarting")
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    assert len(c.watch()[0].get(timeout=5).devices) == 2
+    c.close()
+    assert d.stop() == 0
+    k2.stop()
+
+
+def test_waits_for_kubelet_with_backoff(scratch):
+    d = harness.Daemon(scratch, env={}).start()
+    d.wait_log("retrying in 1000 ms", timeout=15)
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    reg = k.wait_registration(20)
+    assert reg.resource_name == "amd.com/gpu"
+    assert d.stop() == 0
+    k.stop()
+
+
+def test_rejected_registration_retries(scratch):
+    k = kubelet.StubKubelet(sock(scratch), reject_with="nope").start()
+    d = harness.Daemon(scratch).start()
+    d.wait_log("plugin start failed", timeout=15)
+    assert "nope" in d.log()
+    assert d.proc.poll() is None
+    assert d.stop() == 0
+    k.stop()
+
+
+def test_fail_on_init_error_true_exits(scratch):
+    fx = fixtures.node(1)
+    fx["init_status"] = 8
+    d = harness.Daemon(scratch, fx).start()
+    assert d.proc.wait(10) == 1
+    assert "failed to initialize amdsmi" in d.log()
+
+
+def test_fail_on_init_error_false_blocks(scratch):
+    d = harness.Daemon(scratch, args=["--fail-on-init-error=false"],
+                       env={"AMD_SMI_LIB": "/nonexistent/libamd_smi.so"}).start()
+    d.wait_log("blocking until terminated")
+    time.sleep(0.3)
+    assert d.proc.poll() is None
+    d.signal(signal.SIGHUP)  # not a terminating signal
+    time.sleep(0.2)
+    assert d.proc.poll() is None
+    assert d.stop() == 0
+
+
+def test_fail_on_init_error_from_env(scratch):
+    d = harness.Daemon(scratch, env={"AMD_SMI_LIB": "/nonexistent.so", "FAIL_ON_INIT_ERROR": "false"}).start()
+    d.wait_log("blocking until terminated")
+    assert d.stop() == 0
+
+
+def test_no_devices_waits_indefinitely(scratch):
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, {"gpus": []}).start()
+    d.wait_log("no devices found; waiting indefinitely")
+    assert k.registrations.empty()
+    assert d.stop() == 0
+    k.stop()
+
+
+def test_strategy_error_is_fatal(scratch):
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, fixtures.node(2, ["SPX", "CPX"], memory="NPS2"),
+                       args=["--partition-strategy", "single"]).start()
+    assert d.proc.wait(10) == 1
+    assert "same compute partition mode" in d.log()
+    k.stop()
+
+
+def test_mixed_strategy_runs_one_socket_per_resource(scratch):
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, fixtures.CONFIGS["mixed8"](), args=["--partition-strategy", "mixed"]).start()
+    regs = {k.wait_registration().resource_name for _ in range(2)}
+    assert regs == {"amd.com/gpu", "amd.com/cpx-1xcd.36gb"}
+    assert os.path.exists(os.path.join(scratch, "amd-cpx-1xcd.36gb.sock"))
+    assert d.stop() == 0
+    k.stop()
+
+
+@pytest.mark.parametrize("args,msg", [
+    (["--device-list-strategy", "bogus"], "invalid --device-list-strategy option: bogus"),
+    (["--device-id-strategy", "bogus"], "invalid --device-id-strategy option: bogus"),
+    (["--partition-strategy", "bogus"], "invalid --partition-strategy option: bogus"),
+    (["--resource-config", "gpu:x"], "invalid --resource-config option"),
+    (["--replica-policy", "bogus"], "invalid --replica-policy option"),
+])
+def test_invalid_flags(scratch, args, msg):
+    d = harness.Daemon(scratch, args=args).start()
+    assert d.proc.wait(10) == 1
+    assert msg in d.log()
+
+
+def test_unknown_flag_and_version_and_help():
+    r = subprocess.run([DAEMON, "--bogus"], capture_output=True, text=True, timeout=10)
+    assert r.returncode == 1 and "flag provided but not defined: --bogus" in r.stderr
+    r = subprocess.run([DAEMON, "--version"], capture_output=True, text=True, timeout=10)
+    assert r.returncode == 0 and "amdgpu-device-plugin version" in r.stdout
+    r = subprocess.run([DAEMON, "--help"], capture_output=True, text=True, timeout=10)
+    assert "--partition-strategy" in r.stdout and "FAIL_ON_INIT_ERROR" in r.stdout
+
+
+def test_sigusr1_dumps_stats(scratch):
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch).start()
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    for _ in range(5):
+        c.allocate([ids[0]])
+    d.signal(signal.SIGUSR1)
+    d.wait_log('"allocate_calls": 5')
+    c.close()
+    assert d.stop() == 0
+    k.stop()
