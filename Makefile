@@ -1,0 +1,52 @@
+# Developer entry points (the reference's Makefile: fmt/vet/lint/build/test/coverage).
+BUILD      ?= build/native
+JOBS       ?= 8
+PY         ?= python3
+GPURUN     ?= /usr/local/graft/bin/gpurun
+
+.PHONY: all build probe test test-native test-gpu bench asan tsan lint image clean
+
+all: build
+
+build:
+	cmake -S native -B $(BUILD) -G Ninja -DCMAKE_BUILD_TYPE=Release >/dev/null
+	ninja -C $(BUILD) -j$(JOBS)
+
+probe:
+	$(PY) -c "from k8s_gpu_sharing_plugin_amd.utils import build; build.build_probe()"
+
+test-native: build
+	$(BUILD)/adp_unit_tests
+
+test: build
+	$(PY) -m pytest tests -q -m "not gpu"
+
+# Real MI355X (one GPU box): GPU tests, smoke, bench, rocprof of the probe.
+test-gpu:
+	$(GPURUN) --timeout 1200 -- 'bash tools/gpu_check.sh'
+
+bench: build
+	$(PY) bench.py --steps 20 --warmup 2
+
+# Sanitizer builds of the native unit + stress tests (host code only).
+asan:
+	cmake -S native -B build/asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DADP_SANITIZE=ON >/dev/null
+	ninja -C build/asan -j$(JOBS) adp_unit_tests adp_stress
+	ASAN_OPTIONS=detect_leaks=1 build/asan/adp_unit_tests
+	build/asan/adp_stress
+
+tsan:
+	cmake -S native -B build/tsan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DADP_TSAN=ON >/dev/null
+	ninja -C build/tsan -j$(JOBS) adp_unit_tests adp_stress
+	TSAN_OPTIONS=halt_on_error=1 build/tsan/adp_unit_tests
+	TSAN_OPTIONS=halt_on_error=1 build/tsan/adp_stress
+
+lint:
+	@command -v clang-format >/dev/null && find native -name '*.cc' -o -name '*.h' | xargs clang-format --dry-run -Werror || echo "clang-format not installed; skipped"
+	$(PY) -m pyflakes k8s_gpu_sharing_plugin_amd tests 2>/dev/null || true
+
+image:
+	docker build -f deployments/container/Dockerfile -t amdgpu-device-plugin:0.1.0 .
+
+clean:
+	rm -rf build

@@ -1,0 +1,38 @@
+{{/* Chart name, possibly overridden. */}}
+{{- define "amdgpu-dp.name" -}}
+{{- .Values.nameOverride | default .Chart.Name | trunc 63 | trimSuffix "-" }}
+{{- end }}
+
+{{/* Release-qualified name (DNS label, <= 63 chars). */}}
+{{- define "amdgpu-dp.fullname" -}}
+{{- if .Values.fullnameOverride }}
+{{- .Values.fullnameOverride | trunc 63 | trimSuffix "-" }}
+{{- else }}
+{{- $name := include "amdgpu-dp.name" . }}
+{{- if contains $name .Release.Name }}
+{{- .Release.Name | trunc 63 | trimSuffix "-" }}
+{{- else }}
+{{- printf "%s-%s" .Release.Name $name | trunc 63 | trimSuffix "-" }}
+{{- end }}
+{{- end }}
+{{- end }}
+
+{{- define "amdgpu-dp.selectorLabels" -}}
+{{- if .Values.selectorLabelsOverride }}
+{{- toYaml .Values.selectorLabelsOverride }}
+{{- else }}
+app.kubernetes.io/name: {{ include "amdgpu-dp.name" . }}
+app.kubernetes.io/instance: {{ .Release.Name }}
+{{- end }}
+{{- end }}
+
+{{- define "amdgpu-dp.labels" -}}
+helm.sh/chart: {{ printf "%s-%s" .Chart.Name .Chart.Version | replace "+" "_" | trunc 63 | trimSuffix "-" }}
+{{ include "amdgpu-dp.selectorLabels" . }}
+app.kubernetes.io/version: {{ .Chart.AppVersion | quote }}
+app.kubernetes.io/managed-by: {{ .Release.Service }}
+{{- end }}
+
+{{- define "amdgpu-dp.image" -}}
+{{- printf "%s:%s" .Values.image.repository (.Values.image.tag | default .Chart.AppVersion) }}
+{{- end }}

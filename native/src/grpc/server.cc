@@ -378,7 +378,16 @@ void ServerStream::Finish(const Status& st) {
 
 // ------------------------- Server -------------------------
 
-Server::Server(std::string name) : name_(std::move(name)) {}
+Server::Server(std::string name) : name_(std::move(name)) {
+  // Created up front so Post() works before Start(): work posted in between runs
+  // as soon as the loop starts instead of being lost.
+  epoll_fd_ = epoll_create1(EPOLL_CLOEXEC);
+  event_fd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  epoll_event ev{};
+  ev.events = EPOLLIN;
+  ev.data.fd = event_fd_;
+  epoll_ctl(epoll_fd_, EPOLL_CTL_ADD, event_fd_, &ev);
+}
 
 Server::~Server() { Stop(); }
 
@@ -415,24 +424,20 @@ Status Server::Listen(const std::string& socket_path) {
 
 Status Server::Start(std::function<void()> on_fatal) {
   if (listen_fd_ < 0) return FailedPrecondition("Start() before Listen()");
+  if (stopping_.load()) return FailedPrecondition("server already stopped");
   on_fatal_ = std::move(on_fatal);
-  epoll_fd_ = epoll_create1(EPOLL_CLOEXEC);
-  event_fd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
   if (epoll_fd_ < 0 || event_fd_ < 0) return Internal("epoll/eventfd setup failed");
   epoll_event ev{};
   ev.events = EPOLLIN;
   ev.data.fd = listen_fd_;
   epoll_ctl(epoll_fd_, EPOLL_CTL_ADD, listen_fd_, &ev);
-  ev.data.fd = event_fd_;
-  epoll_ctl(epoll_fd_, EPOLL_CTL_ADD, event_fd_, &ev);
-  stopping_.store(false);
   thread_ = std::thread([this] { LoopMain(); });
   return Status::Ok();
 }
 
 void Server::Stop() {
+  stopping_.store(true);  // later Post() calls are dropped
   if (thread_.joinable()) {
-    stopping_.store(true);
     uint64_t one = 1;
     ssize_t w = write(event_fd_, &one, sizeof(one));
     (void)w;

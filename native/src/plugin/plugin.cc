@@ -295,25 +295,32 @@ Status Plugin::Register() {
 }
 
 Status Plugin::Start(std::function<void()> on_fatal) {
-  if (server_) return FailedPrecondition("plugin already started");
-  server_ = std::make_unique<grpc::Server>(spec_.resource_name);
-  server_->AddUnary(std::string(kSvc) + "GetDevicePluginOptions",
-                    [this](std::string_view q, std::string* r) { return HandleGetOptions(q, r); });
-  server_->AddUnary(std::string(kSvc) + "Allocate",
-                    [this](std::string_view q, std::string* r) { return HandleAllocate(q, r); });
-  server_->AddUnary(std::string(kSvc) + "GetPreferredAllocation",
-                    [this](std::string_view q, std::string* r) { return HandlePreferred(q, r); });
-  server_->AddUnary(std::string(kSvc) + "PreStartContainer",
-                    [this](std::string_view q, std::string* r) { return HandlePreStart(q, r); });
-  server_->AddServerStream(std::string(kSvc) + "ListAndWatch",
-                           [this](std::string_view, std::shared_ptr<grpc::ServerStream> s) {
-                             law_streams_.push_back(s);
-                             s->Send(law_bytes_);
-                             stats_.law_sends.fetch_add(1, std::memory_order_relaxed);
-                             return Status::Ok();
-                           });
-  Status st = server_->Listen(socket_path());
-  if (st.ok()) st = server_->Start(std::move(on_fatal));
+  if (running()) return FailedPrecondition("plugin already started");
+  auto srv = std::make_unique<grpc::Server>(spec_.resource_name);
+  srv->AddUnary(std::string(kSvc) + "GetDevicePluginOptions",
+                [this](std::string_view q, std::string* r) { return HandleGetOptions(q, r); });
+  srv->AddUnary(std::string(kSvc) + "Allocate",
+                [this](std::string_view q, std::string* r) { return HandleAllocate(q, r); });
+  srv->AddUnary(std::string(kSvc) + "GetPreferredAllocation",
+                [this](std::string_view q, std::string* r) { return HandlePreferred(q, r); });
+  srv->AddUnary(std::string(kSvc) + "PreStartContainer",
+                [this](std::string_view q, std::string* r) { return HandlePreStart(q, r); });
+  srv->AddServerStream(std::string(kSvc) + "ListAndWatch",
+                       [this](std::string_view, std::shared_ptr<grpc::ServerStream> s) {
+                         law_streams_.push_back(s);
+                         s->Send(law_bytes_);
+                         stats_.law_sends.fetch_add(1, std::memory_order_relaxed);
+                         return Status::Ok();
+                       });
+  // Publish before the loop starts: from here on health updates are posted to the
+  // loop (queued until it runs) instead of being applied on the caller's thread.
+  grpc::Server* raw = srv.get();
+  {
+    std::lock_guard<std::mutex> lk(server_mu_);
+    server_ = std::move(srv);
+  }
+  Status st = raw->Listen(socket_path());
+  if (st.ok()) st = raw->Start(std::move(on_fatal));
   if (st.ok()) {
     // Block until the server answers, like the reference's self-dial (server.go:207-213).
     auto probe = grpc::Channel::Dial(socket_path(), opts_.dial_timeout_ms);
@@ -322,8 +329,7 @@ Status Plugin::Start(std::function<void()> on_fatal) {
   if (!st.ok()) {
     LOG_ERROR(kComp, "could not start device plugin for '%s': %s", spec_.resource_name.c_str(),
               st.ToString().c_str());
-    server_->Stop();
-    server_.reset();
+    Stop();
     return st;
   }
   LOG_INFO(kComp, "serving '%s' on %s (%zu devices, %zu advertised)", spec_.resource_name.c_str(),
@@ -342,19 +348,22 @@ Status Plugin::Start(std::function<void()> on_fatal) {
 }
 
 void Plugin::Stop() {
-  if (!server_) return;
+  // Held throughout: the loop thread never takes server_mu_, and a concurrent
+  // PostHealth must not fall back to a direct ApplyHealth while the loop still runs.
+  std::lock_guard<std::mutex> lk(server_mu_);
+  std::unique_ptr<grpc::Server> srv = std::move(server_);
+  if (!srv) return;
   LOG_INFO(kComp, "stopping '%s' on %s", spec_.resource_name.c_str(), socket_path().c_str());
   // End open ListAndWatch streams cleanly (the reference returns nil on stop).
   auto done = std::make_shared<std::promise<void>>();
   auto fut = done->get_future();
-  server_->Post([this, done] {
+  srv->Post([this, done] {
     for (auto& s : law_streams_) s->Finish(Status::Ok());
     law_streams_.clear();
     done->set_value();
   });
   fut.wait_for(std::chrono::milliseconds(500));
-  server_->Stop();
-  server_.reset();
+  srv->Stop();
   law_streams_.clear();
 }
 
@@ -383,18 +392,21 @@ void Plugin::SetHandleHealth(int handle, bool healthy, const std::string& reason
   for (size_t i = 0; i < units_.size(); ++i)
     for (int h : units_[i].handles)
       if (h == handle) us.push_back(static_cast<int>(i));
-  if (us.empty()) return;
-  if (server_) server_->Post([this, us, healthy, reason] { ApplyHealth(us, healthy, reason); });
-  else ApplyHealth(us, healthy, reason);
+  PostHealth(std::move(us), healthy, reason);
 }
 
 void Plugin::SetGpuHealth(int gpu, bool healthy, const std::string& reason) {
   std::vector<int> us;
   for (size_t i = 0; i < units_.size(); ++i)
     if (units_[i].gpu == gpu) us.push_back(static_cast<int>(i));
+  PostHealth(std::move(us), healthy, reason);
+}
+
+void Plugin::PostHealth(std::vector<int> us, bool healthy, const std::string& reason) {
   if (us.empty()) return;
+  std::lock_guard<std::mutex> lk(server_mu_);
   if (server_) server_->Post([this, us, healthy, reason] { ApplyHealth(us, healthy, reason); });
-  else ApplyHealth(us, healthy, reason);
+  else ApplyHealth(us, healthy, reason);  // not serving: the lock serialises callers
 }
 
 std::string Plugin::StatsJson() const {

@@ -28,6 +28,7 @@
 #include <atomic>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -109,7 +110,10 @@ class Plugin {
   // Serve -> self-dial -> Register. On failure everything is torn down again.
   Status Start(std::function<void()> on_fatal = nullptr);
   void Stop();
-  bool running() const { return server_ != nullptr; }
+  bool running() const {
+    std::lock_guard<std::mutex> lk(server_mu_);
+    return server_ != nullptr;
+  }
 
   // Thread-safe. Marks every device that contains amdsmi handle `handle`.
   void SetHandleHealth(int handle, bool healthy, const std::string& reason);
@@ -129,6 +133,7 @@ class Plugin {
   void BuildUnits();
   void RebuildListAndWatch();
   void ApplyHealth(const std::vector<int>& units, bool healthy, const std::string& reason);
+  void PostHealth(std::vector<int> units, bool healthy, const std::string& reason);
   Status Register();
 
   std::shared_ptr<const inventory::Snapshot> snap_;
@@ -149,6 +154,9 @@ class Plugin {
   std::string law_bytes_;
   std::vector<std::shared_ptr<grpc::ServerStream>> law_streams_;
 
+  // Guards server_ itself (not the loop-thread state): health updates arrive from
+  // the monitor thread while the supervisor may be stopping the plugin.
+  mutable std::mutex server_mu_;
   std::unique_ptr<grpc::Server> server_;
   RpcStats stats_;
 };

@@ -7,6 +7,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cstdio>
 #include <functional>
 #include <string>
@@ -281,6 +282,30 @@ static void TestGrpcLoopback() {
     CHECK((*ch)->Recv(*sid, &m, 2000).code() == Code::kNotFound);
   }
   srv.Stop();
+  unlink(sock.c_str());
+
+  // Crash budget (server.go:177-205): a loop that keeps failing within the hour
+  // is fatal on the 7th failure; it keeps serving until then.
+  g_case = "grpc/crash-budget";
+  grpc::Server flaky("flaky");
+  flaky.AddUnary("/t.S/Echo", [](std::string_view q, std::string* r) { r->assign(q); return Status::Ok(); });
+  std::atomic<int> fatal{0};
+  CHECK(flaky.Listen(sock).ok());
+  CHECK(flaky.Start([&] { fatal.fetch_add(1); }).ok());
+  for (int i = 0; i < 6; ++i) {
+    flaky.InjectLoopFailureForTest();
+    flaky.Post([] {});
+    usleep(20 * 1000);
+  }
+  CHECK(fatal.load() == 0);
+  auto ch2 = grpc::Channel::Dial(sock, 2000);
+  std::string r2;
+  CHECK(ch2.ok() && (*ch2)->Unary("/t.S/Echo", "still", &r2, 2000).ok() && r2 == "still");
+  flaky.InjectLoopFailureForTest();
+  flaky.Post([] {});
+  for (int i = 0; i < 100 && fatal.load() == 0; ++i) usleep(10 * 1000);
+  CHECK(fatal.load() == 1);
+  flaky.Stop();
   unlink(sock.c_str());
   rmdir(dir.c_str());
 }

@@ -1,0 +1,88 @@
+"""Packaging consistency: helm values/templates, static manifests, example pods.
+
+Every environment variable a manifest sets must be one the daemon reads (its
+--help lists them), and the helm values keep the reference chart's key names
+(reference deployments/helm/nvidia-device-plugin/values.yaml:1-47) where the
+meaning carries over.
+"""
+
+import glob
+import os
+import re
+import subprocess
+
+import yaml
+
+from k8s_gpu_sharing_plugin_amd import DAEMON
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHART = os.path.join(ROOT, "deployments", "helm", "amd-gpu-device-plugin")
+KNOWN_EXTRA_ENV = {"DP_DISABLE_HEALTHCHECKS", "DP_HEALTH_POLL_MS"}
+
+
+def daemon_envs():
+    out = subprocess.run([DAEMON, "--help"], capture_output=True, text=True, timeout=10).stdout
+    return set(re.findall(r"\(env ([A-Z_]+)", out)) | KNOWN_EXTRA_ENV
+
+
+def test_helm_values_keep_compatible_keys():
+    with open(os.path.join(CHART, "values.yaml")) as f:
+        v = yaml.safe_load(f)
+    for key in ("legacyDaemonsetAPI", "compatWithCPUManager", "failOnInitError", "deviceListStrategy",
+                "deviceIDStrategy", "resourceConfig", "nameOverride", "fullnameOverride",
+                "selectorLabelsOverride", "namespace", "image", "updateStrategy", "podSecurityContext",
+                "securityContext", "resources", "nodeSelector", "affinity", "tolerations", "runtimeClassName"):
+        assert key in v, key
+    assert v["partitionStrategy"] == "none"  # replaces migStrategy
+    assert v["driverRoot"] == "/"            # replaces nvidiaDriverRoot
+    assert v["resourceConfig"] == "gpu:gpu-mem-gb:-1"
+    assert v["nodeSelector"] == {"gpushare": "true"}
+    assert {"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"} in v["tolerations"]
+
+
+def test_helm_template_envs_are_daemon_envs():
+    with open(os.path.join(CHART, "templates", "daemonset.yaml")) as f:
+        text = f.read()
+    names = set(re.findall(r"name: ([A-Z][A-Z_]+)", text))
+    assert names and names <= daemon_envs(), names - daemon_envs()
+    assert "system-node-critical" in text
+    assert "/var/lib/kubelet/device-plugins" in text
+
+
+def test_static_manifests():
+    files = glob.glob(os.path.join(ROOT, "deployments", "static", "*.yml")) + [
+        os.path.join(ROOT, "amd-gpu-device-plugin.yml")]
+    assert len(files) >= 4
+    envs = daemon_envs()
+    for path in files:
+        with open(path) as f:
+            doc = yaml.safe_load(f)
+        assert doc["kind"] == "DaemonSet"
+        spec = doc["spec"]["template"]["spec"]
+        c = spec["containers"][0]
+        for e in c["env"]:
+            assert e["name"] in envs, (path, e["name"])
+        mounts = {m["mountPath"] for m in c["volumeMounts"]}
+        assert "/var/lib/kubelet/device-plugins" in mounts
+        assert spec["priorityClassName"] == "system-node-critical"
+        if "extensions-v1beta1" in path:
+            assert doc["apiVersion"] == "extensions/v1beta1"
+        else:
+            assert doc["apiVersion"] == "apps/v1"
+            assert doc["spec"]["selector"]["matchLabels"] == doc["spec"]["template"]["metadata"]["labels"]
+        if "cpumanager" in path:
+            assert c["securityContext"] == {"privileged": True}
+
+
+def test_example_pods_request_amd_resources():
+    seen = set()
+    for path in glob.glob(os.path.join(ROOT, "examples", "pods", "*.yml")):
+        with open(path) as f:
+            pod = yaml.safe_load(f)
+        assert pod["kind"] == "Pod"
+        for c in pod["spec"]["containers"]:
+            limits = (c.get("resources") or {}).get("limits") or {}
+            for r in limits:
+                assert r.startswith("amd.com/"), (path, r)
+                seen.add(r)
+    assert {"amd.com/gpu", "amd.com/sharedgpu", "amd.com/gpu-mem-gb", "amd.com/cpx-1xcd.36gb"} <= seen
