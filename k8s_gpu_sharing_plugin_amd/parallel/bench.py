@@ -41,6 +41,41 @@ def _sync(torch_mod):
         torch_mod.cuda.synchronize()
 
 
+def _server_stats(daemon):
+    """Asks the daemon for its RPC counters (SIGUSR1) and parses the log line."""
+    import signal
+    if daemon is None:
+        return {}
+    try:
+        before = daemon.log().count("stats: {")
+        daemon.signal(signal.SIGUSR1)
+        text = daemon.wait_log("stats: {", timeout=5, count=before + 1)
+        line = [ln for ln in text.splitlines() if "stats: {" in ln][-1]
+        return json.loads(line.split("stats: ", 1)[1])
+    except Exception:
+        return {}
+
+
+def _grpcio_allocate_p50(socket_path, calls=300):
+    try:
+        from ..utils import kubelet
+        c = kubelet.PluginClient(socket_path)
+        q, call = c.watch()
+        dev = q.get(timeout=5).devices[0].ID
+        call.cancel()
+        lat = []
+        for i in range(calls + 50):
+            t = time.perf_counter()
+            c.allocate([dev])
+            if i >= 50:
+                lat.append((time.perf_counter() - t) * 1e6)
+        c.close()
+        lat.sort()
+        return round(lat[len(lat) // 2], 2)
+    except Exception:
+        return None
+
+
 def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_mock=False,
         probe=True, log=print):
     try:
@@ -117,6 +152,8 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
             everyone = [None] * world
             dist.all_gather_object(everyone, stats)
         if rank == 0:
+            server = _server_stats(daemon)
+            grpcio = _grpcio_allocate_p50(info["socket"])
             ms_per_step = max(s["elapsed_s"] for s in everyone) / steps * 1e3
             p50 = max(s["allocate"]["p50_us"] for s in everyone)
             total_pods = sum(s["pods"] for s in everyone)
@@ -149,6 +186,11 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                 "preferred_p50_us": round(max(s["preferred"]["p50_us"] for s in everyone), 2),
                 "pod_p50_us": round(max(s["pod"]["p50_us"] for s in everyone), 2),
                 "pods_per_s": round(total_pods / (max(s["elapsed_s"] for s in everyone)), 1),
+                # in-daemon time of the Allocate handler (decode + lookup + encode), from SIGUSR1 stats
+                "server_allocate_handler_avg_us": server.get("allocate_handler_avg_us"),
+                # the same Allocate through grpcio (gRPC C-core + Python), i.e. what a
+                # heavyweight gRPC client stack adds on top of the plugin
+                "grpcio_client_allocate_p50_us": grpcio,
                 "per_rank": [{k: s[k] for k in ("rank", "rank_devices", "pods", "allocate", "preferred")}
                              for s in everyone],
             }

@@ -248,7 +248,8 @@ int RunDaemon(const Config& cfg) {
             LOG_INFO(kComp, "received SIGHUP, restarting");
             do_restart = true;
           } else if (si.ssi_signo == SIGUSR1) {
-            for (auto& p : plugins) LOG_INFO(kComp, "stats: %s", p->StatsJson().c_str());
+            // Explicitly requested: printed whatever the log level.
+            for (auto& p : plugins) Logf(LogLevel::kInfo, kComp, "stats: %s", p->StatsJson().c_str());
           } else {
             LOG_INFO(kComp, "received signal %s, shutting down", strsignal(static_cast<int>(si.ssi_signo)));
             quit = true;

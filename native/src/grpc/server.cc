@@ -94,6 +94,7 @@ class ServerConn {
 
   Server* srv_;
   std::map<int32_t, StreamState> streams_;
+  uint32_t epoll_events = 0;  // interest set currently registered with epoll
 
  private:
   void SubmitTrailersOnly(int32_t sid, int code, const std::string& msg);
@@ -495,6 +496,7 @@ void Server::AcceptAll() {
     ev.events = EPOLLIN | (conn->want_epollout() ? static_cast<uint32_t>(EPOLLOUT) : 0u);
     ev.data.fd = fd;
     epoll_ctl(epoll_fd_, EPOLL_CTL_ADD, fd, &ev);
+    conn->epoll_events = ev.events;
     stats_.connections.fetch_add(1, std::memory_order_relaxed);
     conns_[fd] = std::move(conn);
   }
@@ -533,10 +535,13 @@ Status Server::RunLoop() {
     std::vector<int> dead;
     for (auto& [fd, c] : conns_) {
       if (!c->Flush() || c->Done()) { dead.push_back(fd); continue; }
+      uint32_t want = EPOLLIN | (c->want_epollout() ? static_cast<uint32_t>(EPOLLOUT) : 0u);
+      if (want == c->epoll_events) continue;  // no syscall on the common path
       epoll_event ev{};
-      ev.events = EPOLLIN | (c->want_epollout() ? static_cast<uint32_t>(EPOLLOUT) : 0u);
+      ev.events = want;
       ev.data.fd = fd;
       epoll_ctl(epoll_fd_, EPOLL_CTL_MOD, fd, &ev);
+      c->epoll_events = want;
     }
     for (int fd : dead) CloseConn(fd);
   }
