@@ -51,6 +51,19 @@ def run(device: int = 0, nbytes: int = 1 << 30, iters: int = 10) -> dict:
     return res
 
 
+def bw_sweep(device: int = 0, nbytes: int = 1 << 30, iters: int = 10) -> list:
+    """HBM copy bandwidth of each copy-kernel variant (unroll x NT stores x grid)."""
+    so = _lib()
+    so.adp_probe_bw_sweep.argtypes = [ctypes.c_int, ctypes.c_ulonglong, ctypes.c_int, ctypes.c_char_p,
+                                      ctypes.c_int]
+    buf = ctypes.create_string_buffer(1 << 16)
+    rc = so.adp_probe_bw_sweep(device, nbytes, iters, buf, len(buf))
+    res = json.loads(buf.value.decode())
+    if rc != 0:
+        raise ProbeError(res)
+    return res
+
+
 def device_for_bdf(bdf: str) -> int:
     """HIP ordinal of the GPU at PCI address `bdf` ("dddd:bb:dd.f"), function ignored."""
     want = bdf.lower().rsplit(".", 1)[0]

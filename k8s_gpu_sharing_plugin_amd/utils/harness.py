@@ -85,31 +85,46 @@ class NativeKubelet:
 
     def start(self):
         self.proc = subprocess.Popen([KUBELET_STUB, "serve", "--kubelet-socket", self.socket_path],
-                                     stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+                                     stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
         self.wait(lambda e: e.get("event") == "listening", 10)
         return self
 
     def wait(self, pred, timeout=10.0):
+        """Returns the first event (old or new) matching `pred`.
+
+        Reads the pipe with os.read on the raw fd: a buffered readline() after
+        select() can strand a second line in Python's buffer where select() no
+        longer sees it.
+        """
         import json
         import select
         deadline = time.time() + timeout
         for e in self.events:
             if pred(e):
                 return e
+        fd = self.proc.stdout.fileno()
+        if not hasattr(self, "_pending"):
+            self._pending = b""
         while time.time() < deadline:
-            r, _, _ = select.select([self.proc.stdout], [], [], 0.1)
+            r, _, _ = select.select([fd], [], [], 0.1)
             if not r:
                 continue
-            line = self.proc.stdout.readline()
-            if not line:
+            chunk = os.read(fd, 65536)
+            if not chunk:
                 break
-            try:
-                e = json.loads(line)
-            except ValueError:
-                continue
-            self.events.append(e)
-            if pred(e):
-                return e
+            self._pending += chunk
+            *lines, self._pending = self._pending.split(b"\n")
+            hit = None
+            for line in lines:
+                try:
+                    e = json.loads(line)
+                except ValueError:
+                    continue
+                self.events.append(e)
+                if hit is None and pred(e):
+                    hit = e
+            if hit is not None:
+                return hit
         raise TimeoutError(f"event not seen; got {self.events[-5:]}")
 
     def stop(self):

@@ -63,18 +63,30 @@ __global__ void __launch_bounds__(256) FillKernel(uint4* p, size_t n) {
   }
 }
 
-__global__ void __launch_bounds__(256) CopyKernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
-                                                  size_t n) {
-  size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+// Tunable streaming copy for the bandwidth sweep: UNROLL independent 16-byte
+// loads in flight per lane, optional non-temporal (streaming) stores.
+template <int UNROLL, bool NT>
+__global__ void __launch_bounds__(256) CopyKernelT(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                   size_t n) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
   size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  // Two independent 16-byte loads in flight per lane per iteration.
-  for (; i + stride < n; i += 2 * stride) {
-    uint4 a = src[i];
-    uint4 b = src[i + stride];
-    dst[i] = a;
-    dst[i + stride] = b;
+  for (; i + (UNROLL - 1) * stride < n; i += UNROLL * stride) {
+    uint4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      if (NT) {
+        __builtin_nontemporal_store(v[u].x, &dst[i + u * stride].x);
+        __builtin_nontemporal_store(v[u].y, &dst[i + u * stride].y);
+        __builtin_nontemporal_store(v[u].z, &dst[i + u * stride].z);
+        __builtin_nontemporal_store(v[u].w, &dst[i + u * stride].w);
+      } else {
+        dst[i + u * stride] = v[u];
+      }
+    }
   }
-  if (i < n) dst[i] = src[i];
+  for (; i < n; i += stride) dst[i] = src[i];
 }
 
 __global__ void __launch_bounds__(256) SumKernel(const uint4* __restrict__ p, size_t n,
@@ -109,6 +121,57 @@ int Fail(char* out, int len, hipError_t e, const char* where) {
   } while (0)
 
 }  // namespace
+
+// Bandwidth sweep over copy-kernel variants (unroll x store policy x grid size),
+// used to pick the probe's default copy configuration on real hardware.
+extern "C" int adp_probe_bw_sweep(int device, unsigned long long bytes, int iters, char* out, int len) {
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  const int cus = prop.multiProcessorCount;
+  size_t n = bytes / sizeof(uint4);
+  uint4 *src = nullptr, *dst = nullptr;
+  HIP_TRY(hipMalloc(&src, n * sizeof(uint4)));
+  HIP_TRY(hipMalloc(&dst, n * sizeof(uint4)));
+  hipLaunchKernelGGL(FillKernel, dim3(cus * 8), dim3(256), 0, 0, src, n);
+  hipEvent_t e0, e1;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  using Launch = void (*)(dim3, const uint4*, uint4*, size_t);
+  struct Variant { const char* name; Launch fn; };
+#define V(U, NT) {#U "x" #NT, [](dim3 g, const uint4* s, uint4* d, size_t m) { \
+    hipLaunchKernelGGL((CopyKernelT<U, NT>), g, dim3(256), 0, 0, s, d, m); }}
+  Variant variants[] = {V(1, false), V(2, false), V(4, false), V(8, false),
+                        V(1, true),  V(2, true),  V(4, true),  V(8, true)};
+#undef V
+  std::string s = "[";
+  bool first = true;
+  for (int bpc : {2, 4, 8, 16}) {
+    for (const auto& var : variants) {
+      dim3 grid(cus * bpc);
+      var.fn(grid, src, dst, n);  // warm-up
+      HIP_TRY(hipEventRecord(e0, 0));
+      for (int i = 0; i < iters; ++i) var.fn(grid, src, dst, n);
+      HIP_TRY(hipEventRecord(e1, 0));
+      HIP_TRY(hipEventSynchronize(e1));
+      float ms = 0;
+      HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+      double gbps = (2.0 * n * sizeof(uint4) * iters) / (ms * 1e-3) / 1e9;
+      char buf[160];
+      snprintf(buf, sizeof(buf), "%s{\"blocks_per_cu\": %d, \"variant\": \"%s\", \"gbps\": %.1f}",
+               first ? "" : ", ", bpc, var.name, gbps);
+      s += buf;
+      first = false;
+    }
+  }
+  s += "]";
+  HIP_TRY(hipEventDestroy(e0));
+  HIP_TRY(hipEventDestroy(e1));
+  HIP_TRY(hipFree(src));
+  HIP_TRY(hipFree(dst));
+  snprintf(out, len, "%s", s.c_str());
+  return 0;
+}
 
 extern "C" int adp_probe_device_count() {
   int n = 0;
@@ -167,15 +230,19 @@ extern "C" int adp_probe_run(int device, unsigned long long bytes, int iters, ch
   HIP_TRY(hipMalloc(&dst, n * sizeof(uint4)));
   HIP_TRY(hipMalloc(&d_sum, sizeof(unsigned long long)));
   const int blocks = cus * 8;
+  // Copy shape picked by adp_probe_bw_sweep on MI355X (profiles/probe_bw_sweep_r1.json):
+  // 2 workgroups/CU, 2 x 16 B loads in flight per lane, non-temporal stores:
+  // 5.72 TB/s vs 4.63 TB/s for the first-cut 8 WG/CU shape.
+  const int copy_blocks = cus * 2;
   hipLaunchKernelGGL(FillKernel, dim3(blocks), dim3(256), 0, 0, src, n);
-  hipLaunchKernelGGL(CopyKernel, dim3(blocks), dim3(256), 0, 0, src, dst, n);  // warm-up
+  hipLaunchKernelGGL((CopyKernelT<2, true>), dim3(copy_blocks), dim3(256), 0, 0, src, dst, n);  // warm-up
   HIP_TRY(hipGetLastError());
   hipEvent_t e0, e1;
   HIP_TRY(hipEventCreate(&e0));
   HIP_TRY(hipEventCreate(&e1));
   HIP_TRY(hipEventRecord(e0, 0));
   for (int i = 0; i < iters; ++i)
-    hipLaunchKernelGGL(CopyKernel, dim3(blocks), dim3(256), 0, 0, src, dst, n);
+    hipLaunchKernelGGL((CopyKernelT<2, true>), dim3(copy_blocks), dim3(256), 0, 0, src, dst, n);
   HIP_TRY(hipEventRecord(e1, 0));
   HIP_TRY(hipEventSynchronize(e1));
   float ms = 0;

@@ -156,6 +156,7 @@ void Plugin::RebuildListAndWatch() {
     pb::PutLen(&out, 1, dev);
   }
   law_bytes_ = std::move(out);
+  law_bytes_size_.store(law_bytes_.size(), std::memory_order_relaxed);
 }
 
 Status Plugin::HandleGetOptions(std::string_view, std::string* resp) {
@@ -245,6 +246,16 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
 }
 
 Status Plugin::HandlePreferred(std::string_view req, std::string* resp) {
+  uint64_t t0 = NowNs();
+  Status st = PreferredImpl(req, resp);
+  uint64_t dt = NowNs() - t0;
+  stats_.preferred_ns_total.fetch_add(dt, std::memory_order_relaxed);
+  uint64_t prev = stats_.preferred_ns_max.load(std::memory_order_relaxed);
+  while (dt > prev && !stats_.preferred_ns_max.compare_exchange_weak(prev, dt)) {}
+  return st;
+}
+
+Status Plugin::PreferredImpl(std::string_view req, std::string* resp) {
   pb::PreferredAllocationRequest r;
   ADP_RETURN_IF_ERROR(pb::Decode(req, &r));
   pb::PreferredAllocationResponse out;
@@ -412,15 +423,18 @@ void Plugin::PostHealth(std::vector<int> us, bool healthy, const std::string& re
 std::string Plugin::StatsJson() const {
   uint64_t n = stats_.allocate_calls.load();
   double avg = n ? stats_.allocate_ns_total.load() / 1e3 / n : 0.0;
-  char buf[512];
+  uint64_t np = stats_.preferred_calls.load();
+  double pavg = np ? stats_.preferred_ns_total.load() / 1e3 / np : 0.0;
+  char buf[640];
   snprintf(buf, sizeof(buf),
            "{\"resource\": \"%s\", \"devices\": %zu, \"advertised\": %zu, \"allocate_calls\": %llu, "
            "\"allocate_handler_avg_us\": %.3f, \"allocate_handler_max_us\": %.3f, "
-           "\"preferred_calls\": %llu, \"law_sends\": %llu}",
+           "\"preferred_calls\": %llu, \"preferred_handler_avg_us\": %.3f, "
+           "\"preferred_handler_max_us\": %.3f, \"law_sends\": %llu, \"law_bytes\": %zu}",
            JsonEscape(spec_.resource_name).c_str(), units_.size(), advertised_.size(),
            static_cast<unsigned long long>(n), avg, stats_.allocate_ns_max.load() / 1e3,
-           static_cast<unsigned long long>(stats_.preferred_calls.load()),
-           static_cast<unsigned long long>(stats_.law_sends.load()));
+           static_cast<unsigned long long>(np), pavg, stats_.preferred_ns_max.load() / 1e3,
+           static_cast<unsigned long long>(stats_.law_sends.load()), law_bytes_size_.load());
   return buf;
 }
 

@@ -88,6 +88,8 @@ struct RpcStats {
   std::atomic<uint64_t> allocate_ns_total{0};
   std::atomic<uint64_t> allocate_ns_max{0};
   std::atomic<uint64_t> preferred_calls{0};
+  std::atomic<uint64_t> preferred_ns_total{0};
+  std::atomic<uint64_t> preferred_ns_max{0};
   std::atomic<uint64_t> law_sends{0};
 };
 
@@ -131,6 +133,7 @@ class Plugin {
 
  private:
   void BuildUnits();
+  Status PreferredImpl(std::string_view req, std::string* resp);
   void RebuildListAndWatch();
   void ApplyHealth(const std::vector<int>& units, bool healthy, const std::string& reason);
   void PostHealth(std::vector<int> units, bool healthy, const std::string& reason);
@@ -152,6 +155,7 @@ class Plugin {
   // Loop-thread state.
   std::vector<uint8_t> healthy_;
   std::string law_bytes_;
+  std::atomic<size_t> law_bytes_size_{0};  // readable from any thread (stats)
   std::vector<std::shared_ptr<grpc::ServerStream>> law_streams_;
 
   // Guards server_ itself (not the loop-thread state): health updates arrive from
