@@ -1,8 +1,11 @@
 #include "alloc/replicas.h"
 
 #include <algorithm>
+#include <cstdint>
+#include <cstring>
 #include <map>
 #include <set>
+#include <unordered_map>
 
 namespace adp::alloc {
 
@@ -38,32 +41,65 @@ bool ParseReplicaPolicy(std::string_view s, ReplicaPolicy* out) {
 
 namespace {
 
-// Replicas still available on one physical device.
+// Replicas still available on one physical device. Views point into the
+// caller's request buffer; nothing is copied until the result is built.
 struct PhysicalPool {
+  std::string_view prefix;
   bool allocated = false;
-  std::vector<std::string> replicas;  // sorted at construction
+  std::vector<std::string_view> replicas;  // [head, end) are still available
+  size_t head = 0;
+  size_t sorted_upto = 0;  // [head, sorted_upto) is sorted and holds the smallest
+  bool fully_sorted = false;
 
+  size_t size() const { return replicas.size() - head; }
+
+  // Replicas share `prefix`, so comparing the suffixes gives the reference's
+  // lexicographic order (sort.Strings) at a fraction of the cost.
+  bool Less(std::string_view a, std::string_view b) const {
+    return a.substr(prefix.size()) < b.substr(prefix.size());
+  }
+  void SortAll() {
+    if (fully_sorted) return;
+    std::sort(replicas.begin() + head, replicas.end(),
+              [this](std::string_view a, std::string_view b) { return Less(a, b); });
+    fully_sorted = true;
+    sorted_upto = replicas.size();
+  }
   // Take a specific replica. The reference removes by swapping the last element
   // into the hole (replica.go:55-59); that order is observable through later
-  // TakeAny() calls, so it is reproduced exactly.
-  bool Take(const std::string& id) {
-    auto it = std::find(replicas.begin(), replicas.end(), id);
+  // TakeAny() calls, so it is reproduced exactly (on the fully sorted list).
+  bool Take(std::string_view id) {
+    SortAll();
+    auto it = std::find(replicas.begin() + head, replicas.end(), id);
     if (it == replicas.end()) return false;
     *it = replicas.back();
     replicas.pop_back();
+    sorted_upto = replicas.size();
     allocated = true;
     return true;
   }
-  std::string TakeAny() {
-    std::string id = replicas.front();
-    replicas.erase(replicas.begin());
+  // Smallest remaining replica (sort.Strings order). Sorts lazily in growing
+  // chunks: a spread request takes one replica per GPU, so a 294-replica pool
+  // usually needs a partial sort of a handful of elements, not a full sort.
+  std::string_view TakeAny() {
+    if (head == sorted_upto) {
+      size_t chunk = std::min(size(), std::max<size_t>(8, 2 * (sorted_upto - 0)));
+      std::partial_sort(replicas.begin() + head, replicas.begin() + head + chunk, replicas.end(),
+                        [this](std::string_view a, std::string_view b) { return Less(a, b); });
+      sorted_upto = head + chunk;
+    }
     allocated = true;
-    return id;
+    return replicas[head++];
   }
 };
 
-std::string MissingMsg(const std::string& id) {
-  return "device '" + id + "' in mustIncludeDeviceIDs is missing from availableDeviceIDs";
+std::string MissingMsg(std::string_view id) {
+  return "device '" + std::string(id) + "' in mustIncludeDeviceIDs is missing from availableDeviceIDs";
+}
+
+std::string_view StripView(std::string_view id, std::string_view join) {
+  size_t p = join.empty() ? std::string_view::npos : id.find(join);
+  return p == std::string_view::npos ? id : id.substr(0, p);
 }
 
 }  // namespace
@@ -72,77 +108,129 @@ Result<Prioritized> PrioritizeDevices(const std::vector<std::string>& available,
                                       const std::vector<std::string>& must_include,
                                       int allocation_size, ReplicaPolicy policy,
                                       std::string_view join) {
+  std::vector<std::string_view> a(available.begin(), available.end());
+  std::vector<std::string_view> m(must_include.begin(), must_include.end());
+  return PrioritizeDeviceViews(a, m, allocation_size, policy, join);
+}
+
+Result<Prioritized> PrioritizeDeviceViews(const std::vector<std::string_view>& available,
+                                      const std::vector<std::string_view>& must_include,
+                                      int allocation_size, ReplicaPolicy policy,
+                                      std::string_view join) {
   if (allocation_size < 0) return InvalidArgument("negative allocation size");
   if (static_cast<int>(must_include.size()) > allocation_size) {
     return InvalidArgument("mustIncludeDeviceIDs (" + std::to_string(must_include.size()) +
                            ") exceeds allocation size (" + std::to_string(allocation_size) + ")");
   }
 
-  // Ordered map == the reference's sorted key walk (replica.go:142-147).
-  std::map<std::string, PhysicalPool> pools;
-  for (const auto& id : available) pools[StripReplica(id, join)].replicas.push_back(id);
-  for (auto& [_, p] : pools) std::sort(p.replicas.begin(), p.replicas.end());
+  // Group by physical device. Pools are then visited in lexicographic order of
+  // the device ID, the reference's sorted key walk (replica.go:142-147).
+  // A node has few physical devices (8 GPUs, 64 partitions) and thousands of
+  // replicas: find the pool by a linear scan keyed on (length, first 8 bytes),
+  // confirmed with one memcmp, instead of hashing every ID.
+  std::vector<PhysicalPool> pools;
+  std::vector<uint64_t> tags;
+  pools.reserve(64);
+  auto tag_of = [](std::string_view s) {
+    uint64_t t = 0;
+    memcpy(&t, s.data(), std::min<size_t>(8, s.size()));
+    return t ^ (static_cast<uint64_t>(s.size()) << 56);
+  };
+  size_t last = SIZE_MAX;
+  for (std::string_view id : available) {
+    std::string_view dev = StripView(id, join);
+    size_t at = SIZE_MAX;
+    if (last != SIZE_MAX && pools[last].prefix == dev) {
+      at = last;  // runs of the same device are common (sorted lists)
+    } else {
+      uint64_t t = tag_of(dev);
+      for (size_t i = 0; i < pools.size(); ++i)
+        if (tags[i] == t && pools[i].prefix == dev) { at = i; break; }
+      if (at == SIZE_MAX) {
+        at = pools.size();
+        pools.emplace_back();
+        pools.back().prefix = dev;
+        pools.back().replicas.reserve(available.size() / 8 + 1);
+        tags.push_back(t);
+      }
+    }
+    pools[at].replicas.push_back(id);
+    last = at;
+  }
+  auto find_pool = [&](std::string_view dev) -> PhysicalPool* {
+    for (auto& p : pools)
+      if (p.prefix == dev) return &p;
+    return nullptr;
+  };
+  std::vector<PhysicalPool*> order;
+  order.reserve(pools.size());
+  for (auto& p : pools) order.push_back(&p);
+  std::sort(order.begin(), order.end(),
+            [](const PhysicalPool* x, const PhysicalPool* y) { return x->prefix < y->prefix; });
 
-  Prioritized out;
-  out.ids.reserve(allocation_size);
+  std::vector<std::string_view> chosen;
+  chosen.reserve(allocation_size);
   bool unique = true;
-  for (const auto& id : must_include) {
-    auto it = pools.find(StripReplica(id, join));
-    if (it == pools.end()) return NotFound(MissingMsg(id));
-    if (it->second.allocated) unique = false;
-    if (!it->second.Take(id)) return NotFound(MissingMsg(id));
-    out.ids.push_back(id);
+  for (std::string_view id : must_include) {
+    PhysicalPool* found = find_pool(StripView(id, join));
+    if (!found) return NotFound(MissingMsg(id));
+    PhysicalPool& pool = *found;
+    if (pool.allocated) unique = false;
+    if (!pool.Take(id)) return NotFound(MissingMsg(id));
+    chosen.push_back(id);
   }
 
+  Prioritized out;
   if (policy == ReplicaPolicy::kSpread) {
-    for (int i = static_cast<int>(out.ids.size()); i < allocation_size; ++i) {
+    for (int i = static_cast<int>(chosen.size()); i < allocation_size; ++i) {
       // First priority: a physical device not yet used by this request; second:
       // the one with the most replicas left. Ties -> lexicographically first.
       PhysicalPool* best_unalloc = nullptr;
       PhysicalPool* best_alloc = nullptr;
       size_t hi_unalloc = 0, hi_alloc = 0;
-      for (auto& [_, p] : pools) {
-        size_t n = p.replicas.size();
-        if (p.allocated) {
-          if (n > hi_alloc) { best_alloc = &p; hi_alloc = n; }
+      for (PhysicalPool* p : order) {
+        size_t n = p->size();
+        if (p->allocated) {
+          if (n > hi_alloc) { best_alloc = p; hi_alloc = n; }
         } else {
-          if (n > hi_unalloc) { best_unalloc = &p; hi_unalloc = n; }
+          if (n > hi_unalloc) { best_unalloc = p; hi_unalloc = n; }
         }
       }
       PhysicalPool* pick = best_unalloc ? best_unalloc : best_alloc;
       if (!pick) return FailedPrecondition("no devices left to allocate");
       if (pick->allocated) unique = false;
-      out.ids.push_back(pick->TakeAny());
+      chosen.push_back(pick->TakeAny());
     }
     out.non_unique = !unique;
   } else {
     // Pack: finish on devices this request already touches, then best-fit the
     // remainder onto as few untouched devices as possible.
-    int need = allocation_size - static_cast<int>(out.ids.size());
-    for (auto& [_, p] : pools) {
-      while (need > 0 && p.allocated && !p.replicas.empty()) {
-        out.ids.push_back(p.TakeAny());
+    int need = allocation_size - static_cast<int>(chosen.size());
+    for (PhysicalPool* p : order) {
+      while (need > 0 && p->allocated && p->size() > 0) {
+        chosen.push_back(p->TakeAny());
         --need;
       }
     }
     while (need > 0) {
-      PhysicalPool* fit = nullptr;     // smallest pool that fits the remainder
-      PhysicalPool* largest = nullptr; // otherwise drain the largest
-      for (auto& [_, p] : pools) {
-        if (p.allocated || p.replicas.empty()) continue;
-        size_t n = p.replicas.size();
-        if (n >= static_cast<size_t>(need) && (!fit || n < fit->replicas.size())) fit = &p;
-        if (!largest || n > largest->replicas.size()) largest = &p;
+      PhysicalPool* fit = nullptr;      // smallest pool that fits the remainder
+      PhysicalPool* largest = nullptr;  // otherwise drain the largest
+      for (PhysicalPool* p : order) {
+        if (p->allocated || p->size() == 0) continue;
+        size_t n = p->size();
+        if (n >= static_cast<size_t>(need) && (!fit || n < fit->size())) fit = p;
+        if (!largest || n > largest->size()) largest = p;
       }
       PhysicalPool* pick = fit ? fit : largest;
       if (!pick) return FailedPrecondition("no devices left to allocate");
-      while (need > 0 && !pick->replicas.empty()) {
-        out.ids.push_back(pick->TakeAny());
+      while (need > 0 && pick->size() > 0) {
+        chosen.push_back(pick->TakeAny());
         --need;
       }
     }
   }
-  std::sort(out.ids.begin(), out.ids.end());
+  std::sort(chosen.begin(), chosen.end());
+  out.ids.assign(chosen.begin(), chosen.end());
   return out;
 }
 

@@ -54,6 +54,12 @@ inline constexpr const char* kNonUniqueMessage =
     "allocation resulted in non-unique devices due to requesting multiple GPU replicas and not "
     "having enough physical GPUs";
 
+// Zero-copy variant (views into the request buffer); the daemon's RPC path.
+Result<Prioritized> PrioritizeDeviceViews(const std::vector<std::string_view>& available,
+                                      const std::vector<std::string_view>& must_include,
+                                      int allocation_size,
+                                      ReplicaPolicy policy = ReplicaPolicy::kSpread,
+                                      std::string_view join = kReplicaJoin);
 Result<Prioritized> PrioritizeDevices(const std::vector<std::string>& available,
                                       const std::vector<std::string>& must_include,
                                       int allocation_size,

@@ -44,90 +44,94 @@ DeviceGraph::DeviceGraph(std::vector<int> parent, std::vector<int> scores)
 
 namespace {
 
-// Calls fn(mask) for every subset of `bits` (list of bit positions) of size s.
-void ForEachCombination(const std::vector<int>& bits, int s, const std::function<void(uint32_t)>& fn) {
-  int n = static_cast<int>(bits.size());
-  if (s < 0 || s > n) return;
-  if (s == 0) { fn(0); return; }
-  std::vector<int> idx(s);
-  for (int i = 0; i < s; ++i) idx[i] = i;
+constexpr int kExactMax = 12;  // exact search up to 12 whole GPUs (4096 DP states)
+
+// Calls fn(sub) for every subset of `pool` with exactly `sz` bits, in
+// lexicographic order of bit positions. No allocation.
+template <typename Fn>
+void Combinations(uint32_t pool, int sz, Fn&& fn) {
+  int pos[32], n = 0;
+  for (uint32_t a = pool; a; a &= a - 1) pos[n++] = __builtin_ctz(a);
+  if (sz < 0 || sz > n) return;
+  if (sz == 0) { fn(0u); return; }
+  int idx[32];
+  for (int i = 0; i < sz; ++i) idx[i] = i;
   while (true) {
     uint32_t m = 0;
-    for (int i : idx) m |= 1u << bits[i];
+    for (int i = 0; i < sz; ++i) m |= 1u << pos[idx[i]];
     fn(m);
-    int i = s - 1;
-    while (i >= 0 && idx[i] == n - s + i) --i;
+    int i = sz - 1;
+    while (i >= 0 && idx[i] == n - sz + i) --i;
     if (i < 0) return;
     ++idx[i];
-    for (int j = i + 1; j < s; ++j) idx[j] = idx[j - 1] + 1;
+    for (int j = i + 1; j < sz; ++j) idx[j] = idx[j - 1] + 1;
   }
 }
 
-std::vector<int> Bits(uint32_t mask) {
-  std::vector<int> out;
-  for (int i = 0; mask; ++i, mask >>= 1)
-    if (mask & 1) out.push_back(i);
-  return out;
-}
+// The reference objective, solved by memoized DP over subsets: f(S) = best total
+// intra-group score of splitting S into groups of size k (plus one group of the
+// remainder size when |S| is not a multiple of k).
+struct ExactSearch {
+  int m, k, r;
+  int s[kExactMax][kExactMax];
+  int memo[1 << kExactMax];
 
-std::vector<int> ExactSearch(const DeviceGraph& g, const std::vector<int>& avail,
-                             const std::vector<int>& required, int k) {
-  int m = static_cast<int>(avail.size());
-  int r = m % k;
-  auto set_score = [&](uint32_t mask) {
-    auto b = Bits(mask);
-    int s = 0;
-    for (size_t i = 0; i < b.size(); ++i)
-      for (size_t j = i + 1; j < b.size(); ++j) s += g.Score(avail[b[i]], avail[b[j]]);
-    return s;
-  };
-  std::vector<int> memo(1u << m, INT_MIN);
-  std::function<int(uint32_t)> f = [&](uint32_t mask) -> int {
+  int SetScore(uint32_t mask) const {
+    int t = 0;
+    for (uint32_t a = mask; a; a &= a - 1) {
+      int i = __builtin_ctz(a);
+      for (uint32_t b = a & (a - 1); b; b &= b - 1) t += s[i][__builtin_ctz(b)];
+    }
+    return t;
+  }
+
+  int F(uint32_t mask) {
     if (!mask) return 0;
     if (memo[mask] != INT_MIN) return memo[mask];
     int low = __builtin_ctz(mask);
     uint32_t rest = mask & ~(1u << low);
     int cnt = __builtin_popcount(mask);
     int best = INT_MIN / 2;
-    std::vector<int> sizes;
-    if (cnt >= k) sizes.push_back(k);
-    if (r > 0 && cnt % k == r) sizes.push_back(r);
-    auto rb = Bits(rest);
-    for (int sz : sizes) {
-      ForEachCombination(rb, sz - 1, [&](uint32_t sub) {
+    auto try_size = [&](int sz) {
+      Combinations(rest, sz - 1, [&](uint32_t sub) {
         uint32_t grp = sub | (1u << low);
-        int v = set_score(grp) + f(mask & ~grp);
+        int v = SetScore(grp) + F(mask & ~grp);
         if (v > best) best = v;
       });
-    }
-    memo[mask] = best;
-    return best;
-  };
+    };
+    if (cnt >= k) try_size(k);
+    if (r > 0 && cnt % k == r) try_size(r);
+    return memo[mask] = best;
+  }
 
-  uint32_t full = (m == 32) ? 0xffffffffu : ((1u << m) - 1);
-  uint32_t req = 0;
-  for (int d : required)
+  std::vector<int> Run(const DeviceGraph& g, const std::vector<int>& avail,
+                       const std::vector<int>& required) {
+    m = static_cast<int>(avail.size());
+    r = m % k;
     for (int i = 0; i < m; ++i)
-      if (avail[i] == d) req |= 1u << i;
-  auto free_bits = Bits(full & ~req);
-  int need = k - __builtin_popcount(req);
-  uint32_t best_grp = 0;
-  int best_total = INT_MIN, best_set = INT_MIN;
-  ForEachCombination(free_bits, need, [&](uint32_t sub) {
-    uint32_t grp = sub | req;
-    int s = set_score(grp);
-    int total = s + f(full & ~grp);
-    if (total > best_total || (total == best_total && s > best_set)) {
-      best_total = total;
-      best_set = s;
-      best_grp = grp;
-    }
-  });
-  std::vector<int> out;
-  for (int i : Bits(best_grp)) out.push_back(avail[i]);
-  std::sort(out.begin(), out.end());
-  return out;
-}
+      for (int j = 0; j < m; ++j) s[i][j] = i == j ? 0 : g.Score(avail[i], avail[j]);
+    std::fill(memo, memo + (1 << m), INT_MIN);
+    uint32_t full = (1u << m) - 1, req = 0;
+    for (int d : required)
+      for (int i = 0; i < m; ++i)
+        if (avail[i] == d) req |= 1u << i;
+    uint32_t best_grp = 0;
+    int best_total = INT_MIN, best_set = INT_MIN;
+    Combinations(full & ~req, k - __builtin_popcount(req), [&](uint32_t sub) {
+      uint32_t grp = sub | req;
+      int sc = SetScore(grp);
+      int total = sc + F(full & ~grp);
+      if (total > best_total || (total == best_total && sc > best_set)) {
+        best_total = total;
+        best_set = sc;
+        best_grp = grp;
+      }
+    });
+    std::vector<int> out;
+    for (uint32_t a = best_grp; a; a &= a - 1) out.push_back(avail[__builtin_ctz(a)]);
+    return out;  // ascending, since avail is sorted
+  }
+};
 
 std::vector<int> Hierarchical(const DeviceGraph& g, const std::vector<int>& avail,
                               const std::vector<int>& required, int size) {
@@ -208,7 +212,14 @@ std::vector<int> BestEffortAllocate(const DeviceGraph& g, const std::vector<int>
   std::set<int> parents;
   for (int d : avail) parents.insert(g.parent(d));
   bool distinct = parents.size() == avail.size();
-  if (distinct && avail.size() <= 12) return ExactSearch(g, avail, req, size);
+  if (distinct && avail.size() <= static_cast<size_t>(kExactMax)) {
+    // k == 1: every split scores 0, so the objective picks the required device or
+    // the first available one -- skip the search.
+    if (size == 1) return req.empty() ? std::vector<int>{avail.front()} : req;
+    ExactSearch search;
+    search.k = size;
+    return search.Run(g, avail, req);
+  }
   return Hierarchical(g, avail, req, size);
 }
 

@@ -177,17 +177,17 @@ Status Plugin::HandlePreStart(std::string_view req, std::string*) {
 
 Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
   uint64_t t0 = NowNs();
-  pb::AllocateRequest r;
-  ADP_RETURN_IF_ERROR(pb::Decode(req, &r));
+  std::vector<std::vector<std::string_view>> containers;
+  ADP_RETURN_IF_ERROR(pb::DecodeView(req, &containers));
   std::vector<int> us;
   std::string c, joined;
-  for (const auto& ids : r.container_requests) {
+  for (const auto& ids : containers) {
     us.clear();
-    for (const auto& id : ids) {
+    for (std::string_view id : ids) {
       auto it = advertised_index_.find(id);
       if (it == advertised_index_.end())
         return InvalidArgument("invalid allocation request for '" + spec_.resource_name +
-                               "': unknown device: " + id);
+                               "': unknown device: " + std::string(id));
       us.push_back(it->second);
     }
     // Unique physical devices. uuid strategy: sorted by ID (stripReplicas order,
@@ -256,30 +256,32 @@ Status Plugin::HandlePreferred(std::string_view req, std::string* resp) {
 }
 
 Status Plugin::PreferredImpl(std::string_view req, std::string* resp) {
-  pb::PreferredAllocationRequest r;
-  ADP_RETURN_IF_ERROR(pb::Decode(req, &r));
+  std::vector<pb::ContainerPreferredAllocationRequestView> reqs;
+  ADP_RETURN_IF_ERROR(pb::DecodeView(req, &reqs));
   pb::PreferredAllocationResponse out;
   stats_.preferred_calls.fetch_add(1, std::memory_order_relaxed);
-  for (const auto& cr : r.container_requests) {
+  for (const auto& cr : reqs) {
     if (replicated_) {
-      auto res = alloc::PrioritizeDevices(cr.available, cr.must_include, cr.allocation_size,
-                                          opts_.replica_policy);
+      auto res = alloc::PrioritizeDeviceViews(cr.available, cr.must_include, cr.allocation_size,
+                                              opts_.replica_policy);
       if (!res.ok()) return res.status();
       if (res->non_unique) LOG_DEBUG(kComp, "ignoring: %s", alloc::kNonUniqueMessage);
       out.container_responses.push_back(std::move(res->ids));
       continue;
     }
     std::vector<int> avail, must;
-    for (const auto& id : cr.available) {
+    for (std::string_view id : cr.available) {
       auto it = advertised_index_.find(id);
       if (it == advertised_index_.end())
-        return InvalidArgument("unable to retrieve list of available devices: unknown device " + id);
+        return InvalidArgument("unable to retrieve list of available devices: unknown device " +
+                               std::string(id));
       avail.push_back(it->second);
     }
-    for (const auto& id : cr.must_include) {
+    for (std::string_view id : cr.must_include) {
       auto it = advertised_index_.find(id);
       if (it == advertised_index_.end())
-        return InvalidArgument("unable to retrieve list of required devices: unknown device " + id);
+        return InvalidArgument("unable to retrieve list of required devices: unknown device " +
+                               std::string(id));
       must.push_back(it->second);
     }
     std::vector<std::string> ids;

@@ -148,7 +148,8 @@ class Plugin {
   std::unordered_map<std::string, int> unit_by_id_;
   std::vector<std::string> advertised_;       // advertised IDs (replicas or plain)
   std::vector<int> advertised_unit_;
-  std::unordered_map<std::string, int> advertised_index_;  // advertised ID -> unit
+  // advertised ID -> unit; keys view into advertised_ (never modified after build)
+  std::unordered_map<std::string_view, int> advertised_index_;
   std::string kfd_spec_bytes_;
   alloc::DeviceGraph graph_;
 

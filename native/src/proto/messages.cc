@@ -343,6 +343,56 @@ Status Decode(std::string_view b, AllocateResponse* m) {
   });
 }
 
+namespace {
+bool ReadView(Reader& r, WireType wt, std::vector<std::string_view>* v) {
+  if (wt != kLen) return false;
+  std::string_view s;
+  if (!r.ReadLen(&s)) return false;
+  v->push_back(s);
+  return true;
+}
+}  // namespace
+
+Status DecodeView(std::string_view b, std::vector<ContainerPreferredAllocationRequestView>* m) {
+  m->clear();
+  return ForEachField(b, "PreferredAllocationRequest", [&](uint32_t f, WireType wt, Reader& r) {
+    if (f != 1) return r.Skip(wt);
+    if (wt != kLen) return false;
+    std::string_view c;
+    if (!r.ReadLen(&c)) return false;
+    m->emplace_back();
+    auto& cr = m->back();
+    return ForEachField(c, "ContainerPreferredAllocationRequest", [&](uint32_t cf, WireType cwt, Reader& cr_r) {
+             if (cf == 1) return ReadView(cr_r, cwt, &cr.available);
+             if (cf == 2) return ReadView(cr_r, cwt, &cr.must_include);
+             if (cf == 3) {
+               if (cwt != kVarint) return false;
+               uint64_t v;
+               if (!cr_r.ReadVarint(&v)) return false;
+               cr.allocation_size = static_cast<int32_t>(static_cast<int64_t>(v));
+               return true;
+             }
+             return cr_r.Skip(cwt);
+           }).ok();
+  });
+}
+
+Status DecodeView(std::string_view b, std::vector<std::vector<std::string_view>>* m) {
+  m->clear();
+  return ForEachField(b, "AllocateRequest", [&](uint32_t f, WireType wt, Reader& r) {
+    if (f != 1) return r.Skip(wt);
+    if (wt != kLen) return false;
+    std::string_view c;
+    if (!r.ReadLen(&c)) return false;
+    m->emplace_back();
+    auto& ids = m->back();
+    return ForEachField(c, "ContainerAllocateRequest", [&](uint32_t cf, WireType cwt, Reader& cr) {
+             if (cf == 1) return ReadView(cr, cwt, &ids);
+             return cr.Skip(cwt);
+           }).ok();
+  });
+}
+
 Status Decode(std::string_view b, PreStartContainerRequest* m) {
   *m = {};
   return DecodeIdList(b, "PreStartContainerRequest", &m->device_ids);

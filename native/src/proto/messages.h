@@ -87,6 +87,19 @@ struct PreStartContainerRequest {
   std::vector<std::string> device_ids;
 };
 
+// --- zero-copy request views (string_views into the request buffer) ---
+// The RPC handlers decode into these: a GetPreferredAllocation for a node with
+// ~2.3k memory-unit replicas carries ~115 KB of IDs, and copying each into its
+// own std::string dominated the handler.
+struct ContainerPreferredAllocationRequestView {
+  std::vector<std::string_view> available;
+  std::vector<std::string_view> must_include;
+  int32_t allocation_size = 0;
+};
+Status DecodeView(std::string_view b, std::vector<ContainerPreferredAllocationRequestView>* m);
+// AllocateRequest: one ID list per container.
+Status DecodeView(std::string_view b, std::vector<std::vector<std::string_view>>* m);
+
 // --- encoders (append to *out) ---
 void Encode(const DevicePluginOptions& m, std::string* out);
 void Encode(const RegisterRequest& m, std::string* out);

@@ -1,0 +1,120 @@
+// In-process microbenchmarks of the RPC handlers (no transport): how long the
+// daemon spends inside Allocate / GetPreferredAllocation / a ListAndWatch
+// rebuild for the node shapes of BASELINE.json. Prints one JSON object.
+//
+// usage: adp_microbench [iterations]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "inventory/inventory.h"
+#include "plugin/plugin.h"
+#include "proto/messages.h"
+#include "strategy/strategy.h"
+
+using namespace adp;
+using Clock = std::chrono::steady_clock;
+
+namespace {
+
+std::shared_ptr<const inventory::Snapshot> Node(int gpus, int parts) {
+  std::vector<smi::ProcessorInfo> procs;
+  for (int g = 0; g < gpus; ++g) {
+    for (int p = 0; p < parts; ++p) {
+      smi::ProcessorInfo pi;
+      char uuid[64];
+      snprintf(uuid, sizeof(uuid), "%08x-0000-1%x00-80c0-bf9907890000", 0x75a30000 + g, p);
+      pi.uuid = uuid;
+      pi.bdf_id = (static_cast<uint64_t>(0x0c + 0x20 * g) << 8) | static_cast<uint64_t>(p);
+      pi.render_minor = 128 + 8 * g + p;
+      pi.numa_node = g < 4 ? 0 : 1;
+      pi.vram_mib = 294896 / parts;
+      pi.compute_partition = parts == 1 ? "SPX" : "CPX";
+      pi.memory_partition = parts == 1 ? "NPS1" : "NPS2";
+      pi.partition_id = p;
+      pi.num_cu = 256 / parts;
+      pi.xcd_count = 8 / parts;
+      procs.push_back(pi);
+    }
+  }
+  auto s = inventory::GroupProcessors(procs, {});
+  auto& snap = *s;
+  size_t n = snap->gpus.size();
+  for (size_t a = 0; a < n; ++a)
+    for (size_t b = 0; b < n; ++b)
+      if (a != b) { snap->gpu_links[a * n + b] = inventory::LinkClass::kXgmi; snap->gpu_hops[a * n + b] = 1; }
+  return snap;
+}
+
+template <typename Fn>
+double TimeUs(int iters, Fn fn) {
+  auto t0 = Clock::now();
+  for (int i = 0; i < iters; ++i) fn();
+  return std::chrono::duration<double, std::micro>(Clock::now() - t0).count() / iters;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  int iters = argc > 1 ? atoi(argv[1]) : 2000;
+  struct Case {
+    const char* name;
+    int gpus, parts;
+    strategy::PartitionStrategy ps;
+    const char* rc;
+    alloc::ReplicaPolicy pol;
+    int k;
+  };
+  std::vector<Case> cases = {
+      {"spx8_none", 8, 1, strategy::PartitionStrategy::kNone, "", alloc::ReplicaPolicy::kSpread, 1},
+      {"spx8_none_k4", 8, 1, strategy::PartitionStrategy::kNone, "", alloc::ReplicaPolicy::kSpread, 4},
+      {"spx8_timeslice4", 8, 1, strategy::PartitionStrategy::kNone, "gpu:sharedgpu:4", alloc::ReplicaPolicy::kSpread, 1},
+      {"cpx64_single_k4", 8, 8, strategy::PartitionStrategy::kSingle, "", alloc::ReplicaPolicy::kSpread, 4},
+      {"automem2352_spread_k1", 8, 1, strategy::PartitionStrategy::kNone, "gpu:gpu-mem-gb:-1", alloc::ReplicaPolicy::kSpread, 1},
+      {"automem2352_pack_k36", 8, 1, strategy::PartitionStrategy::kNone, "gpu:gpu-mem-gb:-1", alloc::ReplicaPolicy::kPack, 36},
+  };
+  printf("{");
+  bool first = true;
+  for (const auto& c : cases) {
+    auto snap = Node(c.gpus, c.parts);
+    auto rc = strategy::ResourceConfig::Parse(c.rc);
+    auto specs = strategy::BuildPluginSpecs(*snap, c.ps, *rc);
+    plugin::PluginOptions po;
+    po.register_with_kubelet = false;
+    po.replica_policy = c.pol;
+    plugin::Plugin p(snap, (*specs)[0], po);
+    const auto& ids = p.advertised_ids();
+    // GetPreferredAllocation with every advertised device free (a fresh node).
+    pb::PreferredAllocationRequest pr;
+    pr.container_requests.push_back({ids, {}, c.k});
+    std::string preq = pb::Encode(pr), presp;
+    double pref_us = TimeUs(iters / 4 + 1, [&] { presp.clear(); p.HandlePreferred(preq, &presp); });
+    pb::PreferredAllocationResponse prr;
+    pb::Decode(presp, &prr);
+    // Allocate the preferred set.
+    pb::AllocateRequest ar;
+    ar.container_requests.push_back(prr.container_responses.at(0));
+    std::string areq = pb::Encode(ar), aresp;
+    double alloc_us = TimeUs(iters, [&] { aresp.clear(); p.HandleAllocate(areq, &aresp); });
+    double decode_us = TimeUs(iters / 4 + 1, [&] {
+      std::vector<pb::ContainerPreferredAllocationRequestView> x;
+      pb::DecodeView(preq, &x);
+    });
+    double prio_us = 0;
+    if (p.replicated()) {
+      std::vector<std::string_view> views(ids.begin(), ids.end());
+      prio_us = TimeUs(iters / 4 + 1, [&] { alloc::PrioritizeDeviceViews(views, {}, c.k, c.pol); });
+    }
+    printf("%s\n \"%s_parts\": {\"decode_view_us\": %.3f, \"prioritize_us\": %.3f}", first ? "" : ",", c.name,
+           decode_us, prio_us);
+    first = false;
+    printf("%s\n \"%s\": {\"advertised\": %zu, \"k\": %d, \"preferred_us\": %.3f, \"preferred_request_bytes\": %zu, "
+           "\"preferred_decode_us\": %.3f, \"allocate_us\": %.3f, \"allocate_response_bytes\": %zu}",
+           first ? "" : ",", c.name, ids.size(), c.k, pref_us, preq.size(), decode_us, alloc_us, aresp.size());
+    first = false;
+  }
+  printf("\n}\n");
+  return 0;
+}
