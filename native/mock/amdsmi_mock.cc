@@ -198,8 +198,23 @@ bool Dead(const MockProc* p) {
   return stat(f.c_str(), &st) == 0;
 }
 
+// Call accounting for tests that pin "no device-library calls on the RPC path"
+// (reference defect B5): every query bumps a counter that is mirrored into
+// $AMDSMI_MOCK_CALL_COUNT_FILE when set.
+unsigned long long g_calls = 0;
+void CountCall() {
+  ++g_calls;
+  const char* f = getenv("AMDSMI_MOCK_CALL_COUNT_FILE");
+  if (!f) return;
+  FILE* fp = fopen(f, "w");
+  if (!fp) return;
+  fprintf(fp, "%llu\n", g_calls);
+  fclose(fp);
+}
+
 #define GET_PROC(h)                                   \
   std::lock_guard<std::mutex> lk(g_mu);               \
+  CountCall();                                        \
   MockProc* p = P(h);                                 \
   if (!p) return AMDSMI_STATUS_INVAL;                 \
   if (Dead(p)) return AMDSMI_STATUS_NOT_FOUND;
@@ -250,6 +265,7 @@ amdsmi_status_t amdsmi_status_code_to_string(amdsmi_status_t status, const char*
 
 amdsmi_status_t amdsmi_get_socket_handles(uint32_t* count, amdsmi_socket_handle* out) {
   std::lock_guard<std::mutex> lk(g_mu);
+  CountCall();
   if (!g || !count) return AMDSMI_STATUS_INVAL;
   uint32_t n = static_cast<uint32_t>(g->gpus.size());
   if (!out) { *count = n; return AMDSMI_STATUS_SUCCESS; }
@@ -262,6 +278,7 @@ amdsmi_status_t amdsmi_get_socket_handles(uint32_t* count, amdsmi_socket_handle*
 amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle sock, uint32_t* count,
                                              amdsmi_processor_handle* out) {
   std::lock_guard<std::mutex> lk(g_mu);
+  CountCall();
   if (!g || !count) return AMDSMI_STATUS_INVAL;
   MockGpu* mg = static_cast<MockGpu*>(sock);
   uint32_t n = static_cast<uint32_t>(mg->procs.size());
@@ -377,6 +394,7 @@ amdsmi_status_t amdsmi_get_gpu_xcd_counter(amdsmi_processor_handle h, uint16_t* 
 amdsmi_status_t amdsmi_topo_get_link_type(amdsmi_processor_handle a, amdsmi_processor_handle b,
                                           uint64_t* hops, amdsmi_link_type_t* type) {
   std::lock_guard<std::mutex> lk(g_mu);
+  CountCall();
   MockProc* pa = P(a);
   MockProc* pb = P(b);
   if (!pa || !pb) return AMDSMI_STATUS_INVAL;
@@ -396,6 +414,7 @@ amdsmi_status_t amdsmi_topo_get_link_type(amdsmi_processor_handle a, amdsmi_proc
 amdsmi_status_t amdsmi_topo_get_link_weight(amdsmi_processor_handle a, amdsmi_processor_handle b,
                                             uint64_t* w) {
   std::lock_guard<std::mutex> lk(g_mu);
+  CountCall();
   MockProc* pa = P(a);
   MockProc* pb = P(b);
   if (!pa || !pb) return AMDSMI_STATUS_INVAL;

@@ -75,6 +75,12 @@ const std::vector<FlagDef>& Table() {
       {"include-card-nodes", "INCLUDE_CARD_NODES", "includeCardNodes", Kind::kBool,
        "also pass /dev/dri/card<N> nodes (not needed for compute)",
        [](Flags& f) -> void* { return &f.include_card_nodes; }},
+      {"trace", "ADP_TRACE", "trace", Kind::kBool,
+       "log every RPC (method, status, sizes, handler time)",
+       [](Flags& f) -> void* { return &f.trace; }},
+      {"cdi-spec-dir", "CDI_SPEC_DIR", "cdiSpecDir", Kind::kString,
+       "directory for the generated CDI spec (cdi-annotations / cdi-cri strategies)",
+       [](Flags& f) -> void* { return &f.cdi_spec_dir; }},
   };
   return t;
 }

@@ -41,6 +41,8 @@ struct Flags {
   uint64_t auto_replica_unit_mib = 1000;
   std::string resource_prefix = "amd.com";
   bool include_card_nodes = false;
+  bool trace = false;
+  std::string cdi_spec_dir = "/var/run/cdi";
 };
 
 struct Config {

@@ -58,6 +58,8 @@ Result<Validated> Validate(const Config& cfg) {
   v.popts.pass_device_specs = f.pass_device_specs;
   v.popts.driver_root = f.driver_root;
   v.popts.auto_replica_unit_mib = f.auto_replica_unit_mib;
+  v.popts.trace = f.trace;
+  v.popts.cdi_spec_dir = f.cdi_spec_dir;
   v.bopts.driver_root = f.driver_root;
   v.bopts.include_card_nodes = f.include_card_nodes;
   std::string devs = Trim(f.devices);

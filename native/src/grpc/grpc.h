@@ -114,6 +114,8 @@ class Server {
   bool OnLoopThread() const;
   const std::string& socket_path() const { return socket_path_; }
   const ServerStats& stats() const { return stats_; }
+  // Log every unary call (method, status, sizes, handler time). Set before Start().
+  void set_trace(bool on) { trace_ = on; }
 
   // Test hook: make the next loop iteration fail as if epoll_wait errored.
   void InjectLoopFailureForTest() { inject_failure_.store(true); }
@@ -143,6 +145,7 @@ class Server {
   std::vector<std::function<void()>> posted_;
   std::map<int, std::unique_ptr<ServerConn>> conns_;
   uint64_t next_stream_id_ = 1;
+  bool trace_ = false;
   ServerStats stats_;
 };
 

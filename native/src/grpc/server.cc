@@ -311,7 +311,13 @@ void ServerConn::Dispatch(int32_t sid) {
   auto u = srv_->unary_.find(st->path);
   if (u != srv_->unary_.end()) {
     std::string resp;
+    auto t0 = srv_->trace_ ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
     Status s = u->second(req, &resp);
+    if (srv_->trace_) {
+      double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      Logf(LogLevel::kInfo, "trace", "%s %s %s req=%zuB resp=%zuB handler=%.2fus", srv_->name_.c_str(),
+           st->path.c_str(), s.ok() ? "OK" : s.ToString().c_str(), req.size(), resp.size(), us);
+    }
     st = Find(sid);  // handler cannot erase streams, but be defensive
     if (!st) return;
     if (!s.ok()) {

@@ -1,7 +1,11 @@
 #include "plugin/plugin.h"
 
+#include <errno.h>
+#include <sys/stat.h>
+
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <future>
 
 #include "common/log.h"
@@ -309,7 +313,13 @@ Status Plugin::Register() {
 
 Status Plugin::Start(std::function<void()> on_fatal) {
   if (running()) return FailedPrecondition("plugin already started");
+  if (opts_.list_strategy == DeviceListStrategy::kCdiAnnotations ||
+      opts_.list_strategy == DeviceListStrategy::kCdiCri) {
+    Status cs = WriteCdiSpec();
+    if (!cs.ok()) return cs;
+  }
   auto srv = std::make_unique<grpc::Server>(spec_.resource_name);
+  srv->set_trace(opts_.trace);
   srv->AddUnary(std::string(kSvc) + "GetDevicePluginOptions",
                 [this](std::string_view q, std::string* r) { return HandleGetOptions(q, r); });
   srv->AddUnary(std::string(kSvc) + "Allocate",
@@ -420,6 +430,45 @@ void Plugin::PostHealth(std::vector<int> us, bool healthy, const std::string& re
   std::lock_guard<std::mutex> lk(server_mu_);
   if (server_) server_->Post([this, us, healthy, reason] { ApplyHealth(us, healthy, reason); });
   else ApplyHealth(us, healthy, reason);  // not serving: the lock serialises callers
+}
+
+std::string Plugin::CdiSpecPath() const {
+  std::string name = spec_.resource_name;
+  for (auto& ch : name)
+    if (ch == '/') ch = '-';
+  return PathJoin(opts_.cdi_spec_dir, name + ".json");
+}
+
+std::string Plugin::CdiSpecJson() const {
+  auto node = [&](const std::string& path) {
+    return "{\"path\": \"" + JsonEscape(path) + "\", \"hostPath\": \"" +
+           JsonEscape(PathJoin(opts_.driver_root, path)) + "\", \"permissions\": \"rw\"}";
+  };
+  std::string out = "{\n  \"cdiVersion\": \"0.5.0\",\n  \"kind\": \"" + std::string(kCdiVendorClass) +
+                    "\",\n  \"containerEdits\": {\"deviceNodes\": [" + node("/dev/kfd") + "]},\n  \"devices\": [";
+  for (size_t i = 0; i < units_.size(); ++i) {
+    const Unit& u = units_[i];
+    out += i ? ",\n    " : "\n    ";
+    out += "{\"name\": \"" + JsonEscape(u.visible_id) + "\", \"containerEdits\": {\"deviceNodes\": [";
+    for (size_t p = 0; p < u.paths.size(); ++p) out += (p ? ", " : "") + node(u.paths[p]);
+    out += "]}}";
+  }
+  return out + "\n  ]\n}\n";
+}
+
+Status Plugin::WriteCdiSpec() const {
+  std::string path = CdiSpecPath();
+  std::string tmp = path + ".tmp";
+  mkdir(opts_.cdi_spec_dir.c_str(), 0755);
+  FILE* f = fopen(tmp.c_str(), "w");
+  if (!f) return Unavailable("cannot write CDI spec " + tmp + ": " + strerror(errno));
+  std::string body = CdiSpecJson();
+  bool ok = fwrite(body.data(), 1, body.size(), f) == body.size();
+  ok = (fclose(f) == 0) && ok;
+  if (!ok || rename(tmp.c_str(), path.c_str()) != 0)
+    return Unavailable("cannot write CDI spec " + path + ": " + strerror(errno));
+  LOG_INFO(kComp, "wrote CDI spec %s (%zu devices)", path.c_str(), units_.size());
+  return Status::Ok();
 }
 
 std::string Plugin::StatsJson() const {

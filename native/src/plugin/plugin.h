@@ -66,6 +66,8 @@ struct PluginOptions {
   uint64_t auto_replica_unit_mib = 1000;  // reference: TotalMemory / 1000 (server.go:102)
   int dial_timeout_ms = 5000;             // server.go:208,219
   bool register_with_kubelet = true;
+  bool trace = false;                     // log every RPC with its handler time
+  std::string cdi_spec_dir = "/var/run/cdi";  // where cdi-* strategies write the CDI spec
 };
 
 // One allocatable device (whole GPU or partition) after snapshot resolution.
@@ -138,6 +140,15 @@ class Plugin {
   void ApplyHealth(const std::vector<int>& units, bool healthy, const std::string& reason);
   void PostHealth(std::vector<int> units, bool healthy, const std::string& reason);
   Status Register();
+
+ public:
+  // CDI (Container Device Interface) spec describing this plugin's devices, for
+  // the cdi-annotations / cdi-cri device-list strategies. Returns its JSON text.
+  std::string CdiSpecJson() const;
+  std::string CdiSpecPath() const;
+  Status WriteCdiSpec() const;
+
+ private:
 
   std::shared_ptr<const inventory::Snapshot> snap_;
   strategy::PluginSpec spec_;

@@ -93,6 +93,62 @@ def test_driver_root_prefixes_host_paths(running, scratch):
     c.close()
 
 
+def test_no_device_library_calls_on_the_rpc_path(running, scratch):
+    """B5: the reference re-enumerates NVML twice per GetPreferredAllocation; we never touch amdsmi."""
+    counter = os.path.join(scratch + ".fixture", "calls")
+    os.makedirs(scratch + ".fixture", exist_ok=True)
+    d, k = running(fixtures.node(8), env={"AMDSMI_MOCK_CALL_COUNT_FILE": counter,
+                                         "DP_DISABLE_HEALTHCHECKS": "all"})
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    before = open(counter).read()
+    for size in (1, 2, 4, 8):
+        got = list(c.preferred(ids, [], size).container_responses[0].deviceIDs)
+        c.allocate(got)
+    assert open(counter).read() == before
+    c.close()
+
+
+def test_cdi_spec_and_cdi_names(running, scratch):
+    import json
+    cdi = os.path.join(scratch, "cdi")
+    d, k = running(fixtures.node(2), args=["--device-list-strategy", "cdi-cri", "--cdi-spec-dir", cdi])
+    reg = k.wait_registration()
+    spec = json.load(open(os.path.join(cdi, "amd.com-gpu.json")))
+    assert spec["kind"] == "amd.com/gpu" and spec["cdiVersion"] == "0.5.0"
+    assert spec["containerEdits"]["deviceNodes"][0]["path"] == "/dev/kfd"
+    names = [dev["name"] for dev in spec["devices"]]
+    assert spec["devices"][1]["containerEdits"]["deviceNodes"][0]["path"] == "/dev/dri/renderD136"
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    r = c.allocate([ids[1]]).container_responses[0]
+    assert [x.name for x in r.cdi_devices] == [f"amd.com/gpu={names[1]}"]
+    c.close()
+
+
+def test_cdi_annotations(running, scratch):
+    d, k = running(fixtures.node(2), args=["--device-list-strategy", "cdi-annotations", "--cdi-spec-dir",
+                                           os.path.join(scratch, "cdi"), "--device-id-strategy", "index"])
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    r = c.allocate(ids).container_responses[0]
+    assert dict(r.annotations) == {"cdi.k8s.io/amd-gpu-device-plugin_0": "amd.com/gpu=0,amd.com/gpu=1"}
+    c.close()
+
+
+def test_trace_logs_each_rpc(running, scratch):
+    d, k = running(fixtures.node(1), args=["--trace"])
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    c.allocate(ids)
+    log = d.wait_log("/v1beta1.DevicePlugin/Allocate OK")
+    assert "handler=" in log
+    c.close()
+
+
 def test_native_stub_kubelet_sees_devices(scratch):
     """Same flow through the native stub kubelet (amdgpu-dp-kubelet serve)."""
     k = harness.NativeKubelet(os.path.join(scratch, "kubelet.sock")).start()
