@@ -52,6 +52,7 @@ struct MockProc {
   uint32_t num_cu = 0;
   uint16_t xcd = 0;
   std::string market;
+  std::string serial;
   std::string cmode, mmode;
   int links_down = 0;
   bool evt_init = false;
@@ -171,6 +172,9 @@ bool Load() {
       mp->num_cu = nparts > 1 ? ncu / nparts : ncu;
       mp->xcd = nparts > 1 ? static_cast<uint16_t>(xcd / nparts ? xcd / nparts : 1) : xcd;
       mp->market = jg.value("market_name", std::string("AMD Instinct MI355X"));
+      char defserial[32];
+      snprintf(defserial, sizeof(defserial), "0x09C0BF99078973%02X", gi);
+      mp->serial = jg.value("asic_serial", std::string(defserial));
       mp->cmode = cmode;
       mp->mmode = mmode;
       mp->links_down = jg.value("xgmi_links_down", 0);
@@ -378,6 +382,7 @@ amdsmi_status_t amdsmi_get_gpu_asic_info(amdsmi_processor_handle h, amdsmi_asic_
   GET_PROC(h);
   memset(info, 0, sizeof(*info));
   CopyStr(info->market_name, sizeof(info->market_name), p->market);
+  CopyStr(info->asic_serial, sizeof(info->asic_serial), p->serial);
   info->vendor_id = 0x1002;
   info->device_id = 0x75a3;
   info->num_of_compute_units = p->num_cu;

@@ -65,13 +65,16 @@ Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo
                                                   const BuildOptions& opt) {
   auto snap = std::make_shared<Snapshot>();
   snap->procs = std::move(procs);
-  // Group handles into physical GPUs by PCI domain:bus:device (partitions differ
-  // only in the function number); fall back to the UUID when no BDF is known.
+  // Group handles into physical GPUs. Compute partitions of one GPU report the
+  // same ASIC serial; without one, group by PCI domain:bus:device (partitions
+  // differ only in the function number); last resort, the UUID.
   std::vector<std::string> order;
   std::map<std::string, std::vector<int>> groups;
   for (size_t i = 0; i < snap->procs.size(); ++i) {
     const auto& p = snap->procs[i];
-    std::string key = p.bdf_id ? "bdf:" + std::to_string(p.bdf_id & ~uint64_t{7}) : "uuid:" + p.uuid;
+    std::string key = !p.asic_serial.empty() ? "serial:" + p.asic_serial
+                      : p.bdf_id             ? "bdf:" + std::to_string(p.bdf_id & ~uint64_t{7})
+                                             : "uuid:" + p.uuid;
     if (!groups.count(key)) order.push_back(key);
     groups[key].push_back(static_cast<int>(i));
   }

@@ -222,6 +222,8 @@ Result<std::vector<ProcessorInfo>> Library::Enumerate() {
         amdsmi_asic_info_t ai{};
         if (f_->asic_info(h, &ai) == AMDSMI_STATUS_SUCCESS) {
           p.market_name = ai.market_name;
+          p.asic_serial.assign(ai.asic_serial, strnlen(ai.asic_serial, sizeof(ai.asic_serial)));
+          if (p.asic_serial == "N/A" || p.asic_serial == "0" || p.asic_serial == "0x0") p.asic_serial.clear();
           if (ai.num_of_compute_units != 0xffffffffu) p.num_cu = ai.num_of_compute_units;
         }
       }

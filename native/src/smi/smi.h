@@ -41,6 +41,7 @@ struct ProcessorInfo {
   uint32_t num_cu = 0;
   uint32_t xcd_count = 0;         // 0 = unknown
   std::string market_name;
+  std::string asic_serial;        // same for every partition of one physical GPU ("" if unknown)
 };
 
 enum class LinkType { kInternal = 0, kPcie = 1, kXgmi = 2, kNotApplicable = 3, kUnknown = 4 };

@@ -135,6 +135,18 @@ def test_partition_ids_when_amdsmi_reports_shared_uuids(mock_env):
     assert ids == [fx["gpus"][0]["uuid"] + f"-p{i}" for i in range(4)]
 
 
+def test_partitions_grouped_by_asic_serial_even_across_pci_functions(mock_env):
+    # Partitions of one GPU may not share a PCI bus/device; the ASIC serial still groups them.
+    fx = fixtures.node(2, "QPX", memory="NPS1")
+    out = specs(mock_env, fx, strategy="single")[0]
+    assert out["advertised"] == 8 and {d["gpu"] for d in out["devices"]} == {0, 1}
+    # Without serials, fall back to the PCI bus/device grouping: same answer.
+    for g in fx["gpus"]:
+        g["asic_serial"] = ""
+    out2 = specs(mock_env, fx, strategy="single")[0]
+    assert [d["id"] for d in out2["devices"]] == [d["id"] for d in out["devices"]]
+
+
 @pytest.mark.parametrize("text,err", [
     ("gpu:x", "colon"), ("gpu:x:-2", "positive"), ("gpu:x:0", "positive"), ("gpu:x:y", "integer"),
     ("gpu::1", "invalid new resource name"),

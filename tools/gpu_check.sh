@@ -14,5 +14,5 @@ timeout -k 10 180 python __graft_entry__.py smoke > $out/smoke.log 2>&1 || { tai
 tail -2 $out/smoke.log
 timeout -k 10 300 python bench.py --steps 20 --warmup 2 > $out/bench.json 2> $out/bench.err || { tail -20 $out/bench.err; exit 1; }
 cat $out/bench.json
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$out/prof -o probe -- python3 $GRAFT_REPO_ROOT/tools/probe_once.py > $GRAFT_REPO_ROOT/$out/rocprof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/$out/rocprof.log; exit 1; }
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $GRAFT_REPO_ROOT/$out/prof -o probe -- python3 $GRAFT_REPO_ROOT/tools/probe_once.py > $GRAFT_REPO_ROOT/$out/rocprof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/$out/rocprof.log; exit 1; }
 echo rocprof done
