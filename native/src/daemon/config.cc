@@ -78,6 +78,9 @@ const std::vector<FlagDef>& Table() {
       {"trace", "ADP_TRACE", "trace", Kind::kBool,
        "log every RPC (method, status, sizes, handler time)",
        [](Flags& f) -> void* { return &f.trace; }},
+      {"dry-run", "ADP_DRY_RUN", "", Kind::kBool,
+       "print the resources/devices this node would advertise as JSON and exit",
+       [](Flags& f) -> void* { return &f.dry_run; }},
       {"cdi-spec-dir", "CDI_SPEC_DIR", "cdiSpecDir", Kind::kString,
        "directory for the generated CDI spec (cdi-annotations / cdi-cri strategies)",
        [](Flags& f) -> void* { return &f.cdi_spec_dir; }},

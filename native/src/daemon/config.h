@@ -43,6 +43,7 @@ struct Flags {
   bool include_card_nodes = false;
   bool trace = false;
   std::string cdi_spec_dir = "/var/run/cdi";
+  bool dry_run = false;
 };
 
 struct Config {

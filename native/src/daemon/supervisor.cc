@@ -7,6 +7,7 @@
 #include <sys/eventfd.h>
 #include <sys/inotify.h>
 #include <sys/signalfd.h>
+#include <sys/stat.h>
 #include <sys/timerfd.h>
 #include <unistd.h>
 
@@ -73,6 +74,43 @@ Result<Validated> Validate(const Config& cfg) {
   return v;
 }
 
+// --dry-run: what this node would advertise, as JSON on stdout.
+int DryRun(smi::Library* lib, const Validated& v, const Config& cfg) {
+  auto snap = inventory::BuildSnapshot(lib, v.bopts);
+  if (!snap.ok()) {
+    LOG_ERROR(kComp, "device enumeration failed: %s", snap.status().ToString().c_str());
+    return 1;
+  }
+  auto specs = strategy::BuildPluginSpecs(**snap, v.partition, v.rc, cfg.flags.resource_prefix);
+  if (!specs.ok()) {
+    LOG_ERROR(kComp, "error creating partition strategy: %s", specs.status().message().c_str());
+    return 1;
+  }
+  std::string out = "{\"amdsmi\": \"" + JsonEscape((*snap)->smi_version) + "\", \"gpus\": [";
+  for (size_t i = 0; i < (*snap)->gpus.size(); ++i) {
+    const auto& g = (*snap)->gpus[i];
+    out += (i ? ", " : "") + std::string("{\"index\": ") + std::to_string(g.node_index) + ", \"uuid\": \"" +
+           JsonEscape(g.uuid) + "\", \"bdf\": \"" + g.bdf + "\", \"mode\": \"" + g.compute_mode + "/" +
+           g.memory_mode + "\", \"partitions\": " + std::to_string(g.partitions.size()) +
+           ", \"vram_mib\": " + std::to_string(g.vram_mib) + ", \"numa\": " + std::to_string(g.numa) + "}";
+  }
+  out += "], \"resources\": [";
+  bool first = true;
+  for (const auto& s : *specs) {
+    plugin::Plugin p(*snap, s, v.popts);
+    if (p.device_count() == 0) continue;
+    out += std::string(first ? "" : ", ") + "{\"resource\": \"" + JsonEscape(s.resource_name) +
+           "\", \"socket\": \"" + JsonEscape(p.socket_path()) + "\", \"devices\": " +
+           std::to_string(p.device_count()) + ", \"allocatable\": " + std::to_string(p.advertised_count()) +
+           ", \"replicated\": " + (p.replicated() ? "true" : "false") + "}";
+    first = false;
+  }
+  out += "]}";
+  printf("%s\n", out.c_str());
+  fflush(stdout);
+  return 0;
+}
+
 void ArmTimer(int tfd, int ms) {
   itimerspec its{};
   its.it_value.tv_sec = ms / 1000;
@@ -118,6 +156,7 @@ int RunDaemon(const Config& cfg) {
     }
   }
   LOG_INFO(kComp, "amdsmi %s loaded from %s", (*lib)->Version().c_str(), (*lib)->path().c_str());
+  if (cfg.flags.dry_run) return DryRun(lib->get(), v, cfg);
 
   std::string kubelet_sock =
       v.popts.kubelet_socket.empty() ? PathJoin(v.popts.plugin_dir, "kubelet.sock") : v.popts.kubelet_socket;
@@ -126,10 +165,12 @@ int RunDaemon(const Config& cfg) {
   std::string kubelet_name = BaseName(kubelet_sock);
   LOG_INFO(kComp, "starting FS watcher on %s", watch_dir.c_str());
   int ifd = inotify_init1(IN_NONBLOCK | IN_CLOEXEC);
-  if (ifd < 0 || inotify_add_watch(ifd, watch_dir.c_str(), IN_CREATE | IN_MOVED_TO) < 0) {
+  if (ifd < 0 || inotify_add_watch(ifd, watch_dir.c_str(), IN_CREATE | IN_MOVED_TO | IN_DELETE) < 0) {
     LOG_ERROR(kComp, "failed to create FS watcher on %s: %s", watch_dir.c_str(), strerror(errno));
     return 1;
   }
+  if (PathJoin(v.popts.plugin_dir, "") != PathJoin(watch_dir, ""))
+    inotify_add_watch(ifd, v.popts.plugin_dir.c_str(), IN_DELETE);
   int tfd = timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC | TFD_NONBLOCK);
   int efd = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   int ep = epoll_create1(EPOLL_CLOEXEC);
@@ -239,6 +280,18 @@ int RunDaemon(const Config& cfg) {
               LOG_INFO(kComp, "inotify: %s created, restarting", kubelet_sock.c_str());
               backoff_ms = 1000;
               do_restart = true;
+            }
+            // One of our own sockets removed from under us (not by our own Stop():
+            // those are re-created before this event is read, so stat finds them).
+            if (e->len && (e->mask & IN_DELETE)) {
+              for (auto& pl : plugins) {
+                struct stat st;
+                if (pl->running() && BaseName(pl->socket_path()) == e->name &&
+                    stat(pl->socket_path().c_str(), &st) != 0) {
+                  LOG_WARN(kComp, "inotify: %s was removed, restarting", pl->socket_path().c_str());
+                  do_restart = true;
+                }
+              }
             }
             p += sizeof(inotify_event) + e->len;
           }

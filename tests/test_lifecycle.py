@@ -73,6 +73,24 @@ def test_kubelet_restart_is_detected(scratch):
     k2.stop()
 
 
+def test_deleted_plugin_socket_is_recreated(scratch):
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch).start()
+    k.wait_registration()
+    os.unlink(os.path.join(scratch, "amd-gpu.sock"))
+    reg = k.wait_registration(15)  # restarted and registered again
+    assert reg.endpoint == "amd-gpu.sock"
+    assert os.path.exists(os.path.join(scratch, "amd-gpu.sock"))
+    assert "was removed, restarting" in d.log()
+    # our own restarts (SIGHUP) must not loop on the deletions they cause
+    d.signal(signal.SIGHUP)
+    k.wait_registration(15)
+    time.sleep(0.5)
+    assert d.log().count("was removed, restarting") == 1
+    assert d.stop() == 0
+    k.stop()
+
+
 def test_waits_for_kubelet_with_backoff(scratch):
     d = harness.Daemon(scratch, env={}).start()
     d.wait_log("retrying in 1000 ms", timeout=15)
@@ -167,6 +185,21 @@ def test_unknown_flag_and_version_and_help():
     assert r.returncode == 0 and "amdgpu-device-plugin version" in r.stdout
     r = subprocess.run([DAEMON, "--help"], capture_output=True, text=True, timeout=10)
     assert "--partition-strategy" in r.stdout and "FAIL_ON_INIT_ERROR" in r.stdout
+
+
+def test_dry_run_reports_allocatable(scratch):
+    import json
+    fx = fixtures.write(fixtures.CONFIGS["mixed8"](), scratch + ".fixture")
+    env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB, AMDSMI_MOCK_FIXTURE=fx, ADP_LOG_LEVEL="error")
+    r = subprocess.run([DAEMON, "--dry-run", "--partition-strategy", "mixed", "--resource-config",
+                        "gpu:gpu:2", "--device-plugin-path", scratch], capture_output=True, text=True,
+                       timeout=20, env=env)
+    assert r.returncode == 0, r.stderr
+    rep = json.loads(r.stdout)
+    assert len(rep["gpus"]) == 8
+    res = {x["resource"]: x["allocatable"] for x in rep["resources"]}
+    assert res == {"amd.com/gpu": 8, "amd.com/cpx-1xcd.36gb": 32}
+    assert not os.path.exists(os.path.join(scratch, "amd-gpu.sock"))
 
 
 def test_sigusr1_dumps_stats(scratch):
