@@ -37,15 +37,22 @@ def build_native(jobs: int = 8, build_type: str = "Release", build_dir: str = BU
     return build_dir
 
 
+PROBE_MAIN = os.path.join(NATIVE_SRC, "probe", "probe_main.cpp")
+PROBE_EXE = os.path.join(PROBE_DIR, "amdgpu-dp-probe")
+
+
 def build_probe(arch: str = "gfx950") -> str:
-    """Compile the HIP visibility probe into build/probe/libadp_probe.so."""
+    """Compile the HIP visibility probe: build/probe/libadp_probe.so + amdgpu-dp-probe."""
     os.makedirs(PROBE_DIR, exist_ok=True)
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-    src_mtime = os.path.getmtime(PROBE_SRC)
-    if os.path.exists(PROBE_LIB) and os.path.getmtime(PROBE_LIB) >= src_mtime:
+    src_mtime = max(os.path.getmtime(PROBE_SRC), os.path.getmtime(PROBE_MAIN))
+    fresh = all(os.path.exists(p) and os.path.getmtime(p) >= src_mtime for p in (PROBE_LIB, PROBE_EXE))
+    if fresh:
         return PROBE_LIB
     _run([hipcc, f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-shared",
           "-Wall", "-o", PROBE_LIB, PROBE_SRC])
+    _run([hipcc, f"--offload-arch={arch}", "-O3", "-std=c++17", "-Wall", "-o", PROBE_EXE, PROBE_SRC,
+          PROBE_MAIN])
     return PROBE_LIB
 
 

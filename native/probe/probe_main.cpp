@@ -1,0 +1,81 @@
+// amdgpu-dp-probe: validate the GPU(s) a container was given.
+//
+//   amdgpu-dp-probe [--list] [--device N] [--bytes B] [--iters I]
+//                   [--expect-xcds X] [--expect-cus C] [--min-gbps G]
+//
+// Runs the visibility probe (visibility_probe.hip) on every visible HIP device
+// (or one) and prints one JSON line per device. Exits non-zero when a device
+// fails its checksum or does not have the expected shape -- e.g. a pod that
+// requested one CPX partition must see exactly 1 XCD / 32 CUs:
+//   amdgpu-dp-probe --expect-xcds 1 --expect-cus 32
+// See examples/pods/pod-validate.yml.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+extern "C" int adp_probe_device_count();
+extern "C" int adp_probe_list(char* out, int len);
+extern "C" int adp_probe_run(int device, unsigned long long bytes, int iters, char* out, int len);
+
+namespace {
+
+long JsonInt(const char* json, const char* key) {
+  std::string k = std::string("\"") + key + "\": ";
+  const char* p = strstr(json, k.c_str());
+  return p ? strtol(p + k.size(), nullptr, 10) : -1;
+}
+
+double JsonDouble(const char* json, const char* key) {
+  std::string k = std::string("\"") + key + "\": ";
+  const char* p = strstr(json, k.c_str());
+  return p ? strtod(p + k.size(), nullptr) : -1.0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  int device = -1, iters = 5;
+  unsigned long long bytes = 256ull << 20;
+  long expect_xcds = -1, expect_cus = -1;
+  double min_gbps = -1;
+  bool list = false;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : "0"; };
+    if (a == "--list") list = true;
+    else if (a == "--device") device = atoi(next());
+    else if (a == "--bytes") bytes = strtoull(next(), nullptr, 10);
+    else if (a == "--iters") iters = atoi(next());
+    else if (a == "--expect-xcds") expect_xcds = atol(next());
+    else if (a == "--expect-cus") expect_cus = atol(next());
+    else if (a == "--min-gbps") min_gbps = atof(next());
+    else {
+      fprintf(stderr, "usage: %s [--list] [--device N] [--bytes B] [--iters I] [--expect-xcds X] "
+                      "[--expect-cus C] [--min-gbps G]\n", argv[0]);
+      return 2;
+    }
+  }
+  static char buf[1 << 16];
+  if (list) {
+    int rc = adp_probe_list(buf, sizeof(buf));
+    printf("%s\n", buf);
+    return rc ? 1 : 0;
+  }
+  int n = adp_probe_device_count();
+  if (n <= 0) {
+    fprintf(stderr, "no HIP devices visible (is /dev/kfd + a render node mounted?)\n");
+    return 1;
+  }
+  int failures = 0;
+  for (int d = (device < 0 ? 0 : device); d < (device < 0 ? n : device + 1); ++d) {
+    int rc = adp_probe_run(d, bytes, iters, buf, sizeof(buf));
+    printf("%s\n", buf);
+    if (rc != 0) { ++failures; continue; }
+    if (expect_xcds >= 0 && JsonInt(buf, "xccs_seen") != expect_xcds) ++failures;
+    if (expect_cus >= 0 && JsonInt(buf, "cus") != expect_cus) ++failures;
+    if (min_gbps >= 0 && JsonDouble(buf, "hbm_copy_gbps") < min_gbps) ++failures;
+  }
+  fflush(stdout);
+  return failures ? 1 : 0;
+}

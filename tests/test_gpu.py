@@ -90,6 +90,19 @@ def test_probe_on_allocated_gpu(snap, probe_built):
         assert res["hbm_copy_gbps"] > 2000, res  # whole MI355X streams several TB/s
 
 
+def test_probe_cli_validates_shape(snap, probe_built):
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd.utils.build import PROBE_EXE
+    g = snap["gpus"][0]
+    xcds, cus = (8, 256) if not g["partitioned"] else (g["partitions"][0]["xcds"], g["partitions"][0]["cus"])
+    ok = subprocess.run([PROBE_EXE, "--device", "0", "--expect-xcds", str(xcds), "--expect-cus", str(cus)],
+                        capture_output=True, text=True, timeout=120)
+    assert ok.returncode == 0, ok.stdout + ok.stderr
+    bad = subprocess.run([PROBE_EXE, "--device", "0", "--expect-xcds", "1"], capture_output=True, text=True,
+                         timeout=120)
+    assert bad.returncode == (1 if xcds != 1 else 0)
+
+
 def test_health_monitor_starts_on_real_gpu(scratch, snap):
     """Event notification may need privileges; either way the daemon must stay healthy."""
     k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
