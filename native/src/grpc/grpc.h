@@ -65,7 +65,9 @@ class ServerConn;
 // called on the server's loop thread (use Server::Post from elsewhere).
 class ServerStream {
  public:
-  // Queues one message. Returns false once the peer has gone away.
+  // Queues one message. Returns false once the peer has gone away. Messages are
+  // state snapshots: if the peer is slow, unsent older messages are replaced by
+  // the newest one (latest wins), bounding the memory a stuck client can pin.
   bool Send(std::string_view message);
   // Ends the call with trailers carrying `st`.
   void Finish(const Status& st);

@@ -46,6 +46,10 @@ struct StreamState {
   bool dispatched = false;
   std::string out;       // framed response bytes not yet handed to nghttp2
   size_t out_off = 0;
+  // Server streams carry state snapshots (ListAndWatch): while `out` is still
+  // being sent, only the newest queued message is kept here (latest wins), so a
+  // peer that stops reading costs at most two messages of memory.
+  std::string pending;
   bool finishing = false;  // send trailers once `out` drains
   bool deferred = false;
   int grpc_status = 0;
@@ -237,7 +241,11 @@ ssize_t ServerConn::ReadData(int32_t sid, uint8_t* buf, size_t len, uint32_t* fl
   if (n) {
     memcpy(buf, st->out.data() + st->out_off, n);
     st->out_off += n;
-    if (st->out_off == st->out.size()) { st->out.clear(); st->out_off = 0; }
+    if (st->out_off == st->out.size()) {
+      st->out.clear();
+      st->out_off = 0;
+      if (!st->pending.empty()) st->out.swap(st->pending);  // next (latest) message
+    }
   }
   if (st->out.size() == st->out_off) {
     if (st->finishing) {
@@ -347,7 +355,17 @@ void ServerConn::Dispatch(int32_t sid) {
 bool ServerConn::QueueMessage(int32_t sid, std::string_view msg) {
   StreamState* st = Find(sid);
   if (!st || st->finishing) return false;
-  FrameMessage(msg, &st->out);
+  if (st->out.size() == st->out_off) {
+    st->out.clear();
+    st->out_off = 0;
+    FrameMessage(msg, &st->out);
+  } else if (st->out_off == 0) {
+    st->out.clear();  // nothing of the queued message went out yet: replace it
+    FrameMessage(msg, &st->out);
+  } else {
+    st->pending.clear();  // finish the message in flight, then send only the newest
+    FrameMessage(msg, &st->pending);
+  }
   if (st->deferred) {
     st->deferred = false;
     nghttp2_session_resume_data(session_, sid);
