@@ -84,6 +84,9 @@ const std::vector<FlagDef>& Table() {
       {"cdi-spec-dir", "CDI_SPEC_DIR", "cdiSpecDir", Kind::kString,
        "directory for the generated CDI spec (cdi-annotations / cdi-cri strategies)",
        [](Flags& f) -> void* { return &f.cdi_spec_dir; }},
+      {"server-threads", "DP_SERVER_THREADS", "serverThreads", Kind::kUint,
+       "gRPC loop threads per plugin socket (0 = min(4, CPUs))",
+       [](Flags& f) -> void* { return &f.server_threads; }},
   };
   return t;
 }

@@ -44,6 +44,7 @@ struct Flags {
   bool trace = false;
   std::string cdi_spec_dir = "/var/run/cdi";
   bool dry_run = false;
+  uint64_t server_threads = 0;  // 0 -> plugin::DefaultServerThreads()
 };
 
 struct Config {

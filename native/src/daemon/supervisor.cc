@@ -59,6 +59,7 @@ Result<Validated> Validate(const Config& cfg) {
   v.popts.pass_device_specs = f.pass_device_specs;
   v.popts.driver_root = f.driver_root;
   v.popts.auto_replica_unit_mib = f.auto_replica_unit_mib;
+  v.popts.server_threads = static_cast<int>(std::min<uint64_t>(f.server_threads, 64));
   v.popts.trace = f.trace;
   v.popts.cdi_spec_dir = f.cdi_spec_dir;
   v.bopts.driver_root = f.driver_root;

@@ -13,9 +13,11 @@
 //     the plugin and pushes a new device list on every health transition).
 // nghttp2 provides HPACK, flow control, SETTINGS/PING/GOAWAY handling.
 //
-// Threading: each Server runs one epoll loop thread. Handlers execute on that
-// thread (they are O(k) in-memory work, so an inline call is cheaper than any
-// hand-off); other threads inject work with Post().
+// Threading: a Server runs N epoll loop threads; every connection is owned by
+// one loop and its handlers execute inline on that loop (they are O(k)
+// in-memory work, so an inline call is cheaper than any hand-off). Handlers
+// may therefore run concurrently on different loops and must only read shared
+// state or synchronise. Other threads inject work with Post()/PostAll().
 #pragma once
 
 #include <atomic>
@@ -73,6 +75,7 @@ class ServerStream {
   void Finish(const Status& st);
   bool closed() const { return closed_; }
   uint64_t id() const { return id_; }
+  int loop() const { return loop_; }  // the server loop that owns this stream
 
  private:
   friend class Server;
@@ -80,6 +83,7 @@ class ServerStream {
   ServerConn* conn_ = nullptr;
   int32_t stream_id_ = 0;
   uint64_t id_ = 0;
+  int loop_ = 0;
   bool closed_ = false;
 };
 
@@ -95,7 +99,10 @@ struct ServerStats {
 
 class Server {
  public:
-  explicit Server(std::string name);
+  // `threads` epoll loops serve the connections: the listener lives on loop 0 and
+  // accepted connections are dealt round-robin, so concurrent clients are served
+  // in parallel (each connection stays on one loop for its lifetime).
+  explicit Server(std::string name, int threads = 1);
   ~Server();
   Server(const Server&) = delete;
   Server& operator=(const Server&) = delete;
@@ -105,48 +112,51 @@ class Server {
 
   // Removes a stale socket file, binds and listens.
   Status Listen(const std::string& socket_path);
-  // Starts the loop thread. `on_fatal` runs (on the loop thread) if the loop
-  // fails more than 5 times with less than an hour between failures -- the
+  // Starts the loop threads. `on_fatal` runs (on a loop thread) if a loop fails
+  // more than 5 times with less than an hour between failures -- the
   // reference's crash budget (server.go:177-205).
   Status Start(std::function<void()> on_fatal = nullptr);
-  // Closes every connection and the listener, joins the thread. Idempotent.
+  // Closes every connection and the listener, joins the threads. Idempotent.
   void Stop();
-  // Runs `fn` on the loop thread. Safe from any thread; dropped after Stop().
+  // Runs `fn` on loop 0. Safe from any thread; queued before Start(), dropped
+  // after Stop().
   void Post(std::function<void()> fn);
+  // Runs `fn(loop)` on every loop.
+  void PostAll(std::function<void(int loop)> fn);
+  int loops() const { return static_cast<int>(loops_.size()); }
   bool OnLoopThread() const;
   const std::string& socket_path() const { return socket_path_; }
   const ServerStats& stats() const { return stats_; }
   // Log every unary call (method, status, sizes, handler time). Set before Start().
   void set_trace(bool on) { trace_ = on; }
 
-  // Test hook: make the next loop iteration fail as if epoll_wait errored.
+  // Test hook: make the next iteration of loop 0 fail as if epoll_wait errored.
   void InjectLoopFailureForTest() { inject_failure_.store(true); }
+
+  struct Loop;
 
  private:
   friend class ServerConn;
   friend class ServerStream;
-  Status RunLoop();
-  void LoopMain();
+  Status RunLoop(Loop& l);
+  void LoopMain(Loop& l);
   void AcceptAll();
-  void CloseConn(int fd);
-  void DrainPosted();
+  void AddConn(Loop& l, int fd);
+  void CloseConn(Loop& l, int fd);
+  void DrainPosted(Loop& l);
+  void PostTo(Loop& l, std::function<void()> fn);
 
   std::string name_;
   std::string socket_path_;
   std::map<std::string, UnaryHandler> unary_;
   std::map<std::string, StreamHandler> streams_;
   int listen_fd_ = -1;
-  int epoll_fd_ = -1;
-  int event_fd_ = -1;
-  std::thread thread_;
-  std::thread::id loop_tid_;
+  std::vector<std::unique_ptr<Loop>> loops_;
+  std::atomic<unsigned> next_loop_{0};
   std::atomic<bool> stopping_{false};
   std::atomic<bool> inject_failure_{false};
   std::function<void()> on_fatal_;
-  std::mutex post_mu_;
-  std::vector<std::function<void()>> posted_;
-  std::map<int, std::unique_ptr<ServerConn>> conns_;
-  uint64_t next_stream_id_ = 1;
+  std::atomic<uint64_t> next_stream_id_{1};
   bool trace_ = false;
   ServerStats stats_;
 };

@@ -59,7 +59,7 @@ struct StreamState {
 
 class ServerConn {
  public:
-  ServerConn(Server* srv, int fd) : srv_(srv), fd_(fd) {}
+  ServerConn(Server* srv, int loop, int fd) : srv_(srv), loop_(loop), fd_(fd) {}
   ~ServerConn() {
     for (auto& [_, st] : streams_) {
       if (st.stream) { st.stream->closed_ = true; st.stream->conn_ = nullptr; }
@@ -97,6 +97,7 @@ class ServerConn {
   void Finish(int32_t sid, const Status& st);
 
   Server* srv_;
+  int loop_;
   std::map<int32_t, StreamState> streams_;
   uint32_t epoll_events = 0;  // interest set currently registered with epoll
 
@@ -342,7 +343,8 @@ void ServerConn::Dispatch(int32_t sid) {
     auto stream = std::make_shared<ServerStream>();
     stream->conn_ = this;
     stream->stream_id_ = sid;
-    stream->id_ = srv_->next_stream_id_++;
+    stream->id_ = srv_->next_stream_id_.fetch_add(1, std::memory_order_relaxed);
+    stream->loop_ = loop_;
     st->stream = stream;
     SubmitResponse(sid);
     Status s = ss->second(req, stream);
@@ -403,15 +405,32 @@ void ServerStream::Finish(const Status& st) {
 
 // ------------------------- Server -------------------------
 
-Server::Server(std::string name) : name_(std::move(name)) {
-  // Created up front so Post() works before Start(): work posted in between runs
-  // as soon as the loop starts instead of being lost.
-  epoll_fd_ = epoll_create1(EPOLL_CLOEXEC);
-  event_fd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
-  epoll_event ev{};
-  ev.events = EPOLLIN;
-  ev.data.fd = event_fd_;
-  epoll_ctl(epoll_fd_, EPOLL_CTL_ADD, event_fd_, &ev);
+struct Server::Loop {
+  int index = 0;
+  int epoll_fd = -1;
+  int event_fd = -1;
+  std::thread thread;
+  std::thread::id tid;
+  std::mutex post_mu;
+  std::vector<std::function<void()>> posted;
+  std::map<int, std::unique_ptr<ServerConn>> conns;
+};
+
+Server::Server(std::string name, int threads) : name_(std::move(name)) {
+  // Loops (epoll + eventfd) exist from construction so Post() works before
+  // Start(): work posted in between runs as soon as the loops start.
+  if (threads < 1) threads = 1;
+  for (int i = 0; i < threads; ++i) {
+    auto l = std::make_unique<Loop>();
+    l->index = i;
+    l->epoll_fd = epoll_create1(EPOLL_CLOEXEC);
+    l->event_fd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.fd = l->event_fd;
+    epoll_ctl(l->epoll_fd, EPOLL_CTL_ADD, l->event_fd, &ev);
+    loops_.push_back(std::move(l));
+  }
 }
 
 Server::~Server() { Stop(); }
@@ -451,60 +470,92 @@ Status Server::Start(std::function<void()> on_fatal) {
   if (listen_fd_ < 0) return FailedPrecondition("Start() before Listen()");
   if (stopping_.load()) return FailedPrecondition("server already stopped");
   on_fatal_ = std::move(on_fatal);
-  if (epoll_fd_ < 0 || event_fd_ < 0) return Internal("epoll/eventfd setup failed");
+  for (auto& l : loops_)
+    if (l->epoll_fd < 0 || l->event_fd < 0) return Internal("epoll/eventfd setup failed");
   epoll_event ev{};
   ev.events = EPOLLIN;
   ev.data.fd = listen_fd_;
-  epoll_ctl(epoll_fd_, EPOLL_CTL_ADD, listen_fd_, &ev);
-  thread_ = std::thread([this] { LoopMain(); });
+  epoll_ctl(loops_[0]->epoll_fd, EPOLL_CTL_ADD, listen_fd_, &ev);
+  for (auto& l : loops_) {
+    Loop* lp = l.get();
+    l->thread = std::thread([this, lp] { LoopMain(*lp); });
+  }
   return Status::Ok();
 }
 
 void Server::Stop() {
   stopping_.store(true);  // later Post() calls are dropped
-  if (thread_.joinable()) {
+  for (auto& l : loops_) {
+    if (!l->thread.joinable()) continue;
     uint64_t one = 1;
-    ssize_t w = write(event_fd_, &one, sizeof(one));
+    ssize_t w = write(l->event_fd, &one, sizeof(one));
     (void)w;
-    thread_.join();
+    l->thread.join();
   }
-  conns_.clear();  // loop is gone; safe to tear down here
-  {
-    std::lock_guard<std::mutex> lk(post_mu_);
-    posted_.clear();
+  for (auto& l : loops_) {
+    l->conns.clear();  // loops are gone; safe to tear down here
+    std::lock_guard<std::mutex> lk(l->post_mu);
+    l->posted.clear();
   }
   if (listen_fd_ >= 0) {
     close(listen_fd_);
     listen_fd_ = -1;
     if (!socket_path_.empty()) unlink(socket_path_.c_str());
   }
-  if (epoll_fd_ >= 0) { close(epoll_fd_); epoll_fd_ = -1; }
-  if (event_fd_ >= 0) { close(event_fd_); event_fd_ = -1; }
+  for (auto& l : loops_) {
+    if (l->epoll_fd >= 0) { close(l->epoll_fd); l->epoll_fd = -1; }
+    if (l->event_fd >= 0) { close(l->event_fd); l->event_fd = -1; }
+  }
 }
 
-void Server::Post(std::function<void()> fn) {
-  if (stopping_.load() || event_fd_ < 0) return;
+void Server::PostTo(Loop& l, std::function<void()> fn) {
+  if (stopping_.load() || l.event_fd < 0) return;
   {
-    std::lock_guard<std::mutex> lk(post_mu_);
-    posted_.push_back(std::move(fn));
+    std::lock_guard<std::mutex> lk(l.post_mu);
+    l.posted.push_back(std::move(fn));
   }
   uint64_t one = 1;
-  ssize_t w = write(event_fd_, &one, sizeof(one));
+  ssize_t w = write(l.event_fd, &one, sizeof(one));
   (void)w;
 }
 
-bool Server::OnLoopThread() const { return std::this_thread::get_id() == loop_tid_; }
+void Server::Post(std::function<void()> fn) { PostTo(*loops_[0], std::move(fn)); }
 
-void Server::DrainPosted() {
+void Server::PostAll(std::function<void(int)> fn) {
+  for (auto& l : loops_) {
+    int i = l->index;
+    PostTo(*l, [fn, i] { fn(i); });
+  }
+}
+
+bool Server::OnLoopThread() const {
+  for (const auto& l : loops_)
+    if (std::this_thread::get_id() == l->tid) return true;
+  return false;
+}
+
+void Server::DrainPosted(Loop& l) {
   uint64_t v;
-  ssize_t r = read(event_fd_, &v, sizeof(v));
+  ssize_t r = read(l.event_fd, &v, sizeof(v));
   (void)r;
   std::vector<std::function<void()>> work;
   {
-    std::lock_guard<std::mutex> lk(post_mu_);
-    work.swap(posted_);
+    std::lock_guard<std::mutex> lk(l.post_mu);
+    work.swap(l.posted);
   }
   for (auto& fn : work) fn();
+}
+
+void Server::AddConn(Loop& l, int fd) {
+  auto conn = std::make_unique<ServerConn>(this, l.index, fd);
+  if (!conn->Init()) return;  // closes fd
+  epoll_event ev{};
+  ev.events = EPOLLIN | (conn->want_epollout() ? static_cast<uint32_t>(EPOLLOUT) : 0u);
+  ev.data.fd = fd;
+  epoll_ctl(l.epoll_fd, EPOLL_CTL_ADD, fd, &ev);
+  conn->epoll_events = ev.events;
+  stats_.connections.fetch_add(1, std::memory_order_relaxed);
+  l.conns[fd] = std::move(conn);
 }
 
 void Server::AcceptAll() {
@@ -514,72 +565,70 @@ void Server::AcceptAll() {
       if (errno == EINTR) continue;
       return;  // EAGAIN or transient (EMFILE...): retry on next readiness
     }
-    auto conn = std::make_unique<ServerConn>(this, fd);
-    if (!conn->Init()) continue;
-    epoll_event ev{};
-    ev.events = EPOLLIN | (conn->want_epollout() ? static_cast<uint32_t>(EPOLLOUT) : 0u);
-    ev.data.fd = fd;
-    epoll_ctl(epoll_fd_, EPOLL_CTL_ADD, fd, &ev);
-    conn->epoll_events = ev.events;
-    stats_.connections.fetch_add(1, std::memory_order_relaxed);
-    conns_[fd] = std::move(conn);
+    Loop& target = *loops_[next_loop_.fetch_add(1, std::memory_order_relaxed) % loops_.size()];
+    if (&target == loops_[0].get()) {
+      AddConn(target, fd);
+    } else {
+      Loop* t = &target;
+      PostTo(target, [this, t, fd] { AddConn(*t, fd); });
+    }
   }
 }
 
-void Server::CloseConn(int fd) {
-  auto it = conns_.find(fd);
-  if (it == conns_.end()) return;
-  epoll_ctl(epoll_fd_, EPOLL_CTL_DEL, fd, nullptr);
-  conns_.erase(it);
+void Server::CloseConn(Loop& l, int fd) {
+  auto it = l.conns.find(fd);
+  if (it == l.conns.end()) return;
+  epoll_ctl(l.epoll_fd, EPOLL_CTL_DEL, fd, nullptr);
+  l.conns.erase(it);
 }
 
-Status Server::RunLoop() {
+Status Server::RunLoop(Loop& l) {
   epoll_event events[64];
   while (!stopping_.load()) {
-    int n = epoll_wait(epoll_fd_, events, 64, -1);
-    if (inject_failure_.exchange(false)) return Internal("injected loop failure");
+    int n = epoll_wait(l.epoll_fd, events, 64, -1);
+    if (l.index == 0 && inject_failure_.exchange(false)) return Internal("injected loop failure");
     if (n < 0) {
       if (errno == EINTR) continue;
       return Internal(std::string("epoll_wait: ") + strerror(errno));
     }
     for (int i = 0; i < n; ++i) {
       int fd = events[i].data.fd;
-      if (fd == listen_fd_) { AcceptAll(); continue; }
-      if (fd == event_fd_) { DrainPosted(); continue; }
-      auto it = conns_.find(fd);
-      if (it == conns_.end()) continue;
+      if (fd == listen_fd_ && l.index == 0) { AcceptAll(); continue; }
+      if (fd == l.event_fd) { DrainPosted(l); continue; }
+      auto it = l.conns.find(fd);
+      if (it == l.conns.end()) continue;
       ServerConn* c = it->second.get();
       bool ok = true;
       if (events[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) ok = c->OnReadable();
       else if (events[i].events & EPOLLOUT) ok = c->Flush();
-      if (!ok || c->Done()) { CloseConn(fd); continue; }
+      if (!ok || c->Done()) { CloseConn(l, fd); continue; }
     }
     // Flush every connection (handlers and posted work may have queued data on
     // any of them) and refresh EPOLLOUT interest.
     std::vector<int> dead;
-    for (auto& [fd, c] : conns_) {
+    for (auto& [fd, c] : l.conns) {
       if (!c->Flush() || c->Done()) { dead.push_back(fd); continue; }
       uint32_t want = EPOLLIN | (c->want_epollout() ? static_cast<uint32_t>(EPOLLOUT) : 0u);
       if (want == c->epoll_events) continue;  // no syscall on the common path
       epoll_event ev{};
       ev.events = want;
       ev.data.fd = fd;
-      epoll_ctl(epoll_fd_, EPOLL_CTL_MOD, fd, &ev);
+      epoll_ctl(l.epoll_fd, EPOLL_CTL_MOD, fd, &ev);
       c->epoll_events = want;
     }
-    for (int fd : dead) CloseConn(fd);
+    for (int fd : dead) CloseConn(l, fd);
   }
   return Status::Ok();
 }
 
-void Server::LoopMain() {
-  loop_tid_ = std::this_thread::get_id();
+void Server::LoopMain(Loop& l) {
+  l.tid = std::this_thread::get_id();
   using Clock = std::chrono::steady_clock;
   auto last_crash = Clock::now();
   int restarts = 0;
   while (!stopping_.load()) {
-    LOG_DEBUG(kComp, "starting gRPC loop for '%s'", name_.c_str());
-    Status st = RunLoop();
+    LOG_DEBUG(kComp, "starting gRPC loop %d for '%s'", l.index, name_.c_str());
+    Status st = RunLoop(l);
     if (st.ok() || stopping_.load()) break;
     LOG_ERROR(kComp, "gRPC server for '%s' crashed: %s", name_.c_str(), st.ToString().c_str());
     if (restarts > 5) {

@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cstring>
 #include <future>
+#include <thread>
 
 #include "common/log.h"
 #include "common/strings.h"
@@ -49,6 +50,11 @@ const char* DeviceListStrategyName(DeviceListStrategy s) {
     case DeviceListStrategy::kCdiCri: return "cdi-cri";
   }
   return "?";
+}
+
+int DefaultServerThreads() {
+  unsigned n = std::thread::hardware_concurrency();
+  return static_cast<int>(std::clamp(n, 1u, 4u));
 }
 
 const char* DeviceIdStrategyName(DeviceIdStrategy s) {
@@ -159,8 +165,34 @@ void Plugin::RebuildListAndWatch() {
     pb::Encode(d, &dev);
     pb::PutLen(&out, 1, dev);
   }
-  law_bytes_ = std::move(out);
-  law_bytes_size_.store(law_bytes_.size(), std::memory_order_relaxed);
+  auto snap = std::make_shared<LawSnapshot>();
+  snap->version = ++law_version_;
+  snap->bytes = std::move(out);
+  law_bytes_size_.store(snap->bytes.size(), std::memory_order_relaxed);
+  std::lock_guard<std::mutex> lk(law_mu_);
+  law_ = std::move(snap);
+}
+
+std::shared_ptr<const Plugin::LawSnapshot> Plugin::CurrentLaw() const {
+  std::lock_guard<std::mutex> lk(law_mu_);
+  return law_;
+}
+
+void Plugin::BroadcastLaw(int loop) {
+  // Always the newest snapshot (latest wins); a stream that already carries it
+  // -- e.g. it opened after the transition -- is not sent a duplicate.
+  auto law = CurrentLaw();
+  auto& streams = law_streams_[loop];
+  size_t keep = 0;
+  for (auto& ls : streams) {
+    if (ls.stream->closed()) continue;
+    if (ls.sent_version != law->version) {
+      if (ls.stream->Send(law->bytes)) stats_.law_sends.fetch_add(1, std::memory_order_relaxed);
+      ls.sent_version = law->version;
+    }
+    streams[keep++] = std::move(ls);
+  }
+  streams.resize(keep);
 }
 
 Status Plugin::HandleGetOptions(std::string_view, std::string* resp) {
@@ -318,7 +350,9 @@ Status Plugin::Start(std::function<void()> on_fatal) {
     Status cs = WriteCdiSpec();
     if (!cs.ok()) return cs;
   }
-  auto srv = std::make_unique<grpc::Server>(spec_.resource_name);
+  int threads = opts_.server_threads > 0 ? opts_.server_threads : DefaultServerThreads();
+  auto srv = std::make_unique<grpc::Server>(spec_.resource_name, threads);
+  law_streams_.assign(threads, {});
   srv->set_trace(opts_.trace);
   srv->AddUnary(std::string(kSvc) + "GetDevicePluginOptions",
                 [this](std::string_view q, std::string* r) { return HandleGetOptions(q, r); });
@@ -330,9 +364,10 @@ Status Plugin::Start(std::function<void()> on_fatal) {
                 [this](std::string_view q, std::string* r) { return HandlePreStart(q, r); });
   srv->AddServerStream(std::string(kSvc) + "ListAndWatch",
                        [this](std::string_view, std::shared_ptr<grpc::ServerStream> s) {
-                         law_streams_.push_back(s);
-                         s->Send(law_bytes_);
+                         auto law = CurrentLaw();
+                         s->Send(law->bytes);
                          stats_.law_sends.fetch_add(1, std::memory_order_relaxed);
+                         law_streams_[s->loop()].push_back({s, law->version});
                          return Status::Ok();
                        });
   // Publish before the loop starts: from here on health updates are posted to the
@@ -377,20 +412,26 @@ void Plugin::Stop() {
   std::unique_ptr<grpc::Server> srv = std::move(server_);
   if (!srv) return;
   LOG_INFO(kComp, "stopping '%s' on %s", spec_.resource_name.c_str(), socket_path().c_str());
-  // End open ListAndWatch streams cleanly (the reference returns nil on stop).
-  auto done = std::make_shared<std::promise<void>>();
-  auto fut = done->get_future();
-  srv->Post([this, done] {
-    for (auto& s : law_streams_) s->Finish(Status::Ok());
-    law_streams_.clear();
-    done->set_value();
+  // End open ListAndWatch streams cleanly (the reference returns nil on stop);
+  // each loop finishes the streams it owns.
+  struct Pending {
+    std::atomic<int> left;
+    std::promise<void> done;
+  };
+  auto pending = std::make_shared<Pending>();
+  pending->left.store(srv->loops());
+  auto fut = pending->done.get_future();
+  srv->PostAll([this, pending](int loop) {
+    for (auto& ls : law_streams_[loop]) ls.stream->Finish(Status::Ok());
+    law_streams_[loop].clear();
+    if (pending->left.fetch_sub(1) == 1) pending->done.set_value();
   });
   fut.wait_for(std::chrono::milliseconds(500));
   srv->Stop();
-  law_streams_.clear();
+  for (auto& v : law_streams_) v.clear();
 }
 
-void Plugin::ApplyHealth(const std::vector<int>& us, bool healthy, const std::string& reason) {
+bool Plugin::ApplyHealth(const std::vector<int>& us, bool healthy, const std::string& reason) {
   bool changed = false;
   for (int u : us) {
     if (static_cast<bool>(healthy_[u]) == healthy) continue;
@@ -399,15 +440,8 @@ void Plugin::ApplyHealth(const std::vector<int>& us, bool healthy, const std::st
     LOG_INFO(kComp, "'%s' device %s marked %s: %s", spec_.resource_name.c_str(), units_[u].id.c_str(),
              healthy ? "healthy" : "unhealthy", reason.c_str());
   }
-  if (!changed) return;
-  RebuildListAndWatch();
-  std::vector<std::shared_ptr<grpc::ServerStream>> live;
-  for (auto& s : law_streams_) {
-    if (s->closed()) continue;
-    if (s->Send(law_bytes_)) stats_.law_sends.fetch_add(1, std::memory_order_relaxed);
-    live.push_back(s);
-  }
-  law_streams_.swap(live);
+  if (changed) RebuildListAndWatch();
+  return changed;
 }
 
 void Plugin::SetHandleHealth(int handle, bool healthy, const std::string& reason) {
@@ -428,8 +462,15 @@ void Plugin::SetGpuHealth(int gpu, bool healthy, const std::string& reason) {
 void Plugin::PostHealth(std::vector<int> us, bool healthy, const std::string& reason) {
   if (us.empty()) return;
   std::lock_guard<std::mutex> lk(server_mu_);
-  if (server_) server_->Post([this, us, healthy, reason] { ApplyHealth(us, healthy, reason); });
-  else ApplyHealth(us, healthy, reason);  // not serving: the lock serialises callers
+  if (server_) {
+    // Loops outlive every task they run, so the raw pointer stays valid.
+    grpc::Server* srv = server_.get();
+    srv->Post([this, srv, us, healthy, reason] {
+      if (ApplyHealth(us, healthy, reason)) srv->PostAll([this](int loop) { BroadcastLaw(loop); });
+    });
+  } else {
+    ApplyHealth(us, healthy, reason);  // not serving: the lock serialises callers
+  }
 }
 
 std::string Plugin::CdiSpecPath() const {

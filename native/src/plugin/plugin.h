@@ -19,9 +19,12 @@
 //    encoded ListAndWatch response, the topology graph. Allocate is O(k) hash
 //    lookups plus byte concatenation with zero SMI calls (reference: linear
 //    scans over all replicas, server.go:377-394, and os.Stat per call :453-462).
-//  * Mutable state (health, open ListAndWatch streams) lives on the gRPC loop
-//    thread; other threads reach it through Server::Post, so there are no locks
-//    on the RPC path and no data races (reference defects B13/B14).
+//  * The socket is served by `server_threads` epoll loops (concurrent kubelet /
+//    benchmark clients are handled in parallel). Allocate/GetPreferredAllocation
+//    only read immutable tables. Health lives on loop 0 (other threads reach it
+//    through Server::Post); each health transition publishes a new immutable,
+//    versioned ListAndWatch snapshot that every loop pushes to the streams it
+//    owns -- no locks on the Allocate path, no data races (reference B13/B14).
 //  * Health propagates to every replica of a device and recovers (B1, B15).
 #pragma once
 
@@ -68,7 +71,12 @@ struct PluginOptions {
   bool register_with_kubelet = true;
   bool trace = false;                     // log every RPC with its handler time
   std::string cdi_spec_dir = "/var/run/cdi";  // where cdi-* strategies write the CDI spec
+  int server_threads = 0;                 // gRPC loops; <=0 -> DefaultServerThreads()
 };
+
+// min(4, online CPUs): enough to serve the kubelet plus a few concurrent clients
+// without taking a node's cores from workloads.
+int DefaultServerThreads();
 
 // One allocatable device (whole GPU or partition) after snapshot resolution.
 struct Unit {
@@ -137,7 +145,7 @@ class Plugin {
   void BuildUnits();
   Status PreferredImpl(std::string_view req, std::string* resp);
   void RebuildListAndWatch();
-  void ApplyHealth(const std::vector<int>& units, bool healthy, const std::string& reason);
+  bool ApplyHealth(const std::vector<int>& units, bool healthy, const std::string& reason);
   void PostHealth(std::vector<int> units, bool healthy, const std::string& reason);
   Status Register();
 
@@ -164,11 +172,25 @@ class Plugin {
   std::string kfd_spec_bytes_;
   alloc::DeviceGraph graph_;
 
-  // Loop-thread state.
+  struct LawSnapshot {
+    uint64_t version = 0;
+    std::string bytes;  // encoded ListAndWatchResponse
+  };
+  struct LawStream {
+    std::shared_ptr<grpc::ServerStream> stream;
+    uint64_t sent_version = 0;
+  };
+  std::shared_ptr<const LawSnapshot> CurrentLaw() const;
+  void BroadcastLaw(int loop);  // on loop `loop`: push the newest snapshot to its streams
+
+  // Health: loop 0 (or under server_mu_ when not serving).
   std::vector<uint8_t> healthy_;
-  std::string law_bytes_;
+  uint64_t law_version_ = 0;
+  mutable std::mutex law_mu_;  // guards law_ (the pointer; snapshots are immutable)
+  std::shared_ptr<const LawSnapshot> law_;
   std::atomic<size_t> law_bytes_size_{0};  // readable from any thread (stats)
-  std::vector<std::shared_ptr<grpc::ServerStream>> law_streams_;
+  // law_streams_[i] is confined to server loop i.
+  std::vector<std::vector<LawStream>> law_streams_;
 
   // Guards server_ itself (not the loop-thread state): health updates arrive from
   // the monitor thread while the supervisor may be stopping the plugin.

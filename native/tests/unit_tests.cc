@@ -10,7 +10,10 @@
 #include <atomic>
 #include <cstdio>
 #include <functional>
+#include <mutex>
+#include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "alloc/replicas.h"
@@ -326,6 +329,88 @@ static void TestGrpcLoopback() {
   rmdir(dir.c_str());
 }
 
+// N loops: connections are dealt round-robin, handlers of different connections
+// run on different threads, PostAll reaches every loop, and each stream is
+// only touched by the loop that owns it.
+static void TestGrpcMultiLoop() {
+  g_case = "grpc/multi-loop";
+  std::string dir = "/tmp/adp-unit-ml-" + std::to_string(getpid());
+  mkdir(dir.c_str(), 0755);
+  std::string sock = dir + "/m.sock";
+  constexpr int kLoops = 4, kClients = 8;
+  grpc::Server srv("multi", kLoops);
+  CHECK(srv.loops() == kLoops);
+  std::mutex mu;
+  std::set<std::thread::id> threads;
+  std::vector<std::vector<std::shared_ptr<grpc::ServerStream>>> per_loop(kLoops);
+  std::atomic<int> early{0}, off_loop{0};
+  srv.Post([&] { early.fetch_add(1); });  // queued before Start()
+  srv.AddUnary("/t.S/Who", [&](std::string_view q, std::string* r) {
+    std::lock_guard<std::mutex> lk(mu);
+    threads.insert(std::this_thread::get_id());
+    r->assign(q);
+    return Status::Ok();
+  });
+  srv.AddServerStream("/t.S/Watch", [&](std::string_view, std::shared_ptr<grpc::ServerStream> s) {
+    if (!srv.OnLoopThread()) off_loop.fetch_add(1);
+    per_loop[s->loop()].push_back(s);  // confined to loop s->loop()
+    s->Send("hello");
+    return Status::Ok();
+  });
+  CHECK(srv.Listen(sock).ok());
+  CHECK(srv.Start().ok());
+  std::vector<std::unique_ptr<grpc::Channel>> chans;
+  std::vector<int32_t> sids;
+  for (int i = 0; i < kClients; ++i) {
+    auto ch = grpc::Channel::Dial(sock, 2000);
+    CHECK(ch.ok());
+    if (!ch.ok()) break;
+    chans.push_back(std::move(*ch));
+  }
+  for (auto& ch : chans) {
+    std::string r;
+    CHECK(ch->Unary("/t.S/Who", "x", &r, 2000).ok() && r == "x");
+    auto sid = ch->StartStream("/t.S/Watch", "");
+    CHECK(sid.ok());
+    std::string m;
+    CHECK(sid.ok() && ch->Recv(*sid, &m, 2000).ok() && m == "hello");
+    sids.push_back(sid.ok() ? *sid : 0);
+  }
+  CHECK(early.load() == 1);
+  CHECK(off_loop.load() == 0);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    CHECK(static_cast<int>(threads.size()) == kLoops);
+  }
+  std::atomic<int> reached{0};
+  srv.PostAll([&](int loop) {
+    reached.fetch_add(1);
+    for (auto& s : per_loop[loop]) s->Send("update-" + std::to_string(loop));
+  });
+  for (size_t i = 0; i < chans.size(); ++i) {
+    std::string m;
+    CHECK(chans[i]->Recv(sids[i], &m, 2000).ok() && StartsWith(m, "update-"));
+  }
+  CHECK(reached.load() == kLoops);
+  int streams = 0;
+  for (auto& v : per_loop) streams += static_cast<int>(v.size());
+  CHECK(streams == kClients);
+  for (auto& v : per_loop) CHECK(v.size() == kClients / kLoops);  // round-robin
+  srv.PostAll([&](int loop) {
+    for (auto& s : per_loop[loop]) s->Finish(Status::Ok());
+  });
+  for (size_t i = 0; i < chans.size(); ++i) {
+    std::string m;
+    CHECK(chans[i]->Recv(sids[i], &m, 2000).code() == Code::kNotFound);
+  }
+  srv.Stop();
+  srv.Stop();  // idempotent
+  srv.Post([] {});  // dropped after Stop
+  chans.clear();
+  for (auto& v : per_loop) v.clear();
+  rmdir(dir.c_str());
+}
+
 int main() {
   TestPrioritize();
   TestStrip();
@@ -335,6 +420,7 @@ int main() {
   TestTopology();
   TestConfig();
   TestGrpcLoopback();
+  TestGrpcMultiLoop();
   printf("%d checks, %d failed\n", g_checks, g_failed);
   return g_failed ? 1 : 0;
 }
