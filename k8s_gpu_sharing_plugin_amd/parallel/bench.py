@@ -178,6 +178,7 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                     "parallelism": f"ranks{world} (one kubelet client per GPU)",
                     "partition_strategy": strategy,
                     "resource_config": rc,
+                    "server_threads": server.get("server_threads"),
                 },
                 "allocatable": info["allocatable"],
                 "advertised": info["advertised"],

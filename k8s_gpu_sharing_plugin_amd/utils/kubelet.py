@@ -76,7 +76,10 @@ class PluginClient:
     def __init__(self, socket_path: str):
         m = messages()
         self.m = m
-        self.channel = grpc.insecure_channel("unix:" + socket_path)
+        # Own subchannel pool: every client is its own connection (grpcio would
+        # otherwise share one between channels to the same target).
+        self.channel = grpc.insecure_channel("unix:" + socket_path,
+                                             options=[("grpc.use_local_subchannel_pool", 1)])
         svc = "/v1beta1.DevicePlugin/"
 
         def uu(name, req, resp):

@@ -85,7 +85,7 @@ const std::vector<FlagDef>& Table() {
        "directory for the generated CDI spec (cdi-annotations / cdi-cri strategies)",
        [](Flags& f) -> void* { return &f.cdi_spec_dir; }},
       {"server-threads", "DP_SERVER_THREADS", "serverThreads", Kind::kUint,
-       "gRPC loop threads per plugin socket (0 = min(4, CPUs))",
+       "gRPC loop threads per plugin socket (0 = min(8, CPUs))",
        [](Flags& f) -> void* { return &f.server_threads; }},
   };
   return t;

@@ -54,7 +54,7 @@ const char* DeviceListStrategyName(DeviceListStrategy s) {
 
 int DefaultServerThreads() {
   unsigned n = std::thread::hardware_concurrency();
-  return static_cast<int>(std::clamp(n, 1u, 4u));
+  return static_cast<int>(std::clamp(n, 1u, 8u));
 }
 
 const char* DeviceIdStrategyName(DeviceIdStrategy s) {
@@ -517,16 +517,22 @@ std::string Plugin::StatsJson() const {
   double avg = n ? stats_.allocate_ns_total.load() / 1e3 / n : 0.0;
   uint64_t np = stats_.preferred_calls.load();
   double pavg = np ? stats_.preferred_ns_total.load() / 1e3 / np : 0.0;
-  char buf[640];
+  int loops = 0;
+  {
+    std::lock_guard<std::mutex> lk(server_mu_);
+    if (server_) loops = server_->loops();
+  }
+  char buf[704];
   snprintf(buf, sizeof(buf),
            "{\"resource\": \"%s\", \"devices\": %zu, \"advertised\": %zu, \"allocate_calls\": %llu, "
            "\"allocate_handler_avg_us\": %.3f, \"allocate_handler_max_us\": %.3f, "
            "\"preferred_calls\": %llu, \"preferred_handler_avg_us\": %.3f, "
-           "\"preferred_handler_max_us\": %.3f, \"law_sends\": %llu, \"law_bytes\": %zu}",
+           "\"preferred_handler_max_us\": %.3f, \"law_sends\": %llu, \"law_bytes\": %zu, "
+           "\"server_threads\": %d}",
            JsonEscape(spec_.resource_name).c_str(), units_.size(), advertised_.size(),
            static_cast<unsigned long long>(n), avg, stats_.allocate_ns_max.load() / 1e3,
            static_cast<unsigned long long>(np), pavg, stats_.preferred_ns_max.load() / 1e3,
-           static_cast<unsigned long long>(stats_.law_sends.load()), law_bytes_size_.load());
+           static_cast<unsigned long long>(stats_.law_sends.load()), law_bytes_size_.load(), loops);
   return buf;
 }
 

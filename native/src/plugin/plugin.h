@@ -74,8 +74,8 @@ struct PluginOptions {
   int server_threads = 0;                 // gRPC loops; <=0 -> DefaultServerThreads()
 };
 
-// min(4, online CPUs): enough to serve the kubelet plus a few concurrent clients
-// without taking a node's cores from workloads.
+// min(8, online CPUs): one loop per GPU of an 8-GPU node. Idle loops sit in
+// epoll_wait and cost no CPU; they only matter under concurrent clients.
 int DefaultServerThreads();
 
 // One allocatable device (whole GPU or partition) after snapshot resolution.

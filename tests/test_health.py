@@ -48,7 +48,8 @@ class Node:
         self.d = harness.Daemon(scratch, fx, args=args, env=env, event_fifo=self.fifo,
                                 state_dir=self.state).start()
         reg = self.k.wait_registration()
-        self.c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        self.c_path = os.path.join(scratch, reg.endpoint)
+        self.c = kubelet.PluginClient(self.c_path)
         self.q, self.call = self.c.watch()
         self.first = self.q.get(timeout=5)
 
@@ -172,3 +173,23 @@ def test_events_unsupported_falls_back_to_polling(node):
     assert "using polling only" in n.d.log()
     open(os.path.join(n.state, "gpu0.dead"), "w").close()
     assert "Unhealthy" in n.health(n.next()).values()
+
+
+def test_every_watcher_on_every_loop_sees_each_transition(node):
+    """Watchers are spread over the server's loops; one transition reaches each once."""
+    n = node(args=["--server-threads", "4"])
+    ids = [x.ID for x in n.first.devices]
+    extra = []
+    for _ in range(7):  # 8 connections over 4 loops (+ the self-dial probe)
+        c = kubelet.PluginClient(n.c_path)
+        q, call = c.watch()
+        assert n.health(q.get(timeout=5)) == {i: "Healthy" for i in ids}
+        extra.append((c, q, call))
+    n.inject("1 3")
+    for q in [n.q] + [e[1] for e in extra]:
+        assert n.health(q.get(timeout=5))[ids[1]] == "Unhealthy"
+    time.sleep(0.3)
+    assert all(q.empty() for q in [n.q] + [e[1] for e in extra])  # no duplicates
+    for c, _, call in extra:
+        call.cancel()
+        c.close()
