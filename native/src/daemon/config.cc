@@ -24,7 +24,27 @@ struct FlagDef {
   Kind kind;
   const char* help;
   std::function<void*(Flags&)> field;
+  bool allow_zero = false;  // kUint: 0 is a meaningful value ("auto")
 };
+
+// Names the reference (NVIDIA-derived) deployment used for the same settings, so
+// an existing DaemonSet/config file keeps working when switched to this plugin.
+// The canonical name wins when both are given at the same precedence level.
+struct AliasDef {
+  const char* name;       // command line alias
+  const char* env;        // environment alias ("" = none)
+  const char* file_key;   // config-file alias ("" = none)
+  const char* canonical;  // FlagDef::name
+};
+
+const std::vector<AliasDef>& Aliases() {
+  static const std::vector<AliasDef> t = {
+      {"mig-strategy", "MIG_STRATEGY", "migStrategy", "partition-strategy"},  // main.go:63-71
+      {"nvidia-driver-root", "NVIDIA_DRIVER_ROOT", "nvidiaDriverRoot", "driver-root"},  // :108-116
+      {"", "NVIDIA_DRIVER_RESOURCE_CONFIG", "", "resource-config"},  // main.go:123-129
+  };
+  return t;
+}
 
 const std::vector<FlagDef>& Table() {
   static const std::vector<FlagDef> t = {
@@ -86,7 +106,7 @@ const std::vector<FlagDef>& Table() {
        [](Flags& f) -> void* { return &f.cdi_spec_dir; }},
       {"server-threads", "DP_SERVER_THREADS", "serverThreads", Kind::kUint,
        "gRPC loop threads per plugin socket (0 = min(8, CPUs))",
-       [](Flags& f) -> void* { return &f.server_threads; }},
+       [](Flags& f) -> void* { return &f.server_threads; }, true},
   };
   return t;
 }
@@ -105,7 +125,7 @@ Status Assign(const FlagDef& d, Flags& f, const std::string& value, const std::s
     }
     case Kind::kUint: {
       auto u = ParseUint(Trim(value));
-      if (!u || *u == 0) return InvalidArgument("invalid value '" + value + "' for " + d.name + " (" + origin + ")");
+      if (!u || (*u == 0 && !d.allow_zero)) return InvalidArgument("invalid value '" + value + "' for " + d.name + " (" + origin + ")");
       *static_cast<uint64_t*>(p) = *u;
       return Status::Ok();
     }
@@ -264,6 +284,14 @@ Result<Config> LoadConfig(int argc, const char* const* argv,
     const FlagDef* def = nullptr;
     for (const auto& d : Table())
       if (name == d.name) def = &d;
+    std::string key = name;
+    for (const auto& a : Aliases()) {
+      if (def || !*a.name || name != a.name) continue;
+      for (const auto& d : Table())
+        if (std::string(a.canonical) == d.name) def = &d;
+      key = std::string("alias:") + a.canonical;
+      cfg.deprecations.push_back("--" + name + " is accepted for compatibility; use --" + a.canonical);
+    }
     if (!def) return InvalidArgument("flag provided but not defined: --" + name);
     if (!has_value) {
       if (def->kind == Kind::kBool) {
@@ -273,7 +301,7 @@ Result<Config> LoadConfig(int argc, const char* const* argv,
         value = argv[++i];
       }
     }
-    cli[name] = value;
+    cli[key] = value;
   }
   if (cfg.config_file.empty() && env.count("CONFIG_FILE")) cfg.config_file = env["CONFIG_FILE"];
 
@@ -290,13 +318,32 @@ Result<Config> LoadConfig(int argc, const char* const* argv,
     file = std::move(*parsed);
   }
 
-  // Precedence: command line > environment > config file > default.
+  // Precedence: command line > environment > config file > default; at each
+  // level the canonical name beats its compatibility alias.
   for (const auto& d : Table()) {
+    const AliasDef* alias = nullptr;
+    for (const auto& a : Aliases())
+      if (std::string(a.canonical) == d.name) alias = &a;
+    std::string alias_cli = std::string("alias:") + d.name;
+    std::string file_key = std::string("flags.") + d.file_key;
+    std::string alias_file = alias && *alias->file_key ? std::string("flags.") + alias->file_key : "";
     Status st;
-    if (cli.count(d.name)) st = Assign(d, cfg.flags, cli[d.name], std::string("--") + d.name);
-    else if (*d.env && env.count(d.env)) st = Assign(d, cfg.flags, env[d.env], d.env);
-    else if (*d.file_key && file.count(std::string("flags.") + d.file_key))
-      st = Assign(d, cfg.flags, file[std::string("flags.") + d.file_key], cfg.config_file);
+    if (cli.count(d.name)) {
+      st = Assign(d, cfg.flags, cli[d.name], std::string("--") + d.name);
+    } else if (alias && cli.count(alias_cli)) {
+      st = Assign(d, cfg.flags, cli[alias_cli], std::string("--") + alias->name);
+    } else if (*d.env && env.count(d.env)) {
+      st = Assign(d, cfg.flags, env[d.env], d.env);
+    } else if (alias && *alias->env && env.count(alias->env)) {
+      st = Assign(d, cfg.flags, env[alias->env], alias->env);
+      cfg.deprecations.push_back(std::string(alias->env) + " is accepted for compatibility; use " + d.env);
+    } else if (*d.file_key && file.count(file_key)) {
+      st = Assign(d, cfg.flags, file[file_key], cfg.config_file);
+    } else if (!alias_file.empty() && file.count(alias_file)) {
+      st = Assign(d, cfg.flags, file[alias_file], cfg.config_file);
+      cfg.deprecations.push_back(std::string("config key ") + alias->file_key +
+                                 " is accepted for compatibility; use " + d.file_key);
+    }
     if (!st.ok()) return st;
   }
   return cfg;
@@ -324,6 +371,13 @@ std::string UsageText() {
          ")\n      " + d.help + "\n";
   }
   s += "  --config-file  (env CONFIG_FILE)\n      versioned YAML/JSON config (version: v1, flags: {...})\n";
+  s += "\nCompatibility aliases (reference deployments):\n";
+  for (const auto& a : Aliases()) {
+    s += "  ";
+    if (*a.name) s += std::string("--") + a.name + "  ";
+    if (*a.env) s += std::string("(env ") + a.env + ")  ";
+    s += std::string("-> --") + a.canonical + "\n";
+  }
   s += "  --version, --help\n";
   return s;
 }

@@ -53,6 +53,7 @@ struct Config {
   std::string config_file;
   bool show_version = false;
   bool show_help = false;
+  std::vector<std::string> deprecations;  // compatibility aliases that were used
   std::string ToJson() const;
 };
 

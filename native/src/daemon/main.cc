@@ -27,5 +27,6 @@ int main(int argc, char** argv) {
     return 0;
   }
   LOG_INFO("main", "amdgpu-device-plugin %s", ADP_VERSION);
+  for (const auto& d : cfg->deprecations) LOG_WARN("main", "%s", d.c_str());
   return adp::daemon::RunDaemon(*cfg);
 }

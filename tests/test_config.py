@@ -114,3 +114,41 @@ def test_resource_config_env_renames_resource(scratch):
     c.close()
     d.stop()
     k.stop()
+
+
+def test_reference_flag_names_are_accepted(scratch):
+    """A reference DaemonSet/config (mig-strategy, nvidia-driver-root,
+    NVIDIA_DRIVER_RESOURCE_CONFIG; main.go:63-129) keeps working unchanged."""
+    body = "version: v1\nflags:\n  migStrategy: mixed\n  nvidiaDriverRoot: /run/nvidia/driver\n"
+    f = effective_config(scratch, file_body=body,
+                         env={"NVIDIA_DRIVER_RESOURCE_CONFIG": "gpu:sharedgpu:2"})
+    assert f["partitionStrategy"] == "mixed"
+    assert f["driverRoot"] == "/run/nvidia/driver"
+    assert f["resourceConfig"] == "gpu:sharedgpu:2"
+    f = effective_config(scratch, args=["--mig-strategy", "single", "--nvidia-driver-root=/x"],
+                         env={"MIG_STRATEGY": "mixed"})
+    assert f["partitionStrategy"] == "single" and f["driverRoot"] == "/x"
+    f = effective_config(scratch, env={"MIG_STRATEGY": "single"})
+    assert f["partitionStrategy"] == "single"
+
+
+def test_canonical_name_beats_alias(scratch):
+    f = effective_config(scratch, args=["--mig-strategy", "mixed", "--partition-strategy", "single"],
+                         env={"MIG_STRATEGY": "mixed", "NVIDIA_DRIVER_RESOURCE_CONFIG": "gpu:a:2",
+                              "RESOURCE_CONFIG": "gpu:b:3"})
+    assert f["partitionStrategy"] == "single"
+    assert f["resourceConfig"] == "gpu:b:3"
+
+
+def test_alias_use_is_logged(scratch):
+    d = harness.Daemon(scratch, args=["--mig-strategy", "none"]).start()
+    text = d.wait_log("running with resource config")
+    d.stop()
+    assert "--mig-strategy is accepted for compatibility; use --partition-strategy" in text
+
+
+def test_server_threads_zero_means_auto(scratch):
+    f = effective_config(scratch, args=["--server-threads", "0"])
+    assert f["serverThreads"] == 0
+    f = effective_config(scratch, env={"DP_SERVER_THREADS": "3"})
+    assert f["serverThreads"] == 3
