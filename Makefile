@@ -4,7 +4,7 @@ JOBS       ?= 8
 PY         ?= python3
 GPURUN     ?= /usr/local/graft/bin/gpurun
 
-.PHONY: all build probe test test-native test-gpu bench asan tsan lint image clean
+.PHONY: all build probe test test-native test-gpu bench asan tsan tsan-e2e lint image clean
 
 all: build
 
@@ -40,6 +40,17 @@ tsan:
 	ninja -C build/tsan -j$(JOBS) adp_unit_tests adp_stress
 	TSAN_OPTIONS=halt_on_error=1 build/tsan/adp_unit_tests
 	TSAN_OPTIONS=halt_on_error=1 build/tsan/adp_stress
+
+# The daemon itself under TSan, driven by the end-to-end suites (tests that load
+# the C API into Python are skipped: a TSan .so cannot be dlopen'ed there).
+tsan-e2e:
+	cmake -S native -B build/tsan -G Ninja -DCMAKE_BUILD_TYPE=RelWithDebInfo -DADP_TSAN=ON >/dev/null
+	ninja -C build/tsan -j$(JOBS) amdgpu-device-plugin amdgpu-dp-kubelet amdsmi_mock
+	rm -rf build/tsan-logs && mkdir -p build/tsan-logs
+	ADP_BUILD_DIR=$(CURDIR)/build/tsan TSAN_OPTIONS=log_path=$(CURDIR)/build/tsan-logs/daemon \
+	  $(PY) -m pytest -q -p no:cacheprovider tests/test_e2e_mock.py tests/test_health.py \
+	  tests/test_metrics.py tests/test_lifecycle.py -k "not additional_ids and not classification"
+	@if ls build/tsan-logs/* >/dev/null 2>&1; then cat build/tsan-logs/*; exit 1; fi
 
 lint:
 	@command -v clang-format >/dev/null && find native -name '*.cc' -o -name '*.h' | xargs clang-format --dry-run -Werror || echo "clang-format not installed; skipped"

@@ -107,6 +107,9 @@ const std::vector<FlagDef>& Table() {
       {"server-threads", "DP_SERVER_THREADS", "serverThreads", Kind::kUint,
        "gRPC loop threads per plugin socket (0 = min(8, CPUs))",
        [](Flags& f) -> void* { return &f.server_threads; }, true},
+      {"metrics-addr", "DP_METRICS_ADDR", "metricsAddr", Kind::kString,
+       "serve Prometheus /metrics and /healthz on this TCP address, e.g. ':9400' (empty = off)",
+       [](Flags& f) -> void* { return &f.metrics_addr; }},
   };
   return t;
 }

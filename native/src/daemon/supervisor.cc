@@ -13,7 +13,9 @@
 
 #include <algorithm>
 #include <cstring>
+#include <atomic>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "alloc/replicas.h"
@@ -21,6 +23,7 @@
 #include "common/strings.h"
 #include "health/health.h"
 #include "inventory/inventory.h"
+#include "metrics/metrics.h"
 #include "plugin/plugin.h"
 #include "smi/smi.h"
 #include "strategy/strategy.h"
@@ -183,15 +186,57 @@ int RunDaemon(const Config& cfg) {
   }
 
   std::vector<std::unique_ptr<plugin::Plugin>> plugins;
+  // The metrics thread reads `plugins`; the vector is only changed under this
+  // lock (plugin objects themselves are safe to read while they start/stop).
+  std::mutex plugins_mu;
+  std::atomic<uint64_t> restarts{0};
+  std::atomic<bool> serving{false};
   std::unique_ptr<health::Monitor> monitor;
   int backoff_ms = 1000;
   int exit_code = 0;
   bool quit = false;
 
+  std::unique_ptr<metrics::HttpServer> http;
+  if (!cfg.flags.metrics_addr.empty()) {
+    std::string smi_version = (*lib)->Version();
+    http = std::make_unique<metrics::HttpServer>(
+        [&, smi_version] {
+          std::string out =
+              "# HELP amdgpu_dp_build_info Plugin and amdsmi versions.\n"
+              "# TYPE amdgpu_dp_build_info gauge\n"
+              "amdgpu_dp_build_info{version=\"" ADP_VERSION "\",amdsmi=\"" +
+              metrics::LabelValue(smi_version) +
+              "\"} 1\n"
+              "# HELP amdgpu_dp_restarts_total Plugin (re)starts: kubelet restart, SIGHUP, retries.\n"
+              "# TYPE amdgpu_dp_restarts_total counter\n"
+              "amdgpu_dp_restarts_total " + std::to_string(restarts.load()) + "\n";
+          std::lock_guard<std::mutex> lk(plugins_mu);
+          std::vector<const plugin::Plugin*> ps;
+          for (auto& p : plugins)
+            if (p->device_count() > 0) ps.push_back(p.get());
+          plugin::Plugin::AppendPrometheus(ps, &out);
+          return out;
+        },
+        [&] {
+          if (!serving.load()) return false;
+          std::lock_guard<std::mutex> lk(plugins_mu);
+          for (auto& p : plugins)
+            if (p->device_count() > 0 && !p->running()) return false;
+          return true;
+        });
+    Status ms = http->Start(cfg.flags.metrics_addr);
+    if (!ms.ok()) {
+      LOG_ERROR(kComp, "%s", ms.ToString().c_str());
+      return 1;
+    }
+  }
+
   auto stop_all = [&] {
+    serving.store(false);
     if (monitor) monitor->Stop();
     monitor.reset();
     for (auto& p : plugins) p->Stop();
+    std::lock_guard<std::mutex> lk(plugins_mu);
     plugins.clear();
   };
 
@@ -218,7 +263,11 @@ int RunDaemon(const Config& cfg) {
       quit = true;
       return;
     }
-    for (auto& s : *specs) plugins.push_back(std::make_unique<plugin::Plugin>(*snap, s, v.popts));
+    restarts.fetch_add(1);
+    {
+      std::lock_guard<std::mutex> lk(plugins_mu);
+      for (auto& s : *specs) plugins.push_back(std::make_unique<plugin::Plugin>(*snap, s, v.popts));
+    }
     int started = 0;
     for (auto& p : plugins) {
       if (p->device_count() == 0) continue;
@@ -236,6 +285,7 @@ int RunDaemon(const Config& cfg) {
       ++started;
     }
     backoff_ms = 1000;
+    serving.store(true);
     if (started == 0) LOG_INFO(kComp, "no devices found; waiting indefinitely");
     monitor = std::make_unique<health::Monitor>(lib->get(), *snap, health::HealthConfig::FromEnv());
     for (auto& p : plugins) {
@@ -316,6 +366,7 @@ int RunDaemon(const Config& cfg) {
     if (do_restart && !quit) restart();
   }
   stop_all();
+  if (http) http->Stop();
   for (int fd : {ep, sfd, ifd, tfd, efd}) close(fd);
   LOG_INFO(kComp, "shutdown complete (exit %d)", exit_code);
   return exit_code;

@@ -1,5 +1,9 @@
 #include "health/health.h"
 
+#include <poll.h>
+#include <sys/eventfd.h>
+#include <unistd.h>
+
 #include <chrono>
 #include <cstdlib>
 
@@ -104,18 +108,27 @@ Status Monitor::Start() {
   }
   if (!events_ok_ && cfg_.poll_interval_ms == 0) return Status::Ok();
   stop_.store(false);
+  if (wake_fd_ < 0) wake_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   thread_ = std::thread([this] { Run(); });
   return Status::Ok();
 }
 
+void Monitor::Sleep(int ms) {
+  pollfd p{wake_fd_, POLLIN, 0};
+  poll(&p, 1, ms);
+}
+
 void Monitor::Stop() {
   if (thread_.joinable()) {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_.store(true);
-    }
-    cv_.notify_all();
+    stop_.store(true);
+    uint64_t one = 1;
+    ssize_t w = write(wake_fd_, &one, sizeof(one));
+    (void)w;
     thread_.join();
+  }
+  if (wake_fd_ >= 0) {
+    close(wake_fd_);
+    wake_fd_ = -1;
   }
   if (events_ok_) {
     lib_->EventsStop(handles_);
@@ -157,8 +170,7 @@ void Monitor::Run() {
       Status st = lib_->EventsWait(slice, &events);
       if (!st.ok()) {
         LOG_WARN(kComp, "event wait failed: %s", st.ToString().c_str());
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait_for(lk, std::chrono::milliseconds(slice), [this] { return stop_.load(); });
+        Sleep(slice);
       }
       for (const auto& e : events) {
         int gpu = -1;
@@ -179,8 +191,7 @@ void Monitor::Run() {
         Notify(gpu, verdict > 0, std::string(EventName(e.type)) + ": " + e.message);
       }
     } else {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait_for(lk, std::chrono::milliseconds(slice), [this] { return stop_.load(); });
+      Sleep(slice);
     }
     if (cfg_.poll_interval_ms > 0 && Clock::now() >= next_poll) {
       PollOnce();

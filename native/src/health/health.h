@@ -26,7 +26,6 @@
 #pragma once
 
 #include <atomic>
-#include <condition_variable>
 #include <cstdint>
 #include <functional>
 #include <memory>
@@ -82,8 +81,8 @@ class Monitor {
   bool events_ok_ = false;
   std::thread thread_;
   std::atomic<bool> stop_{false};
-  std::mutex mu_;
-  std::condition_variable cv_;
+  int wake_fd_ = -1;  // eventfd: Stop() wakes the idle wait at once
+  void Sleep(int ms);
   // Per-GPU polling state.
   std::vector<uint64_t> ecc_baseline_;
   std::vector<uint8_t> unresponsive_;

@@ -1,0 +1,214 @@
+#include "metrics/metrics.h"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+
+#include "common/log.h"
+#include "common/strings.h"
+
+namespace adp::metrics {
+namespace {
+constexpr const char* kComp = "metrics";
+}
+
+const double Histogram::kBoundsSec[kBuckets] = {
+    250e-9, 500e-9, 1e-6, 2e-6, 5e-6, 10e-6, 20e-6, 50e-6, 100e-6, 200e-6,
+    500e-6, 1e-3,   2e-3, 5e-3, 10e-3, 20e-3, 50e-3, 100e-3, 500e-3, 1.0};
+
+void Histogram::Observe(uint64_t ns) {
+  int b = 0;
+  while (b < kBuckets && ns > static_cast<uint64_t>(kBoundsSec[b] * 1e9 + 0.5)) ++b;
+  buckets_[b].fetch_add(1, std::memory_order_relaxed);
+  count_.fetch_add(1, std::memory_order_relaxed);
+  sum_ns_.fetch_add(ns, std::memory_order_relaxed);
+}
+
+double Histogram::QuantileUs(double q) const {
+  uint64_t total = 0;
+  uint64_t counts[kBuckets + 1];
+  for (int b = 0; b <= kBuckets; ++b) total += counts[b] = buckets_[b].load(std::memory_order_relaxed);
+  if (total == 0) return 0.0;
+  uint64_t rank = static_cast<uint64_t>(q * static_cast<double>(total - 1)) + 1;
+  uint64_t seen = 0;
+  for (int b = 0; b <= kBuckets; ++b) {
+    seen += counts[b];
+    if (seen >= rank) return (b < kBuckets ? kBoundsSec[b] : kBoundsSec[kBuckets - 1] * 10) * 1e6;
+  }
+  return kBoundsSec[kBuckets - 1] * 1e6;
+}
+
+void Histogram::AppendPrometheus(const std::string& name, const std::string& labels,
+                                 std::string* out) const {
+  uint64_t cum = 0;
+  char line[512];
+  std::string sep = labels.empty() ? "" : ",";
+  for (int b = 0; b <= kBuckets; ++b) {
+    cum += buckets_[b].load(std::memory_order_relaxed);
+    if (b < kBuckets)
+      snprintf(line, sizeof(line), "%s_bucket{%s%sle=\"%g\"} %llu\n", name.c_str(), labels.c_str(),
+               sep.c_str(), kBoundsSec[b], static_cast<unsigned long long>(cum));
+    else
+      snprintf(line, sizeof(line), "%s_bucket{%s%sle=\"+Inf\"} %llu\n", name.c_str(), labels.c_str(),
+               sep.c_str(), static_cast<unsigned long long>(cum));
+    *out += line;
+  }
+  snprintf(line, sizeof(line), "%s_sum{%s} %.9f\n%s_count{%s} %llu\n", name.c_str(), labels.c_str(),
+           sum_seconds(), name.c_str(), labels.c_str(), static_cast<unsigned long long>(cum));
+  *out += line;
+}
+
+void Histogram::Reset() {
+  for (auto& b : buckets_) b.store(0, std::memory_order_relaxed);
+  count_.store(0, std::memory_order_relaxed);
+  sum_ns_.store(0, std::memory_order_relaxed);
+}
+
+std::string LabelValue(const std::string& v) {
+  std::string o;
+  o.reserve(v.size());
+  for (char c : v) {
+    if (c == '\\') o += "\\\\";
+    else if (c == '"') o += "\\\"";
+    else if (c == '\n') o += "\\n";
+    else o += c;
+  }
+  return o;
+}
+
+HttpServer::HttpServer(Render render, Healthy healthy)
+    : render_(std::move(render)), healthy_(std::move(healthy)) {}
+
+HttpServer::~HttpServer() { Stop(); }
+
+Status HttpServer::Start(const std::string& addr) {
+  std::string host, port = addr;
+  size_t colon = addr.rfind(':');
+  if (colon != std::string::npos) {
+    host = addr.substr(0, colon);
+    port = addr.substr(colon + 1);
+  }
+  if (!host.empty() && host.front() == '[' && host.back() == ']') host = host.substr(1, host.size() - 2);
+  auto p = ParseUint(port);
+  if (!p || *p > 65535) return InvalidArgument("invalid --metrics-addr '" + addr + "'");
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  hints.ai_flags = AI_PASSIVE | AI_NUMERICSERV;
+  int rc = getaddrinfo(host.empty() ? nullptr : host.c_str(), port.c_str(), &hints, &res);
+  if (rc != 0) return InvalidArgument("invalid --metrics-addr '" + addr + "': " + gai_strerror(rc));
+  Status st = Unavailable("no usable address for " + addr);
+  for (addrinfo* ai = res; ai; ai = ai->ai_next) {
+    int fd = socket(ai->ai_family, ai->ai_socktype | SOCK_CLOEXEC | SOCK_NONBLOCK, ai->ai_protocol);
+    if (fd < 0) continue;
+    int one = 1;
+    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    if (bind(fd, ai->ai_addr, ai->ai_addrlen) == 0 && listen(fd, 16) == 0) {
+      listen_fd_ = fd;
+      sockaddr_storage ss{};
+      socklen_t len = sizeof(ss);
+      getsockname(fd, reinterpret_cast<sockaddr*>(&ss), &len);
+      port_ = ntohs(ss.ss_family == AF_INET6 ? reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port
+                                             : reinterpret_cast<sockaddr_in*>(&ss)->sin_port);
+      break;
+    }
+    st = Unavailable("metrics listen on " + addr + ": " + strerror(errno));
+    close(fd);
+  }
+  freeaddrinfo(res);
+  if (listen_fd_ < 0) return st;
+  stop_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  thread_ = std::thread([this] { Run(); });
+  LOG_INFO(kComp, "serving /metrics and /healthz on port %d", port_);
+  return Status::Ok();
+}
+
+void HttpServer::Stop() {
+  if (thread_.joinable()) {
+    uint64_t one = 1;
+    ssize_t w = write(stop_fd_, &one, sizeof(one));
+    (void)w;
+    thread_.join();
+  }
+  if (listen_fd_ >= 0) close(listen_fd_);
+  if (stop_fd_ >= 0) close(stop_fd_);
+  listen_fd_ = stop_fd_ = -1;
+}
+
+void HttpServer::Run() {
+  while (true) {
+    pollfd p[2] = {{listen_fd_, POLLIN, 0}, {stop_fd_, POLLIN, 0}};
+    if (poll(p, 2, -1) < 0) {
+      if (errno == EINTR) continue;
+      return;
+    }
+    if (p[1].revents) return;
+    int fd = accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK);
+    if (fd >= 0) {
+      Serve(fd);
+      close(fd);
+    }
+  }
+}
+
+// One request per connection, 2 s budget for the whole exchange (a scraper on
+// the node, not a general web server).
+void HttpServer::Serve(int fd) {
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(2);
+  auto left_ms = [&] {
+    auto d = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now());
+    return static_cast<int>(std::max<long long>(0, d.count()));
+  };
+  std::string req;
+  char buf[2048];
+  while (req.find("\r\n\r\n") == std::string::npos && req.size() < 8192) {
+    pollfd p{fd, POLLIN, 0};
+    if (poll(&p, 1, left_ms()) <= 0) return;
+    ssize_t n = read(fd, buf, sizeof(buf));
+    if (n <= 0) return;
+    req.append(buf, static_cast<size_t>(n));
+  }
+  std::string line = req.substr(0, req.find("\r\n"));
+  auto parts = Split(line, ' ');
+  std::string status = "200 OK", type = "text/plain; version=0.0.4; charset=utf-8", body;
+  std::string path = parts.size() >= 2 ? parts[1] : "";
+  if (size_t q = path.find('?'); q != std::string::npos) path.resize(q);
+  if (parts.size() < 3 || (parts[0] != "GET" && parts[0] != "HEAD")) {
+    status = "405 Method Not Allowed";
+    body = "only GET\n";
+  } else if (path == "/metrics") {
+    body = render_();
+  } else if (path == "/healthz") {
+    bool ok = healthy_();
+    status = ok ? "200 OK" : "503 Service Unavailable";
+    body = ok ? "ok\n" : "plugins not serving\n";
+  } else {
+    status = "404 Not Found";
+    body = "try /metrics or /healthz\n";
+  }
+  std::string resp = "HTTP/1.1 " + status + "\r\nContent-Type: " + type +
+                     "\r\nContent-Length: " + std::to_string(body.size()) + "\r\nConnection: close\r\n\r\n";
+  if (parts.empty() || parts[0] != "HEAD") resp += body;
+  size_t off = 0;
+  while (off < resp.size()) {
+    ssize_t n = send(fd, resp.data() + off, resp.size() - off, MSG_NOSIGNAL);
+    if (n > 0) { off += static_cast<size_t>(n); continue; }
+    if (n < 0 && errno == EAGAIN) {
+      pollfd p{fd, POLLOUT, 0};
+      if (poll(&p, 1, left_ms()) > 0) continue;
+    }
+    return;
+  }
+}
+
+}  // namespace adp::metrics

@@ -1,0 +1,69 @@
+// Observability: lock-free latency histograms and a Prometheus text endpoint.
+//
+// The reference has no metrics (Go `log` lines only). Here every
+// plugin keeps per-RPC handler-time histograms (atomic bucket counters, one
+// relaxed increment per call -- nothing on the Allocate path blocks), dumped by
+// SIGUSR1 and, when --metrics-addr is set, served as Prometheus text on
+// GET /metrics together with per-device health and build info. GET /healthz
+// answers 200 while every plugin that has devices is serving (a DaemonSet
+// liveness probe).
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <functional>
+#include <string>
+#include <thread>
+
+#include "common/status.h"
+
+namespace adp::metrics {
+
+// Fixed 1-2-5 buckets from 250 ns to 1 s (upper bounds, seconds).
+class Histogram {
+ public:
+  static constexpr int kBuckets = 20;
+  static const double kBoundsSec[kBuckets];
+
+  void Observe(uint64_t ns);
+  uint64_t count() const { return count_.load(std::memory_order_relaxed); }
+  double sum_seconds() const { return sum_ns_.load(std::memory_order_relaxed) / 1e9; }
+  // Upper bound of the bucket holding quantile q (0 if empty), in microseconds.
+  double QuantileUs(double q) const;
+  // Appends `name_bucket{labels,le=..}`, `name_sum`, `name_count` lines.
+  void AppendPrometheus(const std::string& name, const std::string& labels, std::string* out) const;
+  void Reset();
+
+ private:
+  std::atomic<uint64_t> buckets_[kBuckets + 1] = {};  // last = +Inf
+  std::atomic<uint64_t> count_{0};
+  std::atomic<uint64_t> sum_ns_{0};
+};
+
+// Escapes a Prometheus label value (backslash, quote, newline).
+std::string LabelValue(const std::string& v);
+
+// Minimal HTTP/1.1 server for /metrics and /healthz on one TCP address.
+class HttpServer {
+ public:
+  using Render = std::function<std::string()>;
+  using Healthy = std::function<bool()>;
+  HttpServer(Render render, Healthy healthy);
+  ~HttpServer();
+  // addr: "host:port", ":port" (all interfaces) or "port". Port 0 picks a free port.
+  Status Start(const std::string& addr);
+  void Stop();
+  int port() const { return port_; }
+
+ private:
+  void Run();
+  void Serve(int fd);
+  Render render_;
+  Healthy healthy_;
+  int listen_fd_ = -1;
+  int stop_fd_ = -1;
+  int port_ = 0;
+  std::thread thread_;
+};
+
+}  // namespace adp::metrics

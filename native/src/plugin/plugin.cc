@@ -168,6 +168,7 @@ void Plugin::RebuildListAndWatch() {
   auto snap = std::make_shared<LawSnapshot>();
   snap->version = ++law_version_;
   snap->bytes = std::move(out);
+  snap->healthy = healthy_;
   law_bytes_size_.store(snap->bytes.size(), std::memory_order_relaxed);
   std::lock_guard<std::mutex> lk(law_mu_);
   law_ = std::move(snap);
@@ -274,6 +275,7 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
               joined.c_str());
   }
   uint64_t dt = NowNs() - t0;
+  stats_.allocate_hist.Observe(dt);
   stats_.allocate_calls.fetch_add(1, std::memory_order_relaxed);
   stats_.allocate_ns_total.fetch_add(dt, std::memory_order_relaxed);
   uint64_t prev = stats_.allocate_ns_max.load(std::memory_order_relaxed);
@@ -285,6 +287,7 @@ Status Plugin::HandlePreferred(std::string_view req, std::string* resp) {
   uint64_t t0 = NowNs();
   Status st = PreferredImpl(req, resp);
   uint64_t dt = NowNs() - t0;
+  stats_.preferred_hist.Observe(dt);
   stats_.preferred_ns_total.fetch_add(dt, std::memory_order_relaxed);
   uint64_t prev = stats_.preferred_ns_max.load(std::memory_order_relaxed);
   while (dt > prev && !stats_.preferred_ns_max.compare_exchange_weak(prev, dt)) {}
@@ -401,6 +404,7 @@ Status Plugin::Start(std::function<void()> on_fatal) {
       return st;
     }
     LOG_INFO(kComp, "registered device plugin for '%s' with kubelet", spec_.resource_name.c_str());
+    registered_.store(true);
   }
   return Status::Ok();
 }
@@ -411,6 +415,7 @@ void Plugin::Stop() {
   std::lock_guard<std::mutex> lk(server_mu_);
   std::unique_ptr<grpc::Server> srv = std::move(server_);
   if (!srv) return;
+  registered_.store(false);
   LOG_INFO(kComp, "stopping '%s' on %s", spec_.resource_name.c_str(), socket_path().c_str());
   // End open ListAndWatch streams cleanly (the reference returns nil on stop);
   // each loop finishes the streams it owns.
@@ -522,18 +527,90 @@ std::string Plugin::StatsJson() const {
     std::lock_guard<std::mutex> lk(server_mu_);
     if (server_) loops = server_->loops();
   }
-  char buf[704];
+  char buf[960];
   snprintf(buf, sizeof(buf),
            "{\"resource\": \"%s\", \"devices\": %zu, \"advertised\": %zu, \"allocate_calls\": %llu, "
            "\"allocate_handler_avg_us\": %.3f, \"allocate_handler_max_us\": %.3f, "
            "\"preferred_calls\": %llu, \"preferred_handler_avg_us\": %.3f, "
            "\"preferred_handler_max_us\": %.3f, \"law_sends\": %llu, \"law_bytes\": %zu, "
-           "\"server_threads\": %d}",
+           "\"server_threads\": %d, \"allocate_handler_p50_le_us\": %g, "
+           "\"allocate_handler_p99_le_us\": %g, \"preferred_handler_p50_le_us\": %g, "
+           "\"preferred_handler_p99_le_us\": %g}",
            JsonEscape(spec_.resource_name).c_str(), units_.size(), advertised_.size(),
            static_cast<unsigned long long>(n), avg, stats_.allocate_ns_max.load() / 1e3,
            static_cast<unsigned long long>(np), pavg, stats_.preferred_ns_max.load() / 1e3,
-           static_cast<unsigned long long>(stats_.law_sends.load()), law_bytes_size_.load(), loops);
+           static_cast<unsigned long long>(stats_.law_sends.load()), law_bytes_size_.load(), loops,
+           stats_.allocate_hist.QuantileUs(0.5), stats_.allocate_hist.QuantileUs(0.99),
+           stats_.preferred_hist.QuantileUs(0.5), stats_.preferred_hist.QuantileUs(0.99));
   return buf;
+}
+
+size_t Plugin::healthy_count() const {
+  auto law = CurrentLaw();
+  size_t n = 0;
+  for (uint8_t h : law->healthy) n += h;
+  return n;
+}
+
+void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::string* out) {
+  using metrics::LabelValue;
+  char line[512];
+  auto family = [&](const char* name, const char* type, const char* help) {
+    snprintf(line, sizeof(line), "# HELP %s %s\n# TYPE %s %s\n", name, help, name, type);
+    *out += line;
+  };
+  auto gauge = [&](const char* name, const std::string& labels, double v) {
+    snprintf(line, sizeof(line), "%s{%s} %.17g\n", name, labels.c_str(), v);
+    *out += line;
+  };
+  auto res = [](const Plugin* p) { return "resource=\"" + LabelValue(p->spec_.resource_name) + "\""; };
+
+  family("amdgpu_dp_devices", "gauge", "Physical devices (GPUs or partitions) served by the plugin.");
+  for (auto* p : plugins) gauge("amdgpu_dp_devices", res(p), static_cast<double>(p->units_.size()));
+  family("amdgpu_dp_allocatable", "gauge", "Device IDs advertised to the kubelet (replicas included).");
+  for (auto* p : plugins) gauge("amdgpu_dp_allocatable", res(p), static_cast<double>(p->advertised_.size()));
+  family("amdgpu_dp_healthy_devices", "gauge", "Physical devices currently advertised Healthy.");
+  for (auto* p : plugins) gauge("amdgpu_dp_healthy_devices", res(p), static_cast<double>(p->healthy_count()));
+  family("amdgpu_dp_registered", "gauge", "1 while the plugin is serving and registered with the kubelet.");
+  for (auto* p : plugins) gauge("amdgpu_dp_registered", res(p), p->registered() ? 1 : 0);
+  family("amdgpu_dp_device_healthy", "gauge", "Per-device health (1 Healthy, 0 Unhealthy).");
+  for (auto* p : plugins) {
+    auto law = p->CurrentLaw();
+    for (size_t i = 0; i < p->units_.size(); ++i) {
+      const Unit& u = p->units_[i];
+      gauge("amdgpu_dp_device_healthy",
+            res(p) + ",device=\"" + LabelValue(u.id) + "\",index=\"" + LabelValue(u.index) +
+                "\",numa=\"" + std::to_string(u.numa) + "\"",
+            i < law->healthy.size() ? law->healthy[i] : 0);
+    }
+  }
+  family("amdgpu_dp_rpc_total", "counter", "Handled kubelet RPCs by method.");
+  for (auto* p : plugins) {
+    gauge("amdgpu_dp_rpc_total", res(p) + ",method=\"Allocate\"",
+          static_cast<double>(p->stats_.allocate_calls.load()));
+    gauge("amdgpu_dp_rpc_total", res(p) + ",method=\"GetPreferredAllocation\"",
+          static_cast<double>(p->stats_.preferred_calls.load()));
+    gauge("amdgpu_dp_rpc_total", res(p) + ",method=\"ListAndWatch\"",
+          static_cast<double>(p->stats_.law_sends.load()));
+  }
+  family("amdgpu_dp_handler_seconds", "histogram",
+         "In-daemon handler time per RPC (request decode, device lookup, response encode).");
+  for (auto* p : plugins) {
+    p->stats_.allocate_hist.AppendPrometheus("amdgpu_dp_handler_seconds", res(p) + ",method=\"Allocate\"", out);
+    p->stats_.preferred_hist.AppendPrometheus("amdgpu_dp_handler_seconds",
+                                              res(p) + ",method=\"GetPreferredAllocation\"", out);
+  }
+  struct Conn { const Plugin* p; uint64_t connections, errors; };
+  std::vector<Conn> conns;
+  for (auto* p : plugins) {
+    std::lock_guard<std::mutex> lk(p->server_mu_);
+    if (p->server_)
+      conns.push_back({p, p->server_->stats().connections.load(), p->server_->stats().errors.load()});
+  }
+  family("amdgpu_dp_grpc_connections_total", "counter", "Accepted connections on the plugin socket.");
+  for (auto& c : conns) gauge("amdgpu_dp_grpc_connections_total", res(c.p), static_cast<double>(c.connections));
+  family("amdgpu_dp_grpc_errors_total", "counter", "RPCs answered with a non-OK gRPC status.");
+  for (auto& c : conns) gauge("amdgpu_dp_grpc_errors_total", res(c.p), static_cast<double>(c.errors));
 }
 
 }  // namespace adp::plugin

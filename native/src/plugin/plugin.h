@@ -40,6 +40,7 @@
 #include "alloc/topology.h"
 #include "grpc/grpc.h"
 #include "inventory/inventory.h"
+#include "metrics/metrics.h"
 #include "strategy/strategy.h"
 
 namespace adp::plugin {
@@ -101,6 +102,8 @@ struct RpcStats {
   std::atomic<uint64_t> preferred_ns_total{0};
   std::atomic<uint64_t> preferred_ns_max{0};
   std::atomic<uint64_t> law_sends{0};
+  metrics::Histogram allocate_hist;   // handler time (decode + lookup + encode)
+  metrics::Histogram preferred_hist;
 };
 
 class Plugin {
@@ -134,6 +137,10 @@ class Plugin {
 
   const RpcStats& stats() const { return stats_; }
   std::string StatsJson() const;
+  bool registered() const { return registered_.load(); }
+  size_t healthy_count() const;
+  // Prometheus text for a set of plugins (one HELP/TYPE header per family).
+  static void AppendPrometheus(const std::vector<const Plugin*>& plugins, std::string* out);
 
   // Handlers (public for in-process tests and benchmarks; loop thread only when serving).
   Status HandleGetOptions(std::string_view req, std::string* resp);
@@ -174,7 +181,8 @@ class Plugin {
 
   struct LawSnapshot {
     uint64_t version = 0;
-    std::string bytes;  // encoded ListAndWatchResponse
+    std::string bytes;             // encoded ListAndWatchResponse
+    std::vector<uint8_t> healthy;  // per unit, as advertised in `bytes`
   };
   struct LawStream {
     std::shared_ptr<grpc::ServerStream> stream;
@@ -197,6 +205,7 @@ class Plugin {
   mutable std::mutex server_mu_;
   std::unique_ptr<grpc::Server> server_;
   RpcStats stats_;
+  std::atomic<bool> registered_{false};
 };
 
 }  // namespace adp::plugin

@@ -1,0 +1,130 @@
+"""Prometheus /metrics and /healthz endpoint (--metrics-addr).
+
+The reference has no metrics ("Metrics / logging / observability:
+minimal"); this pins the endpoint the DaemonSet's scrape config and liveness
+probe use: device/allocatable/health gauges per resource, per-RPC counters and
+handler-time histograms, restart counter, and /healthz tracking plugin state.
+"""
+
+import os
+import re
+import time
+import urllib.error
+import urllib.request
+
+import pytest
+
+from k8s_gpu_sharing_plugin_amd.models import fixtures
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
+
+
+def _get(port, path):
+    try:
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}{path}", timeout=5) as r:
+            return r.status, r.read().decode()
+    except urllib.error.HTTPError as e:
+        return e.code, e.read().decode()
+
+
+def _parse(text):
+    """{(name, frozenset(labels)): value} for every sample line."""
+    out = {}
+    for line in text.splitlines():
+        if not line or line.startswith("#"):
+            continue
+        m = re.match(r'^([a-zA-Z_:][a-zA-Z0-9_:]*)(?:\{(.*)\})? (\S+)$', line)
+        assert m, f"bad sample line: {line!r}"
+        labels = frozenset(re.findall(r'(\w+)="((?:[^"\\]|\\.)*)"', m.group(2) or ""))
+        out[(m.group(1), labels)] = float(m.group(3))
+    return out
+
+
+def _value(samples, name, **labels):
+    want = set(labels.items())
+    hits = [v for (n, ls), v in samples.items() if n == name and want <= set(ls)]
+    assert len(hits) == 1, (name, labels, hits)
+    return hits[0]
+
+
+@pytest.fixture
+def served(scratch):
+    fx = fixtures.node(2)
+    fifo = os.path.join(scratch + ".fixture", "events")
+    os.makedirs(os.path.dirname(fifo), exist_ok=True)
+    os.mkfifo(fifo)
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fx, args=["--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:sharedgpu:3"],
+                       event_fifo=fifo).start()
+    text = d.wait_log("serving /metrics and /healthz on port")
+    port = int(re.search(r"serving /metrics and /healthz on port (\d+)", text).group(1))
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    yield d, k, c, port, fifo
+    c.close()
+    d.stop()
+    k.stop()
+
+
+def test_metrics_exposition(served):
+    d, k, c, port, _ = served
+    q, call = c.watch()
+    law = q.get(timeout=5)
+    ids = [x.ID for x in law.devices]
+    for _ in range(5):
+        c.allocate([ids[0]])
+    c.preferred(ids, size=2)
+    status, text = _get(port, "/metrics")
+    assert status == 200
+    # Families are grouped: every TYPE line names a family not seen before.
+    types = [l.split()[2] for l in text.splitlines() if l.startswith("# TYPE")]
+    assert len(types) == len(set(types))
+    s = _parse(text)
+    r = "amd.com/sharedgpu"
+    assert _value(s, "amdgpu_dp_devices", resource=r) == 2
+    assert _value(s, "amdgpu_dp_allocatable", resource=r) == 6
+    assert _value(s, "amdgpu_dp_healthy_devices", resource=r) == 2
+    assert _value(s, "amdgpu_dp_registered", resource=r) == 1
+    assert _value(s, "amdgpu_dp_rpc_total", resource=r, method="Allocate") == 5
+    assert _value(s, "amdgpu_dp_rpc_total", resource=r, method="GetPreferredAllocation") == 1
+    assert _value(s, "amdgpu_dp_handler_seconds_count", resource=r, method="Allocate") == 5
+    assert _value(s, "amdgpu_dp_handler_seconds_bucket", resource=r, method="Allocate", le="+Inf") == 5
+    assert _value(s, "amdgpu_dp_handler_seconds_sum", resource=r, method="Allocate") < 0.01
+    assert _value(s, "amdgpu_dp_restarts_total") == 1
+    assert _value(s, "amdgpu_dp_build_info") == 1
+    assert _value(s, "amdgpu_dp_grpc_connections_total", resource=r) >= 2
+    per_dev = [v for (n, ls), v in s.items() if n == "amdgpu_dp_device_healthy"]
+    assert per_dev == [1.0, 1.0]
+    call.cancel()
+
+
+def test_metrics_follow_health_and_healthz(served):
+    d, k, c, port, fifo = served
+    assert _get(port, "/healthz") == (200, "ok\n")
+    fd = os.open(fifo, os.O_WRONLY | os.O_NONBLOCK)
+    os.write(fd, b"1 3 pre-reset\n")
+    os.close(fd)
+    deadline = time.time() + 5
+    while time.time() < deadline:
+        s = _parse(_get(port, "/metrics")[1])
+        if _value(s, "amdgpu_dp_healthy_devices", resource="amd.com/sharedgpu") == 1:
+            break
+        time.sleep(0.05)
+    assert _value(s, "amdgpu_dp_healthy_devices", resource="amd.com/sharedgpu") == 1
+    assert sorted(v for (n, ls), v in s.items() if n == "amdgpu_dp_device_healthy") == [0.0, 1.0]
+    assert _get(port, "/nope")[0] == 404
+    # kubelet goes away and comes back: restart counter moves, healthz stays up after re-registration
+    k.stop()
+    k2 = kubelet.StubKubelet(k.socket_path).start()
+    k2.wait_registration()
+    deadline = time.time() + 5
+    while time.time() < deadline and _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_restarts_total") < 2:
+        time.sleep(0.05)
+    assert _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_restarts_total") == 2
+    assert _get(port, "/healthz")[0] == 200
+    k2.stop()
+
+
+def test_metrics_addr_invalid(scratch):
+    d = harness.Daemon(scratch, args=["--metrics-addr", "nohost:notaport"]).start()
+    assert d.proc.wait(10) == 1
+    assert "invalid --metrics-addr" in d.log()
