@@ -57,7 +57,7 @@ lint:
 	$(PY) -m pyflakes k8s_gpu_sharing_plugin_amd tests 2>/dev/null || true
 
 image:
-	docker build -f deployments/container/Dockerfile -t amdgpu-device-plugin:0.1.0 .
+	$(MAKE) -f deployments/container/Makefile build-ubuntu
 
 clean:
 	rm -rf build

@@ -18,7 +18,10 @@
 //                 "render_minor": 128, "card_minor": 0, "xgmi_links_down": 0 } ] }
 // Runtime injection:
 //   event FIFO lines: "<gpu>[:<partition>] <event-type> [message]"
-//   state_dir files:  gpu<i>.ecc (uncorrectable count), gpu<i>.dead (device gone)
+//   state_dir files:  gpu<i>.ecc (uncorrectable count), gpu<i>.dead (device gone),
+//                     gpu<i>.partition ("CPX NPS2": live partition-mode override)
+//   amdsmi_shut_down + amdsmi_init re-reads the fixture (re-enumeration after a
+//   re-partition).
 #include <amd_smi/amdsmi.h>
 #include <fcntl.h>
 #include <poll.h>
@@ -355,17 +358,27 @@ amdsmi_status_t amdsmi_get_gpu_memory_total(amdsmi_processor_handle h, amdsmi_me
   return AMDSMI_STATUS_SUCCESS;
 }
 
+// state_dir/gpu<i>.partition ("CPX NPS2") overrides the fixture's modes: an
+// operator re-partitioning the GPU behind the daemon's back.
+static bool PartitionOverride(const MockProc* p, std::string* cmode, std::string* mmode) {
+  if (!g || g->state_dir.empty()) return false;
+  std::ifstream f(g->state_dir + "/gpu" + std::to_string(p->gpu) + ".partition");
+  return f && (f >> *cmode >> *mmode);
+}
+
 amdsmi_status_t amdsmi_get_gpu_compute_partition(amdsmi_processor_handle h, char* buf,
                                                  uint32_t len) {
   GET_PROC(h);
-  CopyStr(buf, len, p->cmode);
+  std::string c, m;
+  CopyStr(buf, len, PartitionOverride(p, &c, &m) ? c : p->cmode);
   return AMDSMI_STATUS_SUCCESS;
 }
 
 amdsmi_status_t amdsmi_get_gpu_memory_partition(amdsmi_processor_handle h, char* buf,
                                                 uint32_t len) {
   GET_PROC(h);
-  CopyStr(buf, len, p->mmode);
+  std::string c, m;
+  CopyStr(buf, len, PartitionOverride(p, &c, &m) ? m : p->mmode);
   return AMDSMI_STATUS_SUCCESS;
 }
 

@@ -177,8 +177,9 @@ int RunDaemon(const Config& cfg) {
     inotify_add_watch(ifd, v.popts.plugin_dir.c_str(), IN_DELETE);
   int tfd = timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC | TFD_NONBLOCK);
   int efd = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  int lfd = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);  // health monitor: partition layout changed
   int ep = epoll_create1(EPOLL_CLOEXEC);
-  for (int fd : {sfd, ifd, tfd, efd}) {
+  for (int fd : {sfd, ifd, tfd, efd, lfd}) {
     epoll_event ev{};
     ev.events = EPOLLIN;
     ev.data.fd = fd;
@@ -195,6 +196,9 @@ int RunDaemon(const Config& cfg) {
   int backoff_ms = 1000;
   int exit_code = 0;
   bool quit = false;
+  // Re-initialise amdsmi before the next enumeration (SIGHUP, a detected
+  // re-partition, or a retry): a re-partitioned GPU gets new processor handles.
+  bool reinit = false;
 
   std::unique_ptr<metrics::HttpServer> http;
   if (!cfg.flags.metrics_addr.empty()) {
@@ -249,10 +253,21 @@ int RunDaemon(const Config& cfg) {
   auto restart = [&] {
     stop_all();
     ArmTimer(tfd, 0);  // disarm
+    if (reinit) {
+      Status rs = (*lib)->Reinit();
+      if (!rs.ok()) {
+        LOG_ERROR(kComp, "amdsmi re-initialisation failed: %s", rs.ToString().c_str());
+        schedule_retry("amdsmi re-init failed");
+        return;
+      }
+      reinit = false;
+      LOG_INFO(kComp, "amdsmi re-initialised");
+    }
     LOG_INFO(kComp, "retrieving plugins");
     auto snap = inventory::BuildSnapshot(lib->get(), v.bopts);
     if (!snap.ok()) {
       LOG_ERROR(kComp, "device enumeration failed: %s", snap.status().ToString().c_str());
+      reinit = true;
       schedule_retry("enumeration failed");
       return;
     }
@@ -288,6 +303,11 @@ int RunDaemon(const Config& cfg) {
     serving.store(true);
     if (started == 0) LOG_INFO(kComp, "no devices found; waiting indefinitely");
     monitor = std::make_unique<health::Monitor>(lib->get(), *snap, health::HealthConfig::FromEnv());
+    monitor->SetLayoutListener([lfd](const std::string&) {
+      uint64_t one = 1;
+      ssize_t w = write(lfd, &one, sizeof(one));
+      (void)w;
+    });
     for (auto& p : plugins) {
       plugin::Plugin* raw = p.get();
       monitor->AddListener([raw](int gpu, bool ok, const std::string& why) { raw->SetGpuHealth(gpu, ok, why); });
@@ -321,6 +341,13 @@ int RunDaemon(const Config& cfg) {
         LOG_ERROR(kComp, "a gRPC server exhausted its crash budget; exiting");
         exit_code = 1;
         quit = true;
+      } else if (fd == lfd) {
+        uint64_t x;
+        ssize_t r = read(lfd, &x, sizeof(x));
+        (void)r;
+        LOG_INFO(kComp, "partition layout changed, re-enumerating");
+        reinit = true;
+        do_restart = true;
       } else if (fd == ifd) {
         char buf[4096] __attribute__((aligned(__alignof__(inotify_event))));
         ssize_t len;
@@ -352,6 +379,7 @@ int RunDaemon(const Config& cfg) {
         while (read(sfd, &si, sizeof(si)) == sizeof(si)) {
           if (si.ssi_signo == SIGHUP) {
             LOG_INFO(kComp, "received SIGHUP, restarting");
+            reinit = true;
             do_restart = true;
           } else if (si.ssi_signo == SIGUSR1) {
             // Explicitly requested: printed whatever the log level.
@@ -367,7 +395,7 @@ int RunDaemon(const Config& cfg) {
   }
   stop_all();
   if (http) http->Stop();
-  for (int fd : {ep, sfd, ifd, tfd, efd}) close(fd);
+  for (int fd : {ep, sfd, ifd, tfd, efd, lfd}) close(fd);
   LOG_INFO(kComp, "shutdown complete (exit %d)", exit_code);
   return exit_code;
 }

@@ -4,6 +4,7 @@
 #include <sys/eventfd.h>
 #include <unistd.h>
 
+#include <cctype>
 #include <chrono>
 #include <cstdlib>
 
@@ -139,6 +140,21 @@ void Monitor::Stop() {
 void Monitor::PollOnce() {
   for (const auto& g : snap_->gpus) {
     void* h = snap_->procs[g.partitions.front().handle].handle;
+    if (layout_listener_ && !layout_changed_) {
+      auto [compute, memory] = lib_->PartitionModes(h);
+      for (auto& c : compute) c = static_cast<char>(toupper(static_cast<unsigned char>(c)));
+      for (auto& c : memory) c = static_cast<char>(toupper(static_cast<unsigned char>(c)));
+      bool changed = (!compute.empty() && compute != g.reported_compute) ||
+                     (!memory.empty() && memory != g.reported_memory);
+      if (changed) {
+        layout_changed_ = true;
+        std::string why = "GPU " + g.bdf + " partition mode changed " + g.reported_compute + "/" +
+                          g.reported_memory + " -> " + compute + "/" + memory;
+        LOG_WARN(kComp, "%s", why.c_str());
+        layout_listener_(why);
+        return;  // handles are about to be re-created; no health verdicts from them
+      }
+    }
     bool alive = lib_->Responsive(h);
     if (!alive && !unresponsive_[g.index]) {
       unresponsive_[g.index] = 1;

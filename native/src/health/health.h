@@ -60,6 +60,10 @@ class Monitor {
   Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> snap, HealthConfig cfg);
   ~Monitor();
   void AddListener(Listener l);
+  // Called once (from the monitor thread) when polling sees a GPU whose compute
+  // or memory partition mode differs from the snapshot: the node was
+  // re-partitioned and must be re-enumerated.
+  void SetLayoutListener(std::function<void(const std::string& why)> l) { layout_listener_ = std::move(l); }
   Status Start();
   void Stop();
   bool events_enabled() const { return events_ok_; }
@@ -81,6 +85,8 @@ class Monitor {
   bool events_ok_ = false;
   std::thread thread_;
   std::atomic<bool> stop_{false};
+  std::function<void(const std::string&)> layout_listener_;
+  bool layout_changed_ = false;
   int wake_fd_ = -1;  // eventfd: Stop() wakes the idle wait at once
   void Sleep(int ms);
   // Per-GPU polling state.

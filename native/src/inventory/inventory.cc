@@ -95,9 +95,11 @@ Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo
     g.bdf = smi::FormatBdf(first.bdf_id & ~uint64_t{7});
     g.numa = first.numa_node;
     g.market_name = first.market_name;
-    g.compute_mode = Upper(first.compute_partition);
+    g.reported_compute = Upper(first.compute_partition);
+    g.reported_memory = Upper(first.memory_partition);
+    g.compute_mode = g.reported_compute;
     if (g.compute_mode.empty()) g.compute_mode = ModeForCount(handles.size());
-    g.memory_mode = Upper(first.memory_partition);
+    g.memory_mode = g.reported_memory;
 
     // Partition IDs must be unique and stable across restarts: the handle UUID
     // when amdsmi reports distinct ones, else "<uuid>-p<partition>".

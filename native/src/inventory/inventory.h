@@ -55,6 +55,10 @@ struct PhysicalGpu {
   uint32_t cus = 0;
   std::string compute_mode;       // SPX / DPX / TPX / QPX / CPX ("SPX" if unknown)
   std::string memory_mode;        // NPS1 / NPS2 / ... ("" if unknown)
+  // The modes exactly as amdsmi reported them at enumeration (upper-cased; ""
+  // if not reported): the health monitor compares live queries against these
+  // to detect re-partitioning.
+  std::string reported_compute, reported_memory;
   std::string market_name;
   std::vector<Partition> partitions;  // one per amdsmi handle; sorted by partition_id
   int xgmi_links_down = 0;

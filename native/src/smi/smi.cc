@@ -308,6 +308,33 @@ Result<uint64_t> Library::UncorrectableErrors(void* h) {
   return static_cast<uint64_t>(ec.uncorrectable_count);
 }
 
+std::pair<std::string, std::string> Library::PartitionModes(void* h) {
+  std::pair<std::string, std::string> out;
+  char buf[64];
+  if (f_->compute_partition) {
+    memset(buf, 0, sizeof(buf));
+    if (f_->compute_partition(h, buf, sizeof(buf) - 1) == AMDSMI_STATUS_SUCCESS) out.first = buf;
+  }
+  if (f_->memory_partition) {
+    memset(buf, 0, sizeof(buf));
+    if (f_->memory_partition(h, buf, sizeof(buf) - 1) == AMDSMI_STATUS_SUCCESS) out.second = buf;
+  }
+  return out;
+}
+
+Status Library::Reinit() {
+  if (initialized_) f_->shut_down();
+  initialized_ = false;
+  amdsmi_status_t st = f_->init(AMDSMI_INIT_AMD_GPUS);
+  if (st != AMDSMI_STATUS_SUCCESS) {
+    const char* s = nullptr;
+    if (f_->status_string) f_->status_string(st, &s);
+    return Unavailable("amdsmi_init failed: " + std::string(s ? s : std::to_string(st)));
+  }
+  initialized_ = true;
+  return Status::Ok();
+}
+
 bool Library::Responsive(void* h) {
   char uuid[AMDSMI_GPU_UUID_SIZE + 16] = {0};
   unsigned int ulen = sizeof(uuid);

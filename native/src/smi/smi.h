@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "common/status.h"
@@ -95,6 +96,15 @@ class Library {
   // RAS polling (fallback health when events are unavailable).
   Result<uint64_t> UncorrectableErrors(void* h);
   bool Responsive(void* h);
+
+  // Current compute/memory partition mode of a processor, e.g. {"CPX", "NPS2"}
+  // (empty strings when the query is unavailable).
+  std::pair<std::string, std::string> PartitionModes(void* h);
+
+  // amdsmi_shut_down + amdsmi_init: picks up a changed partition layout (the
+  // driver re-creates processors when a GPU is re-partitioned). Invalidates all
+  // handles; callers must have stopped every user of the old ones.
+  Status Reinit();
 
  private:
   Library() = default;

@@ -86,3 +86,24 @@ def test_example_pods_request_amd_resources():
                 assert r.startswith("amd.com/"), (path, r)
                 seen.add(r)
     assert {"amd.com/gpu", "amd.com/sharedgpu", "amd.com/gpu-mem-gb", "amd.com/cpx-1xcd.36gb"} <= seen
+
+
+def test_release_versions_agree():
+    """RELEASE.md step 1: every place that carries the version says the same."""
+    import glob
+    import re
+    import k8s_gpu_sharing_plugin_amd as pkg
+    root = pkg.REPO_ROOT
+
+    def read(p):
+        with open(os.path.join(root, p)) as f:
+            return f.read()
+    version = re.search(r"^VERSION\s*\?=\s*(\S+)", read("versions.mk"), re.M).group(1)
+    assert pkg.__version__ == version
+    assert f'set(ADP_VERSION "{version}"' in read("native/CMakeLists.txt")
+    chart = read("deployments/helm/amd-gpu-device-plugin/Chart.yaml")
+    assert f'version: "{version}"' in chart and f'appVersion: "{version}"' in chart
+    for m in ["amd-gpu-device-plugin.yml", *glob.glob(os.path.join(root, "deployments/static/*.yml"))]:
+        assert f"amdgpu-device-plugin:{version}" in read(m), m
+    for d in ("ubuntu", "ubi9"):
+        assert "ENTRYPOINT" in read(f"deployments/container/Dockerfile.{d}")

@@ -124,3 +124,5 @@ def test_health_monitor_starts_on_real_gpu(scratch, snap):
         k.stop()
     log = d.log()
     assert ("event notification unavailable" in log) or ("health checks disabled" not in log)
+    # live partition-mode queries agree with the enumeration: no spurious re-partition restarts
+    assert "partition mode changed" not in log and "amdsmi re-initialised" not in log

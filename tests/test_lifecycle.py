@@ -215,3 +215,37 @@ def test_sigusr1_dumps_stats(scratch):
     c.close()
     assert d.stop() == 0
     k.stop()
+
+
+def test_repartition_is_detected_and_reenumerated(scratch):
+    """An operator re-partitions GPU 0 (SPX/NPS1 -> CPX/NPS2) under the running
+    daemon: polling sees the mode change, amdsmi is re-initialised, the node is
+    re-enumerated and the new partition resource registers (the reference needs a
+    manual restart after MIG reconfiguration)."""
+    fixture_dir = scratch + ".fixture"
+    state = os.path.join(fixture_dir, "state")
+    os.makedirs(state, exist_ok=True)
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(2), args=["--partition-strategy", "mixed"], state_dir=state,
+                       env={"DP_HEALTH_POLL_MS": "100"}).start()
+    try:
+        assert k.wait_registration().resource_name == "amd.com/gpu"
+        fx = fixtures.node(2, ["CPX", "SPX"], memory="NPS2")
+        fx["state_dir"] = state
+        fixtures.write(fx, fixture_dir)
+        with open(os.path.join(state, "gpu0.partition"), "w") as f:
+            f.write("CPX NPS2\n")
+        names = {k.wait_registration(10).resource_name for _ in range(2)}
+        assert "amd.com/gpu" in names
+        part = [n for n in names if n != "amd.com/gpu"]
+        assert len(part) == 1 and part[0].startswith("amd.com/cpx-1xcd."), names
+        log = d.wait_log("amdsmi re-initialised")
+        assert "partition mode changed SPX/NPS1 -> CPX/NPS2" in log
+        c = kubelet.PluginClient(os.path.join(scratch, "amd-" + part[0].split("/")[1] + ".sock"))
+        assert len(c.watch()[0].get(timeout=5).devices) == 8
+        c.close()
+        time.sleep(0.5)  # several poll periods: no second re-enumeration
+        assert d.log().count("amdsmi re-initialised") == 1
+    finally:
+        assert d.stop() == 0
+        k.stop()
