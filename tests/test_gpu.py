@@ -126,3 +126,25 @@ def test_health_monitor_starts_on_real_gpu(scratch, snap):
     assert ("event notification unavailable" in log) or ("health checks disabled" not in log)
     # live partition-mode queries agree with the enumeration: no spurious re-partition restarts
     assert "partition mode changed" not in log and "amdsmi re-initialised" not in log
+
+
+def test_metrics_endpoint_on_real_gpu(scratch, snap):
+    import re
+    import urllib.request
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--metrics-addr", "127.0.0.1:0"]).start()
+    try:
+        text = d.wait_log("serving /metrics and /healthz on port", 30)
+        port = int(re.search(r"on port (\d+)", text).group(1))
+        k.wait_registration(30)
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=5) as r:
+            assert r.status == 200
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
+            body = r.read().decode()
+        g = snap["gpus"][0]
+        assert f'amdgpu_dp_device_healthy{{resource="amd.com/gpu",device="{g["uuid"]}"' in body
+        assert 'amdgpu_dp_allocatable{resource="amd.com/gpu"} 1' in body
+        assert 'amdgpu_dp_build_info{version=' in body
+    finally:
+        assert d.stop() == 0
+        k.stop()
