@@ -107,6 +107,10 @@ const std::vector<FlagDef>& Table() {
       {"server-threads", "DP_SERVER_THREADS", "serverThreads", Kind::kUint,
        "gRPC loop threads per plugin socket (0 = min(8, CPUs))",
        [](Flags& f) -> void* { return &f.server_threads; }, true},
+      {"busy-poll-us", "DP_BUSY_POLL_US", "busyPollUs", Kind::kUint,
+       "after serving a request a gRPC loop polls without sleeping for this many "
+       "microseconds, so follow-up calls skip a scheduler wake-up (0 = always sleep)",
+       [](Flags& f) -> void* { return &f.busy_poll_us; }, true},
       {"metrics-addr", "DP_METRICS_ADDR", "metricsAddr", Kind::kString,
        "serve Prometheus /metrics and /healthz on this TCP address, e.g. ':9400' (empty = off)",
        [](Flags& f) -> void* { return &f.metrics_addr; }},

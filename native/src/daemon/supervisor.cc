@@ -64,6 +64,7 @@ Result<Validated> Validate(const Config& cfg) {
   v.popts.auto_replica_unit_mib = f.auto_replica_unit_mib;
   v.popts.server_threads = static_cast<int>(std::min<uint64_t>(f.server_threads, 64));
   v.popts.trace = f.trace;
+  v.popts.busy_poll_us = static_cast<int>(std::min<uint64_t>(f.busy_poll_us, 100000));
   v.popts.cdi_spec_dir = f.cdi_spec_dir;
   v.bopts.driver_root = f.driver_root;
   v.bopts.include_card_nodes = f.include_card_nodes;

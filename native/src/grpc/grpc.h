@@ -129,6 +129,8 @@ class Server {
   const ServerStats& stats() const { return stats_; }
   // Log every unary call (method, status, sizes, handler time). Set before Start().
   void set_trace(bool on) { trace_ = on; }
+  // Keep polling (no sleep) for this long after each burst of activity. Set before Start().
+  void set_busy_poll_us(int us) { busy_poll_us_ = us < 0 ? 0 : us; }
 
   // Test hook: make the next iteration of loop 0 fail as if epoll_wait errored.
   void InjectLoopFailureForTest() { inject_failure_.store(true); }
@@ -158,6 +160,7 @@ class Server {
   std::function<void()> on_fatal_;
   std::atomic<uint64_t> next_stream_id_{1};
   bool trace_ = false;
+  int busy_poll_us_ = 0;
   ServerStats stats_;
 };
 

@@ -584,12 +584,28 @@ void Server::CloseConn(Loop& l, int fd) {
 
 Status Server::RunLoop(Loop& l) {
   epoll_event events[64];
+  // Adaptive busy-poll: after serving a request, keep polling without sleeping
+  // for busy_poll_us_ so the kubelet's follow-up call (Allocate after
+  // GetPreferredAllocation, the next pod of a burst) does not pay a scheduler
+  // wake-up. An idle loop blocks in epoll_wait as usual (no CPU when idle).
+  using Clock = std::chrono::steady_clock;
+  const auto spin = std::chrono::microseconds(busy_poll_us_);
+  Clock::time_point spin_until{};
+  bool spinning = false;
   while (!stopping_.load()) {
-    int n = epoll_wait(l.epoll_fd, events, 64, -1);
+    int n = epoll_wait(l.epoll_fd, events, 64, spinning ? 0 : -1);
     if (l.index == 0 && inject_failure_.exchange(false)) return Internal("injected loop failure");
     if (n < 0) {
       if (errno == EINTR) continue;
       return Internal(std::string("epoll_wait: ") + strerror(errno));
+    }
+    if (n == 0) {
+      if (spinning && Clock::now() >= spin_until) spinning = false;
+      continue;
+    }
+    if (busy_poll_us_ > 0) {
+      spinning = true;
+      spin_until = Clock::now() + spin;
     }
     for (int i = 0; i < n; ++i) {
       int fd = events[i].data.fd;

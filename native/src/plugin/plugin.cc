@@ -357,6 +357,7 @@ Status Plugin::Start(std::function<void()> on_fatal) {
   auto srv = std::make_unique<grpc::Server>(spec_.resource_name, threads);
   law_streams_.assign(threads, {});
   srv->set_trace(opts_.trace);
+  srv->set_busy_poll_us(opts_.busy_poll_us);
   srv->AddUnary(std::string(kSvc) + "GetDevicePluginOptions",
                 [this](std::string_view q, std::string* r) { return HandleGetOptions(q, r); });
   srv->AddUnary(std::string(kSvc) + "Allocate",

@@ -73,6 +73,7 @@ struct PluginOptions {
   bool trace = false;                     // log every RPC with its handler time
   std::string cdi_spec_dir = "/var/run/cdi";  // where cdi-* strategies write the CDI spec
   int server_threads = 0;                 // gRPC loops; <=0 -> DefaultServerThreads()
+  int busy_poll_us = 50;                  // loop keeps polling this long after activity
 };
 
 // min(8, online CPUs): one loop per GPU of an 8-GPU node. Idle loops sit in

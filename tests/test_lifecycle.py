@@ -249,3 +249,31 @@ def test_repartition_is_detected_and_reenumerated(scratch):
     finally:
         assert d.stop() == 0
         k.stop()
+
+
+def _cpu_seconds(pid):
+    with open(f"/proc/{pid}/stat") as f:
+        fields = f.read().rsplit(")", 1)[1].split()
+    return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")  # utime + stime
+
+
+def test_idle_daemon_uses_no_cpu(scratch):
+    """Busy-polling only follows activity: an idle daemon (after a burst of RPCs)
+    sleeps in epoll_wait and burns no CPU."""
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(8), args=["--busy-poll-us", "1000"]).start()
+    try:
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        law = c.watch()[0].get(timeout=5)
+        for x in law.devices:
+            c.allocate([x.ID])
+        time.sleep(0.2)
+        before = _cpu_seconds(d.proc.pid)
+        time.sleep(2.0)
+        used = _cpu_seconds(d.proc.pid) - before
+        assert used < 0.1, f"idle daemon used {used:.2f} CPU-s in 2 s"
+        c.close()
+    finally:
+        assert d.stop() == 0
+        k.stop()

@@ -7,7 +7,7 @@ per-concurrency p50/p99 Allocate latency and aggregate pods/s. This is the load
 shape of the driver's multi-GPU bench (one client per GPU rank against one
 daemon) and shows what the multi-loop server buys.
 
-  python tools/concurrency.py [--gpus 8] [--pods 4000] [--server-threads 0]
+  python tools/concurrency.py [--gpus 8] [--pods 4000] [--server-threads 0] [--busy-poll-us N]
 """
 
 import argparse
@@ -29,14 +29,17 @@ def main():
     ap.add_argument("--pods", type=int, default=4000)
     ap.add_argument("--clients", default="1,2,4,8")
     ap.add_argument("--server-threads", type=int, default=0)
+    ap.add_argument("--busy-poll-us", type=int, default=None)
     a = ap.parse_args()
     d = harness.scratch_dir("adpconc")
     k = harness.NativeKubelet(os.path.join(d, "kubelet.sock")).start()
     args = ["--server-threads", str(a.server_threads)] if a.server_threads else []
+    if a.busy_poll_us is not None:
+        args += ["--busy-poll-us", str(a.busy_poll_us)]
     dm = harness.Daemon(d, fixtures.node(a.gpus), args=args,
                         env={"ADP_LOG_LEVEL": "warn", "DP_HEALTH_POLL_MS": "0"}).start()
     out = {"gpus": a.gpus, "pods_per_client": a.pods, "server_threads": a.server_threads or "default",
-           "runs": []}
+           "busy_poll_us": "default" if a.busy_poll_us is None else a.busy_poll_us, "runs": []}
     try:
         reg = k.wait(lambda e: e.get("event") == "register", 20)
         sock = os.path.join(d, reg["endpoint"])
