@@ -3,6 +3,7 @@
 #include <cstdio>
 
 #include "common/log.h"
+#include "common/sampler.h"
 #include "daemon/config.h"
 #include "daemon/supervisor.h"
 
@@ -28,5 +29,8 @@ int main(int argc, char** argv) {
   }
   LOG_INFO("main", "amdgpu-device-plugin %s", ADP_VERSION);
   for (const auto& d : cfg->deprecations) LOG_WARN("main", "%s", d.c_str());
-  return adp::daemon::RunDaemon(*cfg);
+  bool profiling = adp::StartSamplerFromEnv();
+  int rc = adp::daemon::RunDaemon(*cfg);
+  if (profiling) adp::StopSamplerAndReport();
+  return rc;
 }

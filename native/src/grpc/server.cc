@@ -177,7 +177,13 @@ bool ServerConn::Init() {
   nghttp2_session_callbacks_set_on_data_chunk_recv_callback(cbs, OnDataChunk);
   nghttp2_session_callbacks_set_on_frame_recv_callback(cbs, OnFrameRecv);
   nghttp2_session_callbacks_set_on_stream_close_callback(cbs, OnStreamCloseCb);
-  int rv = nghttp2_session_server_new(&session_, cbs, this);
+  // Closed streams are not retained for the RFC 7540 priority tree (gRPC never
+  // uses priorities); keeping them roughly doubles nghttp2's per-call cost.
+  nghttp2_option* opt;
+  nghttp2_option_new(&opt);
+  nghttp2_option_set_no_closed_streams(opt, 1);
+  int rv = nghttp2_session_server_new2(&session_, cbs, this, opt);
+  nghttp2_option_del(opt);
   nghttp2_session_callbacks_del(cbs);
   if (rv != 0) return false;
   nghttp2_settings_entry iv[] = {

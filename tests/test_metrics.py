@@ -128,3 +128,23 @@ def test_metrics_addr_invalid(scratch):
     d = harness.Daemon(scratch, args=["--metrics-addr", "nohost:notaport"]).start()
     assert d.proc.wait(10) == 1
     assert "invalid --metrics-addr" in d.log()
+
+
+def test_builtin_sampler_writes_profile(scratch):
+    """ADP_PROFILE_OUT: the daemon's own CPU sampler reports where its time went."""
+    out = os.path.join(scratch + ".fixture", "profile.txt")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, env={"ADP_PROFILE_OUT": out, "ADP_PROFILE_HZ": "2000"}).start()
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    deadline = time.time() + 1.0
+    while time.time() < deadline:
+        c.allocate([ids[0]])
+    c.close()
+    assert d.stop() == 0
+    k.stop()
+    text = open(out).read()
+    assert text.startswith("samples ")
+    assert "== by shared object ==" in text and "== by symbol ==" in text
