@@ -75,6 +75,7 @@ std::string Plugin::socket_path() const { return PathJoin(opts_.plugin_dir, spec
 void Plugin::BuildUnits() {
   const auto& v = spec_.variant;
   replicated_ = v.replicas > 1 || v.auto_replicas;
+  memory_units_ = v.auto_replicas;
   for (const auto& ref : spec_.devices) {
     const auto& g = snap_->gpus[ref.gpu];
     Unit u;
@@ -216,7 +217,7 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
   uint64_t t0 = NowNs();
   std::vector<std::vector<std::string_view>> containers;
   ADP_RETURN_IF_ERROR(pb::DecodeView(req, &containers));
-  std::vector<int> us;
+  std::vector<int> us, units_per;
   std::string c, joined;
   for (const auto& ids : containers) {
     us.clear();
@@ -230,6 +231,11 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
     // Unique physical devices. uuid strategy: sorted by ID (stripReplicas order,
     // server.go:325); index strategy: enumeration order (server.go:406-411).
     std::sort(us.begin(), us.end());
+    if (memory_units_) {
+      // Memory units granted per device (us is sorted, so runs are contiguous).
+      units_per.assign(units_.size(), 0);
+      for (int u : us) ++units_per[u];
+    }
     us.erase(std::unique(us.begin(), us.end()), us.end());
     if (opts_.id_strategy == DeviceIdStrategy::kUuid)
       std::sort(us.begin(), us.end(), [&](int a, int b) { return units_[a].id < units_[b].id; });
@@ -265,6 +271,24 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
           pb::PutLen(&c, 5, n);
         }
         break;
+    }
+    if (memory_units_ && !us.empty()) {
+      // Memory-unit resources (replicas = -1): tell the container how much HBM it
+      // was granted on each device, in AMD_VISIBLE_DEVICES order, so frameworks
+      // can cap themselves (e.g. torch.cuda.set_per_process_memory_fraction).
+      // The reference hands out memory units without telling the workload.
+      std::string mib, frac;
+      char buf[32];
+      for (size_t i = 0; i < us.size(); ++i) {
+        const Unit& u = units_[us[i]];
+        uint64_t granted = static_cast<uint64_t>(units_per[us[i]]) * opts_.auto_replica_unit_mib;
+        if (i) { mib += ','; frac += ','; }
+        mib += std::to_string(granted);
+        snprintf(buf, sizeof(buf), "%.4f", u.vram_mib ? std::min(1.0, double(granted) / u.vram_mib) : 0.0);
+        frac += buf;
+      }
+      pb::PutMapEntry(&c, 1, kMemoryLimitEnv, mib);
+      pb::PutMapEntry(&c, 1, kMemoryFractionEnv, frac);
     }
     if (opts_.pass_device_specs) {
       c += kfd_spec_bytes_;

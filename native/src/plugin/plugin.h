@@ -57,6 +57,10 @@ inline constexpr const char* kVisibleDevicesEnv = "AMD_VISIBLE_DEVICES";
 inline constexpr const char* kVolumeMountHostPath = "/dev/null";
 inline constexpr const char* kVolumeMountRoot = "/var/run/amd-container-devices";
 inline constexpr const char* kCdiVendorClass = "amd.com/gpu";
+// Set on Allocate for memory-unit resources: MiB granted per allocated device and
+// that share of the device's HBM, comma separated in AMD_VISIBLE_DEVICES order.
+inline constexpr const char* kMemoryLimitEnv = "AMD_GPU_MEMORY_LIMIT_MIB";
+inline constexpr const char* kMemoryFractionEnv = "AMD_GPU_MEMORY_FRACTION";
 
 struct PluginOptions {
   std::string plugin_dir = kDefaultPluginDir;
@@ -170,6 +174,7 @@ class Plugin {
   strategy::PluginSpec spec_;
   PluginOptions opts_;
   bool replicated_ = false;
+  bool memory_units_ = false;  // auto replicas: one ID per auto_replica_unit_mib of HBM
 
   std::vector<Unit> units_;
   std::unordered_map<std::string, int> unit_by_id_;

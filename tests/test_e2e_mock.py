@@ -162,3 +162,34 @@ def test_native_stub_kubelet_sees_devices(scratch):
     finally:
         assert d.stop() == 0
         k.stop()
+
+
+def test_memory_units_report_granted_hbm(running, scratch):
+    """gpu-mem-gb (replicas=-1): the container learns how much HBM it was granted
+    per device, in AMD_VISIBLE_DEVICES order; plain and time-slice resources do not."""
+    d, k = running(args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack"])
+    reg = k.wait_registration()
+    assert reg.resource_name == "amd.com/gpu-mem-gb"
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    assert len(ids) == 2 * 294
+    gpu0 = [i for i in ids if i.startswith(ids[0].split("-replica-")[0])]
+    gpu1 = [i for i in ids if i not in gpu0]
+    envs = dict(c.allocate(gpu0[:36]).container_responses[0].envs)
+    assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "36000"
+    assert envs["AMD_GPU_MEMORY_FRACTION"] == f"{36000 / 294896:.4f}"
+    envs = dict(c.allocate(gpu1[:2] + gpu0[:3]).container_responses[0].envs)
+    order = envs["AMD_VISIBLE_DEVICES"].split(",")
+    want = {gpu0[0].split("-replica-")[0]: "3000", gpu1[0].split("-replica-")[0]: "2000"}
+    assert envs["AMD_GPU_MEMORY_LIMIT_MIB"].split(",") == [want[u] for u in order]
+    c.close()
+
+
+def test_time_slice_replicas_carry_no_memory_envs(running, scratch):
+    d, k = running(args=["--resource-config", "gpu:sharedgpu:4"])
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    envs = dict(c.allocate(ids[:2]).container_responses[0].envs)
+    assert "AMD_GPU_MEMORY_LIMIT_MIB" not in envs
+    c.close()
