@@ -64,8 +64,29 @@ __global__ void __launch_bounds__(256) FillKernel(uint4* p, size_t n) {
 }
 
 // Tunable streaming copy for the bandwidth sweep: UNROLL independent 16-byte
-// loads in flight per lane, optional non-temporal (streaming) stores.
-template <int UNROLL, bool NT>
+// loads in flight per lane, optional non-temporal (streaming) loads / stores.
+template <bool NT>
+__device__ __forceinline__ uint4 Load16(const uint4* p) {
+  if (!NT) return *p;
+  uint4 v;
+  v.x = __builtin_nontemporal_load(&p->x);
+  v.y = __builtin_nontemporal_load(&p->y);
+  v.z = __builtin_nontemporal_load(&p->z);
+  v.w = __builtin_nontemporal_load(&p->w);
+  return v;
+}
+
+template <bool NT>
+__device__ __forceinline__ void Store16(uint4* p, const uint4& v) {
+  if (!NT) { *p = v; return; }
+  __builtin_nontemporal_store(v.x, &p->x);
+  __builtin_nontemporal_store(v.y, &p->y);
+  __builtin_nontemporal_store(v.z, &p->z);
+  __builtin_nontemporal_store(v.w, &p->w);
+}
+
+// Grid-stride form: consecutive workgroups touch adjacent 4 KiB slices.
+template <int UNROLL, bool NT, bool NTL = false>
 __global__ void __launch_bounds__(256) CopyKernelT(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                                    size_t n) {
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
@@ -73,20 +94,31 @@ __global__ void __launch_bounds__(256) CopyKernelT(const uint4* __restrict__ src
   for (; i + (UNROLL - 1) * stride < n; i += UNROLL * stride) {
     uint4 v[UNROLL];
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) v[u] = src[i + u * stride];
+    for (int u = 0; u < UNROLL; ++u) v[u] = Load16<NTL>(&src[i + u * stride]);
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      if (NT) {
-        __builtin_nontemporal_store(v[u].x, &dst[i + u * stride].x);
-        __builtin_nontemporal_store(v[u].y, &dst[i + u * stride].y);
-        __builtin_nontemporal_store(v[u].z, &dst[i + u * stride].z);
-        __builtin_nontemporal_store(v[u].w, &dst[i + u * stride].w);
-      } else {
-        dst[i + u * stride] = v[u];
-      }
-    }
+    for (int u = 0; u < UNROLL; ++u) Store16<NT>(&dst[i + u * stride], v[u]);
   }
   for (; i < n; i += stride) dst[i] = src[i];
+}
+
+// Chunked form: each workgroup streams one contiguous chunk of the buffer
+// (long DRAM-page runs per workgroup instead of a chip-wide interleave).
+template <int UNROLL, bool NT, bool NTL = false>
+__global__ void __launch_bounds__(256) CopyChunkT(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                  size_t n) {
+  const size_t step = static_cast<size_t>(blockDim.x) * UNROLL;
+  const size_t per = ((n + gridDim.x - 1) / gridDim.x + step - 1) / step * step;
+  const size_t begin = per * blockIdx.x;
+  const size_t end = begin + per < n ? begin + per : n;
+  size_t i = begin + threadIdx.x;
+  for (; i + (UNROLL - 1) * blockDim.x < end; i += step) {
+    uint4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = Load16<NTL>(&src[i + u * blockDim.x]);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) Store16<NT>(&dst[i + u * blockDim.x], v[u]);
+  }
+  for (; i < end; i += blockDim.x) dst[i] = src[i];
 }
 
 __global__ void __launch_bounds__(256) SumKernel(const uint4* __restrict__ p, size_t n,
@@ -139,14 +171,18 @@ extern "C" int adp_probe_bw_sweep(int device, unsigned long long bytes, int iter
   HIP_TRY(hipEventCreate(&e1));
   using Launch = void (*)(dim3, const uint4*, uint4*, size_t);
   struct Variant { const char* name; Launch fn; };
-#define V(U, NT) {#U "x" #NT, [](dim3 g, const uint4* s, uint4* d, size_t m) { \
-    hipLaunchKernelGGL((CopyKernelT<U, NT>), g, dim3(256), 0, 0, s, d, m); }}
-  Variant variants[] = {V(1, false), V(2, false), V(4, false), V(8, false),
-                        V(1, true),  V(2, true),  V(4, true),  V(8, true)};
+#define V(K, U, NT, NTL) {#K "-" #U "x-st" #NT "-ld" #NTL, [](dim3 g, const uint4* s, uint4* d, size_t m) { \
+    hipLaunchKernelGGL((K<U, NT, NTL>), g, dim3(256), 0, 0, s, d, m); }}
+  Variant variants[] = {
+      V(CopyKernelT, 1, false, false), V(CopyKernelT, 2, false, false), V(CopyKernelT, 4, false, false),
+      V(CopyKernelT, 2, true, false),  V(CopyKernelT, 4, true, false),  V(CopyKernelT, 8, true, false),
+      V(CopyKernelT, 2, true, true),   V(CopyKernelT, 4, true, true),
+      V(CopyChunkT, 2, true, false),   V(CopyChunkT, 4, true, false),   V(CopyChunkT, 8, true, false),
+      V(CopyChunkT, 4, true, true),    V(CopyChunkT, 4, false, false)};
 #undef V
   std::string s = "[";
   bool first = true;
-  for (int bpc : {2, 4, 8, 16}) {
+  for (int bpc : {1, 2, 4, 8}) {
     for (const auto& var : variants) {
       dim3 grid(cus * bpc);
       var.fn(grid, src, dst, n);  // warm-up
@@ -157,7 +193,7 @@ extern "C" int adp_probe_bw_sweep(int device, unsigned long long bytes, int iter
       float ms = 0;
       HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
       double gbps = (2.0 * n * sizeof(uint4) * iters) / (ms * 1e-3) / 1e9;
-      char buf[160];
+      char buf[192];
       snprintf(buf, sizeof(buf), "%s{\"blocks_per_cu\": %d, \"variant\": \"%s\", \"gbps\": %.1f}",
                first ? "" : ", ", bpc, var.name, gbps);
       s += buf;
@@ -230,19 +266,20 @@ extern "C" int adp_probe_run(int device, unsigned long long bytes, int iters, ch
   HIP_TRY(hipMalloc(&dst, n * sizeof(uint4)));
   HIP_TRY(hipMalloc(&d_sum, sizeof(unsigned long long)));
   const int blocks = cus * 8;
-  // Copy shape picked by adp_probe_bw_sweep on MI355X (profiles/probe_bw_sweep_r1.json):
-  // 2 workgroups/CU, 2 x 16 B loads in flight per lane, non-temporal stores:
-  // 5.72 TB/s vs 4.63 TB/s for the first-cut 8 WG/CU shape.
-  const int copy_blocks = cus * 2;
+  // Copy shape picked by adp_probe_bw_sweep on MI355X (profiles/r1/session7/sweep_*.json):
+  // 1 workgroup/CU, 4 x 16 B loads in flight per lane, non-temporal loads and
+  // stores: 6.27 TB/s on 2 GiB (the ~6.3 TB/s achievable of an 8 TB/s part) vs
+  // 5.90 TB/s for 2 WG/CU x2 with plain loads and 4.63 TB/s for the first cut.
+  const int copy_blocks = cus;
   hipLaunchKernelGGL(FillKernel, dim3(blocks), dim3(256), 0, 0, src, n);
-  hipLaunchKernelGGL((CopyKernelT<2, true>), dim3(copy_blocks), dim3(256), 0, 0, src, dst, n);  // warm-up
+  hipLaunchKernelGGL((CopyKernelT<4, true, true>), dim3(copy_blocks), dim3(256), 0, 0, src, dst, n);  // warm-up
   HIP_TRY(hipGetLastError());
   hipEvent_t e0, e1;
   HIP_TRY(hipEventCreate(&e0));
   HIP_TRY(hipEventCreate(&e1));
   HIP_TRY(hipEventRecord(e0, 0));
   for (int i = 0; i < iters; ++i)
-    hipLaunchKernelGGL((CopyKernelT<2, true>), dim3(copy_blocks), dim3(256), 0, 0, src, dst, n);
+    hipLaunchKernelGGL((CopyKernelT<4, true, true>), dim3(copy_blocks), dim3(256), 0, 0, src, dst, n);
   HIP_TRY(hipEventRecord(e1, 0));
   HIP_TRY(hipEventSynchronize(e1));
   float ms = 0;

@@ -148,3 +148,38 @@ def test_metrics_endpoint_on_real_gpu(scratch, snap):
     finally:
         assert d.stop() == 0
         k.stop()
+
+
+def test_memory_unit_grant_caps_pytorch(scratch, snap):
+    """gpu-mem-gb on the real MI355X: the granted share from Allocate() caps a
+    PyTorch allocator -- inside the grant succeeds, beyond it is refused."""
+    import subprocess
+    import sys
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--resource-config", "gpu:gpu-mem-gb:-1",
+                                                     "--replica-policy", "pack"]).start()
+    try:
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=10).devices]
+        assert len(ids) == snap["gpus"][0]["vram_mib"] // 1000
+        envs = dict(c.allocate(ids[:8]).container_responses[0].envs)
+        c.close()
+    finally:
+        assert d.stop() == 0
+        k.stop()
+    assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "8000"
+    code = (
+        "import os, torch\n"
+        "f = float(os.environ['AMD_GPU_MEMORY_FRACTION'])\n"
+        "torch.cuda.set_per_process_memory_fraction(f, 0)\n"
+        "x = torch.empty(6000 << 20, dtype=torch.uint8, device='cuda')\n"
+        "try:\n"
+        "    y = torch.empty(4000 << 20, dtype=torch.uint8, device='cuda')\n"
+        "    print('NOT CAPPED')\n"
+        "except torch.OutOfMemoryError:\n"
+        "    print('CAPPED')\n")
+    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **envs}, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().endswith("CAPPED") and "NOT" not in r.stdout
