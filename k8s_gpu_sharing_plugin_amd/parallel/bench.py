@@ -94,10 +94,13 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
     have_gpu = torch is not None and torch.cuda.is_available()
     real = have_gpu and not force_mock
     if world > 1:
-        backend = "nccl" if have_gpu else "gloo"
-        if have_gpu:
+        # RCCL between GPU ranks; gloo when the run is on the mock (no GPU, or
+        # --mock on a GPU box: then no rank touches the device at all).
+        backend = "nccl" if real else "gloo"
+        if real:
             torch.cuda.set_device(local_rank)
         dist.init_process_group(backend=backend)
+    sync = _sync if real else (lambda _t: None)
 
     strategy, rc, desc = CONFIGS[config]
     daemon = kub = None
@@ -128,11 +131,11 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
 
         if world > 1:
             dist.barrier()
-        _sync(torch)
+        sync(torch)
         t0 = time.perf_counter()
         for _ in range(steps):
             client.run(pods_per_step, record=True)
-        _sync(torch)
+        sync(torch)
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
