@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "common/status.h"
+#include "metrics/metrics.h"
 
 namespace adp::grpc {
 
@@ -92,9 +93,9 @@ using StreamHandler =
     std::function<Status(std::string_view request, std::shared_ptr<ServerStream> stream)>;
 
 struct ServerStats {
-  std::atomic<uint64_t> connections{0};
-  std::atomic<uint64_t> calls{0};
-  std::atomic<uint64_t> errors{0};
+  std::atomic<uint64_t> connections{0};  // per accept: not on the call path
+  metrics::Counter calls;                // per call, from every loop: sharded
+  metrics::Counter errors;
 };
 
 class Server {

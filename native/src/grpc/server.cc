@@ -281,7 +281,7 @@ void ServerConn::SubmitTrailersOnly(int32_t sid, int code, const std::string& ms
   nghttp2_nv nva[4] = {MakeNv(":status", status), MakeNv("content-type", ct),
                        MakeNv("grpc-status", c), MakeNv("grpc-message", m)};
   nghttp2_submit_response(session_, sid, nva, m.empty() ? 3 : 4, nullptr);
-  srv_->stats_.errors.fetch_add(1, std::memory_order_relaxed);
+  srv_->stats_.errors.Add(1);
 }
 
 void ServerConn::SubmitResponse(int32_t sid) {
@@ -297,7 +297,7 @@ void ServerConn::Dispatch(int32_t sid) {
   StreamState* st = Find(sid);
   if (!st || st->dispatched) return;
   st->dispatched = true;
-  srv_->stats_.calls.fetch_add(1, std::memory_order_relaxed);
+  srv_->stats_.calls.Add(1);
 
   if (!StartsWithGrpc(st->content_type)) {
     SubmitTrailersOnly(sid, kGrpcInternal, "invalid content-type: " + st->content_type);

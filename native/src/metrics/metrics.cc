@@ -10,6 +10,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -26,18 +27,63 @@ const double Histogram::kBoundsSec[kBuckets] = {
     250e-9, 500e-9, 1e-6, 2e-6, 5e-6, 10e-6, 20e-6, 50e-6, 100e-6, 200e-6,
     500e-6, 1e-3,   2e-3, 5e-3, 10e-3, 20e-3, 50e-3, 100e-3, 500e-3, 1.0};
 
+int ShardIndex() {
+  static std::atomic<int> next{0};
+  thread_local int idx = next.fetch_add(1, std::memory_order_relaxed) % kShards;
+  return idx;
+}
+
+uint64_t Counter::Value() const {
+  uint64_t t = 0;
+  for (const auto& s : s_) t += s.v.load(std::memory_order_relaxed);
+  return t;
+}
+
+void MaxGauge::Observe(uint64_t v) {
+  auto& a = s_[ShardIndex()].v;
+  uint64_t prev = a.load(std::memory_order_relaxed);
+  while (v > prev && !a.compare_exchange_weak(prev, v, std::memory_order_relaxed)) {}
+}
+
+uint64_t MaxGauge::Value() const {
+  uint64_t m = 0;
+  for (const auto& s : s_) m = std::max(m, s.v.load(std::memory_order_relaxed));
+  return m;
+}
+
 void Histogram::Observe(uint64_t ns) {
   int b = 0;
   while (b < kBuckets && ns > static_cast<uint64_t>(kBoundsSec[b] * 1e9 + 0.5)) ++b;
-  buckets_[b].fetch_add(1, std::memory_order_relaxed);
-  count_.fetch_add(1, std::memory_order_relaxed);
-  sum_ns_.fetch_add(ns, std::memory_order_relaxed);
+  Shard& s = shards_[ShardIndex()];
+  s.buckets[b].fetch_add(1, std::memory_order_relaxed);
+  s.sum_ns.fetch_add(ns, std::memory_order_relaxed);
+}
+
+void Histogram::Totals(uint64_t counts[kBuckets + 1]) const {
+  for (int b = 0; b <= kBuckets; ++b) {
+    counts[b] = 0;
+    for (const auto& s : shards_) counts[b] += s.buckets[b].load(std::memory_order_relaxed);
+  }
+}
+
+uint64_t Histogram::count() const {
+  uint64_t counts[kBuckets + 1], t = 0;
+  Totals(counts);
+  for (uint64_t c : counts) t += c;
+  return t;
+}
+
+double Histogram::sum_seconds() const {
+  uint64_t t = 0;
+  for (const auto& s : shards_) t += s.sum_ns.load(std::memory_order_relaxed);
+  return t / 1e9;
 }
 
 double Histogram::QuantileUs(double q) const {
-  uint64_t total = 0;
   uint64_t counts[kBuckets + 1];
-  for (int b = 0; b <= kBuckets; ++b) total += counts[b] = buckets_[b].load(std::memory_order_relaxed);
+  Totals(counts);
+  uint64_t total = 0;
+  for (uint64_t c : counts) total += c;
   if (total == 0) return 0.0;
   uint64_t rank = static_cast<uint64_t>(q * static_cast<double>(total - 1)) + 1;
   uint64_t seen = 0;
@@ -50,11 +96,13 @@ double Histogram::QuantileUs(double q) const {
 
 void Histogram::AppendPrometheus(const std::string& name, const std::string& labels,
                                  std::string* out) const {
+  uint64_t counts[kBuckets + 1];
+  Totals(counts);
   uint64_t cum = 0;
   char line[512];
   std::string sep = labels.empty() ? "" : ",";
   for (int b = 0; b <= kBuckets; ++b) {
-    cum += buckets_[b].load(std::memory_order_relaxed);
+    cum += counts[b];
     if (b < kBuckets)
       snprintf(line, sizeof(line), "%s_bucket{%s%sle=\"%g\"} %llu\n", name.c_str(), labels.c_str(),
                sep.c_str(), kBoundsSec[b], static_cast<unsigned long long>(cum));
@@ -69,9 +117,10 @@ void Histogram::AppendPrometheus(const std::string& name, const std::string& lab
 }
 
 void Histogram::Reset() {
-  for (auto& b : buckets_) b.store(0, std::memory_order_relaxed);
-  count_.store(0, std::memory_order_relaxed);
-  sum_ns_.store(0, std::memory_order_relaxed);
+  for (auto& s : shards_) {
+    for (auto& b : s.buckets) b.store(0, std::memory_order_relaxed);
+    s.sum_ns.store(0, std::memory_order_relaxed);
+  }
 }
 
 std::string LabelValue(const std::string& v) {

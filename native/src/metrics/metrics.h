@@ -19,15 +19,42 @@
 
 namespace adp::metrics {
 
-// Fixed 1-2-5 buckets from 250 ns to 1 s (upper bounds, seconds).
+// Counters written on the RPC path are sharded per thread: with N server loops
+// serving concurrent clients, one shared cache line per counter would bounce
+// between cores on every call. A thread gets a shard index round-robin on first
+// use; readers sum the shards.
+constexpr int kShards = 16;
+int ShardIndex();
+
+class Counter {
+ public:
+  void Add(uint64_t n) { s_[ShardIndex()].v.fetch_add(n, std::memory_order_relaxed); }
+  uint64_t Value() const;
+
+ private:
+  struct alignas(64) Slot { std::atomic<uint64_t> v{0}; };
+  Slot s_[kShards];
+};
+
+class MaxGauge {
+ public:
+  void Observe(uint64_t v);
+  uint64_t Value() const;
+
+ private:
+  struct alignas(64) Slot { std::atomic<uint64_t> v{0}; };
+  Slot s_[kShards];
+};
+
+// Fixed 1-2-5 buckets from 250 ns to 1 s (upper bounds, seconds); sharded.
 class Histogram {
  public:
   static constexpr int kBuckets = 20;
   static const double kBoundsSec[kBuckets];
 
   void Observe(uint64_t ns);
-  uint64_t count() const { return count_.load(std::memory_order_relaxed); }
-  double sum_seconds() const { return sum_ns_.load(std::memory_order_relaxed) / 1e9; }
+  uint64_t count() const;
+  double sum_seconds() const;
   // Upper bound of the bucket holding quantile q (0 if empty), in microseconds.
   double QuantileUs(double q) const;
   // Appends `name_bucket{labels,le=..}`, `name_sum`, `name_count` lines.
@@ -35,9 +62,12 @@ class Histogram {
   void Reset();
 
  private:
-  std::atomic<uint64_t> buckets_[kBuckets + 1] = {};  // last = +Inf
-  std::atomic<uint64_t> count_{0};
-  std::atomic<uint64_t> sum_ns_{0};
+  struct alignas(64) Shard {
+    std::atomic<uint64_t> buckets[kBuckets + 1] = {};  // last = +Inf
+    std::atomic<uint64_t> sum_ns{0};
+  };
+  void Totals(uint64_t counts[kBuckets + 1]) const;
+  Shard shards_[kShards];
 };
 
 // Escapes a Prometheus label value (backslash, quote, newline).

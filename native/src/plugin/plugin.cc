@@ -189,7 +189,7 @@ void Plugin::BroadcastLaw(int loop) {
   for (auto& ls : streams) {
     if (ls.stream->closed()) continue;
     if (ls.sent_version != law->version) {
-      if (ls.stream->Send(law->bytes)) stats_.law_sends.fetch_add(1, std::memory_order_relaxed);
+      if (ls.stream->Send(law->bytes)) stats_.law_sends.Add(1);
       ls.sent_version = law->version;
     }
     streams[keep++] = std::move(ls);
@@ -300,10 +300,9 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
   }
   uint64_t dt = NowNs() - t0;
   stats_.allocate_hist.Observe(dt);
-  stats_.allocate_calls.fetch_add(1, std::memory_order_relaxed);
-  stats_.allocate_ns_total.fetch_add(dt, std::memory_order_relaxed);
-  uint64_t prev = stats_.allocate_ns_max.load(std::memory_order_relaxed);
-  while (dt > prev && !stats_.allocate_ns_max.compare_exchange_weak(prev, dt)) {}
+  stats_.allocate_calls.Add(1);
+  stats_.allocate_ns_total.Add(dt);
+  stats_.allocate_ns_max.Observe(dt);
   return Status::Ok();
 }
 
@@ -312,9 +311,8 @@ Status Plugin::HandlePreferred(std::string_view req, std::string* resp) {
   Status st = PreferredImpl(req, resp);
   uint64_t dt = NowNs() - t0;
   stats_.preferred_hist.Observe(dt);
-  stats_.preferred_ns_total.fetch_add(dt, std::memory_order_relaxed);
-  uint64_t prev = stats_.preferred_ns_max.load(std::memory_order_relaxed);
-  while (dt > prev && !stats_.preferred_ns_max.compare_exchange_weak(prev, dt)) {}
+  stats_.preferred_ns_total.Add(dt);
+  stats_.preferred_ns_max.Observe(dt);
   return st;
 }
 
@@ -322,7 +320,7 @@ Status Plugin::PreferredImpl(std::string_view req, std::string* resp) {
   std::vector<pb::ContainerPreferredAllocationRequestView> reqs;
   ADP_RETURN_IF_ERROR(pb::DecodeView(req, &reqs));
   pb::PreferredAllocationResponse out;
-  stats_.preferred_calls.fetch_add(1, std::memory_order_relaxed);
+  stats_.preferred_calls.Add(1);
   for (const auto& cr : reqs) {
     if (replicated_) {
       auto res = alloc::PrioritizeDeviceViews(cr.available, cr.must_include, cr.allocation_size,
@@ -394,7 +392,7 @@ Status Plugin::Start(std::function<void()> on_fatal) {
                        [this](std::string_view, std::shared_ptr<grpc::ServerStream> s) {
                          auto law = CurrentLaw();
                          s->Send(law->bytes);
-                         stats_.law_sends.fetch_add(1, std::memory_order_relaxed);
+                         stats_.law_sends.Add(1);
                          law_streams_[s->loop()].push_back({s, law->version});
                          return Status::Ok();
                        });
@@ -543,10 +541,10 @@ Status Plugin::WriteCdiSpec() const {
 }
 
 std::string Plugin::StatsJson() const {
-  uint64_t n = stats_.allocate_calls.load();
-  double avg = n ? stats_.allocate_ns_total.load() / 1e3 / n : 0.0;
-  uint64_t np = stats_.preferred_calls.load();
-  double pavg = np ? stats_.preferred_ns_total.load() / 1e3 / np : 0.0;
+  uint64_t n = stats_.allocate_calls.Value();
+  double avg = n ? stats_.allocate_ns_total.Value() / 1e3 / n : 0.0;
+  uint64_t np = stats_.preferred_calls.Value();
+  double pavg = np ? stats_.preferred_ns_total.Value() / 1e3 / np : 0.0;
   int loops = 0;
   {
     std::lock_guard<std::mutex> lk(server_mu_);
@@ -562,9 +560,9 @@ std::string Plugin::StatsJson() const {
            "\"allocate_handler_p99_le_us\": %g, \"preferred_handler_p50_le_us\": %g, "
            "\"preferred_handler_p99_le_us\": %g}",
            JsonEscape(spec_.resource_name).c_str(), units_.size(), advertised_.size(),
-           static_cast<unsigned long long>(n), avg, stats_.allocate_ns_max.load() / 1e3,
-           static_cast<unsigned long long>(np), pavg, stats_.preferred_ns_max.load() / 1e3,
-           static_cast<unsigned long long>(stats_.law_sends.load()), law_bytes_size_.load(), loops,
+           static_cast<unsigned long long>(n), avg, stats_.allocate_ns_max.Value() / 1e3,
+           static_cast<unsigned long long>(np), pavg, stats_.preferred_ns_max.Value() / 1e3,
+           static_cast<unsigned long long>(stats_.law_sends.Value()), law_bytes_size_.load(), loops,
            stats_.allocate_hist.QuantileUs(0.5), stats_.allocate_hist.QuantileUs(0.99),
            stats_.preferred_hist.QuantileUs(0.5), stats_.preferred_hist.QuantileUs(0.99));
   return buf;
@@ -612,11 +610,11 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
   family("amdgpu_dp_rpc_total", "counter", "Handled kubelet RPCs by method.");
   for (auto* p : plugins) {
     gauge("amdgpu_dp_rpc_total", res(p) + ",method=\"Allocate\"",
-          static_cast<double>(p->stats_.allocate_calls.load()));
+          static_cast<double>(p->stats_.allocate_calls.Value()));
     gauge("amdgpu_dp_rpc_total", res(p) + ",method=\"GetPreferredAllocation\"",
-          static_cast<double>(p->stats_.preferred_calls.load()));
+          static_cast<double>(p->stats_.preferred_calls.Value()));
     gauge("amdgpu_dp_rpc_total", res(p) + ",method=\"ListAndWatch\"",
-          static_cast<double>(p->stats_.law_sends.load()));
+          static_cast<double>(p->stats_.law_sends.Value()));
   }
   family("amdgpu_dp_handler_seconds", "histogram",
          "In-daemon handler time per RPC (request decode, device lookup, response encode).");
@@ -630,7 +628,7 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
   for (auto* p : plugins) {
     std::lock_guard<std::mutex> lk(p->server_mu_);
     if (p->server_)
-      conns.push_back({p, p->server_->stats().connections.load(), p->server_->stats().errors.load()});
+      conns.push_back({p, p->server_->stats().connections.load(), p->server_->stats().errors.Value()});
   }
   family("amdgpu_dp_grpc_connections_total", "counter", "Accepted connections on the plugin socket.");
   for (auto& c : conns) gauge("amdgpu_dp_grpc_connections_total", res(c.p), static_cast<double>(c.connections));

@@ -99,14 +99,15 @@ struct Unit {
   unsigned replicas = 1;
 };
 
+// Written by every server loop on every call: sharded per thread (metrics.h).
 struct RpcStats {
-  std::atomic<uint64_t> allocate_calls{0};
-  std::atomic<uint64_t> allocate_ns_total{0};
-  std::atomic<uint64_t> allocate_ns_max{0};
-  std::atomic<uint64_t> preferred_calls{0};
-  std::atomic<uint64_t> preferred_ns_total{0};
-  std::atomic<uint64_t> preferred_ns_max{0};
-  std::atomic<uint64_t> law_sends{0};
+  metrics::Counter allocate_calls;
+  metrics::Counter allocate_ns_total;
+  metrics::MaxGauge allocate_ns_max;
+  metrics::Counter preferred_calls;
+  metrics::Counter preferred_ns_total;
+  metrics::MaxGauge preferred_ns_max;
+  metrics::Counter law_sends;
   metrics::Histogram allocate_hist;   // handler time (decode + lookup + encode)
   metrics::Histogram preferred_hist;
 };

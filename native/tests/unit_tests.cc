@@ -22,6 +22,7 @@
 #include "daemon/config.h"
 #include "grpc/grpc.h"
 #include "health/health.h"
+#include "metrics/metrics.h"
 #include "proto/messages.h"
 #include "strategy/strategy.h"
 
@@ -411,7 +412,36 @@ static void TestGrpcMultiLoop() {
   rmdir(dir.c_str());
 }
 
+// Sharded counters/histograms: exact totals from many writer threads.
+static void TestMetrics() {
+  g_case = "metrics";
+  metrics::Counter c;
+  metrics::MaxGauge m;
+  metrics::Histogram h;
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 20; ++t)
+    ts.emplace_back([&, t] {
+      for (int i = 0; i < 10000; ++i) {
+        c.Add(1);
+        m.Observe(static_cast<uint64_t>(t) * 1000 + i % 7);
+        h.Observe(i % 2 ? 300 : 3000);  // 500 ns and 5 us buckets
+      }
+    });
+  for (auto& t : ts) t.join();
+  CHECK(c.Value() == 200000);
+  CHECK(m.Value() == 19 * 1000 + 6);
+  CHECK(h.count() == 200000);
+  CHECK(h.QuantileUs(0.25) == 0.5);
+  CHECK(h.QuantileUs(0.99) == 5.0);
+  std::string text;
+  h.AppendPrometheus("x_seconds", "a=\"b\"", &text);
+  CHECK(text.find("x_seconds_bucket{a=\"b\",le=\"+Inf\"} 200000\n") != std::string::npos);
+  CHECK(text.find("x_seconds_count{a=\"b\"} 200000\n") != std::string::npos);
+  CHECK(metrics::LabelValue("a\"b\\c\n") == "a\\\"b\\\\c\\n");
+}
+
 int main() {
+  TestMetrics();
   TestPrioritize();
   TestStrip();
   TestAdditionalIds();
