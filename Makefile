@@ -49,7 +49,7 @@ tsan-e2e:
 	rm -rf build/tsan-logs && mkdir -p build/tsan-logs
 	ADP_BUILD_DIR=$(CURDIR)/build/tsan TSAN_OPTIONS=log_path=$(CURDIR)/build/tsan-logs/daemon \
 	  $(PY) -m pytest -q -p no:cacheprovider tests/test_e2e_mock.py tests/test_health.py \
-	  tests/test_metrics.py tests/test_lifecycle.py -k "not additional_ids and not classification"
+	  tests/test_metrics.py tests/test_lifecycle.py tests/test_robustness.py -k "not additional_ids and not classification"
 	@if ls build/tsan-logs/* >/dev/null 2>&1; then cat build/tsan-logs/*; exit 1; fi
 
 lint:
