@@ -575,8 +575,22 @@ void Server::AcceptAll() {
     if (&target == loops_[0].get()) {
       AddConn(target, fd);
     } else {
+      // The fd travels in an owner that closes it if the hand-off is dropped
+      // (server stopping, or the queue cleared before the loop ran it).
+      struct OwnedFd {
+        explicit OwnedFd(int f) : fd(f) {}
+        OwnedFd(const OwnedFd&) = delete;
+        OwnedFd& operator=(const OwnedFd&) = delete;
+        ~OwnedFd() { if (fd >= 0) close(fd); }
+        int fd;
+      };
+      auto owned = std::make_shared<OwnedFd>(fd);
       Loop* t = &target;
-      PostTo(target, [this, t, fd] { AddConn(*t, fd); });
+      PostTo(target, [this, t, owned] {
+        int f = owned->fd;
+        owned->fd = -1;
+        AddConn(*t, f);
+      });
     }
   }
 }
