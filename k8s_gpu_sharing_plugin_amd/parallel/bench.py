@@ -26,7 +26,12 @@ CONFIGS = {
     "timeslice4": ("none", "gpu:gpu:4", "{n}xMI355X SPX, time-slice sharing 4 replicas/GPU ({p} concurrent pods)"),
     "auto-mem": ("none", "gpu:gpu-mem-gb:-1", "{n}xMI355X SPX, auto memory replicas (gpu-mem-gb)"),
     "cpx-single": ("single", "", "{n}xMI355X CPX, partitionStrategy=single, 8 partitions/GPU"),
+    # BASELINE config 5: always an 8-GPU node (6 SPX + 2 CPX, node model); one
+    # kubelet client admits amd.com/gpu:4 pods, so every admission runs the
+    # xGMI/NUMA-aware GetPreferredAllocation over the free SPX GPUs.
+    "mixed-gpu4": ("mixed", "", "8xMI355X mixed 6 SPX + 2 CPX, xGMI-aware GetPreferredAllocation for amd.com/gpu:4 pods"),
 }
+POD_SIZE = {"mixed-gpu4": 4}
 
 
 def _env_int(name, default):
@@ -114,10 +119,17 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                 args += ["--resource-config", rc]
             mode = "CPX" if config == "cpx-single" else "SPX"
             fx = None if real else fixtures.node(gpus, mode, memory="NPS2" if mode == "CPX" else "NPS1")
+            if config == "mixed-gpu4":
+                if real or world != 1:
+                    raise SystemExit("mixed-gpu4 runs on the 8-GPU node model with one client (--mock, 1 rank)")
+                fx = fixtures.node(8, ["SPX"] * 6 + ["CPX"] * 2, memory="NPS1")
+                args = ["--partition-strategy", strategy]
             daemon = harness.Daemon(d, fx, args=args, real_smi=real,
                                     env={"DP_HEALTH_POLL_MS": "0", "ADP_LOG_LEVEL": "warn"}).start()
-            reg = kub.wait(lambda e: e.get("event") == "register", 20)
-            devs = kub.wait(lambda e: e.get("event") == "devices", 20)
+            # The measured resource is amd.com/gpu (mixed registers partition resources too).
+            reg = kub.wait(lambda e: e.get("event") == "register" and
+                           (config not in POD_SIZE or e.get("resource", "").endswith("/gpu")), 20)
+            devs = kub.wait(lambda e: e.get("event") == "devices" and e.get("resource") == reg["resource"], 20)
             info = {"socket": os.path.join(d, reg["endpoint"]), "resource": reg["resource"],
                     "allocatable": devs["healthy"], "advertised": devs["total"], "scratch": d}
         if world > 1:
@@ -125,7 +137,7 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
             dist.broadcast_object_list(box, src=0)
             info = box[0]
 
-        client = native.ChurnClient(info["socket"], pod_size=1, rank=rank, world=world)
+        client = native.ChurnClient(info["socket"], pod_size=POD_SIZE.get(config, 1), rank=rank, world=world)
         client.run(max(1, warmup) * pods_per_step, record=False)
         client.reset()
 

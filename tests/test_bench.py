@@ -45,7 +45,8 @@ def test_bench_two_ranks_gloo():
     assert all(p["rank_devices"] == 1 for p in res["per_rank"])
 
 
-@pytest.mark.parametrize("config,advertised", [("timeslice4", 4), ("cpx-single", 8), ("auto-mem", 294)])
+@pytest.mark.parametrize("config,advertised", [("timeslice4", 4), ("cpx-single", 8), ("auto-mem", 294),
+                                               ("mixed-gpu4", 6)])
 def test_bench_configs_on_mock(config, advertised, monkeypatch):
     sys.path.insert(0, ROOT)
     from k8s_gpu_sharing_plugin_amd.parallel import bench
@@ -54,3 +55,13 @@ def test_bench_configs_on_mock(config, advertised, monkeypatch):
     assert res["advertised"] == advertised
     assert res["allocatable"] == advertised
     assert res["per_rank"][0]["allocate"]["n"] == 50
+
+
+def test_bench_mixed_gpu4_admits_four_gpu_pods(monkeypatch):
+    """BASELINE config 5: every admission is a 4-GPU preferred allocation on the SPX part."""
+    sys.path.insert(0, ROOT)
+    from k8s_gpu_sharing_plugin_amd.parallel import bench
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    res = bench.run(gpus=1, steps=1, warmup=1, pods_per_step=20, config="mixed-gpu4", force_mock=True, probe=False)
+    assert res["resource"] == "amd.com/gpu" and res["advertised"] == 6
+    assert res["per_rank"][0]["preferred"]["n"] == 20
