@@ -19,7 +19,8 @@
 // Runtime injection:
 //   event FIFO lines: "<gpu>[:<partition>] <event-type> [message]"
 //   state_dir files:  gpu<i>.ecc (uncorrectable count), gpu<i>.dead (device gone),
-//                     gpu<i>.partition ("CPX NPS2": live partition-mode override)
+//                     gpu<i>.partition ("CPX NPS2": live partition-mode override),
+//                     gpu<i>.xgmi_down (number of xGMI links reported down)
 //   amdsmi_shut_down + amdsmi_init re-reads the fixture (re-enumeration after a
 //   re-partition).
 #include <amd_smi/amdsmi.h>
@@ -447,8 +448,14 @@ amdsmi_status_t amdsmi_get_gpu_xgmi_link_status(amdsmi_processor_handle h,
   GET_PROC(h);
   memset(s, 0, sizeof(*s));
   s->total_links = 8;
+  int down = p->links_down;
+  if (!g->state_dir.empty()) {  // gpu<i>.xgmi_down: live override (a link failing)
+    std::ifstream f(g->state_dir + "/gpu" + std::to_string(p->gpu) + ".xgmi_down");
+    int v;
+    if (f >> v) down = v;
+  }
   for (int i = 0; i < 8; ++i)
-    s->status[i] = i < p->links_down ? AMDSMI_XGMI_LINK_DOWN : AMDSMI_XGMI_LINK_UP;
+    s->status[i] = i < down ? AMDSMI_XGMI_LINK_DOWN : AMDSMI_XGMI_LINK_UP;
   return AMDSMI_STATUS_SUCCESS;
 }
 

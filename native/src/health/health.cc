@@ -75,6 +75,7 @@ Monitor::Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> s
   ecc_baseline_.assign(n, 0);
   unresponsive_.assign(n, 0);
   ecc_failed_.assign(n, 0);
+  link_change_polls_.assign(n, 0);
 }
 
 Monitor::~Monitor() { Stop(); }
@@ -153,6 +154,22 @@ void Monitor::PollOnce() {
         LOG_WARN(kComp, "%s", why.c_str());
         layout_listener_(why);
         return;  // handles are about to be re-created; no health verdicts from them
+      }
+      // xGMI links that went down (or came back) change the topology scores
+      // GetPreferredAllocation uses; re-enumerate once the new count has held for
+      // two consecutive polls (a flapping link does not cause restart storms).
+      int down = lib_->XgmiLinksDown(h);
+      if (down != g.xgmi_links_down) {
+        if (++link_change_polls_[g.index] >= 2) {
+          layout_changed_ = true;
+          std::string why = "GPU " + g.bdf + " xGMI links down " + std::to_string(g.xgmi_links_down) +
+                            " -> " + std::to_string(down);
+          LOG_WARN(kComp, "%s", why.c_str());
+          layout_listener_(why);
+          return;
+        }
+      } else {
+        link_change_polls_[g.index] = 0;
       }
     }
     bool alive = lib_->Responsive(h);

@@ -93,6 +93,7 @@ class Monitor {
   std::vector<uint64_t> ecc_baseline_;
   std::vector<uint8_t> unresponsive_;
   std::vector<uint8_t> ecc_failed_;
+  std::vector<int> link_change_polls_;
 };
 
 }  // namespace adp::health

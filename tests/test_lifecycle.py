@@ -277,3 +277,35 @@ def test_idle_daemon_uses_no_cpu(scratch):
     finally:
         assert d.stop() == 0
         k.stop()
+
+
+def test_xgmi_link_loss_rescores_topology(scratch):
+    """xGMI links of GPU 2 go down: after two polls the node is re-enumerated and
+    GetPreferredAllocation steers a 2-GPU pod away from the degraded GPU."""
+    state = os.path.join(scratch + ".fixture", "state")
+    os.makedirs(state, exist_ok=True)
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(4), state_dir=state, env={"DP_HEALTH_POLL_MS": "100"}).start()
+    try:
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        avail = ids[1:4]
+        before = list(c.preferred(avail, size=2).container_responses[0].deviceIDs)
+        assert ids[2] in before  # equal scores: the lowest-index pair
+        c.close()
+        with open(os.path.join(state, "gpu2.xgmi_down"), "w") as f:
+            f.write("3\n")
+        k.wait_registration(10)  # re-registered after re-enumeration
+        log = d.wait_log("amdsmi re-initialised")
+        assert "xGMI links down 0 -> 3" in log
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        c.watch()[0].get(timeout=5)
+        after = list(c.preferred(avail, size=2).container_responses[0].deviceIDs)
+        assert sorted(after) == sorted([ids[1], ids[3]])
+        c.close()
+        time.sleep(0.5)
+        assert d.log().count("amdsmi re-initialised") == 1
+    finally:
+        assert d.stop() == 0
+        k.stop()
