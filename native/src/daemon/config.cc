@@ -111,6 +111,10 @@ const std::vector<FlagDef>& Table() {
        "after serving a request a gRPC loop polls without sleeping for this many "
        "microseconds, so follow-up calls skip a scheduler wake-up (0 = always sleep)",
        [](Flags& f) -> void* { return &f.busy_poll_us; }, true},
+      {"node-labels-file", "DP_NODE_LABELS_FILE", "nodeLabelsFile", Kind::kString,
+       "write node-feature labels (amd.com/gpu.product, .count, .memory-mib, partition modes, "
+       "interconnect) to this file for node-feature-discovery's local source (empty = off)",
+       [](Flags& f) -> void* { return &f.node_labels_file; }},
       {"metrics-addr", "DP_METRICS_ADDR", "metricsAddr", Kind::kString,
        "serve Prometheus /metrics and /healthz on this TCP address, e.g. ':9400' (empty = off)",
        [](Flags& f) -> void* { return &f.metrics_addr; }},

@@ -46,6 +46,7 @@ struct Flags {
   bool dry_run = false;
   uint64_t server_threads = 0;  // 0 -> plugin::DefaultServerThreads()
   std::string metrics_addr;     // "" = no metrics endpoint
+  std::string node_labels_file; // "" = no NFD feature file
   uint64_t busy_poll_us = 50;
 };
 

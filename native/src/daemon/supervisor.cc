@@ -99,7 +99,13 @@ int DryRun(smi::Library* lib, const Validated& v, const Config& cfg) {
            g.memory_mode + "\", \"partitions\": " + std::to_string(g.partitions.size()) +
            ", \"vram_mib\": " + std::to_string(g.vram_mib) + ", \"numa\": " + std::to_string(g.numa) + "}";
   }
-  out += "], \"resources\": [";
+  out += "], \"labels\": {";
+  bool first_label = true;
+  for (const auto& [k, v] : inventory::NodeLabels(**snap)) {
+    out += std::string(first_label ? "" : ", ") + "\"" + JsonEscape(k) + "\": \"" + JsonEscape(v) + "\"";
+    first_label = false;
+  }
+  out += "}, \"resources\": [";
   bool first = true;
   for (const auto& s : *specs) {
     plugin::Plugin p(*snap, s, v.popts);
@@ -114,6 +120,22 @@ int DryRun(smi::Library* lib, const Validated& v, const Config& cfg) {
   printf("%s\n", out.c_str());
   fflush(stdout);
   return 0;
+}
+
+// Atomically replaces `path` with one `key=value` line per label.
+void WriteLabels(const std::string& path, const inventory::Snapshot& snap) {
+  std::string body;
+  for (const auto& [k, v] : inventory::NodeLabels(snap)) body += k + "=" + v + "\n";
+  std::string tmp = path + ".tmp";
+  FILE* f = fopen(tmp.c_str(), "w");
+  bool ok = f && fwrite(body.data(), 1, body.size(), f) == body.size();
+  if (f) ok = (fclose(f) == 0) && ok;
+  if (!ok || rename(tmp.c_str(), path.c_str()) != 0) {
+    LOG_WARN(kComp, "cannot write node labels to %s: %s", path.c_str(), strerror(errno));
+    unlink(tmp.c_str());
+    return;
+  }
+  LOG_INFO(kComp, "wrote node labels to %s", path.c_str());
 }
 
 void ArmTimer(int tfd, int ms) {
@@ -272,6 +294,7 @@ int RunDaemon(const Config& cfg) {
       schedule_retry("enumeration failed");
       return;
     }
+    if (!cfg.flags.node_labels_file.empty()) WriteLabels(cfg.flags.node_labels_file, **snap);
     auto specs = strategy::BuildPluginSpecs(**snap, v.partition, v.rc, cfg.flags.resource_prefix);
     if (!specs.ok()) {
       LOG_ERROR(kComp, "error creating partition strategy: %s", specs.status().message().c_str());
@@ -396,6 +419,8 @@ int RunDaemon(const Config& cfg) {
   }
   stop_all();
   if (http) http->Stop();
+  // Labels describe a node this daemon is serving; do not leave them behind.
+  if (!cfg.flags.node_labels_file.empty()) unlink(cfg.flags.node_labels_file.c_str());
   for (int fd : {ep, sfd, ifd, tfd, efd, lfd}) close(fd);
   LOG_INFO(kComp, "shutdown complete (exit %d)", exit_code);
   return exit_code;

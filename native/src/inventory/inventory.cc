@@ -1,5 +1,7 @@
 #include "inventory/inventory.h"
 
+#include <cctype>
+
 #include <algorithm>
 #include <map>
 #include <set>
@@ -184,6 +186,61 @@ Result<std::shared_ptr<const Snapshot>> BuildSnapshot(smi::Library* lib, const B
              g.partitions.front().render_path.c_str());
   }
   return std::shared_ptr<const Snapshot>(snap);
+}
+
+namespace {
+
+std::string LabelSafe(std::string v) {
+  for (auto& c : v)
+    if (!isalnum(static_cast<unsigned char>(c)) && c != '.' && c != '_' && c != '-') c = '-';
+  while (!v.empty() && !isalnum(static_cast<unsigned char>(v.front()))) v.erase(v.begin());
+  while (!v.empty() && !isalnum(static_cast<unsigned char>(v.back()))) v.pop_back();
+  if (v.size() > 63) v.resize(63);
+  return v;
+}
+
+}  // namespace
+
+std::vector<std::pair<std::string, std::string>> NodeLabels(const Snapshot& snap) {
+  std::vector<std::pair<std::string, std::string>> out;
+  const size_t n = snap.gpus.size();
+  out.emplace_back("amd.com/gpu.present", n ? "true" : "false");
+  out.emplace_back("amd.com/gpu.count", std::to_string(n));
+  if (n == 0) return out;
+  auto uniform = [&](auto get) {
+    std::string v = get(snap.gpus[0]);
+    for (const auto& g : snap.gpus)
+      if (get(g) != v) return std::string("mixed");
+    return v;
+  };
+  out.emplace_back("amd.com/gpu.product", LabelSafe(uniform([](const PhysicalGpu& g) { return g.market_name; })));
+  uint64_t vram = snap.gpus[0].vram_mib;
+  size_t parts = 0;
+  for (const auto& g : snap.gpus) {
+    vram = std::min(vram, g.vram_mib);
+    parts += g.partitions.size();
+  }
+  out.emplace_back("amd.com/gpu.memory-mib", std::to_string(vram));
+  out.emplace_back("amd.com/gpu.compute-partition", LabelSafe(uniform([](const PhysicalGpu& g) { return g.compute_mode; })));
+  out.emplace_back("amd.com/gpu.memory-partition",
+                   LabelSafe(uniform([](const PhysicalGpu& g) { return g.memory_mode.empty() ? std::string("unknown") : g.memory_mode; })));
+  out.emplace_back("amd.com/gpu.partitions", std::to_string(parts));
+  std::string profile = uniform([](const PhysicalGpu& g) { return g.PartitionProfile(); });
+  if (!profile.empty()) out.emplace_back("amd.com/gpu.partition-profile", LabelSafe(profile));
+  // Interconnect: every distinct pair over xGMI -> "xgmi-full-mesh".
+  bool all_xgmi = n > 1, any_xgmi = false;
+  for (size_t a = 0; a < n; ++a)
+    for (size_t b = 0; b < n; ++b) {
+      if (a == b) continue;
+      bool x = snap.Link(static_cast<int>(a), static_cast<int>(b)) == LinkClass::kXgmi;
+      all_xgmi = all_xgmi && x;
+      any_xgmi = any_xgmi || x;
+    }
+  out.emplace_back("amd.com/gpu.interconnect", n == 1 ? "single" : all_xgmi ? "xgmi-full-mesh" : any_xgmi ? "xgmi-partial" : "pcie");
+  int down = 0;
+  for (const auto& g : snap.gpus) down += g.xgmi_links_down;
+  out.emplace_back("amd.com/gpu.xgmi-links-down", std::to_string(down));
+  return out;
 }
 
 }  // namespace adp::inventory

@@ -25,6 +25,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "common/status.h"
@@ -88,6 +89,12 @@ struct Snapshot {
   // Physical GPU that owns amdsmi handle index `h` (-1 if none).
   int GpuOfHandle(int h) const;
 };
+
+// Node-feature labels describing the GPUs of a snapshot, for Kubernetes
+// node-feature-discovery's local source (key=value lines): product, count,
+// HBM per GPU, compute/memory partition modes, partitions, xGMI connectivity.
+// Values are sanitised to label syntax ([A-Za-z0-9._-], <= 63 chars).
+std::vector<std::pair<std::string, std::string>> NodeLabels(const Snapshot& snap);
 
 struct BuildOptions {
   std::string driver_root = "/";

@@ -183,3 +183,16 @@ def test_memory_unit_grant_caps_pytorch(scratch, snap):
                        timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().endswith("CAPPED") and "NOT" not in r.stdout
+
+
+def test_dry_run_labels_on_real_gpu(snap):
+    import json
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import DAEMON
+    env = {k: v for k, v in os.environ.items() if k != "AMD_SMI_LIB"}
+    r = subprocess.run([DAEMON, "--dry-run", "--devices", "0"], capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lab = json.loads(r.stdout)["labels"]
+    assert lab["amd.com/gpu.count"] == "1" and "MI355" in lab["amd.com/gpu.product"]
+    assert lab["amd.com/gpu.memory-mib"] == str(snap["gpus"][0]["vram_mib"])
+    assert lab["amd.com/gpu.compute-partition"] == snap["gpus"][0]["compute_mode"]

@@ -200,6 +200,9 @@ def test_dry_run_reports_allocatable(scratch):
     res = {x["resource"]: x["allocatable"] for x in rep["resources"]}
     assert res == {"amd.com/gpu": 8, "amd.com/cpx-1xcd.36gb": 32}
     assert not os.path.exists(os.path.join(scratch, "amd-gpu.sock"))
+    lab = rep["labels"]
+    assert lab["amd.com/gpu.count"] == "8" and lab["amd.com/gpu.product"] == "AMD-Instinct-MI355X"
+    assert lab["amd.com/gpu.compute-partition"] == "mixed" and lab["amd.com/gpu.interconnect"] == "xgmi-full-mesh"
 
 
 def test_sigusr1_dumps_stats(scratch):
@@ -309,3 +312,28 @@ def test_xgmi_link_loss_rescores_topology(scratch):
     finally:
         assert d.stop() == 0
         k.stop()
+
+
+def test_node_labels_file_for_nfd(scratch):
+    """--node-labels-file: node-feature-discovery local-source file, rewritten on
+    every re-enumeration and removed when the daemon exits."""
+    path = os.path.join(scratch + ".fixture", "amd-gpu.features")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, fixtures.node(4, "CPX", memory="NPS2"),
+                       args=["--node-labels-file", path, "--partition-strategy", "single"]).start()
+    try:
+        k.wait_registration()
+        d.wait_log("wrote node labels")
+        labels = dict(line.split("=", 1) for line in open(path).read().splitlines())
+        assert labels == {
+            "amd.com/gpu.present": "true", "amd.com/gpu.count": "4",
+            "amd.com/gpu.product": "AMD-Instinct-MI355X", "amd.com/gpu.memory-mib": str(fixtures.MI355X_VRAM_MIB),
+            "amd.com/gpu.compute-partition": "CPX", "amd.com/gpu.memory-partition": "NPS2",
+            "amd.com/gpu.partitions": "32", "amd.com/gpu.partition-profile": "cpx-1xcd.36gb",
+            "amd.com/gpu.interconnect": "xgmi-full-mesh", "amd.com/gpu.xgmi-links-down": "0"}
+        assert all(len(v) <= 63 for v in labels.values())
+    finally:
+        assert d.stop() == 0
+        k.stop()
+    assert not os.path.exists(path)
