@@ -115,6 +115,10 @@ const std::vector<FlagDef>& Table() {
        "write node-feature labels (amd.com/gpu.product, .count, .memory-mib, partition modes, "
        "interconnect) to this file for node-feature-discovery's local source (empty = off)",
        [](Flags& f) -> void* { return &f.node_labels_file; }},
+      {"pod-resources-socket", "DP_POD_RESOURCES_SOCKET", "podResourcesSocket", Kind::kString,
+       "kubelet PodResources socket; with --metrics-addr, per-device allocations and "
+       "sharing (pods per GPU) are exported (empty = off)",
+       [](Flags& f) -> void* { return &f.pod_resources_socket; }},
       {"metrics-addr", "DP_METRICS_ADDR", "metricsAddr", Kind::kString,
        "serve Prometheus /metrics and /healthz on this TCP address, e.g. ':9400' (empty = off)",
        [](Flags& f) -> void* { return &f.metrics_addr; }},

@@ -47,6 +47,7 @@ struct Flags {
   uint64_t server_threads = 0;  // 0 -> plugin::DefaultServerThreads()
   std::string metrics_addr;     // "" = no metrics endpoint
   std::string node_labels_file; // "" = no NFD feature file
+  std::string pod_resources_socket = "/var/lib/kubelet/pod-resources/kubelet.sock";
   uint64_t busy_poll_us = 50;
 };
 

@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <atomic>
 #include <memory>
@@ -24,6 +25,7 @@
 #include "health/health.h"
 #include "inventory/inventory.h"
 #include "metrics/metrics.h"
+#include "podresources/podresources.h"
 #include "plugin/plugin.h"
 #include "smi/smi.h"
 #include "strategy/strategy.h"
@@ -224,6 +226,10 @@ int RunDaemon(const Config& cfg) {
   bool reinit = false;
 
   std::unique_ptr<metrics::HttpServer> http;
+  std::unique_ptr<podresources::CachedLister> pod_lister;
+  if (!cfg.flags.metrics_addr.empty() && !cfg.flags.pod_resources_socket.empty())
+    pod_lister = std::make_unique<podresources::CachedLister>(cfg.flags.pod_resources_socket,
+                                                              std::chrono::milliseconds(2000));
   if (!cfg.flags.metrics_addr.empty()) {
     std::string smi_version = (*lib)->Version();
     http = std::make_unique<metrics::HttpServer>(
@@ -237,11 +243,19 @@ int RunDaemon(const Config& cfg) {
               "# HELP amdgpu_dp_restarts_total Plugin (re)starts: kubelet restart, SIGHUP, retries.\n"
               "# TYPE amdgpu_dp_restarts_total counter\n"
               "amdgpu_dp_restarts_total " + std::to_string(restarts.load()) + "\n";
+          // Ask the kubelet who holds which device (cached; outside the plugins lock).
+          Result<std::vector<podresources::Assignment>> assigned = Unavailable("off");
+          if (pod_lister) {
+            assigned = pod_lister->Get();
+            out += "# HELP amdgpu_dp_pod_resources_up 1 if the kubelet PodResources API answered.\n"
+                   "# TYPE amdgpu_dp_pod_resources_up gauge\n"
+                   "amdgpu_dp_pod_resources_up " + std::string(assigned.ok() ? "1" : "0") + "\n";
+          }
           std::lock_guard<std::mutex> lk(plugins_mu);
           std::vector<const plugin::Plugin*> ps;
           for (auto& p : plugins)
             if (p->device_count() > 0) ps.push_back(p.get());
-          plugin::Plugin::AppendPrometheus(ps, &out);
+          plugin::Plugin::AppendPrometheus(ps, &out, assigned.ok() ? &*assigned : nullptr);
           return out;
         },
         [&] {

@@ -4,6 +4,9 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <tuple>
+#include <set>
+#include <map>
 #include <chrono>
 #include <cstring>
 #include <future>
@@ -575,7 +578,8 @@ size_t Plugin::healthy_count() const {
   return n;
 }
 
-void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::string* out) {
+void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::string* out,
+                              const std::vector<podresources::Assignment>* assignments) {
   using metrics::LabelValue;
   char line[512];
   auto family = [&](const char* name, const char* type, const char* help) {
@@ -622,6 +626,51 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
     p->stats_.allocate_hist.AppendPrometheus("amdgpu_dp_handler_seconds", res(p) + ",method=\"Allocate\"", out);
     p->stats_.preferred_hist.AppendPrometheus("amdgpu_dp_handler_seconds",
                                               res(p) + ",method=\"GetPreferredAllocation\"", out);
+  }
+  if (assignments) {
+    // Per physical device: advertised IDs held by running containers and the
+    // number of distinct pods holding them (the sharing factor), plus one
+    // series per (pod, container, device).
+    struct Use { std::vector<uint64_t> ids; std::vector<std::set<std::string>> pods; };
+    std::map<std::tuple<const Plugin*, int, std::string, std::string, std::string>, uint64_t> per_pod;
+    std::vector<Use> uses(plugins.size());
+    for (size_t i = 0; i < plugins.size(); ++i) {
+      uses[i].ids.assign(plugins[i]->units_.size(), 0);
+      uses[i].pods.resize(plugins[i]->units_.size());
+    }
+    for (const auto& a : *assignments) {
+      for (size_t i = 0; i < plugins.size(); ++i) {
+        const Plugin* p = plugins[i];
+        if (a.resource != p->spec_.resource_name) continue;
+        auto it = p->advertised_index_.find(a.device_id);
+        if (it == p->advertised_index_.end()) continue;
+        ++uses[i].ids[it->second];
+        uses[i].pods[it->second].insert(a.ns + "/" + a.pod);
+        ++per_pod[{p, it->second, a.ns, a.pod, a.container}];
+      }
+    }
+    auto dev = [&](const Plugin* p, int u) {
+      return res(p) + ",device=\"" + LabelValue(p->units_[u].id) + "\"";
+    };
+    family("amdgpu_dp_device_allocated_ids", "gauge",
+           "Advertised IDs (replicas / memory units) of the device held by running containers.");
+    for (size_t i = 0; i < plugins.size(); ++i)
+      for (size_t u = 0; u < uses[i].ids.size(); ++u)
+        gauge("amdgpu_dp_device_allocated_ids", dev(plugins[i], static_cast<int>(u)),
+              static_cast<double>(uses[i].ids[u]));
+    family("amdgpu_dp_device_pods", "gauge", "Distinct pods sharing the device.");
+    for (size_t i = 0; i < plugins.size(); ++i)
+      for (size_t u = 0; u < uses[i].pods.size(); ++u)
+        gauge("amdgpu_dp_device_pods", dev(plugins[i], static_cast<int>(u)),
+              static_cast<double>(uses[i].pods[u].size()));
+    family("amdgpu_dp_container_device_ids", "gauge", "Advertised IDs of a device held by one container.");
+    for (const auto& [k, n] : per_pod) {
+      const auto& [p, u, ns, pod, ctr] = k;
+      gauge("amdgpu_dp_container_device_ids",
+            dev(p, u) + ",namespace=\"" + LabelValue(ns) + "\",pod=\"" + LabelValue(pod) +
+                "\",container=\"" + LabelValue(ctr) + "\"",
+            static_cast<double>(n));
+    }
   }
   struct Conn { const Plugin* p; uint64_t connections, errors; };
   std::vector<Conn> conns;

@@ -41,6 +41,7 @@
 #include "grpc/grpc.h"
 #include "inventory/inventory.h"
 #include "metrics/metrics.h"
+#include "podresources/podresources.h"
 #include "strategy/strategy.h"
 
 namespace adp::plugin {
@@ -146,7 +147,9 @@ class Plugin {
   bool registered() const { return registered_.load(); }
   size_t healthy_count() const;
   // Prometheus text for a set of plugins (one HELP/TYPE header per family).
-  static void AppendPrometheus(const std::vector<const Plugin*>& plugins, std::string* out);
+  // `assignments` (kubelet PodResources, may be null) adds per-device usage.
+  static void AppendPrometheus(const std::vector<const Plugin*>& plugins, std::string* out,
+                               const std::vector<podresources::Assignment>* assignments = nullptr);
 
   // Handlers (public for in-process tests and benchmarks; loop thread only when serving).
   Status HandleGetOptions(std::string_view req, std::string* resp);

@@ -23,6 +23,8 @@
 #include "grpc/grpc.h"
 #include "health/health.h"
 #include "metrics/metrics.h"
+#include "podresources/podresources.h"
+#include "proto/wire.h"
 #include "proto/messages.h"
 #include "strategy/strategy.h"
 
@@ -440,7 +442,34 @@ static void TestMetrics() {
   CHECK(metrics::LabelValue("a\"b\\c\n") == "a\\\"b\\\\c\\n");
 }
 
+static void TestPodResources() {
+  g_case = "podresources";
+  // pod_resources { name: "p" namespace: "n" containers { name: "c"
+  //   devices { resource_name: "amd.com/gpu" device_ids: "a" device_ids: "b" } } }
+  std::string devs, ctr, pod, resp;
+  pb::PutStr(&devs, 1, "amd.com/gpu");
+  pb::PutLen(&devs, 2, "a");
+  pb::PutLen(&devs, 2, "b");
+  pb::PutInt64(&devs, 7, 42);  // unknown field: skipped
+  pb::PutStr(&ctr, 1, "c");
+  pb::PutLen(&ctr, 2, devs);
+  pb::PutStr(&pod, 1, "p");
+  pb::PutStr(&pod, 2, "n");
+  pb::PutLen(&pod, 3, ctr);
+  pb::PutLen(&resp, 1, pod);
+  std::vector<podresources::Assignment> out;
+  CHECK(podresources::DecodeList(resp, &out).ok());
+  CHECK(out.size() == 2);
+  if (out.size() == 2)
+    CHECK(out[1].pod == "p" && out[1].ns == "n" && out[1].container == "c" && out[1].resource == "amd.com/gpu" &&
+          out[1].device_id == "b");
+  out.clear();
+  CHECK(!podresources::DecodeList(resp.substr(0, resp.size() - 3), &out).ok());
+  CHECK(!podresources::DecodeList("\x0a\xff\xff\xff\xff\x0f", &out).ok());
+}
+
 int main() {
+  TestPodResources();
   TestMetrics();
   TestPrioritize();
   TestStrip();

@@ -148,3 +148,89 @@ def test_builtin_sampler_writes_profile(scratch):
     text = open(out).read()
     assert text.startswith("samples ")
     assert "== by shared object ==" in text and "== by symbol ==" in text
+
+
+# --- kubelet PodResources: who holds which device -------------------------------
+
+def _pb_len(field, payload: bytes) -> bytes:
+    def varint(v):
+        out = b""
+        while v >= 0x80:
+            out += bytes([(v & 0x7F) | 0x80])
+            v >>= 7
+        return out + bytes([v])
+    return varint(field << 3 | 2) + varint(len(payload)) + payload
+
+
+def _list_response(pods):
+    """pods: [(namespace, pod, container, resource, [ids])] -> ListPodResourcesResponse bytes."""
+    out = b""
+    for ns, pod, ctr, res, ids in pods:
+        devs = _pb_len(1, res.encode()) + b"".join(_pb_len(2, i.encode()) for i in ids)
+        container = _pb_len(1, ctr.encode()) + _pb_len(2, devs)
+        out += _pb_len(1, _pb_len(1, pod.encode()) + _pb_len(2, ns.encode()) + _pb_len(3, container))
+    return out
+
+
+class PodResourcesStub:
+    def __init__(self, path):
+        import grpc
+        from concurrent import futures
+        self.payload = b""
+        self.calls = 0
+
+        def handle(req, ctx):
+            self.calls += 1
+            return self.payload
+        h = grpc.method_handlers_generic_handler(
+            "v1.PodResourcesLister", {"List": grpc.unary_unary_rpc_method_handler(handle)})
+        self.server = grpc.server(futures.ThreadPoolExecutor(2), handlers=[h])
+        self.server.add_insecure_port("unix:" + path)
+        self.server.start()
+
+    def stop(self):
+        self.server.stop(0)
+
+
+def test_pod_resources_sharing_metrics(scratch):
+    pr_sock = os.path.join(scratch + ".fixture", "pod-resources.sock")
+    os.makedirs(os.path.dirname(pr_sock), exist_ok=True)
+    pr = PodResourcesStub(pr_sock)
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(2), args=[
+        "--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:sharedgpu:4",
+        "--pod-resources-socket", pr_sock]).start()
+    try:
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics")).group(1))
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        c.close()
+        g0 = ids[0].split("-replica-")[0]
+        g1 = ids[4].split("-replica-")[0]
+        pr.payload = _list_response([
+            ("ml", "train-a", "main", "amd.com/sharedgpu", [ids[0], ids[1]]),
+            ("ml", "train-b", "main", "amd.com/sharedgpu", [ids[2]]),
+            ("web", "infer", "srv", "amd.com/sharedgpu", [ids[4]]),
+            ("other", "cpu-pod", "x", "example.com/foo", ["whatever"]),
+        ])
+        s = _parse(_get(port, "/metrics")[1])
+        r = "amd.com/sharedgpu"
+        assert _value(s, "amdgpu_dp_pod_resources_up") == 1
+        assert _value(s, "amdgpu_dp_device_allocated_ids", resource=r, device=g0) == 3
+        assert _value(s, "amdgpu_dp_device_pods", resource=r, device=g0) == 2
+        assert _value(s, "amdgpu_dp_device_pods", resource=r, device=g1) == 1
+        assert _value(s, "amdgpu_dp_container_device_ids", device=g0, namespace="ml", pod="train-a") == 2
+        _get(port, "/metrics")
+        assert pr.calls == 1  # cached between scrapes
+        pr.stop()
+        pr = None
+        time.sleep(2.1)
+        s = _parse(_get(port, "/metrics")[1])
+        assert _value(s, "amdgpu_dp_pod_resources_up") == 0
+        assert not any(n == "amdgpu_dp_device_pods" for (n, _) in s)
+    finally:
+        if pr:
+            pr.stop()
+        d.stop()
+        k.stop()
