@@ -64,6 +64,18 @@ def bw_sweep(device: int = 0, nbytes: int = 1 << 30, iters: int = 10) -> list:
     return res
 
 
+def p2p(ndev: int = 0, nbytes: int = 256 << 20, iters: int = 5) -> dict:
+    """xGMI peer-read GB/s for every ordered pair of the first `ndev` devices (0 = all)."""
+    so = _lib()
+    so.adp_probe_p2p.argtypes = [ctypes.c_int, ctypes.c_ulonglong, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    buf = ctypes.create_string_buffer(1 << 16)
+    rc = so.adp_probe_p2p(ndev, nbytes, iters, buf, len(buf))
+    res = json.loads(buf.value.decode())
+    if rc != 0:
+        raise ProbeError(res)
+    return res
+
+
 def device_for_bdf(bdf: str) -> int:
     """HIP ordinal of the GPU at PCI address `bdf` ("dddd:bb:dd.f"), function ignored."""
     want = bdf.lower().rsplit(".", 1)[0]

@@ -2,13 +2,17 @@
 //
 //   amdgpu-dp-probe [--list] [--device N] [--bytes B] [--iters I]
 //                   [--expect-xcds X] [--expect-cus C] [--min-gbps G]
+//                   [--p2p [--min-p2p-gbps P]]
 //
 // Runs the visibility probe (visibility_probe.hip) on every visible HIP device
 // (or one) and prints one JSON line per device. Exits non-zero when a device
 // fails its checksum or does not have the expected shape -- e.g. a pod that
 // requested one CPX partition must see exactly 1 XCD / 32 CUs:
 //   amdgpu-dp-probe --expect-xcds 1 --expect-cus 32
-// See examples/pods/pod-validate.yml.
+// See examples/pods/pod-validate.yml. --p2p additionally measures xGMI peer-read
+// bandwidth between every pair of the pod's GPUs (a multi-GPU pod placed by the
+// xGMI-aware preferred allocation should see every pair connected); it fails if a
+// pair has no peer access or is below --min-p2p-gbps.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -17,6 +21,7 @@
 extern "C" int adp_probe_device_count();
 extern "C" int adp_probe_list(char* out, int len);
 extern "C" int adp_probe_run(int device, unsigned long long bytes, int iters, char* out, int len);
+extern "C" int adp_probe_p2p(int ndev, unsigned long long bytes, int iters, char* out, int len);
 
 namespace {
 
@@ -38,8 +43,8 @@ int main(int argc, char** argv) {
   int device = -1, iters = 5;
   unsigned long long bytes = 256ull << 20;
   long expect_xcds = -1, expect_cus = -1;
-  double min_gbps = -1;
-  bool list = false;
+  double min_gbps = -1, min_p2p_gbps = -1;
+  bool list = false, p2p = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : "0"; };
@@ -50,9 +55,11 @@ int main(int argc, char** argv) {
     else if (a == "--expect-xcds") expect_xcds = atol(next());
     else if (a == "--expect-cus") expect_cus = atol(next());
     else if (a == "--min-gbps") min_gbps = atof(next());
+    else if (a == "--p2p") p2p = true;
+    else if (a == "--min-p2p-gbps") min_p2p_gbps = atof(next());
     else {
       fprintf(stderr, "usage: %s [--list] [--device N] [--bytes B] [--iters I] [--expect-xcds X] "
-                      "[--expect-cus C] [--min-gbps G]\n", argv[0]);
+                      "[--expect-cus C] [--min-gbps G] [--p2p [--min-p2p-gbps P]]\n", argv[0]);
       return 2;
     }
   }
@@ -75,6 +82,15 @@ int main(int argc, char** argv) {
     if (expect_xcds >= 0 && JsonInt(buf, "xccs_seen") != expect_xcds) ++failures;
     if (expect_cus >= 0 && JsonInt(buf, "cus") != expect_cus) ++failures;
     if (min_gbps >= 0 && JsonDouble(buf, "hbm_copy_gbps") < min_gbps) ++failures;
+  }
+  if (p2p) {
+    int rc = adp_probe_p2p(n, bytes, iters, buf, sizeof(buf));
+    printf("%s\n", buf);
+    if (rc != 0 || strstr(buf, "no-peer-access")) ++failures;
+    if (min_p2p_gbps >= 0) {
+      for (const char* q = strstr(buf, "\"gbps\": "); q; q = strstr(q + 1, "\"gbps\": "))
+        if (strtod(q + 8, nullptr) < min_p2p_gbps) ++failures;
+    }
   }
   fflush(stdout);
   return failures ? 1 : 0;

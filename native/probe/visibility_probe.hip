@@ -209,6 +209,81 @@ extern "C" int adp_probe_bw_sweep(int device, unsigned long long bytes, int iter
   return 0;
 }
 
+// xGMI peer-read bandwidth between every ordered pair of visible devices: the
+// kernel runs on device i and streams a buffer that lives on device j into local
+// memory (the traffic a multi-GPU pod's collectives put on the link). A pair is
+// only measured after hipDeviceEnablePeerAccess succeeded -- a kernel must never
+// touch peer memory it has no mapping for. Output: {"devices": [...],
+// "pairs": [{"dst": i, "src": j, "gbps": x | "no-peer-access": true}]}.
+extern "C" int adp_probe_p2p(int ndev, unsigned long long bytes, int iters, char* out, int len) {
+  int count = 0;
+  HIP_TRY(hipGetDeviceCount(&count));
+  if (ndev <= 0 || ndev > count) ndev = count;
+  size_t n = bytes / sizeof(uint4);
+  std::string s = "{\"devices\": " + std::to_string(ndev) + ", \"bytes\": " + std::to_string(n * sizeof(uint4)) +
+                  ", \"pairs\": [";
+  bool first = true;
+  for (int i = 0; i < ndev; ++i) {
+    for (int j = 0; j < ndev; ++j) {
+      if (i == j) continue;
+      char buf[160];
+      int can = 0;
+      HIP_TRY(hipDeviceCanAccessPeer(&can, i, j));
+      if (can) {
+        HIP_TRY(hipSetDevice(i));
+        hipError_t e = hipDeviceEnablePeerAccess(j, 0);
+        if (e == hipErrorPeerAccessAlreadyEnabled) {
+          (void)hipGetLastError();  // clear the sticky "already enabled" status
+          e = hipSuccess;
+        }
+        can = e == hipSuccess;
+      }
+      if (!can) {
+        snprintf(buf, sizeof(buf), "%s{\"dst\": %d, \"src\": %d, \"no-peer-access\": true}", first ? "" : ", ", i, j);
+        s += buf;
+        first = false;
+        continue;
+      }
+      uint4 *src = nullptr, *dst = nullptr;
+      HIP_TRY(hipSetDevice(j));
+      HIP_TRY(hipMalloc(&src, n * sizeof(uint4)));
+      hipDeviceProp_t pj;
+      HIP_TRY(hipGetDeviceProperties(&pj, j));
+      hipLaunchKernelGGL(FillKernel, dim3(pj.multiProcessorCount * 4), dim3(256), 0, 0, src, n);
+      HIP_TRY(hipDeviceSynchronize());
+      HIP_TRY(hipSetDevice(i));
+      HIP_TRY(hipMalloc(&dst, n * sizeof(uint4)));
+      hipDeviceProp_t pi;
+      HIP_TRY(hipGetDeviceProperties(&pi, i));
+      dim3 grid(pi.multiProcessorCount);
+      hipLaunchKernelGGL((CopyKernelT<4, true, true>), grid, dim3(256), 0, 0, src, dst, n);  // warm-up
+      HIP_TRY(hipGetLastError());
+      hipEvent_t e0, e1;
+      HIP_TRY(hipEventCreate(&e0));
+      HIP_TRY(hipEventCreate(&e1));
+      HIP_TRY(hipEventRecord(e0, 0));
+      for (int k = 0; k < iters; ++k)
+        hipLaunchKernelGGL((CopyKernelT<4, true, true>), grid, dim3(256), 0, 0, src, dst, n);
+      HIP_TRY(hipEventRecord(e1, 0));
+      HIP_TRY(hipEventSynchronize(e1));
+      float ms = 0;
+      HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+      HIP_TRY(hipEventDestroy(e0));
+      HIP_TRY(hipEventDestroy(e1));
+      HIP_TRY(hipFree(dst));
+      HIP_TRY(hipSetDevice(j));
+      HIP_TRY(hipFree(src));
+      double gbps = ms > 0 ? (static_cast<double>(n) * sizeof(uint4) * iters) / (ms * 1e-3) / 1e9 : 0.0;
+      snprintf(buf, sizeof(buf), "%s{\"dst\": %d, \"src\": %d, \"gbps\": %.1f}", first ? "" : ", ", i, j, gbps);
+      s += buf;
+      first = false;
+    }
+  }
+  s += "]}";
+  snprintf(out, len, "%s", s.c_str());
+  return 0;
+}
+
 extern "C" int adp_probe_device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return -1;

@@ -196,3 +196,21 @@ def test_dry_run_labels_on_real_gpu(snap):
     assert lab["amd.com/gpu.count"] == "1" and "MI355" in lab["amd.com/gpu.product"]
     assert lab["amd.com/gpu.memory-mib"] == str(snap["gpus"][0]["vram_mib"])
     assert lab["amd.com/gpu.compute-partition"] == snap["gpus"][0]["compute_mode"]
+
+
+def test_probe_p2p_single_gpu_box(probe_built):
+    """--p2p on the one-GPU box: no pairs to measure, nothing touches peer memory, exit 0."""
+    import json
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd.utils.build import PROBE_EXE
+    res = probe_built.p2p()
+    assert res["devices"] >= 1
+    assert len(res["pairs"]) == res["devices"] * (res["devices"] - 1)
+    for p in res["pairs"]:
+        assert "gbps" in p or p.get("no-peer-access")
+    r = subprocess.run([PROBE_EXE, "--device", "0", "--p2p", "--bytes", str(64 << 20)], capture_output=True,
+                       text=True, timeout=120)
+    lines = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert any("pairs" in x for x in lines)
+    if res["devices"] == 1:
+        assert r.returncode == 0, r.stdout + r.stderr
