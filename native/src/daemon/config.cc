@@ -382,8 +382,9 @@ std::string UsageText() {
       "Usage: amdgpu-device-plugin [flags]\n\nFlags:\n";
   Flags defaults;
   for (const auto& d : Table()) {
-    s += "  --" + std::string(d.name) + "  (env " + d.env + ", default " + ValueOf(d, defaults) +
-         ")\n      " + d.help + "\n";
+    s += "  --" + std::string(d.name) + "  (env " + d.env +
+         (*d.file_key ? std::string(", file flags.") + d.file_key : std::string()) + ", default " +
+         ValueOf(d, defaults) + ")\n      " + d.help + "\n";
   }
   s += "  --config-file  (env CONFIG_FILE)\n      versioned YAML/JSON config (version: v1, flags: {...})\n";
   s += "\nCompatibility aliases (reference deployments):\n";
