@@ -76,6 +76,18 @@ def p2p(ndev: int = 0, nbytes: int = 256 << 20, iters: int = 5) -> dict:
     return res
 
 
+def mfma(device: int = 0, iters: int = 1 << 14) -> dict:
+    """bf16 MFMA rate (TFLOP/s) and exactness of every accumulator on `device`."""
+    so = _lib()
+    so.adp_probe_mfma.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    buf = ctypes.create_string_buffer(1 << 12)
+    rc = so.adp_probe_mfma(device, iters, buf, len(buf))
+    res = json.loads(buf.value.decode())
+    if rc != 0:
+        raise ProbeError(res)
+    return res
+
+
 def device_for_bdf(bdf: str) -> int:
     """HIP ordinal of the GPU at PCI address `bdf` ("dddd:bb:dd.f"), function ignored."""
     want = bdf.lower().rsplit(".", 1)[0]

@@ -2,7 +2,7 @@
 //
 //   amdgpu-dp-probe [--list] [--device N] [--bytes B] [--iters I]
 //                   [--expect-xcds X] [--expect-cus C] [--min-gbps G]
-//                   [--p2p [--min-p2p-gbps P]]
+//                   [--p2p [--min-p2p-gbps P]] [--mfma [--min-tflops T]]
 //
 // Runs the visibility probe (visibility_probe.hip) on every visible HIP device
 // (or one) and prints one JSON line per device. Exits non-zero when a device
@@ -12,7 +12,9 @@
 // See examples/pods/pod-validate.yml. --p2p additionally measures xGMI peer-read
 // bandwidth between every pair of the pod's GPUs (a multi-GPU pod placed by the
 // xGMI-aware preferred allocation should see every pair connected); it fails if a
-// pair has no peer access or is below --min-p2p-gbps.
+// pair has no peer access or is below --min-p2p-gbps. --mfma runs the bf16
+// matrix cores flat out (v_mfma_f32_32x32x16_bf16) and checks every result is
+// exact; it fails on a wrong element or a rate below --min-tflops.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -22,6 +24,7 @@ extern "C" int adp_probe_device_count();
 extern "C" int adp_probe_list(char* out, int len);
 extern "C" int adp_probe_run(int device, unsigned long long bytes, int iters, char* out, int len);
 extern "C" int adp_probe_p2p(int ndev, unsigned long long bytes, int iters, char* out, int len);
+extern "C" int adp_probe_mfma(int device, int iters, char* out, int len);
 
 namespace {
 
@@ -43,8 +46,8 @@ int main(int argc, char** argv) {
   int device = -1, iters = 5;
   unsigned long long bytes = 256ull << 20;
   long expect_xcds = -1, expect_cus = -1;
-  double min_gbps = -1, min_p2p_gbps = -1;
-  bool list = false, p2p = false;
+  double min_gbps = -1, min_p2p_gbps = -1, min_tflops = -1;
+  bool list = false, p2p = false, mfma = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : "0"; };
@@ -57,9 +60,12 @@ int main(int argc, char** argv) {
     else if (a == "--min-gbps") min_gbps = atof(next());
     else if (a == "--p2p") p2p = true;
     else if (a == "--min-p2p-gbps") min_p2p_gbps = atof(next());
+    else if (a == "--mfma") mfma = true;
+    else if (a == "--min-tflops") min_tflops = atof(next());
     else {
       fprintf(stderr, "usage: %s [--list] [--device N] [--bytes B] [--iters I] [--expect-xcds X] "
-                      "[--expect-cus C] [--min-gbps G] [--p2p [--min-p2p-gbps P]]\n", argv[0]);
+                      "[--expect-cus C] [--min-gbps G] [--p2p [--min-p2p-gbps P]] [--mfma [--min-tflops T]]\n",
+              argv[0]);
       return 2;
     }
   }
@@ -82,6 +88,12 @@ int main(int argc, char** argv) {
     if (expect_xcds >= 0 && JsonInt(buf, "xccs_seen") != expect_xcds) ++failures;
     if (expect_cus >= 0 && JsonInt(buf, "cus") != expect_cus) ++failures;
     if (min_gbps >= 0 && JsonDouble(buf, "hbm_copy_gbps") < min_gbps) ++failures;
+    if (mfma) {
+      int mrc = adp_probe_mfma(d, 1 << 14, buf, sizeof(buf));
+      printf("%s\n", buf);
+      if (mrc != 0) ++failures;
+      if (min_tflops >= 0 && JsonDouble(buf, "bf16_tflops") < min_tflops) ++failures;
+    }
   }
   if (p2p) {
     int rc = adp_probe_p2p(n, bytes, iters, buf, sizeof(buf));

@@ -121,6 +121,39 @@ __global__ void __launch_bounds__(256) CopyChunkT(const uint4* __restrict__ src,
   for (; i < end; i += blockDim.x) dst[i] = src[i];
 }
 
+// Matrix-core check: every wave keeps CHAINS independent 32x32 f32 accumulators
+// and issues back-to-back v_mfma_f32_32x32x16_bf16 on them (one wave per SIMD,
+// 4 per workgroup, one workgroup per CU), so the MFMA pipes never wait on a
+// dependency. A = B = all ones (exact in bf16), so after n steps every
+// accumulator element must be exactly 16 n -- a wrong element flags a bad
+// matrix core. Rate = waves x iters x CHAINS x 32768 FLOP / time.
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+template <int CHAINS>
+__global__ void __launch_bounds__(256) MfmaKernel(float one, int iters, unsigned int* bad) {
+  bf16x8 a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = static_cast<__bf16>(one);  // runtime value: nothing for the compiler to fold
+    b[j] = static_cast<__bf16>(one);
+  }
+  f32x16 acc[CHAINS];
+#pragma unroll
+  for (int c = 0; c < CHAINS; ++c) acc[c] = f32x16{};
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[c], 0, 0, 0);
+  }
+  const float want = 16.0f * static_cast<float>(iters) * one * one;
+  unsigned int wrong = 0;
+#pragma unroll
+  for (int c = 0; c < CHAINS; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) wrong += acc[c][r] != want;
+  if (wrong) atomicAdd(bad, wrong);
+}
+
 __global__ void __launch_bounds__(256) SumKernel(const uint4* __restrict__ p, size_t n,
                                                  unsigned long long* total) {
   size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
@@ -282,6 +315,44 @@ extern "C" int adp_probe_p2p(int ndev, unsigned long long bytes, int iters, char
   s += "]}";
   snprintf(out, len, "%s", s.c_str());
   return 0;
+}
+
+// bf16 MFMA throughput + exactness on `device` (see MfmaKernel).
+extern "C" int adp_probe_mfma(int device, int iters, char* out, int len) {
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (iters <= 0 || iters > (1 << 20)) iters = 1 << 14;  // 16 n stays exact in f32 up to 2^20
+  constexpr int kChains = 4;
+  unsigned int* d_bad = nullptr;
+  HIP_TRY(hipMalloc(&d_bad, sizeof(unsigned int)));
+  HIP_TRY(hipMemset(d_bad, 0, sizeof(unsigned int)));
+  const dim3 grid(prop.multiProcessorCount), block(256);
+  hipLaunchKernelGGL(MfmaKernel<kChains>, grid, block, 0, 0, 1.0f, 64, d_bad);  // warm-up / clocks up
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemset(d_bad, 0, sizeof(unsigned int)));
+  hipEvent_t e0, e1;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(hipEventRecord(e0, 0));
+  hipLaunchKernelGGL(MfmaKernel<kChains>, grid, block, 0, 0, 1.0f, iters, d_bad);
+  HIP_TRY(hipEventRecord(e1, 0));
+  HIP_TRY(hipEventSynchronize(e1));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  unsigned int bad = 0;
+  HIP_TRY(hipMemcpy(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost));
+  HIP_TRY(hipEventDestroy(e0));
+  HIP_TRY(hipEventDestroy(e1));
+  HIP_TRY(hipFree(d_bad));
+  const double waves = static_cast<double>(grid.x) * (block.x / 64);
+  const double flops = waves * iters * kChains * (2.0 * 32 * 32 * 16);
+  snprintf(out, len,
+           "{\"device\": %d, \"instruction\": \"v_mfma_f32_32x32x16_bf16\", \"waves\": %.0f, "
+           "\"iters\": %d, \"ms\": %.4f, \"bf16_tflops\": %.1f, \"wrong_elements\": %u, \"mfma_ok\": %s}",
+           device, waves, iters, ms, ms > 0 ? flops / (ms * 1e-3) / 1e12 : 0.0, bad, bad == 0 ? "true" : "false");
+  return bad == 0 ? 0 : 1;
 }
 
 extern "C" int adp_probe_device_count() {

@@ -214,3 +214,13 @@ def test_probe_p2p_single_gpu_box(probe_built):
     assert any("pairs" in x for x in lines)
     if res["devices"] == 1:
         assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_probe_mfma_matrix_cores(snap, probe_built):
+    """Every bf16 MFMA result exact; the whole MI355X runs the matrix cores at a
+    large fraction of the ~2.5 PFLOP/s dense bf16 peak."""
+    res = probe_built.mfma(0)
+    assert res["mfma_ok"] and res["wrong_elements"] == 0, res
+    if not snap["gpus"][0]["partitioned"]:
+        assert res["waves"] == 256 * 4
+        assert res["bf16_tflops"] > 1000, res
