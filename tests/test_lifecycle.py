@@ -337,3 +337,15 @@ def test_node_labels_file_for_nfd(scratch):
         assert d.stop() == 0
         k.stop()
     assert not os.path.exists(path)
+
+
+def test_python_cli_report_on_mock(scratch):
+    import sys
+    fx = fixtures.write(fixtures.CONFIGS["mixed8"](), scratch + ".fixture")
+    env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB, AMDSMI_MOCK_FIXTURE=fx, ADP_LOG_LEVEL="error")
+    r = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "report", "--partition-strategy", "mixed",
+                        "--device-plugin-path", scratch], capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0, r.stderr
+    assert "amd.com/cpx-1xcd.36gb" in r.stdout and "amd.com/gpu.count=8" in r.stdout
+    h = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "--help"], capture_output=True, text=True)
+    assert h.returncode == 0 and "validate" in h.stdout
