@@ -224,3 +224,12 @@ def test_probe_mfma_matrix_cores(snap, probe_built):
     if not snap["gpus"][0]["partitioned"]:
         assert res["waves"] == 256 * 4
         assert res["bf16_tflops"] > 1000, res
+
+
+def test_python_cli_validate_on_real_gpu():
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "validate", "--device", "0", "--mfma",
+                        "--bytes", str(128 << 20)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert '"mfma_ok": true' in r.stdout and '"checksum_ok": true' in r.stdout
