@@ -140,8 +140,12 @@ static int OnDataChunk(nghttp2_session* s, uint8_t, int32_t sid, const uint8_t* 
   auto* c = static_cast<ServerConn*>(ud);
   StreamState* st = c->Find(sid);
   if (!st) return 0;
+  if (st->dispatched) return 0;
   if (st->body.size() + len > kMaxRequestBytes) {
     nghttp2_submit_rst_stream(s, NGHTTP2_FLAG_NONE, sid, NGHTTP2_REFUSED_STREAM);
+    st->dispatched = true;  // never hand a truncated request to a handler
+    st->body.clear();
+    st->body.shrink_to_fit();
     return 0;
   }
   st->body.append(reinterpret_cast<const char*>(data), len);

@@ -127,3 +127,13 @@ def test_watchers_vanishing_mid_stream(plugin):
         q.get(timeout=5)
         w.close()  # drop the connection with the stream open
     _still_serving(dm, c, ids)
+
+
+def test_oversized_request_is_refused(plugin):
+    dm, sock, c, ids = plugin
+    ch = grpc.insecure_channel("unix:" + sock, options=[("grpc.max_send_message_length", 64 << 20)])
+    raw = ch.unary_unary("/v1beta1.DevicePlugin/Allocate")
+    with pytest.raises(grpc.RpcError):
+        raw(b"\x0a" + b"\xff" * (17 << 20), timeout=20)
+    ch.close()
+    _still_serving(dm, c, ids)
