@@ -4,7 +4,7 @@ JOBS       ?= 8
 PY         ?= python3
 GPURUN     ?= /usr/local/graft/bin/gpurun
 
-.PHONY: all build probe test test-native test-gpu bench asan tsan tsan-e2e lint image clean
+.PHONY: all build probe test test-native test-gpu bench asan tsan tsan-e2e coverage lint image clean
 
 all: build
 
@@ -51,6 +51,10 @@ tsan-e2e:
 	  $(PY) -m pytest -q -p no:cacheprovider tests/test_e2e_mock.py tests/test_health.py \
 	  tests/test_metrics.py tests/test_lifecycle.py tests/test_robustness.py -k "not additional_ids and not classification"
 	@if ls build/tsan-logs/* >/dev/null 2>&1; then cat build/tsan-logs/*; exit 1; fi
+
+# Line coverage of native/src from the unit, stress and CPU end-to-end suites.
+coverage:
+	$(PY) tools/coverage.py --out build/coverage.txt
 
 lint:
 	@command -v clang-format >/dev/null && find native -name '*.cc' -o -name '*.h' | xargs clang-format --dry-run -Werror || echo "clang-format not installed; skipped"
