@@ -349,3 +349,33 @@ def test_python_cli_report_on_mock(scratch):
     assert "amd.com/cpx-1xcd.36gb" in r.stdout and "amd.com/gpu.count=8" in r.stdout
     h = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "--help"], capture_output=True, text=True)
     assert h.returncode == 0 and "validate" in h.stdout
+
+
+@pytest.mark.parametrize("fixture_name,args", [
+    ("spx8", ["--resource-config", "gpu:gpu-mem-gb:-1"]),
+    ("cpx8", ["--partition-strategy", "single"]),
+    ("mixed8", ["--partition-strategy", "mixed", "--resource-config", "gpu:sharedgpu:3"]),
+])
+def test_device_ids_survive_daemon_restarts(scratch, fixture_name, args):
+    """The kubelet checkpoints allocated IDs across plugin restarts (SURVEY §5,
+    checkpoint/resume): every advertised ID -- replicas and partitions included --
+    must be identical after the daemon is restarted from scratch."""
+    def advertised():
+        k = kubelet.StubKubelet(sock(scratch)).start()
+        d = harness.Daemon(scratch, fixtures.CONFIGS[fixture_name](), args=args).start()
+        try:
+            out = {}
+            regs = 2 if fixture_name == "mixed8" else 1
+            for _ in range(regs):
+                reg = k.wait_registration()
+                c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+                out[reg.resource_name] = sorted(x.ID for x in c.watch()[0].get(timeout=5).devices)
+                c.close()
+            return out
+        finally:
+            assert d.stop() == 0
+            k.stop()
+    first = advertised()
+    second = advertised()
+    assert first == second and all(first.values())
+    assert all(len(i) <= 63 for ids in first.values() for i in ids)
