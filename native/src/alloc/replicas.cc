@@ -1,6 +1,7 @@
 #include "alloc/replicas.h"
 
 #include <algorithm>
+#include <climits>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -116,7 +117,7 @@ Result<Prioritized> PrioritizeDevices(const std::vector<std::string>& available,
 Result<Prioritized> PrioritizeDeviceViews(const std::vector<std::string_view>& available,
                                       const std::vector<std::string_view>& must_include,
                                       int allocation_size, ReplicaPolicy policy,
-                                      std::string_view join) {
+                                      std::string_view join, const DeviceAffinity* affinity) {
   if (allocation_size < 0) return InvalidArgument("negative allocation size");
   if (static_cast<int>(must_include.size()) > allocation_size) {
     return InvalidArgument("mustIncludeDeviceIDs (" + std::to_string(must_include.size()) +
@@ -213,10 +214,28 @@ Result<Prioritized> PrioritizeDeviceViews(const std::vector<std::string_view>& a
       }
     }
     while (need > 0) {
+      // With devices already in the request, only the closest untouched ones
+      // compete (NUMA/xGMI affinity); among those: best fit, else the largest.
+      long best_aff = LONG_MIN;
+      if (affinity) {
+        for (PhysicalPool* p : order) {
+          if (p->allocated || p->size() == 0) continue;
+          long aff = 0;
+          for (PhysicalPool* q : order)
+            if (q->allocated) aff += (*affinity)(p->prefix, q->prefix);
+          best_aff = std::max(best_aff, aff);
+        }
+      }
       PhysicalPool* fit = nullptr;      // smallest pool that fits the remainder
       PhysicalPool* largest = nullptr;  // otherwise drain the largest
       for (PhysicalPool* p : order) {
         if (p->allocated || p->size() == 0) continue;
+        if (affinity) {
+          long aff = 0;
+          for (PhysicalPool* q : order)
+            if (q->allocated) aff += (*affinity)(p->prefix, q->prefix);
+          if (aff < best_aff) continue;
+        }
         size_t n = p->size();
         if (n >= static_cast<size_t>(need) && (!fit || n < fit->size())) fit = p;
         if (!largest || n > largest->size()) largest = p;

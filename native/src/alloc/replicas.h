@@ -21,6 +21,7 @@
 //    as few physical devices as possible, best-fit first (defect B19).
 #pragma once
 
+#include <functional>
 #include <string>
 #include <string_view>
 #include <vector>
@@ -55,11 +56,18 @@ inline constexpr const char* kNonUniqueMessage =
     "having enough physical GPUs";
 
 // Zero-copy variant (views into the request buffer); the daemon's RPC path.
+// Affinity between two physical devices (by ID), higher = closer. Used by the
+// pack policy when a request spans several devices: after the first device,
+// the next one is the closest to those already chosen (NUMA / xGMI), and only
+// then the best fit.
+using DeviceAffinity = std::function<long(std::string_view a, std::string_view b)>;
+
 Result<Prioritized> PrioritizeDeviceViews(const std::vector<std::string_view>& available,
                                       const std::vector<std::string_view>& must_include,
                                       int allocation_size,
                                       ReplicaPolicy policy = ReplicaPolicy::kSpread,
-                                      std::string_view join = kReplicaJoin);
+                                      std::string_view join = kReplicaJoin,
+                                      const DeviceAffinity* affinity = nullptr);
 Result<Prioritized> PrioritizeDevices(const std::vector<std::string>& available,
                                       const std::vector<std::string>& must_include,
                                       int allocation_size,

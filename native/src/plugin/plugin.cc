@@ -124,6 +124,7 @@ void Plugin::BuildUnits() {
   for (size_t i = 0; i < units_.size(); ++i) {
     const auto& u = units_[i];
     unit_by_id_[u.id] = static_cast<int>(i);
+    unit_index_by_id_[u.id] = static_cast<int>(i);  // view into units_[i].id (never modified)
     if (replicated_) {
       LOG_INFO(kComp, "replicating device %s (%s, %llu MiB) %u times", u.id.c_str(), u.index.c_str(),
                static_cast<unsigned long long>(u.vram_mib), u.replicas);
@@ -326,8 +327,16 @@ Status Plugin::PreferredImpl(std::string_view req, std::string* resp) {
   stats_.preferred_calls.Add(1);
   for (const auto& cr : reqs) {
     if (replicated_) {
+      // Multi-device pack requests grow towards the devices already chosen
+      // (same NUMA node / xGMI score), the memory-unit analogue of the
+      // best-effort policy below.
+      alloc::DeviceAffinity affinity = [this](std::string_view a, std::string_view b) -> long {
+        auto ia = unit_index_by_id_.find(a), ib = unit_index_by_id_.find(b);
+        if (ia == unit_index_by_id_.end() || ib == unit_index_by_id_.end()) return 0;
+        return graph_.Score(ia->second, ib->second);
+      };
       auto res = alloc::PrioritizeDeviceViews(cr.available, cr.must_include, cr.allocation_size,
-                                              opts_.replica_policy);
+                                              opts_.replica_policy, alloc::kReplicaJoin, &affinity);
       if (!res.ok()) return res.status();
       if (res->non_unique) LOG_DEBUG(kComp, "ignoring: %s", alloc::kNonUniqueMessage);
       out.container_responses.push_back(std::move(res->ids));

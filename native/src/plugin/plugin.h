@@ -182,6 +182,7 @@ class Plugin {
 
   std::vector<Unit> units_;
   std::unordered_map<std::string, int> unit_by_id_;
+  std::unordered_map<std::string_view, int> unit_index_by_id_;  // keys view units_[i].id
   std::vector<std::string> advertised_;       // advertised IDs (replicas or plain)
   std::vector<int> advertised_unit_;
   // advertised ID -> unit; keys view into advertised_ (never modified after build)

@@ -159,3 +159,24 @@ def test_exact_search_matches_bruteforce_objective():
             t = score(got) + sum(score(x) for x in p)
             total_got = t if total_got is None else max(total_got, t)
         assert (total_got, score(got)) == best, (n, k, req, got, best)
+
+
+def test_pack_spanning_gpus_stays_numa_local(plugin):
+    """A memory-unit request larger than one GPU: after the first GPU, the pack
+    policy continues on a GPU of the same NUMA node (not simply the best fit)."""
+    c, ids = plugin(fixtures.node(8), args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack"])
+    per = fixtures.MI355X_VRAM_MIB // 1000
+
+    def units(gpu, n):
+        prefix = ids[gpu * per].split("-replica-")[0]
+        return [i for i in ids if i.startswith(prefix + "-")][:n]
+    avail = units(0, per) + units(1, 150) + units(5, 120)   # GPU 0,1 on NUMA 0; GPU 5 on NUMA 1
+    got = pref(c, avail, size=per + 106)
+    by_gpu = {}
+    for g in got:
+        by_gpu.setdefault(g.split("-replica-")[0], 0)
+        by_gpu[g.split("-replica-")[0]] += 1
+    gpu1 = ids[1 * per].split("-replica-")[0]
+    gpu5 = ids[5 * per].split("-replica-")[0]
+    assert len(got) == per + 106
+    assert by_gpu.get(gpu1) == 106 and gpu5 not in by_gpu, by_gpu
