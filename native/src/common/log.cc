@@ -6,6 +6,7 @@
 #include <cstring>
 #include <ctime>
 #include <mutex>
+#include <string>
 #include <sys/time.h>
 
 #include "common/status.h"
@@ -24,6 +25,34 @@ LogLevel InitialLevel() {
 
 std::atomic<int> g_level{static_cast<int>(InitialLevel())};
 std::mutex g_mu;
+// ADP_LOG_FORMAT=json: one JSON object per line for log pipelines.
+const bool g_json = [] {
+  const char* e = std::getenv("ADP_LOG_FORMAT");
+  return e && !strcasecmp(e, "json");
+}();
+
+const char* LevelWord(LogLevel l) {
+  switch (l) {
+    case LogLevel::kDebug: return "debug";
+    case LogLevel::kInfo: return "info";
+    case LogLevel::kWarn: return "warn";
+    case LogLevel::kError: return "error";
+  }
+  return "unknown";
+}
+
+std::string JsonStr(const char* s) {
+  std::string o = "\"";
+  for (const char* p = s; *p; ++p) {
+    unsigned char c = static_cast<unsigned char>(*p);
+    if (c == '"' || c == '\\') { o += '\\'; o += static_cast<char>(c); }
+    else if (c == '\n') o += "\\n";
+    else if (c == '\t') o += "\\t";
+    else if (c < 0x20) { char b[8]; snprintf(b, sizeof(b), "\\u%04x", c); o += b; }
+    else o += static_cast<char>(c);
+  }
+  return o + "\"";
+}
 
 const char* LevelName(LogLevel l) {
   switch (l) {
@@ -54,8 +83,12 @@ void Logf(LogLevel l, const char* component, const char* fmt, ...) {
   char ts[32];
   strftime(ts, sizeof(ts), "%Y-%m-%dT%H:%M:%S", &tm);
   std::lock_guard<std::mutex> lk(g_mu);
-  fprintf(stderr, "%s.%06ldZ %s %s: %s\n", ts, static_cast<long>(tv.tv_usec), LevelName(l),
-          component, msg);
+  if (g_json) {
+    fprintf(stderr, "{\"ts\": \"%s.%06ldZ\", \"level\": \"%s\", \"component\": %s, \"msg\": %s}\n", ts,
+            static_cast<long>(tv.tv_usec), LevelWord(l), JsonStr(component).c_str(), JsonStr(msg).c_str());
+  } else {
+    fprintf(stderr, "%s.%06ldZ %s %s: %s\n", ts, static_cast<long>(tv.tv_usec), LevelName(l), component, msg);
+  }
   fflush(stderr);
 }
 

@@ -379,3 +379,19 @@ def test_device_ids_survive_daemon_restarts(scratch, fixture_name, args):
     second = advertised()
     assert first == second and all(first.values())
     assert all(len(i) <= 63 for ids in first.values() for i in ids)
+
+
+def test_json_log_format(scratch):
+    import json
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, env={"ADP_LOG_FORMAT": "json"}).start()
+    try:
+        k.wait_registration()
+        d.wait_log("registered device plugin")
+    finally:
+        assert d.stop() == 0
+        k.stop()
+    recs = [json.loads(line) for line in d.log().splitlines() if line.strip()]
+    assert recs and all({"ts", "level", "component", "msg"} <= set(r) for r in recs)
+    cfg = [r for r in recs if r["msg"].startswith("running with config:")]
+    assert cfg and "\n" in cfg[0]["msg"]  # multi-line messages stay one record
