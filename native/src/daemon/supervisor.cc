@@ -149,7 +149,8 @@ void ArmTimer(int tfd, int ms) {
 
 }  // namespace
 
-int RunDaemon(const Config& cfg) {
+int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload) {
+  Config cfg = startup_cfg;  // replaced on a successful reload
   auto validated = Validate(cfg);
   if (!validated.ok()) {
     LOG_ERROR(kComp, "unable to validate flags: %s", validated.status().message().c_str());
@@ -200,6 +201,17 @@ int RunDaemon(const Config& cfg) {
   }
   if (PathJoin(v.popts.plugin_dir, "") != PathJoin(watch_dir, ""))
     inotify_add_watch(ifd, v.popts.plugin_dir.c_str(), IN_DELETE);
+  // Config file: watch its directory (editors and ConfigMap updates replace the
+  // file rather than writing it in place).
+  int config_wd = -1;
+  std::string config_name;
+  if (reload && !cfg.config_file.empty()) {
+    std::string dir = cfg.config_file.substr(0, cfg.config_file.rfind('/') + 1);
+    if (dir.empty()) dir = ".";
+    config_name = BaseName(cfg.config_file);
+    config_wd = inotify_add_watch(ifd, dir.c_str(), IN_CLOSE_WRITE | IN_MOVED_TO | IN_CREATE);
+    if (config_wd < 0) LOG_WARN(kComp, "cannot watch config file %s: %s", cfg.config_file.c_str(), strerror(errno));
+  }
   int tfd = timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC | TFD_NONBLOCK);
   int efd = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   int lfd = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);  // health monitor: partition layout changed
@@ -354,6 +366,46 @@ int RunDaemon(const Config& cfg) {
     if (!hs.ok()) LOG_WARN(kComp, "health monitor: %s", hs.ToString().c_str());
   };
 
+  // Re-reads flags/env/file; on success adopts the new config (startup-bound
+  // settings excepted). Returns false when the new config is invalid.
+  auto reload_config = [&](const char* why) -> bool {
+    if (!reload) return true;
+    auto next = reload();
+    if (!next.ok()) {
+      LOG_ERROR(kComp, "%s: config not reloaded: %s", why, next.status().message().c_str());
+      return false;
+    }
+    auto nv = Validate(*next);
+    if (!nv.ok()) {
+      LOG_ERROR(kComp, "%s: config not reloaded: %s", why, nv.status().message().c_str());
+      return false;
+    }
+    const Flags& was = cfg.flags;
+    const Flags& now = next->flags;
+    if (now.amdsmi_lib != was.amdsmi_lib || now.metrics_addr != was.metrics_addr ||
+        now.pod_resources_socket != was.pod_resources_socket || now.node_labels_file != was.node_labels_file ||
+        now.plugin_dir != was.plugin_dir || now.kubelet_socket != was.kubelet_socket)
+      LOG_WARN(kComp, "%s: amdsmiLib, metricsAddr, podResourcesSocket, nodeLabelsFile, devicePluginPath and "
+                      "kubeletSocket apply at startup only", why);
+    std::string old_json = cfg.ToJson();
+    Config merged = *next;
+    merged.flags.amdsmi_lib = was.amdsmi_lib;
+    merged.flags.metrics_addr = was.metrics_addr;
+    merged.flags.pod_resources_socket = was.pod_resources_socket;
+    merged.flags.node_labels_file = was.node_labels_file;
+    merged.flags.plugin_dir = was.plugin_dir;
+    merged.flags.kubelet_socket = was.kubelet_socket;
+    auto mv = Validate(merged);
+    if (!mv.ok()) return false;
+    if (merged.ToJson() != old_json) {
+      cfg = std::move(merged);
+      v = std::move(*mv);
+      LOG_INFO(kComp, "%s: reloaded config:\n%s", why, cfg.ToJson().c_str());
+      LOG_INFO(kComp, "running with resource config: %s", v.rc.ToJson().c_str());
+    }
+    return true;
+  };
+
   restart();
   while (!quit) {
     epoll_event events[8];
@@ -392,6 +444,17 @@ int RunDaemon(const Config& cfg) {
         while ((len = read(ifd, buf, sizeof(buf))) > 0) {
           for (char* p = buf; p < buf + len;) {
             auto* e = reinterpret_cast<inotify_event*>(p);
+            if (config_wd >= 0 && e->wd == config_wd && e->len &&
+                (config_name == e->name || std::string(e->name) == "..data")) {
+              LOG_INFO(kComp, "inotify: config file %s changed", cfg.config_file.c_str());
+              std::string before = cfg.ToJson();
+              if (reload_config("config file changed") && cfg.ToJson() != before) {
+                reinit = true;
+                do_restart = true;
+              }
+              p += sizeof(inotify_event) + e->len;
+              continue;
+            }
             if (e->len && kubelet_name == e->name && (e->mask & (IN_CREATE | IN_MOVED_TO))) {
               LOG_INFO(kComp, "inotify: %s created, restarting", kubelet_sock.c_str());
               backoff_ms = 1000;
@@ -417,6 +480,7 @@ int RunDaemon(const Config& cfg) {
         while (read(sfd, &si, sizeof(si)) == sizeof(si)) {
           if (si.ssi_signo == SIGHUP) {
             LOG_INFO(kComp, "received SIGHUP, restarting");
+            reload_config("SIGHUP");
             reinit = true;
             do_restart = true;
           } else if (si.ssi_signo == SIGUSR1) {

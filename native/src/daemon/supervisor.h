@@ -12,13 +12,23 @@
 // that gRPC servers use to report an exhausted crash budget. Plugin start
 // failures restart with exponential backoff (1 s .. 30 s) instead of
 // immediately (defect B17). SIGUSR1 dumps per-plugin RPC counters.
+//
+// Config reload: on SIGHUP, and whenever the config file (--config-file; a
+// ConfigMap mount's atomic `..data` swap included) changes, `reload` re-reads
+// command line + environment + file. A valid new config replaces the running
+// one (strategy, resourceConfig, list/ID strategies, replica policy, devices,
+// ...) and the plugins restart with it; an invalid one is logged and ignored.
+// Settings bound at startup (amdsmi library, metrics address, PodResources
+// socket, node-labels file) keep their original values.
 #pragma once
+
+#include <functional>
 
 #include "daemon/config.h"
 
 namespace adp::daemon {
 
 // Runs the daemon until a terminating signal. Returns the process exit code.
-int RunDaemon(const Config& cfg);
+int RunDaemon(const Config& cfg, std::function<Result<Config>()> reload = nullptr);
 
 }  // namespace adp::daemon

@@ -395,3 +395,74 @@ def test_json_log_format(scratch):
     assert recs and all({"ts", "level", "component", "msg"} <= set(r) for r in recs)
     cfg = [r for r in recs if r["msg"].startswith("running with config:")]
     assert cfg and "\n" in cfg[0]["msg"]  # multi-line messages stay one record
+
+
+def test_config_file_changes_are_applied_live(scratch):
+    """Editing the config file (atomic replace, like a ConfigMap update) reloads
+    it and re-registers with the new resources; a broken edit is ignored."""
+    cfg_dir = scratch + ".fixture"
+    os.makedirs(cfg_dir, exist_ok=True)
+    path = os.path.join(cfg_dir, "config.yaml")
+
+    def write(body):
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(body)
+        os.rename(tmp, path)
+    write("version: v1\nflags:\n  resourceConfig: gpu:sharedgpu:2\n")
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, args=["--config-file", path]).start()
+    try:
+        reg = k.wait_registration()
+        assert reg.resource_name == "amd.com/sharedgpu"
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        assert len(c.watch()[0].get(timeout=5).devices) == 4
+        c.close()
+        write("version: v1\nflags:\n  resourceConfig: gpu:sharedgpu:3\n")
+        reg = k.wait_registration(10)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        assert len(c.watch()[0].get(timeout=5).devices) == 6
+        c.close()
+        write("version: v2\n")  # invalid: logged, running config kept
+        d.wait_log("config not reloaded")
+        write("version: v1\nflags:\n  resourceConfig: gpu:timeshared:1\n")
+        assert k.wait_registration(10).resource_name == "amd.com/timeshared"
+        # SIGHUP re-reads too (environment / flags / file)
+        write("version: v1\nflags:\n  resourceConfig: gpu:sharedgpu:5\n  deviceIDStrategy: index\n")
+        reg = k.wait_registration(10)
+        assert reg.resource_name == "amd.com/sharedgpu"
+        d.signal(signal.SIGHUP)
+        reg = k.wait_registration(10)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        assert len(c.watch()[0].get(timeout=5).devices) == 10
+        c.close()
+        assert "reloaded config" in d.log()
+    finally:
+        assert d.stop() == 0
+        k.stop()
+
+
+def test_configmap_style_update_is_applied(scratch):
+    """Kubernetes updates a mounted ConfigMap by swapping the `..data` symlink."""
+    cm = scratch + ".cm"
+    os.makedirs(cm, exist_ok=True)
+
+    def publish(n, body):
+        ts = os.path.join(cm, f"..ts{n}")
+        os.makedirs(ts)
+        with open(os.path.join(ts, "config.yaml"), "w") as f:
+            f.write(body)
+        tmp = os.path.join(cm, "..data_tmp")
+        os.symlink(f"..ts{n}", tmp)
+        os.rename(tmp, os.path.join(cm, "..data"))
+    publish(1, "version: v1\nflags:\n  resourceConfig: gpu:sharedgpu:2\n")
+    os.symlink("..data/config.yaml", os.path.join(cm, "config.yaml"))
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, args=["--config-file", os.path.join(cm, "config.yaml")]).start()
+    try:
+        assert k.wait_registration().resource_name == "amd.com/sharedgpu"
+        publish(2, "version: v1\nflags:\n  resourceConfig: gpu:cmgpu:2\n")
+        assert k.wait_registration(10).resource_name == "amd.com/cmgpu"
+    finally:
+        assert d.stop() == 0
+        k.stop()
