@@ -31,13 +31,13 @@ bench: build
 # Sanitizer builds of the native unit + stress tests (host code only).
 asan:
 	cmake -S native -B build/asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DADP_SANITIZE=ON >/dev/null
-	ninja -C build/asan -j$(JOBS) adp_unit_tests adp_stress
+	ninja -C build/asan -j$(JOBS) adp_unit_tests adp_stress amdsmi_mock
 	ASAN_OPTIONS=detect_leaks=1 build/asan/adp_unit_tests
 	build/asan/adp_stress
 
 tsan:
 	cmake -S native -B build/tsan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DADP_TSAN=ON >/dev/null
-	ninja -C build/tsan -j$(JOBS) adp_unit_tests adp_stress
+	ninja -C build/tsan -j$(JOBS) adp_unit_tests adp_stress amdsmi_mock
 	TSAN_OPTIONS=halt_on_error=1 build/tsan/adp_unit_tests
 	TSAN_OPTIONS=halt_on_error=1 build/tsan/adp_stress
 
