@@ -89,8 +89,8 @@ class NativeKubelet:
         self.wait(lambda e: e.get("event") == "listening", 10)
         return self
 
-    def wait(self, pred, timeout=10.0):
-        """Returns the first event (old or new) matching `pred`.
+    def wait(self, pred, timeout=10.0, since=0):
+        """Returns the first event (old or new, from index `since` on) matching `pred`.
 
         Reads the pipe with os.read on the raw fd: a buffered readline() after
         select() can strand a second line in Python's buffer where select() no
@@ -99,7 +99,7 @@ class NativeKubelet:
         import json
         import select
         deadline = time.time() + timeout
-        for e in self.events:
+        for e in self.events[since:]:
             if pred(e):
                 return e
         fd = self.proc.stdout.fileno()

@@ -1,0 +1,131 @@
+"""Soak test: the daemon under continuous pod churn, periodic SIGHUP restarts,
+kubelet restarts and metric scrapes; samples its RSS, open fds and threads.
+
+  python tools/soak.py [--seconds 300] [--clients 4] [--real] [--out soak.json]
+
+Prints one progress line per sample (every 10 s) and a final JSON summary with
+pods served, restarts, and first/last/max RSS/fds/threads. Exit code 1 if the
+daemon died, RSS grew by more than --max-rss-growth-mib, or fds/threads leaked.
+"""
+
+import argparse
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+import urllib.request
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from k8s_gpu_sharing_plugin_amd import KUBELET_STUB  # noqa: E402
+from k8s_gpu_sharing_plugin_amd.models import fixtures  # noqa: E402
+from k8s_gpu_sharing_plugin_amd.utils import harness  # noqa: E402
+
+
+def proc_stats(pid):
+    rss = threads = 0
+    with open(f"/proc/{pid}/status") as f:
+        for line in f:
+            if line.startswith("VmRSS:"):
+                rss = int(line.split()[1]) // 1024
+            elif line.startswith("Threads:"):
+                threads = int(line.split()[1])
+    fds = len(os.listdir(f"/proc/{pid}/fd"))
+    return {"rss_mib": rss, "fds": fds, "threads": threads}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=int, default=300)
+    ap.add_argument("--clients", type=int, default=4)
+    ap.add_argument("--real", action="store_true")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--max-rss-growth-mib", type=int, default=16)
+    a = ap.parse_args()
+    d = harness.scratch_dir("adpsoak")
+    ksock = os.path.join(d, "kubelet.sock")
+    kub = harness.NativeKubelet(ksock).start()
+    import socket
+    with socket.socket() as s0:  # a free port for the metrics endpoint
+        s0.bind(("127.0.0.1", 0))
+        port = s0.getsockname()[1]
+    args = ["--metrics-addr", f"127.0.0.1:{port}", "--resource-config", "gpu:gpu:4"]
+    if a.real:
+        args += ["--devices", "0"]
+    dm = harness.Daemon(d, None if a.real else fixtures.node(8), args=args, real_smi=a.real,
+                        env={"ADP_LOG_LEVEL": "warn", "DP_HEALTH_POLL_MS": "200"}).start()
+    samples, pods, hups, kubelet_restarts, scrapes = [], 0, 0, 0, 0
+    ok = True
+    t_end = time.time() + a.seconds
+    next_sample = time.time()
+    try:
+        reg = kub.wait(lambda e: e.get("event") == "register", 30)
+        sock = os.path.join(d, reg["endpoint"])
+        round_no = 0
+        while time.time() < t_end:
+            round_no += 1
+            procs = [subprocess.Popen([KUBELET_STUB, "bench", "--socket", sock, "--pods", "3000", "--warmup", "0",
+                                       "--rank", str(r), "--world", str(a.clients)],
+                                      stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+                     for r in range(a.clients)]
+            for p in procs:
+                out, _ = p.communicate(timeout=120)
+                if p.returncode == 0 and out.strip():
+                    pods += json.loads(out)["pods"]
+            if dm.proc.poll() is not None:
+                ok = False
+                print("daemon died", flush=True)
+                break
+            # every 5th round: SIGHUP (full restart); every 7th: kubelet restart
+            if round_no % 5 == 0:
+                mark = len(kub.events)
+                dm.signal(signal.SIGHUP)
+                hups += 1
+                reg = kub.wait(lambda e: e.get("event") == "register", 30, since=mark)
+            if round_no % 7 == 0:
+                kub.stop()
+                kub = harness.NativeKubelet(ksock).start()
+                kubelet_restarts += 1
+                reg = kub.wait(lambda e: e.get("event") == "register", 30)
+            sock = os.path.join(d, reg["endpoint"])
+            with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
+                r.read()
+            scrapes += 1
+            if time.time() >= next_sample:
+                s = proc_stats(dm.proc.pid)
+                s.update({"t": round(a.seconds - (t_end - time.time()), 1), "pods": pods})
+                samples.append(s)
+                print(json.dumps(s), flush=True)
+                next_sample = time.time() + 10
+    finally:
+        code = dm.stop()
+        kub.stop()
+    if code not in (0, None):
+        ok = False
+    warm = samples[min(2, len(samples) - 1)] if samples else {}
+    last = samples[-1] if samples else {}
+    summary = {
+        "seconds": a.seconds, "clients": a.clients, "real_amdsmi": a.real, "pods": pods, "sighups": hups,
+        "kubelet_restarts": kubelet_restarts, "metric_scrapes": scrapes, "samples": len(samples),
+        "rss_mib_after_warmup": warm.get("rss_mib"), "rss_mib_last": last.get("rss_mib"),
+        "rss_mib_max": max((s["rss_mib"] for s in samples), default=None),
+        "fds_after_warmup": warm.get("fds"), "fds_last": last.get("fds"),
+        "threads_after_warmup": warm.get("threads"), "threads_last": last.get("threads"),
+        "exit_code": code,
+    }
+    if samples and last["rss_mib"] - warm["rss_mib"] > a.max_rss_growth_mib:
+        ok = False
+    if samples and (last["fds"] > warm["fds"] + 4 or last["threads"] > warm["threads"] + 2):
+        ok = False
+    summary["ok"] = ok
+    print(json.dumps(summary), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"summary": summary, "samples": samples}, f, indent=1)
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
