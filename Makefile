@@ -4,7 +4,7 @@ JOBS       ?= 8
 PY         ?= python3
 GPURUN     ?= /usr/local/graft/bin/gpurun
 
-.PHONY: all build probe test test-native test-gpu bench asan tsan tsan-e2e coverage lint image clean
+.PHONY: all build probe test test-native test-gpu bench asan tsan tsan-e2e asan-e2e coverage lint image clean
 
 all: build
 
@@ -51,6 +51,17 @@ tsan-e2e:
 	  $(PY) -m pytest -q -p no:cacheprovider tests/test_e2e_mock.py tests/test_health.py \
 	  tests/test_metrics.py tests/test_lifecycle.py tests/test_robustness.py -k "not additional_ids and not classification"
 	@if ls build/tsan-logs/* >/dev/null 2>&1; then cat build/tsan-logs/*; exit 1; fi
+
+# The daemon under ASan/UBSan/LSan, driven by the same end-to-end suites.
+asan-e2e:
+	cmake -S native -B build/asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DADP_SANITIZE=ON >/dev/null
+	ninja -C build/asan -j$(JOBS) amdgpu-device-plugin amdgpu-dp-kubelet amdsmi_mock
+	rm -rf build/asan-logs && mkdir -p build/asan-logs
+	ADP_BUILD_DIR=$(CURDIR)/build/asan ASAN_OPTIONS=log_path=$(CURDIR)/build/asan-logs/daemon:detect_leaks=1 \
+	  UBSAN_OPTIONS=print_stacktrace=1:log_path=$(CURDIR)/build/asan-logs/ubsan \
+	  $(PY) -m pytest -q -p no:cacheprovider tests/test_e2e_mock.py tests/test_health.py \
+	  tests/test_metrics.py tests/test_lifecycle.py tests/test_robustness.py -k "not additional_ids and not classification"
+	@if ls build/asan-logs/* >/dev/null 2>&1; then cat build/asan-logs/*; exit 1; fi
 
 # Line coverage of native/src from the unit, stress and CPU end-to-end suites.
 coverage:

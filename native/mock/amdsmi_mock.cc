@@ -241,7 +241,13 @@ extern "C" {
 amdsmi_status_t amdsmi_init(uint64_t) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!Load()) return AMDSMI_STATUS_INIT_ERROR;
-  return static_cast<amdsmi_status_t>(g->init_status);
+  auto st = static_cast<amdsmi_status_t>(g->init_status);
+  if (st != AMDSMI_STATUS_SUCCESS) {  // a failed init leaves nothing to shut down
+    if (g->fifo_fd >= 0) close(g->fifo_fd);
+    delete g;
+    g = nullptr;
+  }
+  return st;
 }
 
 amdsmi_status_t amdsmi_shut_down(void) {
