@@ -122,16 +122,17 @@ __global__ void __launch_bounds__(256) CopyChunkT(const uint4* __restrict__ src,
 }
 
 // Matrix-core check: every wave keeps CHAINS independent 32x32 f32 accumulators
-// and issues back-to-back v_mfma_f32_32x32x16_bf16 on them (one wave per SIMD,
-// 4 per workgroup, one workgroup per CU), so the MFMA pipes never wait on a
-// dependency. A = B = all ones (exact in bf16), so after n steps every
+// and issues back-to-back v_mfma_f32_32x32x16_bf16 on them (two waves per SIMD,
+// 8 per workgroup, one workgroup per CU), so the MFMA pipes never wait on a
+// dependency. Shape from tools/hip/mfma_sweep.hip on the MI355X: 4 chains x 2
+// waves/SIMD 2.35 PF/s vs 2.18 with one wave per SIMD; 8 chains spill. A = B = all ones (exact in bf16), so after n steps every
 // accumulator element must be exactly 16 n -- a wrong element flags a bad
 // matrix core. Rate = waves x iters x CHAINS x 32768 FLOP / time.
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
 template <int CHAINS>
-__global__ void __launch_bounds__(256) MfmaKernel(float one, int iters, unsigned int* bad) {
+__global__ void __launch_bounds__(512) MfmaKernel(float one, int iters, unsigned int* bad) {
   bf16x8 a, b;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -327,7 +328,7 @@ extern "C" int adp_probe_mfma(int device, int iters, char* out, int len) {
   unsigned int* d_bad = nullptr;
   HIP_TRY(hipMalloc(&d_bad, sizeof(unsigned int)));
   HIP_TRY(hipMemset(d_bad, 0, sizeof(unsigned int)));
-  const dim3 grid(prop.multiProcessorCount), block(256);
+  const dim3 grid(prop.multiProcessorCount), block(512);
   hipLaunchKernelGGL(MfmaKernel<kChains>, grid, block, 0, 0, 1.0f, 64, d_bad);  // warm-up / clocks up
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipDeviceSynchronize());

@@ -222,7 +222,7 @@ def test_probe_mfma_matrix_cores(snap, probe_built):
     res = probe_built.mfma(0)
     assert res["mfma_ok"] and res["wrong_elements"] == 0, res
     if not snap["gpus"][0]["partitioned"]:
-        assert res["waves"] == 256 * 4
+        assert res["waves"] == 256 * 8
         assert res["bf16_tflops"] > 1000, res
 
 
