@@ -133,33 +133,50 @@ struct ExactSearch {
   }
 };
 
+// Flat-array form (parents are small dense indices): no maps/sets on the RPC
+// path. Selection order is fixed by parent index and available-device order,
+// so the result is deterministic.
 std::vector<int> Hierarchical(const DeviceGraph& g, const std::vector<int>& avail,
                               const std::vector<int>& required, int size) {
-  std::set<int> chosen(required.begin(), required.end());
-  std::map<int, std::vector<int>> remaining;  // parent -> unchosen available devices
-  std::map<int, int> rep;                     // parent -> representative device
+  int np = 0;
+  for (int d : avail) np = std::max(np, g.parent(d) + 1);
+  // Unchosen available devices grouped by parent (counting sort keeps avail order).
+  std::vector<int> begin(np + 1, 0), rep(np, -1);
+  std::vector<char> is_req(g.size(), 0), in_set(np, 0);
+  for (int d : required) is_req[d] = 1;
   for (int d : avail) {
-    rep.emplace(g.parent(d), d);
-    if (!chosen.count(d)) remaining[g.parent(d)].push_back(d);
+    int p = g.parent(d);
+    if (rep[p] < 0) rep[p] = d;
+    if (!is_req[d]) ++begin[p + 1];
   }
-  std::set<int> parents;
-  for (int d : required) parents.insert(g.parent(d));
-  int need = size - static_cast<int>(chosen.size());
+  for (int p = 0; p < np; ++p) begin[p + 1] += begin[p];
+  std::vector<int> devs(begin[np]), fill(begin.begin(), begin.end() - 1);
+  for (int d : avail)
+    if (!is_req[d]) devs[fill[g.parent(d)]++] = d;
+  std::vector<int> next(begin.begin(), begin.end() - 1);  // first untaken per parent
+  auto remaining = [&](int p) { return begin[p + 1] - next[p]; };
 
+  std::vector<int> chosen(required.begin(), required.end());
+  std::vector<int> parents;  // parents in the set, in insertion order
+  for (int d : required) {
+    int p = g.parent(d);
+    if (!in_set[p]) { in_set[p] = 1; parents.push_back(p); }
+  }
+  int need = size - static_cast<int>(chosen.size());
   auto take = [&](int p) {
-    auto& v = remaining[p];
-    while (need > 0 && !v.empty()) {
-      chosen.insert(v.front());
-      v.erase(v.begin());
+    while (need > 0 && next[p] < begin[p + 1]) {
+      chosen.push_back(devs[next[p]++]);
       --need;
     }
-    parents.insert(p);
+    if (!in_set[p]) { in_set[p] = 1; parents.push_back(p); }
   };
 
-  // 1. Finish on the GPUs the required devices already occupy (most room first).
-  std::vector<int> req_parents(parents.begin(), parents.end());
+  // 1. Finish on the GPUs the required devices already occupy (most room first,
+  //    ties by parent index).
+  std::vector<int> req_parents(parents);
+  std::sort(req_parents.begin(), req_parents.end());
   std::stable_sort(req_parents.begin(), req_parents.end(),
-                   [&](int a, int b) { return remaining[a].size() > remaining[b].size(); });
+                   [&](int a, int b) { return remaining(a) > remaining(b); });
   for (int p : req_parents) take(p);
 
   // 2. Grow: affinity to the GPUs already chosen, then best fit, then index.
@@ -167,29 +184,31 @@ std::vector<int> Hierarchical(const DeviceGraph& g, const std::vector<int>& avai
     int best = -1;
     long best_aff = LONG_MIN;
     bool best_fits = false;
-    size_t best_room = 0;
-    for (auto& [p, v] : remaining) {
-      if (v.empty() || parents.count(p)) continue;
+    int best_room = 0;
+    for (int p = 0; p < np; ++p) {
+      int room = remaining(p);
+      if (room == 0 || in_set[p]) continue;
       long aff = 0;
       for (int q : parents) aff += g.Score(rep[p], rep[q]);
-      bool fits = v.size() >= static_cast<size_t>(need);
+      bool fits = room >= need;
       bool better;
       if (best < 0) better = true;
       else if (aff != best_aff) better = aff > best_aff;
       else if (fits != best_fits) better = fits;
-      else if (fits) better = v.size() < best_room;   // best fit: tightest hole
-      else better = v.size() > best_room;             // else: biggest chunk first
+      else if (fits) better = room < best_room;   // best fit: tightest hole
+      else better = room > best_room;             // else: biggest chunk first
       if (better) {
         best = p;
         best_aff = aff;
         best_fits = fits;
-        best_room = v.size();
+        best_room = room;
       }
     }
     if (best < 0) return {};
     take(best);
   }
-  return std::vector<int>(chosen.begin(), chosen.end());
+  std::sort(chosen.begin(), chosen.end());
+  return chosen;
 }
 
 }  // namespace
@@ -209,9 +228,11 @@ std::vector<int> BestEffortAllocate(const DeviceGraph& g, const std::vector<int>
   for (int d : avail)
     if (d < 0 || d >= g.size()) return {};
 
-  std::set<int> parents;
-  for (int d : avail) parents.insert(g.parent(d));
-  bool distinct = parents.size() == avail.size();
+  std::vector<int> ps;
+  ps.reserve(avail.size());
+  for (int d : avail) ps.push_back(g.parent(d));
+  std::sort(ps.begin(), ps.end());
+  bool distinct = std::adjacent_find(ps.begin(), ps.end()) == ps.end();
   if (distinct && avail.size() <= static_cast<size_t>(kExactMax)) {
     // k == 1: every split scores 0, so the objective picks the required device or
     // the first available one -- skip the search.

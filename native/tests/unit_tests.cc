@@ -10,6 +10,8 @@
 #include <atomic>
 #include <cstdio>
 #include <functional>
+#include <climits>
+#include <map>
 #include <mutex>
 #include <set>
 #include <string>
@@ -198,6 +200,107 @@ static void TestProto() {
 
   pb::AllocateRequest bad;
   CHECK(!pb::Decode(std::string("\x0a\x05\x0a\x09", 4), &bad).ok());  // truncated
+}
+
+// The original map/set implementation of the hierarchical (partition) policy,
+// kept as the oracle for the flat-array one in alloc/topology.cc.
+static std::vector<int> OracleHierarchical(const alloc::DeviceGraph& g, const std::vector<int>& avail,
+                              const std::vector<int>& required, int size) {
+  std::set<int> chosen(required.begin(), required.end());
+  std::map<int, std::vector<int>> remaining;  // parent -> unchosen available devices
+  std::map<int, int> rep;                     // parent -> representative device
+  for (int d : avail) {
+    rep.emplace(g.parent(d), d);
+    if (!chosen.count(d)) remaining[g.parent(d)].push_back(d);
+  }
+  std::set<int> parents;
+  for (int d : required) parents.insert(g.parent(d));
+  int need = size - static_cast<int>(chosen.size());
+
+  auto take = [&](int p) {
+    auto& v = remaining[p];
+    while (need > 0 && !v.empty()) {
+      chosen.insert(v.front());
+      v.erase(v.begin());
+      --need;
+    }
+    parents.insert(p);
+  };
+
+  // 1. Finish on the GPUs the required devices already occupy (most room first).
+  std::vector<int> req_parents(parents.begin(), parents.end());
+  std::stable_sort(req_parents.begin(), req_parents.end(),
+                   [&](int a, int b) { return remaining[a].size() > remaining[b].size(); });
+  for (int p : req_parents) take(p);
+
+  // 2. Grow: affinity to the GPUs already chosen, then best fit, then index.
+  while (need > 0) {
+    int best = -1;
+    long best_aff = LONG_MIN;
+    bool best_fits = false;
+    size_t best_room = 0;
+    for (auto& [p, v] : remaining) {
+      if (v.empty() || parents.count(p)) continue;
+      long aff = 0;
+      for (int q : parents) aff += g.Score(rep[p], rep[q]);
+      bool fits = v.size() >= static_cast<size_t>(need);
+      bool better;
+      if (best < 0) better = true;
+      else if (aff != best_aff) better = aff > best_aff;
+      else if (fits != best_fits) better = fits;
+      else if (fits) better = v.size() < best_room;   // best fit: tightest hole
+      else better = v.size() > best_room;             // else: biggest chunk first
+      if (better) {
+        best = p;
+        best_aff = aff;
+        best_fits = fits;
+        best_room = v.size();
+      }
+    }
+    if (best < 0) return {};
+    take(best);
+  }
+  return std::vector<int>(chosen.begin(), chosen.end());
+}
+
+// Randomised differential test: partition graphs always take the hierarchical
+// path; every result must equal the oracle's.
+static void TestHierarchicalMatchesOracle() {
+  g_case = "topology/hierarchical-differential";
+  uint64_t seed = 0x9e3779b97f4a7c15ull;
+  auto rnd = [&](int n) {
+    seed ^= seed << 13; seed ^= seed >> 7; seed ^= seed << 17;
+    return static_cast<int>(seed % static_cast<uint64_t>(n));
+  };
+  int mismatches = 0, cases = 0;
+  for (int iter = 0; iter < 3000; ++iter) {
+    int gpus = 1 + rnd(8), per = 1 + rnd(8), n = gpus * per;
+    std::vector<int> parent(n), score(n * n);
+    for (int i = 0; i < n; ++i) parent[i] = i / per;
+    std::vector<int> gscore(gpus * gpus);
+    for (int a = 0; a < gpus; ++a)
+      for (int b = a; b < gpus; ++b) gscore[a * gpus + b] = gscore[b * gpus + a] = 100 + 10 * rnd(3);
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j)
+        score[i * n + j] = i == j ? 0 : parent[i] == parent[j] ? 1000 : gscore[parent[i] * gpus + parent[j]];
+    alloc::DeviceGraph g(parent, score);
+    std::vector<int> avail, req;
+    for (int i = 0; i < n; ++i)
+      if (rnd(4)) avail.push_back(i);
+    if (avail.empty()) continue;
+    for (int d : avail)
+      if (rnd(10) == 0) req.push_back(d);
+    int size = static_cast<int>(req.size()) + rnd(static_cast<int>(avail.size() - req.size()) + 1);
+    if (size <= 0) continue;
+    bool distinct = per == 1;
+    if (distinct && avail.size() <= 12) continue;  // exact path, covered elsewhere
+    ++cases;
+    auto got = alloc::BestEffortAllocate(g, avail, req, size);
+    auto want = OracleHierarchical(g, avail, req, size);
+    if (got != want) ++mismatches;
+  }
+  CHECK(cases > 1000);
+  CHECK(mismatches == 0);
 }
 
 static void TestTopology() {
@@ -477,6 +580,7 @@ int main() {
   TestResourceConfig();
   TestProto();
   TestTopology();
+  TestHierarchicalMatchesOracle();
   TestConfig();
   TestGrpcLoopback();
   TestGrpcMultiLoop();
