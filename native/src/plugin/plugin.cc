@@ -148,6 +148,8 @@ void Plugin::BuildUnits() {
   pb::Encode(kfd, &kb);
   pb::PutLen(&kfd_spec_bytes_, 3, kb);
   graph_ = alloc::DeviceGraph(*snap_, spec_.devices);
+  if (!replicated_ && units_.size() <= 8)
+    best_effort_cache_.reset(new std::atomic<uint16_t>[256u * 256u * 9u]());
   healthy_.assign(units_.size(), 1);
   RebuildListAndWatch();
 }
@@ -358,12 +360,41 @@ Status Plugin::PreferredImpl(std::string_view req, std::string* resp) {
       must.push_back(it->second);
     }
     std::vector<std::string> ids;
-    for (int u : alloc::BestEffortAllocate(graph_, avail, must, cr.allocation_size))
+    for (int u : CachedBestEffort(avail, must, cr.allocation_size))
       ids.push_back(units_[u].id);  // advertised ID (no replica suffix here), fixes B6
     out.container_responses.push_back(std::move(ids));
   }
   pb::Encode(out, resp);
   return Status::Ok();
+}
+
+std::vector<int> Plugin::CachedBestEffort(const std::vector<int>& avail, const std::vector<int>& must,
+                                          int size) {
+  // Up to 8 devices the answer is a pure function of (available set, required
+  // set, size) over an immutable graph: 256 x 256 x 9 entries of 16 bits,
+  // filled lazily (0 = not computed, else 1 + result mask, kEmpty = no answer).
+  constexpr int kMax = 8;
+  constexpr uint16_t kEmpty = 0x200;
+  const int n = static_cast<int>(units_.size());
+  if (n > kMax || size < 0 || size > kMax || !best_effort_cache_)
+    return alloc::BestEffortAllocate(graph_, avail, must, size);
+  uint32_t am = 0, rm = 0;
+  for (int u : avail) am |= 1u << u;
+  for (int u : must) rm |= 1u << u;
+  if ((rm & ~am) != 0) return {};
+  std::atomic<uint16_t>& slot = best_effort_cache_[(am * 256u + rm) * (kMax + 1) + static_cast<uint32_t>(size)];
+  uint16_t v = slot.load(std::memory_order_relaxed);
+  if (v == 0) {
+    std::vector<int> r = alloc::BestEffortAllocate(graph_, avail, must, size);
+    uint32_t mask = 0;
+    for (int u : r) mask |= 1u << u;
+    v = r.empty() ? kEmpty : static_cast<uint16_t>(1 + mask);
+    slot.store(v, std::memory_order_relaxed);  // racing writers store the same value
+  }
+  std::vector<int> out;
+  if (v == kEmpty) return out;
+  for (uint32_t m = v - 1u; m; m &= m - 1) out.push_back(__builtin_ctz(m));
+  return out;
 }
 
 Status Plugin::Register() {

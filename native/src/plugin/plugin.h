@@ -160,6 +160,7 @@ class Plugin {
  private:
   void BuildUnits();
   Status PreferredImpl(std::string_view req, std::string* resp);
+  std::vector<int> CachedBestEffort(const std::vector<int>& avail, const std::vector<int>& must, int size);
   void RebuildListAndWatch();
   bool ApplyHealth(const std::vector<int>& units, bool healthy, const std::string& reason);
   void PostHealth(std::vector<int> units, bool healthy, const std::string& reason);
@@ -189,6 +190,8 @@ class Plugin {
   std::unordered_map<std::string_view, int> advertised_index_;
   std::string kfd_spec_bytes_;
   alloc::DeviceGraph graph_;
+  // Memoised best-effort answers for <= 8 whole devices (see CachedBestEffort).
+  std::unique_ptr<std::atomic<uint16_t>[]> best_effort_cache_;
 
   struct LawSnapshot {
     uint64_t version = 0;

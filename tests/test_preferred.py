@@ -180,3 +180,41 @@ def test_pack_spanning_gpus_stays_numa_local(plugin):
     gpu5 = ids[5 * per].split("-replica-")[0]
     assert len(got) == per + 106
     assert by_gpu.get(gpu1) == 106 and gpu5 not in by_gpu, by_gpu
+
+
+def test_memoised_answers_match_fresh_computation(plugin, scratch):
+    """<= 8 whole GPUs: answers are memoised per (available, required, size).
+    Replayed requests, and the same requests to a fresh daemon (empty cache),
+    must give identical answers."""
+    import random
+    fx = fixtures.node(8)
+    fx["gpus"][2]["xgmi_links_down"] = 2
+    fx["gpus"][6]["xgmi_links_down"] = 1
+    rnd = random.Random(11)
+    c, ids = plugin(fx)
+    reqs = []
+    for _ in range(40):
+        avail = sorted(rnd.sample(ids, rnd.randint(1, 8)))
+        k = rnd.randint(1, len(avail))
+        must = rnd.sample(avail, rnd.randint(0, min(2, k)))
+        reqs.append((avail, must, k))
+    first = [pref(c, a, m, k) for a, m, k in reqs]
+    again = [pref(c, a, m, k) for a, m, k in reqs]
+    assert first == again
+    # a fresh daemon (empty cache, own plugin directory) computes every answer anew
+    d2dir = scratch + ".second"
+    os.makedirs(d2dir)
+    k2 = kubelet.StubKubelet(os.path.join(d2dir, "kubelet.sock")).start()
+    d2 = harness.Daemon(d2dir, fx).start()
+    try:
+        reg = k2.wait_registration()
+        c2 = kubelet.PluginClient(os.path.join(d2dir, reg.endpoint))
+        assert [x.ID for x in c2.watch()[0].get(timeout=5).devices] == ids
+        fresh = [pref(c2, a, m, k) for a, m, k in reqs]
+        c2.close()
+    finally:
+        d2.stop()
+        k2.stop()
+    assert fresh == first
+    for (a, m, k), got in zip(reqs, first):
+        assert len(got) == k and set(m) <= set(got) <= set(a)
