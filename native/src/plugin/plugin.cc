@@ -1,6 +1,7 @@
 #include "plugin/plugin.h"
 
 #include <errno.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -148,8 +149,11 @@ void Plugin::BuildUnits() {
   pb::Encode(kfd, &kb);
   pb::PutLen(&kfd_spec_bytes_, 3, kb);
   graph_ = alloc::DeviceGraph(*snap_, spec_.devices);
-  if (!replicated_ && units_.size() <= 8)
-    best_effort_cache_.reset(new std::atomic<uint16_t>[256u * 256u * 9u]());
+  if (!replicated_ && units_.size() <= 8) {
+    // Anonymous zero pages: only the pages of entries actually used get memory.
+    void* p = mmap(nullptr, kBestEffortCacheBytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p != MAP_FAILED) best_effort_cache_.reset(static_cast<std::atomic<uint16_t>*>(p));
+  }
   healthy_.assign(units_.size(), 1);
   RebuildListAndWatch();
 }
@@ -368,6 +372,8 @@ Status Plugin::PreferredImpl(std::string_view req, std::string* resp) {
   return Status::Ok();
 }
 
+void Plugin::Unmap::operator()(std::atomic<uint16_t>* p) const { munmap(p, kBestEffortCacheBytes); }
+
 std::vector<int> Plugin::CachedBestEffort(const std::vector<int>& avail, const std::vector<int>& must,
                                           int size) {
   // Up to 8 devices the answer is a pure function of (available set, required
@@ -382,7 +388,8 @@ std::vector<int> Plugin::CachedBestEffort(const std::vector<int>& avail, const s
   for (int u : avail) am |= 1u << u;
   for (int u : must) rm |= 1u << u;
   if ((rm & ~am) != 0) return {};
-  std::atomic<uint16_t>& slot = best_effort_cache_[(am * 256u + rm) * (kMax + 1) + static_cast<uint32_t>(size)];
+  std::atomic<uint16_t>& slot =
+      best_effort_cache_.get()[(am * 256u + rm) * (kMax + 1) + static_cast<uint32_t>(size)];
   uint16_t v = slot.load(std::memory_order_relaxed);
   if (v == 0) {
     std::vector<int> r = alloc::BestEffortAllocate(graph_, avail, must, size);

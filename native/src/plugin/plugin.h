@@ -190,8 +190,13 @@ class Plugin {
   std::unordered_map<std::string_view, int> advertised_index_;
   std::string kfd_spec_bytes_;
   alloc::DeviceGraph graph_;
-  // Memoised best-effort answers for <= 8 whole devices (see CachedBestEffort).
-  std::unique_ptr<std::atomic<uint16_t>[]> best_effort_cache_;
+  // Memoised best-effort answers for <= 8 whole devices (see CachedBestEffort),
+  // in anonymous zero-filled pages (an all-zero atomic<uint16_t> is "empty").
+  static constexpr size_t kBestEffortCacheBytes = 256u * 256u * 9u * sizeof(uint16_t);
+  struct Unmap {
+    void operator()(std::atomic<uint16_t>* p) const;
+  };
+  std::unique_ptr<std::atomic<uint16_t>, Unmap> best_effort_cache_;
 
   struct LawSnapshot {
     uint64_t version = 0;
