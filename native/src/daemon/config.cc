@@ -85,7 +85,7 @@ const std::vector<FlagDef>& Table() {
        "path of libamd_smi.so to load (default: search the loader path and /opt/rocm/lib)",
        [](Flags& f) -> void* { return &f.amdsmi_lib; }},
       {"devices", "AMD_DP_DEVICES", "devices", Kind::kString,
-       "only serve these node GPU indices, comma separated (default: all)",
+       "only serve these GPUs: node indices, UUIDs or PCI addresses, comma separated (default: all)",
        [](Flags& f) -> void* { return &f.devices; }},
       {"auto-replica-unit-mib", "AUTO_REPLICA_UNIT_MIB", "autoReplicaUnitMiB", Kind::kUint,
        "MiB of VRAM per replica when replicas=-1",

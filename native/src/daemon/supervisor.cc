@@ -73,9 +73,10 @@ Result<Validated> Validate(const Config& cfg) {
   std::string devs = Trim(f.devices);
   if (!devs.empty() && devs != "all") {
     for (const auto& d : Split(devs, ',')) {
-      auto n = ParseUint(Trim(d));
-      if (!n) return InvalidArgument("invalid --devices entry: '" + d + "'");
-      v.bopts.only_gpus.push_back(static_cast<int>(*n));
+      std::string t = Trim(d);
+      if (t.empty()) continue;
+      if (auto n = ParseUint(t)) v.bopts.only_gpus.push_back(static_cast<int>(*n));
+      else v.bopts.only_ids.push_back(t);  // GPU UUID or PCI address
     }
   }
   return v;

@@ -88,8 +88,21 @@ Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo
     std::sort(handles.begin(), handles.end(), [&](int a, int b) {
       return snap->procs[a].partition_id < snap->procs[b].partition_id;
     });
-    if (!only.empty() && !only.count(static_cast<int>(gi))) continue;
     const auto& first = snap->procs[handles.front()];
+    if (!only.empty() || !opt.only_ids.empty()) {
+      bool keep = only.count(static_cast<int>(gi)) > 0;
+      std::string bdf = smi::FormatBdf(first.bdf_id & ~uint64_t{7});
+      std::string bus = bdf.substr(0, bdf.rfind('.'));  // "dddd:bb:dd"
+      for (const auto& id : opt.only_ids) {
+        std::string want = ToLower(id);
+        if (want == ToLower(first.uuid)) keep = true;
+        if (want.find(':') == std::string::npos) continue;
+        if (size_t dot = want.rfind('.'); dot != std::string::npos) want.resize(dot);  // function ignored
+        if (std::count(want.begin(), want.end(), ':') == 1) want = "0000:" + want;    // domain optional
+        if (want == bus) keep = true;
+      }
+      if (!keep) continue;
+    }
     PhysicalGpu g;
     g.index = index++;
     g.node_index = static_cast<int>(gi);

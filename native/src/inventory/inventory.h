@@ -101,6 +101,8 @@ struct BuildOptions {
   // Restrict to these physical GPU indices (empty = all). Used by the benchmark
   // to serve exactly N GPUs of a node, and by operators to carve a node.
   std::vector<int> only_gpus;
+  // ... or by GPU UUID / PCI address ("0000:0c:00.0", function ignored).
+  std::vector<std::string> only_ids;
   bool include_card_nodes = false;
 };
 

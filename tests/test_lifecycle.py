@@ -466,3 +466,21 @@ def test_configmap_style_update_is_applied(scratch):
     finally:
         assert d.stop() == 0
         k.stop()
+
+
+def test_devices_filter_by_index_uuid_and_pci_address(scratch):
+    import json
+    fx = fixtures.node(4)
+    path = fixtures.write(fx, scratch + ".fixture")
+    env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB, AMDSMI_MOCK_FIXTURE=path, ADP_LOG_LEVEL="error")
+    uuid2 = fx["gpus"][2]["uuid"]
+    bdf3 = fx["gpus"][3]["bdf"]            # "0000:6c:00.0"
+    short1 = fx["gpus"][1]["bdf"][5:-2]    # "2c:00" (no domain, no function)
+    r = subprocess.run([DAEMON, "--dry-run", "--devices", f"0,{uuid2.upper()},{bdf3},{short1}",
+                        "--device-plugin-path", scratch], capture_output=True, text=True, timeout=20, env=env)
+    assert r.returncode == 0, r.stderr
+    got = sorted(g["uuid"] for g in json.loads(r.stdout)["gpus"])
+    assert got == sorted(fx["gpus"][i]["uuid"] for i in range(4))
+    r = subprocess.run([DAEMON, "--dry-run", "--devices", uuid2, "--device-plugin-path", scratch],
+                       capture_output=True, text=True, timeout=20, env=env)
+    assert [g["uuid"] for g in json.loads(r.stdout)["gpus"]] == [uuid2]
