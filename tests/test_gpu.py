@@ -233,3 +233,15 @@ def test_python_cli_validate_on_real_gpu():
                         "--bytes", str(128 << 20)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert '"mfma_ok": true' in r.stdout and '"checksum_ok": true' in r.stdout
+
+
+def test_devices_filter_by_real_pci_address(snap):
+    import json
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import DAEMON
+    env = {k: v for k, v in os.environ.items() if k != "AMD_SMI_LIB"}
+    g = snap["gpus"][0]
+    r = subprocess.run([DAEMON, "--dry-run", "--devices", g["bdf"]], capture_output=True, text=True, timeout=60,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert [x["uuid"] for x in json.loads(r.stdout)["gpus"]] == [g["uuid"]]
