@@ -107,3 +107,12 @@ def test_release_versions_agree():
         assert f"amdgpu-device-plugin:{version}" in read(m), m
     for d in ("ubuntu", "ubi9"):
         assert "ENTRYPOINT" in read(f"deployments/container/Dockerfile.{d}")
+
+
+def test_helm_template_accepts_reference_value_names():
+    """A reference values file (values.yaml:3,7 migStrategy / nvidiaDriverRoot)
+    keeps working: the template prefers those names when they are set."""
+    with open(os.path.join(CHART, "templates", "daemonset.yaml")) as f:
+        text = f.read()
+    assert "coalesce .Values.migStrategy .Values.partitionStrategy" in text
+    assert "coalesce .Values.nvidiaDriverRoot .Values.driverRoot" in text
