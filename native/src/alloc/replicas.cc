@@ -46,6 +46,10 @@ namespace {
 // caller's request buffer; nothing is copied until the result is built.
 struct PhysicalPool {
   std::string_view prefix;
+  // prefix + join can only split at prefix.size() (no occurrence of join starts
+  // inside prefix and runs into the join), so IDs of this pool can be matched
+  // by two memcmps instead of a substring search.
+  bool join_safe = false;
   bool allocated = false;
   std::vector<std::string_view> replicas;  // [head, end) are still available
   size_t head = 0;
@@ -139,10 +143,21 @@ Result<Prioritized> PrioritizeDeviceViews(const std::vector<std::string_view>& a
   };
   size_t last = SIZE_MAX;
   for (std::string_view id : available) {
+    // Runs of the same device are common (the kubelet sends sorted lists):
+    // check "<last prefix><join>..." before searching for the join.
+    if (last != SIZE_MAX && pools[last].join_safe) {
+      std::string_view pre = pools[last].prefix;
+      if (id.size() >= pre.size() + join.size() &&
+          memcmp(id.data(), pre.data(), pre.size()) == 0 &&
+          memcmp(id.data() + pre.size(), join.data(), join.size()) == 0) {
+        pools[last].replicas.push_back(id);
+        continue;
+      }
+    }
     std::string_view dev = StripView(id, join);
     size_t at = SIZE_MAX;
     if (last != SIZE_MAX && pools[last].prefix == dev) {
-      at = last;  // runs of the same device are common (sorted lists)
+      at = last;
     } else {
       uint64_t t = tag_of(dev);
       for (size_t i = 0; i < pools.size(); ++i)
@@ -151,6 +166,12 @@ Result<Prioritized> PrioritizeDeviceViews(const std::vector<std::string_view>& a
         at = pools.size();
         pools.emplace_back();
         pools.back().prefix = dev;
+        if (!join.empty()) {
+          std::string probe(dev.substr(dev.size() - std::min(dev.size(), join.size() - 1)));
+          size_t tail = probe.size();
+          probe.append(join);
+          pools.back().join_safe = probe.find(join) == tail;
+        }
         pools.back().replicas.reserve(available.size() / 8 + 1);
         tags.push_back(t);
       }

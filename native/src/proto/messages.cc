@@ -362,6 +362,9 @@ Status DecodeView(std::string_view b, std::vector<ContainerPreferredAllocationRe
     if (!r.ReadLen(&c)) return false;
     m->emplace_back();
     auto& cr = m->back();
+    // One growth step up front: each entry is >= 2 wire bytes plus its ID,
+    // and device IDs are rarely shorter than 16 bytes.
+    cr.available.reserve(c.size() / 18 + 1);
     return ForEachField(c, "ContainerPreferredAllocationRequest", [&](uint32_t cf, WireType cwt, Reader& cr_r) {
              if (cf == 1) return ReadView(cr_r, cwt, &cr.available);
              if (cf == 2) return ReadView(cr_r, cwt, &cr.must_include);

@@ -12,7 +12,7 @@ void PutMapEntry(std::string* o, uint32_t field, std::string_view k, std::string
   PutLen(o, 2, v);
 }
 
-bool Reader::ReadVarint(uint64_t* v) {
+bool Reader::ReadVarintSlow(uint64_t* v) {
   uint64_t r = 0;
   for (int shift = 0; shift < 64; shift += 7) {
     if (p_ >= end_) { ok_ = false; return false; }
@@ -22,25 +22,6 @@ bool Reader::ReadVarint(uint64_t* v) {
   }
   ok_ = false;
   return false;
-}
-
-bool Reader::Next(uint32_t* field, WireType* wt) {
-  if (!ok_ || p_ >= end_) return false;
-  uint64_t tag;
-  if (!ReadVarint(&tag)) return false;
-  *field = static_cast<uint32_t>(tag >> 3);
-  *wt = static_cast<WireType>(tag & 7);
-  if (*field == 0) { ok_ = false; return false; }
-  return true;
-}
-
-bool Reader::ReadLen(std::string_view* v) {
-  uint64_t n;
-  if (!ReadVarint(&n)) return false;
-  if (n > static_cast<uint64_t>(end_ - p_)) { ok_ = false; return false; }
-  *v = std::string_view(p_, n);
-  p_ += n;
-  return true;
 }
 
 bool Reader::Skip(WireType wt) {

@@ -61,13 +61,38 @@ class Reader {
   explicit Reader(std::string_view buf) : p_(buf.data()), end_(buf.data() + buf.size()) {}
   // Advances to the next field. Returns false at end of buffer or on error
   // (check ok()).
-  bool Next(uint32_t* field, WireType* wt);
-  bool ReadVarint(uint64_t* v);
-  bool ReadLen(std::string_view* v);
+  bool Next(uint32_t* field, WireType* wt) {
+    if (!ok_ || p_ >= end_) return false;
+    uint64_t tag;
+    if (!ReadVarint(&tag)) return false;
+    *field = static_cast<uint32_t>(tag >> 3);
+    *wt = static_cast<WireType>(tag & 7);
+    if (*field == 0) { ok_ = false; return false; }
+    return true;
+  }
+  // Inline one-byte fast path: every tag and most lengths in the kubelet API
+  // (device IDs are < 128 bytes) are single-byte varints.
+  bool ReadVarint(uint64_t* v) {
+    if (p_ < end_ && !(static_cast<uint8_t>(*p_) & 0x80)) {
+      *v = static_cast<uint8_t>(*p_++);
+      return true;
+    }
+    return ReadVarintSlow(v);
+  }
+  bool ReadLen(std::string_view* v) {
+    uint64_t n;
+    if (!ReadVarint(&n)) return false;
+    if (n > static_cast<uint64_t>(end_ - p_)) { ok_ = false; return false; }
+    *v = std::string_view(p_, n);
+    p_ += n;
+    return true;
+  }
   bool Skip(WireType wt);
   bool ok() const { return ok_; }
+  size_t remaining() const { return static_cast<size_t>(end_ - p_); }
 
  private:
+  bool ReadVarintSlow(uint64_t* v);
   const char* p_;
   const char* end_;
   bool ok_ = true;

@@ -86,3 +86,78 @@ def test_spread_vs_pack_on_the_same_input():
     assert {i.split("-replica-")[0] for i in spread} == {"a", "b"} and not nu
     pack, _ = native.prioritize(avail, [], 2, policy="pack")
     assert len({i.split("-replica-")[0] for i in pack}) == 1
+
+
+def _reference_prioritize(avail, must, size, join="-replica-"):
+    """Executable model of the reference's prioritizeDevices
+    (cmd/nvidia-device-plugin/replica.go:95-198): group by the text before the
+    first join, sort each group, take must-includes by swap-remove, then pick
+    the unallocated device with the most replicas left (ties: first in sorted
+    key order), else the allocated one with the most left."""
+    pools = {}
+    for i in avail:
+        pools.setdefault(i.split(join)[0], []).append(i)
+    for v in pools.values():
+        v.sort()
+    used = set()
+    out = list(must)
+    unique = True
+    for m in must:
+        dev = m.split(join)[0]
+        if dev not in pools or m not in pools[dev]:
+            return None, None
+        if dev in used:
+            unique = False
+        lst = pools[dev]
+        k = lst.index(m)
+        lst[k] = lst[-1]
+        lst.pop()
+        used.add(dev)
+    for _ in range(len(out), size):
+        best_u = best_a = None
+        hi_u = hi_a = 0
+        for dev in sorted(pools):
+            n = len(pools[dev])
+            if dev in used:
+                if n > hi_a:
+                    best_a, hi_a = dev, n
+            elif n > hi_u:
+                best_u, hi_u = dev, n
+        pick = best_u if best_u is not None else best_a
+        if pick is None:
+            return None, None
+        if pick in used:
+            unique = False
+        out.append(pools[pick].pop(0))
+        used.add(pick)
+    return sorted(out), not unique
+
+
+def test_prioritize_matches_reference_model_on_random_and_adversarial_ids():
+    """Randomised differential test of the C++ prioritizer against the model
+    above, including IDs where the join overlaps the device prefix
+    ("x-replica" + "-replica-0"), IDs without a join and unsorted lists."""
+    import random
+    rng = random.Random(7)
+    stems = ["a", "b", "x-replica", "x", "gpu-7-replica", "75a30000-0000-1000-80c0-bf9907890000", "-", "r-"]
+    for trial in range(400):
+        avail = []
+        for s in rng.sample(stems, rng.randint(1, len(stems))):
+            n = rng.randint(0, 6)
+            avail += [f"{s}-replica-{i}" for i in rng.sample(range(20), n)]
+            if rng.random() < 0.2:
+                avail.append(s)  # a non-replicated ID
+        avail = list(dict.fromkeys(avail))
+        if rng.random() < 0.5:
+            avail.sort()
+        else:
+            rng.shuffle(avail)
+        must = rng.sample(avail, min(len(avail), rng.randint(0, 2)))
+        size = rng.randint(len(must), len(must) + 4)
+        want, want_nu = _reference_prioritize(avail, must, size)
+        if want is None:
+            with pytest.raises(native.NativeError):
+                native.prioritize(avail, must, size)
+            continue
+        ids, nu = native.prioritize(avail, must, size)
+        assert (ids, nu) == (want, want_nu), (trial, avail, must, size)
