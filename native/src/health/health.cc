@@ -108,6 +108,8 @@ Status Monitor::Start() {
     auto ecc = lib_->UncorrectableErrors(h);
     ecc_baseline_[g.index] = ecc.ok() ? *ecc : 0;
   }
+  LOG_INFO(kComp, "health monitor watching %zu GPU(s) (events %s, poll every %d ms)", snap_->gpus.size(),
+           events_ok_ ? "on" : "off", cfg_.poll_interval_ms);
   if (!events_ok_ && cfg_.poll_interval_ms == 0) return Status::Ok();
   stop_.store(false);
   if (wake_fd_ < 0) wake_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);

@@ -52,14 +52,26 @@ class Node:
         self.c = kubelet.PluginClient(self.c_path)
         self.q, self.call = self.c.watch()
         self.first = self.q.get(timeout=5)
+        # The monitor starts after registration (reference server.go:148): wait until
+        # it has taken its ECC baselines and registered for events.
+        disabled = (env or {}).get("DP_DISABLE_HEALTHCHECKS", "").lower()
+        self.d.wait_log("health checks disabled" if disabled in ("all", "xids") else "health monitor watching")
 
-    def inject(self, line):
-        try:
-            fd = os.open(self.fifo, os.O_WRONLY | os.O_NONBLOCK)
-        except OSError as e:
-            if e.errno == 6:  # ENXIO: nobody reads events (health checks disabled)
-                return
-            raise
+    def inject(self, line, reader=True):
+        # The health thread opens the FIFO when it registers for events, which can
+        # come after the first ListAndWatch: wait for it unless none is expected.
+        deadline = time.monotonic() + (5 if reader else 0)
+        while True:
+            try:
+                fd = os.open(self.fifo, os.O_WRONLY | os.O_NONBLOCK)
+                break
+            except OSError as e:
+                if e.errno != 6:  # ENXIO: no reader (yet, or health checks disabled)
+                    raise
+                if time.monotonic() >= deadline:
+                    assert not reader, "health thread never opened the event FIFO"
+                    return
+                time.sleep(0.02)
         os.write(fd, (line + "\n").encode())
         os.close(fd)
 
@@ -105,9 +117,12 @@ def test_application_events_are_ignored(node):
     n = node()
     n.inject("1 1 vm fault")
     n.inject("1 2 thermal")
-    time.sleep(0.8)
+    deadline = time.monotonic() + 5
+    while n.d.log().count("(ignored)") < 2 and time.monotonic() < deadline:
+        time.sleep(0.05)
+    assert n.d.log().count("(ignored)") >= 2
+    time.sleep(0.3)
     assert n.q.empty()
-    assert "(ignored)" in n.d.log()
 
 
 def test_health_reaches_every_replica(node):
@@ -138,7 +153,7 @@ def test_disable_healthchecks_ignores_configured_ids(node):
 
 def test_disable_all(node):
     n = node(env={"DP_DISABLE_HEALTHCHECKS": "all"})
-    n.inject("0 3")
+    n.inject("0 3", reader=False)
     time.sleep(0.8)
     assert n.q.empty()
     assert "health checks disabled" in n.d.log()
