@@ -3,6 +3,7 @@
 //   amdgpu-dp-probe [--list] [--device N] [--bytes B] [--iters I]
 //                   [--expect-xcds X] [--expect-cus C] [--min-gbps G]
 //                   [--p2p [--min-p2p-gbps P]] [--mfma [--min-tflops T]]
+//                   [--census [--expect-cus-seen C]]
 //
 // Runs the visibility probe (visibility_probe.hip) on every visible HIP device
 // (or one) and prints one JSON line per device. Exits non-zero when a device
@@ -14,7 +15,9 @@
 // xGMI-aware preferred allocation should see every pair connected); it fails if a
 // pair has no peer access or is below --min-p2p-gbps. --mfma runs the bf16
 // matrix cores flat out (v_mfma_f32_32x32x16_bf16) and checks every result is
-// exact; it fails on a wrong element or a rate below --min-tflops.
+// exact; it fails on a wrong element or a rate below --min-tflops. --census
+// prints which XCDs/CUs the process's queues can use (the CU share of a
+// CU-partitioned replica, HSA_CU_MASK); --expect-cus-seen checks that count.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -25,6 +28,7 @@ extern "C" int adp_probe_list(char* out, int len);
 extern "C" int adp_probe_run(int device, unsigned long long bytes, int iters, char* out, int len);
 extern "C" int adp_probe_p2p(int ndev, unsigned long long bytes, int iters, char* out, int len);
 extern "C" int adp_probe_mfma(int device, int iters, char* out, int len);
+extern "C" int adp_probe_census(int device, char* out, int len);
 
 namespace {
 
@@ -47,7 +51,8 @@ int main(int argc, char** argv) {
   unsigned long long bytes = 256ull << 20;
   long expect_xcds = -1, expect_cus = -1;
   double min_gbps = -1, min_p2p_gbps = -1, min_tflops = -1;
-  bool list = false, p2p = false, mfma = false;
+  long expect_cus_seen = -1;
+  bool list = false, p2p = false, mfma = false, census = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : "0"; };
@@ -62,9 +67,12 @@ int main(int argc, char** argv) {
     else if (a == "--min-p2p-gbps") min_p2p_gbps = atof(next());
     else if (a == "--mfma") mfma = true;
     else if (a == "--min-tflops") min_tflops = atof(next());
+    else if (a == "--census") census = true;
+    else if (a == "--expect-cus-seen") expect_cus_seen = atol(next());
     else {
       fprintf(stderr, "usage: %s [--list] [--device N] [--bytes B] [--iters I] [--expect-xcds X] "
-                      "[--expect-cus C] [--min-gbps G] [--p2p [--min-p2p-gbps P]] [--mfma [--min-tflops T]]\n",
+                      "[--expect-cus C] [--min-gbps G] [--p2p [--min-p2p-gbps P]] [--mfma [--min-tflops T]] "
+                      "[--census [--expect-cus-seen C]]\n",
               argv[0]);
       return 2;
     }
@@ -82,6 +90,13 @@ int main(int argc, char** argv) {
   }
   int failures = 0;
   for (int d = (device < 0 ? 0 : device); d < (device < 0 ? n : device + 1); ++d) {
+    if (census) {
+      int crc = adp_probe_census(d, buf, sizeof(buf));
+      printf("%s\n", buf);
+      if (crc != 0) ++failures;
+      else if (expect_cus_seen >= 0 && JsonInt(buf, "cus_seen") != expect_cus_seen) ++failures;
+      continue;
+    }
     int rc = adp_probe_run(d, bytes, iters, buf, sizeof(buf));
     printf("%s\n", buf);
     if (rc != 0) { ++failures; continue; }

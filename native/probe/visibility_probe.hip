@@ -55,6 +55,20 @@ __global__ void __launch_bounds__(64) CensusKernel(uint32_t* out) {
   }
 }
 
+// Placement census for CU masks: every workgroup records where it ran and then
+// holds its CU for ~`hold_ticks` of the 100 MHz wall clock, so the dispatcher
+// spreads the grid over every CU the queue may use (a bounded wait: each wave
+// exits after at most hold_ticks).
+__global__ void __launch_bounds__(64) HoldCensusKernel(uint32_t* out, uint64_t hold_ticks) {
+  if (threadIdx.x == 0) {
+    uint32_t xcc = ReadXccId();
+    uint32_t hw = ReadHwId();
+    out[blockIdx.x] = (xcc << 16) | ((hw >> 8) & 0xff);
+    uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < hold_ticks) __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 __global__ void __launch_bounds__(256) FillKernel(uint4* p, size_t n) {
   size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
   for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -378,6 +392,48 @@ extern "C" int adp_probe_list(char* out, int len) {
     s += buf;
   }
   s += "]";
+  snprintf(out, len, "%s", s.c_str());
+  return 0;
+}
+
+// Which XCDs / CUs a queue of this process can use: under HSA_CU_MASK (e.g. a
+// CU-partitioned time-slice replica, docs/SHARING_TUTORIAL.md) only the masked
+// CUs show up. Returns {"xccs_seen", "cus_seen", "per_xcc": [...], "keys": [...]}
+// with keys = xcc << 16 | HW_ID[15:8] (SE/SH/CU).
+extern "C" int adp_probe_census(int device, char* out, int len) {
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  const int blocks = prop.multiProcessorCount * 4;
+  uint32_t* d = nullptr;
+  HIP_TRY(hipMalloc(&d, blocks * sizeof(uint32_t)));
+  HIP_TRY(hipMemset(d, 0xff, blocks * sizeof(uint32_t)));
+  hipLaunchKernelGGL(HoldCensusKernel, dim3(blocks), dim3(64), 0, 0, d, 2000ull);  // 20 us per WG
+  HIP_TRY(hipGetLastError());
+  std::vector<uint32_t> rec(blocks);
+  HIP_TRY(hipMemcpy(rec.data(), d, blocks * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipFree(d));
+  std::set<uint32_t> keys, xccs;
+  for (uint32_t r : rec) {
+    if (r == 0xffffffffu) continue;
+    keys.insert(r);
+    xccs.insert(r >> 16);
+  }
+  std::vector<int> per_xcc(16, 0);
+  for (uint32_t k : keys) ++per_xcc[(k >> 16) & 0xf];
+  std::string s = "{\"device\": " + std::to_string(device) + ", \"cus\": " +
+                  std::to_string(prop.multiProcessorCount) + ", \"xccs_seen\": " + std::to_string(xccs.size()) +
+                  ", \"cus_seen\": " + std::to_string(keys.size()) + ", \"per_xcc\": [";
+  int nx = xccs.empty() ? 0 : static_cast<int>(*xccs.rbegin()) + 1;
+  for (int x = 0; x < nx; ++x) s += (x ? ", " : "") + std::to_string(per_xcc[x]);
+  s += "], \"keys\": [";
+  bool first = true;
+  for (uint32_t k : keys) {
+    s += (first ? "" : ", ") + std::to_string(k);
+    first = false;
+  }
+  s += "]}";
+  if (static_cast<int>(s.size()) >= len) return 3;
   snprintf(out, len, "%s", s.c_str());
   return 0;
 }

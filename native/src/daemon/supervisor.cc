@@ -62,6 +62,7 @@ Result<Validated> Validate(const Config& cfg) {
   v.popts.plugin_dir = f.plugin_dir;
   v.popts.kubelet_socket = f.kubelet_socket;
   v.popts.pass_device_specs = f.pass_device_specs;
+  v.popts.replica_cu_mask = f.replica_cu_mask;
   v.popts.driver_root = f.driver_root;
   v.popts.auto_replica_unit_mib = f.auto_replica_unit_mib;
   v.popts.server_threads = static_cast<int>(std::min<uint64_t>(f.server_threads, 64));
@@ -100,7 +101,8 @@ int DryRun(smi::Library* lib, const Validated& v, const Config& cfg) {
     out += (i ? ", " : "") + std::string("{\"index\": ") + std::to_string(g.node_index) + ", \"uuid\": \"" +
            JsonEscape(g.uuid) + "\", \"bdf\": \"" + g.bdf + "\", \"mode\": \"" + g.compute_mode + "/" +
            g.memory_mode + "\", \"partitions\": " + std::to_string(g.partitions.size()) +
-           ", \"vram_mib\": " + std::to_string(g.vram_mib) + ", \"numa\": " + std::to_string(g.numa) + "}";
+           ", \"vram_mib\": " + std::to_string(g.vram_mib) + ", \"numa\": " + std::to_string(g.numa) +
+           ", \"xcds\": " + std::to_string(g.xcds) + ", \"cus\": " + std::to_string(g.cus) + "}";
   }
   out += "], \"labels\": {";
   bool first_label = true;
@@ -116,7 +118,14 @@ int DryRun(smi::Library* lib, const Validated& v, const Config& cfg) {
     out += std::string(first ? "" : ", ") + "{\"resource\": \"" + JsonEscape(s.resource_name) +
            "\", \"socket\": \"" + JsonEscape(p.socket_path()) + "\", \"devices\": " +
            std::to_string(p.device_count()) + ", \"allocatable\": " + std::to_string(p.advertised_count()) +
-           ", \"replicated\": " + (p.replicated() ? "true" : "false") + "}";
+           ", \"replicated\": " + (p.replicated() ? "true" : "false");
+    // --replica-cu-mask: CUs of each replica's share per device ([] = not CU-partitioned).
+    out += ", \"replica_cus\": [";
+    for (size_t i = 0; i < p.units().size(); ++i) {
+      const auto& rc = p.units()[i].replica_cus;
+      out += (i ? ", " : "") + std::to_string(rc.empty() ? 0 : rc[0].second - rc[0].first + 1);
+    }
+    out += "]}";
     first = false;
   }
   out += "]}";

@@ -56,6 +56,19 @@ const char* DeviceListStrategyName(DeviceListStrategy s) {
   return "?";
 }
 
+std::vector<std::pair<uint32_t, uint32_t>> ReplicaCuRanges(uint32_t cus, uint32_t xcds, unsigned replicas) {
+  std::vector<std::pair<uint32_t, uint32_t>> out;
+  if (replicas < 2 || cus == 0 || xcds == 0 || cus % xcds != 0) return out;
+  const uint32_t per = cus / xcds;  // CUs per XCD
+  if (replicas > per) return out;
+  for (unsigned r = 0; r < replicas; ++r) {
+    uint32_t lo = static_cast<uint32_t>(uint64_t(r) * per / replicas) * xcds;
+    uint32_t hi = static_cast<uint32_t>(uint64_t(r + 1) * per / replicas) * xcds - 1;
+    out.emplace_back(lo, hi);
+  }
+  return out;
+}
+
 int DefaultServerThreads() {
   unsigned n = std::thread::hardware_concurrency();
   return static_cast<int>(std::clamp(n, 1u, 8u));
@@ -109,6 +122,14 @@ void Plugin::BuildUnits() {
     u.replicas = v.auto_replicas
                      ? static_cast<unsigned>(std::max<uint64_t>(1, u.vram_mib / opts_.auto_replica_unit_mib))
                      : std::max(1u, v.replicas);
+    u.cus = ref.partition < 0 ? g.cus : g.partitions[ref.partition].cus;
+    u.xcds = ref.partition < 0 ? g.xcds : g.partitions[ref.partition].xcds;
+    if (opts_.replica_cu_mask && replicated_ && !memory_units_) {
+      u.replica_cus = ReplicaCuRanges(u.cus, u.xcds, u.replicas);
+      if (u.replica_cus.empty() && u.replicas > 1)
+        LOG_WARN(kComp, "device %s: %u CUs over %u XCDs cannot be split into %u CU shares; its replicas "
+                 "share all CUs", u.id.c_str(), u.cus, u.xcds, u.replicas);
+    }
     u.visible_id = opts_.id_strategy == DeviceIdStrategy::kIndex ? u.index : u.id;
     for (const auto& path : u.paths) {
       pb::DeviceSpec ds{path, PathJoin(opts_.driver_root, path), "rw"};
@@ -228,15 +249,24 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
   std::vector<std::vector<std::string_view>> containers;
   ADP_RETURN_IF_ERROR(pb::DecodeView(req, &containers));
   std::vector<int> us, units_per;
-  std::string c, joined;
+  std::vector<std::pair<int, uint32_t>> shares;  // (unit, replica) of CU-partitioned units
+  std::string c, joined, cu_mask;
   for (const auto& ids : containers) {
     us.clear();
+    shares.clear();
     for (std::string_view id : ids) {
       auto it = advertised_index_.find(id);
       if (it == advertised_index_.end())
         return InvalidArgument("invalid allocation request for '" + spec_.resource_name +
                                "': unknown device: " + std::string(id));
       us.push_back(it->second);
+      if (!units_[it->second].replica_cus.empty()) {
+        // An advertised replica ID ends in "<join><r>" (alloc::ReplicaId).
+        uint32_t r = 0, scale = 1;
+        for (size_t k = id.size(); k > 0 && id[k - 1] >= '0' && id[k - 1] <= '9'; --k, scale *= 10)
+          r += static_cast<uint32_t>(id[k - 1] - '0') * scale;
+        shares.emplace_back(it->second, r);
+      }
     }
     // Unique physical devices. uuid strategy: sorted by ID (stripReplicas order,
     // server.go:325); index strategy: enumeration order (server.go:406-411).
@@ -247,6 +277,32 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       for (int u : us) ++units_per[u];
     }
     us.erase(std::unique(us.begin(), us.end()), us.end());
+    cu_mask.clear();
+    if (!shares.empty()) {
+      // HSA_CU_MASK="<agent>:<first>-<last>,...;...": agents are numbered in the
+      // container in enumeration order (= unit order, us is sorted by unit), and
+      // devices without an entry keep all their CUs. Adjacent replica shares merge.
+      std::sort(shares.begin(), shares.end());
+      shares.erase(std::unique(shares.begin(), shares.end()), shares.end());
+      size_t k = 0;
+      for (size_t ord = 0; ord < us.size(); ++ord) {
+        while (k < shares.size() && shares[k].first < us[ord]) ++k;
+        if (k == shares.size() || shares[k].first != us[ord]) continue;
+        const auto& ranges = units_[us[ord]].replica_cus;
+        if (!cu_mask.empty()) cu_mask += ';';
+        cu_mask += std::to_string(ord);
+        char sep = ':';
+        while (k < shares.size() && shares[k].first == us[ord]) {
+          uint32_t lo = ranges[shares[k].second].first, hi = ranges[shares[k].second].second;
+          for (++k; k < shares.size() && shares[k].first == us[ord] &&
+                    ranges[shares[k].second].first == hi + 1; ++k)
+            hi = ranges[shares[k].second].second;
+          cu_mask += sep;
+          cu_mask += std::to_string(lo) + "-" + std::to_string(hi);
+          sep = ',';
+        }
+      }
+    }
     if (opts_.id_strategy == DeviceIdStrategy::kUuid)
       std::sort(us.begin(), us.end(), [&](int a, int b) { return units_[a].id < units_[b].id; });
 
@@ -300,6 +356,7 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       pb::PutMapEntry(&c, 1, kMemoryLimitEnv, mib);
       pb::PutMapEntry(&c, 1, kMemoryFractionEnv, frac);
     }
+    if (!cu_mask.empty()) pb::PutMapEntry(&c, 1, kCuMaskEnv, cu_mask);
     if (opts_.pass_device_specs) {
       c += kfd_spec_bytes_;
       for (int u : us) c += units_[u].spec_bytes;

@@ -62,6 +62,9 @@ inline constexpr const char* kCdiVendorClass = "amd.com/gpu";
 // that share of the device's HBM, comma separated in AMD_VISIBLE_DEVICES order.
 inline constexpr const char* kMemoryLimitEnv = "AMD_GPU_MEMORY_LIMIT_MIB";
 inline constexpr const char* kMemoryFractionEnv = "AMD_GPU_MEMORY_FRACTION";
+// Set on Allocate for CU-partitioned time-slice replicas (--replica-cu-mask): the
+// ROCm runtime restricts every queue of the container to the listed CUs.
+inline constexpr const char* kCuMaskEnv = "HSA_CU_MASK";
 
 struct PluginOptions {
   std::string plugin_dir = kDefaultPluginDir;
@@ -79,7 +82,19 @@ struct PluginOptions {
   std::string cdi_spec_dir = "/var/run/cdi";  // where cdi-* strategies write the CDI spec
   int server_threads = 0;                 // gRPC loops; <=0 -> DefaultServerThreads()
   int busy_poll_us = 50;                  // loop keeps polling this long after activity
+  // Time-slice replicas also split the device's CUs: replica r of R gets its own
+  // 1/R of every XCD's CUs (HSA_CU_MASK), so co-scheduled pods stop contending
+  // for the same CUs -- the MI355X analogue of an MPS active-thread share.
+  bool replica_cu_mask = false;
 };
+
+// HSA_CU_MASK bit ranges [first, last] of each of `replicas` CU shares of a device
+// with `cus` CUs over `xcds` XCDs. The kernel driver deals mask bit i to XCD
+// i % xcds (measured on MI355X: profiles/r1/session18/), so ranges whose ends are
+// multiples of `xcds` give every replica the same CUs on every XCD and never
+// leave an XCD without CUs. Empty when the split is impossible (unknown shape,
+// fewer than one CU per XCD per replica) or pointless (replicas < 2).
+std::vector<std::pair<uint32_t, uint32_t>> ReplicaCuRanges(uint32_t cus, uint32_t xcds, unsigned replicas);
 
 // min(8, online CPUs): one loop per GPU of an 8-GPU node. Idle loops sit in
 // epoll_wait and cost no CPU; they only matter under concurrent clients.
@@ -98,6 +113,9 @@ struct Unit {
   std::string spec_bytes;          // pre-encoded ContainerAllocateResponse.devices entries
   std::string mount_bytes;         // pre-encoded ContainerAllocateResponse.mounts entry
   unsigned replicas = 1;
+  uint32_t cus = 0, xcds = 0;      // compute units / XCDs of this GPU or partition
+  // --replica-cu-mask: CU bit range of each replica (empty = whole device).
+  std::vector<std::pair<uint32_t, uint32_t>> replica_cus;
 };
 
 // Written by every server loop on every call: sharded per thread (metrics.h).

@@ -25,6 +25,7 @@
 #include "grpc/grpc.h"
 #include "health/health.h"
 #include "metrics/metrics.h"
+#include "plugin/plugin.h"
 #include "podresources/podresources.h"
 #include "proto/wire.h"
 #include "proto/messages.h"
@@ -571,7 +572,31 @@ static void TestPodResources() {
   CHECK(!podresources::DecodeList("\x0a\xff\xff\xff\xff\x0f", &out).ok());
 }
 
+static void TestReplicaCuRanges() {
+  g_case = "replica-cu-ranges";
+  using R = std::vector<std::pair<uint32_t, uint32_t>>;
+  // MI355X SPX: 256 CUs over 8 XCDs; mask bit i lands on XCD i % 8.
+  CHECK((plugin::ReplicaCuRanges(256, 8, 4) == R{{0, 63}, {64, 127}, {128, 191}, {192, 255}}));
+  CHECK((plugin::ReplicaCuRanges(256, 8, 2) == R{{0, 127}, {128, 255}}));
+  // Uneven split: every share still ends on an XCD boundary and is non-empty.
+  R three = plugin::ReplicaCuRanges(256, 8, 3);
+  CHECK((three == R{{0, 79}, {80, 167}, {168, 255}}));
+  for (auto [lo, hi] : three) CHECK(lo % 8 == 0 && (hi + 1) % 8 == 0 && hi > lo);
+  R r32 = plugin::ReplicaCuRanges(256, 8, 32);
+  CHECK(r32.size() == 32 && r32[31] == std::make_pair(248u, 255u));
+  for (size_t i = 0; i < r32.size(); ++i) CHECK(r32[i].first == 8 * i && r32[i].second == 8 * i + 7);
+  // CPX partition: 32 CUs on one XCD.
+  CHECK((plugin::ReplicaCuRanges(32, 1, 4) == R{{0, 7}, {8, 15}, {16, 23}, {24, 31}}));
+  // Impossible or pointless splits.
+  CHECK(plugin::ReplicaCuRanges(256, 8, 33).empty());  // < 1 CU per XCD per replica
+  CHECK(plugin::ReplicaCuRanges(256, 8, 1).empty());
+  CHECK(plugin::ReplicaCuRanges(0, 8, 4).empty());
+  CHECK(plugin::ReplicaCuRanges(256, 0, 4).empty());
+  CHECK(plugin::ReplicaCuRanges(250, 8, 4).empty());  // CUs not uniform over XCDs
+}
+
 int main() {
+  TestReplicaCuRanges();
   TestPodResources();
   TestMetrics();
   TestPrioritize();

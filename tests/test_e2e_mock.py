@@ -192,4 +192,51 @@ def test_time_slice_replicas_carry_no_memory_envs(running, scratch):
     ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
     envs = dict(c.allocate(ids[:2]).container_responses[0].envs)
     assert "AMD_GPU_MEMORY_LIMIT_MIB" not in envs
+    assert "HSA_CU_MASK" not in envs  # CU shares are opt-in (--replica-cu-mask)
+    c.close()
+
+
+def test_replica_cu_mask_splits_compute_units(running, scratch):
+    """--replica-cu-mask: replica r of 4 runs on its own quarter of every XCD's CUs
+    (HSA_CU_MASK bit i -> XCD i % 8, profiles/r1/session18/); adjacent shares merge,
+    agents are numbered in enumeration order inside the container."""
+    d, k = running(args=["--resource-config", "gpu:sharedgpu:4", "--replica-cu-mask"])
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    g0, g1 = ids[:4], ids[4:]  # advertised in enumeration order, replicas 0..3
+    assert all(i.endswith(f"-replica-{r}") for r, i in enumerate(g0))
+
+    def mask(req):
+        return dict(c.allocate(req).container_responses[0].envs).get("HSA_CU_MASK")
+    assert mask([g0[0]]) == "0:0-63"
+    assert mask([g0[3]]) == "0:192-255"
+    assert mask([g0[2], g0[1]]) == "0:64-191"
+    assert mask([g0[3], g0[1]]) == "0:64-127,192-255"
+    assert mask([g1[2], g0[0]]) == "0:0-63;1:128-191"
+    assert mask([g1[1]]) == "0:64-127"
+    c.close()
+
+
+def test_replica_cu_mask_on_cpx_partitions(running, scratch):
+    fx = fixtures.node(1, "CPX", memory="NPS2")
+    d, k = running(fx, args=["--partition-strategy", "single", "--resource-config", "gpu:gpu:4",
+                             "--replica-cu-mask"])
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    assert len(ids) == 32
+    envs = dict(c.allocate([ids[5]]).container_responses[0].envs)
+    assert envs["HSA_CU_MASK"] == "0:8-15"  # one XCD, 32 CUs: replica 1 of 4
+    c.close()
+
+
+def test_replica_cu_mask_needs_a_possible_split(running, scratch):
+    # 64 replicas > 32 CUs per XCD: no split, the daemon says so, no mask is set.
+    d, k = running(args=["--resource-config", "gpu:sharedgpu:64", "--replica-cu-mask"])
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    assert "HSA_CU_MASK" not in dict(c.allocate(ids[:1]).container_responses[0].envs)
+    assert "cannot be split into 64 CU shares" in d.log()
     c.close()

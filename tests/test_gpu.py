@@ -245,3 +245,47 @@ def test_devices_filter_by_real_pci_address(snap):
                        env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert [x["uuid"] for x in json.loads(r.stdout)["gpus"]] == [g["uuid"]]
+
+
+def test_replica_cu_mask_shares_are_disjoint_on_mi355x(scratch, snap, probe_built):
+    """--replica-cu-mask on the real MI355X: each of 4 time-slice replicas gets a
+    HSA_CU_MASK from Allocate(); under it the probe's census sees exactly 1/4 of
+    the CUs, the same number on every XCD, and the 4 shares are disjoint and
+    together cover every CU the unmasked census sees."""
+    import json
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd.utils.build import PROBE_EXE
+    g = snap["gpus"][0]
+    if g["partitioned"]:
+        pytest.skip("box GPU is partitioned")
+    assert g["xcds"] == 8 and g["cus"] == 256, g
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--resource-config", "gpu:sharedgpu:4",
+                                                     "--replica-cu-mask"]).start()
+    try:
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=10).devices]
+        assert len(ids) == 4
+        masks = [dict(c.allocate([i]).container_responses[0].envs)["HSA_CU_MASK"] for i in ids]
+        c.close()
+    finally:
+        assert d.stop() == 0
+        k.stop()
+    assert masks == ["0:0-63", "0:64-127", "0:128-191", "0:192-255"]
+
+    def census(mask):
+        env = {k: v for k, v in os.environ.items() if k != "HSA_CU_MASK"}
+        if mask:
+            env["HSA_CU_MASK"] = mask
+        r = subprocess.run([PROBE_EXE, "--device", "0", "--census"], env=env, capture_output=True, text=True,
+                           timeout=60)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    full = census(None)
+    shares = [census(m) for m in masks]
+    for s in shares:
+        assert s["cus_seen"] == 64 and s["per_xcc"] == [8] * 8, s
+    keys = [set(s["keys"]) for s in shares]
+    assert all(not (keys[a] & keys[b]) for a in range(4) for b in range(a + 1, 4))
+    assert set().union(*keys) == set(full["keys"]) and len(full["keys"]) == 256
