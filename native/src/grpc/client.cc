@@ -179,26 +179,32 @@ Result<std::unique_ptr<Channel>> Channel::Dial(const std::string& uds_path, int 
 }
 
 Status Channel::Flush() {
+  // Every frame nghttp2 has ready (a request's HEADERS + DATA, WINDOW_UPDATEs,
+  // SETTINGS acks) goes out in one write, like grpc-go's batching writer: the
+  // peer wakes up once per request instead of once per frame.
   auto* s = static_cast<nghttp2_session*>(session_);
+  wbuf_.clear();
   while (true) {
     const uint8_t* data;
     ssize_t n = nghttp2_session_mem_send(s, &data);
     if (n < 0) { dead_ = true; return Internal(nghttp2_strerror(static_cast<int>(n))); }
-    if (n == 0) return Status::Ok();
-    ssize_t off = 0;
-    while (off < n) {
-      ssize_t w = send(fd_, data + off, n - off, MSG_NOSIGNAL);
-      if (w > 0) { off += w; continue; }
-      if (w < 0 && errno == EINTR) continue;
-      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-        pollfd p{fd_, POLLOUT, 0};
-        poll(&p, 1, 1000);
-        continue;
-      }
-      dead_ = true;
-      return Unavailable(std::string("write: ") + strerror(errno));
-    }
+    if (n == 0) break;
+    wbuf_.append(reinterpret_cast<const char*>(data), static_cast<size_t>(n));
   }
+  size_t off = 0;
+  while (off < wbuf_.size()) {
+    ssize_t w = send(fd_, wbuf_.data() + off, wbuf_.size() - off, MSG_NOSIGNAL);
+    if (w > 0) { off += static_cast<size_t>(w); continue; }
+    if (w < 0 && errno == EINTR) continue;
+    if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+      pollfd p{fd_, POLLOUT, 0};
+      poll(&p, 1, 1000);
+      continue;
+    }
+    dead_ = true;
+    return Unavailable(std::string("write: ") + strerror(errno));
+  }
+  return Status::Ok();
 }
 
 Status Channel::Pump(int timeout_ms) {

@@ -151,8 +151,9 @@ class Server {
 
   std::string name_;
   std::string socket_path_;
-  std::map<std::string, UnaryHandler> unary_;
-  std::map<std::string, StreamHandler> streams_;
+  // std::less<>: looked up by string_view straight from the HPACK-decoded :path.
+  std::map<std::string, UnaryHandler, std::less<>> unary_;
+  std::map<std::string, StreamHandler, std::less<>> streams_;
   int listen_fd_ = -1;
   std::vector<std::unique_ptr<Loop>> loops_;
   std::atomic<unsigned> next_loop_{0};
@@ -194,6 +195,7 @@ class Channel {
   void* session_ = nullptr;  // nghttp2_session*
   bool dead_ = false;
   bool got_settings_ = false;
+  std::string wbuf_;  // frames gathered by Flush() for one write
   std::map<int32_t, std::unique_ptr<CallState>> calls_;
   friend struct ChannelCallbacks;
 };

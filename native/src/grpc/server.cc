@@ -25,12 +25,12 @@ namespace {
 constexpr size_t kMaxRequestBytes = 16u << 20;  // 16 MiB, >> any kubelet request
 constexpr const char* kComp = "grpc-server";
 
-bool StartsWithGrpc(const std::string& ct) { return ct.rfind("application/grpc", 0) == 0; }
+bool StartsWithGrpc(std::string_view ct) { return ct.substr(0, 16) == "application/grpc"; }
 
-nghttp2_nv MakeNv(const char* name, const std::string& value) {
+nghttp2_nv MakeNv(std::string_view name, std::string_view value) {
   nghttp2_nv nv;
-  nv.name = reinterpret_cast<uint8_t*>(const_cast<char*>(name));
-  nv.namelen = strlen(name);
+  nv.name = reinterpret_cast<uint8_t*>(const_cast<char*>(name.data()));
+  nv.namelen = name.size();
   nv.value = reinterpret_cast<uint8_t*>(const_cast<char*>(value.data()));
   nv.valuelen = value.size();
   nv.flags = NGHTTP2_NV_FLAG_NONE;
@@ -40,8 +40,13 @@ nghttp2_nv MakeNv(const char* name, const std::string& value) {
 }  // namespace
 
 struct StreamState {
+  // Resolved from :path as the header arrives; `path` itself is only kept when
+  // it names no method (for the error) or calls are traced.
+  const UnaryHandler* unary = nullptr;
+  const StreamHandler* stream_handler = nullptr;
   std::string path;
-  std::string content_type;
+  bool grpc_content_type = false;
+  std::string content_type;  // only kept when it is not application/grpc*
   std::string body;
   bool dispatched = false;
   std::string out;       // framed response bytes not yet handed to nghttp2
@@ -84,6 +89,20 @@ class ServerConn {
     return it == streams_.end() ? nullptr : &it->second;
   }
   void Dispatch(int32_t sid);
+  void OnPath(StreamState* st, std::string_view v) {
+    auto u = srv_->unary_.find(v);
+    if (u != srv_->unary_.end()) {
+      st->unary = &u->second;
+    } else {
+      auto h = srv_->streams_.find(v);
+      if (h != srv_->streams_.end()) st->stream_handler = &h->second;
+    }
+    if ((!st->unary && !st->stream_handler) || srv_->trace_) st->path.assign(v);
+  }
+  void OnContentType(StreamState* st, std::string_view v) {
+    st->grpc_content_type = StartsWithGrpc(v);
+    if (!st->grpc_content_type) st->content_type.assign(v);
+  }
   void OnStreamClose(int32_t sid) {
     auto it = streams_.find(sid);
     if (it == streams_.end()) return;
@@ -109,6 +128,7 @@ class ServerConn {
   int fd_;
   nghttp2_session* session_ = nullptr;
   std::string wbuf_;
+  std::string resp_buf_;  // unary handler output, framed into the stream's `out`
   size_t woff_ = 0;
 };
 
@@ -130,8 +150,8 @@ static int OnHeader(nghttp2_session*, const nghttp2_frame* frame, const uint8_t*
   if (!st) return 0;
   std::string_view n(reinterpret_cast<const char*>(name), namelen);
   std::string_view v(reinterpret_cast<const char*>(value), valuelen);
-  if (n == ":path") st->path.assign(v);
-  else if (n == "content-type") st->content_type.assign(v);
+  if (n == ":path") c->OnPath(st, v);
+  else if (n == "content-type") c->OnContentType(st, v);
   return 0;
 }
 
@@ -186,6 +206,10 @@ bool ServerConn::Init() {
   nghttp2_option* opt;
   nghttp2_option_new(&opt);
   nghttp2_option_set_no_closed_streams(opt, 1);
+  // No per-header RFC 7540 §8 validation: the server only reads :path and
+  // content-type and answers anything else with a gRPC status (saves a pass over
+  // every header name and value per call).
+  nghttp2_option_set_no_http_messaging(opt, 1);
   int rv = nghttp2_session_server_new2(&session_, cbs, this, opt);
   nghttp2_option_del(opt);
   nghttp2_session_callbacks_del(cbs);
@@ -280,17 +304,16 @@ void ServerConn::SubmitTrailers(int32_t sid, StreamState* st) {
 }
 
 void ServerConn::SubmitTrailersOnly(int32_t sid, int code, const std::string& msg) {
-  std::string status = "200", ct = "application/grpc", c = std::to_string(code);
+  std::string c = std::to_string(code);
   std::string m = PercentEncode(msg);
-  nghttp2_nv nva[4] = {MakeNv(":status", status), MakeNv("content-type", ct),
+  nghttp2_nv nva[4] = {MakeNv(":status", "200"), MakeNv("content-type", "application/grpc"),
                        MakeNv("grpc-status", c), MakeNv("grpc-message", m)};
   nghttp2_submit_response(session_, sid, nva, m.empty() ? 3 : 4, nullptr);
   srv_->stats_.errors.Add(1);
 }
 
 void ServerConn::SubmitResponse(int32_t sid) {
-  std::string status = "200", ct = "application/grpc";
-  nghttp2_nv nva[2] = {MakeNv(":status", status), MakeNv("content-type", ct)};
+  nghttp2_nv nva[2] = {MakeNv(":status", "200"), MakeNv("content-type", "application/grpc")};
   nghttp2_data_provider prd;
   prd.source.ptr = nullptr;
   prd.read_callback = ReadCallback;
@@ -303,7 +326,7 @@ void ServerConn::Dispatch(int32_t sid) {
   st->dispatched = true;
   srv_->stats_.calls.Add(1);
 
-  if (!StartsWithGrpc(st->content_type)) {
+  if (!st->grpc_content_type) {
     SubmitTrailersOnly(sid, kGrpcInternal, "invalid content-type: " + st->content_type);
     return;
   }
@@ -327,11 +350,11 @@ void ServerConn::Dispatch(int32_t sid) {
     req = std::string_view(st->body).substr(5);
   }
 
-  auto u = srv_->unary_.find(st->path);
-  if (u != srv_->unary_.end()) {
-    std::string resp;
+  if (st->unary) {
+    std::string& resp = resp_buf_;  // reused across calls: no allocation once warm
+    resp.clear();
     auto t0 = srv_->trace_ ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
-    Status s = u->second(req, &resp);
+    Status s = (*st->unary)(req, &resp);
     if (srv_->trace_) {
       double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
       Logf(LogLevel::kInfo, "trace", "%s %s %s req=%zuB resp=%zuB handler=%.2fus", srv_->name_.c_str(),
@@ -348,8 +371,7 @@ void ServerConn::Dispatch(int32_t sid) {
     SubmitResponse(sid);
     return;
   }
-  auto ss = srv_->streams_.find(st->path);
-  if (ss != srv_->streams_.end()) {
+  if (st->stream_handler) {
     auto stream = std::make_shared<ServerStream>();
     stream->conn_ = this;
     stream->stream_id_ = sid;
@@ -357,7 +379,7 @@ void ServerConn::Dispatch(int32_t sid) {
     stream->loop_ = loop_;
     st->stream = stream;
     SubmitResponse(sid);
-    Status s = ss->second(req, stream);
+    Status s = (*st->stream_handler)(req, stream);
     if (!s.ok() && !stream->closed_) stream->Finish(s);
     return;
   }

@@ -8,6 +8,7 @@
 //   amdgpu-dp-uds-floor [--iters N] [--busy-poll-us U] [--req B] [--resp B]
 #include <poll.h>
 #include <sys/epoll.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -24,6 +25,14 @@
 namespace {
 
 using Clock = std::chrono::steady_clock;
+
+double ThreadCpuUs() {
+  rusage ru{};
+  getrusage(RUSAGE_THREAD, &ru);
+  return (ru.ru_utime.tv_sec + ru.ru_stime.tv_sec) * 1e6 + ru.ru_utime.tv_usec + ru.ru_stime.tv_usec;
+}
+
+std::atomic<double> g_server_cpu_us{0};
 
 void Server(int fd, int busy_poll_us, size_t resp_bytes, std::atomic<bool>* stop) {
   int ep = epoll_create1(0);
@@ -50,6 +59,7 @@ void Server(int fd, int busy_poll_us, size_t resp_bytes, std::atomic<bool>* stop
     }
   }
   close(ep);
+  g_server_cpu_us.store(ThreadCpuUs());
 }
 
 }  // namespace
@@ -91,10 +101,12 @@ int main(int argc, char** argv) {
   stop.store(true);
   shutdown(sv[0], SHUT_RDWR);
   t.join();
+  double client_cpu_us = ThreadCpuUs();
   std::sort(us.begin(), us.end());
   auto pct = [&](double p) { return us[static_cast<size_t>(p / 100.0 * (us.size() - 1))]; };
   printf("{\"iters\": %d, \"busy_poll_us\": %d, \"req_bytes\": %zu, \"resp_bytes\": %zu, \"p50_us\": %.2f, "
-         "\"p99_us\": %.2f, \"min_us\": %.2f}\n",
-         iters, busy, req, resp, pct(50), pct(99), us.front());
+         "\"p99_us\": %.2f, \"min_us\": %.2f, \"server_cpu_us_per_req\": %.3f, \"client_cpu_us_per_req\": %.3f}\n",
+         iters, busy, req, resp, pct(50), pct(99), us.front(), g_server_cpu_us.load() / (iters + 1000),
+         client_cpu_us / (iters + 1000));
   return 0;
 }

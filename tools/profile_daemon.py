@@ -20,6 +20,13 @@ from k8s_gpu_sharing_plugin_amd.models import fixtures  # noqa: E402
 from k8s_gpu_sharing_plugin_amd.utils import harness  # noqa: E402
 
 
+def _cpu_s(pid):
+    """utime + stime of a process, in seconds (/proc/<pid>/stat fields 14 and 15)."""
+    with open(f"/proc/{pid}/stat") as f:
+        fields = f.read().rsplit(")", 1)[1].split()
+    return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
@@ -38,9 +45,13 @@ def main():
     try:
         reg = k.wait(lambda e: e.get("event") == "register", 20)
         sock = os.path.join(d, reg["endpoint"])
+        cpu0 = _cpu_s(dm.proc.pid)
         r = json.loads(subprocess.run([KUBELET_STUB, "bench", "--socket", sock, "--pods", str(a.pods),
                                        "--warmup", "1000"], capture_output=True, text=True, timeout=600).stdout)
-        print(json.dumps({"allocate_p50_us": r["allocate"]["p50_us"], "pods_per_s": r["pods_per_s"]}))
+        cpu = _cpu_s(dm.proc.pid) - cpu0
+        rpcs = 2 * (a.pods + 1000)  # GetPreferredAllocation + Allocate per pod, warm-up included
+        print(json.dumps({"allocate_p50_us": r["allocate"]["p50_us"], "pods_per_s": r["pods_per_s"],
+                          "daemon_cpu_s": round(cpu, 3), "daemon_cpu_us_per_rpc": round(cpu / rpcs * 1e6, 3)}))
     finally:
         dm.stop()
         k.stop()
