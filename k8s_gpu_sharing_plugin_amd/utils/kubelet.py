@@ -64,7 +64,9 @@ class StubKubelet:
         return self
 
     def stop(self):
-        self._server.stop(0)
+        # Wait for the shutdown to finish: grpcio removes the socket file when it
+        # does, which would otherwise delete a new kubelet's socket at the same path.
+        self._server.stop(0).wait(10)
 
     def wait_registration(self, timeout=10.0):
         return self.registrations.get(timeout=timeout)

@@ -99,6 +99,12 @@ def test_metrics_exposition(served):
 
 def test_metrics_follow_health_and_healthz(served):
     d, k, c, port, fifo = served
+    # Registration reaches the kubelet before the daemon marks itself serving and
+    # starts the health monitor (which opens the event FIFO): wait for both.
+    d.wait_log("health monitor watching")
+    deadline = time.time() + 5
+    while time.time() < deadline and _get(port, "/healthz")[0] != 200:
+        time.sleep(0.05)
     assert _get(port, "/healthz") == (200, "ok\n")
     fd = os.open(fifo, os.O_WRONLY | os.O_NONBLOCK)
     os.write(fd, b"1 3 pre-reset\n")
