@@ -3,7 +3,7 @@
 //   amdgpu-dp-probe [--list] [--device N] [--bytes B] [--iters I]
 //                   [--expect-xcds X] [--expect-cus C] [--min-gbps G]
 //                   [--p2p [--min-p2p-gbps P]] [--mfma [--min-tflops T]]
-//                   [--census [--expect-cus-seen C]]
+//                   [--census [--expect-cus-seen C]] [--latency N] [--aggressor SECONDS]
 //
 // Runs the visibility probe (visibility_probe.hip) on every visible HIP device
 // (or one) and prints one JSON line per device. Exits non-zero when a device
@@ -18,6 +18,8 @@
 // exact; it fails on a wrong element or a rate below --min-tflops. --census
 // prints which XCDs/CUs the process's queues can use (the CU share of a
 // CU-partitioned replica, HSA_CU_MASK); --expect-cus-seen checks that count.
+// --latency N times N launches of a small kernel (what a latency-sensitive pod
+// sees); --aggressor S saturates the GPU for S seconds (a noisy neighbour).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -29,6 +31,8 @@ extern "C" int adp_probe_run(int device, unsigned long long bytes, int iters, ch
 extern "C" int adp_probe_p2p(int ndev, unsigned long long bytes, int iters, char* out, int len);
 extern "C" int adp_probe_mfma(int device, int iters, char* out, int len);
 extern "C" int adp_probe_census(int device, char* out, int len);
+extern "C" int adp_probe_latency(int device, int n, char* out, int len);
+extern "C" int adp_probe_aggressor(int device, double seconds, char* out, int len);
 
 namespace {
 
@@ -52,6 +56,8 @@ int main(int argc, char** argv) {
   long expect_xcds = -1, expect_cus = -1;
   double min_gbps = -1, min_p2p_gbps = -1, min_tflops = -1;
   long expect_cus_seen = -1;
+  int latency = 0;
+  double aggressor = 0;
   bool list = false, p2p = false, mfma = false, census = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -69,10 +75,12 @@ int main(int argc, char** argv) {
     else if (a == "--min-tflops") min_tflops = atof(next());
     else if (a == "--census") census = true;
     else if (a == "--expect-cus-seen") expect_cus_seen = atol(next());
+    else if (a == "--latency") latency = atoi(next());
+    else if (a == "--aggressor") aggressor = atof(next());
     else {
       fprintf(stderr, "usage: %s [--list] [--device N] [--bytes B] [--iters I] [--expect-xcds X] "
                       "[--expect-cus C] [--min-gbps G] [--p2p [--min-p2p-gbps P]] [--mfma [--min-tflops T]] "
-                      "[--census [--expect-cus-seen C]]\n",
+                      "[--census [--expect-cus-seen C]] [--latency N] [--aggressor SECONDS]\n",
               argv[0]);
       return 2;
     }
@@ -90,6 +98,13 @@ int main(int argc, char** argv) {
   }
   int failures = 0;
   for (int d = (device < 0 ? 0 : device); d < (device < 0 ? n : device + 1); ++d) {
+    if (aggressor > 0 || latency > 0) {
+      int arc = aggressor > 0 ? adp_probe_aggressor(d, aggressor, buf, sizeof(buf))
+                              : adp_probe_latency(d, latency, buf, sizeof(buf));
+      printf("%s\n", buf);
+      if (arc != 0) ++failures;
+      continue;
+    }
     if (census) {
       int crc = adp_probe_census(d, buf, sizeof(buf));
       printf("%s\n", buf);

@@ -25,6 +25,8 @@
 // Return 0 on success, a hipError_t (>0) on failure; `out` holds JSON either way.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -67,6 +69,28 @@ __global__ void __launch_bounds__(64) HoldCensusKernel(uint32_t* out, uint64_t h
     uint64_t t0 = wall_clock64();
     while (wall_clock64() - t0 < hold_ticks) __builtin_amdgcn_s_sleep(2);
   }
+}
+
+// Sharing-interference pair (amdgpu-dp-probe --latency / --aggressor): what a
+// latency-sensitive pod sees while a neighbour on the same GPU saturates it.
+// Victim: a short fixed chain of FMAs per lane (one small launch, ~10 us solo).
+__global__ void __launch_bounds__(256) VictimKernel(float* out, int iters) {
+  float a = threadIdx.x * 1e-3f, b = 1.0001f;
+  for (int i = 0; i < iters; ++i) a = __builtin_fmaf(a, b, 1e-7f);
+  if (a == -1.0f) out[blockIdx.x] = a;  // never true: keeps the chain alive
+}
+
+// Aggressor: every workgroup keeps its SIMD busy with dependent FMAs until
+// `ticks` of the 100 MHz wall clock have passed (a bounded spin: each wave exits
+// on its own clock check).
+__global__ void __launch_bounds__(256) AggressorKernel(float* out, uint64_t ticks) {
+  float a = threadIdx.x * 1e-3f, b = 0.9999f;
+  uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) a = __builtin_fmaf(a, b, 1e-7f);
+  }
+  if (a == -1.0f) out[blockIdx.x] = a;
 }
 
 __global__ void __launch_bounds__(256) FillKernel(uint4* p, size_t n) {
@@ -435,6 +459,59 @@ extern "C" int adp_probe_census(int device, char* out, int len) {
   s += "]}";
   if (static_cast<int>(s.size()) >= len) return 3;
   snprintf(out, len, "%s", s.c_str());
+  return 0;
+}
+
+// Launch-to-completion latency of a small kernel (VictimKernel, 2 workgroups per
+// CU) timed on the host, `n` times after a warm-up: {"p50_us", "p99_us", ...}.
+extern "C" int adp_probe_latency(int device, int n, char* out, int len) {
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (n < 1) n = 1;
+  float* d = nullptr;
+  const int blocks = prop.multiProcessorCount * 2;
+  HIP_TRY(hipMalloc(&d, blocks * sizeof(float)));
+  hipStream_t st;
+  HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  std::vector<double> us;
+  us.reserve(n);
+  for (int i = 0; i < n + 50; ++i) {
+    auto t0 = std::chrono::steady_clock::now();
+    hipLaunchKernelGGL(VictimKernel, dim3(blocks), dim3(256), 0, st, d, 2048);
+    HIP_TRY(hipStreamSynchronize(st));
+    if (i >= 50) us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+  }
+  HIP_TRY(hipStreamDestroy(st));
+  HIP_TRY(hipFree(d));
+  std::sort(us.begin(), us.end());
+  auto pct = [&](double p) { return us[static_cast<size_t>(p / 100.0 * (us.size() - 1))]; };
+  snprintf(out, len,
+           "{\"device\": %d, \"launches\": %d, \"p50_us\": %.1f, \"p90_us\": %.1f, \"p99_us\": %.1f, "
+           "\"max_us\": %.1f}",
+           device, n, pct(50), pct(90), pct(99), us.back());
+  return 0;
+}
+
+// Saturates the device for `seconds`: back-to-back AggressorKernel launches of
+// 8 workgroups x 256 lanes per CU, each holding its CUs for ~1 ms.
+extern "C" int adp_probe_aggressor(int device, double seconds, char* out, int len) {
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  float* d = nullptr;
+  const int blocks = prop.multiProcessorCount * 8;
+  HIP_TRY(hipMalloc(&d, blocks * sizeof(float)));
+  auto t0 = std::chrono::steady_clock::now();
+  long launches = 0;
+  while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < seconds) {
+    for (int k = 0; k < 4; ++k, ++launches)
+      hipLaunchKernelGGL(AggressorKernel, dim3(blocks), dim3(256), 0, 0, d, 100000ull);  // 1 ms
+    HIP_TRY(hipDeviceSynchronize());
+  }
+  HIP_TRY(hipFree(d));
+  snprintf(out, len, "{\"device\": %d, \"aggressor_launches\": %ld, \"seconds\": %.2f}", device, launches,
+           std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
   return 0;
 }
 
