@@ -115,6 +115,10 @@ const std::vector<FlagDef>& Table() {
        "after serving a request a gRPC loop polls without sleeping for this many "
        "microseconds, so follow-up calls skip a scheduler wake-up (0 = always sleep)",
        [](Flags& f) -> void* { return &f.busy_poll_us; }, true},
+      {"http2-server", "DP_HTTP2_SERVER", "http2Server", Kind::kString,
+       "HTTP/2 engine of the plugin sockets: [native | nghttp2] (native: hand-written framing "
+       "and flow control, nghttp2 HPACK decoding; nghttp2: its full session layer)",
+       [](Flags& f) -> void* { return &f.http2_server; }},
       {"node-labels-file", "DP_NODE_LABELS_FILE", "nodeLabelsFile", Kind::kString,
        "write node-feature labels (amd.com/gpu.product, .count, .memory-mib, partition modes, "
        "interconnect) to this file for node-feature-discovery's local source (empty = off)",

@@ -50,6 +50,7 @@ struct Flags {
   std::string node_labels_file; // "" = no NFD feature file
   std::string pod_resources_socket = "/var/lib/kubelet/pod-resources/kubelet.sock";
   uint64_t busy_poll_us = 50;
+  std::string http2_server = "native";
 };
 
 struct Config {

@@ -63,6 +63,9 @@ Result<Validated> Validate(const Config& cfg) {
   v.popts.kubelet_socket = f.kubelet_socket;
   v.popts.pass_device_specs = f.pass_device_specs;
   v.popts.replica_cu_mask = f.replica_cu_mask;
+  if (f.http2_server != "native" && f.http2_server != "nghttp2")
+    return InvalidArgument("invalid --http2-server option: " + f.http2_server);
+  v.popts.native_http2 = f.http2_server == "native";
   v.popts.driver_root = f.driver_root;
   v.popts.auto_replica_unit_mib = f.auto_replica_unit_mib;
   v.popts.server_threads = static_cast<int>(std::min<uint64_t>(f.server_threads, 64));

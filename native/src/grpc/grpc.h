@@ -11,7 +11,9 @@
 //     trailers-only responses for errors,
 //   * unary and server-streaming calls (ListAndWatch stays open for the life of
 //     the plugin and pushes a new device list on every health transition).
-// nghttp2 provides HPACK, flow control, SETTINGS/PING/GOAWAY handling.
+// The server's HTTP/2 connection layer is native (h2_conn.cc: framing, flow
+// control, SETTINGS/PING/GOAWAY; nghttp2 only for HPACK decoding); nghttp2's
+// session layer remains selectable for the server and drives the client.
 //
 // Threading: a Server runs N epoll loop threads; every connection is owned by
 // one loop and its handlers execute inline on that loop (they are O(k)
@@ -132,6 +134,9 @@ class Server {
   void set_trace(bool on) { trace_ = on; }
   // Keep polling (no sleep) for this long after each burst of activity. Set before Start().
   void set_busy_poll_us(int us) { busy_poll_us_ = us < 0 ? 0 : us; }
+  // HTTP/2 engine for accepted connections: the native one (default) or
+  // nghttp2's session layer. Set before Start().
+  void set_native_http2(bool on) { native_http2_ = on; }
 
   // Test hook: make the next iteration of loop 0 fail as if epoll_wait errored.
   void InjectLoopFailureForTest() { inject_failure_.store(true); }
@@ -163,6 +168,7 @@ class Server {
   std::atomic<uint64_t> next_stream_id_{1};
   bool trace_ = false;
   int busy_poll_us_ = 0;
+  bool native_http2_ = true;
   ServerStats stats_;
 };
 

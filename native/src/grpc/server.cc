@@ -18,6 +18,7 @@
 
 #include "common/log.h"
 #include "grpc/grpc.h"
+#include "grpc/server_conn.h"
 
 namespace adp::grpc {
 namespace {
@@ -62,26 +63,23 @@ struct StreamState {
   std::shared_ptr<ServerStream> stream;
 };
 
-class ServerConn {
+class Nghttp2Conn final : public ServerConn {
  public:
-  ServerConn(Server* srv, int loop, int fd) : srv_(srv), loop_(loop), fd_(fd) {}
-  ~ServerConn() {
-    for (auto& [_, st] : streams_) {
-      if (st.stream) { st.stream->closed_ = true; st.stream->conn_ = nullptr; }
-    }
+  Nghttp2Conn(Server* srv, int loop, int fd) : ServerConn(srv, loop, fd) {}
+  ~Nghttp2Conn() override {
+    for (auto& [_, st] : streams_) Detach(st.stream.get());
     if (session_) nghttp2_session_del(session_);
     if (fd_ >= 0) close(fd_);
   }
 
-  bool Init();
-  bool OnReadable();
-  bool Flush();
-  bool Done() const {
+  bool Init() override;
+  bool OnReadable() override;
+  bool Flush() override;
+  bool Done() const override {
     return !nghttp2_session_want_read(session_) && !nghttp2_session_want_write(session_) &&
            wbuf_.size() == woff_;
   }
-  bool want_epollout() const { return wbuf_.size() > woff_; }
-  int fd() const { return fd_; }
+  bool want_epollout() const override { return wbuf_.size() > woff_; }
 
   // --- called from nghttp2 callbacks ---
   StreamState* Find(int32_t sid) {
@@ -90,14 +88,9 @@ class ServerConn {
   }
   void Dispatch(int32_t sid);
   void OnPath(StreamState* st, std::string_view v) {
-    auto u = srv_->unary_.find(v);
-    if (u != srv_->unary_.end()) {
-      st->unary = &u->second;
-    } else {
-      auto h = srv_->streams_.find(v);
-      if (h != srv_->streams_.end()) st->stream_handler = &h->second;
-    }
-    if ((!st->unary && !st->stream_handler) || srv_->trace_) st->path.assign(v);
+    st->unary = FindUnary(v);
+    if (!st->unary) st->stream_handler = FindStreamHandler(v);
+    if ((!st->unary && !st->stream_handler) || tracing()) st->path.assign(v);
   }
   void OnContentType(StreamState* st, std::string_view v) {
     st->grpc_content_type = StartsWithGrpc(v);
@@ -106,26 +99,22 @@ class ServerConn {
   void OnStreamClose(int32_t sid) {
     auto it = streams_.find(sid);
     if (it == streams_.end()) return;
-    if (it->second.stream) { it->second.stream->closed_ = true; it->second.stream->conn_ = nullptr; }
+    Detach(it->second.stream.get());
     streams_.erase(it);
   }
   ssize_t ReadData(int32_t sid, uint8_t* buf, size_t len, uint32_t* flags);
 
   // --- used by ServerStream ---
-  bool QueueMessage(int32_t sid, std::string_view msg);
-  void Finish(int32_t sid, const Status& st);
+  bool QueueMessage(int32_t sid, std::string_view msg) override;
+  void Finish(int32_t sid, const Status& st) override;
 
-  Server* srv_;
-  int loop_;
   std::map<int32_t, StreamState> streams_;
-  uint32_t epoll_events = 0;  // interest set currently registered with epoll
 
  private:
   void SubmitTrailersOnly(int32_t sid, int code, const std::string& msg);
   void SubmitResponse(int32_t sid);
   void SubmitTrailers(int32_t sid, StreamState* st);
 
-  int fd_;
   nghttp2_session* session_ = nullptr;
   std::string wbuf_;
   std::string resp_buf_;  // unary handler output, framed into the stream's `out`
@@ -135,7 +124,7 @@ class ServerConn {
 // ------------------------- nghttp2 callbacks -------------------------
 
 static int OnBeginHeaders(nghttp2_session*, const nghttp2_frame* frame, void* ud) {
-  auto* c = static_cast<ServerConn*>(ud);
+  auto* c = static_cast<Nghttp2Conn*>(ud);
   if (frame->hd.type == NGHTTP2_HEADERS && frame->headers.cat == NGHTTP2_HCAT_REQUEST) {
     c->streams_[frame->hd.stream_id];
   }
@@ -144,7 +133,7 @@ static int OnBeginHeaders(nghttp2_session*, const nghttp2_frame* frame, void* ud
 
 static int OnHeader(nghttp2_session*, const nghttp2_frame* frame, const uint8_t* name,
                     size_t namelen, const uint8_t* value, size_t valuelen, uint8_t, void* ud) {
-  auto* c = static_cast<ServerConn*>(ud);
+  auto* c = static_cast<Nghttp2Conn*>(ud);
   if (frame->hd.type != NGHTTP2_HEADERS) return 0;
   StreamState* st = c->Find(frame->hd.stream_id);
   if (!st) return 0;
@@ -157,7 +146,7 @@ static int OnHeader(nghttp2_session*, const nghttp2_frame* frame, const uint8_t*
 
 static int OnDataChunk(nghttp2_session* s, uint8_t, int32_t sid, const uint8_t* data, size_t len,
                        void* ud) {
-  auto* c = static_cast<ServerConn*>(ud);
+  auto* c = static_cast<Nghttp2Conn*>(ud);
   StreamState* st = c->Find(sid);
   if (!st) return 0;
   if (st->dispatched) return 0;
@@ -173,7 +162,7 @@ static int OnDataChunk(nghttp2_session* s, uint8_t, int32_t sid, const uint8_t* 
 }
 
 static int OnFrameRecv(nghttp2_session*, const nghttp2_frame* frame, void* ud) {
-  auto* c = static_cast<ServerConn*>(ud);
+  auto* c = static_cast<Nghttp2Conn*>(ud);
   if ((frame->hd.type == NGHTTP2_DATA || frame->hd.type == NGHTTP2_HEADERS) &&
       (frame->hd.flags & NGHTTP2_FLAG_END_STREAM)) {
     c->Dispatch(frame->hd.stream_id);
@@ -182,18 +171,18 @@ static int OnFrameRecv(nghttp2_session*, const nghttp2_frame* frame, void* ud) {
 }
 
 static int OnStreamCloseCb(nghttp2_session*, int32_t sid, uint32_t, void* ud) {
-  static_cast<ServerConn*>(ud)->OnStreamClose(sid);
+  static_cast<Nghttp2Conn*>(ud)->OnStreamClose(sid);
   return 0;
 }
 
 static ssize_t ReadCallback(nghttp2_session*, int32_t sid, uint8_t* buf, size_t length,
                             uint32_t* data_flags, nghttp2_data_source*, void* ud) {
-  return static_cast<ServerConn*>(ud)->ReadData(sid, buf, length, data_flags);
+  return static_cast<Nghttp2Conn*>(ud)->ReadData(sid, buf, length, data_flags);
 }
 
-// ------------------------- ServerConn -------------------------
+// ------------------------- Nghttp2Conn -------------------------
 
-bool ServerConn::Init() {
+bool Nghttp2Conn::Init() {
   nghttp2_session_callbacks* cbs;
   nghttp2_session_callbacks_new(&cbs);
   nghttp2_session_callbacks_set_on_begin_headers_callback(cbs, OnBeginHeaders);
@@ -225,7 +214,7 @@ bool ServerConn::Init() {
   return Flush();
 }
 
-bool ServerConn::OnReadable() {
+bool Nghttp2Conn::OnReadable() {
   char buf[64 * 1024];
   while (true) {
     ssize_t n = read(fd_, buf, sizeof(buf));
@@ -246,7 +235,7 @@ bool ServerConn::OnReadable() {
   return Flush();
 }
 
-bool ServerConn::Flush() {
+bool Nghttp2Conn::Flush() {
   // Pull frames out of nghttp2 until it has nothing more (flow control bounds
   // how much it produces), then write as much as the socket takes.
   while (true) {
@@ -268,7 +257,7 @@ bool ServerConn::Flush() {
   return true;
 }
 
-ssize_t ServerConn::ReadData(int32_t sid, uint8_t* buf, size_t len, uint32_t* flags) {
+ssize_t Nghttp2Conn::ReadData(int32_t sid, uint8_t* buf, size_t len, uint32_t* flags) {
   StreamState* st = Find(sid);
   if (!st) return NGHTTP2_ERR_TEMPORAL_CALLBACK_FAILURE;
   size_t avail = st->out.size() - st->out_off;
@@ -296,23 +285,23 @@ ssize_t ServerConn::ReadData(int32_t sid, uint8_t* buf, size_t len, uint32_t* fl
   return static_cast<ssize_t>(n);
 }
 
-void ServerConn::SubmitTrailers(int32_t sid, StreamState* st) {
+void Nghttp2Conn::SubmitTrailers(int32_t sid, StreamState* st) {
   std::string code = std::to_string(st->grpc_status);
   std::string msg = PercentEncode(st->grpc_message);
   nghttp2_nv nva[2] = {MakeNv("grpc-status", code), MakeNv("grpc-message", msg)};
   nghttp2_submit_trailer(session_, sid, nva, msg.empty() ? 1 : 2);
 }
 
-void ServerConn::SubmitTrailersOnly(int32_t sid, int code, const std::string& msg) {
+void Nghttp2Conn::SubmitTrailersOnly(int32_t sid, int code, const std::string& msg) {
   std::string c = std::to_string(code);
   std::string m = PercentEncode(msg);
   nghttp2_nv nva[4] = {MakeNv(":status", "200"), MakeNv("content-type", "application/grpc"),
                        MakeNv("grpc-status", c), MakeNv("grpc-message", m)};
   nghttp2_submit_response(session_, sid, nva, m.empty() ? 3 : 4, nullptr);
-  srv_->stats_.errors.Add(1);
+  CountError();
 }
 
-void ServerConn::SubmitResponse(int32_t sid) {
+void Nghttp2Conn::SubmitResponse(int32_t sid) {
   nghttp2_nv nva[2] = {MakeNv(":status", "200"), MakeNv("content-type", "application/grpc")};
   nghttp2_data_provider prd;
   prd.source.ptr = nullptr;
@@ -320,11 +309,11 @@ void ServerConn::SubmitResponse(int32_t sid) {
   nghttp2_submit_response(session_, sid, nva, 2, &prd);
 }
 
-void ServerConn::Dispatch(int32_t sid) {
+void Nghttp2Conn::Dispatch(int32_t sid) {
   StreamState* st = Find(sid);
   if (!st || st->dispatched) return;
   st->dispatched = true;
-  srv_->stats_.calls.Add(1);
+  CountCall();
 
   if (!st->grpc_content_type) {
     SubmitTrailersOnly(sid, kGrpcInternal, "invalid content-type: " + st->content_type);
@@ -353,11 +342,11 @@ void ServerConn::Dispatch(int32_t sid) {
   if (st->unary) {
     std::string& resp = resp_buf_;  // reused across calls: no allocation once warm
     resp.clear();
-    auto t0 = srv_->trace_ ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
+    auto t0 = tracing() ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
     Status s = (*st->unary)(req, &resp);
-    if (srv_->trace_) {
+    if (tracing()) {
       double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-      Logf(LogLevel::kInfo, "trace", "%s %s %s req=%zuB resp=%zuB handler=%.2fus", srv_->name_.c_str(),
+      Logf(LogLevel::kInfo, "trace", "%s %s %s req=%zuB resp=%zuB handler=%.2fus", server_name().c_str(),
            st->path.c_str(), s.ok() ? "OK" : s.ToString().c_str(), req.size(), resp.size(), us);
     }
     st = Find(sid);  // handler cannot erase streams, but be defensive
@@ -372,21 +361,17 @@ void ServerConn::Dispatch(int32_t sid) {
     return;
   }
   if (st->stream_handler) {
-    auto stream = std::make_shared<ServerStream>();
-    stream->conn_ = this;
-    stream->stream_id_ = sid;
-    stream->id_ = srv_->next_stream_id_.fetch_add(1, std::memory_order_relaxed);
-    stream->loop_ = loop_;
+    auto stream = OpenStream(sid);
     st->stream = stream;
     SubmitResponse(sid);
     Status s = (*st->stream_handler)(req, stream);
-    if (!s.ok() && !stream->closed_) stream->Finish(s);
+    if (!s.ok() && !StreamClosed(*stream)) stream->Finish(s);
     return;
   }
   SubmitTrailersOnly(sid, kGrpcUnimplemented, "unknown method " + st->path);
 }
 
-bool ServerConn::QueueMessage(int32_t sid, std::string_view msg) {
+bool Nghttp2Conn::QueueMessage(int32_t sid, std::string_view msg) {
   StreamState* st = Find(sid);
   if (!st || st->finishing) return false;
   if (st->out.size() == st->out_off) {
@@ -407,7 +392,7 @@ bool ServerConn::QueueMessage(int32_t sid, std::string_view msg) {
   return true;
 }
 
-void ServerConn::Finish(int32_t sid, const Status& s) {
+void Nghttp2Conn::Finish(int32_t sid, const Status& s) {
   StreamState* st = Find(sid);
   if (!st || st->finishing) return;
   st->finishing = true;
@@ -417,6 +402,10 @@ void ServerConn::Finish(int32_t sid, const Status& s) {
     st->deferred = false;
     nghttp2_session_resume_data(session_, sid);
   }
+}
+
+std::unique_ptr<ServerConn> MakeNghttp2Conn(Server* srv, int loop, int fd) {
+  return std::make_unique<Nghttp2Conn>(srv, loop, fd);
 }
 
 // ------------------------- ServerStream -------------------------
@@ -579,7 +568,7 @@ void Server::DrainPosted(Loop& l) {
 }
 
 void Server::AddConn(Loop& l, int fd) {
-  auto conn = std::make_unique<ServerConn>(this, l.index, fd);
+  auto conn = native_http2_ ? MakeH2Conn(this, l.index, fd) : MakeNghttp2Conn(this, l.index, fd);
   if (!conn->Init()) return;  // closes fd
   epoll_event ev{};
   ev.events = EPOLLIN | (conn->want_epollout() ? static_cast<uint32_t>(EPOLLOUT) : 0u);

@@ -487,6 +487,7 @@ Status Plugin::Start(std::function<void()> on_fatal) {
   law_streams_.assign(threads, {});
   srv->set_trace(opts_.trace);
   srv->set_busy_poll_us(opts_.busy_poll_us);
+  srv->set_native_http2(opts_.native_http2);
   srv->AddUnary(std::string(kSvc) + "GetDevicePluginOptions",
                 [this](std::string_view q, std::string* r) { return HandleGetOptions(q, r); });
   srv->AddUnary(std::string(kSvc) + "Allocate",

@@ -86,6 +86,7 @@ struct PluginOptions {
   // 1/R of every XCD's CUs (HSA_CU_MASK), so co-scheduled pods stop contending
   // for the same CUs -- the MI355X analogue of an MPS active-thread share.
   bool replica_cu_mask = false;
+  bool native_http2 = true;  // HTTP/2 engine of the plugin sockets (false: nghttp2)
 };
 
 // HSA_CU_MASK bit ranges [first, last] of each of `replicas` CU shares of a device

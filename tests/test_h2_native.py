@@ -1,0 +1,302 @@
+"""The native HTTP/2 engine (native/src/grpc/h2_conn.cc) at the frame level.
+
+A raw-socket HTTP/2 client drives the protocol corners that gRPC peers (grpc-go
+in the kubelet, grpcio here) may use but the end-to-end suites do not force:
+CONTINUATION, padding and priority fields, PING and SETTINGS acknowledgements,
+a peer that shrinks the stream window to a few bytes and the HPACK table to 0
+(server DATA must follow the windows; its next header block must start with a
+table size update), and connection errors answered with GOAWAY. The server's
+header blocks use only static-table indices and raw literals, so this client
+decodes them without a full HPACK implementation.
+"""
+
+import os
+import socket
+import struct
+
+import pytest
+
+from k8s_gpu_sharing_plugin_amd.models import fixtures
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
+
+PREFACE = b"PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n"
+DATA, HEADERS, PRIORITY, RST_STREAM, SETTINGS, PUSH_PROMISE, PING, GOAWAY, WINDOW_UPDATE, CONTINUATION = range(10)
+END_STREAM, ACK, END_HEADERS, PADDED, PRIO = 0x1, 0x1, 0x4, 0x8, 0x20
+SVC = "/v1beta1.DevicePlugin/"
+
+
+def frame(ftype, flags, sid, payload=b""):
+    return struct.pack(">I", len(payload))[1:] + bytes([ftype, flags]) + struct.pack(">I", sid) + payload
+
+
+def hpack_int(v, prefix, first=0):
+    mx = (1 << prefix) - 1
+    if v < mx:
+        return bytes([first | v])
+    out = [first | mx]
+    v -= mx
+    while v >= 128:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    return bytes(out + [v])
+
+
+def literal(name, value):
+    n, v = name.encode(), value.encode()
+    return b"\x00" + hpack_int(len(n), 7) + n + hpack_int(len(v), 7) + v
+
+
+def request_block(method):
+    return b"".join(literal(k, v) for k, v in [
+        (":method", "POST"), (":scheme", "http"), (":path", SVC + method), (":authority", "localhost"),
+        ("content-type", "application/grpc"), ("te", "trailers")])
+
+
+def pb_len(field, payload):
+    return hpack_varint(field << 3 | 2) + hpack_varint(len(payload)) + payload
+
+
+def hpack_varint(v):
+    out = b""
+    while v >= 0x80:
+        out += bytes([(v & 0x7F) | 0x80])
+        v >>= 7
+    return out + bytes([v])
+
+
+def grpc_frame(msg):
+    return b"\x00" + struct.pack(">I", len(msg)) + msg
+
+
+STATIC = {8: (":status", "200"), 31: ("content-type", None)}
+
+
+def decode_block(b):
+    """Server header blocks: indexed static fields, literals without indexing, size updates."""
+    out, i, updates = [], 0, []
+
+    def integer(prefix):
+        nonlocal i
+        mx = (1 << prefix) - 1
+        v = b[i] & mx
+        i += 1
+        if v < mx:
+            return v
+        m = 0
+        while True:
+            c = b[i]
+            i += 1
+            v += (c & 0x7F) << m
+            m += 7
+            if not c & 0x80:
+                return v
+
+    def string():
+        nonlocal i
+        assert not b[i] & 0x80, "server header strings are never Huffman-coded"
+        n = integer(7)
+        s = b[i:i + n].decode()
+        i += n
+        return s
+    while i < len(b):
+        c = b[i]
+        if c & 0x80:
+            out.append(STATIC[integer(7)])
+        elif c & 0xE0 == 0x20:
+            updates.append(integer(5))
+        else:
+            assert c & 0xF0 == 0x00, f"unexpected HPACK representation {c:#x}"
+            idx = integer(4)
+            name = STATIC[idx][0] if idx else string()
+            out.append((name, string()))
+    return out, updates
+
+
+class Conn:
+    def __init__(self, path, settings=b""):
+        self.s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        self.s.settimeout(5)
+        self.s.connect(path)
+        self.buf = b""
+        self.s.sendall(PREFACE + frame(SETTINGS, 0, 0, settings))
+
+    def send(self, *frames):
+        self.s.sendall(b"".join(frames))
+
+    def read_frame(self):
+        while len(self.buf) < 9 or len(self.buf) < 9 + int.from_bytes(self.buf[:3], "big"):
+            chunk = self.s.recv(1 << 20)
+            if not chunk:
+                raise ConnectionError("closed")
+            self.buf += chunk
+        n = int.from_bytes(self.buf[:3], "big")
+        f = (self.buf[3], self.buf[4], int.from_bytes(self.buf[5:9], "big") & 0x7FFFFFFF, self.buf[9:9 + n])
+        self.buf = self.buf[9 + n:]
+        return f
+
+    def call(self, sid, on_frame=None):
+        """Frames of stream `sid` until END_STREAM: (headers, data, trailers, all frames)."""
+        blocks, data, seen = [], b"", []
+        while True:
+            ftype, flags, fsid, payload = self.read_frame()
+            seen.append((ftype, flags, fsid, len(payload)))
+            if on_frame:
+                on_frame(ftype, flags, fsid, payload)
+            if fsid != sid:
+                continue
+            if ftype == HEADERS:
+                blocks.append(payload)
+            elif ftype == DATA:
+                data += payload
+            if flags & END_STREAM and ftype in (HEADERS, DATA):
+                return blocks, data, seen
+
+    def close(self):
+        self.s.close()
+
+
+@pytest.fixture
+def plugin(scratch):
+    started = []
+
+    def start(fx=None, args=()):
+        k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+        d = harness.Daemon(scratch, fx or fixtures.node(2), args=list(args)).start()
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        started.append((d, k, c))
+        return d, os.path.join(scratch, reg.endpoint), ids
+    yield start
+    for d, k, c in started:
+        c.close()
+        d.stop()
+        k.stop()
+
+
+def allocate_msg(ids):
+    return grpc_frame(pb_len(1, b"".join(pb_len(1, i.encode()) for i in ids)))
+
+
+def test_continuation_padding_priority_and_split_data(plugin):
+    d, path, ids = plugin()
+    c = Conn(path)
+    block = request_block("Allocate")
+    # HEADERS: padded (3 bytes) + priority fields, first half of the block; CONTINUATION: the rest.
+    h = bytes([3]) + struct.pack(">IB", 0, 15) + block[:20] + b"\x00" * 3
+    msg = allocate_msg([ids[1]])
+    c.send(frame(HEADERS, PADDED | PRIO, 1, h), frame(CONTINUATION, END_HEADERS, 1, block[20:]),
+           frame(DATA, PADDED, 1, bytes([4]) + msg[:7] + b"\x00" * 4),
+           frame(DATA, END_STREAM, 1, msg[7:]))
+    blocks, data, _ = c.call(1)
+    heads, _ = decode_block(blocks[0])
+    assert (":status", "200") in heads and ("content-type", "application/grpc") in heads
+    trailers, _ = decode_block(blocks[-1])
+    assert ("grpc-status", "0") in trailers
+    assert data[0] == 0 and int.from_bytes(data[1:5], "big") == len(data) - 5
+    assert b"/dev/kfd" in data and b"renderD136" in data  # GPU 1's render node
+    c.close()
+
+
+def test_ping_settings_ack_and_unknown_frames(plugin):
+    d, path, ids = plugin()
+    c = Conn(path)
+    c.send(frame(0xEE, 0, 0, b"ignored extension frame"), frame(PING, 0, 0, b"12345678"))
+    got = set()
+    while not {"settings", "settings-ack", "ping"} <= got:
+        ftype, flags, sid, payload = c.read_frame()
+        if ftype == SETTINGS and not flags & ACK:
+            got.add("settings")
+            params = {struct.unpack(">H", payload[i:i + 2])[0]: struct.unpack(">I", payload[i + 2:i + 6])[0]
+                      for i in range(0, len(payload), 6)}
+            assert params[0x3] == 1024 and params[0x4] == 1 << 20  # MAX_CONCURRENT_STREAMS, INITIAL_WINDOW_SIZE
+        elif ftype == SETTINGS:
+            got.add("settings-ack")
+        elif ftype == PING:
+            assert flags & ACK and payload == b"12345678"
+            got.add("ping")
+    # Unknown method and bad content-type: trailers-only gRPC errors, connection stays up.
+    c.send(frame(HEADERS, END_HEADERS | END_STREAM, 1, request_block("Nope")))
+    blocks, _, _ = c.call(1)
+    fields = dict(decode_block(blocks[0])[0])
+    assert fields["grpc-status"] == "12" and "unknown method" in fields["grpc-message"]
+    c.send(frame(HEADERS, END_HEADERS, 3, request_block("Allocate")),
+           frame(DATA, END_STREAM, 3, allocate_msg([ids[0]])))
+    blocks, data, _ = c.call(3)
+    assert ("grpc-status", "0") in decode_block(blocks[-1])[0] and b"/dev/kfd" in data
+    c.close()
+
+
+def test_tiny_windows_and_zero_header_table(plugin):
+    """A peer with a 1000-byte stream window and an HPACK table of 0: the 154 KB
+    ListAndWatch of a 2,352-unit node arrives in window-sized DATA frames as the
+    peer grants credit, and the response header block opens with a size update."""
+    d, path, ids = plugin(fixtures.node(8), ["--resource-config", "gpu:gpu-mem-gb:-1"])
+    assert len(ids) == 2352
+    win = 1000
+    c = Conn(path, struct.pack(">HI", 0x1, 0) + struct.pack(">HI", 0x4, win))
+    c.send(frame(HEADERS, END_HEADERS, 1, request_block("ListAndWatch")), frame(DATA, END_STREAM, 1, b""))
+    blocks, data, frames = [], b"", 0
+    while len(data) < 5 or len(data) < 5 + int.from_bytes(data[1:5], "big"):
+        ftype, flags, sid, payload = c.read_frame()
+        if sid != 1:
+            continue
+        if ftype == HEADERS:
+            blocks.append(payload)
+        elif ftype == DATA:
+            assert len(payload) <= win, "DATA beyond the stream window"
+            data += payload
+            frames += 1
+            # grant exactly what was consumed, on the stream and the connection
+            c.send(frame(WINDOW_UPDATE, 0, 1, struct.pack(">I", len(payload))),
+                   frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", len(payload))))
+    heads, updates = decode_block(blocks[0])
+    assert updates == [0] and (":status", "200") in heads
+    assert frames >= len(data) // win and len(data) > 150_000
+    assert data.count(b"-replica-") == 2352
+    c.close()
+
+
+@pytest.mark.parametrize("bad", [
+    frame(DATA, 0, 0, b"x"),                               # DATA on stream 0
+    frame(HEADERS, END_HEADERS, 2, b""),                   # even (server-initiated) stream id
+    frame(PUSH_PROMISE, END_HEADERS, 1, b"\x00" * 4),      # clients never push
+    frame(SETTINGS, 0, 0, b"\x00\x04\x80\x00\x00\x00"),    # INITIAL_WINDOW_SIZE > 2^31-1
+    frame(HEADERS, 0, 1, b"\x82") + frame(PING, 0, 0, b"8 bytes!"),  # CONTINUATION expected
+    frame(PING, 0, 0, b"short"),                           # PING length
+    frame(HEADERS, END_HEADERS, 1, b"\xff\xff\xff\xff\x0f"),  # undecodable HPACK
+])
+def test_connection_errors_are_answered_with_goaway(plugin, bad):
+    d, path, ids = plugin()
+    c = Conn(path)
+    c.send(bad)
+    while True:
+        try:
+            ftype, flags, sid, payload = c.read_frame()
+        except (ConnectionError, socket.timeout, ConnectionResetError):
+            pytest.fail("connection closed without GOAWAY")
+        if ftype == GOAWAY:
+            assert struct.unpack(">I", payload[4:8])[0] != 0  # an error code, not NO_ERROR
+            break
+    c.close()
+    # the daemon keeps serving
+    c2 = Conn(path)
+    c2.send(frame(HEADERS, END_HEADERS, 1, request_block("Allocate")), frame(DATA, END_STREAM, 1, allocate_msg(ids[:1])))
+    blocks, data, _ = c2.call(1)
+    assert ("grpc-status", "0") in decode_block(blocks[-1])[0]
+    c2.close()
+
+
+def test_rst_stream_cancels_a_watch(plugin):
+    d, path, ids = plugin()
+    c = Conn(path)
+    c.send(frame(HEADERS, END_HEADERS, 1, request_block("ListAndWatch")), frame(DATA, END_STREAM, 1, b""))
+    while True:
+        ftype, flags, sid, payload = c.read_frame()
+        if sid == 1 and ftype == DATA:
+            break
+    c.send(frame(RST_STREAM, 0, 1, struct.pack(">I", 8)),  # CANCEL
+           frame(HEADERS, END_HEADERS, 3, request_block("Allocate")), frame(DATA, END_STREAM, 3, allocate_msg(ids[:1])))
+    blocks, data, _ = c.call(3)
+    assert ("grpc-status", "0") in decode_block(blocks[-1])[0]
+    c.close()
