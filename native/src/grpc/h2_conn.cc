@@ -17,8 +17,8 @@
 // size update it implies); PING/ACK; GOAWAY (received: finish open streams;
 // sent on connection errors); RST_STREAM; WINDOW_UPDATE; connection and stream
 // flow control in both directions; HEADERS with PADDED/PRIORITY and
-// CONTINUATION; padded DATA; unknown frame types ignored. Responses never use
-// the HPACK dynamic table (literal-without-indexing / static indices only).
+// CONTINUATION; padded DATA; unknown frame types ignored. The response encoder
+// indexes only content-type and grpc-status 0 (see PutContentType).
 // Peer compatibility: exercised against grpcio (gRPC C-core) and nghttp2
 // clients by the end-to-end and robustness suites.
 #include <errno.h>
@@ -108,13 +108,13 @@ void PutLiteral(std::string* o, std::string_view name, std::string_view value) {
   o->append(value);
 }
 
-// ":status: 200" (static index 8) + "content-type: application/grpc" (literal
-// without indexing, name = static index 31).
-constexpr char kResponseHeaders[] = "\x88\x0f\x10\x10" "application/grpc";
-constexpr size_t kResponseHeadersLen = sizeof(kResponseHeaders) - 1;
-// "grpc-status: 0" as a literal without indexing.
-constexpr char kTrailersOk[] = "\x00\x0bgrpc-status\x01" "0";
-constexpr size_t kTrailersOkLen = sizeof(kTrailersOk) - 1;
+// The two header fields every response repeats. The encoder inserts each into
+// the HPACK dynamic table the first time it sends it (literal with incremental
+// indexing) and refers to it by index afterwards, so the peer's decoder does a
+// table lookup instead of copying strings -- what nghttp2's deflater would do.
+// Nothing else is ever inserted, so the table holds at most these two entries
+// (32 + 12 + 16 and 32 + 11 + 1 = 104 bytes) and never evicts.
+constexpr size_t kDynEntriesSize = 104;
 
 struct H2Stream {
   const UnaryHandler* unary = nullptr;
@@ -207,6 +207,11 @@ class H2Conn final : public ServerConn {
   int64_t conn_send_window_ = kDefaultWindow;
   uint32_t hpack_table_size_ = 4096;  // our encoder's table limit as the peer set it
   bool hpack_size_update_ = false;    // emit a table size update in the next block
+  // HPACK encoder dynamic table: insertion number of content-type / grpc-status 0
+  // (-1 = not inserted); index = 62 + (inserted - 1 - number).
+  int dyn_ct_ = -1, dyn_status0_ = -1, dyn_inserted_ = 0;
+  void PutContentType(std::string* b);
+  void PutStatusOk(std::string* b);
 
   // Receive side.
   uint32_t conn_recv_unacked_ = 0;
@@ -502,10 +507,12 @@ bool H2Conn::OnSettings(uint8_t flags, uint32_t sid, const uint8_t* p, size_t le
     uint16_t id = static_cast<uint16_t>((p[i] << 8) | p[i + 1]);
     uint32_t v = Get32(p + i + 2);
     switch (id) {
-      case 0x1:  // HEADER_TABLE_SIZE: our encoder must not exceed it (we never index)
+      case 0x1:  // HEADER_TABLE_SIZE: our encoder must not exceed it
         if (v < hpack_table_size_) {
           hpack_table_size_ = v;
-          hpack_size_update_ = true;
+          hpack_size_update_ = true;  // next block: size update 0 + v, table restarts empty
+          dyn_ct_ = dyn_status0_ = -1;
+          dyn_inserted_ = 0;
         }
         break;
       case 0x2:  // ENABLE_PUSH
@@ -580,16 +587,39 @@ void H2Conn::WindowUpdate(uint32_t sid, uint32_t inc) {
   Put32(&wbuf_, inc);
 }
 
+void H2Conn::PutContentType(std::string* b) {
+  if (dyn_ct_ >= 0) {
+    PutHpackInt(b, 0x80, 7, 62 + (dyn_inserted_ - 1 - dyn_ct_));
+  } else if (hpack_table_size_ >= kDynEntriesSize) {
+    b->append("\x5f\x10" "application/grpc");  // incremental indexing, name = static 31
+    dyn_ct_ = dyn_inserted_++;
+  } else {
+    b->append("\x0f\x10\x10" "application/grpc");  // without indexing
+  }
+}
+
+void H2Conn::PutStatusOk(std::string* b) {
+  if (dyn_status0_ >= 0) {
+    PutHpackInt(b, 0x80, 7, 62 + (dyn_inserted_ - 1 - dyn_status0_));
+  } else if (hpack_table_size_ >= kDynEntriesSize) {
+    b->append("\x40\x0bgrpc-status\x01" "0", 15);  // incremental indexing, new name
+    dyn_status0_ = dyn_inserted_++;
+  } else {
+    PutLiteral(b, "grpc-status", "0");
+  }
+}
+
 void H2Conn::SendHeaderBlock(uint32_t sid, std::string_view block, bool end_stream) {
+  // `block` was encoded against the table state after any pending size update
+  // (the callers build it after this connection's SETTINGS were applied).
   std::string_view prefix;
-  char upd[8];
-  size_t upd_len = 0;
-  if (hpack_size_update_) {  // RFC 7541 §4.2: first block after the peer lowered the limit
-    std::string u;
-    PutHpackInt(&u, 0x20, 5, hpack_table_size_);
-    upd_len = u.size();
-    memcpy(upd, u.data(), upd_len);
-    prefix = std::string_view(upd, upd_len);
+  std::string upd;
+  if (hpack_size_update_) {
+    // RFC 7541 §4.2: first block after the peer lowered SETTINGS_HEADER_TABLE_SIZE.
+    // Size 0 first (evicts everything), then the new limit.
+    upd.push_back(0x20);
+    if (hpack_table_size_ > 0) PutHpackInt(&upd, 0x20, 5, hpack_table_size_);
+    prefix = upd;
     hpack_size_update_ = false;
   }
   const size_t total = prefix.size() + block.size();
@@ -616,11 +646,14 @@ void H2Conn::SendHeaderBlock(uint32_t sid, std::string_view block, bool end_stre
 }
 
 void H2Conn::SendResponseHeaders(uint32_t sid) {
-  SendHeaderBlock(sid, std::string_view(kResponseHeaders, kResponseHeadersLen), false);
+  hblock_.assign(1, '\x88');  // :status 200 (static index 8)
+  PutContentType(&hblock_);
+  SendHeaderBlock(sid, hblock_, false);
 }
 
 void H2Conn::SendTrailersOnly(uint32_t sid, int code, std::string_view msg) {
-  hblock_.assign(kResponseHeaders, kResponseHeadersLen);
+  hblock_.assign(1, '\x88');
+  PutContentType(&hblock_);
   PutLiteral(&hblock_, "grpc-status", std::to_string(code));
   std::string m = PercentEncode(msg.substr(0, kMaxGrpcMessageHeader));
   if (!m.empty()) PutLiteral(&hblock_, "grpc-message", m);
@@ -630,7 +663,9 @@ void H2Conn::SendTrailersOnly(uint32_t sid, int code, std::string_view msg) {
 
 void H2Conn::SendTrailers(uint32_t sid, H2Stream& st) {
   if (st.grpc_status == 0 && st.grpc_message.empty()) {
-    SendHeaderBlock(sid, std::string_view(kTrailersOk, kTrailersOkLen), true);
+    hblock_.clear();
+    PutStatusOk(&hblock_);
+    SendHeaderBlock(sid, hblock_, true);
   } else {
     hblock_.clear();
     PutLiteral(&hblock_, "grpc-status", std::to_string(st.grpc_status));

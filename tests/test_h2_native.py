@@ -5,9 +5,9 @@ in the kubelet, grpcio here) may use but the end-to-end suites do not force:
 CONTINUATION, padding and priority fields, PING and SETTINGS acknowledgements,
 a peer that shrinks the stream window to a few bytes and the HPACK table to 0
 (server DATA must follow the windows; its next header block must start with a
-table size update), and connection errors answered with GOAWAY. The server's
-header blocks use only static-table indices and raw literals, so this client
-decodes them without a full HPACK implementation.
+table size update and must not index), and connection errors answered with
+GOAWAY. The server's header blocks use static indices, raw literals and at most
+two dynamic-table entries, so a small decoder here follows them exactly.
 """
 
 import os
@@ -68,11 +68,14 @@ def grpc_frame(msg):
     return b"\x00" + struct.pack(">I", len(msg)) + msg
 
 
-STATIC = {8: (":status", "200"), 31: ("content-type", None)}
+STATIC = {8: (":status", "200"), 31: ("content-type", "")}
 
 
-def decode_block(b):
-    """Server header blocks: indexed static fields, literals without indexing, size updates."""
+def decode_block(b, dyn=None):
+    """Server header blocks: indexed fields (static or dynamic), literals with or
+    without indexing, size updates. `dyn` is the connection's dynamic table
+    (newest first), updated in place."""
+    dyn = [] if dyn is None else dyn
     out, i, updates = [], 0, []
 
     def integer(prefix):
@@ -98,16 +101,28 @@ def decode_block(b):
         s = b[i:i + n].decode()
         i += n
         return s
+
+    def entry(idx):
+        return STATIC[idx] if idx < 62 else dyn[idx - 62]
     while i < len(b):
         c = b[i]
         if c & 0x80:
-            out.append(STATIC[integer(7)])
+            out.append(entry(integer(7)))
+        elif c & 0xC0 == 0x40:  # literal with incremental indexing
+            idx = integer(6)
+            name = entry(idx)[0] if idx else string()
+            field = (name, string())
+            dyn.insert(0, field)
+            out.append(field)
         elif c & 0xE0 == 0x20:
-            updates.append(integer(5))
+            size = integer(5)
+            updates.append(size)
+            if size == 0:
+                dyn.clear()
         else:
-            assert c & 0xF0 == 0x00, f"unexpected HPACK representation {c:#x}"
+            assert c & 0xE0 == 0x00, f"unexpected HPACK representation {c:#x}"
             idx = integer(4)
-            name = STATIC[idx][0] if idx else string()
+            name = entry(idx)[0] if idx else string()
             out.append((name, string()))
     return out, updates
 
@@ -118,7 +133,11 @@ class Conn:
         self.s.settimeout(5)
         self.s.connect(path)
         self.buf = b""
+        self.dyn = []  # the server encoder's HPACK dynamic table, as this decoder sees it
         self.s.sendall(PREFACE + frame(SETTINGS, 0, 0, settings))
+
+    def decode(self, block):
+        return decode_block(block, self.dyn)
 
     def send(self, *frames):
         self.s.sendall(b"".join(frames))
@@ -135,17 +154,21 @@ class Conn:
         return f
 
     def call(self, sid, on_frame=None):
-        """Frames of stream `sid` until END_STREAM: (headers, data, trailers, all frames)."""
+        """Frames of stream `sid` until END_STREAM: (decoded header blocks as
+        (fields, size updates), data, all frames). Every HEADERS block is decoded
+        in arrival order so the dynamic table stays in step with the server's."""
         blocks, data, seen = [], b"", []
         while True:
             ftype, flags, fsid, payload = self.read_frame()
             seen.append((ftype, flags, fsid, len(payload)))
             if on_frame:
                 on_frame(ftype, flags, fsid, payload)
+            if ftype == HEADERS:
+                decoded = self.decode(payload)
+                if fsid == sid:
+                    blocks.append(decoded)
             if fsid != sid:
                 continue
-            if ftype == HEADERS:
-                blocks.append(payload)
             elif ftype == DATA:
                 data += payload
             if flags & END_STREAM and ftype in (HEADERS, DATA):
@@ -189,9 +212,9 @@ def test_continuation_padding_priority_and_split_data(plugin):
            frame(DATA, PADDED, 1, bytes([4]) + msg[:7] + b"\x00" * 4),
            frame(DATA, END_STREAM, 1, msg[7:]))
     blocks, data, _ = c.call(1)
-    heads, _ = decode_block(blocks[0])
+    heads, _ = blocks[0]
     assert (":status", "200") in heads and ("content-type", "application/grpc") in heads
-    trailers, _ = decode_block(blocks[-1])
+    trailers, _ = blocks[-1]
     assert ("grpc-status", "0") in trailers
     assert data[0] == 0 and int.from_bytes(data[1:5], "big") == len(data) - 5
     assert b"/dev/kfd" in data and b"renderD136" in data  # GPU 1's render node
@@ -218,12 +241,19 @@ def test_ping_settings_ack_and_unknown_frames(plugin):
     # Unknown method and bad content-type: trailers-only gRPC errors, connection stays up.
     c.send(frame(HEADERS, END_HEADERS | END_STREAM, 1, request_block("Nope")))
     blocks, _, _ = c.call(1)
-    fields = dict(decode_block(blocks[0])[0])
+    fields = dict(blocks[0][0])
     assert fields["grpc-status"] == "12" and "unknown method" in fields["grpc-message"]
     c.send(frame(HEADERS, END_HEADERS, 3, request_block("Allocate")),
            frame(DATA, END_STREAM, 3, allocate_msg([ids[0]])))
     blocks, data, _ = c.call(3)
-    assert ("grpc-status", "0") in decode_block(blocks[-1])[0] and b"/dev/kfd" in data
+    assert ("grpc-status", "0") in blocks[-1][0] and b"/dev/kfd" in data
+    # From now on both repeated fields come from the dynamic table: 2 + 1 bytes of headers.
+    c.send(frame(HEADERS, END_HEADERS, 5, request_block("Allocate")),
+           frame(DATA, END_STREAM, 5, allocate_msg([ids[1]])))
+    blocks, data, seen = c.call(5)
+    assert [n for t, f, sid, n in seen if t == HEADERS and sid == 5] == [2, 1]
+    assert (":status", "200") in blocks[0][0] and ("content-type", "application/grpc") in blocks[0][0]
+    assert blocks[-1][0] == [("grpc-status", "0")]
     c.close()
 
 
@@ -242,7 +272,7 @@ def test_tiny_windows_and_zero_header_table(plugin):
         if sid != 1:
             continue
         if ftype == HEADERS:
-            blocks.append(payload)
+            blocks.append(c.decode(payload))
         elif ftype == DATA:
             assert len(payload) <= win, "DATA beyond the stream window"
             data += payload
@@ -250,7 +280,7 @@ def test_tiny_windows_and_zero_header_table(plugin):
             # grant exactly what was consumed, on the stream and the connection
             c.send(frame(WINDOW_UPDATE, 0, 1, struct.pack(">I", len(payload))),
                    frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", len(payload))))
-    heads, updates = decode_block(blocks[0])
+    heads, updates = blocks[0]
     assert updates == [0] and (":status", "200") in heads
     assert frames >= len(data) // win and len(data) > 150_000
     assert data.count(b"-replica-") == 2352
@@ -283,7 +313,7 @@ def test_connection_errors_are_answered_with_goaway(plugin, bad):
     c2 = Conn(path)
     c2.send(frame(HEADERS, END_HEADERS, 1, request_block("Allocate")), frame(DATA, END_STREAM, 1, allocate_msg(ids[:1])))
     blocks, data, _ = c2.call(1)
-    assert ("grpc-status", "0") in decode_block(blocks[-1])[0]
+    assert ("grpc-status", "0") in blocks[-1][0]
     c2.close()
 
 
@@ -293,10 +323,12 @@ def test_rst_stream_cancels_a_watch(plugin):
     c.send(frame(HEADERS, END_HEADERS, 1, request_block("ListAndWatch")), frame(DATA, END_STREAM, 1, b""))
     while True:
         ftype, flags, sid, payload = c.read_frame()
+        if ftype == HEADERS:
+            c.decode(payload)
         if sid == 1 and ftype == DATA:
             break
     c.send(frame(RST_STREAM, 0, 1, struct.pack(">I", 8)),  # CANCEL
            frame(HEADERS, END_HEADERS, 3, request_block("Allocate")), frame(DATA, END_STREAM, 3, allocate_msg(ids[:1])))
     blocks, data, _ = c.call(3)
-    assert ("grpc-status", "0") in decode_block(blocks[-1])[0]
+    assert ("grpc-status", "0") in blocks[-1][0]
     c.close()
