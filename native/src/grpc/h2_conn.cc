@@ -62,6 +62,9 @@ constexpr uint32_t kMaxStreams = 1024;             // SETTINGS_MAX_CONCURRENT_ST
 constexpr size_t kMaxHeaderBlock = 64u << 10;      // HEADERS + CONTINUATION bytes per block
 constexpr size_t kMaxRequestBytes = 16u << 20;     // >> any kubelet request
 constexpr size_t kMaxGrpcMessageHeader = 4096;     // grpc-message is truncated beyond this
+// A peer that keeps sending (PINGs, SETTINGS, requests) without reading our
+// replies is cut off once this much output is queued (ENHANCE_YOUR_CALM).
+constexpr size_t kMaxQueuedOutput = 16u << 20;
 
 bool StartsWithGrpc(std::string_view ct) { return ct.substr(0, 16) == "application/grpc"; }
 
@@ -192,6 +195,7 @@ class H2Conn final : public ServerConn {
   bool preface_ok_ = false;
   bool closing_ = false;      // connection error: GOAWAY queued, close after the write
   bool peer_goaway_ = false;  // peer sent GOAWAY: finish open streams, then close
+  bool aborted_ = false;      // close now, dropping queued output
   std::string rbuf_;          // incomplete frame carried over to the next read
   std::string wbuf_;
   size_t woff_ = 0;
@@ -269,7 +273,7 @@ bool H2Conn::OnReadable() {
     if (errno == EAGAIN || errno == EWOULDBLOCK) break;
     return false;
   }
-  if (eof) return false;  // peer closed the connection
+  if (eof || aborted_) return false;  // peer closed the connection, or it is cut off
   return Flush();
 }
 
@@ -293,6 +297,11 @@ size_t H2Conn::Consume(const uint8_t* p, size_t n) {
       return n;
     }
     if (n - off - 9 < len) break;
+    if (wbuf_.size() - woff_ > kMaxQueuedOutput) {
+      ConnError(kEnhanceYourCalm, "peer does not read its replies");
+      aborted_ = true;  // the GOAWAY could never be written either: just close
+      return n;
+    }
     if (!OnFrame(h[3], h[4], Get32(h + 5) & 0x7fffffff, h + 9, len)) return n;
     off += 9 + len;
   }

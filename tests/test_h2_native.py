@@ -332,3 +332,30 @@ def test_rst_stream_cancels_a_watch(plugin):
     blocks, data, _ = c.call(3)
     assert ("grpc-status", "0") in blocks[-1][0]
     c.close()
+
+
+def test_ping_flood_without_reading_is_cut_off(plugin):
+    """A peer that floods PINGs and never reads the ACKs is disconnected once the
+    queued output passes the cap; the daemon keeps serving others."""
+    d, path, ids = plugin()
+    s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)
+    s.settimeout(10)
+    s.connect(path)
+    s.sendall(PREFACE + frame(SETTINGS, 0, 0))
+    burst = frame(PING, 0, 0, b"flooding") * 4096
+    sent = 0
+    try:
+        while sent < (200 << 20):  # far more ACK bytes than the cap
+            s.sendall(burst)
+            sent += len(burst)
+    except (BrokenPipeError, ConnectionResetError):
+        pass
+    s.close()
+    assert sent < (200 << 20), "the flooding peer was never disconnected"
+    assert d.proc.poll() is None
+    c2 = Conn(path)
+    c2.send(frame(HEADERS, END_HEADERS, 1, request_block("Allocate")), frame(DATA, END_STREAM, 1, allocate_msg(ids[:1])))
+    blocks, data, _ = c2.call(1)
+    assert ("grpc-status", "0") in blocks[-1][0]
+    c2.close()
