@@ -4,6 +4,7 @@
 //   cmd/nvidia-device-plugin/replica_test.go:120-122 (3 stripReplicas cases)
 //   cmd/nvidia-device-plugin/nvidia_test.go:31-64    (10 getAdditionalXids cases)
 // plus codec, config, resource-config, topology and gRPC loopback tests.
+#include <sys/socket.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -23,6 +24,7 @@
 #include "common/strings.h"
 #include "daemon/config.h"
 #include "grpc/grpc.h"
+#include "grpc/server_conn.h"
 #include "health/health.h"
 #include "metrics/metrics.h"
 #include "plugin/plugin.h"
@@ -355,12 +357,13 @@ static void TestConfig() {
   CHECK(!daemon::LoadConfig(2, bad, &env).ok());
 }
 
-static void TestGrpcLoopback() {
-  g_case = "grpc";
+static void TestGrpcLoopback(bool native_http2) {
+  g_case = native_http2 ? "grpc" : "grpc/nghttp2";
   std::string dir = "/tmp/adp-unit-" + std::to_string(getpid());
   mkdir(dir.c_str(), 0755);
   std::string sock = dir + "/t.sock";
   grpc::Server srv("test");
+  srv.set_native_http2(native_http2);
   srv.AddUnary("/t.S/Echo", [](std::string_view q, std::string* r) {
     r->assign(q);
     return Status::Ok();
@@ -405,10 +408,14 @@ static void TestGrpcLoopback() {
     srv.Post([&] { keep->Send(std::string(100000, 'y')); keep->Finish(Status::Ok()); });
     CHECK((*ch)->Recv(*sid, &m, 2000).ok() && m.size() == 100000);
     CHECK((*ch)->Recv(*sid, &m, 2000).code() == Code::kNotFound);
-    g_case = "grpc";
+    g_case = native_http2 ? "grpc" : "grpc/nghttp2";
   }
   srv.Stop();
   unlink(sock.c_str());
+  if (!native_http2) {
+    rmdir(dir.c_str());
+    return;
+  }
 
   // Crash budget (server.go:177-205): a loop that keeps failing within the hour
   // is fatal on the 7th failure; it keeps serving until then.
@@ -434,6 +441,91 @@ static void TestGrpcLoopback() {
   flaky.Stop();
   unlink(sock.c_str());
   rmdir(dir.c_str());
+}
+
+// The native HTTP/2 parser on hostile input (run under ASan/UBSan by `make
+// asan`): a valid preface and SETTINGS, then random mixes of well-formed
+// requests and random frames (types, flags, stream ids, lengths, payloads),
+// delivered in random-sized chunks. The connection may end at any point, but
+// must never crash, read out of bounds or leak.
+static void TestH2Fuzz() {
+  g_case = "h2-fuzz";
+  grpc::Server srv("fuzz");
+  srv.AddUnary("/t.S/Echo", [](std::string_view q, std::string* r) { r->assign(q); return Status::Ok(); });
+  srv.AddServerStream("/t.S/Watch", [](std::string_view, std::shared_ptr<grpc::ServerStream> s) {
+    s->Send(std::string(70000, 'w'));
+    return Status::Ok();
+  });
+  uint64_t rng = 0x9e3779b97f4a7c15ull;
+  auto next = [&] {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return rng;
+  };
+  auto frame = [](uint8_t type, uint8_t flags, uint32_t sid, const std::string& p) {
+    std::string f;
+    f.push_back(static_cast<char>(p.size() >> 16));
+    f.push_back(static_cast<char>(p.size() >> 8));
+    f.push_back(static_cast<char>(p.size()));
+    f.push_back(static_cast<char>(type));
+    f.push_back(static_cast<char>(flags));
+    for (int i = 3; i >= 0; --i) f.push_back(static_cast<char>(sid >> (8 * i)));
+    return f + p;
+  };
+  auto lit = [](const std::string& n, const std::string& v) {
+    return std::string(1, '\0') + static_cast<char>(n.size()) + n + static_cast<char>(v.size()) + v;
+  };
+  int survived = 0, conns = 0;
+  for (int round = 0; round < 1500; ++round) {
+    int sv[2];
+    if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK, 0, sv) != 0) break;
+    auto conn = grpc::MakeH2Conn(&srv, 0, sv[1]);  // owns sv[1]
+    if (!conn->Init()) { close(sv[0]); continue; }
+    ++conns;
+    std::string in = std::string("PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n") + frame(4, 0, 0, "");
+    uint32_t sid = 1;
+    int nframes = 1 + static_cast<int>(next() % 24);
+    for (int i = 0; i < nframes; ++i) {
+      uint64_t r = next();
+      if (r % 3 == 0) {  // a well-formed call, sometimes split or padded
+        std::string path = (r & 8) ? "/t.S/Watch" : "/t.S/Echo";
+        std::string hb = lit(":method", "POST") + lit(":path", path) + lit("content-type", "application/grpc");
+        std::string msg = std::string(1, '\0') + std::string("\0\0\0\3", 4) + "abc";
+        if (r & 16) {
+          in += frame(1, 0, sid, hb.substr(0, 5)) + frame(9, 4, sid, hb.substr(5));
+        } else {
+          in += frame(1, 4, sid, hb);
+        }
+        in += frame(0, 1 | ((r & 32) ? 8 : 0), sid, (r & 32) ? std::string(1, '\2') + msg + "xx" : msg);
+        sid += 2;
+      } else {  // a random frame
+        std::string payload;
+        size_t len = next() % ((r & 64) ? 70000 : 40);
+        for (size_t k = 0; k < len; ++k) payload.push_back(static_cast<char>(next()));
+        uint32_t fsid = (r & 128) ? 0 : static_cast<uint32_t>(next() % 16);
+        in += frame(static_cast<uint8_t>(next() % 12), static_cast<uint8_t>(next()), fsid, payload);
+      }
+    }
+    if (next() % 4 == 0) in.resize(next() % (in.size() + 1));  // truncated mid-frame
+    bool alive = true;
+    size_t off = 0;
+    char sink[65536];
+    while (alive && off < in.size()) {
+      size_t chunk = std::min<size_t>(in.size() - off, 1 + next() % 9000);
+      ssize_t w = write(sv[0], in.data() + off, chunk);
+      if (w > 0) off += static_cast<size_t>(w);
+      alive = conn->OnReadable() && !conn->Done();
+      while (read(sv[0], sink, sizeof(sink)) > 0) {
+      }
+      if (w <= 0) alive = alive && conn->Flush();
+    }
+    if (alive) ++survived;
+    conn.reset();
+    close(sv[0]);
+  }
+  CHECK(conns == 1500);
+  CHECK(survived > 0 && survived < conns);  // both outcomes were exercised
 }
 
 // N loops: connections are dealt round-robin, handlers of different connections
@@ -607,7 +699,9 @@ int main() {
   TestTopology();
   TestHierarchicalMatchesOracle();
   TestConfig();
-  TestGrpcLoopback();
+  TestGrpcLoopback(true);
+  TestGrpcLoopback(false);
+  TestH2Fuzz();
   TestGrpcMultiLoop();
   printf("%d checks, %d failed\n", g_checks, g_failed);
   return g_failed ? 1 : 0;
