@@ -76,8 +76,9 @@ const std::vector<FlagDef>& Table() {
        "preferred allocation over replicas: [spread | pack] (pack suits memory-unit resources)",
        [](Flags& f) -> void* { return &f.replica_policy; }},
       {"replica-cu-mask", "REPLICA_CU_MASK", "replicaCuMask", Kind::kBool,
-       "time-slice replicas also split the device's compute units: replica r of R runs on its "
-       "own 1/R of every XCD's CUs (HSA_CU_MASK on Allocate)",
+       "replicas also split the device's compute units (HSA_CU_MASK on Allocate): time-slice "
+       "replica r of R runs on its own 1/R of every XCD's CUs; memory units get CUs in "
+       "proportion to the units held",
        [](Flags& f) -> void* { return &f.replica_cu_mask; }},
       {"device-plugin-path", "DP_PLUGIN_DIR", "devicePluginPath", Kind::kString,
        "kubelet device-plugin directory",

@@ -69,6 +69,18 @@ std::vector<std::pair<uint32_t, uint32_t>> ReplicaCuRanges(uint32_t cus, uint32_
   return out;
 }
 
+std::vector<std::pair<uint32_t, uint32_t>> MemoryUnitCuRanges(uint32_t cus, uint32_t xcds, unsigned units) {
+  std::vector<std::pair<uint32_t, uint32_t>> out;
+  if (units < 2 || cus == 0 || xcds == 0 || cus % xcds != 0) return out;
+  const uint32_t per = cus / xcds;
+  out.reserve(units);
+  for (unsigned i = 0; i < units; ++i) {
+    uint32_t slot = static_cast<uint32_t>(uint64_t(i) * per / units);
+    out.emplace_back(slot * xcds, slot * xcds + xcds - 1);
+  }
+  return out;
+}
+
 int DefaultServerThreads() {
   unsigned n = std::thread::hardware_concurrency();
   return static_cast<int>(std::clamp(n, 1u, 8u));
@@ -124,8 +136,9 @@ void Plugin::BuildUnits() {
                      : std::max(1u, v.replicas);
     u.cus = ref.partition < 0 ? g.cus : g.partitions[ref.partition].cus;
     u.xcds = ref.partition < 0 ? g.xcds : g.partitions[ref.partition].xcds;
-    if (opts_.replica_cu_mask && replicated_ && !memory_units_) {
-      u.replica_cus = ReplicaCuRanges(u.cus, u.xcds, u.replicas);
+    if (opts_.replica_cu_mask && replicated_) {
+      u.replica_cus = memory_units_ ? MemoryUnitCuRanges(u.cus, u.xcds, u.replicas)
+                                    : ReplicaCuRanges(u.cus, u.xcds, u.replicas);
       if (u.replica_cus.empty() && u.replicas > 1)
         LOG_WARN(kComp, "device %s: %u CUs over %u XCDs cannot be split into %u CU shares; its replicas "
                  "share all CUs", u.id.c_str(), u.cus, u.xcds, u.replicas);
@@ -294,9 +307,11 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
         char sep = ':';
         while (k < shares.size() && shares[k].first == us[ord]) {
           uint32_t lo = ranges[shares[k].second].first, hi = ranges[shares[k].second].second;
+          // Ranges grow with the replica index; memory units share slots, so
+          // equal and adjacent ranges both merge.
           for (++k; k < shares.size() && shares[k].first == us[ord] &&
-                    ranges[shares[k].second].first == hi + 1; ++k)
-            hi = ranges[shares[k].second].second;
+                    ranges[shares[k].second].first <= hi + 1; ++k)
+            hi = std::max(hi, ranges[shares[k].second].second);
           cu_mask += sep;
           cu_mask += std::to_string(lo) + "-" + std::to_string(hi);
           sep = ',';

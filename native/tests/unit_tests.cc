@@ -685,6 +685,20 @@ static void TestReplicaCuRanges() {
   CHECK(plugin::ReplicaCuRanges(0, 8, 4).empty());
   CHECK(plugin::ReplicaCuRanges(256, 0, 4).empty());
   CHECK(plugin::ReplicaCuRanges(250, 8, 4).empty());  // CUs not uniform over XCDs
+  // Memory units: 294 x 1000 MiB of an MI355X over 32 CU slots (8 CUs each).
+  R mu = plugin::MemoryUnitCuRanges(256, 8, 294);
+  CHECK(mu.size() == 294);
+  CHECK(mu[0] == std::make_pair(0u, 7u) && mu[293] == std::make_pair(248u, 255u));
+  size_t prev = 0;
+  std::set<uint32_t> slots;
+  for (size_t i = 0; i < mu.size(); ++i) {
+    CHECK(mu[i].first % 8 == 0 && mu[i].second == mu[i].first + 7);
+    CHECK(mu[i].first >= prev);  // monotonic in the unit index
+    prev = mu[i].first;
+    slots.insert(mu[i].first);
+  }
+  CHECK(slots.size() == 32);  // every slot is owned by some unit
+  CHECK(plugin::MemoryUnitCuRanges(256, 0, 294).empty());
 }
 
 int main() {

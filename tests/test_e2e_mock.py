@@ -240,3 +240,21 @@ def test_replica_cu_mask_needs_a_possible_split(running, scratch):
     assert "HSA_CU_MASK" not in dict(c.allocate(ids[:1]).container_responses[0].envs)
     assert "cannot be split into 64 CU shares" in d.log()
     c.close()
+
+
+def test_memory_units_get_proportional_cu_shares(running, scratch):
+    """gpu-mem-gb with --replica-cu-mask: a pod's CUs follow the HBM it holds
+    (unit i owns CU slot floor(i*32/294), one CU per XCD per slot) -- a soft
+    MIG-style slice; neighbours may share one boundary slot."""
+    d, k = running(args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack",
+                         "--replica-cu-mask"])
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    g0 = ids[:294]
+    assert all(i.endswith(f"-replica-{r}") for r, i in enumerate(g0))
+    envs = dict(c.allocate(g0[:36]).container_responses[0].envs)
+    assert envs["HSA_CU_MASK"] == "0:0-31" and envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "36000"
+    assert dict(c.allocate(g0[36:72]).container_responses[0].envs)["HSA_CU_MASK"] == "0:24-63"
+    assert dict(c.allocate(g0[:294]).container_responses[0].envs)["HSA_CU_MASK"] == "0:0-255"
+    c.close()

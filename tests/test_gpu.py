@@ -334,3 +334,31 @@ def test_replica_cu_shares_isolate_a_noisy_neighbour(scratch, snap, probe_built)
     assert agg.returncode == 0, err[-2000:]
     assert json.loads(out.strip().splitlines()[-1])["aggressor_launches"] > 100
     assert shared["p50_us"] < 1.5 * solo["p50_us"], (solo, shared)
+
+
+def test_memory_unit_cu_share_on_mi355x(scratch, snap, probe_built):
+    """gpu-mem-gb + --replica-cu-mask on the MI355X: 72 units (72 GB) own CU slots
+    0-7, so the pod's census shows 64 CUs, 8 on every XCD."""
+    import json
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd.utils.build import PROBE_EXE
+    if snap["gpus"][0]["partitioned"]:
+        pytest.skip("box GPU is partitioned")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--resource-config", "gpu:gpu-mem-gb:-1",
+                                                     "--replica-policy", "pack", "--replica-cu-mask"]).start()
+    try:
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=10).devices]
+        envs = dict(c.allocate(ids[:72]).container_responses[0].envs)
+        c.close()
+    finally:
+        assert d.stop() == 0
+        k.stop()
+    assert envs["HSA_CU_MASK"] == "0:0-63" and envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "72000"
+    env = {**{k: v for k, v in os.environ.items() if k != "HSA_CU_MASK"}, "HSA_CU_MASK": envs["HSA_CU_MASK"]}
+    r = subprocess.run([PROBE_EXE, "--device", "0", "--census", "--expect-cus-seen", "64"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["per_xcc"] == [8] * 8
