@@ -721,43 +721,17 @@ void H2Conn::PumpAll() {
 void H2Conn::Dispatch(uint32_t sid, H2Stream& st, std::string_view body) {
   st.dispatched = true;
   CountCall();
-  if (!st.grpc_content_type) {
-    SendTrailersOnly(sid, kGrpcInternal, "invalid content-type: " + st.content_type);
+  std::string_view req;
+  int code = 0;
+  std::string msg;
+  if (!ParseRequest(st.grpc_content_type, st.content_type, body, &req, &code, &msg)) {
+    SendTrailersOnly(sid, code, msg);
     st.trailers_sent = true;
     return;
   }
-  // Exactly one length-prefixed message (an empty body is an empty message).
-  std::string_view req;
-  if (!body.empty()) {
-    if (body.size() < 5) {
-      SendTrailersOnly(sid, kGrpcInternal, "truncated gRPC message header");
-      st.trailers_sent = true;
-      return;
-    }
-    const auto* b = reinterpret_cast<const uint8_t*>(body.data());
-    if (b[0] != 0) {
-      SendTrailersOnly(sid, kGrpcUnimplemented, "compressed messages are not supported");
-      st.trailers_sent = true;
-      return;
-    }
-    uint32_t n = Get32(b + 1);
-    if (body.size() != 5 + static_cast<size_t>(n)) {
-      SendTrailersOnly(sid, kGrpcInternal, "gRPC message length mismatch");
-      st.trailers_sent = true;
-      return;
-    }
-    req = body.substr(5);
-  }
   if (st.unary) {
     std::string& resp = resp_buf_;
-    resp.clear();
-    auto t0 = tracing() ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
-    Status s = (*st.unary)(req, &resp);
-    if (tracing()) {
-      double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-      Logf(LogLevel::kInfo, "trace", "%s %s %s req=%zuB resp=%zuB handler=%.2fus", server_name().c_str(),
-           st.path.c_str(), s.ok() ? "OK" : s.ToString().c_str(), req.size(), resp.size(), us);
-    }
+    Status s = RunUnary(*st.unary, st.path, req, &resp);
     if (!s.ok()) {
       SendTrailersOnly(sid, ToGrpcCode(s.code()), s.message());
       st.trailers_sent = true;

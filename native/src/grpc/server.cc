@@ -315,40 +315,16 @@ void Nghttp2Conn::Dispatch(int32_t sid) {
   st->dispatched = true;
   CountCall();
 
-  if (!st->grpc_content_type) {
-    SubmitTrailersOnly(sid, kGrpcInternal, "invalid content-type: " + st->content_type);
+  std::string_view req;
+  int code = 0;
+  std::string msg;
+  if (!ParseRequest(st->grpc_content_type, st->content_type, st->body, &req, &code, &msg)) {
+    SubmitTrailersOnly(sid, code, msg);
     return;
   }
-  // Exactly one length-prefixed message (an empty body is treated as an empty message).
-  std::string_view req;
-  if (!st->body.empty()) {
-    if (st->body.size() < 5) {
-      SubmitTrailersOnly(sid, kGrpcInternal, "truncated gRPC message header");
-      return;
-    }
-    const auto* b = reinterpret_cast<const uint8_t*>(st->body.data());
-    if (b[0] != 0) {
-      SubmitTrailersOnly(sid, kGrpcUnimplemented, "compressed messages are not supported");
-      return;
-    }
-    uint32_t n = (uint32_t(b[1]) << 24) | (uint32_t(b[2]) << 16) | (uint32_t(b[3]) << 8) | b[4];
-    if (st->body.size() != 5 + static_cast<size_t>(n)) {
-      SubmitTrailersOnly(sid, kGrpcInternal, "gRPC message length mismatch");
-      return;
-    }
-    req = std::string_view(st->body).substr(5);
-  }
-
   if (st->unary) {
     std::string& resp = resp_buf_;  // reused across calls: no allocation once warm
-    resp.clear();
-    auto t0 = tracing() ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
-    Status s = (*st->unary)(req, &resp);
-    if (tracing()) {
-      double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-      Logf(LogLevel::kInfo, "trace", "%s %s %s req=%zuB resp=%zuB handler=%.2fus", server_name().c_str(),
-           st->path.c_str(), s.ok() ? "OK" : s.ToString().c_str(), req.size(), resp.size(), us);
-    }
+    Status s = RunUnary(*st->unary, st->path, req, &resp);
     st = Find(sid);  // handler cannot erase streams, but be defensive
     if (!st) return;
     if (!s.ok()) {
@@ -402,6 +378,48 @@ void Nghttp2Conn::Finish(int32_t sid, const Status& s) {
     st->deferred = false;
     nghttp2_session_resume_data(session_, sid);
   }
+}
+
+bool ServerConn::ParseRequest(bool grpc_content_type, std::string_view content_type, std::string_view body,
+                              std::string_view* req, int* code, std::string* msg) {
+  if (!grpc_content_type) {
+    *code = kGrpcInternal;
+    *msg = "invalid content-type: " + std::string(content_type);
+    return false;
+  }
+  *req = std::string_view();
+  if (body.empty()) return true;
+  const auto* b = reinterpret_cast<const uint8_t*>(body.data());
+  if (body.size() < 5) {
+    *code = kGrpcInternal;
+    *msg = "truncated gRPC message header";
+    return false;
+  }
+  if (b[0] != 0) {
+    *code = kGrpcUnimplemented;
+    *msg = "compressed messages are not supported";
+    return false;
+  }
+  uint32_t n = (uint32_t(b[1]) << 24) | (uint32_t(b[2]) << 16) | (uint32_t(b[3]) << 8) | b[4];
+  if (body.size() != 5 + static_cast<size_t>(n)) {
+    *code = kGrpcInternal;
+    *msg = "gRPC message length mismatch";
+    return false;
+  }
+  *req = body.substr(5);
+  return true;
+}
+
+Status ServerConn::RunUnary(const UnaryHandler& h, std::string_view path, std::string_view req, std::string* resp) {
+  resp->clear();
+  if (!tracing()) return h(req, resp);
+  auto t0 = std::chrono::steady_clock::now();
+  Status s = h(req, resp);
+  double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  Logf(LogLevel::kInfo, "trace", "%s %.*s %s req=%zuB resp=%zuB handler=%.2fus", server_name().c_str(),
+       static_cast<int>(path.size()), path.data(), s.ok() ? "OK" : s.ToString().c_str(), req.size(),
+       resp->size(), us);
+  return s;
 }
 
 std::unique_ptr<ServerConn> MakeNghttp2Conn(Server* srv, int loop, int fd) {

@@ -66,6 +66,14 @@ class ServerConn {
   }
   static bool StreamClosed(const ServerStream& s) { return s.closed_; }
 
+  // The request of a call as gRPC frames it: exactly one uncompressed
+  // length-prefixed message (an empty body is an empty message). On a bad
+  // request returns false with the gRPC status to answer in *code / *msg.
+  static bool ParseRequest(bool grpc_content_type, std::string_view content_type, std::string_view body,
+                           std::string_view* req, int* code, std::string* msg);
+  // Runs a unary handler into *resp (cleared first), logging it when traced.
+  Status RunUnary(const UnaryHandler& h, std::string_view path, std::string_view req, std::string* resp);
+
   Server* srv_;
   int loop_;
   int fd_;
