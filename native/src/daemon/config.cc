@@ -120,6 +120,10 @@ const std::vector<FlagDef>& Table() {
        "HTTP/2 engine of the plugin sockets: [native | nghttp2] (native: hand-written framing "
        "and flow control, nghttp2 HPACK decoding; nghttp2: its full session layer)",
        [](Flags& f) -> void* { return &f.http2_server; }},
+      {"loop-affinity", "DP_LOOP_AFFINITY", "loopAffinity", Kind::kString,
+       "where a gRPC loop runs once it takes a connection: [peer-l3 | none] (peer-l3: on the "
+       "CPUs sharing the L3 cache with the caller's last CPU, when the caller is visible)",
+       [](Flags& f) -> void* { return &f.loop_affinity; }},
       {"node-labels-file", "DP_NODE_LABELS_FILE", "nodeLabelsFile", Kind::kString,
        "write node-feature labels (amd.com/gpu.product, .count, .memory-mib, partition modes, "
        "interconnect) to this file for node-feature-discovery's local source (empty = off)",

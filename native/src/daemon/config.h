@@ -51,6 +51,7 @@ struct Flags {
   std::string pod_resources_socket = "/var/lib/kubelet/pod-resources/kubelet.sock";
   uint64_t busy_poll_us = 50;
   std::string http2_server = "native";
+  std::string loop_affinity = "peer-l3";
 };
 
 struct Config {

@@ -66,6 +66,9 @@ Result<Validated> Validate(const Config& cfg) {
   if (f.http2_server != "native" && f.http2_server != "nghttp2")
     return InvalidArgument("invalid --http2-server option: " + f.http2_server);
   v.popts.native_http2 = f.http2_server == "native";
+  if (f.loop_affinity != "peer-l3" && f.loop_affinity != "none")
+    return InvalidArgument("invalid --loop-affinity option: " + f.loop_affinity);
+  v.popts.follow_peer_l3 = f.loop_affinity == "peer-l3";
   v.popts.driver_root = f.driver_root;
   v.popts.auto_replica_unit_mib = f.auto_replica_unit_mib;
   v.popts.server_threads = static_cast<int>(std::min<uint64_t>(f.server_threads, 64));

@@ -22,6 +22,8 @@
 // state or synchronise. Other threads inject work with Post()/PostAll().
 #pragma once
 
+#include <sched.h>
+
 #include <atomic>
 #include <cstdint>
 #include <functional>
@@ -137,6 +139,9 @@ class Server {
   // HTTP/2 engine for accepted connections: the native one (default) or
   // nghttp2's session layer. Set before Start().
   void set_native_http2(bool on) { native_http2_ = on; }
+  // Serve each connection from a loop thread on the L3 of the peer process's
+  // last CPU (see FollowPeerL3). Set before Start().
+  void set_follow_peer_l3(bool on) { follow_peer_l3_ = on; }
 
   // Test hook: make the next iteration of loop 0 fail as if epoll_wait errored.
   void InjectLoopFailureForTest() { inject_failure_.store(true); }
@@ -150,6 +155,7 @@ class Server {
   void LoopMain(Loop& l);
   void AcceptAll();
   void AddConn(Loop& l, int fd);
+  void FollowPeerL3(int fd);
   void CloseConn(Loop& l, int fd);
   void DrainPosted(Loop& l);
   void PostTo(Loop& l, std::function<void()> fn);
@@ -169,6 +175,8 @@ class Server {
   bool trace_ = false;
   int busy_poll_us_ = 0;
   bool native_http2_ = true;
+  bool follow_peer_l3_ = true;
+  cpu_set_t process_cpus_;  // CPUs the process may run on (at construction)
   ServerStats stats_;
 };
 

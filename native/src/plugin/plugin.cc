@@ -503,6 +503,7 @@ Status Plugin::Start(std::function<void()> on_fatal) {
   srv->set_trace(opts_.trace);
   srv->set_busy_poll_us(opts_.busy_poll_us);
   srv->set_native_http2(opts_.native_http2);
+  srv->set_follow_peer_l3(opts_.follow_peer_l3);
   srv->AddUnary(std::string(kSvc) + "GetDevicePluginOptions",
                 [this](std::string_view q, std::string* r) { return HandleGetOptions(q, r); });
   srv->AddUnary(std::string(kSvc) + "Allocate",

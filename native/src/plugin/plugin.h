@@ -87,6 +87,7 @@ struct PluginOptions {
   // for the same CUs -- the MI355X analogue of an MPS active-thread share.
   bool replica_cu_mask = false;
   bool native_http2 = true;  // HTTP/2 engine of the plugin sockets (false: nghttp2)
+  bool follow_peer_l3 = true;  // loops serve a connection from the caller's L3
 };
 
 // HSA_CU_MASK bit ranges [first, last] of each of `replicas` CU shares of a device
