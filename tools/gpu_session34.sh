@@ -2,7 +2,7 @@
 # GPU-box session 34: --loop-affinity peer-l3 vs none, interleaved x8, 1-client
 # bench unpinned (the driver's N=1 shape); then 4/8-rank node model x2 each.
 set -o pipefail
-out=gpurun_out/s34
+out=${OUT:-gpurun_out/s34}
 mkdir -p $out
 for i in $(seq 1 8); do
   for aff in peer-l3 none; do
