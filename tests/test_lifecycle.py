@@ -171,6 +171,8 @@ def test_mixed_strategy_runs_one_socket_per_resource(scratch):
     (["--partition-strategy", "bogus"], "invalid --partition-strategy option: bogus"),
     (["--resource-config", "gpu:x"], "invalid --resource-config option"),
     (["--replica-policy", "bogus"], "invalid --replica-policy option"),
+    (["--http2-server", "h3"], "invalid --http2-server option"),
+    (["--loop-affinity", "numa"], "invalid --loop-affinity option"),
 ])
 def test_invalid_flags(scratch, args, msg):
     d = harness.Daemon(scratch, args=args).start()
@@ -484,3 +486,20 @@ def test_devices_filter_by_index_uuid_and_pci_address(scratch):
     r = subprocess.run([DAEMON, "--dry-run", "--devices", uuid2, "--device-plugin-path", scratch],
                        capture_output=True, text=True, timeout=20, env=env)
     assert [g["uuid"] for g in json.loads(r.stdout)["gpus"]] == [uuid2]
+
+
+@pytest.mark.parametrize("args", [["--http2-server", "nghttp2", "--loop-affinity", "none"],
+                                  ["--http2-server", "native", "--loop-affinity", "peer-l3"]])
+def test_engine_and_affinity_options_serve(scratch, args):
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, args=args, env={"ADP_LOG_LEVEL": "debug"}).start()
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    assert c.allocate(ids[:1]).container_responses[0].devices
+    c.close()
+    # peer-l3 follows the (visible) caller; none never moves a loop
+    if os.path.exists("/sys/devices/system/cpu/cpu0/cache/index3/shared_cpu_list"):
+        assert ("served from its L3" in d.log()) == ("peer-l3" in args)
+    assert d.stop() == 0
+    k.stop()
