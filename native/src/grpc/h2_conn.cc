@@ -160,7 +160,8 @@ class H2Conn final : public ServerConn {
   void Finish(int32_t sid, const Status& st) override;
 
  private:
-  // Returns bytes consumed; false in *ok on a connection error (GOAWAY queued).
+  // Processes whole frames; returns the bytes consumed (all of them after a
+  // connection error, which queues GOAWAY and sets closing_).
   size_t Consume(const uint8_t* p, size_t n);
   bool OnFrame(uint8_t type, uint8_t flags, uint32_t sid, const uint8_t* p, size_t len);
   bool OnData(uint8_t flags, uint32_t sid, const uint8_t* p, size_t len);
