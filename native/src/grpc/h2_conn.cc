@@ -65,6 +65,9 @@ constexpr size_t kMaxGrpcMessageHeader = 4096;     // grpc-message is truncated 
 // A peer that keeps sending (PINGs, SETTINGS, requests) without reading our
 // replies is cut off once this much output is queued (ENHANCE_YOUR_CALM).
 constexpr size_t kMaxQueuedOutput = 16u << 20;
+// Request bytes buffered over all of a connection's open streams (each stream
+// is also capped at kMaxRequestBytes): beyond it the peer is cut off.
+constexpr size_t kMaxBufferedRequests = 64u << 20;
 
 bool StartsWithGrpc(std::string_view ct) { return ct.substr(0, 16) == "application/grpc"; }
 
@@ -205,6 +208,7 @@ class H2Conn final : public ServerConn {
 
   std::map<uint32_t, H2Stream> streams_;
   uint32_t last_sid_ = 0;  // highest client stream id seen
+  size_t buffered_ = 0;    // sum of the open streams' request bodies
 
   // Peer settings / send side.
   uint32_t peer_max_frame_ = 16384;
@@ -406,7 +410,10 @@ bool H2Conn::OnData(uint8_t flags, uint32_t sid, const uint8_t* p, size_t len) {
       if ((st = Find(sid))) MaybeErase(sid, *st);
       return true;
     }
+    if (buffered_ + dlen > kMaxBufferedRequests)
+      return ConnError(kEnhanceYourCalm, "too many request bytes buffered");
     st->body.append(reinterpret_cast<const char*>(data), dlen);
+    buffered_ += dlen;
   }
   if (end) {
     st->remote_closed = true;
@@ -582,6 +589,7 @@ bool H2Conn::OnWindowUpdate(uint32_t sid, const uint8_t* p, size_t len) {
 void H2Conn::Erase(uint32_t sid) {
   auto it = streams_.find(sid);
   if (it == streams_.end()) return;
+  buffered_ -= it->second.body.size();
   Detach(it->second.stream.get());
   streams_.erase(it);
 }

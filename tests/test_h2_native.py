@@ -359,3 +359,29 @@ def test_ping_flood_without_reading_is_cut_off(plugin):
     blocks, data, _ = c2.call(1)
     assert ("grpc-status", "0") in blocks[-1][0]
     c2.close()
+
+
+def test_buffered_request_bytes_are_capped(plugin):
+    """Streams that keep sending request bytes without ever ending are cut off at
+    64 MiB buffered per connection (GOAWAY ENHANCE_YOUR_CALM)."""
+    d, path, ids = plugin()
+    c = Conn(path)
+    payload = b"\x00" * 60000
+    got_goaway = None
+    try:
+        for n in range(80):
+            sid = 1 + 2 * n
+            c.send(frame(HEADERS, END_HEADERS, sid, request_block("Allocate")),
+                   *[frame(DATA, 0, sid, payload) for _ in range(18)])  # ~1 MiB, stream left open
+    except (BrokenPipeError, ConnectionResetError):
+        pass
+    try:
+        while got_goaway is None:
+            ftype, flags, sid, p = c.read_frame()
+            if ftype == GOAWAY:
+                got_goaway = struct.unpack(">I", p[4:8])[0]
+    except (ConnectionError, socket.timeout, ConnectionResetError):
+        pass
+    assert got_goaway == 11
+    c.close()
+    assert d.proc.poll() is None
