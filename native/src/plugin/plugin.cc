@@ -73,10 +73,17 @@ std::vector<std::pair<uint32_t, uint32_t>> MemoryUnitCuRanges(uint32_t cus, uint
   std::vector<std::pair<uint32_t, uint32_t>> out;
   if (units < 2 || cus == 0 || xcds == 0 || cus % xcds != 0) return out;
   const uint32_t per = cus / xcds;
-  out.reserve(units);
-  for (unsigned i = 0; i < units; ++i) {
-    uint32_t slot = static_cast<uint32_t>(uint64_t(i) * per / units);
-    out.emplace_back(slot * xcds, slot * xcds + xcds - 1);
+  // Slots follow the IDs' lexicographic order ("-replica-0" < "-replica-1" <
+  // "-replica-10" < ...), the order the replica prioritizer takes free IDs in:
+  // a pack request gets consecutive ranks, hence contiguous slots.
+  std::vector<unsigned> by_name(units);
+  for (unsigned r = 0; r < units; ++r) by_name[r] = r;
+  std::sort(by_name.begin(), by_name.end(),
+            [](unsigned a, unsigned b) { return std::to_string(a) < std::to_string(b); });
+  out.resize(units);
+  for (unsigned rank = 0; rank < units; ++rank) {
+    uint32_t slot = static_cast<uint32_t>(uint64_t(rank) * per / units);
+    out[by_name[rank]] = {slot * xcds, slot * xcds + xcds - 1};
   }
   return out;
 }
@@ -295,7 +302,14 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       // HSA_CU_MASK="<agent>:<first>-<last>,...;...": agents are numbered in the
       // container in enumeration order (= unit order, us is sorted by unit), and
       // devices without an entry keep all their CUs. Adjacent replica shares merge.
-      std::sort(shares.begin(), shares.end());
+      // By unit, then by where the replica's range starts (memory-unit ranges
+      // follow the IDs' lexicographic order, not the replica number).
+      std::sort(shares.begin(), shares.end(), [&](const auto& a, const auto& b) {
+        if (a.first != b.first) return a.first < b.first;
+        const auto& ra = units_[a.first].replica_cus[a.second];
+        const auto& rb = units_[b.first].replica_cus[b.second];
+        return ra != rb ? ra < rb : a.second < b.second;
+      });
       shares.erase(std::unique(shares.begin(), shares.end()), shares.end());
       size_t k = 0;
       for (size_t ord = 0; ord < us.size(); ++ord) {
@@ -307,8 +321,8 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
         char sep = ':';
         while (k < shares.size() && shares[k].first == us[ord]) {
           uint32_t lo = ranges[shares[k].second].first, hi = ranges[shares[k].second].second;
-          // Ranges grow with the replica index; memory units share slots, so
-          // equal and adjacent ranges both merge.
+          // Shares are sorted by range; memory units share slots, so equal and
+          // adjacent ranges both merge.
           for (++k; k < shares.size() && shares[k].first == us[ord] &&
                     ranges[shares[k].second].first <= hi + 1; ++k)
             hi = std::max(hi, ranges[shares[k].second].second);

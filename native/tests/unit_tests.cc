@@ -688,14 +688,19 @@ static void TestReplicaCuRanges() {
   // Memory units: 294 x 1000 MiB of an MI355X over 32 CU slots (8 CUs each).
   R mu = plugin::MemoryUnitCuRanges(256, 8, 294);
   CHECK(mu.size() == 294);
-  CHECK(mu[0] == std::make_pair(0u, 7u) && mu[293] == std::make_pair(248u, 255u));
+  // replica 0 is first by name, replica 99 last ("99" > "293" > ... lexicographically)
+  CHECK(mu[0] == std::make_pair(0u, 7u) && mu[99] == std::make_pair(248u, 255u));
+  std::vector<unsigned> by_name(294);
+  for (unsigned r = 0; r < 294; ++r) by_name[r] = r;
+  std::sort(by_name.begin(), by_name.end(),
+            [](unsigned a, unsigned b) { return std::to_string(a) < std::to_string(b); });
   size_t prev = 0;
   std::set<uint32_t> slots;
-  for (size_t i = 0; i < mu.size(); ++i) {
-    CHECK(mu[i].first % 8 == 0 && mu[i].second == mu[i].first + 7);
-    CHECK(mu[i].first >= prev);  // monotonic in the unit index
-    prev = mu[i].first;
-    slots.insert(mu[i].first);
+  for (unsigned r : by_name) {
+    CHECK(mu[r].first % 8 == 0 && mu[r].second == mu[r].first + 7);
+    CHECK(mu[r].first >= prev);  // monotonic in the IDs' name order
+    prev = mu[r].first;
+    slots.insert(mu[r].first);
   }
   CHECK(slots.size() == 32);  // every slot is owned by some unit
   CHECK(plugin::MemoryUnitCuRanges(256, 0, 294).empty());

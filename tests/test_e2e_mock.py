@@ -243,18 +243,24 @@ def test_replica_cu_mask_needs_a_possible_split(running, scratch):
 
 
 def test_memory_units_get_proportional_cu_shares(running, scratch):
-    """gpu-mem-gb with --replica-cu-mask: a pod's CUs follow the HBM it holds
-    (unit i owns CU slot floor(i*32/294), one CU per XCD per slot) -- a soft
-    MIG-style slice; neighbours may share one boundary slot."""
+    """gpu-mem-gb with --replica-cu-mask: a pod's CUs follow the HBM it holds. The
+    k-th unit ID in name order owns CU slot floor(k*32/294) (one CU per XCD per
+    slot), so pods admitted the kubelet's way (GetPreferredAllocation with pack,
+    then Allocate) get contiguous slots -- a soft MIG-style slice; neighbours may
+    share one boundary slot."""
     d, k = running(args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack",
                          "--replica-cu-mask"])
     reg = k.wait_registration()
     c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
-    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
-    g0 = ids[:294]
-    assert all(i.endswith(f"-replica-{r}") for r, i in enumerate(g0))
-    envs = dict(c.allocate(g0[:36]).container_responses[0].envs)
+    free = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+
+    def admit(size):
+        ids = list(c.preferred(free, size=size).container_responses[0].deviceIDs)
+        for i in ids:
+            free.remove(i)
+        return dict(c.allocate(ids).container_responses[0].envs)
+    envs = admit(36)
     assert envs["HSA_CU_MASK"] == "0:0-31" and envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "36000"
-    assert dict(c.allocate(g0[36:72]).container_responses[0].envs)["HSA_CU_MASK"] == "0:24-63"
-    assert dict(c.allocate(g0[:294]).container_responses[0].envs)["HSA_CU_MASK"] == "0:0-255"
+    assert admit(36)["HSA_CU_MASK"] == "0:24-63"  # shares slot 3 with the first pod
+    assert admit(222)["HSA_CU_MASK"] == "0:56-255"  # the rest of GPU 0
     c.close()

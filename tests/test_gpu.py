@@ -337,8 +337,9 @@ def test_replica_cu_shares_isolate_a_noisy_neighbour(scratch, snap, probe_built)
 
 
 def test_memory_unit_cu_share_on_mi355x(scratch, snap, probe_built):
-    """gpu-mem-gb + --replica-cu-mask on the MI355X: 72 units (72 GB) own CU slots
-    0-7, so the pod's census shows 64 CUs, 8 on every XCD."""
+    """gpu-mem-gb + --replica-cu-mask on the MI355X: a 72-unit (72 GB) pod admitted
+    through GetPreferredAllocation (pack) owns CU slots 0-7, so its census shows
+    64 CUs, 8 on every XCD."""
     import json
     import subprocess
     from k8s_gpu_sharing_plugin_amd.utils.build import PROBE_EXE
@@ -351,7 +352,8 @@ def test_memory_unit_cu_share_on_mi355x(scratch, snap, probe_built):
         reg = k.wait_registration(30)
         c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
         ids = [x.ID for x in c.watch()[0].get(timeout=10).devices]
-        envs = dict(c.allocate(ids[:72]).container_responses[0].envs)
+        chosen = list(c.preferred(ids, size=72).container_responses[0].deviceIDs)
+        envs = dict(c.allocate(chosen).container_responses[0].envs)
         c.close()
     finally:
         assert d.stop() == 0
