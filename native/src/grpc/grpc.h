@@ -155,7 +155,7 @@ class Server {
   void LoopMain(Loop& l);
   void AcceptAll();
   void AddConn(Loop& l, int fd);
-  void FollowPeerL3(int fd);
+  void FollowPeerL3(Loop& l, int pid);
   void CloseConn(Loop& l, int fd);
   void DrainPosted(Loop& l);
   void PostTo(Loop& l, std::function<void()> fn);

@@ -457,6 +457,11 @@ struct Server::Loop {
   std::mutex post_mu;
   std::vector<std::function<void()>> posted;
   std::map<int, std::unique_ptr<ServerConn>> conns;
+  // --loop-affinity peer-l3: the peer process this loop follows and the L3 it
+  // is pinned to (first CPU of that L3's list), re-checked while busy.
+  int follow_pid = 0;
+  int follow_l3 = -1;
+  std::chrono::steady_clock::time_point next_follow_check{};
 };
 
 Server::Server(std::string name, int threads) : name_(std::move(name)) {
@@ -628,19 +633,20 @@ bool SysfsCpuList(int cpu, const char* rel, cpu_set_t* set) {
 
 }  // namespace
 
-void Server::FollowPeerL3(int fd) {
+void Server::FollowPeerL3(Loop& l, int pid) {
   // A request and its reply cross the socket twice; when caller and loop sit on
   // different CCDs every crossing pays an L3-to-L3 transfer (on the MI355X box's
   // EPYC 9575F: 4.4 us p50 on one L3 vs 5.0-5.3 us across, profiles/r1/session33/).
-  // So the loop that takes a connection moves onto the L3 of the CPU the peer
-  // process last ran on -- if the peer is visible (same PID namespace, not us)
-  // and that L3 is within the CPUs this process may use.
-  ucred cr{};
-  socklen_t len = sizeof(cr);
-  if (getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cr, &len) != 0 || cr.pid <= 0 || cr.pid == getpid()) return;
-  int cpu = LastCpuOf(cr.pid);
+  // So the loop moves onto the L3 of the CPU the peer process last ran on --
+  // within the CPUs this process may use -- and re-checks while it is busy, in
+  // case the peer was moved to another CCD.
+  int cpu = LastCpuOf(pid);
   cpu_set_t l3, core;
   if (cpu < 0 || !SysfsCpuList(cpu, "cache/index3/shared_cpu_list", &l3)) return;
+  int l3_id = -1;
+  for (int c = 0; c < CPU_SETSIZE && l3_id < 0; ++c)
+    if (CPU_ISSET(c, &l3)) l3_id = c;
+  if (l.follow_pid == pid && l.follow_l3 == l3_id) return;  // already there
   // The process-wide mask, not this thread's (it may already follow another peer).
   CPU_AND(&l3, &l3, &process_cpus_);
   // Not the peer's own core: a spinning loop on its SMT sibling slows both
@@ -652,13 +658,22 @@ void Server::FollowPeerL3(int fd) {
     if (CPU_COUNT(&rest) > 0) l3 = rest;
   }
   if (CPU_COUNT(&l3) == 0) return;
-  if (pthread_setaffinity_np(pthread_self(), sizeof(l3), &l3) == 0)
-    LOG_DEBUG(kComp, "'%s': connection from pid %d (cpu %d) served from its L3 (%d CPUs)", name_.c_str(),
-              static_cast<int>(cr.pid), cpu, CPU_COUNT(&l3));
+  if (pthread_setaffinity_np(pthread_self(), sizeof(l3), &l3) == 0) {
+    LOG_DEBUG(kComp, "'%s': connection from pid %d (cpu %d) served from its L3 (%d CPUs)%s", name_.c_str(), pid,
+              cpu, CPU_COUNT(&l3), l.follow_pid == pid ? " after the peer moved" : "");
+    l.follow_pid = pid;
+    l.follow_l3 = l3_id;
+  }
 }
 
 void Server::AddConn(Loop& l, int fd) {
-  if (follow_peer_l3_) FollowPeerL3(fd);
+  if (follow_peer_l3_) {
+    ucred cr{};
+    socklen_t len = sizeof(cr);
+    // Only a visible peer (same PID namespace) that is not this process.
+    if (getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cr, &len) == 0 && cr.pid > 0 && cr.pid != getpid())
+      FollowPeerL3(l, cr.pid);
+  }
   auto conn = native_http2_ ? MakeH2Conn(this, l.index, fd) : MakeNghttp2Conn(this, l.index, fd);
   if (!conn->Init()) return;  // closes fd
   epoll_event ev{};
@@ -732,6 +747,13 @@ Status Server::RunLoop(Loop& l) {
     if (busy_poll_us_ > 0) {
       spinning = true;
       spin_until = Clock::now() + spin;
+    }
+    if (l.follow_pid > 0) {  // busy: is the peer still on the L3 we follow? (every 50 ms)
+      auto now = Clock::now();
+      if (now >= l.next_follow_check) {
+        l.next_follow_check = now + std::chrono::milliseconds(50);
+        FollowPeerL3(l, l.follow_pid);
+      }
     }
     for (int i = 0; i < n; ++i) {
       int fd = events[i].data.fd;
