@@ -2,7 +2,7 @@
 # GPU-box session 40: spread of the driver-shaped headline run (python bench.py,
 # defaults) over 10 back-to-back runs on one box.
 set -o pipefail
-out=gpurun_out/s40
+out=${OUT:-gpurun_out/s40}
 mkdir -p $out
 for i in $(seq 1 10); do
   timeout -k 10 300 python bench.py --no-probe > $out/bench_$i.json 2> $out/bench_$i.err || { tail -5 $out/bench_$i.err; exit 1; }
