@@ -24,7 +24,12 @@ def main():
     ap.add_argument("--runs", type=int, default=8)
     ap.add_argument("--pods", type=int, default=3000)
     ap.add_argument("--mock", action="store_true")
+    ap.add_argument("--init-hip", action="store_true", help="initialise HIP in the client process first (as bench.py does)")
     a = ap.parse_args()
+    if a.init_hip:
+        import torch
+        torch.cuda.is_available()
+        torch.cuda.synchronize()
     for i in range(a.runs):
         d = harness.scratch_dir("adpdiag")
         k = harness.NativeKubelet(os.path.join(d, "kubelet.sock")).start()
@@ -33,7 +38,7 @@ def main():
             from k8s_gpu_sharing_plugin_amd.models import fixtures
             fx = fixtures.node(1)
         dm = harness.Daemon(d, fx, real_smi=not a.mock, args=["--devices", "0"],
-                            env={"DP_HEALTH_POLL_MS": "0", "ADP_LOG_LEVEL": "debug"}).start()
+                            env={"DP_HEALTH_POLL_MS": "0", "ADP_LOG_LEVEL": os.environ.get("DIAG_LOG_LEVEL", "debug")}).start()
         try:
             reg = k.wait(lambda e: e.get("event") == "register", 30)
             c0 = cpu_now()
