@@ -23,7 +23,7 @@ test: build
 
 # Real MI355X (one GPU box): GPU tests, smoke, bench, rocprof of the probe.
 test-gpu:
-	$(GPURUN) --timeout 1200 -- 'bash tools/gpu_check.sh'
+	$(GPURUN) --timeout 1200 -- 'OUT=gpurun_out/check bash tools/gpu_session.sh tests smoke bench prof'
 
 bench: build
 	$(PY) bench.py --steps 20 --warmup 2

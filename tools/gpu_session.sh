@@ -1,0 +1,127 @@
+#!/bin/bash
+# One parameterised GPU-box session (replaces round 1's gpu_check*.sh and
+# gpu_session<N>.sh one-offs). Usage, from the repo root on the box:
+#
+#   OUT=gpurun_out/<name> bash tools/gpu_session.sh <step> [<step> ...]
+#
+# Steps (run in the order given; the session stops at the first failure, and
+# every GPU step runs under its own `timeout -k`):
+#   build        compile every native artefact (only needed if the tree was
+#                shipped without build/; normally built on the CPU side)
+#   tests        pytest -m gpu (thread-method timeouts, so a hang names its test)
+#   smoke        __graft_entry__.smoke()
+#   bench        the driver-shaped headline run (python bench.py, defaults)
+#   configs      bench for the three real-hardware configs (spx-none,
+#                timeslice4, auto-mem), 50 steps each
+#   health       the daemon on real libamd_smi with health checks on, its log
+#                and health report kept (events on/off, ECC polls)
+#   partition    what libamd_smi reports for the partition APIs (JSON)
+#   prof         rocprofv3 --kernel-trace --stats of the HIP probe (copy, MFMA,
+#                census, latency kernels)
+#   pmc          rocprofv3 --pmc, one counter per pass (FETCH_SIZE, WRITE_SIZE,
+#                SQ_INSTS_VALU_MFMA_BF16)
+#   census       HSA_CU_MASK -> XCD/CU census of the probe (quarter shares)
+#   interference noisy-neighbour victim latency with and without CU shares
+#   floor        UDS ping-pong floor, busy-poll on and off
+#   spread       10 back-to-back headline runs (bench.py --no-probe)
+set -o pipefail
+out=${OUT:-gpurun_out/session}
+mkdir -p "$out"
+export TMPDIR=/tmp
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+P=$ROOT/build/probe/amdgpu-dp-probe
+
+die() { echo "$1 FAILED"; [ -n "$2" ] && tail -40 "$2"; exit 1; }
+
+step_build() {
+  timeout -k 10 600 python -c "import __graft_entry__ as g; g.build()" > $out/build.log 2>&1 || die build $out/build.log
+  echo built
+}
+step_tests() {
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    -p no:cacheprovider > $out/pytest_gpu.log 2>&1 || die "GPU TESTS" $out/pytest_gpu.log
+  tail -2 $out/pytest_gpu.log
+}
+step_smoke() {
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.json 2> $out/smoke.err || die SMOKE $out/smoke.err
+  tail -1 $out/smoke.json
+}
+step_bench() {
+  timeout -k 10 300 python bench.py > $out/bench_default.json 2> $out/bench_default.err || die BENCH $out/bench_default.err
+  cat $out/bench_default.json
+}
+step_configs() {
+  for cfg in spx-none timeslice4 auto-mem; do
+    timeout -k 10 300 python bench.py --steps 50 --warmup 5 --config $cfg > $out/bench_$cfg.json 2> $out/bench_$cfg.err || die "BENCH $cfg" $out/bench_$cfg.err
+    python -c "import json; d=json.load(open('$out/bench_$cfg.json')); print('$cfg', d['allocatable'], d['value'], d['allocate_p99_us'], d['preferred_p50_us'], d['server_allocate_handler_avg_us'], d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'])"
+  done
+}
+step_health() {
+  timeout -k 10 120 python tools/health_report.py --out $out/health > $out/health.json 2> $out/health.err || die HEALTH $out/health.err
+  cat $out/health.json
+}
+step_partition() {
+  timeout -k 10 60 python -c "import json; from k8s_gpu_sharing_plugin_amd.utils import native; print(json.dumps(native.snapshot(), indent=1))" > $out/snapshot.json 2> $out/snapshot.err || die PARTITION $out/snapshot.err
+  python -c "import json; d=json.load(open('$out/snapshot.json')); g=d['gpus'][0]; print({k: g.get(k) for k in ('bdf','vram_bytes','compute_partition','memory_partition','partition_profile')}); print([ (p.get('profile'), p.get('vram_bytes')) for p in g['partitions']][:8])"
+}
+step_prof() {
+  ( cd /tmp && \
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $ROOT/$out/prof -o probe -- $P --device 0 --bytes 1073741824 --iters 3 --mfma > $ROOT/$out/prof.log 2>&1 && \
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $ROOT/$out/prof_census -o census -- $P --device 0 --census > $ROOT/$out/prof_census.log 2>&1 && \
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $ROOT/$out/prof_latency -o latency -- $P --device 0 --latency 500 > $ROOT/$out/prof_latency.log 2>&1 ) || die PROF $out/prof.log
+  find $out -name "*kernel_stats.csv" -exec cat {} \;
+}
+step_pmc() {
+  for c in FETCH_SIZE WRITE_SIZE SQ_INSTS_VALU_MFMA_BF16; do
+    ( cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace -f csv -d $ROOT/$out/pmc_$c -o probe -- $P --device 0 --bytes 1073741824 --iters 3 --mfma > $ROOT/$out/pmc_$c.log 2>&1 ) || die "PMC $c" $out/pmc_$c.log
+    echo "== $c"; find $out/pmc_$c -name "*counter_collection*.csv" | head -2
+  done
+}
+census_one() {  # name mask
+  if [ -z "$2" ]; then timeout -k 5 60 $P --device 0 --census > $out/census_$1.json 2> $out/census_$1.err
+  else HSA_CU_MASK="$2" timeout -k 5 60 $P --device 0 --census > $out/census_$1.json 2> $out/census_$1.err; fi || die "CENSUS $1" $out/census_$1.err
+  python3 -c "import json; d=json.load(open('$out/census_$1.json')); print('$1', repr('$2'), 'cus', d['cus'], 'seen', d['cus_seen'], 'xccs', d['xccs_seen'], 'per_xcc', d['per_xcc'])"
+}
+step_census() {
+  census_one full ""
+  for r in 0 1 2 3; do census_one r4_$r "0:$((r*64))-$((r*64+63))"; done
+}
+lat_one() {  # name victim_mask aggressor_mask(or "none")
+  local apid=
+  if [ "$3" != "none" ]; then
+    if [ -n "$3" ]; then HSA_CU_MASK="$3" timeout -k 5 40 $P --device 0 --aggressor 8 > $out/aggr_$1.json 2>&1 &
+    else timeout -k 5 40 $P --device 0 --aggressor 8 > $out/aggr_$1.json 2>&1 & fi
+    apid=$!
+    sleep 1.5
+  fi
+  if [ -n "$2" ]; then HSA_CU_MASK="$2" timeout -k 5 60 $P --device 0 --latency 2000 > $out/lat_$1.json 2> $out/lat_$1.err
+  else timeout -k 5 60 $P --device 0 --latency 2000 > $out/lat_$1.json 2> $out/lat_$1.err; fi || die "LATENCY $1" $out/lat_$1.err
+  if [ -n "$apid" ]; then wait $apid || die "AGGRESSOR $1" $out/aggr_$1.json; fi
+  echo "$1 victim_mask='$2' aggressor_mask='$3' $(cat $out/lat_$1.json)"
+}
+step_interference() {
+  lat_one solo_full "" none
+  lat_one solo_quarter "0:0-63" none
+  lat_one shared_nomask "" ""
+  lat_one shared_masked "0:0-63" "0:64-255"
+}
+step_floor() {
+  for b in 50 0; do
+    timeout -k 10 120 build/native/amdgpu-dp-uds-floor --iters 200000 --busy-poll-us $b > $out/floor_bp$b.json || die FLOOR
+    cat $out/floor_bp$b.json
+  done
+}
+step_spread() {
+  for i in $(seq 1 10); do
+    timeout -k 10 300 python bench.py --no-probe > $out/spread_$i.json 2> $out/spread_$i.err || die "SPREAD $i" $out/spread_$i.err
+    python -c "import json; d=json.load(open('$out/spread_$i.json')); print('R $i', d['value'], d['allocate_p99_us'], d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'])"
+  done
+}
+
+[ $# -gt 0 ] || set -- tests smoke bench prof
+for s in "$@"; do
+  declare -F step_$s > /dev/null || { echo "unknown step $s"; exit 2; }
+  echo "== $s"
+  step_$s
+done
+echo "session done"
