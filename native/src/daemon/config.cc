@@ -132,6 +132,15 @@ const std::vector<FlagDef>& Table() {
        "kubelet PodResources socket; with --metrics-addr, per-device allocations and "
        "sharing (pods per GPU) are exported (empty = off)",
        [](Flags& f) -> void* { return &f.pod_resources_socket; }},
+      {"health-state-file", "DP_HEALTH_STATE_FILE", "healthStateFile", Kind::kString,
+       "persist per-GPU health verdicts (ECC baseline, failures awaiting GPU_POST_RESET) in this "
+       "file so they survive a container restart; outside the kubelet's device-plugin directory, "
+       "which the kubelet empties when it restarts (empty = kept in memory across plugin restarts only)",
+       [](Flags& f) -> void* { return &f.health_state_file; }},
+      {"reject-unhealthy", "DP_REJECT_UNHEALTHY", "rejectUnhealthy", Kind::kBool,
+       "fail Allocate() for a device currently advertised Unhealthy (default: allocate it and log a "
+       "warning, as the reference does)",
+       [](Flags& f) -> void* { return &f.reject_unhealthy; }},
       {"metrics-addr", "DP_METRICS_ADDR", "metricsAddr", Kind::kString,
        "serve Prometheus /metrics and /healthz on this TCP address, e.g. ':9400' (empty = off)",
        [](Flags& f) -> void* { return &f.metrics_addr; }},

@@ -52,6 +52,8 @@ struct Flags {
   uint64_t busy_poll_us = 50;
   std::string http2_server = "native";
   std::string loop_affinity = "peer-l3";
+  std::string health_state_file;  // "" = health verdicts kept in memory only
+  bool reject_unhealthy = false;  // Allocate() of an Unhealthy device fails instead of warning
 };
 
 struct Config {

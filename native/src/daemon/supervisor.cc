@@ -75,6 +75,7 @@ Result<Validated> Validate(const Config& cfg) {
   v.popts.trace = f.trace;
   v.popts.busy_poll_us = static_cast<int>(std::min<uint64_t>(f.busy_poll_us, 100000));
   v.popts.cdi_spec_dir = f.cdi_spec_dir;
+  v.popts.reject_unhealthy = f.reject_unhealthy;
   v.bopts.driver_root = f.driver_root;
   v.bopts.include_card_nodes = f.include_card_nodes;
   std::string devs = Trim(f.devices);
@@ -246,6 +247,9 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   std::atomic<uint64_t> restarts{0};
   std::atomic<bool> serving{false};
   std::unique_ptr<health::Monitor> monitor;
+  // Health verdicts outlive every plugin generation (and, with a state file,
+  // the process): a restart must not re-advertise a failed GPU as Healthy.
+  health::Ledger ledger(cfg.flags.health_state_file);
   int backoff_ms = 1000;
   int exit_code = 0;
   bool quit = false;
@@ -345,9 +349,19 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
       return;
     }
     restarts.fetch_add(1);
+    health::HealthConfig hcfg = health::HealthConfig::FromEnv();
     {
       std::lock_guard<std::mutex> lk(plugins_mu);
       for (auto& s : *specs) plugins.push_back(std::make_unique<plugin::Plugin>(*snap, s, v.popts));
+    }
+    // Failures recorded by earlier generations apply before the first
+    // ListAndWatch of this one.
+    if (!hcfg.disabled) {
+      for (const auto& [gpu, why] : ledger.Failed(**snap)) {
+        LOG_WARN(kComp, "GPU %s is unhealthy since an earlier plugin generation: %s",
+                 (*snap)->gpus[gpu].bdf.c_str(), why.c_str());
+        for (auto& p : plugins) p->SetGpuHealth(gpu, false, why);
+      }
     }
     int started = 0;
     for (auto& p : plugins) {
@@ -368,7 +382,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     backoff_ms = 1000;
     serving.store(true);
     if (started == 0) LOG_INFO(kComp, "no devices found; waiting indefinitely");
-    monitor = std::make_unique<health::Monitor>(lib->get(), *snap, health::HealthConfig::FromEnv());
+    monitor = std::make_unique<health::Monitor>(lib->get(), *snap, hcfg, &ledger);
     monitor->SetLayoutListener([lfd](const std::string&) {
       uint64_t one = 1;
       ssize_t w = write(lfd, &one, sizeof(one));
@@ -400,9 +414,10 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     const Flags& now = next->flags;
     if (now.amdsmi_lib != was.amdsmi_lib || now.metrics_addr != was.metrics_addr ||
         now.pod_resources_socket != was.pod_resources_socket || now.node_labels_file != was.node_labels_file ||
-        now.plugin_dir != was.plugin_dir || now.kubelet_socket != was.kubelet_socket)
-      LOG_WARN(kComp, "%s: amdsmiLib, metricsAddr, podResourcesSocket, nodeLabelsFile, devicePluginPath and "
-                      "kubeletSocket apply at startup only", why);
+        now.plugin_dir != was.plugin_dir || now.kubelet_socket != was.kubelet_socket ||
+        now.health_state_file != was.health_state_file)
+      LOG_WARN(kComp, "%s: amdsmiLib, metricsAddr, podResourcesSocket, nodeLabelsFile, devicePluginPath, "
+                      "kubeletSocket and healthStateFile apply at startup only", why);
     std::string old_json = cfg.ToJson();
     Config merged = *next;
     merged.flags.amdsmi_lib = was.amdsmi_lib;
@@ -411,6 +426,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     merged.flags.node_labels_file = was.node_labels_file;
     merged.flags.plugin_dir = was.plugin_dir;
     merged.flags.kubelet_socket = was.kubelet_socket;
+    merged.flags.health_state_file = was.health_state_file;
     auto mv = Validate(merged);
     if (!mv.ok()) return false;
     if (merged.ToJson() != old_json) {

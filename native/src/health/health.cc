@@ -5,8 +5,12 @@
 #include <unistd.h>
 
 #include <cctype>
+#include <cerrno>
 #include <chrono>
 #include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
 
 #include "common/log.h"
 #include "common/strings.h"
@@ -68,13 +72,129 @@ int Monitor::Classify(const HealthConfig& cfg, uint32_t type) {
   return -1;
 }
 
-Monitor::Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> snap, HealthConfig cfg)
-    : lib_(lib), snap_(std::move(snap)), cfg_(std::move(cfg)) {
+Ledger::Ledger(std::string path) : path_(std::move(path)) {
+  if (path_.empty()) return;
+  std::ifstream in(path_);
+  if (!in) {
+    if (errno != ENOENT)
+      LOG_WARN(kComp, "cannot read health state %s: %s; starting empty", path_.c_str(), strerror(errno));
+    return;
+  }
+  std::stringstream ss;
+  ss << in.rdbuf();
+  recs_ = Parse(ss.str());
+  size_t failed = 0;
+  for (const auto& [_, r] : recs_) failed += r.fail != 0;
+  LOG_INFO(kComp, "health state %s: %zu GPU record(s), %zu unhealthy", path_.c_str(), recs_.size(), failed);
+}
+
+std::string Ledger::Serialize(const std::map<std::string, GpuRecord>& m) {
+  std::string out = "adp-health v1\n";
+  for (const auto& [k, r] : m) {
+    std::string reason = r.reason;
+    for (auto& c : reason)
+      if (c == '\t' || c == '\n' || c == '\r') c = ' ';
+    out += k + "\t" + (r.has_baseline ? std::to_string(r.ecc_baseline) : "-") + "\t" +
+           std::to_string(r.ecc_seen) + "\t" + std::to_string(r.fail) + "\t" + reason + "\n";
+  }
+  return out;
+}
+
+std::map<std::string, GpuRecord> Ledger::Parse(const std::string& body) {
+  std::map<std::string, GpuRecord> out;
+  std::istringstream in(body);
+  std::string line;
+  bool header = false;
+  while (std::getline(in, line)) {
+    if (!header) {
+      if (Trim(line) != "adp-health v1") {
+        LOG_WARN(kComp, "health state: unknown format '%s'; ignored", line.c_str());
+        return {};
+      }
+      header = true;
+      continue;
+    }
+    if (Trim(line).empty()) continue;
+    auto f = Split(line, '\t');
+    if (f.size() < 4 || f[0].empty()) {
+      LOG_WARN(kComp, "health state: malformed line '%s' skipped", line.c_str());
+      continue;
+    }
+    GpuRecord r;
+    auto seen = ParseUint(f[2]);
+    auto fail = ParseUint(f[3]);
+    if (f[1] != "-") {
+      auto b = ParseUint(f[1]);
+      if (!b) { LOG_WARN(kComp, "health state: malformed line '%s' skipped", line.c_str()); continue; }
+      r.has_baseline = true;
+      r.ecc_baseline = *b;
+    }
+    if (!seen || !fail) {
+      LOG_WARN(kComp, "health state: malformed line '%s' skipped", line.c_str());
+      continue;
+    }
+    r.ecc_seen = *seen;
+    r.fail = static_cast<uint32_t>(*fail) & (kFailEcc | kFailUnresponsive | kFailResetPending | kFailEvent);
+    if (f.size() > 4) r.reason = f[4];
+    out[f[0]] = std::move(r);
+  }
+  return out;
+}
+
+GpuRecord Ledger::Get(const std::string& key) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = recs_.find(key);
+  return it == recs_.end() ? GpuRecord{} : it->second;
+}
+
+std::map<std::string, GpuRecord> Ledger::All() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return recs_;
+}
+
+void Ledger::Put(const std::string& key, const GpuRecord& r) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = recs_.find(key);
+  if (it != recs_.end() && it->second.has_baseline == r.has_baseline && it->second.ecc_baseline == r.ecc_baseline &&
+      it->second.ecc_seen == r.ecc_seen && it->second.fail == r.fail && it->second.reason == r.reason)
+    return;
+  recs_[key] = r;
+  SaveLocked();
+}
+
+void Ledger::SaveLocked() const {
+  if (path_.empty()) return;
+  std::string body = Serialize(recs_);
+  std::string tmp = path_ + ".tmp";
+  FILE* f = fopen(tmp.c_str(), "w");
+  bool ok = f && fwrite(body.data(), 1, body.size(), f) == body.size();
+  if (f) ok = (fflush(f) == 0) && (fsync(fileno(f)) == 0) && ok;
+  if (f) ok = (fclose(f) == 0) && ok;
+  if (!ok || rename(tmp.c_str(), path_.c_str()) != 0) {
+    LOG_WARN(kComp, "cannot write health state %s: %s", path_.c_str(), strerror(errno));
+    unlink(tmp.c_str());
+  }
+}
+
+std::vector<std::pair<int, std::string>> Ledger::Failed(const inventory::Snapshot& snap) const {
+  std::vector<std::pair<int, std::string>> out;
+  std::lock_guard<std::mutex> lk(mu_);
+  for (const auto& g : snap.gpus) {
+    auto it = recs_.find(KeyOf(g));
+    if (it != recs_.end() && it->second.fail) out.emplace_back(g.index, it->second.reason);
+  }
+  return out;
+}
+
+Monitor::Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> snap, HealthConfig cfg,
+                 Ledger* ledger)
+    : lib_(lib), snap_(std::move(snap)), cfg_(std::move(cfg)), ledger_(ledger ? ledger : &own_ledger_) {
   for (const auto& p : snap_->procs) handles_.push_back(p.handle);
   size_t n = snap_->gpus.size();
+  keys_.resize(n);
+  for (const auto& g : snap_->gpus) keys_[g.index] = Ledger::KeyOf(g);
   ecc_baseline_.assign(n, 0);
-  unresponsive_.assign(n, 0);
-  ecc_failed_.assign(n, 0);
+  fail_.assign(n, 0);
   link_change_polls_.assign(n, 0);
 }
 
@@ -103,10 +223,32 @@ Status Monitor::Start() {
   if (!events_ok_)
     LOG_WARN(kComp, "amdsmi event notification unavailable (%s); using polling only",
              st.ToString().c_str());
+  // The ECC baseline is the one recorded at the first observation of the GPU,
+  // not the current count: errors that accrued across a restart still count.
   for (const auto& g : snap_->gpus) {
     void* h = snap_->procs[g.partitions.front().handle].handle;
     auto ecc = lib_->UncorrectableErrors(h);
-    ecc_baseline_[g.index] = ecc.ok() ? *ecc : 0;
+    GpuRecord r = ledger_->Get(keys_[g.index]);
+    if (!r.has_baseline && ecc.ok()) {
+      r.has_baseline = true;
+      r.ecc_baseline = r.ecc_seen = *ecc;
+    } else if (ecc.ok() && *ecc < r.ecc_seen) {
+      LOG_INFO(kComp, "GPU %s: uncorrectable ECC count %llu below the %llu seen before (counters reset); "
+               "re-baselined", g.bdf.c_str(), static_cast<unsigned long long>(*ecc),
+               static_cast<unsigned long long>(r.ecc_seen));
+      r.ecc_baseline = r.ecc_seen = *ecc;
+      if (r.fail & kFailEcc) {
+        r.fail &= ~kFailEcc;
+        if (!r.fail) r.reason.clear();
+      }
+    }
+    ecc_baseline_[g.index] = r.ecc_baseline;
+    fail_[g.index] = r.fail;
+    ledger_->Put(keys_[g.index], r);
+    if (r.fail) {
+      LOG_WARN(kComp, "GPU %s stays unhealthy from an earlier generation: %s", g.bdf.c_str(), r.reason.c_str());
+      Notify(g.index, false, r.reason);
+    }
   }
   LOG_INFO(kComp, "health monitor watching %zu GPU(s) (events %s, poll every %d ms)", snap_->gpus.size(),
            events_ok_ ? "on" : "off", cfg_.poll_interval_ms);
@@ -175,21 +317,54 @@ void Monitor::PollOnce() {
       }
     }
     bool alive = lib_->Responsive(h);
-    if (!alive && !unresponsive_[g.index]) {
-      unresponsive_[g.index] = 1;
-      Notify(g.index, false, "device not responding to amdsmi");
-    } else if (alive && unresponsive_[g.index]) {
-      unresponsive_[g.index] = 0;
-      if (!ecc_failed_[g.index]) Notify(g.index, true, "device responding again");
+    uint32_t& fail = fail_[g.index];
+    if (!alive && !(fail & kFailUnresponsive)) {
+      Update(g.index, kFailUnresponsive, 0, "device not responding to amdsmi");
+    } else if (alive && (fail & kFailUnresponsive)) {
+      Update(g.index, 0, kFailUnresponsive, "device responding again");
     }
     if (!alive) continue;
     auto ecc = lib_->UncorrectableErrors(h);
-    if (ecc.ok() && *ecc > ecc_baseline_[g.index] && !ecc_failed_[g.index]) {
-      ecc_failed_[g.index] = 1;
-      Notify(g.index, false,
+    if (!ecc.ok()) continue;
+    GpuRecord r = ledger_->Get(keys_[g.index]);
+    if (*ecc < r.ecc_seen) {
+      // The driver reset its RAS counters (GPU reset / driver reload): the
+      // errors that failed the GPU are gone with the state they described.
+      LOG_INFO(kComp, "GPU %s: uncorrectable ECC count fell %llu -> %llu (counters reset); re-baselined",
+               g.bdf.c_str(), static_cast<unsigned long long>(r.ecc_seen), static_cast<unsigned long long>(*ecc));
+      ecc_baseline_[g.index] = *ecc;
+      r.has_baseline = true;
+      r.ecc_baseline = r.ecc_seen = *ecc;
+      ledger_->Put(keys_[g.index], r);
+      if (fail & kFailEcc) Update(g.index, 0, kFailEcc, "uncorrectable ECC counters reset");
+      continue;
+    }
+    if (*ecc > r.ecc_seen) {
+      r.ecc_seen = *ecc;
+      ledger_->Put(keys_[g.index], r);
+    }
+    if (*ecc > ecc_baseline_[g.index] && !(fail & kFailEcc)) {
+      Update(g.index, kFailEcc, 0,
              "uncorrectable ECC errors rose to " + std::to_string(*ecc) + " (baseline " +
                  std::to_string(ecc_baseline_[g.index]) + ")");
     }
+  }
+}
+
+void Monitor::Update(int gpu, uint32_t set, uint32_t clear, const std::string& reason) {
+  uint32_t before = fail_[gpu];
+  uint32_t after = (before | set) & ~clear;
+  fail_[gpu] = after;
+  GpuRecord r = ledger_->Get(keys_[gpu]);
+  r.fail = after;
+  if (!after) r.reason.clear();
+  else if (set & ~before) r.reason = reason;
+  ledger_->Put(keys_[gpu], r);
+  if ((before == 0) != (after == 0)) {
+    Notify(gpu, after == 0, reason);
+  } else if (after) {
+    LOG_INFO(kComp, "GPU %s stays unhealthy (%s; failure bits %u -> %u)", snap_->gpus[gpu].bdf.c_str(),
+             reason.c_str(), before, after);
   }
 }
 
@@ -215,15 +390,24 @@ void Monitor::Run() {
         LOG_INFO(kComp, "event %s(%u) on GPU %d: %s%s", EventName(e.type), e.type, gpu,
                  e.message.c_str(), verdict == 0 ? " (ignored)" : "");
         if (gpu < 0 || verdict == 0) continue;
+        std::string why = std::string(EventName(e.type)) + ": " + e.message;
         if (verdict > 0) {
-          // A completed reset clears poll-detected failures as well.
-          unresponsive_[gpu] = 0;
-          ecc_failed_[gpu] = 0;
+          // A completed reset clears every failure, poll-detected ones included,
+          // and the ECC count after the reset is the new baseline.
           void* h = snap_->procs[snap_->gpus[gpu].partitions.front().handle].handle;
           auto ecc = lib_->UncorrectableErrors(h);
-          if (ecc.ok()) ecc_baseline_[gpu] = *ecc;
+          if (ecc.ok()) {
+            ecc_baseline_[gpu] = *ecc;
+            GpuRecord r = ledger_->Get(keys_[gpu]);
+            r.has_baseline = true;
+            r.ecc_baseline = r.ecc_seen = *ecc;
+            ledger_->Put(keys_[gpu], r);
+          }
+          if (fail_[gpu] == 0) Notify(gpu, true, why);  // keep the reference's idempotent notify
+          Update(gpu, 0, ~0u, why);
+        } else {
+          Update(gpu, e.type == smi::kEvtGpuPreReset ? kFailResetPending : kFailEvent, 0, why);
         }
-        Notify(gpu, verdict > 0, std::string(EventName(e.type)) + ": " + e.message);
       }
     } else {
       Sleep(slice);

@@ -23,11 +23,23 @@
 // One Monitor per daemon generation serves all plugins (amdsmi event delivery
 // is process-wide, so per-plugin pumps as in the reference would steal each
 // other's events).
+//
+// Failure state outlives a Monitor: every restart (SIGHUP, kubelet.sock
+// re-creation, config reload, re-partition, xGMI link change) builds a new
+// Monitor and new Plugin objects, so the per-GPU verdicts live in a Ledger
+// owned by the supervisor, keyed by GPU UUID (BDF when there is none), and --
+// with --health-state-file -- in a small file that also survives a container
+// restart. A new generation starts its plugins with the ledger's failures
+// already applied, keeps the ECC baseline of the FIRST observation, and only a
+// GPU_POST_RESET event (or a device that answers again, for "unresponsive")
+// clears a failure. The reference keeps Device health only for one
+// ListAndWatch lifetime (server.go:95-116,251-265) and never recovers it.
 #pragma once
 
 #include <atomic>
 #include <cstdint>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <set>
@@ -55,9 +67,54 @@ struct HealthConfig {
 
 using Listener = std::function<void(int gpu, bool healthy, const std::string& reason)>;
 
+// Why a GPU is Unhealthy; a GPU is Healthy iff no bit is set.
+enum FailBits : uint32_t {
+  kFailEcc = 1u << 0,           // uncorrectable ECC count rose above the baseline
+  kFailUnresponsive = 1u << 1,  // amdsmi stopped answering (clears when it answers)
+  kFailResetPending = 1u << 2,  // GPU_PRE_RESET without a GPU_POST_RESET yet
+  kFailEvent = 1u << 3,         // any other non-ignored amdsmi event
+};
+
+struct GpuRecord {
+  bool has_baseline = false;
+  uint64_t ecc_baseline = 0;  // uncorrectable count at the first observation (or last reset)
+  uint64_t ecc_seen = 0;      // highest count observed since; a lower count means a counter reset
+  uint32_t fail = 0;
+  std::string reason;  // last failure reason (empty when healthy)
+};
+
+// Per-GPU health verdicts shared by all Monitor generations of a daemon.
+// Thread-safe. With a path, every change is written through (atomic rename)
+// and the file is loaded at construction; a missing or unreadable file starts
+// empty (logged), a malformed line is skipped.
+class Ledger {
+ public:
+  explicit Ledger(std::string path = "");
+  static std::string KeyOf(const inventory::PhysicalGpu& g) { return g.uuid.empty() ? g.bdf : g.uuid; }
+  GpuRecord Get(const std::string& key) const;
+  void Put(const std::string& key, const GpuRecord& r);
+  std::map<std::string, GpuRecord> All() const;
+  // (gpu index, reason) of every GPU of `snap` the ledger holds as failed.
+  std::vector<std::pair<int, std::string>> Failed(const inventory::Snapshot& snap) const;
+  const std::string& path() const { return path_; }
+  // File format, exposed for tests: "adp-health v1" header, then one
+  // tab-separated line per GPU: key, ecc baseline ("-" = none), highest ECC
+  // count seen, fail bits, reason.
+  static std::string Serialize(const std::map<std::string, GpuRecord>& m);
+  static std::map<std::string, GpuRecord> Parse(const std::string& body);
+
+ private:
+  void SaveLocked() const;
+  mutable std::mutex mu_;
+  std::map<std::string, GpuRecord> recs_;
+  std::string path_;
+};
+
 class Monitor {
  public:
-  Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> snap, HealthConfig cfg);
+  // `ledger` may be null: the Monitor then keeps its verdicts to itself.
+  Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> snap, HealthConfig cfg,
+          Ledger* ledger = nullptr);
   ~Monitor();
   void AddListener(Listener l);
   // Called once (from the monitor thread) when polling sees a GPU whose compute
@@ -76,6 +133,9 @@ class Monitor {
   void Run();
   void Notify(int gpu, bool healthy, const std::string& reason);
   void PollOnce();
+  // Sets/clears failure bits of a GPU, records them in the ledger and notifies
+  // listeners when the GPU's overall health flips.
+  void Update(int gpu, uint32_t set, uint32_t clear, const std::string& reason);
 
   smi::Library* lib_;
   std::shared_ptr<const inventory::Snapshot> snap_;
@@ -89,10 +149,12 @@ class Monitor {
   bool layout_changed_ = false;
   int wake_fd_ = -1;  // eventfd: Stop() wakes the idle wait at once
   void Sleep(int ms);
-  // Per-GPU polling state.
+  // Per-GPU state (mirrored into the ledger).
+  Ledger own_ledger_;
+  Ledger* ledger_;
+  std::vector<std::string> keys_;
   std::vector<uint64_t> ecc_baseline_;
-  std::vector<uint8_t> unresponsive_;
-  std::vector<uint8_t> ecc_failed_;
+  std::vector<uint32_t> fail_;
   std::vector<int> link_change_polls_;
 };
 

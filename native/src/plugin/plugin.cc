@@ -222,6 +222,9 @@ void Plugin::RebuildListAndWatch() {
   snap->bytes = std::move(out);
   snap->healthy = healthy_;
   law_bytes_size_.store(snap->bytes.size(), std::memory_order_relaxed);
+  size_t unhealthy = 0;
+  for (uint8_t h : healthy_) unhealthy += !h;
+  unhealthy_units_.store(unhealthy, std::memory_order_relaxed);
   std::lock_guard<std::mutex> lk(law_mu_);
   law_ = std::move(snap);
 }
@@ -270,7 +273,7 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
   ADP_RETURN_IF_ERROR(pb::DecodeView(req, &containers));
   std::vector<int> us, units_per;
   std::vector<std::pair<int, uint32_t>> shares;  // (unit, replica) of CU-partitioned units
-  std::string c, joined, cu_mask;
+  std::string c, joined, cu_mask, mem_mib, mem_frac, mem_devs;
   for (const auto& ids : containers) {
     us.clear();
     shares.clear();
@@ -297,6 +300,41 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       for (int u : us) ++units_per[u];
     }
     us.erase(std::unique(us.begin(), us.end()), us.end());
+    if (unhealthy_units_.load(std::memory_order_relaxed) != 0) {
+      // A kubelet racing a health transition (or holding a stale device list)
+      // can name a device that is Unhealthy right now.
+      auto law = CurrentLaw();
+      for (int u : us) {
+        if (law->healthy[u]) continue;
+        stats_.unhealthy_allocations.Add(1);
+        if (opts_.reject_unhealthy)
+          return FailedPrecondition("allocation request for '" + spec_.resource_name + "': device " +
+                                    units_[u].id + " is Unhealthy");
+        LOG_WARN(kComp, "allocate '%s': device %s is Unhealthy (allocated anyway; --reject-unhealthy refuses)",
+                 spec_.resource_name.c_str(), units_[u].id.c_str());
+      }
+    }
+    // Memory-unit resources (replicas = -1): tell the container how much HBM it
+    // was granted on each device so frameworks can cap themselves (e.g.
+    // torch.cuda.set_per_process_memory_fraction). Listed in enumeration order
+    // -- the order HIP numbers the container's devices and HSA_CU_MASK uses --
+    // whatever order the ID strategy gives AMD_VISIBLE_DEVICES. The reference
+    // hands out memory units without telling the workload.
+    mem_mib.clear();
+    mem_frac.clear();
+    mem_devs.clear();
+    if (memory_units_) {
+      char buf[32];
+      for (size_t i = 0; i < us.size(); ++i) {
+        const Unit& u = units_[us[i]];
+        uint64_t granted = static_cast<uint64_t>(units_per[us[i]]) * opts_.auto_replica_unit_mib;
+        if (i) { mem_mib += ','; mem_frac += ','; mem_devs += ','; }
+        mem_devs += u.visible_id;
+        mem_mib += std::to_string(granted);
+        snprintf(buf, sizeof(buf), "%.4f", u.vram_mib ? std::min(1.0, double(granted) / u.vram_mib) : 0.0);
+        mem_frac += buf;
+      }
+    }
     cu_mask.clear();
     if (!shares.empty()) {
       // HSA_CU_MASK="<agent>:<first>-<last>,...;...": agents are numbered in the
@@ -367,23 +405,10 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
         }
         break;
     }
-    if (memory_units_ && !us.empty()) {
-      // Memory-unit resources (replicas = -1): tell the container how much HBM it
-      // was granted on each device, in AMD_VISIBLE_DEVICES order, so frameworks
-      // can cap themselves (e.g. torch.cuda.set_per_process_memory_fraction).
-      // The reference hands out memory units without telling the workload.
-      std::string mib, frac;
-      char buf[32];
-      for (size_t i = 0; i < us.size(); ++i) {
-        const Unit& u = units_[us[i]];
-        uint64_t granted = static_cast<uint64_t>(units_per[us[i]]) * opts_.auto_replica_unit_mib;
-        if (i) { mib += ','; frac += ','; }
-        mib += std::to_string(granted);
-        snprintf(buf, sizeof(buf), "%.4f", u.vram_mib ? std::min(1.0, double(granted) / u.vram_mib) : 0.0);
-        frac += buf;
-      }
-      pb::PutMapEntry(&c, 1, kMemoryLimitEnv, mib);
-      pb::PutMapEntry(&c, 1, kMemoryFractionEnv, frac);
+    if (!mem_mib.empty()) {
+      pb::PutMapEntry(&c, 1, kMemoryLimitEnv, mem_mib);
+      pb::PutMapEntry(&c, 1, kMemoryFractionEnv, mem_frac);
+      pb::PutMapEntry(&c, 1, kMemoryDevicesEnv, mem_devs);
     }
     if (!cu_mask.empty()) pb::PutMapEntry(&c, 1, kCuMaskEnv, cu_mask);
     if (opts_.pass_device_specs) {
@@ -688,7 +713,7 @@ std::string Plugin::StatsJson() const {
     std::lock_guard<std::mutex> lk(server_mu_);
     if (server_) loops = server_->loops();
   }
-  char buf[960];
+  char buf[1280];
   snprintf(buf, sizeof(buf),
            "{\"resource\": \"%s\", \"devices\": %zu, \"advertised\": %zu, \"allocate_calls\": %llu, "
            "\"allocate_handler_avg_us\": %.3f, \"allocate_handler_max_us\": %.3f, "
@@ -696,13 +721,14 @@ std::string Plugin::StatsJson() const {
            "\"preferred_handler_max_us\": %.3f, \"law_sends\": %llu, \"law_bytes\": %zu, "
            "\"server_threads\": %d, \"allocate_handler_p50_le_us\": %g, "
            "\"allocate_handler_p99_le_us\": %g, \"preferred_handler_p50_le_us\": %g, "
-           "\"preferred_handler_p99_le_us\": %g}",
+           "\"preferred_handler_p99_le_us\": %g, \"unhealthy_allocations\": %llu}",
            JsonEscape(spec_.resource_name).c_str(), units_.size(), advertised_.size(),
            static_cast<unsigned long long>(n), avg, stats_.allocate_ns_max.Value() / 1e3,
            static_cast<unsigned long long>(np), pavg, stats_.preferred_ns_max.Value() / 1e3,
            static_cast<unsigned long long>(stats_.law_sends.Value()), law_bytes_size_.load(), loops,
            stats_.allocate_hist.QuantileUs(0.5), stats_.allocate_hist.QuantileUs(0.99),
-           stats_.preferred_hist.QuantileUs(0.5), stats_.preferred_hist.QuantileUs(0.99));
+           stats_.preferred_hist.QuantileUs(0.5), stats_.preferred_hist.QuantileUs(0.99),
+           static_cast<unsigned long long>(stats_.unhealthy_allocations.Value()));
   return buf;
 }
 
@@ -755,6 +781,11 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
     gauge("amdgpu_dp_rpc_total", res(p) + ",method=\"ListAndWatch\"",
           static_cast<double>(p->stats_.law_sends.Value()));
   }
+  family("amdgpu_dp_unhealthy_allocations_total", "counter",
+         "Allocate() calls that named a device advertised Unhealthy at the time.");
+  for (auto* p : plugins)
+    gauge("amdgpu_dp_unhealthy_allocations_total", res(p),
+          static_cast<double>(p->stats_.unhealthy_allocations.Value()));
   family("amdgpu_dp_handler_seconds", "histogram",
          "In-daemon handler time per RPC (request decode, device lookup, response encode).");
   for (auto* p : plugins) {

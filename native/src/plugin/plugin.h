@@ -62,6 +62,8 @@ inline constexpr const char* kCdiVendorClass = "amd.com/gpu";
 // that share of the device's HBM, comma separated in AMD_VISIBLE_DEVICES order.
 inline constexpr const char* kMemoryLimitEnv = "AMD_GPU_MEMORY_LIMIT_MIB";
 inline constexpr const char* kMemoryFractionEnv = "AMD_GPU_MEMORY_FRACTION";
+// The device IDs the two lists above refer to, in the same (enumeration) order.
+inline constexpr const char* kMemoryDevicesEnv = "AMD_GPU_MEMORY_DEVICES";
 // Set on Allocate for CU-partitioned time-slice replicas (--replica-cu-mask): the
 // ROCm runtime restricts every queue of the container to the listed CUs.
 inline constexpr const char* kCuMaskEnv = "HSA_CU_MASK";
@@ -88,6 +90,10 @@ struct PluginOptions {
   bool replica_cu_mask = false;
   bool native_http2 = true;  // HTTP/2 engine of the plugin sockets (false: nghttp2)
   bool follow_peer_l3 = true;  // loops serve a connection from the caller's L3
+  // Allocate() of a device currently advertised Unhealthy: false = allocate it
+  // and log a warning (the reference allocates silently, server.go:316-353);
+  // true = fail the call with FAILED_PRECONDITION naming the device.
+  bool reject_unhealthy = false;
 };
 
 // HSA_CU_MASK bit ranges [first, last] of each of `replicas` CU shares of a device
@@ -138,6 +144,7 @@ struct RpcStats {
   metrics::Counter preferred_ns_total;
   metrics::MaxGauge preferred_ns_max;
   metrics::Counter law_sends;
+  metrics::Counter unhealthy_allocations;  // Allocate() calls that named an Unhealthy device
   metrics::Histogram allocate_hist;   // handler time (decode + lookup + encode)
   metrics::Histogram preferred_hist;
 };
@@ -245,6 +252,9 @@ class Plugin {
   mutable std::mutex law_mu_;  // guards law_ (the pointer; snapshots are immutable)
   std::shared_ptr<const LawSnapshot> law_;
   std::atomic<size_t> law_bytes_size_{0};  // readable from any thread (stats)
+  // Units advertised Unhealthy in law_: Allocate() only looks health up when
+  // this is non-zero, so the healthy fast path costs one relaxed load.
+  std::atomic<size_t> unhealthy_units_{0};
   // law_streams_[i] is confined to server loop i.
   std::vector<std::vector<LawStream>> law_streams_;
 

@@ -166,7 +166,8 @@ def test_native_stub_kubelet_sees_devices(scratch):
 
 def test_memory_units_report_granted_hbm(running, scratch):
     """gpu-mem-gb (replicas=-1): the container learns how much HBM it was granted
-    per device, in AMD_VISIBLE_DEVICES order; plain and time-slice resources do not."""
+    per device, in enumeration order (AMD_GPU_MEMORY_DEVICES names the devices);
+    plain and time-slice resources do not."""
     d, k = running(args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack"])
     reg = k.wait_registration()
     assert reg.resource_name == "amd.com/gpu-mem-gb"
@@ -179,9 +180,32 @@ def test_memory_units_report_granted_hbm(running, scratch):
     assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "36000"
     assert envs["AMD_GPU_MEMORY_FRACTION"] == f"{36000 / 294896:.4f}"
     envs = dict(c.allocate(gpu1[:2] + gpu0[:3]).container_responses[0].envs)
-    order = envs["AMD_VISIBLE_DEVICES"].split(",")
+    order = envs["AMD_GPU_MEMORY_DEVICES"].split(",")
+    assert sorted(order) == sorted(envs["AMD_VISIBLE_DEVICES"].split(","))
     want = {gpu0[0].split("-replica-")[0]: "3000", gpu1[0].split("-replica-")[0]: "2000"}
     assert envs["AMD_GPU_MEMORY_LIMIT_MIB"].split(",") == [want[u] for u in order]
+    c.close()
+
+
+def test_memory_lists_follow_enumeration_order_not_uuid_order(running, scratch):
+    """GPU 0's UUID sorts after GPU 1's: AMD_VISIBLE_DEVICES (uuid strategy) lists
+    GPU 1 first, but the memory lists -- like HSA_CU_MASK and HIP's device
+    ordinals inside the container -- follow enumeration order."""
+    fx = fixtures.node(2)
+    fx["gpus"][0]["uuid"] = "ffffffff-0000-1000-80c0-000000000000"
+    fx["gpus"][1]["uuid"] = "00000000-0000-1000-80c0-000000000001"
+    d, k = running(fx, args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack",
+                             "--replica-cu-mask"])
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    g0 = sorted(i for i in ids if i.startswith("ffffffff"))
+    g1 = sorted(i for i in ids if i.startswith("00000000"))
+    envs = dict(c.allocate(g0[:5] + g1[:2]).container_responses[0].envs)
+    assert envs["AMD_VISIBLE_DEVICES"].split(",")[0].startswith("00000000")  # UUID order
+    assert envs["AMD_GPU_MEMORY_DEVICES"].split(",")[0].startswith("ffffffff")  # enumeration order
+    assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "5000,2000"
+    assert envs["HSA_CU_MASK"].startswith("0:")  # agent 0 = GPU 0, same order
     c.close()
 
 
