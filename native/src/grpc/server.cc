@@ -462,6 +462,7 @@ struct Server::Loop {
   int follow_pid = 0;
   int follow_l3 = -1;
   std::chrono::steady_clock::time_point next_follow_check{};
+  std::map<int, int> peer_pid;  // fd -> visible peer pid (connections that may be followed)
 };
 
 Server::Server(std::string name, int threads) : name_(std::move(name)) {
@@ -671,11 +672,16 @@ void Server::AddConn(Loop& l, int fd) {
     ucred cr{};
     socklen_t len = sizeof(cr);
     // Only a visible peer (same PID namespace) that is not this process.
-    if (getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cr, &len) == 0 && cr.pid > 0 && cr.pid != getpid())
+    if (getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cr, &len) == 0 && cr.pid > 0 && cr.pid != getpid()) {
+      l.peer_pid[fd] = cr.pid;
       FollowPeerL3(l, cr.pid);
+    }
   }
   auto conn = native_http2_ ? MakeH2Conn(this, l.index, fd) : MakeNghttp2Conn(this, l.index, fd);
-  if (!conn->Init()) return;  // closes fd
+  if (!conn->Init()) {  // closes fd
+    l.peer_pid.erase(fd);
+    return;
+  }
   epoll_event ev{};
   ev.events = EPOLLIN | (conn->want_epollout() ? static_cast<uint32_t>(EPOLLOUT) : 0u);
   ev.data.fd = fd;
@@ -721,6 +727,19 @@ void Server::CloseConn(Loop& l, int fd) {
   if (it == l.conns.end()) return;
   epoll_ctl(l.epoll_fd, EPOLL_CTL_DEL, fd, nullptr);
   l.conns.erase(it);
+  auto pp = l.peer_pid.find(fd);
+  if (pp == l.peer_pid.end()) return;
+  int pid = pp->second;
+  l.peer_pid.erase(pp);
+  if (pid != l.follow_pid) return;
+  for (const auto& [_, other] : l.peer_pid)
+    if (other == pid) return;  // the followed peer still has a connection here
+  // The last connection of the followed peer closed: give the loop back the
+  // whole process mask instead of leaving it pinned to that peer's L3.
+  pthread_setaffinity_np(pthread_self(), sizeof(process_cpus_), &process_cpus_);
+  LOG_DEBUG(kComp, "'%s': followed peer %d disconnected; loop unpinned", name_.c_str(), pid);
+  l.follow_pid = 0;
+  l.follow_l3 = -1;
 }
 
 Status Server::RunLoop(Loop& l) {
