@@ -9,6 +9,7 @@
 #include <sstream>
 
 #include "common/strings.h"
+#include "daemon/yaml.h"
 
 extern char** environ;
 
@@ -180,107 +181,137 @@ std::string ValueOf(const FlagDef& d, Flags& f) {
   return "null";
 }
 
+// A config-file value into a flag: the reference unmarshals the YAML into
+// typed Go fields (a string where a bool belongs is an error, and vice versa);
+// here a quoted "true"/"false" is also accepted for a bool and a quoted number
+// for an integer. null leaves the flag unset.
+Status AssignFile(const FlagDef& d, Flags& f, const FileValue& v, const std::string& key,
+                  const std::string& origin) {
+  if (v.type == 'n') return Status::Ok();
+  auto mismatch = [&](const char* want) {
+    const char* have = v.type == 'b' ? "bool" : v.type == 's' ? "string" : "number";
+    return InvalidArgument("unmarshal error: line " + std::to_string(v.line) + ": cannot unmarshal " + have +
+                           " into " + key + " of type " + want + " (" + origin + ")");
+  };
+  switch (d.kind) {
+    case Kind::kString:
+      if (v.type != 's') return mismatch("string");
+      break;
+    case Kind::kBool:
+      if (v.type != 'b' && v.type != 's') return mismatch("bool");
+      break;
+    case Kind::kUint:
+      if (v.type != 'i' && v.type != 's') return mismatch("integer");
+      break;
+  }
+  return Assign(d, f, v.text, origin);
+}
+
 }  // namespace
 
 namespace {
 
-// Flattens a JSON object into dotted keys with scalar string values.
-Status FlattenJson(const nlohmann::json& j, const std::string& prefix,
-                   std::map<std::string, std::string>* out) {
-  for (auto it = j.begin(); it != j.end(); ++it) {
-    std::string key = prefix.empty() ? it.key() : prefix + "." + it.key();
-    const auto& v = it.value();
-    if (v.is_object()) {
-      ADP_RETURN_IF_ERROR(FlattenJson(v, key, out));
-    } else if (v.is_string()) {
-      (*out)[key] = v.get<std::string>();
-    } else if (v.is_boolean()) {
-      (*out)[key] = v.get<bool>() ? "true" : "false";
-    } else if (v.is_number_integer()) {
-      (*out)[key] = std::to_string(v.get<long long>());
-    } else if (v.is_number_unsigned()) {
-      (*out)[key] = std::to_string(v.get<unsigned long long>());
-    } else if (v.is_null()) {
-      (*out)[key] = "";
-    } else {
-      return InvalidArgument("unmarshal error: unsupported value for " + key);
-    }
+// JSON documents when libyaml is unavailable (with libyaml, JSON is parsed as
+// the YAML flow document it is).
+yaml::Node FromJson(const nlohmann::json& j) {
+  yaml::Node n;
+  if (j.is_object()) {
+    n.kind = yaml::Node::kMap;
+    for (auto it = j.begin(); it != j.end(); ++it) n.map.emplace_back(it.key(), FromJson(it.value()));
+  } else if (j.is_array()) {
+    n.kind = yaml::Node::kSeq;
+    for (const auto& v : j) n.seq.push_back(FromJson(v));
+  } else if (j.is_null()) {
+    n.kind = yaml::Node::kNull;
+  } else if (j.is_string()) {
+    n.kind = yaml::Node::kScalar;
+    n.value = j.get<std::string>();
+  } else {
+    n.kind = yaml::Node::kScalar;
+    n.plain = true;  // true/false/numbers resolve as in YAML
+    n.value = j.dump();
   }
-  return Status::Ok();
+  return n;
 }
 
-std::string Unquote(const std::string& v) {
-  if (v.size() >= 2 && ((v.front() == '"' && v.back() == '"') || (v.front() == '\'' && v.back() == '\'')))
-    return v.substr(1, v.size() - 2);
-  return v;
+bool KnownFileKey(const std::string& key) {
+  for (const auto& d : Table())
+    if (*d.file_key && key == d.file_key) return true;
+  for (const auto& a : Aliases())
+    if (*a.file_key && key == a.file_key) return true;
+  return false;
 }
 
-// Block-style YAML subset: nested mappings by indentation, scalar values,
-// '#' comments, single/double quotes. (The config schema has nothing else.)
-Status ParseYamlBlock(const std::string& body, std::map<std::string, std::string>* out) {
-  std::vector<std::pair<int, std::string>> stack;  // (indent, key) of open mappings
-  std::istringstream in(body);
-  std::string line;
-  int lineno = 0;
-  while (std::getline(in, line)) {
-    ++lineno;
-    // Strip comments outside quotes.
-    char quote = 0;
-    for (size_t i = 0; i < line.size(); ++i) {
-      char c = line[i];
-      if (quote) { if (c == quote) quote = 0; continue; }
-      if (c == '"' || c == '\'') quote = c;
-      else if (c == '#' && (i == 0 || isspace(static_cast<unsigned char>(line[i - 1])))) { line.resize(i); break; }
-    }
-    std::string t = Trim(line);
-    if (t.empty() || t == "---" || t == "...") continue;
-    if (t[0] == '-') return InvalidArgument("unmarshal error: sequences are not valid (line " + std::to_string(lineno) + ")");
-    int indent = 0;
-    while (indent < static_cast<int>(line.size()) && line[indent] == ' ') ++indent;
-    size_t colon = std::string::npos;
-    quote = 0;
-    for (size_t i = 0; i < t.size(); ++i) {
-      char c = t[i];
-      if (quote) { if (c == quote) quote = 0; continue; }
-      if (c == '"' || c == '\'') quote = c;
-      else if (c == ':' && (i + 1 == t.size() || t[i + 1] == ' ')) { colon = i; break; }
-    }
-    if (colon == std::string::npos)
-      return InvalidArgument("unmarshal error: expected 'key: value' at line " + std::to_string(lineno));
-    std::string key = Unquote(Trim(t.substr(0, colon)));
-    std::string val = Trim(t.substr(colon + 1));
-    while (!stack.empty() && stack.back().first >= indent) stack.pop_back();
-    std::string full;
-    for (const auto& [_, k] : stack) full += k + ".";
-    full += key;
-    if (val.empty()) {
-      stack.emplace_back(indent, key);
-    } else {
-      (*out)[full] = Unquote(val);
-    }
+char TypeCode(yaml::ScalarType t) {
+  switch (t) {
+    case yaml::ScalarType::kNull: return 'n';
+    case yaml::ScalarType::kBool: return 'b';
+    case yaml::ScalarType::kInt: return 'i';
+    case yaml::ScalarType::kFloat: return 'f';
+    case yaml::ScalarType::kString: return 's';
   }
-  return Status::Ok();
+  return 's';
 }
 
 }  // namespace
 
-Result<std::map<std::string, std::string>> ParseConfigFile(const std::string& body) {
-  std::map<std::string, std::string> out;
+Result<ConfigFile> ParseConfigFile(const std::string& body) {
+  Result<yaml::Node> doc = Unavailable("unparsed");
+  bool extra_docs = false;
   std::string t = Trim(body);
-  if (!t.empty() && t[0] == '{') {
-    nlohmann::json j;
+  if (!yaml::Available() && !t.empty() && t[0] == '{') {
     try {
-      j = nlohmann::json::parse(t);
+      doc = FromJson(nlohmann::json::parse(t));
     } catch (const std::exception& e) {
       return InvalidArgument(std::string("unmarshal error: ") + e.what());
     }
-    if (!j.is_object()) return InvalidArgument("unmarshal error: top level must be an object");
-    ADP_RETURN_IF_ERROR(FlattenJson(j, "", &out));
   } else {
-    ADP_RETURN_IF_ERROR(ParseYamlBlock(body, &out));
+    doc = yaml::Parse(body, &extra_docs);
   }
-  if (!out.count("version") || out["version"].empty()) return InvalidArgument("missing version field");
-  if (out["version"] != "v1") return InvalidArgument("unknown version: " + out["version"]);
+  if (!doc.ok()) return InvalidArgument("unmarshal error: " + doc.status().message());
+  const yaml::Node& root = *doc;
+  ConfigFile out;
+  if (extra_docs) out.warnings.push_back("config file: only the first YAML document is read");
+  if (root.kind == yaml::Node::kNull) return InvalidArgument("missing version field");
+  if (root.kind != yaml::Node::kMap)
+    return InvalidArgument("unmarshal error: the config file must be a mapping (version: v1, flags: {...})");
+  auto scalar = [](const yaml::Node& n, const std::string& key, FileValue* v) -> Status {
+    if (n.kind == yaml::Node::kMap || n.kind == yaml::Node::kSeq)
+      return InvalidArgument("unmarshal error: line " + std::to_string(n.line) + ": " + key + " must be a scalar, not a " +
+                             (n.kind == yaml::Node::kMap ? "mapping" : "sequence"));
+    std::string canon;
+    v->type = TypeCode(yaml::Resolve(n, &canon));
+    v->text = canon;
+    v->line = n.line;
+    return Status::Ok();
+  };
+  for (const auto& [k, v] : root.map) {
+    if (k == "version") {
+      FileValue fv;
+      ADP_RETURN_IF_ERROR(scalar(v, "version", &fv));
+      out.values["version"] = fv;
+    } else if (k == "flags") {
+      if (v.kind == yaml::Node::kNull) continue;
+      if (v.kind != yaml::Node::kMap)
+        return InvalidArgument("unmarshal error: line " + std::to_string(v.line) + ": flags must be a mapping");
+      for (const auto& [fk, fv_node] : v.map) {
+        if (!KnownFileKey(fk)) {
+          out.warnings.push_back("config file line " + std::to_string(fv_node.line) + ": unknown key flags." + fk +
+                                 " (ignored)");
+          continue;
+        }
+        FileValue fv;
+        ADP_RETURN_IF_ERROR(scalar(fv_node, "flags." + fk, &fv));
+        out.values["flags." + fk] = fv;
+      }
+    } else {
+      out.warnings.push_back("config file line " + std::to_string(v.line) + ": unknown key " + k + " (ignored)");
+    }
+  }
+  auto ver = out.values.find("version");
+  if (ver == out.values.end() || ver->second.type == 'n' || ver->second.text.empty())
+    return InvalidArgument("missing version field");
+  if (ver->second.text != "v1") return InvalidArgument("unknown version: " + ver->second.text);
   return out;
 }
 
@@ -342,7 +373,7 @@ Result<Config> LoadConfig(int argc, const char* const* argv,
   }
   if (cfg.config_file.empty() && env.count("CONFIG_FILE")) cfg.config_file = env["CONFIG_FILE"];
 
-  std::map<std::string, std::string> file;
+  std::map<std::string, FileValue> file;
   if (!cfg.config_file.empty()) {
     std::ifstream in(cfg.config_file);
     if (!in) return InvalidArgument("unable to parse config file: error opening config file: " + cfg.config_file);
@@ -352,7 +383,8 @@ Result<Config> LoadConfig(int argc, const char* const* argv,
     if (!parsed.ok())
       return InvalidArgument("unable to parse config file: error parsing config file: " +
                              parsed.status().message());
-    file = std::move(*parsed);
+    file = std::move(parsed->values);
+    cfg.warnings = std::move(parsed->warnings);
   }
 
   // Precedence: command line > environment > config file > default; at each
@@ -374,10 +406,10 @@ Result<Config> LoadConfig(int argc, const char* const* argv,
     } else if (alias && *alias->env && env.count(alias->env)) {
       st = Assign(d, cfg.flags, env[alias->env], alias->env);
       cfg.deprecations.push_back(std::string(alias->env) + " is accepted for compatibility; use " + d.env);
-    } else if (*d.file_key && file.count(file_key)) {
-      st = Assign(d, cfg.flags, file[file_key], cfg.config_file);
-    } else if (!alias_file.empty() && file.count(alias_file)) {
-      st = Assign(d, cfg.flags, file[alias_file], cfg.config_file);
+    } else if (*d.file_key && file.count(file_key) && file[file_key].type != 'n') {
+      st = AssignFile(d, cfg.flags, file[file_key], file_key, cfg.config_file);
+    } else if (!alias_file.empty() && file.count(alias_file) && file[alias_file].type != 'n') {
+      st = AssignFile(d, cfg.flags, file[alias_file], alias_file, cfg.config_file);
       cfg.deprecations.push_back(std::string("config key ") + alias->file_key +
                                  " is accepted for compatibility; use " + d.file_key);
     }

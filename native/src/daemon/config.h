@@ -63,7 +63,21 @@ struct Config {
   bool show_version = false;
   bool show_help = false;
   std::vector<std::string> deprecations;  // compatibility aliases that were used
+  std::vector<std::string> warnings;      // e.g. unknown config-file keys (logged at startup)
   std::string ToJson() const;
+};
+
+// A config-file value: its text and the YAML type it resolved to
+// ('s' string, 'b' bool, 'i' int, 'f' float, 'n' null).
+struct FileValue {
+  std::string text;
+  char type = 's';
+  int line = 0;
+};
+
+struct ConfigFile {
+  std::map<std::string, FileValue> values;  // "version", "flags.<key>"
+  std::vector<std::string> warnings;
 };
 
 // Parses argv + environment (+ the config file they name). `env` lets tests
@@ -71,8 +85,11 @@ struct Config {
 Result<Config> LoadConfig(int argc, const char* const* argv,
                           const std::map<std::string, std::string>* env = nullptr);
 
-// Parses a versioned config file body into (camelCase key -> scalar value).
-Result<std::map<std::string, std::string>> ParseConfigFile(const std::string& body);
+// Parses a versioned config file body (any YAML document, JSON included) into
+// (dotted camelCase key -> scalar value). Unknown keys become warnings; a
+// `flags` that is not a mapping, or a mapping/sequence where a setting's
+// scalar belongs, is an error.
+Result<ConfigFile> ParseConfigFile(const std::string& body);
 
 std::string UsageText();
 

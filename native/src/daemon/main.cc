@@ -29,6 +29,7 @@ int main(int argc, char** argv) {
   }
   LOG_INFO("main", "amdgpu-device-plugin %s", ADP_VERSION);
   for (const auto& d : cfg->deprecations) LOG_WARN("main", "%s", d.c_str());
+  for (const auto& w : cfg->warnings) LOG_WARN("main", "%s", w.c_str());
   bool profiling = adp::StartSamplerFromEnv();
   int rc = adp::daemon::RunDaemon(*cfg, [argc, argv] { return adp::daemon::LoadConfig(argc, argv); });
   if (profiling) adp::StopSamplerAndReport();

@@ -405,6 +405,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
       LOG_ERROR(kComp, "%s: config not reloaded: %s", why, next.status().message().c_str());
       return false;
     }
+    for (const auto& w : next->warnings) LOG_WARN(kComp, "%s: %s", why, w.c_str());
     auto nv = Validate(*next);
     if (!nv.ok()) {
       LOG_ERROR(kComp, "%s: config not reloaded: %s", why, nv.status().message().c_str());

@@ -346,13 +346,21 @@ static void TestConfig() {
   auto f = daemon::ParseConfigFile("version: v1\nflags:\n  failOnInitError: false # comment\n  resourceConfig: 'gpu:g:2'\n");
   CHECK(f.ok());
   if (f.ok()) {
-    CHECK((*f)["flags.failOnInitError"] == "false");
-    CHECK((*f)["flags.resourceConfig"] == "gpu:g:2");
+    CHECK(f->values["flags.failOnInitError"].text == "false" && f->values["flags.failOnInitError"].type == 'b');
+    CHECK(f->values["flags.resourceConfig"].text == "gpu:g:2" && f->values["flags.resourceConfig"].type == 's');
   }
   CHECK(!daemon::ParseConfigFile("flags:\n  a: b\n").ok());
   CHECK(!daemon::ParseConfigFile("version: v2\n").ok());
   auto j = daemon::ParseConfigFile("{\"version\": \"v1\", \"flags\": {\"passDeviceSpecs\": false}}");
-  CHECK(j.ok() && (*j)["flags.passDeviceSpecs"] == "false");
+  CHECK(j.ok() && j->values["flags.passDeviceSpecs"].text == "false");
+  // Flow style, as sigs.k8s.io/yaml accepts it (the round-1 parser dropped it).
+  auto flow = daemon::ParseConfigFile("version: v1\nflags: {migStrategy: single, failOnInitError: no}\n");
+  CHECK(flow.ok() && flow->values["flags.migStrategy"].text == "single" &&
+        flow->values["flags.failOnInitError"].text == "false");
+  CHECK(!daemon::ParseConfigFile("version: v1\nflags: [a, b]\n").ok());
+  CHECK(!daemon::ParseConfigFile("version: v1\nflags: single\n").ok());
+  auto unknown = daemon::ParseConfigFile("version: v1\nflags:\n  migStrategi: single\nextra: 1\n");
+  CHECK(unknown.ok() && unknown->warnings.size() == 2 && unknown->values.count("flags.migStrategi") == 0);
   const char* bad[] = {"x", "--no-such-flag"};
   CHECK(!daemon::LoadConfig(2, bad, &env).ok());
 }

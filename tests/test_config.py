@@ -91,7 +91,15 @@ def test_config_file_from_env(scratch):
     ("flags:\n  deviceIDStrategy: index\n", "missing version field"),
     ("version: v2\n", "unknown version: v2"),
     ("version: v1\nflags:\n  failOnInitError: maybe\n", "invalid boolean 'maybe'"),
-    ("version: v1\nflags:\n  - a\n", "sequences are not valid"),
+    ("version: v1\nflags:\n  - a\n", "flags must be a mapping"),
+    ("version: v1\nflags: single\n", "flags must be a mapping"),
+    ("version: v1\nflags: {migStrategy: [a, b]}\n", "flags.migStrategy must be a scalar, not a sequence"),
+    # typed fields, as the reference's json.Unmarshal into Go structs
+    ("version: v1\nflags:\n  migStrategy: yes\n", "cannot unmarshal bool into flags.migStrategy of type string"),
+    ("version: v1\nflags:\n  passDeviceSpecs: 3\n", "cannot unmarshal number into flags.passDeviceSpecs of type bool"),
+    ("version: 1\n", "unknown version: 1"),
+    ("version: v1\nflags: {a: b\n", "unmarshal error: yaml: line"),
+    ("- version: v1\n", "must be a mapping"),
 ])
 def test_bad_config_files(scratch, body, msg):
     log = effective_config(scratch, file_body=body, expect_exit=1)
@@ -152,3 +160,105 @@ def test_server_threads_zero_means_auto(scratch):
     assert f["serverThreads"] == 0
     f = effective_config(scratch, env={"DP_SERVER_THREADS": "3"})
     assert f["serverThreads"] == 3
+
+
+# --- YAML as the reference's sigs.k8s.io/yaml reads it (config.go:70-94) ---
+
+def test_flow_mapping_flags(scratch):
+    """The round-1 line parser silently ignored this; go-yaml reads it."""
+    body = "version: v1\nflags: {migStrategy: single, failOnInitError: false}\n"
+    f = effective_config(scratch, file_body=body)
+    assert f["partitionStrategy"] == "single" and f["failOnInitError"] is False
+
+
+def test_block_scalars_quotes_and_yaml11_bools(scratch):
+    body = """version: "v1"
+flags:
+  resourceConfig: >-
+    gpu:sharedgpu:4,
+    cpx-1xcd.36gb:small:2
+  driverRoot: '/run/it''s'
+  deviceIDStrategy: "ind\\x65x"
+  passDeviceSpecs: off
+  failOnInitError: No
+  includeCardNodes: "true"
+  serverThreads: 0x4
+"""
+    f = effective_config(scratch, file_body=body)
+    assert f["resourceConfig"] == "gpu:sharedgpu:4, cpx-1xcd.36gb:small:2"
+    assert f["driverRoot"] == "/run/it's"
+    assert f["deviceIDStrategy"] == "index"
+    assert f["passDeviceSpecs"] is False and f["failOnInitError"] is False
+    assert f["includeCardNodes"] is True  # quoted bool accepted (lenient)
+    assert f["serverThreads"] == 4
+
+
+def test_literal_block_scalar(scratch):
+    body = "version: v1\nflags:\n  resourceConfig: |-\n    gpu:sharedgpu:3\n"
+    assert effective_config(scratch, file_body=body)["resourceConfig"] == "gpu:sharedgpu:3"
+
+
+def test_anchors_aliases_and_merge_keys(scratch):
+    body = """version: v1
+defaults: &d
+  deviceIDStrategy: index
+  passDeviceSpecs: false
+flags:
+  <<: *d
+  passDeviceSpecs: true
+  resourceConfig: &rc gpu:sharedgpu:2
+"""
+    text = effective_config(scratch, file_body=body + "", expect_exit=None)
+    assert text["deviceIDStrategy"] == "index"      # merged
+    assert text["passDeviceSpecs"] is True          # explicit key wins over the merge
+    assert text["resourceConfig"] == "gpu:sharedgpu:2"
+
+
+def test_null_values_leave_defaults(scratch):
+    f = effective_config(scratch, file_body="version: v1\nflags:\n  migStrategy: ~\n  driverRoot:\n")
+    assert f["partitionStrategy"] == "none" and f["driverRoot"] == "/"
+
+
+def test_unknown_keys_are_warned_about(scratch):
+    body = "version: v1\nflags:\n  migStrategi: single\n  deviceIDStrategy: index\nsharing: {}\n"
+    d = harness.Daemon(scratch, args=["--config-file", _write(scratch, body)]).start()
+    text = d.wait_log("running with resource config")
+    d.stop()
+    assert "unknown key flags.migStrategi (ignored)" in text
+    assert "unknown key sharing (ignored)" in text
+    assert '"deviceIDStrategy": "index"' in text
+
+
+def test_only_the_first_document_is_read(scratch):
+    body = "version: v1\nflags: {deviceIDStrategy: index}\n---\nversion: v2\n"
+    assert effective_config(scratch, file_body=body)["deviceIDStrategy"] == "index"
+
+
+def test_json_with_yaml_types(scratch):
+    body = '{"version": "v1", "flags": {"failOnInitError": false, "serverThreads": 2, "migStrategy": null}}'
+    f = effective_config(scratch, file_body=body)
+    assert f["failOnInitError"] is False and f["serverThreads"] == 2 and f["partitionStrategy"] == "none"
+
+
+def test_without_libyaml_unsupported_yaml_is_an_error_not_ignored(scratch):
+    """The strict fallback parser (libyaml missing) refuses what it cannot read."""
+    env = {"ADP_LIBYAML": "/nonexistent/libyaml.so"}
+    log = effective_config(scratch, env=env, expect_exit=1,
+                           file_body="version: v1\nflags: {migStrategy: single}\n")
+    assert "a flow collection needs libyaml" in log
+    log = effective_config(scratch, env=env, expect_exit=1,
+                           file_body="version: v1\nflags:\n  resourceConfig: >-\n    gpu:a:2\n")
+    assert "a block scalar needs libyaml" in log
+    # plain block style still works without it
+    f = effective_config(scratch, env=env,
+                         file_body="version: v1\nflags:\n  migStrategy: single\n  failOnInitError: no\n")
+    assert f["partitionStrategy"] == "single" and f["failOnInitError"] is False
+    f = effective_config(scratch, env=env, file_body='{"version": "v1", "flags": {"migStrategy": "mixed"}}')
+    assert f["partitionStrategy"] == "mixed"
+
+
+def _write(scratch, body):
+    path = os.path.join(scratch, "config.yaml")
+    with open(path, "w") as f:
+        f.write(body)
+    return path
