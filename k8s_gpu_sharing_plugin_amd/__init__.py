@@ -40,3 +40,4 @@ CAPI_LIB = binary("libadp_capi.so")
 MOCK_LIB = binary("libamdsmi_mock.so")
 UNIT_TESTS = binary("adp_unit_tests")
 PROBE_LIB = os.path.join(PROBE_DIR, "libadp_probe.so")
+PROBE_BIN = os.path.join(PROBE_DIR, "amdgpu-dp-probe")
