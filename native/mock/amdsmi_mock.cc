@@ -15,7 +15,17 @@
 //                 "num_cu": 256, "xcd": 8, "market_name": "...",
 //                 "compute_partition": "SPX"|"DPX"|"QPX"|"CPX", "memory_partition": "NPS1",
 //                 "partitions": N, "partition_uuids": "distinct"|"shared",
-//                 "render_minor": 128, "card_minor": 0, "xgmi_links_down": 0 } ] }
+//                 "render_minor": 128, "card_minor": 0, "xgmi_links_down": 0,
+//                 -- how a partitioned GPU reports itself (real amdsmi shapes differ):
+//                 "partition_vram": "share"|"pool"|"whole",  per-handle vram_info =
+//                     GPU/partitions (default) | the handle's NPS pool | the whole GPU
+//                 "partition_vram_mib": [..],  explicit per-partition values
+//                 "asic_serial": "",            no ASIC serial (grouped by BDF)
+//                 "partition_numa": "gpu"|"memory",  NUMA node of the GPU (default) or
+//                     one node per memory partition (numa*NPS + pool index)
+//                 "report_profile": true,       amdsmi_get_gpu_accelerator_partition_profile
+//                 "report_numa_ranges": true,   amdsmi_get_gpu_memory_partition_config
+//               } ] }
 // Runtime injection:
 //   event FIFO lines: "<gpu>[:<partition>] <event-type> [message]"
 //   state_dir files:  gpu<i>.ecc (uncorrectable count), gpu<i>.dead (device gone),
@@ -58,6 +68,12 @@ struct MockProc {
   std::string market;
   std::string serial;
   std::string cmode, mmode;
+  int nparts = 1;
+  int nmem = 1;                 // memory partitions (NPS count)
+  uint64_t gpu_vram_mib = 0;    // physical HBM of the whole GPU
+  uint16_t gpu_xcd = 0;
+  bool report_profile = true;
+  bool report_numa_ranges = true;
   int links_down = 0;
   bool evt_init = false;
   uint64_t evt_mask = 0;
@@ -153,6 +169,14 @@ bool Load() {
     uint32_t ncu = jg.value("num_cu", 256u);
     uint16_t xcd = static_cast<uint16_t>(jg.value("xcd", 8));
     bool shared = jg.value("partition_uuids", std::string("distinct")) == "shared";
+    int nmem = 1;
+    if (mmode.size() > 3 && mmode.compare(0, 3, "NPS") == 0) nmem = atoi(mmode.c_str() + 3);
+    if (nmem < 1) nmem = 1;
+    std::string vram_shape = jg.value("partition_vram", std::string("share"));
+    std::vector<uint64_t> explicit_vram;
+    if (jg.count("partition_vram_mib"))
+      for (const auto& v : jg["partition_vram_mib"]) explicit_vram.push_back(v.get<uint64_t>());
+    bool numa_per_memory = jg.value("partition_numa", std::string("gpu")) == "memory";
     for (int p = 0; p < nparts; ++p) {
       auto mp = std::make_unique<MockProc>();
       mp->gpu = gi;
@@ -171,8 +195,19 @@ bool Load() {
       mp->render = render + p;
       mp->card = card + p;
       mp->numa = jg.value("numa", gi < 4 ? 0 : 1);
-      // In a partitioned mode amdsmi reports each partition's share of the pool.
-      mp->vram_mib = nparts > 1 ? vram / nparts : vram;
+      int pool = nparts >= nmem ? p * nmem / nparts : 0;
+      if (numa_per_memory) mp->numa = mp->numa * nmem + pool;
+      // What a partition handle's vram_info reports (see the schema above).
+      if (static_cast<size_t>(p) < explicit_vram.size()) mp->vram_mib = explicit_vram[p];
+      else if (nparts == 1 || vram_shape == "whole") mp->vram_mib = vram;
+      else if (vram_shape == "pool") mp->vram_mib = vram / nmem;
+      else mp->vram_mib = vram / nparts;
+      mp->nparts = nparts;
+      mp->nmem = nmem;
+      mp->gpu_vram_mib = vram;
+      mp->gpu_xcd = xcd;
+      mp->report_profile = jg.value("report_profile", true);
+      mp->report_numa_ranges = jg.value("report_numa_ranges", true);
       mp->num_cu = nparts > 1 ? ncu / nparts : ncu;
       mp->xcd = nparts > 1 ? static_cast<uint16_t>(xcd / nparts ? xcd / nparts : 1) : xcd;
       mp->market = jg.value("market_name", std::string("AMD Instinct MI355X"));
@@ -386,6 +421,77 @@ amdsmi_status_t amdsmi_get_gpu_memory_partition(amdsmi_processor_handle h, char*
   GET_PROC(h);
   std::string c, m;
   CopyStr(buf, len, PartitionOverride(p, &c, &m) ? m : p->mmode);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+namespace {
+amdsmi_accelerator_partition_type_t ProfileType(const std::string& mode) {
+  if (mode == "SPX") return AMDSMI_ACCELERATOR_PARTITION_SPX;
+  if (mode == "DPX") return AMDSMI_ACCELERATOR_PARTITION_DPX;
+  if (mode == "TPX") return AMDSMI_ACCELERATOR_PARTITION_TPX;
+  if (mode == "QPX") return AMDSMI_ACCELERATOR_PARTITION_QPX;
+  if (mode == "CPX") return AMDSMI_ACCELERATOR_PARTITION_CPX;
+  return AMDSMI_ACCELERATOR_PARTITION_INVALID;
+}
+}  // namespace
+
+// The current accelerator partition profile: type, partition count and, per
+// partition, the index of its XCC resource profile (profile_config below).
+amdsmi_status_t amdsmi_get_gpu_accelerator_partition_profile(amdsmi_processor_handle h,
+                                                             amdsmi_accelerator_partition_profile_t* prof,
+                                                             uint32_t* partition_id) {
+  GET_PROC(h);
+  if (!p->report_profile) return AMDSMI_STATUS_NOT_SUPPORTED;
+  memset(prof, 0, sizeof(*prof));
+  prof->profile_type = ProfileType(p->cmode);
+  prof->num_partitions = static_cast<uint32_t>(p->nparts);
+  prof->memory_caps.nps_cap_mask = 0x3;  // NPS1 | NPS2
+  prof->profile_index = static_cast<uint32_t>(prof->profile_type) - 1;
+  prof->num_resources = 1;
+  for (int i = 0; i < p->nparts && i < AMDSMI_MAX_ACCELERATOR_PARTITIONS; ++i) prof->resources[i][0] = prof->profile_index;
+  if (partition_id) *partition_id = static_cast<uint32_t>(p->part);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_accelerator_partition_profile_config(
+    amdsmi_processor_handle h, amdsmi_accelerator_partition_profile_config_t* cfg) {
+  GET_PROC(h);
+  if (!p->report_profile) return AMDSMI_STATUS_NOT_SUPPORTED;
+  memset(cfg, 0, sizeof(*cfg));
+  static const char* modes[] = {"SPX", "DPX", "QPX", "CPX"};
+  static const int parts[] = {1, 2, 4, 8};
+  cfg->num_profiles = 4;
+  cfg->num_resource_profiles = 4;
+  for (int i = 0; i < 4; ++i) {
+    auto t = ProfileType(modes[i]);
+    cfg->profiles[i].profile_type = t;
+    cfg->profiles[i].num_partitions = static_cast<uint32_t>(parts[i]);
+    cfg->profiles[i].profile_index = static_cast<uint32_t>(t) - 1;
+    cfg->resource_profiles[i].profile_index = static_cast<uint32_t>(t) - 1;
+    cfg->resource_profiles[i].resource_type = AMDSMI_ACCELERATOR_XCC;
+    cfg->resource_profiles[i].partition_resource = static_cast<uint32_t>(p->gpu_xcd / parts[i]);
+    cfg->resource_profiles[i].num_partitions_share_resource = 1;
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+// NUMA memory ranges of the GPU (one per memory partition), whichever handle asks.
+amdsmi_status_t amdsmi_get_gpu_memory_partition_config(amdsmi_processor_handle h,
+                                                       amdsmi_memory_partition_config_t* cfg) {
+  GET_PROC(h);
+  if (!p->report_numa_ranges) return AMDSMI_STATUS_NOT_SUPPORTED;
+  memset(cfg, 0, sizeof(*cfg));
+  cfg->partition_caps.nps_cap_mask = 0x3;
+  cfg->mp_mode = p->nmem == 1 ? AMDSMI_MEMORY_PARTITION_NPS1
+                : p->nmem == 2 ? AMDSMI_MEMORY_PARTITION_NPS2
+                : p->nmem == 4 ? AMDSMI_MEMORY_PARTITION_NPS4 : AMDSMI_MEMORY_PARTITION_NPS8;
+  cfg->num_numa_ranges = static_cast<uint32_t>(p->nmem);
+  uint64_t per = (p->gpu_vram_mib << 20) / static_cast<uint64_t>(p->nmem);
+  for (int i = 0; i < p->nmem && i < AMDSMI_MAX_NUM_NUMA_NODES; ++i) {
+    cfg->numa_range[i].memory_type = AMDSMI_VRAM_TYPE_HBM3E;
+    cfg->numa_range[i].start = per * static_cast<uint64_t>(i);
+    cfg->numa_range[i].end = per * static_cast<uint64_t>(i + 1) - 1;
+  }
   return AMDSMI_STATUS_SUCCESS;
 }
 

@@ -43,16 +43,25 @@ json SnapshotJson(const adp::inventory::Snapshot& s) {
   for (const auto& g : s.gpus) {
     json parts = json::array();
     for (const auto& p : g.partitions) {
+      const auto& raw = s.procs[p.handle];
       parts.push_back({{"uuid", p.uuid}, {"partition_id", p.partition_id}, {"render", p.render_path},
                        {"card", p.card_path}, {"numa", p.numa}, {"vram_mib", p.vram_mib},
-                       {"xcds", p.xcds}, {"cus", p.cus}});
+                       {"xcds", p.xcds}, {"cus", p.cus},
+                       // what amdsmi itself reported for this handle
+                       {"reported", {{"vram_mib", raw.vram_mib}, {"xcd_count", raw.xcd_count},
+                                     {"profile_type", raw.profile_type},
+                                     {"profile_partitions", raw.profile_partitions},
+                                     {"profile_xccs", raw.profile_xccs}, {"mem_ranges", raw.mem_ranges},
+                                     {"mem_ranges_mib", raw.mem_ranges_mib},
+                                     {"asic_serial", raw.asic_serial}, {"bdf", raw.bdf}}}});
     }
     gpus.push_back({{"index", g.index}, {"node_index", g.node_index}, {"uuid", g.uuid}, {"bdf", g.bdf},
                     {"numa", g.numa}, {"vram_mib", g.vram_mib}, {"xcds", g.xcds}, {"cus", g.cus},
                     {"compute_mode", g.compute_mode}, {"memory_mode", g.memory_mode},
                     {"market_name", g.market_name}, {"profile", g.PartitionProfile()},
                     {"partitioned", g.partitioned()}, {"xgmi_links_down", g.xgmi_links_down},
-                    {"partitions", parts}});
+                    {"vram_source", g.vram_source}, {"driver_profile", g.driver_profile},
+                    {"model_hbm_mib", adp::inventory::ModelHbmMib(g.market_name)}, {"partitions", parts}});
   }
   json links = json::array();
   for (size_t a = 0; a < s.gpus.size(); ++a) {

@@ -33,7 +33,34 @@ std::string ModeForCount(size_t n) {
 // MI355X: 32 CUs per XCD. Used only when amdsmi cannot report XCD counts.
 constexpr uint32_t kCusPerXcd = 32;
 
+std::string ModeForProfile(const std::string& compute, const std::string& profile, size_t handles) {
+  if (!compute.empty()) return compute;
+  if (!profile.empty()) return profile;
+  return ModeForCount(handles);
+}
+
+bool Near(uint64_t a, uint64_t b) {  // within 3 %
+  uint64_t hi = std::max(a, b), lo = std::min(a, b);
+  return hi - lo <= hi * 3 / 100;
+}
+
+int NpsCount(const std::string& memory_mode) {
+  if (memory_mode.size() > 3 && memory_mode.compare(0, 3, "NPS") == 0) {
+    int k = atoi(memory_mode.c_str() + 3);
+    return k > 0 ? k : 1;
+  }
+  return 1;
+}
+
 }  // namespace
+
+uint64_t ModelHbmMib(const std::string& market_name) {
+  std::string m = Upper(market_name);
+  if (m.find("MI355") != std::string::npos || m.find("MI350") != std::string::npos) return 294896;
+  if (m.find("MI325") != std::string::npos) return 262144;
+  if (m.find("MI300X") != std::string::npos || m.find("MI308") != std::string::npos) return 196608;
+  return 0;
+}
 
 std::string RenderPath(uint32_t minor) { return "/dev/dri/renderD" + std::to_string(minor); }
 std::string CardPath(uint32_t minor) { return "/dev/dri/card" + std::to_string(minor); }
@@ -81,6 +108,84 @@ Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo
     groups[key].push_back(static_cast<int>(i));
   }
 
+  // Per-partition HBM, pinned to the driver: a partition handle's vram_info may
+  // report its own share, its memory partition's pool, or the whole GPU
+  // depending on the amdsmi/driver version. The GPU's physical HBM is taken
+  // from the most authoritative source available and every partition gets
+  // its share, physical / partitions, so resources named "...36gb" and memory
+  // units always add up to the HBM that exists.
+  auto PinPartitionVram = [](PhysicalGpu* g, const std::vector<int>& handles, const Snapshot& s) -> bool {
+    const auto& first = s.procs[handles.front()];
+    size_t n = handles.size();
+    int k = NpsCount(g->memory_mode);
+    uint64_t model = ModelHbmMib(first.market_name);
+    uint64_t sum = 0, lo = UINT64_MAX, hi = 0, ranges_mib = 0;
+    uint32_t ranges = 0;
+    for (int h : handles) {
+      uint64_t v = s.procs[h].vram_mib;
+      sum += v;
+      lo = std::min(lo, v);
+      hi = std::max(hi, v);
+      if (s.procs[h].mem_ranges_mib > ranges_mib) {
+        ranges_mib = s.procs[h].mem_ranges_mib;
+        ranges = s.procs[h].mem_ranges;
+      }
+    }
+    uint64_t phys = 0;
+    if (ranges_mib && (static_cast<int>(ranges) == k || g->memory_mode.empty())) {
+      if (!model || Near(ranges_mib, model)) {
+        phys = ranges_mib;
+        g->vram_source = "memory-partition-config";
+      } else {
+        LOG_WARN(kComp, "GPU %s (%s): memory-partition ranges add up to %llu MiB, not the model's %llu; ignored",
+                 g->bdf.c_str(), first.market_name.c_str(), static_cast<unsigned long long>(ranges_mib),
+                 static_cast<unsigned long long>(model));
+      }
+    }
+    if (phys) {
+      // pinned by the driver's memory ranges
+    } else if (n == 1) {
+      phys = hi;  // SPX: the handle is the whole GPU, whatever the model table says
+      g->vram_source = "spx";
+    } else if (lo == hi) {
+      struct Cand { uint64_t mib; const char* what; };
+      std::vector<Cand> cands = {{hi * n, "share"}};
+      if (k > 1 && static_cast<size_t>(k) < n) cands.push_back({hi * static_cast<uint64_t>(k), "pool"});
+      cands.push_back({hi, "whole"});
+      if (model) {
+        for (const auto& c : cands)
+          if (Near(c.mib, model)) {
+            phys = c.mib;
+            g->vram_source = c.what;
+            break;
+          }
+      } else {
+        phys = hi * n;
+        g->vram_source = "share-unpinned";
+        LOG_WARN(kComp, "GPU %s (%s): partitions each report %llu MiB and the model's HBM is unknown; "
+                 "assuming that is each partition's share", g->bdf.c_str(), first.market_name.c_str(),
+                 static_cast<unsigned long long>(hi));
+      }
+    } else if (!model || Near(sum, model)) {
+      phys = sum;  // uneven shares that add up
+      g->vram_source = model ? "share" : "share-unpinned";
+    }
+    if (!phys) {
+      std::string got;
+      for (int h : handles) got += (got.empty() ? "" : ",") + std::to_string(s.procs[h].vram_mib);
+      LOG_ERROR(kComp, "GPU %s (%s, %s/%s): partition VRAM [%s] MiB is inconsistent with the model's %llu MiB "
+                "of HBM under every reading (share / memory-partition pool / whole GPU); the GPU is not served",
+                g->bdf.c_str(), first.market_name.c_str(), g->compute_mode.c_str(), g->memory_mode.c_str(),
+                got.c_str(), static_cast<unsigned long long>(model));
+      return false;
+    }
+    g->vram_mib = phys;
+    bool keep_reported = g->vram_source == "share" && lo != hi;  // uneven split, reported as such
+    for (auto& part : g->partitions)
+      if (!keep_reported) part.vram_mib = phys / n;
+    return true;
+  };
+
   std::set<int> only(opt.only_gpus.begin(), opt.only_gpus.end());
   int index = 0;
   for (size_t gi = 0; gi < order.size(); ++gi) {
@@ -104,7 +209,7 @@ Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo
       if (!keep) continue;
     }
     PhysicalGpu g;
-    g.index = index++;
+    g.index = index;
     g.node_index = static_cast<int>(gi);
     g.uuid = first.uuid;
     g.bdf = smi::FormatBdf(first.bdf_id & ~uint64_t{7});
@@ -112,9 +217,15 @@ Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo
     g.market_name = first.market_name;
     g.reported_compute = Upper(first.compute_partition);
     g.reported_memory = Upper(first.memory_partition);
-    g.compute_mode = g.reported_compute;
-    if (g.compute_mode.empty()) g.compute_mode = ModeForCount(handles.size());
+    g.driver_profile = first.profile_type;
+    g.compute_mode = ModeForProfile(g.reported_compute, g.driver_profile, handles.size());
     g.memory_mode = g.reported_memory;
+    if (!g.driver_profile.empty() && !g.reported_compute.empty() && g.driver_profile != g.reported_compute)
+      LOG_WARN(kComp, "GPU %s: compute partition %s but accelerator partition profile %s", g.bdf.c_str(),
+               g.reported_compute.c_str(), g.driver_profile.c_str());
+    if (first.profile_partitions && first.profile_partitions != handles.size())
+      LOG_WARN(kComp, "GPU %s: the partition profile has %u partitions, amdsmi lists %zu handles", g.bdf.c_str(),
+               first.profile_partitions, handles.size());
 
     // Partition IDs must be unique and stable across restarts: the handle UUID
     // when amdsmi reports distinct ones, else "<uuid>-p<partition>".
@@ -133,20 +244,20 @@ Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo
       if (opt.include_card_nodes && p.card_minor != 0xffffffffu) part.card_path = CardPath(p.card_minor);
       part.numa = p.numa_node;
       part.vram_mib = p.vram_mib;
-      part.xcds = p.xcd_count;
+      part.xcds = p.profile_xccs ? p.profile_xccs : p.xcd_count;
       part.cus = p.num_cu;
-      g.vram_mib += p.vram_mib;
-      g.xcds += p.xcd_count;
+      g.xcds += part.xcds;
       g.cus += p.num_cu;
       g.partitions.push_back(std::move(part));
     }
-    (void)opt;
+    if (!PinPartitionVram(&g, handles, *snap)) continue;  // inconsistent: not served (logged)
     if (g.compute_mode == "SPX" && handles.size() > 1) {
       LOG_WARN(kComp, "GPU %s reports SPX but has %zu handles; treating as %s", g.bdf.c_str(),
                handles.size(), ModeForCount(handles.size()).c_str());
       g.compute_mode = ModeForCount(handles.size());
     }
     snap->gpus.push_back(std::move(g));
+    ++index;
   }
   size_t n = snap->gpus.size();
   snap->gpu_links.assign(n * n, LinkClass::kUnknown);
@@ -190,10 +301,10 @@ Result<std::shared_ptr<const Snapshot>> BuildSnapshot(smi::Library* lib, const B
     LOG_WARN(kComp, "%s is not visible to the plugin; it is still passed to containers", kfd.c_str());
   for (const auto& g : snap->gpus) {
     LOG_INFO(kComp,
-             "GPU %d: %s bdf=%s numa=%d vram=%llu MiB mode=%s/%s partitions=%zu profile=%s "
+             "GPU %d: %s bdf=%s numa=%d vram=%llu MiB (%s) mode=%s/%s partitions=%zu profile=%s "
              "render=%s",
              g.index, g.uuid.c_str(), g.bdf.c_str(), g.numa,
-             static_cast<unsigned long long>(g.vram_mib), g.compute_mode.c_str(),
+             static_cast<unsigned long long>(g.vram_mib), g.vram_source.c_str(), g.compute_mode.c_str(),
              g.memory_mode.empty() ? "?" : g.memory_mode.c_str(), g.partitions.size(),
              g.PartitionProfile().empty() ? "-" : g.PartitionProfile().c_str(),
              g.partitions.front().render_path.c_str());

@@ -63,11 +63,24 @@ struct PhysicalGpu {
   std::string market_name;
   std::vector<Partition> partitions;  // one per amdsmi handle; sorted by partition_id
   int xgmi_links_down = 0;
+  // How vram_mib (the physical HBM) was established, most authoritative first:
+  // "memory-partition-config" (sum of the driver's NUMA memory ranges), "spx"
+  // (the one handle's vram_info), "share"/"pool"/"whole" (what each partition
+  // handle's vram_info turned out to mean, pinned by the model's known HBM),
+  // "share-unpinned" (no reference to check against; assumed per-partition).
+  std::string vram_source;
+  // The driver's accelerator partition profile ("CPX", ...; "" if unavailable).
+  std::string driver_profile;
 
   bool partitioned() const { return compute_mode != "SPX"; }
   // Resource name of this GPU's partitions, e.g. "cpx-1xcd.36gb" (empty if SPX).
   std::string PartitionProfile() const;
 };
+
+// Known HBM of a GPU model by market name (MiB), 0 if unknown. The sanity
+// bound for what partition handles report (MI355X/MI350X: 288 GB, 294,896 MiB
+// as amdsmi reports it on the MI355X box).
+uint64_t ModelHbmMib(const std::string& market_name);
 
 // Link classification between two physical GPUs, the analogue of NVML's P2P
 // level + NVLink count (vendor/.../nvml/nvml.go:132-154,592-658).

@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 
 #include "common/log.h"
@@ -34,6 +35,9 @@ struct Library::Fns {
   decltype(&amdsmi_get_gpu_kfd_info) kfd_info = nullptr;
   decltype(&amdsmi_get_gpu_asic_info) asic_info = nullptr;
   decltype(&amdsmi_get_gpu_xcd_counter) xcd_counter = nullptr;
+  decltype(&amdsmi_get_gpu_accelerator_partition_profile) accel_profile = nullptr;
+  decltype(&amdsmi_get_gpu_accelerator_partition_profile_config) accel_profile_config = nullptr;
+  decltype(&amdsmi_get_gpu_memory_partition_config) memory_partition_config = nullptr;
   decltype(&amdsmi_topo_get_link_type) link_type = nullptr;
   decltype(&amdsmi_topo_get_link_weight) link_weight = nullptr;
   decltype(&amdsmi_get_gpu_xgmi_link_status) xgmi_link_status = nullptr;
@@ -112,6 +116,9 @@ Result<std::unique_ptr<Library>> Library::Open(const std::string& path,
   Resolve(dl, "amdsmi_get_gpu_kfd_info", &f->kfd_info);
   Resolve(dl, "amdsmi_get_gpu_asic_info", &f->asic_info);
   Resolve(dl, "amdsmi_get_gpu_xcd_counter", &f->xcd_counter);
+  Resolve(dl, "amdsmi_get_gpu_accelerator_partition_profile", &f->accel_profile);
+  Resolve(dl, "amdsmi_get_gpu_accelerator_partition_profile_config", &f->accel_profile_config);
+  Resolve(dl, "amdsmi_get_gpu_memory_partition_config", &f->memory_partition_config);
   Resolve(dl, "amdsmi_topo_get_link_type", &f->link_type);
   Resolve(dl, "amdsmi_topo_get_link_weight", &f->link_weight);
   Resolve(dl, "amdsmi_get_gpu_xgmi_link_status", &f->xgmi_link_status);
@@ -231,10 +238,48 @@ Result<std::vector<ProcessorInfo>> Library::Enumerate() {
         uint16_t x = 0;
         if (f_->xcd_counter(h, &x) == AMDSMI_STATUS_SUCCESS) p.xcd_count = x;
       }
+      ReadPartitionProfile(h, &p);
       out.push_back(std::move(p));
     }
   }
   return out;
+}
+
+void Library::ReadPartitionProfile(void* h, ProcessorInfo* p) {
+  if (f_->accel_profile) {
+    // Both structs are large (the config is ~10 KiB): heap, not the stack.
+    auto prof = std::make_unique<amdsmi_accelerator_partition_profile_t>();
+    uint32_t pid = 0;
+    if (f_->accel_profile(h, prof.get(), &pid) == AMDSMI_STATUS_SUCCESS) {
+      static const char* names[] = {"", "SPX", "DPX", "TPX", "QPX", "CPX"};
+      unsigned t = static_cast<unsigned>(prof->profile_type);
+      if (t >= 1 && t <= 5) p->profile_type = names[t];
+      p->profile_partitions = prof->num_partitions;
+      if (f_->accel_profile_config) {
+        auto cfg = std::make_unique<amdsmi_accelerator_partition_profile_config_t>();
+        if (f_->accel_profile_config(h, cfg.get()) == AMDSMI_STATUS_SUCCESS) {
+          uint32_t n = std::min<uint32_t>(cfg->num_resource_profiles, AMDSMI_MAX_CP_PROFILE_RESOURCES);
+          for (uint32_t i = 0; i < n; ++i) {
+            const auto& r = cfg->resource_profiles[i];
+            if (r.profile_index == prof->profile_index && r.resource_type == AMDSMI_ACCELERATOR_XCC)
+              p->profile_xccs = r.partition_resource;
+          }
+        }
+      }
+    }
+  }
+  if (f_->memory_partition_config) {
+    auto mc = std::make_unique<amdsmi_memory_partition_config_t>();
+    if (f_->memory_partition_config(h, mc.get()) == AMDSMI_STATUS_SUCCESS) {
+      uint32_t n = std::min<uint32_t>(mc->num_numa_ranges, AMDSMI_MAX_NUM_NUMA_NODES);
+      uint64_t bytes = 0;
+      for (uint32_t i = 0; i < n; ++i)
+        if (mc->numa_range[i].end > mc->numa_range[i].start)
+          bytes += mc->numa_range[i].end - mc->numa_range[i].start + 1;
+      p->mem_ranges = n;
+      p->mem_ranges_mib = bytes >> 20;
+    }
+  }
 }
 
 Link Library::GetLink(void* src, void* dst) {

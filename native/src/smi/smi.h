@@ -43,6 +43,14 @@ struct ProcessorInfo {
   uint32_t xcd_count = 0;         // 0 = unknown
   std::string market_name;
   std::string asic_serial;        // same for every partition of one physical GPU ("" if unknown)
+  // amdsmi_get_gpu_accelerator_partition_profile (+ _config for the XCC count):
+  // the driver's own description of the current compute partitioning.
+  std::string profile_type;       // "SPX".."CPX" ("" = query unavailable)
+  uint32_t profile_partitions = 0;  // partitions of that profile (0 = unknown)
+  uint32_t profile_xccs = 0;        // XCCs per partition (0 = unknown)
+  // amdsmi_get_gpu_memory_partition_config: the GPU's NUMA memory ranges.
+  uint32_t mem_ranges = 0;        // number of ranges (= memory partitions; 0 = unknown)
+  uint64_t mem_ranges_mib = 0;    // their total size
 };
 
 enum class LinkType { kInternal = 0, kPcie = 1, kXgmi = 2, kNotApplicable = 3, kUnknown = 4 };
@@ -108,6 +116,7 @@ class Library {
 
  private:
   Library() = default;
+  void ReadPartitionProfile(void* h, ProcessorInfo* p);
   struct Fns;
   void* dl_ = nullptr;
   std::unique_ptr<Fns> f_;
