@@ -250,6 +250,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   // Health verdicts outlive every plugin generation (and, with a state file,
   // the process): a restart must not re-advertise a failed GPU as Healthy.
   health::Ledger ledger(cfg.flags.health_state_file);
+  health::HealthCounters health_counters;
   int backoff_ms = 1000;
   int exit_code = 0;
   bool quit = false;
@@ -274,7 +275,20 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
               "\"} 1\n"
               "# HELP amdgpu_dp_restarts_total Plugin (re)starts: kubelet restart, SIGHUP, retries.\n"
               "# TYPE amdgpu_dp_restarts_total counter\n"
-              "amdgpu_dp_restarts_total " + std::to_string(restarts.load()) + "\n";
+              "amdgpu_dp_restarts_total " + std::to_string(restarts.load()) + "\n"
+              "# HELP amdgpu_dp_health_events_enabled 1 if amdsmi event notification is registered (-1 not started).\n"
+              "# TYPE amdgpu_dp_health_events_enabled gauge\n"
+              "amdgpu_dp_health_events_enabled " + std::to_string(health_counters.events_enabled.load()) + "\n"
+              "# HELP amdgpu_dp_health_polls_total Health polls (liveness + uncorrectable ECC) run.\n"
+              "# TYPE amdgpu_dp_health_polls_total counter\n"
+              "amdgpu_dp_health_polls_total " + std::to_string(health_counters.polls.load()) + "\n"
+              "# HELP amdgpu_dp_health_ecc_reads_total Uncorrectable-ECC reads by result.\n"
+              "# TYPE amdgpu_dp_health_ecc_reads_total counter\n"
+              "amdgpu_dp_health_ecc_reads_total{result=\"ok\"} " + std::to_string(health_counters.ecc_reads_ok.load()) + "\n"
+              "amdgpu_dp_health_ecc_reads_total{result=\"error\"} " + std::to_string(health_counters.ecc_read_errors.load()) + "\n"
+              "# HELP amdgpu_dp_health_events_total amdsmi events received.\n"
+              "# TYPE amdgpu_dp_health_events_total counter\n"
+              "amdgpu_dp_health_events_total " + std::to_string(health_counters.events_received.load()) + "\n";
           // Ask the kubelet who holds which device (cached; outside the plugins lock).
           Result<std::vector<podresources::Assignment>> assigned = Unavailable("off");
           if (pod_lister) {
@@ -382,7 +396,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     backoff_ms = 1000;
     serving.store(true);
     if (started == 0) LOG_INFO(kComp, "no devices found; waiting indefinitely");
-    monitor = std::make_unique<health::Monitor>(lib->get(), *snap, hcfg, &ledger);
+    monitor = std::make_unique<health::Monitor>(lib->get(), *snap, hcfg, &ledger, &health_counters);
     monitor->SetLayoutListener([lfd](const std::string&) {
       uint64_t one = 1;
       ssize_t w = write(lfd, &one, sizeof(one));
@@ -519,6 +533,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
           } else if (si.ssi_signo == SIGUSR1) {
             // Explicitly requested: printed whatever the log level.
             for (auto& p : plugins) Logf(LogLevel::kInfo, kComp, "stats: %s", p->StatsJson().c_str());
+            Logf(LogLevel::kInfo, kComp, "health: %s", health_counters.Json().c_str());
           } else {
             LOG_INFO(kComp, "received signal %s, shutting down", strsignal(static_cast<int>(si.ssi_signo)));
             quit = true;

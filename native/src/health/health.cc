@@ -4,6 +4,7 @@
 #include <sys/eventfd.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cctype>
 #include <cerrno>
 #include <chrono>
@@ -186,9 +187,23 @@ std::vector<std::pair<int, std::string>> Ledger::Failed(const inventory::Snapsho
   return out;
 }
 
+std::string HealthCounters::Json() const {
+  char buf[320];
+  int e = events_enabled.load();
+  snprintf(buf, sizeof(buf),
+           "{\"events\": \"%s\", \"polls\": %llu, \"responsive\": %llu, \"ecc_reads_ok\": %llu, "
+           "\"ecc_read_errors\": %llu, \"events_received\": %llu}",
+           e < 0 ? "not started" : e ? "on" : "off", static_cast<unsigned long long>(polls.load()),
+           static_cast<unsigned long long>(responsive.load()), static_cast<unsigned long long>(ecc_reads_ok.load()),
+           static_cast<unsigned long long>(ecc_read_errors.load()),
+           static_cast<unsigned long long>(events_received.load()));
+  return buf;
+}
+
 Monitor::Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> snap, HealthConfig cfg,
-                 Ledger* ledger)
-    : lib_(lib), snap_(std::move(snap)), cfg_(std::move(cfg)), ledger_(ledger ? ledger : &own_ledger_) {
+                 Ledger* ledger, HealthCounters* counters)
+    : lib_(lib), snap_(std::move(snap)), cfg_(std::move(cfg)), ledger_(ledger ? ledger : &own_ledger_),
+      counters_(counters ? counters : &own_counters_) {
   for (const auto& p : snap_->procs) handles_.push_back(p.handle);
   size_t n = snap_->gpus.size();
   keys_.resize(n);
@@ -220,6 +235,8 @@ Status Monitor::Start() {
                   smi::EventMask(smi::kEvtVmFault) | smi::EventMask(smi::kEvtThermalThrottle);
   Status st = lib_->EventsInit(handles_, mask);
   events_ok_ = st.ok();
+  counters_->events_enabled.store(events_ok_ ? 1 : 0);
+  events_reason_ = events_ok_ ? "" : st.ToString();
   if (!events_ok_)
     LOG_WARN(kComp, "amdsmi event notification unavailable (%s); using polling only",
              st.ToString().c_str());
@@ -283,6 +300,9 @@ void Monitor::Stop() {
 }
 
 void Monitor::PollOnce() {
+  uint64_t poll = counters_->polls.fetch_add(1) + 1;
+  size_t answered = 0, ecc_ok = 0;
+  std::string counts;
   for (const auto& g : snap_->gpus) {
     void* h = snap_->procs[g.partitions.front().handle].handle;
     if (layout_listener_ && !layout_changed_) {
@@ -324,8 +344,19 @@ void Monitor::PollOnce() {
       Update(g.index, 0, kFailUnresponsive, "device responding again");
     }
     if (!alive) continue;
+    ++answered;
+    counters_->responsive.fetch_add(1);
     auto ecc = lib_->UncorrectableErrors(h);
-    if (!ecc.ok()) continue;
+    if (!ecc.ok()) {
+      counters_->ecc_read_errors.fetch_add(1);
+      if (poll == 1)
+        LOG_WARN(kComp, "GPU %s: uncorrectable ECC count unreadable (%s); ECC polling is off for it",
+                 g.bdf.c_str(), ecc.status().ToString().c_str());
+      continue;
+    }
+    ++ecc_ok;
+    counters_->ecc_reads_ok.fetch_add(1);
+    counts += (counts.empty() ? "" : ",") + std::to_string(*ecc);
     GpuRecord r = ledger_->Get(keys_[g.index]);
     if (*ecc < r.ecc_seen) {
       // The driver reset its RAS counters (GPU reset / driver reload): the
@@ -349,6 +380,10 @@ void Monitor::PollOnce() {
                  std::to_string(ecc_baseline_[g.index]) + ")");
     }
   }
+  if (poll == 1)
+    LOG_INFO(kComp, "health poll #1: %zu/%zu GPU(s) responding, uncorrectable ECC readable on %zu (counts [%s]); "
+             "events %s%s%s", answered, snap_->gpus.size(), ecc_ok, counts.c_str(), events_ok_ ? "on" : "off",
+             events_ok_ ? "" : ": ", events_reason_.c_str());
 }
 
 void Monitor::Update(int gpu, uint32_t set, uint32_t clear, const std::string& reason) {
@@ -375,6 +410,10 @@ void Monitor::Run() {
   while (!stop_.load()) {
     int slice = 500;  // bounded so Stop() is prompt; the reference waits 5000 ms per call
     if (cfg_.wait_ms > 0 && cfg_.wait_ms < slice) slice = cfg_.wait_ms;
+    if (cfg_.poll_interval_ms > 0) {  // wake for the next poll, not a slice later
+      auto until = std::chrono::duration_cast<std::chrono::milliseconds>(next_poll - Clock::now()).count();
+      slice = static_cast<int>(std::max<long long>(1, std::min<long long>(slice, until)));
+    }
     if (events_ok_) {
       events.clear();
       Status st = lib_->EventsWait(slice, &events);
@@ -383,6 +422,7 @@ void Monitor::Run() {
         Sleep(slice);
       }
       for (const auto& e : events) {
+        counters_->events_received.fetch_add(1);
         int gpu = -1;
         for (size_t i = 0; i < snap_->procs.size(); ++i)
           if (snap_->procs[i].handle == e.handle) gpu = snap_->GpuOfHandle(static_cast<int>(i));

@@ -83,6 +83,19 @@ struct GpuRecord {
   std::string reason;  // last failure reason (empty when healthy)
 };
 
+// Liveness of the health machinery itself, shared by all Monitor generations
+// (the metrics thread reads it while monitors come and go): whether event
+// notification is registered, and how many polls / ECC reads succeeded.
+struct HealthCounters {
+  std::atomic<int> events_enabled{-1};  // -1 not started, 0 off, 1 on
+  std::atomic<uint64_t> polls{0};
+  std::atomic<uint64_t> responsive{0};       // GPU answered amdsmi in a poll
+  std::atomic<uint64_t> ecc_reads_ok{0};
+  std::atomic<uint64_t> ecc_read_errors{0};
+  std::atomic<uint64_t> events_received{0};
+  std::string Json() const;
+};
+
 // Per-GPU health verdicts shared by all Monitor generations of a daemon.
 // Thread-safe. With a path, every change is written through (atomic rename)
 // and the file is loaded at construction; a missing or unreadable file starts
@@ -112,9 +125,9 @@ class Ledger {
 
 class Monitor {
  public:
-  // `ledger` may be null: the Monitor then keeps its verdicts to itself.
+  // `ledger` / `counters` may be null: the Monitor then keeps its own.
   Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> snap, HealthConfig cfg,
-          Ledger* ledger = nullptr);
+          Ledger* ledger = nullptr, HealthCounters* counters = nullptr);
   ~Monitor();
   void AddListener(Listener l);
   // Called once (from the monitor thread) when polling sees a GPU whose compute
@@ -152,6 +165,9 @@ class Monitor {
   // Per-GPU state (mirrored into the ledger).
   Ledger own_ledger_;
   Ledger* ledger_;
+  HealthCounters own_counters_;
+  HealthCounters* counters_;
+  std::string events_reason_;  // why event notification is off ("" when on)
   std::vector<std::string> keys_;
   std::vector<uint64_t> ecc_baseline_;
   std::vector<uint32_t> fail_;

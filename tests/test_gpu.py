@@ -103,8 +103,15 @@ def test_probe_cli_validates_shape(snap, probe_built):
     assert bad.returncode == (1 if xcds != 1 else 0)
 
 
-def test_health_monitor_starts_on_real_gpu(scratch, snap):
-    """Event notification may need privileges; either way the daemon must stay healthy."""
+def test_health_monitor_is_live_on_real_gpu(scratch, snap):
+    """Health must be live on the MI355X, by events or by polling: the daemon
+    reports whether amdsmi event notification registered (and why not) and the
+    result of its first poll (GPU answering, uncorrectable ECC readable). The
+    test fails if neither events nor ECC polling work. The daemon log is kept
+    under gpurun_out/health/ for profiles/."""
+    import re
+    import shutil
+    import time
     k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
     d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0"],
                        env={"DP_HEALTH_POLL_MS": "200"}).start()
@@ -114,18 +121,45 @@ def test_health_monitor_starts_on_real_gpu(scratch, snap):
         q, call = c.watch()
         law = q.get(timeout=10)
         assert all(x.health == "Healthy" for x in law.devices)
-        import time
-        time.sleep(1.0)  # several poll periods
+        log = d.wait_log("health poll #1:", 15)
+        time.sleep(1.0)  # several more poll periods
         assert q.empty(), "device flapped unhealthy on an idle healthy GPU"
         call.cancel()
         c.close()
     finally:
         assert d.stop() == 0
         k.stop()
+        out = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "health")
+        os.makedirs(out, exist_ok=True)
+        shutil.copy(d.log_path, os.path.join(out, "daemon_real_amdsmi_health.log"))
     log = d.log()
-    assert ("event notification unavailable" in log) or ("health checks disabled" not in log)
+    assert "health checks disabled" not in log
+    m = re.search(r"health poll #1: (\d+)/(\d+) GPU\(s\) responding, uncorrectable ECC readable on (\d+) "
+                  r"\(counts \[([0-9,]*)\]\); events (on|off)(?:: (.*))?", log)
+    assert m, log[-3000:]
+    answering, total, ecc_ok, events = int(m.group(1)), int(m.group(2)), int(m.group(3)), m.group(5)
+    assert answering == total == 1, m.group(0)  # amdsmi liveness polling works
+    assert events == "on" or ecc_ok == 1, f"neither events nor ECC polling is live: {m.group(0)}"
     # live partition-mode queries agree with the enumeration: no spurious re-partition restarts
     assert "partition mode changed" not in log and "amdsmi re-initialised" not in log
+
+
+def test_real_partition_profile_is_recorded(snap):
+    """What amdsmi's partition APIs report on this box (SPX here): the inventory
+    takes the GPU's HBM from the most authoritative source and names it."""
+    import json
+    g = snap["gpus"][0]
+    out = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "health")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "partition_apis.json"), "w") as f:
+        json.dump(g, f, indent=1)
+    assert g["vram_source"] in ("memory-partition-config", "spx"), g
+    assert abs(g["vram_mib"] - 294896) <= 294896 * 3 // 100, g
+    assert g["model_hbm_mib"] == 294896
+    rep = g["partitions"][0]["reported"]
+    if rep["profile_type"]:
+        assert rep["profile_type"] == g["compute_mode"], rep
+        assert rep["profile_partitions"] == len(g["partitions"]), rep
 
 
 def test_metrics_endpoint_on_real_gpu(scratch, snap):

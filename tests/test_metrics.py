@@ -240,3 +240,35 @@ def test_pod_resources_sharing_metrics(scratch):
             pr.stop()
         d.stop()
         k.stop()
+
+
+def test_health_liveness_is_reported(scratch):
+    """Events registered or not (and why), polls, ECC reads: in the log after the
+    first poll, in /metrics and in the SIGUSR1 dump (the real-GPU test asserts
+    on the same report)."""
+    import signal
+    state = os.path.join(scratch + ".fixture", "state")
+    os.makedirs(state, exist_ok=True)
+    fx = fixtures.node(2)
+    fx["events_supported"] = False
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fx, args=["--metrics-addr", "127.0.0.1:0"], state_dir=state,
+                       env={"DP_HEALTH_POLL_MS": "100"}).start()
+    try:
+        text = d.wait_log("serving /metrics and /healthz on port")
+        port = int(re.search(r"serving /metrics and /healthz on port (\d+)", text).group(1))
+        k.wait_registration()
+        log = d.wait_log("health poll #1:")
+        assert re.search(r"health poll #1: 2/2 GPU\(s\) responding, uncorrectable ECC readable on 2 "
+                         r"\(counts \[0,0\]\); events off: ", log), log
+        time.sleep(0.35)
+        s = _parse(_get(port, "/metrics")[1])
+        assert _value(s, "amdgpu_dp_health_events_enabled") == 0
+        assert _value(s, "amdgpu_dp_health_polls_total") >= 2
+        assert _value(s, "amdgpu_dp_health_ecc_reads_total", result="ok") >= 4
+        assert _value(s, "amdgpu_dp_health_ecc_reads_total", result="error") == 0
+        d.signal(signal.SIGUSR1)
+        d.wait_log('health: {"events": "off", "polls": ')
+    finally:
+        d.stop()
+        k.stop()

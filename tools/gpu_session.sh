@@ -13,8 +13,8 @@
 #   bench        the driver-shaped headline run (python bench.py, defaults)
 #   configs      bench for the three real-hardware configs (spx-none,
 #                timeslice4, auto-mem), 50 steps each
-#   health       the daemon on real libamd_smi with health checks on, its log
-#                and health report kept (events on/off, ECC polls)
+#   health       the GPU tests for health liveness (events on/off and why, first
+#                ECC poll) and the partition APIs; evidence in gpurun_out/health/
 #   partition    what libamd_smi reports for the partition APIs (JSON)
 #   prof         rocprofv3 --kernel-trace --stats of the HIP probe (copy, MFMA,
 #                census, latency kernels)
@@ -57,8 +57,11 @@ step_configs() {
   done
 }
 step_health() {
-  timeout -k 10 120 python tools/health_report.py --out $out/health > $out/health.json 2> $out/health.err || die HEALTH $out/health.err
-  cat $out/health.json
+  # The GPU tests that check health liveness and record the partition APIs keep
+  # their evidence in gpurun_out/health/ (daemon log, partition_apis.json).
+  timeout -k 10 300 python -u -m pytest tests/test_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread \
+    -p no:cacheprovider -k "health or partition_profile" > $out/health.log 2>&1 || die HEALTH $out/health.log
+  grep -h "health poll #1\|event notification" gpurun_out/health/daemon_real_amdsmi_health.log || true
 }
 step_partition() {
   timeout -k 10 60 python -c "import json; from k8s_gpu_sharing_plugin_amd.utils import native; print(json.dumps(native.snapshot(), indent=1))" > $out/snapshot.json 2> $out/snapshot.err || die PARTITION $out/snapshot.err
