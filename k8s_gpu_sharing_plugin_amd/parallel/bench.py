@@ -10,8 +10,12 @@ the node is full. One step = ``pods_per_step`` pods per rank. The K timed steps
 run between barrier + device-synchronize brackets; the job reports the max
 over ranks.
 
-After the timed region each rank runs the HIP probe on its GPU (real hardware
-only) to show the allocated device is usable and has the advertised shape.
+After the timed region each rank runs the HIP probe on the GPU its kubelet
+client admitted (real hardware only) -- found by PCI address, since amdsmi's
+enumeration order and HIP's device order can differ -- to show the allocated
+device is usable and has the advertised shape. The JSON records the RCCL world
+as torch.distributed saw it, the backend, and per rank the BDF it admitted
+next to the BDF the probe ran on.
 """
 
 import json
@@ -81,6 +85,28 @@ def _grpcio_allocate_p50(socket_path, calls=300):
         return None
 
 
+def _bdf_map(real, fixture):
+    """Device ID (GPU or partition UUID) -> PCI address of its GPU."""
+    from .. import MOCK_LIB
+    from ..utils import native
+    try:
+        if real:
+            snap = native.snapshot()
+        else:
+            import tempfile
+            from ..models import fixtures
+            os.environ["AMDSMI_MOCK_FIXTURE"] = fixtures.write(fixture, tempfile.mkdtemp(prefix="adpbdf"))
+            snap = native.snapshot(MOCK_LIB)
+    except Exception:
+        return {}
+    out = {}
+    for g in snap["gpus"]:
+        out[g["uuid"]] = g["bdf"]
+        for p in g["partitions"]:
+            out[p["uuid"]] = g["bdf"]
+    return out
+
+
 def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_mock=False,
         probe=True, log=print):
     try:
@@ -98,6 +124,8 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
         raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={world}")
     have_gpu = torch is not None and torch.cuda.is_available()
     real = have_gpu and not force_mock
+    if real and torch.cuda.device_count() < gpus:
+        raise SystemExit(f"--gpus {gpus} but only {torch.cuda.device_count()} GPU(s) are visible to HIP")
     if world > 1:
         # RCCL between GPU ranks; gloo when the run is on the mock (no GPU, or
         # --mock on a GPU box: then no rank touches the device at all).
@@ -131,7 +159,8 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                            (config not in POD_SIZE or e.get("resource", "").endswith("/gpu")), 20)
             devs = kub.wait(lambda e: e.get("event") == "devices" and e.get("resource") == reg["resource"], 20)
             info = {"socket": os.path.join(d, reg["endpoint"]), "resource": reg["resource"],
-                    "allocatable": devs["healthy"], "advertised": devs["total"], "scratch": d}
+                    "allocatable": devs["healthy"], "advertised": devs["total"], "scratch": d,
+                    "bdf_of": _bdf_map(real, fx)}
         if world > 1:
             box = [info]
             dist.broadcast_object_list(box, src=0)
@@ -155,10 +184,16 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
         stats["elapsed_s"] = elapsed
         client.close()
 
+        bdf_of = info.get("bdf_of") or {}
+        stats["admitted_bdfs"] = sorted({bdf_of.get(i, "?") for i in stats.get("device_ids", [])})
         if real and probe:
             from ..ops import probe as hip_probe
             try:
-                stats["probe"] = hip_probe.run(local_rank, 256 << 20, 5)
+                # The GPU this rank's client admitted, by PCI address (not local_rank).
+                bdf = stats["admitted_bdfs"][0] if stats["admitted_bdfs"] else None
+                dev = hip_probe.device_for_bdf(bdf) if bdf and bdf != "?" else local_rank
+                stats["probe"] = hip_probe.run(dev, 256 << 20, 5)
+                stats["probe_bdf"] = stats["probe"].get("pci")
             except Exception as e:  # reported, not fatal for the latency metric
                 stats["probe"] = {"error": str(e)}
 
@@ -207,7 +242,11 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                 # the same Allocate through grpcio (gRPC C-core + Python), i.e. what a
                 # heavyweight gRPC client stack adds on top of the plugin
                 "grpcio_client_allocate_p50_us": grpcio,
-                "per_rank": [{k: s[k] for k in ("rank", "rank_devices", "pods", "allocate", "preferred")}
+                # what torch.distributed actually ran with (RCCL on the GPU box)
+                "rccl_world": dist.get_world_size() if world > 1 else 1,
+                "backend": dist.get_backend() if world > 1 else "none",
+                "per_rank": [{**{k: s[k] for k in ("rank", "rank_devices", "pods", "allocate", "preferred")},
+                              "admitted_bdfs": s.get("admitted_bdfs"), "probe_bdf": s.get("probe_bdf")}
                              for s in everyone],
             }
             probes = [s.get("probe") for s in everyone if s.get("probe")]

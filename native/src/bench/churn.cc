@@ -1,5 +1,8 @@
 #include "bench/churn.h"
 
+#include "alloc/replicas.h"
+#include "common/strings.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -64,6 +67,7 @@ Result<std::unique_ptr<ChurnClient>> ChurnClient::Open(const std::string& socket
       c->free_.push_back(law.devices[i].id);
   }
   c->mine_ = c->free_.size();
+  c->mine_ids_ = alloc::StripReplicas(c->free_);
   if (c->mine_ < static_cast<size_t>(opt.pod_size))
     return FailedPrecondition("only " + std::to_string(c->mine_) + " healthy devices for rank " +
                               std::to_string(opt.rank) + ", pod size " + std::to_string(opt.pod_size));
@@ -145,7 +149,11 @@ std::string ChurnClient::StatsJson() const {
            "\"pod_size\": %d, \"pods\": %zu, \"seconds\": %.6f, \"pods_per_s\": %.1f, ",
            opt_.rank, opt_.world, advertised_, allocatable_, mine_, opt_.pod_size, run_pods_, run_seconds_,
            run_seconds_ > 0 ? run_pods_ / run_seconds_ : 0.0);
-  return std::string(head) + ToJson("allocate", Summarize(alloc_us_)) + ", " +
+  std::string ids = "\"device_ids\": [";
+  for (size_t i = 0; i < mine_ids_.size() && i < 64; ++i)
+    ids += (i ? ", \"" : "\"") + JsonEscape(mine_ids_[i]) + "\"";
+  ids += "], ";
+  return std::string(head) + ids + ToJson("allocate", Summarize(alloc_us_)) + ", " +
          ToJson("preferred", Summarize(pref_us_)) + ", " + ToJson("pod", Summarize(pod_us_)) + "}";
 }
 

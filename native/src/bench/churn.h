@@ -53,6 +53,7 @@ class ChurnClient {
   ChurnOptions opt_;
   size_t advertised_ = 0, allocatable_ = 0, mine_ = 0;
   std::vector<std::string> free_;
+  std::vector<std::string> mine_ids_;  // physical device IDs this rank churns (replica suffix stripped)
   std::vector<std::vector<std::string>> live_;  // FIFO of admitted pods
   size_t live_head_ = 0;
   std::vector<double> alloc_us_, pref_us_, pod_us_;

@@ -29,6 +29,8 @@ def test_bench_single_process_contract():
     assert res["allocatable"] == 1
     assert 0 < res["value"] < 5000
     assert res["per_rank"][0]["allocate"]["n"] == 300
+    assert res["rccl_world"] == 1 and res["backend"] == "none"
+    assert res["per_rank"][0]["admitted_bdfs"] == ["0000:0c:00.0"]  # GPU 0 of the node model
 
 
 @pytest.mark.slow
@@ -43,6 +45,9 @@ def test_bench_two_ranks_gloo():
     assert res["n_gpus"] == 2 and res["allocatable"] == 2
     assert sorted(p["rank"] for p in res["per_rank"]) == [0, 1]
     assert all(p["rank_devices"] == 1 for p in res["per_rank"])
+    assert res["rccl_world"] == 2 and res["backend"] == "gloo"  # nccl (RCCL) on the GPU box
+    bdfs = {p["rank"]: p["admitted_bdfs"] for p in res["per_rank"]}
+    assert bdfs == {0: ["0000:0c:00.0"], 1: ["0000:2c:00.0"]}  # each rank admits its own GPU
 
 
 @pytest.mark.parametrize("config,advertised", [("timeslice4", 4), ("cpx-single", 8), ("auto-mem", 294),

@@ -65,7 +65,7 @@ step_health() {
 }
 step_partition() {
   timeout -k 10 60 python -c "import json; from k8s_gpu_sharing_plugin_amd.utils import native; print(json.dumps(native.snapshot(), indent=1))" > $out/snapshot.json 2> $out/snapshot.err || die PARTITION $out/snapshot.err
-  python -c "import json; d=json.load(open('$out/snapshot.json')); g=d['gpus'][0]; print({k: g.get(k) for k in ('bdf','vram_bytes','compute_partition','memory_partition','partition_profile')}); print([ (p.get('profile'), p.get('vram_bytes')) for p in g['partitions']][:8])"
+  python -c "import json; d=json.load(open('$out/snapshot.json')); g=d['gpus'][0]; print({k: g.get(k) for k in ('bdf','vram_mib','vram_source','driver_profile','compute_mode','memory_mode','profile','model_hbm_mib')}); print([p.get('reported') for p in g['partitions']][:8])"
 }
 step_prof() {
   ( cd /tmp && \
