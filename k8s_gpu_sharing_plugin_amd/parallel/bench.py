@@ -65,13 +65,17 @@ def _server_stats(daemon):
         return {}
 
 
-def _grpcio_allocate_p50(socket_path, calls=300):
+def _grpcio_allocate_p50(socket_path, device=None, calls=300):
+    """Allocate p50 through grpcio (gRPC C-core + Python): an independent gRPC
+    client stack, next to the native client's number."""
     try:
         from ..utils import kubelet
         c = kubelet.PluginClient(socket_path)
         q, call = c.watch()
-        dev = q.get(timeout=5).devices[0].ID
+        devs = q.get(timeout=5).devices
         call.cancel()
+        ids = [d.ID for d in devs]
+        dev = next((i for i in ids if device and i.startswith(device)), ids[0])
         lat = []
         for i in range(calls + 50):
             t = time.perf_counter()
@@ -183,6 +187,9 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
         stats = client.stats()
         stats["elapsed_s"] = elapsed
         client.close()
+        # Every rank also times its own device through grpcio (after the timed region).
+        stats["grpcio_allocate_p50_us"] = _grpcio_allocate_p50(
+            info["socket"], (stats.get("device_ids") or [None])[0])
 
         bdf_of = info.get("bdf_of") or {}
         stats["admitted_bdfs"] = sorted({bdf_of.get(i, "?") for i in stats.get("device_ids", [])})
@@ -203,7 +210,8 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
             dist.all_gather_object(everyone, stats)
         if rank == 0:
             server = _server_stats(daemon)
-            grpcio = _grpcio_allocate_p50(info["socket"])
+            grpcio = [s.get("grpcio_allocate_p50_us") for s in everyone]
+            grpcio = max(grpcio) if all(g is not None for g in grpcio) else None
             ms_per_step = max(s["elapsed_s"] for s in everyone) / steps * 1e3
             p50 = max(s["allocate"]["p50_us"] for s in everyone)
             total_pods = sum(s["pods"] for s in everyone)
@@ -240,13 +248,14 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                 # in-daemon time of the Allocate handler (decode + lookup + encode), from SIGUSR1 stats
                 "server_allocate_handler_avg_us": server.get("allocate_handler_avg_us"),
                 # the same Allocate through grpcio (gRPC C-core + Python), i.e. what a
-                # heavyweight gRPC client stack adds on top of the plugin
+                # heavyweight gRPC client stack adds on top of the plugin (max over ranks)
                 "grpcio_client_allocate_p50_us": grpcio,
                 # what torch.distributed actually ran with (RCCL on the GPU box)
                 "rccl_world": dist.get_world_size() if world > 1 else 1,
                 "backend": dist.get_backend() if world > 1 else "none",
                 "per_rank": [{**{k: s[k] for k in ("rank", "rank_devices", "pods", "allocate", "preferred")},
-                              "admitted_bdfs": s.get("admitted_bdfs"), "probe_bdf": s.get("probe_bdf")}
+                              "admitted_bdfs": s.get("admitted_bdfs"), "probe_bdf": s.get("probe_bdf"),
+                              "grpcio_allocate_p50_us": s.get("grpcio_allocate_p50_us")}
                              for s in everyone],
             }
             probes = [s.get("probe") for s in everyone if s.get("probe")]

@@ -48,6 +48,9 @@ def test_bench_two_ranks_gloo():
     assert res["rccl_world"] == 2 and res["backend"] == "gloo"  # nccl (RCCL) on the GPU box
     bdfs = {p["rank"]: p["admitted_bdfs"] for p in res["per_rank"]}
     assert bdfs == {0: ["0000:0c:00.0"], 1: ["0000:2c:00.0"]}  # each rank admits its own GPU
+    # an independent gRPC stack (grpcio) per rank, max over ranks at the top
+    per = [p["grpcio_allocate_p50_us"] for p in res["per_rank"]]
+    assert all(v and v > 0 for v in per) and res["grpcio_client_allocate_p50_us"] == max(per)
 
 
 @pytest.mark.parametrize("config,advertised", [("timeslice4", 4), ("cpx-single", 8), ("auto-mem", 294),
