@@ -204,6 +204,8 @@ class Builder {
           if (m.kind == Node::kMap) sources.push_back(&m);
           else if (m.kind == Node::kSeq)
             for (const auto& s : m.seq) sources.push_back(&s);
+          else
+            sources.push_back(&m);  // rejected below
           for (const Node* s : sources) {
             if (s->kind != Node::kMap)
               return InvalidArgument("yaml: line " + std::to_string(s->line) +

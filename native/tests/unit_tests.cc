@@ -23,6 +23,7 @@
 #include "alloc/topology.h"
 #include "common/strings.h"
 #include "daemon/config.h"
+#include "daemon/yaml.h"
 #include "grpc/grpc.h"
 #include "grpc/server_conn.h"
 #include "health/health.h"
@@ -714,7 +715,94 @@ static void TestReplicaCuRanges() {
   CHECK(plugin::MemoryUnitCuRanges(256, 0, 294).empty());
 }
 
+
+static void TestYaml() {
+  using adp::yaml::Node;
+  using adp::yaml::ScalarType;
+  auto plain = [](const char* v) {
+    Node n;
+    n.kind = Node::kScalar;
+    n.plain = true;
+    n.value = v;
+    return n;
+  };
+  std::string c;
+  // go-yaml v2 resolution
+  CHECK(adp::yaml::Resolve(plain("yes"), &c) == ScalarType::kBool && c == "true");
+  CHECK(adp::yaml::Resolve(plain("Off"), &c) == ScalarType::kBool && c == "false");
+  CHECK(adp::yaml::Resolve(plain("n"), &c) == ScalarType::kBool && c == "false");
+  CHECK(adp::yaml::Resolve(plain("0x1F"), &c) == ScalarType::kInt && c == "31");
+  CHECK(adp::yaml::Resolve(plain("0o17"), &c) == ScalarType::kInt && c == "15");
+  CHECK(adp::yaml::Resolve(plain("017"), &c) == ScalarType::kInt && c == "15");
+  CHECK(adp::yaml::Resolve(plain("0b101"), &c) == ScalarType::kInt && c == "5");
+  CHECK(adp::yaml::Resolve(plain("1_000"), &c) == ScalarType::kInt && c == "1000");
+  CHECK(adp::yaml::Resolve(plain("-42"), &c) == ScalarType::kInt && c == "-42");
+  CHECK(adp::yaml::Resolve(plain("99999999999999999999"), &c) == ScalarType::kFloat);
+  CHECK(adp::yaml::Resolve(plain("1.5e3"), &c) == ScalarType::kFloat);
+  CHECK(adp::yaml::Resolve(plain(".inf"), &c) == ScalarType::kFloat);
+  CHECK(adp::yaml::Resolve(plain("~"), &c) == ScalarType::kNull);
+  CHECK(adp::yaml::Resolve(plain("gpu:sharedgpu:4"), &c) == ScalarType::kString);
+  CHECK(adp::yaml::Resolve(plain("1.2.3"), &c) == ScalarType::kString);
+  Node quoted = plain("true");
+  quoted.plain = false;
+  CHECK(adp::yaml::Resolve(quoted, &c) == ScalarType::kString);
+  Node tagged = plain("12");
+  tagged.plain = false;
+  tagged.tag = "tag:yaml.org,2002:str";
+  CHECK(adp::yaml::Resolve(tagged, &c) == ScalarType::kString);
+  tagged.tag = "tag:yaml.org,2002:int";
+  CHECK(adp::yaml::Resolve(tagged, &c) == ScalarType::kInt && c == "12");
+
+  if (adp::yaml::Available()) {
+    CHECK(!adp::yaml::LibraryVersion().empty());
+    auto doc = adp::yaml::Parse("a: &x {b: 1, c: [1, 2]}\nd: *x\ne:\n  <<: [*x, {f: 2}]\n  b: 9\n");
+    CHECK(doc.ok());
+    if (doc.ok()) {
+      const Node* d = doc->Get("d");
+      CHECK(d && d->kind == Node::kMap && d->Get("c") && d->Get("c")->seq.size() == 2);
+      const Node* e = doc->Get("e");
+      CHECK(e && e->Get("b") && e->Get("b")->value == "9" && e->Get("f") && e->Get("c"));
+    }
+    CHECK(!adp::yaml::Parse("a: *nope\n").ok());
+    CHECK(!adp::yaml::Parse("a: [1, 2\n").ok());
+    CHECK(!adp::yaml::Parse("{[1]: 2}\n").ok());  // non-scalar key
+    CHECK(!adp::yaml::Parse("a: {<<: 3}\n").ok());  // merge of a scalar
+    // billion laughs: alias expansion is bounded
+    std::string bomb = "a: &a [x, x, x, x, x, x, x, x, x, x]\n";
+    for (char k = 'b'; k <= 'j'; ++k)
+      bomb += std::string(1, k) + ": &" + k + " [*" + char(k - 1) + ", *" + char(k - 1) + ", *" + char(k - 1) +
+              ", *" + char(k - 1) + ", *" + char(k - 1) + ", *" + char(k - 1) + ", *" + char(k - 1) + ", *" +
+              char(k - 1) + ", *" + char(k - 1) + ", *" + char(k - 1) + "]\n";
+    auto b = adp::yaml::Parse(bomb);
+    CHECK(!b.ok() && b.status().message().find("too large") != std::string::npos);
+    bool extra = false;
+    auto two = adp::yaml::Parse("a: 1\n---\nb: 2\n", &extra);
+    CHECK(two.ok() && extra && two->Get("a") && !two->Get("b"));
+    auto empty = adp::yaml::Parse("");
+    CHECK(empty.ok() && empty->kind == Node::kNull);
+  }
+
+  // The strict subset parser (no libyaml).
+  auto ok = adp::yaml::ParseSubset("# c\nversion: v1\nflags:\n  a: 'it''s'  # c\n  b: \"x\\ty\"\n  c:\n  d: ~\ntop: 1\n");
+  CHECK(ok.ok());
+  if (ok.ok()) {
+    const Node* f = ok->Get("flags");
+    CHECK(f && f->kind == Node::kMap && f->Get("a")->value == "it's" && f->Get("b")->value == "x\ty");
+    CHECK(f->Get("c")->kind == Node::kNull && f->Get("d")->kind == Node::kNull && ok->Get("top")->value == "1");
+  }
+  const char* refused[] = {"a: {b: 1}\n", "a: [1]\n", "a: |\n  x\n", "a: >\n  x\n", "a: &x 1\n", "a: *x\n",
+                           "a: !!str 1\n", "- a\n", "a: 1\n---\nb: 2\n", "%YAML 1.1\n---\na: 1\n",
+                           "? a\n: b\n", "a:\n  <<: x\n", "a: \"open\n", "a: \"\\x41\"\n"};
+  for (const char* r : refused) {
+    auto st = adp::yaml::ParseSubset(r);
+    CHECK(!st.ok() && st.status().message().find("libyaml") != std::string::npos);
+  }
+  const char* bad[] = {"a: 1\n b: 2\n", "a: 1\na: 2\n", "just text\n", "a: @x\n", "  a: 1\nb: 2\n"};
+  for (const char* r : bad) CHECK(!adp::yaml::ParseSubset(r).ok());
+}
+
 int main() {
+  TestYaml();
   TestReplicaCuRanges();
   TestPodResources();
   TestMetrics();
