@@ -196,6 +196,7 @@ void Plugin::BuildUnits() {
     if (p != MAP_FAILED) best_effort_cache_.reset(static_cast<std::atomic<uint16_t>*>(p));
   }
   healthy_.assign(units_.size(), 1);
+  warned_law_.reset(new std::atomic<uint64_t>[units_.size()]());
   RebuildListAndWatch();
 }
 
@@ -310,8 +311,9 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
         if (opts_.reject_unhealthy)
           return FailedPrecondition("allocation request for '" + spec_.resource_name + "': device " +
                                     units_[u].id + " is Unhealthy");
-        LOG_WARN(kComp, "allocate '%s': device %s is Unhealthy (allocated anyway; --reject-unhealthy refuses)",
-                 spec_.resource_name.c_str(), units_[u].id.c_str());
+        if (warned_law_[u].exchange(law->version, std::memory_order_relaxed) != law->version)
+          LOG_WARN(kComp, "allocate '%s': device %s is Unhealthy (allocated anyway; --reject-unhealthy refuses)",
+                   spec_.resource_name.c_str(), units_[u].id.c_str());
       }
     }
     // Memory-unit resources (replicas = -1): tell the container how much HBM it

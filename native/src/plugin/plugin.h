@@ -255,6 +255,9 @@ class Plugin {
   // Units advertised Unhealthy in law_: Allocate() only looks health up when
   // this is non-zero, so the healthy fast path costs one relaxed load.
   std::atomic<size_t> unhealthy_units_{0};
+  // Per unit: the ListAndWatch version of the last "allocated while Unhealthy"
+  // warning, so a kubelet retrying the same device logs once per transition.
+  std::unique_ptr<std::atomic<uint64_t>[]> warned_law_;
   // law_streams_[i] is confined to server loop i.
   std::vector<std::vector<LawStream>> law_streams_;
 

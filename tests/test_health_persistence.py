@@ -278,7 +278,10 @@ def test_allocate_of_unhealthy_device(mk, reject):
         assert ids[1] in e.value.details() and "Unhealthy" in e.value.details()
     else:
         assert c.allocate([ids[1]]).container_responses
+        assert c.allocate([ids[1]]).container_responses  # a retry: counted, not logged again
         n.d.wait_log(f"device {ids[1]} is Unhealthy (allocated anyway")
+        time.sleep(0.2)
+        assert n.d.log().count(f"device {ids[1]} is Unhealthy (allocated anyway") == 1
     n.inject("1 4 post-reset")
     n.wait_health(lambda h: h[ids[1]] == "Healthy")
     assert c.allocate([ids[1]]).container_responses
