@@ -130,7 +130,11 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
     real = have_gpu and not force_mock
     if real and torch.cuda.device_count() < gpus:
         raise SystemExit(f"--gpus {gpus} but only {torch.cuda.device_count()} GPU(s) are visible to HIP")
-    if world > 1:
+    # A process group whenever a launcher started us (torchrun sets MASTER_ADDR),
+    # even with one rank: the 1-rank torchrun run then exercises the same RCCL
+    # init + object collectives the driver's multi-GPU run uses.
+    use_dist = dist is not None and (world > 1 or ("MASTER_ADDR" in os.environ and "RANK" in os.environ))
+    if use_dist:
         # RCCL between GPU ranks; gloo when the run is on the mock (no GPU, or
         # --mock on a GPU box: then no rank touches the device at all).
         backend = "nccl" if real else "gloo"
@@ -165,7 +169,7 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
             info = {"socket": os.path.join(d, reg["endpoint"]), "resource": reg["resource"],
                     "allocatable": devs["healthy"], "advertised": devs["total"], "scratch": d,
                     "bdf_of": _bdf_map(real, fx)}
-        if world > 1:
+        if use_dist:
             box = [info]
             dist.broadcast_object_list(box, src=0)
             info = box[0]
@@ -174,14 +178,14 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
         client.run(max(1, warmup) * pods_per_step, record=False)
         client.reset()
 
-        if world > 1:
+        if use_dist:
             dist.barrier()
         sync(torch)
         t0 = time.perf_counter()
         for _ in range(steps):
             client.run(pods_per_step, record=True)
         sync(torch)
-        if world > 1:
+        if use_dist:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         stats = client.stats()
@@ -205,7 +209,7 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                 stats["probe"] = {"error": str(e)}
 
         everyone = [stats]
-        if world > 1:
+        if use_dist:
             everyone = [None] * world
             dist.all_gather_object(everyone, stats)
         if rank == 0:
@@ -251,8 +255,8 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                 # heavyweight gRPC client stack adds on top of the plugin (max over ranks)
                 "grpcio_client_allocate_p50_us": grpcio,
                 # what torch.distributed actually ran with (RCCL on the GPU box)
-                "rccl_world": dist.get_world_size() if world > 1 else 1,
-                "backend": dist.get_backend() if world > 1 else "none",
+                "rccl_world": dist.get_world_size() if use_dist else 1,
+                "backend": dist.get_backend() if use_dist else "none",
                 "per_rank": [{**{k: s[k] for k in ("rank", "rank_devices", "pods", "allocate", "preferred")},
                               "admitted_bdfs": s.get("admitted_bdfs"), "probe_bdf": s.get("probe_bdf"),
                               "grpcio_allocate_p50_us": s.get("grpcio_allocate_p50_us")}
@@ -271,7 +275,7 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                     log(f"daemon exited with {code}:\n{daemon.log()[-3000:]}")
             if kub is not None:
                 kub.stop()
-        if world > 1 and dist.is_initialized():
+        if use_dist and dist.is_initialized():
             dist.destroy_process_group()
 
 

@@ -73,3 +73,16 @@ def test_bench_mixed_gpu4_admits_four_gpu_pods(monkeypatch):
     res = bench.run(gpus=1, steps=1, warmup=1, pods_per_step=20, config="mixed-gpu4", force_mock=True, probe=False)
     assert res["resource"] == "amd.com/gpu" and res["advertised"] == 6
     assert res["per_rank"][0]["preferred"]["n"] == 20
+
+
+def test_bench_one_rank_under_torchrun_uses_a_process_group():
+    """torchrun with one rank runs the same collectives as the multi-GPU job
+    (gloo here on the mock; RCCL on the GPU box, tests/test_gpu.py)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", "29563", "bench.py", "--gpus", "1",
+                        "--steps", "2", "--warmup", "1", "--mock"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = _last_json(r.stdout)
+    assert res["rccl_world"] == 1 and res["backend"] == "gloo"

@@ -433,3 +433,25 @@ def test_pytorch_matmul_runs_on_its_cu_share(snap):
     ratio = share["tflops"] / full["tflops"]
     print(json.dumps({"full_tflops": full["tflops"], "share_tflops": share["tflops"], "ratio": ratio}))
     assert 0.12 < ratio < 0.6, (full, share)
+
+
+def test_bench_under_torchrun_runs_rccl(snap):
+    """The driver's multi-GPU bench path on one GPU: torchrun, one rank, a real
+    RCCL process group (broadcast_object_list / all_gather_object / barrier
+    over nccl), the probe on the admitted GPU by PCI address."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", "29571", "bench.py", "--gpus", "1",
+                        "--steps", "3", "--warmup", "1"],
+                       cwd=root, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["backend"] == "nccl" and res["rccl_world"] == 1, res
+    rank0 = res["per_rank"][0]
+    assert rank0["admitted_bdfs"] == [snap["gpus"][0]["bdf"]]
+    assert rank0["probe_bdf"] == snap["gpus"][0]["bdf"]
+    assert res["probe"][0]["checksum_ok"]
