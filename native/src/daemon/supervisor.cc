@@ -528,6 +528,9 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
           if (si.ssi_signo == SIGHUP) {
             LOG_INFO(kComp, "received SIGHUP, restarting");
             reload_config("SIGHUP");
+            // The monitor is stopped first so it cannot write the old verdicts back.
+            if (monitor) monitor->Stop();
+            ledger.Reload();
             reinit = true;
             do_restart = true;
           } else if (si.ssi_signo == SIGUSR1) {

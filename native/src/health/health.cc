@@ -89,6 +89,26 @@ Ledger::Ledger(std::string path) : path_(std::move(path)) {
   LOG_INFO(kComp, "health state %s: %zu GPU record(s), %zu unhealthy", path_.c_str(), recs_.size(), failed);
 }
 
+void Ledger::Reload() {
+  if (path_.empty()) return;
+  std::ifstream in(path_);
+  std::map<std::string, GpuRecord> next;
+  if (in) {
+    std::stringstream ss;
+    ss << in.rdbuf();
+    next = Parse(ss.str());
+  } else if (errno != ENOENT) {
+    LOG_WARN(kComp, "cannot re-read health state %s: %s; keeping the current state", path_.c_str(), strerror(errno));
+    return;
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  for (const auto& [k, r] : recs_)
+    if (r.fail && (!next.count(k) || !next[k].fail))
+      LOG_INFO(kComp, "health state %s: GPU %s cleared by the operator (was: %s)", path_.c_str(), k.c_str(),
+               r.reason.c_str());
+  recs_ = std::move(next);
+}
+
 std::string Ledger::Serialize(const std::map<std::string, GpuRecord>& m) {
   std::string out = "adp-health v1\n";
   for (const auto& [k, r] : m) {

@@ -110,6 +110,10 @@ class Ledger {
   // (gpu index, reason) of every GPU of `snap` the ledger holds as failed.
   std::vector<std::pair<int, std::string>> Failed(const inventory::Snapshot& snap) const;
   const std::string& path() const { return path_; }
+  // Re-reads the state file (SIGHUP): records an operator removed from it are
+  // forgotten, i.e. those GPUs are Healthy again with a fresh ECC baseline.
+  // No-op without a file; an unreadable file keeps the in-memory state.
+  void Reload();
   // File format, exposed for tests: "adp-health v1" header, then one
   // tab-separated line per GPU: key, ecc baseline ("-" = none), highest ECC
   // count seen, fail bits, reason.

@@ -285,3 +285,35 @@ def test_allocate_of_unhealthy_device(mk, reject):
     n.inject("1 4 post-reset")
     n.wait_health(lambda h: h[ids[1]] == "Healthy")
     assert c.allocate([ids[1]]).container_responses
+
+
+def test_operator_clears_a_gpu_from_the_state_file_and_sighups(mk, scratch):
+    """Returning a repaired GPU to service without a reset event: remove its
+    line from the state file and SIGHUP; it comes back Healthy, re-baselined."""
+    state_file = os.path.join(scratch + ".fixture", "health.state")
+    n = mk(args=["--health-state-file", state_file])
+    ids = sorted(n.start())
+    n.set_ecc(1, 7)
+    n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+    lines = open(state_file).read().splitlines()
+    kept = [ln for ln in lines if not ln.startswith(ids[1])]
+    assert len(kept) == len(lines) - 1
+    with open(state_file + ".edit", "w") as f:
+        f.write("\n".join(kept) + "\n")
+    os.rename(state_file + ".edit", state_file)
+    n.d.signal(signal.SIGHUP)
+    assert n.first_law() == {ids[0]: "Healthy", ids[1]: "Healthy"}
+    n.d.wait_log(f"GPU {ids[1]} cleared by the operator")
+    time.sleep(0.4)  # polls see ECC 7 = the new baseline: stays Healthy
+    assert n.q.empty()
+    assert "\t7\t7\t0\t" in open(state_file).read()
+
+
+def test_sighup_without_edits_keeps_the_state_file_verdicts(mk, scratch):
+    state_file = os.path.join(scratch + ".fixture", "health.state")
+    n = mk(args=["--health-state-file", state_file])
+    ids = sorted(n.start())
+    n.set_ecc(0, 3)
+    n.wait_health(lambda h: h[ids[0]] == "Unhealthy")
+    n.d.signal(signal.SIGHUP)
+    assert n.first_law() == {ids[0]: "Unhealthy", ids[1]: "Healthy"}
