@@ -24,6 +24,8 @@
 #   interference noisy-neighbour victim latency with and without CU shares
 #   floor        UDS ping-pong floor, busy-poll on and off
 #   spread       10 back-to-back headline runs (bench.py --no-probe)
+#   soak         3 minutes of churn + SIGHUP + kubelet restarts + scrapes on
+#                real libamd_smi (health polling, state file): RSS/fd/thread leaks
 set -o pipefail
 out=${OUT:-gpurun_out/session}
 mkdir -p "$out"
@@ -119,6 +121,10 @@ step_spread() {
     timeout -k 10 300 python bench.py --no-probe > $out/spread_$i.json 2> $out/spread_$i.err || die "SPREAD $i" $out/spread_$i.err
     python -c "import json; d=json.load(open('$out/spread_$i.json')); print('R $i', d['value'], d['allocate_p99_us'], d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'])"
   done
+}
+step_soak() {
+  timeout -k 10 400 python -u tools/soak.py --seconds 180 --real --out $out/soak.json > $out/soak.log 2>&1 || die SOAK $out/soak.log
+  tail -1 $out/soak.log
 }
 
 [ $# -gt 0 ] || set -- tests smoke bench prof

@@ -51,7 +51,8 @@ def main():
     with socket.socket() as s0:  # a free port for the metrics endpoint
         s0.bind(("127.0.0.1", 0))
         port = s0.getsockname()[1]
-    args = ["--metrics-addr", f"127.0.0.1:{port}", "--resource-config", "gpu:gpu:4"]
+    args = ["--metrics-addr", f"127.0.0.1:{port}", "--resource-config", "gpu:gpu:4",
+            "--health-state-file", os.path.join(d, "health.state")]
     if a.real:
         args += ["--devices", "0"]
     dm = harness.Daemon(d, None if a.real else fixtures.node(8), args=args, real_smi=a.real,
