@@ -257,20 +257,33 @@ void Library::ReadPartitionProfile(void* h, ProcessorInfo* p) {
       p->profile_partitions = prof->num_partitions;
       if (f_->accel_profile_config) {
         auto cfg = std::make_unique<amdsmi_accelerator_partition_profile_config_t>();
-        if (f_->accel_profile_config(h, cfg.get()) == AMDSMI_STATUS_SUCCESS) {
+        amdsmi_status_t cs = f_->accel_profile_config(h, cfg.get());
+        if (cs == AMDSMI_STATUS_SUCCESS) {
           uint32_t n = std::min<uint32_t>(cfg->num_resource_profiles, AMDSMI_MAX_CP_PROFILE_RESOURCES);
           for (uint32_t i = 0; i < n; ++i) {
             const auto& r = cfg->resource_profiles[i];
+            LOG_DEBUG(kComp, "%s: partition resource profile %u: profile_index=%u type=%d resource=%u shared_by=%u",
+                      p->bdf.c_str(), i, r.profile_index, static_cast<int>(r.resource_type), r.partition_resource,
+                      r.num_partitions_share_resource);
             if (r.profile_index == prof->profile_index && r.resource_type == AMDSMI_ACCELERATOR_XCC)
               p->profile_xccs = r.partition_resource;
           }
+        } else {
+          LOG_DEBUG(kComp, "%s: accelerator partition profile config unavailable (status %d)", p->bdf.c_str(),
+                    static_cast<int>(cs));
         }
+        LOG_DEBUG(kComp, "%s: accelerator partition profile type=%s partitions=%u index=%u resources=%u xccs=%u",
+                  p->bdf.c_str(), p->profile_type.c_str(), prof->num_partitions, prof->profile_index,
+                  prof->num_resources, p->profile_xccs);
       }
     }
   }
   if (f_->memory_partition_config) {
     auto mc = std::make_unique<amdsmi_memory_partition_config_t>();
-    if (f_->memory_partition_config(h, mc.get()) == AMDSMI_STATUS_SUCCESS) {
+    amdsmi_status_t ms = f_->memory_partition_config(h, mc.get());
+    if (ms != AMDSMI_STATUS_SUCCESS)
+      LOG_DEBUG(kComp, "%s: memory partition config unavailable (status %d)", p->bdf.c_str(), static_cast<int>(ms));
+    if (ms == AMDSMI_STATUS_SUCCESS) {
       uint32_t n = std::min<uint32_t>(mc->num_numa_ranges, AMDSMI_MAX_NUM_NUMA_NODES);
       uint64_t bytes = 0;
       for (uint32_t i = 0; i < n; ++i)
