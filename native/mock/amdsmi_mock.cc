@@ -28,7 +28,8 @@
 //               } ] }
 // Runtime injection:
 //   event FIFO lines: "<gpu>[:<partition>] <event-type> [message]"
-//   state_dir files:  gpu<i>.ecc (uncorrectable count), gpu<i>.dead (device gone),
+//   state_dir files:  gpu<i>.ecc (uncorrectable count; not a number = query fails),
+//                     gpu<i>.dead (device gone),
 //                     gpu<i>.partition ("CPX NPS2": live partition-mode override),
 //                     gpu<i>.xgmi_down (number of xGMI links reported down)
 //   amdsmi_shut_down + amdsmi_init re-reads the fixture (re-enumeration after a
@@ -579,6 +580,7 @@ amdsmi_status_t amdsmi_get_gpu_total_ecc_count(amdsmi_processor_handle h,
     std::ifstream f(g->state_dir + "/gpu" + std::to_string(p->gpu) + ".ecc");
     uint64_t v = 0;
     if (f >> v) ec->uncorrectable_count = v;
+    else if (f.is_open()) return AMDSMI_STATUS_NOT_SUPPORTED;  // e.g. "unsupported": the query fails
   }
   return AMDSMI_STATUS_SUCCESS;
 }

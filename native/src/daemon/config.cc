@@ -183,8 +183,8 @@ std::string ValueOf(const FlagDef& d, Flags& f) {
 
 // A config-file value into a flag: the reference unmarshals the YAML into
 // typed Go fields (a string where a bool belongs is an error, and vice versa);
-// here a quoted "true"/"false" is also accepted for a bool and a quoted number
-// for an integer. null leaves the flag unset.
+// here a quoted "true"/"false" is also accepted for a bool, a quoted number
+// for an integer and a number for a string. null leaves the flag unset.
 Status AssignFile(const FlagDef& d, Flags& f, const FileValue& v, const std::string& key,
                   const std::string& origin) {
   if (v.type == 'n') return Status::Ok();
@@ -195,7 +195,9 @@ Status AssignFile(const FlagDef& d, Flags& f, const FileValue& v, const std::str
   };
   switch (d.kind) {
     case Kind::kString:
-      if (v.type != 's') return mismatch("string");
+      // Numbers are taken as their text (`devices: 0`); a YAML boolean is not
+      // (`on` would silently become "true").
+      if (v.type == 'b') return mismatch("string");
       break;
     case Kind::kBool:
       if (v.type != 'b' && v.type != 's') return mismatch("bool");

@@ -378,6 +378,13 @@ void Monitor::PollOnce() {
     counters_->ecc_reads_ok.fetch_add(1);
     counts += (counts.empty() ? "" : ",") + std::to_string(*ecc);
     GpuRecord r = ledger_->Get(keys_[g.index]);
+    if (!r.has_baseline) {  // unreadable when the monitor started: the first read is the baseline
+      r.has_baseline = true;
+      r.ecc_baseline = r.ecc_seen = *ecc;
+      ecc_baseline_[g.index] = *ecc;
+      ledger_->Put(keys_[g.index], r);
+      continue;
+    }
     if (*ecc < r.ecc_seen) {
       // The driver reset its RAS counters (GPU reset / driver reload): the
       // errors that failed the GPU are gone with the state they described.

@@ -262,3 +262,8 @@ def _write(scratch, body):
     with open(path, "w") as f:
         f.write(body)
     return path
+
+
+def test_numbers_are_accepted_for_string_settings(scratch):
+    f = effective_config(scratch, file_body="version: v1\nflags:\n  devices: 0\n  resourcePrefix: 1.5\n")
+    assert f["devices"] == "0" and f["resourcePrefix"] == "1.5"

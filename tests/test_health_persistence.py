@@ -317,3 +317,20 @@ def test_sighup_without_edits_keeps_the_state_file_verdicts(mk, scratch):
     n.wait_health(lambda h: h[ids[0]] == "Unhealthy")
     n.d.signal(signal.SIGHUP)
     assert n.first_law() == {ids[0]: "Unhealthy", ids[1]: "Healthy"}
+
+
+def test_ecc_unreadable_at_start_takes_the_first_read_as_baseline(mk):
+    """A GPU whose ECC count could not be read when the monitor started is not
+    failed by the first count that does read."""
+    n = mk()
+    ecc = os.path.join(n.state, "gpu1.ecc")
+    with open(ecc, "w") as f:
+        f.write("unsupported\n")  # the mock fails the query
+    ids = sorted(n.start())
+    n.d.wait_log("health monitor watching")
+    n.set_ecc(1, 5)
+    time.sleep(0.5)
+    assert n.q.empty(), "first readable ECC count treated as a rise"
+    n.set_ecc(1, 6)
+    n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+    assert "rose to 6 (baseline 5)" in n.d.log()
