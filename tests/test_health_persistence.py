@@ -46,7 +46,12 @@ class Node:
     def start(self):
         self.d = harness.Daemon(self.scratch, self.fx, args=self.args, env=self.env, event_fifo=self.fifo,
                                 state_dir=self.state).start()
-        return self.first_law()
+        law = self.first_law()
+        # The monitor takes its ECC baselines after registration: fault injection
+        # before that would become the baseline.
+        disabled = self.env.get("DP_DISABLE_HEALTHCHECKS", "").lower() in ("all", "xids")
+        self.d.wait_log("health checks disabled" if disabled else "health monitor watching")
+        return law
 
     def first_law(self, timeout=10):
         reg = self.k.wait_registration(timeout)
