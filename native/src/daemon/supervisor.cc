@@ -108,7 +108,8 @@ int DryRun(smi::Library* lib, const Validated& v, const Config& cfg) {
     out += (i ? ", " : "") + std::string("{\"index\": ") + std::to_string(g.node_index) + ", \"uuid\": \"" +
            JsonEscape(g.uuid) + "\", \"bdf\": \"" + g.bdf + "\", \"mode\": \"" + g.compute_mode + "/" +
            g.memory_mode + "\", \"partitions\": " + std::to_string(g.partitions.size()) +
-           ", \"vram_mib\": " + std::to_string(g.vram_mib) + ", \"numa\": " + std::to_string(g.numa) +
+           ", \"vram_mib\": " + std::to_string(g.vram_mib) + ", \"vram_source\": \"" + g.vram_source +
+           "\", \"profile\": \"" + JsonEscape(g.PartitionProfile()) + "\", \"numa\": " + std::to_string(g.numa) +
            ", \"xcds\": " + std::to_string(g.xcds) + ", \"cus\": " + std::to_string(g.cus) + "}";
   }
   out += "], \"labels\": {";

@@ -63,10 +63,12 @@ def test_every_shape_gives_the_same_resources(scratch, vram, ranges, profile, se
     rep = json.loads(r.stdout)
     assert len(rep["gpus"]) == 8
     assert all(g["partitions"] == 8 and g["vram_mib"] == 294896 for g in rep["gpus"]), rep["gpus"]
+    assert all(g["profile"] == "cpx-1xcd.36gb" for g in rep["gpus"])
     res = {x["resource"]: (x["devices"], x["allocatable"]) for x in rep["resources"]}
     assert res == {"amd.com/gpu-mem-gb": (64, 64 * 36)}, res
     want_source = "memory-partition-config" if ranges else vram
     assert r.stderr.count(f"vram=294896 MiB ({want_source}) mode=CPX/NPS2") == 8, r.stderr
+    assert {g["vram_source"] for g in rep["gpus"]} == {want_source}
 
 
 def test_profile_name_without_renaming(scratch):
