@@ -801,8 +801,47 @@ static void TestYaml() {
   for (const char* r : bad) CHECK(!adp::yaml::ParseSubset(r).ok());
 }
 
+// Random mutations of valid config documents: ParseConfigFile (libyaml and the
+// subset parser) must return a Status, never crash or hang (run under ASan).
+static void TestConfigFuzz() {
+  const char* seeds[] = {
+      "version: v1\nflags:\n  migStrategy: single\n  failOnInitError: false\n",
+      "version: v1\nflags: {migStrategy: mixed, resourceConfig: 'gpu:a:2', serverThreads: 4}\n",
+      "version: v1\nd: &d {deviceIDStrategy: index}\nflags:\n  <<: *d\n  resourceConfig: >-\n    gpu:a:2,\n    gpu:b:3\n",
+      "{\"version\": \"v1\", \"flags\": {\"passDeviceSpecs\": false, \"devices\": \"0,1\"}}\n",
+  };
+  const char alphabet[] = "{}[]:,-&*!|>'\"#\n \t?%@`<~.0123456789abcxyzv";
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  auto rnd = [&x]() {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    return x;
+  };
+  int ok = 0, failed = 0;
+  for (int i = 0; i < 20000; ++i) {
+    std::string doc = seeds[rnd() % 4];
+    int edits = 1 + static_cast<int>(rnd() % 6);
+    for (int e = 0; e < edits && !doc.empty(); ++e) {
+      size_t pos = rnd() % (doc.size() + 1);
+      switch (rnd() % 4) {
+        case 0: doc.insert(pos, 1, alphabet[rnd() % (sizeof(alphabet) - 1)]); break;
+        case 1: if (pos < doc.size()) doc.erase(pos, 1 + rnd() % 4); break;
+        case 2: if (pos < doc.size()) doc[pos] = alphabet[rnd() % (sizeof(alphabet) - 1)]; break;
+        case 3: doc.insert(pos, doc.substr(rnd() % doc.size(), rnd() % 12)); break;
+      }
+    }
+    auto r = adp::daemon::ParseConfigFile(doc);
+    (r.ok() ? ok : failed)++;
+    auto sub = adp::yaml::ParseSubset(doc);
+    (void)sub;
+  }
+  CHECK(ok > 0 && failed > 0);
+}
+
 int main() {
   TestYaml();
+  TestConfigFuzz();
   TestReplicaCuRanges();
   TestPodResources();
   TestMetrics();
