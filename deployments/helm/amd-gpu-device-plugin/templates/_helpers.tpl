@@ -20,7 +20,7 @@
 {{- define "amdgpu-dp.selectorLabels" -}}
 {{- if .Values.selectorLabelsOverride }}
 {{- toYaml .Values.selectorLabelsOverride }}
-{{- else }}
+{{- else -}}
 app.kubernetes.io/name: {{ include "amdgpu-dp.name" . }}
 app.kubernetes.io/instance: {{ .Release.Name }}
 {{- end }}

@@ -1,0 +1,144 @@
+"""The helm chart, rendered: valid Kubernetes objects for every values combination.
+
+No helm binary exists in the image, so tools/helm_render.py implements the Go
+template + sprig subset the chart uses; these tests render the chart with the
+default values and with each feature switch, parse the output as YAML and
+check the DaemonSet: env names the daemon understands, every volumeMount backed
+by a volume, health state / metrics / NFD / reference value names wired up.
+
+Parity: the reference chart (deployments/helm/nvidia-device-plugin/templates/
+daemonset.yml:15-106) renders the same DaemonSet shape from the same keys.
+"""
+
+import os
+import subprocess
+import sys
+
+import pytest
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import helm_render  # noqa: E402
+
+from k8s_gpu_sharing_plugin_amd import DAEMON  # noqa: E402
+
+
+def daemon_envs():
+    text = subprocess.run([DAEMON, "--help"], capture_output=True, text=True, check=True).stdout
+    names = set()
+    for tok in text.replace("(", " ").replace(",", " ").replace(")", " ").split():
+        if tok.isupper() and "_" in tok:
+            names.add(tok)
+    # environment-only settings documented in docs/USER_GUIDE.md
+    return names | {"DP_DISABLE_HEALTHCHECKS", "DP_HEALTH_POLL_MS", "ADP_LOG_LEVEL", "ADP_LOG_FORMAT"}
+
+
+def daemonset(values=None):
+    out = helm_render.render(values)
+    docs = [d for d in yaml.safe_load_all(out["daemonset.yaml"]) if d]
+    assert len(docs) == 1
+    return docs[0]
+
+
+def container(ds):
+    return ds["spec"]["template"]["spec"]["containers"][0]
+
+
+def env(ds):
+    return {e["name"]: e.get("value") for e in container(ds)["env"]}
+
+
+def check_consistent(ds):
+    spec = ds["spec"]["template"]["spec"]
+    vols = {v["name"] for v in spec["volumes"]}
+    mounts = {m["name"] for m in container(ds)["volumeMounts"]}
+    assert mounts <= vols, mounts - vols
+    assert set(env(ds)) <= daemon_envs(), set(env(ds)) - daemon_envs()
+    assert spec["priorityClassName"] == "system-node-critical"
+    labels = ds["spec"]["template"]["metadata"]["labels"]
+    if ds["apiVersion"] == "apps/v1":
+        assert ds["spec"]["selector"]["matchLabels"].items() <= labels.items()
+
+
+def test_defaults_render_a_valid_daemonset():
+    ds = daemonset()
+    check_consistent(ds)
+    assert ds["apiVersion"] == "apps/v1" and ds["kind"] == "DaemonSet"
+    assert ds["metadata"]["name"] == "amdgpu-amd-gpu-device-plugin"
+    e = env(ds)
+    assert e["PARTITION_STRATEGY"] == "none" and e["RESOURCE_CONFIG"] == "gpu:gpu-mem-gb:-1"
+    assert e["REPLICA_POLICY"] == "pack" and e["FAIL_ON_INIT_ERROR"] == "true"
+    # health state on by default: env + hostPath volume
+    assert e["DP_HEALTH_STATE_FILE"] == "/var/lib/amdgpu-device-plugin/health.state"
+    vol = {v["name"]: v for v in ds["spec"]["template"]["spec"]["volumes"]}["health-state"]
+    assert vol["hostPath"] == {"path": "/var/lib/amdgpu-device-plugin", "type": "DirectoryOrCreate"}
+    assert container(ds)["image"] == "amdgpu-device-plugin:0.1.0"
+    sc = container(ds)["securityContext"]
+    assert sc["allowPrivilegeEscalation"] is False and sc["capabilities"]["drop"] == ["ALL"]
+    assert "livenessProbe" not in container(ds)
+
+
+def test_health_state_can_be_turned_off():
+    ds = daemonset({"healthState": {"enabled": False}, "rejectUnhealthy": True})
+    check_consistent(ds)
+    assert "DP_HEALTH_STATE_FILE" not in env(ds)
+    assert env(ds)["DP_REJECT_UNHEALTHY"] == "true"
+    assert "health-state" not in {v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]}
+
+
+def test_metrics_and_node_feature_labels():
+    ds = daemonset({"metrics": {"enabled": True, "port": 9500}, "nodeFeatureLabels": {"enabled": True}})
+    check_consistent(ds)
+    c = container(ds)
+    assert env(ds)["DP_METRICS_ADDR"] == ":9500" and env(ds)["DP_NODE_LABELS_FILE"]
+    assert c["ports"] == [{"name": "metrics", "containerPort": 9500, "protocol": "TCP"}]
+    assert c["livenessProbe"]["httpGet"] == {"path": "/healthz", "port": "metrics"}
+    ann = ds["spec"]["template"]["metadata"]["annotations"]
+    assert ann["prometheus.io/scrape"] == "true" and ann["prometheus.io/port"] == "9500"
+    vols = {v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]}
+    assert {"pod-resources", "nfd-features"} <= vols
+
+
+def test_reference_value_names_win():
+    """A reference values file: migStrategy / nvidiaDriverRoot, compatWithCPUManager."""
+    ds = daemonset({"migStrategy": "mixed", "nvidiaDriverRoot": "/run/amd", "compatWithCPUManager": True,
+                    "passDeviceSpecs": False})
+    check_consistent(ds)
+    e = env(ds)
+    assert e["PARTITION_STRATEGY"] == "mixed" and e["DRIVER_ROOT"] == "/run/amd"
+    assert e["PASS_DEVICE_SPECS"] == "true"  # compat mode always passes device specs
+    assert container(ds)["securityContext"] == {"privileged": True}
+
+
+def test_legacy_api_and_overrides():
+    ds = daemonset({"legacyDaemonsetAPI": True, "fullnameOverride": "gpu-plugin",
+                    "image": {"tag": "v9"}, "devices": "0,1", "disableHealthChecks": "all",
+                    "extraEnv": [{"name": "ADP_LOG_LEVEL", "value": "debug"}],
+                    "selectorLabelsOverride": {"app": "gpu"}, "runtimeClassName": "amd"})
+    check_consistent(ds)
+    assert ds["apiVersion"] == "extensions/v1beta1" and "selector" not in ds["spec"]
+    assert ds["metadata"]["name"] == "gpu-plugin"
+    assert container(ds)["image"] == "amdgpu-device-plugin:v9"
+    e = env(ds)
+    assert e["AMD_DP_DEVICES"] == "0,1" and e["DP_DISABLE_HEALTHCHECKS"] == "all" and e["ADP_LOG_LEVEL"] == "debug"
+    assert ds["spec"]["template"]["metadata"]["labels"] == {"app": "gpu"}
+    assert ds["spec"]["template"]["spec"]["runtimeClassName"] == "amd"
+
+
+@pytest.mark.parametrize("strategy", ["none", "single", "mixed"])
+def test_partition_strategies(strategy):
+    ds = daemonset({"partitionStrategy": strategy, "resourceConfig": "", "replicaCuMask": True})
+    check_consistent(ds)
+    assert env(ds)["PARTITION_STRATEGY"] == strategy
+    assert "RESOURCE_CONFIG" not in env(ds) and env(ds)["REPLICA_CU_MASK"] == "true"
+
+
+def test_renderer_trims_and_pipes_like_go_templates():
+    r = helm_render.Renderer({"a": {"b": ""}, "n": 0, "s": "x+y"}, {}, {"Name": "rel"})
+    nodes = r.load('{{- define "t" -}} [{{ . | quote }}] {{- end }}'
+                   'A {{- .Values.a.b | default "d" | quote }} {{ include "t" "v" }}\n'
+                   '{{- if .Values.n }}no{{ else if .Values.s }} {{ .Values.s | replace "+" "_" }}{{ end }}'
+                   '{{ $x := printf "%s-%s" .Release.Name "c" }}{{ $x | trunc 4 }}{{/* c */}}')
+    assert r.render_nodes(nodes, r.root, {}) == 'A"d" ["v"] x_yrel-'
