@@ -54,6 +54,7 @@ Result<std::unique_ptr<ChurnClient>> ChurnClient::Open(const std::string& socket
   auto ch = grpc::Channel::Dial(socket, opt.timeout_ms);
   if (!ch.ok()) return ch.status();
   c->ch_ = std::move(*ch);
+  c->ch_->EmulateGrpcGo(opt.grpc_go);
   auto sid = c->ch_->StartStream("/v1beta1.DevicePlugin/ListAndWatch", "");
   if (!sid.ok()) return sid.status();
   std::string msg;
@@ -107,6 +108,7 @@ Status ChurnClient::Run(int pods, bool record) {
       auto a0 = Clock::now();
       ADP_RETURN_IF_ERROR(ch_->Unary("/v1beta1.DevicePlugin/GetPreferredAllocation", req, &resp, opt_.timeout_ms));
       auto a1 = Clock::now();
+      ADP_RETURN_IF_ERROR(ch_->SendBdpPing());
       pb::PreferredAllocationResponse prr;
       ADP_RETURN_IF_ERROR(pb::Decode(resp, &prr));
       if (!prr.container_responses.empty()) chosen = std::move(prr.container_responses[0]);
@@ -125,6 +127,7 @@ Status ChurnClient::Run(int pods, bool record) {
     auto a0 = Clock::now();
     ADP_RETURN_IF_ERROR(ch_->Unary("/v1beta1.DevicePlugin/Allocate", req, &resp, opt_.timeout_ms));
     auto a1 = Clock::now();
+    ADP_RETURN_IF_ERROR(ch_->SendBdpPing());
     pb::AllocateResponse arr;
     ADP_RETURN_IF_ERROR(pb::Decode(resp, &arr));
     if (arr.container_responses.size() != 1 || arr.container_responses[0].devices.empty())
@@ -143,12 +146,14 @@ Status ChurnClient::Run(int pods, bool record) {
 }
 
 std::string ChurnClient::StatsJson() const {
-  char head[320];
+  char head[400];
   snprintf(head, sizeof(head),
            "{\"rank\": %d, \"world\": %d, \"advertised\": %zu, \"allocatable\": %zu, \"rank_devices\": %zu, "
-           "\"pod_size\": %d, \"pods\": %zu, \"seconds\": %.6f, \"pods_per_s\": %.1f, ",
+           "\"pod_size\": %d, \"pods\": %zu, \"seconds\": %.6f, \"pods_per_s\": %.1f, "
+           "\"client\": \"%s\", \"bdp_pings\": %llu, ",
            opt_.rank, opt_.world, advertised_, allocatable_, mine_, opt_.pod_size, run_pods_, run_seconds_,
-           run_seconds_ > 0 ? run_pods_ / run_seconds_ : 0.0);
+           run_seconds_ > 0 ? run_pods_ / run_seconds_ : 0.0, opt_.grpc_go ? "grpc-go" : "native",
+           static_cast<unsigned long long>(ch_->bdp_pings_sent()));
   std::string ids = "\"device_ids\": [";
   for (size_t i = 0; i < mine_ids_.size() && i < 64; ++i)
     ids += (i ? ", \"" : "\"") + JsonEscape(mine_ids_[i]) + "\"";

@@ -24,6 +24,7 @@ struct ChurnOptions {
   int rank = 0;   // this client churns devices i with i % world == rank
   int world = 1;
   int timeout_ms = 5000;
+  bool grpc_go = false;  // kubelet (grpc-go) client frame pattern, grpc::Channel::EmulateGrpcGo
 };
 
 struct LatencyStats {

@@ -230,7 +230,7 @@ char* adp_proto_roundtrip(const char* type, const unsigned char* bytes, size_t l
 
 extern "C" {
 
-// {"socket": "...", "pod_size": 1, "rank": 0, "world": 1, "preferred": true} -> handle or null
+// {"socket": "...", "pod_size": 1, "rank": 0, "world": 1, "preferred": true, "grpc_go": false} -> handle or null
 void* adp_bench_open(const char* in, char** err) {
   try {
     json j = json::parse(in);
@@ -239,6 +239,7 @@ void* adp_bench_open(const char* in, char** err) {
     o.rank = j.value("rank", 0);
     o.world = j.value("world", 1);
     o.preferred = j.value("preferred", true);
+    o.grpc_go = j.value("grpc_go", false);
     auto c = adp::bench::ChurnClient::Open(j["socket"].get<std::string>(), o);
     if (!c.ok()) {
       *err = Dup(c.status().ToString());

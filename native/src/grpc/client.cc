@@ -72,6 +72,9 @@ struct ChannelCallbacks {
   static int OnData(nghttp2_session*, uint8_t, int32_t sid, const uint8_t* data, size_t len,
                     void* ud) {
     auto* ch = static_cast<Channel*>(ud);
+    // grpc-go's bdpEstimator.add(): the first DATA after the last ping's ACK
+    // starts a new sample (written by SendBdpPing()).
+    if (ch->grpc_go_ && !ch->bdp_outstanding_) ch->bdp_due_ = true;
     Channel::CallState* c = Find(ch, sid);
     if (!c) return 0;
     c->buf.append(reinterpret_cast<const char*>(data), len);
@@ -90,6 +93,7 @@ struct ChannelCallbacks {
     if (frame->hd.type == NGHTTP2_SETTINGS && !(frame->hd.flags & NGHTTP2_FLAG_ACK))
       ch->got_settings_ = true;
     if (frame->hd.type == NGHTTP2_GOAWAY) ch->dead_ = true;
+    if (frame->hd.type == NGHTTP2_PING && (frame->hd.flags & NGHTTP2_FLAG_ACK)) ch->bdp_outstanding_ = false;
     return 0;
   }
   static int OnStreamClose(nghttp2_session*, int32_t sid, uint32_t code, void* ud) {
@@ -244,6 +248,17 @@ Status Channel::WaitFor(const std::function<bool()>& done, int timeout_ms) {
   return Status::Ok();
 }
 
+Status Channel::SendBdpPing() {
+  if (!bdp_due_ || dead_) return Status::Ok();
+  static const uint8_t kBdpPayload[8] = {2, 4, 16, 16, 9, 14, 7, 7};  // grpc-go's bdpPing data
+  bdp_due_ = false;
+  if (nghttp2_submit_ping(static_cast<nghttp2_session*>(session_), NGHTTP2_FLAG_NONE, kBdpPayload) != 0)
+    return Internal("nghttp2_submit_ping failed");
+  bdp_outstanding_ = true;
+  ++bdp_pings_;
+  return Flush();
+}
+
 Result<int32_t> Channel::Submit(const std::string& path, std::string_view request) {
   if (dead_) return Unavailable("connection closed");
   auto call = std::make_unique<CallState>();
@@ -252,7 +267,7 @@ Result<int32_t> Channel::Submit(const std::string& path, std::string_view reques
       Nv(":method", "POST"),       Nv(":scheme", "http"),
       Nv(":path", path.c_str()),   Nv(":authority", "localhost"),
       Nv("content-type", "application/grpc"), Nv("te", "trailers"),
-      Nv("user-agent", "amdgpu-dp-grpc/1.0"),
+      Nv("user-agent", grpc_go_ ? "grpc-go/1.65.0" : "amdgpu-dp-grpc/1.0"),
   };
   nghttp2_data_provider prd;
   prd.source.ptr = nullptr;

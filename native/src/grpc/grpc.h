@@ -198,6 +198,18 @@ class Channel {
   Status Pump(int timeout_ms);
   bool alive() const;
 
+  // Client frame pattern of the kubelet's grpc-go transport (BDP estimation on,
+  // the default for a kubelet dial): a PING with an 8-byte payload after the
+  // first DATA frame received while no such ping is outstanding -- i.e. about
+  // one per sequential unary call -- and a grpc-go user-agent. grpc-go's loopy
+  // writer goroutine writes that ping on its own while the application already
+  // has its response, so here the caller writes it with SendBdpPing() after the
+  // call returns (its own write, outside a timed call). Reference peer: the
+  // kubelet's grpc-go client of cmd/nvidia-device-plugin/server.go:168-240.
+  void EmulateGrpcGo(bool on) { grpc_go_ = on; }
+  Status SendBdpPing();
+  uint64_t bdp_pings_sent() const { return bdp_pings_; }
+
  private:
   struct CallState;
   Channel() = default;
@@ -209,6 +221,10 @@ class Channel {
   void* session_ = nullptr;  // nghttp2_session*
   bool dead_ = false;
   bool got_settings_ = false;
+  bool grpc_go_ = false;
+  bool bdp_outstanding_ = false;
+  bool bdp_due_ = false;
+  uint64_t bdp_pings_ = 0;
   std::string wbuf_;  // frames gathered by Flush() for one write
   std::map<int32_t, std::unique_ptr<CallState>> calls_;
   friend struct ChannelCallbacks;

@@ -31,6 +31,10 @@ def test_bench_single_process_contract():
     assert res["per_rank"][0]["allocate"]["n"] == 300
     assert res["rccl_world"] == 1 and res["backend"] == "none"
     assert res["per_rank"][0]["admitted_bdfs"] == ["0000:0c:00.0"]  # GPU 0 of the node model
+    # the kubelet's grpc-go frame pattern: a BDP PING after (about) every response
+    gg = res["per_rank"][0]["grpc_go_shaped"]
+    assert gg["allocate"]["n"] == 300 and gg["bdp_pings"] >= gg["pods"]
+    assert res["grpc_go_shaped_allocate_p50_us"] == gg["allocate"]["p50_us"] > 0
 
 
 @pytest.mark.slow
@@ -51,6 +55,8 @@ def test_bench_two_ranks_gloo():
     # an independent gRPC stack (grpcio) per rank, max over ranks at the top
     per = [p["grpcio_allocate_p50_us"] for p in res["per_rank"]]
     assert all(v and v > 0 for v in per) and res["grpcio_client_allocate_p50_us"] == max(per)
+    gg = [p["grpc_go_shaped"]["allocate"]["p50_us"] for p in res["per_rank"]]
+    assert res["grpc_go_shaped_allocate_p50_us"] == max(gg)
 
 
 @pytest.mark.parametrize("config,advertised", [("timeslice4", 4), ("cpx-single", 8), ("auto-mem", 294),

@@ -55,7 +55,7 @@ step_bench() {
 step_configs() {
   for cfg in spx-none timeslice4 auto-mem; do
     timeout -k 10 300 python bench.py --steps 50 --warmup 5 --config $cfg > $out/bench_$cfg.json 2> $out/bench_$cfg.err || die "BENCH $cfg" $out/bench_$cfg.err
-    python -c "import json; d=json.load(open('$out/bench_$cfg.json')); print('$cfg', d['allocatable'], d['value'], d['allocate_p99_us'], d['preferred_p50_us'], d['server_allocate_handler_avg_us'], d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'])"
+    python -c "import json; d=json.load(open('$out/bench_$cfg.json')); print('$cfg', d['allocatable'], d['value'], d['allocate_p99_us'], d['preferred_p50_us'], d['server_allocate_handler_avg_us'], d.get('grpc_go_shaped_allocate_p50_us'), d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'])"
   done
 }
 step_health() {
@@ -119,7 +119,7 @@ step_floor() {
 step_spread() {
   for i in $(seq 1 10); do
     timeout -k 10 300 python bench.py --no-probe > $out/spread_$i.json 2> $out/spread_$i.err || die "SPREAD $i" $out/spread_$i.err
-    python -c "import json; d=json.load(open('$out/spread_$i.json')); print('R $i', d['value'], d['allocate_p99_us'], d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'])"
+    python -c "import json; d=json.load(open('$out/spread_$i.json')); print('R $i', d['value'], d['allocate_p99_us'], d.get('grpc_go_shaped_allocate_p50_us'), d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'])"
   done
 }
 step_soak() {
