@@ -6,6 +6,22 @@ GPURUN     ?= /usr/local/graft/bin/gpurun
 
 .PHONY: all build probe test test-native test-gpu bench asan tsan tsan-e2e asan-e2e coverage lint image clean
 
+# Containerised targets (reference Makefile:44-74): `make docker-<target>` runs
+# `make <target>` in the development image built from docker/Dockerfile.devel.
+DOCKER        ?= docker
+ROCM_VERSION  ?= 7.2
+BUILDIMAGE    ?= amdgpu-device-plugin-build:rocm$(ROCM_VERSION)
+DOCKER_TARGETS := $(patsubst %,docker-%,build test test-native lint asan tsan asan-e2e tsan-e2e coverage)
+.PHONY: .build-image $(DOCKER_TARGETS)
+.build-image: docker/Dockerfile.devel
+	if [ -z "$(SKIP_IMAGE_BUILD)" ]; then \
+	  $(DOCKER) build --build-arg ROCM_VERSION=$(ROCM_VERSION) --tag $(BUILDIMAGE) -f $< docker; \
+	fi
+$(DOCKER_TARGETS): docker-%: .build-image
+	@echo "Running 'make $(*)' in docker container $(BUILDIMAGE)"
+	$(DOCKER) run --rm -v $(CURDIR):$(CURDIR) -w $(CURDIR) --user $$(id -u):$$(id -g) \
+	  -e HOME=/tmp $(BUILDIMAGE) make $(*)
+
 all: build
 
 build:

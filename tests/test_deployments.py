@@ -116,3 +116,17 @@ def test_helm_template_accepts_reference_value_names():
         text = f.read()
     assert "coalesce .Values.migStrategy .Values.partitionStrategy" in text
     assert "coalesce .Values.nvidiaDriverRoot .Values.driverRoot" in text
+
+
+def test_dev_image_and_docker_targets():
+    """B02: the development image carries the build/test toolchain, and every
+    docker-<target> rule runs `make <target>` in it (reference Makefile:44-74)."""
+    text = open(os.path.join(ROOT, "docker", "Dockerfile.devel")).read()
+    for pkg in ("cmake", "ninja-build", "libnghttp2-dev", "libyaml-dev", "amd-smi-lib", "pytest", "grpcio"):
+        assert pkg in text, pkg
+    for target in ("build", "test", "lint", "asan", "tsan", "coverage"):
+        r = subprocess.run(["make", "-n", f"docker-{target}", "SKIP_IMAGE_BUILD=1", "DOCKER=docker"], cwd=ROOT,
+                           capture_output=True, text=True, timeout=30)
+        assert r.returncode == 0, r.stderr
+        run = [ln for ln in r.stdout.splitlines() if "docker run" in ln or "make " + target in ln]
+        assert run and run[-1].rstrip().endswith(f"make {target}"), r.stdout
