@@ -203,6 +203,8 @@ Result<Prioritized> PrioritizeDeviceViews(const std::vector<std::string_view>& a
   }
 
   Prioritized out;
+  out.devices.reserve(pools.size());
+  for (const auto& p : pools) out.devices.emplace_back(p.prefix);
   if (policy == ReplicaPolicy::kSpread) {
     for (int i = static_cast<int>(chosen.size()); i < allocation_size; ++i) {
       // First priority: a physical device not yet used by this request; second:

@@ -46,6 +46,10 @@ bool ParseReplicaPolicy(std::string_view s, ReplicaPolicy* out);
 
 struct Prioritized {
   std::vector<std::string> ids;  // sorted
+  // The physical devices the available IDs name (replica suffix stripped), in
+  // first-seen order: callers check them against their device table, as the
+  // reference does with gpuallocator.NewDevicesFrom (server.go:274-278).
+  std::vector<std::string> devices;
   // True when more than one replica of the same physical device was chosen in
   // spread mode (the reference's NonUniqueError, which the caller only logs).
   bool non_unique = false;

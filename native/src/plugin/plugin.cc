@@ -457,6 +457,27 @@ Status Plugin::PreferredImpl(std::string_view req, std::string* resp) {
       auto res = alloc::PrioritizeDeviceViews(cr.available, cr.must_include, cr.allocation_size,
                                               opts_.replica_policy, alloc::kReplicaJoin, &affinity);
       if (!res.ok()) return res.status();
+      // Physical devices must be ours (reference: NewDevicesFrom fails on an
+      // unknown UUID, server.go:274-278) -- one lookup per device, not per
+      // replica -- and so must every ID handed back.
+      for (const auto& dev : res->devices)
+        if (!unit_index_by_id_.count(dev))
+          return InvalidArgument("unable to retrieve list of available devices: unknown device " + dev);
+      for (size_t i = 0; i < res->ids.size(); ++i) {
+        if (!advertised_index_.count(res->ids[i]))
+          return InvalidArgument("unable to retrieve list of available devices: unknown device " + res->ids[i]);
+        if (i && res->ids[i] == res->ids[i - 1]) {
+          // An ID listed twice in availableDeviceIDs was chosen twice: choose
+          // again from the de-duplicated list (off the common path).
+          std::vector<std::string_view> avail(cr.available.begin(), cr.available.end());
+          std::sort(avail.begin(), avail.end());
+          avail.erase(std::unique(avail.begin(), avail.end()), avail.end());
+          res = alloc::PrioritizeDeviceViews(avail, cr.must_include, cr.allocation_size, opts_.replica_policy,
+                                             alloc::kReplicaJoin, &affinity);
+          if (!res.ok()) return res.status();
+          break;
+        }
+      }
       if (res->non_unique) LOG_DEBUG(kComp, "ignoring: %s", alloc::kNonUniqueMessage);
       out.container_responses.push_back(std::move(res->ids));
       continue;

@@ -99,6 +99,21 @@ def test_replicated_resource_uses_prioritizer_and_advertised_ids(plugin):
     assert len({g.split("-replica-")[0] for g in got}) == 2  # spread over both GPUs
 
 
+def test_replicated_request_names_only_our_devices_and_no_id_twice(plugin):
+    """Replicated resources: a physical device we do not serve is an error (the
+    reference's NewDevicesFrom check, server.go:274-278), and an ID listed twice
+    in availableDeviceIDs is never handed back twice."""
+    c, ids = plugin(fixtures.node(2), args=["--resource-config", "gpu:gpu:3"])
+    with pytest.raises(grpc.RpcError) as e:
+        c.preferred(["x-replica-0"] + ids, size=1)
+    assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT and "unknown device x" in e.value.details()
+    with pytest.raises(grpc.RpcError) as e:  # our GPU, a replica number we never advertised
+        c.preferred([ids[0].rsplit("-replica-", 1)[0] + "-replica-99"], size=1)
+    assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+    got = pref(c, [ids[0], ids[0], ids[1]], size=2)
+    assert sorted(got) == sorted({ids[0], ids[1]})
+
+
 def test_pack_policy_over_the_wire(plugin):
     c, ids = plugin(fixtures.node(2), args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack"])
     assert len(ids) == 2 * (fixtures.MI355X_VRAM_MIB // 1000)
