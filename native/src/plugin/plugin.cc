@@ -198,6 +198,15 @@ void Plugin::BuildUnits() {
   healthy_.assign(units_.size(), 1);
   warned_law_.reset(new std::atomic<uint64_t>[units_.size()]());
   RebuildListAndWatch();
+  // grpc-go clients -- the kubelet's device manager dials without raising it --
+  // refuse messages above 4 MiB, so a larger device list never reaches the
+  // kubelet and the resource stays at 0 allocatable.
+  constexpr size_t kKubeletMaxRecv = 4u << 20;
+  if (law_bytes_size_.load() + 5 > kKubeletMaxRecv)
+    LOG_ERROR(kComp, "'%s': the ListAndWatch device list is %zu bytes (%zu IDs), above the 4 MiB a kubelet's gRPC "
+              "client accepts; the kubelet will not see these devices. Lower the replica count (resource-config) "
+              "or raise the memory unit (--auto-replica-unit-mib)", spec_.resource_name.c_str(),
+              law_bytes_size_.load(), advertised_.size());
 }
 
 void Plugin::RebuildListAndWatch() {

@@ -104,10 +104,32 @@ std::string PartitionInvalidReason(const inventory::PhysicalGpu& g) {
   return "";
 }
 
+namespace {
+Result<std::vector<PluginSpec>> BuildSpecs(const inventory::Snapshot& snap, PartitionStrategy strategy,
+                                           const ResourceConfig& rc, const std::string& prefix);
+}  // namespace
+
 Result<std::vector<PluginSpec>> BuildPluginSpecs(const inventory::Snapshot& snap,
                                                  PartitionStrategy strategy,
                                                  const ResourceConfig& rc,
                                                  const std::string& prefix) {
+  auto specs = BuildSpecs(snap, strategy, rc, prefix);
+  if (!specs.ok()) return specs;
+  // An entry keyed by something that is neither "gpu" nor a partition profile
+  // present on this node renames nothing (typo, or a profile of another node).
+  std::set<std::string> known = {"gpu"};
+  for (const auto& g : snap.gpus)
+    if (g.partitioned()) known.insert(g.PartitionProfile());
+  for (const auto& [orig, v] : rc.entries())
+    if (!known.count(orig))
+      LOG_WARN(kComp, "resource-config entry '%s:%s' matches no resource on this node (known: %s)", orig.c_str(),
+               v.name.c_str(), Join(std::vector<std::string>(known.begin(), known.end()), ", ").c_str());
+  return specs;
+}
+
+namespace {
+Result<std::vector<PluginSpec>> BuildSpecs(const inventory::Snapshot& snap, PartitionStrategy strategy,
+                                           const ResourceConfig& rc, const std::string& prefix) {
   auto full_gpu_plugin = [&](bool skip_partitioned) {
     PluginSpec s;
     s.original = "gpu";
@@ -134,7 +156,7 @@ Result<std::vector<PluginSpec>> BuildPluginSpecs(const inventory::Snapshot& snap
       for (const auto& g : snap.gpus) (g.partitioned() ? parted : whole).push_back(&g);
       if (parted.empty()) {
         LOG_INFO(kComp, "no partitioned GPUs found; falling back to partitionStrategy=none");
-        return BuildPluginSpecs(snap, PartitionStrategy::kNone, rc, prefix);
+        return BuildSpecs(snap, PartitionStrategy::kNone, rc, prefix);
       }
       if (!whole.empty())
         return FailedPrecondition(
@@ -189,5 +211,6 @@ Result<std::vector<PluginSpec>> BuildPluginSpecs(const inventory::Snapshot& snap
   }
   return InvalidArgument("unknown partition strategy");
 }
+}  // namespace
 
 }  // namespace adp::strategy

@@ -207,6 +207,26 @@ def test_dry_run_reports_allocatable(scratch):
     assert lab["amd.com/gpu.compute-partition"] == "mixed" and lab["amd.com/gpu.interconnect"] == "xgmi-full-mesh"
 
 
+@pytest.mark.parametrize("rc,needle", [
+    ("gpu:gpu:1,cpx-2xcd.72gb:half:1", "resource-config entry 'cpx-2xcd.72gb:half' matches no resource on this node"),
+    ("gpu:shared:40000", "above the 4 MiB a kubelet's gRPC client accepts"),
+])
+def test_dry_run_flags_config_that_cannot_work(scratch, rc, needle):
+    """A resource-config key that names no resource here (typo, another node's
+    profile) is warned about; a device list too big for the kubelet's gRPC
+    client (4 MiB receive limit) is an error in the log."""
+    fx = fixtures.write(fixtures.CONFIGS["mixed8"](), scratch + ".fixture")
+    env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB, AMDSMI_MOCK_FIXTURE=fx, ADP_LOG_LEVEL="warn")
+    r = subprocess.run([DAEMON, "--dry-run", "--partition-strategy", "mixed", "--resource-config", rc,
+                        "--device-plugin-path", scratch], capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0, r.stderr
+    assert needle in r.stdout + r.stderr
+    ok = subprocess.run([DAEMON, "--dry-run", "--partition-strategy", "mixed", "--resource-config",
+                         "gpu:gpu:4,cpx-1xcd.36gb:cpx:2", "--device-plugin-path", scratch],
+                        capture_output=True, text=True, timeout=60, env=env)
+    assert "matches no resource" not in ok.stdout + ok.stderr and "4 MiB" not in ok.stdout + ok.stderr
+
+
 def test_sigusr1_dumps_stats(scratch):
     k = kubelet.StubKubelet(sock(scratch)).start()
     d = harness.Daemon(scratch).start()
