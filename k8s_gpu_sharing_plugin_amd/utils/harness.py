@@ -17,7 +17,7 @@ from ..models import fixtures
 
 class Daemon:
     def __init__(self, plugin_dir: str, fixture: dict = None, args=(), env=None, real_smi=False,
-                 event_fifo: str = None, state_dir: str = None):
+                 event_fifo: str = None, state_dir: str = None, nofile: int = None):
         self.plugin_dir = plugin_dir
         self.args = list(args)
         self.env = dict(os.environ)
@@ -36,11 +36,18 @@ class Daemon:
         self.env.update(env or {})
         self.log_path = plugin_dir + ".daemon.log"
         self.proc = None
+        self.nofile = nofile  # RLIMIT_NOFILE for the daemon (descriptor exhaustion tests)
 
     def start(self):
         self._log = open(self.log_path, "w")
+        preexec = None
+        if self.nofile:
+            import resource
+            lim = self.nofile
+            preexec = lambda: resource.setrlimit(resource.RLIMIT_NOFILE, (lim, lim))  # noqa: E731
         self.proc = subprocess.Popen([DAEMON, "--device-plugin-path", self.plugin_dir, *self.args],
-                                     env=self.env, stdout=self._log, stderr=subprocess.STDOUT)
+                                     env=self.env, stdout=self._log, stderr=subprocess.STDOUT,
+                                     preexec_fn=preexec)
         return self
 
     def log(self) -> str:

@@ -98,6 +98,7 @@ using StreamHandler =
 
 struct ServerStats {
   std::atomic<uint64_t> connections{0};  // per accept: not on the call path
+  std::atomic<uint64_t> shed_connections{0};  // refused for lack of file descriptors
   metrics::Counter calls;                // per call, from every loop: sharded
   metrics::Counter errors;
 };
@@ -166,6 +167,7 @@ class Server {
   std::map<std::string, UnaryHandler, std::less<>> unary_;
   std::map<std::string, StreamHandler, std::less<>> streams_;
   int listen_fd_ = -1;
+  int spare_fd_ = -1;  // reserve descriptor for shedding connections at EMFILE
   std::vector<std::unique_ptr<Loop>> loops_;
   std::atomic<unsigned> next_loop_{0};
   std::atomic<bool> stopping_{false};

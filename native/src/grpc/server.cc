@@ -513,6 +513,9 @@ Status Server::Listen(const std::string& socket_path) {
     listen_fd_ = -1;
     return s;
   }
+  // Held in reserve for AcceptAll(): with no descriptor left, a pending
+  // connection keeps the (level-triggered) listener readable forever.
+  if (spare_fd_ < 0) spare_fd_ = open("/dev/null", O_RDONLY | O_CLOEXEC);
   return Status::Ok();
 }
 
@@ -546,6 +549,10 @@ void Server::Stop() {
     l->conns.clear();  // loops are gone; safe to tear down here
     std::lock_guard<std::mutex> lk(l->post_mu);
     l->posted.clear();
+  }
+  if (spare_fd_ >= 0) {
+    close(spare_fd_);
+    spare_fd_ = -1;
   }
   if (listen_fd_ >= 0) {
     close(listen_fd_);
@@ -696,7 +703,21 @@ void Server::AcceptAll() {
     int fd = accept4(listen_fd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
     if (fd < 0) {
       if (errno == EINTR) continue;
-      return;  // EAGAIN or transient (EMFILE...): retry on next readiness
+      if ((errno == EMFILE || errno == ENFILE) && spare_fd_ >= 0) {
+        // Out of descriptors: the listener would stay readable and the loop
+        // would spin on it. Free the reserve, accept the connection and close
+        // it (the client sees a reset and retries), then take the reserve back.
+        close(spare_fd_);
+        int shed = accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
+        if (shed >= 0) close(shed);
+        spare_fd_ = open("/dev/null", O_RDONLY | O_CLOEXEC);
+        uint64_t n = stats_.shed_connections.fetch_add(1, std::memory_order_relaxed);
+        if ((n & (n + 1)) == 0)  // 1st, 2nd, 4th, 8th ... time
+          LOG_WARN(kComp, "'%s': out of file descriptors; refused connection #%llu (raise the open-files limit)",
+                   name_.c_str(), static_cast<unsigned long long>(n + 1));
+        if (shed >= 0) continue;
+      }
+      return;  // EAGAIN or transient: retry on next readiness
     }
     Loop& target = *loops_[next_loop_.fetch_add(1, std::memory_order_relaxed) % loops_.size()];
     if (&target == loops_[0].get()) {

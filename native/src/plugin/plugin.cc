@@ -870,15 +870,19 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
             static_cast<double>(n));
     }
   }
-  struct Conn { const Plugin* p; uint64_t connections, errors; };
+  struct Conn { const Plugin* p; uint64_t connections, shed, errors; };
   std::vector<Conn> conns;
   for (auto* p : plugins) {
     std::lock_guard<std::mutex> lk(p->server_mu_);
     if (p->server_)
-      conns.push_back({p, p->server_->stats().connections.load(), p->server_->stats().errors.Value()});
+      conns.push_back({p, p->server_->stats().connections.load(), p->server_->stats().shed_connections.load(),
+                       p->server_->stats().errors.Value()});
   }
   family("amdgpu_dp_grpc_connections_total", "counter", "Accepted connections on the plugin socket.");
   for (auto& c : conns) gauge("amdgpu_dp_grpc_connections_total", res(c.p), static_cast<double>(c.connections));
+  family("amdgpu_dp_grpc_connections_shed_total", "counter",
+         "Connections closed on accept because the process was out of file descriptors.");
+  for (auto& c : conns) gauge("amdgpu_dp_grpc_connections_shed_total", res(c.p), static_cast<double>(c.shed));
   family("amdgpu_dp_grpc_errors_total", "counter", "RPCs answered with a non-OK gRPC status.");
   for (auto& c : conns) gauge("amdgpu_dp_grpc_errors_total", res(c.p), static_cast<double>(c.errors));
 }

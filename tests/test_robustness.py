@@ -137,3 +137,43 @@ def test_oversized_request_is_refused(plugin):
         raw(b"\x0a" + b"\xff" * (17 << 20), timeout=20)
     ch.close()
     _still_serving(dm, c, ids)
+
+
+def test_descriptor_exhaustion_sheds_connections_without_spinning(tmp_path):
+    """At the open-files limit the listener stays readable while connections
+    are pending; the daemon sheds them with a reserve descriptor (warning +
+    amdgpu_dp_grpc_connections_shed_total) instead of spinning on accept, and
+    serves normally once descriptors are free again."""
+    import time
+    d = str(tmp_path / "dp")
+    os.makedirs(d)
+    k = kubelet.StubKubelet(os.path.join(d, "kubelet.sock")).start()
+    dm = harness.Daemon(d, args=["--server-threads", "1"], nofile=64).start()
+    try:
+        reg = k.wait_registration()
+        path = os.path.join(d, reg.endpoint)
+        socks = []
+        for _ in range(120):
+            s = socket.socket(socket.AF_UNIX)
+            s.connect(path)
+            socks.append(s)
+
+        def cpu_s():
+            f = open(f"/proc/{dm.proc.pid}/stat").read().rsplit(")", 1)[1].split()
+            return (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
+        time.sleep(0.5)
+        c0 = cpu_s()
+        time.sleep(1.5)
+        assert cpu_s() - c0 < 0.5  # a spinning accept loop burns the whole 1.5 s
+        dm.wait_log("out of file descriptors; refused connection #1")
+        for s in socks:
+            s.close()
+        time.sleep(0.3)
+        c = kubelet.PluginClient(path)
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        assert len(c.allocate(ids[:1]).container_responses) == 1
+        c.close()
+        assert dm.proc.poll() is None
+    finally:
+        dm.stop()
+        k.stop()
