@@ -14,6 +14,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "common/log.h"
 #include "common/strings.h"
@@ -177,6 +178,7 @@ Status HttpServer::Start(const std::string& addr) {
   freeaddrinfo(res);
   if (listen_fd_ < 0) return st;
   stop_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  spare_fd_ = open("/dev/null", O_RDONLY | O_CLOEXEC);
   thread_ = std::thread([this] { Run(); });
   LOG_INFO(kComp, "serving /metrics and /healthz on port %d", port_);
   return Status::Ok();
@@ -191,42 +193,96 @@ void HttpServer::Stop() {
   }
   if (listen_fd_ >= 0) close(listen_fd_);
   if (stop_fd_ >= 0) close(stop_fd_);
-  listen_fd_ = stop_fd_ = -1;
+  if (spare_fd_ >= 0) close(spare_fd_);
+  listen_fd_ = stop_fd_ = spare_fd_ = -1;
 }
 
+// Connections are served concurrently from one poll loop, each with a 2 s
+// budget for the whole exchange: a slow or idle client (or many) cannot hold
+// up the kubelet-side liveness probe on /healthz. One request per connection
+// (a scraper on the node, not a general web server).
 void HttpServer::Run() {
+  using Clock = std::chrono::steady_clock;
+  constexpr size_t kMaxClients = 64;
+  struct Client {
+    int fd;
+    Clock::time_point deadline;
+    std::string in, out;
+    size_t off = 0;
+    bool responding = false;
+  };
+  std::vector<Client> cs;
+  std::vector<pollfd> p;
+  auto drop = [&](size_t i) {
+    close(cs[i].fd);
+    cs[i] = std::move(cs.back());
+    cs.pop_back();
+  };
   while (true) {
-    pollfd p[2] = {{listen_fd_, POLLIN, 0}, {stop_fd_, POLLIN, 0}};
-    if (poll(p, 2, -1) < 0) {
-      if (errno == EINTR) continue;
-      return;
+    p.clear();
+    p.push_back({stop_fd_, POLLIN, 0});
+    p.push_back({cs.size() < kMaxClients ? listen_fd_ : -1, POLLIN, 0});  // full: leave them in the backlog
+    int timeout = -1;
+    auto now = Clock::now();
+    for (const auto& c : cs) {
+      p.push_back({c.fd, static_cast<short>(c.responding ? POLLOUT : POLLIN), 0});
+      int ms = static_cast<int>(
+          std::max<long long>(0, std::chrono::duration_cast<std::chrono::milliseconds>(c.deadline - now).count()) + 1);
+      timeout = timeout < 0 ? ms : std::min(timeout, ms);
     }
-    if (p[1].revents) return;
-    int fd = accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK);
-    if (fd >= 0) {
-      Serve(fd);
-      close(fd);
+    if (poll(p.data(), p.size(), timeout) < 0) {
+      if (errno == EINTR) continue;
+      break;
+    }
+    if (p[0].revents) break;
+    // Clients first (their pollfds follow the two fixed entries, in order).
+    now = Clock::now();
+    for (size_t i = cs.size(); i-- > 0;) {
+      Client& c = cs[i];
+      short re = p[2 + i].revents;
+      bool done = false;
+      if (re && !c.responding) {
+        char buf[2048];
+        ssize_t n = read(c.fd, buf, sizeof(buf));
+        if (n > 0) c.in.append(buf, static_cast<size_t>(n));
+        if (n == 0 || (n < 0 && errno != EAGAIN && errno != EINTR)) {
+          done = true;
+        } else if (c.in.find("\r\n\r\n") != std::string::npos || c.in.size() >= 8192) {
+          c.out = Respond(c.in);
+          c.responding = true;
+        }
+      }
+      if (!done && c.responding && c.off < c.out.size()) {
+        ssize_t n = send(c.fd, c.out.data() + c.off, c.out.size() - c.off, MSG_NOSIGNAL);
+        if (n > 0) c.off += static_cast<size_t>(n);
+        else if (n < 0 && errno != EAGAIN && errno != EINTR) done = true;
+        if (c.off == c.out.size()) done = true;
+      }
+      if (done || now >= c.deadline) drop(i);
+    }
+    if (p[1].revents) {
+      while (cs.size() < kMaxClients) {
+        int fd = accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK);
+        if (fd >= 0) {
+          cs.push_back({fd, Clock::now() + std::chrono::seconds(2), {}, {}, 0, false});
+          continue;
+        }
+        if (errno == EINTR) continue;
+        if ((errno == EMFILE || errno == ENFILE) && spare_fd_ >= 0) {
+          close(spare_fd_);
+          int shed = accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
+          if (shed >= 0) close(shed);
+          spare_fd_ = open("/dev/null", O_RDONLY | O_CLOEXEC);
+          if (shed >= 0) continue;
+        }
+        break;
+      }
     }
   }
+  for (auto& c : cs) close(c.fd);
 }
 
-// One request per connection, 2 s budget for the whole exchange (a scraper on
-// the node, not a general web server).
-void HttpServer::Serve(int fd) {
-  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(2);
-  auto left_ms = [&] {
-    auto d = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now());
-    return static_cast<int>(std::max<long long>(0, d.count()));
-  };
-  std::string req;
-  char buf[2048];
-  while (req.find("\r\n\r\n") == std::string::npos && req.size() < 8192) {
-    pollfd p{fd, POLLIN, 0};
-    if (poll(&p, 1, left_ms()) <= 0) return;
-    ssize_t n = read(fd, buf, sizeof(buf));
-    if (n <= 0) return;
-    req.append(buf, static_cast<size_t>(n));
-  }
+std::string HttpServer::Respond(const std::string& req) {
   std::string line = req.substr(0, req.find("\r\n"));
   auto parts = Split(line, ' ');
   std::string status = "200 OK", type = "text/plain; version=0.0.4; charset=utf-8", body;
@@ -248,16 +304,7 @@ void HttpServer::Serve(int fd) {
   std::string resp = "HTTP/1.1 " + status + "\r\nContent-Type: " + type +
                      "\r\nContent-Length: " + std::to_string(body.size()) + "\r\nConnection: close\r\n\r\n";
   if (parts.empty() || parts[0] != "HEAD") resp += body;
-  size_t off = 0;
-  while (off < resp.size()) {
-    ssize_t n = send(fd, resp.data() + off, resp.size() - off, MSG_NOSIGNAL);
-    if (n > 0) { off += static_cast<size_t>(n); continue; }
-    if (n < 0 && errno == EAGAIN) {
-      pollfd p{fd, POLLOUT, 0};
-      if (poll(&p, 1, left_ms()) > 0) continue;
-    }
-    return;
-  }
+  return resp;
 }
 
 }  // namespace adp::metrics

@@ -87,11 +87,12 @@ class HttpServer {
 
  private:
   void Run();
-  void Serve(int fd);
+  std::string Respond(const std::string& request);
   Render render_;
   Healthy healthy_;
   int listen_fd_ = -1;
   int stop_fd_ = -1;
+  int spare_fd_ = -1;  // reserve descriptor: shed connections at EMFILE instead of spinning
   int port_ = 0;
   std::thread thread_;
 };

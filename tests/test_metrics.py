@@ -130,6 +130,27 @@ def test_metrics_follow_health_and_healthz(served):
     k2.stop()
 
 
+def test_slow_clients_do_not_hold_up_healthz(served):
+    """Idle / trickling HTTP clients each have their own 2 s budget and are
+    served side by side: the liveness probe on /healthz answers at once, and a
+    client that never finishes its request is closed at its deadline."""
+    import socket
+    _, _, _, port, _ = served
+    idle = []
+    for _ in range(20):
+        s = socket.create_connection(("127.0.0.1", port))
+        s.sendall(b"GET /metr")  # never finishes the request line
+        idle.append(s)
+    t = time.time()
+    assert _get(port, "/healthz")[0] in (200, 503)
+    assert _get(port, "/metrics")[0] == 200
+    assert time.time() - t < 1.0
+    idle[0].settimeout(4)
+    assert idle[0].recv(100) == b""  # closed by the server after its 2 s
+    for s in idle:
+        s.close()
+
+
 def test_metrics_addr_invalid(scratch):
     d = harness.Daemon(scratch, args=["--metrics-addr", "nohost:notaport"]).start()
     assert d.proc.wait(10) == 1
