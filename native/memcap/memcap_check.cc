@@ -1,0 +1,66 @@
+// Drives libadp_memcap.so the way a framework does -- HIP calls through the PLT
+// of a binary linked against the HIP library (here the CPU mock) -- and prints
+// one JSON line per step: {"step": ..., "rc": <hipError_t>, ...}. Run with
+// LD_PRELOAD=libadp_memcap.so AMD_GPU_MEMORY_LIMIT_MIB=100,50 (tests/test_memcap.py).
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <cstdio>
+
+namespace {
+constexpr size_t kMiB = size_t{1} << 20;
+void Out(const char* step, hipError_t rc) { printf("{\"step\": \"%s\", \"rc\": %d}\n", step, static_cast<int>(rc)); }
+void Info(const char* step) {
+  size_t f = 0, t = 0;
+  hipError_t rc = hipMemGetInfo(&f, &t);
+  printf("{\"step\": \"%s\", \"rc\": %d, \"free_mib\": %zu, \"total_mib\": %zu}\n", step, static_cast<int>(rc),
+         f / kMiB, t / kMiB);
+}
+}  // namespace
+
+int main() {
+  void *a = nullptr, *b = nullptr, *c = nullptr;
+  (void)hipSetDevice(0);
+  Out("d0 malloc 60", hipMalloc(&a, 60 * kMiB));
+  Out("d0 malloc 50", hipMalloc(&b, 50 * kMiB));
+  printf("{\"step\": \"d0 refused ptr\", \"null\": %s}\n", b ? "false" : "true");
+  Info("d0 info");
+  Out("d0 free 60", hipFree(a));
+  Out("d0 malloc 50 again", hipMalloc(&b, 50 * kMiB));
+  Info("d0 info after");
+  size_t pitch = 0;
+  Out("d0 pitch 1000x1000", hipMallocPitch(&c, &pitch, 1000, 1000));  // 1024 x 1000 bytes really
+  Info("d0 info pitch");
+  Out("d0 free pitch", hipFree(c));
+  hipMemGenericAllocationHandle_t h = nullptr;
+  hipMemAllocationProp prop{};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = 0;
+  Out("d0 memcreate 60", hipMemCreate(&h, 60 * kMiB, &prop, 0));
+  Out("d0 memcreate 40", hipMemCreate(&h, 40 * kMiB, &prop, 0));
+  Out("d0 memrelease 40", hipMemRelease(h));
+  Info("d0 info vmm");
+
+  (void)hipSetDevice(1);
+  auto s1 = reinterpret_cast<hipStream_t>(uintptr_t{2});  // mock stream of device 1
+  Out("d1 malloc 60", hipMalloc(&a, 60 * kMiB));
+  Out("d1 mallocasync 40", hipMallocAsync(&a, 40 * kMiB, s1));
+  Out("d1 mallocasync 20", hipMallocAsync(&b, 20 * kMiB, s1));
+  Out("d1 freeasync 40", hipFreeAsync(a, s1));
+  Out("d1 mallocasync 20 again", hipMallocAsync(&b, 20 * kMiB, s1));
+  Info("d1 info");
+  size_t tot = 0;
+  Out("d1 totalmem", hipDeviceTotalMem(&tot, 1));
+  printf("{\"step\": \"d1 totalmem value\", \"mib\": %zu}\n", tot / kMiB);
+
+  (void)hipSetDevice(2);
+  Out("d2 malloc 100000", hipMalloc(&a, 100000 * kMiB));  // not capped
+  Info("d2 info");
+  hipDeviceProp_tR0600 p0{}, p2{};
+  (void)hipGetDevicePropertiesR0600(&p0, 0);
+  (void)hipGetDevicePropertiesR0600(&p2, 2);
+  printf("{\"step\": \"props\", \"d0_mib\": %zu, \"d2_mib\": %zu}\n", p0.totalGlobalMem / kMiB,
+         p2.totalGlobalMem / kMiB);
+  return 0;
+}

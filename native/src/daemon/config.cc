@@ -142,6 +142,14 @@ const std::vector<FlagDef>& Table() {
        "fail Allocate() for a device currently advertised Unhealthy (default: allocate it and log a "
        "warning, as the reference does)",
        [](Flags& f) -> void* { return &f.reject_unhealthy; }},
+      {"enforce-memory-units", "DP_ENFORCE_MEMORY_UNITS", "enforceMemoryUnits", Kind::kBool,
+       "memory-unit resources (replicas -1): mount and preload libadp_memcap.so in the container, which caps "
+       "each device's HIP allocations at the HBM the pod was granted (AMD_GPU_MEMORY_LIMIT_MIB)",
+       [](Flags& f) -> void* { return &f.enforce_memory_units; }},
+      {"memcap-lib", "DP_MEMCAP_LIB", "memcapLib", Kind::kString,
+       "path of libadp_memcap.so in the plugin's filesystem (default: next to the binary, then "
+       "/usr/lib/amdgpu-device-plugin/)",
+       [](Flags& f) -> void* { return &f.memcap_lib; }},
       {"metrics-addr", "DP_METRICS_ADDR", "metricsAddr", Kind::kString,
        "serve Prometheus /metrics and /healthz on this TCP address, e.g. ':9400' (empty = off)",
        [](Flags& f) -> void* { return &f.metrics_addr; }},

@@ -54,6 +54,8 @@ struct Flags {
   std::string loop_affinity = "peer-l3";
   std::string health_state_file;  // "" = health verdicts kept in memory only
   bool reject_unhealthy = false;  // Allocate() of an Unhealthy device fails instead of warning
+  bool enforce_memory_units = false;  // memory-unit pods get the HBM-cap shim (LD_PRELOAD)
+  std::string memcap_lib;  // the shim in the plugin's filesystem ("" = next to the binary, then /usr/lib/...)
 };
 
 struct Config {

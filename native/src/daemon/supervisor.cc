@@ -43,6 +43,64 @@ struct Validated {
   inventory::BuildOptions bopts;
 };
 
+// The HBM-cap shim shipped with the daemon: --memcap-lib, else next to the
+// binary, else the image's library directory. "" if none exists.
+std::string MemcapSource(const Flags& f) {
+  struct stat st;
+  if (!f.memcap_lib.empty()) return stat(f.memcap_lib.c_str(), &st) == 0 ? f.memcap_lib : "";
+  char exe[4096];
+  ssize_t n = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+  std::vector<std::string> cands;
+  if (n > 0) {
+    std::string self(exe, static_cast<size_t>(n));
+    cands.push_back(self.substr(0, self.rfind('/') + 1) + "libadp_memcap.so");
+  }
+  cands.push_back("/usr/lib/amdgpu-device-plugin/libadp_memcap.so");
+  for (const auto& c : cands)
+    if (stat(c.c_str(), &st) == 0) return c;
+  return "";
+}
+
+// --enforce-memory-units: copies the shim into <plugin dir>/amdgpu-dp/ -- a
+// host path the container runtime can bind-mount into pods (the kubelet wipes
+// the directory when it restarts; every plugin (re)start installs it again) --
+// and returns that path, or "" (logged) when it cannot.
+std::string InstallMemcap(const Flags& f) {
+  std::string src = MemcapSource(f);
+  FILE* in = src.empty() ? nullptr : fopen(src.c_str(), "rb");
+  if (!in) {
+    LOG_ERROR(kComp, "--enforce-memory-units: cannot read %s: %s; memory units are not enforced",
+              src.empty() ? "libadp_memcap.so" : src.c_str(), strerror(errno));
+    return "";
+  }
+  std::string body;
+  char buf[65536];
+  for (size_t n; (n = fread(buf, 1, sizeof(buf), in)) > 0;) body.append(buf, n);
+  fclose(in);
+  std::string dir = PathJoin(f.plugin_dir, "amdgpu-dp");
+  std::string dst = PathJoin(dir, "libadp_memcap.so");
+  if (FILE* cur = fopen(dst.c_str(), "rb")) {  // already there and identical: keep the inode
+    std::string have;
+    for (size_t n; (n = fread(buf, 1, sizeof(buf), cur)) > 0;) have.append(buf, n);
+    fclose(cur);
+    if (have == body) return dst;
+  }
+  mkdir(dir.c_str(), 0755);
+  std::string tmp = dst + ".tmp";
+  FILE* out = fopen(tmp.c_str(), "wb");
+  bool ok = out && fwrite(body.data(), 1, body.size(), out) == body.size();
+  if (out) ok = (fclose(out) == 0) && ok;
+  // A new inode each time: running containers keep the library they mapped.
+  if (!ok || chmod(tmp.c_str(), 0644) != 0 || rename(tmp.c_str(), dst.c_str()) != 0) {
+    LOG_ERROR(kComp, "--enforce-memory-units: cannot install %s: %s; memory units are not enforced", dst.c_str(),
+              strerror(errno));
+    unlink(tmp.c_str());
+    return "";
+  }
+  LOG_INFO(kComp, "HBM-cap shim installed at %s (from %s)", dst.c_str(), src.c_str());
+  return dst;
+}
+
 Result<Validated> Validate(const Config& cfg) {
   Validated v;
   const Flags& f = cfg.flags;
@@ -76,6 +134,10 @@ Result<Validated> Validate(const Config& cfg) {
   v.popts.busy_poll_us = static_cast<int>(std::min<uint64_t>(f.busy_poll_us, 100000));
   v.popts.cdi_spec_dir = f.cdi_spec_dir;
   v.popts.reject_unhealthy = f.reject_unhealthy;
+  if (f.enforce_memory_units && MemcapSource(f).empty())
+    return InvalidArgument("--enforce-memory-units: libadp_memcap.so not found (" +
+                           (f.memcap_lib.empty() ? std::string("next to the binary or in /usr/lib/amdgpu-device-plugin")
+                                                 : f.memcap_lib) + "); set --memcap-lib");
   v.bopts.driver_root = f.driver_root;
   v.bopts.include_card_nodes = f.include_card_nodes;
   std::string devs = Trim(f.devices);
@@ -364,6 +426,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
       return;
     }
     restarts.fetch_add(1);
+    v.popts.memcap_host_path = cfg.flags.enforce_memory_units ? InstallMemcap(cfg.flags) : "";
     health::HealthConfig hcfg = health::HealthConfig::FromEnv();
     {
       std::lock_guard<std::mutex> lk(plugins_mu);

@@ -185,6 +185,13 @@ void Plugin::BuildUnits() {
       LOG_WARN(kComp, "device ID '%s' exceeds 63 characters", advertised_[i].c_str());
     advertised_index_[advertised_[i]] = advertised_unit_[i];
   }
+  if (memory_units_ && !opts_.memcap_host_path.empty()) {
+    pb::PutMapEntry(&memcap_bytes_, 1, "LD_PRELOAD", kMemcapContainerPath);
+    pb::Mount m{kMemcapContainerPath, opts_.memcap_host_path, true};
+    std::string mb;
+    pb::Encode(m, &mb);
+    pb::PutLen(&memcap_bytes_, 2, mb);
+  }
   pb::DeviceSpec kfd{"/dev/kfd", PathJoin(opts_.driver_root, "/dev/kfd"), "rw"};
   std::string kb;
   pb::Encode(kfd, &kb);
@@ -420,6 +427,7 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       pb::PutMapEntry(&c, 1, kMemoryLimitEnv, mem_mib);
       pb::PutMapEntry(&c, 1, kMemoryFractionEnv, mem_frac);
       pb::PutMapEntry(&c, 1, kMemoryDevicesEnv, mem_devs);
+      c += memcap_bytes_;  // the container enforces the grant (empty unless --enforce-memory-units)
     }
     if (!cu_mask.empty()) pb::PutMapEntry(&c, 1, kCuMaskEnv, cu_mask);
     if (opts_.pass_device_specs) {

@@ -67,6 +67,8 @@ inline constexpr const char* kMemoryDevicesEnv = "AMD_GPU_MEMORY_DEVICES";
 // Set on Allocate for CU-partitioned time-slice replicas (--replica-cu-mask): the
 // ROCm runtime restricts every queue of the container to the listed CUs.
 inline constexpr const char* kCuMaskEnv = "HSA_CU_MASK";
+// --enforce-memory-units: where the HBM-cap shim is mounted in the container.
+inline constexpr const char* kMemcapContainerPath = "/usr/local/lib/amdgpu-dp/libadp_memcap.so";
 
 struct PluginOptions {
   std::string plugin_dir = kDefaultPluginDir;
@@ -94,6 +96,9 @@ struct PluginOptions {
   // and log a warning (the reference allocates silently, server.go:316-353);
   // true = fail the call with FAILED_PRECONDITION naming the device.
   bool reject_unhealthy = false;
+  // Host path of the HBM-cap shim; non-empty: memory-unit resources mount it
+  // read-only at kMemcapContainerPath and set LD_PRELOAD to it.
+  std::string memcap_host_path;
 };
 
 // HSA_CU_MASK bit ranges [first, last] of each of `replicas` CU shares of a device
@@ -225,6 +230,7 @@ class Plugin {
   // advertised ID -> unit; keys view into advertised_ (never modified after build)
   std::unordered_map<std::string_view, int> advertised_index_;
   std::string kfd_spec_bytes_;
+  std::string memcap_bytes_;  // pre-encoded LD_PRELOAD env + shim mount (--enforce-memory-units)
   alloc::DeviceGraph graph_;
   // Memoised best-effort answers for <= 8 whole devices (see CachedBestEffort),
   // in anonymous zero-filled pages (an all-zero atomic<uint16_t> is "empty").

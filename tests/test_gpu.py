@@ -219,6 +219,64 @@ def test_memory_unit_grant_caps_pytorch(scratch, snap):
     assert r.stdout.strip().endswith("CAPPED") and "NOT" not in r.stdout
 
 
+def test_memcap_shim_enforces_the_grant_on_pytorch(scratch, snap):
+    """--enforce-memory-units on the real MI355X: the Allocate() response mounts
+    and preloads libadp_memcap.so; PyTorch -- which does NOT opt in -- then sees
+    the grant as the GPU's memory (mem_get_info, device properties), can use it,
+    and gets OutOfMemoryError beyond it; memory freed is usable again."""
+    import json
+    import subprocess
+    import sys
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    shim = os.path.join(BUILD_DIR, "libadp_memcap.so")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--resource-config", "gpu:gpu-mem-gb:-1",
+                                                     "--replica-policy", "pack", "--enforce-memory-units",
+                                                     "--memcap-lib", shim]).start()
+    try:
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=10).devices]
+        resp = c.allocate(ids[:4]).container_responses[0]
+        c.close()
+    finally:
+        assert d.stop() == 0
+        k.stop()
+    envs = dict(resp.envs)
+    assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "4000"
+    (mount,) = [m for m in resp.mounts if m.container_path == envs["LD_PRELOAD"]]
+    assert mount.read_only and os.path.exists(mount.host_path)
+    envs["LD_PRELOAD"] = mount.host_path  # what the bind mount gives the container
+    code = (
+        "import json, torch\n"
+        "free, total = torch.cuda.mem_get_info(0)\n"
+        "props = torch.cuda.get_device_properties(0).total_memory\n"
+        "a = torch.empty(3 << 30, dtype=torch.uint8, device='cuda')\n"
+        "a.fill_(1)\n"
+        "try:\n"
+        "    b = torch.empty(2 << 30, dtype=torch.uint8, device='cuda')\n"
+        "    over = False\n"
+        "except torch.OutOfMemoryError:\n"
+        "    over = True\n"
+        "del a\n"
+        "torch.cuda.empty_cache()\n"
+        "c = torch.empty(3500 << 20, dtype=torch.uint8, device='cuda')\n"
+        "c.fill_(2)\n"
+        "torch.cuda.synchronize()\n"
+        "print(json.dumps({'total_mib': total >> 20, 'free_mib': free >> 20, 'props_mib': props >> 20,\n"
+        "                  'over_refused': over, 'reuse_ok': int(c[-1].item()) == 2}))\n")
+    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **envs}, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["total_mib"] == 4000 and out["props_mib"] == 4000 and out["free_mib"] <= 4000, out
+    assert out["over_refused"] and out["reuse_ok"], out
+    assert "amdgpu-dp memcap: device 0: refused" in r.stderr
+    os.makedirs("gpurun_out/memcap", exist_ok=True)
+    with open("gpurun_out/memcap/torch_under_shim.json", "w") as f:
+        json.dump({"allocate_envs": envs, "result": out, "stderr_tail": r.stderr[-1500:]}, f, indent=1)
+
+
 def test_dry_run_labels_on_real_gpu(snap):
     import json
     import subprocess

@@ -46,7 +46,8 @@ PACKAGES = {
 # Libraries the daemon itself dlopens (native/src/smi/smi.cc, native/src/daemon/yaml.cc).
 DAEMON_DLOPENS = {"libamd_smi.so.26", "libyaml-0.so.2"}
 # The build stage's outputs, as built in this tree.
-BUILT = {"/build/amdgpu-device-plugin": DAEMON, "/build/amdgpu-dp-probe": PROBE_BIN}
+BUILT = {"/build/amdgpu-device-plugin": DAEMON, "/build/amdgpu-dp-probe": PROBE_BIN,
+         "/build/libadp_memcap.so": os.path.join(os.path.dirname(DAEMON), "libadp_memcap.so")}
 
 
 def stages(path):

@@ -1,0 +1,106 @@
+"""HBM caps for memory-unit sharing (--enforce-memory-units, libadp_memcap.so).
+
+The reference hands out `gpu-mem-gb` units without telling or limiting the
+workload (server.go:99-111). Here Allocate() of a memory-unit resource can
+mount + preload a shim that refuses HIP allocations past the granted HBM and
+reports the grant as the device's memory. CPU: the shim in front of a
+libamdhip64 stand-in, called through the PLT like a framework does, and the
+daemon's Allocate() responses on the amdsmi mock. The real-HIP / PyTorch run is
+tests/test_gpu.py::test_memcap_caps_torch_allocations.
+"""
+
+import json
+import os
+import subprocess
+
+from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
+
+SHIM = os.path.join(BUILD_DIR, "libadp_memcap.so")
+CHECK = os.path.join(BUILD_DIR, "adp_memcap_check")
+
+
+def _run(env_extra):
+    env = dict(os.environ, **env_extra)
+    r = subprocess.run([CHECK], capture_output=True, text=True, timeout=30, env=env)
+    assert r.returncode == 0, r.stderr
+    return {d["step"]: d for d in map(json.loads, r.stdout.splitlines())}, r.stderr
+
+
+def test_without_the_shim_nothing_is_capped():
+    out, _ = _run({})
+    assert out["d0 malloc 50"]["rc"] == 0 and out["d0 info"]["total_mib"] == 294912
+
+
+def test_caps_per_device_in_hip_order():
+    out, err = _run({"LD_PRELOAD": SHIM, "AMD_GPU_MEMORY_LIMIT_MIB": "100,50"})
+    oom = 2  # hipErrorOutOfMemory
+    # device 0: 100 MiB
+    assert out["d0 malloc 60"]["rc"] == 0
+    assert out["d0 malloc 50"]["rc"] == oom and out["d0 refused ptr"]["null"]
+    assert (out["d0 info"]["free_mib"], out["d0 info"]["total_mib"]) == (40, 100)
+    assert out["d0 malloc 50 again"]["rc"] == 0  # after the free
+    assert out["d0 info after"]["free_mib"] == 50
+    assert out["d0 info pitch"]["free_mib"] == 49  # counted at the padded pitch, once
+    assert out["d0 memcreate 60"]["rc"] == oom and out["d0 memcreate 40"]["rc"] == 0  # VMM handles
+    assert out["d0 info vmm"]["free_mib"] == 50  # released
+    # device 1: 50 MiB, stream-ordered allocations on a device-1 stream
+    assert out["d1 malloc 60"]["rc"] == oom
+    assert out["d1 mallocasync 40"]["rc"] == 0 and out["d1 mallocasync 20"]["rc"] == oom
+    assert out["d1 mallocasync 20 again"]["rc"] == 0  # after hipFreeAsync
+    assert (out["d1 info"]["free_mib"], out["d1 info"]["total_mib"]) == (30, 50)
+    assert out["d1 totalmem value"]["mib"] == 50
+    # device 2: past the list, not capped
+    assert out["d2 malloc 100000"]["rc"] == 0 and out["d2 info"]["total_mib"] == 294912
+    assert out["props"] == {"step": "props", "d0_mib": 100, "d2_mib": 294912}
+    assert "device 0: refused 50.0 MiB (60.0 of 100.0 MiB in use" in err  # once per device
+
+
+def test_shim_exports_hip_versioned_entry_points_only():
+    r = subprocess.run(["nm", "-D", "--defined-only", SHIM], capture_output=True, text=True, check=True)
+    syms = {ln.split()[-1] for ln in r.stdout.splitlines() if " T " in ln}
+    assert {"hipMalloc@@hip_4.2", "hipFree@@hip_4.2", "hipMemGetInfo@@hip_4.2", "hipMallocAsync@@hip_5.1",
+            "hipMemCreate@@hip_5.1", "hipGetDevicePropertiesR0600@@hip_6.0"} <= syms
+    assert all(s.startswith("hip") for s in syms), syms
+    r = subprocess.run(["ldd", SHIM], capture_output=True, text=True, check=True)
+    assert "libamdhip64" not in r.stdout and "libstdc++" not in r.stdout  # resolved at run time; static C++
+
+
+def _allocate(scratch, rc, extra=()):
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, args=["--resource-config", rc, "--replica-policy", "pack",
+                                      "--enforce-memory-units", "--memcap-lib", SHIM, *extra]).start()
+    try:
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        resp = c.allocate(ids[:3]).container_responses[0]
+        c.close()
+        return resp, d.log()
+    finally:
+        d.stop()
+        k.stop()
+
+
+def test_memory_unit_pods_get_the_shim(scratch):
+    resp, log = _allocate(scratch, "gpu:gpu-mem-gb:-1")
+    envs = dict(resp.envs)
+    installed = os.path.join(scratch, "amdgpu-dp", "libadp_memcap.so")
+    assert envs["LD_PRELOAD"] == "/usr/local/lib/amdgpu-dp/libadp_memcap.so"
+    assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "3000"
+    mounts = [(m.container_path, m.host_path, m.read_only) for m in resp.mounts]
+    assert mounts == [("/usr/local/lib/amdgpu-dp/libadp_memcap.so", installed, True)]
+    assert open(installed, "rb").read() == open(SHIM, "rb").read()
+    assert "HBM-cap shim installed at" in log
+
+
+def test_time_slice_pods_do_not_get_the_shim(scratch):
+    resp, _ = _allocate(scratch, "gpu:shared:4")
+    assert "LD_PRELOAD" not in dict(resp.envs) and not list(resp.mounts)
+
+
+def test_missing_shim_is_a_startup_error(scratch):
+    d = harness.Daemon(scratch, args=["--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units",
+                                      "--memcap-lib", "/nonexistent/libadp_memcap.so"]).start()
+    assert d.proc.wait(20) == 1
+    assert "libadp_memcap.so not found" in d.log()
