@@ -349,7 +349,10 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
         if (i) { mem_mib += ','; mem_frac += ','; mem_devs += ','; }
         mem_devs += u.visible_id;
         mem_mib += std::to_string(granted);
-        snprintf(buf, sizeof(buf), "%.4f", u.vram_mib ? std::min(1.0, double(granted) / u.vram_mib) : 0.0);
+        // Under the HBM-cap shim the device reports the grant as its memory, so
+        // the grant is all of what the workload sees.
+        double frac = !memcap_bytes_.empty() ? 1.0 : u.vram_mib ? std::min(1.0, double(granted) / u.vram_mib) : 0.0;
+        snprintf(buf, sizeof(buf), "%.4f", frac);
         mem_frac += buf;
       }
     }

@@ -243,12 +243,13 @@ def test_memcap_shim_enforces_the_grant_on_pytorch(scratch, snap):
         assert d.stop() == 0
         k.stop()
     envs = dict(resp.envs)
-    assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "4000"
+    assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "4000" and envs["AMD_GPU_MEMORY_FRACTION"] == "1.0000"
     (mount,) = [m for m in resp.mounts if m.container_path == envs["LD_PRELOAD"]]
     assert mount.read_only and os.path.exists(mount.host_path)
     envs["LD_PRELOAD"] = mount.host_path  # what the bind mount gives the container
     code = (
-        "import json, torch\n"
+        "import json, os, torch\n"
+        "torch.cuda.set_per_process_memory_fraction(float(os.environ['AMD_GPU_MEMORY_FRACTION']), 0)\n"
         "free, total = torch.cuda.mem_get_info(0)\n"
         "props = torch.cuda.get_device_properties(0).total_memory\n"
         "a = torch.empty(3 << 30, dtype=torch.uint8, device='cuda')\n"

@@ -88,6 +88,8 @@ def test_memory_unit_pods_get_the_shim(scratch):
     installed = os.path.join(scratch, "amdgpu-dp", "libadp_memcap.so")
     assert envs["LD_PRELOAD"] == "/usr/local/lib/amdgpu-dp/libadp_memcap.so"
     assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "3000"
+    # the device reports the grant as its memory under the shim: the fraction of it is 1
+    assert envs["AMD_GPU_MEMORY_FRACTION"] == "1.0000"
     mounts = [(m.container_path, m.host_path, m.read_only) for m in resp.mounts]
     assert mounts == [("/usr/local/lib/amdgpu-dp/libadp_memcap.so", installed, True)]
     assert open(installed, "rb").read() == open(SHIM, "rb").read()
