@@ -47,15 +47,20 @@ bench: build
 # Sanitizer builds of the native unit + stress tests (host code only).
 asan:
 	cmake -S native -B build/asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DADP_SANITIZE=ON >/dev/null
-	ninja -C build/asan -j$(JOBS) adp_unit_tests adp_stress amdsmi_mock
+	ninja -C build/asan -j$(JOBS) adp_unit_tests adp_stress amdsmi_mock adp_memcap adp_memcap_check
 	ASAN_OPTIONS=detect_leaks=1 build/asan/adp_unit_tests
 	build/asan/adp_stress
+	LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $(CURDIR)/build/asan/libadp_memcap.so" ASAN_OPTIONS=detect_leaks=0 \
+	  AMD_GPU_MEMORY_LIMIT_MIB=100,50 build/asan/adp_memcap_check
 
 tsan:
 	cmake -S native -B build/tsan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DADP_TSAN=ON >/dev/null
-	ninja -C build/tsan -j$(JOBS) adp_unit_tests adp_stress amdsmi_mock
+	ninja -C build/tsan -j$(JOBS) adp_unit_tests adp_stress amdsmi_mock adp_memcap adp_memcap_check
 	TSAN_OPTIONS=halt_on_error=1 build/tsan/adp_unit_tests
 	TSAN_OPTIONS=halt_on_error=1 build/tsan/adp_stress
+	# the HBM-cap shim: 8 threads of allocations against a cap
+	TSAN_OPTIONS=halt_on_error=1 LD_PRELOAD="$$(gcc -print-file-name=libtsan.so) $(CURDIR)/build/tsan/libadp_memcap.so" \
+	  AMD_GPU_MEMORY_LIMIT_MIB=100 build/tsan/adp_memcap_check stress
 
 # The daemon itself under TSan, driven by the end-to-end suites (tests that load
 # the C API into Python are skipped: a TSan .so cannot be dlopen'ed there).

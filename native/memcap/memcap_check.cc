@@ -6,6 +6,10 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
+#include <random>
+#include <thread>
+#include <vector>
 
 namespace {
 constexpr size_t kMiB = size_t{1} << 20;
@@ -18,7 +22,41 @@ void Info(const char* step) {
 }
 }  // namespace
 
-int main() {
+// `stress`: 8 threads allocate and free random sizes on device 0 (sync and
+// stream-ordered) against the cap; at the end every byte must be back.
+int Stress() {
+  std::vector<std::thread> ts;
+  std::vector<int> refused(8, 0), granted(8, 0);
+  for (int t = 0; t < 8; ++t)
+    ts.emplace_back([t, &refused, &granted] {
+      (void)hipSetDevice(0);
+      std::mt19937 rng(t);
+      std::vector<void*> held;
+      auto s0 = reinterpret_cast<hipStream_t>(uintptr_t{1});
+      for (int i = 0; i < 20000; ++i) {
+        if (!held.empty() && (rng() % 2 || held.size() > 16)) {
+          void* p = held.back();
+          held.pop_back();
+          (void)(rng() % 2 ? hipFree(p) : hipFreeAsync(p, s0));
+          continue;
+        }
+        void* p = nullptr;
+        size_t sz = (1 + rng() % 8) * kMiB;
+        hipError_t rc = rng() % 2 ? hipMalloc(&p, sz) : hipMallocAsync(&p, sz, s0);
+        if (rc == hipSuccess) { held.push_back(p); ++granted[t]; } else { ++refused[t]; }
+      }
+      for (void* p : held) (void)hipFree(p);
+    });
+  for (auto& t : ts) t.join();
+  int r = 0, g = 0;
+  for (int t = 0; t < 8; ++t) { r += refused[t]; g += granted[t]; }
+  printf("{\"step\": \"stress\", \"granted\": %d, \"refused\": %d}\n", g, r);
+  Info("stress info");
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && strcmp(argv[1], "stress") == 0) return Stress();
   void *a = nullptr, *b = nullptr, *c = nullptr;
   (void)hipSetDevice(0);
   Out("d0 malloc 60", hipMalloc(&a, 60 * kMiB));

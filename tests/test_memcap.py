@@ -20,9 +20,9 @@ SHIM = os.path.join(BUILD_DIR, "libadp_memcap.so")
 CHECK = os.path.join(BUILD_DIR, "adp_memcap_check")
 
 
-def _run(env_extra):
+def _run(env_extra, *args):
     env = dict(os.environ, **env_extra)
-    r = subprocess.run([CHECK], capture_output=True, text=True, timeout=30, env=env)
+    r = subprocess.run([CHECK, *args], capture_output=True, text=True, timeout=60, env=env)
     assert r.returncode == 0, r.stderr
     return {d["step"]: d for d in map(json.loads, r.stdout.splitlines())}, r.stderr
 
@@ -54,6 +54,14 @@ def test_caps_per_device_in_hip_order():
     assert out["d2 malloc 100000"]["rc"] == 0 and out["d2 info"]["total_mib"] == 294912
     assert out["props"] == {"step": "props", "d0_mib": 100, "d2_mib": 294912}
     assert "device 0: refused 50.0 MiB (60.0 of 100.0 MiB in use" in err  # once per device
+
+
+def test_accounting_is_exact_under_concurrent_allocations():
+    """8 threads x 20k sync / stream-ordered allocations and frees against a
+    100 MiB cap: some are refused, and when all is freed the whole cap is free."""
+    out, _ = _run({"LD_PRELOAD": SHIM, "AMD_GPU_MEMORY_LIMIT_MIB": "100"}, "stress")
+    assert out["stress"]["granted"] > 1000 and out["stress"]["refused"] > 1000
+    assert (out["stress info"]["free_mib"], out["stress info"]["total_mib"]) == (100, 100)
 
 
 def test_shim_exports_hip_versioned_entry_points_only():
