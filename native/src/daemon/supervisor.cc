@@ -574,6 +574,12 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
             // One of our own sockets removed from under us (not by our own Stop():
             // those are re-created before this event is read, so stat finds them).
             if (e->len && (e->mask & IN_DELETE)) {
+              // The HBM-cap shim's directory wiped (a kubelet cleaning its
+              // plugin directory): put it back for the next memory-unit pod.
+              if (!v.popts.memcap_host_path.empty() && std::string(e->name) == "amdgpu-dp") {
+                LOG_WARN(kComp, "inotify: %s was removed; reinstalling", v.popts.memcap_host_path.c_str());
+                InstallMemcap(cfg.flags);
+              }
               for (auto& pl : plugins) {
                 struct stat st;
                 if (pl->running() && BaseName(pl->socket_path()) == e->name &&

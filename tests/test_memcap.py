@@ -104,6 +104,29 @@ def test_memory_unit_pods_get_the_shim(scratch):
     assert "HBM-cap shim installed at" in log
 
 
+def test_shim_reinstalled_when_its_directory_is_wiped(scratch):
+    """A kubelet cleaning its plugin directory removes the shim; the daemon puts
+    it back (the path in Allocate() responses stays valid)."""
+    import shutil
+    import time
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, args=["--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units",
+                                      "--memcap-lib", SHIM]).start()
+    try:
+        k.wait_registration()
+        installed = os.path.join(scratch, "amdgpu-dp", "libadp_memcap.so")
+        assert os.path.exists(installed)
+        shutil.rmtree(os.path.join(scratch, "amdgpu-dp"))
+        deadline = time.time() + 5
+        while time.time() < deadline and not os.path.exists(installed):
+            time.sleep(0.02)
+        assert os.path.exists(installed) and open(installed, "rb").read() == open(SHIM, "rb").read()
+        d.wait_log("was removed; reinstalling")
+    finally:
+        d.stop()
+        k.stop()
+
+
 def test_time_slice_pods_do_not_get_the_shim(scratch):
     resp, _ = _allocate(scratch, "gpu:shared:4")
     assert "LD_PRELOAD" not in dict(resp.envs) and not list(resp.mounts)
