@@ -60,7 +60,7 @@ tsan:
 	TSAN_OPTIONS=halt_on_error=1 build/tsan/adp_stress
 	# the HBM-cap shim: 8 threads of allocations against a cap
 	TSAN_OPTIONS=halt_on_error=1 LD_PRELOAD="$$(gcc -print-file-name=libtsan.so) $(CURDIR)/build/tsan/libadp_memcap.so" \
-	  AMD_GPU_MEMORY_LIMIT_MIB=100 build/tsan/adp_memcap_check stress
+	  AMD_GPU_MEMORY_LIMIT_MIB=40 build/tsan/adp_memcap_check stress
 
 # The daemon itself under TSan, driven by the end-to-end suites (tests that load
 # the C API into Python are skipped: a TSan .so cannot be dlopen'ed there).

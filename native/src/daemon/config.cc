@@ -142,6 +142,10 @@ const std::vector<FlagDef>& Table() {
        "fail Allocate() for a device currently advertised Unhealthy (default: allocate it and log a "
        "warning, as the reference does)",
        [](Flags& f) -> void* { return &f.reject_unhealthy; }},
+      {"replica-hbm-share", "DP_REPLICA_HBM_SHARE", "replicaHbmShare", Kind::kBool,
+       "time-slice replicas (replicas > 1) each hold 1/R of the device's HBM: Allocate() reports the grant "
+       "like a memory unit's (AMD_GPU_MEMORY_LIMIT_MIB ...), and --enforce-memory-units caps it",
+       [](Flags& f) -> void* { return &f.replica_hbm_share; }},
       {"enforce-memory-units", "DP_ENFORCE_MEMORY_UNITS", "enforceMemoryUnits", Kind::kBool,
        "memory-unit resources (replicas -1): mount and preload libadp_memcap.so in the container, which caps "
        "each device's HIP allocations at the HBM the pod was granted (AMD_GPU_MEMORY_LIMIT_MIB)",

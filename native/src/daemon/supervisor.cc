@@ -134,6 +134,7 @@ Result<Validated> Validate(const Config& cfg) {
   v.popts.busy_poll_us = static_cast<int>(std::min<uint64_t>(f.busy_poll_us, 100000));
   v.popts.cdi_spec_dir = f.cdi_spec_dir;
   v.popts.reject_unhealthy = f.reject_unhealthy;
+  v.popts.replica_hbm_share = f.replica_hbm_share;
   if (f.enforce_memory_units && MemcapSource(f).empty())
     return InvalidArgument("--enforce-memory-units: libadp_memcap.so not found (" +
                            (f.memcap_lib.empty() ? std::string("next to the binary or in /usr/lib/amdgpu-device-plugin")

@@ -112,6 +112,7 @@ void Plugin::BuildUnits() {
   const auto& v = spec_.variant;
   replicated_ = v.replicas > 1 || v.auto_replicas;
   memory_units_ = v.auto_replicas;
+  hbm_grants_ = memory_units_ || (opts_.replica_hbm_share && replicated_);
   for (const auto& ref : spec_.devices) {
     const auto& g = snap_->gpus[ref.gpu];
     Unit u;
@@ -141,6 +142,7 @@ void Plugin::BuildUnits() {
     u.replicas = v.auto_replicas
                      ? static_cast<unsigned>(std::max<uint64_t>(1, u.vram_mib / opts_.auto_replica_unit_mib))
                      : std::max(1u, v.replicas);
+    if (hbm_grants_) u.grant_mib = memory_units_ ? opts_.auto_replica_unit_mib : u.vram_mib / u.replicas;
     u.cus = ref.partition < 0 ? g.cus : g.partitions[ref.partition].cus;
     u.xcds = ref.partition < 0 ? g.xcds : g.partitions[ref.partition].xcds;
     if (opts_.replica_cu_mask && replicated_) {
@@ -185,7 +187,7 @@ void Plugin::BuildUnits() {
       LOG_WARN(kComp, "device ID '%s' exceeds 63 characters", advertised_[i].c_str());
     advertised_index_[advertised_[i]] = advertised_unit_[i];
   }
-  if (memory_units_ && !opts_.memcap_host_path.empty()) {
+  if (hbm_grants_ && !opts_.memcap_host_path.empty()) {
     pb::PutMapEntry(&memcap_bytes_, 1, "LD_PRELOAD", kMemcapContainerPath);
     pb::Mount m{kMemcapContainerPath, opts_.memcap_host_path, true};
     std::string mb;
@@ -311,8 +313,8 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
     // Unique physical devices. uuid strategy: sorted by ID (stripReplicas order,
     // server.go:325); index strategy: enumeration order (server.go:406-411).
     std::sort(us.begin(), us.end());
-    if (memory_units_) {
-      // Memory units granted per device (us is sorted, so runs are contiguous).
+    if (hbm_grants_) {
+      // Replicas (memory units / HBM shares) granted per device (us is sorted, so runs are contiguous).
       units_per.assign(units_.size(), 0);
       for (int u : us) ++units_per[u];
     }
@@ -341,11 +343,11 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
     mem_mib.clear();
     mem_frac.clear();
     mem_devs.clear();
-    if (memory_units_) {
+    if (hbm_grants_) {
       char buf[32];
       for (size_t i = 0; i < us.size(); ++i) {
         const Unit& u = units_[us[i]];
-        uint64_t granted = static_cast<uint64_t>(units_per[us[i]]) * opts_.auto_replica_unit_mib;
+        uint64_t granted = static_cast<uint64_t>(units_per[us[i]]) * u.grant_mib;
         if (i) { mem_mib += ','; mem_frac += ','; mem_devs += ','; }
         mem_devs += u.visible_id;
         mem_mib += std::to_string(granted);

@@ -96,6 +96,9 @@ struct PluginOptions {
   // and log a warning (the reference allocates silently, server.go:316-353);
   // true = fail the call with FAILED_PRECONDITION naming the device.
   bool reject_unhealthy = false;
+  // Time-slice replicas also hold 1/R of the device's HBM each: Allocate()
+  // reports it like a memory-unit grant (and --enforce-memory-units caps it).
+  bool replica_hbm_share = false;
   // Host path of the HBM-cap shim; non-empty: memory-unit resources mount it
   // read-only at kMemcapContainerPath and set LD_PRELOAD to it.
   std::string memcap_host_path;
@@ -135,6 +138,7 @@ struct Unit {
   std::string spec_bytes;          // pre-encoded ContainerAllocateResponse.devices entries
   std::string mount_bytes;         // pre-encoded ContainerAllocateResponse.mounts entry
   unsigned replicas = 1;
+  uint64_t grant_mib = 0;          // HBM one replica holds (memory units, --replica-hbm-share); 0 = none
   uint32_t cus = 0, xcds = 0;      // compute units / XCDs of this GPU or partition
   // --replica-cu-mask: CU bit range of each replica (empty = whole device).
   std::vector<std::pair<uint32_t, uint32_t>> replica_cus;
@@ -221,6 +225,7 @@ class Plugin {
   PluginOptions opts_;
   bool replicated_ = false;
   bool memory_units_ = false;  // auto replicas: one ID per auto_replica_unit_mib of HBM
+  bool hbm_grants_ = false;    // Allocate() reports (and may enforce) HBM per replica: memory units or HBM shares
 
   std::vector<Unit> units_;
   std::unordered_map<std::string, int> unit_by_id_;

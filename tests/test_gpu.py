@@ -278,6 +278,48 @@ def test_memcap_shim_enforces_the_grant_on_pytorch(scratch, snap):
         json.dump({"allocate_envs": envs, "result": out, "stderr_tail": r.stderr[-1500:]}, f, indent=1)
 
 
+def test_soft_partition_replica_on_mi355x(scratch, snap):
+    """gpu:shared:4 with --replica-cu-mask --replica-hbm-share
+    --enforce-memory-units: one replica is a soft partition -- a quarter of the
+    CUs (HSA_CU_MASK) and a quarter of the HBM, which PyTorch sees as the GPU's
+    memory and cannot exceed."""
+    import json
+    import subprocess
+    import sys
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, real_smi=True, args=[
+        "--devices", "0", "--resource-config", "gpu:shared:4", "--replica-cu-mask", "--replica-hbm-share",
+        "--enforce-memory-units", "--memcap-lib", os.path.join(BUILD_DIR, "libadp_memcap.so")]).start()
+    try:
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=10).devices]
+        resp = c.allocate(ids[1:2]).container_responses[0]
+        c.close()
+    finally:
+        assert d.stop() == 0
+        k.stop()
+    envs = dict(resp.envs)
+    quarter = snap["gpus"][0]["vram_mib"] // 4
+    assert envs["HSA_CU_MASK"] == "0:64-127" and envs["AMD_GPU_MEMORY_LIMIT_MIB"] == str(quarter)
+    envs["LD_PRELOAD"] = resp.mounts[0].host_path
+    code = ("import json, torch\n"
+            "free, total = torch.cuda.mem_get_info(0)\n"
+            "x = torch.empty((total >> 20) - 2048 << 20, dtype=torch.uint8, device='cuda')\n"
+            "try:\n"
+            "    y = torch.empty(4 << 30, dtype=torch.uint8, device='cuda')\n"
+            "    over = False\n"
+            "except torch.OutOfMemoryError:\n"
+            "    over = True\n"
+            "print(json.dumps({'total_mib': total >> 20, 'over_refused': over}))\n")
+    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **envs}, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out == {"total_mib": quarter, "over_refused": True}, out
+
+
 def test_dry_run_labels_on_real_gpu(snap):
     import json
     import subprocess
