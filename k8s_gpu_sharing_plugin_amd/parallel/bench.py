@@ -230,6 +230,10 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                 stats["probe_bdf"] = stats["probe"].get("pci")
             except Exception as e:  # reported, not fatal for the latency metric
                 stats["probe"] = {"error": str(e)}
+            # The probe may have run on another HIP device than this rank's (amdsmi
+            # and HIP orders can differ); the collectives below use the rank's own.
+            # (The probe restores the caller's device itself; this is the backstop.)
+            torch.cuda.set_device(local_rank)
 
         everyone = [stats]
         if use_dist:

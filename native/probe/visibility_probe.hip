@@ -218,6 +218,21 @@ int Fail(char* out, int len, hipError_t e, const char* where) {
   return static_cast<int>(e) ? static_cast<int>(e) : 1;
 }
 
+// The probe runs inside other programs (the bench's torch.distributed ranks,
+// where RCCL is bound to the rank's device): every entry point leaves the
+// caller's current HIP device as it found it, on every return path.
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 #define HIP_TRY(expr)                                   \
   do {                                                  \
     hipError_t _e = (expr);                             \
@@ -229,6 +244,7 @@ int Fail(char* out, int len, hipError_t e, const char* where) {
 // Bandwidth sweep over copy-kernel variants (unroll x store policy x grid size),
 // used to pick the probe's default copy configuration on real hardware.
 extern "C" int adp_probe_bw_sweep(int device, unsigned long long bytes, int iters, char* out, int len) {
+  DeviceGuard device_guard;
   HIP_TRY(hipSetDevice(device));
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -288,6 +304,7 @@ extern "C" int adp_probe_bw_sweep(int device, unsigned long long bytes, int iter
 // touch peer memory it has no mapping for. Output: {"devices": [...],
 // "pairs": [{"dst": i, "src": j, "gbps": x | "no-peer-access": true}]}.
 extern "C" int adp_probe_p2p(int ndev, unsigned long long bytes, int iters, char* out, int len) {
+  DeviceGuard device_guard;
   int count = 0;
   HIP_TRY(hipGetDeviceCount(&count));
   if (ndev <= 0 || ndev > count) ndev = count;
@@ -358,6 +375,7 @@ extern "C" int adp_probe_p2p(int ndev, unsigned long long bytes, int iters, char
 
 // bf16 MFMA throughput + exactness on `device` (see MfmaKernel).
 extern "C" int adp_probe_mfma(int device, int iters, char* out, int len) {
+  DeviceGuard device_guard;
   HIP_TRY(hipSetDevice(device));
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -425,6 +443,7 @@ extern "C" int adp_probe_list(char* out, int len) {
 // CUs show up. Returns {"xccs_seen", "cus_seen", "per_xcc": [...], "keys": [...]}
 // with keys = xcc << 16 | HW_ID[15:8] (SE/SH/CU).
 extern "C" int adp_probe_census(int device, char* out, int len) {
+  DeviceGuard device_guard;
   HIP_TRY(hipSetDevice(device));
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -465,6 +484,7 @@ extern "C" int adp_probe_census(int device, char* out, int len) {
 // Launch-to-completion latency of a small kernel (VictimKernel, 2 workgroups per
 // CU) timed on the host, `n` times after a warm-up: {"p50_us", "p99_us", ...}.
 extern "C" int adp_probe_latency(int device, int n, char* out, int len) {
+  DeviceGuard device_guard;
   HIP_TRY(hipSetDevice(device));
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -496,6 +516,7 @@ extern "C" int adp_probe_latency(int device, int n, char* out, int len) {
 // Saturates the device for `seconds`: back-to-back AggressorKernel launches of
 // 8 workgroups x 256 lanes per CU, each holding its CUs for ~1 ms.
 extern "C" int adp_probe_aggressor(int device, double seconds, char* out, int len) {
+  DeviceGuard device_guard;
   HIP_TRY(hipSetDevice(device));
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -516,6 +537,7 @@ extern "C" int adp_probe_aggressor(int device, double seconds, char* out, int le
 }
 
 extern "C" int adp_probe_run(int device, unsigned long long bytes, int iters, char* out, int len) {
+  DeviceGuard device_guard;
   HIP_TRY(hipSetDevice(device));
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
