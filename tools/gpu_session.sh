@@ -123,7 +123,7 @@ step_spread() {
   done
 }
 step_soak() {
-  timeout -k 10 400 python -u tools/soak.py --seconds 180 --real --out $out/soak.json > $out/soak.log 2>&1 || die SOAK $out/soak.log
+  timeout -k 10 400 python -u tools/soak.py --seconds 180 --real ${SOAK_ARGS:-} --out $out/soak.json > $out/soak.log 2>&1 || die SOAK $out/soak.log
   tail -1 $out/soak.log
 }
 

@@ -1,7 +1,7 @@
 """Soak test: the daemon under continuous pod churn, periodic SIGHUP restarts,
 kubelet restarts and metric scrapes; samples its RSS, open fds and threads.
 
-  python tools/soak.py [--seconds 300] [--clients 4] [--real] [--out soak.json]
+  python tools/soak.py [--seconds 300] [--clients 4] [--real] [--enforce] [--out soak.json]
 
 Prints one progress line per sample (every 10 s) and a final JSON summary with
 pods served, restarts, and first/last/max RSS/fds/threads. Exit code 1 if the
@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--real", action="store_true")
     ap.add_argument("--out", default=None)
     ap.add_argument("--max-rss-growth-mib", type=int, default=16)
+    ap.add_argument("--enforce", action="store_true",
+                    help="replicas with HBM shares enforced by the HBM-cap shim (re-installed on every restart)")
     a = ap.parse_args()
     d = harness.scratch_dir("adpsoak")
     ksock = os.path.join(d, "kubelet.sock")
@@ -55,6 +57,10 @@ def main():
             "--health-state-file", os.path.join(d, "health.state")]
     if a.real:
         args += ["--devices", "0"]
+    if a.enforce:
+        from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+        args += ["--replica-hbm-share", "--enforce-memory-units",
+                 "--memcap-lib", os.path.join(BUILD_DIR, "libadp_memcap.so")]
     dm = harness.Daemon(d, None if a.real else fixtures.node(8), args=args, real_smi=a.real,
                         env={"ADP_LOG_LEVEL": "warn", "DP_HEALTH_POLL_MS": "200"}).start()
     samples, pods, hups, kubelet_restarts, scrapes = [], 0, 0, 0, 0
@@ -108,7 +114,8 @@ def main():
     warm = samples[min(2, len(samples) - 1)] if samples else {}
     last = samples[-1] if samples else {}
     summary = {
-        "seconds": a.seconds, "clients": a.clients, "real_amdsmi": a.real, "pods": pods, "sighups": hups,
+        "seconds": a.seconds, "clients": a.clients, "real_amdsmi": a.real, "enforce": a.enforce, "pods": pods,
+        "sighups": hups,
         "kubelet_restarts": kubelet_restarts, "metric_scrapes": scrapes, "samples": len(samples),
         "rss_mib_after_warmup": warm.get("rss_mib"), "rss_mib_last": last.get("rss_mib"),
         "rss_mib_max": max((s["rss_mib"] for s in samples), default=None),
