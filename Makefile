@@ -51,7 +51,10 @@ asan:
 	ASAN_OPTIONS=detect_leaks=1 build/asan/adp_unit_tests
 	build/asan/adp_stress
 	LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $(CURDIR)/build/asan/libadp_memcap.so" ASAN_OPTIONS=detect_leaks=0 \
-	  AMD_GPU_MEMORY_LIMIT_MIB=100,50 build/asan/adp_memcap_check
+	  AMD_GPU_MEMORY_LIMIT_MIB=100,50 ADP_MEMCAP_KEY=make-asan-$$$$ build/asan/adp_memcap_check
+	LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $(CURDIR)/build/asan/libadp_memcap.so" ASAN_OPTIONS=detect_leaks=0 \
+	  AMD_GPU_MEMORY_LIMIT_MIB=40 ADP_MEMCAP_KEY=make-asan-stress-$$$$ build/asan/adp_memcap_check stress
+	rm -f /dev/shm/adp-memcap-key-make-asan-*
 
 tsan:
 	cmake -S native -B build/tsan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DADP_TSAN=ON >/dev/null
@@ -60,7 +63,10 @@ tsan:
 	TSAN_OPTIONS=halt_on_error=1 build/tsan/adp_stress
 	# the HBM-cap shim: 8 threads of allocations against a cap
 	TSAN_OPTIONS=halt_on_error=1 LD_PRELOAD="$$(gcc -print-file-name=libtsan.so) $(CURDIR)/build/tsan/libadp_memcap.so" \
-	  AMD_GPU_MEMORY_LIMIT_MIB=40 build/tsan/adp_memcap_check stress
+	  AMD_GPU_MEMORY_LIMIT_MIB=40 ADP_MEMCAP_KEY=make-tsan-$$$$ build/tsan/adp_memcap_check stress
+	TSAN_OPTIONS=halt_on_error=1 LD_PRELOAD="$$(gcc -print-file-name=libtsan.so) $(CURDIR)/build/tsan/libadp_memcap.so" \
+	  AMD_GPU_MEMORY_LIMIT_MIB=100 ADP_MEMCAP_KEY=make-tsan-fork-$$$$ build/tsan/adp_memcap_check fork 60
+	rm -f /dev/shm/adp-memcap-key-make-tsan-*
 
 # The daemon itself under TSan, driven by the end-to-end suites (tests that load
 # the C API into Python are skipped: a TSan .so cannot be dlopen'ed there).

@@ -14,12 +14,19 @@
 //
 // Caps: AMD_GPU_MEMORY_LIMIT_MIB="<mib>[,<mib>...]", one per device in the
 // container's HIP order (the plugin writes it in that order); devices past the
-// list are not capped. ADP_MEMCAP_VERBOSE=1 logs every decision to stderr.
+// list are not capped. The grant is the container's: its processes share the
+// counters (POSIX shared memory, see AttachShared). ADP_MEMCAP_VERBOSE=1 logs
+// every decision to stderr.
 //
 // No link-time dependency on libamdhip64: the real entry points are resolved
 // lazily (RTLD_NEXT, else the already-loaded libamdhip64). The exported
 // symbols carry libamdhip64's version nodes (memcap.map).
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
 
@@ -30,6 +37,7 @@
 #include <cstring>
 #include <algorithm>
 #include <mutex>
+#include <new>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -43,33 +51,45 @@ struct Alloc {
   size_t bytes;
 };
 
-struct State {
-  std::mutex mu;
-  std::unordered_map<const void*, Alloc> allocs;  // device pointer or VMM handle -> owner
-  size_t used[kMaxDevices] = {};
-  size_t cap[kMaxDevices] = {};  // 0 = not capped
-  bool verbose = false;
-  std::atomic<bool> warned[kMaxDevices] = {};
+// ---- container-wide accounting ------------------------------------------
+// Every process of the container draws on one grant: the counters live in a
+// POSIX shared-memory segment named after the container (its cgroup, or
+// ADP_MEMCAP_KEY). Each process owns a slot recording what it holds, so the
+// bytes of a process that exits -- or is killed -- are given back: at exit by
+// the process itself, otherwise by the next process that would be refused.
+// Without /dev/shm the accounting is per process.
+constexpr uint32_t kMagic = 0x434d4441;  // "ADMC"
+constexpr int kSlots = 256;
+
+struct SharedSlot {
+  std::atomic<int32_t> pid;     // 0 free, > 0 owner, -1 being reclaimed
+  std::atomic<uint64_t> start;  // owner's start time (/proc/<pid>/stat field 22): pid reuse guard
+  std::atomic<uint64_t> bytes[kMaxDevices];
 };
 
-State& S() {
-  static State* s = [] {
-    auto* st = new State();  // never destroyed: frees may run from atexit handlers
-    const char* v = getenv("ADP_MEMCAP_VERBOSE");
-    st->verbose = v && *v && *v != '0';
-    const char* lim = getenv("AMD_GPU_MEMORY_LIMIT_MIB");
-    int dev = 0;
-    for (const char* p = lim; p && *p && dev < kMaxDevices; ++dev) {
-      char* end = nullptr;
-      unsigned long long mib = strtoull(p, &end, 10);
-      if (end != p) st->cap[dev] = static_cast<size_t>(mib) << 20;
-      p = strchr(p, ',');
-      if (p) ++p;
-    }
-    return st;
-  }();
-  return *s;
-}
+struct SharedArea {
+  std::atomic<uint32_t> magic;
+  uint32_t version;
+  std::atomic<uint64_t> used[kMaxDevices];
+  SharedSlot slots[kSlots];
+};
+static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared counters must be address-free");
+
+struct State {
+  std::mutex mu;
+  std::unordered_map<const void*, Alloc> allocs;  // device pointer or VMM handle -> owner (this process)
+  size_t local_used[kMaxDevices] = {};            // used when there is no shared segment
+  size_t cap[kMaxDevices] = {};                   // 0 = not capped
+  bool verbose = false;
+  std::atomic<bool> warned[kMaxDevices] = {};
+  SharedArea* area = nullptr;
+  int slot = -1;
+  pid_t slot_pid = 0;
+  bool released = false;  // this process's slot was handed back (exit): stop touching the counters
+  std::string key;
+};
+
+State& S();
 
 void Log(const char* fmt, ...) {
   char buf[512];
@@ -78,6 +98,192 @@ void Log(const char* fmt, ...) {
   vsnprintf(buf, sizeof(buf), fmt, ap);
   va_end(ap);
   fprintf(stderr, "amdgpu-dp memcap: %s\n", buf);
+}
+
+uint64_t StartTime(pid_t pid) {
+  char path[64];
+  snprintf(path, sizeof(path), "/proc/%d/stat", static_cast<int>(pid));
+  FILE* f = fopen(path, "r");
+  if (!f) return 0;
+  char buf[1024];
+  size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  const char* p = strrchr(buf, ')');  // comm may contain spaces
+  if (!p) return 0;
+  unsigned long long v = 0;
+  // fields after ")": 3 state ... 22 starttime
+  int field = 2;
+  for (const char* q = p + 1; *q; ++q)
+    if (*q == ' ' && ++field == 22) {
+      v = strtoull(q + 1, nullptr, 10);
+      break;
+    }
+  return v;
+}
+
+bool Alive(pid_t pid, uint64_t start) {
+  if (kill(pid, 0) != 0 && errno == ESRCH) return false;
+  uint64_t now = StartTime(pid);
+  return !(start && now && now != start);  // a recycled pid is a different process
+}
+
+void SubSat(std::atomic<uint64_t>& a, uint64_t v) {
+  uint64_t cur = a.load();
+  while (!a.compare_exchange_weak(cur, cur - std::min(cur, v))) {
+  }
+}
+
+// Hands the bytes of dead owners back (and frees their slots).
+void ReclaimDead(SharedArea* a, int mine) {
+  for (int i = 0; i < kSlots; ++i) {
+    if (i == mine) continue;
+    SharedSlot& sl = a->slots[i];
+    int32_t pid = sl.pid.load();
+    if (pid <= 0 || Alive(pid, sl.start.load())) continue;
+    if (!sl.pid.compare_exchange_strong(pid, -1)) continue;  // someone else reclaims it
+    for (int d = 0; d < kMaxDevices; ++d) SubSat(a->used[d], sl.bytes[d].exchange(0));
+    sl.start.store(0);
+    sl.pid.store(0);
+  }
+}
+
+void ReleaseSlot() {
+  State& s = S();
+  std::lock_guard<std::mutex> lk(s.mu);
+  if (!s.area || s.slot < 0 || s.slot_pid != getpid() || s.released) return;
+  SharedSlot& sl = s.area->slots[s.slot];
+  for (int d = 0; d < kMaxDevices; ++d) SubSat(s.area->used[d], sl.bytes[d].exchange(0));
+  sl.start.store(0);
+  sl.pid.store(0);
+  s.released = true;
+}
+
+// Maps the container's segment and claims a slot for this process (called
+// with s.mu held, on first use and again in a forked child).
+void AttachShared(State& s) {
+  s.slot = -1;
+  s.slot_pid = getpid();
+  if (!s.area) {
+    std::string name = "/adp-memcap-" + s.key;
+    int fd = shm_open(name.c_str(), O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0600);
+    bool creator = fd >= 0;
+    if (!creator) fd = shm_open(name.c_str(), O_RDWR | O_CLOEXEC, 0);
+    if (fd < 0) {
+      if (s.verbose) Log("no shared segment %s (%s): accounting per process", name.c_str(), strerror(errno));
+      return;
+    }
+    bool ok = true;
+    if (creator) {
+      ok = ftruncate(fd, sizeof(SharedArea)) == 0;
+    } else {
+      struct stat st;
+      for (int i = 0; i < 1000 && ok; ++i) {  // the creator may still be sizing it
+        if (fstat(fd, &st) != 0) ok = false;
+        else if (static_cast<size_t>(st.st_size) >= sizeof(SharedArea)) break;
+        usleep(1000);
+      }
+    }
+    void* m = ok ? mmap(nullptr, sizeof(SharedArea), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0) : MAP_FAILED;
+    close(fd);
+    if (m == MAP_FAILED) {
+      if (s.verbose) Log("cannot map %s: accounting per process", name.c_str());
+      return;
+    }
+    auto* a = static_cast<SharedArea*>(m);
+    if (creator) {
+      a->version = 1;
+      a->magic.store(kMagic, std::memory_order_release);
+    } else {
+      for (int i = 0; i < 1000 && a->magic.load(std::memory_order_acquire) != kMagic; ++i) usleep(1000);
+      if (a->magic.load(std::memory_order_acquire) != kMagic) {
+        munmap(m, sizeof(SharedArea));
+        Log("shared segment %s not initialised: accounting per process", name.c_str());
+        return;
+      }
+    }
+    s.area = a;
+  }
+  uint64_t start = StartTime(s.slot_pid);
+  for (int pass = 0; pass < 2 && s.slot < 0; ++pass) {
+    if (pass) ReclaimDead(s.area, -1);
+    for (int i = 0; i < kSlots; ++i) {
+      int32_t zero = 0;
+      if (s.area->slots[i].pid.compare_exchange_strong(zero, static_cast<int32_t>(s.slot_pid))) {
+        s.area->slots[i].start.store(start);
+        s.slot = i;
+        break;
+      }
+    }
+  }
+  if (s.slot < 0) {
+    Log("no free slot in the shared segment: accounting per process");
+    munmap(s.area, sizeof(SharedArea));
+    s.area = nullptr;
+  }
+}
+
+void AtForkChild() {
+  // The child holds no device memory of its own yet: fresh local state, own slot.
+  State& s = S();
+  new (&s.mu) std::mutex();
+  s.allocs.clear();
+  for (auto& u : s.local_used) u = 0;
+  s.released = false;
+  if (s.area) AttachShared(s);
+}
+
+State& S() {
+  static State* s = [] {
+    auto* st = new State();  // never destroyed: frees may run from atexit handlers
+    const char* v = getenv("ADP_MEMCAP_VERBOSE");
+    st->verbose = v && *v && *v != '0';
+    const char* lim = getenv("AMD_GPU_MEMORY_LIMIT_MIB");
+    int dev = 0;
+    bool any = false;
+    for (const char* p = lim; p && *p && dev < kMaxDevices; ++dev) {
+      char* end = nullptr;
+      unsigned long long mib = strtoull(p, &end, 10);
+      if (end != p) st->cap[dev] = static_cast<size_t>(mib) << 20;
+      any = any || st->cap[dev];
+      p = strchr(p, ',');
+      if (p) ++p;
+    }
+    if (!any) return st;
+    // The container: its cgroup (shared by all its processes), unless named.
+    const char* k = getenv("ADP_MEMCAP_KEY");
+    std::string basis;
+    if (k && *k) {
+      basis = k;
+    } else if (FILE* f = fopen("/proc/self/cgroup", "r")) {
+      char buf[4096];
+      size_t n = fread(buf, 1, sizeof(buf), f);
+      fclose(f);
+      basis.assign(buf, n);
+    }
+    basis += "|";
+    basis += lim;  // a different grant is a different budget
+    uint64_t h = 1469598103934665603ull;  // FNV-1a
+    for (unsigned char c : basis) h = (h ^ c) * 1099511628211ull;
+    char hex[17];
+    snprintf(hex, sizeof(hex), "%016llx", static_cast<unsigned long long>(h));
+    st->key = hex;
+    if (k && *k && strlen(k) <= 64 && strspn(k, "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789_.-") ==
+                                          strlen(k))
+      st->key = std::string("key-") + k + "-" + st->key.substr(0, 8);  // a named budget, findable in /dev/shm
+    {
+      std::lock_guard<std::mutex> lk(st->mu);
+      AttachShared(*st);
+    }
+    pthread_atfork(nullptr, nullptr, AtForkChild);
+    atexit(ReleaseSlot);
+    return st;
+  }();
+  return *s;
+}
+
+size_t UsedLocked(State& s, int dev) {
+  return s.area ? static_cast<size_t>(s.area->used[dev].load()) : s.local_used[dev];
 }
 
 void* RealSym(const char* name) {
@@ -121,26 +327,50 @@ int StreamDevice(hipStream_t stream) {
   return CurrentDevice();
 }
 
-// Reserves `bytes` on `dev`; false if that would pass the cap.
+// Reserves `bytes` on `dev` for this process; false if that would take the
+// container past the cap.
 bool Reserve(int dev, size_t bytes) {
   State& s = S();
   if (!s.cap[dev]) return true;
   std::lock_guard<std::mutex> lk(s.mu);
-  if (s.used[dev] + bytes > s.cap[dev]) {
-    if (s.verbose || !s.warned[dev].exchange(true))
-      Log("device %d: refused %.1f MiB (%.1f of %.1f MiB in use; AMD_GPU_MEMORY_LIMIT_MIB)", dev,
-          bytes / 1048576.0, s.used[dev] / 1048576.0, s.cap[dev] / 1048576.0);
-    return false;
+  if (s.area && s.slot_pid != getpid()) AttachShared(s);  // forked without pthread_atfork (vfork-like paths)
+  if (s.area && !s.released) {
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      uint64_t cur = s.area->used[dev].load();
+      while (cur + bytes <= s.cap[dev]) {
+        if (s.area->used[dev].compare_exchange_weak(cur, cur + bytes)) {
+          s.area->slots[s.slot].bytes[dev].fetch_add(bytes);
+          return true;
+        }
+      }
+      if (attempt == 0) ReclaimDead(s.area, s.slot);  // a dead process may still be counted
+    }
+  } else if (s.local_used[dev] + bytes <= s.cap[dev]) {
+    s.local_used[dev] += bytes;
+    return true;
   }
-  s.used[dev] += bytes;
-  return true;
+  if (s.verbose || !s.warned[dev].exchange(true))
+    Log("device %d: refused %.1f MiB (%.1f of %.1f MiB in use%s; AMD_GPU_MEMORY_LIMIT_MIB)", dev,
+        bytes / 1048576.0, UsedLocked(s, dev) / 1048576.0, s.cap[dev] / 1048576.0,
+        s.area ? " by the container" : "");
+  return false;
+}
+
+void UnreserveLocked(State& s, int dev, size_t bytes) {
+  if (s.area) {
+    if (s.released || s.slot_pid != getpid()) return;
+    SubSat(s.area->slots[s.slot].bytes[dev], bytes);
+    SubSat(s.area->used[dev], bytes);
+  } else {
+    s.local_used[dev] -= std::min(bytes, s.local_used[dev]);
+  }
 }
 
 void Unreserve(int dev, size_t bytes) {
   State& s = S();
   if (!s.cap[dev]) return;
   std::lock_guard<std::mutex> lk(s.mu);
-  s.used[dev] -= std::min(bytes, s.used[dev]);
+  UnreserveLocked(s, dev, bytes);
 }
 
 void Track(const void* key, int dev, size_t bytes) {
@@ -148,7 +378,7 @@ void Track(const void* key, int dev, size_t bytes) {
   if (!s.cap[dev] || !key) return;
   std::lock_guard<std::mutex> lk(s.mu);
   s.allocs[key] = {dev, bytes};
-  if (s.verbose) Log("device %d: +%zu bytes (%zu in use)", dev, bytes, s.used[dev]);
+  if (s.verbose) Log("device %d: +%zu bytes (%zu in use)", dev, bytes, UsedLocked(s, dev));
 }
 
 void Untrack(const void* key) {
@@ -157,9 +387,9 @@ void Untrack(const void* key) {
   std::lock_guard<std::mutex> lk(s.mu);
   auto it = s.allocs.find(key);
   if (it == s.allocs.end()) return;  // not ours (uncapped device, or before a cap)
-  s.used[it->second.device] -= std::min(it->second.bytes, s.used[it->second.device]);
+  UnreserveLocked(s, it->second.device, it->second.bytes);
   if (s.verbose) Log("device %d: -%zu bytes (%zu in use)", it->second.device, it->second.bytes,
-                     s.used[it->second.device]);
+                     UsedLocked(s, it->second.device));
   s.allocs.erase(it);
 }
 
@@ -219,7 +449,13 @@ hipError_t hipMallocPitch(void** ptr, size_t* pitch, size_t width, size_t height
   State& s = S();
   if (t_depth == 0 && e == hipSuccess && ptr && *ptr && pitch && *pitch > width && s.cap[dev]) {
     std::lock_guard<std::mutex> lk(s.mu);
-    s.used[dev] += (*pitch - width) * height;
+    size_t extra = (*pitch - width) * height;  // the padding, counted without a second check
+    if (!s.area) {
+      s.local_used[dev] += extra;
+    } else if (!s.released && s.slot_pid == getpid()) {
+      s.area->used[dev].fetch_add(extra);
+      s.area->slots[s.slot].bytes[dev].fetch_add(extra);
+    }
     s.allocs[*ptr].bytes = *pitch * height;
   }
   return e;
@@ -283,7 +519,8 @@ hipError_t hipMemGetInfo(size_t* free_bytes, size_t* total_bytes) {
   State& s = S();
   if (e != hipSuccess || !s.cap[dev]) return e;
   std::lock_guard<std::mutex> lk(s.mu);
-  size_t left = s.cap[dev] - std::min(s.used[dev], s.cap[dev]);
+  if (s.area) ReclaimDead(s.area, s.slot);  // what died without saying so is free again
+  size_t left = s.cap[dev] - std::min(UsedLocked(s, dev), s.cap[dev]);
   if (free_bytes) *free_bytes = std::min(*free_bytes, left);
   if (total_bytes) *total_bytes = std::min(*total_bytes, s.cap[dev]);
   return e;

@@ -8,6 +8,10 @@
 #include <cstdio>
 #include <cstring>
 #include <random>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <cstdlib>
 #include <thread>
 #include <vector>
 
@@ -55,8 +59,49 @@ int Stress() {
   return 0;
 }
 
+// Several processes of one container (tests/test_memcap.py):
+//   hold <dev> <mib>  allocate, report, then hold it until stdin closes (normal exit)
+//   try <dev> <mib>   allocate once, report rc and what is left, exit
+//   fork <mib>        allocate, fork a child that tries <mib> and <mib>/2, report both
+int Processes(int argc, char** argv) {
+  const char* mode = argv[1];
+  if (!strcmp(mode, "fork")) {
+    size_t mib = strtoull(argv[2], nullptr, 10);
+    void* p = nullptr;
+    Out("parent malloc", hipMalloc(&p, mib * kMiB));
+    fflush(stdout);
+    pid_t c = fork();
+    if (c == 0) {
+      void *a = nullptr, *b = nullptr;
+      Out("child malloc full", hipMalloc(&a, mib * kMiB));
+      Out("child malloc half", hipMalloc(&b, mib / 2 * kMiB));
+      fflush(stdout);
+      _exit(0);
+    }
+    int st = 0;
+    waitpid(c, &st, 0);
+    Info("parent info after child");
+    return 0;
+  }
+  if (argc < 4) return 2;
+  int dev = atoi(argv[2]);
+  size_t mib = strtoull(argv[3], nullptr, 10);
+  (void)hipSetDevice(dev);
+  void* p = nullptr;
+  Out(mode, hipMalloc(&p, mib * kMiB));
+  Info("info");
+  fflush(stdout);
+  if (!strcmp(mode, "hold")) {
+    char buf[16];
+    while (read(0, buf, sizeof(buf)) > 0) {
+    }
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && strcmp(argv[1], "stress") == 0) return Stress();
+  if (argc > 2) return Processes(argc, argv);
   void *a = nullptr, *b = nullptr, *c = nullptr;
   (void)hipSetDevice(0);
   Out("d0 malloc 60", hipMalloc(&a, 60 * kMiB));

@@ -219,6 +219,12 @@ def test_memory_unit_grant_caps_pytorch(scratch, snap):
     assert r.stdout.strip().endswith("CAPPED") and "NOT" not in r.stdout
 
 
+def _drop_memcap_segments(key):
+    import glob
+    for f in glob.glob(f"/dev/shm/adp-memcap-key-{key}-*"):
+        os.unlink(f)
+
+
 def test_memcap_shim_enforces_the_grant_on_pytorch(scratch, snap):
     """--enforce-memory-units on the real MI355X: the Allocate() response mounts
     and preloads libadp_memcap.so; PyTorch -- which does NOT opt in -- then sees
@@ -247,6 +253,7 @@ def test_memcap_shim_enforces_the_grant_on_pytorch(scratch, snap):
     (mount,) = [m for m in resp.mounts if m.container_path == envs["LD_PRELOAD"]]
     assert mount.read_only and os.path.exists(mount.host_path)
     envs["LD_PRELOAD"] = mount.host_path  # what the bind mount gives the container
+    envs["ADP_MEMCAP_KEY"] = f"gputest-{os.getpid()}"  # the container's budget, named so it can be removed
     code = (
         "import json, os, torch\n"
         "torch.cuda.set_per_process_memory_fraction(float(os.environ['AMD_GPU_MEMORY_FRACTION']), 0)\n"
@@ -273,6 +280,7 @@ def test_memcap_shim_enforces_the_grant_on_pytorch(scratch, snap):
     assert out["total_mib"] == 4000 and out["props_mib"] == 4000 and out["free_mib"] <= 4000, out
     assert out["over_refused"] and out["reuse_ok"], out
     assert "amdgpu-dp memcap: device 0: refused" in r.stderr
+    _drop_memcap_segments(envs["ADP_MEMCAP_KEY"])
     os.makedirs("gpurun_out/memcap", exist_ok=True)
     with open("gpurun_out/memcap/torch_under_shim.json", "w") as f:
         json.dump({"allocate_envs": envs, "result": out, "stderr_tail": r.stderr[-1500:]}, f, indent=1)
@@ -304,6 +312,7 @@ def test_soft_partition_replica_on_mi355x(scratch, snap):
     quarter = snap["gpus"][0]["vram_mib"] // 4
     assert envs["HSA_CU_MASK"] == "0:64-127" and envs["AMD_GPU_MEMORY_LIMIT_MIB"] == str(quarter)
     envs["LD_PRELOAD"] = resp.mounts[0].host_path
+    envs["ADP_MEMCAP_KEY"] = f"gputest-soft-{os.getpid()}"
     code = ("import json, torch\n"
             "free, total = torch.cuda.mem_get_info(0)\n"
             "x = torch.empty((total >> 20) - 2048 << 20, dtype=torch.uint8, device='cuda')\n"
@@ -317,6 +326,7 @@ def test_soft_partition_replica_on_mi355x(scratch, snap):
                        timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
+    _drop_memcap_segments(envs["ADP_MEMCAP_KEY"])
     assert out == {"total_mib": quarter, "over_refused": True}, out
 
 

@@ -9,9 +9,13 @@ daemon's Allocate() responses on the amdsmi mock. The real-HIP / PyTorch run is
 tests/test_gpu.py::test_memcap_caps_torch_allocations.
 """
 
+import glob
 import json
 import os
 import subprocess
+import time
+
+import pytest
 
 from k8s_gpu_sharing_plugin_amd import BUILD_DIR
 from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
@@ -20,8 +24,19 @@ SHIM = os.path.join(BUILD_DIR, "libadp_memcap.so")
 CHECK = os.path.join(BUILD_DIR, "adp_memcap_check")
 
 
+@pytest.fixture(autouse=True)
+def _no_leftover_segments():
+    """The shim's container-wide counters live in /dev/shm/adp-memcap-*; drop
+    the ones a test created (in a pod they go with the pod)."""
+    before = set(glob.glob("/dev/shm/adp-memcap-*"))
+    yield
+    for f in set(glob.glob("/dev/shm/adp-memcap-*")) - before:
+        os.unlink(f)
+
+
 def _run(env_extra, *args):
     env = dict(os.environ, **env_extra)
+    env.setdefault("ADP_MEMCAP_KEY", f"test-{os.getpid()}-{time.monotonic_ns()}")
     r = subprocess.run([CHECK, *args], capture_output=True, text=True, timeout=60, env=env)
     assert r.returncode == 0, r.stderr
     return {d["step"]: d for d in map(json.loads, r.stdout.splitlines())}, r.stderr
@@ -63,6 +78,70 @@ def test_accounting_is_exact_under_concurrent_allocations():
     out, _ = _run({"LD_PRELOAD": SHIM, "AMD_GPU_MEMORY_LIMIT_MIB": "40"}, "stress")
     assert out["stress"]["granted"] > 1000 and out["stress"]["refused"] > 100
     assert (out["stress info"]["free_mib"], out["stress info"]["total_mib"]) == (40, 40)
+
+
+def _env(key, cap="100"):
+    return dict(os.environ, LD_PRELOAD=SHIM, AMD_GPU_MEMORY_LIMIT_MIB=cap, ADP_MEMCAP_KEY=key)
+
+
+def _hold(env, mib):
+    p = subprocess.Popen([CHECK, "hold", "0", str(mib)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                         stderr=subprocess.DEVNULL, text=True, env=env)
+    first = json.loads(p.stdout.readline())
+    assert first == {"step": "hold", "rc": 0}
+    p.stdout.readline()  # info
+    return p
+
+
+def _try(env, mib):
+    r = subprocess.run([CHECK, "try", "0", str(mib)], capture_output=True, text=True, timeout=30, env=env)
+    assert r.returncode == 0, r.stderr
+    lines = [json.loads(ln) for ln in r.stdout.splitlines()]
+    return lines[0]["rc"], lines[1]["free_mib"]
+
+
+def test_processes_of_a_container_share_one_grant():
+    """The grant is the container's: a second process gets what the first left
+    over, and a process that exits gives its bytes back."""
+    env = _env(f"share-{time.monotonic_ns()}")
+    a = _hold(env, 60)
+    try:
+        assert _try(env, 50) == (2, 40)  # refused: 60 of 100 held by the other process
+        assert _try(env, 40) == (0, 0)   # fits, and is given back when that process exits
+        assert _try(env, 40) == (0, 0)
+    finally:
+        a.stdin.close()
+        assert a.wait(10) == 0
+    assert _try(env, 90) == (0, 10)  # the holder exited normally: its 60 MiB are back
+
+
+def test_bytes_of_a_killed_process_are_reclaimed():
+    import signal
+    env = _env(f"kill-{time.monotonic_ns()}")
+    a = _hold(env, 60)
+    a.send_signal(signal.SIGKILL)
+    a.wait(10)
+    assert _try(env, 90) == (0, 10)  # the dead holder's slot was reclaimed on the refusal path
+
+
+def test_forked_child_draws_on_the_same_grant():
+    env = _env(f"fork-{time.monotonic_ns()}")
+    r = subprocess.run([CHECK, "fork", "60"], capture_output=True, text=True, timeout=30, env=env)
+    out = {d["step"]: d for d in map(json.loads, r.stdout.splitlines())}
+    assert out["parent malloc"]["rc"] == 0
+    assert out["child malloc full"]["rc"] == 2 and out["child malloc half"]["rc"] == 0
+    assert out["parent info after child"]["free_mib"] == 40  # the child's 30 MiB came back at its exit
+
+
+def test_other_grants_and_other_containers_are_separate():
+    key = f"sep-{time.monotonic_ns()}"
+    a = _hold(_env(key), 60)
+    try:
+        assert _try(_env(key + "-other"), 90) == (0, 10)  # another container
+        assert _try(_env(key, cap="200"), 150) == (0, 50)  # another grant
+    finally:
+        a.stdin.close()
+        a.wait(10)
 
 
 def test_shim_exports_hip_versioned_entry_points_only():
