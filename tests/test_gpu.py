@@ -286,6 +286,40 @@ def test_memcap_shim_enforces_the_grant_on_pytorch(scratch, snap):
         json.dump({"allocate_envs": envs, "result": out, "stderr_tail": r.stderr[-1500:]}, f, indent=1)
 
 
+def test_memcap_grant_is_shared_by_the_containers_processes():
+    """Two PyTorch processes of one container under one 4000 MiB grant: while
+    the first holds 3 GiB the second is refused 2 GiB; after the first exits
+    the second gets it."""
+    import subprocess
+    import sys
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    key = f"gputest-share-{os.getpid()}"
+    env = {**os.environ, "LD_PRELOAD": os.path.join(BUILD_DIR, "libadp_memcap.so"),
+           "AMD_GPU_MEMORY_LIMIT_MIB": "4000", "ADP_MEMCAP_KEY": key}
+    holder = subprocess.Popen([sys.executable, "-c",
+                               "import sys, torch\n"
+                               "x = torch.empty(3 << 30, dtype=torch.uint8, device='cuda')\n"
+                               "print('held', flush=True)\n"
+                               "sys.stdin.read()\n"], env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True)
+    try:
+        assert holder.stdout.readline().strip() == "held", holder.stderr.read()[-2000:]
+        probe = ("import torch\n"
+                 "try:\n"
+                 "    y = torch.empty(2 << 30, dtype=torch.uint8, device='cuda')\n"
+                 "    print('granted')\n"
+                 "except torch.OutOfMemoryError:\n"
+                 "    print('refused')\n")
+        r = subprocess.run([sys.executable, "-c", probe], env=env, capture_output=True, text=True, timeout=300)
+        assert r.stdout.strip() == "refused", r.stderr[-2000:]
+    finally:
+        holder.stdin.close()
+        holder.wait(60)
+    r = subprocess.run([sys.executable, "-c", probe], env=env, capture_output=True, text=True, timeout=300)
+    _drop_memcap_segments(key)
+    assert r.stdout.strip() == "granted", r.stderr[-2000:]
+
+
 def test_soft_partition_replica_on_mi355x(scratch, snap):
     """gpu:shared:4 with --replica-cu-mask --replica-hbm-share
     --enforce-memory-units: one replica is a soft partition -- a quarter of the
