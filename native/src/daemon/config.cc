@@ -142,6 +142,10 @@ const std::vector<FlagDef>& Table() {
        "fail Allocate() for a device currently advertised Unhealthy (default: allocate it and log a "
        "warning, as the reference does)",
        [](Flags& f) -> void* { return &f.reject_unhealthy; }},
+      {"prestart-health-check", "DP_PRESTART_HEALTH_CHECK", "prestartHealthCheck", Kind::kBool,
+       "ask the kubelet to call PreStartContainer before each container start and refuse the start when one "
+       "of the container's devices is Unhealthy at that moment (the reference's PreStartContainer is a no-op)",
+       [](Flags& f) -> void* { return &f.prestart_health_check; }},
       {"replica-hbm-share", "DP_REPLICA_HBM_SHARE", "replicaHbmShare", Kind::kBool,
        "time-slice replicas (replicas > 1) each hold 1/R of the device's HBM: Allocate() reports the grant "
        "like a memory unit's (AMD_GPU_MEMORY_LIMIT_MIB ...), and --enforce-memory-units caps it",

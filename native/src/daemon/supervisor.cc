@@ -135,6 +135,7 @@ Result<Validated> Validate(const Config& cfg) {
   v.popts.cdi_spec_dir = f.cdi_spec_dir;
   v.popts.reject_unhealthy = f.reject_unhealthy;
   v.popts.replica_hbm_share = f.replica_hbm_share;
+  v.popts.prestart_health_check = f.prestart_health_check;
   if (f.enforce_memory_units && MemcapSource(f).empty())
     return InvalidArgument("--enforce-memory-units: libadp_memcap.so not found (" +
                            (f.memcap_lib.empty() ? std::string("next to the binary or in /usr/lib/amdgpu-device-plugin")

@@ -275,7 +275,7 @@ Status Plugin::HandleGetOptions(std::string_view, std::string* resp) {
   // GPUs and partitions use the topology policy (server.go:243-248 offered it
   // only with a policy or replicas).
   pb::DevicePluginOptions o;
-  o.pre_start_required = false;
+  o.pre_start_required = opts_.prestart_health_check;
   o.get_preferred_allocation_available = true;
   pb::Encode(o, resp);
   return Status::Ok();
@@ -283,7 +283,25 @@ Status Plugin::HandleGetOptions(std::string_view, std::string* resp) {
 
 Status Plugin::HandlePreStart(std::string_view req, std::string*) {
   pb::PreStartContainerRequest r;
-  return pb::Decode(req, &r);
+  ADP_RETURN_IF_ERROR(pb::Decode(req, &r));
+  if (!opts_.prestart_health_check) return Status::Ok();  // the reference's no-op (server.go:356-358)
+  // --prestart-health-check: the kubelet asks right before it starts each
+  // container; a device that went Unhealthy since admission stops the start
+  // (the kubelet retries the container) instead of handing the workload a
+  // resetting or failed GPU.
+  auto law = CurrentLaw();
+  for (const auto& id : r.device_ids) {
+    auto it = advertised_index_.find(id);
+    if (it == advertised_index_.end())
+      return InvalidArgument("PreStartContainer for '" + spec_.resource_name + "': unknown device: " + id);
+    if (law->healthy[it->second]) continue;
+    stats_.prestart_refusals.Add(1);
+    LOG_WARN(kComp, "PreStartContainer '%s': device %s is Unhealthy; container start refused",
+             spec_.resource_name.c_str(), units_[it->second].id.c_str());
+    return FailedPrecondition("device " + units_[it->second].id + " of '" + spec_.resource_name +
+                              "' is Unhealthy; not starting the container on it");
+  }
+  return Status::Ok();
 }
 
 Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
@@ -569,6 +587,7 @@ Status Plugin::Register() {
   rr.resource_name = spec_.resource_name;
   rr.has_options = true;
   rr.options.get_preferred_allocation_available = true;
+  rr.options.pre_start_required = opts_.prestart_health_check;
   std::string resp;
   return (*ch)->Unary("/v1beta1.Registration/Register", pb::Encode(rr), &resp,
                       opts_.dial_timeout_ms);
@@ -831,6 +850,10 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
   for (auto* p : plugins)
     gauge("amdgpu_dp_unhealthy_allocations_total", res(p),
           static_cast<double>(p->stats_.unhealthy_allocations.Value()));
+  family("amdgpu_dp_prestart_refusals_total", "counter",
+         "Container starts refused because a device was Unhealthy (--prestart-health-check).");
+  for (auto* p : plugins)
+    gauge("amdgpu_dp_prestart_refusals_total", res(p), static_cast<double>(p->stats_.prestart_refusals.Value()));
   family("amdgpu_dp_handler_seconds", "histogram",
          "In-daemon handler time per RPC (request decode, device lookup, response encode).");
   for (auto* p : plugins) {

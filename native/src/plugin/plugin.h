@@ -99,6 +99,9 @@ struct PluginOptions {
   // Time-slice replicas also hold 1/R of the device's HBM each: Allocate()
   // reports it like a memory-unit grant (and --enforce-memory-units caps it).
   bool replica_hbm_share = false;
+  // Ask the kubelet for PreStartContainer and refuse to start a container on a
+  // device that is Unhealthy at that moment.
+  bool prestart_health_check = false;
   // Host path of the HBM-cap shim; non-empty: memory-unit resources mount it
   // read-only at kMemcapContainerPath and set LD_PRELOAD to it.
   std::string memcap_host_path;
@@ -154,6 +157,7 @@ struct RpcStats {
   metrics::MaxGauge preferred_ns_max;
   metrics::Counter law_sends;
   metrics::Counter unhealthy_allocations;  // Allocate() calls that named an Unhealthy device
+  metrics::Counter prestart_refusals;      // container starts refused by --prestart-health-check
   metrics::Histogram allocate_hist;   // handler time (decode + lookup + encode)
   metrics::Histogram preferred_hist;
 };

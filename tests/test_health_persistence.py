@@ -55,6 +55,7 @@ class Node:
 
     def first_law(self, timeout=10):
         reg = self.k.wait_registration(timeout)
+        self.reg = reg
         c = kubelet.PluginClient(os.path.join(self.scratch, reg.endpoint))
         q, call = c.watch()
         self.clients.append((c, call))
@@ -290,6 +291,36 @@ def test_allocate_of_unhealthy_device(mk, reject):
     n.inject("1 4 post-reset")
     n.wait_health(lambda h: h[ids[1]] == "Healthy")
     assert c.allocate([ids[1]]).container_responses
+
+
+@pytest.mark.parametrize("gate", [False, True])
+def test_prestart_health_check(mk, gate):
+    """--prestart-health-check: registration and GetDevicePluginOptions ask the
+    kubelet for PreStartContainer, which refuses a container whose device went
+    Unhealthy after admission (the kubelet retries the start); without the flag
+    PreStartContainer is the reference's no-op."""
+    n = mk(args=["--prestart-health-check"] if gate else [])
+    ids = sorted(n.start())
+    c = n.clients[-1][0]
+    assert c.options().pre_start_required is gate
+    assert n.reg.options.pre_start_required is gate
+    c.prestart([ids[0], ids[1]])  # all healthy: fine either way
+    n.inject("1 3 pre-reset")
+    n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+    c.prestart([ids[0]])
+    if gate:
+        with pytest.raises(grpc.RpcError) as e:
+            c.prestart([ids[0], ids[1]])
+        assert e.value.code() == grpc.StatusCode.FAILED_PRECONDITION and ids[1] in e.value.details()
+        with pytest.raises(grpc.RpcError) as e:
+            c.prestart(["no-such-device"])
+        assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+        n.d.wait_log(f"device {ids[1]} is Unhealthy; container start refused")
+    else:
+        c.prestart([ids[0], ids[1]])
+    n.inject("1 4 post-reset")
+    n.wait_health(lambda h: h[ids[1]] == "Healthy")
+    c.prestart([ids[0], ids[1]])
 
 
 def test_operator_clears_a_gpu_from_the_state_file_and_sighups(mk, scratch):
