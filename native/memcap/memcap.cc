@@ -37,7 +37,6 @@
 #include <cstring>
 #include <algorithm>
 #include <mutex>
-#include <new>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -223,10 +222,16 @@ void AttachShared(State& s) {
   }
 }
 
+// fork(): the state is locked across it, so the child never sees the map or
+// the counters half-updated by another thread.
+void AtForkPrepare() { S().mu.lock(); }
+void AtForkParent() { S().mu.unlock(); }
+
 void AtForkChild() {
   // The child holds no device memory of its own yet: fresh local state, own slot.
   State& s = S();
-  new (&s.mu) std::mutex();
+  s.mu.unlock();
+  std::lock_guard<std::mutex> lk(s.mu);
   s.allocs.clear();
   for (auto& u : s.local_used) u = 0;
   s.released = false;
@@ -275,7 +280,7 @@ State& S() {
       std::lock_guard<std::mutex> lk(st->mu);
       AttachShared(*st);
     }
-    pthread_atfork(nullptr, nullptr, AtForkChild);
+    pthread_atfork(AtForkPrepare, AtForkParent, AtForkChild);
     atexit(ReleaseSlot);
     return st;
   }();
