@@ -88,6 +88,22 @@ def test_health_state_can_be_turned_off():
     assert "health-state" not in {v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]}
 
 
+def test_sharing_and_health_gate_switches():
+    """enforceMemoryUnits / replicaHbmShare / prestartHealthCheck reach the
+    daemon; the shim is installed under the device-plugin dir, which must be
+    mounted at its host path (the runtime bind-mounts that host path into pods)."""
+    ds = daemonset({"enforceMemoryUnits": True, "replicaHbmShare": True, "prestartHealthCheck": True})
+    check_consistent(ds)
+    e = env(ds)
+    assert e["DP_ENFORCE_MEMORY_UNITS"] == "true" and e["DP_REPLICA_HBM_SHARE"] == "true"
+    assert e["DP_PRESTART_HEALTH_CHECK"] == "true"
+    vols = {v["name"]: v for v in ds["spec"]["template"]["spec"]["volumes"]}
+    (dp,) = [m for m in container(ds)["volumeMounts"] if m["mountPath"] == "/var/lib/kubelet/device-plugins"]
+    assert vols[dp["name"]]["hostPath"]["path"] == dp["mountPath"]
+    off = env(daemonset())
+    assert off["DP_ENFORCE_MEMORY_UNITS"] == "false" and off["DP_PRESTART_HEALTH_CHECK"] == "false"
+
+
 def test_metrics_and_node_feature_labels():
     ds = daemonset({"metrics": {"enabled": True, "port": 9500}, "nodeFeatureLabels": {"enabled": True}})
     check_consistent(ds)
