@@ -56,6 +56,20 @@ def build_probe(arch: str = "gfx950") -> str:
     return PROBE_LIB
 
 
+MEMCAP_BENCH_SRC = os.path.join(NATIVE_SRC, "memcap", "memcap_bench.cpp")
+MEMCAP_BENCH = os.path.join(PROBE_DIR, "amdgpu-dp-memcap-bench")
+
+
+def build_memcap_bench() -> str:
+    """HIP host program timing the allocation path with / without the HBM-cap shim."""
+    os.makedirs(PROBE_DIR, exist_ok=True)
+    if os.path.exists(MEMCAP_BENCH) and os.path.getmtime(MEMCAP_BENCH) >= os.path.getmtime(MEMCAP_BENCH_SRC):
+        return MEMCAP_BENCH
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    _run([hipcc, "-O2", "-std=c++17", "-Wall", "-o", MEMCAP_BENCH, MEMCAP_BENCH_SRC])
+    return MEMCAP_BENCH
+
+
 def build_descriptor() -> str:
     """protoc --descriptor_set_out for the kubelet API (used by the grpcio stub)."""
     if os.path.exists(DESCRIPTOR) and os.path.getmtime(DESCRIPTOR) >= os.path.getmtime(PROTO_SRC):
@@ -78,6 +92,7 @@ def build_all(probe: bool = True) -> None:
     build_descriptor()
     if probe:
         build_probe()
+        build_memcap_bench()
 
 
 if __name__ == "__main__":

@@ -219,6 +219,12 @@ def test_memory_unit_grant_caps_pytorch(scratch, snap):
     assert r.stdout.strip().endswith("CAPPED") and "NOT" not in r.stdout
 
 
+def _with_preload(lib):
+    """LD_PRELOAD for a child: the shim after whatever this environment already
+    preloads (a pod has nothing there; a test host's own preloads stay)."""
+    return " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), lib) if x)
+
+
 def _drop_memcap_segments(key):
     import glob
     for f in glob.glob(f"/dev/shm/adp-memcap-key-{key}-*"):
@@ -252,7 +258,7 @@ def test_memcap_shim_enforces_the_grant_on_pytorch(scratch, snap):
     assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "4000" and envs["AMD_GPU_MEMORY_FRACTION"] == "1.0000"
     (mount,) = [m for m in resp.mounts if m.container_path == envs["LD_PRELOAD"]]
     assert mount.read_only and os.path.exists(mount.host_path)
-    envs["LD_PRELOAD"] = mount.host_path  # what the bind mount gives the container
+    envs["LD_PRELOAD"] = _with_preload(mount.host_path)  # what the bind mount gives the container
     envs["ADP_MEMCAP_KEY"] = f"gputest-{os.getpid()}"  # the container's budget, named so it can be removed
     code = (
         "import json, os, torch\n"
@@ -294,7 +300,7 @@ def test_memcap_grant_is_shared_by_the_containers_processes():
     import sys
     from k8s_gpu_sharing_plugin_amd import BUILD_DIR
     key = f"gputest-share-{os.getpid()}"
-    env = {**os.environ, "LD_PRELOAD": os.path.join(BUILD_DIR, "libadp_memcap.so"),
+    env = {**os.environ, "LD_PRELOAD": _with_preload(os.path.join(BUILD_DIR, "libadp_memcap.so")),
            "AMD_GPU_MEMORY_LIMIT_MIB": "4000", "ADP_MEMCAP_KEY": key}
     holder = subprocess.Popen([sys.executable, "-c",
                                "import sys, torch\n"
@@ -345,7 +351,7 @@ def test_soft_partition_replica_on_mi355x(scratch, snap):
     envs = dict(resp.envs)
     quarter = snap["gpus"][0]["vram_mib"] // 4
     assert envs["HSA_CU_MASK"] == "0:64-127" and envs["AMD_GPU_MEMORY_LIMIT_MIB"] == str(quarter)
-    envs["LD_PRELOAD"] = resp.mounts[0].host_path
+    envs["LD_PRELOAD"] = _with_preload(resp.mounts[0].host_path)
     envs["ADP_MEMCAP_KEY"] = f"gputest-soft-{os.getpid()}"
     code = ("import json, torch\n"
             "free, total = torch.cuda.mem_get_info(0)\n"

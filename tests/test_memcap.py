@@ -21,6 +21,8 @@ from k8s_gpu_sharing_plugin_amd import BUILD_DIR
 from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
 
 SHIM = os.path.join(BUILD_DIR, "libadp_memcap.so")
+# The shim after whatever this environment already preloads.
+PRELOAD = " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), SHIM) if x)
 CHECK = os.path.join(BUILD_DIR, "adp_memcap_check")
 
 
@@ -48,7 +50,7 @@ def test_without_the_shim_nothing_is_capped():
 
 
 def test_caps_per_device_in_hip_order():
-    out, err = _run({"LD_PRELOAD": SHIM, "AMD_GPU_MEMORY_LIMIT_MIB": "100,50"})
+    out, err = _run({"LD_PRELOAD": PRELOAD, "AMD_GPU_MEMORY_LIMIT_MIB": "100,50"})
     oom = 2  # hipErrorOutOfMemory
     # device 0: 100 MiB
     assert out["d0 malloc 60"]["rc"] == 0
@@ -75,13 +77,13 @@ def test_accounting_is_exact_under_concurrent_allocations():
     """8 threads x 20k sync / stream-ordered allocations and frees against a
     40 MiB cap (one thread alone holds more than that): some are refused, and
     when all is freed the whole cap is free."""
-    out, _ = _run({"LD_PRELOAD": SHIM, "AMD_GPU_MEMORY_LIMIT_MIB": "40"}, "stress")
+    out, _ = _run({"LD_PRELOAD": PRELOAD, "AMD_GPU_MEMORY_LIMIT_MIB": "40"}, "stress")
     assert out["stress"]["granted"] > 1000 and out["stress"]["refused"] > 100
     assert (out["stress info"]["free_mib"], out["stress info"]["total_mib"]) == (40, 40)
 
 
 def _env(key, cap="100"):
-    return dict(os.environ, LD_PRELOAD=SHIM, AMD_GPU_MEMORY_LIMIT_MIB=cap, ADP_MEMCAP_KEY=key)
+    return dict(os.environ, LD_PRELOAD=PRELOAD, AMD_GPU_MEMORY_LIMIT_MIB=cap, ADP_MEMCAP_KEY=key)
 
 
 def _hold(env, mib):
