@@ -480,7 +480,9 @@ Status Plugin::HandlePreferred(std::string_view req, std::string* resp) {
 }
 
 Status Plugin::PreferredImpl(std::string_view req, std::string* resp) {
-  std::vector<pb::ContainerPreferredAllocationRequestView> reqs;
+  // Per loop thread, kept across calls: a memory-unit request names every free
+  // unit of the node (2,352 IDs on 8 MI355X), decoded into reused capacity.
+  static thread_local std::vector<pb::ContainerPreferredAllocationRequestView> reqs;
   ADP_RETURN_IF_ERROR(pb::DecodeView(req, &reqs));
   pb::PreferredAllocationResponse out;
   stats_.preferred_calls.Add(1);

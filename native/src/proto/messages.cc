@@ -354,17 +354,34 @@ bool ReadView(Reader& r, WireType wt, std::vector<std::string_view>* v) {
 }  // namespace
 
 Status DecodeView(std::string_view b, std::vector<ContainerPreferredAllocationRequestView>* m) {
-  m->clear();
-  return ForEachField(b, "PreferredAllocationRequest", [&](uint32_t f, WireType wt, Reader& r) {
+  // Elements already in *m are reused with their capacity (a caller that keeps
+  // the vector across calls decodes 2,352-ID requests without touching malloc).
+  size_t n = 0;
+  Status st = ForEachField(b, "PreferredAllocationRequest", [&](uint32_t f, WireType wt, Reader& r) {
     if (f != 1) return r.Skip(wt);
     if (wt != kLen) return false;
     std::string_view c;
     if (!r.ReadLen(&c)) return false;
-    m->emplace_back();
-    auto& cr = m->back();
-    // One growth step up front: each entry is >= 2 wire bytes plus its ID,
-    // and device IDs are rarely shorter than 16 bytes.
-    cr.available.reserve(c.size() / 18 + 1);
+    if (n == m->size()) m->emplace_back();
+    auto& cr = (*m)[n++];
+    cr.available.clear();
+    cr.must_include.clear();
+    cr.allocation_size = 0;
+    // One growth step up front, sized from the first entry (tag + length + ID;
+    // the kubelet's IDs of one resource have one shape).
+    size_t first = c.size() >= 2 ? static_cast<uint8_t>(c[1]) : 0;
+    if (c.size() >= 2 && c[0] == 0x0a && first < 0x80) cr.available.reserve(c.size() / (2 + first + (first == 0)) + 1);
+    // Fast path: the run of available_deviceIDs (field 1, length < 128) the
+    // kubelet writes first -- two header bytes per ID, no varint loop.
+    const char* p = c.data();
+    const char* end = p + c.size();
+    while (end - p >= 2 && p[0] == 0x0a && !(static_cast<uint8_t>(p[1]) & 0x80)) {
+      size_t len = static_cast<uint8_t>(p[1]);
+      if (static_cast<size_t>(end - p - 2) < len) return false;
+      cr.available.emplace_back(p + 2, len);
+      p += 2 + len;
+    }
+    c.remove_prefix(static_cast<size_t>(p - c.data()));
     return ForEachField(c, "ContainerPreferredAllocationRequest", [&](uint32_t cf, WireType cwt, Reader& cr_r) {
              if (cf == 1) return ReadView(cr_r, cwt, &cr.available);
              if (cf == 2) return ReadView(cr_r, cwt, &cr.must_include);
@@ -378,6 +395,8 @@ Status DecodeView(std::string_view b, std::vector<ContainerPreferredAllocationRe
              return cr_r.Skip(cwt);
            }).ok();
   });
+  m->resize(n);
+  return st;
 }
 
 Status DecodeView(std::string_view b, std::vector<std::vector<std::string_view>>* m) {
