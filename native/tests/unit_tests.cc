@@ -206,6 +206,71 @@ static void TestProto() {
   CHECK(!pb::Decode(std::string("\x0a\x05\x0a\x09", 4), &bad).ok());  // truncated
 }
 
+// DecodeView (zero-copy, fast path over the run of available IDs, reused
+// capacity) against the owning Decode: random requests -- IDs of 0..200 bytes
+// (two-byte and three-byte headers), must_include before or after, several
+// container requests -- and random corruptions of them.
+static void TestPreferredViewFuzz() {
+  g_case = "proto/preferred-view-differential";
+  uint64_t seed = 0x2545f4914f6cdd1dull;
+  auto rnd = [&](uint64_t n) {
+    seed ^= seed << 13;
+    seed ^= seed >> 7;
+    seed ^= seed << 17;
+    return n ? seed % n : 0;
+  };
+  std::vector<pb::ContainerPreferredAllocationRequestView> views;  // reused across iterations
+  int agreed = 0, rejected = 0;
+  for (int it = 0; it < 4000; ++it) {
+    pb::PreferredAllocationRequest pr;
+    int ncr = 1 + static_cast<int>(rnd(3));
+    for (int c = 0; c < ncr; ++c) {
+      pb::ContainerPreferredAllocationRequest cr;
+      int n = static_cast<int>(rnd(60));
+      for (int i = 0; i < n; ++i) cr.available.push_back(std::string(rnd(8) ? 20 + rnd(60) : rnd(201), 'a' + rnd(26)));
+      for (int i = 0, m = static_cast<int>(rnd(3)); i < m; ++i) cr.must_include.push_back(std::string(1 + rnd(40), 'x'));
+      cr.allocation_size = static_cast<int32_t>(rnd(9)) - 1;
+      pr.container_requests.push_back(std::move(cr));
+    }
+    std::string b = pb::Encode(pr);
+    if (rnd(4) == 0) {  // must_include first: re-encode the fields of the first request in the other order
+      std::string c0, rest;
+      for (const auto& id : pr.container_requests[0].must_include) pb::PutLen(&c0, 2, id);
+      for (const auto& id : pr.container_requests[0].available) pb::PutLen(&c0, 1, id);
+      pb::PutInt32(&c0, 3, pr.container_requests[0].allocation_size);
+      pb::PutLen(&rest, 1, c0);
+      for (size_t c = 1; c < pr.container_requests.size(); ++c) {
+        pb::PreferredAllocationRequest one;
+        one.container_requests.push_back(pr.container_requests[c]);
+        rest += pb::Encode(one);
+      }
+      b = rest;
+    }
+    if (rnd(3) == 0 && !b.empty()) {  // corrupt: flip, truncate or extend
+      switch (rnd(3)) {
+        case 0: b[rnd(b.size())] ^= static_cast<char>(1 + rnd(255)); break;
+        case 1: b.resize(rnd(b.size())); break;
+        default: b += std::string(1 + rnd(4), static_cast<char>(rnd(256)));
+      }
+    }
+    pb::PreferredAllocationRequest owned;
+    bool ok_owned = pb::Decode(b, &owned).ok();
+    bool ok_view = pb::DecodeView(b, &views).ok();
+    CHECK(ok_owned == ok_view);
+    if (!ok_owned) { ++rejected; continue; }
+    CHECK(views.size() == owned.container_requests.size());
+    for (size_t c = 0; c < views.size() && c < owned.container_requests.size(); ++c) {
+      const auto& o = owned.container_requests[c];
+      const auto& v = views[c];
+      CHECK(v.allocation_size == o.allocation_size);
+      CHECK(std::vector<std::string>(v.available.begin(), v.available.end()) == o.available);
+      CHECK(std::vector<std::string>(v.must_include.begin(), v.must_include.end()) == o.must_include);
+    }
+    ++agreed;
+  }
+  CHECK(agreed > 1000 && rejected > 100);
+}
+
 // The original map/set implementation of the hierarchical (partition) policy,
 // kept as the oracle for the flat-array one in alloc/topology.cc.
 static std::vector<int> OracleHierarchical(const alloc::DeviceGraph& g, const std::vector<int>& avail,
@@ -856,6 +921,7 @@ int main() {
   TestGrpcLoopback(true);
   TestGrpcLoopback(false);
   TestH2Fuzz();
+  TestPreferredViewFuzz();
   TestGrpcMultiLoop();
   printf("%d checks, %d failed\n", g_checks, g_failed);
   return g_failed ? 1 : 0;
