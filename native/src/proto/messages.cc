@@ -370,7 +370,8 @@ Status DecodeView(std::string_view b, std::vector<ContainerPreferredAllocationRe
     // One growth step up front, sized from the first entry (tag + length + ID;
     // the kubelet's IDs of one resource have one shape).
     size_t first = c.size() >= 2 ? static_cast<uint8_t>(c[1]) : 0;
-    if (c.size() >= 2 && c[0] == 0x0a && first < 0x80) cr.available.reserve(c.size() / (2 + first + (first == 0)) + 1);
+    if (c.size() >= 2 && c[0] == 0x0a && first < 0x80)  // bounded: a tiny first ID must not pin megabytes
+      cr.available.reserve(std::min<size_t>(c.size() / (2 + first + (first == 0)) + 1, 16384));
     // Fast path: the run of available_deviceIDs (field 1, length < 128) the
     // kubelet writes first -- two header bytes per ID, no varint loop.
     const char* p = c.data();
