@@ -1,6 +1,7 @@
 #include "proto/messages.h"
 
 #include "proto/wire.h"
+#include <algorithm>
 
 namespace adp::pb {
 namespace {
