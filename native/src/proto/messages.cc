@@ -1,7 +1,8 @@
 #include "proto/messages.h"
 
-#include "proto/wire.h"
 #include <algorithm>
+
+#include "proto/wire.h"
 
 namespace adp::pb {
 namespace {
