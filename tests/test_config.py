@@ -267,3 +267,19 @@ def _write(scratch, body):
 def test_numbers_are_accepted_for_string_settings(scratch):
     f = effective_config(scratch, file_body="version: v1\nflags:\n  devices: 0\n  resourcePrefix: 1.5\n")
     assert f["devices"] == "0" and f["resourcePrefix"] == "1.5"
+
+
+def test_sharing_and_health_gate_settings_from_file_and_env(scratch):
+    """The round-2 settings have file keys and env names like every other flag
+    (the memcap library must exist for enforcement to validate)."""
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    shim = os.path.join(BUILD_DIR, "libadp_memcap.so")
+    body = f"""
+version: v1
+flags: {{enforceMemoryUnits: true, memcapLib: "{shim}", replicaHbmShare: yes, prestartHealthCheck: true}}
+"""
+    f = effective_config(scratch, file_body=body)
+    assert f["enforceMemoryUnits"] is True and f["memcapLib"] == shim
+    assert f["replicaHbmShare"] is True and f["prestartHealthCheck"] is True
+    f = effective_config(scratch, env={"DP_PRESTART_HEALTH_CHECK": "true", "DP_REPLICA_HBM_SHARE": "false"})
+    assert f["prestartHealthCheck"] is True and f["replicaHbmShare"] is False and f["enforceMemoryUnits"] is False
