@@ -96,6 +96,21 @@ struct PhysicalPool {
     allocated = true;
     return replicas[head++];
   }
+  // The n smallest remaining replicas, in order -- what n TakeAny() calls
+  // return -- with one partial sort instead of growing chunks.
+  size_t TakeSmallest(size_t n, std::vector<std::string_view>* out) {
+    n = std::min(n, size());
+    if (n == 0) return 0;
+    if (sorted_upto < head + n) {
+      std::partial_sort(replicas.begin() + head, replicas.begin() + head + n, replicas.end(),
+                        [this](std::string_view a, std::string_view b) { return Less(a, b); });
+      sorted_upto = head + n;
+    }
+    allocated = true;
+    out->insert(out->end(), replicas.begin() + head, replicas.begin() + head + n);
+    head += n;
+    return n;
+  }
 };
 
 std::string MissingMsg(std::string_view id) {
@@ -230,12 +245,8 @@ Result<Prioritized> PrioritizeDeviceViews(const std::vector<std::string_view>& a
     // Pack: finish on devices this request already touches, then best-fit the
     // remainder onto as few untouched devices as possible.
     int need = allocation_size - static_cast<int>(chosen.size());
-    for (PhysicalPool* p : order) {
-      while (need > 0 && p->allocated && p->size() > 0) {
-        chosen.push_back(p->TakeAny());
-        --need;
-      }
-    }
+    for (PhysicalPool* p : order)
+      if (need > 0 && p->allocated) need -= static_cast<int>(p->TakeSmallest(static_cast<size_t>(need), &chosen));
     while (need > 0) {
       // With devices already in the request, only the closest untouched ones
       // compete (NUMA/xGMI affinity); among those: best fit, else the largest.
@@ -265,10 +276,7 @@ Result<Prioritized> PrioritizeDeviceViews(const std::vector<std::string_view>& a
       }
       PhysicalPool* pick = fit ? fit : largest;
       if (!pick) return FailedPrecondition("no devices left to allocate");
-      while (need > 0 && pick->size() > 0) {
-        chosen.push_back(pick->TakeAny());
-        --need;
-      }
+      need -= static_cast<int>(pick->TakeSmallest(static_cast<size_t>(need), &chosen));
     }
   }
   std::sort(chosen.begin(), chosen.end());

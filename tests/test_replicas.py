@@ -161,3 +161,74 @@ def test_prioritize_matches_reference_model_on_random_and_adversarial_ids():
             continue
         ids, nu = native.prioritize(avail, must, size)
         assert (ids, nu) == (want, want_nu), (trial, avail, must, size)
+
+
+def _pack_model(avail, must, size, join="-replica-"):
+    """Executable model of the pack policy (no topology affinity): must-includes
+    as in the reference, then finish on the devices the request already touches
+    (sorted key order), then best fit -- the smallest untouched device that
+    holds the rest, else the largest -- taking each device's smallest IDs."""
+    pools = {}
+    for i in avail:
+        pools.setdefault(i.split(join)[0], []).append(i)
+    for v in pools.values():
+        v.sort()
+    used, out = set(), list(must)
+    for m in must:
+        dev = m.split(join)[0]
+        if dev not in pools or m not in pools[dev]:
+            return None
+        lst = pools[dev]
+        k = lst.index(m)
+        lst[k] = lst[-1]
+        lst.pop()
+        used.add(dev)
+    need = size - len(out)
+
+    def take(dev, n):
+        got = pools[dev][:n]
+        del pools[dev][:n]
+        out.extend(got)
+        used.add(dev)
+        return len(got)
+    for dev in sorted(pools):
+        if need > 0 and dev in used:
+            need -= take(dev, need)
+    while need > 0:
+        fit = largest = None
+        for dev in sorted(pools):
+            n = len(pools[dev])
+            if dev in used or n == 0:
+                continue
+            if n >= need and (fit is None or n < len(pools[fit])):
+                fit = dev
+            if largest is None or n > len(pools[largest]):
+                largest = dev
+        pick = fit if fit is not None else largest
+        if pick is None:
+            return None
+        need -= take(pick, need)
+    return sorted(out)
+
+
+def test_pack_matches_its_model_on_random_ids():
+    """Randomised differential test of the pack policy (one partial sort per
+    device taken from) against the model above."""
+    import random
+    rng = random.Random(11)
+    stems = ["a", "b", "c", "x-replica", "75a30000-0000-1000-80c0-bf9907890000", "r-"]
+    for trial in range(400):
+        avail = []
+        for s in rng.sample(stems, rng.randint(1, len(stems))):
+            avail += [f"{s}-replica-{i}" for i in rng.sample(range(40), rng.randint(0, 12))]
+        avail = list(dict.fromkeys(avail))
+        rng.shuffle(avail)
+        must = rng.sample(avail, min(len(avail), rng.randint(0, 2)))
+        size = rng.randint(len(must), len(must) + 20)
+        want = _pack_model(avail, must, size)
+        if want is None:
+            with pytest.raises(native.NativeError):
+                native.prioritize(avail, must, size, policy="pack")
+            continue
+        ids, _ = native.prioritize(avail, must, size, policy="pack")
+        assert ids == want, (trial, avail, must, size)
