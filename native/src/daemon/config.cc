@@ -111,11 +111,13 @@ const std::vector<FlagDef>& Table() {
        "directory for the generated CDI spec (cdi-annotations / cdi-cri strategies)",
        [](Flags& f) -> void* { return &f.cdi_spec_dir; }},
       {"server-threads", "DP_SERVER_THREADS", "serverThreads", Kind::kUint,
-       "gRPC loop threads per plugin socket (0 = min(8, CPUs))",
+       "gRPC loop threads per plugin socket (0 = the CPU budget -- affinity mask and cgroup CPU quota -- "
+       "rounded up, at most 8)",
        [](Flags& f) -> void* { return &f.server_threads; }, true},
       {"busy-poll-us", "DP_BUSY_POLL_US", "busyPollUs", Kind::kUint,
        "after serving a request a gRPC loop polls without sleeping for this many "
-       "microseconds, so follow-up calls skip a scheduler wake-up (0 = always sleep)",
+       "microseconds, so follow-up calls skip a scheduler wake-up (0 = always sleep; off under a CPU "
+       "budget below 2 CPUs)",
        [](Flags& f) -> void* { return &f.busy_poll_us; }, true},
       {"http2-server", "DP_HTTP2_SERVER", "http2Server", Kind::kString,
        "HTTP/2 engine of the plugin sockets: [native | nghttp2] (native: hand-written framing "

@@ -1,10 +1,12 @@
 #include "plugin/plugin.h"
 
 #include <errno.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <cmath>
 #include <tuple>
 #include <set>
 #include <map>
@@ -88,9 +90,38 @@ std::vector<std::pair<uint32_t, uint32_t>> MemoryUnitCuRanges(uint32_t cus, uint
   return out;
 }
 
+double CpuBudget() {
+  // The affinity mask first (taskset, cpuset cgroups)...
+  cpu_set_t set;
+  double cpus = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set)
+                                                              : std::max(1u, std::thread::hardware_concurrency());
+  // ... then a CFS quota: a DaemonSet with resources.limits.cpu. cgroup v2
+  // "cpu.max" is "<quota> <period>" or "max <period>"; v1 splits it in two files.
+  const char* env = getenv("ADP_CGROUP_ROOT");  // tests point this at a fake tree
+  std::string root = env && *env ? env : "/sys/fs/cgroup";
+  double quota = 0;
+  if (FILE* f = fopen((root + "/cpu.max").c_str(), "r")) {
+    char q[32] = {0};
+    unsigned long long period = 0;
+    if (fscanf(f, "%31s %llu", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0)
+      quota = strtod(q, nullptr) / static_cast<double>(period);
+    fclose(f);
+  } else if (FILE* fq = fopen((root + "/cpu/cpu.cfs_quota_us").c_str(), "r")) {
+    long long q = -1, period = 0;
+    if (fscanf(fq, "%lld", &q) != 1) q = -1;
+    fclose(fq);
+    if (FILE* fp = fopen((root + "/cpu/cpu.cfs_period_us").c_str(), "r")) {
+      if (fscanf(fp, "%lld", &period) != 1) period = 0;
+      fclose(fp);
+    }
+    if (q > 0 && period > 0) quota = static_cast<double>(q) / static_cast<double>(period);
+  }
+  return quota > 0 ? std::min(cpus, quota) : cpus;
+}
+
 int DefaultServerThreads() {
-  unsigned n = std::thread::hardware_concurrency();
-  return static_cast<int>(std::clamp(n, 1u, 8u));
+  double budget = CpuBudget();
+  return static_cast<int>(std::clamp(std::ceil(budget), 1.0, 8.0));
 }
 
 const char* DeviceIdStrategyName(DeviceIdStrategy s) {
@@ -606,7 +637,16 @@ Status Plugin::Start(std::function<void()> on_fatal) {
   auto srv = std::make_unique<grpc::Server>(spec_.resource_name, threads);
   law_streams_.assign(threads, {});
   srv->set_trace(opts_.trace);
-  srv->set_busy_poll_us(opts_.busy_poll_us);
+  int spin = opts_.busy_poll_us;
+  if (double budget = CpuBudget(); budget < 2 && spin > 0) {
+    // Under a CPU quota below two CPUs a spinning loop only burns the quota
+    // and gets the process throttled: block in epoll_wait instead.
+    static std::atomic<bool> logged{false};
+    if (!logged.exchange(true))
+      LOG_INFO(kComp, "CPU budget %.2f CPUs: busy-poll off, %d gRPC loop(s) per socket", budget, threads);
+    spin = 0;
+  }
+  srv->set_busy_poll_us(spin);
   srv->set_native_http2(opts_.native_http2);
   srv->set_follow_peer_l3(opts_.follow_peer_l3);
   srv->AddUnary(std::string(kSvc) + "GetDevicePluginOptions",

@@ -126,6 +126,11 @@ std::vector<std::pair<uint32_t, uint32_t>> MemoryUnitCuRanges(uint32_t cus, uint
 
 // min(8, online CPUs): one loop per GPU of an 8-GPU node. Idle loops sit in
 // epoll_wait and cost no CPU; they only matter under concurrent clients.
+// CPUs this process may use: its affinity mask, bounded by a cgroup CPU quota
+// (cgroup v2 cpu.max / v1 cfs quota; fractional).
+double CpuBudget();
+// gRPC loops per plugin socket when --server-threads is 0: the CPU budget
+// rounded up, at most 8.
 int DefaultServerThreads();
 
 // One allocatable device (whole GPU or partition) after snapshot resolution.

@@ -227,6 +227,29 @@ def test_dry_run_flags_config_that_cannot_work(scratch, rc, needle):
     assert "matches no resource" not in ok.stdout + ok.stderr and "4 MiB" not in ok.stdout + ok.stderr
 
 
+@pytest.mark.parametrize("cpu_max,threads,spin", [("50000 100000", 1, False), ("300000 100000", 3, True),
+                                                   ("max 100000", None, True)])
+def test_cpu_limit_sizes_loops_and_busy_poll(scratch, tmp_path, cpu_max, threads, spin):
+    """A DaemonSet with resources.limits.cpu: the default loop count follows the
+    cgroup CPU quota, and below 2 CPUs the loops block instead of spinning."""
+    import json
+    import signal
+    (tmp_path / "cpu.max").write_text(cpu_max + "\n")
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, env={"ADP_CGROUP_ROOT": str(tmp_path)}).start()
+    try:
+        k.wait_registration()
+        d.signal(signal.SIGUSR1)
+        text = d.wait_log("stats: {")
+        stats = json.loads([ln for ln in text.splitlines() if "stats: {" in ln][-1].split("stats: ", 1)[1])
+        want = threads if threads is not None else min(8, len(os.sched_getaffinity(0)))
+        assert stats["server_threads"] == want
+        assert ("busy-poll off" in text) is (not spin)
+    finally:
+        d.stop()
+        k.stop()
+
+
 def test_sigusr1_dumps_stats(scratch):
     k = kubelet.StubKubelet(sock(scratch)).start()
     d = harness.Daemon(scratch).start()
