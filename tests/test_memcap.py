@@ -211,6 +211,23 @@ def test_shim_reinstalled_when_its_directory_is_wiped(scratch):
         k.stop()
 
 
+@pytest.mark.parametrize("extra", [["--device-list-strategy", "volume-mounts"],
+                                   ["--device-list-strategy", "cdi-annotations"],
+                                   ["--device-list-strategy", "cdi-cri"],
+                                   ["--device-id-strategy", "index"]])
+def test_shim_with_every_device_list_and_id_strategy(tmp_path, extra):
+    d = str(tmp_path / "dp")
+    os.makedirs(d)
+    args = [*extra, "--cdi-spec-dir", str(tmp_path / "cdi")]
+    resp, _ = _allocate(d, "gpu:gpu-mem-gb:-1", args)
+    envs = dict(resp.envs)
+    assert envs["LD_PRELOAD"] == "/usr/local/lib/amdgpu-dp/libadp_memcap.so"
+    assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "3000"
+    shim = [m for m in resp.mounts if m.container_path == envs["LD_PRELOAD"]]
+    assert len(shim) == 1 and shim[0].read_only and shim[0].host_path.endswith("amdgpu-dp/libadp_memcap.so")
+    assert any(dev.container_path == "/dev/kfd" for dev in resp.devices)
+
+
 def test_time_slice_pods_do_not_get_the_shim(scratch):
     resp, _ = _allocate(scratch, "gpu:shared:4")
     assert "LD_PRELOAD" not in dict(resp.envs) and not list(resp.mounts)
