@@ -15,48 +15,122 @@
 // Caps: AMD_GPU_MEMORY_LIMIT_MIB="<mib>[,<mib>...]", one per device in the
 // container's HIP order (the plugin writes it in that order); devices past the
 // list are not capped. The grant is the container's: its processes share the
-// counters (POSIX shared memory, see AttachShared). ADP_MEMCAP_VERBOSE=1 logs
-// every decision to stderr.
+// counters (a shared-memory segment, see AttachShared). ADP_MEMCAP_VERBOSE=1
+// logs every decision to stderr.
 //
-// No link-time dependency on libamdhip64: the real entry points are resolved
-// lazily (RTLD_NEXT, else the already-loaded libamdhip64). The exported
-// symbols carry libamdhip64's version nodes (memcap.map).
+// It has to load into whatever the workload's image is -- PyTorch-ROCm wheels
+// target glibc 2.28 -- so it needs nothing but old libc symbols: no libstdc++
+// runtime (no allocation through operator new, no std::mutex / std::string /
+// containers, no guarded statics), libc entry points pinned to their
+// GLIBC_2.2.5 versions where newer glibc re-versioned them, and no link-time
+// dependency on libamdhip64 (the real entry points are resolved lazily:
+// RTLD_NEXT, else the already-loaded libamdhip64). The exported symbols carry
+// libamdhip64's version nodes (memcap.map). tests/test_memcap.py checks the
+// imported symbol versions.
 #include <dlfcn.h>
+#include <errno.h>
 #include <fcntl.h>
-#include <signal.h>
-#include <sys/mman.h>
-#include <sys/stat.h>
-#include <unistd.h>
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
+#include <signal.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <atomic>
-#include <cstdarg>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <algorithm>
-#include <mutex>
-#include <string>
-#include <unordered_map>
-#include <vector>
+
+// glibc 2.34 moved these into libc under new default versions; bind the
+// original ones, which every glibc since 2.2.5 exports.
+__asm__(".symver dlsym,dlsym@GLIBC_2.2.5");
+__asm__(".symver dlopen,dlopen@GLIBC_2.2.5");
+__asm__(".symver pthread_once,pthread_once@GLIBC_2.2.5");
 
 namespace {
 
 constexpr int kMaxDevices = 64;
 
-struct Alloc {
-  int device;
-  size_t bytes;
+template <typename T>
+T Min(T a, T b) {
+  return a < b ? a : b;
+}
+
+// ---- the process-local table: device pointer / VMM handle -> owner ---------
+// Open addressing over calloc'd memory (no operator new: see the file comment).
+struct Entry {
+  const void* key;  // nullptr = empty, Tomb() = erased
+  int32_t device;
+  uint64_t bytes;
+};
+inline const void* Tomb() { return reinterpret_cast<const void*>(uintptr_t{1}); }  // not a constant expression
+
+struct Table {
+  Entry* e = nullptr;
+  size_t cap = 0, used = 0, tombs = 0;  // used counts live entries
+
+  static size_t Hash(const void* k, size_t cap) {
+    return static_cast<size_t>((reinterpret_cast<uintptr_t>(k) >> 4) * 0x9E3779B97F4A7C15ull) & (cap - 1);
+  }
+  Entry* Find(const void* k) {
+    if (!cap) return nullptr;
+    for (size_t i = Hash(k, cap), n = 0; n < cap; i = (i + 1) & (cap - 1), ++n) {
+      if (e[i].key == k) return &e[i];
+      if (!e[i].key) return nullptr;
+    }
+    return nullptr;
+  }
+  bool Grow() {
+    size_t ncap = cap ? cap * 2 : 1024;
+    Entry* ne = static_cast<Entry*>(calloc(ncap, sizeof(Entry)));
+    if (!ne) return false;
+    for (size_t i = 0; i < cap; ++i) {
+      if (!e[i].key || e[i].key == Tomb()) continue;
+      size_t j = Hash(e[i].key, ncap);
+      while (ne[j].key) j = (j + 1) & (ncap - 1);
+      ne[j] = e[i];
+    }
+    free(e);
+    e = ne;
+    cap = ncap;
+    tombs = 0;
+    return true;
+  }
+  // Inserts or overwrites; false only when memory is exhausted.
+  bool Put(const void* k, int32_t device, uint64_t bytes) {
+    if (Entry* x = Find(k)) {
+      x->device = device;
+      x->bytes = bytes;
+      return true;
+    }
+    if ((used + tombs + 1) * 2 > cap && !Grow()) return false;
+    size_t i = Hash(k, cap);
+    while (e[i].key && e[i].key != Tomb()) i = (i + 1) & (cap - 1);
+    if (e[i].key == Tomb()) --tombs;
+    e[i] = {k, device, bytes};
+    ++used;
+    return true;
+  }
+  void Erase(Entry* x) {
+    x->key = Tomb();
+    --used;
+    ++tombs;
+  }
+  void Clear() {
+    if (cap) memset(e, 0, cap * sizeof(Entry));
+    used = tombs = 0;
+  }
 };
 
 // ---- container-wide accounting ------------------------------------------
 // Every process of the container draws on one grant: the counters live in a
-// POSIX shared-memory segment named after the container (its cgroup, or
+// shared-memory segment named after the container (its cgroup, or
 // ADP_MEMCAP_KEY). Each process owns a slot recording what it holds, so the
 // bytes of a process that exits -- or is killed -- are given back: at exit by
-// the process itself, otherwise by the next process that would be refused.
-// Without /dev/shm the accounting is per process.
+// the process itself, otherwise by the next process that would be refused or
+// asks for free memory. Without /dev/shm the accounting is per process.
 constexpr uint32_t kMagic = 0x434d4441;  // "ADMC"
 constexpr int kSlots = 256;
 
@@ -75,20 +149,30 @@ struct SharedArea {
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared counters must be address-free");
 
 struct State {
-  std::mutex mu;
-  std::unordered_map<const void*, Alloc> allocs;  // device pointer or VMM handle -> owner (this process)
-  size_t local_used[kMaxDevices] = {};            // used when there is no shared segment
-  size_t cap[kMaxDevices] = {};                   // 0 = not capped
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+  Table allocs;                               // this process's allocations
+  uint64_t local_used[kMaxDevices] = {};      // used when there is no shared segment
+  uint64_t cap[kMaxDevices] = {};             // 0 = not capped
   bool verbose = false;
+  bool any_cap = false;
   std::atomic<bool> warned[kMaxDevices] = {};
   SharedArea* area = nullptr;
   int slot = -1;
   pid_t slot_pid = 0;
   bool released = false;  // this process's slot was handed back (exit): stop touching the counters
-  std::string key;
+  char shm_path[160] = {0};
 };
 
-State& S();
+State g_state;  // constant-initialised: no constructor runs at load time
+pthread_once_t g_once = PTHREAD_ONCE_INIT;
+
+struct Locked {
+  explicit Locked(State& s) : s_(s) { pthread_mutex_lock(&s_.mu); }
+  ~Locked() { pthread_mutex_unlock(&s_.mu); }
+  Locked(const Locked&) = delete;
+  Locked& operator=(const Locked&) = delete;
+  State& s_;
+};
 
 void Log(const char* fmt, ...) {
   char buf[512];
@@ -110,15 +194,10 @@ uint64_t StartTime(pid_t pid) {
   buf[n] = 0;
   const char* p = strrchr(buf, ')');  // comm may contain spaces
   if (!p) return 0;
-  unsigned long long v = 0;
-  // fields after ")": 3 state ... 22 starttime
-  int field = 2;
+  int field = 2;  // fields after ")": 3 state ... 22 starttime
   for (const char* q = p + 1; *q; ++q)
-    if (*q == ' ' && ++field == 22) {
-      v = strtoull(q + 1, nullptr, 10);
-      break;
-    }
-  return v;
+    if (*q == ' ' && ++field == 22) return strtoull(q + 1, nullptr, 10);
+  return 0;
 }
 
 bool Alive(pid_t pid, uint64_t start) {
@@ -129,7 +208,7 @@ bool Alive(pid_t pid, uint64_t start) {
 
 void SubSat(std::atomic<uint64_t>& a, uint64_t v) {
   uint64_t cur = a.load();
-  while (!a.compare_exchange_weak(cur, cur - std::min(cur, v))) {
+  while (!a.compare_exchange_weak(cur, cur - Min(cur, v))) {
   }
 }
 
@@ -148,8 +227,8 @@ void ReclaimDead(SharedArea* a, int mine) {
 }
 
 void ReleaseSlot() {
-  State& s = S();
-  std::lock_guard<std::mutex> lk(s.mu);
+  State& s = g_state;
+  Locked lk(s);
   if (!s.area || s.slot < 0 || s.slot_pid != getpid() || s.released) return;
   SharedSlot& sl = s.area->slots[s.slot];
   for (int d = 0; d < kMaxDevices; ++d) SubSat(s.area->used[d], sl.bytes[d].exchange(0));
@@ -159,34 +238,34 @@ void ReleaseSlot() {
 }
 
 // Maps the container's segment and claims a slot for this process (called
-// with s.mu held, on first use and again in a forked child).
+// with the lock held, at initialisation and again in a forked child).
 void AttachShared(State& s) {
   s.slot = -1;
   s.slot_pid = getpid();
   if (!s.area) {
-    std::string name = "/adp-memcap-" + s.key;
-    int fd = shm_open(name.c_str(), O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0600);
+    // shm_open(3) is open(2) under /dev/shm, and moved libraries across glibc versions.
+    int fd = open(s.shm_path, O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC | O_NOFOLLOW, 0600);
     bool creator = fd >= 0;
-    if (!creator) fd = shm_open(name.c_str(), O_RDWR | O_CLOEXEC, 0);
+    if (!creator) fd = open(s.shm_path, O_RDWR | O_CLOEXEC | O_NOFOLLOW);
     if (fd < 0) {
-      if (s.verbose) Log("no shared segment %s (%s): accounting per process", name.c_str(), strerror(errno));
+      if (s.verbose) Log("no shared segment %s (%s): accounting per process", s.shm_path, strerror(errno));
       return;
     }
     bool ok = true;
     if (creator) {
       ok = ftruncate(fd, sizeof(SharedArea)) == 0;
     } else {
-      struct stat st;
       for (int i = 0; i < 1000 && ok; ++i) {  // the creator may still be sizing it
-        if (fstat(fd, &st) != 0) ok = false;
-        else if (static_cast<size_t>(st.st_size) >= sizeof(SharedArea)) break;
+        off_t size = lseek(fd, 0, SEEK_END);
+        if (size < 0) ok = false;
+        else if (static_cast<size_t>(size) >= sizeof(SharedArea)) break;
         usleep(1000);
       }
     }
     void* m = ok ? mmap(nullptr, sizeof(SharedArea), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0) : MAP_FAILED;
     close(fd);
     if (m == MAP_FAILED) {
-      if (s.verbose) Log("cannot map %s: accounting per process", name.c_str());
+      if (s.verbose) Log("cannot map %s: accounting per process", s.shm_path);
       return;
     }
     auto* a = static_cast<SharedArea*>(m);
@@ -197,7 +276,7 @@ void AttachShared(State& s) {
       for (int i = 0; i < 1000 && a->magic.load(std::memory_order_acquire) != kMagic; ++i) usleep(1000);
       if (a->magic.load(std::memory_order_acquire) != kMagic) {
         munmap(m, sizeof(SharedArea));
-        Log("shared segment %s not initialised: accounting per process", name.c_str());
+        Log("shared segment %s not initialised: accounting per process", s.shm_path);
         return;
       }
     }
@@ -222,111 +301,124 @@ void AttachShared(State& s) {
   }
 }
 
-// fork(): the state is locked across it, so the child never sees the map or
+// fork(): the state is locked across it, so the child never sees the table or
 // the counters half-updated by another thread.
-void AtForkPrepare() { S().mu.lock(); }
-void AtForkParent() { S().mu.unlock(); }
-
+void AtForkPrepare() { pthread_mutex_lock(&g_state.mu); }
+void AtForkParent() { pthread_mutex_unlock(&g_state.mu); }
 void AtForkChild() {
   // The child holds no device memory of its own yet: fresh local state, own slot.
-  State& s = S();
-  s.mu.unlock();
-  std::lock_guard<std::mutex> lk(s.mu);
-  s.allocs.clear();
+  State& s = g_state;
+  pthread_mutex_unlock(&s.mu);
+  Locked lk(s);
+  s.allocs.Clear();
   for (auto& u : s.local_used) u = 0;
   s.released = false;
   if (s.area) AttachShared(s);
 }
 
-State& S() {
-  static State* s = [] {
-    auto* st = new State();  // never destroyed: frees may run from atexit handlers
-    const char* v = getenv("ADP_MEMCAP_VERBOSE");
-    st->verbose = v && *v && *v != '0';
-    const char* lim = getenv("AMD_GPU_MEMORY_LIMIT_MIB");
-    int dev = 0;
-    bool any = false;
-    for (const char* p = lim; p && *p && dev < kMaxDevices; ++dev) {
-      char* end = nullptr;
-      unsigned long long mib = strtoull(p, &end, 10);
-      if (end != p) st->cap[dev] = static_cast<size_t>(mib) << 20;
-      any = any || st->cap[dev];
-      p = strchr(p, ',');
-      if (p) ++p;
-    }
-    if (!any) return st;
-    // The container: its cgroup (shared by all its processes), unless named.
-    const char* k = getenv("ADP_MEMCAP_KEY");
-    std::string basis;
-    if (k && *k) {
-      basis = k;
-    } else if (FILE* f = fopen("/proc/self/cgroup", "r")) {
-      char buf[4096];
-      size_t n = fread(buf, 1, sizeof(buf), f);
-      fclose(f);
-      basis.assign(buf, n);
-    }
-    basis += "|";
-    basis += lim;  // a different grant is a different budget
-    uint64_t h = 1469598103934665603ull;  // FNV-1a
-    for (unsigned char c : basis) h = (h ^ c) * 1099511628211ull;
-    char hex[17];
-    snprintf(hex, sizeof(hex), "%016llx", static_cast<unsigned long long>(h));
-    st->key = hex;
-    if (k && *k && strlen(k) <= 64 && strspn(k, "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789_.-") ==
-                                          strlen(k))
-      st->key = std::string("key-") + k + "-" + st->key.substr(0, 8);  // a named budget, findable in /dev/shm
-    {
-      std::lock_guard<std::mutex> lk(st->mu);
-      AttachShared(*st);
-    }
-    pthread_atfork(AtForkPrepare, AtForkParent, AtForkChild);
-    atexit(ReleaseSlot);
-    return st;
-  }();
-  return *s;
+void Init() {
+  State& s = g_state;
+  const char* v = getenv("ADP_MEMCAP_VERBOSE");
+  s.verbose = v && *v && *v != '0';
+  const char* lim = getenv("AMD_GPU_MEMORY_LIMIT_MIB");
+  int dev = 0;
+  for (const char* p = lim; p && *p && dev < kMaxDevices; ++dev) {
+    char* end = nullptr;
+    unsigned long long mib = strtoull(p, &end, 10);
+    if (end != p) s.cap[dev] = static_cast<uint64_t>(mib) << 20;
+    s.any_cap = s.any_cap || s.cap[dev];
+    p = strchr(p, ',');
+    if (p) ++p;
+  }
+  if (!s.any_cap) return;
+  // The container: its cgroup (shared by all its processes), unless named; and
+  // the grant (a different grant is a different budget).
+  uint64_t h = 1469598103934665603ull;  // FNV-1a
+  auto mix = [&h](const char* b, size_t n) {
+    for (size_t i = 0; i < n; ++i) h = (h ^ static_cast<unsigned char>(b[i])) * 1099511628211ull;
+  };
+  const char* k = getenv("ADP_MEMCAP_KEY");
+  if (k && *k) {
+    mix(k, strlen(k));
+  } else if (FILE* f = fopen("/proc/self/cgroup", "r")) {
+    char buf[4096];
+    size_t n = fread(buf, 1, sizeof(buf), f);
+    fclose(f);
+    mix(buf, n);
+  }
+  mix("|", 1);
+  mix(lim, strlen(lim));
+  const char* safe = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789_.-";
+  if (k && *k && strlen(k) <= 64 && strspn(k, safe) == strlen(k))  // a named budget, findable in /dev/shm
+    snprintf(s.shm_path, sizeof(s.shm_path), "/dev/shm/adp-memcap-key-%s-%08llx", k,
+             static_cast<unsigned long long>(h >> 32));
+  else
+    snprintf(s.shm_path, sizeof(s.shm_path), "/dev/shm/adp-memcap-%016llx", static_cast<unsigned long long>(h));
+  {
+    Locked lk(s);
+    AttachShared(s);
+  }
+  pthread_atfork(AtForkPrepare, AtForkParent, AtForkChild);
+  atexit(ReleaseSlot);
 }
 
-size_t UsedLocked(State& s, int dev) {
-  return s.area ? static_cast<size_t>(s.area->used[dev].load()) : s.local_used[dev];
+State& S() {
+  pthread_once(&g_once, Init);
+  return g_state;
+}
+
+uint64_t UsedLocked(State& s, int dev) { return s.area ? s.area->used[dev].load() : s.local_used[dev]; }
+
+// Resolved entry points are cached in constant-initialised atomics (no guard
+// variables): racing first callers store the same pointer.
+void* HipLibrary() {
+  static std::atomic<void*> lib{nullptr};
+  void* h = lib.load(std::memory_order_acquire);
+  if (h) return h;
+  const char* env = getenv("ADP_MEMCAP_HIP_LIB");
+  const char* names[] = {env, "libamdhip64.so", "libamdhip64.so.7", "libamdhip64.so.6"};
+  for (const char* n : names)
+    if (!h && n && *n) h = dlopen(n, RTLD_LAZY | RTLD_NOLOAD);
+  for (const char* n : names)
+    if (!h && n && *n) h = dlopen(n, RTLD_LAZY);
+  if (h) lib.store(h, std::memory_order_release);
+  return h;
 }
 
 void* RealSym(const char* name) {
   if (void* f = dlsym(RTLD_NEXT, name)) return f;
   // libamdhip64 pulled in by a library dlopen'ed RTLD_LOCAL is not in the
   // global scope RTLD_NEXT searches: take it by name (already loaded).
-  static void* lib = [] {
-    const char* env = getenv("ADP_MEMCAP_HIP_LIB");
-    const char* names[] = {env, "libamdhip64.so", "libamdhip64.so.7", "libamdhip64.so.6"};
-    for (const char* n : names)
-      if (n && *n)
-        if (void* h = dlopen(n, RTLD_LAZY | RTLD_NOLOAD)) return h;
-    for (const char* n : names)
-      if (n && *n)
-        if (void* h = dlopen(n, RTLD_LAZY)) return h;
-    return static_cast<void*>(nullptr);
-  }();
+  void* lib = HipLibrary();
   return lib ? dlsym(lib, name) : nullptr;
 }
 
-template <typename F>
-F Real(const char* name) {
-  return reinterpret_cast<F>(RealSym(name));
+void* Cached(std::atomic<void*>& slot, const char* name) {
+  void* p = slot.load(std::memory_order_acquire);
+  if (!p) {
+    p = RealSym(name);
+    if (p) slot.store(p, std::memory_order_release);
+  }
+  return p;
 }
 
 // The header also declares C++ template overloads of several entry points, so
 // the real function's type is spelled out at each use.
-#define REAL(fn, type) static auto real = Real<type>(#fn)
+#define REAL(fn, type)                         \
+  static std::atomic<void*> real_slot{nullptr}; \
+  auto real = reinterpret_cast<type>(Cached(real_slot, #fn))
 
 int CurrentDevice() {
-  static auto get = Real<hipError_t (*)(int*)>("hipGetDevice");
+  static std::atomic<void*> slot{nullptr};
+  auto get = reinterpret_cast<hipError_t (*)(int*)>(Cached(slot, "hipGetDevice"));
   int d = 0;
   if (!get || get(&d) != hipSuccess || d < 0 || d >= kMaxDevices) return 0;
   return d;
 }
 
 int StreamDevice(hipStream_t stream) {
-  static auto get = Real<hipError_t (*)(hipStream_t, hipDevice_t*)>("hipStreamGetDevice");
+  static std::atomic<void*> slot{nullptr};
+  auto get = reinterpret_cast<hipError_t (*)(hipStream_t, hipDevice_t*)>(Cached(slot, "hipStreamGetDevice"));
   hipDevice_t d = 0;
   if (stream && get && get(stream, &d) == hipSuccess && d >= 0 && d < kMaxDevices) return d;
   return CurrentDevice();
@@ -334,11 +426,11 @@ int StreamDevice(hipStream_t stream) {
 
 // Reserves `bytes` on `dev` for this process; false if that would take the
 // container past the cap.
-bool Reserve(int dev, size_t bytes) {
+bool Reserve(int dev, uint64_t bytes) {
   State& s = S();
   if (!s.cap[dev]) return true;
-  std::lock_guard<std::mutex> lk(s.mu);
-  if (s.area && s.slot_pid != getpid()) AttachShared(s);  // forked without pthread_atfork (vfork-like paths)
+  Locked lk(s);
+  if (s.area && s.slot_pid != getpid()) AttachShared(s);  // a child forked around pthread_atfork
   if (s.area && !s.released) {
     for (int attempt = 0; attempt < 2; ++attempt) {
       uint64_t cur = s.area->used[dev].load();
@@ -361,41 +453,56 @@ bool Reserve(int dev, size_t bytes) {
   return false;
 }
 
-void UnreserveLocked(State& s, int dev, size_t bytes) {
+void AddLocked(State& s, int dev, uint64_t bytes) {
+  if (!s.area) {
+    s.local_used[dev] += bytes;
+  } else if (!s.released && s.slot_pid == getpid()) {
+    s.area->used[dev].fetch_add(bytes);
+    s.area->slots[s.slot].bytes[dev].fetch_add(bytes);
+  }
+}
+
+void UnreserveLocked(State& s, int dev, uint64_t bytes) {
   if (s.area) {
     if (s.released || s.slot_pid != getpid()) return;
     SubSat(s.area->slots[s.slot].bytes[dev], bytes);
     SubSat(s.area->used[dev], bytes);
   } else {
-    s.local_used[dev] -= std::min(bytes, s.local_used[dev]);
+    s.local_used[dev] -= Min(bytes, s.local_used[dev]);
   }
 }
 
-void Unreserve(int dev, size_t bytes) {
+void Unreserve(int dev, uint64_t bytes) {
   State& s = S();
   if (!s.cap[dev]) return;
-  std::lock_guard<std::mutex> lk(s.mu);
+  Locked lk(s);
   UnreserveLocked(s, dev, bytes);
 }
 
-void Track(const void* key, int dev, size_t bytes) {
+void Track(const void* key, int dev, uint64_t bytes) {
   State& s = S();
   if (!s.cap[dev] || !key) return;
-  std::lock_guard<std::mutex> lk(s.mu);
-  s.allocs[key] = {dev, bytes};
-  if (s.verbose) Log("device %d: +%zu bytes (%zu in use)", dev, bytes, UsedLocked(s, dev));
+  Locked lk(s);
+  if (!s.allocs.Put(key, dev, bytes)) {
+    UnreserveLocked(s, dev, bytes);  // out of host memory: cannot follow it, so do not count it
+    return;
+  }
+  if (s.verbose) Log("device %d: +%llu bytes (%llu in use)", dev, static_cast<unsigned long long>(bytes),
+                     static_cast<unsigned long long>(UsedLocked(s, dev)));
 }
 
 void Untrack(const void* key) {
   State& s = S();
-  if (!key) return;
-  std::lock_guard<std::mutex> lk(s.mu);
-  auto it = s.allocs.find(key);
-  if (it == s.allocs.end()) return;  // not ours (uncapped device, or before a cap)
-  UnreserveLocked(s, it->second.device, it->second.bytes);
-  if (s.verbose) Log("device %d: -%zu bytes (%zu in use)", it->second.device, it->second.bytes,
-                     UsedLocked(s, it->second.device));
-  s.allocs.erase(it);
+  if (!key || !s.any_cap) return;
+  Locked lk(s);
+  Entry* x = s.allocs.Find(key);
+  if (!x) return;  // not ours (uncapped device, or before a cap)
+  int dev = x->device;
+  uint64_t bytes = x->bytes;
+  UnreserveLocked(s, dev, bytes);
+  s.allocs.Erase(x);
+  if (s.verbose) Log("device %d: -%llu bytes (%llu in use)", dev, static_cast<unsigned long long>(bytes),
+                     static_cast<unsigned long long>(UsedLocked(s, dev)));
 }
 
 // Depth of interposed allocator calls on this thread: an entry point the HIP
@@ -405,7 +512,7 @@ thread_local int t_depth = 0;
 
 // Common path of every allocator: reserve, call the real one, track or roll back.
 template <typename Call>
-hipError_t Capped(int dev, size_t bytes, void** out, Call call) {
+hipError_t Capped(int dev, uint64_t bytes, void** out, Call call) {
   if (t_depth > 0) return call();
   if (!Reserve(dev, bytes)) {
     if (out) *out = nullptr;
@@ -447,21 +554,17 @@ hipError_t hipMallocManaged(void** ptr, size_t size, unsigned int flags) {
 hipError_t hipMallocPitch(void** ptr, size_t* pitch, size_t width, size_t height) {
   REAL(hipMallocPitch, hipError_t (*)(void**, size_t*, size_t, size_t));
   if (!real) return hipErrorNotInitialized;
-  // The pitch is only known afterwards: reserve the unpadded size, then track
-  // what was really allocated.
+  // The pitch is only known afterwards: reserve the unpadded size, then count
+  // the padding too (without a second check) and track what was allocated.
   int dev = CurrentDevice();
-  hipError_t e = Capped(dev, width * height, ptr, [&] { return real(ptr, pitch, width, height); });
+  hipError_t e = Capped(dev, uint64_t{width} * height, ptr, [&] { return real(ptr, pitch, width, height); });
   State& s = S();
   if (t_depth == 0 && e == hipSuccess && ptr && *ptr && pitch && *pitch > width && s.cap[dev]) {
-    std::lock_guard<std::mutex> lk(s.mu);
-    size_t extra = (*pitch - width) * height;  // the padding, counted without a second check
-    if (!s.area) {
-      s.local_used[dev] += extra;
-    } else if (!s.released && s.slot_pid == getpid()) {
-      s.area->used[dev].fetch_add(extra);
-      s.area->slots[s.slot].bytes[dev].fetch_add(extra);
+    Locked lk(s);
+    if (Entry* x = s.allocs.Find(*ptr)) {
+      AddLocked(s, dev, uint64_t{*pitch - width} * height);
+      x->bytes = uint64_t{*pitch} * height;
     }
-    s.allocs[*ptr].bytes = *pitch * height;
   }
   return e;
 }
@@ -498,7 +601,8 @@ hipError_t hipFreeAsync(void* ptr, hipStream_t stream) {
 // is created per handle.
 hipError_t hipMemCreate(hipMemGenericAllocationHandle_t* handle, size_t size, const hipMemAllocationProp* prop,
                         unsigned long long flags) {
-  REAL(hipMemCreate, hipError_t (*)(hipMemGenericAllocationHandle_t*, size_t, const hipMemAllocationProp*, unsigned long long));
+  REAL(hipMemCreate,
+       hipError_t (*)(hipMemGenericAllocationHandle_t*, size_t, const hipMemAllocationProp*, unsigned long long));
   if (!real) return hipErrorNotInitialized;
   int dev = (prop && prop->location.type == hipMemLocationTypeDevice && prop->location.id >= 0 &&
              prop->location.id < kMaxDevices)
@@ -523,11 +627,11 @@ hipError_t hipMemGetInfo(size_t* free_bytes, size_t* total_bytes) {
   int dev = CurrentDevice();
   State& s = S();
   if (e != hipSuccess || !s.cap[dev]) return e;
-  std::lock_guard<std::mutex> lk(s.mu);
+  Locked lk(s);
   if (s.area) ReclaimDead(s.area, s.slot);  // what died without saying so is free again
-  size_t left = s.cap[dev] - std::min(UsedLocked(s, dev), s.cap[dev]);
-  if (free_bytes) *free_bytes = std::min(*free_bytes, left);
-  if (total_bytes) *total_bytes = std::min(*total_bytes, s.cap[dev]);
+  uint64_t left = s.cap[dev] - Min(UsedLocked(s, dev), s.cap[dev]);
+  if (free_bytes) *free_bytes = Min<uint64_t>(*free_bytes, left);
+  if (total_bytes) *total_bytes = Min<uint64_t>(*total_bytes, s.cap[dev]);
   return e;
 }
 
@@ -536,7 +640,7 @@ hipError_t hipDeviceTotalMem(size_t* bytes, hipDevice_t device) {
   if (!real) return hipErrorNotInitialized;
   hipError_t e = real(bytes, device);
   if (e == hipSuccess && bytes && device >= 0 && device < kMaxDevices && S().cap[device])
-    *bytes = std::min(*bytes, S().cap[device]);
+    *bytes = Min<uint64_t>(*bytes, S().cap[device]);
   return e;
 }
 
@@ -545,7 +649,7 @@ hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600* prop, int device) {
   if (!real) return hipErrorNotInitialized;
   hipError_t e = real(prop, device);
   if (e == hipSuccess && prop && device >= 0 && device < kMaxDevices && S().cap[device])
-    prop->totalGlobalMem = std::min(prop->totalGlobalMem, S().cap[device]);
+    prop->totalGlobalMem = Min<uint64_t>(prop->totalGlobalMem, S().cap[device]);
   return e;
 }
 

@@ -8,6 +8,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <atomic>
 #include <cstdio>
 #include <functional>
@@ -473,9 +474,14 @@ static void TestGrpcLoopback(bool native_http2) {
     usleep(200 * 1000);
     int received = 0;
     std::string last;
-    while ((*ch)->Recv(*sid, &m, 300).ok()) {
-      ++received;
-      last = m;
+    // Read until the newest snapshot arrives (a sanitizer build produces the 30 MB
+    // slowly: no fixed per-message timeout), within a generous overall deadline.
+    auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(20);
+    while (!EndsWith(last, "299") && std::chrono::steady_clock::now() < deadline) {
+      if ((*ch)->Recv(*sid, &m, 1000).ok()) {
+        ++received;
+        last = m;
+      }
     }
     CHECK(received >= 1 && received < 300);
     CHECK(EndsWith(last, "299"));

@@ -153,7 +153,22 @@ def test_shim_exports_hip_versioned_entry_points_only():
             "hipMemCreate@@hip_5.1", "hipGetDevicePropertiesR0600@@hip_6.0"} <= syms
     assert all(s.startswith("hip") for s in syms), syms
     r = subprocess.run(["ldd", SHIM], capture_output=True, text=True, check=True)
-    assert "libamdhip64" not in r.stdout and "libstdc++" not in r.stdout  # resolved at run time; static C++
+    assert "libamdhip64" not in r.stdout and "libstdc++" not in r.stdout  # resolved at run time; no C++ runtime
+
+
+def test_shim_loads_into_old_glibc_images():
+    """PyTorch-ROCm wheels target glibc 2.28 (manylinux_2_28): the shim imports
+    only libc symbols at versions every glibc since 2.4 has, nothing from the
+    C++ runtime, and runs no initialiser when it is preloaded."""
+    import re
+    r = subprocess.run(["objdump", "-T", SHIM], capture_output=True, text=True, check=True)
+    versions = set(re.findall(r"\((GLIBC_[0-9.]+)\)", r.stdout))
+    newest = max(tuple(int(x) for x in v[6:].split(".")) for v in versions)
+    assert newest <= (2, 4), sorted(versions)
+    undefined = [ln.split()[-1] for ln in r.stdout.splitlines() if "*UND*" in ln]
+    assert not [u for u in undefined if u.startswith("_Z") or "cxa_guard" in u or "gxx" in u], undefined
+    nm = subprocess.run(["nm", SHIM], capture_output=True, text=True, check=True).stdout
+    assert "_GLOBAL__sub_I" not in nm  # nothing runs at load: the state is constant-initialised
 
 
 def _allocate(scratch, rc, extra=(), take=3, enforce=True):
