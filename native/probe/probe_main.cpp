@@ -4,6 +4,7 @@
 //                   [--expect-xcds X] [--expect-cus C] [--min-gbps G]
 //                   [--p2p [--min-p2p-gbps P]] [--mfma [--min-tflops T]]
 //                   [--census [--expect-cus-seen C]] [--latency N] [--aggressor SECONDS]
+//                   [--check-grant]
 //
 // Runs the visibility probe (visibility_probe.hip) on every visible HIP device
 // (or one) and prints one JSON line per device. Exits non-zero when a device
@@ -20,6 +21,9 @@
 // CU-partitioned replica, HSA_CU_MASK); --expect-cus-seen checks that count.
 // --latency N times N launches of a small kernel (what a latency-sensitive pod
 // sees); --aggressor S saturates the GPU for S seconds (a noisy neighbour).
+// --check-grant checks an enforced memory-unit grant (AMD_GPU_MEMORY_LIMIT_MIB,
+// --enforce-memory-units): each device reports its grant as its memory,
+// refuses an allocation past it and allows one of half of it.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -33,6 +37,7 @@ extern "C" int adp_probe_mfma(int device, int iters, char* out, int len);
 extern "C" int adp_probe_census(int device, char* out, int len);
 extern "C" int adp_probe_latency(int device, int n, char* out, int len);
 extern "C" int adp_probe_aggressor(int device, double seconds, char* out, int len);
+extern "C" int adp_probe_grant(int device, unsigned long long grant_mib, char* out, int len);
 
 namespace {
 
@@ -58,7 +63,7 @@ int main(int argc, char** argv) {
   long expect_cus_seen = -1;
   int latency = 0;
   double aggressor = 0;
-  bool list = false, p2p = false, mfma = false, census = false;
+  bool list = false, p2p = false, mfma = false, census = false, check_grant = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : "0"; };
@@ -77,10 +82,11 @@ int main(int argc, char** argv) {
     else if (a == "--expect-cus-seen") expect_cus_seen = atol(next());
     else if (a == "--latency") latency = atoi(next());
     else if (a == "--aggressor") aggressor = atof(next());
+    else if (a == "--check-grant") check_grant = true;
     else {
       fprintf(stderr, "usage: %s [--list] [--device N] [--bytes B] [--iters I] [--expect-xcds X] "
                       "[--expect-cus C] [--min-gbps G] [--p2p [--min-p2p-gbps P]] [--mfma [--min-tflops T]] "
-                      "[--census [--expect-cus-seen C]] [--latency N] [--aggressor SECONDS]\n",
+                      "[--census [--expect-cus-seen C]] [--latency N] [--aggressor SECONDS] [--check-grant]\n",
               argv[0]);
       return 2;
     }
@@ -103,6 +109,25 @@ int main(int argc, char** argv) {
                               : adp_probe_latency(d, latency, buf, sizeof(buf));
       printf("%s\n", buf);
       if (arc != 0) ++failures;
+      continue;
+    }
+    if (check_grant) {
+      // The grant of the d-th device of the container: AMD_GPU_MEMORY_LIMIT_MIB, in HIP order.
+      const char* lim = getenv("AMD_GPU_MEMORY_LIMIT_MIB");
+      const char* p = lim;
+      for (int k = 0; p && k < d; ++k) {
+        p = strchr(p, ',');
+        if (p) ++p;
+      }
+      unsigned long long grant = p ? strtoull(p, nullptr, 10) : 0;
+      if (!grant) {
+        printf("{\"device\": %d, \"error\": \"no AMD_GPU_MEMORY_LIMIT_MIB entry for this device\"}\n", d);
+        ++failures;
+        continue;
+      }
+      int grc = adp_probe_grant(d, grant, buf, sizeof(buf));
+      printf("%s\n", buf);
+      if (grc != 0) ++failures;
       continue;
     }
     if (census) {

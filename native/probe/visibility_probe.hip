@@ -614,3 +614,31 @@ extern "C" int adp_probe_run(int device, unsigned long long bytes, int iters, ch
            n * sizeof(uint4), iters, ms, gbps, got == want ? "true" : "false");
   return got == want ? 0 : 2;
 }
+
+// Memory-unit grant check (--enforce-memory-units): inside a pod the device
+// must report the grant as its memory, refuse an allocation past it and allow
+// one well inside it. Host-side HIP calls only.
+extern "C" int adp_probe_grant(int device, unsigned long long grant_mib, char* out, int len) {
+  DeviceGuard device_guard;
+  HIP_TRY(hipSetDevice(device));
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  const size_t grant = static_cast<size_t>(grant_mib) << 20;
+  void* p = nullptr;
+  bool over_refused = hipMalloc(&p, grant + (size_t{64} << 20)) != hipSuccess;
+  if (!over_refused) (void)hipFree(p);
+  (void)hipGetLastError();  // the refusal is expected: clear it
+  p = nullptr;
+  bool half_ok = hipMalloc(&p, grant / 2) == hipSuccess;
+  if (half_ok) (void)hipFree(p);
+  (void)hipGetLastError();
+  bool ok = over_refused && half_ok && (total_b >> 20) == grant_mib && (prop.totalGlobalMem >> 20) == grant_mib;
+  snprintf(out, len,
+           "{\"device\": %d, \"grant_mib\": %llu, \"total_mib\": %zu, \"free_mib\": %zu, \"props_mib\": %zu, "
+           "\"over_grant_refused\": %s, \"half_grant_ok\": %s, \"enforced\": %s}",
+           device, grant_mib, total_b >> 20, free_b >> 20, static_cast<size_t>(prop.totalGlobalMem >> 20),
+           over_refused ? "true" : "false", half_ok ? "true" : "false", ok ? "true" : "false");
+  return ok ? 0 : 3;
+}

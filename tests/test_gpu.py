@@ -326,6 +326,26 @@ def test_memcap_grant_is_shared_by_the_containers_processes():
     assert r.stdout.strip() == "granted", r.stderr[-2000:]
 
 
+def test_probe_checks_an_enforced_grant(probe_built):
+    """amdgpu-dp-probe --check-grant, the in-pod validation of an enforced
+    memory-unit grant: passes under the shim, fails without it."""
+    import json
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR, PROBE_BIN
+    key = f"gputest-probe-{os.getpid()}"
+    base = {**os.environ, "AMD_GPU_MEMORY_LIMIT_MIB": "4000", "ADP_MEMCAP_KEY": key}
+    on = subprocess.run([PROBE_BIN, "--check-grant", "--device", "0"], capture_output=True, text=True, timeout=120,
+                        env={**base, "LD_PRELOAD": _with_preload(os.path.join(BUILD_DIR, "libadp_memcap.so"))})
+    _drop_memcap_segments(key)
+    assert on.returncode == 0, on.stdout + on.stderr[-2000:]
+    res = json.loads(on.stdout.strip().splitlines()[-1])
+    assert res["enforced"] and res["total_mib"] == res["props_mib"] == 4000, res
+    off = subprocess.run([PROBE_BIN, "--check-grant", "--device", "0"], capture_output=True, text=True, timeout=120,
+                         env=base)
+    assert off.returncode == 1, off.stdout
+    assert json.loads(off.stdout.strip().splitlines()[-1])["enforced"] is False
+
+
 def test_soft_partition_replica_on_mi355x(scratch, snap):
     """gpu:shared:4 with --replica-cu-mask --replica-hbm-share
     --enforce-memory-units: one replica is a soft partition -- a quarter of the
