@@ -31,7 +31,9 @@
 //   state_dir files:  gpu<i>.ecc (uncorrectable count; not a number = query fails),
 //                     gpu<i>.dead (device gone),
 //                     gpu<i>.partition ("CPX NPS2": live partition-mode override),
-//                     gpu<i>.xgmi_down (number of xGMI links reported down)
+//                     gpu<i>.xgmi_down (number of xGMI links reported down),
+//                     gpu<i>.badpages (retired HBM pages; not a number = query fails),
+//                     gpu<i>.badpage_threshold (absent = the query needs root, as unprivileged)
 //   amdsmi_shut_down + amdsmi_init re-reads the fixture (re-enumeration after a
 //   re-partition).
 #include <amd_smi/amdsmi.h>
@@ -40,6 +42,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -582,6 +585,29 @@ amdsmi_status_t amdsmi_get_gpu_total_ecc_count(amdsmi_processor_handle h,
     if (f >> v) ec->uncorrectable_count = v;
     else if (f.is_open()) return AMDSMI_STATUS_NOT_SUPPORTED;  // e.g. "unsupported": the query fails
   }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_bad_page_info(amdsmi_processor_handle h, uint32_t* num_pages,
+                                             amdsmi_retired_page_record_t* info) {
+  GET_PROC(h);
+  uint32_t n = 0;
+  if (!g->state_dir.empty()) {
+    std::ifstream f(g->state_dir + "/gpu" + std::to_string(p->gpu) + ".badpages");
+    if (!(f >> n) && f.is_open()) return AMDSMI_STATUS_NOT_SUPPORTED;
+  }
+  if (info)
+    for (uint32_t i = 0; i < std::min(n, *num_pages); ++i)
+      info[i] = {0x100000000ull + i * 4096ull, 4096, AMDSMI_MEM_PAGE_STATUS_RESERVED};
+  *num_pages = n;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_bad_page_threshold(amdsmi_processor_handle h, uint32_t* threshold) {
+  GET_PROC(h);
+  if (g->state_dir.empty()) return AMDSMI_STATUS_NO_PERM;
+  std::ifstream f(g->state_dir + "/gpu" + std::to_string(p->gpu) + ".badpage_threshold");
+  if (!(f >> *threshold)) return AMDSMI_STATUS_NO_PERM;
   return AMDSMI_STATUS_SUCCESS;
 }
 

@@ -353,7 +353,19 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
               "amdgpu_dp_health_ecc_reads_total{result=\"error\"} " + std::to_string(health_counters.ecc_read_errors.load()) + "\n"
               "# HELP amdgpu_dp_health_events_total amdsmi events received.\n"
               "# TYPE amdgpu_dp_health_events_total counter\n"
-              "amdgpu_dp_health_events_total " + std::to_string(health_counters.events_received.load()) + "\n";
+              "amdgpu_dp_health_events_total " + std::to_string(health_counters.events_received.load()) + "\n"
+              "# HELP amdgpu_dp_health_retired_page_reads_total Retired-HBM-page reads by result.\n"
+              "# TYPE amdgpu_dp_health_retired_page_reads_total counter\n"
+              "amdgpu_dp_health_retired_page_reads_total{result=\"ok\"} " +
+              std::to_string(health_counters.retired_reads_ok.load()) + "\n"
+              "amdgpu_dp_health_retired_page_reads_total{result=\"error\"} " +
+              std::to_string(health_counters.retired_read_errors.load()) + "\n";
+          if (auto retired = health_counters.RetiredPages(); !retired.empty()) {
+            out += "# HELP amdgpu_dp_retired_pages HBM pages the driver retired (last health poll).\n"
+                   "# TYPE amdgpu_dp_retired_pages gauge\n";
+            for (const auto& [bdf, n] : retired)
+              out += "amdgpu_dp_retired_pages{bdf=\"" + metrics::LabelValue(bdf) + "\"} " + std::to_string(n) + "\n";
+          }
           // Ask the kubelet who holds which device (cached; outside the plugins lock).
           Result<std::vector<podresources::Assignment>> assigned = Unavailable("off");
           if (pod_lister) {

@@ -64,7 +64,23 @@ HealthConfig HealthConfig::FromValues(const char* disable_value, const char* pol
 }
 
 HealthConfig HealthConfig::FromEnv() {
-  return FromValues(std::getenv("DP_DISABLE_HEALTHCHECKS"), std::getenv("DP_HEALTH_POLL_MS"));
+  HealthConfig c = FromValues(std::getenv("DP_DISABLE_HEALTHCHECKS"), std::getenv("DP_HEALTH_POLL_MS"));
+  if (const char* v = std::getenv("DP_MAX_RETIRED_PAGES"); v && *v) {
+    auto n = ParseInt(v);
+    if (n && *n >= -1) c.max_retired_pages = *n;
+    else LOG_WARN(kComp, "ignoring DP_MAX_RETIRED_PAGES=%s (want -1, 0 or a page count)", v);
+  }
+  return c;
+}
+
+void HealthCounters::SetRetiredPages(const std::string& bdf, uint32_t n) {
+  std::lock_guard<std::mutex> lk(mu_);
+  retired_[bdf] = n;
+}
+
+std::map<std::string, uint32_t> HealthCounters::RetiredPages() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return retired_;
 }
 
 int Monitor::Classify(const HealthConfig& cfg, uint32_t type) {
@@ -155,7 +171,8 @@ std::map<std::string, GpuRecord> Ledger::Parse(const std::string& body) {
       continue;
     }
     r.ecc_seen = *seen;
-    r.fail = static_cast<uint32_t>(*fail) & (kFailEcc | kFailUnresponsive | kFailResetPending | kFailEvent);
+    r.fail = static_cast<uint32_t>(*fail) &
+             (kFailEcc | kFailUnresponsive | kFailResetPending | kFailEvent | kFailRetiredPages);
     if (f.size() > 4) r.reason = f[4];
     out[f[0]] = std::move(r);
   }
@@ -208,15 +225,18 @@ std::vector<std::pair<int, std::string>> Ledger::Failed(const inventory::Snapsho
 }
 
 std::string HealthCounters::Json() const {
-  char buf[320];
+  char buf[400];
   int e = events_enabled.load();
   snprintf(buf, sizeof(buf),
            "{\"events\": \"%s\", \"polls\": %llu, \"responsive\": %llu, \"ecc_reads_ok\": %llu, "
-           "\"ecc_read_errors\": %llu, \"events_received\": %llu}",
+           "\"ecc_read_errors\": %llu, \"events_received\": %llu, \"retired_reads_ok\": %llu, "
+           "\"retired_read_errors\": %llu}",
            e < 0 ? "not started" : e ? "on" : "off", static_cast<unsigned long long>(polls.load()),
            static_cast<unsigned long long>(responsive.load()), static_cast<unsigned long long>(ecc_reads_ok.load()),
            static_cast<unsigned long long>(ecc_read_errors.load()),
-           static_cast<unsigned long long>(events_received.load()));
+           static_cast<unsigned long long>(events_received.load()),
+           static_cast<unsigned long long>(retired_reads_ok.load()),
+           static_cast<unsigned long long>(retired_read_errors.load()));
   return buf;
 }
 
@@ -231,6 +251,7 @@ Monitor::Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> s
   ecc_baseline_.assign(n, 0);
   fail_.assign(n, 0);
   link_change_polls_.assign(n, 0);
+  retired_threshold_.assign(n, 0);
 }
 
 Monitor::~Monitor() { Stop(); }
@@ -280,6 +301,13 @@ Status Monitor::Start() {
       }
     }
     ecc_baseline_[g.index] = r.ecc_baseline;
+    // Retired-page threshold: explicit, else the driver's when readable (root).
+    if (cfg_.max_retired_pages > 0) {
+      retired_threshold_[g.index] = static_cast<uint32_t>(cfg_.max_retired_pages);
+    } else if (cfg_.max_retired_pages < 0) {
+      auto t = lib_->RetiredPageThreshold(h);
+      retired_threshold_[g.index] = t.ok() ? *t : 0;
+    }
     fail_[g.index] = r.fail;
     ledger_->Put(keys_[g.index], r);
     if (r.fail) {
@@ -321,7 +349,7 @@ void Monitor::Stop() {
 
 void Monitor::PollOnce() {
   uint64_t poll = counters_->polls.fetch_add(1) + 1;
-  size_t answered = 0, ecc_ok = 0;
+  size_t answered = 0, ecc_ok = 0, retired_ok = 0;
   std::string counts;
   for (const auto& g : snap_->gpus) {
     void* h = snap_->procs[g.partitions.front().handle].handle;
@@ -366,6 +394,23 @@ void Monitor::PollOnce() {
     if (!alive) continue;
     ++answered;
     counters_->responsive.fetch_add(1);
+    // Retired HBM pages: the driver takes a page out of service after an
+    // uncorrectable error in it; past the threshold the GPU is not trusted
+    // with new work (the reference has no such check).
+    if (auto bp = lib_->RetiredPages(h); bp.ok()) {
+      ++retired_ok;
+      counters_->retired_reads_ok.fetch_add(1);
+      counters_->SetRetiredPages(g.bdf, *bp);
+      uint32_t thr = retired_threshold_[g.index];
+      if (thr && *bp >= thr && !(fail & kFailRetiredPages)) {
+        Update(g.index, kFailRetiredPages, 0,
+               std::to_string(*bp) + " retired HBM pages (threshold " + std::to_string(thr) + ")");
+      } else if ((fail & kFailRetiredPages) && (!thr || *bp < thr)) {
+        Update(g.index, 0, kFailRetiredPages, "retired HBM pages below the threshold");
+      }
+    } else {
+      counters_->retired_read_errors.fetch_add(1);
+    }
     auto ecc = lib_->UncorrectableErrors(h);
     if (!ecc.ok()) {
       counters_->ecc_read_errors.fetch_add(1);
@@ -407,10 +452,14 @@ void Monitor::PollOnce() {
                  std::to_string(ecc_baseline_[g.index]) + ")");
     }
   }
-  if (poll == 1)
-    LOG_INFO(kComp, "health poll #1: %zu/%zu GPU(s) responding, uncorrectable ECC readable on %zu (counts [%s]); "
-             "events %s%s%s", answered, snap_->gpus.size(), ecc_ok, counts.c_str(), events_ok_ ? "on" : "off",
-             events_ok_ ? "" : ": ", events_reason_.c_str());
+  if (poll == 1) {
+    size_t thresholds = 0;
+    for (uint32_t t : retired_threshold_) thresholds += t != 0;
+    LOG_INFO(kComp, "health poll #1: %zu/%zu GPU(s) responding, uncorrectable ECC readable on %zu (counts [%s]), "
+             "retired pages readable on %zu (threshold on %zu); events %s%s%s", answered, snap_->gpus.size(), ecc_ok,
+             counts.c_str(), retired_ok, thresholds, events_ok_ ? "on" : "off", events_ok_ ? "" : ": ",
+             events_reason_.c_str());
+  }
 }
 
 void Monitor::Update(int gpu, uint32_t set, uint32_t clear, const std::string& reason) {

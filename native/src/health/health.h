@@ -61,6 +61,10 @@ struct HealthConfig {
   std::set<uint32_t> ignored{smi::kEvtVmFault, smi::kEvtThermalThrottle};
   int wait_ms = 5000;
   int poll_interval_ms = 5000;
+  // Retired HBM pages at which a GPU is Unhealthy (DP_MAX_RETIRED_PAGES):
+  // -1 = the driver's own threshold when amdsmi can read it (root), else off;
+  // 0 = off; N = N pages.
+  int64_t max_retired_pages = -1;
   static HealthConfig FromEnv();
   static HealthConfig FromValues(const char* disable_value, const char* poll_ms_value);
 };
@@ -73,6 +77,7 @@ enum FailBits : uint32_t {
   kFailUnresponsive = 1u << 1,  // amdsmi stopped answering (clears when it answers)
   kFailResetPending = 1u << 2,  // GPU_PRE_RESET without a GPU_POST_RESET yet
   kFailEvent = 1u << 3,         // any other non-ignored amdsmi event
+  kFailRetiredPages = 1u << 4,  // retired HBM pages reached the threshold
 };
 
 struct GpuRecord {
@@ -93,7 +98,16 @@ struct HealthCounters {
   std::atomic<uint64_t> ecc_reads_ok{0};
   std::atomic<uint64_t> ecc_read_errors{0};
   std::atomic<uint64_t> events_received{0};
+  std::atomic<uint64_t> retired_reads_ok{0};
+  std::atomic<uint64_t> retired_read_errors{0};
+  // Last retired-page count per GPU (by PCI address), for /metrics.
+  void SetRetiredPages(const std::string& bdf, uint32_t n);
+  std::map<std::string, uint32_t> RetiredPages() const;
   std::string Json() const;
+
+ private:
+  mutable std::mutex mu_;
+  std::map<std::string, uint32_t> retired_;
 };
 
 // Per-GPU health verdicts shared by all Monitor generations of a daemon.
@@ -176,6 +190,7 @@ class Monitor {
   std::vector<uint64_t> ecc_baseline_;
   std::vector<uint32_t> fail_;
   std::vector<int> link_change_polls_;
+  std::vector<uint32_t> retired_threshold_;  // 0 = not checked
 };
 
 }  // namespace adp::health

@@ -46,6 +46,8 @@ struct Library::Fns {
   decltype(&amdsmi_get_gpu_event_notification) evt_get = nullptr;
   decltype(&amdsmi_stop_gpu_event_notification) evt_stop = nullptr;
   decltype(&amdsmi_get_gpu_total_ecc_count) ecc_total = nullptr;
+  decltype(&amdsmi_get_gpu_bad_page_info) bad_pages = nullptr;
+  decltype(&amdsmi_get_gpu_bad_page_threshold) bad_page_threshold = nullptr;
   decltype(&amdsmi_status_code_to_string) status_string = nullptr;
   decltype(&amdsmi_get_lib_version) lib_version = nullptr;
 };
@@ -127,6 +129,8 @@ Result<std::unique_ptr<Library>> Library::Open(const std::string& path,
   Resolve(dl, "amdsmi_get_gpu_event_notification", &f->evt_get);
   Resolve(dl, "amdsmi_stop_gpu_event_notification", &f->evt_stop);
   Resolve(dl, "amdsmi_get_gpu_total_ecc_count", &f->ecc_total);
+  Resolve(dl, "amdsmi_get_gpu_bad_page_info", &f->bad_pages);
+  Resolve(dl, "amdsmi_get_gpu_bad_page_threshold", &f->bad_page_threshold);
   Resolve(dl, "amdsmi_status_code_to_string", &f->status_string);
   Resolve(dl, "amdsmi_get_lib_version", &f->lib_version);
   if (!f->init || !f->shut_down || !f->socket_handles || !f->processor_handles || !f->uuid ||
@@ -364,6 +368,22 @@ Result<uint64_t> Library::UncorrectableErrors(void* h) {
   amdsmi_status_t st = f_->ecc_total(h, &ec);
   if (st != AMDSMI_STATUS_SUCCESS) return Unavailable("ecc query failed (" + std::to_string(st) + ")");
   return static_cast<uint64_t>(ec.uncorrectable_count);
+}
+
+Result<uint32_t> Library::RetiredPages(void* h) {
+  if (!f_->bad_pages) return NotSupported("bad page query not present");
+  uint32_t n = 0;
+  amdsmi_status_t st = f_->bad_pages(h, &n, nullptr);  // count only
+  if (st != AMDSMI_STATUS_SUCCESS) return Unavailable("bad page query failed (" + std::to_string(st) + ")");
+  return n;
+}
+
+Result<uint32_t> Library::RetiredPageThreshold(void* h) {
+  if (!f_->bad_page_threshold) return NotSupported("bad page threshold query not present");
+  uint32_t t = 0;
+  amdsmi_status_t st = f_->bad_page_threshold(h, &t);  // root only on current drivers
+  if (st != AMDSMI_STATUS_SUCCESS) return Unavailable("bad page threshold query failed (" + std::to_string(st) + ")");
+  return t;
 }
 
 std::pair<std::string, std::string> Library::PartitionModes(void* h) {

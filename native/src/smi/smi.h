@@ -103,6 +103,10 @@ class Library {
 
   // RAS polling (fallback health when events are unavailable).
   Result<uint64_t> UncorrectableErrors(void* h);
+  // HBM pages the driver retired after uncorrectable errors, and the count at
+  // which the driver itself gives up on the GPU (needs root on current drivers).
+  Result<uint32_t> RetiredPages(void* h);
+  Result<uint32_t> RetiredPageThreshold(void* h);
   bool Responsive(void* h);
 
   // Current compute/memory partition mode of a processor, e.g. {"CPX", "NPS2"}

@@ -135,9 +135,10 @@ def test_health_monitor_is_live_on_real_gpu(scratch, snap):
     log = d.log()
     assert "health checks disabled" not in log
     m = re.search(r"health poll #1: (\d+)/(\d+) GPU\(s\) responding, uncorrectable ECC readable on (\d+) "
-                  r"\(counts \[([0-9,]*)\]\); events (on|off)(?:: (.*))?", log)
+                  r"\(counts \[([0-9,]*)\]\), retired pages readable on (\d+) \(threshold on (\d+)\); "
+                  r"events (on|off)(?:: (.*))?", log)
     assert m, log[-3000:]
-    answering, total, ecc_ok, events = int(m.group(1)), int(m.group(2)), int(m.group(3)), m.group(5)
+    answering, total, ecc_ok, events = int(m.group(1)), int(m.group(2)), int(m.group(3)), m.group(7)
     assert answering == total == 1, m.group(0)  # amdsmi liveness polling works
     assert events == "on" or ecc_ok == 1, f"neither events nor ECC polling is live: {m.group(0)}"
     # live partition-mode queries agree with the enumeration: no spurious re-partition restarts

@@ -370,3 +370,44 @@ def test_ecc_unreadable_at_start_takes_the_first_read_as_baseline(mk):
     n.set_ecc(1, 6)
     n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
     assert "rose to 6 (baseline 5)" in n.d.log()
+
+
+def _set_state(n, name, value):
+    with open(os.path.join(n.state, name), "w") as f:
+        f.write(f"{value}\n")
+
+
+def test_retired_hbm_pages_past_the_threshold(mk):
+    """DP_MAX_RETIRED_PAGES=5: a GPU whose driver has retired 5 HBM pages is
+    Unhealthy, stays so across a restart, and comes back if the count is
+    below the threshold again (e.g. a replaced board)."""
+    n = mk(env={"DP_MAX_RETIRED_PAGES": "5"})
+    ids = sorted(n.start())
+    _set_state(n, "gpu1.badpages", 3)
+    time.sleep(0.4)
+    _set_state(n, "gpu1.badpages", 5)
+    h = n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+    assert h[ids[0]] == "Healthy"
+    n.d.wait_log("5 retired HBM pages (threshold 5)")
+    _restart_sighup(n)
+    assert n.first_law() == {ids[0]: "Healthy", ids[1]: "Unhealthy"}  # the verdict survives the restart
+    _set_state(n, "gpu1.badpages", 0)
+    n.wait_health(lambda h: h[ids[1]] == "Healthy")
+
+
+@pytest.mark.parametrize("readable", [True, False])
+def test_retired_pages_default_to_the_drivers_threshold(mk, readable):
+    """Default (-1): the driver's own bad-page threshold when amdsmi can read it
+    (root); unprivileged it cannot, and retired pages are only reported."""
+    n = mk()
+    if readable:
+        _set_state(n, "gpu0.badpage_threshold", 10)
+    ids = sorted(n.start())
+    n.d.wait_log("health poll #1")
+    assert f"threshold on {1 if readable else 0})" in n.d.log()
+    _set_state(n, "gpu0.badpages", 10)
+    if readable:
+        n.wait_health(lambda h: h[ids[0]] == "Unhealthy")
+    else:
+        time.sleep(0.5)
+        assert "retired HBM pages" not in n.d.log()

@@ -32,7 +32,8 @@ def daemon_envs():
         if tok.isupper() and "_" in tok:
             names.add(tok)
     # environment-only settings documented in docs/USER_GUIDE.md
-    return names | {"DP_DISABLE_HEALTHCHECKS", "DP_HEALTH_POLL_MS", "ADP_LOG_LEVEL", "ADP_LOG_FORMAT"}
+    return names | {"DP_DISABLE_HEALTHCHECKS", "DP_HEALTH_POLL_MS", "DP_MAX_RETIRED_PAGES", "ADP_LOG_LEVEL",
+                    "ADP_LOG_FORMAT"}
 
 
 def daemonset(values=None):

@@ -281,9 +281,14 @@ def test_health_liveness_is_reported(scratch):
         k.wait_registration()
         log = d.wait_log("health poll #1:")
         assert re.search(r"health poll #1: 2/2 GPU\(s\) responding, uncorrectable ECC readable on 2 "
-                         r"\(counts \[0,0\]\); events off: ", log), log
+                         r"\(counts \[0,0\]\), retired pages readable on 2 \(threshold on 0\); events off: ",
+                         log), log
+        with open(os.path.join(state, "gpu1.badpages"), "w") as f:
+            f.write("3\n")
         time.sleep(0.35)
         s = _parse(_get(port, "/metrics")[1])
+        assert sorted(v for (n, ls), v in s.items() if n == "amdgpu_dp_retired_pages") == [0.0, 3.0]
+        assert _value(s, "amdgpu_dp_health_retired_page_reads_total", result="ok") >= 4
         assert _value(s, "amdgpu_dp_health_events_enabled") == 0
         assert _value(s, "amdgpu_dp_health_polls_total") >= 2
         assert _value(s, "amdgpu_dp_health_ecc_reads_total", result="ok") >= 4
