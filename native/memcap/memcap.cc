@@ -43,6 +43,8 @@
 
 #include <atomic>
 
+#include "memcap_area.h"
+
 // glibc 2.34 moved these into libc under new default versions; bind the
 // original ones, which every glibc since 2.2.5 exports.
 __asm__(".symver dlsym,dlsym@GLIBC_2.2.5");
@@ -51,7 +53,7 @@ __asm__(".symver pthread_once,pthread_once@GLIBC_2.2.5");
 
 namespace {
 
-constexpr int kMaxDevices = 64;
+using adp_memcap::kMaxDevices;
 
 template <typename T>
 T Min(T a, T b) {
@@ -126,33 +128,25 @@ struct Table {
 
 // ---- container-wide accounting ------------------------------------------
 // Every process of the container draws on one grant: the counters live in a
-// shared-memory segment named after the container (its cgroup, or
-// ADP_MEMCAP_KEY). Each process owns a slot recording what it holds, so the
-// bytes of a process that exits -- or is killed -- are given back: at exit by
-// the process itself, otherwise by the next process that would be refused or
-// asks for free memory. Without /dev/shm the accounting is per process.
-constexpr uint32_t kMagic = 0x434d4441;  // "ADMC"
-constexpr int kSlots = 256;
-
-struct SharedSlot {
-  std::atomic<int32_t> pid;     // 0 free, > 0 owner, -1 being reclaimed
-  std::atomic<uint64_t> start;  // owner's start time (/proc/<pid>/stat field 22): pid reuse guard
-  std::atomic<uint64_t> bytes[kMaxDevices];
-};
-
-struct SharedArea {
-  std::atomic<uint32_t> magic;
-  uint32_t version;
-  std::atomic<uint64_t> used[kMaxDevices];
-  SharedSlot slots[kSlots];
-};
-static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared counters must be address-free");
+// shared file (memcap_area.h) -- the one the daemon bind-mounted for this
+// allocation (ADP_MEMCAP_FILE), else a segment in /dev/shm named after the
+// container (its cgroup, or ADP_MEMCAP_KEY). Each process owns a slot
+// recording what it holds, so the bytes of a process that exits -- or is
+// killed -- are given back: at exit by the process itself, otherwise by the
+// next process that would be refused, asks for free memory or attaches.
+// Without either file the accounting is per process.
+using adp_memcap::kMagic;
+using adp_memcap::kSlots;
+using adp_memcap::kVersion;
+using SharedArea = adp_memcap::Area;
+using SharedSlot = adp_memcap::Slot;
 
 struct State {
   pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
   Table allocs;                               // this process's allocations
   uint64_t local_used[kMaxDevices] = {};      // used when there is no shared segment
   uint64_t cap[kMaxDevices] = {};             // 0 = not capped
+  int devices = 0;                            // entries in AMD_GPU_MEMORY_LIMIT_MIB
   bool verbose = false;
   bool any_cap = false;
   std::atomic<bool> warned[kMaxDevices] = {};
@@ -161,6 +155,7 @@ struct State {
   pid_t slot_pid = 0;
   bool released = false;  // this process's slot was handed back (exit): stop touching the counters
   char shm_path[160] = {0};
+  char file_path[256] = {0};  // the daemon's accounting file (ADP_MEMCAP_FILE), "" if none
 };
 
 State g_state;  // constant-initialised: no constructor runs at load time
@@ -212,6 +207,12 @@ void SubSat(std::atomic<uint64_t>& a, uint64_t v) {
   }
 }
 
+void RaisePeak(std::atomic<uint64_t>& peak, uint64_t v) {
+  uint64_t cur = peak.load();
+  while (cur < v && !peak.compare_exchange_weak(cur, v)) {
+  }
+}
+
 // Hands the bytes of dead owners back (and frees their slots).
 void ReclaimDead(SharedArea* a, int mine) {
   for (int i = 0; i < kSlots; ++i) {
@@ -237,50 +238,89 @@ void ReleaseSlot() {
   s.released = true;
 }
 
-// Maps the container's segment and claims a slot for this process (called
-// with the lock held, at initialisation and again in a forked child).
+// Maps the daemon's accounting file for this grant: created and filled in by
+// the daemon (grant, IDs); nullptr if it is absent or not a valid file.
+SharedArea* MapDaemonFile(State& s) {
+  int fd = open(s.file_path, O_RDWR | O_CLOEXEC | O_NOFOLLOW);
+  if (fd < 0) {
+    if (s.verbose) Log("no accounting file %s (%s)", s.file_path, strerror(errno));
+    return nullptr;
+  }
+  off_t size = lseek(fd, 0, SEEK_END);
+  void* m = size >= static_cast<off_t>(sizeof(SharedArea))
+                ? mmap(nullptr, sizeof(SharedArea), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0)
+                : MAP_FAILED;
+  close(fd);
+  if (m == MAP_FAILED) {
+    Log("accounting file %s unusable (size %lld)", s.file_path, static_cast<long long>(size));
+    return nullptr;
+  }
+  auto* a = static_cast<SharedArea*>(m);
+  if (a->magic.load(std::memory_order_acquire) != kMagic || a->version != kVersion) {
+    Log("accounting file %s has no valid header", s.file_path);
+    munmap(m, sizeof(SharedArea));
+    return nullptr;
+  }
+  return a;
+}
+
+// Maps (creating it if this process is first) the container's segment in /dev/shm.
+SharedArea* MapShmSegment(State& s, bool* creator_out) {
+  // shm_open(3) is open(2) under /dev/shm, and moved libraries across glibc versions.
+  int fd = open(s.shm_path, O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC | O_NOFOLLOW, 0600);
+  bool creator = fd >= 0;
+  if (!creator) fd = open(s.shm_path, O_RDWR | O_CLOEXEC | O_NOFOLLOW);
+  if (fd < 0) {
+    if (s.verbose) Log("no shared segment %s (%s): accounting per process", s.shm_path, strerror(errno));
+    return nullptr;
+  }
+  bool ok = true;
+  if (creator) {
+    ok = ftruncate(fd, sizeof(SharedArea)) == 0;
+  } else {
+    for (int i = 0; i < 1000 && ok; ++i) {  // the creator may still be sizing it
+      off_t size = lseek(fd, 0, SEEK_END);
+      if (size < 0) ok = false;
+      else if (static_cast<size_t>(size) >= sizeof(SharedArea)) break;
+      usleep(1000);
+    }
+  }
+  void* m = ok ? mmap(nullptr, sizeof(SharedArea), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0) : MAP_FAILED;
+  close(fd);
+  if (m == MAP_FAILED) {
+    if (s.verbose) Log("cannot map %s: accounting per process", s.shm_path);
+    return nullptr;
+  }
+  auto* a = static_cast<SharedArea*>(m);
+  if (creator) {
+    a->version = kVersion;
+    a->devices = static_cast<uint32_t>(s.devices);
+    for (int d = 0; d < kMaxDevices; ++d) a->cap[d].store(s.cap[d]);
+    a->magic.store(kMagic, std::memory_order_release);
+  } else {
+    for (int i = 0; i < 1000 && a->magic.load(std::memory_order_acquire) != kMagic; ++i) usleep(1000);
+    if (a->magic.load(std::memory_order_acquire) != kMagic || a->version != kVersion) {
+      munmap(m, sizeof(SharedArea));
+      Log("shared segment %s not initialised: accounting per process", s.shm_path);
+      return nullptr;
+    }
+  }
+  *creator_out = creator;
+  return a;
+}
+
+// Maps the container's accounting file and claims a slot for this process
+// (called with the lock held, at initialisation and again in a forked child).
 void AttachShared(State& s) {
   s.slot = -1;
   s.slot_pid = getpid();
   if (!s.area) {
-    // shm_open(3) is open(2) under /dev/shm, and moved libraries across glibc versions.
-    int fd = open(s.shm_path, O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC | O_NOFOLLOW, 0600);
-    bool creator = fd >= 0;
-    if (!creator) fd = open(s.shm_path, O_RDWR | O_CLOEXEC | O_NOFOLLOW);
-    if (fd < 0) {
-      if (s.verbose) Log("no shared segment %s (%s): accounting per process", s.shm_path, strerror(errno));
-      return;
-    }
-    bool ok = true;
-    if (creator) {
-      ok = ftruncate(fd, sizeof(SharedArea)) == 0;
-    } else {
-      for (int i = 0; i < 1000 && ok; ++i) {  // the creator may still be sizing it
-        off_t size = lseek(fd, 0, SEEK_END);
-        if (size < 0) ok = false;
-        else if (static_cast<size_t>(size) >= sizeof(SharedArea)) break;
-        usleep(1000);
-      }
-    }
-    void* m = ok ? mmap(nullptr, sizeof(SharedArea), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0) : MAP_FAILED;
-    close(fd);
-    if (m == MAP_FAILED) {
-      if (s.verbose) Log("cannot map %s: accounting per process", s.shm_path);
-      return;
-    }
-    auto* a = static_cast<SharedArea*>(m);
-    if (creator) {
-      a->version = 1;
-      a->magic.store(kMagic, std::memory_order_release);
-    } else {
-      for (int i = 0; i < 1000 && a->magic.load(std::memory_order_acquire) != kMagic; ++i) usleep(1000);
-      if (a->magic.load(std::memory_order_acquire) != kMagic) {
-        munmap(m, sizeof(SharedArea));
-        Log("shared segment %s not initialised: accounting per process", s.shm_path);
-        return;
-      }
-    }
-    s.area = a;
+    bool creator = false;
+    if (s.file_path[0]) s.area = MapDaemonFile(s);
+    if (!s.area) s.area = MapShmSegment(s, &creator);
+    if (!s.area) return;
+    // A restarted container finds its predecessor's processes still counted.
+    if (!creator) ReclaimDead(s.area, -1);
   }
   uint64_t start = StartTime(s.slot_pid);
   for (int pass = 0; pass < 2 && s.slot < 0; ++pass) {
@@ -330,7 +370,10 @@ void Init() {
     p = strchr(p, ',');
     if (p) ++p;
   }
+  s.devices = dev;
   if (!s.any_cap) return;
+  const char* file = getenv("ADP_MEMCAP_FILE");
+  if (file && file[0] == '/' && strlen(file) < sizeof(s.file_path)) strcpy(s.file_path, file);
   // The container: its cgroup (shared by all its processes), unless named; and
   // the grant (a different grant is a different budget).
   uint64_t h = 1469598103934665603ull;  // FNV-1a
@@ -437,6 +480,7 @@ bool Reserve(int dev, uint64_t bytes) {
       while (cur + bytes <= s.cap[dev]) {
         if (s.area->used[dev].compare_exchange_weak(cur, cur + bytes)) {
           s.area->slots[s.slot].bytes[dev].fetch_add(bytes);
+          RaisePeak(s.area->peak[dev], cur + bytes);
           return true;
         }
       }
@@ -446,6 +490,7 @@ bool Reserve(int dev, uint64_t bytes) {
     s.local_used[dev] += bytes;
     return true;
   }
+  if (s.area && !s.released) s.area->refused[dev].fetch_add(1);
   if (s.verbose || !s.warned[dev].exchange(true))
     Log("device %d: refused %.1f MiB (%.1f of %.1f MiB in use%s; AMD_GPU_MEMORY_LIMIT_MIB)", dev,
         bytes / 1048576.0, UsedLocked(s, dev) / 1048576.0, s.cap[dev] / 1048576.0,
@@ -457,7 +502,7 @@ void AddLocked(State& s, int dev, uint64_t bytes) {
   if (!s.area) {
     s.local_used[dev] += bytes;
   } else if (!s.released && s.slot_pid == getpid()) {
-    s.area->used[dev].fetch_add(bytes);
+    RaisePeak(s.area->peak[dev], s.area->used[dev].fetch_add(bytes) + bytes);
     s.area->slots[s.slot].bytes[dev].fetch_add(bytes);
   }
 }

@@ -160,6 +160,10 @@ const std::vector<FlagDef>& Table() {
        "path of libadp_memcap.so in the plugin's filesystem (default: next to the binary, then "
        "/usr/lib/amdgpu-device-plugin/)",
        [](Flags& f) -> void* { return &f.memcap_lib; }},
+      {"container-hbm-metrics", "DP_CONTAINER_HBM_METRICS", "containerHbmMetrics", Kind::kBool,
+       "with --enforce-memory-units and --metrics-addr: mount a per-grant accounting file (read-write) into "
+       "each memory-unit container so /metrics reports the HBM it uses, its peak and refused allocations",
+       [](Flags& f) -> void* { return &f.container_hbm_metrics; }},
       {"metrics-addr", "DP_METRICS_ADDR", "metricsAddr", Kind::kString,
        "serve Prometheus /metrics and /healthz on this TCP address, e.g. ':9400' (empty = off)",
        [](Flags& f) -> void* { return &f.metrics_addr; }},

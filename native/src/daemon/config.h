@@ -56,6 +56,7 @@ struct Flags {
   bool reject_unhealthy = false;  // Allocate() of an Unhealthy device fails instead of warning
   bool enforce_memory_units = false;  // memory-unit pods get the HBM-cap shim (LD_PRELOAD)
   bool replica_hbm_share = false;     // time-slice replicas hold 1/R of the HBM each
+  bool container_hbm_metrics = true;   // per-container HBM use in /metrics (with the HBM-cap shim)
   bool prestart_health_check = false;  // PreStartContainer refuses Unhealthy devices
   std::string memcap_lib;  // the shim in the plugin's filesystem ("" = next to the binary, then /usr/lib/...)
 };

@@ -441,6 +441,10 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     }
     restarts.fetch_add(1);
     v.popts.memcap_host_path = cfg.flags.enforce_memory_units ? InstallMemcap(cfg.flags) : "";
+    v.popts.memcap_usage_dir = !v.popts.memcap_host_path.empty() && cfg.flags.container_hbm_metrics &&
+                                       !cfg.flags.metrics_addr.empty()
+                                   ? PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage")
+                                   : "";
     health::HealthConfig hcfg = health::HealthConfig::FromEnv();
     {
       std::lock_guard<std::mutex> lk(plugins_mu);

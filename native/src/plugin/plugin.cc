@@ -17,6 +17,7 @@
 
 #include "common/log.h"
 #include "common/strings.h"
+#include "memcap/usage.h"
 #include "proto/messages.h"
 #include "proto/wire.h"
 
@@ -342,6 +343,7 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
   std::vector<int> us, units_per;
   std::vector<std::pair<int, uint32_t>> shares;  // (unit, replica) of CU-partitioned units
   std::string c, joined, cu_mask, mem_mib, mem_frac, mem_devs;
+  std::vector<uint64_t> grant_bytes;
   for (const auto& ids : containers) {
     us.clear();
     shares.clear();
@@ -392,6 +394,7 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
     mem_mib.clear();
     mem_frac.clear();
     mem_devs.clear();
+    grant_bytes.clear();
     if (hbm_grants_) {
       char buf[32];
       for (size_t i = 0; i < us.size(); ++i) {
@@ -400,6 +403,7 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
         if (i) { mem_mib += ','; mem_frac += ','; mem_devs += ','; }
         mem_devs += u.visible_id;
         mem_mib += std::to_string(granted);
+        grant_bytes.push_back(granted << 20);
         // Under the HBM-cap shim the device reports the grant as its memory, so
         // the grant is all of what the workload sees.
         double frac = !memcap_bytes_.empty() ? 1.0 : u.vram_mib ? std::min(1.0, double(granted) / u.vram_mib) : 0.0;
@@ -482,6 +486,7 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       pb::PutMapEntry(&c, 1, kMemoryFractionEnv, mem_frac);
       pb::PutMapEntry(&c, 1, kMemoryDevicesEnv, mem_devs);
       c += memcap_bytes_;  // the container enforces the grant (empty unless --enforce-memory-units)
+      if (!memcap_bytes_.empty() && !opts_.memcap_usage_dir.empty()) AddUsageFile(ids, grant_bytes, &c);
     }
     if (!cu_mask.empty()) pb::PutMapEntry(&c, 1, kCuMaskEnv, cu_mask);
     if (opts_.pass_device_specs) {
@@ -498,6 +503,33 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
   stats_.allocate_ns_total.Add(dt);
   stats_.allocate_ns_max.Observe(dt);
   return Status::Ok();
+}
+
+// The grant's accounting file (memcap/usage.h), mounted read-write where the
+// shim looks for it. Without it the shim counts in the pod's /dev/shm: the cap
+// holds either way, only /metrics does not see the container's use.
+void Plugin::AddUsageFile(const std::vector<std::string_view>& ids, const std::vector<uint64_t>& grant_bytes,
+                          std::string* c) {
+  std::string key = memcap::AllocationKey(ids);
+  std::vector<std::string_view> sorted(ids);
+  std::sort(sorted.begin(), sorted.end());
+  std::string joined;
+  for (size_t i = 0; i < sorted.size(); ++i) {
+    if (i) joined += ',';
+    joined += sorted[i];
+  }
+  Status st = memcap::CreateGrantFile(opts_.memcap_usage_dir, key, grant_bytes, joined);
+  if (!st.ok()) {
+    if (!usage_file_warned_.exchange(true, std::memory_order_relaxed))
+      LOG_WARN(kComp, "allocate '%s': %s; the container's HBM use is not reported", spec_.resource_name.c_str(),
+               st.ToString().c_str());
+    return;
+  }
+  pb::PutMapEntry(c, 1, kMemcapFileEnv, kMemcapUsageContainerPath);
+  pb::Mount m{kMemcapUsageContainerPath, opts_.memcap_usage_dir + "/" + key + ".memcap", false};
+  std::string mb;
+  pb::Encode(m, &mb);
+  pb::PutLen(c, 2, mb);
 }
 
 Status Plugin::HandlePreferred(std::string_view req, std::string* resp) {
@@ -948,6 +980,11 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
             static_cast<double>(n));
     }
   }
+  for (auto* p : plugins) {
+    if (p->memcap_bytes_.empty() || p->opts_.memcap_usage_dir.empty()) continue;
+    AppendMemcapUsage(plugins, p->opts_.memcap_usage_dir, assignments, out);
+    break;
+  }
   struct Conn { const Plugin* p; uint64_t connections, shed, errors; };
   std::vector<Conn> conns;
   for (auto* p : plugins) {
@@ -963,6 +1000,101 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
   for (auto& c : conns) gauge("amdgpu_dp_grpc_connections_shed_total", res(c.p), static_cast<double>(c.shed));
   family("amdgpu_dp_grpc_errors_total", "counter", "RPCs answered with a non-OK gRPC status.");
   for (auto& c : conns) gauge("amdgpu_dp_grpc_errors_total", res(c.p), static_cast<double>(c.errors));
+}
+
+// Per-container HBM use of enforced grants, from the shim's accounting files
+// (memcap/usage.h): a container listed by PodResources is found by its device
+// IDs; without PodResources every file is reported by its own (verified) IDs.
+// Files of containers gone for two minutes are removed here.
+void Plugin::AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const std::string& dir,
+                               const std::vector<podresources::Assignment>* assignments, std::string* out) {
+  using metrics::LabelValue;
+  struct Row {
+    const Plugin* p;
+    std::string labels;
+    std::vector<int> units;  // the container's devices in HIP order
+    memcap::Usage u;
+  };
+  auto enforced = [&](std::string_view resource) -> const Plugin* {
+    for (auto* p : plugins)
+      if (p->spec_.resource_name == resource && !p->memcap_bytes_.empty()) return p;
+    return nullptr;
+  };
+  auto units_of = [](const Plugin* p, const std::vector<std::string_view>& ids, std::vector<int>* units) {
+    for (auto id : ids) {
+      auto it = p->advertised_index_.find(id);
+      if (it == p->advertised_index_.end()) return false;
+      units->push_back(it->second);
+    }
+    std::sort(units->begin(), units->end());
+    units->erase(std::unique(units->begin(), units->end()), units->end());
+    return true;
+  };
+  std::vector<Row> rows;
+  std::set<std::string> live;
+  if (assignments) {
+    std::map<std::tuple<std::string, std::string, std::string, std::string>, std::vector<std::string_view>> ctrs;
+    for (const auto& a : *assignments) ctrs[{a.ns, a.pod, a.container, a.resource}].push_back(a.device_id);
+    for (const auto& [k, ids] : ctrs) {
+      const auto& [ns, pod, ctr, resource] = k;
+      const Plugin* p = enforced(resource);
+      if (!p) continue;
+      std::string key = memcap::AllocationKey(ids);
+      live.insert(key);
+      auto u = memcap::ReadGrant(dir, key);
+      Row r{p, "", {}, {}};
+      if (!u.ok() || !units_of(p, ids, &r.units)) continue;
+      r.u = std::move(*u);
+      r.labels = "resource=\"" + LabelValue(resource) + "\",namespace=\"" + LabelValue(ns) + "\",pod=\"" +
+                 LabelValue(pod) + "\",container=\"" + LabelValue(ctr) + "\"";
+      rows.push_back(std::move(r));
+    }
+  } else {
+    for (auto& u : memcap::ReadAll(dir)) {
+      std::vector<std::string_view> ids;
+      for (size_t b = 0; !u.ids.empty() && b <= u.ids.size();) {
+        size_t e = std::min(u.ids.find(',', b), u.ids.size());
+        ids.push_back(std::string_view(u.ids).substr(b, e - b));
+        b = e + 1;
+      }
+      for (auto* p : plugins) {
+        Row r{p, "", {}, {}};
+        if (ids.empty() || p->memcap_bytes_.empty() || !units_of(p, ids, &r.units)) continue;
+        r.labels = "resource=\"" + LabelValue(p->spec_.resource_name) + "\",allocation=\"" + u.key + "\"";
+        r.u = std::move(u);
+        rows.push_back(std::move(r));
+        break;
+      }
+    }
+  }
+  memcap::Collect(dir, assignments ? &live : nullptr, 120, 4096);
+
+  char line[640];
+  auto family = [&](const char* name, const char* type, const char* help) {
+    snprintf(line, sizeof(line), "# HELP %s %s\n# TYPE %s %s\n", name, help, name, type);
+    *out += line;
+  };
+  auto column = [&](const char* name, const char* type, const char* help,
+                    std::vector<uint64_t> memcap::Usage::*col) {
+    family(name, type, help);
+    for (const auto& r : rows) {
+      const auto& v = r.u.*col;
+      for (size_t i = 0; i < v.size(); ++i) {
+        std::string dev = i < r.units.size() ? r.p->units_[r.units[i]].id : "hip" + std::to_string(i);
+        snprintf(line, sizeof(line), "%s{%s,device=\"%s\"} %llu\n", name, r.labels.c_str(),
+                 LabelValue(dev).c_str(), static_cast<unsigned long long>(v[i]));
+        *out += line;
+      }
+    }
+  };
+  column("amdgpu_dp_container_hbm_used_bytes", "gauge",
+         "HBM the container's processes hold on the device (HBM-cap shim).", &memcap::Usage::used);
+  column("amdgpu_dp_container_hbm_granted_bytes", "gauge", "HBM granted to the container on the device.",
+         &memcap::Usage::cap);
+  column("amdgpu_dp_container_hbm_peak_bytes", "gauge", "Most HBM the container has held on the device.",
+         &memcap::Usage::peak);
+  column("amdgpu_dp_container_hbm_refusals_total", "counter",
+         "HIP allocations refused because they would pass the container's grant.", &memcap::Usage::refused);
 }
 
 }  // namespace adp::plugin

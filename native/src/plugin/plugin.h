@@ -69,6 +69,10 @@ inline constexpr const char* kMemoryDevicesEnv = "AMD_GPU_MEMORY_DEVICES";
 inline constexpr const char* kCuMaskEnv = "HSA_CU_MASK";
 // --enforce-memory-units: where the HBM-cap shim is mounted in the container.
 inline constexpr const char* kMemcapContainerPath = "/usr/local/lib/amdgpu-dp/libadp_memcap.so";
+// ... and where the grant's accounting file is mounted (memcap/usage.h), named
+// to the shim by ADP_MEMCAP_FILE.
+inline constexpr const char* kMemcapUsageContainerPath = "/run/amdgpu-dp/memcap";
+inline constexpr const char* kMemcapFileEnv = "ADP_MEMCAP_FILE";
 
 struct PluginOptions {
   std::string plugin_dir = kDefaultPluginDir;
@@ -105,6 +109,10 @@ struct PluginOptions {
   // Host path of the HBM-cap shim; non-empty: memory-unit resources mount it
   // read-only at kMemcapContainerPath and set LD_PRELOAD to it.
   std::string memcap_host_path;
+  // Non-empty (with the shim): each such Allocate() creates the grant's
+  // accounting file here and mounts it, so /metrics reports what the
+  // container uses (memcap/usage.h).
+  std::string memcap_usage_dir;
 };
 
 // HSA_CU_MASK bit ranges [first, last] of each of `replicas` CU shares of a device
@@ -219,6 +227,10 @@ class Plugin {
   bool ApplyHealth(const std::vector<int>& units, bool healthy, const std::string& reason);
   void PostHealth(std::vector<int> units, bool healthy, const std::string& reason);
   Status Register();
+  static void AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const std::string& dir,
+                                const std::vector<podresources::Assignment>* assignments, std::string* out);
+  void AddUsageFile(const std::vector<std::string_view>& ids, const std::vector<uint64_t>& grant_bytes,
+                    std::string* c);
 
  public:
   // CDI (Container Device Interface) spec describing this plugin's devices, for
@@ -245,6 +257,7 @@ class Plugin {
   std::unordered_map<std::string_view, int> advertised_index_;
   std::string kfd_spec_bytes_;
   std::string memcap_bytes_;  // pre-encoded LD_PRELOAD env + shim mount (--enforce-memory-units)
+  std::atomic<bool> usage_file_warned_{false};
   alloc::DeviceGraph graph_;
   // Memoised best-effort answers for <= 8 whole devices (see CachedBestEffort),
   // in anonymous zero-filled pages (an all-zero atomic<uint16_t> is "empty").

@@ -293,6 +293,77 @@ def test_memcap_shim_enforces_the_grant_on_pytorch(scratch, snap):
         json.dump({"allocate_envs": envs, "result": out, "stderr_tail": r.stderr[-1500:]}, f, indent=1)
 
 
+def test_container_hbm_metrics_follow_pytorch(scratch, snap):
+    """--enforce-memory-units + --metrics-addr on the real MI355X: the grant's
+    accounting file is mounted, and /metrics shows what an unmodified PyTorch
+    process holds while it runs, its refused allocation, and the peak after it
+    exits."""
+    import json
+    import re
+    import subprocess
+    import sys
+    import urllib.request
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    shim = os.path.join(BUILD_DIR, "libadp_memcap.so")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--resource-config", "gpu:gpu-mem-gb:-1",
+                                                     "--replica-policy", "pack", "--enforce-memory-units",
+                                                     "--memcap-lib", shim, "--metrics-addr", "127.0.0.1:0"]).start()
+    p = None
+
+    def scrape():
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
+            body = r.read().decode()
+        vals = {}
+        for m in re.finditer(r'^(amdgpu_dp_container_hbm_\w+)\{[^}]*\} (\d+)$', body, re.M):
+            vals[m.group(1)] = int(m.group(2))
+        return vals
+    try:
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics and /healthz on port", 30)).group(1))
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=10).devices]
+        resp = c.allocate(ids[:4]).container_responses[0]
+        c.close()
+        envs = dict(resp.envs)
+        mounts = {m.container_path: m.host_path for m in resp.mounts}
+        envs["LD_PRELOAD"] = _with_preload(mounts[envs["LD_PRELOAD"]])
+        envs["ADP_MEMCAP_FILE"] = mounts[envs["ADP_MEMCAP_FILE"]]  # what the bind mount gives the container
+        code = (
+            "import sys, torch\n"
+            "a = torch.empty(3 << 30, dtype=torch.uint8, device='cuda')\n"
+            "a.fill_(1)\n"
+            "try:\n"
+            "    b = torch.empty(2 << 30, dtype=torch.uint8, device='cuda')\n"
+            "except torch.OutOfMemoryError:\n"
+            "    pass\n"
+            "torch.cuda.synchronize()\n"
+            "print('holding', flush=True)\n"
+            "sys.stdin.read()\n")
+        p = subprocess.Popen([sys.executable, "-c", code], env={**os.environ, **envs}, stdin=subprocess.PIPE,
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        assert p.stdout.readline().strip() == "holding", p.stderr.read()[-2000:]
+        held = scrape()
+        p.stdin.close()
+        assert p.wait(60) == 0
+        p = None
+        after = scrape()
+        mib = 1 << 20
+        assert held["amdgpu_dp_container_hbm_granted_bytes"] == 4000 * mib
+        assert 3 << 30 <= held["amdgpu_dp_container_hbm_used_bytes"] <= 4000 * mib, held
+        assert held["amdgpu_dp_container_hbm_refusals_total"] >= 1, held
+        assert after["amdgpu_dp_container_hbm_used_bytes"] == 0, after
+        assert after["amdgpu_dp_container_hbm_peak_bytes"] >= 3 << 30, after
+        os.makedirs("gpurun_out/memcap", exist_ok=True)
+        with open("gpurun_out/memcap/container_hbm_metrics.json", "w") as f:
+            json.dump({"while_holding": held, "after_exit": after}, f, indent=1)
+    finally:
+        if p:
+            p.kill()
+        assert d.stop() == 0
+        k.stop()
+
+
 def test_memcap_grant_is_shared_by_the_containers_processes():
     """Two PyTorch processes of one container under one 4000 MiB grant: while
     the first holds 3 GiB the second is refused 2 GiB; after the first exits

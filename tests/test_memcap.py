@@ -274,3 +274,30 @@ def test_missing_shim_is_a_startup_error(scratch):
                                       "--memcap-lib", "/nonexistent/libadp_memcap.so"]).start()
     assert d.proc.wait(20) == 1
     assert "libadp_memcap.so not found" in d.log()
+
+
+def test_missing_accounting_file_falls_back_to_dev_shm():
+    """ADP_MEMCAP_FILE names the daemon's per-grant file; when it is absent
+    (say the kubelet wiped the plugin directory) the grant is still enforced,
+    counted in the pod's /dev/shm."""
+    env = dict(_env(f"nofile-{time.monotonic_ns()}"), ADP_MEMCAP_FILE="/nonexistent/memcap")
+    a = _hold(env, 60)
+    try:
+        assert _try(env, 50) == (2, 40)  # the two processes still share the grant
+    finally:
+        a.stdin.close()
+        a.wait(10)
+
+
+def test_memory_unit_pods_get_an_accounting_file_with_metrics(scratch):
+    resp, _ = _allocate(scratch, "gpu:gpu-mem-gb:-1", ["--metrics-addr", "127.0.0.1:0"])
+    envs = dict(resp.envs)
+    assert envs["ADP_MEMCAP_FILE"] == "/run/amdgpu-dp/memcap"
+    mounts = {m.container_path: (m.host_path, m.read_only) for m in resp.mounts}
+    host, ro = mounts["/run/amdgpu-dp/memcap"]
+    assert not ro and host.startswith(os.path.join(scratch, "amdgpu-dp", "usage") + "/")
+    assert os.path.getsize(host) > 100_000  # the whole accounting area
+    # opted out, or no metrics endpoint: nothing extra is mounted
+    resp, _ = _allocate(scratch, "gpu:gpu-mem-gb:-1", ["--metrics-addr", "127.0.0.1:0",
+                                                      "--container-hbm-metrics=false"])
+    assert "ADP_MEMCAP_FILE" not in dict(resp.envs) and len(resp.mounts) == 1

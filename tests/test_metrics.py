@@ -298,3 +298,140 @@ def test_health_liveness_is_reported(scratch):
     finally:
         d.stop()
         k.stop()
+
+
+def test_container_hbm_use_of_enforced_grants(scratch):
+    """--enforce-memory-units with /metrics: each memory-unit container gets its
+    grant's accounting file mounted (ADP_MEMCAP_FILE); the shim's processes
+    count into it and /metrics reports used / granted / peak bytes and refused
+    allocations per (pod, container, device). Files of containers the kubelet
+    no longer lists are removed after two minutes."""
+    import json
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    shim = os.path.join(BUILD_DIR, "libadp_memcap.so")
+    check = os.path.join(BUILD_DIR, "adp_memcap_check")
+    pr_sock = os.path.join(scratch + ".fixture", "pod-resources.sock")
+    os.makedirs(os.path.dirname(pr_sock), exist_ok=True)
+    pr = PodResourcesStub(pr_sock)
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(2), args=[
+        "--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack",
+        "--enforce-memory-units", "--memcap-lib", shim, "--pod-resources-socket", pr_sock]).start()
+    holder = None
+    try:
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics")).group(1))
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        resp = c.allocate(ids[:3]).container_responses[0]
+        c.close()
+        envs = dict(resp.envs)
+        assert envs["ADP_MEMCAP_FILE"] == "/run/amdgpu-dp/memcap"
+        usage = [m for m in resp.mounts if m.container_path == "/run/amdgpu-dp/memcap"]
+        assert len(usage) == 1 and not usage[0].read_only
+        host = usage[0].host_path
+        assert os.path.dirname(host) == os.path.join(scratch, "amdgpu-dp", "usage") and os.path.isfile(host)
+        assert oct(os.stat(host).st_mode & 0o777) == "0o666"  # any uid in the container
+
+        # The container: the shim (device 0 capped at 3000 MiB) with the file at its host path.
+        env = dict(os.environ, LD_PRELOAD=" ".join(x for x in (os.environ.get("LD_PRELOAD", ""), shim) if x),
+                   AMD_GPU_MEMORY_LIMIT_MIB=envs["AMD_GPU_MEMORY_LIMIT_MIB"], ADP_MEMCAP_FILE=host)
+        env.pop("ADP_MEMCAP_KEY", None)
+        holder = subprocess.Popen([check, "hold", "0", "2000"], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                  stderr=subprocess.DEVNULL, text=True, env=env)
+        assert json.loads(holder.stdout.readline()) == {"step": "hold", "rc": 0}
+        holder.stdout.readline()
+        r = subprocess.run([check, "try", "0", "1500"], capture_output=True, text=True, timeout=30, env=env)
+        assert json.loads(r.stdout.splitlines()[0])["rc"] == 2  # 2000 of 3000 held by the other process
+
+        g0 = ids[0].split("-replica-")[0]
+        pr.payload = _list_response([("ml", "infer", "srv", "amd.com/gpu-mem-gb", ids[:3])])
+        s = _parse(_get(port, "/metrics")[1])
+        lab = dict(namespace="ml", pod="infer", container="srv", device=g0)
+        mib = 1 << 20
+        assert _value(s, "amdgpu_dp_container_hbm_used_bytes", **lab) == 2000 * mib
+        assert _value(s, "amdgpu_dp_container_hbm_granted_bytes", **lab) == 3000 * mib
+        assert _value(s, "amdgpu_dp_container_hbm_peak_bytes", **lab) == 2000 * mib
+        assert _value(s, "amdgpu_dp_container_hbm_refusals_total", **lab) == 1
+        holder.stdin.close()
+        assert holder.wait(10) == 0
+        holder = None
+        time.sleep(2.1)  # PodResources cache
+        s = _parse(_get(port, "/metrics")[1])
+        assert _value(s, "amdgpu_dp_container_hbm_used_bytes", **lab) == 0  # given back at exit
+        assert _value(s, "amdgpu_dp_container_hbm_peak_bytes", **lab) == 2000 * mib
+
+        # The pod is gone: its file goes once it is two minutes old.
+        pr.payload = _list_response([])
+        time.sleep(2.1)
+        _get(port, "/metrics")
+        assert os.path.exists(host)  # too young
+        os.utime(host, (time.time() - 300, time.time() - 300))
+        s = _parse(_get(port, "/metrics")[1])
+        assert not os.path.exists(host)
+        assert not any(n == "amdgpu_dp_container_hbm_used_bytes" for (n, _) in s)
+    finally:
+        if holder:
+            holder.kill()
+        pr.stop()
+        d.stop()
+        k.stop()
+
+
+def test_container_hbm_files_without_pod_resources_and_tampered(scratch):
+    """Without PodResources a grant file is reported by its own device IDs
+    (allocation label). The files are the containers' to write: a symlink, a
+    non-regular file or a bad header is skipped, IDs that do not hash to the
+    file name are not believed, and a file grown past its size is trimmed."""
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    shim = os.path.join(BUILD_DIR, "libadp_memcap.so")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(2), args=[
+        "--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack",
+        "--enforce-memory-units", "--memcap-lib", shim]).start()
+    try:
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics")).group(1))
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        first = c.allocate(ids[:2]).container_responses[0]
+        second = c.allocate(ids[2:3]).container_responses[0]
+        c.close()
+        path = lambda r: [m.host_path for m in r.mounts if m.container_path == "/run/amdgpu-dp/memcap"][0]
+        p1, p2 = path(first), path(second)
+        key1 = os.path.basename(p1).split(".")[0]
+        s = _parse(_get(port, "/metrics")[1])
+        g0 = ids[0].split("-replica-")[0]
+        assert _value(s, "amdgpu_dp_container_hbm_granted_bytes", allocation=key1, device=g0) == 2000 << 20
+        assert _value(s, "amdgpu_dp_container_hbm_used_bytes", allocation=key1) == 0
+
+        usage_dir = os.path.dirname(p1)
+        # The second container rewrites its IDs to claim the first one's devices... 
+        with open(p2, "r+b") as f:
+            f.seek(16 + 4 * 64 * 8)  # ids[] after the four per-device columns
+            f.write(b"somebody-else,")
+        # ... a link and a directory posing as grant files ...
+        os.symlink("/etc/passwd", os.path.join(usage_dir, "00000000000000aa.memcap"))
+        os.mkdir(os.path.join(usage_dir, "00000000000000bb.memcap"))
+        # ... and the first one grows its file.
+        with open(p1, "r+b") as f:
+            f.truncate(1 << 30)
+        s = _parse(_get(port, "/metrics")[1])
+        allocs = {dict(ls).get("allocation") for (n, ls), _ in s.items() if n == "amdgpu_dp_container_hbm_used_bytes"}
+        assert allocs == {key1}
+        assert os.path.getsize(p1) < 1 << 20  # trimmed back to the accounting area
+        assert os.path.islink(os.path.join(usage_dir, "00000000000000aa.memcap"))  # not followed, not removed
+        assert open("/etc/passwd").read()  # untouched
+        # The trimmed file still works for the shim.
+        env = dict(os.environ, LD_PRELOAD=" ".join(x for x in (os.environ.get("LD_PRELOAD", ""), shim) if x),
+                   AMD_GPU_MEMORY_LIMIT_MIB="2000", ADP_MEMCAP_FILE=p1)
+        r = subprocess.run([os.path.join(BUILD_DIR, "adp_memcap_check"), "try", "0", "1500"], capture_output=True,
+                           text=True, timeout=30, env=env)
+        assert r.returncode == 0 and '"rc": 0' in r.stdout.splitlines()[0], r.stdout
+        s = _parse(_get(port, "/metrics")[1])
+        assert _value(s, "amdgpu_dp_container_hbm_peak_bytes", allocation=key1) == 1500 << 20
+    finally:
+        d.stop()
+        k.stop()
