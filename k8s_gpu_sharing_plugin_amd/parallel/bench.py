@@ -29,6 +29,10 @@ CONFIGS = {
     "spx-none": ("none", "", "{n}xMI355X SPX, partitionStrategy=none, one amd.com/gpu:1 pod per GPU"),
     "timeslice4": ("none", "gpu:gpu:4", "{n}xMI355X SPX, time-slice sharing 4 replicas/GPU ({p} concurrent pods)"),
     "auto-mem": ("none", "gpu:gpu-mem-gb:-1", "{n}xMI355X SPX, auto memory replicas (gpu-mem-gb)"),
+    # auto-mem with the grant enforced in the pod and reported on /metrics: each
+    # Allocate() also writes the grant's accounting file (memcap/usage.h).
+    "auto-mem-enforced": ("none", "gpu:gpu-mem-gb:-1",
+                          "{n}xMI355X SPX, auto memory replicas, HBM-cap shim + per-grant accounting files"),
     "cpx-single": ("single", "", "{n}xMI355X CPX, partitionStrategy=single, 8 partitions/GPU"),
     # BASELINE config 5: always an 8-GPU node (6 SPX + 2 CPX, node model); one
     # kubelet client admits amd.com/gpu:4 pods, so every admission runs the
@@ -173,6 +177,10 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                 args += ["--resource-config", rc]
             mode = "CPX" if config == "cpx-single" else "SPX"
             fx = None if real else fixtures.node(gpus, mode, memory="NPS2" if mode == "CPX" else "NPS1")
+            if config == "auto-mem-enforced":
+                from .. import BUILD_DIR
+                args += ["--enforce-memory-units", "--memcap-lib", os.path.join(BUILD_DIR, "libadp_memcap.so"),
+                         "--metrics-addr", "127.0.0.1:0"]
             if config == "mixed-gpu4":
                 if real or world != 1:
                     raise SystemExit("mixed-gpu4 runs on the 8-GPU node model with one client (--mock, 1 rank)")

@@ -8,8 +8,12 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
+#include <thread>
 
+#include "common/log.h"
 #include "memcap_area.h"
 
 namespace adp::memcap {
@@ -61,7 +65,8 @@ std::string AllocationKey(std::vector<std::string_view> ids) {
 Status CreateGrantFile(const std::string& dir, const std::string& key, const std::vector<uint64_t>& cap_bytes,
                        std::string_view ids_joined) {
   if (cap_bytes.size() > static_cast<size_t>(area::kMaxDevices)) return InvalidArgument("too many devices");
-  std::vector<unsigned char> hdr(area::kHeaderBytes, 0);
+  // Only up to the IDs: the rest of the file is sparse zeros.
+  std::vector<unsigned char> hdr(offsetof(area::Area, ids) + std::min<size_t>(ids_joined.size(), area::kIdsBytes), 0);
   auto put = [&](size_t off, const void* p, size_t n) { memcpy(hdr.data() + off, p, n); };
   uint32_t magic = area::kMagic, version = area::kVersion, devices = static_cast<uint32_t>(cap_bytes.size());
   uint32_t ids_len = static_cast<uint32_t>(std::min<size_t>(ids_joined.size(), area::kIdsBytes));
@@ -94,6 +99,66 @@ Status CreateGrantFile(const std::string& dir, const std::string& key, const std
     return Internal("create " + path + ": " + strerror(err));
   }
   return Status::Ok();
+}
+
+namespace {
+
+struct Job {
+  std::string dir, key, ids;
+  std::vector<uint64_t> caps;
+};
+
+// One writer per process, never destroyed (its thread outlives every plugin).
+struct Writer {
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  std::deque<Job> jobs;
+  uint64_t queued = 0, done = 0;
+  bool warned = false;
+
+  Writer() { std::thread([this] { Run(); }).detach(); }
+  void Run() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [this] { return !jobs.empty(); });
+      Job j = std::move(jobs.front());
+      jobs.pop_front();
+      lk.unlock();
+      Status st = CreateGrantFile(j.dir, j.key, j.caps, j.ids);
+      lk.lock();
+      if (!st.ok() && !warned) {
+        warned = true;
+        LOG_WARN("memcap", "%s; containers' HBM use is not reported", st.ToString().c_str());
+      }
+      ++done;
+      done_cv.notify_all();
+    }
+  }
+};
+
+Writer& TheWriter() {
+  static Writer* w = new Writer;
+  return *w;
+}
+
+constexpr size_t kMaxPending = 4096;
+
+}  // namespace
+
+void CreateGrantFileAsync(std::string dir, std::string key, std::vector<uint64_t> cap_bytes, std::string ids_joined) {
+  Writer& w = TheWriter();
+  std::lock_guard<std::mutex> lk(w.mu);
+  if (w.jobs.size() >= kMaxPending) return;  // the filesystem is stuck: the shim falls back to /dev/shm
+  w.jobs.push_back({std::move(dir), std::move(key), std::move(ids_joined), std::move(cap_bytes)});
+  ++w.queued;
+  w.cv.notify_one();
+}
+
+void Flush() {
+  Writer& w = TheWriter();
+  std::unique_lock<std::mutex> lk(w.mu);
+  uint64_t target = w.queued;
+  w.done_cv.wait(lk, [&] { return w.done >= target; });
 }
 
 Result<Usage> ReadGrant(const std::string& dir, const std::string& key) {

@@ -36,6 +36,13 @@ std::string AllocationKey(std::vector<std::string_view> ids);
 Status CreateGrantFile(const std::string& dir, const std::string& key, const std::vector<uint64_t>& cap_bytes,
                        std::string_view ids_joined);
 
+// CreateGrantFile on a background thread, so Allocate() -- on a gRPC loop --
+// never waits for the filesystem (the container starts milliseconds later,
+// after the kubelet has the response). Jobs run in order; a failure is logged
+// once per process. Flush() waits until every job queued before it is done.
+void CreateGrantFileAsync(std::string dir, std::string key, std::vector<uint64_t> cap_bytes, std::string ids_joined);
+void Flush();
+
 struct Usage {
   std::string key;
   std::string ids;  // the IDs the file names, "" unless they hash to its key

@@ -506,8 +506,9 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
 }
 
 // The grant's accounting file (memcap/usage.h), mounted read-write where the
-// shim looks for it. Without it the shim counts in the pod's /dev/shm: the cap
-// holds either way, only /metrics does not see the container's use.
+// shim looks for it; written by a background thread, long before the runtime
+// mounts it. Without it the shim counts in the pod's /dev/shm: the cap holds
+// either way, only /metrics does not see the container's use.
 void Plugin::AddUsageFile(const std::vector<std::string_view>& ids, const std::vector<uint64_t>& grant_bytes,
                           std::string* c) {
   std::string key = memcap::AllocationKey(ids);
@@ -518,15 +519,10 @@ void Plugin::AddUsageFile(const std::vector<std::string_view>& ids, const std::v
     if (i) joined += ',';
     joined += sorted[i];
   }
-  Status st = memcap::CreateGrantFile(opts_.memcap_usage_dir, key, grant_bytes, joined);
-  if (!st.ok()) {
-    if (!usage_file_warned_.exchange(true, std::memory_order_relaxed))
-      LOG_WARN(kComp, "allocate '%s': %s; the container's HBM use is not reported", spec_.resource_name.c_str(),
-               st.ToString().c_str());
-    return;
-  }
+  std::string host = opts_.memcap_usage_dir + "/" + key + ".memcap";
+  memcap::CreateGrantFileAsync(opts_.memcap_usage_dir, std::move(key), grant_bytes, std::move(joined));
   pb::PutMapEntry(c, 1, kMemcapFileEnv, kMemcapUsageContainerPath);
-  pb::Mount m{kMemcapUsageContainerPath, opts_.memcap_usage_dir + "/" + key + ".memcap", false};
+  pb::Mount m{kMemcapUsageContainerPath, std::move(host), false};
   std::string mb;
   pb::Encode(m, &mb);
   pb::PutLen(c, 2, mb);

@@ -4,6 +4,7 @@ Run with: python -m pytest tests -m gpu
 """
 
 import os
+import time
 import stat
 
 import pytest
@@ -329,6 +330,10 @@ def test_container_hbm_metrics_follow_pytorch(scratch, snap):
         mounts = {m.container_path: m.host_path for m in resp.mounts}
         envs["LD_PRELOAD"] = _with_preload(mounts[envs["LD_PRELOAD"]])
         envs["ADP_MEMCAP_FILE"] = mounts[envs["ADP_MEMCAP_FILE"]]  # what the bind mount gives the container
+        for _ in range(500):  # written by the daemon just after Allocate() returns
+            if os.path.isfile(envs["ADP_MEMCAP_FILE"]):
+                break
+            time.sleep(0.01)
         code = (
             "import sys, torch\n"
             "a = torch.empty(3 << 30, dtype=torch.uint8, device='cuda')\n"

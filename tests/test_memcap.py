@@ -296,6 +296,9 @@ def test_memory_unit_pods_get_an_accounting_file_with_metrics(scratch):
     mounts = {m.container_path: (m.host_path, m.read_only) for m in resp.mounts}
     host, ro = mounts["/run/amdgpu-dp/memcap"]
     assert not ro and host.startswith(os.path.join(scratch, "amdgpu-dp", "usage") + "/")
+    deadline = time.time() + 5
+    while not os.path.isfile(host) and time.time() < deadline:  # written just after Allocate() returns
+        time.sleep(0.005)
     assert os.path.getsize(host) > 100_000  # the whole accounting area
     # opted out, or no metrics endpoint: nothing extra is mounted
     resp, _ = _allocate(scratch, "gpu:gpu-mem-gb:-1", ["--metrics-addr", "127.0.0.1:0",

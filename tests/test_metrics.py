@@ -177,6 +177,15 @@ def test_builtin_sampler_writes_profile(scratch):
     assert "== by shared object ==" in text and "== by symbol ==" in text
 
 
+def _wait_file(path, timeout=5.0):
+    """Grant files are written by the daemon's background writer, just after
+    Allocate() returns (long before a runtime would mount them)."""
+    deadline = time.time() + timeout
+    while not os.path.isfile(path) and time.time() < deadline:
+        time.sleep(0.005)
+    return os.path.isfile(path)
+
+
 # --- kubelet PodResources: who holds which device -------------------------------
 
 def _pb_len(field, payload: bytes) -> bytes:
@@ -331,7 +340,7 @@ def test_container_hbm_use_of_enforced_grants(scratch):
         usage = [m for m in resp.mounts if m.container_path == "/run/amdgpu-dp/memcap"]
         assert len(usage) == 1 and not usage[0].read_only
         host = usage[0].host_path
-        assert os.path.dirname(host) == os.path.join(scratch, "amdgpu-dp", "usage") and os.path.isfile(host)
+        assert os.path.dirname(host) == os.path.join(scratch, "amdgpu-dp", "usage") and _wait_file(host)
         assert oct(os.stat(host).st_mode & 0o777) == "0o666"  # any uid in the container
 
         # The container: the shim (device 0 capped at 3000 MiB) with the file at its host path.
@@ -401,6 +410,7 @@ def test_container_hbm_files_without_pod_resources_and_tampered(scratch):
         c.close()
         path = lambda r: [m.host_path for m in r.mounts if m.container_path == "/run/amdgpu-dp/memcap"][0]
         p1, p2 = path(first), path(second)
+        assert _wait_file(p1) and _wait_file(p2)
         key1 = os.path.basename(p1).split(".")[0]
         s = _parse(_get(port, "/metrics")[1])
         g0 = ids[0].split("-replica-")[0]

@@ -53,7 +53,7 @@ step_bench() {
   cat $out/bench_default.json
 }
 step_configs() {
-  for cfg in spx-none timeslice4 auto-mem; do
+  for cfg in spx-none timeslice4 auto-mem auto-mem-enforced; do
     timeout -k 10 300 python bench.py --steps 50 --warmup 5 --config $cfg > $out/bench_$cfg.json 2> $out/bench_$cfg.err || die "BENCH $cfg" $out/bench_$cfg.err
     python -c "import json; d=json.load(open('$out/bench_$cfg.json')); print('$cfg', d['allocatable'], d['value'], d['allocate_p99_us'], d['preferred_p50_us'], d['server_allocate_handler_avg_us'], d.get('grpc_go_shaped_allocate_p50_us'), d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'])"
   done
