@@ -6,10 +6,14 @@
   python -m k8s_gpu_sharing_plugin_amd validate [--mfma] [--p2p]
                                                           # probe every visible GPU
   python -m k8s_gpu_sharing_plugin_amd bench [bench.py flags...]
+  python -m k8s_gpu_sharing_plugin_amd hbm [daemon flags...]  # HBM use of enforced grants
 
 `report` runs `amdgpu-device-plugin --dry-run` (real libamd_smi unless
 AMD_SMI_LIB points elsewhere) and prints a table; `validate` runs
-`amdgpu-dp-probe`; `bench` is the headline benchmark (see bench.py).
+`amdgpu-dp-probe`; `bench` is the headline benchmark (see bench.py); `hbm`
+runs `amdgpu-device-plugin --list-grants` (the accounting files of
+--enforce-memory-units with /metrics under <device-plugin dir>/amdgpu-dp/usage)
+and prints a table.
 """
 
 import json
@@ -46,6 +50,21 @@ def _validate(args) -> int:
     return subprocess.run([PROBE_EXE, *args]).returncode
 
 
+def _hbm(args) -> int:
+    r = subprocess.run([DAEMON, "--list-grants", *args], capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stderr)
+        return r.returncode
+    rep = json.loads(r.stdout)
+    mib = 1 << 20
+    print(f"{'grant':<16} {'dev':>3} {'used MiB':>9} {'granted MiB':>11} {'peak MiB':>9} {'refused':>7}  ids")
+    for g in rep["grants"]:
+        for i in range(len(g["used"])):
+            print(f"{g['key']:<16} {i:>3} {g['used'][i] // mib:>9} {g['granted'][i] // mib:>11} "
+                  f"{g['peak'][i] // mib:>9} {g['refused'][i]:>7}  {g['ids'] if i == 0 else ''}")
+    return 0
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     if not argv or argv[0] in ("-h", "--help"):
@@ -60,6 +79,8 @@ def main(argv=None) -> int:
         return _report(rest)
     if cmd == "validate":
         return _validate(rest)
+    if cmd == "hbm":
+        return _hbm(rest)
     if cmd == "bench":
         from .parallel import bench
         bench.main(rest)

@@ -107,6 +107,10 @@ const std::vector<FlagDef>& Table() {
       {"dry-run", "ADP_DRY_RUN", "", Kind::kBool,
        "print the resources/devices this node would advertise as JSON and exit",
        [](Flags& f) -> void* { return &f.dry_run; }},
+      {"list-grants", "ADP_LIST_GRANTS", "", Kind::kBool,
+       "print the HBM use of enforced grants (the accounting files under <device-plugin-path>/amdgpu-dp/usage) "
+       "as JSON and exit",
+       [](Flags& f) -> void* { return &f.list_grants; }},
       {"cdi-spec-dir", "CDI_SPEC_DIR", "cdiSpecDir", Kind::kString,
        "directory for the generated CDI spec (cdi-annotations / cdi-cri strategies)",
        [](Flags& f) -> void* { return &f.cdi_spec_dir; }},

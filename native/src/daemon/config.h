@@ -45,6 +45,7 @@ struct Flags {
   bool trace = false;
   std::string cdi_spec_dir = "/var/run/cdi";
   bool dry_run = false;
+  bool list_grants = false;
   uint64_t server_threads = 0;  // 0 -> plugin::DefaultServerThreads()
   std::string metrics_addr;     // "" = no metrics endpoint
   std::string node_labels_file; // "" = no NFD feature file

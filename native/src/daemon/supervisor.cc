@@ -25,6 +25,7 @@
 #include "health/health.h"
 #include "inventory/inventory.h"
 #include "metrics/metrics.h"
+#include "memcap/usage.h"
 #include "podresources/podresources.h"
 #include "plugin/plugin.h"
 #include "smi/smi.h"
@@ -154,6 +155,34 @@ Result<Validated> Validate(const Config& cfg) {
   return v;
 }
 
+// --list-grants: the enforced grants' accounting files, as JSON on stdout
+// (kubectl exec into the plugin pod; the numbers /metrics reports per pod).
+int ListGrants(const std::string& dir) {
+  std::string out = "{\"dir\": \"" + JsonEscape(dir) + "\", \"grants\": [";
+  auto list = [&out](const std::vector<uint64_t>& v) {
+    out += '[';
+    for (size_t i = 0; i < v.size(); ++i) out += (i ? ", " : "") + std::to_string(v[i]);
+    out += ']';
+  };
+  bool first = true;
+  for (const auto& u : memcap::ReadAll(dir)) {
+    out += first ? "\n  " : ",\n  ";
+    first = false;
+    out += "{\"key\": \"" + u.key + "\", \"ids\": \"" + JsonEscape(u.ids) + "\", \"used\": ";
+    list(u.used);
+    out += ", \"granted\": ";
+    list(u.cap);
+    out += ", \"peak\": ";
+    list(u.peak);
+    out += ", \"refused\": ";
+    list(u.refused);
+    out += ", \"mtime\": " + std::to_string(u.mtime_s) + "}";
+  }
+  out += first ? "]}\n" : "\n]}\n";
+  fputs(out.c_str(), stdout);
+  return 0;
+}
+
 // --dry-run: what this node would advertise, as JSON on stdout.
 int DryRun(smi::Library* lib, const Validated& v, const Config& cfg) {
   auto snap = inventory::BuildSnapshot(lib, v.bopts);
@@ -241,6 +270,8 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   Validated v = std::move(*validated);
   LOG_INFO(kComp, "running with config:\n%s", cfg.ToJson().c_str());
   LOG_INFO(kComp, "running with resource config: %s", v.rc.ToJson().c_str());
+
+  if (cfg.flags.list_grants) return ListGrants(PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage"));
 
   // Signals are consumed through a signalfd; block them before any thread starts.
   sigset_t sigs;
@@ -636,6 +667,9 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   }
   stop_all();
   if (http) http->Stop();
+  // Grant files of containers allocated just before the signal: the runtime mounts them next.
+  if (!v.popts.memcap_usage_dir.empty() && !memcap::Flush(2000))
+    LOG_WARN(kComp, "grant accounting files still being written at exit");
   // Labels describe a node this daemon is serving; do not leave them behind.
   if (!cfg.flags.node_labels_file.empty()) unlink(cfg.flags.node_labels_file.c_str());
   for (int fd : {ep, sfd, ifd, tfd, efd, lfd}) close(fd);

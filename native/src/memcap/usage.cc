@@ -8,6 +8,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -154,11 +155,11 @@ void CreateGrantFileAsync(std::string dir, std::string key, std::vector<uint64_t
   w.cv.notify_one();
 }
 
-void Flush() {
+bool Flush(int timeout_ms) {
   Writer& w = TheWriter();
   std::unique_lock<std::mutex> lk(w.mu);
   uint64_t target = w.queued;
-  w.done_cv.wait(lk, [&] { return w.done >= target; });
+  return w.done_cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return w.done >= target; });
 }
 
 Result<Usage> ReadGrant(const std::string& dir, const std::string& key) {

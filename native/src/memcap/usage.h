@@ -39,9 +39,10 @@ Status CreateGrantFile(const std::string& dir, const std::string& key, const std
 // CreateGrantFile on a background thread, so Allocate() -- on a gRPC loop --
 // never waits for the filesystem (the container starts milliseconds later,
 // after the kubelet has the response). Jobs run in order; a failure is logged
-// once per process. Flush() waits until every job queued before it is done.
+// once per process. Flush() waits (at most `timeout_ms`) until every job
+// queued before it is done; false on timeout.
 void CreateGrantFileAsync(std::string dir, std::string key, std::vector<uint64_t> cap_bytes, std::string ids_joined);
-void Flush();
+bool Flush(int timeout_ms = 5000);
 
 struct Usage {
   std::string key;

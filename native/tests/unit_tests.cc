@@ -28,6 +28,7 @@
 #include "grpc/grpc.h"
 #include "grpc/server_conn.h"
 #include "health/health.h"
+#include "memcap/usage.h"
 #include "metrics/metrics.h"
 #include "plugin/plugin.h"
 #include "podresources/podresources.h"
@@ -910,11 +911,56 @@ static void TestConfigFuzz() {
   CHECK(ok > 0 && failed > 0);
 }
 
+// Grant accounting files: written by the background writer from several
+// threads at once (Allocate() runs on every gRPC loop), read back, collected.
+void TestMemcapUsage() {
+  char tmpl[] = "/tmp/adp-usage-XXXXXX";
+  char* root = mkdtemp(tmpl);
+  CHECK(root != nullptr);
+  if (!root) return;
+  std::string dir = std::string(root) + "/amdgpu-dp/usage";  // created on first use
+  CHECK(memcap::AllocationKey({"b", "a"}) == memcap::AllocationKey({"a", "b"}));
+  CHECK(memcap::AllocationKey({"a", "b"}).size() == 16);
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 4; ++t)
+    ts.emplace_back([&, t] {
+      for (int i = 0; i < 50; ++i) {
+        std::string id = "gpu" + std::to_string(t) + "-replica-" + std::to_string(i);
+        memcap::CreateGrantFileAsync(dir, memcap::AllocationKey({id}), {uint64_t(i + 1) << 20}, id);
+      }
+    });
+  for (auto& t : ts) t.join();
+  memcap::Flush();
+  auto all = memcap::ReadAll(dir);
+  CHECK(all.size() == 200);
+  auto one = memcap::ReadGrant(dir, memcap::AllocationKey({"gpu2-replica-7"}));
+  CHECK(one.ok());
+  if (one.ok()) {
+    CHECK(one->ids == "gpu2-replica-7");
+    CHECK(one->cap.size() == 1 && one->cap[0] == (uint64_t(8) << 20));
+    CHECK(one->used.size() == 1 && one->used[0] == 0 && one->peak[0] == 0 && one->refused[0] == 0);
+  }
+  CHECK(memcap::ReadGrant(dir, "0123456789abcdef").status().code() == Code::kNotFound);
+  // Live: the gpu0 grants; everything else is too young to collect ...
+  std::set<std::string> live;
+  for (int i = 0; i < 50; ++i) live.insert(memcap::AllocationKey({"gpu0-replica-" + std::to_string(i)}));
+  CHECK(memcap::Collect(dir, &live, 120, 4096) == 0);
+  // ... until it is not; and without a live set only the newest max_files stay.
+  CHECK(memcap::Collect(dir, &live, 0, 4096) == 150);
+  CHECK(memcap::ReadAll(dir).size() == 50);
+  CHECK(memcap::Collect(dir, nullptr, 0, 10) == 40);
+  CHECK(memcap::Collect(dir, nullptr, 0, 0) == 10);
+  rmdir(dir.c_str());
+  rmdir((std::string(root) + "/amdgpu-dp").c_str());
+  rmdir(root);
+}
+
 int main() {
   TestYaml();
   TestConfigFuzz();
   TestReplicaCuRanges();
   TestPodResources();
+  TestMemcapUsage();
   TestMetrics();
   TestPrioritize();
   TestStrip();

@@ -304,3 +304,34 @@ def test_memory_unit_pods_get_an_accounting_file_with_metrics(scratch):
     resp, _ = _allocate(scratch, "gpu:gpu-mem-gb:-1", ["--metrics-addr", "127.0.0.1:0",
                                                       "--container-hbm-metrics=false"])
     assert "ADP_MEMCAP_FILE" not in dict(resp.envs) and len(resp.mounts) == 1
+
+
+def test_hbm_command_lists_grant_files(scratch):
+    """`amdgpu-device-plugin --list-grants` (kubectl exec into the plugin pod)
+    and `python -m k8s_gpu_sharing_plugin_amd hbm`: what each enforced grant
+    holds, from its accounting file."""
+    import sys
+    resp, _ = _allocate(scratch, "gpu:gpu-mem-gb:-1", ["--metrics-addr", "127.0.0.1:0"])
+    envs = dict(resp.envs)
+    host = {m.container_path: m.host_path for m in resp.mounts}["/run/amdgpu-dp/memcap"]
+    assert os.path.isfile(host)  # written before the daemon exited
+    env = dict(os.environ, LD_PRELOAD=PRELOAD, AMD_GPU_MEMORY_LIMIT_MIB=envs["AMD_GPU_MEMORY_LIMIT_MIB"],
+               ADP_MEMCAP_FILE=host)
+    env.pop("ADP_MEMCAP_KEY", None)
+    a = _hold(env, 1200)
+    try:
+        r = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "hbm",
+                            "--device-plugin-path", scratch], capture_output=True, text=True, timeout=60)
+        listed = json.loads(subprocess.run([harness.DAEMON, "--list-grants", "--device-plugin-path", scratch],
+                                           capture_output=True, text=True, timeout=60, check=True).stdout)
+    finally:
+        a.stdin.close()
+        a.wait(10)
+    assert r.returncode == 0, r.stderr
+    rows = [ln.split() for ln in r.stdout.splitlines()[1:]]
+    key = os.path.basename(host)[:-len(".memcap")]
+    assert len(rows) == 1 and rows[0][:6] == [key, "0", "1200", "3000", "1200", "0"]
+    assert rows[0][6].count("-replica-") == 3  # the grant's three memory units
+    (g,) = listed["grants"]
+    assert (g["key"], g["used"], g["granted"], g["peak"], g["refused"]) == (key, [1200 << 20], [3000 << 20],
+                                                                             [1200 << 20], [0])
