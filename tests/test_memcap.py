@@ -335,3 +335,20 @@ def test_hbm_command_lists_grant_files(scratch):
     (g,) = listed["grants"]
     assert (g["key"], g["used"], g["granted"], g["peak"], g["refused"]) == (key, [1200 << 20], [3000 << 20],
                                                                              [1200 << 20], [0])
+
+
+def test_restarted_container_reclaims_its_predecessors_bytes(scratch):
+    """A restarted container keeps its Allocate() response, so the same grant
+    file: the bytes of the killed processes are reclaimed when the first
+    process of the new container attaches."""
+    import signal
+    resp, _ = _allocate(scratch, "gpu:gpu-mem-gb:-1", ["--metrics-addr", "127.0.0.1:0"])
+    envs = dict(resp.envs)
+    host = {m.container_path: m.host_path for m in resp.mounts}["/run/amdgpu-dp/memcap"]
+    env = dict(os.environ, LD_PRELOAD=PRELOAD, AMD_GPU_MEMORY_LIMIT_MIB=envs["AMD_GPU_MEMORY_LIMIT_MIB"],
+               ADP_MEMCAP_FILE=host)
+    env.pop("ADP_MEMCAP_KEY", None)
+    a = _hold(env, 2500)
+    a.send_signal(signal.SIGKILL)  # the container is killed
+    a.wait(10)
+    assert _try(env, 2900) == (0, 100)  # all 3000 MiB are the new container's
