@@ -161,3 +161,37 @@ def test_renderer_trims_and_pipes_like_go_templates():
                    '{{- if .Values.n }}no{{ else if .Values.s }} {{ .Values.s | replace "+" "_" }}{{ end }}'
                    '{{ $x := printf "%s-%s" .Release.Name "c" }}{{ $x | trunc 4 }}{{/* c */}}')
     assert r.render_nodes(nodes, r.root, {}) == 'A"d" ["v"] x_yrel-'
+
+
+def test_prometheus_operator_objects():
+    """metrics.serviceMonitor / metrics.prometheusRule: a headless Service over
+    the pods' metrics port, a ServiceMonitor selecting it, and alert rules whose
+    metrics the daemon exports; nothing without metrics.enabled."""
+    import glob
+    import re
+    vals = {"metrics": {"enabled": True, "port": 9500, "serviceMonitor": {"enabled": True, "labels": {"release": "kp"}},
+                        "prometheusRule": {"enabled": True, "hbmGrantRatio": 0.9}}}
+    out = helm_render.render(vals)
+    svc, sm = [d for d in yaml.safe_load_all(out["servicemonitor.yaml"]) if d]
+    (rule,) = [d for d in yaml.safe_load_all(out["prometheusrule.yaml"]) if d]
+    ds = daemonset(vals)
+    pod_labels = ds["spec"]["template"]["metadata"]["labels"]
+    assert svc["kind"] == "Service" and svc["spec"]["clusterIP"] == "None"
+    assert svc["spec"]["selector"].items() <= pod_labels.items()
+    (port,) = svc["spec"]["ports"]
+    assert port["port"] == 9500 and port["targetPort"] == "metrics"
+    assert {p["name"] for p in container(ds)["ports"]} == {"metrics"}
+    assert sm["kind"] == "ServiceMonitor" and sm["metadata"]["labels"]["release"] == "kp"
+    assert sm["spec"]["selector"]["matchLabels"].items() <= svc["metadata"]["labels"].items()
+    assert sm["spec"]["endpoints"] == [{"port": "metrics", "path": "/metrics", "interval": "30s"}]
+    rules = rule["spec"]["groups"][0]["rules"]
+    assert len(rules) == 5 and all(r["alert"].startswith("AmdGpu") for r in rules)
+    assert "> 0.9" in [r for r in rules if r["alert"] == "AmdGpuContainerNearHbmGrant"][0]["expr"]
+    # every metric an alert uses is one the daemon exports
+    src = "".join(open(f).read() for f in glob.glob(os.path.join(ROOT, "native", "src", "*", "*.cc")))
+    for r in rules:
+        for name in re.findall(r"amdgpu_dp_\w+", r["expr"]):
+            assert f'"{name}' in src or f"{name} " in src or f"{name}{{" in src, name
+    off = helm_render.render({"metrics": {"enabled": False, "serviceMonitor": {"enabled": True},
+                                          "prometheusRule": {"enabled": True}}})
+    assert not off["servicemonitor.yaml"].strip() and not off["prometheusrule.yaml"].strip()

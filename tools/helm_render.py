@@ -51,7 +51,7 @@ def _lex(src):
                 pos += 1
 
 
-_TOKEN = re.compile(r'\s*(?:(?P<str>"(?:[^"\\]|\\.)*")|(?P<num>-?\d+)|(?P<assign>:=)|(?P<pipe>\|)'
+_TOKEN = re.compile(r'\s*(?:(?P<str>"(?:[^"\\]|\\.)*")|(?P<num>-?\d+(?:\.\d+)?)|(?P<assign>:=)|(?P<pipe>\|)'
                     r'|(?P<lp>\()|(?P<rp>\))|(?P<var>\$[A-Za-z0-9_]*(?:\.[A-Za-z0-9_]+)*)'
                     r'|(?P<field>\.[A-Za-z0-9_.]*)|(?P<ident>[A-Za-z_][A-Za-z0-9_]*))')
 
@@ -216,7 +216,7 @@ class Renderer:
         if kind == "str":
             return bytes(val[1:-1], "utf-8").decode("unicode_escape")
         if kind == "num":
-            return int(val)
+            return float(val) if "." in val else int(val)
         if kind == "field":
             return dot if val == "." else self.lookup(val, dot)
         if kind == "var":
