@@ -240,14 +240,18 @@ size_t Collect(const std::string& dir, const std::set<std::string>* live, int64_
     if ((!grant && !tmp) || fstatat(dfd, name.c_str(), &st, AT_SYMLINK_NOFOLLOW) != 0) continue;
     bool old = now - st.st_mtime >= min_age_s;
     if ((tmp && old) || (grant && live && old && !live->count(key))) {
-      removed += unlinkat(dfd, name.c_str(), 0) == 0;
+      // A directory: a runtime that mounted the path before the writer got to
+      // it creates one (the shim then counts in /dev/shm); removed once empty.
+      removed += unlinkat(dfd, name.c_str(), S_ISDIR(st.st_mode) ? AT_REMOVEDIR : 0) == 0;
       continue;
     }
     if (grant) kept.emplace_back(static_cast<int64_t>(st.st_mtime), name);
   }
   if (kept.size() > max_files) {
     std::sort(kept.begin(), kept.end());
-    for (size_t i = 0; i + max_files < kept.size(); ++i) removed += unlinkat(dfd, kept[i].second.c_str(), 0) == 0;
+    for (size_t i = 0; i + max_files < kept.size(); ++i)
+      removed += unlinkat(dfd, kept[i].second.c_str(), 0) == 0 ||
+                 unlinkat(dfd, kept[i].second.c_str(), AT_REMOVEDIR) == 0;
   }
   closedir(d);
   return removed;

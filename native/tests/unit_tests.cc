@@ -944,9 +944,11 @@ void TestMemcapUsage() {
   // Live: the gpu0 grants; everything else is too young to collect ...
   std::set<std::string> live;
   for (int i = 0; i < 50; ++i) live.insert(memcap::AllocationKey({"gpu0-replica-" + std::to_string(i)}));
+  // (a runtime that mounted a path before it was written leaves a directory)
+  CHECK(mkdir((dir + "/00000000000000aa.memcap").c_str(), 0755) == 0);
   CHECK(memcap::Collect(dir, &live, 120, 4096) == 0);
   // ... until it is not; and without a live set only the newest max_files stay.
-  CHECK(memcap::Collect(dir, &live, 0, 4096) == 150);
+  CHECK(memcap::Collect(dir, &live, 0, 4096) == 151);
   CHECK(memcap::ReadAll(dir).size() == 50);
   CHECK(memcap::Collect(dir, nullptr, 0, 10) == 40);
   CHECK(memcap::Collect(dir, nullptr, 0, 0) == 10);
