@@ -213,13 +213,18 @@ void RaisePeak(std::atomic<uint64_t>& peak, uint64_t v) {
   }
 }
 
-// Hands the bytes of dead owners back (and frees their slots).
-void ReclaimDead(SharedArea* a, int mine) {
+// Hands the bytes of dead owners back (and frees their slots). `full` also
+// catches a recycled pid (one /proc read per live slot); otherwise only
+// owners that are gone (kill(2): ESRCH) are reclaimed -- cheap enough for
+// every hipMemGetInfo.
+void ReclaimDead(SharedArea* a, int mine, bool full = true) {
   for (int i = 0; i < kSlots; ++i) {
     if (i == mine) continue;
     SharedSlot& sl = a->slots[i];
     int32_t pid = sl.pid.load();
-    if (pid <= 0 || Alive(pid, sl.start.load())) continue;
+    if (pid <= 0) continue;
+    bool dead = full ? !Alive(pid, sl.start.load()) : kill(pid, 0) != 0 && errno == ESRCH;
+    if (!dead) continue;
     if (!sl.pid.compare_exchange_strong(pid, -1)) continue;  // someone else reclaims it
     for (int d = 0; d < kMaxDevices; ++d) SubSat(a->used[d], sl.bytes[d].exchange(0));
     sl.start.store(0);
@@ -673,7 +678,7 @@ hipError_t hipMemGetInfo(size_t* free_bytes, size_t* total_bytes) {
   State& s = S();
   if (e != hipSuccess || !s.cap[dev]) return e;
   Locked lk(s);
-  if (s.area) ReclaimDead(s.area, s.slot);  // what died without saying so is free again
+  if (s.area) ReclaimDead(s.area, s.slot, false);  // what died without saying so is free again
   uint64_t left = s.cap[dev] - Min(UsedLocked(s, dev), s.cap[dev]);
   if (free_bytes) *free_bytes = Min<uint64_t>(*free_bytes, left);
   if (total_bytes) *total_bytes = Min<uint64_t>(*total_bytes, s.cap[dev]);
