@@ -309,6 +309,8 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
             probes = [s.get("probe") for s in everyone if s.get("probe")]
             if probes:
                 result["probe"] = probes
+            # Last: how long a node is without the resource when the kubelet restarts.
+            kub, result["kubelet_restart"] = _kubelet_restart(kub, info["resource"])
             return result
         return None
     finally:
@@ -321,6 +323,29 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                 kub.stop()
         if use_dist and dist.is_initialized():
             dist.destroy_process_group()
+
+
+def _kubelet_restart(kub, resource, rounds=5):
+    """Restarts the stub kubelet `rounds` times (its socket re-created, as a
+    kubelet restart does) and times, on the stub's monotonic clock, from its
+    socket listening to the plugin's Register() and to the first device list
+    (the node can schedule the resource again). Returns the running stub and
+    the medians in ms."""
+    import statistics
+    from ..utils import harness
+    reg, devs = [], []
+    for _ in range(rounds):
+        kub.stop()
+        kub = harness.NativeKubelet(kub.socket_path).start()
+        t0 = next(e["t_us"] for e in kub.events if e.get("event") == "listening")
+        r = kub.wait(lambda e: e.get("event") == "register" and e.get("resource") == resource, 20)
+        d = kub.wait(lambda e: e.get("event") == "devices" and e.get("resource") == resource, 20)
+        if r is None or d is None:
+            return kub, None
+        reg.append((r["t_us"] - t0) / 1e3)
+        devs.append((d["t_us"] - t0) / 1e3)
+    return kub, {"rounds": rounds, "register_ms": round(statistics.median(reg), 3),
+                 "devices_ms": round(statistics.median(devs), 3), "devices_ms_max": round(max(devs), 3)}
 
 
 def main(argv=None):

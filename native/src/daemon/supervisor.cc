@@ -353,6 +353,11 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   // Re-initialise amdsmi before the next enumeration (SIGHUP, a detected
   // re-partition, or a retry): a re-partitioned GPU gets new processor handles.
   bool reinit = false;
+  // The running generation's node snapshot and plugin specs: a kubelet restart
+  // re-registers the same plugins without re-enumerating or restarting the
+  // health monitor (whose amdsmi event wait cannot be interrupted).
+  std::shared_ptr<const inventory::Snapshot> cur_snap;
+  std::vector<strategy::PluginSpec> cur_specs;
 
   std::unique_ptr<metrics::HttpServer> http;
   std::unique_ptr<podresources::CachedLister> pod_lister;
@@ -471,6 +476,8 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
       return;
     }
     restarts.fetch_add(1);
+    cur_snap = *snap;
+    cur_specs = *specs;
     v.popts.memcap_host_path = cfg.flags.enforce_memory_units ? InstallMemcap(cfg.flags) : "";
     v.popts.memcap_usage_dir = !v.popts.memcap_host_path.empty() && cfg.flags.container_hbm_metrics &&
                                        !cfg.flags.metrics_addr.empty()
@@ -515,12 +522,59 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
       ssize_t w = write(lfd, &one, sizeof(one));
       (void)w;
     });
-    for (auto& p : plugins) {
-      plugin::Plugin* raw = p.get();
-      monitor->AddListener([raw](int gpu, bool ok, const std::string& why) { raw->SetGpuHealth(gpu, ok, why); });
-    }
+    // Verdicts go to whichever plugins are serving (re-registration replaces them).
+    monitor->AddListener([&plugins, &plugins_mu](int gpu, bool ok, const std::string& why) {
+      std::lock_guard<std::mutex> lk(plugins_mu);
+      for (auto& p : plugins) p->SetGpuHealth(gpu, ok, why);
+    });
     Status hs = monitor->Start();
     if (!hs.ok()) LOG_WARN(kComp, "health monitor: %s", hs.ToString().c_str());
+  };
+
+  // Kubelet restarted (or our socket vanished): same devices, same health
+  // monitor; only the plugins are replaced and register again.
+  auto reregister = [&] {
+    if (!monitor || !cur_snap) {
+      restart();
+      return;
+    }
+    serving.store(false);
+    ArmTimer(tfd, 0);
+    for (auto& p : plugins) p->Stop();
+    {
+      std::lock_guard<std::mutex> lk(plugins_mu);
+      plugins.clear();
+    }
+    restarts.fetch_add(1);
+    LOG_INFO(kComp, "re-registering plugins (devices and health monitor unchanged)");
+    if (cfg.flags.enforce_memory_units) v.popts.memcap_host_path = InstallMemcap(cfg.flags);
+    {
+      std::lock_guard<std::mutex> lk(plugins_mu);
+      for (auto& s : cur_specs) plugins.push_back(std::make_unique<plugin::Plugin>(cur_snap, s, v.popts));
+    }
+    if (!health::HealthConfig::FromEnv().disabled) {
+      for (const auto& [gpu, why] : ledger.Failed(*cur_snap)) {
+        LOG_WARN(kComp, "GPU %s is unhealthy since an earlier plugin generation: %s",
+                 cur_snap->gpus[gpu].bdf.c_str(), why.c_str());
+        for (auto& p : plugins) p->SetGpuHealth(gpu, false, why);
+      }
+    }
+    for (auto& p : plugins) {
+      if (p->device_count() == 0) continue;
+      Status st = p->Start([efd] {
+        uint64_t one = 1;
+        ssize_t w = write(efd, &one, sizeof(one));
+        (void)w;
+      });
+      if (!st.ok()) {
+        LOG_ERROR(kComp, "could not contact kubelet, retrying (is the device-plugin feature "
+                         "enabled and is %s present?)", kubelet_sock.c_str());
+        schedule_retry("plugin start failed");
+        return;
+      }
+    }
+    backoff_ms = 1000;
+    serving.store(true);
   };
 
   // Re-reads flags/env/file; on success adopts the new config (startup-bound
@@ -577,6 +631,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
       break;
     }
     bool do_restart = false;
+    bool do_reregister = false;  // a lighter restart: see reregister
     for (int i = 0; i < n && !quit; ++i) {
       int fd = events[i].data.fd;
       if (fd == tfd) {
@@ -618,7 +673,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
             if (e->len && kubelet_name == e->name && (e->mask & (IN_CREATE | IN_MOVED_TO))) {
               LOG_INFO(kComp, "inotify: %s created, restarting", kubelet_sock.c_str());
               backoff_ms = 1000;
-              do_restart = true;
+              do_reregister = true;
             }
             // One of our own sockets removed from under us (not by our own Stop():
             // those are re-created before this event is read, so stat finds them).
@@ -634,7 +689,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
                 if (pl->running() && BaseName(pl->socket_path()) == e->name &&
                     stat(pl->socket_path().c_str(), &st) != 0) {
                   LOG_WARN(kComp, "inotify: %s was removed, restarting", pl->socket_path().c_str());
-                  do_restart = true;
+                  do_reregister = true;
                 }
               }
             }
@@ -664,6 +719,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
       }
     }
     if (do_restart && !quit) restart();
+    else if (do_reregister && !quit) reregister();
   }
   stop_all();
   if (http) http->Stop();

@@ -17,6 +17,7 @@
 // The reference has no such harness (no fake kubelet, no gRPC
 // tests); BASELINE.md §4 defines the metrics this measures.
 #include <signal.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -42,9 +43,14 @@ using namespace adp;
 namespace {
 
 std::mutex g_out_mu;
+// One JSON object per line, stamped with CLOCK_MONOTONIC microseconds ("t_us").
 void Emit(const std::string& line) {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  std::string stamped = "{\"t_us\": " + std::to_string(int64_t(ts.tv_sec) * 1000000 + ts.tv_nsec / 1000) +
+                        (line.size() > 2 ? ", " : "") + line.substr(1);
   std::lock_guard<std::mutex> lk(g_out_mu);
-  fputs(line.c_str(), stdout);
+  fputs(stamped.c_str(), stdout);
   fputc('\n', stdout);
   fflush(stdout);
 }

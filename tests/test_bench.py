@@ -35,6 +35,10 @@ def test_bench_single_process_contract():
     gg = res["per_rank"][0]["grpc_go_shaped"]
     assert gg["allocate"]["n"] == 300 and gg["bdp_pings"] >= gg["pods"]
     assert res["grpc_go_shaped_allocate_p50_us"] == gg["allocate"]["p50_us"] > 0
+    # kubelet restarts: re-registered without re-enumeration or a health-monitor
+    # restart (whose amdsmi event wait took up to 500 ms to stop)
+    kr = res["kubelet_restart"]
+    assert kr["rounds"] == 5 and 0 < kr["register_ms"] <= kr["devices_ms"] < 150, kr
 
 
 @pytest.mark.slow
