@@ -159,7 +159,10 @@ bool Flush(int timeout_ms) {
   Writer& w = TheWriter();
   std::unique_lock<std::mutex> lk(w.mu);
   uint64_t target = w.queued;
-  return w.done_cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return w.done >= target; });
+  // system_clock: pthread_cond_timedwait (a steady_clock wait is
+  // pthread_cond_clockwait, which this toolchain's TSan does not intercept).
+  return w.done_cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms),
+                              [&] { return w.done >= target; });
 }
 
 Result<Usage> ReadGrant(const std::string& dir, const std::string& key) {
