@@ -484,7 +484,7 @@ void Monitor::Run() {
   auto next_poll = Clock::now() + std::chrono::milliseconds(cfg_.poll_interval_ms);
   std::vector<smi::Event> events;
   while (!stop_.load()) {
-    int slice = 500;  // bounded so Stop() is prompt; the reference waits 5000 ms per call
+    int slice = 100;  // bounded so Stop() (SIGHUP, config, re-partition, exit) is prompt; the reference waits 5000 ms
     if (cfg_.wait_ms > 0 && cfg_.wait_ms < slice) slice = cfg_.wait_ms;
     if (cfg_.poll_interval_ms > 0) {  // wake for the next poll, not a slice later
       auto until = std::chrono::duration_cast<std::chrono::milliseconds>(next_poll - Clock::now()).count();
