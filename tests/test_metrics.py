@@ -177,6 +177,19 @@ def test_builtin_sampler_writes_profile(scratch):
     assert "== by shared object ==" in text and "== by symbol ==" in text
 
 
+def _preloadable_shim():
+    """The HBM-cap shim and its check program from BUILD_DIR, or a skip when
+    that is a sanitizer build (the shim then needs its runtime preloaded first:
+    the e2e sanitizer suites run the daemon, not workloads)."""
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    shim = os.path.join(BUILD_DIR, "libadp_memcap.so")
+    deps = subprocess.run(["ldd", shim], capture_output=True, text=True).stdout
+    if "libasan" in deps or "libtsan" in deps:
+        pytest.skip("sanitizer build of the shim")
+    return shim, os.path.join(BUILD_DIR, "adp_memcap_check")
+
+
 def _wait_file(path, timeout=5.0):
     """Grant files are written by the daemon's background writer, just after
     Allocate() returns (long before a runtime would mount them)."""
@@ -317,9 +330,7 @@ def test_container_hbm_use_of_enforced_grants(scratch):
     no longer lists are removed after two minutes."""
     import json
     import subprocess
-    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
-    shim = os.path.join(BUILD_DIR, "libadp_memcap.so")
-    check = os.path.join(BUILD_DIR, "adp_memcap_check")
+    shim, check = _preloadable_shim()
     pr_sock = os.path.join(scratch + ".fixture", "pod-resources.sock")
     os.makedirs(os.path.dirname(pr_sock), exist_ok=True)
     pr = PodResourcesStub(pr_sock)
@@ -394,8 +405,7 @@ def test_container_hbm_files_without_pod_resources_and_tampered(scratch):
     non-regular file or a bad header is skipped, IDs that do not hash to the
     file name are not believed, and a file grown past its size is trimmed."""
     import subprocess
-    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
-    shim = os.path.join(BUILD_DIR, "libadp_memcap.so")
+    shim, check = _preloadable_shim()
     k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
     d = harness.Daemon(scratch, fixtures.node(2), args=[
         "--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack",
@@ -437,7 +447,7 @@ def test_container_hbm_files_without_pod_resources_and_tampered(scratch):
         # The trimmed file still works for the shim.
         env = dict(os.environ, LD_PRELOAD=" ".join(x for x in (os.environ.get("LD_PRELOAD", ""), shim) if x),
                    AMD_GPU_MEMORY_LIMIT_MIB="2000", ADP_MEMCAP_FILE=p1)
-        r = subprocess.run([os.path.join(BUILD_DIR, "adp_memcap_check"), "try", "0", "1500"], capture_output=True,
+        r = subprocess.run([check, "try", "0", "1500"], capture_output=True,
                            text=True, timeout=30, env=env)
         assert r.returncode == 0 and '"rc": 0' in r.stdout.splitlines()[0], r.stdout
         s = _parse(_get(port, "/metrics")[1])
