@@ -4,6 +4,7 @@
 //   cmd/nvidia-device-plugin/replica_test.go:120-122 (3 stripReplicas cases)
 //   cmd/nvidia-device-plugin/nvidia_test.go:31-64    (10 getAdditionalXids cases)
 // plus codec, config, resource-config, topology and gRPC loopback tests.
+#include <fcntl.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -15,6 +16,7 @@
 #include <climits>
 #include <map>
 #include <mutex>
+#include <random>
 #include <set>
 #include <string>
 #include <thread>
@@ -952,6 +954,35 @@ void TestMemcapUsage() {
   CHECK(memcap::ReadAll(dir).size() == 50);
   CHECK(memcap::Collect(dir, nullptr, 0, 10) == 40);
   CHECK(memcap::Collect(dir, nullptr, 0, 0) == 10);
+  // Whatever a container writes into its file: a bounded result or an error.
+  std::mt19937 rng(7);
+  std::string key = memcap::AllocationKey({"fuzz"});
+  CHECK(memcap::CreateGrantFile(dir, key, {1u << 20}, "fuzz").ok());
+  std::string path = dir + "/" + key + ".memcap";
+  for (int it = 0; it < 300; ++it) {
+    int fd = open(path.c_str(), O_RDWR);
+    CHECK(fd >= 0);
+    if (fd < 0) break;
+    if (it % 3 == 0) {  // a short or grown file
+      int r = ftruncate(fd, static_cast<off_t>(rng() % (300 * 1024)));
+      (void)r;
+    }
+    for (int k = 0; k < 8; ++k) {  // scribble over the header (magic/version kept half the time)
+      uint32_t off = rng() % 6200, v = rng();
+      if (it % 2 == 0 && off < 8) continue;
+      ssize_t w = pwrite(fd, &v, sizeof(v), off);
+      (void)w;
+    }
+    close(fd);
+    auto u = memcap::ReadGrant(dir, key);
+    if (u.ok()) {
+      CHECK(u->used.size() <= 64 && u->cap.size() == u->used.size() && u->peak.size() == u->used.size());
+      CHECK(u->ids.empty() || memcap::AllocationKey({u->ids}) == key);
+    }
+    struct stat st;
+    CHECK(stat(path.c_str(), &st) == 0 && st.st_size <= 2 * 150000);  // trimmed when grown
+  }
+  unlink(path.c_str());
   rmdir(dir.c_str());
   rmdir((std::string(root) + "/amdgpu-dp").c_str());
   rmdir(root);
