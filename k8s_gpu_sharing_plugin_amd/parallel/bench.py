@@ -309,8 +309,12 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
             probes = [s.get("probe") for s in everyone if s.get("probe")]
             if probes:
                 result["probe"] = probes
-            # Last: how long a node is without the resource when the kubelet restarts.
-            kub, result["kubelet_restart"] = _kubelet_restart(kub, info["resource"])
+            # Last: how long a node is without the resource when the kubelet restarts
+            # (reported, never fatal for the headline).
+            try:
+                kub, result["kubelet_restart"] = _kubelet_restart(kub, info["resource"])
+            except Exception as e:
+                result["kubelet_restart"] = {"error": str(e)}
             return result
         return None
     finally:
@@ -337,7 +341,9 @@ def _kubelet_restart(kub, resource, rounds=5):
     for _ in range(rounds):
         kub.stop()
         kub = harness.NativeKubelet(kub.socket_path).start()
-        t0 = next(e["t_us"] for e in kub.events if e.get("event") == "listening")
+        t0 = next((e["t_us"] for e in kub.events if e.get("event") == "listening"), None)
+        if t0 is None:
+            return kub, None
         r = kub.wait(lambda e: e.get("event") == "register" and e.get("resource") == resource, 20)
         d = kub.wait(lambda e: e.get("event") == "devices" and e.get("resource") == resource, 20)
         if r is None or d is None:
