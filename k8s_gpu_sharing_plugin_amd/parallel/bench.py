@@ -340,7 +340,11 @@ def _kubelet_restart(kub, resource, rounds=5):
     reg, devs = [], []
     for _ in range(rounds):
         kub.stop()
-        kub = harness.NativeKubelet(kub.socket_path).start()
+        kub = harness.NativeKubelet(kub.socket_path)
+        try:
+            kub.start()
+        except Exception as e:  # the caller stops `kub` whatever happened
+            return kub, {"error": str(e)}
         t0 = next((e["t_us"] for e in kub.events if e.get("event") == "listening"), None)
         if t0 is None:
             return kub, None
