@@ -404,6 +404,18 @@ amdsmi_status_t amdsmi_get_gpu_memory_total(amdsmi_processor_handle h, amdsmi_me
   return AMDSMI_STATUS_SUCCESS;
 }
 
+// state_dir/gpu<i>.vram_used: MiB in use (default 0).
+amdsmi_status_t amdsmi_get_gpu_memory_usage(amdsmi_processor_handle h, amdsmi_memory_type_t, uint64_t* used) {
+  GET_PROC(h);
+  uint64_t mib = 0;
+  if (!g->state_dir.empty()) {
+    std::ifstream f(g->state_dir + "/gpu" + std::to_string(p->gpu) + ".vram_used");
+    if (!(f >> mib) && f.is_open()) return AMDSMI_STATUS_NOT_SUPPORTED;
+  }
+  *used = mib << 20;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
 // state_dir/gpu<i>.partition ("CPX NPS2") overrides the fixture's modes: an
 // operator re-partitioning the GPU behind the daemon's back.
 static bool PartitionOverride(const MockProc* p, std::string* cmode, std::string* mmode) {

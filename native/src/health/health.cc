@@ -83,6 +83,16 @@ std::map<std::string, uint32_t> HealthCounters::RetiredPages() const {
   return retired_;
 }
 
+void HealthCounters::SetVramUsed(const std::string& bdf, uint64_t bytes) {
+  std::lock_guard<std::mutex> lk(mu_);
+  vram_used_[bdf] = bytes;
+}
+
+std::map<std::string, uint64_t> HealthCounters::VramUsed() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return vram_used_;
+}
+
 int Monitor::Classify(const HealthConfig& cfg, uint32_t type) {
   if (cfg.ignored.count(type)) return 0;
   if (type == smi::kEvtGpuPostReset) return +1;
@@ -411,6 +421,7 @@ void Monitor::PollOnce() {
     } else {
       counters_->retired_read_errors.fetch_add(1);
     }
+    if (auto used = lib_->VramUsed(h); used.ok()) counters_->SetVramUsed(g.bdf, *used);
     auto ecc = lib_->UncorrectableErrors(h);
     if (!ecc.ok()) {
       counters_->ecc_read_errors.fetch_add(1);

@@ -103,11 +103,15 @@ struct HealthCounters {
   // Last retired-page count per GPU (by PCI address), for /metrics.
   void SetRetiredPages(const std::string& bdf, uint32_t n);
   std::map<std::string, uint32_t> RetiredPages() const;
+  // Last HBM-in-use reading per GPU (bytes, all processes), for /metrics.
+  void SetVramUsed(const std::string& bdf, uint64_t bytes);
+  std::map<std::string, uint64_t> VramUsed() const;
   std::string Json() const;
 
  private:
   mutable std::mutex mu_;
   std::map<std::string, uint32_t> retired_;
+  std::map<std::string, uint64_t> vram_used_;
 };
 
 // Per-GPU health verdicts shared by all Monitor generations of a daemon.

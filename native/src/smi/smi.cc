@@ -30,6 +30,7 @@ struct Library::Fns {
   decltype(&amdsmi_get_gpu_topo_numa_affinity) numa = nullptr;
   decltype(&amdsmi_get_gpu_vram_info) vram_info = nullptr;
   decltype(&amdsmi_get_gpu_memory_total) memory_total = nullptr;
+  decltype(&amdsmi_get_gpu_memory_usage) memory_usage = nullptr;
   decltype(&amdsmi_get_gpu_compute_partition) compute_partition = nullptr;
   decltype(&amdsmi_get_gpu_memory_partition) memory_partition = nullptr;
   decltype(&amdsmi_get_gpu_kfd_info) kfd_info = nullptr;
@@ -113,6 +114,7 @@ Result<std::unique_ptr<Library>> Library::Open(const std::string& path,
   Resolve(dl, "amdsmi_get_gpu_topo_numa_affinity", &f->numa);
   Resolve(dl, "amdsmi_get_gpu_vram_info", &f->vram_info);
   Resolve(dl, "amdsmi_get_gpu_memory_total", &f->memory_total);
+  Resolve(dl, "amdsmi_get_gpu_memory_usage", &f->memory_usage);
   Resolve(dl, "amdsmi_get_gpu_compute_partition", &f->compute_partition);
   Resolve(dl, "amdsmi_get_gpu_memory_partition", &f->memory_partition);
   Resolve(dl, "amdsmi_get_gpu_kfd_info", &f->kfd_info);
@@ -376,6 +378,14 @@ Result<uint32_t> Library::RetiredPages(void* h) {
   amdsmi_status_t st = f_->bad_pages(h, &n, nullptr);  // count only
   if (st != AMDSMI_STATUS_SUCCESS) return Unavailable("bad page query failed (" + std::to_string(st) + ")");
   return n;
+}
+
+Result<uint64_t> Library::VramUsed(void* h) {
+  if (!f_->memory_usage) return NotSupported("memory usage query not present");
+  uint64_t used = 0;
+  amdsmi_status_t st = f_->memory_usage(h, AMDSMI_MEM_TYPE_VRAM, &used);
+  if (st != AMDSMI_STATUS_SUCCESS) return Unavailable("memory usage query failed (" + std::to_string(st) + ")");
+  return used;
 }
 
 Result<uint32_t> Library::RetiredPageThreshold(void* h) {

@@ -107,6 +107,8 @@ class Library {
   // which the driver itself gives up on the GPU (needs root on current drivers).
   Result<uint32_t> RetiredPages(void* h);
   Result<uint32_t> RetiredPageThreshold(void* h);
+  // HBM in use on the device (bytes, every process: amdsmi_get_gpu_memory_usage).
+  Result<uint64_t> VramUsed(void* h);
   bool Responsive(void* h);
 
   // Current compute/memory partition mode of a processor, e.g. {"CPX", "NPS2"}

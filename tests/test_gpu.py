@@ -309,14 +309,16 @@ def test_container_hbm_metrics_follow_pytorch(scratch, snap):
     k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
     d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--resource-config", "gpu:gpu-mem-gb:-1",
                                                      "--replica-policy", "pack", "--enforce-memory-units",
-                                                     "--memcap-lib", shim, "--metrics-addr", "127.0.0.1:0"]).start()
+                                                     "--memcap-lib", shim, "--metrics-addr", "127.0.0.1:0"],
+                       env={"DP_HEALTH_POLL_MS": "100"}).start()
     p = None
 
     def scrape():
         with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
             body = r.read().decode()
         vals = {}
-        for m in re.finditer(r'^(amdgpu_dp_container_hbm_\w+)\{[^}]*\} (\d+)$', body, re.M):
+        for m in re.finditer(r'^(amdgpu_dp_container_hbm_\w+|amdgpu_dp_gpu_hbm_used_bytes)\{[^}]*\} (\d+)$',
+                             body, re.M):
             vals[m.group(1)] = int(m.group(2))
         return vals
     try:
@@ -348,6 +350,7 @@ def test_container_hbm_metrics_follow_pytorch(scratch, snap):
         p = subprocess.Popen([sys.executable, "-c", code], env={**os.environ, **envs}, stdin=subprocess.PIPE,
                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         assert p.stdout.readline().strip() == "holding", p.stderr.read()[-2000:]
+        time.sleep(0.3)  # a health poll reads the driver's view of the GPU
         held = scrape()
         p.stdin.close()
         assert p.wait(60) == 0
@@ -357,6 +360,8 @@ def test_container_hbm_metrics_follow_pytorch(scratch, snap):
         assert held["amdgpu_dp_container_hbm_granted_bytes"] == 4000 * mib
         assert 3 << 30 <= held["amdgpu_dp_container_hbm_used_bytes"] <= 4000 * mib, held
         assert held["amdgpu_dp_container_hbm_refusals_total"] >= 1, held
+        # the driver sees at least what the shim counted for the container
+        assert held["amdgpu_dp_gpu_hbm_used_bytes"] >= held["amdgpu_dp_container_hbm_used_bytes"], held
         assert after["amdgpu_dp_container_hbm_used_bytes"] == 0, after
         assert after["amdgpu_dp_container_hbm_peak_bytes"] >= 3 << 30, after
         os.makedirs("gpurun_out/memcap", exist_ok=True)
