@@ -229,6 +229,7 @@ void ReclaimDead(SharedArea* a, int mine, bool full = true) {
     for (int d = 0; d < kMaxDevices; ++d) SubSat(a->used[d], sl.bytes[d].exchange(0));
     sl.start.store(0);
     sl.pid.store(0);
+    a->processes.fetch_sub(1);
   }
 }
 
@@ -240,6 +241,7 @@ void ReleaseSlot() {
   for (int d = 0; d < kMaxDevices; ++d) SubSat(s.area->used[d], sl.bytes[d].exchange(0));
   sl.start.store(0);
   sl.pid.store(0);
+  s.area->processes.fetch_sub(1);
   s.released = true;
 }
 
@@ -334,6 +336,7 @@ void AttachShared(State& s) {
       int32_t zero = 0;
       if (s.area->slots[i].pid.compare_exchange_strong(zero, static_cast<int32_t>(s.slot_pid))) {
         s.area->slots[i].start.store(start);
+        s.area->processes.fetch_add(1);
         s.slot = i;
         break;
       }

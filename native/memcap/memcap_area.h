@@ -35,6 +35,8 @@ struct Area {
   uint32_t version;
   uint32_t devices;  // entries of cap[] in the grant
   uint32_t ids_len;  // bytes of ids[]
+  std::atomic<uint32_t> processes;  // slots held: processes of the container that use the shim
+  uint32_t reserved;
   std::atomic<uint64_t> used[kMaxDevices];     // bytes held by the container, per HIP device
   std::atomic<uint64_t> cap[kMaxDevices];      // bytes granted (0 = not capped)
   std::atomic<uint64_t> peak[kMaxDevices];     // high-water mark of used[]

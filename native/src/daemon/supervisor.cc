@@ -176,7 +176,7 @@ int ListGrants(const std::string& dir) {
     list(u.peak);
     out += ", \"refused\": ";
     list(u.refused);
-    out += ", \"mtime\": " + std::to_string(u.mtime_s) + "}";
+    out += ", \"processes\": " + std::to_string(u.processes) + ", \"mtime\": " + std::to_string(u.mtime_s) + "}";
   }
   out += first ? "]}\n" : "\n]}\n";
   fputs(out.c_str(), stdout);

@@ -198,6 +198,7 @@ Result<Usage> ReadGrant(const std::string& dir, const std::string& key) {
   u.cap = Column(h, offsetof(area::Area, cap), devices);
   u.peak = Column(h, offsetof(area::Area, peak), devices);
   u.refused = Column(h, offsetof(area::Area, refused), devices);
+  u.processes = std::min<uint32_t>(Field<uint32_t>(h, offsetof(area::Area, processes)), area::kSlots);
   // The container may have rewritten the IDs: kept only if they still name this file.
   std::string ids(reinterpret_cast<const char*>(h + offsetof(area::Area, ids)), ids_len);
   std::vector<std::string_view> parts;

@@ -48,6 +48,7 @@ struct Usage {
   std::string key;
   std::string ids;  // the IDs the file names, "" unless they hash to its key
   std::vector<uint64_t> used, cap, peak, refused;  // per HIP device of the container
+  uint32_t processes = 0;                          // the container's processes holding a slot
   int64_t mtime_s = 0;
 };
 

@@ -1091,6 +1091,11 @@ void Plugin::AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const 
          &memcap::Usage::peak);
   column("amdgpu_dp_container_hbm_refusals_total", "counter",
          "HIP allocations refused because they would pass the container's grant.", &memcap::Usage::refused);
+  family("amdgpu_dp_container_hbm_processes", "gauge", "Processes of the container using the HBM-cap shim.");
+  for (const auto& r : rows) {
+    snprintf(line, sizeof(line), "amdgpu_dp_container_hbm_processes{%s} %u\n", r.labels.c_str(), r.u.processes);
+    *out += line;
+  }
 }
 
 }  // namespace adp::plugin

@@ -360,6 +360,7 @@ def test_container_hbm_metrics_follow_pytorch(scratch, snap):
         assert held["amdgpu_dp_container_hbm_granted_bytes"] == 4000 * mib
         assert 3 << 30 <= held["amdgpu_dp_container_hbm_used_bytes"] <= 4000 * mib, held
         assert held["amdgpu_dp_container_hbm_refusals_total"] >= 1, held
+        assert held["amdgpu_dp_container_hbm_processes"] == 1 and after["amdgpu_dp_container_hbm_processes"] == 0
         # the driver sees at least what the shim counted for the container
         assert held["amdgpu_dp_gpu_hbm_used_bytes"] >= held["amdgpu_dp_container_hbm_used_bytes"], held
         assert after["amdgpu_dp_container_hbm_used_bytes"] == 0, after

@@ -377,6 +377,7 @@ def test_container_hbm_use_of_enforced_grants(scratch):
         assert _value(s, "amdgpu_dp_container_hbm_granted_bytes", **lab) == 3000 * mib
         assert _value(s, "amdgpu_dp_container_hbm_peak_bytes", **lab) == 2000 * mib
         assert _value(s, "amdgpu_dp_container_hbm_refusals_total", **lab) == 1
+        assert _value(s, "amdgpu_dp_container_hbm_processes", namespace="ml", pod="infer") == 1  # the holder
         holder.stdin.close()
         assert holder.wait(10) == 0
         holder = None
@@ -384,6 +385,7 @@ def test_container_hbm_use_of_enforced_grants(scratch):
         s = _parse(_get(port, "/metrics")[1])
         assert _value(s, "amdgpu_dp_container_hbm_used_bytes", **lab) == 0  # given back at exit
         assert _value(s, "amdgpu_dp_container_hbm_peak_bytes", **lab) == 2000 * mib
+        assert _value(s, "amdgpu_dp_container_hbm_processes", namespace="ml", pod="infer") == 0
 
         # The pod is gone: its file goes once it is two minutes old.
         pr.payload = _list_response([])
@@ -433,7 +435,7 @@ def test_container_hbm_files_without_pod_resources_and_tampered(scratch):
         usage_dir = os.path.dirname(p1)
         # The second container rewrites its IDs to claim the first one's devices... 
         with open(p2, "r+b") as f:
-            f.seek(16 + 4 * 64 * 8)  # ids[] after the four per-device columns
+            f.seek(24 + 4 * 64 * 8)  # ids[] after the header words and the four per-device columns
             f.write(b"somebody-else,")
         # ... a link and a directory posing as grant files ...
         os.symlink("/etc/passwd", os.path.join(usage_dir, "00000000000000aa.memcap"))
