@@ -160,6 +160,10 @@ const std::vector<FlagDef>& Table() {
        "memory-unit resources (replicas -1): mount and preload libadp_memcap.so in the container, which caps "
        "each device's HIP allocations at the HBM the pod was granted (AMD_GPU_MEMORY_LIMIT_MIB)",
        [](Flags& f) -> void* { return &f.enforce_memory_units; }},
+      {"memcap-ld-so-preload", "DP_MEMCAP_LD_SO_PRELOAD", "memcapLdSoPreload", Kind::kBool,
+       "with --enforce-memory-units: also mount a read-only /etc/ld.so.preload naming the shim, so a pod that "
+       "sets its own LD_PRELOAD still loads it (replaces the image's /etc/ld.so.preload, if any)",
+       [](Flags& f) -> void* { return &f.memcap_ld_so_preload; }},
       {"memcap-lib", "DP_MEMCAP_LIB", "memcapLib", Kind::kString,
        "path of libadp_memcap.so in the plugin's filesystem (default: next to the binary, then "
        "/usr/lib/amdgpu-device-plugin/)",

@@ -59,6 +59,7 @@ struct Flags {
   bool replica_hbm_share = false;     // time-slice replicas hold 1/R of the HBM each
   bool container_hbm_metrics = true;   // per-container HBM use in /metrics (with the HBM-cap shim)
   bool prestart_health_check = false;  // PreStartContainer refuses Unhealthy devices
+  bool memcap_ld_so_preload = false;  // also mount /etc/ld.so.preload naming the shim
   std::string memcap_lib;  // the shim in the plugin's filesystem ("" = next to the binary, then /usr/lib/...)
 };
 

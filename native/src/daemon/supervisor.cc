@@ -102,6 +102,29 @@ std::string InstallMemcap(const Flags& f) {
   return dst;
 }
 
+// --memcap-ld-so-preload: <plugin dir>/amdgpu-dp/ld.so.preload naming the
+// shim's path in the container; returns its path, or "" (logged).
+std::string InstallPreloadList(const Flags& f) {
+  std::string path = PathJoin(PathJoin(f.plugin_dir, "amdgpu-dp"), "ld.so.preload");
+  std::string want = std::string(plugin::kMemcapContainerPath) + "\n";
+  if (FILE* cur = fopen(path.c_str(), "rb")) {
+    char buf[512];
+    size_t n = fread(buf, 1, sizeof(buf), cur);
+    fclose(cur);
+    if (std::string(buf, n) == want) return path;
+  }
+  std::string tmp = path + ".tmp";
+  FILE* out = fopen(tmp.c_str(), "wb");
+  bool ok = out && fwrite(want.data(), 1, want.size(), out) == want.size();
+  if (out) ok = (fclose(out) == 0) && ok;
+  if (!ok || chmod(tmp.c_str(), 0644) != 0 || rename(tmp.c_str(), path.c_str()) != 0) {
+    LOG_ERROR(kComp, "--memcap-ld-so-preload: cannot write %s: %s", path.c_str(), strerror(errno));
+    unlink(tmp.c_str());
+    return "";
+  }
+  return path;
+}
+
 Result<Validated> Validate(const Config& cfg) {
   Validated v;
   const Flags& f = cfg.flags;
@@ -485,6 +508,9 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     cur_snap = *snap;
     cur_specs = *specs;
     v.popts.memcap_host_path = cfg.flags.enforce_memory_units ? InstallMemcap(cfg.flags) : "";
+    v.popts.memcap_preload_list = !v.popts.memcap_host_path.empty() && cfg.flags.memcap_ld_so_preload
+                                      ? InstallPreloadList(cfg.flags)
+                                      : "";
     v.popts.memcap_usage_dir = !v.popts.memcap_host_path.empty() && cfg.flags.container_hbm_metrics &&
                                        !cfg.flags.metrics_addr.empty()
                                    ? PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage")
@@ -554,6 +580,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     restarts.fetch_add(1);
     LOG_INFO(kComp, "re-registering plugins (devices and health monitor unchanged)");
     if (cfg.flags.enforce_memory_units) v.popts.memcap_host_path = InstallMemcap(cfg.flags);
+    if (!v.popts.memcap_preload_list.empty()) v.popts.memcap_preload_list = InstallPreloadList(cfg.flags);
     {
       std::lock_guard<std::mutex> lk(plugins_mu);
       for (auto& s : cur_specs) plugins.push_back(std::make_unique<plugin::Plugin>(cur_snap, s, v.popts));
@@ -689,6 +716,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
               if (!v.popts.memcap_host_path.empty() && std::string(e->name) == "amdgpu-dp") {
                 LOG_WARN(kComp, "inotify: %s was removed; reinstalling", v.popts.memcap_host_path.c_str());
                 InstallMemcap(cfg.flags);
+                if (!v.popts.memcap_preload_list.empty()) InstallPreloadList(cfg.flags);
               }
               for (auto& pl : plugins) {
                 struct stat st;

@@ -225,6 +225,12 @@ void Plugin::BuildUnits() {
     std::string mb;
     pb::Encode(m, &mb);
     pb::PutLen(&memcap_bytes_, 2, mb);
+    if (!opts_.memcap_preload_list.empty()) {
+      pb::Mount pl{"/etc/ld.so.preload", opts_.memcap_preload_list, true};
+      std::string pb_;
+      pb::Encode(pl, &pb_);
+      pb::PutLen(&memcap_bytes_, 2, pb_);
+    }
   }
   pb::DeviceSpec kfd{"/dev/kfd", PathJoin(opts_.driver_root, "/dev/kfd"), "rw"};
   std::string kb;

@@ -109,6 +109,9 @@ struct PluginOptions {
   // Host path of the HBM-cap shim; non-empty: memory-unit resources mount it
   // read-only at kMemcapContainerPath and set LD_PRELOAD to it.
   std::string memcap_host_path;
+  // Non-empty (with the shim): a host file naming the shim, mounted read-only
+  // at /etc/ld.so.preload, so the pod's own LD_PRELOAD cannot drop it.
+  std::string memcap_preload_list;
   // Non-empty (with the shim): each such Allocate() creates the grant's
   // accounting file here and mounts it, so /metrics reports what the
   // container uses (memcap/usage.h).

@@ -103,7 +103,8 @@ def test_sharing_and_health_gate_switches():
     assert vols[dp["name"]]["hostPath"]["path"] == dp["mountPath"]
     off = env(daemonset())
     assert off["DP_ENFORCE_MEMORY_UNITS"] == "false" and off["DP_PRESTART_HEALTH_CHECK"] == "false"
-    assert off["DP_CONTAINER_HBM_METRICS"] == "true"
+    assert off["DP_CONTAINER_HBM_METRICS"] == "true" and off["DP_MEMCAP_LD_SO_PRELOAD"] == "false"
+    assert env(daemonset({"memcapLdSoPreload": True}))["DP_MEMCAP_LD_SO_PRELOAD"] == "true"
     assert env(daemonset({"containerHbmMetrics": False}))["DP_CONTAINER_HBM_METRICS"] == "false"
 
 

@@ -352,3 +352,18 @@ def test_restarted_container_reclaims_its_predecessors_bytes(scratch):
     a.send_signal(signal.SIGKILL)  # the container is killed
     a.wait(10)
     assert _try(env, 2900) == (0, 100)  # all 3000 MiB are the new container's
+
+
+def test_ld_so_preload_list_keeps_the_shim_under_a_pods_own_ld_preload(scratch):
+    """--memcap-ld-so-preload: the response also mounts, read-only, an
+    /etc/ld.so.preload naming the shim -- glibc's loader reads it for every
+    process whatever LD_PRELOAD the pod spec sets (which overrides the
+    plugin's variable)."""
+    resp, log = _allocate(scratch, "gpu:gpu-mem-gb:-1", ["--memcap-ld-so-preload"])
+    mounts = {m.container_path: (m.host_path, m.read_only) for m in resp.mounts}
+    host, ro = mounts["/etc/ld.so.preload"]
+    assert ro and host == os.path.join(scratch, "amdgpu-dp", "ld.so.preload")
+    assert open(host).read() == "/usr/local/lib/amdgpu-dp/libadp_memcap.so\n"
+    assert dict(resp.envs)["LD_PRELOAD"] == "/usr/local/lib/amdgpu-dp/libadp_memcap.so"
+    resp, _ = _allocate(scratch, "gpu:gpu-mem-gb:-1")  # off by default
+    assert "/etc/ld.so.preload" not in {m.container_path for m in resp.mounts}
