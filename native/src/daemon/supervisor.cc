@@ -475,6 +475,30 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     backoff_ms = std::min(kMaxBackoffMs, backoff_ms * 2);
   };
 
+  // Starts (serves + registers) every plugin with devices; the number started,
+  // or -1 after scheduling a retry because the kubelet could not be reached.
+  auto start_plugins = [&]() -> int {
+    int started = 0;
+    for (auto& p : plugins) {
+      if (p->device_count() == 0) continue;
+      Status st = p->Start([efd] {
+        uint64_t one = 1;
+        ssize_t w = write(efd, &one, sizeof(one));
+        (void)w;
+      });
+      if (!st.ok()) {
+        LOG_ERROR(kComp, "could not contact kubelet, retrying (is the device-plugin feature "
+                         "enabled and is %s present?)", kubelet_sock.c_str());
+        schedule_retry("plugin start failed");
+        return -1;
+      }
+      ++started;
+    }
+    backoff_ms = 1000;
+    serving.store(true);
+    return started;
+  };
+
   auto restart = [&] {
     stop_all();
     ArmTimer(tfd, 0);  // disarm
@@ -529,24 +553,8 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
         for (auto& p : plugins) p->SetGpuHealth(gpu, false, why);
       }
     }
-    int started = 0;
-    for (auto& p : plugins) {
-      if (p->device_count() == 0) continue;
-      Status st = p->Start([efd] {
-        uint64_t one = 1;
-        ssize_t w = write(efd, &one, sizeof(one));
-        (void)w;
-      });
-      if (!st.ok()) {
-        LOG_ERROR(kComp, "could not contact kubelet, retrying (is the device-plugin feature "
-                         "enabled and is %s present?)", kubelet_sock.c_str());
-        schedule_retry("plugin start failed");
-        return;
-      }
-      ++started;
-    }
-    backoff_ms = 1000;
-    serving.store(true);
+    int started = start_plugins();
+    if (started < 0) return;
     if (started == 0) LOG_INFO(kComp, "no devices found; waiting indefinitely");
     monitor = std::make_unique<health::Monitor>(lib->get(), *snap, hcfg, &ledger, &health_counters);
     monitor->SetLayoutListener([lfd](const std::string&) {
@@ -592,22 +600,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
         for (auto& p : plugins) p->SetGpuHealth(gpu, false, why);
       }
     }
-    for (auto& p : plugins) {
-      if (p->device_count() == 0) continue;
-      Status st = p->Start([efd] {
-        uint64_t one = 1;
-        ssize_t w = write(efd, &one, sizeof(one));
-        (void)w;
-      });
-      if (!st.ok()) {
-        LOG_ERROR(kComp, "could not contact kubelet, retrying (is the device-plugin feature "
-                         "enabled and is %s present?)", kubelet_sock.c_str());
-        schedule_retry("plugin start failed");
-        return;
-      }
-    }
-    backoff_ms = 1000;
-    serving.store(true);
+    start_plugins();
   };
 
   // Re-reads flags/env/file; on success adopts the new config (startup-bound
