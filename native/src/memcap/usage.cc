@@ -149,7 +149,14 @@ constexpr size_t kMaxPending = 4096;
 void CreateGrantFileAsync(std::string dir, std::string key, std::vector<uint64_t> cap_bytes, std::string ids_joined) {
   Writer& w = TheWriter();
   std::lock_guard<std::mutex> lk(w.mu);
-  if (w.jobs.size() >= kMaxPending) return;  // the filesystem is stuck: the shim falls back to /dev/shm
+  if (w.jobs.size() >= kMaxPending) {  // the filesystem is stuck: the shim falls back to /dev/shm
+    if (!w.warned) {
+      w.warned = true;
+      LOG_WARN("memcap", "%zu grant files waiting to be written; dropping new ones (HBM use not reported)",
+               w.jobs.size());
+    }
+    return;
+  }
   w.jobs.push_back({std::move(dir), std::move(key), std::move(ids_joined), std::move(cap_bytes)});
   ++w.queued;
   w.cv.notify_one();
