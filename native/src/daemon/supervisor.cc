@@ -425,6 +425,12 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
             for (const auto& [bdf, n] : retired)
               out += "amdgpu_dp_retired_pages{bdf=\"" + metrics::LabelValue(bdf) + "\"} " + std::to_string(n) + "\n";
           }
+          if (auto total = health_counters.VramTotal(); !total.empty()) {
+            out += "# HELP amdgpu_dp_gpu_hbm_total_bytes HBM of the GPU.\n"
+                   "# TYPE amdgpu_dp_gpu_hbm_total_bytes gauge\n";
+            for (const auto& [bdf, n] : total)
+              out += "amdgpu_dp_gpu_hbm_total_bytes{bdf=\"" + metrics::LabelValue(bdf) + "\"} " + std::to_string(n) + "\n";
+          }
           if (auto used = health_counters.VramUsed(); !used.empty()) {
             out += "# HELP amdgpu_dp_gpu_hbm_used_bytes HBM in use on the GPU, all processes (last health poll).\n"
                    "# TYPE amdgpu_dp_gpu_hbm_used_bytes gauge\n";

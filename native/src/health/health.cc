@@ -93,6 +93,16 @@ std::map<std::string, uint64_t> HealthCounters::VramUsed() const {
   return vram_used_;
 }
 
+void HealthCounters::SetVramTotal(const std::string& bdf, uint64_t bytes) {
+  std::lock_guard<std::mutex> lk(mu_);
+  vram_total_[bdf] = bytes;
+}
+
+std::map<std::string, uint64_t> HealthCounters::VramTotal() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return vram_total_;
+}
+
 int Monitor::Classify(const HealthConfig& cfg, uint32_t type) {
   if (cfg.ignored.count(type)) return 0;
   if (type == smi::kEvtGpuPostReset) return +1;
@@ -325,6 +335,7 @@ Status Monitor::Start() {
       Notify(g.index, false, r.reason);
     }
   }
+  for (const auto& g : snap_->gpus) counters_->SetVramTotal(g.bdf, g.vram_mib << 20);
   LOG_INFO(kComp, "health monitor watching %zu GPU(s) (events %s, poll every %d ms)", snap_->gpus.size(),
            events_ok_ ? "on" : "off", cfg_.poll_interval_ms);
   if (!events_ok_ && cfg_.poll_interval_ms == 0) return Status::Ok();

@@ -106,12 +106,15 @@ struct HealthCounters {
   // Last HBM-in-use reading per GPU (bytes, all processes), for /metrics.
   void SetVramUsed(const std::string& bdf, uint64_t bytes);
   std::map<std::string, uint64_t> VramUsed() const;
+  // HBM of each GPU (bytes, from the snapshot), next to VramUsed().
+  void SetVramTotal(const std::string& bdf, uint64_t bytes);
+  std::map<std::string, uint64_t> VramTotal() const;
   std::string Json() const;
 
  private:
   mutable std::mutex mu_;
   std::map<std::string, uint32_t> retired_;
-  std::map<std::string, uint64_t> vram_used_;
+  std::map<std::string, uint64_t> vram_used_, vram_total_;
 };
 
 // Per-GPU health verdicts shared by all Monitor generations of a daemon.

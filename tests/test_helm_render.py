@@ -186,7 +186,7 @@ def test_prometheus_operator_objects():
     assert sm["spec"]["selector"]["matchLabels"].items() <= svc["metadata"]["labels"].items()
     assert sm["spec"]["endpoints"] == [{"port": "metrics", "path": "/metrics", "interval": "30s"}]
     rules = rule["spec"]["groups"][0]["rules"]
-    assert len(rules) == 5 and all(r["alert"].startswith("AmdGpu") for r in rules)
+    assert len(rules) == 6 and all(r["alert"].startswith("AmdGpu") for r in rules)
     assert "> 0.9" in [r for r in rules if r["alert"] == "AmdGpuContainerNearHbmGrant"][0]["expr"]
     # every metric an alert uses is one the daemon exports
     src = "".join(open(f).read() for f in glob.glob(os.path.join(ROOT, "native", "src", "*", "*.cc")))

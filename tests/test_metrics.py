@@ -313,6 +313,8 @@ def test_health_liveness_is_reported(scratch):
         s = _parse(_get(port, "/metrics")[1])
         assert sorted(v for (n, ls), v in s.items() if n == "amdgpu_dp_retired_pages") == [0.0, 3.0]
         assert sorted(v for (n, ls), v in s.items() if n == "amdgpu_dp_gpu_hbm_used_bytes") == [0.0, 1234 << 20]
+        assert sorted(v for (n, ls), v in s.items() if n == "amdgpu_dp_gpu_hbm_total_bytes") == \
+            [float(fixtures.MI355X_VRAM_MIB << 20)] * 2
         assert _value(s, "amdgpu_dp_health_retired_page_reads_total", result="ok") >= 4
         assert _value(s, "amdgpu_dp_health_events_enabled") == 0
         assert _value(s, "amdgpu_dp_health_polls_total") >= 2
