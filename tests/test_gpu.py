@@ -181,6 +181,8 @@ def test_metrics_endpoint_on_real_gpu(scratch, snap):
         assert f'amdgpu_dp_device_healthy{{resource="amd.com/gpu",device="{g["uuid"]}"' in body
         assert 'amdgpu_dp_allocatable{resource="amd.com/gpu"} 1' in body
         assert 'amdgpu_dp_build_info{version=' in body
+        # the GPU's HBM as enumerated (294,896 MiB on an MI355X), for used/total alerts
+        assert f'amdgpu_dp_gpu_hbm_total_bytes{{bdf="{g["bdf"]}"}} {g["vram_mib"] << 20}' in body
     finally:
         assert d.stop() == 0
         k.stop()
