@@ -23,7 +23,9 @@
 //   int adp_probe_list(char* out, int len);                       // JSON array
 //   int adp_probe_run(int device, unsigned long long bytes, int iters, char* out, int len);
 // Return 0 on success, a hipError_t (>0) on failure; `out` holds JSON either way.
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -33,6 +35,8 @@
 #include <set>
 #include <string>
 #include <vector>
+
+#include "../memcap/memcap_area.h"
 
 namespace {
 
@@ -632,13 +636,31 @@ extern "C" int adp_probe_grant(int device, unsigned long long grant_mib, char* o
   (void)hipGetLastError();  // the refusal is expected: clear it
   p = nullptr;
   bool half_ok = hipMalloc(&p, grant / 2) == hipSuccess;
+  // While it is held: the grant's free memory went down by it, and -- when the
+  // plugin mounted the grant's accounting file -- the file counts it (what
+  // /metrics reports for this container).
+  size_t free_held = 0, total_held = 0;
+  bool accounted = half_ok && hipMemGetInfo(&free_held, &total_held) == hipSuccess && free_held + grant / 2 <= free_b;
+  const char* file_state = "null";
+  if (const char* f = getenv("ADP_MEMCAP_FILE"); f && half_ok) {
+    uint64_t used = 0;
+    int fd = open(f, O_RDONLY | O_CLOEXEC);
+    bool got = fd >= 0 && device >= 0 && device < adp_memcap::kMaxDevices &&
+               pread(fd, &used, sizeof(used), offsetof(adp_memcap::Area, used) + device * sizeof(uint64_t)) ==
+                   static_cast<ssize_t>(sizeof(used));
+    if (fd >= 0) close(fd);
+    file_state = got && used >= grant / 2 ? "true" : "false";
+  }
   if (half_ok) (void)hipFree(p);
   (void)hipGetLastError();
-  bool ok = over_refused && half_ok && (total_b >> 20) == grant_mib && (prop.totalGlobalMem >> 20) == grant_mib;
+  bool ok = over_refused && half_ok && accounted && (total_b >> 20) == grant_mib &&
+            (prop.totalGlobalMem >> 20) == grant_mib && strcmp(file_state, "false") != 0;
   snprintf(out, len,
            "{\"device\": %d, \"grant_mib\": %llu, \"total_mib\": %zu, \"free_mib\": %zu, \"props_mib\": %zu, "
-           "\"over_grant_refused\": %s, \"half_grant_ok\": %s, \"enforced\": %s}",
+           "\"over_grant_refused\": %s, \"half_grant_ok\": %s, \"accounted\": %s, \"grant_file_counts\": %s, "
+           "\"enforced\": %s}",
            device, grant_mib, total_b >> 20, free_b >> 20, static_cast<size_t>(prop.totalGlobalMem >> 20),
-           over_refused ? "true" : "false", half_ok ? "true" : "false", ok ? "true" : "false");
+           over_refused ? "true" : "false", half_ok ? "true" : "false", accounted ? "true" : "false", file_state,
+           ok ? "true" : "false");
   return ok ? 0 : 3;
 }

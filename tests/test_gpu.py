@@ -296,7 +296,7 @@ def test_memcap_shim_enforces_the_grant_on_pytorch(scratch, snap):
         json.dump({"allocate_envs": envs, "result": out, "stderr_tail": r.stderr[-1500:]}, f, indent=1)
 
 
-def test_container_hbm_metrics_follow_pytorch(scratch, snap):
+def test_container_hbm_metrics_follow_pytorch(scratch, snap, probe_built):
     """--enforce-memory-units + --metrics-addr on the real MI355X: the grant's
     accounting file is mounted, and /metrics shows what an unmodified PyTorch
     process holds while it runs, its refused allocation, and the peak after it
@@ -367,9 +367,16 @@ def test_container_hbm_metrics_follow_pytorch(scratch, snap):
         assert held["amdgpu_dp_gpu_hbm_used_bytes"] >= held["amdgpu_dp_container_hbm_used_bytes"], held
         assert after["amdgpu_dp_container_hbm_used_bytes"] == 0, after
         assert after["amdgpu_dp_container_hbm_peak_bytes"] >= 3 << 30, after
+        # The in-pod validation sees its allocation counted in the grant file too.
+        from k8s_gpu_sharing_plugin_amd import PROBE_BIN
+        pr = subprocess.run([PROBE_BIN, "--check-grant", "--device", "0"], capture_output=True, text=True,
+                            timeout=120, env={**os.environ, **envs})
+        assert pr.returncode == 0, pr.stdout + pr.stderr[-2000:]
+        check = json.loads(pr.stdout.strip().splitlines()[-1])
+        assert check["enforced"] and check["accounted"] and check["grant_file_counts"] is True, check
         os.makedirs("gpurun_out/memcap", exist_ok=True)
         with open("gpurun_out/memcap/container_hbm_metrics.json", "w") as f:
-            json.dump({"while_holding": held, "after_exit": after}, f, indent=1)
+            json.dump({"while_holding": held, "after_exit": after, "probe_check_grant": check}, f, indent=1)
     finally:
         if p:
             p.kill()
