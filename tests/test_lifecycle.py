@@ -69,6 +69,10 @@ def test_kubelet_restart_is_detected(scratch):
     c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
     assert len(c.watch()[0].get(timeout=5).devices) == 2
     c.close()
+    # the same plugins re-registered: no re-enumeration, the health monitor kept
+    log = d.log()
+    assert "re-registering plugins (devices and health monitor unchanged)" in log
+    assert log.count("health monitor watching") == 1 and log.count("retrieving plugins") == 1
     assert d.stop() == 0
     k2.stop()
 
