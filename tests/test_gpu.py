@@ -354,6 +354,11 @@ def test_container_hbm_metrics_follow_pytorch(scratch, snap, probe_built):
         assert p.stdout.readline().strip() == "holding", p.stderr.read()[-2000:]
         time.sleep(0.3)  # a health poll reads the driver's view of the GPU
         held = scrape()
+        from k8s_gpu_sharing_plugin_amd import DAEMON
+        listed = json.loads(subprocess.run([DAEMON, "--list-grants", "--device-plugin-path", scratch],
+                                           capture_output=True, text=True, timeout=30, check=True).stdout)
+        (grant,) = listed["grants"]
+        assert grant["used"] == [held["amdgpu_dp_container_hbm_used_bytes"]] and grant["processes"] == 1, grant
         p.stdin.close()
         assert p.wait(60) == 0
         p = None
