@@ -537,6 +537,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     restarts.fetch_add(1);
     cur_snap = *snap;
     cur_specs = *specs;
+    for (const auto& g : cur_snap->gpus) health_counters.SetVramTotal(g.bdf, g.vram_mib << 20);
     v.popts.memcap_host_path = cfg.flags.enforce_memory_units ? InstallMemcap(cfg.flags) : "";
     v.popts.memcap_preload_list = !v.popts.memcap_host_path.empty() && cfg.flags.memcap_ld_so_preload
                                       ? InstallPreloadList(cfg.flags)

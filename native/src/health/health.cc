@@ -335,7 +335,6 @@ Status Monitor::Start() {
       Notify(g.index, false, r.reason);
     }
   }
-  for (const auto& g : snap_->gpus) counters_->SetVramTotal(g.bdf, g.vram_mib << 20);
   LOG_INFO(kComp, "health monitor watching %zu GPU(s) (events %s, poll every %d ms)", snap_->gpus.size(),
            events_ok_ ? "on" : "off", cfg_.poll_interval_ms);
   if (!events_ok_ && cfg_.poll_interval_ms == 0) return Status::Ok();

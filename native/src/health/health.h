@@ -106,7 +106,7 @@ struct HealthCounters {
   // Last HBM-in-use reading per GPU (bytes, all processes), for /metrics.
   void SetVramUsed(const std::string& bdf, uint64_t bytes);
   std::map<std::string, uint64_t> VramUsed() const;
-  // HBM of each GPU (bytes, from the snapshot), next to VramUsed().
+  // HBM of each GPU (bytes, from the snapshot; set by the supervisor), next to VramUsed().
   void SetVramTotal(const std::string& bdf, uint64_t bytes);
   std::map<std::string, uint64_t> VramTotal() const;
   std::string Json() const;
