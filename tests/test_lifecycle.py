@@ -59,6 +59,9 @@ def test_kubelet_restart_is_detected(scratch):
     k = kubelet.StubKubelet(sock(scratch)).start()
     d = harness.Daemon(scratch).start()
     k.wait_registration()
+    # the daemon has the Register() response (stopping the stub earlier fails
+    # the call, and the retry is a full restart) and its monitor runs
+    d.wait_log("health monitor watching")
     k.stop()
     if os.path.exists(sock(scratch)):
         os.unlink(sock(scratch))
