@@ -1,21 +1,33 @@
 """Multi-rank pod-churn benchmark of the device plugin.
 
-One process per GPU (torchrun). Rank 0 starts the native stub kubelet and the
-real ``amdgpu-device-plugin`` daemon serving exactly the N GPUs of the job
-(``--devices 0..N-1``; real libamd_smi on a GPU box, the amdsmi mock with an
-N x MI355X node model elsewhere). Every rank then plays kubelet for its own
-GPU's devices: each "pod" is GetPreferredAllocation(free, 1) + Allocate(chosen)
+One process per GPU. ``python bench.py --gpus N`` with N > 1 and no launcher
+starts the N ranks itself (``torch.distributed.run`` as a child process,
+before this process touches the GPU) and exits with the job's status; under a
+launcher every rank runs ``run()``.
+
+Every rank names its own GPU by PCI address (HIP device ``LOCAL_RANK`` on a
+GPU box; GPU ``LOCAL_RANK`` of the 8-GPU node model on the mock), the addresses
+are all-gathered, and rank 0 starts the native stub kubelet and the real
+``amdgpu-device-plugin`` daemon serving exactly those GPUs (``--devices
+<bdf>,...``: amdsmi's enumeration order and HIP's can differ, and amdsmi ignores
+``HIP_VISIBLE_DEVICES``). Rank 0 records the node as the daemon's inventory code
+sees it -- compute/memory mode and xGMI links down per GPU, the N x N link
+type / hops / weight matrix -- and one real GetPreferredAllocation(k=min(4,N))
+answer over the whole served set. Then each rank plays kubelet for the devices
+of its own GPU: a "pod" is GetPreferredAllocation(free, 1) + Allocate(chosen)
 on one persistent gRPC connection, retiring the oldest pod when its share of
 the node is full. One step = ``pods_per_step`` pods per rank. The K timed steps
 run between barrier + device-synchronize brackets; the job reports the max
 over ranks.
 
 After the timed region each rank runs the HIP probe on the GPU its kubelet
-client admitted (real hardware only) -- found by PCI address, since amdsmi's
-enumeration order and HIP's device order can differ -- to show the allocated
-device is usable and has the advertised shape. The JSON records the RCCL world
-as torch.distributed saw it, the backend, and per rank the BDF it admitted
-next to the BDF the probe ran on.
+client admitted (real hardware only) to show the allocated device is usable
+and has the advertised shape. The JSON records the RCCL world as
+torch.distributed saw it, the backend, and per rank the BDF it owns, the BDFs
+it admitted and the BDF the probe ran on.
+
+Reference: the kubelet-facing calls timed here are
+/root/reference/cmd/nvidia-device-plugin/server.go:268-353.
 """
 
 import json
@@ -93,13 +105,13 @@ def _grpcio_allocate_p50(socket_path, device=None, calls=300):
         return None
 
 
-def _grpc_go_shaped(socket_path, pod_size, rank, world, warm, pods):
+def _grpc_go_shaped(socket_path, pod_size, rank, world, warm, pods, owned=None):
     """Allocate / GetPreferredAllocation latency with the client frame pattern of
     the kubelet's grpc-go transport (grpc::Channel::EmulateGrpcGo): what the
     plugin costs a real kubelet, next to the plain native-client headline."""
     from ..utils import native
     try:
-        c = native.ChurnClient(socket_path, pod_size=pod_size, rank=rank, world=world, grpc_go=True)
+        c = native.ChurnClient(socket_path, pod_size=pod_size, rank=rank, world=world, grpc_go=True, owned=owned)
         c.run(warm, record=False)
         c.reset()
         c.run(pods, record=True)
@@ -111,26 +123,82 @@ def _grpc_go_shaped(socket_path, pod_size, rank, world, warm, pods):
         return {"error": str(e)}
 
 
-def _bdf_map(real, fixture):
-    """Device ID (GPU or partition UUID) -> PCI address of its GPU."""
+def _node_snapshot(real, fixture, devices=None):
+    """The served GPUs as the daemon's inventory code enumerates them (the same
+    BuildSnapshot, through libadp_capi), or {} when enumeration fails."""
     from .. import MOCK_LIB
     from ..utils import native
     try:
         if real:
-            snap = native.snapshot()
-        else:
-            import tempfile
-            from ..models import fixtures
-            os.environ["AMDSMI_MOCK_FIXTURE"] = fixtures.write(fixture, tempfile.mkdtemp(prefix="adpbdf"))
-            snap = native.snapshot(MOCK_LIB)
+            return native.snapshot(devices=devices)
+        import tempfile
+        from ..models import fixtures
+        os.environ["AMDSMI_MOCK_FIXTURE"] = fixtures.write(fixture, tempfile.mkdtemp(prefix="adpbdf"))
+        return native.snapshot(MOCK_LIB, devices=devices)
     except Exception:
         return {}
+
+
+def _bdf_map(snap):
+    """Device ID (GPU or partition UUID) -> PCI address of its GPU."""
     out = {}
-    for g in snap["gpus"]:
+    for g in snap.get("gpus", []):
         out[g["uuid"]] = g["bdf"]
         for p in g["partitions"]:
             out[p["uuid"]] = g["bdf"]
     return out
+
+
+def _topology(snap, rank_bdfs):
+    """The node block of the JSON: what GetPreferredAllocation scores against."""
+    if not snap:
+        return {"error": "enumeration failed"}
+    return {
+        "amdsmi": snap.get("smi_version"),
+        "rank_bdfs": rank_bdfs,
+        "served_bdfs": [g["bdf"] for g in snap["gpus"]],
+        "gpus": [{"bdf": g["bdf"], "uuid": g["uuid"], "product": g.get("market_name"),
+                  "compute_mode": g["compute_mode"], "memory_mode": g["memory_mode"],
+                  "partitions": len(g["partitions"]), "numa": g["numa"], "vram_mib": g["vram_mib"],
+                  "xgmi_links_down": g["xgmi_links_down"]} for g in snap["gpus"]],
+        # rows/columns in served_bdfs order
+        "link_types": snap.get("link_types"),
+        "hops": snap.get("hops"),
+        "weights": snap.get("weights"),
+        "link_class": snap.get("links"),  # inventory::LinkClass the allocator scores
+    }
+
+
+def _rank_bdf(real, torch_mod, local_rank, fixture):
+    """PCI address of this rank's GPU: HIP device `local_rank` on a GPU box
+    (what torch.cuda.set_device binds), GPU `local_rank` of the node model on the mock."""
+    if real:
+        p = torch_mod.cuda.get_device_properties(local_rank)
+        return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    # ADP_BENCH_MOCK_GPUS="5,2": rank r owns node GPU list[r] -- a job that was
+    # given some of the node's GPUs, in an order that is not amdsmi's.
+    order = [int(x) for x in os.environ.get("ADP_BENCH_MOCK_GPUS", "").split(",") if x.strip()]
+    return fixture["gpus"][order[local_rank] if order else local_rank]["bdf"]
+
+
+def _preferred_probe(socket_path, k, bdf_of):
+    """One GetPreferredAllocation(k) over every advertised device, all free,
+    through grpcio (an independent gRPC stack): the placement a k-GPU pod gets."""
+    try:
+        from ..utils import kubelet
+        c = kubelet.PluginClient(socket_path)
+        q, call = c.watch()
+        ids = [d.ID for d in q.get(timeout=5).devices if d.health == "Healthy"]
+        call.cancel()
+        k = min(k, len(ids))
+        resp = c.preferred(ids, (), k)
+        c.close()
+        got = list(resp.container_responses[0].deviceIDs)
+        from ..utils import native
+        return {"k": k, "available": len(ids), "device_ids": got,
+                "bdfs": [bdf_of.get(i, bdf_of.get(native.strip_replicas([i])[0], "?")) for i in got]}
+    except Exception as e:  # reported, not fatal for the headline
+        return {"error": str(e)}
 
 
 def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_mock=False,
@@ -166,41 +234,63 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
     sync = _sync if real else (lambda _t: None)
 
     strategy, rc, desc = CONFIGS[config]
+    mode = "CPX" if config == "cpx-single" else "SPX"
+    # The mock plays a whole 8-GPU node (as on the driver's node, the job may
+    # own only some of its GPUs); mixed-gpu4 is BASELINE config 5's fixed node.
+    if config == "mixed-gpu4":
+        if real or world != 1:
+            raise SystemExit("mixed-gpu4 runs on the 8-GPU node model with one client (--mock, 1 rank)")
+        fx = fixtures.node(8, ["SPX"] * 6 + ["CPX"] * 2, memory="NPS1")
+    else:
+        fx = None if real else fixtures.node(max(8, gpus), mode, memory="NPS2" if mode == "CPX" else "NPS1")
+    my_bdf = _rank_bdf(real, torch, local_rank, fx)
+    rank_bdfs = [my_bdf]
+    if use_dist:
+        rank_bdfs = [None] * world
+        dist.all_gather_object(rank_bdfs, my_bdf)
     daemon = kub = None
     info = {}
     try:
         if rank == 0:
             d = harness.scratch_dir("adpbench")
             kub = harness.NativeKubelet(os.path.join(d, "kubelet.sock")).start()
-            args = ["--partition-strategy", strategy, "--devices", ",".join(str(i) for i in range(gpus))]
+            served = None if config == "mixed-gpu4" else rank_bdfs
+            args = ["--partition-strategy", strategy]
+            if served:
+                args += ["--devices", ",".join(served)]
             if rc:
                 args += ["--resource-config", rc]
-            mode = "CPX" if config == "cpx-single" else "SPX"
-            fx = None if real else fixtures.node(gpus, mode, memory="NPS2" if mode == "CPX" else "NPS1")
             if config == "auto-mem-enforced":
                 from .. import BUILD_DIR
                 args += ["--enforce-memory-units", "--memcap-lib", os.path.join(BUILD_DIR, "libadp_memcap.so"),
                          "--metrics-addr", "127.0.0.1:0"]
-            if config == "mixed-gpu4":
-                if real or world != 1:
-                    raise SystemExit("mixed-gpu4 runs on the 8-GPU node model with one client (--mock, 1 rank)")
-                fx = fixtures.node(8, ["SPX"] * 6 + ["CPX"] * 2, memory="NPS1")
-                args = ["--partition-strategy", strategy]
             daemon = harness.Daemon(d, fx, args=args, real_smi=real,
                                     env={"DP_HEALTH_POLL_MS": "0", "ADP_LOG_LEVEL": "warn"}).start()
             # The measured resource is amd.com/gpu (mixed registers partition resources too).
             reg = kub.wait(lambda e: e.get("event") == "register" and
                            (config not in POD_SIZE or e.get("resource", "").endswith("/gpu")), 20)
             devs = kub.wait(lambda e: e.get("event") == "devices" and e.get("resource") == reg["resource"], 20)
-            info = {"socket": os.path.join(d, reg["endpoint"]), "resource": reg["resource"],
+            snap = _node_snapshot(real, fx, served)
+            bdf_of = _bdf_map(snap)
+            sock = os.path.join(d, reg["endpoint"])
+            info = {"socket": sock, "resource": reg["resource"],
                     "allocatable": devs["healthy"], "advertised": devs["total"], "scratch": d,
-                    "bdf_of": _bdf_map(real, fx)}
+                    "bdf_of": bdf_of, "topology": _topology(snap, rank_bdfs),
+                    "preferred_k": _preferred_probe(sock, min(4, len(snap.get("gpus", [])) or 1), bdf_of)}
         if use_dist:
             box = [info]
             dist.broadcast_object_list(box, src=0)
             info = box[0]
 
-        client = native.ChurnClient(info["socket"], pod_size=POD_SIZE.get(config, 1), rank=rank, world=world)
+        # This rank churns the devices of its own GPU (every device when one
+        # client serves a multi-GPU pod size).
+        owned = None
+        if config not in POD_SIZE:
+            owned = sorted(i for i, b in info["bdf_of"].items() if b == my_bdf)
+            if not owned:
+                raise SystemExit(f"rank {rank}: the daemon serves no device on {my_bdf}")
+        client = native.ChurnClient(info["socket"], pod_size=POD_SIZE.get(config, 1), rank=rank, world=world,
+                                    owned=owned)
         client.run(max(1, warmup) * pods_per_step, record=False)
         client.reset()
 
@@ -221,13 +311,14 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
         # pattern (a BDP PING per response, grpc-go user-agent) ...
         stats["grpc_go_shaped"] = _grpc_go_shaped(info["socket"], POD_SIZE.get(config, 1), rank, world,
                                                   max(1, warmup) * pods_per_step,
-                                                  min(steps * pods_per_step, 2000))
+                                                  min(steps * pods_per_step, 2000), owned)
         # ... and every rank times its own device through grpcio.
         stats["grpcio_allocate_p50_us"] = _grpcio_allocate_p50(
             info["socket"], (stats.get("device_ids") or [None])[0])
 
         bdf_of = info.get("bdf_of") or {}
         stats["admitted_bdfs"] = sorted({bdf_of.get(i, "?") for i in stats.get("device_ids", [])})
+        stats["rank_bdf"] = my_bdf
         if real and probe:
             from ..ops import probe as hip_probe
             try:
@@ -301,11 +392,15 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                 "rccl_world": dist.get_world_size() if use_dist else 1,
                 "backend": dist.get_backend() if use_dist else "none",
                 "per_rank": [{**{k: s[k] for k in ("rank", "rank_devices", "pods", "allocate", "preferred")},
+                              "rank_bdf": s.get("rank_bdf"),
                               "admitted_bdfs": s.get("admitted_bdfs"), "probe_bdf": s.get("probe_bdf"),
                               "grpcio_allocate_p50_us": s.get("grpcio_allocate_p50_us"),
                               "grpc_go_shaped": s.get("grpc_go_shaped")}
                              for s in everyone],
             }
+            # The node the daemon served, and a k-GPU pod's placement on it.
+            result["topology"] = info.get("topology")
+            result["preferred_k"] = info.get("preferred_k")
             probes = [s.get("probe") for s in everyone if s.get("probe")]
             if probes:
                 result["probe"] = probes
@@ -358,8 +453,33 @@ def _kubelet_restart(kub, resource, rounds=5):
                  "devices_ms": round(statistics.median(devs), 3), "devices_ms_max": round(max(devs), 3)}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(gpus, argv):
+    """Runs this benchmark as a `gpus`-rank job: torch.distributed.run as a
+    child process (one rank per GPU, rendezvous on 127.0.0.1) and returns its
+    exit status. Called before anything in this process touches the GPU, so
+    the parent never holds a device while the ranks run."""
+    import subprocess
+    import sys
+    from .. import REPO_ROOT
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO_ROOT, "bench.py"), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL between ranks
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv=None):
     import argparse
+    import sys
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -369,6 +489,9 @@ def main(argv=None):
     ap.add_argument("--mock", action="store_true", help="use the amdsmi mock even on a GPU box")
     ap.add_argument("--no-probe", action="store_true")
     a = ap.parse_args(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # No launcher: start the ranks ourselves (rank 0 prints the JSON line).
+        raise SystemExit(launch_ranks(a.gpus, argv))
     res = run(a.gpus, a.steps, a.warmup, a.pods_per_step, a.config, a.mock, not a.no_probe)
     if res is not None:
         print(json.dumps(res), flush=True)

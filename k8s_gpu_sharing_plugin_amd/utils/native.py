@@ -107,7 +107,8 @@ def plugin_specs(lib_path: str = "", strategy="none", resource_config="", device
 class ChurnClient:
     """In-process pod-churn client (native/src/bench/churn.cc) on one plugin socket."""
 
-    def __init__(self, socket_path: str, pod_size=1, rank=0, world=1, preferred=True, grpc_go=False):
+    def __init__(self, socket_path: str, pod_size=1, rank=0, world=1, preferred=True, grpc_go=False,
+                 owned=None):
         so = lib()
         so.adp_bench_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
         so.adp_bench_open.restype = ctypes.c_void_p
@@ -119,7 +120,8 @@ class ChurnClient:
         so.adp_bench_close.argtypes = [ctypes.c_void_p]
         err = ctypes.c_void_p()
         cfg = json.dumps({"socket": socket_path, "pod_size": pod_size, "rank": rank, "world": world,
-                          "preferred": preferred, "grpc_go": grpc_go}).encode()
+                          "preferred": preferred, "grpc_go": grpc_go,
+                          **({"owned": list(owned)} if owned else {})}).encode()
         self._h = so.adp_bench_open(cfg, ctypes.byref(err))
         if not self._h:
             msg = ctypes.string_at(err.value).decode() if err.value else "unknown error"

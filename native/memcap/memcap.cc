@@ -12,11 +12,19 @@
 // that size themselves from free memory (PyTorch's mem_get_info, vLLM's
 // gpu_memory_utilization) stay inside the grant.
 //
-// Caps: AMD_GPU_MEMORY_LIMIT_MIB="<mib>[,<mib>...]", one per device in the
-// container's HIP order (the plugin writes it in that order); devices past the
-// list are not capped. The grant is the container's: its processes share the
-// counters (a shared-memory segment, see AttachShared). ADP_MEMCAP_VERBOSE=1
+// Caps: the grant files the daemon mounts read-only under /run/amdgpu-dp/grant/
+// (memcap_area.h kGrantDir: "<hip ordinal>" -> MiB) are authoritative; the
+// pod's AMD_GPU_MEMORY_LIMIT_MIB="<mib>[,<mib>...]" (one per device in HIP
+// order) can only lower them -- empty, missing or larger values change nothing
+// -- and is the whole cap only where no grant file is mounted. Devices past
+// both lists are not capped. The grant is the container's: its processes share
+// the counters (a shared-memory segment, see AttachShared). ADP_MEMCAP_VERBOSE=1
 // logs every decision to stderr.
+//
+// Stream-ordered pools: hipFreeAsync returns a block to its pool, which keeps
+// the memory reserved (release threshold) -- the bytes stay counted until a
+// refusal (or hipMemGetInfo) trims the pools and reads back what they still
+// reserve (ReconcilePools), so the pool can never hold memory past the cap.
 //
 // It has to load into whatever the workload's image is -- PyTorch-ROCm wheels
 // target glibc 2.28 -- so it needs nothing but old libc symbols: no libstdc++
@@ -31,6 +39,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime_api.h>
+#include <hip/hip_deprecated.h>
 #include <pthread.h>
 #include <signal.h>
 #include <stdarg.h>
@@ -65,6 +74,7 @@ T Min(T a, T b) {
 struct Entry {
   const void* key;  // nullptr = empty, Tomb() = erased
   int32_t device;
+  int32_t pooled;  // 1: a stream-ordered (pool) allocation
   uint64_t bytes;
 };
 inline const void* Tomb() { return reinterpret_cast<const void*>(uintptr_t{1}); }  // not a constant expression
@@ -111,7 +121,7 @@ struct Table {
     size_t i = Hash(k, cap);
     while (e[i].key && e[i].key != Tomb()) i = (i + 1) & (cap - 1);
     if (e[i].key == Tomb()) --tombs;
-    e[i] = {k, device, bytes};
+    e[i] = {k, device, 0, bytes};
     ++used;
     return true;
   }
@@ -146,7 +156,11 @@ struct State {
   Table allocs;                               // this process's allocations
   uint64_t local_used[kMaxDevices] = {};      // used when there is no shared segment
   uint64_t cap[kMaxDevices] = {};             // 0 = not capped
-  int devices = 0;                            // entries in AMD_GPU_MEMORY_LIMIT_MIB
+  uint64_t pool_live[kMaxDevices] = {};       // bytes of live stream-ordered allocations (this process)
+  uint64_t pool_held[kMaxDevices] = {};       // bytes freed to a pool, still counted (this process)
+  hipMemPool_t pools[kMaxDevices][4] = {};    // explicit pools seen (hipMallocFromPoolAsync)
+  int devices = 0;                            // devices with a cap entry (grant or env)
+  int granted = 0;                            // devices with a daemon grant file
   bool verbose = false;
   bool any_cap = false;
   std::atomic<bool> warned[kMaxDevices] = {};
@@ -364,21 +378,68 @@ void AtForkChild() {
   if (s.area) AttachShared(s);
 }
 
+// Reads "<dir>/<i>" grant files (i = 0, 1, ... until one is missing) into
+// `mib`; returns how many were read. A file that exists but is not a plain
+// number stops the list there (and is logged).
+int ReadGrantFiles(const char* dir, uint64_t* mib, int max) {
+  int n = 0;
+  for (; n < max; ++n) {
+    char path[256];
+    snprintf(path, sizeof(path), "%s/%d", dir, n);
+    int fd = open(path, O_RDONLY | O_CLOEXEC | O_NOFOLLOW | O_NONBLOCK);
+    if (fd < 0) break;
+    char buf[32];
+    ssize_t r = read(fd, buf, sizeof(buf) - 1);
+    close(fd);
+    if (r <= 0) break;
+    buf[r] = 0;
+    char* end = nullptr;
+    unsigned long long v = strtoull(buf, &end, 10);
+    if (end == buf || (*end && *end != '\n') || v == 0 || v > (uint64_t{1} << 43)) {
+      Log("grant file %s is not a MiB count; devices from %d on are capped by AMD_GPU_MEMORY_LIMIT_MIB only", path, n);
+      break;
+    }
+    mib[n] = v;
+  }
+  return n;
+}
+
+// The grant directory: the daemon's read-only mount; ADP_MEMCAP_GRANT_DIR only
+// where nothing is mounted there (tests), so a pod cannot point it elsewhere.
+const char* GrantDir() {
+  // access(2), not stat(2): stat is a GLIBC_2.33 symbol (see the file comment).
+  if (access(adp_memcap::kGrantDir, F_OK) == 0) return adp_memcap::kGrantDir;
+  const char* env = getenv("ADP_MEMCAP_GRANT_DIR");
+  return env && env[0] == '/' ? env : nullptr;
+}
+
 void Init() {
   State& s = g_state;
   const char* v = getenv("ADP_MEMCAP_VERBOSE");
   s.verbose = v && *v && *v != '0';
+  // The daemon's grant first: authoritative.
+  uint64_t grant_mib[kMaxDevices] = {};
+  const char* gdir = GrantDir();
+  s.granted = gdir ? ReadGrantFiles(gdir, grant_mib, kMaxDevices) : 0;
+  for (int d = 0; d < s.granted; ++d) s.cap[d] = grant_mib[d] << 20;
+  // Then the environment: a lower value wins; never raises or removes a grant.
   const char* lim = getenv("AMD_GPU_MEMORY_LIMIT_MIB");
   int dev = 0;
   for (const char* p = lim; p && *p && dev < kMaxDevices; ++dev) {
     char* end = nullptr;
     unsigned long long mib = strtoull(p, &end, 10);
-    if (end != p) s.cap[dev] = static_cast<uint64_t>(mib) << 20;
-    s.any_cap = s.any_cap || s.cap[dev];
+    if (end != p && mib > 0 && mib < (uint64_t{1} << 43)) {
+      uint64_t b = static_cast<uint64_t>(mib) << 20;
+      if (!s.cap[dev] || b < s.cap[dev]) s.cap[dev] = b;
+    }
     p = strchr(p, ',');
     if (p) ++p;
   }
-  s.devices = dev;
+  s.devices = dev > s.granted ? dev : s.granted;
+  for (int d = 0; d < s.devices; ++d) s.any_cap = s.any_cap || s.cap[d];
+  if (s.verbose)
+    Log("%d device(s) granted by %s, AMD_GPU_MEMORY_LIMIT_MIB=%s", s.granted, gdir ? gdir : "(no grant files)",
+        lim ? lim : "(unset)");
   if (!s.any_cap) return;
   const char* file = getenv("ADP_MEMCAP_FILE");
   if (file && file[0] == '/' && strlen(file) < sizeof(s.file_path)) strcpy(s.file_path, file);
@@ -398,7 +459,7 @@ void Init() {
     mix(buf, n);
   }
   mix("|", 1);
-  mix(lim, strlen(lim));
+  for (int d = 0; d < s.devices; ++d) mix(reinterpret_cast<const char*>(&s.cap[d]), sizeof(s.cap[d]));
   const char* safe = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789_.-";
   if (k && *k && strlen(k) <= 64 && strspn(k, safe) == strlen(k))  // a named budget, findable in /dev/shm
     snprintf(s.shm_path, sizeof(s.shm_path), "/dev/shm/adp-memcap-key-%s-%08llx", k,
@@ -475,17 +536,16 @@ int StreamDevice(hipStream_t stream) {
   return CurrentDevice();
 }
 
-// Reserves `bytes` on `dev` for this process; false if that would take the
-// container past the cap.
-bool Reserve(int dev, uint64_t bytes) {
-  State& s = S();
-  if (!s.cap[dev]) return true;
-  Locked lk(s);
+// Reserves `bytes` on `dev` for this process (lock held); false if that would
+// take the container past the cap.
+bool TryReserveLocked(State& s, int dev, uint64_t bytes) {
   if (s.area && s.slot_pid != getpid()) AttachShared(s);  // a child forked around pthread_atfork
   if (s.area && !s.released) {
     for (int attempt = 0; attempt < 2; ++attempt) {
       uint64_t cur = s.area->used[dev].load();
-      while (cur + bytes <= s.cap[dev]) {
+      // cur + bytes <= cap without wrapping: a request near SIZE_MAX (an OOM
+      // probe, an overflowed size) must be refused, not wrapped under the cap.
+      while (bytes <= s.cap[dev] && cur <= s.cap[dev] - bytes) {
         if (s.area->used[dev].compare_exchange_weak(cur, cur + bytes)) {
           s.area->slots[s.slot].bytes[dev].fetch_add(bytes);
           RaisePeak(s.area->peak[dev], cur + bytes);
@@ -494,16 +554,36 @@ bool Reserve(int dev, uint64_t bytes) {
       }
       if (attempt == 0) ReclaimDead(s.area, s.slot);  // a dead process may still be counted
     }
-  } else if (s.local_used[dev] + bytes <= s.cap[dev]) {
+    return false;
+  }
+  if (bytes <= s.cap[dev] && s.local_used[dev] <= s.cap[dev] - bytes) {
     s.local_used[dev] += bytes;
     return true;
   }
-  if (s.area && !s.released) s.area->refused[dev].fetch_add(1);
-  if (s.verbose || !s.warned[dev].exchange(true))
-    Log("device %d: refused %.1f MiB (%.1f of %.1f MiB in use%s; AMD_GPU_MEMORY_LIMIT_MIB)", dev,
-        bytes / 1048576.0, UsedLocked(s, dev) / 1048576.0, s.cap[dev] / 1048576.0,
-        s.area ? " by the container" : "");
   return false;
+}
+
+void ReconcilePools(int dev);
+
+bool Reserve(int dev, uint64_t bytes) {
+  State& s = S();
+  if (!s.cap[dev]) return true;
+  for (int round = 0;; ++round) {
+    {
+      Locked lk(s);
+      if (TryReserveLocked(s, dev, bytes)) return true;
+      // Blocks freed to a stream-ordered pool are still counted: trim the
+      // pools and count only what they still hold, then try once more.
+      if (round == 0 && s.pool_held[dev] && bytes <= s.cap[dev]) goto reconcile;
+      if (s.area && !s.released) s.area->refused[dev].fetch_add(1);
+      if (s.verbose || !s.warned[dev].exchange(true))
+        Log("device %d: refused %.1f MiB (%.1f of %.1f MiB in use%s; the grant)", dev, bytes / 1048576.0,
+            UsedLocked(s, dev) / 1048576.0, s.cap[dev] / 1048576.0, s.area ? " by the container" : "");
+      return false;
+    }
+  reconcile:
+    ReconcilePools(dev);  // without the lock: it calls into HIP
+  }
 }
 
 void AddLocked(State& s, int dev, uint64_t bytes) {
@@ -552,7 +632,13 @@ void Untrack(const void* key) {
   if (!x) return;  // not ours (uncapped device, or before a cap)
   int dev = x->device;
   uint64_t bytes = x->bytes;
-  UnreserveLocked(s, dev, bytes);
+  if (x->pooled) {
+    // Back to its pool, which may keep it reserved: still counted (ReconcilePools).
+    s.pool_live[dev] -= Min(bytes, s.pool_live[dev]);
+    s.pool_held[dev] += bytes;
+  } else {
+    UnreserveLocked(s, dev, bytes);
+  }
   s.allocs.Erase(x);
   if (s.verbose) Log("device %d: -%llu bytes (%llu in use)", dev, static_cast<unsigned long long>(bytes),
                      static_cast<unsigned long long>(UsedLocked(s, dev)));
@@ -580,6 +666,129 @@ hipError_t Capped(int dev, uint64_t bytes, void** out, Call call) {
   }
   Track(*out, dev, bytes);
   return e;
+}
+
+// A stream-ordered allocation just tracked: from `pool` (nullptr: the
+// device's current pool).
+void MarkPooled(const void* key, int dev, hipMemPool_t pool) {
+  State& s = S();
+  if (!s.cap[dev] || !key) return;
+  Locked lk(s);
+  Entry* x = s.allocs.Find(key);
+  if (!x || x->pooled) return;
+  x->pooled = 1;
+  s.pool_live[dev] += x->bytes;
+  if (!pool) return;
+  for (auto& p : s.pools[dev]) {
+    if (p == pool) return;
+    if (!p) {
+      p = pool;
+      return;
+    }
+  }
+}
+
+// Trims every pool of `dev` this process allocated from and counts only what
+// they still reserve beyond the live allocations (hipMemPoolAttrReservedMemCurrent);
+// the rest of pool_held is given back to the grant.
+void ReconcilePools(int dev) {
+  static std::atomic<void*> s_def{nullptr}, s_cur{nullptr}, s_trim{nullptr}, s_attr{nullptr};
+  auto get_default = reinterpret_cast<hipError_t (*)(hipMemPool_t*, int)>(Cached(s_def, "hipDeviceGetDefaultMemPool"));
+  auto get_current = reinterpret_cast<hipError_t (*)(hipMemPool_t*, int)>(Cached(s_cur, "hipDeviceGetMemPool"));
+  auto trim = reinterpret_cast<hipError_t (*)(hipMemPool_t, size_t)>(Cached(s_trim, "hipMemPoolTrimTo"));
+  auto attr = reinterpret_cast<hipError_t (*)(hipMemPool_t, hipMemPoolAttr, void*)>(
+      Cached(s_attr, "hipMemPoolGetAttribute"));
+  if (!trim || !attr) return;
+  State& s = g_state;
+  hipMemPool_t pools[6] = {};
+  int n = 0;
+  {
+    Locked lk(s);
+    for (auto p : s.pools[dev])
+      if (p) pools[n++] = p;
+  }
+  hipMemPool_t p = nullptr;
+  if (get_default && get_default(&p, dev) == hipSuccess && p) pools[n++] = p;
+  p = nullptr;
+  if (get_current && get_current(&p, dev) == hipSuccess && p) pools[n++] = p;
+  uint64_t reserved = 0;
+  ++t_depth;  // whatever HIP calls back into this library passes through
+  for (int i = 0; i < n; ++i) {
+    bool dup = false;
+    for (int j = 0; j < i; ++j) dup = dup || pools[j] == pools[i];
+    if (dup) continue;
+    (void)trim(pools[i], 0);
+    uint64_t r = 0;
+    if (attr(pools[i], hipMemPoolAttrReservedMemCurrent, &r) != hipSuccess) {
+      --t_depth;
+      return;  // cannot tell: everything stays counted
+    }
+    reserved += r;
+  }
+  --t_depth;
+  Locked lk(s);
+  uint64_t held = reserved > s.pool_live[dev] ? reserved - s.pool_live[dev] : 0;
+  if (held < s.pool_held[dev]) {
+    if (s.verbose)
+      Log("device %d: pools hold %.1f MiB of %.1f MiB freed to them", dev, held / 1048576.0,
+          s.pool_held[dev] / 1048576.0);
+    UnreserveLocked(s, dev, s.pool_held[dev] - held);
+    s.pool_held[dev] = held;
+  }
+}
+
+// Saturating size arithmetic: an overflowing size is refused at the cap.
+uint64_t Mul(uint64_t a, uint64_t b) {
+  if (a && b > UINT64_MAX / a) return UINT64_MAX;
+  return a * b;
+}
+uint64_t Dim(size_t v) { return v ? v : 1; }
+
+// Bytes of one element of a channel format (bits of x, y, z, w).
+uint64_t ChannelBytes(const hipChannelFormatDesc* d) {
+  if (!d) return 0;
+  int bits = (d->x > 0 ? d->x : 0) + (d->y > 0 ? d->y : 0) + (d->z > 0 ? d->z : 0) + (d->w > 0 ? d->w : 0);
+  return static_cast<uint64_t>((bits + 7) / 8);
+}
+
+uint64_t FormatBytes(hipArray_Format f) {
+  switch (f) {
+    case HIP_AD_FORMAT_UNSIGNED_INT8:
+    case HIP_AD_FORMAT_SIGNED_INT8:
+      return 1;
+    case HIP_AD_FORMAT_UNSIGNED_INT16:
+    case HIP_AD_FORMAT_SIGNED_INT16:
+    case HIP_AD_FORMAT_HALF:
+      return 2;
+    default:
+      return 4;
+  }
+}
+
+// Bytes of a mipmapped array: every level, each half the previous (at least 1).
+uint64_t MipmapBytes(uint64_t elem, size_t w, size_t h, size_t d, unsigned levels) {
+  uint64_t total = 0;
+  for (unsigned l = 0; l < (levels ? levels : 1); ++l) {
+    uint64_t b = Mul(Mul(Mul(elem, Dim(w)), Dim(h)), Dim(d));
+    total = b > UINT64_MAX - total ? UINT64_MAX : total + b;
+    w = w > 1 ? w / 2 : w;
+    h = h > 1 ? h / 2 : h;
+    d = d > 1 ? d / 2 : d;
+  }
+  return total;
+}
+
+// Padding of a pitched allocation, counted once the pitch is known.
+void AddPitchPadding(int dev, const void* key, uint64_t bytes_now) {
+  State& s = S();
+  if (!key || !s.cap[dev]) return;
+  Locked lk(s);
+  if (Entry* x = s.allocs.Find(key)) {
+    if (bytes_now > x->bytes) {
+      AddLocked(s, dev, bytes_now - x->bytes);
+      x->bytes = bytes_now;
+    }
+  }
 }
 
 }  // namespace
@@ -610,28 +819,30 @@ hipError_t hipMallocPitch(void** ptr, size_t* pitch, size_t width, size_t height
   // The pitch is only known afterwards: reserve the unpadded size, then count
   // the padding too (without a second check) and track what was allocated.
   int dev = CurrentDevice();
-  hipError_t e = Capped(dev, uint64_t{width} * height, ptr, [&] { return real(ptr, pitch, width, height); });
-  State& s = S();
-  if (t_depth == 0 && e == hipSuccess && ptr && *ptr && pitch && *pitch > width && s.cap[dev]) {
-    Locked lk(s);
-    if (Entry* x = s.allocs.Find(*ptr)) {
-      AddLocked(s, dev, uint64_t{*pitch - width} * height);
-      x->bytes = uint64_t{*pitch} * height;
-    }
-  }
+  bool outer = t_depth == 0;
+  hipError_t e = Capped(dev, Mul(width, height), ptr, [&] { return real(ptr, pitch, width, height); });
+  if (outer && e == hipSuccess && ptr && *ptr && pitch && *pitch > width) AddPitchPadding(dev, *ptr, Mul(*pitch, height));
   return e;
 }
 
 hipError_t hipMallocAsync(void** ptr, size_t size, hipStream_t stream) {
   REAL(hipMallocAsync, hipError_t (*)(void**, size_t, hipStream_t));
   if (!real) return hipErrorNotInitialized;
-  return Capped(StreamDevice(stream), size, ptr, [&] { return real(ptr, size, stream); });
+  int dev = StreamDevice(stream);
+  bool outer = t_depth == 0;
+  hipError_t e = Capped(dev, size, ptr, [&] { return real(ptr, size, stream); });
+  if (outer && e == hipSuccess && ptr && *ptr) MarkPooled(*ptr, dev, nullptr);
+  return e;
 }
 
 hipError_t hipMallocFromPoolAsync(void** ptr, size_t size, hipMemPool_t pool, hipStream_t stream) {
   REAL(hipMallocFromPoolAsync, hipError_t (*)(void**, size_t, hipMemPool_t, hipStream_t));
   if (!real) return hipErrorNotInitialized;
-  return Capped(StreamDevice(stream), size, ptr, [&] { return real(ptr, size, pool, stream); });
+  int dev = StreamDevice(stream);
+  bool outer = t_depth == 0;
+  hipError_t e = Capped(dev, size, ptr, [&] { return real(ptr, size, pool, stream); });
+  if (outer && e == hipSuccess && ptr && *ptr) MarkPooled(*ptr, dev, pool);
+  return e;
 }
 
 hipError_t hipFree(void* ptr) {
@@ -646,7 +857,121 @@ hipError_t hipFreeAsync(void* ptr, hipStream_t stream) {
   REAL(hipFreeAsync, hipError_t (*)(void*, hipStream_t));
   if (!real) return hipErrorNotInitialized;
   hipError_t e = real(ptr, stream);
-  if (e == hipSuccess) Untrack(ptr);  // counted free once the free is enqueued
+  if (e == hipSuccess) Untrack(ptr);  // a pool block: counted until the pool gives it back
+  return e;
+}
+
+// 3D, array and mipmap allocations: device memory like any other. Sizes are
+// computed saturating (an overflowing extent is refused at the cap), pitched
+// ones counted at the padded pitch once it is known.
+hipError_t hipMalloc3D(hipPitchedPtr* pitched, hipExtent extent) {
+  REAL(hipMalloc3D, hipError_t (*)(hipPitchedPtr*, hipExtent));
+  if (!real) return hipErrorNotInitialized;
+  if (!pitched) return real(pitched, extent);
+  int dev = CurrentDevice();
+  bool outer = t_depth == 0;
+  uint64_t rows = Mul(Dim(extent.height), Dim(extent.depth));
+  hipError_t e = Capped(dev, Mul(extent.width, rows), &pitched->ptr, [&] { return real(pitched, extent); });
+  if (outer && e == hipSuccess && pitched->ptr && pitched->pitch > extent.width)
+    AddPitchPadding(dev, pitched->ptr, Mul(pitched->pitch, rows));
+  return e;
+}
+
+hipError_t hipMemAllocPitch(hipDeviceptr_t* dptr, size_t* pitch, size_t width, size_t height, unsigned int elem) {
+  REAL(hipMemAllocPitch, hipError_t (*)(hipDeviceptr_t*, size_t*, size_t, size_t, unsigned int));
+  if (!real) return hipErrorNotInitialized;
+  int dev = CurrentDevice();
+  bool outer = t_depth == 0;
+  hipError_t e = Capped(dev, Mul(width, height), reinterpret_cast<void**>(dptr),
+                        [&] { return real(dptr, pitch, width, height, elem); });
+  if (outer && e == hipSuccess && dptr && *dptr && pitch && *pitch > width)
+    AddPitchPadding(dev, *dptr, Mul(*pitch, height));
+  return e;
+}
+
+hipError_t hipMallocArray(hipArray_t* array, const hipChannelFormatDesc* desc, size_t width, size_t height,
+                          unsigned int flags) {
+  REAL(hipMallocArray, hipError_t (*)(hipArray_t*, const hipChannelFormatDesc*, size_t, size_t, unsigned int));
+  if (!real) return hipErrorNotInitialized;
+  uint64_t bytes = Mul(Mul(ChannelBytes(desc), Dim(width)), Dim(height));
+  return Capped(CurrentDevice(), bytes, reinterpret_cast<void**>(array),
+                [&] { return real(array, desc, width, height, flags); });
+}
+
+hipError_t hipMalloc3DArray(hipArray_t* array, const hipChannelFormatDesc* desc, hipExtent extent,
+                            unsigned int flags) {
+  REAL(hipMalloc3DArray, hipError_t (*)(hipArray_t*, const hipChannelFormatDesc*, hipExtent, unsigned int));
+  if (!real) return hipErrorNotInitialized;
+  uint64_t bytes = Mul(Mul(Mul(ChannelBytes(desc), Dim(extent.width)), Dim(extent.height)), Dim(extent.depth));
+  return Capped(CurrentDevice(), bytes, reinterpret_cast<void**>(array),
+                [&] { return real(array, desc, extent, flags); });
+}
+
+hipError_t hipArrayCreate(hipArray_t* array, const HIP_ARRAY_DESCRIPTOR* d) {
+  REAL(hipArrayCreate, hipError_t (*)(hipArray_t*, const HIP_ARRAY_DESCRIPTOR*));
+  if (!real) return hipErrorNotInitialized;
+  if (!d) return real(array, d);
+  uint64_t bytes = Mul(Mul(Mul(FormatBytes(d->Format), Dim(d->NumChannels)), Dim(d->Width)), Dim(d->Height));
+  return Capped(CurrentDevice(), bytes, reinterpret_cast<void**>(array), [&] { return real(array, d); });
+}
+
+hipError_t hipArray3DCreate(hipArray_t* array, const HIP_ARRAY3D_DESCRIPTOR* d) {
+  REAL(hipArray3DCreate, hipError_t (*)(hipArray_t*, const HIP_ARRAY3D_DESCRIPTOR*));
+  if (!real) return hipErrorNotInitialized;
+  if (!d) return real(array, d);
+  uint64_t bytes = Mul(Mul(Mul(Mul(FormatBytes(d->Format), Dim(d->NumChannels)), Dim(d->Width)), Dim(d->Height)),
+                       Dim(d->Depth));
+  return Capped(CurrentDevice(), bytes, reinterpret_cast<void**>(array), [&] { return real(array, d); });
+}
+
+hipError_t hipMallocMipmappedArray(hipMipmappedArray_t* mm, const hipChannelFormatDesc* desc, hipExtent extent,
+                                   unsigned int levels, unsigned int flags) {
+  REAL(hipMallocMipmappedArray,
+       hipError_t (*)(hipMipmappedArray_t*, const hipChannelFormatDesc*, hipExtent, unsigned int, unsigned int));
+  if (!real) return hipErrorNotInitialized;
+  uint64_t bytes = MipmapBytes(ChannelBytes(desc), extent.width, extent.height, extent.depth, levels);
+  return Capped(CurrentDevice(), bytes, reinterpret_cast<void**>(mm),
+                [&] { return real(mm, desc, extent, levels, flags); });
+}
+
+hipError_t hipMipmappedArrayCreate(hipMipmappedArray_t* mm, HIP_ARRAY3D_DESCRIPTOR* d, unsigned int levels) {
+  REAL(hipMipmappedArrayCreate, hipError_t (*)(hipMipmappedArray_t*, HIP_ARRAY3D_DESCRIPTOR*, unsigned int));
+  if (!real) return hipErrorNotInitialized;
+  if (!d) return real(mm, d, levels);
+  uint64_t bytes = MipmapBytes(Mul(FormatBytes(d->Format), Dim(d->NumChannels)), d->Width, d->Height, d->Depth,
+                               levels);
+  return Capped(CurrentDevice(), bytes, reinterpret_cast<void**>(mm), [&] { return real(mm, d, levels); });
+}
+
+hipError_t hipFreeArray(hipArray_t array) {
+  REAL(hipFreeArray, hipError_t (*)(hipArray_t));
+  if (!real) return hipErrorNotInitialized;
+  hipError_t e = real(array);
+  if (e == hipSuccess) Untrack(array);
+  return e;
+}
+
+hipError_t hipArrayDestroy(hipArray_t array) {
+  REAL(hipArrayDestroy, hipError_t (*)(hipArray_t));
+  if (!real) return hipErrorNotInitialized;
+  hipError_t e = real(array);
+  if (e == hipSuccess) Untrack(array);
+  return e;
+}
+
+hipError_t hipFreeMipmappedArray(hipMipmappedArray_t mm) {
+  REAL(hipFreeMipmappedArray, hipError_t (*)(hipMipmappedArray_t));
+  if (!real) return hipErrorNotInitialized;
+  hipError_t e = real(mm);
+  if (e == hipSuccess) Untrack(mm);
+  return e;
+}
+
+hipError_t hipMipmappedArrayDestroy(hipMipmappedArray_t mm) {
+  REAL(hipMipmappedArrayDestroy, hipError_t (*)(hipMipmappedArray_t));
+  if (!real) return hipErrorNotInitialized;
+  hipError_t e = real(mm);
+  if (e == hipSuccess) Untrack(mm);
   return e;
 }
 
@@ -682,7 +1007,11 @@ hipError_t hipMemGetInfo(size_t* free_bytes, size_t* total_bytes) {
   if (e != hipSuccess || !s.cap[dev]) return e;
   Locked lk(s);
   if (s.area) ReclaimDead(s.area, s.slot, false);  // what died without saying so is free again
-  uint64_t left = s.cap[dev] - Min(UsedLocked(s, dev), s.cap[dev]);
+  // Blocks freed to a stream-ordered pool count as free here: an allocation
+  // that needs them trims the pools first (Reserve -> ReconcilePools).
+  uint64_t used = UsedLocked(s, dev);
+  used -= Min(used, s.pool_held[dev]);
+  uint64_t left = s.cap[dev] - Min(used, s.cap[dev]);
   if (free_bytes) *free_bytes = Min<uint64_t>(*free_bytes, left);
   if (total_bytes) *total_bytes = Min<uint64_t>(*total_bytes, s.cap[dev]);
   return e;
@@ -699,6 +1028,18 @@ hipError_t hipDeviceTotalMem(size_t* bytes, hipDevice_t device) {
 
 hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600* prop, int device) {
   REAL(hipGetDevicePropertiesR0600, hipError_t (*)(hipDeviceProp_tR0600*, int));
+  if (!real) return hipErrorNotInitialized;
+  hipError_t e = real(prop, device);
+  if (e == hipSuccess && prop && device >= 0 && device < kMaxDevices && S().cap[device])
+    prop->totalGlobalMem = Min<uint64_t>(prop->totalGlobalMem, S().cap[device]);
+  return e;
+}
+
+// The pre-R0600 symbol binaries built with HIP 5 import (hipDeviceProp_tR0000).
+hipError_t LegacyGetDeviceProperties(hipDeviceProp_tR0000* prop, int device) __asm__("hipGetDeviceProperties");
+hipError_t LegacyGetDeviceProperties(hipDeviceProp_tR0000* prop, int device) {
+  static std::atomic<void*> slot{nullptr};
+  auto real = reinterpret_cast<hipError_t (*)(hipDeviceProp_tR0000*, int)>(Cached(slot, "hipGetDeviceProperties"));
   if (!real) return hipErrorNotInitialized;
   hipError_t e = real(prop, device);
   if (e == hipSuccess && prop && device >= 0 && device < kMaxDevices && S().cap[device])

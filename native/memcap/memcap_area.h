@@ -24,6 +24,14 @@ constexpr int kMaxDevices = 64;
 constexpr int kSlots = 256;
 constexpr int kIdsBytes = 4096;
 
+// The grant itself, daemon-owned and read-only in the container: one file per
+// device of the grant, named by the device's HIP ordinal ("0", "1", ...), each
+// holding the MiB granted on it ("36000\n"). The daemon bind-mounts them
+// read-only from files it wrote before registering (<plugin dir>/amdgpu-dp/
+// grants/<mib>.mib), so a pod can neither rewrite nor drop its grant; the
+// AMD_GPU_MEMORY_LIMIT_MIB variable can only lower it.
+constexpr const char* kGrantDir = "/run/amdgpu-dp/grant";
+
 struct Slot {
   std::atomic<int32_t> pid;     // 0 free, > 0 owner, -1 being reclaimed
   std::atomic<uint64_t> start;  // owner's start time (/proc/<pid>/stat field 22): pid reuse guard

@@ -3,6 +3,7 @@
 // one JSON line per step: {"step": ..., "rc": <hipError_t>, ...}. Run with
 // LD_PRELOAD=libadp_memcap.so AMD_GPU_MEMORY_LIMIT_MIB=100,50 (tests/test_memcap.py).
 #include <hip/hip_runtime_api.h>
+#include <hip/hip_deprecated.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -25,6 +26,99 @@ void Info(const char* step) {
          f / kMiB, t / kMiB);
 }
 }  // namespace
+
+extern "C" size_t hip_mock_physical_bytes(int dev);  // the mock's test hook
+extern "C" hipError_t LegacyProps(hipDeviceProp_tR0000* prop, int dev) __asm__("hipGetDeviceProperties");
+
+void Phys(const char* step, int dev = 0) {
+  printf("{\"step\": \"%s\", \"physical_mib\": %zu}\n", step, hip_mock_physical_bytes(dev) / kMiB);
+}
+
+// `pool`: stream-ordered allocations under a 100 MiB cap on device 0; the
+// "device" (mock) must never hold more than the cap, pool reserve included.
+int Pool() {
+  (void)hipSetDevice(0);
+  auto s0 = reinterpret_cast<hipStream_t>(uintptr_t{1});
+  void *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr;
+  Out("async 80", hipMallocAsync(&a, 80 * kMiB, s0));
+  Out("freeasync 80", hipFreeAsync(a, s0));
+  Phys("phys after freeasync");  // the pool keeps it reserved
+  Info("info after freeasync");
+  Out("malloc 50", hipMalloc(&b, 50 * kMiB));  // the pool is trimmed first
+  Phys("phys after malloc 50");
+  Out("free 50", hipFree(b));
+  // A pool that cannot give everything back: 60 stays live.
+  Out("async 60", hipMallocAsync(&a, 60 * kMiB, s0));
+  Out("async 30", hipMallocAsync(&c, 30 * kMiB, s0));
+  Out("freeasync 30", hipFreeAsync(c, s0));
+  Out("malloc 40", hipMalloc(&b, 40 * kMiB));  // 60 live + 40: exactly the cap, after trimming the 30
+  Phys("phys after malloc 40");
+  Out("malloc 10", hipMalloc(&d, 10 * kMiB));  // past the cap
+  Phys("phys after malloc 10");
+  hipMemPool_t pool = nullptr;
+  (void)hipDeviceGetDefaultMemPool(&pool, 0);
+  Out("free 40", hipFree(b));
+  Out("frompool 30", hipMallocFromPoolAsync(&c, 30 * kMiB, pool, s0));
+  Out("free pool 30", hipFreeAsync(c, s0));
+  Out("free async 60", hipFreeAsync(a, s0));
+  Out("malloc 100", hipMalloc(&b, 100 * kMiB));  // every pool block trimmed away
+  Phys("phys after malloc 100");
+  Out("free 100", hipFree(b));
+  Info("info end");
+  return 0;
+}
+
+// `arrays`: 3D, array, mipmap and pitched allocations and an overflowing size
+// under a 100 MiB cap on device 0.
+int Arrays() {
+  (void)hipSetDevice(0);
+  hipChannelFormatDesc f4{32, 32, 32, 32, hipChannelFormatKindFloat};
+  hipChannelFormatDesc f1{32, 0, 0, 0, hipChannelFormatKindFloat};
+  hipChannelFormatDesc u8{8, 0, 0, 0, hipChannelFormatKindUnsigned};
+  hipArray_t a1 = nullptr, a2 = nullptr, a3 = nullptr, a4 = nullptr;
+  Out("array 16", hipMallocArray(&a1, &f4, 1024, 1024, 0));
+  Out("3darray 128", hipMalloc3DArray(&a2, &f1, make_hipExtent(1024, 1024, 32), 0));
+  HIP_ARRAY_DESCRIPTOR d2{};
+  d2.Format = HIP_AD_FORMAT_FLOAT;
+  d2.NumChannels = 4;
+  d2.Width = 1024;
+  d2.Height = 1024;
+  Out("arraycreate 16", hipArrayCreate(&a3, &d2));
+  HIP_ARRAY3D_DESCRIPTOR d3{};
+  d3.Format = HIP_AD_FORMAT_FLOAT;
+  d3.NumChannels = 1;
+  d3.Width = 1024;
+  d3.Height = 1024;
+  d3.Depth = 16;
+  Out("array3dcreate 64", hipArray3DCreate(&a4, &d3));
+  Info("info arrays");
+  hipPitchedPtr pp{};
+  Out("malloc3d 1000x1000x5", hipMalloc3D(&pp, make_hipExtent(1000, 1000, 5)));
+  Out("freearray", hipFreeArray(a1));
+  Out("arraydestroy", hipArrayDestroy(a3));
+  Info("info freed");
+  Out("malloc3d again", hipMalloc3D(&pp, make_hipExtent(1000, 1000, 5)));  // 1024 x 1000 x 5 bytes
+  Info("info malloc3d");
+  hipMipmappedArray_t mm = nullptr;
+  Out("mipmap 64", hipMallocMipmappedArray(&mm, &u8, make_hipExtent(8192, 8192, 0), 14, 0));
+  Out("free3d", hipFree(pp.ptr));
+  Out("array3d free", hipFreeArray(a4));
+  Info("info before overflow");
+  void* p = nullptr;
+  Out("malloc 1", hipMalloc(&p, 1 * kMiB));
+  void* huge = nullptr;
+  Out("malloc size_max", hipMalloc(&huge, SIZE_MAX));
+  size_t pitch = 0;
+  Out("pitch overflow", hipMallocPitch(&huge, &pitch, SIZE_MAX / 2, 4));
+  Out("async size_max", hipMallocAsync(&huge, SIZE_MAX, reinterpret_cast<hipStream_t>(uintptr_t{1})));
+  Info("info after overflow");
+  Out("free 1", hipFree(p));
+  hipDeviceProp_tR0000 legacy{};
+  Out("legacy props", LegacyProps(&legacy, 0));
+  printf("{\"step\": \"legacy props value\", \"mib\": %zu}\n", legacy.totalGlobalMem / kMiB);
+  Info("info end");
+  return 0;
+}
 
 // `stress`: 8 threads allocate and free random sizes on device 0 (sync and
 // stream-ordered) against the cap; at the end every byte must be back.
@@ -101,6 +195,8 @@ int Processes(int argc, char** argv) {
 
 int main(int argc, char** argv) {
   if (argc > 1 && strcmp(argv[1], "stress") == 0) return Stress();
+  if (argc > 1 && strcmp(argv[1], "pool") == 0) return Pool();
+  if (argc > 1 && strcmp(argv[1], "arrays") == 0) return Arrays();
   if (argc > 2) return Processes(argc, argv);
   void *a = nullptr, *b = nullptr, *c = nullptr;
   (void)hipSetDevice(0);

@@ -64,8 +64,11 @@ Result<std::unique_ptr<ChurnClient>> ChurnClient::Open(const std::string& socket
   c->advertised_ = law.devices.size();
   for (size_t i = 0; i < law.devices.size(); ++i) {
     if (law.devices[i].health == pb::kHealthy) ++c->allocatable_;
-    if (static_cast<int>(i % opt.world) == opt.rank && law.devices[i].health == pb::kHealthy)
-      c->free_.push_back(law.devices[i].id);
+    bool mine = opt.owned.empty()
+                    ? static_cast<int>(i % opt.world) == opt.rank
+                    : std::find(opt.owned.begin(), opt.owned.end(), alloc::StripReplica(law.devices[i].id)) !=
+                          opt.owned.end();
+    if (mine && law.devices[i].health == pb::kHealthy) c->free_.push_back(law.devices[i].id);
   }
   c->mine_ = c->free_.size();
   c->mine_ids_ = alloc::StripReplicas(c->free_);

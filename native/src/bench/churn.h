@@ -21,8 +21,11 @@ namespace adp::bench {
 struct ChurnOptions {
   int pod_size = 1;
   bool preferred = true;
-  int rank = 0;   // this client churns devices i with i % world == rank
+  int rank = 0;   // this client churns devices i with i % world == rank ...
   int world = 1;
+  // ... unless `owned` is set: then exactly the advertised devices whose
+  // physical ID (replica suffix stripped) is listed -- the rank's own GPU.
+  std::vector<std::string> owned;
   int timeout_ms = 5000;
   bool grpc_go = false;  // kubelet (grpc-go) client frame pattern, grpc::Channel::EmulateGrpcGo
 };

@@ -63,13 +63,27 @@ json SnapshotJson(const adp::inventory::Snapshot& s) {
                     {"vram_source", g.vram_source}, {"driver_profile", g.driver_profile},
                     {"model_hbm_mib", adp::inventory::ModelHbmMib(g.market_name)}, {"partitions", parts}});
   }
-  json links = json::array();
-  for (size_t a = 0; a < s.gpus.size(); ++a) {
-    json row = json::array();
-    for (size_t b = 0; b < s.gpus.size(); ++b) row.push_back(static_cast<int>(s.Link(a, b)));
+  // N x N matrices: the link class the allocator scores (inventory::LinkClass),
+  // and what amdsmi reported per pair (link type name, hops, weight).
+  static const char* kTypeNames[] = {"internal", "pcie", "xgmi", "n/a", "unknown"};
+  json links = json::array(), types = json::array(), hops = json::array(), weights = json::array();
+  const size_t n = s.gpus.size();
+  for (size_t a = 0; a < n; ++a) {
+    json row = json::array(), trow = json::array(), hrow = json::array(), wrow = json::array();
+    for (size_t b = 0; b < n; ++b) {
+      row.push_back(static_cast<int>(s.Link(a, b)));
+      int t = s.gpu_link_types[a * n + b];
+      trow.push_back(a == b ? "self" : (t >= 0 && t <= 4 ? kTypeNames[t] : "error"));
+      hrow.push_back(s.Hops(a, b));
+      wrow.push_back(s.gpu_weights[a * n + b]);
+    }
     links.push_back(row);
+    types.push_back(trow);
+    hops.push_back(hrow);
+    weights.push_back(wrow);
   }
-  return {{"gpus", gpus}, {"links", links}, {"smi_path", s.smi_path}, {"smi_version", s.smi_version}};
+  return {{"gpus", gpus}, {"links", links}, {"link_types", types}, {"hops", hops}, {"weights", weights},
+          {"smi_path", s.smi_path}, {"smi_version", s.smi_version}};
 }
 
 }  // namespace
@@ -141,14 +155,18 @@ char* adp_best_effort(const char* in) {
 }
 
 // Loads libamd_smi (path "" = default search), enumerates, returns the snapshot.
-// {"lib": "...", "devices": [0,1]}
+// {"lib": "...", "devices": [0, 1] | ["0000:0c:00.0", "<uuid>", ...]} (as --devices)
 char* adp_snapshot(const char* in) {
   return Guard([&] {
     json j = json::parse(in);
     auto lib = adp::smi::Library::Open(j.value("lib", std::string()));
     if (!lib.ok()) return Err(lib.status().ToString());
     adp::inventory::BuildOptions opt;
-    if (j.count("devices")) opt.only_gpus = j["devices"].get<std::vector<int>>();
+    if (j.count("devices"))
+      for (const auto& d : j["devices"]) {
+        if (d.is_number_integer()) opt.only_gpus.push_back(d.get<int>());
+        else opt.only_ids.push_back(d.get<std::string>());
+      }
     opt.include_card_nodes = j.value("include_card_nodes", false);
     auto snap = adp::inventory::BuildSnapshot(lib->get(), opt);
     if (!snap.ok()) return Err(snap.status().ToString());
@@ -230,7 +248,8 @@ char* adp_proto_roundtrip(const char* type, const unsigned char* bytes, size_t l
 
 extern "C" {
 
-// {"socket": "...", "pod_size": 1, "rank": 0, "world": 1, "preferred": true, "grpc_go": false} -> handle or null
+// {"socket": "...", "pod_size": 1, "rank": 0, "world": 1, "preferred": true, "grpc_go": false,
+//  "owned": ["<device id>", ...] (optional)} -> handle or null
 void* adp_bench_open(const char* in, char** err) {
   try {
     json j = json::parse(in);
@@ -240,6 +259,7 @@ void* adp_bench_open(const char* in, char** err) {
     o.world = j.value("world", 1);
     o.preferred = j.value("preferred", true);
     o.grpc_go = j.value("grpc_go", false);
+    if (j.count("owned")) o.owned = j["owned"].get<std::vector<std::string>>();
     auto c = adp::bench::ChurnClient::Open(j["socket"].get<std::string>(), o);
     if (!c.ok()) {
       *err = Dup(c.status().ToString());

@@ -717,6 +717,9 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
                 LOG_WARN(kComp, "inotify: %s was removed; reinstalling", v.popts.memcap_host_path.c_str());
                 InstallMemcap(cfg.flags);
                 if (!v.popts.memcap_preload_list.empty()) InstallPreloadList(cfg.flags);
+                for (auto& pl : plugins)
+                  if (Status gs = pl->InstallGrantFiles(); !gs.ok())
+                    LOG_ERROR(kComp, "%s", gs.ToString().c_str());
               }
               for (auto& pl : plugins) {
                 struct stat st;

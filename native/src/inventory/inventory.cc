@@ -262,6 +262,8 @@ Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo
   size_t n = snap->gpus.size();
   snap->gpu_links.assign(n * n, LinkClass::kUnknown);
   snap->gpu_hops.assign(n * n, 0);
+  snap->gpu_weights.assign(n * n, 0);
+  snap->gpu_link_types.assign(n * n, -1);
   for (size_t a = 0; a < n; ++a) snap->gpu_links[a * n + a] = LinkClass::kSame;
   return snap;
 }
@@ -293,6 +295,8 @@ Result<std::shared_ptr<const Snapshot>> BuildSnapshot(smi::Library* lib, const B
       }
       snap->gpu_links[a * n + b] = c;
       snap->gpu_hops[a * n + b] = l.hops;
+      snap->gpu_weights[a * n + b] = l.weight;
+      snap->gpu_link_types[a * n + b] = l.valid ? static_cast<int>(l.type) : -1;
     }
   }
   struct stat st;

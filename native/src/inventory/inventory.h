@@ -92,6 +92,8 @@ struct Snapshot {
   // gpu_links[a * gpus.size() + b]
   std::vector<LinkClass> gpu_links;
   std::vector<uint64_t> gpu_hops;
+  std::vector<uint64_t> gpu_weights;  // amdsmi_topo_get_link_weight (0 = unknown)
+  std::vector<int> gpu_link_types;    // raw smi::LinkType, -1 = query failed
   std::string smi_path;
   std::string smi_version;
 

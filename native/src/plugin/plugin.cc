@@ -4,6 +4,7 @@
 #include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
@@ -18,6 +19,7 @@
 #include "common/log.h"
 #include "common/strings.h"
 #include "memcap/usage.h"
+#include "memcap_area.h"
 #include "proto/messages.h"
 #include "proto/wire.h"
 
@@ -492,6 +494,17 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       pb::PutMapEntry(&c, 1, kMemoryFractionEnv, mem_frac);
       pb::PutMapEntry(&c, 1, kMemoryDevicesEnv, mem_devs);
       c += memcap_bytes_;  // the container enforces the grant (empty unless --enforce-memory-units)
+      if (!memcap_bytes_.empty()) {
+        // The grant itself, read-only: the shim's caps (the env can only lower them).
+        const std::string dir = GrantDir();
+        for (size_t i = 0; i < grant_bytes.size(); ++i) {
+          pb::Mount gm{std::string(adp_memcap::kGrantDir) + "/" + std::to_string(i),
+                       PathJoin(dir, GrantFileName(grant_bytes[i] >> 20)), true};
+          std::string gb;
+          pb::Encode(gm, &gb);
+          pb::PutLen(&c, 2, gb);
+        }
+      }
       if (!memcap_bytes_.empty() && !opts_.memcap_usage_dir.empty()) AddUsageFile(ids, grant_bytes, &c);
     }
     if (!cu_mask.empty()) pb::PutMapEntry(&c, 1, kCuMaskEnv, cu_mask);
@@ -660,8 +673,46 @@ Status Plugin::Register() {
                       opts_.dial_timeout_ms);
 }
 
+std::string GrantFileName(uint64_t mib) { return std::to_string(mib) + ".mib"; }
+
+std::string Plugin::GrantDir() const { return PathJoin(opts_.plugin_dir, "amdgpu-dp/grants"); }
+
+Status Plugin::InstallGrantFiles() const {
+  if (memcap_bytes_.empty()) return Status::Ok();
+  std::string dir = GrantDir();
+  mkdir(PathJoin(opts_.plugin_dir, "amdgpu-dp").c_str(), 0755);
+  mkdir(dir.c_str(), 0755);
+  std::set<uint64_t> sizes;
+  for (const auto& u : units_)
+    for (unsigned k = 1; k <= u.replicas && u.grant_mib; ++k) sizes.insert(uint64_t{k} * u.grant_mib);
+  for (uint64_t mib : sizes) {
+    std::string path = PathJoin(dir, GrantFileName(mib)), want = std::to_string(mib) + "\n";
+    if (FILE* f = fopen(path.c_str(), "rb")) {  // present and right: keep the inode running containers mounted
+      char buf[32];
+      size_t n = fread(buf, 1, sizeof(buf), f);
+      fclose(f);
+      if (std::string(buf, n) == want) continue;
+    }
+    std::string tmp = path + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "wb");
+    bool ok = f && fwrite(want.data(), 1, want.size(), f) == want.size();
+    if (f) ok = (fclose(f) == 0) && ok;
+    if (!ok || chmod(tmp.c_str(), 0444) != 0 || rename(tmp.c_str(), path.c_str()) != 0) {
+      int err = errno;
+      unlink(tmp.c_str());
+      return Internal("cannot write grant file " + path + ": " + strerror(err));
+    }
+  }
+  return Status::Ok();
+}
+
 Status Plugin::Start(std::function<void()> on_fatal) {
   if (running()) return FailedPrecondition("plugin already started");
+  if (Status gs = InstallGrantFiles(); !gs.ok()) {
+    // Without them a container would start with only its (pod-overridable) env caps.
+    LOG_ERROR(kComp, "'%s': %s", spec_.resource_name.c_str(), gs.ToString().c_str());
+    return gs;
+  }
   if (opts_.list_strategy == DeviceListStrategy::kCdiAnnotations ||
       opts_.list_strategy == DeviceListStrategy::kCdiCri) {
     Status cs = WriteCdiSpec();

@@ -59,7 +59,10 @@ inline constexpr const char* kVolumeMountHostPath = "/dev/null";
 inline constexpr const char* kVolumeMountRoot = "/var/run/amd-container-devices";
 inline constexpr const char* kCdiVendorClass = "amd.com/gpu";
 // Set on Allocate for memory-unit resources: MiB granted per allocated device and
-// that share of the device's HBM, comma separated in AMD_VISIBLE_DEVICES order.
+// that share of the device's HBM, comma separated in enumeration order -- the
+// order HIP numbers the container's devices (and HSA_CU_MASK uses) -- which is
+// not AMD_VISIBLE_DEVICES order under the uuid ID strategy (that list is
+// sorted by ID). AMD_GPU_MEMORY_DEVICES names the devices of both lists.
 inline constexpr const char* kMemoryLimitEnv = "AMD_GPU_MEMORY_LIMIT_MIB";
 inline constexpr const char* kMemoryFractionEnv = "AMD_GPU_MEMORY_FRACTION";
 // The device IDs the two lists above refer to, in the same (enumeration) order.
@@ -117,6 +120,13 @@ struct PluginOptions {
   // container uses (memcap/usage.h).
   std::string memcap_usage_dir;
 };
+
+// With the HBM-cap shim: the grant's MiB per device, one read-only file per
+// device mounted at <kGrantDir>/<HIP ordinal> (memcap_area.h). The host files
+// are <plugin dir>/amdgpu-dp/grants/<mib>.mib, one per grant size a device of
+// the plugin can be given, written before the plugin registers -- Allocate()
+// only adds mounts, and a container can never start before its grant exists.
+std::string GrantFileName(uint64_t mib);
 
 // HSA_CU_MASK bit ranges [first, last] of each of `replicas` CU shares of a device
 // with `cus` CUs over `xcds` XCDs. The kernel driver deals mask bit i to XCD
@@ -234,6 +244,14 @@ class Plugin {
                                 const std::vector<podresources::Assignment>* assignments, std::string* out);
   void AddUsageFile(const std::vector<std::string_view>& ids, const std::vector<uint64_t>& grant_bytes,
                     std::string* c);
+
+ public:
+  // With the shim: writes every grant file this plugin's Allocate() can mount
+  // (idempotent; also after a kubelet wiped the directory). Empty Ok otherwise.
+  Status InstallGrantFiles() const;
+  std::string GrantDir() const;
+
+ private:
 
  public:
   // CDI (Container Device Interface) spec describing this plugin's devices, for

@@ -1,4 +1,5 @@
-"""bench.py contract on CPU: single process and a 2-rank torchrun (gloo) job on the mock."""
+"""bench.py contract on CPU: single process, launcher-less multi-rank runs and a
+2-rank torchrun (gloo) job on the mock."""
 
 import json
 import os
@@ -31,6 +32,10 @@ def test_bench_single_process_contract():
     assert res["per_rank"][0]["allocate"]["n"] == 300
     assert res["rccl_world"] == 1 and res["backend"] == "none"
     assert res["per_rank"][0]["admitted_bdfs"] == ["0000:0c:00.0"]  # GPU 0 of the node model
+    # the daemon serves exactly the rank's GPU of the 8-GPU node model
+    topo = res["topology"]
+    assert topo["served_bdfs"] == topo["rank_bdfs"] == ["0000:0c:00.0"]
+    assert res["preferred_k"]["k"] == 1 and res["preferred_k"]["bdfs"] == ["0000:0c:00.0"]
     # the kubelet's grpc-go frame pattern: a BDP PING after (about) every response
     gg = res["per_rank"][0]["grpc_go_shaped"]
     assert gg["allocate"]["n"] == 300 and gg["bdp_pings"] >= gg["pods"]
@@ -61,6 +66,52 @@ def test_bench_two_ranks_gloo():
     assert all(v and v > 0 for v in per) and res["grpcio_client_allocate_p50_us"] == max(per)
     gg = [p["grpc_go_shaped"]["allocate"]["p50_us"] for p in res["per_rank"]]
     assert res["grpc_go_shaped_allocate_p50_us"] == max(gg)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_multi_gpu_without_launcher(n):
+    """`python bench.py --gpus N` starts its N ranks itself (the driver's 1-GPU
+    invocation, N > 1): one process group of N ranks, the daemon serving
+    exactly the ranks' GPUs by PCI address, the node's link matrix and a
+    k=min(4,N) preferred allocation in the JSON."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), "--steps", "2", "--warmup", "1", "--mock",
+                        "--pods-per-step", "20"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = _last_json(r.stdout)
+    assert res["n_gpus"] == n and res["rccl_world"] == n and res["backend"] == "gloo"
+    assert res["allocatable"] == n
+    topo = res["topology"]
+    assert topo["served_bdfs"] == topo["rank_bdfs"] and len(topo["rank_bdfs"]) == n
+    for key in ("link_types", "hops", "weights", "link_class"):
+        assert len(topo[key]) == n and all(len(row) == n for row in topo[key])
+    assert all(topo["link_types"][i][j] == ("self" if i == j else "xgmi") for i in range(n) for j in range(n))
+    assert [g["xgmi_links_down"] for g in topo["gpus"]] == [0] * n
+    pk = res["preferred_k"]
+    assert pk["k"] == min(4, n) and len(set(pk["bdfs"])) == pk["k"] and set(pk["bdfs"]) <= set(topo["served_bdfs"])
+    for p in res["per_rank"]:
+        assert p["admitted_bdfs"] == [p["rank_bdf"]] and p["allocate"]["n"] == 40
+    assert sorted(p["rank_bdf"] for p in res["per_rank"]) == sorted(topo["served_bdfs"])
+
+
+def test_bench_serves_the_ranks_gpus_not_amdsmi_order():
+    """A job given GPUs 5 and 2 of the node (HIP order != amdsmi order): the
+    daemon serves exactly those two, and each rank admits its own."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR")}
+    env["ADP_BENCH_MOCK_GPUS"] = "5,2"
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--mock",
+                        "--pods-per-step", "10", "--config", "timeslice4"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = _last_json(r.stdout)
+    topo = res["topology"]
+    assert topo["rank_bdfs"] == ["0000:ac:00.0", "0000:4c:00.0"]
+    assert sorted(topo["served_bdfs"]) == sorted(topo["rank_bdfs"])
+    assert res["advertised"] == 8  # 2 GPUs x 4 replicas, not 8 GPUs x 4
+    bdfs = {p["rank"]: (p["rank_bdf"], p["admitted_bdfs"]) for p in res["per_rank"]}
+    assert bdfs == {0: ("0000:ac:00.0", ["0000:ac:00.0"]), 1: ("0000:4c:00.0", ["0000:4c:00.0"])}
+    assert all(p["rank_devices"] == 4 for p in res["per_rank"])
 
 
 @pytest.mark.parametrize("config,advertised", [("timeslice4", 4), ("cpx-single", 8), ("auto-mem", 294),

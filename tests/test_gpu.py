@@ -723,3 +723,8 @@ def test_bench_under_torchrun_runs_rccl(snap):
     assert rank0["admitted_bdfs"] == [snap["gpus"][0]["bdf"]]
     assert rank0["probe_bdf"] == snap["gpus"][0]["bdf"]
     assert res["probe"][0]["checksum_ok"]
+    # the daemon served exactly the rank's GPU, named by the PCI address HIP gave the rank
+    topo = res["topology"]
+    assert rank0["rank_bdf"] == snap["gpus"][0]["bdf"]
+    assert topo["served_bdfs"] == topo["rank_bdfs"] == [snap["gpus"][0]["bdf"]]
+    assert topo["link_types"] == [["self"]] and res["preferred_k"]["bdfs"] == [snap["gpus"][0]["bdf"]]

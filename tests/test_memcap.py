@@ -150,7 +150,17 @@ def test_shim_exports_hip_versioned_entry_points_only():
     r = subprocess.run(["nm", "-D", "--defined-only", SHIM], capture_output=True, text=True, check=True)
     syms = {ln.split()[-1] for ln in r.stdout.splitlines() if " T " in ln}
     assert {"hipMalloc@@hip_4.2", "hipFree@@hip_4.2", "hipMemGetInfo@@hip_4.2", "hipMallocAsync@@hip_5.1",
-            "hipMemCreate@@hip_5.1", "hipGetDevicePropertiesR0600@@hip_6.0"} <= syms
+            "hipMemCreate@@hip_5.1", "hipGetDevicePropertiesR0600@@hip_6.0", "hipGetDeviceProperties@@hip_4.2",
+            "hipMalloc3D@@hip_4.2", "hipMallocArray@@hip_4.2", "hipMalloc3DArray@@hip_4.2",
+            "hipArrayCreate@@hip_4.2", "hipArray3DCreate@@hip_4.2", "hipArrayDestroy@@hip_4.3",
+            "hipMemAllocPitch@@hip_4.2", "hipMallocMipmappedArray@@hip_4.2"} <= syms
+    # every interposed symbol carries the version node the real library gives it
+    real = subprocess.run(["objdump", "-T", "/opt/rocm/lib/libamdhip64.so"], capture_output=True, text=True)
+    if real.returncode == 0:
+        nodes = {ln.split()[-1]: ln.split()[-2] for ln in real.stdout.splitlines() if " hip" in ln and "DF" in ln}
+        for sym in syms:
+            name, node = sym.split("@@")
+            assert nodes.get(name, node) == node, (sym, nodes.get(name))
     assert all(s.startswith("hip") for s in syms), syms
     r = subprocess.run(["ldd", SHIM], capture_output=True, text=True, check=True)
     assert "libamdhip64" not in r.stdout and "libstdc++" not in r.stdout  # resolved at run time; no C++ runtime
@@ -198,9 +208,94 @@ def test_memory_unit_pods_get_the_shim(scratch):
     # the device reports the grant as its memory under the shim: the fraction of it is 1
     assert envs["AMD_GPU_MEMORY_FRACTION"] == "1.0000"
     mounts = [(m.container_path, m.host_path, m.read_only) for m in resp.mounts]
-    assert mounts == [("/usr/local/lib/amdgpu-dp/libadp_memcap.so", installed, True)]
+    grant = os.path.join(scratch, "amdgpu-dp", "grants", "3000.mib")
+    # the shim, and the grant itself, read-only, one file per device in HIP order
+    assert mounts == [("/usr/local/lib/amdgpu-dp/libadp_memcap.so", installed, True),
+                      ("/run/amdgpu-dp/grant/0", grant, True)]
     assert open(installed, "rb").read() == open(SHIM, "rb").read()
+    assert open(grant).read() == "3000\n" and os.stat(grant).st_mode & 0o222 == 0
+    # every grant size a device can be given was written before registration
+    sizes = sorted(int(f[:-4]) for f in os.listdir(os.path.dirname(grant)))
+    assert sizes == [1000 * k for k in range(1, 295)]
     assert "HBM-cap shim installed at" in log
+
+
+def _grant_dir(tmp_path, *mib):
+    d = tmp_path / "grant"
+    d.mkdir()
+    for i, m in enumerate(mib):
+        (d / str(i)).write_text(f"{m}\n")
+    return str(d)
+
+
+@pytest.mark.parametrize("env_value", [None, "", "999999,999999", "abc", "0,0"])
+def test_daemon_grant_cannot_be_raised_or_dropped_from_the_env(tmp_path, env_value):
+    """The grant files the daemon mounts read-only are the caps: a pod that
+    empties, drops or raises AMD_GPU_MEMORY_LIMIT_MIB still gets 100/50 MiB."""
+    env = {"LD_PRELOAD": PRELOAD, "ADP_MEMCAP_GRANT_DIR": _grant_dir(tmp_path, 100, 50)}
+    if env_value is not None:
+        env["AMD_GPU_MEMORY_LIMIT_MIB"] = env_value
+    base = dict(os.environ)
+    base.pop("AMD_GPU_MEMORY_LIMIT_MIB", None)
+    r = subprocess.run([CHECK], capture_output=True, text=True, timeout=60,
+                       env=dict(base, ADP_MEMCAP_KEY=f"grant-{os.getpid()}-{time.monotonic_ns()}", **env))
+    assert r.returncode == 0, r.stderr
+    out = {d["step"]: d for d in map(json.loads, r.stdout.splitlines())}
+    assert out["d0 malloc 50"]["rc"] == 2 and out["d0 info"]["total_mib"] == 100
+    assert out["d1 malloc 60"]["rc"] == 2 and out["d1 totalmem value"]["mib"] == 50
+    assert out["d2 info"]["total_mib"] == 294912  # not granted, not capped
+
+
+def test_env_can_only_lower_the_daemon_grant(tmp_path):
+    out, _ = _run({"LD_PRELOAD": PRELOAD, "ADP_MEMCAP_GRANT_DIR": _grant_dir(tmp_path, 100, 50),
+                   "AMD_GPU_MEMORY_LIMIT_MIB": "80,500,20"})
+    assert out["d0 info"]["total_mib"] == 80       # lowered
+    assert out["d1 totalmem value"]["mib"] == 50   # 500 > grant: the grant stands
+    assert out["d2 info"]["total_mib"] == 20       # past the grant: the env still caps
+
+
+def test_stream_ordered_pools_never_hold_memory_past_the_cap():
+    """hipMallocAsync -> hipFreeAsync keeps the block in the pool (reserved);
+    the shim counts it until a refusal trims the pools and reads back what they
+    still hold, so the device (mock: live allocations + pool reserve) never
+    holds more than the grant."""
+    out, _ = _run({"LD_PRELOAD": PRELOAD, "AMD_GPU_MEMORY_LIMIT_MIB": "100"}, "pool")
+    assert out["phys after freeasync"]["physical_mib"] == 80   # the pool keeps the freed block
+    assert out["info after freeasync"]["free_mib"] == 100      # reported as free: it can be trimmed
+    assert out["malloc 50"]["rc"] == 0 and out["phys after malloc 50"]["physical_mib"] == 50  # trimmed first
+    assert out["malloc 40"]["rc"] == 0 and out["phys after malloc 40"]["physical_mib"] == 100
+    assert out["malloc 10"]["rc"] == 2 and out["phys after malloc 10"]["physical_mib"] == 100
+    assert out["frompool 30"]["rc"] == 0 and out["malloc 100"]["rc"] == 0
+    assert out["phys after malloc 100"]["physical_mib"] == 100
+    assert max(v["physical_mib"] for v in out.values() if "physical_mib" in v) <= 100
+    assert (out["info end"]["free_mib"], out["info end"]["total_mib"]) == (100, 100)
+
+
+def test_without_the_shim_a_pool_holds_past_the_cap():
+    """The same sequence uncapped: the pool's reserve plus the next hipMalloc
+    is what the shim has to bound (80 + 50 here)."""
+    out, _ = _run({}, "pool")
+    assert out["phys after malloc 50"]["physical_mib"] == 130
+
+
+def test_arrays_3d_mipmaps_and_overflowing_sizes_are_capped():
+    out, err = _run({"LD_PRELOAD": PRELOAD, "AMD_GPU_MEMORY_LIMIT_MIB": "100"}, "arrays")
+    oom = 2
+    assert out["array 16"]["rc"] == 0 and out["3darray 128"]["rc"] == oom
+    assert out["arraycreate 16"]["rc"] == 0 and out["array3dcreate 64"]["rc"] == 0
+    assert out["info arrays"]["free_mib"] == 4
+    assert out["malloc3d 1000x1000x5"]["rc"] == oom  # 4.9 MiB > 4 left
+    assert out["info freed"]["free_mib"] == 36         # hipFreeArray / hipArrayDestroy give back
+    assert out["malloc3d again"]["rc"] == 0
+    assert out["info malloc3d"]["free_mib"] == 31      # at the 1024-byte pitch: 1024 x 1000 x 5
+    assert out["mipmap 64"]["rc"] == oom               # 64 MiB base + levels > 31 left
+    assert out["info before overflow"]["free_mib"] == 100
+    # SIZE_MAX (an OOM probe, an overflowed size) is refused and leaves the count alone
+    assert out["malloc size_max"]["rc"] == oom and out["pitch overflow"]["rc"] == oom
+    assert out["async size_max"]["rc"] == oom
+    assert out["info after overflow"]["free_mib"] == 99
+    assert out["legacy props"]["rc"] == 0 and out["legacy props value"]["mib"] == 100  # HIP-5 binaries
+    assert out["info end"]["free_mib"] == 100
 
 
 def test_shim_reinstalled_when_its_directory_is_wiped(scratch):
@@ -221,6 +316,11 @@ def test_shim_reinstalled_when_its_directory_is_wiped(scratch):
             time.sleep(0.02)
         assert os.path.exists(installed) and open(installed, "rb").read() == open(SHIM, "rb").read()
         d.wait_log("was removed; reinstalling")
+        grant = os.path.join(scratch, "amdgpu-dp", "grants", "1000.mib")
+        deadline = time.time() + 5
+        while time.time() < deadline and not os.path.exists(grant):
+            time.sleep(0.02)
+        assert open(grant).read() == "1000\n"  # the grants are back too
     finally:
         d.stop()
         k.stop()
@@ -240,6 +340,8 @@ def test_shim_with_every_device_list_and_id_strategy(tmp_path, extra):
     assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "3000"
     shim = [m for m in resp.mounts if m.container_path == envs["LD_PRELOAD"]]
     assert len(shim) == 1 and shim[0].read_only and shim[0].host_path.endswith("amdgpu-dp/libadp_memcap.so")
+    grant = [m for m in resp.mounts if m.container_path.startswith("/run/amdgpu-dp/grant/")]
+    assert [(m.container_path, m.read_only) for m in grant] == [("/run/amdgpu-dp/grant/0", True)]
     assert any(dev.container_path == "/dev/kfd" for dev in resp.devices)
 
 
@@ -266,7 +368,8 @@ def test_time_slice_hbm_shares_enforced(tmp_path):
     resp, _ = _allocate(d, "gpu:shared:4", ["--replica-hbm-share"], take=1)
     envs = dict(resp.envs)
     assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == str(fixtures.MI355X_VRAM_MIB // 4)
-    assert envs["LD_PRELOAD"] == "/usr/local/lib/amdgpu-dp/libadp_memcap.so" and len(resp.mounts) == 1
+    assert envs["LD_PRELOAD"] == "/usr/local/lib/amdgpu-dp/libadp_memcap.so" and len(resp.mounts) == 2
+    assert resp.mounts[1].host_path.endswith(f"/grants/{fixtures.MI355X_VRAM_MIB // 4}.mib")
 
 
 def test_missing_shim_is_a_startup_error(scratch):
@@ -303,7 +406,7 @@ def test_memory_unit_pods_get_an_accounting_file_with_metrics(scratch):
     # opted out, or no metrics endpoint: nothing extra is mounted
     resp, _ = _allocate(scratch, "gpu:gpu-mem-gb:-1", ["--metrics-addr", "127.0.0.1:0",
                                                       "--container-hbm-metrics=false"])
-    assert "ADP_MEMCAP_FILE" not in dict(resp.envs) and len(resp.mounts) == 1
+    assert "ADP_MEMCAP_FILE" not in dict(resp.envs) and len(resp.mounts) == 2  # shim + grant
 
 
 def test_hbm_command_lists_grant_files(scratch):
