@@ -111,6 +111,14 @@ const std::vector<FlagDef>& Table() {
        "print the HBM use of enforced grants (the accounting files under <device-plugin-path>/amdgpu-dp/usage) "
        "as JSON and exit",
        [](Flags& f) -> void* { return &f.list_grants; }},
+      {"smi-report", "ADP_SMI_REPORT", "", Kind::kBool,
+       "print, as JSON, the status of every amdsmi query the plugin uses and whether each device node "
+       "opens (what this container's privileges and device cgroup allow) and exit",
+       [](Flags& f) -> void* { return &f.smi_report; }},
+      {"health-events", "DP_HEALTH_EVENTS", "healthEvents", Kind::kBool,
+       "register amdsmi event notification (GPU_PRE_RESET / GPU_POST_RESET: Unhealthy and back); "
+       "it needs /dev/kfd, which an unprivileged pod's device cgroup denies (false = polling only)",
+       [](Flags& f) -> void* { return &f.health_events; }},
       {"cdi-spec-dir", "CDI_SPEC_DIR", "cdiSpecDir", Kind::kString,
        "directory for the generated CDI spec (cdi-annotations / cdi-cri strategies)",
        [](Flags& f) -> void* { return &f.cdi_spec_dir; }},

@@ -46,13 +46,15 @@ struct Flags {
   std::string cdi_spec_dir = "/var/run/cdi";
   bool dry_run = false;
   bool list_grants = false;
+  bool smi_report = false;       // print every amdsmi query's status + device-node access, exit
+  bool health_events = true;     // register amdsmi event notification (needs /dev/kfd access)
   uint64_t server_threads = 0;  // 0 -> plugin::DefaultServerThreads()
   std::string metrics_addr;     // "" = no metrics endpoint
   std::string node_labels_file; // "" = no NFD feature file
   std::string pod_resources_socket = "/var/lib/kubelet/pod-resources/kubelet.sock";
   uint64_t busy_poll_us = 50;
   std::string http2_server = "native";
-  std::string loop_affinity = "peer-l3";
+  std::string loop_affinity = "none";  // peer-l3 only helps a visible, single-threaded caller
   std::string health_state_file;  // "" = health verdicts kept in memory only
   bool reject_unhealthy = false;  // Allocate() of an Unhealthy device fails instead of warning
   bool enforce_memory_units = false;  // memory-unit pods get the HBM-cap shim (LD_PRELOAD)

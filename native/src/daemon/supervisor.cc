@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <atomic>
 #include <memory>
@@ -258,6 +259,26 @@ int DryRun(smi::Library* lib, const Validated& v, const Config& cfg) {
   return 0;
 }
 
+// --smi-report: every amdsmi query's status per processor, and which device
+// nodes open -- what a pod's privileges and device cgroup leave working.
+int SmiReport(smi::Library* lib, const Validated& v, const Config& cfg) {
+  std::string out = lib->QueryReport();
+  out.pop_back();  // the closing brace
+  out += ", \"device_access\": [";
+  auto snap = inventory::BuildSnapshot(lib, v.bopts);
+  if (snap.ok()) {
+    auto access = inventory::ProbeDeviceAccess(**snap, cfg.flags.driver_root);
+    for (size_t i = 0; i < access.size(); ++i)
+      out += std::string(i ? ", " : "") + "{\"node\": \"" + JsonEscape(access[i].path) + "\", \"errno\": " +
+             std::to_string(access[i].err) + ", \"error\": \"" + (access[i].err ? strerror(access[i].err) : "") +
+             "\"}";
+  }
+  out += "], \"enumeration\": \"" + std::string(snap.ok() ? "ok" : JsonEscape(snap.status().ToString())) + "\"}";
+  printf("%s\n", out.c_str());
+  fflush(stdout);
+  return 0;
+}
+
 // Atomically replaces `path` with one `key=value` line per label.
 void WriteLabels(const std::string& path, const inventory::Snapshot& snap) {
   std::string body;
@@ -323,6 +344,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   }
   LOG_INFO(kComp, "amdsmi %s loaded from %s", (*lib)->Version().c_str(), (*lib)->path().c_str());
   if (cfg.flags.dry_run) return DryRun(lib->get(), v, cfg);
+  if (cfg.flags.smi_report) return SmiReport(lib->get(), v, cfg);
 
   std::string kubelet_sock =
       v.popts.kubelet_socket.empty() ? PathJoin(v.popts.plugin_dir, "kubelet.sock") : v.popts.kubelet_socket;
@@ -382,6 +404,8 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   std::shared_ptr<const inventory::Snapshot> cur_snap;
   std::vector<strategy::PluginSpec> cur_specs;
 
+  std::mutex access_mu;  // node_access: written by restart, read by /metrics
+  std::vector<inventory::NodeAccess> node_access;
   std::unique_ptr<metrics::HttpServer> http;
   std::unique_ptr<podresources::CachedLister> pod_lister;
   if (!cfg.flags.metrics_addr.empty() && !cfg.flags.pod_resources_socket.empty())
@@ -419,6 +443,16 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
               std::to_string(health_counters.retired_reads_ok.load()) + "\n"
               "amdgpu_dp_health_retired_page_reads_total{result=\"error\"} " +
               std::to_string(health_counters.retired_read_errors.load()) + "\n";
+          {
+            std::lock_guard<std::mutex> lk(access_mu);
+            if (!node_access.empty())
+              out += "# HELP amdgpu_dp_device_node_openable 1 if the plugin can open the device node (0: denied, "
+                     "e.g. by the container's device cgroup).\n"
+                     "# TYPE amdgpu_dp_device_node_openable gauge\n";
+            for (const auto& a : node_access)
+              out += "amdgpu_dp_device_node_openable{node=\"" + metrics::LabelValue(a.path) + "\"} " +
+                     (a.err ? "0" : "1") + "\n";
+          }
           if (auto retired = health_counters.RetiredPages(); !retired.empty()) {
             out += "# HELP amdgpu_dp_retired_pages HBM pages the driver retired (last health poll).\n"
                    "# TYPE amdgpu_dp_retired_pages gauge\n";
@@ -505,6 +539,30 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     return started;
   };
 
+  // Creates this generation's plugins and applies the failures recorded by
+  // earlier generations, in ONE critical section with the health listener
+  // (plugins_mu): the monitor writes the ledger before it notifies, so a
+  // verdict that changes concurrently is either in the ledger read here or
+  // notified to the new plugins afterwards -- a GPU_POST_RESET racing a
+  // re-registration can never leave a recovered GPU advertised Unhealthy.
+  const int reregister_delay_ms = [] {  // test hook: widens the window the lock closes
+    const char* e = getenv("ADP_DEBUG_PUBLISH_DELAY_MS");
+    return e ? atoi(e) : 0;
+  }();
+  auto publish_plugins = [&](const std::shared_ptr<const inventory::Snapshot>& snap,
+                             const std::vector<strategy::PluginSpec>& specs, bool apply_ledger) {
+    std::lock_guard<std::mutex> lk(plugins_mu);
+    for (const auto& s : specs) plugins.push_back(std::make_unique<plugin::Plugin>(snap, s, v.popts));
+    if (!apply_ledger) return;
+    auto failed = ledger.Failed(*snap);
+    if (reregister_delay_ms > 0) usleep(static_cast<useconds_t>(reregister_delay_ms) * 1000);
+    for (const auto& [gpu, why] : failed) {
+      LOG_WARN(kComp, "GPU %s is unhealthy since an earlier plugin generation: %s", snap->gpus[gpu].bdf.c_str(),
+               why.c_str());
+      for (auto& p : plugins) p->SetGpuHealth(gpu, false, why);
+    }
+  };
+
   auto restart = [&] {
     stop_all();
     ArmTimer(tfd, 0);  // disarm
@@ -527,6 +585,14 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
       return;
     }
     if (!cfg.flags.node_labels_file.empty()) WriteLabels(cfg.flags.node_labels_file, **snap);
+    {
+      auto access = inventory::ProbeDeviceAccess(**snap, cfg.flags.driver_root);
+      std::string what = inventory::DescribeAccess(access);
+      if (what == "ok") LOG_INFO(kComp, "device access: %zu node(s) openable", access.size());
+      else LOG_WARN(kComp, "device access: %s", what.c_str());
+      std::lock_guard<std::mutex> lk(access_mu);
+      node_access = std::move(access);
+    }
     auto specs = strategy::BuildPluginSpecs(**snap, v.partition, v.rc, cfg.flags.resource_prefix);
     if (!specs.ok()) {
       LOG_ERROR(kComp, "error creating partition strategy: %s", specs.status().message().c_str());
@@ -547,19 +613,9 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
                                    ? PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage")
                                    : "";
     health::HealthConfig hcfg = health::HealthConfig::FromEnv();
-    {
-      std::lock_guard<std::mutex> lk(plugins_mu);
-      for (auto& s : *specs) plugins.push_back(std::make_unique<plugin::Plugin>(*snap, s, v.popts));
-    }
-    // Failures recorded by earlier generations apply before the first
-    // ListAndWatch of this one.
-    if (!hcfg.disabled) {
-      for (const auto& [gpu, why] : ledger.Failed(**snap)) {
-        LOG_WARN(kComp, "GPU %s is unhealthy since an earlier plugin generation: %s",
-                 (*snap)->gpus[gpu].bdf.c_str(), why.c_str());
-        for (auto& p : plugins) p->SetGpuHealth(gpu, false, why);
-      }
-    }
+    hcfg.events = cfg.flags.health_events;
+    hcfg.driver_root = cfg.flags.driver_root;
+    publish_plugins(*snap, *specs, !hcfg.disabled);
     int started = start_plugins();
     if (started < 0) return;
     if (started == 0) LOG_INFO(kComp, "no devices found; waiting indefinitely");
@@ -596,17 +652,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     LOG_INFO(kComp, "re-registering plugins (devices and health monitor unchanged)");
     if (cfg.flags.enforce_memory_units) v.popts.memcap_host_path = InstallMemcap(cfg.flags);
     if (!v.popts.memcap_preload_list.empty()) v.popts.memcap_preload_list = InstallPreloadList(cfg.flags);
-    {
-      std::lock_guard<std::mutex> lk(plugins_mu);
-      for (auto& s : cur_specs) plugins.push_back(std::make_unique<plugin::Plugin>(cur_snap, s, v.popts));
-    }
-    if (!health::HealthConfig::FromEnv().disabled) {
-      for (const auto& [gpu, why] : ledger.Failed(*cur_snap)) {
-        LOG_WARN(kComp, "GPU %s is unhealthy since an earlier plugin generation: %s",
-                 cur_snap->gpus[gpu].bdf.c_str(), why.c_str());
-        for (auto& p : plugins) p->SetGpuHealth(gpu, false, why);
-      }
-    }
+    publish_plugins(cur_snap, cur_specs, !health::HealthConfig::FromEnv().disabled);
     start_plugins();
   };
 

@@ -294,13 +294,27 @@ Status Monitor::Start() {
   handles_ = watched;
   uint64_t mask = smi::EventMask(smi::kEvtGpuPreReset) | smi::EventMask(smi::kEvtGpuPostReset) |
                   smi::EventMask(smi::kEvtVmFault) | smi::EventMask(smi::kEvtThermalThrottle);
-  Status st = lib_->EventsInit(handles_, mask);
-  events_ok_ = st.ok();
+  if (!cfg_.events) {
+    events_ok_ = false;
+    events_reason_ = "off by configuration (--health-events=false)";
+    LOG_INFO(kComp, "amdsmi event notification %s; GPU resets are seen by polling only", events_reason_.c_str());
+  } else {
+    Status st = lib_->EventsInit(handles_, mask);
+    events_ok_ = st.ok();
+    events_reason_ = events_ok_ ? "" : st.ToString();
+    if (!events_ok_) {
+      // Say why: the usual cause in a pod is a device cgroup that denies /dev/kfd.
+      int kerr = inventory::KfdAccessErrno(cfg_.driver_root);
+      if (kerr == EPERM)
+        events_reason_ += "; /dev/kfd not openable (EPERM): the container's device cgroup denies it -- run the "
+                          "plugin privileged (helm healthEvents: true) for GPU_PRE_RESET/POST_RESET events";
+      else if (kerr)
+        events_reason_ += std::string("; /dev/kfd not openable (") + strerror(kerr) + ")";
+      LOG_WARN(kComp, "events off: amdsmi event notification unavailable (%s); using polling only",
+               events_reason_.c_str());
+    }
+  }
   counters_->events_enabled.store(events_ok_ ? 1 : 0);
-  events_reason_ = events_ok_ ? "" : st.ToString();
-  if (!events_ok_)
-    LOG_WARN(kComp, "amdsmi event notification unavailable (%s); using polling only",
-             st.ToString().c_str());
   // The ECC baseline is the one recorded at the first observation of the GPU,
   // not the current count: errors that accrued across a restart still count.
   for (const auto& g : snap_->gpus) {

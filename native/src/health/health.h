@@ -65,6 +65,10 @@ struct HealthConfig {
   // -1 = the driver's own threshold when amdsmi can read it (root), else off;
   // 0 = off; N = N pages.
   int64_t max_retired_pages = -1;
+  // amdsmi event notification (--health-events); off = polling only.
+  bool events = true;
+  // Where /dev/kfd is (--driver-root): why event registration failed.
+  std::string driver_root = "/";
   static HealthConfig FromEnv();
   static HealthConfig FromValues(const char* disable_value, const char* poll_ms_value);
 };

@@ -1,6 +1,11 @@
 #include "inventory/inventory.h"
 
+#include <errno.h>
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <cctype>
+#include <cstring>
 
 #include <algorithm>
 #include <map>
@@ -369,6 +374,48 @@ std::vector<std::pair<std::string, std::string>> NodeLabels(const Snapshot& snap
   for (const auto& g : snap.gpus) down += g.xgmi_links_down;
   out.emplace_back("amd.com/gpu.xgmi-links-down", std::to_string(down));
   return out;
+}
+
+int KfdAccessErrno(const std::string& driver_root) {
+  std::string kfd = PathJoin(driver_root, "/dev/kfd");
+  int fd = open(kfd.c_str(), O_RDWR | O_CLOEXEC | O_NONBLOCK);
+  if (fd < 0) return errno;
+  close(fd);
+  return 0;
+}
+
+std::vector<NodeAccess> ProbeDeviceAccess(const Snapshot& snap, const std::string& driver_root) {
+  std::vector<NodeAccess> out;
+  out.push_back({PathJoin(driver_root, "/dev/kfd"), KfdAccessErrno(driver_root)});
+  for (const auto& g : snap.gpus)
+    for (const auto& p : g.partitions) {
+      if (p.render_path.empty()) continue;
+      std::string path = PathJoin(driver_root, p.render_path);
+      int fd = open(path.c_str(), O_RDWR | O_CLOEXEC | O_NONBLOCK);
+      out.push_back({path, fd < 0 ? errno : 0});
+      if (fd >= 0) close(fd);
+    }
+  return out;
+}
+
+std::string DescribeAccess(const std::vector<NodeAccess>& access) {
+  std::string denied;
+  int err = 0;
+  for (const auto& a : access)
+    if (a.err) {
+      denied += (denied.empty() ? "" : ", ") + a.path;
+      err = a.err;
+    }
+  if (denied.empty()) return "ok";
+  std::string why = std::string(strerror(err)) + ": " + denied;
+  if (err == EPERM)
+    why += " (the container's device cgroup does not allow them -- an unprivileged pod that only "
+           "hostPath-mounts /dev; run the plugin privileged, helm healthEvents: true)";
+  else if (err == ENOENT)
+    why += " (not present: is /dev mounted from the host, and the driver root right?)";
+  else if (err == EACCES)
+    why += " (file permissions: run the plugin as root or in the render group)";
+  return why;
 }
 
 }  // namespace adp::inventory

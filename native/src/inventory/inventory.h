@@ -111,6 +111,21 @@ struct Snapshot {
 // Values are sanitised to label syntax ([A-Za-z0-9._-], <= 63 chars).
 std::vector<std::pair<std::string, std::string>> NodeLabels(const Snapshot& snap);
 
+// Whether this process can open each device node the plugin and amdsmi use
+// (<driver root>/dev/kfd, every GPU's render node): a container's device
+// cgroup answers EPERM for nodes it does not allow -- an unprivileged pod that
+// only hostPath-mounts /dev -- and amdsmi's event notification and libdrm
+// queries need them. err = 0: openable.
+struct NodeAccess {
+  std::string path;
+  int err = 0;
+};
+std::vector<NodeAccess> ProbeDeviceAccess(const Snapshot& snap, const std::string& driver_root);
+// errno of opening <driver root>/dev/kfd read-write (0 = ok).
+int KfdAccessErrno(const std::string& driver_root);
+// One line for the log: "ok" or what failed and the likely cause.
+std::string DescribeAccess(const std::vector<NodeAccess>& access);
+
 struct BuildOptions {
   std::string driver_root = "/";
   // Restrict to these physical GPU indices (empty = all). Used by the benchmark

@@ -49,6 +49,7 @@ struct Library::Fns {
   decltype(&amdsmi_get_gpu_total_ecc_count) ecc_total = nullptr;
   decltype(&amdsmi_get_gpu_bad_page_info) bad_pages = nullptr;
   decltype(&amdsmi_get_gpu_bad_page_threshold) bad_page_threshold = nullptr;
+  decltype(&amdsmi_get_gpu_process_list) process_list = nullptr;
   decltype(&amdsmi_status_code_to_string) status_string = nullptr;
   decltype(&amdsmi_get_lib_version) lib_version = nullptr;
 };
@@ -133,6 +134,7 @@ Result<std::unique_ptr<Library>> Library::Open(const std::string& path,
   Resolve(dl, "amdsmi_get_gpu_total_ecc_count", &f->ecc_total);
   Resolve(dl, "amdsmi_get_gpu_bad_page_info", &f->bad_pages);
   Resolve(dl, "amdsmi_get_gpu_bad_page_threshold", &f->bad_page_threshold);
+  Resolve(dl, "amdsmi_get_gpu_process_list", &f->process_list);
   Resolve(dl, "amdsmi_status_code_to_string", &f->status_string);
   Resolve(dl, "amdsmi_get_lib_version", &f->lib_version);
   if (!f->init || !f->shut_down || !f->socket_handles || !f->processor_handles || !f->uuid ||
@@ -421,6 +423,125 @@ Status Library::Reinit() {
   }
   initialized_ = true;
   return Status::Ok();
+}
+
+Result<std::vector<GpuProcess>> Library::ProcessList(void* h) {
+  if (!f_->process_list) return NotSupported("process list query not present");
+  std::vector<amdsmi_proc_info_t> buf(16);
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    uint32_t n = static_cast<uint32_t>(buf.size());
+    amdsmi_status_t st = f_->process_list(h, &n, buf.data());
+    if (st == AMDSMI_STATUS_OUT_OF_RESOURCES && n > buf.size()) {  // more processes than room: grow, retry
+      buf.resize(n + 8);
+      continue;
+    }
+    if (st != AMDSMI_STATUS_SUCCESS) return Unavailable("process list query failed (" + std::to_string(st) + ")");
+    std::vector<GpuProcess> out;
+    for (uint32_t i = 0; i < n && i < buf.size(); ++i) {
+      GpuProcess g;
+      g.pid = buf[i].pid;
+      g.vram_bytes = buf[i].memory_usage.vram_mem;
+      g.name.assign(buf[i].name, strnlen(buf[i].name, sizeof(buf[i].name)));
+      out.push_back(std::move(g));
+    }
+    return out;
+  }
+  return Unavailable("process list kept growing");
+}
+
+std::string Library::QueryReport() {
+  std::string out = "{\"amdsmi\": \"" + Version() + "\", \"path\": \"" + path_ + "\", \"processors\": [";
+  uint32_t nsock = 0;
+  std::vector<amdsmi_processor_handle> all;
+  if (f_->socket_handles(&nsock, nullptr) == AMDSMI_STATUS_SUCCESS && nsock) {
+    std::vector<amdsmi_socket_handle> socks(nsock);
+    if (f_->socket_handles(&nsock, socks.data()) == AMDSMI_STATUS_SUCCESS)
+      for (uint32_t i = 0; i < nsock && i < socks.size(); ++i) {
+        uint32_t np = 0;
+        if (f_->processor_handles(socks[i], &np, nullptr) != AMDSMI_STATUS_SUCCESS || !np) continue;
+        std::vector<amdsmi_processor_handle> ps(np);
+        if (f_->processor_handles(socks[i], &np, ps.data()) == AMDSMI_STATUS_SUCCESS)
+          all.insert(all.end(), ps.begin(), ps.begin() + std::min<size_t>(np, ps.size()));
+      }
+  }
+  bool first = true;
+  for (auto h : all) {
+    std::string row;
+    auto add = [&row](const char* name, int st, const std::string& value = "") {
+      row += std::string(row.empty() ? "" : ", ") + "\"" + name + "\": {\"status\": " + std::to_string(st);
+      if (!value.empty()) row += ", \"value\": " + value;
+      row += "}";
+    };
+    auto q = [](const std::string& v) { return "\"" + v + "\""; };
+    const int kMissing = -1;  // symbol not in this libamd_smi
+    {
+      char uuid[AMDSMI_GPU_UUID_SIZE + 16] = {0};
+      unsigned int ulen = sizeof(uuid);
+      int st = f_->uuid(h, &ulen, uuid);
+      add("uuid", st, st == 0 ? q(uuid) : "");
+    }
+    {
+      amdsmi_bdf_t b{};
+      int st = f_->bdf(h, &b);
+      add("bdf", st, st == 0 ? q(FormatBdf(b.as_uint)) : "");
+    }
+    if (f_->enum_info) {
+      amdsmi_enumeration_info_t ei{};
+      int st = f_->enum_info(h, &ei);
+      add("enumeration_info", st, st == 0 ? std::to_string(ei.drm_render) : "");
+    } else add("enumeration_info", kMissing);
+    if (f_->numa) { int32_t n = -1; int st = f_->numa(h, &n); add("numa_affinity", st, st == 0 ? std::to_string(n) : ""); }
+    else add("numa_affinity", kMissing);
+    if (f_->vram_info) { amdsmi_vram_info_t vi{}; int st = f_->vram_info(h, &vi); add("vram_info", st, st == 0 ? std::to_string(vi.vram_size) : ""); }
+    else add("vram_info", kMissing);
+    if (f_->memory_usage) { uint64_t u = 0; int st = f_->memory_usage(h, AMDSMI_MEM_TYPE_VRAM, &u); add("memory_usage", st, st == 0 ? std::to_string(u) : ""); }
+    else add("memory_usage", kMissing);
+    if (f_->compute_partition) { char b[64] = {0}; int st = f_->compute_partition(h, b, sizeof(b) - 1); add("compute_partition", st, st == 0 ? q(b) : ""); }
+    else add("compute_partition", kMissing);
+    if (f_->memory_partition) { char b[64] = {0}; int st = f_->memory_partition(h, b, sizeof(b) - 1); add("memory_partition", st, st == 0 ? q(b) : ""); }
+    else add("memory_partition", kMissing);
+    if (f_->kfd_info) { amdsmi_kfd_info_t ki{}; int st = f_->kfd_info(h, &ki); add("kfd_info", st, st == 0 ? std::to_string(ki.kfd_id) : ""); }
+    else add("kfd_info", kMissing);
+    if (f_->asic_info) { amdsmi_asic_info_t ai{}; int st = f_->asic_info(h, &ai); add("asic_info", st, st == 0 ? std::to_string(ai.num_of_compute_units) : ""); }
+    else add("asic_info", kMissing);
+    if (f_->xcd_counter) { uint16_t x = 0; int st = f_->xcd_counter(h, &x); add("xcd_counter", st, st == 0 ? std::to_string(x) : ""); }
+    else add("xcd_counter", kMissing);
+    if (f_->accel_profile) {
+      auto prof = std::make_unique<amdsmi_accelerator_partition_profile_t>();
+      uint32_t pid = 0;
+      add("accelerator_partition_profile", f_->accel_profile(h, prof.get(), &pid));
+    } else add("accelerator_partition_profile", kMissing);
+    if (f_->memory_partition_config) {
+      auto mc = std::make_unique<amdsmi_memory_partition_config_t>();
+      add("memory_partition_config", f_->memory_partition_config(h, mc.get()));
+    } else add("memory_partition_config", kMissing);
+    if (f_->ecc_total) { amdsmi_error_count_t ec{}; int st = f_->ecc_total(h, &ec); add("total_ecc_count", st, st == 0 ? std::to_string(ec.uncorrectable_count) : ""); }
+    else add("total_ecc_count", kMissing);
+    if (f_->bad_pages) { uint32_t n = 0; int st = f_->bad_pages(h, &n, nullptr); add("bad_page_info", st, st == 0 ? std::to_string(n) : ""); }
+    else add("bad_page_info", kMissing);
+    if (f_->bad_page_threshold) { uint32_t t = 0; int st = f_->bad_page_threshold(h, &t); add("bad_page_threshold", st, st == 0 ? std::to_string(t) : ""); }
+    else add("bad_page_threshold", kMissing);
+    if (f_->xgmi_link_status) { amdsmi_xgmi_link_status_t xs{}; int st = f_->xgmi_link_status(h, &xs); add("xgmi_link_status", st, st == 0 ? std::to_string(xs.total_links) : ""); }
+    else add("xgmi_link_status", kMissing);
+    if (f_->process_list) {
+      std::vector<amdsmi_proc_info_t> buf(64);
+      uint32_t n = static_cast<uint32_t>(buf.size());
+      int st = f_->process_list(h, &n, buf.data());
+      add("process_list", st, st == 0 ? std::to_string(n) : "");
+    } else add("process_list", kMissing);
+    if (f_->evt_init && f_->evt_mask && f_->evt_stop) {
+      int st = f_->evt_init(h);
+      add("event_notification_init", st);
+      if (st == 0) {
+        add("event_notification_mask", f_->evt_mask(h, EventMask(kEvtGpuPreReset) | EventMask(kEvtGpuPostReset)));
+        add("event_notification_stop", f_->evt_stop(h));
+      }
+    } else add("event_notification_init", kMissing);
+    out += std::string(first ? "" : ",") + "\n  {" + row + "}";
+    first = false;
+  }
+  out += first ? "]}" : "\n]}";
+  return out;
 }
 
 bool Library::Responsive(void* h) {

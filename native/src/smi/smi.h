@@ -75,6 +75,14 @@ struct Event {
   std::string message;
 };
 
+// One process holding memory on a GPU, as the driver accounts it
+// (amdsmi_get_gpu_process_list). `pid` is in the host's PID namespace.
+struct GpuProcess {
+  uint32_t pid = 0;
+  uint64_t vram_bytes = 0;
+  std::string name;
+};
+
 class Library {
  public:
   ~Library();
@@ -110,6 +118,13 @@ class Library {
   // HBM in use on the device (bytes, every process: amdsmi_get_gpu_memory_usage).
   Result<uint64_t> VramUsed(void* h);
   bool Responsive(void* h);
+  // Processes with memory on the device and their VRAM (driver accounting).
+  Result<std::vector<GpuProcess>> ProcessList(void* h);
+
+  // Every query the plugin uses, run once per processor, with its amdsmi
+  // status: what works in this container (device cgroup, privileges) and what
+  // does not. JSON object text; `--smi-report`.
+  std::string QueryReport();
 
   // Current compute/memory partition mode of a processor, e.g. {"CPX", "NPS2"}
   // (empty strings when the query is unavailable).

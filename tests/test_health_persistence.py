@@ -173,6 +173,31 @@ def test_ecc_failure_survives_every_restart_trigger(mk, trigger):
     assert h[ids[0]] == "Healthy"
 
 
+def test_post_reset_racing_a_reregistration_leaves_the_gpu_healthy(mk):
+    """GPU_POST_RESET handled while a kubelet restart re-registers the plugins:
+    the new generation reads the ledger and applies its failures in one
+    critical section with the health listener, so the GPU ends Healthy every
+    time. ADP_DEBUG_PUBLISH_DELAY_MS holds that section open between the
+    ledger read and the apply -- the window in which the reset lands."""
+    n = mk(env={"ADP_DEBUG_PUBLISH_DELAY_MS": "300"})
+    ids = sorted(n.start())
+    for _ in range(4):
+        n.inject("1 3 pre-reset")
+        n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+        seen = n.d.log().count("re-registering plugins")
+        _restart_kubelet(n)
+        n.d.wait_log("re-registering plugins", count=seen + 1)
+        time.sleep(0.1)  # inside the publish window: the failure was read, not yet applied
+        n.inject("1 4 post-reset")
+        law = n.first_law(15)
+        if law[ids[1]] != "Healthy":
+            law = n.wait_health(lambda h: h[ids[1]] == "Healthy", timeout=5)
+        assert law == {ids[0]: "Healthy", ids[1]: "Healthy"}
+        time.sleep(0.3)  # and it stays so
+        while not n.q.empty():
+            assert health(n.q.get_nowait())[ids[1]] == "Healthy"
+
+
 def test_pre_reset_without_post_reset_survives_sighup(mk):
     n = mk()
     ids = sorted(n.start())

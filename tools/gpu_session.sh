@@ -24,6 +24,12 @@
 #   interference noisy-neighbour victim latency with and without CU shares
 #   floor        UDS ping-pong floor, busy-poll on and off
 #   spread       10 back-to-back headline runs (bench.py --no-probe)
+#   access       device-cgroup denial (EPERM on /dev/kfd, /dev/dri/*, the
+#                errno an unprivileged pod's device cgroup returns) through
+#                libadp_devcgroup_sim.so: --smi-report / --dry-run / the
+#                health monitor's log, with and without the denial
+#   driver       what the driver reports per process (KFD sysfs, DRM fdinfo,
+#                amdsmi_get_gpu_process_list) while PyTorch holds HBM
 #   soak         3 minutes of churn + SIGHUP + kubelet restarts + scrapes on
 #                real libamd_smi (health polling, state file): RSS/fd/thread leaks
 set -o pipefail
@@ -121,6 +127,23 @@ step_spread() {
     timeout -k 10 300 python bench.py --no-probe > $out/spread_$i.json 2> $out/spread_$i.err || die "SPREAD $i" $out/spread_$i.err
     python -c "import json; d=json.load(open('$out/spread_$i.json')); print('R $i', d['value'], d['allocate_p99_us'], d.get('grpc_go_shaped_allocate_p50_us'), d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'])"
   done
+}
+step_access() {
+  local D=build/native/amdgpu-device-plugin SIM=$ROOT/build/native/libadp_devcgroup_sim.so
+  local dp=$(mktemp -d /tmp/adpacc-XXXX)
+  timeout -k 10 60 $D --device-plugin-path $dp --smi-report > $out/smi_report.json 2> $out/smi_report.err || die "SMI REPORT" $out/smi_report.err
+  LD_PRELOAD=$SIM timeout -k 10 60 $D --device-plugin-path $dp --smi-report > $out/smi_report_denied.json 2> $out/smi_report_denied.err || die "SMI REPORT (denied)" $out/smi_report_denied.err
+  ADP_DEVCGROUP_ALLOW=/dev/dri LD_PRELOAD=$SIM timeout -k 10 60 $D --device-plugin-path $dp --smi-report > $out/smi_report_kfd_denied.json 2> $out/smi_report_kfd_denied.err || die "SMI REPORT (kfd denied)" $out/smi_report_kfd_denied.err
+  ADP_DEVCGROUP_ALLOW=/dev/kfd LD_PRELOAD=$SIM timeout -k 10 60 $D --device-plugin-path $dp --smi-report > $out/smi_report_dri_denied.json 2> $out/smi_report_dri_denied.err || die "SMI REPORT (dri denied)" $out/smi_report_dri_denied.err
+  LD_PRELOAD=$SIM timeout -k 10 60 $D --device-plugin-path $dp --dry-run > $out/dry_run_denied.json 2> $out/dry_run_denied.err || die "DRY RUN (denied)" $out/dry_run_denied.err
+  timeout -k 10 120 python tools/access_daemon_check.py $out/daemon_denied.log > $out/daemon_denied.txt 2>&1 || die "DAEMON (denied)" $out/daemon_denied.txt
+  cat $out/daemon_denied.txt
+  python3 tools/compare_smi_reports.py $out/smi_report.json $out/smi_report_denied.json $out/smi_report_kfd_denied.json $out/smi_report_dri_denied.json | tee $out/access_summary.txt
+  rm -rf $dp
+}
+step_driver() {
+  timeout -k 10 180 python tools/probe_driver_usage.py > $out/driver_usage.json 2> $out/driver_usage.err || die DRIVER $out/driver_usage.err
+  python3 -c "import json; d=json.load(open('$out/driver_usage.json')); print(json.dumps({'self_fdinfo': d.get('self_fdinfo'), 'child': {k: v for k, v in d['child'].items() if k != 'cgroup'}})[:3000])"
 }
 step_soak() {
   timeout -k 10 400 python -u tools/soak.py --seconds 180 --real ${SOAK_ARGS:-} --out $out/soak.json > $out/soak.log 2>&1 || die SOAK $out/soak.log

@@ -85,6 +85,37 @@ def smi_process_list():
     return res
 
 
+def fdinfo(pid="self"):
+    """DRM fdinfo of every render-node / kfd fd of `pid` (per-client VRAM)."""
+    out = []
+    base = f"/proc/{pid}/fd"
+    try:
+        fds = os.listdir(base)
+    except OSError as e:
+        return {"error": e.strerror}
+    for fd in fds:
+        try:
+            target = os.readlink(os.path.join(base, fd))
+        except OSError:
+            continue
+        if not (target.startswith("/dev/dri/") or target == "/dev/kfd"):
+            continue
+        try:
+            info = open(f"/proc/{pid}/fdinfo/{fd}").read()
+        except OSError as e:
+            info = f"<{e.strerror}>"
+        out.append({"fd": fd, "target": target,
+                    "fdinfo": [ln for ln in info.splitlines() if ln.startswith("drm-") or ln.startswith("pos")]})
+    return out
+
+
+CHILD = """
+import sys, time, torch
+x = torch.empty(2 << 30, dtype=torch.uint8, device="cuda:0"); x.fill_(2); torch.cuda.synchronize()
+print("ready", flush=True); sys.stdin.read()
+"""
+
+
 def main():
     rep = {"uid": os.getuid(), "pid": os.getpid(), "before": {"kfd_procs": kfd_procs()}, "nodes": kfd_nodes()}
     rep["before"]["smi"] = smi_process_list()
@@ -94,6 +125,20 @@ def main():
     torch.cuda.synchronize()
     time.sleep(1.2)  # amdsmi asks for >= 1 s between process-list reads
     rep["holding_1gib"] = {"kfd_procs": kfd_procs(), "smi": smi_process_list()}
+    rep["self_fdinfo"] = fdinfo()
+    import subprocess
+    child = subprocess.Popen([sys.executable, "-c", CHILD], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    child.stdout.readline()
+    rep["child"] = {"pid": child.pid, "fdinfo": fdinfo(child.pid)}
+    try:
+        rep["child"]["cgroup"] = open(f"/proc/{child.pid}/cgroup").read()
+        rep["child"]["maps_lines"] = sum(1 for _ in open(f"/proc/{child.pid}/maps"))
+    except OSError as e:
+        rep["child"]["proc_error"] = e.strerror
+    time.sleep(1.1)
+    rep["child"]["smi"] = smi_process_list()
+    child.stdin.close()
+    child.wait(30)
     try:
         rep["self_maps_has_kfd"] = sum(1 for ln in open("/proc/self/maps") if "kfd" in ln or "renderD" in ln)
     except OSError:
