@@ -39,6 +39,9 @@ def test_defaults(scratch):
     assert f["deviceIDStrategy"] == "uuid"
     assert f["driverRoot"] == "/"
     assert f["resourceConfig"] == ""
+    # round 3: loop placement is opt-in (peer-l3 only acts on a visible, single-threaded caller)
+    assert f["loopAffinity"] == "none"
+    assert f["healthEvents"] is True
 
 
 def test_file_values_apply(scratch):

@@ -76,9 +76,36 @@ def test_defaults_render_a_valid_daemonset():
     vol = {v["name"]: v for v in ds["spec"]["template"]["spec"]["volumes"]}["health-state"]
     assert vol["hostPath"] == {"path": "/var/lib/amdgpu-device-plugin", "type": "DirectoryOrCreate"}
     assert container(ds)["image"] == "amdgpu-device-plugin:0.1.0"
+    # health events on by default: amdsmi needs /dev/kfd, which only a privileged
+    # pod's device cgroup allows
+    assert e["DP_HEALTH_EVENTS"] == "true" and container(ds)["securityContext"] == {"privileged": True}
+    assert e["DP_MAX_RETIRED_PAGES"] == "-1" and e["DP_LOOP_AFFINITY"] == "none"
+    assert "livenessProbe" not in container(ds)
+
+
+def test_health_events_off_runs_unprivileged():
+    """healthEvents: false -> drop ALL, and the daemon is told events are off
+    (it polls; it does not try /dev/kfd and log a denial)."""
+    ds = daemonset({"healthEvents": False})
+    check_consistent(ds)
     sc = container(ds)["securityContext"]
     assert sc["allowPrivilegeEscalation"] is False and sc["capabilities"]["drop"] == ["ALL"]
-    assert "livenessProbe" not in container(ds)
+    assert env(ds)["DP_HEALTH_EVENTS"] == "false"
+    # an explicit securityContext always wins; compat mode is privileged whatever healthEvents says
+    custom = {"runAsUser": 0, "capabilities": {"add": ["SYS_ADMIN"]}}
+    assert container(daemonset({"securityContext": custom}))["securityContext"] == custom
+    assert container(daemonset({"healthEvents": False, "compatWithCPUManager": True}))["securityContext"] == \
+        {"privileged": True}
+
+
+@pytest.mark.parametrize("value,rendered", [(0, "0"), (-1, "-1"), (25, "25"), (None, "-1")])
+def test_max_retired_pages_renders_zero_as_off(value, rendered):
+    """0 means off: sprig's `default` would have turned it into -1 (the driver's threshold)."""
+    assert env(daemonset({"maxRetiredPages": value}))["DP_MAX_RETIRED_PAGES"] == rendered
+
+
+def test_loop_affinity_value():
+    assert env(daemonset({"loopAffinity": "peer-l3"}))["DP_LOOP_AFFINITY"] == "peer-l3"
 
 
 def test_health_state_can_be_turned_off():

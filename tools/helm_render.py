@@ -3,7 +3,7 @@
 Implements the subset of Go text/template + sprig the chart uses: actions with
 `{{-`/`-}}` whitespace trimming, comments, pipelines, parenthesised commands,
 variables (`$x :=`), `if`/`else if`/`else`, `with`/`else`, `define`/`include`,
-and the functions default, trunc, trimSuffix, contains, printf, toYaml,
+and the functions default, kindIs, trunc, trimSuffix, contains, printf, toYaml,
 nindent, indent, quote, replace, coalesce, or, and, not, eq. Enough to render
 deployments/helm/amd-gpu-device-plugin for tests/test_helm_render.py; it is
 not a general helm implementation.
@@ -174,6 +174,14 @@ def _to_yaml(v):
     return yaml.safe_dump(v, default_flow_style=False, sort_keys=True).rstrip("\n")
 
 
+def _kind_is(kind, v):
+    """sprig kindIs: the Go reflect kind of a values-file value."""
+    kinds = {"invalid": v is None, "bool": isinstance(v, bool), "string": isinstance(v, str),
+             "map": isinstance(v, dict), "slice": isinstance(v, list),
+             "int64": isinstance(v, int) and not isinstance(v, bool), "float64": isinstance(v, float)}
+    return kinds.get(kind, False)
+
+
 class Renderer:
     def __init__(self, values, chart, release):
         self.defines = {}
@@ -194,6 +202,7 @@ class Renderer:
             "and": lambda *a: next((x for x in a if not truthy(x)), a[-1] if a else None),
             "not": lambda x: not truthy(x),
             "eq": lambda a, b: a == b,
+            "kindIs": _kind_is,
             "include": self._include,
         }
 
