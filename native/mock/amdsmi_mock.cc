@@ -9,6 +9,7 @@
 //
 // Fixture: $AMDSMI_MOCK_FIXTURE (JSON). Schema (all keys optional except gpus):
 //   { "init_status": 0, "events_supported": true, "lib_version": [26,2,1],
+//     "events_open_kfd": false,  event registration opens /dev/kfd (EPERM -> NO_PERM)
 //     "event_fifo": "<path>", "state_dir": "<path>", "topology": "xgmi"|"pcie",
 //     "numa_bw_penalty": false,
 //     "gpus": [ { "uuid": "...", "bdf": "0000:0c:00.0", "numa": 0, "vram_mib": 294896,
@@ -37,6 +38,7 @@
 //   amdsmi_shut_down + amdsmi_init re-reads the fixture (re-enumeration after a
 //   re-partition).
 #include <amd_smi/amdsmi.h>
+#include <errno.h>
 #include <fcntl.h>
 #include <poll.h>
 #include <sys/stat.h>
@@ -91,6 +93,9 @@ struct State {
   bool loaded = false;
   int init_status = 0;
   bool events_supported = true;
+  // Like the real library: event notification opens /dev/kfd, so a device
+  // cgroup that denies it fails the registration (libadp_devcgroup_sim.so).
+  bool events_open_kfd = false;
   uint32_t ver[3] = {26, 2, 1};
   std::string topology = "xgmi";
   std::string event_fifo, state_dir;
@@ -145,6 +150,7 @@ bool Load() {
   }
   g->init_status = j.value("init_status", 0);
   g->events_supported = j.value("events_supported", true);
+  g->events_open_kfd = j.value("events_open_kfd", false);
   g->topology = j.value("topology", std::string("xgmi"));
   g->event_fifo = j.value("event_fifo", std::string());
   g->state_dir = j.value("state_dir", std::string());
@@ -626,6 +632,11 @@ amdsmi_status_t amdsmi_get_gpu_bad_page_threshold(amdsmi_processor_handle h, uin
 amdsmi_status_t amdsmi_init_gpu_event_notification(amdsmi_processor_handle h) {
   GET_PROC(h);
   if (!g->events_supported) return AMDSMI_STATUS_NOT_SUPPORTED;
+  if (g->events_open_kfd) {
+    int fd = open("/dev/kfd", O_RDWR | O_CLOEXEC);
+    if (fd < 0 && errno == EPERM) return AMDSMI_STATUS_NO_PERM;
+    if (fd >= 0) close(fd);
+  }
   p->evt_init = true;
   if (g->fifo_fd < 0 && !g->event_fifo.empty()) {
     // O_RDWR keeps a writer open so poll() blocks instead of reporting HUP.

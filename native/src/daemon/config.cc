@@ -119,6 +119,19 @@ const std::vector<FlagDef>& Table() {
        "register amdsmi event notification (GPU_PRE_RESET / GPU_POST_RESET: Unhealthy and back); "
        "it needs /dev/kfd, which an unprivileged pod's device cgroup denies (false = polling only)",
        [](Flags& f) -> void* { return &f.health_events; }},
+      {"driver-hbm-poll-ms", "DP_DRIVER_HBM_POLL_MS", "driverHbmPollMs", Kind::kUint,
+       "with enforced memory units and /metrics: every N ms, read what each process holds on each GPU by the "
+       "driver's count (DRM fdinfo under --host-proc), attribute it to grants and flag grants over their HBM "
+       "(0 = off)",
+       [](Flags& f) -> void* { return &f.driver_hbm_poll_ms; }},
+      {"driver-hbm-slack-mib", "DP_DRIVER_HBM_SLACK_MIB", "driverHbmSlackMib", Kind::kUint,
+       "HBM per process the driver-side check allows above the grant: the HIP runtime's own allocations, "
+       "which never pass through hipMalloc",
+       [](Flags& f) -> void* { return &f.driver_hbm_slack_mib; }},
+      {"host-proc", "DP_HOST_PROC", "hostProc", Kind::kString,
+       "the /proc of the PID namespace the pods run in, for the driver-side HBM check: /proc with hostPID, "
+       "else a hostPath mount of the host's /proc",
+       [](Flags& f) -> void* { return &f.host_proc; }},
       {"cdi-spec-dir", "CDI_SPEC_DIR", "cdiSpecDir", Kind::kString,
        "directory for the generated CDI spec (cdi-annotations / cdi-cri strategies)",
        [](Flags& f) -> void* { return &f.cdi_spec_dir; }},

@@ -48,6 +48,9 @@ struct Flags {
   bool list_grants = false;
   bool smi_report = false;       // print every amdsmi query's status + device-node access, exit
   bool health_events = true;     // register amdsmi event notification (needs /dev/kfd access)
+  uint64_t driver_hbm_poll_ms = 10000;  // driver-side check of enforced grants (0 = off)
+  uint64_t driver_hbm_slack_mib = 512;  // HIP runtime allowance per process in that check
+  std::string host_proc = "/proc";      // the host's /proc (hostPID, or a hostPath mount)
   uint64_t server_threads = 0;  // 0 -> plugin::DefaultServerThreads()
   std::string metrics_addr;     // "" = no metrics endpoint
   std::string node_labels_file; // "" = no NFD feature file

@@ -26,6 +26,7 @@
 #include "health/health.h"
 #include "inventory/inventory.h"
 #include "metrics/metrics.h"
+#include "memcap/driver_usage.h"
 #include "memcap/usage.h"
 #include "podresources/podresources.h"
 #include "plugin/plugin.h"
@@ -404,6 +405,9 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   std::shared_ptr<const inventory::Snapshot> cur_snap;
   std::vector<strategy::PluginSpec> cur_specs;
 
+  // Driver-side check of enforced HBM grants (--driver-hbm-poll-ms): started
+  // with the first generation that enforces grants into an accounting dir.
+  std::unique_ptr<memcap::DriverHbmMonitor> driver_hbm;
   std::mutex access_mu;  // node_access: written by restart, read by /metrics
   std::vector<inventory::NodeAccess> node_access;
   std::unique_ptr<metrics::HttpServer> http;
@@ -479,11 +483,36 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
                    "# TYPE amdgpu_dp_pod_resources_up gauge\n"
                    "amdgpu_dp_pod_resources_up " + std::string(assigned.ok() ? "1" : "0") + "\n";
           }
+          std::unique_ptr<memcap::DriverHbmMonitor::Snapshot> dsnap;
+          if (driver_hbm) {
+            dsnap = std::make_unique<memcap::DriverHbmMonitor::Snapshot>(driver_hbm->Get());
+            out += "# HELP amdgpu_dp_driver_hbm_polls_total Driver-side HBM scans run (DRM fdinfo of every process).\n"
+                   "# TYPE amdgpu_dp_driver_hbm_polls_total counter\n"
+                   "amdgpu_dp_driver_hbm_polls_total " + std::to_string(dsnap->polls) + "\n"
+                   "# HELP amdgpu_dp_driver_hbm_unreadable_processes Processes whose file descriptors the plugin "
+                   "may not read (their HBM is not seen).\n"
+                   "# TYPE amdgpu_dp_driver_hbm_unreadable_processes gauge\n"
+                   "amdgpu_dp_driver_hbm_unreadable_processes " + std::to_string(dsnap->scan.fd_dirs_unreadable) + "\n"
+                   "# HELP amdgpu_dp_hbm_over_grant_events_total Transitions of any grant to over its HBM by the "
+                   "driver's count.\n"
+                   "# TYPE amdgpu_dp_hbm_over_grant_events_total counter\n"
+                   "amdgpu_dp_hbm_over_grant_events_total " + std::to_string(dsnap->over_total) + "\n";
+            out += "# HELP amdgpu_dp_gpu_hbm_driver_bytes HBM every process holds on the GPU by the driver's count.\n"
+                   "# TYPE amdgpu_dp_gpu_hbm_driver_bytes gauge\n";
+            for (const auto& [bdf, n] : dsnap->scan.total)
+              out += "amdgpu_dp_gpu_hbm_driver_bytes{bdf=\"" + metrics::LabelValue(bdf) + "\"} " + std::to_string(n) + "\n";
+            out += "# HELP amdgpu_dp_gpu_hbm_unattributed_bytes HBM on the GPU held by processes outside every "
+                   "enforced grant (no grant file mapped, no grant in their cgroup).\n"
+                   "# TYPE amdgpu_dp_gpu_hbm_unattributed_bytes gauge\n";
+            for (const auto& [bdf, n] : dsnap->scan.unattributed)
+              out += "amdgpu_dp_gpu_hbm_unattributed_bytes{bdf=\"" + metrics::LabelValue(bdf) + "\"} " +
+                     std::to_string(n) + "\n";
+          }
           std::lock_guard<std::mutex> lk(plugins_mu);
           std::vector<const plugin::Plugin*> ps;
           for (auto& p : plugins)
             if (p->device_count() > 0) ps.push_back(p.get());
-          plugin::Plugin::AppendPrometheus(ps, &out, assigned.ok() ? &*assigned : nullptr);
+          plugin::Plugin::AppendPrometheus(ps, &out, assigned.ok() ? &*assigned : nullptr, dsnap.get());
           return out;
         },
         [&] {
@@ -612,6 +641,21 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
                                        !cfg.flags.metrics_addr.empty()
                                    ? PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage")
                                    : "";
+    if (!driver_hbm && !v.popts.memcap_usage_dir.empty() && cfg.flags.driver_hbm_poll_ms > 0) {
+      memcap::DriverHbmMonitor::Options dopt;
+      dopt.proc_root = cfg.flags.host_proc;
+      dopt.usage_dir = v.popts.memcap_usage_dir;
+      dopt.poll_ms = static_cast<int>(std::min<uint64_t>(cfg.flags.driver_hbm_poll_ms, 3600000));
+      dopt.slack_bytes = cfg.flags.driver_hbm_slack_mib << 20;
+      std::string dir = v.popts.memcap_usage_dir;
+      driver_hbm = std::make_unique<memcap::DriverHbmMonitor>(dopt, [&plugins, &plugins_mu, dir] {
+        std::lock_guard<std::mutex> lk(plugins_mu);
+        std::vector<const plugin::Plugin*> ps;
+        for (auto& p : plugins) ps.push_back(p.get());
+        return plugin::Plugin::GrantedByKey(ps, dir);
+      });
+      driver_hbm->Start();
+    }
     health::HealthConfig hcfg = health::HealthConfig::FromEnv();
     hcfg.events = cfg.flags.health_events;
     hcfg.driver_root = cfg.flags.driver_root;
@@ -805,6 +849,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     else if (do_reregister && !quit) reregister();
   }
   stop_all();
+  if (driver_hbm) driver_hbm->Stop();
   if (http) http->Stop();
   // Grant files of containers allocated just before the signal: the runtime mounts them next.
   if (!v.popts.memcap_usage_dir.empty() && !memcap::Flush(2000))

@@ -1,0 +1,274 @@
+#include "memcap/driver_usage.h"
+
+#include <dirent.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <poll.h>
+#include <sys/eventfd.h>
+#include <sys/stat.h>
+#include <sys/sysmacros.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <set>
+
+#include "common/log.h"
+
+namespace adp::memcap {
+namespace {
+
+constexpr const char* kComp = "driver-hbm";
+
+bool IsPid(const char* name) {
+  if (!*name) return false;
+  for (const char* p = name; *p; ++p)
+    if (*p < '0' || *p > '9') return false;
+  return true;
+}
+
+// Small bounded read of a /proc file (fdinfo, cgroup): never blocks, never
+// follows a link out of /proc.
+std::string ReadSmall(const std::string& path, size_t max = 16384) {
+  int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC | O_NONBLOCK);
+  if (fd < 0) return "";
+  std::string out;
+  char buf[4096];
+  ssize_t n;
+  while (out.size() < max && (n = read(fd, buf, sizeof(buf))) > 0) out.append(buf, static_cast<size_t>(n));
+  close(fd);
+  return out;
+}
+
+std::string Field(const std::string& text, const char* key) {
+  size_t klen = strlen(key);
+  for (size_t b = 0; b < text.size();) {
+    size_t e = text.find('\n', b);
+    if (e == std::string::npos) e = text.size();
+    if (e - b > klen && text.compare(b, klen, key) == 0 && text[b + klen] == ':') {
+      size_t v = b + klen + 1;
+      while (v < e && (text[v] == ' ' || text[v] == '\t')) ++v;
+      return text.substr(v, e - v);
+    }
+    b = e + 1;
+  }
+  return "";
+}
+
+// The grant whose accounting file this process maps ("" if none).
+std::string GrantFromMaps(const std::string& maps_path, const std::vector<GrantFile>& grants) {
+  if (grants.empty()) return "";
+  FILE* f = fopen(maps_path.c_str(), "re");
+  if (!f) return "";
+  std::string found;
+  char line[1024];
+  while (found.empty() && fgets(line, sizeof(line), f)) {
+    // "start-end perms offset MAJ:MIN inode path"
+    unsigned maj = 0, mn = 0;
+    unsigned long long ino = 0;
+    if (sscanf(line, "%*s %*s %*s %x:%x %llu", &maj, &mn, &ino) != 3 || ino == 0) continue;
+    for (const auto& g : grants)
+      if (g.ino == ino && g.dev_major == maj && g.dev_minor == mn) {
+        found = g.key;
+        break;
+      }
+    // A line longer than the buffer: skip its remainder.
+    size_t len = strlen(line);
+    while (len && line[len - 1] != '\n' && fgets(line, sizeof(line), f)) len = strlen(line);
+  }
+  fclose(f);
+  return found;
+}
+
+std::string FirstLine(const std::string& s) { return s.substr(0, s.find('\n')); }
+
+}  // namespace
+
+uint64_t ParseFdinfoSize(const std::string& value) {
+  char* end = nullptr;
+  unsigned long long n = strtoull(value.c_str(), &end, 10);
+  if (end == value.c_str()) return 0;
+  while (*end == ' ' || *end == '\t') ++end;
+  uint64_t mul = 1;
+  if (!strncmp(end, "KiB", 3)) mul = 1ull << 10;
+  else if (!strncmp(end, "MiB", 3)) mul = 1ull << 20;
+  else if (!strncmp(end, "GiB", 3)) mul = 1ull << 30;
+  return static_cast<uint64_t>(n) * mul;
+}
+
+std::vector<GrantFile> ListGrantFiles(const std::string& usage_dir) {
+  std::vector<GrantFile> out;
+  DIR* d = opendir(usage_dir.c_str());
+  if (!d) return out;
+  int dfd = dirfd(d);
+  while (dirent* e = readdir(d)) {
+    std::string name = e->d_name;
+    if (name.size() != 16 + 7 || name.compare(16, 7, ".memcap") != 0) continue;
+    struct stat st;
+    if (fstatat(dfd, name.c_str(), &st, AT_SYMLINK_NOFOLLOW) != 0 || !S_ISREG(st.st_mode)) continue;
+    out.push_back({name.substr(0, 16), major(st.st_dev), minor(st.st_dev), static_cast<uint64_t>(st.st_ino)});
+  }
+  closedir(d);
+  return out;
+}
+
+std::string SelfCgroup() { return FirstLine(ReadSmall("/proc/self/cgroup", 4096)); }
+
+DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFile>& grants,
+                         const std::string& self_cgroup) {
+  DriverScan out;
+  DIR* d = opendir(proc_root.c_str());
+  if (!d) return out;
+  std::set<std::pair<std::string, uint64_t>> clients;  // (pdev, drm-client-id): a shared fd counts once
+  struct PidHbm {
+    int pid;
+    std::map<std::string, uint64_t> by_bdf;
+  };
+  std::vector<PidHbm> holders;
+  while (dirent* e = readdir(d)) {
+    if (!IsPid(e->d_name)) continue;
+    ++out.pids_scanned;
+    std::string base = proc_root + "/" + e->d_name;
+    DIR* fds = opendir((base + "/fd").c_str());
+    if (!fds) {
+      if (errno == EACCES || errno == EPERM) ++out.fd_dirs_unreadable;
+      continue;
+    }
+    PidHbm ph{atoi(e->d_name), {}};
+    int fdd = dirfd(fds);
+    while (dirent* f = readdir(fds)) {
+      if (!IsPid(f->d_name)) continue;
+      char target[256];
+      ssize_t n = readlinkat(fdd, f->d_name, target, sizeof(target) - 1);
+      if (n <= 0) continue;
+      target[n] = 0;
+      if (strncmp(target, "/dev/dri/renderD", 16) != 0) continue;
+      std::string info = ReadSmall(base + "/fdinfo/" + f->d_name);
+      std::string pdev = Field(info, "drm-pdev");
+      if (pdev.empty()) continue;
+      uint64_t client = strtoull(Field(info, "drm-client-id").c_str(), nullptr, 10);
+      // A descriptor shared with another process (fork, SCM_RIGHTS) is one
+      // client: its memory counts once, but both processes stay GPU holders
+      // (either may be the one that maps the grant's file).
+      uint64_t bytes = 0;
+      if (clients.insert({pdev, client}).second) {
+        std::string v = Field(info, "drm-resident-vram");
+        if (v.empty()) v = Field(info, "drm-memory-vram");
+        if (v.empty()) v = Field(info, "drm-total-vram");
+        bytes = ParseFdinfoSize(v);
+      }
+      ph.by_bdf[pdev] += bytes;
+    }
+    closedir(fds);
+    if (!ph.by_bdf.empty()) holders.push_back(std::move(ph));
+  }
+  closedir(d);
+
+  // Attribution: own mapping first, then the cgroup of an attributed process.
+  std::map<std::string, std::string> grant_of_cgroup;
+  for (auto& h : holders) {
+    std::string base = proc_root + "/" + std::to_string(h.pid);
+    std::string cg = FirstLine(ReadSmall(base + "/cgroup", 4096));
+    std::string grant = GrantFromMaps(base + "/maps", grants);
+    if (!grant.empty() && !cg.empty() && cg != self_cgroup) grant_of_cgroup.emplace(cg, grant);
+    for (auto& [bdf, bytes] : h.by_bdf) out.procs.push_back({h.pid, bdf, bytes, cg, grant, false});
+  }
+  for (auto& p : out.procs) {
+    if (p.grant.empty() && !p.cgroup.empty() && p.cgroup != self_cgroup) {
+      auto it = grant_of_cgroup.find(p.cgroup);
+      if (it != grant_of_cgroup.end()) {
+        p.grant = it->second;
+        p.via_cgroup = true;
+      }
+    }
+    out.total[p.bdf] += p.bytes;
+    if (p.grant.empty()) {
+      out.unattributed[p.bdf] += p.bytes;
+    } else {
+      out.by_grant[{p.grant, p.bdf}] += p.bytes;
+      if (p.bytes) ++out.grant_procs[{p.grant, p.bdf}];
+    }
+  }
+  return out;
+}
+
+DriverHbmMonitor::DriverHbmMonitor(Options opts, GrantFn grants)
+    : opts_(std::move(opts)), grants_(std::move(grants)), self_cgroup_(SelfCgroup()) {
+  snap_.slack_bytes = opts_.slack_bytes;
+}
+
+DriverHbmMonitor::~DriverHbmMonitor() { Stop(); }
+
+void DriverHbmMonitor::PollOnce() {
+  DriverScan scan = ScanDriverHbm(opts_.proc_root, ListGrantFiles(opts_.usage_dir), self_cgroup_);
+  auto granted = grants_ ? grants_() : std::map<std::string, std::map<std::string, uint64_t>>{};
+  std::map<std::pair<std::string, std::string>, GrantState> states;
+  for (const auto& [key, per_bdf] : granted)
+    for (const auto& [bdf, bytes] : per_bdf) states[{key, bdf}].granted_bytes = bytes;
+  for (const auto& [kb, bytes] : scan.by_grant) {
+    auto& st = states[kb];
+    st.driver_bytes = bytes;
+    st.processes = scan.grant_procs[kb];
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto& [kb, st] : states) {
+    // Not a grant of ours (no granted bytes on that GPU): everything held there is over.
+    uint64_t allowed = st.granted_bytes + static_cast<uint64_t>(st.processes) * opts_.slack_bytes;
+    st.over = st.driver_bytes > allowed;
+    bool was = false;
+    auto prev = snap_.grants.find(kb);
+    if (prev != snap_.grants.end()) was = prev->second.over;
+    if (st.over && !was) {
+      ++transitions_[kb];
+      ++snap_.over_total;
+      LOG_WARN(kComp, "grant %s holds %.1f MiB on GPU %s by the driver's count, granted %.1f MiB (+%.0f MiB "
+               "runtime allowance x %d process(es)): over its grant", kb.first.c_str(), st.driver_bytes / 1048576.0,
+               kb.second.c_str(), st.granted_bytes / 1048576.0, opts_.slack_bytes / 1048576.0, st.processes);
+    }
+    st.over_transitions = transitions_[kb];
+  }
+  if (snap_.polls == 0 && scan.fd_dirs_unreadable)
+    LOG_WARN(kComp, "%zu of %zu processes' file descriptors are not readable: HBM they hold is not seen (run the "
+             "plugin privileged, with the host's PID namespace or /proc at --host-proc)",
+             scan.fd_dirs_unreadable, scan.pids_scanned);
+  snap_.scan = std::move(scan);
+  snap_.grants = std::move(states);
+  ++snap_.polls;
+}
+
+DriverHbmMonitor::Snapshot DriverHbmMonitor::Get() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return snap_;
+}
+
+void DriverHbmMonitor::Start() {
+  if (thread_.joinable() || opts_.poll_ms <= 0) return;
+  stop_.store(false);
+  wake_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  thread_ = std::thread([this] {
+    while (!stop_.load()) {
+      PollOnce();
+      pollfd p{wake_fd_, POLLIN, 0};
+      poll(&p, 1, opts_.poll_ms);
+    }
+  });
+  LOG_INFO(kComp, "checking HBM grants against the driver every %d ms (%s, runtime allowance %.0f MiB/process)",
+           opts_.poll_ms, opts_.proc_root.c_str(), opts_.slack_bytes / 1048576.0);
+}
+
+void DriverHbmMonitor::Stop() {
+  if (thread_.joinable()) {
+    stop_.store(true);
+    uint64_t one = 1;
+    ssize_t w = write(wake_fd_, &one, sizeof(one));
+    (void)w;
+    thread_.join();
+  }
+  if (wake_fd_ >= 0) {
+    close(wake_fd_);
+    wake_fd_ = -1;
+  }
+}
+
+}  // namespace adp::memcap

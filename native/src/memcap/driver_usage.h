@@ -1,0 +1,131 @@
+// Driver-side truth for HBM grants: what every process holds on every GPU as
+// the amdgpu driver accounts it, attributed to the memory-unit grants.
+//
+// The HBM-cap shim (native/memcap/memcap.cc) counts inside the container, so
+// it cannot see a process that goes around it: a dlsym()/ctypes call into
+// libamdhip64, HSA-direct allocations, a forged used[] in the (container-
+// writable) accounting file, a process started without the shim. The driver
+// sees all of them. The source is DRM fdinfo (/proc/<pid>/fdinfo/<fd> of each
+// render-node descriptor: drm-pdev, drm-client-id, drm-resident-vram): it is
+// per process, counts the KFD (HIP) allocations of the process's GPU VM, and --
+// unlike amdsmi_get_gpu_process_list, whose PIDs are the host's (measured:
+// profiles/r3/driver/driver_usage.json) -- it is read in the PID namespace of
+// the /proc it comes from, so it attributes correctly wherever that /proc is
+// mounted from (hostPID, or the host's /proc at --host-proc).
+//
+// Attribution: a process that has its grant's accounting file mapped (the shim
+// maps it; /proc/<pid>/maps device + inode equal the daemon's file) belongs to
+// that grant; a process without the shim belongs to the grant of a process in
+// the same cgroup (the same container), unless that cgroup is the daemon's
+// own. Everything else on a GPU is "unattributed".
+//
+// The reference has nothing of the kind: it counts memory units and never
+// looks at what a pod uses (/root/reference/cmd/nvidia-device-plugin/
+// server.go:99-111).
+#pragma once
+
+#include <stdint.h>
+#include <sys/types.h>
+
+#include <atomic>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
+
+namespace adp::memcap {
+
+// One process's HBM on one GPU.
+struct ProcessHbm {
+  int pid = 0;
+  std::string bdf;       // drm-pdev
+  uint64_t bytes = 0;    // drm-resident-vram (drm-memory-vram on older kernels)
+  std::string cgroup;    // /proc/<pid>/cgroup (first line)
+  std::string grant;     // grant key ("" = unattributed)
+  bool via_cgroup = false;  // attributed through a cgroup sibling, not its own mapping
+};
+
+struct DriverScan {
+  std::vector<ProcessHbm> procs;
+  std::map<std::pair<std::string, std::string>, uint64_t> by_grant;  // (key, bdf) -> bytes
+  std::map<std::pair<std::string, std::string>, int> grant_procs;    // (key, bdf) -> processes
+  std::map<std::string, uint64_t> total;         // bdf -> bytes of every client seen
+  std::map<std::string, uint64_t> unattributed;  // bdf -> bytes outside every grant
+  size_t pids_scanned = 0;
+  size_t fd_dirs_unreadable = 0;  // processes whose fds this daemon may not read (privileges)
+};
+
+// A grant's accounting file as the daemon sees it: processes that mapped it
+// show the same device and inode in /proc/<pid>/maps.
+struct GrantFile {
+  std::string key;
+  unsigned dev_major = 0, dev_minor = 0;
+  uint64_t ino = 0;
+};
+std::vector<GrantFile> ListGrantFiles(const std::string& usage_dir);
+
+// "1195280 KiB" -> bytes; bare numbers are bytes.
+uint64_t ParseFdinfoSize(const std::string& value);
+
+// One pass over <proc_root>/<pid>/fd. `self_cgroup`: the daemon's own cgroup,
+// never used for sibling attribution.
+DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFile>& grants,
+                         const std::string& self_cgroup);
+
+// The cgroup line of the calling process ("" if unreadable).
+std::string SelfCgroup();
+
+// Polls ScanDriverHbm and checks every grant against the driver: a grant is
+// over when its processes hold more on a GPU than granted there plus `slack`
+// per process (the HIP runtime's own allocations -- code objects, queues,
+// scratch -- never pass through hipMalloc; about 0.1 GiB per process measured
+// on MI355X). Transitions into "over" are counted.
+class DriverHbmMonitor {
+ public:
+  struct Options {
+    std::string proc_root = "/proc";
+    std::string usage_dir;
+    int poll_ms = 10000;
+    uint64_t slack_bytes = 512ull << 20;
+  };
+  // key -> bdf -> granted bytes, for every live grant (called on the poll thread).
+  using GrantFn = std::function<std::map<std::string, std::map<std::string, uint64_t>>()>;
+
+  struct GrantState {
+    uint64_t driver_bytes = 0;
+    uint64_t granted_bytes = 0;
+    int processes = 0;
+    bool over = false;
+    uint64_t over_transitions = 0;
+  };
+  struct Snapshot {
+    DriverScan scan;
+    std::map<std::pair<std::string, std::string>, GrantState> grants;  // (key, bdf)
+    uint64_t polls = 0;
+    uint64_t over_total = 0;  // every transition into "over", all grants
+    uint64_t slack_bytes = 0;
+  };
+
+  DriverHbmMonitor(Options opts, GrantFn grants);
+  ~DriverHbmMonitor();
+  void Start();
+  void Stop();
+  void PollOnce();
+  Snapshot Get() const;
+
+ private:
+  Options opts_;
+  GrantFn grants_;
+  std::string self_cgroup_;
+  mutable std::mutex mu_;
+  Snapshot snap_;
+  std::map<std::pair<std::string, std::string>, uint64_t> transitions_;
+  std::atomic<bool> stop_{false};
+  int wake_fd_ = -1;
+  std::thread thread_;
+};
+
+}  // namespace adp::memcap

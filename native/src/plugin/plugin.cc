@@ -930,18 +930,47 @@ size_t Plugin::healthy_count() const {
   return n;
 }
 
+namespace {
+// Exposition lines are appended whole: label values (pod names up to 253
+// characters, ...) have no length bound a fixed buffer could hold, and one
+// truncated line makes Prometheus reject the entire scrape.
+void Family(std::string* out, const char* name, const char* type, const char* help) {
+  *out += "# HELP ";
+  *out += name;
+  *out += ' ';
+  *out += help;
+  *out += "\n# TYPE ";
+  *out += name;
+  *out += ' ';
+  *out += type;
+  *out += '\n';
+}
+void Sample(std::string* out, const char* name, const std::string& labels, double v) {
+  char num[40];
+  snprintf(num, sizeof(num), "%.17g", v);
+  *out += name;
+  *out += '{';
+  *out += labels;
+  *out += "} ";
+  *out += num;
+  *out += '\n';
+}
+void Sample(std::string* out, const char* name, const std::string& labels, uint64_t v) {
+  *out += name;
+  *out += '{';
+  *out += labels;
+  *out += "} ";
+  *out += std::to_string(v);
+  *out += '\n';
+}
+}  // namespace
+
 void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::string* out,
-                              const std::vector<podresources::Assignment>* assignments) {
+                              const std::vector<podresources::Assignment>* assignments,
+                              const memcap::DriverHbmMonitor::Snapshot* driver) {
   using metrics::LabelValue;
-  char line[512];
-  auto family = [&](const char* name, const char* type, const char* help) {
-    snprintf(line, sizeof(line), "# HELP %s %s\n# TYPE %s %s\n", name, help, name, type);
-    *out += line;
-  };
-  auto gauge = [&](const char* name, const std::string& labels, double v) {
-    snprintf(line, sizeof(line), "%s{%s} %.17g\n", name, labels.c_str(), v);
-    *out += line;
-  };
+  auto family = [&](const char* name, const char* type, const char* help) { Family(out, name, type, help); };
+  auto gauge = [&](const char* name, const std::string& labels, double v) { Sample(out, name, labels, v); };
   auto res = [](const Plugin* p) { return "resource=\"" + LabelValue(p->spec_.resource_name) + "\""; };
 
   family("amdgpu_dp_devices", "gauge", "Physical devices (GPUs or partitions) served by the plugin.");
@@ -1035,7 +1064,7 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
   }
   for (auto* p : plugins) {
     if (p->memcap_bytes_.empty() || p->opts_.memcap_usage_dir.empty()) continue;
-    AppendMemcapUsage(plugins, p->opts_.memcap_usage_dir, assignments, out);
+    AppendMemcapUsage(plugins, p->opts_.memcap_usage_dir, assignments, out, driver);
     break;
   }
   struct Conn { const Plugin* p; uint64_t connections, shed, errors; };
@@ -1055,17 +1084,58 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
   for (auto& c : conns) gauge("amdgpu_dp_grpc_errors_total", res(c.p), static_cast<double>(c.errors));
 }
 
+std::vector<std::pair<int, uint64_t>> Plugin::GrantedUnits(const std::vector<std::string_view>& ids) const {
+  std::vector<std::pair<int, uint64_t>> out;  // (unit, bytes), sorted by unit = the container's HIP order
+  if (!hbm_grants_) return out;
+  std::map<int, uint64_t> per;
+  for (auto id : ids) {
+    auto it = advertised_index_.find(id);
+    if (it == advertised_index_.end()) return {};
+    per[it->second] += units_[it->second].grant_mib << 20;
+  }
+  out.assign(per.begin(), per.end());
+  return out;
+}
+
+std::map<std::string, std::map<std::string, uint64_t>> Plugin::GrantedByKey(const std::vector<const Plugin*>& plugins,
+                                                                            const std::string& dir) {
+  std::map<std::string, std::map<std::string, uint64_t>> out;
+  for (auto& u : memcap::ReadAll(dir)) {
+    if (u.ids.empty()) continue;  // IDs that do not hash to the file's name: not believed
+    std::vector<std::string_view> ids;
+    for (size_t b = 0; b <= u.ids.size();) {
+      size_t e = std::min(u.ids.find(',', b), u.ids.size());
+      ids.push_back(std::string_view(u.ids).substr(b, e - b));
+      b = e + 1;
+    }
+    for (auto* p : plugins) {
+      if (p->memcap_bytes_.empty()) continue;
+      auto units = p->GrantedUnits(ids);
+      if (units.empty()) continue;
+      auto& per_bdf = out[u.key];
+      for (const auto& [unit, bytes] : units) per_bdf[p->snap_->gpus[p->units_[unit].gpu].bdf] += bytes;
+      break;
+    }
+  }
+  return out;
+}
+
 // Per-container HBM use of enforced grants, from the shim's accounting files
 // (memcap/usage.h): a container listed by PodResources is found by its device
 // IDs; without PodResources every file is reported by its own (verified) IDs.
-// Files of containers gone for two minutes are removed here.
+// Files of containers gone for two minutes are removed here. The granted
+// bytes are this daemon's (from the container's IDs), never the file's cap[],
+// which the container can rewrite; with `driver`, what the driver counts for
+// the container's processes on each GPU is reported next to them.
 void Plugin::AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const std::string& dir,
-                               const std::vector<podresources::Assignment>* assignments, std::string* out) {
+                               const std::vector<podresources::Assignment>* assignments, std::string* out,
+                               const memcap::DriverHbmMonitor::Snapshot* driver) {
   using metrics::LabelValue;
   struct Row {
     const Plugin* p;
     std::string labels;
-    std::vector<int> units;  // the container's devices in HIP order
+    std::vector<int> units;         // the container's devices in HIP order
+    std::vector<uint64_t> granted;  // bytes granted on each, by this daemon
     memcap::Usage u;
   };
   auto enforced = [&](std::string_view resource) -> const Plugin* {
@@ -1073,15 +1143,12 @@ void Plugin::AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const 
       if (p->spec_.resource_name == resource && !p->memcap_bytes_.empty()) return p;
     return nullptr;
   };
-  auto units_of = [](const Plugin* p, const std::vector<std::string_view>& ids, std::vector<int>* units) {
-    for (auto id : ids) {
-      auto it = p->advertised_index_.find(id);
-      if (it == p->advertised_index_.end()) return false;
-      units->push_back(it->second);
+  auto fill = [](const Plugin* p, const std::vector<std::string_view>& ids, Row* r) {
+    for (const auto& [unit, bytes] : p->GrantedUnits(ids)) {
+      r->units.push_back(unit);
+      r->granted.push_back(bytes);
     }
-    std::sort(units->begin(), units->end());
-    units->erase(std::unique(units->begin(), units->end()), units->end());
-    return true;
+    return !r->units.empty();
   };
   std::vector<Row> rows;
   std::set<std::string> live;
@@ -1095,8 +1162,8 @@ void Plugin::AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const 
       std::string key = memcap::AllocationKey(ids);
       live.insert(key);
       auto u = memcap::ReadGrant(dir, key);
-      Row r{p, "", {}, {}};
-      if (!u.ok() || !units_of(p, ids, &r.units)) continue;
+      Row r{p, "", {}, {}, {}};
+      if (!u.ok() || !fill(p, ids, &r)) continue;
       r.u = std::move(*u);
       r.labels = "resource=\"" + LabelValue(resource) + "\",namespace=\"" + LabelValue(ns) + "\",pod=\"" +
                  LabelValue(pod) + "\",container=\"" + LabelValue(ctr) + "\"";
@@ -1111,8 +1178,8 @@ void Plugin::AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const 
         b = e + 1;
       }
       for (auto* p : plugins) {
-        Row r{p, "", {}, {}};
-        if (ids.empty() || p->memcap_bytes_.empty() || !units_of(p, ids, &r.units)) continue;
+        Row r{p, "", {}, {}, {}};
+        if (ids.empty() || p->memcap_bytes_.empty() || !fill(p, ids, &r)) continue;
         r.labels = "resource=\"" + LabelValue(p->spec_.resource_name) + "\",allocation=\"" + u.key + "\"";
         r.u = std::move(u);
         rows.push_back(std::move(r));
@@ -1122,36 +1189,54 @@ void Plugin::AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const 
   }
   memcap::Collect(dir, assignments ? &live : nullptr, 120, 4096);
 
-  char line[640];
-  auto family = [&](const char* name, const char* type, const char* help) {
-    snprintf(line, sizeof(line), "# HELP %s %s\n# TYPE %s %s\n", name, help, name, type);
-    *out += line;
+  auto dev_label = [](const Row& r, size_t i) {
+    return i < r.units.size() ? r.p->units_[r.units[i]].id : "hip" + std::to_string(i);
   };
   auto column = [&](const char* name, const char* type, const char* help,
                     std::vector<uint64_t> memcap::Usage::*col) {
-    family(name, type, help);
+    Family(out, name, type, help);
     for (const auto& r : rows) {
       const auto& v = r.u.*col;
-      for (size_t i = 0; i < v.size(); ++i) {
-        std::string dev = i < r.units.size() ? r.p->units_[r.units[i]].id : "hip" + std::to_string(i);
-        snprintf(line, sizeof(line), "%s{%s,device=\"%s\"} %llu\n", name, r.labels.c_str(),
-                 LabelValue(dev).c_str(), static_cast<unsigned long long>(v[i]));
-        *out += line;
-      }
+      for (size_t i = 0; i < v.size(); ++i)
+        Sample(out, name, r.labels + ",device=\"" + LabelValue(dev_label(r, i)) + "\"", v[i]);
     }
   };
   column("amdgpu_dp_container_hbm_used_bytes", "gauge",
          "HBM the container's processes hold on the device (HBM-cap shim).", &memcap::Usage::used);
-  column("amdgpu_dp_container_hbm_granted_bytes", "gauge", "HBM granted to the container on the device.",
-         &memcap::Usage::cap);
+  Family(out, "amdgpu_dp_container_hbm_granted_bytes", "gauge", "HBM granted to the container on the device.");
+  for (const auto& r : rows)
+    for (size_t i = 0; i < r.granted.size(); ++i)
+      Sample(out, "amdgpu_dp_container_hbm_granted_bytes",
+             r.labels + ",device=\"" + LabelValue(dev_label(r, i)) + "\"", r.granted[i]);
   column("amdgpu_dp_container_hbm_peak_bytes", "gauge", "Most HBM the container has held on the device.",
          &memcap::Usage::peak);
   column("amdgpu_dp_container_hbm_refusals_total", "counter",
          "HIP allocations refused because they would pass the container's grant.", &memcap::Usage::refused);
-  family("amdgpu_dp_container_hbm_processes", "gauge", "Processes of the container using the HBM-cap shim.");
+  Family(out, "amdgpu_dp_container_hbm_processes", "gauge", "Processes of the container using the HBM-cap shim.");
+  for (const auto& r : rows) Sample(out, "amdgpu_dp_container_hbm_processes", r.labels, uint64_t{r.u.processes});
+  if (!driver) return;
+
+  // Driver-side truth, per GPU of the grant (partitions of one GPU share its PCI address).
+  Family(out, "amdgpu_dp_container_hbm_driver_bytes", "gauge",
+         "HBM the container's processes hold on the GPU by the driver's count (DRM fdinfo), whatever path "
+         "allocated it.");
+  Family(out, "amdgpu_dp_container_hbm_over_grant", "gauge",
+         "1 while the driver counts more HBM for the container on the GPU than granted (+ the runtime allowance "
+         "per process).");
+  Family(out, "amdgpu_dp_container_hbm_over_grant_total", "counter",
+         "Times the container went over its grant on the GPU by the driver's count.");
   for (const auto& r : rows) {
-    snprintf(line, sizeof(line), "amdgpu_dp_container_hbm_processes{%s} %u\n", r.labels.c_str(), r.u.processes);
-    *out += line;
+    std::set<std::string> bdfs;
+    for (int u : r.units) bdfs.insert(r.p->snap_->gpus[r.p->units_[u].gpu].bdf);
+    for (const auto& bdf : bdfs) {
+      auto it = driver->grants.find({r.u.key, bdf});
+      memcap::DriverHbmMonitor::GrantState st;
+      if (it != driver->grants.end()) st = it->second;
+      std::string labels = r.labels + ",bdf=\"" + LabelValue(bdf) + "\"";
+      Sample(out, "amdgpu_dp_container_hbm_driver_bytes", labels, st.driver_bytes);
+      Sample(out, "amdgpu_dp_container_hbm_over_grant", labels, uint64_t{st.over ? 1u : 0u});
+      Sample(out, "amdgpu_dp_container_hbm_over_grant_total", labels, st.over_transitions);
+    }
   }
 }
 

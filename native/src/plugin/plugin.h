@@ -41,6 +41,7 @@
 #include "grpc/grpc.h"
 #include "inventory/inventory.h"
 #include "metrics/metrics.h"
+#include "memcap/driver_usage.h"
 #include "podresources/podresources.h"
 #include "strategy/strategy.h"
 
@@ -224,7 +225,16 @@ class Plugin {
   // Prometheus text for a set of plugins (one HELP/TYPE header per family).
   // `assignments` (kubelet PodResources, may be null) adds per-device usage.
   static void AppendPrometheus(const std::vector<const Plugin*>& plugins, std::string* out,
-                               const std::vector<podresources::Assignment>* assignments = nullptr);
+                               const std::vector<podresources::Assignment>* assignments = nullptr,
+                               const memcap::DriverHbmMonitor::Snapshot* driver = nullptr);
+  // Every live enforced grant (accounting files in `dir` whose IDs hash to
+  // their name) -> PCI address of each GPU -> bytes granted there, from this
+  // daemon's own units (never from the container-writable file's cap[]).
+  static std::map<std::string, std::map<std::string, uint64_t>> GrantedByKey(
+      const std::vector<const Plugin*>& plugins, const std::string& dir);
+  // Bytes `ids` grant per unit, in HIP order (sorted unit index); empty when an
+  // ID is not this plugin's or the plugin grants no HBM.
+  std::vector<std::pair<int, uint64_t>> GrantedUnits(const std::vector<std::string_view>& ids) const;
 
   // Handlers (public for in-process tests and benchmarks; loop thread only when serving).
   Status HandleGetOptions(std::string_view req, std::string* resp);
@@ -241,7 +251,8 @@ class Plugin {
   void PostHealth(std::vector<int> units, bool healthy, const std::string& reason);
   Status Register();
   static void AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const std::string& dir,
-                                const std::vector<podresources::Assignment>* assignments, std::string* out);
+                                const std::vector<podresources::Assignment>* assignments, std::string* out,
+                                const memcap::DriverHbmMonitor::Snapshot* driver);
   void AddUsageFile(const std::vector<std::string_view>& ids, const std::vector<uint64_t>& grant_bytes,
                     std::string* c);
 

@@ -1,0 +1,186 @@
+"""Driver-side truth for enforced HBM grants (--driver-hbm-poll-ms).
+
+The shim counts inside the container; the driver counts every allocation of
+every process (DRM fdinfo, drm-resident-vram). The daemon reads the fdinfo of
+every process under --host-proc, attributes each GPU-holding process to a grant
+-- the grant's accounting file mapped in /proc/<pid>/maps, else a cgroup shared
+with such a process -- and reports, per container and GPU, what the driver
+counts next to the grant, whether it is over (beyond a per-process runtime
+allowance) and how often it went over. CPU: a fake /proc tree with fdinfo in
+the layout the MI355X box showed (profiles/r3/driver/driver_usage.json). The
+real-hardware run (a ctypes hipMalloc that bypasses the shim) is
+tests/test_gpu.py::test_driver_sees_an_allocation_that_bypasses_the_shim.
+
+Reference: none -- the reference counts memory units and never looks at use
+(/root/reference/cmd/nvidia-device-plugin/server.go:99-111).
+"""
+
+import os
+import re
+import time
+
+import pytest
+
+from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+from k8s_gpu_sharing_plugin_amd.models import fixtures
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
+
+from test_metrics import _get, _parse, _value
+
+SHIM = os.path.join(BUILD_DIR, "libadp_memcap.so")
+MIB = 1 << 20
+BDF0 = "0000:0c:00.0"
+
+
+class FakeProc:
+    """<root>/<pid>/{fd/<n> -> /dev/dri/renderD*, fdinfo/<n>, maps, cgroup}."""
+
+    def __init__(self, root):
+        self.root = root
+        os.makedirs(root, exist_ok=True)
+
+    def process(self, pid, cgroup, vram_mib=None, client=None, maps_file=None, bdf=BDF0, extra_fds=()):
+        base = os.path.join(self.root, str(pid))
+        os.makedirs(os.path.join(base, "fd"), exist_ok=True)
+        os.makedirs(os.path.join(base, "fdinfo"), exist_ok=True)
+        with open(os.path.join(base, "cgroup"), "w") as f:
+            f.write(cgroup + "\n")
+        maps = "55d0c0000000-55d0c0021000 r--p 00000000 08:01 131 /usr/bin/python3.10\n"
+        if maps_file:
+            st = os.stat(maps_file)
+            maps += (f"7f0000000000-7f0000100000 rw-s 00000000 {os.major(st.st_dev):02x}:{os.minor(st.st_dev):02x} "
+                     f"{st.st_ino} /run/amdgpu-dp/memcap\n")
+        with open(os.path.join(base, "maps"), "w") as f:
+            f.write(maps)
+        fd = os.path.join(base, "fd", "3")
+        if not os.path.lexists(fd):
+            os.symlink("/dev/kfd", fd)  # the KFD fd carries no memory stats
+        with open(os.path.join(base, "fdinfo", "3"), "w") as f:
+            f.write("pos:\t0\n")
+        if vram_mib is not None:
+            self.render(pid, 7, vram_mib, client if client is not None else pid * 10, bdf)
+        for n, target in extra_fds:
+            p = os.path.join(base, "fd", str(n))
+            if not os.path.lexists(p):
+                os.symlink(target, p)
+
+    def render(self, pid, fd, vram_mib, client, bdf=BDF0):
+        base = os.path.join(self.root, str(pid))
+        link = os.path.join(base, "fd", str(fd))
+        if not os.path.lexists(link):
+            os.symlink("/dev/dri/renderD128", link)
+        kib = vram_mib * 1024
+        with open(os.path.join(base, "fdinfo", str(fd)), "w") as f:
+            f.write(f"pos:\t0\ndrm-driver:\tamdgpu\ndrm-client-id:\t{client}\ndrm-pdev:\t{bdf}\n"
+                    f"drm-total-vram:\t{kib} KiB\ndrm-shared-vram:\t0\ndrm-resident-vram:\t{kib} KiB\n"
+                    f"drm-memory-vram:\t{kib} KiB\n")
+
+
+@pytest.fixture
+def node(scratch, tmp_path):
+    proc = FakeProc(str(tmp_path / "proc"))
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(2), args=[
+        "--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack",
+        "--enforce-memory-units", "--memcap-lib", SHIM, "--host-proc", proc.root,
+        "--driver-hbm-poll-ms", "50", "--driver-hbm-slack-mib", "100"]).start()
+    try:
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics")).group(1))
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        resp = c.allocate(ids[:3]).container_responses[0]  # 3 units = 3000 MiB on GPU 0
+        c.close()
+        host = [m.host_path for m in resp.mounts if m.container_path == "/run/amdgpu-dp/memcap"][0]
+        deadline = time.time() + 5
+        while not os.path.isfile(host) and time.time() < deadline:
+            time.sleep(0.01)
+        yield d, proc, port, host
+    finally:
+        d.stop()
+        k.stop()
+
+
+def _scrape_after_poll(port, min_polls):
+    deadline = time.time() + 5
+    while True:
+        s = _parse(_get(port, "/metrics")[1])
+        if _value(s, "amdgpu_dp_driver_hbm_polls_total") >= min_polls or time.time() > deadline:
+            return s
+        time.sleep(0.02)
+
+
+def _polls(port):
+    return _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_driver_hbm_polls_total")
+
+
+def test_driver_counts_attribute_every_process_of_the_container(node):
+    d, proc, port, host = node
+    key = os.path.basename(host).split(".")[0]
+    ctr = "0::/kubepods.slice/kubepods-pod1234.slice/cri-containerd-abc.scope"
+    proc.process(101, ctr, vram_mib=1000, maps_file=host)     # under the shim: maps the grant's file
+    proc.process(102, ctr, vram_mib=1200)                      # same container, no shim (bypass)
+    proc.process(103, "0::/kubepods.slice/other.scope", vram_mib=1024)  # another tenant, no grant
+    proc.process(104, ctr, vram_mib=None)                      # a child sharing 101's DRM client
+    proc.render(104, 9, 1000, client=1010)
+    proc.process(105, "0::/system.slice/sshd.service")       # no GPU
+    s = _scrape_after_poll(port, _polls(port) + 2)
+    lab = dict(allocation=key, bdf=BDF0)
+    # 1000 + 1200 (the cgroup sibling) counted once each; 104's fd is 101's client
+    assert _value(s, "amdgpu_dp_container_hbm_driver_bytes", **lab) == 2200 * MIB
+    assert _value(s, "amdgpu_dp_container_hbm_over_grant", **lab) == 0  # 2200 <= 3000 + 2 x 100
+    assert _value(s, "amdgpu_dp_container_hbm_granted_bytes", allocation=key) == 3000 * MIB
+    assert _value(s, "amdgpu_dp_gpu_hbm_driver_bytes", bdf=BDF0) == (1000 + 1200 + 1024) * MIB
+    assert _value(s, "amdgpu_dp_gpu_hbm_unattributed_bytes", bdf=BDF0) == 1024 * MIB
+    assert _value(s, "amdgpu_dp_driver_hbm_unreadable_processes") == 0
+
+
+def test_over_grant_is_flagged_and_counted_per_transition(node):
+    d, proc, port, host = node
+    key = os.path.basename(host).split(".")[0]
+    ctr = "0::/kubepods/pod-a/ctr"
+    proc.process(201, ctr, vram_mib=1000, maps_file=host)
+    proc.process(202, ctr, vram_mib=2500)   # e.g. ctypes hipMalloc / HSA direct: the shim never saw it
+    s = _scrape_after_poll(port, _polls(port) + 2)
+    lab = dict(allocation=key, bdf=BDF0)
+    assert _value(s, "amdgpu_dp_container_hbm_driver_bytes", **lab) == 3500 * MIB
+    assert _value(s, "amdgpu_dp_container_hbm_over_grant", **lab) == 1    # 3500 > 3000 + 2 x 100
+    assert _value(s, "amdgpu_dp_container_hbm_over_grant_total", **lab) == 1
+    assert _value(s, "amdgpu_dp_hbm_over_grant_events_total") == 1
+    # the shim's own count (the accounting file) saw none of it
+    assert _value(s, "amdgpu_dp_container_hbm_used_bytes", allocation=key) == 0
+    assert "over its grant" in d.wait_log("over its grant")
+    proc.render(202, 7, 1000, client=2020)  # back under
+    s = _scrape_after_poll(port, _polls(port) + 2)
+    assert _value(s, "amdgpu_dp_container_hbm_over_grant", **lab) == 0
+    assert _value(s, "amdgpu_dp_container_hbm_over_grant_total", **lab) == 1
+    proc.render(202, 7, 2900, client=2020)  # and over again: a second transition
+    s = _scrape_after_poll(port, _polls(port) + 2)
+    assert _value(s, "amdgpu_dp_container_hbm_over_grant_total", **lab) == 2
+    assert _value(s, "amdgpu_dp_hbm_over_grant_events_total") == 2
+
+
+def test_a_forged_accounting_file_does_not_raise_the_grant(node):
+    """The container can rewrite its accounting file (cap[], used[]); the granted
+    bytes /metrics reports and the over-grant check uses are the daemon's own."""
+    d, proc, port, host = node
+    key = os.path.basename(host).split(".")[0]
+    with open(host, "r+b") as f:
+        f.seek(24 + 64 * 8)  # cap[0] (after the header words and used[])
+        f.write((200000 * MIB).to_bytes(8, "little"))
+        f.seek(24)           # used[0]
+        f.write((0).to_bytes(8, "little"))
+    proc.process(301, "0::/kubepods/pod-b/ctr", vram_mib=5000, maps_file=host)
+    s = _scrape_after_poll(port, _polls(port) + 2)
+    assert _value(s, "amdgpu_dp_container_hbm_granted_bytes", allocation=key) == 3000 * MIB
+    assert _value(s, "amdgpu_dp_container_hbm_over_grant", allocation=key, bdf=BDF0) == 1
+
+
+def test_unreadable_processes_are_reported(node):
+    d, proc, port, host = node
+    if os.geteuid() == 0:
+        pytest.skip("root reads every fd directory")
+    os.makedirs(os.path.join(proc.root, "401", "fd"))
+    os.chmod(os.path.join(proc.root, "401", "fd"), 0)
+    s = _scrape_after_poll(port, _polls(port) + 2)
+    assert _value(s, "amdgpu_dp_driver_hbm_unreadable_processes") == 1

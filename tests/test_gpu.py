@@ -728,3 +728,253 @@ def test_bench_under_torchrun_runs_rccl(snap):
     assert rank0["rank_bdf"] == snap["gpus"][0]["bdf"]
     assert topo["served_bdfs"] == topo["rank_bdfs"] == [snap["gpus"][0]["bdf"]]
     assert topo["link_types"] == [["self"]] and res["preferred_k"]["bdfs"] == [snap["gpus"][0]["bdf"]]
+
+
+def _allocate_memory_units(scratch, units, extra=(), env=None):
+    """Daemon on the real GPU with enforced memory units; one Allocate() of
+    `units` units. Returns (daemon, kubelet, response) -- the caller stops both."""
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    shim = os.path.join(BUILD_DIR, "libadp_memcap.so")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--resource-config", "gpu:gpu-mem-gb:-1",
+                                                     "--replica-policy", "pack", "--enforce-memory-units",
+                                                     "--memcap-lib", shim, *extra], env=env).start()
+    try:
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=10).devices]
+        resp = c.allocate(ids[:units]).container_responses[0]
+        c.close()
+    except Exception:
+        d.stop()
+        k.stop()
+        raise
+    return d, k, resp
+
+
+def _container_env(resp, tmpdir):
+    """What the Allocate() response gives a container, emulated on the box: the
+    shim preloaded from its host path, the read-only grant files copied to a
+    directory named by ADP_MEMCAP_GRANT_DIR (the bind mounts at
+    /run/amdgpu-dp/grant/<i> in a pod), the accounting file at its host path."""
+    envs = dict(resp.envs)
+    mounts = {m.container_path: m for m in resp.mounts}
+    envs["LD_PRELOAD"] = _with_preload(mounts[envs["LD_PRELOAD"]].host_path)
+    gdir = os.path.join(tmpdir, "grant")
+    os.makedirs(gdir, exist_ok=True)
+    for path, m in mounts.items():
+        if path.startswith("/run/amdgpu-dp/grant/"):
+            assert m.read_only
+            with open(m.host_path) as src, open(os.path.join(gdir, path.rsplit("/", 1)[1]), "w") as dst:
+                dst.write(src.read())
+    envs["ADP_MEMCAP_GRANT_DIR"] = gdir
+    if "ADP_MEMCAP_FILE" in envs:
+        envs["ADP_MEMCAP_FILE"] = mounts[envs["ADP_MEMCAP_FILE"]].host_path
+        for _ in range(500):
+            if os.path.isfile(envs["ADP_MEMCAP_FILE"]):
+                break
+            time.sleep(0.01)
+    return envs
+
+
+@pytest.mark.parametrize("env_limit", ["", "999999"])
+def test_daemon_grant_holds_whatever_the_pod_sets_on_pytorch(scratch, tmp_path, snap, env_limit):
+    """The grant is the daemon's read-only files: a pod that empties or raises
+    AMD_GPU_MEMORY_LIMIT_MIB still sees 4000 MiB and is refused past it."""
+    import json
+    import subprocess
+    import sys
+    d, k, resp = _allocate_memory_units(scratch, 4)
+    d.stop()
+    k.stop()
+    envs = _container_env(resp, str(tmp_path))
+    envs["AMD_GPU_MEMORY_LIMIT_MIB"] = env_limit  # the pod spec wins over the plugin's env
+    envs["ADP_MEMCAP_KEY"] = f"gpugrant-{os.getpid()}-{env_limit or 'empty'}"
+    code = ("import json, torch\n"
+            "free, total = torch.cuda.mem_get_info(0)\n"
+            "a = torch.empty(3 << 30, dtype=torch.uint8, device='cuda'); a.fill_(1)\n"
+            "try:\n"
+            "    b = torch.empty(2 << 30, dtype=torch.uint8, device='cuda'); over = False\n"
+            "except torch.OutOfMemoryError:\n"
+            "    over = True\n"
+            "print(json.dumps({'total_mib': total >> 20, 'over_refused': over}))\n")
+    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **envs}, capture_output=True, text=True,
+                       timeout=300)
+    _drop_memcap_segments(envs["ADP_MEMCAP_KEY"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out == {"total_mib": 4000, "over_refused": True}, (out, r.stderr[-2000:])
+
+
+def test_stream_ordered_pool_stays_within_the_grant_on_mi355x(tmp_path):
+    """Real HIP: a default pool told to keep everything (release threshold
+    UINT64_MAX, as frameworks set it) keeps a freed 2000 MiB block; under a
+    3000 MiB grant the next hipMalloc(2000 MiB) succeeds only because the shim
+    trims the pool first -- the GPU never holds both (DRM fdinfo)."""
+    import json
+    import subprocess
+    import sys
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    gdir = tmp_path / "grant"
+    gdir.mkdir()
+    (gdir / "0").write_text("3000\n")
+    code = r'''
+import ctypes, json, os
+hip_path = "/opt/rocm/lib/libamdhip64.so"
+ctypes.CDLL(hip_path, mode=os.RTLD_GLOBAL)   # the runtime, for what the shim does not interpose
+g = ctypes.CDLL(None)                         # global scope: the preloaded shim first
+def vram():
+    tot = 0
+    for fd in os.listdir("/proc/self/fd"):
+        try:
+            if not os.readlink(f"/proc/self/fd/{fd}").startswith("/dev/dri/render"): continue
+            for ln in open(f"/proc/self/fdinfo/{fd}"):
+                if ln.startswith("drm-resident-vram:"): tot += int(ln.split()[1]) * 1024
+        except OSError: pass
+    return tot >> 20
+assert g.hipSetDevice(0) == 0
+pool = ctypes.c_void_p()
+assert g.hipDeviceGetDefaultMemPool(ctypes.byref(pool), 0) == 0
+keep = ctypes.c_uint64(2**64 - 1)
+assert g.hipMemPoolSetAttribute(pool, 4, ctypes.byref(keep)) == 0   # hipMemPoolAttrReleaseThreshold
+base = vram()
+a = ctypes.c_void_p(); b = ctypes.c_void_p()
+r1 = g.hipMallocAsync(ctypes.byref(a), ctypes.c_size_t(2000 << 20), None)
+g.hipStreamSynchronize(None)
+r2 = g.hipFreeAsync(a, None)
+g.hipStreamSynchronize(None)
+held = vram() - base
+r3 = g.hipMalloc(ctypes.byref(b), ctypes.c_size_t(2000 << 20))
+g.hipDeviceSynchronize()
+after = vram() - base
+print(json.dumps({"mallocasync": r1, "freeasync": r2, "pool_held_mib": held, "malloc": r3, "after_mib": after}))
+'''
+    env = dict(os.environ, LD_PRELOAD=_with_preload(os.path.join(BUILD_DIR, "libadp_memcap.so")),
+               ADP_MEMCAP_GRANT_DIR=str(gdir), ADP_MEMCAP_KEY=f"gpupool-{os.getpid()}")
+    env.pop("AMD_GPU_MEMORY_LIMIT_MIB", None)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    _drop_memcap_segments(env["ADP_MEMCAP_KEY"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    os.makedirs("gpurun_out/memcap", exist_ok=True)
+    with open("gpurun_out/memcap/pool_retention.json", "w") as f:
+        json.dump(out, f, indent=1)
+    assert out["mallocasync"] == 0 and out["freeasync"] == 0 and out["malloc"] == 0, out
+    assert out["pool_held_mib"] >= 1900, out   # the pool really kept the freed block
+    assert out["after_mib"] < 3000, out         # trimmed before the hipMalloc: never 4000
+
+
+def test_driver_sees_an_allocation_that_bypasses_the_shim(scratch, tmp_path, snap):
+    """A container process that calls libamdhip64's hipMalloc through its own
+    dlopen handle (ctypes) goes around the shim: the shim's count stays at what
+    PyTorch allocated, but the driver's count (DRM fdinfo) has it all, /metrics
+    reports the container over its grant and counts the transition."""
+    import json
+    import re
+    import subprocess
+    import sys
+    import urllib.request
+    d, k, resp = _allocate_memory_units(scratch, 4, extra=["--metrics-addr", "127.0.0.1:0",
+                                                           "--driver-hbm-poll-ms", "200"],
+                                        env={"DP_HEALTH_POLL_MS": "0"})
+    p = None
+    try:
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics and /healthz on port", 30)).group(1))
+        envs = _container_env(resp, str(tmp_path))
+        code = r'''
+import ctypes, sys, torch
+a = torch.empty(1 << 30, dtype=torch.uint8, device="cuda"); a.fill_(1); torch.cuda.synchronize()
+hip = [ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln][0]
+lib = ctypes.CDLL(hip)              # the runtime torch already loaded, by its own handle
+p = ctypes.c_void_p()
+rc = lib.hipMalloc(ctypes.byref(p), ctypes.c_size_t(5 << 30))   # dlsym on the handle: not the shim
+lib.hipMemset(p, 1, ctypes.c_size_t(5 << 30)); lib.hipDeviceSynchronize()
+print("holding", rc, flush=True)
+sys.stdin.read()
+'''
+        p = subprocess.Popen([sys.executable, "-c", code], env={**os.environ, **envs}, stdin=subprocess.PIPE,
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        line = p.stdout.readline().split()
+        assert line[:2] == ["holding", "0"], (line, p.stderr.read()[-2000:] if p.poll() is not None else "")
+
+        def scrape():
+            with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
+                return r.read().decode()
+        deadline = time.time() + 10
+        while True:
+            body = scrape()
+            m = re.search(r'^amdgpu_dp_container_hbm_over_grant\{[^}]*\} (\d+)$', body, re.M)
+            if (m and m.group(1) == "1") or time.time() > deadline:
+                break
+            time.sleep(0.2)
+        vals = {}
+        for mm in re.finditer(r'^(amdgpu_dp_\w+)\{([^}]*)\} (\d+)$', body, re.M):
+            vals.setdefault(mm.group(1), []).append((mm.group(2), int(mm.group(3))))
+        one = lambda name: vals[name][0][1]
+        mib = 1 << 20
+        result = {k: one(k) for k in ("amdgpu_dp_container_hbm_used_bytes", "amdgpu_dp_container_hbm_granted_bytes",
+                                      "amdgpu_dp_container_hbm_driver_bytes", "amdgpu_dp_container_hbm_over_grant",
+                                      "amdgpu_dp_container_hbm_over_grant_total")}
+        result["unattributed"] = vals.get("amdgpu_dp_gpu_hbm_unattributed_bytes")
+        os.makedirs("gpurun_out/memcap", exist_ok=True)
+        with open("gpurun_out/memcap/driver_bypass.json", "w") as f:
+            json.dump({"metrics": result, "daemon_log_tail": d.log()[-2000:]}, f, indent=1)
+        assert result["amdgpu_dp_container_hbm_granted_bytes"] == 4000 * mib
+        assert result["amdgpu_dp_container_hbm_used_bytes"] < 2000 * mib, result      # the shim saw 1 GiB
+        assert result["amdgpu_dp_container_hbm_driver_bytes"] >= 6 << 30, result      # the driver saw 6 GiB
+        assert result["amdgpu_dp_container_hbm_over_grant"] == 1, result
+        assert result["amdgpu_dp_container_hbm_over_grant_total"] >= 1, result
+        assert "over its grant" in d.log()
+    finally:
+        if p:
+            p.stdin.close()
+            p.wait(60)
+        d.stop()
+        k.stop()
+
+
+def test_health_under_device_cgroup_denial(scratch, snap):
+    """An unprivileged pod: open(/dev/kfd) and open(/dev/dri/*) fail with EPERM
+    (what a device cgroup returns; libadp_devcgroup_sim.so). On the real
+    libamd_smi the daemon still enumerates (VRAM from the fallback), registers
+    and polls health (ECC, retired pages, liveness); event notification is off
+    and the log says why."""
+    import json
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR, DAEMON
+    sim = os.path.join(BUILD_DIR, "libadp_devcgroup_sim.so")
+    env = {"LD_PRELOAD": _with_preload(sim), "DP_HEALTH_POLL_MS": "300"}
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0"], env=env).start()
+    try:
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        law = c.watch()[0].get(timeout=10)
+        assert [x.health for x in law.devices] == ["Healthy"]
+        c.close()
+        log = d.wait_log("health poll #1", 30)
+    finally:
+        d.stop()
+        k.stop()
+    os.makedirs("gpurun_out/access", exist_ok=True)
+    with open("gpurun_out/access/daemon_denied.log", "w") as f:
+        f.write(log)
+    assert "device access: Operation not permitted: /dev/kfd" in log
+    events = [ln for ln in log.splitlines() if "events off:" in ln]
+    assert events and "/dev/kfd not openable (EPERM)" in events[0] and "device cgroup" in events[0]
+    poll = [ln for ln in log.splitlines() if "health poll #1" in ln][0]
+    assert "1/1 GPU(s) responding" in poll and "uncorrectable ECC readable on 1" in poll
+    rep = json.loads(subprocess.run([DAEMON, "--device-plugin-path", scratch, "--smi-report", "--devices", "0"],
+                                    capture_output=True, text=True, timeout=60, check=True,
+                                    env={**os.environ, **env}).stdout)
+    proc = rep["processors"][0]
+    assert proc["event_notification_init"]["status"] != 0
+    for q in ("uuid", "bdf", "enumeration_info", "memory_usage", "total_ecc_count", "bad_page_info",
+              "process_list", "compute_partition", "memory_partition"):
+        assert proc[q]["status"] == 0, (q, proc[q])
+    assert rep["enumeration"] == "ok"
+    dry = json.loads(subprocess.run([DAEMON, "--device-plugin-path", scratch, "--dry-run", "--devices", "0"],
+                                    capture_output=True, text=True, timeout=60, check=True,
+                                    env={**os.environ, **env}).stdout)
+    assert dry["gpus"][0]["vram_mib"] == snap["gpus"][0]["vram_mib"]  # vram_info fails; the fallback holds
+    assert dry["resources"][0]["allocatable"] == 1

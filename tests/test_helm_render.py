@@ -104,6 +104,25 @@ def test_max_retired_pages_renders_zero_as_off(value, rendered):
     assert env(daemonset({"maxRetiredPages": value}))["DP_MAX_RETIRED_PAGES"] == rendered
 
 
+def test_driver_hbm_check_mounts_the_hosts_proc():
+    """enforceMemoryUnits + metrics: the driver-side grant check reads the
+    host's processes through a read-only hostPath /proc at /host/proc."""
+    ds = daemonset({"enforceMemoryUnits": True, "metrics": {"enabled": True}})
+    check_consistent(ds)
+    e = env(ds)
+    assert e["DP_HOST_PROC"] == "/host/proc" and e["DP_DRIVER_HBM_POLL_MS"] == "10000"
+    assert e["DP_DRIVER_HBM_SLACK_MIB"] == "512"
+    (m,) = [m for m in container(ds)["volumeMounts"] if m["name"] == "host-proc"]
+    assert m == {"name": "host-proc", "mountPath": "/host/proc", "readOnly": True}
+    vols = {v["name"]: v for v in ds["spec"]["template"]["spec"]["volumes"]}
+    assert vols["host-proc"]["hostPath"]["path"] == "/proc"
+    for vals in ({"enforceMemoryUnits": True}, {"metrics": {"enabled": True}},
+                 {"enforceMemoryUnits": True, "metrics": {"enabled": True}, "driverHbmCheck": {"enabled": False}}):
+        off = daemonset(vals)
+        assert env(off)["DP_DRIVER_HBM_POLL_MS"] == "0" and "DP_HOST_PROC" not in env(off)
+        assert "host-proc" not in {v["name"] for v in off["spec"]["template"]["spec"]["volumes"]}
+
+
 def test_loop_affinity_value():
     assert env(daemonset({"loopAffinity": "peer-l3"}))["DP_LOOP_AFFINITY"] == "peer-l3"
 
@@ -213,7 +232,9 @@ def test_prometheus_operator_objects():
     assert sm["spec"]["selector"]["matchLabels"].items() <= svc["metadata"]["labels"].items()
     assert sm["spec"]["endpoints"] == [{"port": "metrics", "path": "/metrics", "interval": "30s"}]
     rules = rule["spec"]["groups"][0]["rules"]
-    assert len(rules) == 6 and all(r["alert"].startswith("AmdGpu") for r in rules)
+    assert len(rules) == 7 and all(r["alert"].startswith("AmdGpu") for r in rules)
+    over = [r for r in rules if r["alert"] == "AmdGpuContainerOverHbmGrant"][0]
+    assert "amdgpu_dp_container_hbm_over_grant" in over["expr"] and over["labels"]["severity"] == "critical"
     assert "> 0.9" in [r for r in rules if r["alert"] == "AmdGpuContainerNearHbmGrant"][0]["expr"]
     # every metric an alert uses is one the daemon exports
     src = "".join(open(f).read() for f in glob.glob(os.path.join(ROOT, "native", "src", "*", "*.cc")))

@@ -1,6 +1,7 @@
 """Renders the daemon's flag table (from `amdgpu-device-plugin --help`) as Markdown.
 
   python tools/gen_flag_table.py > /tmp/flags.md
+  python tools/gen_flag_table.py --update docs/USER_GUIDE.md   # rewrite the table in place
 Used to keep docs/USER_GUIDE.md in step with the binary (tests/test_docs.py).
 """
 import os
@@ -33,5 +34,19 @@ def table():
     return "\n".join(rows) + "\n"
 
 
+def update(path):
+    """Replaces the first flag table (header row + `--flag` rows) of `path`."""
+    lines = open(path).read().split("\n")
+    start = next(i for i, ln in enumerate(lines) if ln.startswith("| flag |"))
+    end = start + 2
+    while end < len(lines) and lines[end].startswith("| `--"):
+        end += 1
+    lines[start:end] = table().rstrip("\n").split("\n")
+    open(path, "w").write("\n".join(lines))
+
+
 if __name__ == "__main__":
-    sys.stdout.write(table())
+    if len(sys.argv) == 3 and sys.argv[1] == "--update":
+        update(sys.argv[2])
+    else:
+        sys.stdout.write(table())
