@@ -67,12 +67,23 @@ std::string GrantFromMaps(const std::string& maps_path, const std::vector<GrantF
     // "start-end perms offset MAJ:MIN inode path"
     unsigned maj = 0, mn = 0;
     unsigned long long ino = 0;
-    if (sscanf(line, "%*s %*s %*s %x:%x %llu", &maj, &mn, &ino) != 3 || ino == 0) continue;
-    for (const auto& g : grants)
-      if (g.ino == ino && g.dev_major == maj && g.dev_minor == mn) {
+    int path_at = 0;
+    if (sscanf(line, "%*s %*s %*s %x:%x %llu %n", &maj, &mn, &ino, &path_at) != 3 || ino == 0) continue;
+    std::string path = path_at > 0 ? std::string(line + path_at) : "";
+    while (!path.empty() && (path.back() == '\n' || path.back() == ' ')) path.pop_back();
+    auto ends = [&path](const std::string& suffix) {
+      return path.size() >= suffix.size() && path.compare(path.size() - suffix.size(), suffix.size(), suffix) == 0;
+    };
+    for (const auto& g : grants) {
+      if (g.ino != ino) continue;
+      // Same device and inode; or, where the daemon's path is on an overlay
+      // (maps names the underlying device), the same inode under a grant file's
+      // name: the pod's mount point or the file itself.
+      if ((g.dev_major == maj && g.dev_minor == mn) || ends("/amdgpu-dp/memcap") || ends("/" + g.key + ".memcap")) {
         found = g.key;
         break;
       }
+    }
     // A line longer than the buffer: skip its remainder.
     size_t len = strlen(line);
     while (len && line[len - 1] != '\n' && fgets(line, sizeof(line), f)) len = strlen(line);

@@ -39,7 +39,8 @@ class FakeProc:
         self.root = root
         os.makedirs(root, exist_ok=True)
 
-    def process(self, pid, cgroup, vram_mib=None, client=None, maps_file=None, bdf=BDF0, extra_fds=()):
+    def process(self, pid, cgroup, vram_mib=None, client=None, maps_file=None, bdf=BDF0, extra_fds=(),
+                maps_dev=None, maps_path="/run/amdgpu-dp/memcap"):
         base = os.path.join(self.root, str(pid))
         os.makedirs(os.path.join(base, "fd"), exist_ok=True)
         os.makedirs(os.path.join(base, "fdinfo"), exist_ok=True)
@@ -48,8 +49,8 @@ class FakeProc:
         maps = "55d0c0000000-55d0c0021000 r--p 00000000 08:01 131 /usr/bin/python3.10\n"
         if maps_file:
             st = os.stat(maps_file)
-            maps += (f"7f0000000000-7f0000100000 rw-s 00000000 {os.major(st.st_dev):02x}:{os.minor(st.st_dev):02x} "
-                     f"{st.st_ino} /run/amdgpu-dp/memcap\n")
+            dev = maps_dev or f"{os.major(st.st_dev):02x}:{os.minor(st.st_dev):02x}"
+            maps += f"7f0000000000-7f0000100000 rw-s 00000000 {dev} {st.st_ino} {maps_path}\n"
         with open(os.path.join(base, "maps"), "w") as f:
             f.write(maps)
         fd = os.path.join(base, "fd", "3")
@@ -174,6 +175,23 @@ def test_a_forged_accounting_file_does_not_raise_the_grant(node):
     s = _scrape_after_poll(port, _polls(port) + 2)
     assert _value(s, "amdgpu_dp_container_hbm_granted_bytes", allocation=key) == 3000 * MIB
     assert _value(s, "amdgpu_dp_container_hbm_over_grant", allocation=key, bdf=BDF0) == 1
+
+
+def test_attribution_through_an_overlay(node):
+    """An overlay filesystem: /proc/<pid>/maps names the underlying device,
+    stat() the overlay's. The same inode under the pod's mount point (or the
+    grant file's own name) still identifies the grant; a same-numbered inode
+    of some other file does not."""
+    d, proc, port, host = node
+    key = os.path.basename(host).split(".")[0]
+    proc.process(501, "0::/kubepods/pod-c/a", vram_mib=700, maps_file=host, maps_dev="00:2f")
+    proc.process(502, "0::/kubepods/pod-c/b", vram_mib=300, maps_file=host, maps_dev="00:30",
+                 maps_path=f"/var/lib/kubelet/device-plugins/amdgpu-dp/usage/{key}.memcap")
+    proc.process(503, "0::/kubepods/pod-d/c", vram_mib=400, maps_file=host, maps_dev="00:31",
+                 maps_path="/usr/lib/libsomething.so")
+    s = _scrape_after_poll(port, _polls(port) + 2)
+    assert _value(s, "amdgpu_dp_container_hbm_driver_bytes", allocation=key, bdf=BDF0) == 1000 * MIB
+    assert _value(s, "amdgpu_dp_gpu_hbm_unattributed_bytes", bdf=BDF0) == 400 * MIB
 
 
 def test_unreadable_processes_are_reported(node):
