@@ -79,7 +79,7 @@ const std::vector<FlagDef>& Table() {
       {"replica-cu-mask", "REPLICA_CU_MASK", "replicaCuMask", Kind::kBool,
        "replicas also split the device's compute units (HSA_CU_MASK on Allocate): time-slice "
        "replica r of R runs on its own 1/R of every XCD's CUs; memory units get CUs in "
-       "proportion to the units held",
+       "proportion to the units held (proportional, not isolating: neighbours may share a boundary slot)",
        [](Flags& f) -> void* { return &f.replica_cu_mask; }},
       {"device-plugin-path", "DP_PLUGIN_DIR", "devicePluginPath", Kind::kString,
        "kubelet device-plugin directory",

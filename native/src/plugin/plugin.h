@@ -140,10 +140,11 @@ std::vector<std::pair<uint32_t, uint32_t>> ReplicaCuRanges(uint32_t cus, uint32_
 // Memory units (replicas = -1) with --replica-cu-mask: the unit whose ID is
 // k-th in lexicographic order owns CU slot floor(k * per / units) (per = CUs per
 // XCD; a slot is one CU on every XCD), so a pod gets compute in proportion to
-// the HBM it holds -- a soft MIG-style slice -- and a packed request, which takes
-// IDs in that order, gets contiguous slots. About units/per units share a slot,
-// so two pods may share one boundary slot. Indexed by replica number; empty
-// when the shape is unknown or not uniform.
+// the HBM it holds, and a packed request, which takes IDs in that order, gets
+// contiguous slots. Proportional, not isolating: about units/per units share a
+// slot, so two pods may share one boundary slot (never more than one per side
+// of a contiguous range). Indexed by replica number; empty when the shape is
+// unknown or not uniform.
 std::vector<std::pair<uint32_t, uint32_t>> MemoryUnitCuRanges(uint32_t cus, uint32_t xcds, unsigned units);
 
 // min(8, online CPUs): one loop per GPU of an 8-GPU node. Idle loops sit in

@@ -270,8 +270,8 @@ def test_memory_units_get_proportional_cu_shares(running, scratch):
     """gpu-mem-gb with --replica-cu-mask: a pod's CUs follow the HBM it holds. The
     k-th unit ID in name order owns CU slot floor(k*32/294) (one CU per XCD per
     slot), so pods admitted the kubelet's way (GetPreferredAllocation with pack,
-    then Allocate) get contiguous slots -- a soft MIG-style slice; neighbours may
-    share one boundary slot."""
+    then Allocate) get contiguous slots -- a proportional CU share, not an
+    isolating slice: neighbours may share one boundary slot."""
     d, k = running(args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack",
                          "--replica-cu-mask"])
     reg = k.wait_registration()
@@ -288,3 +288,36 @@ def test_memory_units_get_proportional_cu_shares(running, scratch):
     assert admit(36)["HSA_CU_MASK"] == "0:24-63"  # shares slot 3 with the first pod
     assert admit(222)["HSA_CU_MASK"] == "0:56-255"  # the rest of GPU 0
     c.close()
+
+
+@pytest.mark.parametrize("sizes", [[36, 36, 36, 36, 36, 36, 36, 36, 6], [1] * 40, [5, 13, 1, 40, 9, 2, 100, 3],
+                                   [10] * 29])
+def test_memory_unit_cu_shares_overlap_at_most_one_boundary_slot(running, scratch, sizes):
+    """The documented bound of the proportional CU share: pods admitted the
+    kubelet's way (pack) each get one contiguous run of slots, and two pods
+    never share more than one slot -- only at a boundary. A slot is shared only
+    when both pods hold units of it."""
+    d, k = running(fixture=fixtures.node(1), args=["--resource-config", "gpu:gpu-mem-gb:-1",
+                                                   "--replica-policy", "pack", "--replica-cu-mask"])
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    free = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    slots = []
+    for size in sizes:
+        ids = list(c.preferred(free, size=size).container_responses[0].deviceIDs)
+        for i in ids:
+            free.remove(i)
+        mask = dict(c.allocate(ids).container_responses[0].envs)["HSA_CU_MASK"]
+        agent, ranges = mask.split(":")
+        assert agent == "0" and "," not in ranges, mask  # one contiguous range
+        lo, hi = map(int, ranges.split("-"))
+        assert lo % 8 == 0 and (hi + 1) % 8 == 0, mask  # whole slots (one CU on each of 8 XCDs)
+        slots.append(set(range(lo // 8, (hi + 1) // 8)))
+    c.close()
+    for i in range(len(slots)):
+        for j in range(i + 1, len(slots)):
+            shared = slots[i] & slots[j]
+            assert len(shared) <= 1, (sizes[i], sizes[j], sorted(slots[i]), sorted(slots[j]))
+            if shared:  # a boundary of both runs
+                (s_,) = shared
+                assert s_ in (min(slots[i]), max(slots[i])) and s_ in (min(slots[j]), max(slots[j]))
