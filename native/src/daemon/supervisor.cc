@@ -17,6 +17,9 @@
 #include <cstring>
 #include <atomic>
 #include <memory>
+#include <tuple>
+#include <set>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -410,6 +413,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   std::unique_ptr<memcap::DriverHbmMonitor> driver_hbm;
   std::mutex access_mu;  // node_access: written by restart, read by /metrics
   std::vector<inventory::NodeAccess> node_access;
+  const std::string usage_dir = PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage");  // startup-only flag
   std::unique_ptr<metrics::HttpServer> http;
   std::unique_ptr<podresources::CachedLister> pod_lister;
   if (!cfg.flags.metrics_addr.empty() && !cfg.flags.pod_resources_socket.empty())
@@ -483,6 +487,26 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
                    "# TYPE amdgpu_dp_pod_resources_up gauge\n"
                    "amdgpu_dp_pod_resources_up " + std::string(assigned.ok() ? "1" : "0") + "\n";
           }
+          // Grant accounting files: read (and old ones collected) here, before
+          // the plugins lock the health listener also takes -- a slow
+          // filesystem must not hold up health verdicts.
+          std::vector<memcap::Usage> grant_files;
+          bool have_grants = false;
+          {
+            struct stat st;
+            if (stat(usage_dir.c_str(), &st) == 0 && S_ISDIR(st.st_mode)) {
+              have_grants = true;
+              grant_files = memcap::ReadAll(usage_dir);
+              std::set<std::string> live;
+              if (assigned.ok()) {
+                std::map<std::tuple<std::string, std::string, std::string, std::string>,
+                         std::vector<std::string_view>> ctrs;
+                for (const auto& a : *assigned) ctrs[{a.ns, a.pod, a.container, a.resource}].push_back(a.device_id);
+                for (const auto& [k, ids] : ctrs) live.insert(memcap::AllocationKey(ids));
+              }
+              memcap::Collect(usage_dir, assigned.ok() ? &live : nullptr, 120, 4096);
+            }
+          }
           std::unique_ptr<memcap::DriverHbmMonitor::Snapshot> dsnap;
           if (driver_hbm) {
             dsnap = std::make_unique<memcap::DriverHbmMonitor::Snapshot>(driver_hbm->Get());
@@ -512,7 +536,8 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
           std::vector<const plugin::Plugin*> ps;
           for (auto& p : plugins)
             if (p->device_count() > 0) ps.push_back(p.get());
-          plugin::Plugin::AppendPrometheus(ps, &out, assigned.ok() ? &*assigned : nullptr, dsnap.get());
+          plugin::Plugin::AppendPrometheus(ps, &out, assigned.ok() ? &*assigned : nullptr, dsnap.get(),
+                                           have_grants ? &grant_files : nullptr);
           return out;
         },
         [&] {

@@ -967,7 +967,8 @@ void Sample(std::string* out, const char* name, const std::string& labels, uint6
 
 void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::string* out,
                               const std::vector<podresources::Assignment>* assignments,
-                              const memcap::DriverHbmMonitor::Snapshot* driver) {
+                              const memcap::DriverHbmMonitor::Snapshot* driver,
+                              const std::vector<memcap::Usage>* grant_files) {
   using metrics::LabelValue;
   auto family = [&](const char* name, const char* type, const char* help) { Family(out, name, type, help); };
   auto gauge = [&](const char* name, const std::string& labels, double v) { Sample(out, name, labels, v); };
@@ -1064,7 +1065,7 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
   }
   for (auto* p : plugins) {
     if (p->memcap_bytes_.empty() || p->opts_.memcap_usage_dir.empty()) continue;
-    AppendMemcapUsage(plugins, p->opts_.memcap_usage_dir, assignments, out, driver);
+    AppendMemcapUsage(plugins, p->opts_.memcap_usage_dir, assignments, out, driver, grant_files);
     break;
   }
   struct Conn { const Plugin* p; uint64_t connections, shed, errors; };
@@ -1129,7 +1130,8 @@ std::map<std::string, std::map<std::string, uint64_t>> Plugin::GrantedByKey(cons
 // the container's processes on each GPU is reported next to them.
 void Plugin::AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const std::string& dir,
                                const std::vector<podresources::Assignment>* assignments, std::string* out,
-                               const memcap::DriverHbmMonitor::Snapshot* driver) {
+                               const memcap::DriverHbmMonitor::Snapshot* driver,
+                               const std::vector<memcap::Usage>* grant_files) {
   using metrics::LabelValue;
   struct Row {
     const Plugin* p;
@@ -1150,6 +1152,13 @@ void Plugin::AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const 
     }
     return !r->units.empty();
   };
+  // The grant files, read by the caller before it took the plugins lock
+  // (then Collect() ran there too), or here.
+  std::vector<memcap::Usage> own;
+  if (!grant_files) own = memcap::ReadAll(dir);
+  const std::vector<memcap::Usage>& files = grant_files ? *grant_files : own;
+  std::map<std::string, const memcap::Usage*> by_key;
+  for (const auto& u : files) by_key[u.key] = &u;
   std::vector<Row> rows;
   std::set<std::string> live;
   if (assignments) {
@@ -1161,16 +1170,16 @@ void Plugin::AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const 
       if (!p) continue;
       std::string key = memcap::AllocationKey(ids);
       live.insert(key);
-      auto u = memcap::ReadGrant(dir, key);
+      auto u = by_key.find(key);
       Row r{p, "", {}, {}, {}};
-      if (!u.ok() || !fill(p, ids, &r)) continue;
-      r.u = std::move(*u);
+      if (u == by_key.end() || !fill(p, ids, &r)) continue;
+      r.u = *u->second;
       r.labels = "resource=\"" + LabelValue(resource) + "\",namespace=\"" + LabelValue(ns) + "\",pod=\"" +
                  LabelValue(pod) + "\",container=\"" + LabelValue(ctr) + "\"";
       rows.push_back(std::move(r));
     }
   } else {
-    for (auto& u : memcap::ReadAll(dir)) {
+    for (const auto& u : files) {
       std::vector<std::string_view> ids;
       for (size_t b = 0; !u.ids.empty() && b <= u.ids.size();) {
         size_t e = std::min(u.ids.find(',', b), u.ids.size());
@@ -1181,13 +1190,13 @@ void Plugin::AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const 
         Row r{p, "", {}, {}, {}};
         if (ids.empty() || p->memcap_bytes_.empty() || !fill(p, ids, &r)) continue;
         r.labels = "resource=\"" + LabelValue(p->spec_.resource_name) + "\",allocation=\"" + u.key + "\"";
-        r.u = std::move(u);
+        r.u = u;
         rows.push_back(std::move(r));
         break;
       }
     }
   }
-  memcap::Collect(dir, assignments ? &live : nullptr, 120, 4096);
+  if (!grant_files) memcap::Collect(dir, assignments ? &live : nullptr, 120, 4096);
 
   auto dev_label = [](const Row& r, size_t i) {
     return i < r.units.size() ? r.p->units_[r.units[i]].id : "hip" + std::to_string(i);

@@ -42,6 +42,7 @@
 #include "inventory/inventory.h"
 #include "metrics/metrics.h"
 #include "memcap/driver_usage.h"
+#include "memcap/usage.h"
 #include "podresources/podresources.h"
 #include "strategy/strategy.h"
 
@@ -227,7 +228,8 @@ class Plugin {
   // `assignments` (kubelet PodResources, may be null) adds per-device usage.
   static void AppendPrometheus(const std::vector<const Plugin*>& plugins, std::string* out,
                                const std::vector<podresources::Assignment>* assignments = nullptr,
-                               const memcap::DriverHbmMonitor::Snapshot* driver = nullptr);
+                               const memcap::DriverHbmMonitor::Snapshot* driver = nullptr,
+                               const std::vector<memcap::Usage>* grant_files = nullptr);
   // Every live enforced grant (accounting files in `dir` whose IDs hash to
   // their name) -> PCI address of each GPU -> bytes granted there, from this
   // daemon's own units (never from the container-writable file's cap[]).
@@ -253,7 +255,8 @@ class Plugin {
   Status Register();
   static void AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const std::string& dir,
                                 const std::vector<podresources::Assignment>* assignments, std::string* out,
-                                const memcap::DriverHbmMonitor::Snapshot* driver);
+                                const memcap::DriverHbmMonitor::Snapshot* driver,
+                                const std::vector<memcap::Usage>* grant_files);
   void AddUsageFile(const std::vector<std::string_view>& ids, const std::vector<uint64_t>& grant_bytes,
                     std::string* c);
 
