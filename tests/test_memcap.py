@@ -26,19 +26,27 @@ PRELOAD = " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), SHIM) if x)
 CHECK = os.path.join(BUILD_DIR, "adp_memcap_check")
 
 
+# Every grant key of this file carries the test process's tag, so the cleanup
+# below never removes a segment a concurrent test process (pytest -n) still uses.
+TAG = f"w{os.getpid()}"
+
+
+def _key(name):
+    return f"{TAG}-{name}-{time.monotonic_ns()}"
+
+
 @pytest.fixture(autouse=True)
 def _no_leftover_segments():
-    """The shim's container-wide counters live in /dev/shm/adp-memcap-*; drop
-    the ones a test created (in a pod they go with the pod)."""
-    before = set(glob.glob("/dev/shm/adp-memcap-*"))
+    """The shim's container-wide counters live in /dev/shm/adp-memcap-key-*;
+    drop the ones a test created (in a pod they go with the pod)."""
     yield
-    for f in set(glob.glob("/dev/shm/adp-memcap-*")) - before:
+    for f in glob.glob(f"/dev/shm/adp-memcap-key-{TAG}-*"):
         os.unlink(f)
 
 
 def _run(env_extra, *args):
     env = dict(os.environ, **env_extra)
-    env.setdefault("ADP_MEMCAP_KEY", f"test-{os.getpid()}-{time.monotonic_ns()}")
+    env.setdefault("ADP_MEMCAP_KEY", _key("test"))
     r = subprocess.run([CHECK, *args], capture_output=True, text=True, timeout=60, env=env)
     assert r.returncode == 0, r.stderr
     return {d["step"]: d for d in map(json.loads, r.stdout.splitlines())}, r.stderr
@@ -105,7 +113,7 @@ def _try(env, mib):
 def test_processes_of_a_container_share_one_grant():
     """The grant is the container's: a second process gets what the first left
     over, and a process that exits gives its bytes back."""
-    env = _env(f"share-{time.monotonic_ns()}")
+    env = _env(_key("share"))
     a = _hold(env, 60)
     try:
         assert _try(env, 50) == (2, 40)  # refused: 60 of 100 held by the other process
@@ -119,7 +127,7 @@ def test_processes_of_a_container_share_one_grant():
 
 def test_bytes_of_a_killed_process_are_reclaimed():
     import signal
-    env = _env(f"kill-{time.monotonic_ns()}")
+    env = _env(_key("kill"))
     a = _hold(env, 60)
     a.send_signal(signal.SIGKILL)
     a.wait(10)
@@ -127,7 +135,7 @@ def test_bytes_of_a_killed_process_are_reclaimed():
 
 
 def test_forked_child_draws_on_the_same_grant():
-    env = _env(f"fork-{time.monotonic_ns()}")
+    env = _env(_key("fork"))
     r = subprocess.run([CHECK, "fork", "60"], capture_output=True, text=True, timeout=30, env=env)
     out = {d["step"]: d for d in map(json.loads, r.stdout.splitlines())}
     assert out["parent malloc"]["rc"] == 0
@@ -136,7 +144,7 @@ def test_forked_child_draws_on_the_same_grant():
 
 
 def test_other_grants_and_other_containers_are_separate():
-    key = f"sep-{time.monotonic_ns()}"
+    key = _key("sep")
     a = _hold(_env(key), 60)
     try:
         assert _try(_env(key + "-other"), 90) == (0, 10)  # another container
@@ -238,7 +246,7 @@ def test_daemon_grant_cannot_be_raised_or_dropped_from_the_env(tmp_path, env_val
     base = dict(os.environ)
     base.pop("AMD_GPU_MEMORY_LIMIT_MIB", None)
     r = subprocess.run([CHECK], capture_output=True, text=True, timeout=60,
-                       env=dict(base, ADP_MEMCAP_KEY=f"grant-{os.getpid()}-{time.monotonic_ns()}", **env))
+                       env=dict(base, ADP_MEMCAP_KEY=_key("grant"), **env))
     assert r.returncode == 0, r.stderr
     out = {d["step"]: d for d in map(json.loads, r.stdout.splitlines())}
     assert out["d0 malloc 50"]["rc"] == 2 and out["d0 info"]["total_mib"] == 100
@@ -383,7 +391,7 @@ def test_missing_accounting_file_falls_back_to_dev_shm():
     """ADP_MEMCAP_FILE names the daemon's per-grant file; when it is absent
     (say the kubelet wiped the plugin directory) the grant is still enforced,
     counted in the pod's /dev/shm."""
-    env = dict(_env(f"nofile-{time.monotonic_ns()}"), ADP_MEMCAP_FILE="/nonexistent/memcap")
+    env = dict(_env(_key("nofile")), ADP_MEMCAP_FILE="/nonexistent/memcap")
     a = _hold(env, 60)
     try:
         assert _try(env, 50) == (2, 40)  # the two processes still share the grant
