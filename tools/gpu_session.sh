@@ -30,6 +30,11 @@
 #                health monitor's log, with and without the denial
 #   driver       what the driver reports per process (KFD sysfs, DRM fdinfo,
 #                amdsmi_get_gpu_process_list) while PyTorch holds HBM
+#   ab           interleaved headline runs per --loop-affinity mode (AB_MODES,
+#                default "none peer-l3"; AB_PAIRS rounds, default 8), plus the
+#                8-rank mock node (AB_RANKS) per mode
+#   cpus         the CPUs this box lets the session use, grouped by L3 / NUMA
+#   curve        tools/mock_curve.sh (CONFIGS="spx-none" for one config)
 #   soak         3 minutes of churn + SIGHUP + kubelet restarts + scrapes on
 #                real libamd_smi (health polling, state file): RSS/fd/thread leaks
 set -o pipefail
@@ -144,6 +149,31 @@ step_access() {
 step_driver() {
   timeout -k 10 180 python tools/probe_driver_usage.py > $out/driver_usage.json 2> $out/driver_usage.err || die DRIVER $out/driver_usage.err
   python3 -c "import json; d=json.load(open('$out/driver_usage.json')); print(json.dumps({'self_fdinfo': d.get('self_fdinfo'), 'child': {k: v for k, v in d['child'].items() if k != 'cgroup'}})[:3000])"
+}
+step_ab() {
+  local modes=${AB_MODES:-none peer-l3} pairs=${AB_PAIRS:-8} port=29711
+  for i in $(seq 1 $pairs); do
+    for m in $modes; do
+      DP_LOOP_AFFINITY=$m timeout -k 10 300 python bench.py --no-probe > $out/ab_${m}_$i.json 2> $out/ab_${m}_$i.err || die "AB $m $i" $out/ab_${m}_$i.err
+      python -c "import json; d=json.load(open('$out/ab_${m}_$i.json')); print('AB $m $i', d['value'], d['allocate_p99_us'], d.get('grpc_go_shaped_allocate_p50_us'), d['pods_per_s'])"
+    done
+  done
+  for i in $(seq 1 ${AB_RANK_PAIRS:-3}); do
+    for m in $modes; do
+      port=$((port + 1))
+      DP_LOOP_AFFINITY=$m timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${AB_RANKS:-8} \
+        --master-addr 127.0.0.1 --master-port $port bench.py --gpus ${AB_RANKS:-8} --mock --no-probe \
+        > $out/abr_${m}_$i.json 2> $out/abr_${m}_$i.err || die "AB ranks $m $i" $out/abr_${m}_$i.err
+      python -c "import json; d=json.loads(open('$out/abr_${m}_$i.json').read().strip().splitlines()[-1]); print('ABR $m $i', d['value'], d['allocate_p99_us'], d.get('grpc_go_shaped_allocate_p50_us'), d['pods_per_s'])"
+    done
+  done
+}
+step_cpus() {
+  python3 tools/cpu_layout.py > $out/cpus.json || die CPUS
+  cat $out/cpus.json
+}
+step_curve() {
+  bash tools/mock_curve.sh $out/curve || die CURVE
 }
 step_soak() {
   timeout -k 10 400 python -u tools/soak.py --seconds 180 --real ${SOAK_ARGS:-} --out $out/soak.json > $out/soak.log 2>&1 || die SOAK $out/soak.log

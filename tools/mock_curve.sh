@@ -1,4 +1,5 @@
 #!/bin/bash
+# CONFIGS="spx-none" limits the run to the configs named.
 # Allocate() p50 / allocatable curve at 1/2/4/8 GPUs for every BASELINE config on
 # the amdsmi mock node model (gloo ranks, no GPU touched) -- the multi-GPU and
 # partition configurations the one-GPU box cannot host for real.
@@ -6,7 +7,7 @@ set -o pipefail
 out=${1:-gpurun_out/curve}
 mkdir -p $out
 port=29611
-for cfg in spx-none timeslice4 auto-mem cpx-single; do
+for cfg in ${CONFIGS:-spx-none timeslice4 auto-mem cpx-single}; do
   for n in 1 2 4 8; do
     port=$((port + 1))
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
