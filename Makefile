@@ -4,7 +4,7 @@ JOBS       ?= 8
 PY         ?= python3
 GPURUN     ?= /usr/local/graft/bin/gpurun
 
-.PHONY: all build probe test test-native test-gpu bench asan tsan tsan-e2e asan-e2e coverage lint image clean
+.PHONY: all build probe test test-native test-gpu bench asan tsan tsan-e2e asan-e2e fuzz coverage lint image clean
 
 # Containerised targets (reference Makefile:44-74): `make docker-<target>` runs
 # `make <target>` in the development image built from docker/Dockerfile.devel.
@@ -81,6 +81,25 @@ tsan-e2e:
 	@if ls build/tsan-logs/* >/dev/null 2>&1; then cat build/tsan-logs/*; exit 1; fi
 
 # The daemon under ASan/UBSan/LSan, driven by the same end-to-end suites.
+# Coverage-guided fuzzing (libFuzzer, ASan+UBSan, clang from ROCm's LLVM) of
+# every parser that sees bytes from outside: the RPC handlers, HTTP/2, the
+# protobuf codec, the config front end, grant accounting files + /metrics, the
+# driver-side /proc scan (native/fuzz/). FUZZ_SECONDS per target, in parallel;
+# corpora grow in build/fuzz/corpus/<target>; a crash leaves build/fuzz/crash-*.
+FUZZ_TARGETS ?= plugin h2 proto config grantfile procscan
+FUZZ_SECONDS ?= 60
+CLANGXX      ?= /opt/rocm/lib/llvm/bin/clang++
+fuzz:
+	cmake -S native -B build/fuzz -G Ninja -DCMAKE_BUILD_TYPE=RelWithDebInfo -DADP_FUZZ=ON \
+	  -DCMAKE_CXX_COMPILER=$(CLANGXX) -DCMAKE_C_COMPILER=$(dir $(CLANGXX))clang >/dev/null
+	ninja -C build/fuzz -j$(JOBS) $(addprefix fuzz_,$(FUZZ_TARGETS))
+	$(PY) tools/gen_fuzz_seeds.py build/fuzz/corpus/h2
+	cd build/fuzz && for t in $(FUZZ_TARGETS); do mkdir -p corpus/$$t; \
+	  ( ./fuzz_$$t -max_total_time=$(FUZZ_SECONDS) -rss_limit_mb=2048 -print_final_stats=1 corpus/$$t \
+	    > fuzz_$$t.log 2>&1 || echo "fuzz_$$t FAILED (build/fuzz/fuzz_$$t.log)" > fuzz_$$t.failed ) & done; wait; \
+	  for t in $(FUZZ_TARGETS); do grep -h "DONE" fuzz_$$t.log | sed "s/^/$$t /"; done; \
+	  ! cat fuzz_*.failed 2>/dev/null
+
 asan-e2e:
 	cmake -S native -B build/asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DADP_SANITIZE=ON >/dev/null
 	ninja -C build/asan -j$(JOBS) amdgpu-device-plugin amdgpu-dp-kubelet amdsmi_mock

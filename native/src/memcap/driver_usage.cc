@@ -105,6 +105,7 @@ uint64_t ParseFdinfoSize(const std::string& value) {
   if (!strncmp(end, "KiB", 3)) mul = 1ull << 10;
   else if (!strncmp(end, "MiB", 3)) mul = 1ull << 20;
   else if (!strncmp(end, "GiB", 3)) mul = 1ull << 30;
+  if (n > UINT64_MAX / mul) return UINT64_MAX;  // saturate: never wrap a huge claim to a small one
   return static_cast<uint64_t>(n) * mul;
 }
 

@@ -35,6 +35,19 @@ uint64_t NowNs() {
       .count();
 }
 
+// Whether an ID occurs twice (a pod's k is small: pairwise up to 16, else sorted).
+bool HasDuplicate(const std::vector<std::string>& ids) {
+  if (ids.size() <= 16) {
+    for (size_t i = 1; i < ids.size(); ++i)
+      for (size_t j = 0; j < i; ++j)
+        if (ids[i] == ids[j]) return true;
+    return false;
+  }
+  std::vector<std::string_view> v(ids.begin(), ids.end());
+  std::sort(v.begin(), v.end());
+  return std::adjacent_find(v.begin(), v.end()) != v.end();
+}
+
 }  // namespace
 
 bool ParseDeviceListStrategy(std::string_view s, DeviceListStrategy* out) {
@@ -577,27 +590,27 @@ Status Plugin::PreferredImpl(std::string_view req, std::string* resp) {
       auto res = alloc::PrioritizeDeviceViews(cr.available, cr.must_include, cr.allocation_size,
                                               opts_.replica_policy, alloc::kReplicaJoin, &affinity);
       if (!res.ok()) return res.status();
+      if (HasDuplicate(res->ids)) {
+        // An ID listed twice in availableDeviceIDs was chosen twice: choose
+        // again from the de-duplicated list (off the common path).
+        std::vector<std::string_view> avail(cr.available.begin(), cr.available.end());
+        std::sort(avail.begin(), avail.end());
+        avail.erase(std::unique(avail.begin(), avail.end()), avail.end());
+        res = alloc::PrioritizeDeviceViews(avail, cr.must_include, cr.allocation_size, opts_.replica_policy,
+                                           alloc::kReplicaJoin, &affinity);
+        if (!res.ok()) return res.status();
+      }
       // Physical devices must be ours (reference: NewDevicesFrom fails on an
       // unknown UUID, server.go:274-278) -- one lookup per device, not per
-      // replica -- and so must every ID handed back.
+      // replica -- and so must every ID handed back (of the final choice: an
+      // ID the kubelet made up, e.g. "<uuid>-replica-1x", names a device of
+      // ours but was never advertised).
       for (const auto& dev : res->devices)
         if (!unit_index_by_id_.count(dev))
           return InvalidArgument("unable to retrieve list of available devices: unknown device " + dev);
-      for (size_t i = 0; i < res->ids.size(); ++i) {
-        if (!advertised_index_.count(res->ids[i]))
-          return InvalidArgument("unable to retrieve list of available devices: unknown device " + res->ids[i]);
-        if (i && res->ids[i] == res->ids[i - 1]) {
-          // An ID listed twice in availableDeviceIDs was chosen twice: choose
-          // again from the de-duplicated list (off the common path).
-          std::vector<std::string_view> avail(cr.available.begin(), cr.available.end());
-          std::sort(avail.begin(), avail.end());
-          avail.erase(std::unique(avail.begin(), avail.end()), avail.end());
-          res = alloc::PrioritizeDeviceViews(avail, cr.must_include, cr.allocation_size, opts_.replica_policy,
-                                             alloc::kReplicaJoin, &affinity);
-          if (!res.ok()) return res.status();
-          break;
-        }
-      }
+      for (const auto& id : res->ids)
+        if (!advertised_index_.count(id))
+          return InvalidArgument("unable to retrieve list of available devices: unknown device " + id);
       if (res->non_unique) LOG_DEBUG(kComp, "ignoring: %s", alloc::kNonUniqueMessage);
       out.container_responses.push_back(std::move(res->ids));
       continue;

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "inventory/inventory.h"
+#include "node_model.h"
 #include "plugin/plugin.h"
 #include "proto/messages.h"
 #include "strategy/strategy.h"
@@ -18,35 +19,6 @@ using namespace adp;
 using Clock = std::chrono::steady_clock;
 
 namespace {
-
-std::shared_ptr<const inventory::Snapshot> Node(int gpus, int parts) {
-  std::vector<smi::ProcessorInfo> procs;
-  for (int g = 0; g < gpus; ++g) {
-    for (int p = 0; p < parts; ++p) {
-      smi::ProcessorInfo pi;
-      char uuid[64];
-      snprintf(uuid, sizeof(uuid), "%08x-0000-1%x00-80c0-bf9907890000", 0x75a30000 + g, p);
-      pi.uuid = uuid;
-      pi.bdf_id = (static_cast<uint64_t>(0x0c + 0x20 * g) << 8) | static_cast<uint64_t>(p);
-      pi.render_minor = 128 + 8 * g + p;
-      pi.numa_node = g < 4 ? 0 : 1;
-      pi.vram_mib = 294896 / parts;
-      pi.compute_partition = parts == 1 ? "SPX" : "CPX";
-      pi.memory_partition = parts == 1 ? "NPS1" : "NPS2";
-      pi.partition_id = p;
-      pi.num_cu = 256 / parts;
-      pi.xcd_count = 8 / parts;
-      procs.push_back(pi);
-    }
-  }
-  auto s = inventory::GroupProcessors(procs, {});
-  auto& snap = *s;
-  size_t n = snap->gpus.size();
-  for (size_t a = 0; a < n; ++a)
-    for (size_t b = 0; b < n; ++b)
-      if (a != b) { snap->gpu_links[a * n + b] = inventory::LinkClass::kXgmi; snap->gpu_hops[a * n + b] = 1; }
-  return snap;
-}
 
 template <typename Fn>
 double TimeUs(int iters, Fn fn) {
@@ -78,7 +50,7 @@ int main(int argc, char** argv) {
   printf("{");
   bool first = true;
   for (const auto& c : cases) {
-    auto snap = Node(c.gpus, c.parts);
+    auto snap = testing::NodeModel(c.gpus, c.parts);
     auto rc = strategy::ResourceConfig::Parse(c.rc);
     auto specs = strategy::BuildPluginSpecs(*snap, c.ps, *rc);
     plugin::PluginOptions po;

@@ -114,6 +114,21 @@ def test_replicated_request_names_only_our_devices_and_no_id_twice(plugin):
     assert sorted(got) == sorted({ids[0], ids[1]})
 
 
+def test_rechosen_replicas_are_checked_too(plugin):
+    """Found by native/fuzz/fuzz_plugin.cc: an ID listed twice made the handler
+    choose again from the de-duplicated list without checking that choice, so
+    a made-up replica of one of our GPUs ("<uuid>-replica-1x") came back."""
+    c, ids = plugin(fixtures.node(2), args=["--resource-config", "gpu:gpu:3", "--replica-policy", "pack"])
+    g0, g1 = ids[:3], ids[3:]
+    avail = [g0[1], g1[0], g1[1], g1[1] + "x", g0[0] + "x", g1[1]]
+    try:
+        got = pref(c, avail, size=3)
+    except grpc.RpcError as e:
+        assert e.code() == grpc.StatusCode.INVALID_ARGUMENT
+    else:
+        assert len(set(got)) == 3 and set(got) <= set(ids), got
+
+
 def test_pack_policy_over_the_wire(plugin):
     c, ids = plugin(fixtures.node(2), args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack"])
     assert len(ids) == 2 * (fixtures.MI355X_VRAM_MIB // 1000)
