@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Seed inputs for native/fuzz/fuzz_h2.cc: well-formed gRPC exchanges the
+"""Seed inputs for native/fuzz/fuzz_h2.cc and fuzz_h2_diff.cc: well-formed gRPC exchanges the
 fuzzer mutates from, so it starts inside the HTTP/2 state machine instead of
-at the frame-header checks. Written to <dir> (default build/fuzz/corpus/h2).
+at the frame-header checks. Written to each <dir> given (default
+build/fuzz/corpus/h2).
 
 Input layout (fuzz_h2.cc): byte 0 = log2 of the write chunk size, then the
 client's frames after the preface and an empty SETTINGS frame."""
@@ -57,11 +58,11 @@ def seeds():
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else "build/fuzz/corpus/h2"
-    os.makedirs(out, exist_ok=True)
-    for name, data in seeds():
-        with open(os.path.join(out, "seed_" + name), "wb") as f:
-            f.write(data)
+    for out in sys.argv[1:] or ["build/fuzz/corpus/h2"]:
+        os.makedirs(out, exist_ok=True)
+        for name, data in seeds():
+            with open(os.path.join(out, "seed_" + name), "wb") as f:
+                f.write(data)
 
 
 if __name__ == "__main__":
