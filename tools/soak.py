@@ -61,8 +61,11 @@ def main():
         from k8s_gpu_sharing_plugin_amd import BUILD_DIR
         args += ["--replica-hbm-share", "--enforce-memory-units",
                  "--memcap-lib", os.path.join(BUILD_DIR, "libadp_memcap.so")]
-    dm = harness.Daemon(d, None if a.real else fixtures.node(8), args=args, real_smi=a.real,
-                        env={"ADP_LOG_LEVEL": "warn", "DP_HEALTH_POLL_MS": "200"}).start()
+    env = {"ADP_LOG_LEVEL": "warn", "DP_HEALTH_POLL_MS": "200"}
+    if a.enforce:  # grant accounting files per pod, and the driver-side /proc scan every 100 ms
+        env["DP_DRIVER_HBM_POLL_MS"] = "100"
+    dm = harness.Daemon(d, None if a.real else fixtures.node(8), args=args, real_smi=a.real, env=env).start()
+    driver_polls = None
     samples, pods, hups, kubelet_restarts, scrapes = [], 0, 0, 0, 0
     ok = True
     t_end = time.time() + a.seconds
@@ -98,7 +101,9 @@ def main():
                 reg = kub.wait(lambda e: e.get("event") == "register", 30)
             sock = os.path.join(d, reg["endpoint"])
             with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
-                r.read()
+                for line in r.read().decode().splitlines():
+                    if line.startswith("amdgpu_dp_driver_hbm_polls_total "):
+                        driver_polls = int(line.split()[1])
             scrapes += 1
             if time.time() >= next_sample:
                 s = proc_stats(dm.proc.pid)
@@ -121,7 +126,7 @@ def main():
         "rss_mib_max": max((s["rss_mib"] for s in samples), default=None),
         "fds_after_warmup": warm.get("fds"), "fds_last": last.get("fds"),
         "threads_after_warmup": warm.get("threads"), "threads_last": last.get("threads"),
-        "exit_code": code,
+        "exit_code": code, "driver_hbm_polls": driver_polls,
     }
     if samples and last["rss_mib"] - warm["rss_mib"] > a.max_rss_growth_mib:
         ok = False
