@@ -994,3 +994,24 @@ def test_health_under_device_cgroup_denial(scratch, snap):
                                     env={**os.environ, **env}).stdout)
     assert dry["gpus"][0]["vram_mib"] == snap["gpus"][0]["vram_mib"]  # vram_info fails; the fallback holds
     assert dry["resources"][0]["allocatable"] == 1
+
+
+def test_memcap_grant_holds_under_concurrent_pytorch_churn():
+    """Four PyTorch processes of one container churn random tensors under one
+    8000 MiB daemon grant (tools/memcap_stress_gpu.py): allocations are
+    refused at the cap, and the HBM the amdgpu driver counts for the four
+    (DRM fdinfo, sampled every 20 ms) never exceeds the grant plus the HIP
+    runtime's own per-process allocations."""
+    import json
+    import subprocess
+    import sys
+    from k8s_gpu_sharing_plugin_amd import REPO_ROOT
+    r = subprocess.run([sys.executable, os.path.join(REPO_ROOT, "tools", "memcap_stress_gpu.py"),
+                        "--workers", "4", "--grant-mib", "8000", "--seconds", "20"],
+                       capture_output=True, text=True, timeout=240)
+    res = json.loads(r.stdout.strip().splitlines()[-1]) if r.stdout.strip() else {}
+    os.makedirs("gpurun_out/memcap", exist_ok=True)
+    with open("gpurun_out/memcap/concurrent_stress.json", "w") as f:
+        json.dump(res, f, indent=1)
+    assert r.returncode == 0, (res, r.stderr[-3000:])
+    assert res["held"] and res["refused"] > 0 and res["granted"] > 100, res
