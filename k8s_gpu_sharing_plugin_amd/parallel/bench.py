@@ -105,6 +105,36 @@ def _grpcio_allocate_p50(socket_path, device=None, calls=300):
         return None
 
 
+def _cpu_group(cpu, rel):
+    """First CPU of `cpu`'s sysfs group (cache/index3/shared_cpu_list: its L3;
+    topology/thread_siblings_list: its core), -1 if unknown."""
+    try:
+        with open(f"/sys/devices/system/cpu/cpu{cpu}/{rel}") as f:
+            first = f.read().strip().split(",")[0]
+        return int(first.split("-")[0])
+    except (OSError, ValueError):
+        return -1
+
+
+def _placement(client_cpus, loops_before, loops_after):
+    """Where the timed client and the gRPC loop that served it ran (diagnosis
+    of the run's latency mode): the client's CPUs, the loop busiest during the
+    timed region (busy-iteration counts before/after it) and its last CPU, and
+    whether the two shared a core, an L3, or neither."""
+    cpus = {int(c): n for c, n in (client_cpus or {}).items()}
+    before = [b for _, b in (loops_before or [])]
+    loops = [(c, b - (before[i] if i < len(before) else 0)) for i, (c, b) in enumerate(loops_after or [])]
+    out = {"client_cpus": cpus, "loops_during_timed": loops}
+    if cpus and loops and max(b for _, b in loops) > 0:
+        client = max(cpus, key=cpus.get)
+        loop = max(loops, key=lambda x: x[1])[0]
+        same_core = _cpu_group(client, "topology/thread_siblings_list") == _cpu_group(loop, "topology/thread_siblings_list")
+        same_l3 = _cpu_group(client, "cache/index3/shared_cpu_list") == _cpu_group(loop, "cache/index3/shared_cpu_list")
+        out.update({"client_cpu": client, "busiest_loop_cpu": loop,
+                    "relation": "same-core" if same_core else "same-l3" if same_l3 else "other-l3"})
+    return out
+
+
 def _grpc_go_shaped(socket_path, pod_size, rank, world, warm, pods, owned=None):
     """Allocate / GetPreferredAllocation latency with the client frame pattern of
     the kubelet's grpc-go transport (grpc::Channel::EmulateGrpcGo): what the
@@ -118,7 +148,7 @@ def _grpc_go_shaped(socket_path, pod_size, rank, world, warm, pods, owned=None):
         s = c.stats()
         c.close()
         return {"pods": s["pods"], "bdp_pings": s["bdp_pings"], "allocate": s["allocate"],
-                "preferred": s["preferred"]}
+                "preferred": s["preferred"], "cpus": s.get("cpus")}
     except Exception as e:  # reported, not fatal for the headline
         return {"error": str(e)}
 
@@ -294,6 +324,9 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
         client.run(max(1, warmup) * pods_per_step, record=False)
         client.reset()
 
+        # (1 rank: the loops' placement counters before the timed region, to
+        # find the loop that serves it; outside the timing)
+        loops_before = _server_stats(daemon).get("loop_cpus") if world == 1 else None
         if use_dist:
             dist.barrier()
         sync(torch)
@@ -304,6 +337,7 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
         if use_dist:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        loops_after = _server_stats(daemon).get("loop_cpus") if world == 1 else None
         stats = client.stats()
         stats["elapsed_s"] = elapsed
         client.close()
@@ -395,9 +429,13 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                               "rank_bdf": s.get("rank_bdf"),
                               "admitted_bdfs": s.get("admitted_bdfs"), "probe_bdf": s.get("probe_bdf"),
                               "grpcio_allocate_p50_us": s.get("grpcio_allocate_p50_us"),
-                              "grpc_go_shaped": s.get("grpc_go_shaped")}
+                              "grpc_go_shaped": s.get("grpc_go_shaped"),
+                              "client_cpus": s.get("cpus")}
                              for s in everyone],
             }
+            # CPU placement of the timed client vs the gRPC loops (1 rank: directly comparable).
+            if world == 1:
+                result["placement"] = _placement(everyone[0].get("cpus"), loops_before, loops_after)
             # The node the daemon served, and a k-GPU pod's placement on it.
             result["topology"] = info.get("topology")
             result["preferred_k"] = info.get("preferred_k")

@@ -1,5 +1,7 @@
 #include "bench/churn.h"
 
+#include <sched.h>
+
 #include "alloc/replicas.h"
 #include "common/strings.h"
 
@@ -84,6 +86,7 @@ void ChurnClient::ResetStats() {
   pod_us_.clear();
   run_seconds_ = 0;
   run_pods_ = 0;
+  cpus_.clear();
 }
 
 Status ChurnClient::Run(int pods, bool record) {
@@ -140,6 +143,7 @@ Status ChurnClient::Run(int pods, bool record) {
       pod_us_.push_back(Us(p0, a1));
     }
     live_.push_back(std::move(chosen));
+    if (record && (i & 63) == 0) ++cpus_[sched_getcpu()];
   }
   if (record) {
     run_seconds_ += std::chrono::duration<double>(Clock::now() - t_run).count();
@@ -161,7 +165,10 @@ std::string ChurnClient::StatsJson() const {
   for (size_t i = 0; i < mine_ids_.size() && i < 64; ++i)
     ids += (i ? ", \"" : "\"") + JsonEscape(mine_ids_[i]) + "\"";
   ids += "], ";
-  return std::string(head) + ids + ToJson("allocate", Summarize(alloc_us_)) + ", " +
+  std::string cpus = "\"cpus\": {";
+  for (const auto& [cpu, n] : cpus_) cpus += (cpus.size() > 9 ? ", \"" : "\"") + std::to_string(cpu) + "\": " + std::to_string(n);
+  cpus += "}, ";
+  return std::string(head) + ids + cpus + ToJson("allocate", Summarize(alloc_us_)) + ", " +
          ToJson("preferred", Summarize(pref_us_)) + ", " + ToJson("pod", Summarize(pod_us_)) + "}";
 }
 

@@ -9,6 +9,7 @@
 // kubelet talks to a plugin.
 #pragma once
 
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -63,6 +64,7 @@ class ChurnClient {
   std::vector<double> alloc_us_, pref_us_, pod_us_;
   double run_seconds_ = 0;
   size_t run_pods_ = 0;
+  std::map<int, int> cpus_;  // CPU this client ran on, sampled every 64 recorded pods
 };
 
 }  // namespace adp::bench

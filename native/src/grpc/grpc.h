@@ -131,6 +131,8 @@ class Server {
   void PostAll(std::function<void(int loop)> fn);
   int loops() const { return static_cast<int>(loops_.size()); }
   bool OnLoopThread() const;
+  // Per loop: the CPU it last served from (-1 = never) and its busy iterations.
+  std::vector<std::pair<int, uint64_t>> LoopPlacement() const;
   const std::string& socket_path() const { return socket_path_; }
   const ServerStats& stats() const { return stats_; }
   // Log every unary call (method, status, sizes, handler time). Set before Start().

@@ -463,6 +463,11 @@ struct Server::Loop {
   int follow_l3 = -1;
   std::chrono::steady_clock::time_point next_follow_check{};
   std::map<int, int> peer_pid;  // fd -> visible peer pid (connections that may be followed)
+  // Placement report (LoopPlacement): the CPU the loop ran on when it last
+  // served something (sampled every 256 busy iterations) and how many busy
+  // iterations it has had.
+  std::atomic<int> cpu{-1};
+  std::atomic<uint64_t> busy{0};
 };
 
 Server::Server(std::string name, int threads) : name_(std::move(name)) {
@@ -583,6 +588,13 @@ void Server::PostAll(std::function<void(int)> fn) {
     int i = l->index;
     PostTo(*l, [fn, i] { fn(i); });
   }
+}
+
+std::vector<std::pair<int, uint64_t>> Server::LoopPlacement() const {
+  std::vector<std::pair<int, uint64_t>> out;
+  for (const auto& l : loops_)
+    out.emplace_back(l->cpu.load(std::memory_order_relaxed), l->busy.load(std::memory_order_relaxed));
+  return out;
 }
 
 bool Server::OnLoopThread() const {
@@ -784,6 +796,9 @@ Status Server::RunLoop(Loop& l) {
       if (spinning && Clock::now() >= spin_until) spinning = false;
       continue;
     }
+    uint64_t busy = l.busy.load(std::memory_order_relaxed) + 1;  // this loop is the only writer
+    l.busy.store(busy, std::memory_order_relaxed);
+    if ((busy & 255) == 1) l.cpu.store(sched_getcpu(), std::memory_order_relaxed);
     if (busy_poll_us_ > 0) {
       spinning = true;
       spin_until = Clock::now() + spin;

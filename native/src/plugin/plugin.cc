@@ -913,10 +913,16 @@ std::string Plugin::StatsJson() const {
   uint64_t np = stats_.preferred_calls.Value();
   double pavg = np ? stats_.preferred_ns_total.Value() / 1e3 / np : 0.0;
   int loops = 0;
+  std::string placement = "[";
   {
     std::lock_guard<std::mutex> lk(server_mu_);
-    if (server_) loops = server_->loops();
+    if (server_) {
+      loops = server_->loops();
+      for (const auto& [cpu, busy] : server_->LoopPlacement())
+        placement += (placement.size() > 1 ? ", [" : "[") + std::to_string(cpu) + ", " + std::to_string(busy) + "]";
+    }
   }
+  placement += "]";
   char buf[1280];
   snprintf(buf, sizeof(buf),
            "{\"resource\": \"%s\", \"devices\": %zu, \"advertised\": %zu, \"allocate_calls\": %llu, "
@@ -933,7 +939,9 @@ std::string Plugin::StatsJson() const {
            stats_.allocate_hist.QuantileUs(0.5), stats_.allocate_hist.QuantileUs(0.99),
            stats_.preferred_hist.QuantileUs(0.5), stats_.preferred_hist.QuantileUs(0.99),
            static_cast<unsigned long long>(stats_.unhealthy_allocations.Value()));
-  return buf;
+  std::string out(buf);
+  out.pop_back();  // the closing brace
+  return out + ", \"loop_cpus\": " + placement + "}";
 }
 
 size_t Plugin::healthy_count() const {

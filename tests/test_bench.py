@@ -44,6 +44,12 @@ def test_bench_single_process_contract():
     # restart (whose amdsmi event wait took up to 500 ms to stop)
     kr = res["kubelet_restart"]
     assert kr["rounds"] == 5 and 0 < kr["register_ms"] <= kr["devices_ms"] < 150, kr
+    # where the timed client and the loop that served it ran: exactly one loop
+    # was busy during the timed region (its 300 pods = 600 calls)
+    pl = res["placement"]
+    assert pl["relation"] in ("same-core", "same-l3", "other-l3") and pl["client_cpus"], pl
+    busy = [b for _, b in pl["loops_during_timed"] if b > 0]
+    assert len(busy) == 1 and busy[0] >= 300, pl
 
 
 @pytest.mark.slow

@@ -130,7 +130,7 @@ step_floor() {
 step_spread() {
   for i in $(seq 1 10); do
     timeout -k 10 300 python bench.py --no-probe > $out/spread_$i.json 2> $out/spread_$i.err || die "SPREAD $i" $out/spread_$i.err
-    python -c "import json; d=json.load(open('$out/spread_$i.json')); print('R $i', d['value'], d['allocate_p99_us'], d.get('grpc_go_shaped_allocate_p50_us'), d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'])"
+    python -c "import json; d=json.load(open('$out/spread_$i.json')); p=d.get('placement') or {}; print('R $i', d['value'], d['allocate_p99_us'], d.get('grpc_go_shaped_allocate_p50_us'), d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'], p.get('relation'), p.get('client_cpu'), p.get('busiest_loop_cpu'))"
   done
 }
 step_access() {

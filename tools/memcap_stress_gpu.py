@@ -8,9 +8,9 @@ descriptors, the source of the daemon's driver-side check) every 20 ms.
 
 The grant holds if the driver's sum over the workers never exceeds the grant
 plus the HIP runtime's own per-process allocations (code objects, queues,
-scratch -- never requested through hipMalloc; measured at ~0.1-0.15 GiB per
-process, profiles/r3/driver/driver_usage.json), given as --slack-mib per
-process. Prints one JSON object; exit 1 if the grant was exceeded or no
+scratch -- never requested through hipMalloc), measured per worker after it
+loaded its kernels and before its first tensor, plus --slack-mib per process
+for what the runtime adds later. Prints one JSON object; exit 1 if the grant was exceeded or no
 allocation was ever refused (then the test did not reach the cap).
 
   python tools/memcap_stress_gpu.py [--workers 4] [--grant-mib 8000] [--seconds 30]
@@ -32,6 +32,12 @@ import torch
 seed, seconds = int(sys.argv[1]), float(sys.argv[2])
 rng = random.Random(seed)
 torch.cuda.init()
+w = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")  # load the kernels this loop uses
+w.fill_(1)
+w[:: 1 << 10].fill_(2)
+torch.cuda.synchronize()
+del w
+torch.cuda.empty_cache()
 print("ready", flush=True)
 sys.stdin.readline()  # start together
 held, granted, refused, freed = [], 0, 0, 0
@@ -84,7 +90,7 @@ def main():
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--grant-mib", type=int, default=8000)
     ap.add_argument("--seconds", type=float, default=30)
-    ap.add_argument("--slack-mib", type=int, default=512)
+    ap.add_argument("--slack-mib", type=int, default=64)
     a = ap.parse_args()
     from k8s_gpu_sharing_plugin_amd import BUILD_DIR
     gdir = tempfile.mkdtemp(prefix="adpgrant")
@@ -125,12 +131,13 @@ def main():
                 p.kill()
         for f in glob.glob(f"/dev/shm/adp-memcap-key-{key}-*"):
             os.unlink(f)
-    bound = (a.grant_mib + a.workers * a.slack_mib) << 20
+    bound = (a.grant_mib << 20) + sum(base.values()) + (a.workers * a.slack_mib << 20)
     result.update({
         "driver_samples": samples,
         "driver_peak_mib": round(peak / 1048576, 1),
         "runtime_baseline_mib": {str(k): round(v / 1048576, 1) for k, v in base.items()},
         "bound_mib": bound >> 20,
+        "peak_over_grant_mib": round(peak / 1048576 - a.grant_mib, 1),
         "per_worker": outs,
         "granted": sum(o["granted"] for o in outs),
         "refused": sum(o["refused"] for o in outs),
