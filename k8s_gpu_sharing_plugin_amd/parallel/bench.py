@@ -284,7 +284,8 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
         if rank == 0:
             d = harness.scratch_dir("adpbench")
             kub = harness.NativeKubelet(os.path.join(d, "kubelet.sock")).start()
-            served = None if config == "mixed-gpu4" else rank_bdfs
+            # (ranks on compute partitions of one GPU share its address: served once)
+            served = None if config == "mixed-gpu4" else list(dict.fromkeys(rank_bdfs))
             args = ["--partition-strategy", strategy]
             if served:
                 args += ["--devices", ",".join(served)]
