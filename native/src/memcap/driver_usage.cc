@@ -177,13 +177,16 @@ DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFi
   }
   closedir(d);
 
-  // Attribution: own mapping first, then the cgroup of an attributed process.
+  // Attribution: own mapping first, then the cgroup of an attributed process
+  // -- a container's own cgroup, never the root one ("0::/", "N:ctrl:/") that
+  // every process outside a container shares.
+  auto is_root = [](const std::string& cg) { return cg.size() >= 2 && cg.compare(cg.size() - 2, 2, ":/") == 0; };
   std::map<std::string, std::string> grant_of_cgroup;
   for (auto& h : holders) {
     std::string base = proc_root + "/" + std::to_string(h.pid);
     std::string cg = FirstLine(ReadSmall(base + "/cgroup", 4096));
     std::string grant = GrantFromMaps(base + "/maps", grants);
-    if (!grant.empty() && !cg.empty() && cg != self_cgroup) grant_of_cgroup.emplace(cg, grant);
+    if (!grant.empty() && !cg.empty() && cg != self_cgroup && !is_root(cg)) grant_of_cgroup.emplace(cg, grant);
     for (auto& [bdf, bytes] : h.by_bdf) out.procs.push_back({h.pid, bdf, bytes, cg, grant, false});
   }
   for (auto& p : out.procs) {

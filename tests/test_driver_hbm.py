@@ -136,6 +136,21 @@ def test_driver_counts_attribute_every_process_of_the_container(node):
     assert _value(s, "amdgpu_dp_driver_hbm_unreadable_processes") == 0
 
 
+def test_root_cgroup_is_never_a_container(node):
+    """Processes outside any container share the root cgroup: one of them
+    mapping the grant's file (a host-side tool) must not pull every other host
+    GPU process into the grant."""
+    d, proc, port, host = node
+    key = os.path.basename(host).split(".")[0]
+    proc.process(301, "0::/", vram_mib=500, maps_file=host)   # maps the file itself: attributed
+    proc.process(302, "0::/", vram_mib=4000)                 # another host process: not the grant's
+    s = _scrape_after_poll(port, _polls(port) + 2)
+    lab = dict(allocation=key, bdf=BDF0)
+    assert _value(s, "amdgpu_dp_container_hbm_driver_bytes", **lab) == 500 * MIB
+    assert _value(s, "amdgpu_dp_container_hbm_over_grant", **lab) == 0
+    assert _value(s, "amdgpu_dp_gpu_hbm_unattributed_bytes", bdf=BDF0) == 4000 * MIB
+
+
 def test_over_grant_is_flagged_and_counted_per_transition(node):
     d, proc, port, host = node
     key = os.path.basename(host).split(".")[0]
