@@ -138,7 +138,10 @@ static int OnBeginHeaders(nghttp2_session*, const nghttp2_frame* frame, void* ud
 static int OnHeader(nghttp2_session*, const nghttp2_frame* frame, const uint8_t* name,
                     size_t namelen, const uint8_t* value, size_t valuelen, uint8_t, void* ud) {
   auto* c = static_cast<Nghttp2Conn*>(ud);
-  if (frame->hd.type != NGHTTP2_HEADERS) return 0;
+  // The request's own header block only: a trailer block (HCAT_HEADERS) naming
+  // :path or content-type again must not change the call (found by
+  // native/fuzz/fuzz_h2_diff.cc; the native engine reads the first block only).
+  if (frame->hd.type != NGHTTP2_HEADERS || frame->headers.cat != NGHTTP2_HCAT_REQUEST) return 0;
   StreamState* st = c->Find(frame->hd.stream_id);
   if (!st) return 0;
   std::string_view n(reinterpret_cast<const char*>(name), namelen);

@@ -387,3 +387,21 @@ def test_header_block_split_over_continuation_with_huffman(plugin, engine):
     heads, data = c.finish(1)
     assert status_of(heads) == ("0", None) and b"/dev/kfd" in data
     c.close()
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_request_trailers_do_not_change_the_call(plugin, engine):
+    """A client trailer block (HEADERS + END_STREAM after the DATA) that names
+    :path or content-type again does not re-route or re-type the call: the
+    nghttp2 engine used to take the trailers' :path (found by
+    native/fuzz/fuzz_h2_diff.cc, where the two engines disagreed)."""
+    d, path, ids = plugin(engine)
+    c = GoConn(path)
+    block = c.hp.encode(go_request("Allocate"))
+    trailers = c.hp.encode([(":path", SVC + "NoSuchMethod"), ("content-type", "text/plain")])
+    c.send(frame(HEADERS, END_HEADERS, 1, block), frame(DATA, 0, 1, allocate_msg([ids[0]])),
+           frame(HEADERS, END_HEADERS | END_STREAM, 1, trailers))
+    c.next_sid = 3
+    heads, data = c.finish(1)
+    assert status_of(heads) == ("0", None) and b"/dev/kfd" in data
+    c.close()
