@@ -165,10 +165,25 @@ void CheckAllocate(plugin::Plugin& p, FuzzedDataProvider& in) {
   pb::AllocateResponse out;
   if (!pb::Decode(resp, &out).ok()) Fail("allocate response does not decode");
   if (out.container_responses.size() != req.container_requests.size()) Fail("one response per container");
-  for (const auto& cr : out.container_responses) {
+  for (size_t c = 0; c < out.container_responses.size(); ++c) {
+    const auto& cr = out.container_responses[c];
     bool kfd = std::any_of(cr.devices.begin(), cr.devices.end(),
                            [](const pb::DeviceSpec& d) { return d.container_path == "/dev/kfd"; });
     if (!kfd) Fail("no /dev/kfd in an Allocate response");
+    // Memory units: the grant is 1000 MiB per distinct ID, whatever is repeated.
+    auto mib = std::find_if(cr.envs.begin(), cr.envs.end(),
+                            [](const auto& kv) { return kv.first == "AMD_GPU_MEMORY_LIMIT_MIB"; });
+    if (p.resource_name().find("gpu-mem-gb") != std::string::npos && !req.container_requests[c].empty()) {
+      if (mib == cr.envs.end()) Fail("memory units without AMD_GPU_MEMORY_LIMIT_MIB");
+      std::set<std::string> distinct(req.container_requests[c].begin(), req.container_requests[c].end());
+      uint64_t total = 0;
+      for (size_t b = 0; b <= mib->second.size();) {
+        size_t e = std::min(mib->second.find(',', b), mib->second.size());
+        total += strtoull(mib->second.substr(b, e - b).c_str(), nullptr, 10);
+        b = e + 1;
+      }
+      if (total != 1000 * distinct.size()) Fail("granted MiB != 1000 x distinct memory units");
+    }
   }
 }
 

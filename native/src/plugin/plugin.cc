@@ -386,9 +386,13 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
     // server.go:325); index strategy: enumeration order (server.go:406-411).
     std::sort(us.begin(), us.end());
     if (hbm_grants_) {
-      // Replicas (memory units / HBM shares) granted per device (us is sorted, so runs are contiguous).
+      // Replicas (memory units / HBM shares) granted per device: distinct IDs
+      // only (an ID listed twice is one unit, never twice the HBM).
       units_per.assign(units_.size(), 0);
-      for (int u : us) ++units_per[u];
+      std::vector<std::string_view> distinct(ids.begin(), ids.end());
+      std::sort(distinct.begin(), distinct.end());
+      distinct.erase(std::unique(distinct.begin(), distinct.end()), distinct.end());
+      for (std::string_view id : distinct) ++units_per[advertised_index_.find(id)->second];
     }
     us.erase(std::unique(us.begin(), us.end()), us.end());
     if (unhealthy_units_.load(std::memory_order_relaxed) != 0) {

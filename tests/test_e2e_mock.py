@@ -184,6 +184,9 @@ def test_memory_units_report_granted_hbm(running, scratch):
     assert sorted(order) == sorted(envs["AMD_VISIBLE_DEVICES"].split(","))
     want = {gpu0[0].split("-replica-")[0]: "3000", gpu1[0].split("-replica-")[0]: "2000"}
     assert envs["AMD_GPU_MEMORY_LIMIT_MIB"].split(",") == [want[u] for u in order]
+    # an ID listed twice is one unit: never twice the HBM
+    envs = dict(c.allocate([gpu0[0], gpu0[0], gpu0[1]]).container_responses[0].envs)
+    assert envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "2000"
     c.close()
 
 
