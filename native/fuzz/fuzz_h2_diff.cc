@@ -4,7 +4,10 @@
 // connections survive the input, every call that completed on either (its
 // trailers sent) must have completed on both with the same grpc-status and the
 // same response message bytes. Inputs one engine refuses and the other
-// tolerates are not compared (nghttp2 validates more of HTTP messaging).
+// tolerates are not compared (nghttp2 validates more of HTTP messaging), nor
+// are streams either engine reset: a stream error (e.g. a window update past
+// 2^31-1) may land before or after the answer went out, depending on when an
+// engine writes.
 //
 // Seeds: tools/gen_fuzz_seeds.py (shared with fuzz_h2).
 #include <nghttp2/nghttp2.h>
@@ -48,6 +51,7 @@ grpc::Server& Srv() {
 struct Call {
   std::string data;         // DATA payloads, padding removed
   std::string grpc_status;  // from the trailers ("" = not completed)
+  bool reset = false;       // the server reset the stream (RST_STREAM)
 };
 
 struct Outcome {
@@ -70,7 +74,9 @@ void ParseServerBytes(const std::string& out, Outcome* o) {
     if (off + 9 + len > out.size()) break;
     std::string payload = out.substr(off + 9, len);
     off += 9 + len;
-    if (type == 0 /*DATA*/) {
+    if (type == 3 /*RST_STREAM*/) {
+      o->calls[sid].reset = true;
+    } else if (type == 0 /*DATA*/) {
       if (flags & 0x8) {  // PADDED
         if (payload.empty()) continue;
         size_t pad = static_cast<uint8_t>(payload[0]);
@@ -166,8 +172,9 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
   for (const Outcome* x : {&a, &b}) {
     const Outcome* y = x == &a ? &b : &a;
     for (const auto& [sid, call] : x->calls) {
-      if (call.grpc_status.empty()) continue;
+      if (call.grpc_status.empty() || call.reset) continue;
       auto it = y->calls.find(sid);
+      if (it != y->calls.end() && it->second.reset) continue;
       if (it == y->calls.end() || it->second.grpc_status != call.grpc_status || it->second.data != call.data) {
         fprintf(stderr, "engines disagree on stream %u: native status '%s' %zu bytes, nghttp2 status '%s' %zu bytes\n",
                 sid, a.calls[sid].grpc_status.c_str(), a.calls[sid].data.size(), b.calls[sid].grpc_status.c_str(),
