@@ -145,6 +145,9 @@ class Server {
   // Serve each connection from a loop thread on the L3 of the peer process's
   // last CPU (see FollowPeerL3). Set before Start().
   void set_follow_peer_l3(bool on) { follow_peer_l3_ = on; }
+  // Runs on a loop after it has written what its handlers queued (once per
+  // busy iteration): work that must not delay a response. Set before Start().
+  void set_after_flush(std::function<void()> fn) { after_flush_ = std::move(fn); }
 
   // Test hook: make the next iteration of loop 0 fail as if epoll_wait errored.
   void InjectLoopFailureForTest() { inject_failure_.store(true); }
@@ -180,6 +183,7 @@ class Server {
   int busy_poll_us_ = 0;
   bool native_http2_ = true;
   bool follow_peer_l3_ = true;
+  std::function<void()> after_flush_;
   cpu_set_t process_cpus_;  // CPUs the process may run on (at construction)
   ServerStats stats_;
 };

@@ -839,6 +839,7 @@ Status Server::RunLoop(Loop& l) {
       c->epoll_events = want;
     }
     for (int fd : dead) CloseConn(l, fd);
+    if (after_flush_) after_flush_();
   }
   return Status::Ok();
 }

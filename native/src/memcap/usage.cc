@@ -8,6 +8,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -53,14 +54,18 @@ std::vector<uint64_t> Column(const unsigned char* hdr, size_t off, uint32_t n) {
 
 std::string AllocationKey(std::vector<std::string_view> ids) {
   std::sort(ids.begin(), ids.end());
+  return AllocationKeySorted(ids);
+}
+
+std::string AllocationKeySorted(const std::vector<std::string_view>& sorted_ids) {
   uint64_t h = 1469598103934665603ull;  // FNV-1a
-  for (size_t i = 0; i < ids.size(); ++i) {
+  for (size_t i = 0; i < sorted_ids.size(); ++i) {
     if (i) h = (h ^ ',') * 1099511628211ull;
-    for (unsigned char c : ids[i]) h = (h ^ c) * 1099511628211ull;
+    for (unsigned char c : sorted_ids[i]) h = (h ^ c) * 1099511628211ull;
   }
-  char buf[17];
-  snprintf(buf, sizeof(buf), "%016llx", static_cast<unsigned long long>(h));
-  return buf;
+  std::string key(16, '0');
+  for (int i = 15; i >= 0; --i, h >>= 4) key[static_cast<size_t>(i)] = "0123456789abcdef"[h & 15];
+  return key;
 }
 
 Status CreateGrantFile(const std::string& dir, const std::string& key, const std::vector<uint64_t>& cap_bytes,
@@ -116,12 +121,14 @@ struct Writer {
   std::deque<Job> jobs;
   uint64_t queued = 0, done = 0;
   bool warned = false;
+  std::atomic<bool> wake_pending{false};  // a job was queued without waking the writer
 
   Writer() { std::thread([this] { Run(); }).detach(); }
   void Run() {
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      cv.wait(lk, [this] { return !jobs.empty(); });
+      // (bounded wait: a job queued without a wake is picked up in 20 ms at the latest)
+      while (jobs.empty()) cv.wait_for(lk, std::chrono::milliseconds(20));
       Job j = std::move(jobs.front());
       jobs.pop_front();
       lk.unlock();
@@ -146,7 +153,8 @@ constexpr size_t kMaxPending = 4096;
 
 }  // namespace
 
-void CreateGrantFileAsync(std::string dir, std::string key, std::vector<uint64_t> cap_bytes, std::string ids_joined) {
+void CreateGrantFileAsync(std::string dir, std::string key, std::vector<uint64_t> cap_bytes, std::string ids_joined,
+                          bool wake) {
   Writer& w = TheWriter();
   std::lock_guard<std::mutex> lk(w.mu);
   if (w.jobs.size() >= kMaxPending) {  // the filesystem is stuck: the shim falls back to /dev/shm
@@ -159,10 +167,20 @@ void CreateGrantFileAsync(std::string dir, std::string key, std::vector<uint64_t
   }
   w.jobs.push_back({std::move(dir), std::move(key), std::move(ids_joined), std::move(cap_bytes)});
   ++w.queued;
-  w.cv.notify_one();
+  if (wake) w.cv.notify_one();
+  else w.wake_pending.store(true, std::memory_order_release);
+}
+
+void WakeWriter() {
+  Writer& w = TheWriter();
+  // The job was queued under the mutex before the flag was set: the writer's
+  // wait re-checks the queue, so notifying without the lock cannot be missed.
+  if (w.wake_pending.load(std::memory_order_relaxed) && w.wake_pending.exchange(false, std::memory_order_acq_rel))
+    w.cv.notify_one();
 }
 
 bool Flush(int timeout_ms) {
+  WakeWriter();
   Writer& w = TheWriter();
   std::unique_lock<std::mutex> lk(w.mu);
   uint64_t target = w.queued;

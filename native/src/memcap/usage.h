@@ -29,6 +29,8 @@ namespace adp::memcap {
 
 // File name of a grant: FNV-1a of its device IDs, sorted and comma-joined.
 std::string AllocationKey(std::vector<std::string_view> ids);
+// The same for IDs already sorted.
+std::string AllocationKeySorted(const std::vector<std::string_view>& sorted_ids);
 
 // Creates <dir>/<key>.memcap for a grant of `cap_bytes` (one per device, in HIP
 // order) to `ids` (comma-joined), atomically replacing any earlier file of the
@@ -41,7 +43,14 @@ Status CreateGrantFile(const std::string& dir, const std::string& key, const std
 // after the kubelet has the response). Jobs run in order; a failure is logged
 // once per process. Flush() waits (at most `timeout_ms`) until every job
 // queued before it is done; false on timeout.
-void CreateGrantFileAsync(std::string dir, std::string key, std::vector<uint64_t> cap_bytes, std::string ids_joined);
+// With `wake` false the writer thread is not woken here but by the next
+// WakeWriter() -- which the gRPC loops call after writing their responses, so
+// the futex wake of a sleeping writer is off the Allocate() round trip -- or
+// at the latest 20 ms later.
+void CreateGrantFileAsync(std::string dir, std::string key, std::vector<uint64_t> cap_bytes, std::string ids_joined,
+                          bool wake = true);
+// Wakes the writer if a job is waiting for it; one atomic load otherwise.
+void WakeWriter();
 bool Flush(int timeout_ms = 5000);
 
 struct Usage {

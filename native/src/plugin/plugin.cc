@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <charconv>
 #include <cmath>
 #include <tuple>
 #include <set>
@@ -235,6 +236,8 @@ void Plugin::BuildUnits() {
     advertised_index_[advertised_[i]] = advertised_unit_[i];
   }
   if (hbm_grants_ && !opts_.memcap_host_path.empty()) {
+    grant_dir_prefix_ = GrantDir();
+    if (grant_dir_prefix_.empty() || grant_dir_prefix_.back() != '/') grant_dir_prefix_ += '/';
     pb::PutMapEntry(&memcap_bytes_, 1, "LD_PRELOAD", kMemcapContainerPath);
     pb::Mount m{kMemcapContainerPath, opts_.memcap_host_path, true};
     std::string mb;
@@ -362,18 +365,23 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
   std::vector<std::vector<std::string_view>> containers;
   ADP_RETURN_IF_ERROR(pb::DecodeView(req, &containers));
   std::vector<int> us, units_per;
+  // The index entry of each requested ID: one node per advertised ID, so equal
+  // addresses are the same ID (distinct IDs counted without comparing strings).
+  std::vector<const std::pair<const std::string_view, int>*> entries;
   std::vector<std::pair<int, uint32_t>> shares;  // (unit, replica) of CU-partitioned units
   std::string c, joined, cu_mask, mem_mib, mem_frac, mem_devs;
   std::vector<uint64_t> grant_bytes;
   for (const auto& ids : containers) {
     us.clear();
     shares.clear();
+    entries.clear();
     for (std::string_view id : ids) {
       auto it = advertised_index_.find(id);
       if (it == advertised_index_.end())
         return InvalidArgument("invalid allocation request for '" + spec_.resource_name +
                                "': unknown device: " + std::string(id));
       us.push_back(it->second);
+      if (hbm_grants_) entries.push_back(&*it);
       if (!units_[it->second].replica_cus.empty()) {
         // An advertised replica ID ends in "<join><r>" (alloc::ReplicaId).
         uint32_t r = 0, scale = 1;
@@ -389,10 +397,9 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       // Replicas (memory units / HBM shares) granted per device: distinct IDs
       // only (an ID listed twice is one unit, never twice the HBM).
       units_per.assign(units_.size(), 0);
-      std::vector<std::string_view> distinct(ids.begin(), ids.end());
-      std::sort(distinct.begin(), distinct.end());
-      distinct.erase(std::unique(distinct.begin(), distinct.end()), distinct.end());
-      for (std::string_view id : distinct) ++units_per[advertised_index_.find(id)->second];
+      std::sort(entries.begin(), entries.end());
+      entries.erase(std::unique(entries.begin(), entries.end()), entries.end());
+      for (const auto* e : entries) ++units_per[e->second];
     }
     us.erase(std::unique(us.begin(), us.end()), us.end());
     if (unhealthy_units_.load(std::memory_order_relaxed) != 0) {
@@ -513,13 +520,20 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       c += memcap_bytes_;  // the container enforces the grant (empty unless --enforce-memory-units)
       if (!memcap_bytes_.empty()) {
         // The grant itself, read-only: the shim's caps (the env can only lower them).
-        const std::string dir = GrantDir();
+        // Encoded in place (a Mount: container path, host path, read-only).
+        static thread_local std::string gm, cpath, hpath;
         for (size_t i = 0; i < grant_bytes.size(); ++i) {
-          pb::Mount gm{std::string(adp_memcap::kGrantDir) + "/" + std::to_string(i),
-                       PathJoin(dir, GrantFileName(grant_bytes[i] >> 20)), true};
-          std::string gb;
-          pb::Encode(gm, &gb);
-          pb::PutLen(&c, 2, gb);
+          char num[24];
+          cpath.assign(adp_memcap::kGrantDir).push_back('/');
+          cpath.append(num, static_cast<size_t>(std::to_chars(num, num + sizeof(num), i).ptr - num));
+          hpath.assign(grant_dir_prefix_);
+          hpath.append(num, static_cast<size_t>(std::to_chars(num, num + sizeof(num), grant_bytes[i] >> 20).ptr - num));
+          hpath.append(".mib");
+          gm.clear();
+          pb::PutStr(&gm, 1, cpath);
+          pb::PutStr(&gm, 2, hpath);
+          pb::PutBool(&gm, 3, true);
+          pb::PutLen(&c, 2, gm);
         }
       }
       if (!memcap_bytes_.empty() && !opts_.memcap_usage_dir.empty()) AddUsageFile(ids, grant_bytes, &c);
@@ -547,16 +561,22 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
 // either way, only /metrics does not see the container's use.
 void Plugin::AddUsageFile(const std::vector<std::string_view>& ids, const std::vector<uint64_t>& grant_bytes,
                           std::string* c) {
-  std::string key = memcap::AllocationKey(ids);
   std::vector<std::string_view> sorted(ids);
   std::sort(sorted.begin(), sorted.end());
+  std::string key = memcap::AllocationKeySorted(sorted);
+  size_t len = sorted.size();
+  for (std::string_view id : sorted) len += id.size();
   std::string joined;
+  joined.reserve(len);
   for (size_t i = 0; i < sorted.size(); ++i) {
     if (i) joined += ',';
     joined += sorted[i];
   }
-  std::string host = opts_.memcap_usage_dir + "/" + key + ".memcap";
-  memcap::CreateGrantFileAsync(opts_.memcap_usage_dir, std::move(key), grant_bytes, std::move(joined));
+  std::string host;
+  host.reserve(opts_.memcap_usage_dir.size() + 24);
+  host.append(opts_.memcap_usage_dir).append("/").append(key).append(".memcap");
+  memcap::CreateGrantFileAsync(opts_.memcap_usage_dir, std::move(key), grant_bytes, std::move(joined),
+                               /*wake=*/false);  // WakeWriter() after the response is written
   pb::PutMapEntry(c, 1, kMemcapFileEnv, kMemcapUsageContainerPath);
   pb::Mount m{kMemcapUsageContainerPath, std::move(host), false};
   std::string mb;
@@ -751,6 +771,9 @@ Status Plugin::Start(std::function<void()> on_fatal) {
   srv->set_busy_poll_us(spin);
   srv->set_native_http2(opts_.native_http2);
   srv->set_follow_peer_l3(opts_.follow_peer_l3);
+  // Grant accounting files are queued by Allocate(); their writer is woken
+  // once the response is on the wire.
+  if (!memcap_bytes_.empty() && !opts_.memcap_usage_dir.empty()) srv->set_after_flush([] { memcap::WakeWriter(); });
   srv->AddUnary(std::string(kSvc) + "GetDevicePluginOptions",
                 [this](std::string_view q, std::string* r) { return HandleGetOptions(q, r); });
   srv->AddUnary(std::string(kSvc) + "Allocate",

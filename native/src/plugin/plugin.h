@@ -293,6 +293,7 @@ class Plugin {
   std::unordered_map<std::string_view, int> advertised_index_;
   std::string kfd_spec_bytes_;
   std::string memcap_bytes_;  // pre-encoded LD_PRELOAD env + shim mount (--enforce-memory-units)
+  std::string grant_dir_prefix_;  // GrantDir() + "/": host paths of the read-only grant files
   alloc::DeviceGraph graph_;
   // Memoised best-effort answers for <= 8 whole devices (see CachedBestEffort),
   // in anonymous zero-filled pages (an all-zero atomic<uint16_t> is "empty").

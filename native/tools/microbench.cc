@@ -3,6 +3,8 @@
 // rebuild for the node shapes of BASELINE.json. Prints one JSON object.
 //
 // usage: adp_microbench [iterations]
+#include <stdlib.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -38,6 +40,8 @@ int main(int argc, char** argv) {
     const char* rc;
     alloc::ReplicaPolicy pol;
     int k;
+    bool enforce = false;  // --enforce-memory-units (the shim mount + read-only grant files)
+    bool usage_files = false;  // ... + grant accounting files (written to a scratch dir)
   };
   std::vector<Case> cases = {
       {"spx8_none", 8, 1, strategy::PartitionStrategy::kNone, "", alloc::ReplicaPolicy::kSpread, 1},
@@ -46,7 +50,13 @@ int main(int argc, char** argv) {
       {"cpx64_single_k4", 8, 8, strategy::PartitionStrategy::kSingle, "", alloc::ReplicaPolicy::kSpread, 4},
       {"automem2352_spread_k1", 8, 1, strategy::PartitionStrategy::kNone, "gpu:gpu-mem-gb:-1", alloc::ReplicaPolicy::kSpread, 1},
       {"automem2352_pack_k36", 8, 1, strategy::PartitionStrategy::kNone, "gpu:gpu-mem-gb:-1", alloc::ReplicaPolicy::kPack, 36},
+      {"automem2352_enforced_k1", 8, 1, strategy::PartitionStrategy::kNone, "gpu:gpu-mem-gb:-1", alloc::ReplicaPolicy::kPack, 1,
+       true},
+      {"automem2352_enforced_usage_k1", 8, 1, strategy::PartitionStrategy::kNone, "gpu:gpu-mem-gb:-1",
+       alloc::ReplicaPolicy::kPack, 1, true, true},
   };
+  char scratch[] = "/tmp/adp-microbench-XXXXXX";
+  std::string usage_dir = std::string(mkdtemp(scratch)) + "/usage";
   printf("{");
   bool first = true;
   for (const auto& c : cases) {
@@ -56,6 +66,10 @@ int main(int argc, char** argv) {
     plugin::PluginOptions po;
     po.register_with_kubelet = false;
     po.replica_policy = c.pol;
+    if (c.enforce) {
+      po.memcap_host_path = "/nonexistent/libadp_memcap.so";  // only named in the responses
+      if (c.usage_files) po.memcap_usage_dir = usage_dir;
+    }
     plugin::Plugin p(snap, (*specs)[0], po);
     const auto& ids = p.advertised_ids();
     // GetPreferredAllocation with every advertised device free (a fresh node).
