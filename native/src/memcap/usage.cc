@@ -127,8 +127,9 @@ struct Writer {
   void Run() {
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      // (bounded wait: a job queued without a wake is picked up in 20 ms at the latest)
-      while (jobs.empty()) cv.wait_for(lk, std::chrono::milliseconds(20));
+      // (bounded wait: a job queued without a wake is picked up in 20 ms at the
+      // latest; system_clock, see Flush())
+      while (jobs.empty()) cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(20));
       Job j = std::move(jobs.front());
       jobs.pop_front();
       lk.unlock();
