@@ -5,9 +5,9 @@
 // trailers sent) must have completed on both with the same grpc-status and the
 // same response message bytes. Inputs one engine refuses and the other
 // tolerates are not compared (nghttp2 validates more of HTTP messaging), nor
-// are streams either engine reset: a stream error (e.g. a window update past
-// 2^31-1) may land before or after the answer went out, depending on when an
-// engine writes.
+// are streams either side reset: a stream error (e.g. a window update past
+// 2^31-1) or the client's RST_STREAM may land before or after the answer went
+// out, depending on when an engine writes.
 //
 // Seeds: tools/gen_fuzz_seeds.py (shared with fuzz_h2).
 #include <nghttp2/nghttp2.h>
@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <memory>
 #include <string>
 
@@ -119,6 +120,20 @@ void ParseServerBytes(const std::string& out, Outcome* o) {
   nghttp2_hd_inflate_del(inf);
 }
 
+// Streams the client itself reset (RST_STREAM in its bytes, read frame by
+// frame as far as they parse): whether an answer went out first is timing.
+std::set<uint32_t> ClientResets(const std::string& in, size_t preface) {
+  std::set<uint32_t> out;
+  for (size_t off = preface; off + 9 <= in.size();) {
+    const auto* h = reinterpret_cast<const uint8_t*>(in.data() + off);
+    size_t len = (size_t{h[0]} << 16) | (size_t{h[1]} << 8) | h[2];
+    uint32_t sid = ((uint32_t{h[5]} << 24) | (uint32_t{h[6]} << 16) | (uint32_t{h[7]} << 8) | h[8]) & 0x7fffffffu;
+    if (h[3] == 3 /*RST_STREAM*/) out.insert(sid);
+    off += 9 + len;
+  }
+  return out;
+}
+
 Outcome Run(bool native, const std::string& in, size_t chunk) {
   Outcome o;
   int sv[2];
@@ -169,10 +184,11 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         fprintf(stderr, "%s alive=%d stream %u status '%s' %zu bytes\n", x == &a ? "native" : "nghttp2", x->alive,
                 sid, call.grpc_status.c_str(), call.data.size());
   if (!a.alive || !b.alive) return 0;
+  const std::set<uint32_t> client_reset = ClientResets(in, sizeof(kPreface) - 1 - 9);
   for (const Outcome* x : {&a, &b}) {
     const Outcome* y = x == &a ? &b : &a;
     for (const auto& [sid, call] : x->calls) {
-      if (call.grpc_status.empty() || call.reset) continue;
+      if (call.grpc_status.empty() || call.reset || client_reset.count(sid)) continue;
       auto it = y->calls.find(sid);
       if (it != y->calls.end() && it->second.reset) continue;
       if (it == y->calls.end() || it->second.grpc_status != call.grpc_status || it->second.data != call.data) {
