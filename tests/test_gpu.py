@@ -1001,17 +1001,19 @@ def test_memcap_grant_holds_under_concurrent_pytorch_churn():
     8000 MiB daemon grant (tools/memcap_stress_gpu.py): allocations are
     refused at the cap, and the HBM the amdgpu driver counts for the four
     (DRM fdinfo, sampled every 20 ms) never exceeds the grant plus the HIP
-    runtime's own per-process allocations."""
+    runtime's own per-process allocations (and frees the driver has not
+    finished); the same churn without the shim does."""
     import json
     import subprocess
     import sys
     from k8s_gpu_sharing_plugin_amd import REPO_ROOT
     r = subprocess.run([sys.executable, os.path.join(REPO_ROOT, "tools", "memcap_stress_gpu.py"),
-                        "--workers", "4", "--grant-mib", "8000", "--seconds", "20"],
-                       capture_output=True, text=True, timeout=240)
+                        "--workers", "4", "--grant-mib", "8000", "--seconds", "15", "--compare-uncapped"],
+                       capture_output=True, text=True, timeout=280)
     res = json.loads(r.stdout.strip().splitlines()[-1]) if r.stdout.strip() else {}
     os.makedirs("gpurun_out/memcap", exist_ok=True)
     with open("gpurun_out/memcap/concurrent_stress.json", "w") as f:
         json.dump(res, f, indent=1)
     assert r.returncode == 0, (res, r.stderr[-3000:])
     assert res["held"] and res["refused"] > 0 and res["granted"] > 100, res
+    assert res["uncapped_peak_mib"] > res["bound_mib"], res  # without the shim the same churn passes the bound

@@ -10,7 +10,10 @@ The grant holds if the driver's sum over the workers never exceeds the grant
 plus the HIP runtime's own per-process allocations (code objects, queues,
 scratch -- never requested through hipMalloc), measured per worker after it
 loaded its kernels and before its first tensor, plus --slack-mib per process
-for what the runtime adds later. Prints one JSON object; exit 1 if the grant was exceeded or no
+for what the runtime adds later and for blocks PyTorch freed (the shim gives
+their bytes back at hipFree) that the driver has not released yet: on a
+refusal PyTorch empties its cache and retries at once. --compare-uncapped runs
+the same churn without the shim, whose peak must pass that bound. Prints one JSON object; exit 1 if the grant was exceeded or no
 allocation was ever refused (then the test did not reach the cap).
 
   python tools/memcap_stress_gpu.py [--workers 4] [--grant-mib 8000] [--seconds 30]
@@ -85,25 +88,11 @@ def driver_bytes(pid):
     return total
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--workers", type=int, default=4)
-    ap.add_argument("--grant-mib", type=int, default=8000)
-    ap.add_argument("--seconds", type=float, default=30)
-    ap.add_argument("--slack-mib", type=int, default=64)
-    a = ap.parse_args()
-    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
-    gdir = tempfile.mkdtemp(prefix="adpgrant")
-    with open(os.path.join(gdir, "0"), "w") as f:
-        f.write(f"{a.grant_mib}\n")
-    os.chmod(os.path.join(gdir, "0"), 0o444)
-    key = f"stress-{os.getpid()}"
-    preload = " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), os.path.join(BUILD_DIR, "libadp_memcap.so")) if x)
-    env = {**os.environ, "LD_PRELOAD": preload, "ADP_MEMCAP_GRANT_DIR": gdir, "ADP_MEMCAP_KEY": key}
-    env.pop("AMD_GPU_MEMORY_LIMIT_MIB", None)
+def run_workers(a, env):
+    """Starts the workers, samples the driver's count for them while they
+    churn; returns (peak bytes, runtime baseline per pid, worker results, samples)."""
     procs = [subprocess.Popen([sys.executable, "-c", WORKER, str(i), str(a.seconds)], env=env, stdin=subprocess.PIPE,
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for i in range(a.workers)]
-    result = {"workers": a.workers, "grant_mib": a.grant_mib, "seconds": a.seconds, "slack_mib_per_process": a.slack_mib}
     try:
         for p in procs:
             line = p.stdout.readline().strip()
@@ -125,10 +114,35 @@ def main():
             if p.returncode != 0:
                 raise SystemExit(f"worker exited {p.returncode}: {err[-2000:]}")
             outs.append(json.loads(out.strip().splitlines()[-1]))
+        return peak, base, outs, samples
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--grant-mib", type=int, default=8000)
+    ap.add_argument("--seconds", type=float, default=30)
+    ap.add_argument("--slack-mib", type=int, default=256)
+    ap.add_argument("--compare-uncapped", action="store_true",
+                    help="also run the same workers without the shim (their peak must pass the bound)")
+    a = ap.parse_args()
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    gdir = tempfile.mkdtemp(prefix="adpgrant")
+    with open(os.path.join(gdir, "0"), "w") as f:
+        f.write(f"{a.grant_mib}\n")
+    os.chmod(os.path.join(gdir, "0"), 0o444)
+    key = f"stress-{os.getpid()}"
+    preload = " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), os.path.join(BUILD_DIR, "libadp_memcap.so")) if x)
+    env = {**os.environ, "LD_PRELOAD": preload, "ADP_MEMCAP_GRANT_DIR": gdir, "ADP_MEMCAP_KEY": key}
+    env.pop("AMD_GPU_MEMORY_LIMIT_MIB", None)
+    result = {"workers": a.workers, "grant_mib": a.grant_mib, "seconds": a.seconds, "slack_mib_per_process": a.slack_mib}
+    try:
+        peak, base, outs, samples = run_workers(a, env)
+    finally:
         for f in glob.glob(f"/dev/shm/adp-memcap-key-{key}-*"):
             os.unlink(f)
     bound = (a.grant_mib << 20) + sum(base.values()) + (a.workers * a.slack_mib << 20)
@@ -145,6 +159,12 @@ def main():
     })
     result["held"] = peak <= bound
     result["ok"] = result["held"] and result["refused"] > 0 and result["reported_total_mib"] == [a.grant_mib]
+    if a.compare_uncapped:
+        plain = {k: v for k, v in os.environ.items() if k not in ("AMD_GPU_MEMORY_LIMIT_MIB",)}
+        upeak, _, uouts, _ = run_workers(a, plain)
+        result["uncapped_peak_mib"] = round(upeak / 1048576, 1)
+        result["uncapped_refused"] = sum(o["refused"] for o in uouts)
+        result["ok"] = result["ok"] and upeak > bound  # the same churn does pass the bound without the shim
     print(json.dumps(result), flush=True)
     return 0 if result["ok"] else 1
 
