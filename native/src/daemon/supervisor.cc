@@ -461,6 +461,14 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
               out += "amdgpu_dp_device_node_openable{node=\"" + metrics::LabelValue(a.path) + "\"} " +
                      (a.err ? "0" : "1") + "\n";
           }
+          if (auto events = health_counters.EventCounts(); !events.empty()) {
+            out += "# HELP amdgpu_dp_gpu_events_total amdsmi events per GPU and type, ignored ones included "
+                   "(VMFAULT: an application's GPU page fault; THERMAL_THROTTLE; GPU_PRE_RESET / GPU_POST_RESET).\n"
+                   "# TYPE amdgpu_dp_gpu_events_total counter\n";
+            for (const auto& [k, n] : events)
+              out += "amdgpu_dp_gpu_events_total{bdf=\"" + metrics::LabelValue(k.first) + "\",type=\"" +
+                     metrics::LabelValue(k.second) + "\"} " + std::to_string(n) + "\n";
+          }
           if (auto retired = health_counters.RetiredPages(); !retired.empty()) {
             out += "# HELP amdgpu_dp_retired_pages HBM pages the driver retired (last health poll).\n"
                    "# TYPE amdgpu_dp_retired_pages gauge\n";

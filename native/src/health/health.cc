@@ -103,6 +103,16 @@ std::map<std::string, uint64_t> HealthCounters::VramTotal() const {
   return vram_total_;
 }
 
+void HealthCounters::CountEvent(const std::string& bdf, const std::string& type) {
+  std::lock_guard<std::mutex> lk(mu_);
+  ++events_[{bdf, type}];
+}
+
+std::map<std::pair<std::string, std::string>, uint64_t> HealthCounters::EventCounts() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return events_;
+}
+
 int Monitor::Classify(const HealthConfig& cfg, uint32_t type) {
   if (cfg.ignored.count(type)) return 0;
   if (type == smi::kEvtGpuPostReset) return +1;
@@ -540,6 +550,11 @@ void Monitor::Run() {
         int verdict = Classify(cfg_, e.type);
         LOG_INFO(kComp, "event %s(%u) on GPU %d: %s%s", EventName(e.type), e.type, gpu,
                  e.message.c_str(), verdict == 0 ? " (ignored)" : "");
+        if (gpu >= 0) {
+          const char* name = EventName(e.type);
+          counters_->CountEvent(snap_->gpus[gpu].bdf,
+                                strcmp(name, "EVENT") ? std::string(name) : "EVENT_" + std::to_string(e.type));
+        }
         if (gpu < 0 || verdict == 0) continue;
         std::string why = std::string(EventName(e.type)) + ": " + e.message;
         if (verdict > 0) {

@@ -113,12 +113,18 @@ struct HealthCounters {
   // HBM of each GPU (bytes, from the snapshot; set by the supervisor), next to VramUsed().
   void SetVramTotal(const std::string& bdf, uint64_t bytes);
   std::map<std::string, uint64_t> VramTotal() const;
+  // amdsmi events per GPU (by PCI address) and type name, ignored ones too:
+  // application VM faults and thermal throttling never change health but are
+  // worth watching.
+  void CountEvent(const std::string& bdf, const std::string& type);
+  std::map<std::pair<std::string, std::string>, uint64_t> EventCounts() const;
   std::string Json() const;
 
  private:
   mutable std::mutex mu_;
   std::map<std::string, uint32_t> retired_;
   std::map<std::string, uint64_t> vram_used_, vram_total_;
+  std::map<std::pair<std::string, std::string>, uint64_t> events_;
 };
 
 // Per-GPU health verdicts shared by all Monitor generations of a daemon.

@@ -208,3 +208,31 @@ def test_every_watcher_on_every_loop_sees_each_transition(node):
     for c, _, call in extra:
         call.cancel()
         c.close()
+
+
+def test_events_counted_per_gpu_and_type_on_metrics(node):
+    """Every amdsmi event is counted per GPU and type on /metrics, ignored ones
+    too: an application's VM faults and thermal throttling never change health,
+    but an operator wants to see them (amdgpu_dp_gpu_events_total)."""
+    import re
+    import urllib.request
+    n = node(args=["--metrics-addr", "127.0.0.1:0"])
+    port = int(re.search(r"serving /metrics and /healthz on port (\d+)",
+                         n.d.wait_log("serving /metrics and /healthz on port")).group(1))
+    bdfs = [g["bdf"] for g in fixtures.node(2)["gpus"]]
+    for line in ("1 1 vm fault", "1 1 vm fault", "1 2 thermal", "0 3 pre-reset", "0 4 post-reset"):
+        n.inject(line)
+    want = {(bdfs[1], "VMFAULT"): 2, (bdfs[1], "THERMAL_THROTTLE"): 1, (bdfs[0], "GPU_PRE_RESET"): 1,
+            (bdfs[0], "GPU_POST_RESET"): 1}
+    deadline = time.monotonic() + 5
+    while True:
+        body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+        got = {}
+        for ln in body.splitlines():
+            if ln.startswith("amdgpu_dp_gpu_events_total{"):
+                labels = dict(kv.split("=", 1) for kv in ln[ln.index("{") + 1:ln.index("}")].split(","))
+                got[(labels["bdf"].strip('"'), labels["type"].strip('"'))] = int(ln.split()[-1])
+        if got == want or time.monotonic() > deadline:
+            break
+        time.sleep(0.05)
+    assert got == want, body[-2000:]
