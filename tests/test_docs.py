@@ -27,3 +27,16 @@ def test_docs_link_targets_exist():
             if "*" in path or "{" in path or path.endswith("_") or "nvidia" in path:
                 continue
             assert os.path.exists(os.path.join(REPO_ROOT, path)), f"{doc}: {path}"
+
+
+def test_metrics_reference_lists_every_exported_family():
+    """docs/USER_GUIDE.md "Metrics reference" names every metric family the
+    daemon exports, and nothing it does not."""
+    import glob
+    import re
+    src = "".join(open(f).read() for f in glob.glob(os.path.join(REPO_ROOT, "native", "src", "*", "*.cc")))
+    exported = {n for n in re.findall(r"amdgpu_dp_[a-z0-9_]+", src) if not n.endswith(("_bucket", "_sum", "_count"))}
+    guide = open(os.path.join(REPO_ROOT, "docs", "USER_GUIDE.md")).read()
+    section = guide.split("### Metrics reference", 1)[1].split("\n## ", 1)[0]
+    documented = set(re.findall(r"^\| `(amdgpu_dp_[a-z0-9_]+)`", section, re.M))
+    assert documented == exported, (sorted(exported - documented), sorted(documented - exported))
