@@ -35,7 +35,7 @@
 #                8-rank mock node (AB_RANKS) per mode
 #   cpus         the CPUs this box lets the session use, grouped by L3 / NUMA
 #   curve        tools/mock_curve.sh (CONFIGS="spx-none" for one config)
-#   soak         3 minutes of churn + SIGHUP + kubelet restarts + scrapes on
+#   soak         SOAK_SECONDS (default 180) of churn + SIGHUP + kubelet restarts + scrapes on
 #                real libamd_smi (health polling, state file): RSS/fd/thread leaks
 set -o pipefail
 out=${OUT:-gpurun_out/session}
@@ -176,7 +176,8 @@ step_curve() {
   bash tools/mock_curve.sh $out/curve || die CURVE
 }
 step_soak() {
-  timeout -k 10 400 python -u tools/soak.py --seconds 180 --real ${SOAK_ARGS:-} --out $out/soak.json > $out/soak.log 2>&1 || die SOAK $out/soak.log
+  local secs=${SOAK_SECONDS:-180}
+  timeout -k 10 $((secs + 220)) python -u tools/soak.py --seconds $secs --real ${SOAK_ARGS:-} --out $out/soak.json > $out/soak.log 2>&1 || die SOAK $out/soak.log
   tail -1 $out/soak.log
 }
 
