@@ -320,6 +320,15 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
             owned = sorted(i for i, b in info["bdf_of"].items() if b == my_bdf)
             if not owned:
                 raise SystemExit(f"rank {rank}: the daemon serves no device on {my_bdf}")
+        # Diagnostic (ADP_BENCH_PRE_CLIENT=native|grpc-go): a throw-away churn of
+        # 2000 pods on another connection before the timed client's, to tell
+        # "the first client of a run is slower" from "this client kind is slower".
+        pre = os.environ.get("ADP_BENCH_PRE_CLIENT")
+        if pre:
+            pc = native.ChurnClient(info["socket"], pod_size=POD_SIZE.get(config, 1), rank=rank, world=world,
+                                    owned=owned, grpc_go=pre == "grpc-go")
+            pc.run(2000, record=False)
+            pc.close()
         client = native.ChurnClient(info["socket"], pod_size=POD_SIZE.get(config, 1), rank=rank, world=world,
                                     owned=owned)
         client.run(max(1, warmup) * pods_per_step, record=False)
