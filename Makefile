@@ -77,7 +77,7 @@ tsan-e2e:
 	ADP_BUILD_DIR=$(CURDIR)/build/tsan TSAN_OPTIONS=log_path=$(CURDIR)/build/tsan-logs/daemon \
 	  $(PY) -m pytest -q -p no:cacheprovider tests/test_e2e_mock.py tests/test_health.py \
 	  tests/test_metrics.py tests/test_lifecycle.py tests/test_robustness.py tests/test_h2_native.py \
-	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py -k "not additional_ids and not classification"
+	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py tests/test_preferred.py -k "not additional_ids and not classification and not bruteforce"
 	@if ls build/tsan-logs/* >/dev/null 2>&1; then cat build/tsan-logs/*; exit 1; fi
 
 # The daemon under ASan/UBSan/LSan, driven by the same end-to-end suites.
@@ -108,7 +108,7 @@ asan-e2e:
 	  UBSAN_OPTIONS=print_stacktrace=1:log_path=$(CURDIR)/build/asan-logs/ubsan \
 	  $(PY) -m pytest -q -p no:cacheprovider tests/test_e2e_mock.py tests/test_health.py \
 	  tests/test_metrics.py tests/test_lifecycle.py tests/test_robustness.py tests/test_h2_native.py \
-	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py -k "not additional_ids and not classification"
+	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py tests/test_preferred.py -k "not additional_ids and not classification and not bruteforce"
 	@if ls build/asan-logs/* >/dev/null 2>&1; then cat build/asan-logs/*; exit 1; fi
 
 # Line coverage of native/src from the unit, stress and CPU end-to-end suites.
