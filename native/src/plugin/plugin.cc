@@ -1137,10 +1137,11 @@ std::vector<std::pair<int, uint64_t>> Plugin::GrantedUnits(const std::vector<std
   std::vector<std::pair<int, uint64_t>> out;  // (unit, bytes), sorted by unit = the container's HIP order
   if (!hbm_grants_) return out;
   std::map<int, uint64_t> per;
+  std::set<const void*> seen;  // an ID listed twice grants once (as Allocate counts it)
   for (auto id : ids) {
     auto it = advertised_index_.find(id);
     if (it == advertised_index_.end()) return {};
-    per[it->second] += units_[it->second].grant_mib << 20;
+    if (seen.insert(&*it).second) per[it->second] += units_[it->second].grant_mib << 20;
   }
   out.assign(per.begin(), per.end());
   return out;
