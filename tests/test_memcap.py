@@ -15,7 +15,9 @@ import os
 import subprocess
 import time
 
+import hypothesis
 import pytest
+from hypothesis import strategies as st
 
 from k8s_gpu_sharing_plugin_amd import BUILD_DIR
 from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
@@ -478,3 +480,45 @@ def test_ld_so_preload_list_keeps_the_shim_under_a_pods_own_ld_preload(scratch):
     assert dict(resp.envs)["LD_PRELOAD"] == "/usr/local/lib/amdgpu-dp/libadp_memcap.so"
     resp, _ = _allocate(scratch, "gpu:gpu-mem-gb:-1")  # off by default
     assert "/etc/ld.so.preload" not in {m.container_path for m in resp.mounts}
+
+
+def _model_caps(lim, physical=294912, devices=64):
+    """The shim's reading of AMD_GPU_MEMORY_LIMIT_MIB (strtoull per comma field;
+    only 0 < MiB < 2^43 caps), as MiB per device; None = uncapped."""
+    caps, dev, p = {}, 0, 0
+    while p is not None and p < len(lim) and dev < devices:
+        q = p
+        while q < len(lim) and lim[q] in " \t\n\v\f\r":
+            q += 1
+        neg = q < len(lim) and lim[q] == "-"
+        if q < len(lim) and lim[q] in "+-":
+            q += 1
+        d = q
+        while d < len(lim) and lim[d].isdigit() and lim[d].isascii():
+            d += 1
+        if d > q:
+            v = int(lim[q:d])
+            v = (2 ** 64 - 1) if v >= 2 ** 64 else v
+            if neg and v:
+                v = 2 ** 64 - v
+            if 0 < v < 2 ** 43:
+                caps[dev] = v
+        c = lim.find(",", p)
+        p = c + 1 if c >= 0 else None
+        dev += 1
+    return {k: min(v, physical) for k, v in caps.items()}
+
+
+@hypothesis.settings(max_examples=120, deadline=None, suppress_health_check=list(hypothesis.HealthCheck))
+@hypothesis.given(st.lists(st.one_of(st.integers(0, 400000).map(str), st.sampled_from(["", " 7", "+9", "-5", "-0",
+                                       "1e3", "0x10", "18446744073709551617", "8796093022208", "12abc", " "])),
+                           min_size=0, max_size=4).map(",".join))
+def test_env_caps_parse_like_strtoull(lim):
+    """Whatever the pod's AMD_GPU_MEMORY_LIMIT_MIB holds, the shim never
+    crashes and caps exactly the fields strtoull reads as 0 < MiB < 2^43 (a
+    negative, zero, overflowing or non-numeric field leaves its device
+    uncapped)."""
+    out, _ = _run({"LD_PRELOAD": PRELOAD, "AMD_GPU_MEMORY_LIMIT_MIB": lim})
+    want = _model_caps(lim)
+    assert out["d0 info"]["total_mib"] == want.get(0, 294912), (lim, want)
+    assert out["d1 totalmem value"]["mib"] == want.get(1, 294912), (lim, want)
