@@ -10,6 +10,7 @@ tests/test_gpu.py::test_memcap_caps_torch_allocations.
 """
 
 import glob
+import re
 import json
 import os
 import subprocess
@@ -522,3 +523,37 @@ def test_env_caps_parse_like_strtoull(lim):
     want = _model_caps(lim)
     assert out["d0 info"]["total_mib"] == want.get(0, 294912), (lim, want)
     assert out["d1 totalmem value"]["mib"] == want.get(1, 294912), (lim, want)
+
+
+def _model_grant(contents):
+    """The shim's reading of grant files 0, 1, ...: stops at the first that is
+    not a number followed by nothing or a newline (what follows the newline is
+    not read), with 0 < MiB <= 2^43 (strtoull: leading blanks and a sign are
+    read too)."""
+    caps = {}
+    for i, body in enumerate(contents):
+        m = re.fullmatch(r"[ \t\n\v\f\r]*([+-]?)(\d+)(\n.*)?", body[:31], re.S)
+        if not m:
+            break
+        v = min(int(m.group(2)), 2 ** 64 - 1)
+        if m.group(1) == "-" and v:
+            v = 2 ** 64 - v
+        if v == 0 or v > 2 ** 43:
+            break
+        caps[i] = min(v, 294912)
+    return caps
+
+
+@hypothesis.settings(max_examples=80, deadline=None, suppress_health_check=list(hypothesis.HealthCheck))
+@hypothesis.given(st.lists(st.one_of(st.integers(1, 400000).map(lambda v: f"{v}\n"),
+                                     st.sampled_from(["", "0\n", "12", "12\n\n", "12 ", " 5\n", "-3\n", "x\n",
+                                                      "8796093022209\n", "99999999999999999999\n"])),
+                           min_size=0, max_size=3))
+def test_grant_files_parse_and_stop_at_the_first_bad_one(tmp_path_factory, contents):
+    d = tmp_path_factory.mktemp("g")
+    for i, body in enumerate(contents):
+        (d / str(i)).write_text(body)
+    out, _ = _run({"LD_PRELOAD": PRELOAD, "ADP_MEMCAP_GRANT_DIR": str(d)})
+    want = _model_grant(contents)
+    assert out["d0 info"]["total_mib"] == want.get(0, 294912), (contents, want)
+    assert out["d1 totalmem value"]["mib"] == want.get(1, 294912), (contents, want)
