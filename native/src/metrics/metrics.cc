@@ -97,24 +97,25 @@ double Histogram::QuantileUs(double q) const {
 
 void Histogram::AppendPrometheus(const std::string& name, const std::string& labels,
                                  std::string* out) const {
+  // Appended whole (no fixed line buffer: a truncated line breaks the scrape).
   uint64_t counts[kBuckets + 1];
   Totals(counts);
   uint64_t cum = 0;
-  char line[512];
-  std::string sep = labels.empty() ? "" : ",";
+  std::string head = name + "_bucket{" + labels + (labels.empty() ? "" : ",") + "le=\"";
+  char num[48];
   for (int b = 0; b <= kBuckets; ++b) {
     cum += counts[b];
-    if (b < kBuckets)
-      snprintf(line, sizeof(line), "%s_bucket{%s%sle=\"%g\"} %llu\n", name.c_str(), labels.c_str(),
-               sep.c_str(), kBoundsSec[b], static_cast<unsigned long long>(cum));
-    else
-      snprintf(line, sizeof(line), "%s_bucket{%s%sle=\"+Inf\"} %llu\n", name.c_str(), labels.c_str(),
-               sep.c_str(), static_cast<unsigned long long>(cum));
-    *out += line;
+    *out += head;
+    if (b < kBuckets) {
+      snprintf(num, sizeof(num), "%g", kBoundsSec[b]);
+      *out += num;
+    } else {
+      *out += "+Inf";
+    }
+    *out += "\"} " + std::to_string(cum) + "\n";
   }
-  snprintf(line, sizeof(line), "%s_sum{%s} %.9f\n%s_count{%s} %llu\n", name.c_str(), labels.c_str(),
-           sum_seconds(), name.c_str(), labels.c_str(), static_cast<unsigned long long>(cum));
-  *out += line;
+  snprintf(num, sizeof(num), "%.9f", sum_seconds());
+  *out += name + "_sum{" + labels + "} " + num + "\n" + name + "_count{" + labels + "} " + std::to_string(cum) + "\n";
 }
 
 void Histogram::Reset() {
