@@ -115,6 +115,11 @@ const std::vector<FlagDef>& Table() {
        "print, as JSON, the status of every amdsmi query the plugin uses and whether each device node "
        "opens (what this container's privileges and device cgroup allow) and exit",
        [](Flags& f) -> void* { return &f.smi_report; }},
+      {"doctor", "ADP_DOCTOR", "", Kind::kBool,
+       "check what this deployment needs on this node -- amdsmi, enumeration, resources, device-node "
+       "access, health events, ECC, the kubelet socket, the plugin directory, the HBM-cap shim, the host "
+       "/proc, the CPU budget -- print one line per check with what to change, and exit (1 on a failure)",
+       [](Flags& f) -> void* { return &f.doctor; }},
       {"health-events", "DP_HEALTH_EVENTS", "healthEvents", Kind::kBool,
        "register amdsmi event notification (GPU_PRE_RESET / GPU_POST_RESET: Unhealthy and back); "
        "it needs /dev/kfd, which an unprivileged pod's device cgroup denies (false = polling only)",

@@ -47,6 +47,7 @@ struct Flags {
   bool dry_run = false;
   bool list_grants = false;
   bool smi_report = false;       // print every amdsmi query's status + device-node access, exit
+  bool doctor = false;           // check what a deployment needs on this node, say what to change, exit
   bool health_events = true;     // register amdsmi event notification (needs /dev/kfd access)
   uint64_t driver_hbm_poll_ms = 10000;  // driver-side check of enforced grants (0 = off)
   uint64_t driver_hbm_slack_mib = 512;  // HIP runtime allowance per process in that check

@@ -3,6 +3,7 @@
 #include <errno.h>
 #include <poll.h>
 #include <signal.h>
+#include <fcntl.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/inotify.h>
@@ -299,6 +300,127 @@ void WriteLabels(const std::string& path, const inventory::Snapshot& snap) {
   LOG_INFO(kComp, "wrote node labels to %s", path.c_str());
 }
 
+// --doctor: one line per check -- "ok", "warn" (works, with less) or "FAIL"
+// (the plugin cannot serve) -- and what to change; exit 1 on a failure.
+struct DoctorReport {
+  int ok = 0, warn = 0, fail = 0;
+  void Line(const char* level, const std::string& what) {
+    printf("%-5s %s\n", level, what.c_str());
+    if (!strcmp(level, "ok")) ++ok;
+    else if (!strcmp(level, "warn")) ++warn;
+    else ++fail;
+  }
+  int Finish() {
+    printf("doctor: %d ok, %d warning(s), %d failure(s)\n", ok, warn, fail);
+    fflush(stdout);
+    return fail ? 1 : 0;
+  }
+};
+
+int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorReport& d) {
+  const Flags& f = cfg.flags;
+  d.Line("ok", "amdsmi " + lib->Version() + " (" + lib->path() + ")");
+  auto snap = inventory::BuildSnapshot(lib, v.bopts);
+  if (!snap.ok()) {
+    d.Line("FAIL", "enumeration: " + snap.status().ToString() + " -- is the amdgpu driver loaded, and are the "
+                   "GPUs visible to this container?");
+    return d.Finish();
+  }
+  const auto& s = **snap;
+  if (s.gpus.empty()) {
+    d.Line("FAIL", "enumeration: no GPU" + std::string(f.devices.empty() ? "" : " matches --devices " + f.devices));
+    return d.Finish();
+  }
+  size_t parts = 0;
+  for (const auto& g : s.gpus) parts += g.partitions.size();
+  d.Line("ok", "enumeration: " + std::to_string(s.gpus.size()) + " GPU(s), " + std::to_string(parts) +
+                   " compute partition(s), " + s.gpus[0].compute_mode + "/" + s.gpus[0].memory_mode);
+  auto specs = strategy::BuildPluginSpecs(s, v.partition, v.rc, f.resource_prefix);
+  if (!specs.ok()) {
+    d.Line("FAIL", "partition strategy: " + specs.status().message());
+  } else {
+    std::string what;
+    for (const auto& spec : *specs) {
+      plugin::Plugin p(*snap, spec, v.popts);
+      if (p.device_count() == 0) continue;
+      what += (what.empty() ? "" : ", ") + spec.resource_name + " x" + std::to_string(p.advertised_count());
+    }
+    if (what.empty()) d.Line("FAIL", "resources: none would be advertised (partition strategy / --devices)");
+    else d.Line("ok", "resources: " + what);
+  }
+  auto nodes = inventory::ProbeDeviceAccess(s, f.driver_root);
+  std::string acc = inventory::DescribeAccess(nodes);
+  if (acc == "ok") d.Line("ok", "device nodes: " + std::to_string(nodes.size()) + " openable");
+  else d.Line("warn", "device nodes: " + acc);
+  if (!f.health_events) {
+    d.Line("warn", "health events: off by configuration -- resets are seen by polling only");
+  } else {
+    std::vector<void*> handles;
+    for (const auto& p : s.procs) handles.push_back(p.handle);
+    uint64_t mask = smi::EventMask(smi::kEvtGpuPreReset) | smi::EventMask(smi::kEvtGpuPostReset);
+    Status es = lib->EventsInit(handles, mask);
+    if (es.ok()) {
+      lib->EventsStop(handles);
+      d.Line("ok", "health events: amdsmi event notification registers (GPU_PRE_RESET / GPU_POST_RESET)");
+    } else {
+      int kerr = inventory::KfdAccessErrno(f.driver_root);
+      d.Line("warn", "health events: " + es.ToString() +
+                         (kerr == EPERM ? " -- /dev/kfd denied by the device cgroup: run the plugin privileged "
+                                          "(helm healthEvents: true)"
+                                        : ""));
+    }
+  }
+  size_t ecc_ok = 0;
+  for (const auto& g : s.gpus)
+    if (lib->UncorrectableErrors(s.procs[g.partitions.front().handle].handle).ok()) ++ecc_ok;
+  if (ecc_ok == s.gpus.size()) d.Line("ok", "uncorrectable ECC readable on every GPU");
+  else d.Line("warn", "uncorrectable ECC readable on " + std::to_string(ecc_ok) + " of " +
+                          std::to_string(s.gpus.size()) + " GPU(s): ECC failures are not detected on the others");
+  std::string ksock = v.popts.kubelet_socket.empty() ? PathJoin(f.plugin_dir, "kubelet.sock") : v.popts.kubelet_socket;
+  struct stat st;
+  if (stat(ksock.c_str(), &st) == 0 && S_ISSOCK(st.st_mode)) d.Line("ok", "kubelet socket " + ksock);
+  else d.Line("warn", "kubelet socket " + ksock + " not found -- is the kubelet's device-plugin directory mounted "
+                      "(--device-plugin-path)? The plugin waits for it");
+  std::string probe = PathJoin(f.plugin_dir, ".amdgpu-dp-doctor-" + std::to_string(getpid()));
+  int fd = open(probe.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0600);
+  if (fd >= 0) {
+    close(fd);
+    unlink(probe.c_str());
+    d.Line("ok", "plugin directory " + f.plugin_dir + " writable");
+  } else {
+    d.Line("FAIL", "plugin directory " + f.plugin_dir + " not writable (" + strerror(errno) +
+                       "): the plugin sockets go there");
+  }
+  if (f.enforce_memory_units) {
+    std::string src = MemcapSource(f);
+    if (src.empty()) d.Line("FAIL", "--enforce-memory-units: libadp_memcap.so not found (--memcap-lib)");
+    else d.Line("ok", "HBM-cap shim " + src);
+    if (!f.metrics_addr.empty() && f.driver_hbm_poll_ms > 0) {
+      memcap::DriverScan scan = memcap::ScanDriverHbm(f.host_proc, {}, memcap::SelfCgroup());
+      if (scan.fd_dirs_unreadable == 0)
+        d.Line("ok", "driver-side HBM check: " + std::to_string(scan.pids_scanned) + " processes readable under " +
+                         f.host_proc);
+      else
+        d.Line("warn", "driver-side HBM check: " + std::to_string(scan.fd_dirs_unreadable) + " of " +
+                           std::to_string(scan.pids_scanned) + " processes under " + f.host_proc +
+                           " not readable -- run privileged, with hostPID or the host's /proc at --host-proc");
+    }
+  }
+  if (!f.health_state_file.empty()) {
+    std::string dir = f.health_state_file.substr(0, f.health_state_file.rfind('/'));
+    if (access(dir.empty() ? "/" : dir.c_str(), W_OK) == 0) d.Line("ok", "health state file " + f.health_state_file);
+    else d.Line("warn", "health state file " + f.health_state_file + ": directory not writable -- verdicts will "
+                        "not outlive a container restart");
+  }
+  double budget = plugin::CpuBudget();
+  char b[160];
+  snprintf(b, sizeof(b), "CPU budget %.2f CPUs: %d gRPC loop(s) per socket, busy-poll %s", budget,
+           f.server_threads > 0 ? static_cast<int>(f.server_threads) : plugin::DefaultServerThreads(),
+           budget < 2.0 ? "off (under 2 CPUs)" : "on");
+  d.Line("ok", b);
+  return d.Finish();
+}
+
 void ArmTimer(int tfd, int ms) {
   itimerspec its{};
   its.it_value.tv_sec = ms / 1000;
@@ -330,6 +452,11 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
 
   LOG_INFO(kComp, "loading amdsmi");
   auto lib = smi::Library::Open(cfg.flags.amdsmi_lib);
+  if (!lib.ok() && cfg.flags.doctor) {
+    DoctorReport d;
+    d.Line("FAIL", "amdsmi: " + lib.status().message() + " -- is ROCm's libamd_smi.so in the image (--amdsmi-lib)?");
+    return d.Finish();
+  }
   if (!lib.ok()) {
     LOG_ERROR(kComp, "failed to initialize amdsmi: %s", lib.status().message().c_str());
     LOG_ERROR(kComp, "if this is a GPU node, check that the amdgpu driver is loaded and ROCm's "
@@ -349,6 +476,10 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   LOG_INFO(kComp, "amdsmi %s loaded from %s", (*lib)->Version().c_str(), (*lib)->path().c_str());
   if (cfg.flags.dry_run) return DryRun(lib->get(), v, cfg);
   if (cfg.flags.smi_report) return SmiReport(lib->get(), v, cfg);
+  if (cfg.flags.doctor) {
+    DoctorReport d;
+    return Doctor(lib->get(), v, cfg, d);
+  }
 
   std::string kubelet_sock =
       v.popts.kubelet_socket.empty() ? PathJoin(v.popts.plugin_dir, "kubelet.sock") : v.popts.kubelet_socket;

@@ -1,0 +1,71 @@
+"""`amdgpu-device-plugin --doctor`: what a deployment needs on this node, one
+line per check ("ok" / "warn" / "FAIL") with what to change; exit 1 on a
+failure. Real hardware: tests/test_gpu.py::test_doctor_on_real_gpu."""
+
+import os
+import subprocess
+
+from k8s_gpu_sharing_plugin_amd import DAEMON, MOCK_LIB
+from k8s_gpu_sharing_plugin_amd.models import fixtures
+from k8s_gpu_sharing_plugin_amd.utils import kubelet
+
+
+def _doctor(tmp_path, *args, fx=None, lib=MOCK_LIB):
+    env = dict(os.environ, AMD_SMI_LIB=lib,
+               AMDSMI_MOCK_FIXTURE=fixtures.write(fx or fixtures.node(2), str(tmp_path / "fx")))
+    r = subprocess.run([DAEMON, "--doctor", *args], capture_output=True, text=True, timeout=60, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    return r.returncode, lines
+
+
+def _find(lines, text):
+    return next((ln for ln in lines if text in ln), None)
+
+
+def test_healthy_node_with_a_kubelet(tmp_path):
+    d = tmp_path / "dp"
+    d.mkdir()
+    k = kubelet.StubKubelet(str(d / "kubelet.sock")).start()
+    try:
+        rc, lines = _doctor(tmp_path, "--device-plugin-path", str(d), "--resource-config", "gpu:sharedgpu:4")
+    finally:
+        k.stop()
+    assert rc == 0, lines
+    assert _find(lines, "enumeration: 2 GPU(s)").startswith("ok")
+    assert _find(lines, "resources: amd.com/sharedgpu x8").startswith("ok")
+    assert _find(lines, "kubelet socket").startswith("ok")
+    assert _find(lines, "plugin directory").startswith("ok")
+    assert _find(lines, "health events").startswith("ok")
+    assert _find(lines, "CPU budget").startswith("ok")
+    assert lines[-1].startswith("doctor: ") and "0 failure(s)" in lines[-1]
+    # the mock's render nodes do not exist on this machine: a warning that says so
+    dev = _find(lines, "device nodes")
+    assert dev.startswith("warn") and "not present" in dev
+
+
+def test_missing_kubelet_is_a_warning_and_an_unwritable_plugin_dir_a_failure(tmp_path):
+    rc, lines = _doctor(tmp_path, "--device-plugin-path", "/proc/1")
+    assert rc == 1, lines
+    assert _find(lines, "kubelet socket").startswith("warn")
+    assert _find(lines, "plugin directory /proc/1 not writable").startswith("FAIL")
+    assert "1 failure(s)" in lines[-1]
+
+
+def test_no_amdsmi_is_a_failure_with_a_hint(tmp_path):
+    rc, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), lib="/nonexistent/libamd_smi.so")
+    assert rc == 1 and lines[0].startswith("FAIL") and "libamd_smi.so" in lines[0], lines
+
+
+def test_devices_filter_that_matches_nothing_fails(tmp_path):
+    rc, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), "--devices", "0000:99:00.0")
+    assert rc == 1 and _find(lines, "enumeration").startswith("FAIL"), lines
+
+
+def test_enforced_grants_check_the_shim_and_the_host_proc(tmp_path):
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    rc, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), "--resource-config", "gpu:gpu-mem-gb:-1",
+                        "--enforce-memory-units", "--memcap-lib", os.path.join(BUILD_DIR, "libadp_memcap.so"),
+                        "--metrics-addr", "127.0.0.1:0")
+    assert _find(lines, "HBM-cap shim").startswith("ok"), lines
+    assert _find(lines, "driver-side HBM check") is not None, lines
+    assert _find(lines, "resources: amd.com/gpu-mem-gb x588").startswith("ok")

@@ -1017,3 +1017,26 @@ def test_memcap_grant_holds_under_concurrent_pytorch_churn():
     assert r.returncode == 0, (res, r.stderr[-3000:])
     assert res["held"] and res["refused"] > 0 and res["granted"] > 100, res
     assert res["uncapped_peak_mib"] > res["bound_mib"], res  # without the shim the same churn passes the bound
+
+
+def test_doctor_on_real_gpu(scratch, snap):
+    """`--doctor` on the MI355X with real libamd_smi and a kubelet stub: every
+    check passes -- enumeration, device nodes, amdsmi event registration,
+    uncorrectable ECC, the kubelet socket."""
+    import subprocess
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    try:
+        env = {k_: v for k_, v in os.environ.items() if k_ not in ("AMD_SMI_LIB", "AMDSMI_MOCK_FIXTURE")}
+        r = subprocess.run([harness.DAEMON, "--doctor", "--device-plugin-path", scratch, "--devices", "0"],
+                           capture_output=True, text=True, timeout=120, env=env)
+    finally:
+        k.stop()
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    os.makedirs("gpurun_out/doctor", exist_ok=True)
+    with open("gpurun_out/doctor/doctor_real.txt", "w") as f:
+        f.write(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    by = {ln.split(None, 1)[1].split(":")[0].split(" ")[0]: ln.split(None, 1)[0] for ln in lines[:-1]}
+    assert lines[-1].startswith("doctor:") and "0 failure(s)" in lines[-1]
+    for check in ("enumeration", "device", "health", "uncorrectable", "kubelet"):
+        assert by.get(check) == "ok", (check, r.stdout)
