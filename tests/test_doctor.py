@@ -69,3 +69,19 @@ def test_enforced_grants_check_the_shim_and_the_host_proc(tmp_path):
     assert _find(lines, "HBM-cap shim").startswith("ok"), lines
     assert _find(lines, "driver-side HBM check") is not None, lines
     assert _find(lines, "resources: amd.com/gpu-mem-gb x588").startswith("ok")
+
+
+def test_device_cgroup_denial_is_named(tmp_path):
+    """Under a device cgroup that denies /dev/kfd and /dev/dri/* (the EPERM
+    libadp_devcgroup_sim.so injects) the device-node check warns, names the
+    cause and the fix, and the node can still serve (exit 0)."""
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    sim = os.path.join(BUILD_DIR, "libadp_devcgroup_sim.so")
+    env = dict(os.environ, LD_PRELOAD=" ".join(x for x in (os.environ.get("LD_PRELOAD", ""), sim) if x),
+               AMD_SMI_LIB=MOCK_LIB, AMDSMI_MOCK_FIXTURE=fixtures.write(fixtures.node(2), str(tmp_path / "fx")))
+    r = subprocess.run([DAEMON, "--doctor", "--device-plugin-path", str(tmp_path)], capture_output=True, text=True,
+                       timeout=60, env=env)
+    lines = r.stdout.splitlines()
+    dev = _find(lines, "device nodes")
+    assert r.returncode == 0 and dev.startswith("warn"), r.stdout
+    assert "Operation not permitted" in dev and "device cgroup" in dev and "privileged" in dev

@@ -1040,3 +1040,29 @@ def test_doctor_on_real_gpu(scratch, snap):
     assert lines[-1].startswith("doctor:") and "0 failure(s)" in lines[-1]
     for check in ("enumeration", "device", "health", "uncorrectable", "kubelet"):
         assert by.get(check) == "ok", (check, r.stdout)
+
+
+def test_doctor_under_device_cgroup_denial(scratch, snap):
+    """`--doctor` in a pod whose device cgroup denies /dev/kfd and the render
+    nodes (libadp_devcgroup_sim.so): enumeration and ECC still pass, the
+    device-node and event checks warn and name the cause and the fix."""
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+    sim = os.path.join(BUILD_DIR, "libadp_devcgroup_sim.so")
+    env = {k_: v for k_, v in os.environ.items() if k_ not in ("AMD_SMI_LIB", "AMDSMI_MOCK_FIXTURE")}
+    env["LD_PRELOAD"] = _with_preload(sim)
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    try:
+        r = subprocess.run([harness.DAEMON, "--doctor", "--device-plugin-path", scratch, "--devices", "0"],
+                           capture_output=True, text=True, timeout=120, env=env)
+    finally:
+        k.stop()
+    os.makedirs("gpurun_out/doctor", exist_ok=True)
+    with open("gpurun_out/doctor/doctor_denied.txt", "w") as f:
+        f.write(r.stdout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]  # warnings, no failure: the plugin can serve
+    get = lambda word: next(ln for ln in lines if ln.split(None, 1)[1].startswith(word))
+    assert get("enumeration").startswith("ok") and get("uncorrectable").startswith("ok")
+    assert get("device nodes").startswith("warn") and "device cgroup" in get("device nodes")
+    assert get("health events").startswith("warn") and "privileged" in get("health events")
