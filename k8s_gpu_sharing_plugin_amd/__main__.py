@@ -7,13 +7,16 @@
                                                           # probe every visible GPU
   python -m k8s_gpu_sharing_plugin_amd bench [bench.py flags...]
   python -m k8s_gpu_sharing_plugin_amd hbm [daemon flags...]  # HBM use of enforced grants
+  python -m k8s_gpu_sharing_plugin_amd doctor [daemon flags...]
+                                                          # deployment checks, what to change
 
 `report` runs `amdgpu-device-plugin --dry-run` (real libamd_smi unless
 AMD_SMI_LIB points elsewhere) and prints a table; `validate` runs
 `amdgpu-dp-probe`; `bench` is the headline benchmark (see bench.py); `hbm`
 runs `amdgpu-device-plugin --list-grants` (the accounting files of
 --enforce-memory-units with /metrics under <device-plugin dir>/amdgpu-dp/usage)
-and prints a table.
+and prints a table; `doctor` runs `amdgpu-device-plugin --doctor` (exit 1 on a
+failure).
 """
 
 import json
@@ -81,6 +84,8 @@ def main(argv=None) -> int:
         return _validate(rest)
     if cmd == "hbm":
         return _hbm(rest)
+    if cmd == "doctor":
+        return subprocess.run([DAEMON, "--doctor", *rest]).returncode
     if cmd == "bench":
         from .parallel import bench
         bench.main(rest)

@@ -85,3 +85,12 @@ def test_device_cgroup_denial_is_named(tmp_path):
     dev = _find(lines, "device nodes")
     assert r.returncode == 0 and dev.startswith("warn"), r.stdout
     assert "Operation not permitted" in dev and "device cgroup" in dev and "privileged" in dev
+
+
+def test_python_cli_doctor(tmp_path):
+    import sys
+    env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB,
+               AMDSMI_MOCK_FIXTURE=fixtures.write(fixtures.node(1), str(tmp_path / "fx")))
+    r = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "doctor", "--device-plugin-path",
+                        str(tmp_path)], capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0 and "enumeration: 1 GPU(s)" in r.stdout, r.stdout + r.stderr
