@@ -1066,3 +1066,34 @@ def test_doctor_under_device_cgroup_denial(scratch, snap):
     assert get("enumeration").startswith("ok") and get("uncorrectable").startswith("ok")
     assert get("device nodes").startswith("warn") and "device cgroup" in get("device nodes")
     assert get("health events").startswith("warn") and "privileged" in get("health events")
+
+
+@pytest.mark.parametrize("backend", ["native", "cudaMallocAsync"])
+def test_memcap_with_both_pytorch_allocator_backends(tmp_path, backend):
+    """PyTorch's caching allocator and its hipMallocAsync backend (freed blocks
+    stay in the stream-ordered pool) under a 4000 MiB grant: the grant is the
+    device's memory, a freed 3 GiB comes back, 2 GiB more are refused, and
+    allocate/free churn never fails spuriously."""
+    import json
+    import subprocess
+    import sys
+    from k8s_gpu_sharing_plugin_amd import BUILD_DIR, REPO_ROOT
+    gdir = tmp_path / "grant"
+    gdir.mkdir()
+    (gdir / "0").write_text("4000\n")
+    key = f"gpuasync-{os.getpid()}-{backend}"
+    env = {**os.environ, "PYTORCH_CUDA_ALLOC_CONF": f"backend:{backend}",
+           "LD_PRELOAD": _with_preload(os.path.join(BUILD_DIR, "libadp_memcap.so")),
+           "ADP_MEMCAP_GRANT_DIR": str(gdir), "ADP_MEMCAP_KEY": key}
+    env.pop("AMD_GPU_MEMORY_LIMIT_MIB", None)
+    r = subprocess.run([sys.executable, os.path.join(REPO_ROOT, "tools", "memcap_async_check.py")],
+                       capture_output=True, text=True, timeout=200, env=env)
+    _drop_memcap_segments(key)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    os.makedirs("gpurun_out/memcap", exist_ok=True)
+    with open(f"gpurun_out/memcap/allocator_{backend}.json", "w") as f:
+        json.dump(res, f, indent=1)
+    assert res["backend"] == backend and res["total_mib"] == 4000, res
+    assert res["first_3g"] and res["second_3g_after_free"] and not res["extra_2g_while_holding_3g"], res
+    assert res["churn_500m_ok"] == 200, res
