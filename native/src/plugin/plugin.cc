@@ -950,24 +950,26 @@ std::string Plugin::StatsJson() const {
     }
   }
   placement += "]";
-  char buf[1280];
+  // Only numbers go through the fixed buffer (bounded); the resource name is
+  // appended as a string.
+  char buf[1024];
   snprintf(buf, sizeof(buf),
-           "{\"resource\": \"%s\", \"devices\": %zu, \"advertised\": %zu, \"allocate_calls\": %llu, "
+           "\", \"devices\": %zu, \"advertised\": %zu, \"allocate_calls\": %llu, "
            "\"allocate_handler_avg_us\": %.3f, \"allocate_handler_max_us\": %.3f, "
            "\"preferred_calls\": %llu, \"preferred_handler_avg_us\": %.3f, "
            "\"preferred_handler_max_us\": %.3f, \"law_sends\": %llu, \"law_bytes\": %zu, "
            "\"server_threads\": %d, \"allocate_handler_p50_le_us\": %g, "
            "\"allocate_handler_p99_le_us\": %g, \"preferred_handler_p50_le_us\": %g, "
-           "\"preferred_handler_p99_le_us\": %g, \"unhealthy_allocations\": %llu}",
-           JsonEscape(spec_.resource_name).c_str(), units_.size(), advertised_.size(),
+           "\"preferred_handler_p99_le_us\": %g, \"unhealthy_allocations\": %llu",
+           units_.size(), advertised_.size(),
            static_cast<unsigned long long>(n), avg, stats_.allocate_ns_max.Value() / 1e3,
            static_cast<unsigned long long>(np), pavg, stats_.preferred_ns_max.Value() / 1e3,
            static_cast<unsigned long long>(stats_.law_sends.Value()), law_bytes_size_.load(), loops,
            stats_.allocate_hist.QuantileUs(0.5), stats_.allocate_hist.QuantileUs(0.99),
            stats_.preferred_hist.QuantileUs(0.5), stats_.preferred_hist.QuantileUs(0.99),
            static_cast<unsigned long long>(stats_.unhealthy_allocations.Value()));
-  std::string out(buf);
-  out.pop_back();  // the closing brace
+  std::string out = "{\"resource\": \"" + JsonEscape(spec_.resource_name);
+  out += buf;
   return out + ", \"loop_cpus\": " + placement + "}";
 }
 
