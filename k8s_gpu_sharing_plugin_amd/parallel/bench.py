@@ -105,6 +105,28 @@ def _grpcio_allocate_p50(socket_path, device=None, calls=300):
         return None
 
 
+def _residency(before, after):
+    """The daemon's read -> reply-written time (gRPC loop residency, 100 ns bins
+    from the SIGUSR1 stats) of the unary calls served between two stats
+    snapshots: p50/p99 in us, or None without samples."""
+    if not after or "residency_100ns" not in after:
+        return None
+    b = {k: v for k, v in (before or {}).get("residency_100ns", [])}
+    counts = sorted((k, v - b.get(k, 0)) for k, v in after["residency_100ns"] if v > b.get(k, 0))
+    total = sum(v for _, v in counts)
+    if not total:
+        return None
+
+    def q(x):
+        rank, seen = int(x * (total - 1)) + 1, 0
+        for k, v in counts:
+            seen += v
+            if seen >= rank:
+                return round((k + 1) / 10, 1)
+
+    return {"samples": total, "p50_us": q(0.5), "p99_us": q(0.99)}
+
+
 def _cpu_group(cpu, rel):
     """First CPU of `cpu`'s sysfs group (cache/index3/shared_cpu_list: its L3;
     topology/thread_siblings_list: its core), -1 if unknown."""
@@ -336,7 +358,8 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
 
         # (1 rank: the loops' placement counters before the timed region, to
         # find the loop that serves it; outside the timing)
-        loops_before = _server_stats(daemon).get("loop_cpus") if world == 1 else None
+        st_before = _server_stats(daemon) if world == 1 else {}
+        loops_before = st_before.get("loop_cpus")
         if use_dist:
             dist.barrier()
         sync(torch)
@@ -347,7 +370,8 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
         if use_dist:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-        loops_after = _server_stats(daemon).get("loop_cpus") if world == 1 else None
+        st_timed = _server_stats(daemon) if world == 1 else {}
+        loops_after = st_timed.get("loop_cpus")
         stats = client.stats()
         stats["elapsed_s"] = elapsed
         client.close()
@@ -356,9 +380,11 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
         stats["grpc_go_shaped"] = _grpc_go_shaped(info["socket"], POD_SIZE.get(config, 1), rank, world,
                                                   max(1, warmup) * pods_per_step,
                                                   min(steps * pods_per_step, 2000), owned)
+        st_gg = _server_stats(daemon) if world == 1 else {}
         # ... and every rank times its own device through grpcio.
         stats["grpcio_allocate_p50_us"] = _grpcio_allocate_p50(
             info["socket"], (stats.get("device_ids") or [None])[0])
+        st_grpcio = _server_stats(daemon) if world == 1 else {}
 
         bdf_of = info.get("bdf_of") or {}
         stats["admitted_bdfs"] = sorted({bdf_of.get(i, "?") for i in stats.get("device_ids", [])})
@@ -446,6 +472,17 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
             # CPU placement of the timed client vs the gRPC loops (1 rank: directly comparable).
             if world == 1:
                 result["placement"] = _placement(everyone[0].get("cpus"), loops_before, loops_after)
+            # The daemon's own share of each client's latency: unary calls from the
+            # socket read that carried them to the reply written (the headline and
+            # grpc-go-shaped phases mix Allocate and GetPreferredAllocation; the
+            # grpcio phase is Allocate only). Whatever the client stack costs, this
+            # is what the plugin adds to it.
+            if world == 1:
+                result["server_residency"] = {"native_client": _residency(st_before, st_timed),
+                                              "grpc_go_shaped": _residency(st_timed, st_gg),
+                                              "grpcio": _residency(st_gg, st_grpcio)}
+            else:
+                result["server_residency"] = {"all_calls": _residency({}, server)}
             # The node the daemon served, and a k-GPU pod's placement on it.
             result["topology"] = info.get("topology")
             result["preferred_k"] = info.get("preferred_k")

@@ -101,6 +101,9 @@ struct ServerStats {
   std::atomic<uint64_t> shed_connections{0};  // refused for lack of file descriptors
   metrics::Counter calls;                // per call, from every loop: sharded
   metrics::Counter errors;
+  // Unary calls from the read that carried them to their reply fully written
+  // (the daemon's share of what any client sees, whatever its gRPC stack).
+  metrics::FineHistogram residency;
 };
 
 class Server {

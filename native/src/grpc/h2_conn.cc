@@ -253,6 +253,7 @@ bool H2Conn::Init() {
 
 bool H2Conn::OnReadable() {
   uint8_t buf[64 * 1024];
+  ReadStarted();
   bool eof = false;
   while (!eof) {
     ssize_t n = read(fd_, buf, sizeof(buf));
@@ -739,6 +740,7 @@ void H2Conn::Dispatch(uint32_t sid, H2Stream& st, std::string_view body) {
     return;
   }
   if (st.unary) {
+    Answered();
     std::string& resp = resp_buf_;
     Status s = RunUnary(*st.unary, st.path, req, &resp);
     if (!s.ok()) {
@@ -792,6 +794,7 @@ void H2Conn::Finish(int32_t sid, const Status& s) {
 }
 
 bool H2Conn::Flush() {
+  if (woff_ < wbuf_.size()) Sending();
   while (woff_ < wbuf_.size()) {
     ssize_t n = send(fd_, wbuf_.data() + woff_, wbuf_.size() - woff_, MSG_NOSIGNAL);
     if (n > 0) {

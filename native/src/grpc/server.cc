@@ -223,6 +223,7 @@ bool Nghttp2Conn::Init() {
 
 bool Nghttp2Conn::OnReadable() {
   char buf[64 * 1024];
+  ReadStarted();
   while (true) {
     ssize_t n = read(fd_, buf, sizeof(buf));
     if (n > 0) {
@@ -253,6 +254,7 @@ bool Nghttp2Conn::Flush() {
     if (woff_ == wbuf_.size()) { wbuf_.clear(); woff_ = 0; }
     wbuf_.append(reinterpret_cast<const char*>(data), n);
   }
+  if (woff_ < wbuf_.size()) Sending();
   while (woff_ < wbuf_.size()) {
     ssize_t n = send(fd_, wbuf_.data() + woff_, wbuf_.size() - woff_, MSG_NOSIGNAL);
     if (n > 0) { woff_ += n; continue; }
@@ -260,7 +262,10 @@ bool Nghttp2Conn::Flush() {
     if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
     return false;
   }
-  if (woff_ == wbuf_.size()) { wbuf_.clear(); woff_ = 0; }
+  if (woff_ == wbuf_.size()) {
+    wbuf_.clear();
+    woff_ = 0;
+  }
   return true;
 }
 
@@ -330,6 +335,7 @@ void Nghttp2Conn::Dispatch(int32_t sid) {
     return;
   }
   if (st->unary) {
+    Answered();
     std::string& resp = resp_buf_;  // reused across calls: no allocation once warm
     Status s = RunUnary(*st->unary, st->path, req, &resp);
     st = Find(sid);  // handler cannot erase streams, but be defensive

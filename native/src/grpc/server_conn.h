@@ -7,6 +7,7 @@
 #include <memory>
 #include <string>
 #include <string_view>
+#include <time.h>
 
 #include "grpc/grpc.h"
 
@@ -74,9 +75,35 @@ class ServerConn {
   // Runs a unary handler into *resp (cleared first), logging it when traced.
   Status RunUnary(const UnaryHandler& h, std::string_view path, std::string_view req, std::string* resp);
 
+  // Residency of unary calls in the daemon, from the read that carried them to
+  // their reply handed to send() (ServerStats::residency): the engine calls
+  // ReadStarted() when a readable event starts, Answered() when a unary call
+  // got its reply queued and Sending() before writing the queued bytes. One
+  // sample per batch of calls answered together, from the start of the read
+  // that carried the first of them. The send itself is left out: on a UDS it
+  // wakes the peer inside the syscall, so the client can be running with the
+  // reply before send() returns.
+  static uint64_t MonoNs() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return static_cast<uint64_t>(ts.tv_sec) * 1000000000ull + static_cast<uint64_t>(ts.tv_nsec);
+  }
+  void ReadStarted() { read_ns_ = MonoNs(); }
+  void Answered() {
+    if (!answers_++) batch_ns_ = read_ns_;
+  }
+  void Sending() {
+    if (answers_) {
+      srv_->stats_.residency.Observe(MonoNs() - batch_ns_);
+      answers_ = 0;
+    }
+  }
+
   Server* srv_;
   int loop_;
   int fd_;
+  uint64_t read_ns_ = 0, batch_ns_ = 0;
+  uint32_t answers_ = 0;
 };
 
 std::unique_ptr<ServerConn> MakeH2Conn(Server* srv, int loop, int fd);

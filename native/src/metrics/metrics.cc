@@ -125,6 +125,70 @@ void Histogram::Reset() {
   }
 }
 
+FineHistogram::FineHistogram() : shards_(new Shard[kShards]) {}
+
+void FineHistogram::Observe(uint64_t ns) {
+  uint64_t b = ns / kBinNs;
+  Shard& s = shards_[ShardIndex()];
+  s.bins[b < kBins ? b : kBins].fetch_add(1, std::memory_order_relaxed);
+  s.sum_ns.fetch_add(ns, std::memory_order_relaxed);
+}
+
+std::vector<uint64_t> FineHistogram::Counts() const {
+  std::vector<uint64_t> c(kBins + 1, 0);
+  for (int i = 0; i < kShards; ++i)
+    for (int b = 0; b <= kBins; ++b) c[b] += shards_[i].bins[b].load(std::memory_order_relaxed);
+  return c;
+}
+
+uint64_t FineHistogram::sum_ns() const {
+  uint64_t t = 0;
+  for (int i = 0; i < kShards; ++i) t += shards_[i].sum_ns.load(std::memory_order_relaxed);
+  return t;
+}
+
+double FineHistogram::QuantileUs(const std::vector<uint64_t>& counts, double q) {
+  uint64_t total = 0;
+  for (uint64_t c : counts) total += c;
+  if (total == 0) return 0.0;
+  uint64_t rank = static_cast<uint64_t>(q * static_cast<double>(total - 1)) + 1, seen = 0;
+  for (size_t b = 0; b < counts.size(); ++b) {
+    seen += counts[b];
+    if (seen >= rank) return static_cast<double>((b + 1) * kBinNs) / 1e3;
+  }
+  return static_cast<double>(counts.size() * kBinNs) / 1e3;
+}
+
+std::string FineHistogram::SparseJson() const {
+  std::vector<uint64_t> c = Counts();
+  std::string out = "[";
+  for (size_t b = 0; b < c.size(); ++b) {
+    if (!c[b]) continue;
+    if (out.size() > 1) out += ", ";
+    out += "[" + std::to_string(b) + ", " + std::to_string(c[b]) + "]";
+  }
+  return out + "]";
+}
+
+void FineHistogram::AppendPrometheus(const std::string& name, const std::string& labels, std::string* out) const {
+  std::vector<uint64_t> c = Counts();
+  static const double kLe[] = {1e-6, 2e-6, 5e-6, 10e-6, 20e-6, 50e-6, 100e-6};
+  std::string head = name + "_bucket{" + labels + (labels.empty() ? "" : ",") + "le=\"";
+  uint64_t cum = 0;
+  size_t b = 0;
+  char num[48];
+  for (double le : kLe) {
+    // bins entirely below the bound (bin b ends at (b+1) x 100 ns)
+    for (; b < kBins && (b + 1) * kBinNs <= static_cast<uint64_t>(le * 1e9 + 0.5); ++b) cum += c[b];
+    snprintf(num, sizeof(num), "%g", le);
+    *out += head + num + "\"} " + std::to_string(cum) + "\n";
+  }
+  for (; b <= kBins; ++b) cum += c[b];
+  *out += head + "+Inf\"} " + std::to_string(cum) + "\n";
+  snprintf(num, sizeof(num), "%.9f", sum_ns() / 1e9);
+  *out += name + "_sum{" + labels + "} " + num + "\n" + name + "_count{" + labels + "} " + std::to_string(cum) + "\n";
+}
+
 std::string LabelValue(const std::string& v) {
   std::string o;
   o.reserve(v.size());

@@ -12,8 +12,10 @@
 #include <atomic>
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <string>
 #include <thread>
+#include <vector>
 
 #include "common/status.h"
 
@@ -68,6 +70,35 @@ class Histogram {
   };
   void Totals(uint64_t counts[kBuckets + 1]) const;
   Shard shards_[kShards];
+};
+
+// The microsecond regime at full resolution: 100 ns bins up to 102.4 us plus
+// one overflow bin, sharded like Histogram (each loop thread writes its own
+// shard). Holds the gRPC server's per-call residency, whose interesting range
+// (1-10 us) the 1-2-5 buckets above would cover with three buckets.
+class FineHistogram {
+ public:
+  static constexpr int kBins = 1024;
+  static constexpr uint64_t kBinNs = 100;
+
+  FineHistogram();
+  void Observe(uint64_t ns);
+  // Merged counts, kBins + 1 entries (the last is >= 102.4 us).
+  std::vector<uint64_t> Counts() const;
+  uint64_t sum_ns() const;
+  // Upper edge (us) of the bin holding quantile q of `counts` (0 if empty).
+  static double QuantileUs(const std::vector<uint64_t>& counts, double q);
+  // `[[bin, count], ...]` over the nonzero bins (bin b covers [b, b+1) x 100 ns).
+  std::string SparseJson() const;
+  // Prometheus histogram with Histogram's bucket bounds from 1 us to 100 us.
+  void AppendPrometheus(const std::string& name, const std::string& labels, std::string* out) const;
+
+ private:
+  struct Shard {
+    std::atomic<uint64_t> bins[kBins + 1] = {};
+    std::atomic<uint64_t> sum_ns{0};
+  };
+  std::unique_ptr<Shard[]> shards_;
 };
 
 // Escapes a Prometheus label value (backslash, quote, newline).

@@ -940,13 +940,16 @@ std::string Plugin::StatsJson() const {
   uint64_t np = stats_.preferred_calls.Value();
   double pavg = np ? stats_.preferred_ns_total.Value() / 1e3 / np : 0.0;
   int loops = 0;
-  std::string placement = "[";
+  std::string placement = "[", residency = "[]";
+  std::vector<uint64_t> res_counts;
   {
     std::lock_guard<std::mutex> lk(server_mu_);
     if (server_) {
       loops = server_->loops();
       for (const auto& [cpu, busy] : server_->LoopPlacement())
         placement += (placement.size() > 1 ? ", [" : "[") + std::to_string(cpu) + ", " + std::to_string(busy) + "]";
+      res_counts = server_->stats().residency.Counts();
+      residency = server_->stats().residency.SparseJson();
     }
   }
   placement += "]";
@@ -970,7 +973,9 @@ std::string Plugin::StatsJson() const {
            static_cast<unsigned long long>(stats_.unhealthy_allocations.Value()));
   std::string out = "{\"resource\": \"" + JsonEscape(spec_.resource_name);
   out += buf;
-  return out + ", \"loop_cpus\": " + placement + "}";
+  snprintf(buf, sizeof(buf), ", \"residency_p50_us\": %.1f, \"residency_p99_us\": %.1f, \"residency_100ns\": ",
+           metrics::FineHistogram::QuantileUs(res_counts, 0.5), metrics::FineHistogram::QuantileUs(res_counts, 0.99));
+  return out + ", \"loop_cpus\": " + placement + buf + residency + "}";
 }
 
 size_t Plugin::healthy_count() const {
@@ -1067,6 +1072,13 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
     p->stats_.allocate_hist.AppendPrometheus("amdgpu_dp_handler_seconds", res(p) + ",method=\"Allocate\"", out);
     p->stats_.preferred_hist.AppendPrometheus("amdgpu_dp_handler_seconds",
                                               res(p) + ",method=\"GetPreferredAllocation\"", out);
+  }
+  family("amdgpu_dp_rpc_residency_seconds", "histogram",
+         "Unary RPCs from the socket read that carried them to the reply written, in the gRPC loop "
+         "(one sample per batch of calls answered together).");
+  for (auto* p : plugins) {
+    std::lock_guard<std::mutex> lk(p->server_mu_);
+    if (p->server_) p->server_->stats().residency.AppendPrometheus("amdgpu_dp_rpc_residency_seconds", res(p), out);
   }
   if (assignments) {
     // Per physical device: advertised IDs held by running containers and the

@@ -719,6 +719,33 @@ static void TestMetrics() {
   CHECK(text.find("x_seconds_bucket{a=\"b\",le=\"+Inf\"} 200000\n") != std::string::npos);
   CHECK(text.find("x_seconds_count{a=\"b\"} 200000\n") != std::string::npos);
   CHECK(metrics::LabelValue("a\"b\\c\n") == "a\\\"b\\\\c\\n");
+
+  // 100 ns bins: 3,000 x 2.35 us, 1,000 x 7.05 us, 10 beyond the last bin.
+  metrics::FineHistogram f;
+  std::vector<std::thread> fs;
+  for (int t = 0; t < 4; ++t)
+    fs.emplace_back([&, t] {
+      for (int i = 0; i < 1000; ++i) f.Observe(t == 3 ? 7050 : 2350);
+      if (t == 0)
+        for (int i = 0; i < 10; ++i) f.Observe(5000000);
+    });
+  for (auto& t : fs) t.join();
+  std::vector<uint64_t> fc = f.Counts();
+  CHECK(fc.size() == metrics::FineHistogram::kBins + 1);
+  CHECK(fc[23] == 3000 && fc[70] == 1000 && fc[metrics::FineHistogram::kBins] == 10);
+  CHECK(metrics::FineHistogram::QuantileUs(fc, 0.5) == 2.4);
+  CHECK(metrics::FineHistogram::QuantileUs(fc, 0.9) == 7.1);
+  CHECK(metrics::FineHistogram::QuantileUs({}, 0.5) == 0.0);
+  CHECK(f.SparseJson() == "[[23, 3000], [70, 1000], [1024, 10]]");
+  CHECK(f.sum_ns() == 3000ull * 2350 + 1000ull * 7050 + 10ull * 5000000);
+  text.clear();
+  f.AppendPrometheus("r_seconds", "", &text);
+  CHECK(text.find("r_seconds_bucket{le=\"2e-06\"} 0\n") != std::string::npos);
+  CHECK(text.find("r_seconds_bucket{le=\"5e-06\"} 3000\n") != std::string::npos);
+  CHECK(text.find("r_seconds_bucket{le=\"1e-05\"} 4000\n") != std::string::npos);
+  CHECK(text.find("r_seconds_bucket{le=\"0.0001\"} 4000\n") != std::string::npos);
+  CHECK(text.find("r_seconds_bucket{le=\"+Inf\"} 4010\n") != std::string::npos);
+  CHECK(text.find("r_seconds_count{} 4010\n") != std::string::npos);
 }
 
 static void TestPodResources() {

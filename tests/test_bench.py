@@ -50,6 +50,13 @@ def test_bench_single_process_contract():
     assert pl["relation"] in ("same-core", "same-l3", "other-l3") and pl["client_cpus"], pl
     busy = [b for _, b in pl["loops_during_timed"] if b > 0]
     assert len(busy) == 1 and busy[0] >= 300, pl
+    # the daemon's own share of each client's latency (read -> reply handed to
+    # send()): one sample per call, the timed 300 pods being 600 calls
+    sr = res["server_residency"]
+    assert sr["native_client"]["samples"] == 600, sr
+    assert 0 < sr["native_client"]["p50_us"] <= sr["native_client"]["p99_us"]
+    assert sr["native_client"]["p50_us"] < res["pod_p50_us"], (sr, res["pod_p50_us"])
+    assert sr["grpc_go_shaped"]["samples"] >= 600 and 300 <= sr["grpcio"]["samples"] <= 350, sr
 
 
 @pytest.mark.slow
@@ -72,6 +79,7 @@ def test_bench_two_ranks_gloo():
     assert all(v and v > 0 for v in per) and res["grpcio_client_allocate_p50_us"] == max(per)
     gg = [p["grpc_go_shaped"]["allocate"]["p50_us"] for p in res["per_rank"]]
     assert res["grpc_go_shaped_allocate_p50_us"] == max(gg)
+    assert res["server_residency"]["all_calls"]["samples"] > 0
 
 
 @pytest.mark.parametrize("n", [2, 4])

@@ -89,6 +89,14 @@ def test_metrics_exposition(served):
     assert _value(s, "amdgpu_dp_handler_seconds_count", resource=r, method="Allocate") == 5
     assert _value(s, "amdgpu_dp_handler_seconds_bucket", resource=r, method="Allocate", le="+Inf") == 5
     assert _value(s, "amdgpu_dp_handler_seconds_sum", resource=r, method="Allocate") < 0.01
+    # read -> reply residency of the 6 unary calls (one sample per batch answered together)
+    n = _value(s, "amdgpu_dp_rpc_residency_seconds_count", resource=r)
+    assert 1 <= n <= 6
+    assert _value(s, "amdgpu_dp_rpc_residency_seconds_bucket", resource=r, le="+Inf") == n
+    les = sorted(((float(dict(ls)["le"]), v) for (m, ls), v in s.items()
+                  if m == "amdgpu_dp_rpc_residency_seconds_bucket" and dict(ls)["le"] != "+Inf"))
+    assert len(les) == 7 and all(a[1] <= b[1] for a, b in zip(les, les[1:]))
+    assert _value(s, "amdgpu_dp_rpc_residency_seconds_sum", resource=r) < 0.1
     assert _value(s, "amdgpu_dp_restarts_total") == 1
     assert _value(s, "amdgpu_dp_build_info") == 1
     assert _value(s, "amdgpu_dp_grpc_connections_total", resource=r) >= 2
