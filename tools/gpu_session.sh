@@ -23,7 +23,9 @@
 #   census       HSA_CU_MASK -> XCD/CU census of the probe (quarter shares)
 #   interference noisy-neighbour victim latency with and without CU shares
 #   floor        UDS ping-pong floor, busy-poll on and off
-#   spread       10 back-to-back headline runs (bench.py --no-probe)
+#   spread       10 back-to-back headline runs (bench.py --no-probe); line:
+#                R i p50 p99 grpc-go grpcio pods/s relation client_cpu loop_cpu
+#                residency_p50 residency_p99 (the daemon's read -> reply time)
 #   access       device-cgroup denial (EPERM on /dev/kfd, /dev/dri/*, the
 #                errno an unprivileged pod's device cgroup returns) through
 #                libadp_devcgroup_sim.so: --smi-report / --dry-run / the
@@ -130,7 +132,7 @@ step_floor() {
 step_spread() {
   for i in $(seq 1 10); do
     timeout -k 10 300 python bench.py --no-probe > $out/spread_$i.json 2> $out/spread_$i.err || die "SPREAD $i" $out/spread_$i.err
-    python -c "import json; d=json.load(open('$out/spread_$i.json')); p=d.get('placement') or {}; print('R $i', d['value'], d['allocate_p99_us'], d.get('grpc_go_shaped_allocate_p50_us'), d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'], p.get('relation'), p.get('client_cpu'), p.get('busiest_loop_cpu'))"
+    python -c "import json; d=json.load(open('$out/spread_$i.json')); p=d.get('placement') or {}; print('R $i', d['value'], d['allocate_p99_us'], d.get('grpc_go_shaped_allocate_p50_us'), d.get('grpcio_client_allocate_p50_us'), d['pods_per_s'], p.get('relation'), p.get('client_cpu'), p.get('busiest_loop_cpu'), *[(r or {}).get(k) for r in [(d.get('server_residency') or {}).get('native_client')] for k in ('p50_us', 'p99_us')])"
   done
 }
 step_access() {
