@@ -118,7 +118,7 @@ coverage:
 # -Wall -Wextra as errors over the whole native tree, Python byte-compilation,
 # and clang-format / pyflakes when the machine has them.
 lint:
-	cmake -S native -B build/lint -G Ninja -DCMAKE_BUILD_TYPE=Release -DCMAKE_CXX_FLAGS=-Werror >/dev/null
+	cmake -S native -B build/lint -G Ninja -DCMAKE_BUILD_TYPE=Release "-DCMAKE_CXX_FLAGS=-Werror -Wshadow" >/dev/null
 	ninja -C build/lint -j$(JOBS)
 	$(PY) -m compileall -q k8s_gpu_sharing_plugin_amd tests tools bench.py __graft_entry__.py
 	@command -v clang-format >/dev/null && find native -name '*.cc' -o -name '*.h' | xargs clang-format --dry-run -Werror || echo "clang-format not installed; skipped"

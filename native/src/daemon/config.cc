@@ -411,12 +411,12 @@ Result<Config> LoadConfig(int argc, const char* const* argv,
     for (const auto& d : Table())
       if (name == d.name) def = &d;
     std::string key = name;
-    for (const auto& a : Aliases()) {
-      if (def || !*a.name || name != a.name) continue;
+    for (const auto& al : Aliases()) {
+      if (def || !*al.name || name != al.name) continue;
       for (const auto& d : Table())
-        if (std::string(a.canonical) == d.name) def = &d;
-      key = std::string("alias:") + a.canonical;
-      cfg.deprecations.push_back("--" + name + " is accepted for compatibility; use --" + a.canonical);
+        if (std::string(al.canonical) == d.name) def = &d;
+      key = std::string("alias:") + al.canonical;
+      cfg.deprecations.push_back("--" + name + " is accepted for compatibility; use --" + al.canonical);
     }
     if (!def) return InvalidArgument("flag provided but not defined: --" + name);
     if (!has_value) {

@@ -236,8 +236,8 @@ int DryRun(smi::Library* lib, const Validated& v, const Config& cfg) {
   }
   out += "], \"labels\": {";
   bool first_label = true;
-  for (const auto& [k, v] : inventory::NodeLabels(**snap)) {
-    out += std::string(first_label ? "" : ", ") + "\"" + JsonEscape(k) + "\": \"" + JsonEscape(v) + "\"";
+  for (const auto& [k, val] : inventory::NodeLabels(**snap)) {
+    out += std::string(first_label ? "" : ", ") + "\"" + JsonEscape(k) + "\": \"" + JsonEscape(val) + "\"";
     first_label = false;
   }
   out += "}, \"resources\": [";
