@@ -1,14 +1,15 @@
-"""PyTorch under the HBM-cap shim with either allocator backend
+"""PyTorch under the HBM-cap shim with each allocator configuration
 (PYTORCH_CUDA_ALLOC_CONF=backend:native | backend:cudaMallocAsync, the latter
 hipMallocAsync / hipFreeAsync on ROCm, whose freed blocks stay in the
-stream-ordered pool): the grant is the device's memory, a freed 3 GiB can be
+stream-ordered pool; expandable_segments:True is reported unsupported by
+PyTorch 2.10 on ROCm 7 and falls back to the native allocator): the grant is the device's memory, a freed 3 GiB can be
 allocated again, 2 GiB more past a 4000 MiB grant are refused, and 200 rounds
 of 512 MiB allocate/free all succeed. One JSON line; run with the shim
-preloaded and a grant (tests/test_gpu.py::test_memcap_with_both_pytorch_allocator_backends).
+preloaded and a grant (tests/test_gpu.py::test_memcap_with_pytorch_allocator_configs).
 """
 import json, os, sys, torch
 torch.cuda.init()
-res = {"backend": torch.cuda.get_allocator_backend()}
+res = {"backend": torch.cuda.get_allocator_backend(), "conf": os.environ.get("PYTORCH_CUDA_ALLOC_CONF", "")}
 free, total = torch.cuda.mem_get_info()
 res["total_mib"] = total >> 20
 def alloc(gib):
