@@ -244,3 +244,35 @@ def test_prometheus_operator_objects():
     off = helm_render.render({"metrics": {"enabled": False, "serviceMonitor": {"enabled": True},
                                           "prometheusRule": {"enabled": True}}})
     assert not off["servicemonitor.yaml"].strip() and not off["prometheusrule.yaml"].strip()
+
+
+def test_grafana_dashboard_configmap():
+    """metrics.grafanaDashboard: a ConfigMap with the sidecar's label holding the
+    dashboard JSON; every metric a panel queries is one the daemon exports."""
+    import glob
+    import json
+    import re
+    out = helm_render.render({"metrics": {"enabled": True, "grafanaDashboard": {"enabled": True}}})
+    (cm,) = [d for d in yaml.safe_load_all(out["grafana-dashboard.yaml"]) if d]
+    assert cm["kind"] == "ConfigMap" and cm["metadata"]["labels"]["grafana_dashboard"] == "1"
+    assert cm["metadata"]["namespace"] == daemonset({})["metadata"]["namespace"]
+    dash = json.loads(cm["data"]["amdgpu-device-plugin.json"])
+    with open(os.path.join(helm_render.CHART, "dashboards", "amdgpu-device-plugin.json")) as f:
+        assert dash == json.load(f)
+    assert dash["uid"] == "amdgpu-device-plugin" and len(dash["panels"]) >= 8
+    ids = [p["id"] for p in dash["panels"]]
+    assert len(ids) == len(set(ids))
+    src = "".join(open(f).read() for f in glob.glob(os.path.join(ROOT, "native", "src", "*", "*.cc")))
+    exprs = [t["expr"] for p in dash["panels"] for t in p["targets"]]
+    names = {n for e in exprs for n in re.findall(r"amdgpu_dp_\w+", e)}
+    assert "amdgpu_dp_rpc_residency_seconds_bucket" in names
+    for name in names:
+        base = re.sub(r"_(bucket|sum|count)$", "", name)
+        assert f'"{base}' in src or f"{base} " in src or f"{base}{{" in src, name
+    # the sidecar may watch another namespace
+    other = helm_render.render({"metrics": {"enabled": True,
+                                            "grafanaDashboard": {"enabled": True, "namespace": "monitoring"}}})
+    assert yaml.safe_load(other["grafana-dashboard.yaml"])["metadata"]["namespace"] == "monitoring"
+    assert not helm_render.render({"metrics": {"enabled": True}})["grafana-dashboard.yaml"].strip()
+    assert not helm_render.render({"metrics": {"enabled": False, "grafanaDashboard": {"enabled": True}}})[
+        "grafana-dashboard.yaml"].strip()

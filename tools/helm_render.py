@@ -3,7 +3,7 @@
 Implements the subset of Go text/template + sprig the chart uses: actions with
 `{{-`/`-}}` whitespace trimming, comments, pipelines, parenthesised commands,
 variables (`$x :=`), `if`/`else if`/`else`, `with`/`else`, `define`/`include`,
-and the functions default, kindIs, trunc, trimSuffix, contains, printf, toYaml,
+`.Files.Get`, and the functions default, kindIs, trunc, trimSuffix, contains, printf, toYaml,
 nindent, indent, quote, replace, coalesce, or, and, not, eq. Enough to render
 deployments/helm/amd-gpu-device-plugin for tests/test_helm_render.py; it is
 not a general helm implementation.
@@ -247,6 +247,11 @@ class Renderer:
             if has_piped:
                 args.append(piped)
             return self.funcs[head[1]](*args)
+        if head[0] == "field" and len(cmd) > 1:  # a method, e.g. .Files.Get "path"
+            fn = self.arg(head, dot, scope)
+            if callable(fn):
+                args = [self.arg(t, dot, scope) for t in cmd[1:]]
+                return fn(*(args + [piped] if has_piped else args))
         if len(cmd) != 1 or has_piped:
             raise SyntaxError(f"not a function: {cmd}")
         return self.arg(head, dot, scope)
@@ -308,6 +313,14 @@ def render(values_override=None, release="amdgpu", chart_dir=CHART):
     chart = {"Name": chart_yaml["name"], "Version": chart_yaml["version"],
              "AppVersion": chart_yaml.get("appVersion", "")}
     r = Renderer(values, chart, {"Name": release, "Service": "Helm", "Namespace": values.get("namespace")})
+
+    def get_file(path):  # .Files.Get: a file of the chart, "" if absent (as helm)
+        try:
+            with open(os.path.join(chart_dir, path)) as f:
+                return f.read()
+        except OSError:
+            return ""
+    r.root["Files"] = {"Get": get_file}
     tdir = os.path.join(chart_dir, "templates")
     parsed = {}
     for name in sorted(os.listdir(tdir)):
