@@ -127,9 +127,11 @@ struct Writer {
   void Run() {
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      // (bounded wait: a job queued without a wake is picked up in 20 ms at the
-      // latest; system_clock, see Flush())
-      while (jobs.empty()) cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(20));
+      // Every job queued without a wake is followed by WakeWriter() once the
+      // gRPC loop has written the Allocate response; the bounded wait is only a
+      // backstop (an idle daemon wakes twice a second here, not 50 times).
+      // system_clock: see Flush().
+      while (jobs.empty()) cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(500));
       Job j = std::move(jobs.front());
       jobs.pop_front();
       lk.unlock();

@@ -1,0 +1,26 @@
+"""The daemon's idle footprint (tools/idle_footprint.py): registered, health
+monitoring on, /metrics scraped, no pods. An idle DaemonSet must not spin:
+its wake-ups come from the health monitor's 100 ms event-wait slices and the
+grant writer's backstop, not from polling loops."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import idle_footprint  # noqa: E402
+
+
+@pytest.mark.parametrize("enforce", [False, True])
+def test_idle_daemon_sleeps(enforce, capsys):
+    args = ["--seconds", "4", "--scrape-s", "1", "--settle-s", "1"] + (["--enforce"] if enforce else [])
+    assert idle_footprint.main(args) == 0
+    import json
+    res = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert res["daemon_alive"] and res["scrapes"] >= 4
+    # ~10/s from the event-wait slices (+2/s from the grant writer when enforcing)
+    assert res["context_switches_per_s"] < 40, res
+    assert res["cpu_pct_of_a_core"] < 5, res
+    assert res["threads"] < 20 and res["rss_mib"] < 64, res

@@ -37,6 +37,8 @@
 #                8-rank mock node (AB_RANKS) per mode
 #   cpus         the CPUs this box lets the session use, grouped by L3 / NUMA
 #   curve        tools/mock_curve.sh (CONFIGS="spx-none" for one config)
+#   idle         the daemon's idle footprint on real libamd_smi (CPU, wake-ups,
+#                RSS; default config and memory units enforced), IDLE_SECONDS (60)
 #   soak         SOAK_SECONDS (default 180) of churn + SIGHUP + kubelet restarts + scrapes on
 #                real libamd_smi (health polling, state file): RSS/fd/thread leaks
 set -o pipefail
@@ -147,6 +149,12 @@ step_access() {
   cat $out/daemon_denied.txt
   python3 tools/compare_smi_reports.py $out/smi_report.json $out/smi_report_denied.json $out/smi_report_kfd_denied.json $out/smi_report_dri_denied.json | tee $out/access_summary.txt
   rm -rf $dp
+}
+step_idle() {
+  local secs=${IDLE_SECONDS:-60}
+  timeout -k 10 $((secs + 90)) python tools/idle_footprint.py --real --seconds $secs > $out/idle.json 2> $out/idle.err || die IDLE $out/idle.err
+  timeout -k 10 $((secs + 90)) python tools/idle_footprint.py --real --enforce --seconds $secs > $out/idle_enforce.json 2> $out/idle_enforce.err || die "IDLE (enforce)" $out/idle_enforce.err
+  cat $out/idle.json $out/idle_enforce.json
 }
 step_driver() {
   timeout -k 10 180 python tools/probe_driver_usage.py > $out/driver_usage.json 2> $out/driver_usage.err || die DRIVER $out/driver_usage.err
