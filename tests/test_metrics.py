@@ -134,6 +134,11 @@ def test_metrics_follow_health_and_healthz(served):
     while time.time() < deadline and _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_restarts_total") < 2:
         time.sleep(0.05)
     assert _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_restarts_total") == 2
+    # (as at start: Register() reaches the kubelet just before the plugin marks
+    # itself serving again)
+    deadline = time.time() + 5
+    while time.time() < deadline and _get(port, "/healthz")[0] != 200:
+        time.sleep(0.05)
     assert _get(port, "/healthz")[0] == 200
     k2.stop()
 
