@@ -71,11 +71,22 @@ LogLevel GetLogLevel() { return static_cast<LogLevel>(g_level.load()); }
 bool LogEnabled(LogLevel l) { return static_cast<int>(l) >= g_level.load(std::memory_order_relaxed); }
 
 void Logf(LogLevel l, const char* component, const char* fmt, ...) {
-  char msg[4096];
-  va_list ap;
+  // Most lines fit the stack buffer; longer ones (SIGUSR1 stats with a
+  // latency histogram) are formatted again into a string, never truncated.
+  char small[4096];
+  std::string big;
+  const char* msg = small;
+  va_list ap, ap2;
   va_start(ap, fmt);
-  vsnprintf(msg, sizeof(msg), fmt, ap);
+  va_copy(ap2, ap);
+  int n = vsnprintf(small, sizeof(small), fmt, ap);
   va_end(ap);
+  if (n >= static_cast<int>(sizeof(small))) {
+    big.resize(static_cast<size_t>(n));
+    vsnprintf(big.data(), big.size() + 1, fmt, ap2);
+    msg = big.c_str();
+  }
+  va_end(ap2);
   struct timeval tv;
   gettimeofday(&tv, nullptr);
   struct tm tm;

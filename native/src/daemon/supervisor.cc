@@ -977,10 +977,17 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
               }
               for (auto& pl : plugins) {
                 struct stat st;
-                if (pl->running() && BaseName(pl->socket_path()) == e->name &&
-                    stat(pl->socket_path().c_str(), &st) != 0) {
+                if (!pl->running() || BaseName(pl->socket_path()) != e->name) continue;
+                if (stat(pl->socket_path().c_str(), &st) != 0) {
                   LOG_WARN(kComp, "inotify: %s was removed, restarting", pl->socket_path().c_str());
                   do_reregister = true;
+                } else if (!pl->owns_socket()) {
+                  // Another instance (a rollout with maxSurge) unlinked ours and
+                  // bound the path: binding it back would start a tug of war.
+                  // The kubelet now talks to that instance; this one stands by
+                  // until the kubelet restarts or the file disappears again.
+                  LOG_WARN(kComp, "inotify: %s now belongs to another process; '%s' stands by",
+                           pl->socket_path().c_str(), pl->resource_name().c_str());
                 }
               }
             }

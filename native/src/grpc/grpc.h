@@ -23,6 +23,7 @@
 #pragma once
 
 #include <sched.h>
+#include <sys/types.h>
 
 #include <atomic>
 #include <cstdint>
@@ -137,6 +138,9 @@ class Server {
   // Per loop: the CPU it last served from (-1 = never) and its busy iterations.
   std::vector<std::pair<int, uint64_t>> LoopPlacement() const;
   const std::string& socket_path() const { return socket_path_; }
+  // The socket file at socket_path() is still the one Listen() bound (not
+  // removed, not replaced by another process binding the same path).
+  bool OwnsSocketPath() const;
   const ServerStats& stats() const { return stats_; }
   // Log every unary call (method, status, sizes, handler time). Set before Start().
   void set_trace(bool on) { trace_ = on; }
@@ -171,6 +175,8 @@ class Server {
 
   std::string name_;
   std::string socket_path_;
+  dev_t sock_dev_ = 0;  // identity of the socket file Listen() created
+  ino_t sock_ino_ = 0;
   // std::less<>: looked up by string_view straight from the HPACK-decoded :path.
   std::map<std::string, UnaryHandler, std::less<>> unary_;
   std::map<std::string, StreamHandler, std::less<>> streams_;

@@ -521,6 +521,11 @@ Status Server::Listen(const std::string& socket_path) {
     listen_fd_ = -1;
     return s;
   }
+  struct stat st;
+  if (stat(socket_path.c_str(), &st) == 0) {
+    sock_dev_ = st.st_dev;
+    sock_ino_ = st.st_ino;
+  }
   if (listen(listen_fd_, 128) != 0) {
     Status s = Unavailable("listen " + socket_path + ": " + strerror(errno));
     close(listen_fd_);
@@ -531,6 +536,12 @@ Status Server::Listen(const std::string& socket_path) {
   // connection keeps the (level-triggered) listener readable forever.
   if (spare_fd_ < 0) spare_fd_ = open("/dev/null", O_RDONLY | O_CLOEXEC);
   return Status::Ok();
+}
+
+bool Server::OwnsSocketPath() const {
+  struct stat st;
+  return sock_ino_ != 0 && stat(socket_path_.c_str(), &st) == 0 && st.st_dev == sock_dev_ &&
+         st.st_ino == sock_ino_;
 }
 
 Status Server::Start(std::function<void()> on_fatal) {
@@ -571,7 +582,9 @@ void Server::Stop() {
   if (listen_fd_ >= 0) {
     close(listen_fd_);
     listen_fd_ = -1;
-    if (!socket_path_.empty()) unlink(socket_path_.c_str());
+    // Only our own file: another instance of the plugin (a DaemonSet rollout
+    // with maxSurge) may have bound the same path since.
+    if (!socket_path_.empty() && OwnsSocketPath()) unlink(socket_path_.c_str());
   }
   for (auto& l : loops_) {
     if (l->epoll_fd >= 0) { close(l->epoll_fd); l->epoll_fd = -1; }

@@ -156,6 +156,11 @@ Plugin::~Plugin() { Stop(); }
 
 std::string Plugin::socket_path() const { return PathJoin(opts_.plugin_dir, spec_.socket_name); }
 
+bool Plugin::owns_socket() const {
+  std::lock_guard<std::mutex> lk(server_mu_);
+  return server_ && server_->OwnsSocketPath();
+}
+
 void Plugin::BuildUnits() {
   const auto& v = spec_.variant;
   replicated_ = v.replicas > 1 || v.auto_replicas;

@@ -214,6 +214,9 @@ class Plugin {
     std::lock_guard<std::mutex> lk(server_mu_);
     return server_ != nullptr;
   }
+  // Running, and the socket file is still the one this plugin bound (false
+  // once another process has bound the same path).
+  bool owns_socket() const;
 
   // Thread-safe. Marks every device that contains amdsmi handle `handle`.
   void SetHandleHealth(int handle, bool healthy, const std::string& reason);

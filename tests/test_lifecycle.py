@@ -553,3 +553,56 @@ def test_engine_and_affinity_options_serve(scratch, args):
         assert ("served from its L3" in d.log()) == ("peer-l3" in args)
     assert d.stop() == 0
     k.stop()
+
+
+def _foreign_socket(path):
+    """A listening Unix socket bound at `path` by this process (another plugin instance)."""
+    import socket as so
+    s = so.socket(so.AF_UNIX, so.SOCK_STREAM)
+    s.bind(path)
+    s.listen(1)
+    return s
+
+
+def test_replaced_socket_is_not_removed_on_stop(scratch):
+    """A second instance (DaemonSet rollout with maxSurge) that atomically
+    replaced our socket file keeps it when we stop: Stop() removes only the
+    file it bound. (The reference removes its socket path unconditionally.)"""
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch).start()
+    k.wait_registration()
+    path = os.path.join(scratch, "amd-gpu.sock")
+    other = _foreign_socket(path + ".new")
+    os.rename(path + ".new", path)  # atomic takeover: no delete event for the old file
+    ino = os.stat(path).st_ino
+    assert d.stop() == 0
+    assert os.path.exists(path) and os.stat(path).st_ino == ino
+    other.close()
+    k.stop()
+
+
+def test_takeover_by_another_instance_stands_by(scratch):
+    """Our socket unlinked and bound again by another process: no tug of war
+    (re-binding would unlink theirs in turn); we log that we stand by, do not
+    re-register, and leave their socket on exit."""
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch).start()
+    k.wait_registration()
+    path = os.path.join(scratch, "amd-gpu.sock")
+    # Frozen while the other instance unlinks and binds, so the daemon reads
+    # the delete event only once the new file is in place (deterministic).
+    d.signal(signal.SIGSTOP)
+    try:
+        os.unlink(path)
+        other = _foreign_socket(path)
+    finally:
+        d.signal(signal.SIGCONT)
+    ino = os.stat(path).st_ino
+    d.wait_log("now belongs to another process")
+    time.sleep(1.5)  # longer than a restart's first backoff
+    assert "was removed, restarting" not in d.log()
+    assert os.stat(path).st_ino == ino
+    assert d.stop() == 0
+    assert os.path.exists(path) and os.stat(path).st_ino == ino
+    other.close()
+    k.stop()
