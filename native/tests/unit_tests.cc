@@ -24,6 +24,7 @@
 
 #include "alloc/replicas.h"
 #include "alloc/topology.h"
+#include "common/log.h"
 #include "common/strings.h"
 #include "daemon/config.h"
 #include "daemon/yaml.h"
@@ -748,6 +749,29 @@ static void TestMetrics() {
   CHECK(text.find("r_seconds_count{} 4010\n") != std::string::npos);
 }
 
+// Log lines longer than the 4 KiB stack buffer come out whole.
+static void TestLongLogLine() {
+  g_case = "long log line";
+  char path[] = "/tmp/adp_log_XXXXXX";
+  int fd = mkstemp(path);
+  CHECK(fd >= 0);
+  fflush(stderr);
+  int saved = dup(2);
+  dup2(fd, 2);
+  std::string big(10000, 'x');
+  Logf(LogLevel::kError, "test", "head %s tail", big.c_str());
+  fflush(stderr);
+  dup2(saved, 2);
+  close(saved);
+  std::string text;
+  char buf[4096];
+  lseek(fd, 0, SEEK_SET);
+  for (ssize_t n; (n = read(fd, buf, sizeof(buf))) > 0;) text.append(buf, static_cast<size_t>(n));
+  close(fd);
+  unlink(path);
+  CHECK(text.find("head " + big + " tail\n") != std::string::npos);
+}
+
 static void TestPodResources() {
   g_case = "podresources";
   // pod_resources { name: "p" namespace: "n" containers { name: "c"
@@ -1016,6 +1040,7 @@ void TestMemcapUsage() {
 }
 
 int main() {
+  TestLongLogLine();
   TestYaml();
   TestConfigFuzz();
   TestReplicaCuRanges();
