@@ -9,6 +9,7 @@
   python -m k8s_gpu_sharing_plugin_amd hbm [daemon flags...]  # HBM use of enforced grants
   python -m k8s_gpu_sharing_plugin_amd doctor [daemon flags...]
                                                           # deployment checks, what to change
+  python -m k8s_gpu_sharing_plugin_amd status [URL]       # a running daemon, from its /metrics
 
 `report` runs `amdgpu-device-plugin --dry-run` (real libamd_smi unless
 AMD_SMI_LIB points elsewhere) and prints a table; `validate` runs
@@ -16,7 +17,9 @@ AMD_SMI_LIB points elsewhere) and prints a table; `validate` runs
 runs `amdgpu-device-plugin --list-grants` (the accounting files of
 --enforce-memory-units with /metrics under <device-plugin dir>/amdgpu-dp/usage)
 and prints a table; `doctor` runs `amdgpu-device-plugin --doctor` (exit 1 on a
-failure).
+failure); `status` reads a running daemon's /metrics (default
+http://127.0.0.1:9400/metrics) and prints its resources, device health, RPC
+counts with the loops' residency, and the containers' HBM against their grants.
 """
 
 import json
@@ -68,6 +71,85 @@ def _hbm(args) -> int:
     return 0
 
 
+def parse_prometheus(text):
+    """[(name, {label: value}, float)] of a Prometheus text exposition."""
+    import re
+    out = []
+    for line in text.splitlines():
+        if not line or line.startswith("#"):
+            continue
+        m = re.match(r'^([a-zA-Z_:][a-zA-Z0-9_:]*)(?:\{(.*)\})? (\S+)$', line)
+        if not m:
+            continue
+        labels = {k: bytes(v, "utf-8").decode("unicode_escape")
+                  for k, v in re.findall(r'(\w+)="((?:[^"\\]|\\.)*)"', m.group(2) or "")}
+        out.append((m.group(1), labels, float(m.group(3))))
+    return out
+
+
+def _quantile(buckets, q):
+    """Upper bound of the bucket holding quantile q of cumulative (le, count) pairs."""
+    buckets = sorted(buckets)
+    total = buckets[-1][1] if buckets else 0
+    if not total:
+        return None
+    for le, c in buckets:
+        if c >= q * total:
+            return le
+    return buckets[-1][0]
+
+
+def _status(args) -> int:
+    import urllib.request
+    url = args[0] if args else "http://127.0.0.1:9400/metrics"
+    try:
+        with urllib.request.urlopen(url, timeout=5) as r:
+            samples = parse_prometheus(r.read().decode())
+    except OSError as e:
+        print(f"cannot read {url}: {e}", file=sys.stderr)
+        return 1
+
+    def by(name):
+        return [(ls, v) for n, ls, v in samples if n == name]
+
+    build = by("amdgpu_dp_build_info")
+    if build:
+        print("amdgpu-device-plugin " + " ".join(f"{k}={v}" for k, v in sorted(build[0][0].items())))
+    print(f"{'resource':<28} {'devices':>7} {'healthy':>7} {'allocatable':>11} {'registered':>10} "
+          f"{'Allocate':>9} {'Preferred':>9} {'residency p50/p99 us':>21}")
+    for ls, n in by("amdgpu_dp_devices"):
+        res = ls.get("resource")
+
+        def one(name, extra=None):
+            return next((v for l2, v in by(name) if l2.get("resource") == res and
+                         all(l2.get(k) == x for k, x in (extra or {}).items())), 0)
+        buckets = [(float("inf") if l2["le"] == "+Inf" else float(l2["le"]), v)
+                   for l2, v in by("amdgpu_dp_rpc_residency_seconds_bucket") if l2.get("resource") == res]
+        p50, p99 = _quantile(buckets, 0.5), _quantile(buckets, 0.99)
+        resid = "-" if p50 is None else f"<={p50 * 1e6:g} / <={p99 * 1e6:g}"
+        print(f"{res:<28} {int(n):>7} {int(one('amdgpu_dp_healthy_devices')):>7} "
+              f"{int(one('amdgpu_dp_allocatable')):>11} {'yes' if one('amdgpu_dp_registered') else 'no':>10} "
+              f"{int(one('amdgpu_dp_rpc_total', {'method': 'Allocate'})):>9} "
+              f"{int(one('amdgpu_dp_rpc_total', {'method': 'GetPreferredAllocation'})):>9} {resid:>21}")
+    bad = [ls for ls, v in by("amdgpu_dp_device_healthy") if v == 0]
+    for ls in bad:
+        print(f"UNHEALTHY {ls.get('resource')} {ls.get('device')} (index {ls.get('index')})")
+    used = {tuple(sorted(ls.items())): v for ls, v in by("amdgpu_dp_container_hbm_used_bytes")}
+    granted = {tuple(sorted(ls.items())): v for ls, v in by("amdgpu_dp_container_hbm_granted_bytes")}
+    if granted:
+        print()
+        print(f"{'namespace/pod/container':<48} {'device':>6} {'used MiB':>9} {'granted MiB':>11}")
+        for key, g in sorted(granted.items()):
+            ls = dict(key)
+            who = "/".join(ls.get(k, "?") for k in ("namespace", "pod", "container"))
+            print(f"{who:<48} {ls.get('index', ls.get('device', '?')):>6} {int(used.get(key, 0)) >> 20:>9} "
+                  f"{int(g) >> 20:>11}")
+    over = [ls for ls, v in by("amdgpu_dp_container_hbm_over_grant") if v]
+    for ls in over:
+        print(f"OVER GRANT {ls.get('namespace')}/{ls.get('pod')}/{ls.get('container')} on {ls.get('bdf')}")
+    return 1 if bad or over else 0
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     if not argv or argv[0] in ("-h", "--help"):
@@ -84,6 +166,8 @@ def main(argv=None) -> int:
         return _validate(rest)
     if cmd == "hbm":
         return _hbm(rest)
+    if cmd == "status":
+        return _status(rest)
     if cmd == "doctor":
         return subprocess.run([DAEMON, "--doctor", *rest]).returncode
     if cmd == "bench":

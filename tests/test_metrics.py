@@ -14,6 +14,7 @@ import urllib.request
 
 import pytest
 
+from k8s_gpu_sharing_plugin_amd import REPO_ROOT as ROOT
 from k8s_gpu_sharing_plugin_amd.models import fixtures
 from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
 
@@ -475,3 +476,41 @@ def test_container_hbm_files_without_pod_resources_and_tampered(scratch):
     finally:
         d.stop()
         k.stop()
+
+
+def test_status_cli_reads_metrics(served):
+    """`python -m k8s_gpu_sharing_plugin_amd status URL`: the resource line with
+    devices / healthy / allocatable / registered / RPC counts / residency, and
+    exit 1 with an UNHEALTHY line once a device fails."""
+    import subprocess
+    import sys
+    d, k, c, port, fifo = served
+    q, call = c.watch()
+    ids = [x.ID for x in q.get(timeout=5).devices]
+    for _ in range(3):
+        c.allocate([ids[0]])
+    d.wait_log("health monitor watching")
+    url = f"http://127.0.0.1:{port}/metrics"
+    cmd = [sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "status", url]
+    deadline = time.time() + 5
+    while True:  # registered is marked just after Register() reaches the kubelet
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=60)
+        if r.returncode == 0 or time.time() > deadline:
+            break
+        time.sleep(0.1)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = next(ln for ln in r.stdout.splitlines() if ln.startswith("amd.com/sharedgpu"))
+    cols = line.split()
+    assert cols[1:5] == ["2", "2", "6", "yes"] and int(cols[5]) == 3, line
+    assert "<=" in line  # residency quantiles present
+    fd = os.open(fifo, os.O_WRONLY | os.O_NONBLOCK)
+    os.write(fd, b"1 3 pre-reset\n")
+    os.close(fd)
+    deadline = time.time() + 5
+    while True:
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=60)
+        if r.returncode == 1 or time.time() > deadline:
+            break
+        time.sleep(0.1)
+    assert r.returncode == 1 and "UNHEALTHY amd.com/sharedgpu" in r.stdout, r.stdout
+    call.cancel()
