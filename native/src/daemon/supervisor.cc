@@ -978,7 +978,14 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
               for (auto& pl : plugins) {
                 struct stat st;
                 if (!pl->running() || BaseName(pl->socket_path()) != e->name) continue;
-                if (stat(pl->socket_path().c_str(), &st) != 0) {
+                bool gone = stat(pl->socket_path().c_str(), &st) != 0;
+                if (gone) {
+                  // Another instance unlinks the path and binds it microseconds
+                  // later: look again after a moment before taking it back.
+                  usleep(20000);
+                  gone = stat(pl->socket_path().c_str(), &st) != 0;
+                }
+                if (gone) {
                   LOG_WARN(kComp, "inotify: %s was removed, restarting", pl->socket_path().c_str());
                   do_reregister = true;
                 } else if (!pl->owns_socket()) {

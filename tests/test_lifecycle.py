@@ -606,3 +606,24 @@ def test_takeover_by_another_instance_stands_by(scratch):
     assert os.path.exists(path) and os.stat(path).st_ino == ino
     other.close()
     k.stop()
+
+
+def test_unlink_then_bind_takeover_stands_by(scratch):
+    """The other instance's real sequence, unfrozen: unlink our socket, then
+    bind its own microseconds later. The daemon looks again before taking the
+    path back, sees the new file and stands by."""
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch).start()
+    k.wait_registration()
+    path = os.path.join(scratch, "amd-gpu.sock")
+    os.unlink(path)
+    other = _foreign_socket(path)
+    ino = os.stat(path).st_ino
+    d.wait_log("now belongs to another process")
+    time.sleep(1.5)
+    assert "was removed, restarting" not in d.log()
+    assert os.stat(path).st_ino == ino
+    assert d.stop() == 0
+    assert os.stat(path).st_ino == ino
+    other.close()
+    k.stop()
