@@ -685,6 +685,15 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
           for (auto& p : plugins)
             if (p->device_count() > 0 && !p->running()) return false;
           return true;
+        },
+        [&] {  // GET /stats: what SIGUSR1 logs, as one JSON document
+          std::string out = "{\"plugins\": [";
+          {
+            std::lock_guard<std::mutex> lk(plugins_mu);
+            for (size_t i = 0; i < plugins.size(); ++i) out += (i ? ", " : "") + plugins[i]->StatsJson();
+          }
+          return out + "], \"health\": " + health_counters.Json() + ", \"restarts\": " +
+                 std::to_string(restarts.load()) + "}\n";
         });
     Status ms = http->Start(cfg.flags.metrics_addr);
     if (!ms.ok()) {

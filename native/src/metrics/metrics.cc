@@ -201,8 +201,8 @@ std::string LabelValue(const std::string& v) {
   return o;
 }
 
-HttpServer::HttpServer(Render render, Healthy healthy)
-    : render_(std::move(render)), healthy_(std::move(healthy)) {}
+HttpServer::HttpServer(Render render, Healthy healthy, Render stats)
+    : render_(std::move(render)), healthy_(std::move(healthy)), stats_(std::move(stats)) {}
 
 HttpServer::~HttpServer() { Stop(); }
 
@@ -245,7 +245,7 @@ Status HttpServer::Start(const std::string& addr) {
   stop_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   spare_fd_ = open("/dev/null", O_RDONLY | O_CLOEXEC);
   thread_ = std::thread([this] { Run(); });
-  LOG_INFO(kComp, "serving /metrics and /healthz on port %d", port_);
+  LOG_INFO(kComp, "serving /metrics and /healthz on port %d (and /stats)", port_);
   return Status::Ok();
 }
 
@@ -358,13 +358,16 @@ std::string HttpServer::Respond(const std::string& req) {
     body = "only GET\n";
   } else if (path == "/metrics") {
     body = render_();
+  } else if (path == "/stats" && stats_) {
+    type = "application/json";
+    body = stats_();
   } else if (path == "/healthz") {
     bool ok = healthy_();
     status = ok ? "200 OK" : "503 Service Unavailable";
     body = ok ? "ok\n" : "plugins not serving\n";
   } else {
     status = "404 Not Found";
-    body = "try /metrics or /healthz\n";
+    body = "try /metrics, /healthz or /stats\n";
   }
   std::string resp = "HTTP/1.1 " + status + "\r\nContent-Type: " + type +
                      "\r\nContent-Length: " + std::to_string(body.size()) + "\r\nConnection: close\r\n\r\n";

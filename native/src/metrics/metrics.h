@@ -109,7 +109,9 @@ class HttpServer {
  public:
   using Render = std::function<std::string()>;
   using Healthy = std::function<bool()>;
-  HttpServer(Render render, Healthy healthy);
+  // `stats` (optional) answers GET /stats with JSON: the SIGUSR1 counters for
+  // tools that would otherwise parse the log.
+  HttpServer(Render render, Healthy healthy, Render stats = nullptr);
   ~HttpServer();
   // addr: "host:port", ":port" (all interfaces) or "port". Port 0 picks a free port.
   Status Start(const std::string& addr);
@@ -121,6 +123,7 @@ class HttpServer {
   std::string Respond(const std::string& request);
   Render render_;
   Healthy healthy_;
+  Render stats_;
   int listen_fd_ = -1;
   int stop_fd_ = -1;
   int spare_fd_ = -1;  // reserve descriptor: shed connections at EMFILE instead of spinning

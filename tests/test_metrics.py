@@ -514,3 +514,22 @@ def test_status_cli_reads_metrics(served):
         time.sleep(0.1)
     assert r.returncode == 1 and "UNHEALTHY amd.com/sharedgpu" in r.stdout, r.stdout
     call.cancel()
+
+
+def test_stats_endpoint_is_json(served):
+    """GET /stats: the SIGUSR1 counters as one JSON document (plugins with
+    RPC counts and the residency histogram, health counters, restarts)."""
+    import json
+    d, k, c, port, _ = served
+    q, call = c.watch()
+    ids = [x.ID for x in q.get(timeout=5).devices]
+    for _ in range(4):
+        c.allocate([ids[0]])
+    with urllib.request.urlopen(f"http://127.0.0.1:{port}/stats", timeout=5) as r:
+        assert r.headers["Content-Type"] == "application/json"
+        st = json.loads(r.read())
+    (p,) = [p for p in st["plugins"] if p["resource"] == "amd.com/sharedgpu"]
+    assert p["allocate_calls"] == 4 and p["devices"] == 2 and p["advertised"] == 6
+    assert sum(n for _, n in p["residency_100ns"]) >= 4 and p["residency_p50_us"] > 0
+    assert st["health"]["events"] in ("on", "off", "not started") and st["restarts"] >= 1
+    call.cancel()
