@@ -1,5 +1,6 @@
 #include "daemon/supervisor.h"
 
+#include <dirent.h>
 #include <errno.h>
 #include <poll.h>
 #include <signal.h>
@@ -8,7 +9,9 @@
 #include <sys/eventfd.h>
 #include <sys/inotify.h>
 #include <sys/signalfd.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
+#include <sys/un.h>
 #include <sys/timerfd.h>
 #include <unistd.h>
 
@@ -302,6 +305,21 @@ void WriteLabels(const std::string& path, const inventory::Snapshot& snap) {
 
 // --doctor: one line per check -- "ok", "warn" (works, with less) or "FAIL"
 // (the plugin cannot serve) -- and what to change; exit 1 on a failure.
+// A Unix socket something listens on (a connect is accepted or queued); a
+// stale file refuses.
+bool SocketLive(const std::string& path) {
+  sockaddr_un addr{};
+  if (path.size() >= sizeof(addr.sun_path)) return false;
+  int fd = socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  if (fd < 0) return false;
+  addr.sun_family = AF_UNIX;
+  memcpy(addr.sun_path, path.c_str(), path.size());
+  int rc = connect(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr));
+  bool live = rc == 0 || errno == EINPROGRESS || errno == EAGAIN;
+  close(fd);
+  return live;
+}
+
 struct DoctorReport {
   int ok = 0, warn = 0, fail = 0;
   void Line(const char* level, const std::string& what) {
@@ -390,6 +408,39 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
   } else {
     d.Line("FAIL", "plugin directory " + f.plugin_dir + " not writable (" + strerror(errno) +
                        "): the plugin sockets go there");
+  }
+  // Who else serves in the kubelet's directory: another instance of this
+  // plugin (a rollout, or a second DaemonSet with the same resources), or
+  // other device plugins -- a second AMD GPU plugin advertising amd.com/gpu
+  // makes the kubelet keep whichever registered last.
+  {
+    std::set<std::string> ours;
+    if (specs.ok())
+      for (const auto& spec : *specs) ours.insert(spec.socket_name);
+    std::string mine, others;
+    bool gpu_like = false;
+    if (DIR* dir = opendir(f.plugin_dir.c_str())) {
+      while (dirent* e = readdir(dir)) {
+        std::string name = e->d_name, path = PathJoin(f.plugin_dir, name);
+        struct stat sst;
+        if (path == ksock || stat(path.c_str(), &sst) != 0 || !S_ISSOCK(sst.st_mode) || !SocketLive(path)) continue;
+        std::string& list = ours.count(name) ? mine : others;
+        list += (list.empty() ? "" : ", ") + name;
+        if (!ours.count(name) && (ToLower(name).find("amd") != std::string::npos ||
+                                  ToLower(name).find("gpu") != std::string::npos))
+          gpu_like = true;
+      }
+      closedir(dir);
+    }
+    if (!mine.empty())
+      d.Line("warn", "plugin sockets: another instance of this plugin serves " + mine +
+                         " (a rollout in progress, or a second DaemonSet); starting this one takes them over");
+    if (!others.empty())
+      d.Line(gpu_like ? "warn" : "ok",
+             "other device plugins serve here: " + others +
+                 (gpu_like ? " -- if one of them also advertises this plugin's resources, the kubelet keeps "
+                             "whichever registered last: run one GPU plugin per node"
+                           : ""));
   }
   if (f.enforce_memory_units) {
     std::string src = MemcapSource(f);

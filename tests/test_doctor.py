@@ -94,3 +94,39 @@ def test_python_cli_doctor(tmp_path):
     r = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "doctor", "--device-plugin-path",
                         str(tmp_path)], capture_output=True, text=True, timeout=60, env=env)
     assert r.returncode == 0 and "enumeration: 1 GPU(s)" in r.stdout, r.stdout + r.stderr
+
+
+def test_other_plugins_and_a_running_instance_are_reported(tmp_path):
+    """Live sockets in the kubelet's directory: a running instance of this
+    plugin (warn: starting another takes its sockets over), another GPU plugin
+    (warn: the kubelet keeps whichever registered last), a non-GPU plugin (ok);
+    a stale socket file nobody listens on is not reported."""
+    import socket as so
+    from k8s_gpu_sharing_plugin_amd.utils import harness
+    d = tmp_path / "dp"
+    d.mkdir()
+    k = kubelet.StubKubelet(str(d / "kubelet.sock")).start()
+    running = harness.Daemon(str(d), fixtures.node(2), args=["--resource-config", "gpu:sharedgpu:4"]).start()
+    socks = []
+    try:
+        k.wait_registration()
+        for name, listen in (("amd.com_gpu", True), ("rdma-hca.sock", True), ("stale-gpu.sock", False)):
+            s = so.socket(so.AF_UNIX, so.SOCK_STREAM)
+            s.bind(str(d / name))
+            if listen:
+                s.listen(1)
+                socks.append(s)
+            else:
+                s.close()  # the file stays, nothing listens
+        rc, lines = _doctor(tmp_path, "--device-plugin-path", str(d), "--resource-config", "gpu:sharedgpu:4")
+    finally:
+        for s in socks:
+            s.close()
+        running.stop()
+        k.stop()
+    mine = _find(lines, "another instance of this plugin serves")
+    assert mine and mine.startswith("warn") and "amd-gpu.sock" in mine, lines
+    other = _find(lines, "other device plugins serve here")
+    assert other.startswith("warn") and "amd.com_gpu" in other and "rdma-hca.sock" in other, lines
+    assert "stale-gpu.sock" not in other
+    assert rc == 0, lines  # warnings, not failures
