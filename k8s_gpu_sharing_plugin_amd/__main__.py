@@ -112,6 +112,24 @@ def _status(args) -> int:
     def by(name):
         return [(ls, v) for n, ls, v in samples if n == name]
 
+    # /stats on the same port has the residency at 100 ns resolution
+    fine = {}
+    try:
+        with urllib.request.urlopen(url.rsplit("/", 1)[0] + "/stats", timeout=5) as r:
+            for p in json.loads(r.read()).get("plugins", []):
+                fine[p["resource"]] = sorted((int(b), int(n)) for b, n in p.get("residency_100ns", []))
+    except (OSError, ValueError):
+        pass
+
+    def fine_q(bins, q):
+        total = sum(n for _, n in bins)
+        seen = 0
+        for b, n in bins:
+            seen += n
+            if seen >= q * total:
+                return (b + 1) / 10
+        return None
+
     build = by("amdgpu_dp_build_info")
     if build:
         print("amdgpu-device-plugin " + " ".join(f"{k}={v}" for k, v in sorted(build[0][0].items())))
@@ -127,6 +145,8 @@ def _status(args) -> int:
                    for l2, v in by("amdgpu_dp_rpc_residency_seconds_bucket") if l2.get("resource") == res]
         p50, p99 = _quantile(buckets, 0.5), _quantile(buckets, 0.99)
         resid = "-" if p50 is None else f"<={p50 * 1e6:g} / <={p99 * 1e6:g}"
+        if fine.get(res):
+            resid = f"{fine_q(fine[res], 0.5):.1f} / {fine_q(fine[res], 0.99):.1f}"
         print(f"{res:<28} {int(n):>7} {int(one('amdgpu_dp_healthy_devices')):>7} "
               f"{int(one('amdgpu_dp_allocatable')):>11} {'yes' if one('amdgpu_dp_registered') else 'no':>10} "
               f"{int(one('amdgpu_dp_rpc_total', {'method': 'Allocate'})):>9} "
