@@ -24,3 +24,16 @@ def test_idle_daemon_sleeps(enforce, capsys):
     assert res["context_switches_per_s"] < 40, res
     assert res["cpu_pct_of_a_core"] < 5, res
     assert res["threads"] < 20 and res["rss_mib"] < 64, res
+
+
+def test_health_event_reaches_the_kubelet_fast(capsys):
+    """tools/health_latency.py: a GPU_PRE_RESET on one of 8 GPUs reaches the
+    kubelet as an Unhealthy device list, and GPU_POST_RESET as Healthy, within
+    milliseconds (the event path: amdsmi wait -> ledger -> ListAndWatch)."""
+    import json
+    import health_latency
+    assert health_latency.main(["--rounds", "8"]) == 0
+    res = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert res["advertised"] == 32
+    for k in ("event_to_unhealthy", "event_to_healthy"):
+        assert res[k]["n"] == 8 and res[k]["median_ms"] < 50 and res[k]["max_ms"] < 1000, res
