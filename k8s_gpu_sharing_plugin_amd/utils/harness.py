@@ -40,14 +40,14 @@ class Daemon:
 
     def start(self):
         self._log = open(self.log_path, "w")
-        preexec = None
+        argv = [DAEMON, "--device-plugin-path", self.plugin_dir, *self.args]
         if self.nofile:
-            import resource
-            lim = self.nofile
-            preexec = lambda: resource.setrlimit(resource.RLIMIT_NOFILE, (lim, lim))  # noqa: E731
-        self.proc = subprocess.Popen([DAEMON, "--device-plugin-path", self.plugin_dir, *self.args],
-                                     env=self.env, stdout=self._log, stderr=subprocess.STDOUT,
-                                     preexec_fn=preexec)
+            # The limit is set by a shell that then execs the daemon (same pid).
+            # A preexec_fn would run Python between fork and exec, which can
+            # deadlock on a lock another thread (the stub kubelet's gRPC
+            # threads, the import lock) held at fork time.
+            argv = ["/bin/sh", "-c", 'ulimit -n %d && exec "$0" "$@"' % int(self.nofile), *argv]
+        self.proc = subprocess.Popen(argv, env=self.env, stdout=self._log, stderr=subprocess.STDOUT)
         return self
 
     def log(self) -> str:
