@@ -79,8 +79,15 @@ const std::vector<FlagDef>& Table() {
       {"replica-cu-mask", "REPLICA_CU_MASK", "replicaCuMask", Kind::kBool,
        "replicas also split the device's compute units (HSA_CU_MASK on Allocate): time-slice "
        "replica r of R runs on its own 1/R of every XCD's CUs; memory units get CUs in "
-       "proportion to the units held (proportional, not isolating: neighbours may share a boundary slot)",
+       "proportion to the units held (proportional: neighbours may share a boundary slot, unless "
+       "--memory-unit-cu-slots whole)",
        [](Flags& f) -> void* { return &f.replica_cu_mask; }},
+      {"memory-unit-cu-slots", "DP_MEMORY_UNIT_CU_SLOTS", "memoryUnitCuSlots", Kind::kString,
+       "with --replica-cu-mask, which CU slots a memory-unit container gets: [proportional | whole] "
+       "(whole: only the slots all of whose units it holds, so no two containers share a CU; a container "
+       "that fills no slot on a device falls back to its partial slots, counted in "
+       "amdgpu_dp_partial_cu_slot_allocations_total)",
+       [](Flags& f) -> void* { return &f.memory_unit_cu_slots; }},
       {"device-plugin-path", "DP_PLUGIN_DIR", "devicePluginPath", Kind::kString,
        "kubelet device-plugin directory",
        [](Flags& f) -> void* { return &f.plugin_dir; }},

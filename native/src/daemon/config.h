@@ -35,6 +35,7 @@ struct Flags {
   std::string resource_config;
   std::string replica_policy = "spread";
   bool replica_cu_mask = false;
+  std::string memory_unit_cu_slots = "proportional";
   std::string plugin_dir = "/var/lib/kubelet/device-plugins/";
   std::string kubelet_socket;  // default: <plugin_dir>/kubelet.sock
   std::string amdsmi_lib;

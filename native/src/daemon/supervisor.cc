@@ -154,6 +154,10 @@ Result<Validated> Validate(const Config& cfg) {
   v.popts.kubelet_socket = f.kubelet_socket;
   v.popts.pass_device_specs = f.pass_device_specs;
   v.popts.replica_cu_mask = f.replica_cu_mask;
+  if (f.memory_unit_cu_slots != "proportional" && f.memory_unit_cu_slots != "whole")
+    return InvalidArgument("invalid --memory-unit-cu-slots option: " + f.memory_unit_cu_slots +
+                           " (proportional | whole)");
+  v.popts.whole_cu_slots = f.memory_unit_cu_slots == "whole";
   if (f.http2_server != "native" && f.http2_server != "nghttp2")
     return InvalidArgument("invalid --http2-server option: " + f.http2_server);
   v.popts.native_http2 = f.http2_server == "native";

@@ -201,6 +201,10 @@ void Plugin::BuildUnits() {
     if (opts_.replica_cu_mask && replicated_) {
       u.replica_cus = memory_units_ ? MemoryUnitCuRanges(u.cus, u.xcds, u.replicas)
                                     : ReplicaCuRanges(u.cus, u.xcds, u.replicas);
+      if (memory_units_ && opts_.whole_cu_slots && !u.replica_cus.empty()) {
+        u.slot_units.assign(u.cus / u.xcds, 0);
+        for (const auto& rg : u.replica_cus) ++u.slot_units[rg.first / u.xcds];
+      }
       if (u.replica_cus.empty() && u.replicas > 1)
         LOG_WARN(kComp, "device %s: %u CUs over %u XCDs cannot be split into %u CU shares; its replicas "
                  "share all CUs", u.id.c_str(), u.cus, u.xcds, u.replicas);
@@ -466,21 +470,59 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       for (size_t ord = 0; ord < us.size(); ++ord) {
         while (k < shares.size() && shares[k].first < us[ord]) ++k;
         if (k == shares.size() || shares[k].first != us[ord]) continue;
-        const auto& ranges = units_[us[ord]].replica_cus;
+        const Unit& unit = units_[us[ord]];
+        const auto& ranges = unit.replica_cus;
+        size_t end = k;
+        while (end < shares.size() && shares[end].first == us[ord]) ++end;
+        // Shares are sorted by range and distinct; memory units share slots, so a
+        // run of equal ranges is the units of one slot this container holds.
+        auto run_end = [&](size_t g) {
+          size_t h = g + 1;
+          while (h < end && ranges[shares[h].second] == ranges[shares[g].second]) ++h;
+          return h;
+        };
+        auto filled = [&](size_t g, size_t h) {
+          return h - g == unit.slot_units[ranges[shares[g].second].first / unit.xcds];
+        };
+        // --memory-unit-cu-slots whole: keep only the slots whose units are all
+        // this container's, so no neighbour runs on them. A container filling no
+        // slot keeps its partial ones (it needs some CUs) and is counted.
+        bool whole_only = false;
+        if (!unit.slot_units.empty()) {
+          for (size_t g = k; g < end && !whole_only;) {
+            size_t h = run_end(g);
+            whole_only = filled(g, h);
+            g = h;
+          }
+          if (!whole_only) stats_.partial_cu_slot_allocations.Add(1);
+        }
         if (!cu_mask.empty()) cu_mask += ';';
         cu_mask += std::to_string(ord);
         char sep = ':';
-        while (k < shares.size() && shares[k].first == us[ord]) {
-          uint32_t lo = ranges[shares[k].second].first, hi = ranges[shares[k].second].second;
-          // Shares are sorted by range; memory units share slots, so equal and
-          // adjacent ranges both merge.
-          for (++k; k < shares.size() && shares[k].first == us[ord] &&
-                    ranges[shares[k].second].first <= hi + 1; ++k)
-            hi = std::max(hi, ranges[shares[k].second].second);
+        bool open = false;
+        uint32_t lo = 0, hi = 0;
+        auto emit = [&] {
           cu_mask += sep;
           cu_mask += std::to_string(lo) + "-" + std::to_string(hi);
           sep = ',';
+        };
+        for (size_t g = k; g < end;) {
+          size_t h = run_end(g);
+          const auto& rg = ranges[shares[g].second];
+          bool keep = !whole_only || filled(g, h);
+          g = h;
+          if (!keep) continue;
+          if (open && rg.first <= hi + 1) {  // equal and adjacent ranges merge
+            hi = std::max(hi, rg.second);
+            continue;
+          }
+          if (open) emit();
+          lo = rg.first;
+          hi = rg.second;
+          open = true;
         }
+        if (open) emit();
+        k = end;
       }
     }
     if (opts_.id_strategy == DeviceIdStrategy::kUuid)
@@ -1067,6 +1109,12 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
   for (auto* p : plugins)
     gauge("amdgpu_dp_unhealthy_allocations_total", res(p),
           static_cast<double>(p->stats_.unhealthy_allocations.Value()));
+  family("amdgpu_dp_partial_cu_slot_allocations_total", "counter",
+         "Container devices that filled no whole CU slot under --memory-unit-cu-slots whole and got their "
+         "partial (shared) slots.");
+  for (auto* p : plugins)
+    gauge("amdgpu_dp_partial_cu_slot_allocations_total", res(p),
+          static_cast<double>(p->stats_.partial_cu_slot_allocations.Value()));
   family("amdgpu_dp_prestart_refusals_total", "counter",
          "Container starts refused because a device was Unhealthy (--prestart-health-check).");
   for (auto* p : plugins)

@@ -99,6 +99,9 @@ struct PluginOptions {
   // 1/R of every XCD's CUs (HSA_CU_MASK), so co-scheduled pods stop contending
   // for the same CUs -- the MI355X analogue of an MPS active-thread share.
   bool replica_cu_mask = false;
+  // With replica_cu_mask, memory units: a container gets only the CU slots all
+  // of whose units it holds (isolating), not every slot it touches.
+  bool whole_cu_slots = false;
   bool native_http2 = true;  // HTTP/2 engine of the plugin sockets (false: nghttp2)
   bool follow_peer_l3 = true;  // loops serve a connection from the caller's L3
   // Allocate() of a device currently advertised Unhealthy: false = allocate it
@@ -174,6 +177,8 @@ struct Unit {
   uint32_t cus = 0, xcds = 0;      // compute units / XCDs of this GPU or partition
   // --replica-cu-mask: CU bit range of each replica (empty = whole device).
   std::vector<std::pair<uint32_t, uint32_t>> replica_cus;
+  // --memory-unit-cu-slots whole: how many units own each CU slot (empty otherwise).
+  std::vector<uint16_t> slot_units;
 };
 
 // Written by every server loop on every call: sharded per thread (metrics.h).
@@ -186,6 +191,7 @@ struct RpcStats {
   metrics::MaxGauge preferred_ns_max;
   metrics::Counter law_sends;
   metrics::Counter unhealthy_allocations;  // Allocate() calls that named an Unhealthy device
+  metrics::Counter partial_cu_slot_allocations;  // whole CU slots asked for, none filled on a device
   metrics::Counter prestart_refusals;      // container starts refused by --prestart-health-check
   metrics::Histogram allocate_hist;   // handler time (decode + lookup + encode)
   metrics::Histogram preferred_hist;

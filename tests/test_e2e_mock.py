@@ -4,7 +4,11 @@ kubelet receives Register(amd.com/gpu), opens ListAndWatch, sees 2 Healthy
 devices, Allocate(1) returns DeviceSpecs [/dev/kfd, /dev/dri/renderD128].
 """
 
+import collections
 import os
+import re
+import subprocess
+import urllib.request
 
 import grpc
 import pytest
@@ -324,3 +328,67 @@ def test_memory_unit_cu_shares_overlap_at_most_one_boundary_slot(running, scratc
             if shared:  # a boundary of both runs
                 (s_,) = shared
                 assert s_ in (min(slots[i]), max(slots[i])) and s_ in (min(slots[j]), max(slots[j]))
+
+
+def _slot_model(ids, units=294, per=32):
+    """The k-th unit ID in name order owns slot k*per//units (plugin.cc
+    MemoryUnitCuRanges): slot of each ID and the number of units per slot."""
+    num = {i: int(re.search(r"(\d+)$", i).group(1)) for i in ids}
+    by_name = sorted(ids, key=lambda i: str(num[i]))
+    slot = {i: k * per // units for k, i in enumerate(by_name)}
+    size = collections.Counter(slot.values())
+    return slot, size
+
+
+@pytest.mark.parametrize("sizes", [[36, 36, 222], [36] * 8 + [6], [1] * 40, [5, 13, 1, 40, 9, 2, 100, 3],
+                                   [10] * 29, [19] * 15])
+def test_whole_cu_slots_never_share_a_cu(running, scratch, sizes):
+    """--memory-unit-cu-slots whole: a container gets only the CU slots all of
+    whose units it holds, so two containers that each fill a slot never share a
+    CU; one that fills none keeps its partial slots and is counted in
+    amdgpu_dp_partial_cu_slot_allocations_total. Checked against a model of the
+    slot map for every pod, admitted the kubelet's way (pack)."""
+    d, k = running(fixture=fixtures.node(1), args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy",
+                                                   "pack", "--replica-cu-mask", "--memory-unit-cu-slots", "whole",
+                                                   "--metrics-addr", "127.0.0.1:0"])
+    port = int(re.search(r"serving /metrics and /healthz on port (\d+)",
+                         d.wait_log("serving /metrics and /healthz on port")).group(1))
+    reg = k.wait_registration()
+    c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+    free = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+    slot_of, slot_size = _slot_model(free)
+    owned, partial = [], 0
+    for size in sizes:
+        ids = list(c.preferred(free, size=size).container_responses[0].deviceIDs)
+        for i in ids:
+            free.remove(i)
+        held = collections.Counter(slot_of[i] for i in ids)
+        whole = {s for s, n in held.items() if n == slot_size[s]}
+        want = whole or set(held)
+        partial += not whole
+        mask = dict(c.allocate(ids).container_responses[0].envs)["HSA_CU_MASK"]
+        agent, ranges = mask.split(":")
+        got = set()
+        for r in ranges.split(","):
+            lo, hi = map(int, r.split("-"))
+            assert lo % 8 == 0 and (hi + 1) % 8 == 0, mask
+            got |= set(range(lo // 8, (hi + 1) // 8))
+        assert agent == "0" and got == want, (size, mask, sorted(want))
+        if size >= 19:  # any 19 consecutive units fill a slot (at most 10 units each)
+            assert whole, (size, sorted(held.items()))
+        if whole:
+            owned.append(got)
+    c.close()
+    for i in range(len(owned)):
+        for j in range(i + 1, len(owned)):
+            assert not owned[i] & owned[j], (sorted(owned[i]), sorted(owned[j]))
+    with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
+        text = r.read().decode()
+    assert f'amdgpu_dp_partial_cu_slot_allocations_total{{resource="amd.com/gpu-mem-gb"}} {partial}' in text, partial
+
+
+def test_memory_unit_cu_slots_rejects_unknown_modes(scratch):
+    r = subprocess.run([harness.DAEMON, "--device-plugin-path", scratch, "--memory-unit-cu-slots",
+                        "exclusive", "--dry-run"], capture_output=True, text=True, timeout=30,
+                       env=harness.Daemon(scratch, fixtures.node(1)).env)
+    assert r.returncode != 0 and "invalid --memory-unit-cu-slots option: exclusive" in r.stdout + r.stderr

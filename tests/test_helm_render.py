@@ -199,6 +199,13 @@ def test_partition_strategies(strategy):
     check_consistent(ds)
     assert env(ds)["PARTITION_STRATEGY"] == strategy
     assert "RESOURCE_CONFIG" not in env(ds) and env(ds)["REPLICA_CU_MASK"] == "true"
+    assert env(ds)["DP_MEMORY_UNIT_CU_SLOTS"] == "proportional"
+
+
+def test_memory_unit_cu_slots_value():
+    ds = daemonset({"replicaCuMask": True, "memoryUnitCuSlots": "whole"})
+    check_consistent(ds)
+    assert env(ds)["DP_MEMORY_UNIT_CU_SLOTS"] == "whole" and env(ds)["REPLICA_CU_MASK"] == "true"
 
 
 def test_renderer_trims_and_pipes_like_go_templates():
