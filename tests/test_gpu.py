@@ -638,10 +638,12 @@ def test_replica_cu_shares_isolate_a_noisy_neighbour(scratch, snap, probe_built)
     assert shared["p50_us"] < 1.5 * solo["p50_us"], (solo, shared)
 
 
-def test_memory_unit_cu_share_on_mi355x(scratch, snap, probe_built):
+@pytest.mark.parametrize("slots,mask,per_xcd", [("proportional", "0:0-63", 8), ("whole", "0:0-55", 7)])
+def test_memory_unit_cu_share_on_mi355x(scratch, snap, probe_built, slots, mask, per_xcd):
     """gpu-mem-gb + --replica-cu-mask on the MI355X: a 72-unit (72 GB) pod admitted
-    through GetPreferredAllocation (pack) owns CU slots 0-7, so its census shows
-    64 CUs, 8 on every XCD."""
+    through GetPreferredAllocation (pack) touches CU slots 0-7, so its census shows
+    64 CUs, 8 on every XCD; with --memory-unit-cu-slots whole it keeps only slots
+    0-6 (slot 7's units 65-73 are split with the next pod): 56 CUs, 7 per XCD."""
     import json
     import subprocess
     from k8s_gpu_sharing_plugin_amd.utils.build import PROBE_EXE
@@ -649,7 +651,8 @@ def test_memory_unit_cu_share_on_mi355x(scratch, snap, probe_built):
         pytest.skip("box GPU is partitioned")
     k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
     d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--resource-config", "gpu:gpu-mem-gb:-1",
-                                                     "--replica-policy", "pack", "--replica-cu-mask"]).start()
+                                                     "--replica-policy", "pack", "--replica-cu-mask",
+                                                     "--memory-unit-cu-slots", slots]).start()
     try:
         reg = k.wait_registration(30)
         c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
@@ -660,12 +663,12 @@ def test_memory_unit_cu_share_on_mi355x(scratch, snap, probe_built):
     finally:
         assert d.stop() == 0
         k.stop()
-    assert envs["HSA_CU_MASK"] == "0:0-63" and envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "72000"
+    assert envs["HSA_CU_MASK"] == mask and envs["AMD_GPU_MEMORY_LIMIT_MIB"] == "72000"
     env = {**{k: v for k, v in os.environ.items() if k != "HSA_CU_MASK"}, "HSA_CU_MASK": envs["HSA_CU_MASK"]}
-    r = subprocess.run([PROBE_EXE, "--device", "0", "--census", "--expect-cus-seen", "64"], env=env,
+    r = subprocess.run([PROBE_EXE, "--device", "0", "--census", "--expect-cus-seen", str(8 * per_xcd)], env=env,
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
-    assert json.loads(r.stdout.strip().splitlines()[-1])["per_xcc"] == [8] * 8
+    assert json.loads(r.stdout.strip().splitlines()[-1])["per_xcc"] == [per_xcd] * 8
 
 
 def test_pytorch_matmul_runs_on_its_cu_share(snap):
