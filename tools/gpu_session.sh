@@ -22,6 +22,8 @@
 #                SQ_INSTS_VALU_MFMA_BF16)
 #   census       HSA_CU_MASK -> XCD/CU census of the probe (quarter shares)
 #   interference noisy-neighbour victim latency with and without CU shares
+#   unitslots    the interference pair for two packed 36 GB memory-unit pods,
+#                proportional (one shared CU slot) vs --memory-unit-cu-slots whole
 #   floor        UDS ping-pong floor, busy-poll on and off
 #   spread       10 back-to-back headline runs (bench.py --no-probe); line:
 #                R i p50 p99 grpc-go grpcio pods/s relation client_cpu loop_cpu
@@ -124,6 +126,14 @@ step_interference() {
   lat_one solo_quarter "0:0-63" none
   lat_one shared_nomask "" ""
   lat_one shared_masked "0:0-63" "0:64-255"
+}
+step_unitslots() {
+  # Two packed 36 GB memory-unit pods (the masks tests/test_e2e_mock.py pins):
+  # proportional shares slot 3 (CUs 24-31), --memory-unit-cu-slots whole not.
+  lat_one units_prop_solo "0:0-31" none
+  lat_one units_prop_shared "0:0-31" "0:24-63"
+  lat_one units_whole_solo "0:0-23" none
+  lat_one units_whole_shared "0:0-23" "0:32-55"
 }
 step_floor() {
   for b in 50 0; do
