@@ -1,7 +1,8 @@
 // Coverage-guided fuzzing (libFuzzer) of the kubelet-facing RPC handlers:
 // Allocate, GetPreferredAllocation and PreStartContainer of the plugins the
 // daemon builds for BASELINE.json's node shapes (8 x SPX; 4 time-slice
-// replicas per GPU; 64 CPX partitions; 2,352 memory units, spread and pack).
+// replicas per GPU; 64 CPX partitions; 2,352 memory units, spread and pack;
+// CU shares of time-slice replicas and of memory units, proportional and whole).
 //
 // Two kinds of input: raw request bytes (the protobuf decoder and every error
 // path), and a request built from the input over the plugin's own advertised
@@ -11,7 +12,9 @@
 //     one; the same request answered again (a best-effort cache hit for up to
 //     8 devices) gives the same answer.
 //   * Allocate: OK exactly when every ID is advertised, one container response
-//     per container request, /dev/kfd in every response.
+//     per container request, /dev/kfd in every response; an HSA_CU_MASK names
+//     each agent once, in order, with ascending, disjoint, XCD-aligned ranges
+//     inside the device's CUs.
 // The reference's equivalents panic on a required list longer than the
 // request (B12) and answer bare UUIDs for replicated resources (B6).
 #include <fuzzer/FuzzedDataProvider.h>
@@ -37,6 +40,7 @@ struct Shape {
   strategy::PartitionStrategy ps;
   const char* rc;
   alloc::ReplicaPolicy pol;
+  bool cu_mask = false, whole = false;
 };
 
 std::vector<std::unique_ptr<plugin::Plugin>>& Plugins() {
@@ -50,6 +54,9 @@ std::vector<std::unique_ptr<plugin::Plugin>>& Plugins() {
         {8, 1, strategy::PartitionStrategy::kNone, "gpu:gpu-mem-gb:-1", alloc::ReplicaPolicy::kSpread},
         {8, 1, strategy::PartitionStrategy::kNone, "gpu:gpu-mem-gb:-1", alloc::ReplicaPolicy::kPack},
         {2, 1, strategy::PartitionStrategy::kNone, "gpu:gpu:3", alloc::ReplicaPolicy::kPack},
+        {8, 1, strategy::PartitionStrategy::kNone, "gpu:sharedgpu:4", alloc::ReplicaPolicy::kSpread, true},
+        {8, 1, strategy::PartitionStrategy::kNone, "gpu:gpu-mem-gb:-1", alloc::ReplicaPolicy::kPack, true},
+        {8, 1, strategy::PartitionStrategy::kNone, "gpu:gpu-mem-gb:-1", alloc::ReplicaPolicy::kPack, true, true},
     };
     for (const auto& s : shapes) {
       auto snap = testing::NodeModel(s.gpus, s.parts);
@@ -58,6 +65,8 @@ std::vector<std::unique_ptr<plugin::Plugin>>& Plugins() {
       plugin::PluginOptions po;
       po.register_with_kubelet = false;
       po.replica_policy = s.pol;
+      po.replica_cu_mask = s.cu_mask;
+      po.whole_cu_slots = s.whole;
       v->push_back(std::make_unique<plugin::Plugin>(snap, (*specs)[0], po));
     }
     return v;
@@ -142,6 +151,40 @@ void CheckPreferred(plugin::Plugin& p, FuzzedDataProvider& in) {
   if (!p.HandlePreferred(wire, &again).ok() || again != resp) Fail("same request, different answer");
 }
 
+// HSA_CU_MASK="<agent>:<lo>-<hi>,...;...": agents ascending, each once;
+// ranges ascending, disjoint, non-adjacent (adjacent ones merge), whole slots
+// (one CU per XCD) inside the device.
+void CheckCuMask(const plugin::Plugin& p, const pb::ContainerAllocateResponse& cr) {
+  auto it = std::find_if(cr.envs.begin(), cr.envs.end(), [](const auto& kv) { return kv.first == "HSA_CU_MASK"; });
+  if (it == cr.envs.end()) return;
+  const std::string& m = it->second;
+  const auto& u0 = p.units().front();
+  long last_agent = -1;
+  for (size_t b = 0; b < m.size();) {
+    size_t e = std::min(m.find(';', b), m.size());
+    std::string part = m.substr(b, e - b);
+    b = e + 1;
+    size_t colon = part.find(':');
+    if (colon == std::string::npos || colon == 0) Fail("HSA_CU_MASK agent without ':'");
+    long agent = strtol(part.substr(0, colon).c_str(), nullptr, 10);
+    if (agent <= last_agent) Fail("HSA_CU_MASK agents not ascending");
+    last_agent = agent;
+    long prev_hi = -2;
+    for (size_t rb = colon + 1; rb <= part.size();) {
+      size_t re = std::min(part.find(',', rb), part.size());
+      std::string r = part.substr(rb, re - rb);
+      rb = re + 1;
+      size_t dash = r.find('-');
+      if (dash == std::string::npos) Fail("HSA_CU_MASK range without '-'");
+      long lo = strtol(r.substr(0, dash).c_str(), nullptr, 10), hi = strtol(r.substr(dash + 1).c_str(), nullptr, 10);
+      if (lo > hi || lo <= prev_hi + 1) Fail("HSA_CU_MASK ranges not ascending and disjoint");
+      if (lo % u0.xcds != 0 || (hi + 1) % u0.xcds != 0) Fail("HSA_CU_MASK range not XCD-aligned");
+      if (hi >= static_cast<long>(u0.cus)) Fail("HSA_CU_MASK range past the device's CUs");
+      prev_hi = hi;
+    }
+  }
+}
+
 void CheckAllocate(plugin::Plugin& p, FuzzedDataProvider& in) {
   const auto& ids = p.advertised_ids();
   pb::AllocateRequest req;
@@ -170,6 +213,7 @@ void CheckAllocate(plugin::Plugin& p, FuzzedDataProvider& in) {
     bool kfd = std::any_of(cr.devices.begin(), cr.devices.end(),
                            [](const pb::DeviceSpec& d) { return d.container_path == "/dev/kfd"; });
     if (!kfd) Fail("no /dev/kfd in an Allocate response");
+    CheckCuMask(p, cr);
     // Memory units: the grant is 1000 MiB per distinct ID, whatever is repeated.
     auto mib = std::find_if(cr.envs.begin(), cr.envs.end(),
                             [](const auto& kv) { return kv.first == "AMD_GPU_MEMORY_LIMIT_MIB"; });
