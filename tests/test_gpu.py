@@ -638,6 +638,57 @@ def test_replica_cu_shares_isolate_a_noisy_neighbour(scratch, snap, probe_built)
     assert shared["p50_us"] < 1.5 * solo["p50_us"], (solo, shared)
 
 
+def test_whole_cu_slots_isolate_memory_unit_neighbours(scratch, snap, probe_built):
+    """--memory-unit-cu-slots whole on the MI355X: two packed 36 GB memory-unit
+    pods get disjoint CU slots (0:0-23, 0:32-55), so the first keeps its solo
+    kernel latency while the second saturates its CUs. (Proportional slots share
+    slot 3 and the victim measured 130 -> 988 us p50, profiles/r3/README.md.)"""
+    import json
+    import subprocess
+    import time
+    from k8s_gpu_sharing_plugin_amd.utils.build import PROBE_EXE
+    if snap["gpus"][0]["partitioned"]:
+        pytest.skip("box GPU is partitioned")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--resource-config", "gpu:gpu-mem-gb:-1",
+                                                     "--replica-policy", "pack", "--replica-cu-mask",
+                                                     "--memory-unit-cu-slots", "whole"]).start()
+    try:
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        free = [x.ID for x in c.watch()[0].get(timeout=10).devices]
+        masks = []
+        for _ in range(2):
+            ids = list(c.preferred(free, size=36).container_responses[0].deviceIDs)
+            for i in ids:
+                free.remove(i)
+            masks.append(dict(c.allocate(ids).container_responses[0].envs)["HSA_CU_MASK"])
+        c.close()
+    finally:
+        assert d.stop() == 0
+        k.stop()
+    assert masks == ["0:0-23", "0:32-55"]
+    victim, noisy = masks
+    base = {k: v for k, v in os.environ.items() if k != "HSA_CU_MASK"}
+
+    def latency():
+        r = subprocess.run([PROBE_EXE, "--device", "0", "--latency", "1000"], env={**base, "HSA_CU_MASK": victim},
+                           capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    solo = latency()
+    agg = subprocess.Popen([PROBE_EXE, "--device", "0", "--aggressor", "5"], env={**base, "HSA_CU_MASK": noisy},
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(1.0)
+        shared = latency()
+    finally:
+        out, err = agg.communicate(timeout=60)
+    assert agg.returncode == 0, err[-2000:]
+    assert json.loads(out.strip().splitlines()[-1])["aggressor_launches"] > 100
+    assert shared["p50_us"] < 1.5 * solo["p50_us"], (solo, shared)
+
+
 @pytest.mark.parametrize("slots,mask,per_xcd", [("proportional", "0:0-63", 8), ("whole", "0:0-55", 7)])
 def test_memory_unit_cu_share_on_mi355x(scratch, snap, probe_built, slots, mask, per_xcd):
     """gpu-mem-gb + --replica-cu-mask on the MI355X: a 72-unit (72 GB) pod admitted
