@@ -361,14 +361,22 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
   if (!specs.ok()) {
     d.Line("FAIL", "partition strategy: " + specs.status().message());
   } else {
-    std::string what;
+    std::string what, unit_cus;
     for (const auto& spec : *specs) {
       plugin::Plugin p(*snap, spec, v.popts);
       if (p.device_count() == 0) continue;
       what += (what.empty() ? "" : ", ") + spec.resource_name + " x" + std::to_string(p.advertised_count());
+      if (spec.variant.auto_replicas && !p.units().empty() && !p.units().front().replica_cus.empty())
+        unit_cus = spec.resource_name;
     }
     if (what.empty()) d.Line("FAIL", "resources: none would be advertised (partition strategy / --devices)");
     else d.Line("ok", "resources: " + what);
+    if (!unit_cus.empty() && v.popts.whole_cu_slots)
+      d.Line("ok", "CU shares: " + unit_cus + " pods get only the CU slots their units fill (disjoint)");
+    else if (!unit_cus.empty())
+      d.Line("warn", "CU shares: " + unit_cus + " pods get proportional CU slots, so packed neighbours can share "
+                     "a boundary slot and slow each other's kernels -- --memory-unit-cu-slots whole (helm "
+                     "memoryUnitCuSlots: whole) makes them disjoint");
   }
   auto nodes = inventory::ProbeDeviceAccess(s, f.driver_root);
   std::string acc = inventory::DescribeAccess(nodes);

@@ -3,6 +3,8 @@ line per check ("ok" / "warn" / "FAIL") with what to change; exit 1 on a
 failure. Real hardware: tests/test_gpu.py::test_doctor_on_real_gpu."""
 
 import os
+
+import pytest
 import subprocess
 
 from k8s_gpu_sharing_plugin_amd import DAEMON, MOCK_LIB
@@ -130,3 +132,18 @@ def test_other_plugins_and_a_running_instance_are_reported(tmp_path):
     assert other.startswith("warn") and "amd.com_gpu" in other and "rdma-hca.sock" in other, lines
     assert "stale-gpu.sock" not in other
     assert rc == 0, lines  # warnings, not failures
+
+
+@pytest.mark.parametrize("slots,level", [("proportional", "warn"), ("whole", "ok")])
+def test_doctor_reports_memory_unit_cu_slots(tmp_path, slots, level):
+    """Memory units with CU shares: proportional slots are a warning (packed
+    neighbours can share a slot), whole slots are disjoint; no line without
+    --replica-cu-mask."""
+    d = tmp_path / "dp"
+    d.mkdir()
+    args = ["--device-plugin-path", str(d), "--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack"]
+    _, lines = _doctor(tmp_path, *args, "--replica-cu-mask", "--memory-unit-cu-slots", slots)
+    line = _find(lines, "CU shares:")
+    assert line and line.split()[0] == level and "amd.com/gpu-mem-gb" in line, lines
+    _, lines = _doctor(tmp_path, *args)
+    assert _find(lines, "CU shares:") is None
