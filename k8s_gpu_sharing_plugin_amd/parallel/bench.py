@@ -201,6 +201,25 @@ def _bdf_map(snap):
     return out
 
 
+def _device_order(snap, rank_bdfs):
+    """The three orders of the served GPUs: amdsmi's enumeration, KFD topology
+    node (what the plugin orders every per-device container list by: HSA_CU_MASK
+    agents, AMD_GPU_MEMORY_* and grant/<i>) and HIP's -- rank r binds HIP device
+    r, so rank_bdfs is HIP's order of the first N devices. On a multi-GPU node
+    this records whether HIP really follows KFD node order."""
+    gpus = snap["gpus"]
+    amdsmi = [g["bdf"] for g in gpus]
+    known = all(g.get("kfd_node") is not None for g in gpus)
+    kfd = [g["bdf"] for g in sorted(gpus, key=lambda g: g["kfd_node"])] if known else None
+    hip = list(dict.fromkeys(rank_bdfs))
+    out = {"amdsmi_order": amdsmi, "kfd_order": kfd, "hip_order": hip,
+           "kfd_order_differs_from_amdsmi": None if kfd is None else kfd != amdsmi}
+    if sorted(hip) == sorted(amdsmi):  # HIP's view of exactly the served set
+        out["hip_order_is_kfd_order"] = None if kfd is None else hip == kfd
+        out["hip_order_is_amdsmi_order"] = hip == amdsmi
+    return out
+
+
 def _topology(snap, rank_bdfs):
     """The node block of the JSON: what GetPreferredAllocation scores against."""
     if not snap:
@@ -209,9 +228,12 @@ def _topology(snap, rank_bdfs):
         "amdsmi": snap.get("smi_version"),
         "rank_bdfs": rank_bdfs,
         "served_bdfs": [g["bdf"] for g in snap["gpus"]],
+        "device_order": _device_order(snap, rank_bdfs),
         "gpus": [{"bdf": g["bdf"], "uuid": g["uuid"], "product": g.get("market_name"),
                   "compute_mode": g["compute_mode"], "memory_mode": g["memory_mode"],
                   "partitions": len(g["partitions"]), "numa": g["numa"], "vram_mib": g["vram_mib"],
+                  "kfd_node": g.get("kfd_node"),
+                  "hip_id": (g["partitions"][0].get("hip_id") if g["partitions"] else None),
                   "xgmi_links_down": g["xgmi_links_down"]} for g in snap["gpus"]],
         # rows/columns in served_bdfs order
         "link_types": snap.get("link_types"),

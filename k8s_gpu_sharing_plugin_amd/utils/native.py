@@ -23,7 +23,8 @@ def lib() -> ctypes.CDLL:
         raise NativeError(f"{CAPI_LIB} not built; run `python -m k8s_gpu_sharing_plugin_amd.utils.build`")
     so = ctypes.CDLL(CAPI_LIB)
     for name in ("adp_prioritize", "adp_strip_replicas", "adp_parse_additional_ids",
-                 "adp_parse_resource_config", "adp_best_effort", "adp_snapshot", "adp_plugin_specs"):
+                 "adp_parse_resource_config", "adp_best_effort", "adp_snapshot", "adp_plugin_specs",
+                 "adp_driver_scan"):
         fn = getattr(so, name)
         fn.argtypes = [ctypes.c_char_p]
         fn.restype = ctypes.c_void_p
@@ -65,6 +66,12 @@ def prioritize(available, must_include, size, policy="spread"):
     res = _check(_call("adp_prioritize", {"available": list(available), "must_include": list(must_include),
                                            "size": size, "policy": policy}))
     return res["ids"], res["non_unique"]
+
+
+def driver_scan(proc_root, kfd_proc_dir="", usage_dir="", self_cgroup=""):
+    """One driver-side HBM scan (memcap::ScanDriverHbm) of a /proc tree."""
+    return _check(_call("adp_driver_scan", {"proc_root": proc_root, "kfd_proc_dir": kfd_proc_dir,
+                                            "usage_dir": usage_dir, "self_cgroup": self_cgroup}))
 
 
 def strip_replicas(ids):

@@ -26,6 +26,10 @@
 //                     one node per memory partition (numa*NPS + pool index)
 //                 "report_profile": true,       amdsmi_get_gpu_accelerator_partition_profile
 //                 "report_numa_ranges": true,   amdsmi_get_gpu_memory_partition_config
+//                 "kfd_node": 2 + 8*i,          KFD topology node of partition 0 (partition p
+//                     is kfd_node + p): the order ROCr/HIP number the GPUs in, which
+//                     need not be amdsmi's enumeration order ("kfd_node": null =
+//                     amdsmi_get_gpu_kfd_info reports node_id unsupported)
 //               } ] }
 // Runtime injection:
 //   event FIFO lines: "<gpu>[:<partition>] <event-type> [message]"
@@ -81,6 +85,7 @@ struct MockProc {
   bool report_profile = true;
   bool report_numa_ranges = true;
   int links_down = 0;
+  int64_t kfd_node = 0;         // -1: node_id not reported
   bool evt_init = false;
   uint64_t evt_mask = 0;
 };
@@ -227,6 +232,8 @@ bool Load() {
       mp->cmode = cmode;
       mp->mmode = mmode;
       mp->links_down = jg.value("xgmi_links_down", 0);
+      if (jg.count("kfd_node") && jg["kfd_node"].is_null()) mp->kfd_node = -1;
+      else mp->kfd_node = jg.value("kfd_node", static_cast<int64_t>(2 + gi * 8)) + p;
       mg.procs.push_back(mp.get());
       g->procs.push_back(std::move(mp));
     }
@@ -375,13 +382,18 @@ amdsmi_status_t amdsmi_get_gpu_enumeration_info(amdsmi_processor_handle h,
   memset(info, 0, sizeof(*info));
   info->drm_render = p->render;
   info->drm_card = p->card;
-  uint32_t idx = 0;
+  // HIP/HSA number GPUs in KFD topology-node order, not amdsmi's: the rank of
+  // this processor's node among all nodes (amdsmi order when none is reported).
+  uint32_t idx = 0, rank = 0;
   for (auto& q : g->procs) {
     if (q.get() == p) break;
     ++idx;
   }
-  info->hsa_id = idx + 1;
-  info->hip_id = idx;
+  if (p->kfd_node < 0) rank = idx;
+  else
+    for (auto& q : g->procs) rank += q->kfd_node >= 0 && q->kfd_node < p->kfd_node;
+  info->hsa_id = rank + 1;
+  info->hip_id = rank;
   CopyStr(info->hip_uuid, sizeof(info->hip_uuid), "GPU-" + p->uuid);
   return AMDSMI_STATUS_SUCCESS;
 }
@@ -521,7 +533,7 @@ amdsmi_status_t amdsmi_get_gpu_kfd_info(amdsmi_processor_handle h, amdsmi_kfd_in
   GET_PROC(h);
   memset(info, 0, sizeof(*info));
   info->kfd_id = 1000 + p->gpu * 16 + p->part;
-  info->node_id = 2 + p->gpu * 8 + p->part;
+  info->node_id = p->kfd_node < 0 ? 0xffffffffu : static_cast<uint32_t>(p->kfd_node);
   info->current_partition_id = p->part;
   return AMDSMI_STATUS_SUCCESS;
 }

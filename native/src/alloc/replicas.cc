@@ -31,12 +31,13 @@ std::vector<std::string> StripReplicas(const std::vector<std::string>& ids, std:
 }
 
 const char* ReplicaPolicyName(ReplicaPolicy p) {
-  return p == ReplicaPolicy::kPack ? "pack" : "spread";
+  return p == ReplicaPolicy::kPack ? "pack" : p == ReplicaPolicy::kAuto ? "auto" : "spread";
 }
 
 bool ParseReplicaPolicy(std::string_view s, ReplicaPolicy* out) {
   if (s == "spread") { *out = ReplicaPolicy::kSpread; return true; }
   if (s == "pack") { *out = ReplicaPolicy::kPack; return true; }
+  if (s == "auto") { *out = ReplicaPolicy::kAuto; return true; }
   return false;
 }
 
@@ -220,7 +221,7 @@ Result<Prioritized> PrioritizeDeviceViews(const std::vector<std::string_view>& a
   Prioritized out;
   out.devices.reserve(pools.size());
   for (const auto& p : pools) out.devices.emplace_back(p.prefix);
-  if (policy == ReplicaPolicy::kSpread) {
+  if (policy != ReplicaPolicy::kPack) {
     for (int i = static_cast<int>(chosen.size()); i < allocation_size; ++i) {
       // First priority: a physical device not yet used by this request; second:
       // the one with the most replicas left. Ties -> lexicographically first.

@@ -40,7 +40,9 @@ std::string StripReplica(std::string_view id, std::string_view join = kReplicaJo
 std::vector<std::string> StripReplicas(const std::vector<std::string>& ids,
                                        std::string_view join = kReplicaJoin);
 
-enum class ReplicaPolicy { kSpread, kPack };
+// kAuto is resolved per resource by the plugin (memory units -> pack, time-slice
+// replicas -> spread); the prioritizer itself treats it as spread.
+enum class ReplicaPolicy { kSpread, kPack, kAuto };
 const char* ReplicaPolicyName(ReplicaPolicy p);
 bool ParseReplicaPolicy(std::string_view s, ReplicaPolicy* out);
 

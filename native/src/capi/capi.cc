@@ -2,6 +2,7 @@
 // (loaded with ctypes from k8s_gpu_sharing_plugin_amd/native.py). Every function
 // takes and returns JSON strings; returned strings are freed with adp_free().
 // This is a test/tooling surface -- the daemon itself never goes through it.
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <json.hpp>
@@ -10,6 +11,7 @@
 #include "alloc/replicas.h"
 #include "alloc/topology.h"
 #include "health/health.h"
+#include "memcap/driver_usage.h"
 #include "inventory/inventory.h"
 #include "plugin/plugin.h"
 #include "proto/messages.h"
@@ -47,6 +49,8 @@ json SnapshotJson(const adp::inventory::Snapshot& s) {
       parts.push_back({{"uuid", p.uuid}, {"partition_id", p.partition_id}, {"render", p.render_path},
                        {"card", p.card_path}, {"numa", p.numa}, {"vram_mib", p.vram_mib},
                        {"xcds", p.xcds}, {"cus", p.cus},
+                       {"kfd_node", p.kfd_node == adp::inventory::kNoKfdNode ? json(nullptr) : json(p.kfd_node)},
+                       {"hip_id", raw.hip_id == 0xffffffffu ? json(nullptr) : json(raw.hip_id)},
                        // what amdsmi itself reported for this handle
                        {"reported", {{"vram_mib", raw.vram_mib}, {"xcd_count", raw.xcd_count},
                                      {"profile_type", raw.profile_type},
@@ -57,6 +61,7 @@ json SnapshotJson(const adp::inventory::Snapshot& s) {
     }
     gpus.push_back({{"index", g.index}, {"node_index", g.node_index}, {"uuid", g.uuid}, {"bdf", g.bdf},
                     {"numa", g.numa}, {"vram_mib", g.vram_mib}, {"xcds", g.xcds}, {"cus", g.cus},
+                    {"kfd_node", g.kfd_node == adp::inventory::kNoKfdNode ? json(nullptr) : json(g.kfd_node)},
                     {"compute_mode", g.compute_mode}, {"memory_mode", g.memory_mode},
                     {"market_name", g.market_name}, {"profile", g.PartitionProfile()},
                     {"partitioned", g.partitioned()}, {"xgmi_links_down", g.xgmi_links_down},
@@ -105,6 +110,27 @@ char* adp_prioritize(const char* in) {
                                            j["size"].get<int>(), pol);
     if (!r.ok()) return Err(r.status().message());
     return Dup(json{{"ids", r->ids}, {"non_unique", r->non_unique}}.dump());
+  });
+}
+
+// One driver-side HBM scan: {"proc_root", "kfd_proc_dir", "usage_dir", "self_cgroup"} ->
+// {pid_source, pids_scanned, fd_entries, fd_dirs_unreadable, scan_us, procs: [{pid, bdf, bytes, grant}],
+//  total: {bdf: bytes}, unattributed: {bdf: bytes}}
+char* adp_driver_scan(const char* in) {
+  return Guard([&] {
+    json j = json::parse(in);
+    auto t0 = std::chrono::steady_clock::now();
+    auto s = adp::memcap::ScanDriverHbm(j.value("proc_root", std::string("/proc")),
+                                        adp::memcap::ListGrantFiles(j.value("usage_dir", std::string())),
+                                        j.value("self_cgroup", std::string()), j.value("kfd_proc_dir", std::string()));
+    double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    json procs = json::array();
+    for (const auto& p : s.procs)
+      procs.push_back({{"pid", p.pid}, {"bdf", p.bdf}, {"bytes", p.bytes}, {"grant", p.grant}});
+    return Dup(json{{"pid_source", s.pid_source}, {"pids_scanned", s.pids_scanned}, {"fd_entries", s.fd_entries},
+                    {"fd_dirs_unreadable", s.fd_dirs_unreadable}, {"scan_us", us}, {"procs", procs},
+                    {"total", s.total}, {"unattributed", s.unattributed}}
+                   .dump());
   });
 }
 
@@ -205,7 +231,8 @@ char* adp_plugin_specs(const char* in) {
                         {"vram_mib", u.vram_mib}, {"numa", u.numa}, {"gpu", u.gpu}});
       out.push_back({{"resource", s.resource_name}, {"socket", s.socket_name}, {"original", s.original},
                      {"devices", devs}, {"advertised", p.advertised_count()},
-                     {"advertised_ids", p.advertised_ids()}, {"replicated", p.replicated()}});
+                     {"advertised_ids", p.advertised_ids()}, {"replicated", p.replicated()},
+                     {"hip_order_known", p.hip_order_known()}});
     }
     return Dup(out.dump());
   });

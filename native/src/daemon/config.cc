@@ -74,19 +74,20 @@ const std::vector<FlagDef>& Table() {
        "'gpu:sharedgpu:4,cpx-1xcd.36gb:small:2'; replicas -1 = one per 1000 MiB of VRAM",
        [](Flags& f) -> void* { return &f.resource_config; }},
       {"replica-policy", "REPLICA_POLICY", "replicaPolicy", Kind::kString,
-       "preferred allocation over replicas: [spread | pack] (pack suits memory-unit resources)",
+       "preferred allocation over replicas: [auto | spread | pack] (auto: pack for memory-unit resources "
+       "(replicas -1), spread for time-slice replicas; a resource-config entry's 4th field overrides it)",
        [](Flags& f) -> void* { return &f.replica_policy; }},
       {"replica-cu-mask", "REPLICA_CU_MASK", "replicaCuMask", Kind::kBool,
        "replicas also split the device's compute units (HSA_CU_MASK on Allocate): time-slice "
-       "replica r of R runs on its own 1/R of every XCD's CUs; memory units get CUs in "
-       "proportion to the units held (proportional: neighbours may share a boundary slot, unless "
-       "--memory-unit-cu-slots whole)",
+       "replica r of R runs on its own 1/R of every XCD's CUs; memory units become CU slots "
+       "(--auto-replica-unit auto), each a CU on every XCD with its share of the HBM, so every "
+       "pod owns whole slots",
        [](Flags& f) -> void* { return &f.replica_cu_mask; }},
       {"memory-unit-cu-slots", "DP_MEMORY_UNIT_CU_SLOTS", "memoryUnitCuSlots", Kind::kString,
-       "with --replica-cu-mask, which CU slots a memory-unit container gets: [proportional | whole] "
-       "(whole: only the slots all of whose units it holds, so no two containers share a CU; a container "
-       "that fills no slot on a device falls back to its partial slots, counted in "
-       "amdgpu_dp_partial_cu_slot_allocations_total)",
+       "with --replica-cu-mask and MiB memory units (--auto-replica-unit mib), which CU slots a container "
+       "gets: [proportional | whole] (whole: only the slots all of whose units it holds, so no two "
+       "containers share a CU; a container that fills no slot on a device falls back to its partial slots, "
+       "counted in amdgpu_dp_partial_cu_slot_allocations_total). CU-slot units need neither",
        [](Flags& f) -> void* { return &f.memory_unit_cu_slots; }},
       {"device-plugin-path", "DP_PLUGIN_DIR", "devicePluginPath", Kind::kString,
        "kubelet device-plugin directory",
@@ -101,8 +102,14 @@ const std::vector<FlagDef>& Table() {
        "only serve these GPUs: node indices, UUIDs or PCI addresses, comma separated (default: all)",
        [](Flags& f) -> void* { return &f.devices; }},
       {"auto-replica-unit-mib", "AUTO_REPLICA_UNIT_MIB", "autoReplicaUnitMiB", Kind::kUint,
-       "MiB of VRAM per replica when replicas=-1",
+       "MiB of VRAM per replica when replicas=-1 (MiB units)",
        [](Flags& f) -> void* { return &f.auto_replica_unit_mib; }},
+      {"auto-replica-unit", "AUTO_REPLICA_UNIT", "autoReplicaUnit", Kind::kString,
+       "what one memory unit (replicas=-1) is: [auto | mib | cu-slot] (mib: --auto-replica-unit-mib of "
+       "VRAM, the reference's rule; cu-slot: one CU on every XCD plus VRAM / (CUs per XCD) of HBM -- 32 "
+       "units of ~9 GiB on an SPX MI355X -- so CU shares line up with grants; auto: cu-slot with "
+       "--replica-cu-mask, else mib)",
+       [](Flags& f) -> void* { return &f.auto_replica_unit; }},
       {"resource-prefix", "RESOURCE_PREFIX", "resourcePrefix", Kind::kString,
        "extended-resource domain", [](Flags& f) -> void* { return &f.resource_prefix; }},
       {"include-card-nodes", "INCLUDE_CARD_NODES", "includeCardNodes", Kind::kBool,
@@ -131,6 +138,15 @@ const std::vector<FlagDef>& Table() {
        "register amdsmi event notification (GPU_PRE_RESET / GPU_POST_RESET: Unhealthy and back); "
        "it needs /dev/kfd, which an unprivileged pod's device cgroup denies (false = polling only)",
        [](Flags& f) -> void* { return &f.health_events; }},
+      {"health-event-socket", "DP_HEALTH_EVENT_SOCKET", "healthEventSocket", Kind::kString,
+       "receive amdsmi health events from the event relay listening on this Unix socket instead of "
+       "registering them in this process, which then needs no /dev/kfd access (privilege separation: "
+       "only the relay runs privileged; empty = register in-process)",
+       [](Flags& f) -> void* { return &f.health_event_socket; }},
+      {"event-relay", "DP_EVENT_RELAY", "", Kind::kBool,
+       "run as the event relay: register amdsmi event notification (needs /dev/kfd) and forward every "
+       "event to daemons connecting to --health-event-socket; nothing else (no kubelet, no network)",
+       [](Flags& f) -> void* { return &f.event_relay; }},
       {"driver-hbm-poll-ms", "DP_DRIVER_HBM_POLL_MS", "driverHbmPollMs", Kind::kUint,
        "with enforced memory units and /metrics: every N ms, read what each process holds on each GPU by the "
        "driver's count (DRM fdinfo under --host-proc), attribute it to grants and flag grants over their HBM "
@@ -144,6 +160,10 @@ const std::vector<FlagDef>& Table() {
        "the /proc of the PID namespace the pods run in, for the driver-side HBM check: /proc with hostPID, "
        "else a hostPath mount of the host's /proc",
        [](Flags& f) -> void* { return &f.host_proc; }},
+      {"kfd-proc-dir", "DP_KFD_PROC_DIR", "kfdProcDir", Kind::kString,
+       "KFD's list of GPU processes (host PIDs) for the driver-side HBM check: only those processes' "
+       "descriptors are read, not every process's (empty = always walk every process under --host-proc)",
+       [](Flags& f) -> void* { return &f.kfd_proc_dir; }},
       {"cdi-spec-dir", "CDI_SPEC_DIR", "cdiSpecDir", Kind::kString,
        "directory for the generated CDI spec (cdi-annotations / cdi-cri strategies)",
        [](Flags& f) -> void* { return &f.cdi_spec_dir; }},

@@ -33,7 +33,7 @@ struct Flags {
   std::string device_id_strategy = "uuid";
   std::string driver_root = "/";
   std::string resource_config;
-  std::string replica_policy = "spread";
+  std::string replica_policy = "auto";
   bool replica_cu_mask = false;
   std::string memory_unit_cu_slots = "proportional";
   std::string plugin_dir = "/var/lib/kubelet/device-plugins/";
@@ -41,6 +41,7 @@ struct Flags {
   std::string amdsmi_lib;
   std::string devices;         // GPU index filter, e.g. "0,1,2,3" (empty = all)
   uint64_t auto_replica_unit_mib = 1000;
+  std::string auto_replica_unit = "auto";  // auto | mib | cu-slot
   std::string resource_prefix = "amd.com";
   bool include_card_nodes = false;
   bool trace = false;
@@ -50,9 +51,12 @@ struct Flags {
   bool smi_report = false;       // print every amdsmi query's status + device-node access, exit
   bool doctor = false;           // check what a deployment needs on this node, say what to change, exit
   bool health_events = true;     // register amdsmi event notification (needs /dev/kfd access)
+  std::string health_event_socket;  // events from the relay at this socket ("" = in-process)
+  bool event_relay = false;         // run as that relay
   uint64_t driver_hbm_poll_ms = 10000;  // driver-side check of enforced grants (0 = off)
   uint64_t driver_hbm_slack_mib = 512;  // HIP runtime allowance per process in that check
   std::string host_proc = "/proc";      // the host's /proc (hostPID, or a hostPath mount)
+  std::string kfd_proc_dir = "/sys/class/kfd/kfd/proc";  // GPU processes by host PID ("" = walk all)
   uint64_t server_threads = 0;  // 0 -> plugin::DefaultServerThreads()
   std::string metrics_addr;     // "" = no metrics endpoint
   std::string node_labels_file; // "" = no NFD feature file

@@ -31,6 +31,7 @@
 #include "common/log.h"
 #include "common/strings.h"
 #include "health/health.h"
+#include "health/relay.h"
 #include "inventory/inventory.h"
 #include "metrics/metrics.h"
 #include "memcap/driver_usage.h"
@@ -166,6 +167,9 @@ Result<Validated> Validate(const Config& cfg) {
   v.popts.follow_peer_l3 = f.loop_affinity == "peer-l3";
   v.popts.driver_root = f.driver_root;
   v.popts.auto_replica_unit_mib = f.auto_replica_unit_mib;
+  if (f.auto_replica_unit != "auto" && f.auto_replica_unit != "mib" && f.auto_replica_unit != "cu-slot")
+    return InvalidArgument("invalid --auto-replica-unit option: " + f.auto_replica_unit + " (auto | mib | cu-slot)");
+  v.popts.cu_slot_units = f.auto_replica_unit == "cu-slot" || (f.auto_replica_unit == "auto" && f.replica_cu_mask);
   v.popts.server_threads = static_cast<int>(std::min<uint64_t>(f.server_threads, 64));
   v.popts.trace = f.trace;
   v.popts.busy_poll_us = static_cast<int>(std::min<uint64_t>(f.busy_poll_us, 100000));
@@ -371,12 +375,17 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
     }
     if (what.empty()) d.Line("FAIL", "resources: none would be advertised (partition strategy / --devices)");
     else d.Line("ok", "resources: " + what);
-    if (!unit_cus.empty() && v.popts.whole_cu_slots)
-      d.Line("ok", "CU shares: " + unit_cus + " pods get only the CU slots their units fill (disjoint)");
+    if (!unit_cus.empty() && v.popts.cu_slot_units)
+      d.Line("ok", "CU shares: " + unit_cus + " units are CU slots, so every pod owns whole slots (disjoint, "
+                   "none idle)");
+    else if (!unit_cus.empty() && v.popts.whole_cu_slots)
+      d.Line("warn", "CU shares: " + unit_cus + " pods get only the CU slots their units fill (disjoint), but "
+                     "MiB units do not line up with slots, so CUs of partly held slots sit idle -- "
+                     "--auto-replica-unit cu-slot makes every unit a slot");
     else if (!unit_cus.empty())
       d.Line("warn", "CU shares: " + unit_cus + " pods get proportional CU slots, so packed neighbours can share "
-                     "a boundary slot and slow each other's kernels -- --memory-unit-cu-slots whole (helm "
-                     "memoryUnitCuSlots: whole) makes them disjoint");
+                     "a boundary slot and slow each other's kernels -- --auto-replica-unit cu-slot (helm "
+                     "autoReplicaUnit: cu-slot) makes every unit a whole slot");
   }
   auto nodes = inventory::ProbeDeviceAccess(s, f.driver_root);
   std::string acc = inventory::DescribeAccess(nodes);
@@ -484,6 +493,29 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
   return d.Finish();
 }
 
+// Two resources that both hand a container per-device lists numbered from HIP
+// device 0 (HSA_CU_MASK agents, AMD_GPU_MEMORY_*): a container requesting both
+// gets one value per name (the kubelet merges the plugins' envs), numbered as
+// if that plugin's devices were all it had.
+void WarnSharedDeviceLists(const std::vector<std::unique_ptr<plugin::Plugin>>& plugins) {
+  std::vector<std::string> masks, grants;
+  for (const auto& p : plugins) {
+    if (p->device_count() == 0) continue;
+    if (p->sets_cu_masks()) masks.push_back(p->resource_name());
+    if (p->grants_hbm()) grants.push_back(p->resource_name());
+  }
+  auto warn = [](const std::vector<std::string>& rs, const char* what) {
+    if (rs.size() < 2) return;
+    std::string names;
+    for (const auto& r : rs) names += (names.empty() ? "" : ", ") + r;
+    LOG_WARN(kComp, "%s each set %s numbered from the container's first GPU: a container that requests more "
+             "than one of them gets only one plugin's list (the kubelet keeps one value per variable), "
+             "numbered without the other's devices -- request one of them per container", names.c_str(), what);
+  };
+  warn(masks, "HSA_CU_MASK");
+  warn(grants, "AMD_GPU_MEMORY_LIMIT_MIB/_FRACTION/_DEVICES");
+}
+
 void ArmTimer(int tfd, int ms) {
   itimerspec its{};
   its.it_value.tv_sec = ms / 1000;
@@ -543,6 +575,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     DoctorReport d;
     return Doctor(lib->get(), v, cfg, d);
   }
+  if (cfg.flags.event_relay) return health::RunEventRelay(lib->get(), cfg.flags.health_event_socket, sfd, cfg.flags.driver_root);
 
   std::string kubelet_sock =
       v.popts.kubelet_socket.empty() ? PathJoin(v.popts.plugin_dir, "kubelet.sock") : v.popts.kubelet_socket;
@@ -571,13 +604,27 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   int tfd = timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC | TFD_NONBLOCK);
   int efd = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   int lfd = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);  // health monitor: partition layout changed
+  // One-shot: look again at plugin sockets deleted from under us (recheck_sockets).
+  int rfd = timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC | TFD_NONBLOCK);
   int ep = epoll_create1(EPOLL_CLOEXEC);
-  for (int fd : {sfd, ifd, tfd, efd, lfd}) {
+  for (int fd : {sfd, ifd, tfd, efd, lfd, rfd}) {
     epoll_event ev{};
     ev.events = EPOLLIN;
     ev.data.fd = fd;
     epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev);
   }
+  // Plugin sockets found deleted, looked at again when rfd fires.
+  std::set<std::string> recheck_sockets;
+  constexpr int kSocketRecheckMs = 20;
+  auto stand_by = [](const plugin::Plugin& pl) {
+    // Another instance (a rollout with maxSurge) unlinked ours and bound the
+    // path: binding it back would start a tug of war. The kubelet now talks to
+    // that instance; this one stands by until the kubelet restarts or the file
+    // disappears again.
+    LOG_WARN(kComp, "inotify: %s now belongs to another process; '%s' stands by", pl.socket_path().c_str(),
+             pl.resource_name().c_str());
+  };
+
 
   std::vector<std::unique_ptr<plugin::Plugin>> plugins;
   // The metrics thread reads `plugins`; the vector is only changed under this
@@ -719,6 +766,17 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
                    "may not read (their HBM is not seen).\n"
                    "# TYPE amdgpu_dp_driver_hbm_unreadable_processes gauge\n"
                    "amdgpu_dp_driver_hbm_unreadable_processes " + std::to_string(dsnap->scan.fd_dirs_unreadable) + "\n"
+                   "# HELP amdgpu_dp_driver_hbm_scan_processes Processes the last driver-side scan read (the GPU "
+                   "processes KFD lists, or every process without that list).\n"
+                   "# TYPE amdgpu_dp_driver_hbm_scan_processes gauge\n"
+                   "amdgpu_dp_driver_hbm_scan_processes{source=\"" + dsnap->scan.pid_source + "\"} " +
+                   std::to_string(dsnap->scan.pids_scanned) + "\n"
+                   "# HELP amdgpu_dp_driver_hbm_scan_descriptors File descriptors the last driver-side scan examined.\n"
+                   "# TYPE amdgpu_dp_driver_hbm_scan_descriptors gauge\n"
+                   "amdgpu_dp_driver_hbm_scan_descriptors " + std::to_string(dsnap->scan.fd_entries) + "\n"
+                   "# HELP amdgpu_dp_driver_hbm_scan_seconds Wall time of the last driver-side scan.\n"
+                   "# TYPE amdgpu_dp_driver_hbm_scan_seconds gauge\n"
+                   "amdgpu_dp_driver_hbm_scan_seconds " + std::to_string(dsnap->last_scan_ns / 1e9) + "\n"
                    "# HELP amdgpu_dp_hbm_over_grant_events_total Transitions of any grant to over its HBM by the "
                    "driver's count.\n"
                    "# TYPE amdgpu_dp_hbm_over_grant_events_total counter\n"
@@ -818,6 +876,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
                              const std::vector<strategy::PluginSpec>& specs, bool apply_ledger) {
     std::lock_guard<std::mutex> lk(plugins_mu);
     for (const auto& s : specs) plugins.push_back(std::make_unique<plugin::Plugin>(snap, s, v.popts));
+    WarnSharedDeviceLists(plugins);
     if (!apply_ledger) return;
     auto failed = ledger.Failed(*snap);
     if (reregister_delay_ms > 0) usleep(static_cast<useconds_t>(reregister_delay_ms) * 1000);
@@ -831,6 +890,8 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   auto restart = [&] {
     stop_all();
     ArmTimer(tfd, 0);  // disarm
+    ArmTimer(rfd, 0);
+    recheck_sockets.clear();
     if (reinit) {
       Status rs = (*lib)->Reinit();
       if (!rs.ok()) {
@@ -880,21 +941,26 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     if (!driver_hbm && !v.popts.memcap_usage_dir.empty() && cfg.flags.driver_hbm_poll_ms > 0) {
       memcap::DriverHbmMonitor::Options dopt;
       dopt.proc_root = cfg.flags.host_proc;
+      dopt.kfd_proc_dir = cfg.flags.kfd_proc_dir;
       dopt.usage_dir = v.popts.memcap_usage_dir;
       dopt.poll_ms = static_cast<int>(std::min<uint64_t>(cfg.flags.driver_hbm_poll_ms, 3600000));
       dopt.slack_bytes = cfg.flags.driver_hbm_slack_mib << 20;
       std::string dir = v.popts.memcap_usage_dir;
       driver_hbm = std::make_unique<memcap::DriverHbmMonitor>(dopt, [&plugins, &plugins_mu, dir] {
+        // The accounting files are read before taking the lock the health
+        // listener needs (as /metrics does): only ID lookups run under it.
+        std::vector<memcap::Usage> files = memcap::ReadAll(dir);
         std::lock_guard<std::mutex> lk(plugins_mu);
         std::vector<const plugin::Plugin*> ps;
         for (auto& p : plugins) ps.push_back(p.get());
-        return plugin::Plugin::GrantedByKey(ps, dir);
+        return plugin::Plugin::GrantedByKey(ps, files);
       });
       driver_hbm->Start();
     }
     health::HealthConfig hcfg = health::HealthConfig::FromEnv();
     hcfg.events = cfg.flags.health_events;
     hcfg.driver_root = cfg.flags.driver_root;
+    hcfg.event_relay = cfg.flags.health_event_socket;
     publish_plugins(*snap, *specs, !hcfg.disabled);
     int started = start_plugins();
     if (started < 0) return;
@@ -923,6 +989,8 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     }
     serving.store(false);
     ArmTimer(tfd, 0);
+    ArmTimer(rfd, 0);
+    recheck_sockets.clear();
     for (auto& p : plugins) p->Stop();
     {
       std::lock_guard<std::mutex> lk(plugins_mu);
@@ -998,6 +1066,21 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
         ssize_t r = read(tfd, &exp, sizeof(exp));
         (void)r;
         do_restart = true;
+      } else if (fd == rfd) {
+        uint64_t exp;
+        ssize_t r = read(rfd, &exp, sizeof(exp));
+        (void)r;
+        for (auto& pl : plugins) {
+          if (!recheck_sockets.count(pl->socket_path()) || !pl->running()) continue;
+          struct stat st;
+          if (stat(pl->socket_path().c_str(), &st) != 0) {
+            LOG_WARN(kComp, "inotify: %s was removed, restarting", pl->socket_path().c_str());
+            do_reregister = true;
+          } else if (!pl->owns_socket()) {
+            stand_by(*pl);
+          }
+        }
+        recheck_sockets.clear();
       } else if (fd == efd) {
         uint64_t x;
         ssize_t r = read(efd, &x, sizeof(x));
@@ -1050,23 +1133,15 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
               for (auto& pl : plugins) {
                 struct stat st;
                 if (!pl->running() || BaseName(pl->socket_path()) != e->name) continue;
-                bool gone = stat(pl->socket_path().c_str(), &st) != 0;
-                if (gone) {
+                if (stat(pl->socket_path().c_str(), &st) != 0) {
                   // Another instance unlinks the path and binds it microseconds
-                  // later: look again after a moment before taking it back.
-                  usleep(20000);
-                  gone = stat(pl->socket_path().c_str(), &st) != 0;
-                }
-                if (gone) {
-                  LOG_WARN(kComp, "inotify: %s was removed, restarting", pl->socket_path().c_str());
-                  do_reregister = true;
+                  // later: look again after a moment (rfd) before taking it back
+                  // -- without sleeping here, so signals and kubelet events
+                  // are not held up meanwhile.
+                  recheck_sockets.insert(pl->socket_path());
+                  ArmTimer(rfd, kSocketRecheckMs);
                 } else if (!pl->owns_socket()) {
-                  // Another instance (a rollout with maxSurge) unlinked ours and
-                  // bound the path: binding it back would start a tug of war.
-                  // The kubelet now talks to that instance; this one stands by
-                  // until the kubelet restarts or the file disappears again.
-                  LOG_WARN(kComp, "inotify: %s now belongs to another process; '%s' stands by",
-                           pl->socket_path().c_str(), pl->resource_name().c_str());
+                  stand_by(*pl);
                 }
               }
             }
@@ -1106,7 +1181,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     LOG_WARN(kComp, "grant accounting files still being written at exit");
   // Labels describe a node this daemon is serving; do not leave them behind.
   if (!cfg.flags.node_labels_file.empty()) unlink(cfg.flags.node_labels_file.c_str());
-  for (int fd : {ep, sfd, ifd, tfd, efd, lfd}) close(fd);
+  for (int fd : {ep, sfd, ifd, tfd, efd, lfd, rfd}) close(fd);
   LOG_INFO(kComp, "shutdown complete (exit %d)", exit_code);
   return exit_code;
 }

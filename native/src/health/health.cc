@@ -2,6 +2,7 @@
 
 #include <poll.h>
 #include <sys/eventfd.h>
+#include <sys/socket.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -15,6 +16,7 @@
 
 #include "common/log.h"
 #include "common/strings.h"
+#include "health/relay.h"
 
 namespace adp::health {
 namespace {
@@ -308,6 +310,15 @@ Status Monitor::Start() {
     events_ok_ = false;
     events_reason_ = "off by configuration (--health-events=false)";
     LOG_INFO(kComp, "amdsmi event notification %s; GPU resets are seen by polling only", events_reason_.c_str());
+  } else if (!cfg_.event_relay.empty()) {
+    // Privilege separation: the relay holds the registration; this process
+    // needs no /dev/kfd. It asks the relay to re-enumerate (a new generation
+    // may follow a re-partition) and takes its hello as the event state.
+    RelayConnect();
+    if (relay_fd_ >= 0) RelayWait(1000, nullptr);
+    if (!events_ok_)
+      LOG_WARN(kComp, "events via relay %s: %s; polling meanwhile, reconnecting every second",
+               cfg_.event_relay.c_str(), events_reason_.c_str());
   } else {
     Status st = lib_->EventsInit(handles_, mask);
     events_ok_ = st.ok();
@@ -361,7 +372,7 @@ Status Monitor::Start() {
   }
   LOG_INFO(kComp, "health monitor watching %zu GPU(s) (events %s, poll every %d ms)", snap_->gpus.size(),
            events_ok_ ? "on" : "off", cfg_.poll_interval_ms);
-  if (!events_ok_ && cfg_.poll_interval_ms == 0) return Status::Ok();
+  if (!events_ok_ && cfg_.poll_interval_ms == 0 && cfg_.event_relay.empty()) return Status::Ok();
   stop_.store(false);
   if (wake_fd_ < 0) wake_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   thread_ = std::thread([this] { Run(); });
@@ -385,10 +396,82 @@ void Monitor::Stop() {
     close(wake_fd_);
     wake_fd_ = -1;
   }
-  if (events_ok_) {
+  if (relay_fd_ >= 0) {
+    close(relay_fd_);
+    relay_fd_ = -1;
+    events_ok_ = false;
+  } else if (events_ok_) {
     lib_->EventsStop(handles_);
     events_ok_ = false;
   }
+}
+
+namespace {
+int64_t NowMs() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+}  // namespace
+
+void Monitor::RelayConnect() {
+  relay_tried_ms_ = NowMs();
+  relay_fd_ = ConnectRelay(cfg_.event_relay);
+  if (relay_fd_ < 0) {
+    events_reason_ = "event relay " + cfg_.event_relay + " not reachable (" + strerror(errno) + ")";
+    return;
+  }
+  static const char kReinit[] = "reinit\n";
+  if (send(relay_fd_, kReinit, sizeof(kReinit) - 1, MSG_NOSIGNAL) != static_cast<ssize_t>(sizeof(kReinit) - 1)) {
+    RelayClose("cannot write to the event relay");
+    return;
+  }
+  relay_buf_.clear();
+  events_reason_ = "waiting for the event relay's hello";
+}
+
+void Monitor::RelayClose(const std::string& why) {
+  if (relay_fd_ >= 0) close(relay_fd_);
+  relay_fd_ = -1;
+  if (events_ok_) LOG_WARN(kComp, "event relay: %s; polling only until it is back", why.c_str());
+  events_ok_ = false;
+  events_reason_ = why;
+  counters_->events_enabled.store(0);
+}
+
+void Monitor::RelayWait(int ms, std::vector<smi::Event>* out) {
+  pollfd p[2] = {{relay_fd_, POLLIN, 0}, {wake_fd_, POLLIN, 0}};
+  if (poll(p, wake_fd_ >= 0 ? 2 : 1, ms) <= 0 || !(p[0].revents & (POLLIN | POLLHUP | POLLERR))) return;
+  char buf[4096];
+  ssize_t n;
+  while ((n = recv(relay_fd_, buf, sizeof(buf), 0)) > 0) relay_buf_.append(buf, static_cast<size_t>(n));
+  bool closed = n == 0 || (n < 0 && errno != EAGAIN && errno != EINTR);
+  size_t nl;
+  while ((nl = relay_buf_.find('\n')) != std::string::npos) {
+    RelayLine l = ParseRelayLine(std::string_view(relay_buf_).substr(0, nl));
+    relay_buf_.erase(0, nl + 1);
+    if (l.kind == "hello") {
+      bool was = events_ok_;
+      events_ok_ = l.events_ok;
+      events_reason_ = l.events_ok ? "" : "relay: " + l.reason;
+      counters_->events_enabled.store(events_ok_ ? 1 : 0);
+      if (events_ok_ && !was) LOG_INFO(kComp, "events on through the relay at %s", cfg_.event_relay.c_str());
+      if (!events_ok_) LOG_WARN(kComp, "event relay reports %s; using polling only", events_reason_.c_str());
+    } else if (l.kind == "event" && out) {
+      // The relay's processor -> this snapshot's handle: by KFD node when both
+      // know it, else by PCI address and partition.
+      for (const auto& pr : snap_->procs) {
+        bool hit = l.node != 0xffffffffu && pr.kfd_node != 0xffffffffu ? pr.kfd_node == l.node
+                                                                       : pr.bdf == l.bdf && pr.partition_id == l.part;
+        if (!hit) continue;
+        out->push_back({pr.handle, l.type, l.message});
+        break;
+      }
+    } else if (l.kind.empty()) {
+      LOG_WARN(kComp, "event relay: malformed line ignored");
+    }
+  }
+  if (relay_buf_.size() > 65536) relay_buf_.clear();
+  if (closed) RelayClose("the event relay closed the connection");
 }
 
 void Monitor::PollOnce() {
@@ -535,13 +618,26 @@ void Monitor::Run() {
       auto until = std::chrono::duration_cast<std::chrono::milliseconds>(next_poll - Clock::now()).count();
       slice = static_cast<int>(std::max<long long>(1, std::min<long long>(slice, until)));
     }
-    if (events_ok_) {
+    if (!cfg_.event_relay.empty() && cfg_.events) {
+      events.clear();
+      if (relay_fd_ < 0 && NowMs() - relay_tried_ms_ >= 1000) {
+        RelayConnect();
+        if (relay_fd_ >= 0) LOG_INFO(kComp, "connected to the event relay at %s", cfg_.event_relay.c_str());
+      }
+      if (relay_fd_ >= 0) RelayWait(slice, &events);
+      else Sleep(slice);
+    } else if (events_ok_) {
       events.clear();
       Status st = lib_->EventsWait(slice, &events);
       if (!st.ok()) {
         LOG_WARN(kComp, "event wait failed: %s", st.ToString().c_str());
         Sleep(slice);
       }
+    } else {
+      events.clear();
+      Sleep(slice);
+    }
+    {
       for (const auto& e : events) {
         counters_->events_received.fetch_add(1);
         int gpu = -1;
@@ -575,8 +671,6 @@ void Monitor::Run() {
           Update(gpu, e.type == smi::kEvtGpuPreReset ? kFailResetPending : kFailEvent, 0, why);
         }
       }
-    } else {
-      Sleep(slice);
     }
     if (cfg_.poll_interval_ms > 0 && Clock::now() >= next_poll) {
       PollOnce();

@@ -69,6 +69,9 @@ struct HealthConfig {
   bool events = true;
   // Where /dev/kfd is (--driver-root): why event registration failed.
   std::string driver_root = "/";
+  // --health-event-socket: events come from the privileged relay (relay.h) at
+  // this Unix socket instead of an in-process amdsmi registration ("" = in-process).
+  std::string event_relay;
   static HealthConfig FromEnv();
   static HealthConfig FromValues(const char* disable_value, const char* poll_ms_value);
 };
@@ -171,7 +174,7 @@ class Monitor {
   void SetLayoutListener(std::function<void(const std::string& why)> l) { layout_listener_ = std::move(l); }
   Status Start();
   void Stop();
-  bool events_enabled() const { return events_ok_; }
+  bool events_enabled() const { return events_ok_.load(); }
 
   // Decision function, exposed for tests: how an event changes a GPU's health.
   // Returns +1 (healthy), -1 (unhealthy), 0 (no change).
@@ -190,7 +193,17 @@ class Monitor {
   HealthConfig cfg_;
   std::vector<Listener> listeners_;
   std::vector<void*> handles_;
-  bool events_ok_ = false;
+  std::atomic<bool> events_ok_{false};
+  // Relay mode: the connection to the event relay (-1 = not connected), its
+  // partial input line, and when a connection was last tried.
+  int relay_fd_ = -1;
+  std::string relay_buf_;
+  int64_t relay_tried_ms_ = -1000000;
+  void RelayConnect();
+  void RelayClose(const std::string& why);
+  // Reads relay lines for up to `ms`: hellos update events_ok_, events are
+  // mapped to this snapshot's handles and appended.
+  void RelayWait(int ms, std::vector<smi::Event>* out);
   std::thread thread_;
   std::atomic<bool> stop_{false};
   std::function<void(const std::string&)> layout_listener_;

@@ -1,0 +1,272 @@
+#include "health/relay.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <poll.h>
+#include <signal.h>
+#include <sys/signalfd.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "common/log.h"
+#include "common/strings.h"
+#include "inventory/inventory.h"
+
+namespace adp::health {
+namespace {
+
+constexpr const char* kComp = "event-relay";
+
+// Every event type the daemon classifies (health.cc Classify).
+uint64_t RelayMask() {
+  return smi::EventMask(smi::kEvtGpuPreReset) | smi::EventMask(smi::kEvtGpuPostReset) |
+         smi::EventMask(smi::kEvtVmFault) | smi::EventMask(smi::kEvtThermalThrottle);
+}
+
+std::string OneLine(std::string s) {
+  for (char& c : s)
+    if (c == '\n' || c == '\r') c = ' ';
+  return s;
+}
+
+// Value of "key=value" (up to the next space) in `line`, "" if absent.
+std::string_view Kv(std::string_view line, std::string_view key, size_t* end = nullptr) {
+  for (size_t b = 0; b < line.size();) {
+    size_t e = line.find(' ', b);
+    if (e == std::string_view::npos) e = line.size();
+    std::string_view tok = line.substr(b, e - b);
+    if (tok.size() > key.size() && tok.compare(0, key.size(), key) == 0 && tok[key.size()] == '=') {
+      if (end) *end = e;
+      return tok.substr(key.size() + 1);
+    }
+    b = e + 1;
+  }
+  return {};
+}
+
+bool SendAll(int fd, const std::string& s) {
+  size_t off = 0;
+  while (off < s.size()) {
+    ssize_t n = send(fd, s.data() + off, s.size() - off, MSG_NOSIGNAL);
+    if (n < 0 && errno == EINTR) continue;
+    if (n <= 0) return false;  // a daemon that does not read is dropped, never waited for
+    off += static_cast<size_t>(n);
+  }
+  return true;
+}
+
+}  // namespace
+
+RelayLine ParseRelayLine(std::string_view line) {
+  RelayLine r;
+  while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.remove_suffix(1);
+  if (line.rfind("hello ", 0) == 0) {
+    r.kind = "hello";
+    r.events_ok = Kv(line, "events") == "ok";
+    size_t at = line.find(" reason=");
+    if (at != std::string_view::npos) r.reason = std::string(line.substr(at + 8));
+    return r;
+  }
+  if (line.rfind("event ", 0) != 0) return r;
+  size_t end = 0, last = 0;
+  std::string_view node = Kv(line, "node", &end);
+  last = std::max(last, end);
+  r.bdf = std::string(Kv(line, "bdf", &end));
+  last = std::max(last, end);
+  auto part = ParseUint(std::string(Kv(line, "part", &end)));
+  last = std::max(last, end);
+  auto type = ParseUint(std::string(Kv(line, "type", &end)));
+  last = std::max(last, end);
+  if (!part || !type || *type > 0xffffffffu || *part > 0xffffffffu) return r;
+  if (node != "-") {
+    auto n = ParseUint(std::string(node));
+    if (!n || *n >= 0xffffffffu) return r;
+    r.node = static_cast<uint32_t>(*n);
+  }
+  r.part = static_cast<uint32_t>(*part);
+  r.type = static_cast<uint32_t>(*type);
+  if (last < line.size()) r.message = std::string(line.substr(last + 1));
+  r.kind = "event";
+  return r;
+}
+
+std::string FormatRelayEvent(const smi::ProcessorInfo& p, uint32_t type, const std::string& message) {
+  return "event node=" + (p.kfd_node == 0xffffffffu ? std::string("-") : std::to_string(p.kfd_node)) +
+         " bdf=" + (p.bdf.empty() ? std::string("-") : p.bdf) + " part=" + std::to_string(p.partition_id) +
+         " type=" + std::to_string(type) + " " + OneLine(message) + "\n";
+}
+
+int ConnectRelay(const std::string& socket_path) {
+  sockaddr_un addr{};
+  if (socket_path.empty() || socket_path.size() >= sizeof(addr.sun_path)) return -1;
+  int fd = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) return -1;
+  addr.sun_family = AF_UNIX;
+  memcpy(addr.sun_path, socket_path.c_str(), socket_path.size());
+  if (connect(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0) {
+    close(fd);
+    return -1;
+  }
+  fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK);
+  return fd;
+}
+
+int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_fd, const std::string& driver_root) {
+  sockaddr_un addr{};
+  if (socket_path.empty() || socket_path.size() >= sizeof(addr.sun_path)) {
+    LOG_ERROR(kComp, "--event-relay needs --health-event-socket (a path shorter than %zu bytes)",
+              sizeof(addr.sun_path));
+    return 1;
+  }
+  int lfd = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
+  addr.sun_family = AF_UNIX;
+  memcpy(addr.sun_path, socket_path.c_str(), socket_path.size());
+  unlink(socket_path.c_str());
+  mode_t old = umask(0077);  // 0600: only the daemon's uid (root, same pod) may connect
+  int rc = lfd < 0 ? -1 : bind(lfd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr));
+  umask(old);
+  if (rc != 0 || listen(lfd, 8) != 0) {
+    LOG_ERROR(kComp, "cannot listen on %s: %s", socket_path.c_str(), strerror(errno));
+    if (lfd >= 0) close(lfd);
+    return 1;
+  }
+
+  std::vector<smi::ProcessorInfo> procs;
+  std::vector<void*> handles;
+  std::string events_state;  // the hello line's tail
+  bool registered = false;   // event notification is registered on `handles`
+  auto enumerate_and_register = [&](bool reinit) {
+    if (registered) lib->EventsStop(handles);
+    registered = false;
+    handles.clear();
+    procs.clear();
+    if (reinit) {
+      if (Status st = lib->Reinit(); !st.ok()) {
+        events_state = "events=off reason=amdsmi re-initialisation failed: " + OneLine(st.ToString());
+        LOG_ERROR(kComp, "%s", events_state.c_str());
+        return;
+      }
+    }
+    auto en = lib->Enumerate();
+    if (!en.ok()) {
+      events_state = "events=off reason=enumeration failed: " + OneLine(en.status().ToString());
+      LOG_ERROR(kComp, "%s", events_state.c_str());
+      return;
+    }
+    procs = std::move(*en);
+    for (const auto& p : procs) handles.push_back(p.handle);
+    Status st = lib->EventsInit(handles, RelayMask());
+    registered = st.ok();
+    std::string why = st.ok() ? "" : OneLine(st.ToString());
+    if (int kerr = st.ok() ? 0 : inventory::KfdAccessErrno(driver_root); kerr == EPERM)
+      why += "; /dev/kfd not openable (EPERM) in the relay's container: run the relay privileged";
+    events_state = st.ok() ? "events=ok processors=" + std::to_string(procs.size()) : "events=off reason=" + why;
+    if (st.ok()) LOG_INFO(kComp, "event notification registered on %zu processor(s)", procs.size());
+    else LOG_ERROR(kComp, "event notification unavailable: %s", st.ToString().c_str());
+  };
+  enumerate_and_register(false);
+  LOG_INFO(kComp, "relaying amdsmi events on %s", socket_path.c_str());
+
+  struct Client {
+    int fd;
+    std::string in;
+  };
+  std::vector<Client> clients;
+  auto hello = [&]() { return "hello v1 " + events_state + "\n"; };
+  int exit_code = 0;
+  bool quit = false;
+  std::vector<smi::Event> events;
+  while (!quit) {
+    // The amdsmi wait is the relay's clock: at most 100 ms, then sockets and signals.
+    events.clear();
+    if (registered) {
+      if (Status st = lib->EventsWait(100, &events); !st.ok()) {
+        LOG_WARN(kComp, "event wait failed: %s", st.ToString().c_str());
+        usleep(100000);
+      }
+    }
+    for (const auto& e : events) {
+      const smi::ProcessorInfo* p = nullptr;
+      for (const auto& q : procs)
+        if (q.handle == e.handle) p = &q;
+      if (!p) continue;
+      std::string line = FormatRelayEvent(*p, e.type, e.message);
+      LOG_INFO(kComp, "%s", OneLine(line).c_str());
+      for (auto& c : clients)
+        if (c.fd >= 0 && !SendAll(c.fd, line)) {
+          close(c.fd);
+          c.fd = -1;
+        }
+    }
+    std::vector<pollfd> pfds = {{signal_fd, POLLIN, 0}, {lfd, POLLIN, 0}};
+    for (const auto& c : clients) pfds.push_back({c.fd, POLLIN, 0});
+    int wait = registered ? 0 : 100;  // without events, poll is the clock
+    if (poll(pfds.data(), pfds.size(), wait) < 0 && errno != EINTR) break;
+    if (pfds[0].revents & POLLIN) {
+      signalfd_siginfo si;
+      while (read(signal_fd, &si, sizeof(si)) == sizeof(si))
+        if (si.ssi_signo != SIGHUP && si.ssi_signo != SIGUSR1) quit = true;
+    }
+    if (pfds[1].revents & POLLIN) {
+      int cfd;
+      while ((cfd = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK)) >= 0) {
+        if (!SendAll(cfd, hello())) {
+          close(cfd);
+          continue;
+        }
+        clients.push_back({cfd, ""});
+        LOG_INFO(kComp, "daemon connected (%zu client(s))", clients.size());
+      }
+    }
+    bool do_reinit = false;
+    for (size_t i = 0; i < clients.size(); ++i) {
+      auto& c = clients[i];
+      if (c.fd < 0 || !(pfds[2 + i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+      char buf[256];
+      ssize_t n = recv(c.fd, buf, sizeof(buf), 0);
+      if (n <= 0) {
+        if (n < 0 && (errno == EAGAIN || errno == EINTR)) continue;
+        close(c.fd);
+        c.fd = -1;
+        continue;
+      }
+      c.in.append(buf, static_cast<size_t>(n));
+      if (c.in.size() > 4096) {  // nothing legitimate is that long
+        close(c.fd);
+        c.fd = -1;
+        continue;
+      }
+      size_t nl;
+      while ((nl = c.in.find('\n')) != std::string::npos) {
+        if (c.in.compare(0, nl, "reinit") == 0) do_reinit = true;
+        c.in.erase(0, nl + 1);
+      }
+    }
+    clients.erase(std::remove_if(clients.begin(), clients.end(), [](const Client& c) { return c.fd < 0; }),
+                  clients.end());
+    if (do_reinit) {
+      LOG_INFO(kComp, "re-enumerating (a daemon asked)");
+      enumerate_and_register(true);
+      for (auto& c : clients)
+        if (!SendAll(c.fd, hello())) {
+          close(c.fd);
+          c.fd = -1;
+        }
+    }
+  }
+  if (!handles.empty() && registered) lib->EventsStop(handles);
+  for (auto& c : clients)
+    if (c.fd >= 0) close(c.fd);
+  close(lfd);
+  unlink(socket_path.c_str());
+  LOG_INFO(kComp, "event relay stopped");
+  return exit_code;
+}
+
+}  // namespace adp::health

@@ -1,0 +1,53 @@
+// Privilege separation for health events: a minimal relay process registers
+// amdsmi event notification -- the one thing the plugin does that needs
+// /dev/kfd, which an unprivileged pod's device cgroup denies -- and forwards
+// every event record to the daemon over a Unix socket. The daemon (gRPC to the
+// kubelet, /metrics on the network) then runs with every capability dropped.
+//
+// Parity: the reference runs its whole plugin with SYS_ADMIN when MIG
+// monitoring needs it, else drop-ALL
+// (/root/reference/deployments/helm/nvidia-device-plugin/templates/daemonset.yml:80-93);
+// here only the relay container is privileged, and it parses no network or
+// kubelet input -- one line per client, "reinit", is all it reads.
+//
+// Wire protocol (text lines over SOCK_STREAM):
+//   relay -> daemon  "hello v1 events=ok processors=<n>"
+//                    "hello v1 events=off reason=<text>"     (registration failed)
+//                    "event node=<kfd node|-> bdf=<bdf> part=<partition id> type=<t> <message>"
+//   daemon -> relay  "reinit"   re-enumerate (amdsmi_shut_down + init) and register
+//                               again, then a new hello (a new daemon generation,
+//                               e.g. after a re-partition)
+#pragma once
+
+#include <string>
+#include <string_view>
+
+#include "smi/smi.h"
+
+namespace adp::health {
+
+// One parsed relay line (ParseRelayLine). kind: "hello", "event" or "" (malformed).
+struct RelayLine {
+  std::string kind;
+  bool events_ok = false;
+  std::string reason;      // hello with events=off
+  uint32_t node = 0xffffffffu;  // KFD topology node of the processor ("-" = unreported)
+  std::string bdf;
+  uint32_t part = 0;
+  uint32_t type = 0;
+  std::string message;
+};
+RelayLine ParseRelayLine(std::string_view line);
+std::string FormatRelayEvent(const smi::ProcessorInfo& p, uint32_t type, const std::string& message);
+
+// Runs the relay until SIGTERM/SIGINT/SIGQUIT (the caller blocked them and
+// passes their signalfd): binds `socket_path` (mode 0600), registers events on
+// every amdsmi processor and forwards them to every connected daemon. Returns
+// the process exit code.
+int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_fd,
+                  const std::string& driver_root = "/");
+
+// Daemon side: connects to the relay (non-blocking), -1 when not reachable.
+int ConnectRelay(const std::string& socket_path);
+
+}  // namespace adp::health

@@ -251,6 +251,8 @@ Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo
       part.vram_mib = p.vram_mib;
       part.xcds = p.profile_xccs ? p.profile_xccs : p.xcd_count;
       part.cus = p.num_cu;
+      part.kfd_node = p.kfd_node;
+      g.kfd_node = std::min(g.kfd_node, p.kfd_node);
       g.xcds += part.xcds;
       g.cus += p.num_cu;
       g.partitions.push_back(std::move(part));
@@ -310,9 +312,10 @@ Result<std::shared_ptr<const Snapshot>> BuildSnapshot(smi::Library* lib, const B
     LOG_WARN(kComp, "%s is not visible to the plugin; it is still passed to containers", kfd.c_str());
   for (const auto& g : snap->gpus) {
     LOG_INFO(kComp,
-             "GPU %d: %s bdf=%s numa=%d vram=%llu MiB (%s) mode=%s/%s partitions=%zu profile=%s "
+             "GPU %d: %s bdf=%s numa=%d kfd_node=%s vram=%llu MiB (%s) mode=%s/%s partitions=%zu profile=%s "
              "render=%s",
              g.index, g.uuid.c_str(), g.bdf.c_str(), g.numa,
+             g.kfd_node == kNoKfdNode ? "?" : std::to_string(g.kfd_node).c_str(),
              static_cast<unsigned long long>(g.vram_mib), g.vram_source.c_str(), g.compute_mode.c_str(),
              g.memory_mode.empty() ? "?" : g.memory_mode.c_str(), g.partitions.size(),
              g.PartitionProfile().empty() ? "-" : g.PartitionProfile().c_str(),

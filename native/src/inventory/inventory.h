@@ -33,6 +33,8 @@
 
 namespace adp::inventory {
 
+inline constexpr uint32_t kNoKfdNode = 0xffffffffu;  // amdsmi did not report the KFD node
+
 struct Partition {
   int handle = -1;            // index into Snapshot::procs
   uint32_t partition_id = 0;  // amdsmi kfd current_partition_id
@@ -43,6 +45,7 @@ struct Partition {
   uint64_t vram_mib = 0;      // this partition's share of HBM
   uint32_t xcds = 0;
   uint32_t cus = 0;
+  uint32_t kfd_node = kNoKfdNode;  // KFD topology node (the HIP/ROCr order key)
 };
 
 struct PhysicalGpu {
@@ -61,6 +64,9 @@ struct PhysicalGpu {
   // to detect re-partitioning.
   std::string reported_compute, reported_memory;
   std::string market_name;
+  // Lowest KFD topology node of its partitions (kNoKfdNode if unreported): a
+  // container's HIP/ROCr device numbering follows this, not node_index.
+  uint32_t kfd_node = kNoKfdNode;
   std::vector<Partition> partitions;  // one per amdsmi handle; sorted by partition_id
   int xgmi_links_down = 0;
   // How vram_mib (the physical HBM) was established, most authoritative first:

@@ -9,10 +9,12 @@
 #include <sys/sysmacros.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <set>
+#include <tuple>
 
 #include "common/log.h"
 
@@ -127,30 +129,68 @@ std::vector<GrantFile> ListGrantFiles(const std::string& usage_dir) {
 
 std::string SelfCgroup() { return FirstLine(ReadSmall("/proc/self/cgroup", 4096)); }
 
-DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFile>& grants,
-                         const std::string& self_cgroup) {
-  DriverScan out;
-  DIR* d = opendir(proc_root.c_str());
+namespace {
+
+// Numeric entries of a directory (PIDs), in readdir order.
+std::vector<std::string> PidEntries(const std::string& dir, bool* opened) {
+  std::vector<std::string> out;
+  DIR* d = opendir(dir.c_str());
+  *opened = d != nullptr;
   if (!d) return out;
-  std::set<std::pair<std::string, uint64_t>> clients;  // (pdev, drm-client-id): a shared fd counts once
+  while (dirent* e = readdir(d))
+    if (IsPid(e->d_name)) out.emplace_back(e->d_name);
+  closedir(d);
+  return out;
+}
+
+}  // namespace
+
+DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFile>& grants,
+                         const std::string& self_cgroup, const std::string& kfd_proc_dir) {
+  DriverScan out;
+  // Candidates: the driver's own list of GPU processes when there is one whose
+  // PIDs live under proc_root, else every process.
+  std::vector<std::string> pids;
+  bool opened = false;
+  if (!kfd_proc_dir.empty()) {
+    pids = PidEntries(kfd_proc_dir, &opened);
+    struct stat st;
+    bool any_here = false;
+    for (const auto& p : pids)
+      if (stat((proc_root + "/" + p).c_str(), &st) == 0) {
+        any_here = true;
+        break;
+      }
+    if (opened && (pids.empty() || any_here)) out.pid_source = "kfd";
+    else pids.clear();
+  }
+  if (out.pid_source != "kfd") {
+    pids = PidEntries(proc_root, &opened);
+    if (!opened) return out;
+  }
+  // (pdev, drm-client-id): a descriptor shared with another process counts once.
+  std::set<std::pair<std::string, uint64_t>> clients;
+  // Without a drm-client-id (older kernels) a descriptor cannot be matched to
+  // another process's: each (pid, fd) counts on its own.
+  std::set<std::tuple<std::string, int, std::string>> anonymous;
   struct PidHbm {
     int pid;
     std::map<std::string, uint64_t> by_bdf;
   };
   std::vector<PidHbm> holders;
-  while (dirent* e = readdir(d)) {
-    if (!IsPid(e->d_name)) continue;
+  for (const auto& pid : pids) {
     ++out.pids_scanned;
-    std::string base = proc_root + "/" + e->d_name;
+    std::string base = proc_root + "/" + pid;
     DIR* fds = opendir((base + "/fd").c_str());
     if (!fds) {
       if (errno == EACCES || errno == EPERM) ++out.fd_dirs_unreadable;
       continue;
     }
-    PidHbm ph{atoi(e->d_name), {}};
+    PidHbm ph{atoi(pid.c_str()), {}};
     int fdd = dirfd(fds);
     while (dirent* f = readdir(fds)) {
       if (!IsPid(f->d_name)) continue;
+      ++out.fd_entries;
       char target[256];
       ssize_t n = readlinkat(fdd, f->d_name, target, sizeof(target) - 1);
       if (n <= 0) continue;
@@ -159,12 +199,17 @@ DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFi
       std::string info = ReadSmall(base + "/fdinfo/" + f->d_name);
       std::string pdev = Field(info, "drm-pdev");
       if (pdev.empty()) continue;
-      uint64_t client = strtoull(Field(info, "drm-client-id").c_str(), nullptr, 10);
+      std::string client_id = Field(info, "drm-client-id");
+      char* end = nullptr;
+      uint64_t client = strtoull(client_id.c_str(), &end, 10);
+      bool has_client = !client_id.empty() && end && *end == 0;
       // A descriptor shared with another process (fork, SCM_RIGHTS) is one
       // client: its memory counts once, but both processes stay GPU holders
       // (either may be the one that maps the grant's file).
       uint64_t bytes = 0;
-      if (clients.insert({pdev, client}).second) {
+      bool first = has_client ? clients.insert({pdev, client}).second
+                              : anonymous.insert({pdev, ph.pid, f->d_name}).second;
+      if (first) {
         std::string v = Field(info, "drm-resident-vram");
         if (v.empty()) v = Field(info, "drm-memory-vram");
         if (v.empty()) v = Field(info, "drm-total-vram");
@@ -175,7 +220,6 @@ DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFi
     closedir(fds);
     if (!ph.by_bdf.empty()) holders.push_back(std::move(ph));
   }
-  closedir(d);
 
   // Attribution: own mapping first, then the cgroup of an attributed process
   // -- a container's own cgroup, never the root one ("0::/", "N:ctrl:/") that
@@ -216,7 +260,10 @@ DriverHbmMonitor::DriverHbmMonitor(Options opts, GrantFn grants)
 DriverHbmMonitor::~DriverHbmMonitor() { Stop(); }
 
 void DriverHbmMonitor::PollOnce() {
-  DriverScan scan = ScanDriverHbm(opts_.proc_root, ListGrantFiles(opts_.usage_dir), self_cgroup_);
+  auto t0 = std::chrono::steady_clock::now();
+  DriverScan scan = ScanDriverHbm(opts_.proc_root, ListGrantFiles(opts_.usage_dir), self_cgroup_, opts_.kfd_proc_dir);
+  uint64_t scan_ns = static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
   auto granted = grants_ ? grants_() : std::map<std::string, std::map<std::string, uint64_t>>{};
   std::map<std::pair<std::string, std::string>, GrantState> states;
   for (const auto& [key, per_bdf] : granted)
@@ -247,8 +294,14 @@ void DriverHbmMonitor::PollOnce() {
     LOG_WARN(kComp, "%zu of %zu processes' file descriptors are not readable: HBM they hold is not seen (run the "
              "plugin privileged, with the host's PID namespace or /proc at --host-proc)",
              scan.fd_dirs_unreadable, scan.pids_scanned);
+  if (snap_.polls == 0)
+    LOG_INFO(kComp, "first scan: %zu candidate process(es) from %s, %zu descriptor(s), %.2f ms",
+             scan.pids_scanned, scan.pid_source == "kfd" ? opts_.kfd_proc_dir.c_str() : opts_.proc_root.c_str(),
+             scan.fd_entries, scan_ns / 1e6);
   snap_.scan = std::move(scan);
   snap_.grants = std::move(states);
+  snap_.last_scan_ns = scan_ns;
+  snap_.scan_ns_total += scan_ns;
   ++snap_.polls;
 }
 

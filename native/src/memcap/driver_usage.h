@@ -56,6 +56,10 @@ struct DriverScan {
   std::map<std::string, uint64_t> unattributed;  // bdf -> bytes outside every grant
   size_t pids_scanned = 0;
   size_t fd_dirs_unreadable = 0;  // processes whose fds this daemon may not read (privileges)
+  size_t fd_entries = 0;          // descriptor links examined (the scan's cost)
+  // Where the candidate PIDs came from: "kfd" (the driver's list of GPU
+  // processes, /sys/class/kfd/kfd/proc) or "proc" (every process).
+  std::string pid_source = "proc";
 };
 
 // A grant's accounting file as the daemon sees it: processes that mapped it
@@ -71,9 +75,13 @@ std::vector<GrantFile> ListGrantFiles(const std::string& usage_dir);
 uint64_t ParseFdinfoSize(const std::string& value);
 
 // One pass over <proc_root>/<pid>/fd. `self_cgroup`: the daemon's own cgroup,
-// never used for sibling attribution.
+// never used for sibling attribution. With `kfd_proc_dir` (KFD's sysfs list of
+// the processes that opened /dev/kfd, named by host PID) only those PIDs are
+// read, so the cost follows the GPU processes, not every descriptor on the
+// node; the full walk remains when that directory is absent or none of its
+// PIDs is under `proc_root` (a /proc of another PID namespace).
 DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFile>& grants,
-                         const std::string& self_cgroup);
+                         const std::string& self_cgroup, const std::string& kfd_proc_dir = "");
 
 // The cgroup line of the calling process ("" if unreadable).
 std::string SelfCgroup();
@@ -87,6 +95,7 @@ class DriverHbmMonitor {
  public:
   struct Options {
     std::string proc_root = "/proc";
+    std::string kfd_proc_dir = "/sys/class/kfd/kfd/proc";  // "" = always walk every process
     std::string usage_dir;
     int poll_ms = 10000;
     uint64_t slack_bytes = 512ull << 20;
@@ -107,6 +116,8 @@ class DriverHbmMonitor {
     uint64_t polls = 0;
     uint64_t over_total = 0;  // every transition into "over", all grants
     uint64_t slack_bytes = 0;
+    uint64_t last_scan_ns = 0;   // wall time of the last scan
+    uint64_t scan_ns_total = 0;  // all scans
   };
 
   DriverHbmMonitor(Options opts, GrantFn grants);

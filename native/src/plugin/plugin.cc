@@ -161,10 +161,47 @@ bool Plugin::owns_socket() const {
   return server_ && server_->OwnsSocketPath();
 }
 
+static bool OrderForHip(const inventory::Snapshot& snap, std::vector<alloc::DeviceRef>* devices) {
+  // ROCr creates one agent per KFD topology node whose render node the process
+  // can open, in node order, and HIP numbers its devices after the agents: a
+  // container given these devices sees them in KFD-node order, whatever order
+  // amdsmi enumerated them in. Unit order is that order, so every per-device
+  // list a container gets (HSA_CU_MASK agent numbers, AMD_GPU_MEMORY_* lists,
+  // grant/<ordinal> mounts) lines up with its HIP ordinals.
+  auto node = [&](const alloc::DeviceRef& r) {
+    const auto& g = snap.gpus[r.gpu];
+    return r.partition < 0 ? g.kfd_node : g.partitions[r.partition].kfd_node;
+  };
+  for (const auto& r : *devices)
+    if (node(r) == inventory::kNoKfdNode) return false;  // unknown: amdsmi order, the best guess left
+  std::stable_sort(devices->begin(), devices->end(),
+                   [&](const alloc::DeviceRef& a, const alloc::DeviceRef& b) { return node(a) < node(b); });
+  return true;
+}
+
 void Plugin::BuildUnits() {
   const auto& v = spec_.variant;
+  std::vector<alloc::DeviceRef> amdsmi_order = spec_.devices;
+  hip_order_known_ = OrderForHip(*snap_, &spec_.devices);
+  if (!hip_order_known_ && spec_.devices.size() > 1)
+    LOG_WARN(kComp, "'%s': amdsmi does not report KFD topology nodes; per-device container lists (HSA_CU_MASK, "
+             "AMD_GPU_MEMORY_*) assume HIP numbers devices in amdsmi order", spec_.resource_name.c_str());
+  else if (!std::equal(amdsmi_order.begin(), amdsmi_order.end(), spec_.devices.begin(),
+                       [](const alloc::DeviceRef& a, const alloc::DeviceRef& b) {
+                         return a.gpu == b.gpu && a.partition == b.partition;
+                       }))
+    LOG_INFO(kComp, "'%s': KFD topology order differs from amdsmi order; containers' devices are listed in KFD "
+             "(HIP) order", spec_.resource_name.c_str());
   replicated_ = v.replicas > 1 || v.auto_replicas;
   memory_units_ = v.auto_replicas;
+  // Per resource: the resource-config entry's own policy, else --replica-policy,
+  // else (auto) pack for memory units -- a grant's HBM must come from as few
+  // devices as possible -- and the reference's spread for time-slice replicas
+  // (replica.go:149-190).
+  replica_policy_ = v.policy != alloc::ReplicaPolicy::kAuto             ? v.policy
+                    : opts_.replica_policy != alloc::ReplicaPolicy::kAuto ? opts_.replica_policy
+                    : memory_units_                                     ? alloc::ReplicaPolicy::kPack
+                                                                        : alloc::ReplicaPolicy::kSpread;
   hbm_grants_ = memory_units_ || (opts_.replica_hbm_share && replicated_);
   for (const auto& ref : spec_.devices) {
     const auto& g = snap_->gpus[ref.gpu];
@@ -198,6 +235,19 @@ void Plugin::BuildUnits() {
     if (hbm_grants_) u.grant_mib = memory_units_ ? opts_.auto_replica_unit_mib : u.vram_mib / u.replicas;
     u.cus = ref.partition < 0 ? g.cus : g.partitions[ref.partition].cus;
     u.xcds = ref.partition < 0 ? g.xcds : g.partitions[ref.partition].xcds;
+    if (memory_units_ && opts_.cu_slot_units) {
+      // One unit = one CU slot (one CU on every XCD) and that slot's share of
+      // the HBM: 32 units of 9,215 MiB on an SPX MI355X. Every grant is then a
+      // whole number of slots -- no slot is shared, none left idle.
+      const uint32_t per = u.xcds && u.cus % u.xcds == 0 ? u.cus / u.xcds : 0;
+      if (per >= 2 && u.vram_mib / per > 0) {
+        u.replicas = per;
+        u.grant_mib = u.vram_mib / per;
+      } else {
+        LOG_WARN(kComp, "device %s: %u CUs over %u XCDs give no CU slots; its memory units are %llu MiB",
+                 u.id.c_str(), u.cus, u.xcds, static_cast<unsigned long long>(opts_.auto_replica_unit_mib));
+      }
+    }
     if (opts_.replica_cu_mask && replicated_) {
       u.replica_cus = memory_units_ ? MemoryUnitCuRanges(u.cus, u.xcds, u.replicas)
                                     : ReplicaCuRanges(u.cus, u.xcds, u.replicas);
@@ -222,6 +272,13 @@ void Plugin::BuildUnits() {
     pb::PutLen(&u.mount_bytes, 2, mb);
     units_.push_back(std::move(u));
   }
+  if (replicated_)
+    LOG_INFO(kComp, "'%s': preferred allocation %s replicas (%s)", spec_.resource_name.c_str(),
+             replica_policy_ == alloc::ReplicaPolicy::kPack ? "packs" : "spreads",
+             v.policy != alloc::ReplicaPolicy::kAuto             ? "resource-config entry"
+             : opts_.replica_policy != alloc::ReplicaPolicy::kAuto ? "--replica-policy"
+             : memory_units_                                     ? "auto: memory units"
+                                                                 : "auto: time-slice replicas");
   for (size_t i = 0; i < units_.size(); ++i) {
     const auto& u = units_[i];
     unit_by_id_[u.id] = static_cast<int>(i);
@@ -400,7 +457,8 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       }
     }
     // Unique physical devices. uuid strategy: sorted by ID (stripReplicas order,
-    // server.go:325); index strategy: enumeration order (server.go:406-411).
+    // server.go:325); index strategy: enumeration order (server.go:406-411),
+    // which here is unit order = KFD-node order = the container's HIP order.
     std::sort(us.begin(), us.end());
     if (hbm_grants_) {
       // Replicas (memory units / HBM shares) granted per device: distinct IDs
@@ -455,7 +513,7 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
     cu_mask.clear();
     if (!shares.empty()) {
       // HSA_CU_MASK="<agent>:<first>-<last>,...;...": agents are numbered in the
-      // container in enumeration order (= unit order, us is sorted by unit), and
+      // container in KFD-node order (= unit order, us is sorted by unit), and
       // devices without an entry keep all their CUs. Adjacent replica shares merge.
       // By unit, then by where the replica's range starts (memory-unit ranges
       // follow the IDs' lexicographic order, not the replica number).
@@ -659,7 +717,7 @@ Status Plugin::PreferredImpl(std::string_view req, std::string* resp) {
         return graph_.Score(ia->second, ib->second);
       };
       auto res = alloc::PrioritizeDeviceViews(cr.available, cr.must_include, cr.allocation_size,
-                                              opts_.replica_policy, alloc::kReplicaJoin, &affinity);
+                                              replica_policy_, alloc::kReplicaJoin, &affinity);
       if (!res.ok()) return res.status();
       if (HasDuplicate(res->ids)) {
         // An ID listed twice in availableDeviceIDs was chosen twice: choose
@@ -667,7 +725,7 @@ Status Plugin::PreferredImpl(std::string_view req, std::string* resp) {
         std::vector<std::string_view> avail(cr.available.begin(), cr.available.end());
         std::sort(avail.begin(), avail.end());
         avail.erase(std::unique(avail.begin(), avail.end()), avail.end());
-        res = alloc::PrioritizeDeviceViews(avail, cr.must_include, cr.allocation_size, opts_.replica_policy,
+        res = alloc::PrioritizeDeviceViews(avail, cr.must_include, cr.allocation_size, replica_policy_,
                                            alloc::kReplicaJoin, &affinity);
         if (!res.ok()) return res.status();
       }
@@ -1018,7 +1076,9 @@ std::string Plugin::StatsJson() const {
            stats_.allocate_hist.QuantileUs(0.5), stats_.allocate_hist.QuantileUs(0.99),
            stats_.preferred_hist.QuantileUs(0.5), stats_.preferred_hist.QuantileUs(0.99),
            static_cast<unsigned long long>(stats_.unhealthy_allocations.Value()));
-  std::string out = "{\"resource\": \"" + JsonEscape(spec_.resource_name);
+  std::string out = "{\"resource\": \"" + JsonEscape(spec_.resource_name) + "\", \"replica_policy\": \"" +
+                    (replicated_ ? alloc::ReplicaPolicyName(replica_policy_) : "none") + "\", \"hip_order\": \"" +
+                    (hip_order_known_ ? "kfd" : "amdsmi");
   out += buf;
   snprintf(buf, sizeof(buf), ", \"residency_p50_us\": %.1f, \"residency_p99_us\": %.1f, \"residency_100ns\": ",
            metrics::FineHistogram::QuantileUs(res_counts, 0.5), metrics::FineHistogram::QuantileUs(res_counts, 0.99));
@@ -1201,7 +1261,7 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
 }
 
 std::vector<std::pair<int, uint64_t>> Plugin::GrantedUnits(const std::vector<std::string_view>& ids) const {
-  std::vector<std::pair<int, uint64_t>> out;  // (unit, bytes), sorted by unit = the container's HIP order
+  std::vector<std::pair<int, uint64_t>> out;  // (unit, bytes), sorted by unit = the container's HIP order (OrderForHip)
   if (!hbm_grants_) return out;
   std::map<int, uint64_t> per;
   std::set<const void*> seen;  // an ID listed twice grants once (as Allocate counts it)
@@ -1216,8 +1276,13 @@ std::vector<std::pair<int, uint64_t>> Plugin::GrantedUnits(const std::vector<std
 
 std::map<std::string, std::map<std::string, uint64_t>> Plugin::GrantedByKey(const std::vector<const Plugin*>& plugins,
                                                                             const std::string& dir) {
+  return GrantedByKey(plugins, memcap::ReadAll(dir));
+}
+
+std::map<std::string, std::map<std::string, uint64_t>> Plugin::GrantedByKey(
+    const std::vector<const Plugin*>& plugins, const std::vector<memcap::Usage>& files) {
   std::map<std::string, std::map<std::string, uint64_t>> out;
-  for (auto& u : memcap::ReadAll(dir)) {
+  for (auto& u : files) {
     if (u.ids.empty()) continue;  // IDs that do not hash to the file's name: not believed
     std::vector<std::string_view> ids;
     for (size_t b = 0; b <= u.ids.size();) {

@@ -87,8 +87,14 @@ struct PluginOptions {
   bool pass_device_specs = true;
   std::string driver_root = "/";
   std::string envvar = kVisibleDevicesEnv;
-  alloc::ReplicaPolicy replica_policy = alloc::ReplicaPolicy::kSpread;
+  // kAuto: per resource, pack for memory units and spread for time-slice
+  // replicas; a resource-config entry's own policy wins over this.
+  alloc::ReplicaPolicy replica_policy = alloc::ReplicaPolicy::kAuto;
   uint64_t auto_replica_unit_mib = 1000;  // reference: TotalMemory / 1000 (server.go:102)
+  // Memory units are CU slots instead: one unit = one CU on every XCD plus
+  // VRAM / (CUs per XCD) of HBM (--auto-replica-unit cu-slot; the default with
+  // --replica-cu-mask), so every grant fills whole slots.
+  bool cu_slot_units = false;
   int dial_timeout_ms = 5000;             // server.go:208,219
   bool register_with_kubelet = true;
   bool trace = false;                     // log every RPC with its handler time
@@ -210,6 +216,18 @@ class Plugin {
   size_t device_count() const { return units_.size(); }
   size_t advertised_count() const { return advertised_.size(); }
   bool replicated() const { return replicated_; }
+  // Units (and every per-device list Allocate() returns) follow KFD topology
+  // node order -- how HIP numbers a container's devices -- rather than a guess.
+  bool hip_order_known() const { return hip_order_known_; }
+  // Allocate() can set HSA_CU_MASK / the AMD_GPU_MEMORY_* lists.
+  bool sets_cu_masks() const {
+    for (const auto& u : units_)
+      if (!u.replica_cus.empty()) return true;
+    return false;
+  }
+  bool grants_hbm() const { return hbm_grants_; }
+  // GetPreferredAllocation's replica policy for this resource (never kAuto).
+  alloc::ReplicaPolicy replica_policy() const { return replica_policy_; }
   const std::vector<Unit>& units() const { return units_; }
   const std::vector<std::string>& advertised_ids() const { return advertised_; }
 
@@ -244,6 +262,9 @@ class Plugin {
   // daemon's own units (never from the container-writable file's cap[]).
   static std::map<std::string, std::map<std::string, uint64_t>> GrantedByKey(
       const std::vector<const Plugin*>& plugins, const std::string& dir);
+  // The same from accounting files read beforehand (no I/O: only ID lookups).
+  static std::map<std::string, std::map<std::string, uint64_t>> GrantedByKey(
+      const std::vector<const Plugin*>& plugins, const std::vector<memcap::Usage>& files);
   // Bytes `ids` grant per unit, in HIP order (sorted unit index); empty when an
   // ID is not this plugin's or the plugin grants no HBM.
   std::vector<std::pair<int, uint64_t>> GrantedUnits(const std::vector<std::string_view>& ids) const;
@@ -292,6 +313,8 @@ class Plugin {
   bool replicated_ = false;
   bool memory_units_ = false;  // auto replicas: one ID per auto_replica_unit_mib of HBM
   bool hbm_grants_ = false;    // Allocate() reports (and may enforce) HBM per replica: memory units or HBM shares
+  bool hip_order_known_ = true;
+  alloc::ReplicaPolicy replica_policy_ = alloc::ReplicaPolicy::kSpread;  // resolved for this resource  // units are in KFD-node (HIP) order; false: amdsmi order, nodes unreported
 
   std::vector<Unit> units_;
   std::unordered_map<std::string, int> unit_by_id_;

@@ -230,8 +230,10 @@ Result<std::vector<ProcessorInfo>> Library::Enumerate() {
       }
       if (f_->kfd_info) {
         amdsmi_kfd_info_t ki{};
-        if (f_->kfd_info(h, &ki) == AMDSMI_STATUS_SUCCESS && ki.current_partition_id != 0xffffffffu)
-          p.partition_id = ki.current_partition_id;
+        if (f_->kfd_info(h, &ki) == AMDSMI_STATUS_SUCCESS) {
+          if (ki.current_partition_id != 0xffffffffu) p.partition_id = ki.current_partition_id;
+          p.kfd_node = ki.node_id;
+        }
       }
       if (f_->asic_info) {
         amdsmi_asic_info_t ai{};

@@ -39,6 +39,11 @@ struct ProcessorInfo {
   std::string compute_partition;  // "SPX", "DPX", "TPX", "QPX", "CPX" or "" if unknown
   std::string memory_partition;   // "NPS1", "NPS2", ... or ""
   uint32_t partition_id = 0;      // kfd current_partition_id (0 when not reported)
+  // KFD topology node (amdsmi_get_gpu_kfd_info().node_id; 0xffffffff = not
+  // reported). ROCr creates its GPU agents -- and HIP numbers a container's
+  // devices -- in this order, over the nodes whose render node the process can
+  // open; it need not be amdsmi's enumeration order.
+  uint32_t kfd_node = 0xffffffff;
   uint32_t num_cu = 0;
   uint32_t xcd_count = 0;         // 0 = unknown
   std::string market_name;

@@ -26,8 +26,9 @@ Result<ResourceConfig> ResourceConfig::Parse(std::string_view spec) {
     std::string entry = Trim(raw);
     if (entry.empty()) continue;
     auto parts = Split(entry, ':');
-    if (parts.size() != 3)
-      return InvalidArgument("'" + entry + "': an entry must have three parts separated by a colon");
+    if (parts.size() != 3 && parts.size() != 4)
+      return InvalidArgument("'" + entry + "': an entry must have three parts separated by a colon "
+                             "(<original>:<new>:<replicas>), optionally a fourth (:spread or :pack)");
     std::string orig = Trim(parts[0]), name = Trim(parts[1]);
     if (!ValidResourceName(orig)) return InvalidArgument("'" + entry + "': invalid original resource name");
     if (!ValidResourceName(name)) return InvalidArgument("'" + entry + "': invalid new resource name");
@@ -42,6 +43,11 @@ Result<ResourceConfig> ResourceConfig::Parse(std::string_view spec) {
       v.replicas = static_cast<unsigned>(*n);
     } else {
       return InvalidArgument("'" + entry + "': replicas must be a positive integer or -1 (auto)");
+    }
+    if (parts.size() == 4) {
+      std::string pol = Trim(parts[3]);
+      if (!alloc::ParseReplicaPolicy(pol, &v.policy))
+        return InvalidArgument("'" + entry + "': replica policy must be spread, pack or auto");
     }
     if (rc.entries_.count(orig)) LOG_WARN(kComp, "duplicate resource-config entry for '%s'; last wins", orig.c_str());
     rc.entries_[orig] = v;
@@ -65,7 +71,10 @@ std::string ResourceConfig::ToJson() const {
     first = false;
     out += "\"" + JsonEscape(k) + "\": {\"Name\": \"" + JsonEscape(v.name) +
            "\", \"Replicas\": " + std::to_string(v.replicas) +
-           ", \"AutoReplicas\": " + (v.auto_replicas ? "true" : "false") + "}";
+           ", \"AutoReplicas\": " + (v.auto_replicas ? "true" : "false") +
+           (v.policy == alloc::ReplicaPolicy::kAuto ? std::string()
+                                                    : std::string(", \"Policy\": \"") + alloc::ReplicaPolicyName(v.policy) + "\"") +
+           "}";
   }
   return out + "}";
 }

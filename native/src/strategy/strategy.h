@@ -22,6 +22,7 @@
 #include <string_view>
 #include <vector>
 
+#include "alloc/replicas.h"
 #include "alloc/topology.h"
 #include "common/status.h"
 #include "inventory/inventory.h"
@@ -32,6 +33,10 @@ struct Variant {
   std::string name;
   unsigned replicas = 1;
   bool auto_replicas = false;
+  // Optional 4th field of the entry, "<orig>:<new>:<replicas>:<policy>": how
+  // GetPreferredAllocation picks this resource's replicas (spread | pack),
+  // overriding --replica-policy. kAuto = not given.
+  alloc::ReplicaPolicy policy = alloc::ReplicaPolicy::kAuto;
 };
 
 class ResourceConfig {

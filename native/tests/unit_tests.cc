@@ -31,6 +31,7 @@
 #include "grpc/grpc.h"
 #include "grpc/server_conn.h"
 #include "health/health.h"
+#include "health/relay.h"
 #include "memcap/usage.h"
 #include "metrics/metrics.h"
 #include "plugin/plugin.h"
@@ -170,6 +171,40 @@ static void TestResourceConfig() {
   CHECK(!strategy::ResourceConfig::Parse("gpu:x:abc").ok());
   CHECK(!strategy::ResourceConfig::Parse("gpu:bad name:2").ok());
   CHECK(strategy::ResourceConfig::Parse("").ok());
+  // optional 4th field: this resource's replica policy
+  auto p = strategy::ResourceConfig::Parse("gpu:sharedgpu:4:pack,cpx-1xcd.36gb:s:2");
+  CHECK(p.ok() && p->Get("gpu").policy == alloc::ReplicaPolicy::kPack);
+  CHECK(p.ok() && p->Get("cpx-1xcd.36gb").policy == alloc::ReplicaPolicy::kAuto);
+  CHECK(p.ok() && p->ToJson().find("\"Policy\": \"pack\"") != std::string::npos);
+  CHECK(!strategy::ResourceConfig::Parse("gpu:x:2:tight").ok());
+  CHECK(!strategy::ResourceConfig::Parse("gpu:x:2:pack:extra").ok());
+  alloc::ReplicaPolicy pol;
+  CHECK(alloc::ParseReplicaPolicy("auto", &pol) && pol == alloc::ReplicaPolicy::kAuto);
+  CHECK(std::string(alloc::ReplicaPolicyName(alloc::ReplicaPolicy::kAuto)) == "auto");
+}
+
+static void TestRelayLines() {
+  g_case = "relay-lines";
+  smi::ProcessorInfo p;
+  p.kfd_node = 10;
+  p.bdf = "0000:0c:00.1";
+  p.partition_id = 1;
+  std::string line = health::FormatRelayEvent(p, 3, "mode1 reset\nsecond line");
+  CHECK(line == "event node=10 bdf=0000:0c:00.1 part=1 type=3 mode1 reset second line\n");
+  auto r = health::ParseRelayLine(line);
+  CHECK(r.kind == "event" && r.node == 10 && r.bdf == "0000:0c:00.1" && r.part == 1 && r.type == 3);
+  CHECK(r.message == "mode1 reset second line");
+  p.kfd_node = 0xffffffffu;
+  r = health::ParseRelayLine(health::FormatRelayEvent(p, 4, ""));
+  CHECK(r.kind == "event" && r.node == 0xffffffffu && r.type == 4 && r.message.empty());
+  r = health::ParseRelayLine("hello v1 events=ok processors=8");
+  CHECK(r.kind == "hello" && r.events_ok);
+  r = health::ParseRelayLine("hello v1 events=off reason=NO_PERM: denied");
+  CHECK(r.kind == "hello" && !r.events_ok && r.reason == "NO_PERM: denied");
+  for (const char* bad : {"", "event", "event node=x bdf=a part=0 type=3", "event node=1 bdf=a part=0",
+                          "event node=1 bdf=a part=-1 type=3", "event node=4294967295 bdf=a part=0 type=3",
+                          "bogus line", "event node=1 bdf=a part=0 type=99999999999"})
+    CHECK(health::ParseRelayLine(bad).kind.empty());
 }
 
 static void TestProto() {
@@ -1051,6 +1086,7 @@ int main() {
   TestStrip();
   TestAdditionalIds();
   TestResourceConfig();
+  TestRelayLines();
   TestProto();
   TestTopology();
   TestHierarchicalMatchesOracle();

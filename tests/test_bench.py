@@ -126,6 +126,13 @@ def test_bench_serves_the_ranks_gpus_not_amdsmi_order():
     bdfs = {p["rank"]: (p["rank_bdf"], p["admitted_bdfs"]) for p in res["per_rank"]}
     assert bdfs == {0: ("0000:ac:00.0", ["0000:ac:00.0"]), 1: ("0000:4c:00.0", ["0000:4c:00.0"])}
     assert all(p["rank_devices"] == 4 for p in res["per_rank"])
+    # the three device orders: amdsmi's, KFD node order (what container lists
+    # follow) and HIP's (rank r = HIP device r), with the per-GPU KFD node
+    order = topo["device_order"]
+    assert order["amdsmi_order"] == ["0000:4c:00.0", "0000:ac:00.0"] == order["kfd_order"]
+    assert order["hip_order"] == topo["rank_bdfs"]
+    assert order["hip_order_is_kfd_order"] is False and order["hip_order_is_amdsmi_order"] is False
+    assert [g["kfd_node"] for g in topo["gpus"]] == [2 + 8 * 2, 2 + 8 * 5]
 
 
 @pytest.mark.parametrize("config,advertised", [("timeslice4", 4), ("cpx-single", 8), ("auto-mem", 294),

@@ -17,7 +17,8 @@ from k8s_gpu_sharing_plugin_amd import DAEMON
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHART = os.path.join(ROOT, "deployments", "helm", "amd-gpu-device-plugin")
-KNOWN_EXTRA_ENV = {"DP_DISABLE_HEALTHCHECKS", "DP_HEALTH_POLL_MS", "DP_MAX_RETIRED_PAGES"}
+# POD_IP: downward-API value the kubelet expands into DP_METRICS_ADDR
+KNOWN_EXTRA_ENV = {"DP_DISABLE_HEALTHCHECKS", "DP_HEALTH_POLL_MS", "DP_MAX_RETIRED_PAGES", "POD_IP"}
 
 
 def daemon_envs():

@@ -134,16 +134,20 @@ def test_other_plugins_and_a_running_instance_are_reported(tmp_path):
     assert rc == 0, lines  # warnings, not failures
 
 
-@pytest.mark.parametrize("slots,level", [("proportional", "warn"), ("whole", "ok")])
-def test_doctor_reports_memory_unit_cu_slots(tmp_path, slots, level):
-    """Memory units with CU shares: proportional slots are a warning (packed
-    neighbours can share a slot), whole slots are disjoint; no line without
-    --replica-cu-mask."""
+@pytest.mark.parametrize("unit_args,level,says", [
+    (["--auto-replica-unit", "mib", "--memory-unit-cu-slots", "proportional"], "warn", "proportional"),
+    (["--auto-replica-unit", "mib", "--memory-unit-cu-slots", "whole"], "warn", "sit idle"),
+    ([], "ok", "units are CU slots")])
+def test_doctor_reports_memory_unit_cu_slots(tmp_path, unit_args, level, says):
+    """Memory units with CU shares: MiB units get proportional slots (packed
+    neighbours can share one) or whole slots (disjoint, but partly held slots
+    idle) -- both warnings; CU-slot units (the default with --replica-cu-mask)
+    are disjoint with nothing idle; no line without --replica-cu-mask."""
     d = tmp_path / "dp"
     d.mkdir()
-    args = ["--device-plugin-path", str(d), "--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack"]
-    _, lines = _doctor(tmp_path, *args, "--replica-cu-mask", "--memory-unit-cu-slots", slots)
+    args = ["--device-plugin-path", str(d), "--resource-config", "gpu:gpu-mem-gb:-1"]
+    _, lines = _doctor(tmp_path, *args, "--replica-cu-mask", *unit_args)
     line = _find(lines, "CU shares:")
-    assert line and line.split()[0] == level and "amd.com/gpu-mem-gb" in line, lines
+    assert line and line.split()[0] == level and "amd.com/gpu-mem-gb" in line and says in line, lines
     _, lines = _doctor(tmp_path, *args)
     assert _find(lines, "CU shares:") is None

@@ -217,3 +217,109 @@ def test_unreadable_processes_are_reported(node):
     os.chmod(os.path.join(proc.root, "401", "fd"), 0)
     s = _scrape_after_poll(port, _polls(port) + 2)
     assert _value(s, "amdgpu_dp_driver_hbm_unreadable_processes") == 1
+
+
+def _busy_node(root, gpu_pids, others, fds_per_other):
+    """A /proc of GPU processes (render fds) and many non-GPU processes holding
+    `fds_per_other` descriptors each (sockets, files): the load of a busy node."""
+    proc = FakeProc(root)
+    for i, pid in enumerate(gpu_pids):
+        proc.process(pid, f"0::/kubepods/pod{i}/ctr", vram_mib=100 + i)
+    for n in range(others):
+        pid = 100000 + n
+        base = os.path.join(root, str(pid))
+        os.makedirs(os.path.join(base, "fd"))
+        for fd in range(fds_per_other):
+            os.symlink(f"socket:[{pid * 100 + fd}]" if fd % 2 else "/var/log/app.log", os.path.join(base, "fd", str(fd)))
+    return proc
+
+
+def _kfd_dir(path, pids):
+    os.makedirs(path, exist_ok=True)
+    for pid in pids:
+        os.makedirs(os.path.join(path, str(pid)), exist_ok=True)  # /sys/class/kfd/kfd/proc/<pid>/
+    return path
+
+
+def test_scan_reads_only_the_gpu_processes_kfd_lists(tmp_path):
+    """Round-3 review: the scan walked every descriptor of every process. With
+    KFD's list of GPU processes (/sys/class/kfd/kfd/proc/<pid>) it reads just
+    those: its work does not grow with the node's other processes, and the
+    attribution is the same as the full walk's."""
+    from k8s_gpu_sharing_plugin_amd.utils import native
+    gpu = [4100 + i for i in range(8)]
+    results = {}
+    for others in (200, 2000):
+        root = str(tmp_path / f"proc{others}")
+        _busy_node(root, gpu, others, 50)
+        kfd = _kfd_dir(str(tmp_path / f"kfd{others}"), gpu)
+        fast = native.driver_scan(root, kfd_proc_dir=kfd)
+        full = native.driver_scan(root)
+        assert fast["pid_source"] == "kfd" and full["pid_source"] == "proc"
+        assert fast["pids_scanned"] == 8 and full["pids_scanned"] == 8 + others
+        assert fast["fd_entries"] == 8 * 2  # each GPU process: its KFD fd + one render fd
+        assert full["fd_entries"] == 8 * 2 + others * 50
+        key = lambda p: (p["pid"], p["bdf"])  # noqa: E731
+        assert sorted(fast["procs"], key=key) == sorted(full["procs"], key=key)
+        assert fast["total"] == full["total"] == {BDF0: sum(100 + i for i in range(8)) * MIB}
+        results[others] = (fast["scan_us"], full["scan_us"])
+    print("scan us (kfd, full) by non-GPU processes:", results)
+    assert results[2000][1] > results[200][1]  # the full walk grows with the node
+
+
+def test_kfd_pids_from_another_namespace_fall_back_to_the_full_walk(tmp_path):
+    """KFD names host PIDs: with a /proc of another PID namespace none of them
+    is there, so the scan walks every process rather than seeing nothing."""
+    from k8s_gpu_sharing_plugin_amd.utils import native
+    root = str(tmp_path / "proc")
+    _busy_node(root, [41, 42], 3, 4)
+    kfd = _kfd_dir(str(tmp_path / "kfd"), [900001, 900002])
+    s = native.driver_scan(root, kfd_proc_dir=kfd)
+    assert s["pid_source"] == "proc" and s["pids_scanned"] == 5 and len(s["procs"]) == 2
+    # no KFD directory at all (no amdgpu driver visible): the full walk too
+    assert native.driver_scan(root, kfd_proc_dir=str(tmp_path / "absent"))["pid_source"] == "proc"
+    # an empty KFD list is trusted: no GPU process, nothing to read
+    empty = native.driver_scan(root, kfd_proc_dir=_kfd_dir(str(tmp_path / "none"), []))
+    assert empty["pid_source"] == "kfd" and empty["pids_scanned"] == 0 and empty["procs"] == []
+
+
+def test_render_fds_without_client_id_each_count(tmp_path):
+    """Advisor round 3: a kernel whose fdinfo has no drm-client-id made every
+    render fd after the first on a GPU count 0 bytes. Without an ID each
+    (process, fd) counts on its own."""
+    from k8s_gpu_sharing_plugin_amd.utils import native
+    root = str(tmp_path / "proc")
+    proc = FakeProc(root)
+    for pid, mib in ((51, 300), (52, 500)):
+        proc.process(pid, f"0::/kubepods/p{pid}")
+        proc.render(pid, 7, mib, client=0)
+        info = os.path.join(root, str(pid), "fdinfo", "7")
+        text = "".join(ln for ln in open(info).read().splitlines(True) if not ln.startswith("drm-client-id"))
+        open(info, "w").write(text)
+    s = native.driver_scan(root)
+    assert {p["pid"]: p["bytes"] for p in s["procs"]} == {51: 300 * MIB, 52: 500 * MIB}
+    # with IDs, a descriptor shared by two processes still counts once
+    proc.process(61, "0::/kubepods/q", vram_mib=700, client=4242)
+    proc.process(62, "0::/kubepods/q", vram_mib=700, client=4242)
+    s = native.driver_scan(root)
+    assert sum(p["bytes"] for p in s["procs"] if p["pid"] in (61, 62)) == 700 * MIB
+
+
+def test_daemon_scan_uses_the_kfd_list(scratch, tmp_path):
+    proc = _busy_node(str(tmp_path / "proc"), [7001, 7002], 50, 20)
+    kfd = _kfd_dir(str(tmp_path / "kfd"), [7001, 7002])
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(1), args=[
+        "--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units",
+        "--memcap-lib", SHIM, "--host-proc", proc.root, "--kfd-proc-dir", kfd, "--driver-hbm-poll-ms", "50"]).start()
+    try:
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics")).group(1))
+        k.wait_registration()
+        s = _scrape_after_poll(port, 2)
+        assert _value(s, "amdgpu_dp_driver_hbm_scan_processes", source="kfd") == 2
+        assert _value(s, "amdgpu_dp_driver_hbm_scan_descriptors") == 4
+        assert _value(s, "amdgpu_dp_driver_hbm_scan_seconds") >= 0
+        assert "first scan: 2 candidate process(es) from " + kfd in d.log()
+    finally:
+        d.stop()
+        k.stop()

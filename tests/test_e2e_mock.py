@@ -202,7 +202,7 @@ def test_memory_lists_follow_enumeration_order_not_uuid_order(running, scratch):
     fx["gpus"][0]["uuid"] = "ffffffff-0000-1000-80c0-000000000000"
     fx["gpus"][1]["uuid"] = "00000000-0000-1000-80c0-000000000001"
     d, k = running(fx, args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack",
-                             "--replica-cu-mask"])
+                             "--replica-cu-mask", "--auto-replica-unit", "mib"])
     reg = k.wait_registration()
     c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
     ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
@@ -280,7 +280,7 @@ def test_memory_units_get_proportional_cu_shares(running, scratch):
     then Allocate) get contiguous slots -- a proportional CU share, not an
     isolating slice: neighbours may share one boundary slot."""
     d, k = running(args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack",
-                         "--replica-cu-mask"])
+                         "--replica-cu-mask", "--auto-replica-unit", "mib"])
     reg = k.wait_registration()
     c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
     free = [x.ID for x in c.watch()[0].get(timeout=5).devices]
@@ -305,7 +305,7 @@ def test_memory_unit_cu_shares_overlap_at_most_one_boundary_slot(running, scratc
     never share more than one slot -- only at a boundary. A slot is shared only
     when both pods hold units of it."""
     d, k = running(fixture=fixtures.node(1), args=["--resource-config", "gpu:gpu-mem-gb:-1",
-                                                   "--replica-policy", "pack", "--replica-cu-mask"])
+                                                   "--replica-policy", "pack", "--replica-cu-mask", "--auto-replica-unit", "mib"])
     reg = k.wait_registration()
     c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
     free = [x.ID for x in c.watch()[0].get(timeout=5).devices]
@@ -349,7 +349,7 @@ def test_whole_cu_slots_never_share_a_cu(running, scratch, sizes):
     amdgpu_dp_partial_cu_slot_allocations_total. Checked against a model of the
     slot map for every pod, admitted the kubelet's way (pack)."""
     d, k = running(fixture=fixtures.node(1), args=["--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy",
-                                                   "pack", "--replica-cu-mask", "--memory-unit-cu-slots", "whole",
+                                                   "pack", "--replica-cu-mask", "--auto-replica-unit", "mib", "--memory-unit-cu-slots", "whole",
                                                    "--metrics-addr", "127.0.0.1:0"])
     port = int(re.search(r"serving /metrics and /healthz on port (\d+)",
                          d.wait_log("serving /metrics and /healthz on port")).group(1))

@@ -1,0 +1,160 @@
+"""Privilege separation for health events: the event relay.
+
+amdsmi event notification (GPU_PRE_RESET / GPU_POST_RESET) opens /dev/kfd,
+which the device cgroup of an unprivileged pod denies. Instead of running the
+whole plugin -- the kubelet-facing gRPC server and the /metrics HTTP server --
+privileged, `amdgpu-device-plugin --event-relay` registers the events in a
+second, privileged container of the same pod and forwards them over a Unix
+socket (--health-event-socket); the daemon runs drop-ALL. Here the daemon runs
+under libadp_devcgroup_sim.so (its /dev/kfd and render nodes answer EPERM, as
+in an unprivileged pod) and the relay without it; reset events still travel.
+
+Reference: the reference chart escalates the whole plugin (SYS_ADMIN) for MIG
+monitoring, /root/reference/deployments/helm/nvidia-device-plugin/templates/daemonset.yml:80-93.
+"""
+
+import os
+import re
+import signal
+import time
+
+from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+from k8s_gpu_sharing_plugin_amd.models import fixtures
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
+
+from test_metrics import _get, _parse, _value
+
+SIM = os.path.join(BUILD_DIR, "libadp_devcgroup_sim.so")
+
+
+def _preload(*libs):
+    return " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), *libs) if x)
+
+
+class RelayNode:
+    def __init__(self, scratch, relay_env=None):
+        self.scratch = scratch
+        self.fifo = os.path.join(scratch + ".fixture", "events")
+        os.makedirs(scratch + ".fixture", exist_ok=True)
+        os.mkfifo(self.fifo)
+        self.sock = os.path.join(scratch + ".fixture", "events.sock")
+        self.fx = dict(fixtures.node(2), events_open_kfd=True)
+        self.relay_env = relay_env
+        self.relay = None
+        self.start_relay()
+        self.k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+        self.d = harness.Daemon(scratch, self.fx, args=["--health-event-socket", self.sock,
+                                                        "--metrics-addr", "127.0.0.1:0"],
+                                env={"LD_PRELOAD": _preload(SIM), "DP_HEALTH_POLL_MS": "200"}).start()
+        self.port = int(re.search(r"on port (\d+)", self.d.wait_log("serving /metrics")).group(1))
+        reg = self.k.wait_registration()
+        self.c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        self.q, self.call = self.c.watch()
+        self.first = self.q.get(timeout=5)
+
+    def start_relay(self):
+        n = 0 if self.relay is None else len(self.relay.log()) + 1
+        rdir = self.scratch + f"-relay{n}"
+        os.makedirs(rdir, exist_ok=True)
+        self.relay = harness.Daemon(rdir, self.fx, args=["--event-relay", "--health-event-socket", self.sock],
+                                    env=self.relay_env, event_fifo=self.fifo).start()
+        self.relay.wait_log("relaying amdsmi events on")
+
+    def inject(self, line):
+        fd = os.open(self.fifo, os.O_WRONLY | os.O_NONBLOCK)
+        os.write(fd, (line + "\n").encode())
+        os.close(fd)
+
+    def health(self, timeout=5):
+        law = self.q.get(timeout=timeout)
+        return [x.health for x in law.devices]
+
+    def metrics(self):
+        return _parse(_get(self.port, "/metrics")[1])
+
+    def stop(self):
+        self.call.cancel()
+        self.c.close()
+        self.d.stop()
+        self.k.stop()
+        if self.relay.proc.poll() is None:
+            self.relay.stop()
+
+
+def test_reset_events_travel_through_the_relay(scratch):
+    n = RelayNode(scratch)
+    try:
+        log = n.d.wait_log("events on through the relay")
+        assert "device access: Operation not permitted: /dev/kfd" in log  # the daemon itself is denied
+        assert "events off:" not in log
+        assert _value(n.metrics(), "amdgpu_dp_health_events_enabled") == 1
+        n.inject("1 3 mode1 reset")
+        assert n.health() == ["Healthy", "Unhealthy"]
+        n.inject("1 4 reset done")
+        assert n.health() == ["Healthy", "Healthy"]
+        n.inject("0 1 page fault")  # VMFAULT: counted, health unchanged
+        n.d.wait_log("VMFAULT(1) on GPU 0")
+        rlog = n.relay.log()
+        assert "event notification registered on 2 processor(s)" in rlog
+        assert "daemon connected" in rlog and "re-enumerating (a daemon asked)" in rlog
+    finally:
+        n.stop()
+
+
+def test_daemon_reconnects_when_the_relay_restarts(scratch):
+    n = RelayNode(scratch)
+    try:
+        n.d.wait_log("events on through the relay")
+        n.relay.signal(signal.SIGTERM)
+        n.relay.proc.wait(timeout=10)
+        n.d.wait_log("event relay: the event relay closed the connection; polling only")
+        assert _value(n.metrics(), "amdgpu_dp_health_events_enabled") == 0
+        n.start_relay()
+        n.d.wait_log("connected to the event relay", timeout=10)
+        deadline = time.time() + 10
+        while _value(n.metrics(), "amdgpu_dp_health_events_enabled") != 1:
+            assert time.time() < deadline
+            time.sleep(0.1)
+        n.inject("0 3 reset")
+        assert n.health() == ["Unhealthy", "Healthy"]
+    finally:
+        n.stop()
+
+
+def test_relay_without_kfd_reports_events_off(scratch):
+    """A relay that is itself denied /dev/kfd (not privileged) says so to the
+    daemon, which polls and names the relay's reason."""
+    n = RelayNode(scratch, relay_env={"LD_PRELOAD": _preload(SIM)})
+    try:
+        log = n.d.wait_log("event relay reports")
+        line = [ln for ln in log.splitlines() if "event relay reports" in ln][0]
+        assert "relay: " in line and "/dev/kfd not openable (EPERM) in the relay's container" in line
+        assert _value(n.metrics(), "amdgpu_dp_health_events_enabled") == 0
+        assert n.first.devices and all(x.health == "Healthy" for x in n.first.devices)
+    finally:
+        n.stop()
+
+
+def test_daemon_serves_while_the_relay_is_absent(scratch):
+    """No relay yet: devices are served, health is polled, and the daemon keeps
+    trying the socket."""
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(1), args=["--health-event-socket", scratch + ".nosuch.sock"],
+                       env={"DP_HEALTH_POLL_MS": "100"}).start()
+    try:
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        assert [x.health for x in c.watch()[0].get(timeout=5).devices] == ["Healthy"]
+        log = d.wait_log("health poll #1")
+        assert "events via relay" in log and "not reachable" in log
+        c.close()
+    finally:
+        d.stop()
+        k.stop()
+
+
+def test_relay_refuses_without_a_socket(scratch):
+    import subprocess
+    r = subprocess.run([harness.DAEMON, "--device-plugin-path", scratch, "--event-relay"], capture_output=True,
+                       text=True, timeout=30, env=harness.Daemon(scratch, fixtures.node(1)).env)
+    assert r.returncode == 1 and "--event-relay needs --health-event-socket" in r.stdout + r.stderr

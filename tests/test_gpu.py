@@ -652,6 +652,7 @@ def test_whole_cu_slots_isolate_memory_unit_neighbours(scratch, snap, probe_buil
     k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
     d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--resource-config", "gpu:gpu-mem-gb:-1",
                                                      "--replica-policy", "pack", "--replica-cu-mask",
+                                                     "--auto-replica-unit", "mib",
                                                      "--memory-unit-cu-slots", "whole"]).start()
     try:
         reg = k.wait_registration(30)
@@ -703,6 +704,7 @@ def test_memory_unit_cu_share_on_mi355x(scratch, snap, probe_built, slots, mask,
     k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
     d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--resource-config", "gpu:gpu-mem-gb:-1",
                                                      "--replica-policy", "pack", "--replica-cu-mask",
+                                                     "--auto-replica-unit", "mib",
                                                      "--memory-unit-cu-slots", slots]).start()
     try:
         reg = k.wait_registration(30)

@@ -32,8 +32,9 @@ def daemon_envs():
         if tok.isupper() and "_" in tok:
             names.add(tok)
     # environment-only settings documented in docs/USER_GUIDE.md
+    # POD_IP: the downward API value the kubelet expands into DP_METRICS_ADDR
     return names | {"DP_DISABLE_HEALTHCHECKS", "DP_HEALTH_POLL_MS", "DP_MAX_RETIRED_PAGES", "ADP_LOG_LEVEL",
-                    "ADP_LOG_FORMAT"}
+                    "ADP_LOG_FORMAT", "POD_IP"}
 
 
 def daemonset(values=None):
@@ -43,8 +44,14 @@ def daemonset(values=None):
     return docs[0]
 
 
-def container(ds):
-    return ds["spec"]["template"]["spec"]["containers"][0]
+def container(ds, name="amdgpu-device-plugin"):
+    (c,) = [c for c in ds["spec"]["template"]["spec"]["containers"] if c["name"] == name]
+    return c
+
+
+def relay(ds):
+    cs = [c for c in ds["spec"]["template"]["spec"]["containers"] if c["name"] == "event-relay"]
+    return cs[0] if cs else None
 
 
 def env(ds):
@@ -54,8 +61,9 @@ def env(ds):
 def check_consistent(ds):
     spec = ds["spec"]["template"]["spec"]
     vols = {v["name"] for v in spec["volumes"]}
-    mounts = {m["name"] for m in container(ds)["volumeMounts"]}
-    assert mounts <= vols, mounts - vols
+    for c in spec["containers"]:
+        mounts = {m["name"] for m in c["volumeMounts"]}
+        assert mounts <= vols, (c["name"], mounts - vols)
     assert set(env(ds)) <= daemon_envs(), set(env(ds)) - daemon_envs()
     assert spec["priorityClassName"] == "system-node-critical"
     labels = ds["spec"]["template"]["metadata"]["labels"]
@@ -70,15 +78,28 @@ def test_defaults_render_a_valid_daemonset():
     assert ds["metadata"]["name"] == "amdgpu-amd-gpu-device-plugin"
     e = env(ds)
     assert e["PARTITION_STRATEGY"] == "none" and e["RESOURCE_CONFIG"] == "gpu:gpu-mem-gb:-1"
-    assert e["REPLICA_POLICY"] == "pack" and e["FAIL_ON_INIT_ERROR"] == "true"
+    assert e["REPLICA_POLICY"] == "auto" and e["FAIL_ON_INIT_ERROR"] == "true"
+    assert e["AUTO_REPLICA_UNIT"] == "auto"
     # health state on by default: env + hostPath volume
     assert e["DP_HEALTH_STATE_FILE"] == "/var/lib/amdgpu-device-plugin/health.state"
     vol = {v["name"]: v for v in ds["spec"]["template"]["spec"]["volumes"]}["health-state"]
     assert vol["hostPath"] == {"path": "/var/lib/amdgpu-device-plugin", "type": "DirectoryOrCreate"}
     assert container(ds)["image"] == "amdgpu-device-plugin:0.1.0"
-    # health events on by default: amdsmi needs /dev/kfd, which only a privileged
-    # pod's device cgroup allows
-    assert e["DP_HEALTH_EVENTS"] == "true" and container(ds)["securityContext"] == {"privileged": True}
+    # health events on by default through the privileged event relay: the
+    # plugin container itself is drop-ALL (privilege separation)
+    assert e["DP_HEALTH_EVENTS"] == "true"
+    assert e["DP_HEALTH_EVENT_SOCKET"] == "/run/amdgpu-dp-events/events.sock"
+    sc = container(ds)["securityContext"]
+    assert sc == {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}}, sc
+    r = relay(ds)
+    assert r["securityContext"] == {"privileged": True}
+    assert r["args"] == ["--event-relay", "--health-event-socket", "/run/amdgpu-dp-events/events.sock"]
+    assert not r.get("ports") and "livenessProbe" not in r  # no network-facing input
+    shared = {m["name"]: m["mountPath"] for m in r["volumeMounts"]}
+    assert shared["event-socket"] == "/run/amdgpu-dp-events"
+    assert {m["name"]: m["mountPath"] for m in container(ds)["volumeMounts"]}["event-socket"] == "/run/amdgpu-dp-events"
+    vols = {v["name"]: v for v in ds["spec"]["template"]["spec"]["volumes"]}
+    assert vols["event-socket"]["emptyDir"]["medium"] == "Memory"
     assert e["DP_MAX_RETIRED_PAGES"] == "-1" and e["DP_LOOP_AFFINITY"] == "none"
     assert "livenessProbe" not in container(ds)
 
@@ -90,12 +111,15 @@ def test_health_events_off_runs_unprivileged():
     check_consistent(ds)
     sc = container(ds)["securityContext"]
     assert sc["allowPrivilegeEscalation"] is False and sc["capabilities"]["drop"] == ["ALL"]
-    assert env(ds)["DP_HEALTH_EVENTS"] == "false"
+    assert env(ds)["DP_HEALTH_EVENTS"] == "false" and "DP_HEALTH_EVENT_SOCKET" not in env(ds)
+    assert relay(ds) is None  # no privileged container at all
+    assert "event-socket" not in {v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]}
     # an explicit securityContext always wins; compat mode is privileged whatever healthEvents says
     custom = {"runAsUser": 0, "capabilities": {"add": ["SYS_ADMIN"]}}
     assert container(daemonset({"securityContext": custom}))["securityContext"] == custom
-    assert container(daemonset({"healthEvents": False, "compatWithCPUManager": True}))["securityContext"] == \
-        {"privileged": True}
+    compat = daemonset({"compatWithCPUManager": True})
+    assert container(compat)["securityContext"] == {"privileged": True}
+    assert relay(compat) is None and "DP_HEALTH_EVENT_SOCKET" not in env(compat)  # events in-process
 
 
 @pytest.mark.parametrize("value,rendered", [(0, "0"), (-1, "-1"), (25, "25"), (None, "-1")])
@@ -116,11 +140,14 @@ def test_driver_hbm_check_mounts_the_hosts_proc():
     assert m == {"name": "host-proc", "mountPath": "/host/proc", "readOnly": True}
     vols = {v["name"]: v for v in ds["spec"]["template"]["spec"]["volumes"]}
     assert vols["host-proc"]["hostPath"]["path"] == "/proc"
+    # reading other containers' /proc/<pid>/fd needs CAP_SYS_PTRACE: that and nothing else
+    assert container(ds)["securityContext"]["capabilities"] == {"drop": ["ALL"], "add": ["SYS_PTRACE"]}
     for vals in ({"enforceMemoryUnits": True}, {"metrics": {"enabled": True}},
                  {"enforceMemoryUnits": True, "metrics": {"enabled": True}, "driverHbmCheck": {"enabled": False}}):
         off = daemonset(vals)
         assert env(off)["DP_DRIVER_HBM_POLL_MS"] == "0" and "DP_HOST_PROC" not in env(off)
         assert "host-proc" not in {v["name"] for v in off["spec"]["template"]["spec"]["volumes"]}
+        assert container(off)["securityContext"]["capabilities"] == {"drop": ["ALL"]}
 
 
 def test_loop_affinity_value():
@@ -158,7 +185,14 @@ def test_metrics_and_node_feature_labels():
     ds = daemonset({"metrics": {"enabled": True, "port": 9500}, "nodeFeatureLabels": {"enabled": True}})
     check_consistent(ds)
     c = container(ds)
-    assert env(ds)["DP_METRICS_ADDR"] == ":9500" and env(ds)["DP_NODE_LABELS_FILE"]
+    # bound to the pod's own IP (downward API), not every interface
+    assert env(ds)["DP_METRICS_ADDR"] == "$(POD_IP):9500" and env(ds)["DP_NODE_LABELS_FILE"]
+    pod_ip = [e for e in c["env"] if e["name"] == "POD_IP"][0]
+    assert pod_ip["valueFrom"] == {"fieldRef": {"fieldPath": "status.podIP"}}
+    names = [e["name"] for e in c["env"]]
+    assert names.index("POD_IP") < names.index("DP_METRICS_ADDR")  # $(VAR) expands only earlier vars
+    wide = daemonset({"metrics": {"enabled": True, "bindAddress": "0.0.0.0"}})
+    assert env(wide)["DP_METRICS_ADDR"] == "0.0.0.0:9400"
     assert c["ports"] == [{"name": "metrics", "containerPort": 9500, "protocol": "TCP"}]
     assert c["livenessProbe"]["httpGet"] == {"path": "/healthz", "port": "metrics"}
     ann = ds["spec"]["template"]["metadata"]["annotations"]
@@ -200,6 +234,16 @@ def test_partition_strategies(strategy):
     assert env(ds)["PARTITION_STRATEGY"] == strategy
     assert "RESOURCE_CONFIG" not in env(ds) and env(ds)["REPLICA_CU_MASK"] == "true"
     assert env(ds)["DP_MEMORY_UNIT_CU_SLOTS"] == "proportional"
+
+
+@pytest.mark.parametrize("values,policy,unit", [({}, "auto", "auto"),
+                                                ({"replicaPolicy": "spread", "autoReplicaUnit": "cu-slot"},
+                                                 "spread", "cu-slot"),
+                                                ({"replicaPolicy": None, "autoReplicaUnit": None}, "auto", "auto")])
+def test_replica_policy_and_unit_values(values, policy, unit):
+    ds = daemonset(values)
+    check_consistent(ds)
+    assert env(ds)["REPLICA_POLICY"] == policy and env(ds)["AUTO_REPLICA_UNIT"] == unit
 
 
 def test_memory_unit_cu_slots_value():

@@ -41,14 +41,17 @@ CASES = [
 ]
 
 
+# "auto" is the daemon's default: a time-slice resource resolves it to spread,
+# so the reference's vectors hold under it unchanged.
+@pytest.mark.parametrize("policy", ["spread", "auto"])
 @pytest.mark.parametrize("name,avail,must,size,want,non_unique,err", CASES, ids=[c[0] for c in CASES])
-def test_prioritize_devices_reference_vectors(name, avail, must, size, want, non_unique, err):
+def test_prioritize_devices_reference_vectors(name, avail, must, size, want, non_unique, err, policy):
     if err is not None:
         with pytest.raises(native.NativeError) as e:
-            native.prioritize(avail, must, size)
+            native.prioritize(avail, must, size, policy=policy)
         assert str(e.value) == err
         return
-    ids, nu = native.prioritize(avail, must, size)
+    ids, nu = native.prioritize(avail, must, size, policy=policy)
     assert ids == want
     assert nu == non_unique
 
