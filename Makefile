@@ -64,6 +64,9 @@ tsan:
 	# the HBM-cap shim: 8 threads of allocations against a cap
 	TSAN_OPTIONS=halt_on_error=1 LD_PRELOAD="$$(gcc -print-file-name=libtsan.so) $(CURDIR)/build/tsan/libadp_memcap.so" \
 	  AMD_GPU_MEMORY_LIMIT_MIB=40 ADP_MEMCAP_KEY=make-tsan-$$$$ build/tsan/adp_memcap_check stress
+	# stream-ordered allocations racing refusal-triggered pool trims
+	TSAN_OPTIONS=halt_on_error=1 LD_PRELOAD="$$(gcc -print-file-name=libtsan.so) $(CURDIR)/build/tsan/libadp_memcap.so" \
+	  AMD_GPU_MEMORY_LIMIT_MIB=100 ADP_MEMCAP_KEY=make-tsan-race-$$$$ build/tsan/adp_memcap_check poolrace
 	TSAN_OPTIONS=halt_on_error=1 LD_PRELOAD="$$(gcc -print-file-name=libtsan.so) $(CURDIR)/build/tsan/libadp_memcap.so" \
 	  AMD_GPU_MEMORY_LIMIT_MIB=100 ADP_MEMCAP_KEY=make-tsan-fork-$$$$ build/tsan/adp_memcap_check fork 60
 	rm -f /dev/shm/adp-memcap-key-make-tsan-*

@@ -9,8 +9,11 @@
 #include <hip/hip_runtime_api.h>
 #include <hip/hip_deprecated.h>
 
+#include <unistd.h>
+
 #include <atomic>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
@@ -127,7 +130,20 @@ hipError_t hipMemPoolTrimTo(hipMemPool_t pool, size_t keep) {
 }
 hipError_t hipMemPoolGetAttribute(hipMemPool_t pool, hipMemPoolAttr attr, void* value) {
   int d = DevOfPool(pool);
-  std::lock_guard<std::mutex> lk(mu);
+  // Test hook: hold the answer back, so a caller's read races other threads' allocations.
+  static const long delay_us = [] {
+    const char* e = getenv("HIP_MOCK_POOL_ATTR_DELAY_US");
+    return e ? atol(e) : 0L;
+  }();
+  std::unique_lock<std::mutex> lk(mu);
+  if (delay_us > 0) {
+    uint64_t v = attr == hipMemPoolAttrReservedMemCurrent ? pool_reserved[d] : pool_used[d];
+    lk.unlock();
+    usleep(static_cast<useconds_t>(delay_us));
+    if (attr != hipMemPoolAttrReservedMemCurrent && attr != hipMemPoolAttrUsedMemCurrent) return hipErrorInvalidValue;
+    *static_cast<uint64_t*>(value) = v;  // the value as it was when read
+    return hipSuccess;
+  }
   if (attr == hipMemPoolAttrReservedMemCurrent) *static_cast<uint64_t*>(value) = pool_reserved[d];
   else if (attr == hipMemPoolAttrUsedMemCurrent) *static_cast<uint64_t*>(value) = pool_used[d];
   else return hipErrorInvalidValue;

@@ -158,7 +158,11 @@ struct State {
   uint64_t cap[kMaxDevices] = {};             // 0 = not capped
   uint64_t pool_live[kMaxDevices] = {};       // bytes of live stream-ordered allocations (this process)
   uint64_t pool_held[kMaxDevices] = {};       // bytes freed to a pool, still counted (this process)
-  hipMemPool_t pools[kMaxDevices][4] = {};    // explicit pools seen (hipMallocFromPoolAsync)
+  hipMemPool_t pools[kMaxDevices][4] = {};    // pools allocated from (explicit, and current at hipMallocAsync)
+  bool pools_overflow[kMaxDevices] = {};      // more pools than `pools` holds: their reserve is unknown
+  // Bumped by every change of pool_live: ReconcilePools reads the pools'
+  // reserve without the lock and applies it only if nothing moved meanwhile.
+  uint64_t pool_gen[kMaxDevices] = {};
   int devices = 0;                            // devices with a cap entry (grant or env)
   int granted = 0;                            // devices with a daemon grant file
   bool verbose = false;
@@ -563,18 +567,20 @@ bool TryReserveLocked(State& s, int dev, uint64_t bytes) {
   return false;
 }
 
-void ReconcilePools(int dev);
+bool ReconcilePools(int dev);
 
 bool Reserve(int dev, uint64_t bytes) {
   State& s = S();
   if (!s.cap[dev]) return true;
-  for (int round = 0;; ++round) {
+  int reconciles = 0;
+  for (;;) {
     {
       Locked lk(s);
       if (TryReserveLocked(s, dev, bytes)) return true;
       // Blocks freed to a stream-ordered pool are still counted: trim the
-      // pools and count only what they still hold, then try once more.
-      if (round == 0 && s.pool_held[dev] && bytes <= s.cap[dev]) goto reconcile;
+      // pools and count only what they still hold, then try once more (a few
+      // times when other threads' stream-ordered calls keep racing the read).
+      if (reconciles < 4 && s.pool_held[dev] && bytes <= s.cap[dev]) goto reconcile;
       if (s.area && !s.released) s.area->refused[dev].fetch_add(1);
       if (s.verbose || !s.warned[dev].exchange(true))
         Log("device %d: refused %.1f MiB (%.1f of %.1f MiB in use%s; the grant)", dev, bytes / 1048576.0,
@@ -582,7 +588,8 @@ bool Reserve(int dev, uint64_t bytes) {
       return false;
     }
   reconcile:
-    ReconcilePools(dev);  // without the lock: it calls into HIP
+    // Without the lock: it calls into HIP. A settled pass is the last one.
+    reconciles = ReconcilePools(dev) ? 4 : reconciles + 1;
   }
 }
 
@@ -636,6 +643,7 @@ void Untrack(const void* key) {
     // Back to its pool, which may keep it reserved: still counted (ReconcilePools).
     s.pool_live[dev] -= Min(bytes, s.pool_live[dev]);
     s.pool_held[dev] += bytes;
+    ++s.pool_gen[dev];
   } else {
     UnreserveLocked(s, dev, bytes);
   }
@@ -678,6 +686,7 @@ void MarkPooled(const void* key, int dev, hipMemPool_t pool) {
   if (!x || x->pooled) return;
   x->pooled = 1;
   s.pool_live[dev] += x->bytes;
+  ++s.pool_gen[dev];
   if (!pool) return;
   for (auto& p : s.pools[dev]) {
     if (p == pool) return;
@@ -686,26 +695,46 @@ void MarkPooled(const void* key, int dev, hipMemPool_t pool) {
       return;
     }
   }
+  s.pools_overflow[dev] = true;
+}
+
+// The pool hipMallocAsync on `dev` draws from now (hipDeviceSetMemPool may have
+// replaced the default): recorded so a later trim covers it too.
+hipMemPool_t CurrentPool(int dev) {
+  static std::atomic<void*> s_cur{nullptr};
+  auto get_current = reinterpret_cast<hipError_t (*)(hipMemPool_t*, int)>(Cached(s_cur, "hipDeviceGetMemPool"));
+  hipMemPool_t p = nullptr;
+  if (!get_current) return nullptr;
+  ++t_depth;
+  if (get_current(&p, dev) != hipSuccess) p = nullptr;
+  --t_depth;
+  return p;
 }
 
 // Trims every pool of `dev` this process allocated from and counts only what
 // they still reserve beyond the live allocations (hipMemPoolAttrReservedMemCurrent);
-// the rest of pool_held is given back to the grant.
-void ReconcilePools(int dev) {
+// the rest of pool_held is given back to the grant. The reserve is read without
+// the lock; if another thread's stream-ordered allocation or free moved
+// pool_live meanwhile, reserve and pool_live no longer describe one moment and
+// nothing is given back (returns false: the caller may try again).
+bool ReconcilePools(int dev) {
   static std::atomic<void*> s_def{nullptr}, s_cur{nullptr}, s_trim{nullptr}, s_attr{nullptr};
   auto get_default = reinterpret_cast<hipError_t (*)(hipMemPool_t*, int)>(Cached(s_def, "hipDeviceGetDefaultMemPool"));
   auto get_current = reinterpret_cast<hipError_t (*)(hipMemPool_t*, int)>(Cached(s_cur, "hipDeviceGetMemPool"));
   auto trim = reinterpret_cast<hipError_t (*)(hipMemPool_t, size_t)>(Cached(s_trim, "hipMemPoolTrimTo"));
   auto attr = reinterpret_cast<hipError_t (*)(hipMemPool_t, hipMemPoolAttr, void*)>(
       Cached(s_attr, "hipMemPoolGetAttribute"));
-  if (!trim || !attr) return;
+  if (!trim || !attr) return true;
   State& s = g_state;
   hipMemPool_t pools[6] = {};
   int n = 0;
+  uint64_t gen = 0;
   {
     Locked lk(s);
+    if (s.pools_overflow[dev]) return true;  // a pool we cannot name: everything stays counted
     for (auto p : s.pools[dev])
       if (p) pools[n++] = p;
+    gen = s.pool_gen[dev];
   }
   hipMemPool_t p = nullptr;
   if (get_default && get_default(&p, dev) == hipSuccess && p) pools[n++] = p;
@@ -721,12 +750,13 @@ void ReconcilePools(int dev) {
     uint64_t r = 0;
     if (attr(pools[i], hipMemPoolAttrReservedMemCurrent, &r) != hipSuccess) {
       --t_depth;
-      return;  // cannot tell: everything stays counted
+      return true;  // cannot tell: everything stays counted
     }
     reserved += r;
   }
   --t_depth;
   Locked lk(s);
+  if (s.pool_gen[dev] != gen) return false;  // raced: the reserve may not cover pool_live's newest bytes
   uint64_t held = reserved > s.pool_live[dev] ? reserved - s.pool_live[dev] : 0;
   if (held < s.pool_held[dev]) {
     if (s.verbose)
@@ -735,6 +765,7 @@ void ReconcilePools(int dev) {
     UnreserveLocked(s, dev, s.pool_held[dev] - held);
     s.pool_held[dev] = held;
   }
+  return true;
 }
 
 // Saturating size arithmetic: an overflowing size is refused at the cap.
@@ -831,7 +862,7 @@ hipError_t hipMallocAsync(void** ptr, size_t size, hipStream_t stream) {
   int dev = StreamDevice(stream);
   bool outer = t_depth == 0;
   hipError_t e = Capped(dev, size, ptr, [&] { return real(ptr, size, stream); });
-  if (outer && e == hipSuccess && ptr && *ptr) MarkPooled(*ptr, dev, nullptr);
+  if (outer && e == hipSuccess && ptr && *ptr) MarkPooled(*ptr, dev, CurrentPool(dev));
   return e;
 }
 

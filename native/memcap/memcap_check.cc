@@ -12,6 +12,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <thread>
 #include <vector>
@@ -65,6 +66,60 @@ int Pool() {
   Phys("phys after malloc 100");
   Out("free 100", hipFree(b));
   Info("info end");
+  return 0;
+}
+
+// `poolrace`: one thread churns stream-ordered allocations (their frees stay
+// reserved by the pool) while others make synchronous allocations that only
+// fit once the pools are trimmed (ReconcilePools). A monitor samples what the
+// "device" physically holds: with the accounting right it never exceeds the
+// cap, whatever the interleaving. Run with HIP_MOCK_POOL_ATTR_DELAY_US to widen
+// the window between reading a pool's reserve and applying it.
+int PoolRace() {
+  std::atomic<bool> stop{false};
+  std::atomic<size_t> max_phys{0};
+  std::atomic<int> async_ok{0}, sync_ok{0}, refused{0};
+  std::thread monitor([&] {
+    while (!stop.load()) {
+      size_t p = hip_mock_physical_bytes(0);
+      size_t m = max_phys.load();
+      while (p > m && !max_phys.compare_exchange_weak(m, p)) {
+      }
+    }
+  });
+  std::vector<std::thread> ts;
+  ts.emplace_back([&] {
+    (void)hipSetDevice(0);
+    auto s0 = reinterpret_cast<hipStream_t>(uintptr_t{1});
+    for (int i = 0; i < 4000; ++i) {
+      void *a = nullptr, *b = nullptr;
+      if (hipMallocAsync(&a, 20 * kMiB, s0) == hipSuccess) ++async_ok;
+      else ++refused;
+      if (hipMallocAsync(&b, 10 * kMiB, s0) == hipSuccess) ++async_ok;
+      else ++refused;
+      if (a) (void)hipFreeAsync(a, s0);
+      if (b) (void)hipFreeAsync(b, s0);
+    }
+  });
+  for (int t = 0; t < 3; ++t)
+    ts.emplace_back([&, t] {
+      (void)hipSetDevice(0);
+      for (int i = 0; i < 1500; ++i) {
+        void* p = nullptr;
+        if (hipMalloc(&p, (30 + 10 * t) * kMiB) == hipSuccess) {
+          ++sync_ok;
+          (void)hipFree(p);
+        } else {
+          ++refused;
+        }
+      }
+    });
+  for (auto& t : ts) t.join();
+  stop.store(true);
+  monitor.join();
+  printf("{\"step\": \"poolrace\", \"async_ok\": %d, \"sync_ok\": %d, \"refused\": %d, \"max_physical_mib\": %.3f}\n",
+         async_ok.load(), sync_ok.load(), refused.load(), max_phys.load() / double(kMiB));
+  Info("poolrace info");
   return 0;
 }
 
@@ -196,6 +251,7 @@ int Processes(int argc, char** argv) {
 int main(int argc, char** argv) {
   if (argc > 1 && strcmp(argv[1], "stress") == 0) return Stress();
   if (argc > 1 && strcmp(argv[1], "pool") == 0) return Pool();
+  if (argc > 1 && strcmp(argv[1], "poolrace") == 0) return PoolRace();
   if (argc > 1 && strcmp(argv[1], "arrays") == 0) return Arrays();
   if (argc > 2) return Processes(argc, argv);
   void *a = nullptr, *b = nullptr, *c = nullptr;

@@ -393,6 +393,29 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
   else d.Line("warn", "device nodes: " + acc);
   if (!f.health_events) {
     d.Line("warn", "health events: off by configuration -- resets are seen by polling only");
+  } else if (!f.health_event_socket.empty()) {
+    // Privilege separation: the relay holds the registration; ask it.
+    int fd = health::ConnectRelay(f.health_event_socket);
+    std::string hello;
+    if (fd >= 0) {
+      pollfd p{fd, POLLIN, 0};
+      char buf[512];
+      if (poll(&p, 1, 2000) > 0) {
+        ssize_t n = recv(fd, buf, sizeof(buf) - 1, 0);
+        if (n > 0) hello.assign(buf, static_cast<size_t>(n));
+      }
+      close(fd);
+    }
+    hello = hello.substr(0, hello.find('\n'));
+    auto line = health::ParseRelayLine(hello);
+    if (fd < 0)
+      d.Line("warn", "health events: the event relay at " + f.health_event_socket + " is not reachable -- is the "
+                     "event-relay container running? Resets are seen by polling until it is");
+    else if (line.kind == "hello" && line.events_ok)
+      d.Line("ok", "health events: through the event relay at " + f.health_event_socket + " (" + hello + ")");
+    else
+      d.Line("warn", "health events: the event relay at " + f.health_event_socket + " reports " +
+                         (line.reason.empty() ? "no hello" : line.reason));
   } else {
     std::vector<void*> handles;
     for (const auto& p : s.procs) handles.push_back(p.handle);
@@ -615,7 +638,10 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   }
   // Plugin sockets found deleted, looked at again when rfd fires.
   std::set<std::string> recheck_sockets;
-  constexpr int kSocketRecheckMs = 20;
+  const int kSocketRecheckMs = [] {  // test hook: widens the window (default 20 ms)
+    const char* e = getenv("ADP_DEBUG_SOCKET_RECHECK_MS");
+    return e && atoi(e) > 0 ? atoi(e) : 20;
+  }();
   auto stand_by = [](const plugin::Plugin& pl) {
     // Another instance (a rollout with maxSurge) unlinked ours and bound the
     // path: binding it back would start a tug of war. The kubelet now talks to

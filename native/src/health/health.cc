@@ -328,7 +328,8 @@ Status Monitor::Start() {
       int kerr = inventory::KfdAccessErrno(cfg_.driver_root);
       if (kerr == EPERM)
         events_reason_ += "; /dev/kfd not openable (EPERM): the container's device cgroup denies it -- run the "
-                          "plugin privileged (helm healthEvents: true) for GPU_PRE_RESET/POST_RESET events";
+                          "event relay privileged (--event-relay + --health-event-socket; helm healthEvents: true) for "
+                          "GPU_PRE_RESET/POST_RESET events";
       else if (kerr)
         events_reason_ += std::string("; /dev/kfd not openable (") + strerror(kerr) + ")";
       LOG_WARN(kComp, "events off: amdsmi event notification unavailable (%s); using polling only",

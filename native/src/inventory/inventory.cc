@@ -413,7 +413,8 @@ std::string DescribeAccess(const std::vector<NodeAccess>& access) {
   std::string why = std::string(strerror(err)) + ": " + denied;
   if (err == EPERM)
     why += " (the container's device cgroup does not allow them -- an unprivileged pod that only "
-           "hostPath-mounts /dev; run the plugin privileged, helm healthEvents: true)";
+           "hostPath-mounts /dev; the plugin does not need them, amdsmi health events do: helm healthEvents: "
+           "true registers those in its privileged event-relay container)";
   else if (err == ENOENT)
     why += " (not present: is /dev mounted from the host, and the driver root right?)";
   else if (err == EACCES)

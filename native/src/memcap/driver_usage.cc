@@ -145,56 +145,45 @@ std::vector<std::string> PidEntries(const std::string& dir, bool* opened) {
 
 }  // namespace
 
-DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFile>& grants,
-                         const std::string& self_cgroup, const std::string& kfd_proc_dir) {
-  DriverScan out;
-  // Candidates: the driver's own list of GPU processes when there is one whose
-  // PIDs live under proc_root, else every process.
-  std::vector<std::string> pids;
-  bool opened = false;
-  if (!kfd_proc_dir.empty()) {
-    pids = PidEntries(kfd_proc_dir, &opened);
-    struct stat st;
-    bool any_here = false;
-    for (const auto& p : pids)
-      if (stat((proc_root + "/" + p).c_str(), &st) == 0) {
-        any_here = true;
-        break;
-      }
-    if (opened && (pids.empty() || any_here)) out.pid_source = "kfd";
-    else pids.clear();
-  }
-  if (out.pid_source != "kfd") {
-    pids = PidEntries(proc_root, &opened);
-    if (!opened) return out;
-  }
+namespace {
+
+struct PidHbm {
+  int pid;
+  std::map<std::string, uint64_t> by_bdf;
+};
+
+// Reads the descriptors of `pids`: render-node fds with DRM fdinfo become
+// per-GPU bytes. `kfd_holders` counts the processes with /dev/kfd open.
+void ReadPids(const std::string& proc_root, const std::vector<std::string>& pids, DriverScan* out,
+              std::vector<PidHbm>* holders, size_t* present, size_t* kfd_holders) {
   // (pdev, drm-client-id): a descriptor shared with another process counts once.
   std::set<std::pair<std::string, uint64_t>> clients;
   // Without a drm-client-id (older kernels) a descriptor cannot be matched to
   // another process's: each (pid, fd) counts on its own.
   std::set<std::tuple<std::string, int, std::string>> anonymous;
-  struct PidHbm {
-    int pid;
-    std::map<std::string, uint64_t> by_bdf;
-  };
-  std::vector<PidHbm> holders;
   for (const auto& pid : pids) {
-    ++out.pids_scanned;
+    ++out->pids_scanned;
     std::string base = proc_root + "/" + pid;
     DIR* fds = opendir((base + "/fd").c_str());
     if (!fds) {
-      if (errno == EACCES || errno == EPERM) ++out.fd_dirs_unreadable;
+      if (errno == EACCES || errno == EPERM) {
+        ++out->fd_dirs_unreadable;
+        ++*present;
+      }
       continue;
     }
+    ++*present;
     PidHbm ph{atoi(pid.c_str()), {}};
+    bool kfd = false;
     int fdd = dirfd(fds);
     while (dirent* f = readdir(fds)) {
       if (!IsPid(f->d_name)) continue;
-      ++out.fd_entries;
+      ++out->fd_entries;
       char target[256];
       ssize_t n = readlinkat(fdd, f->d_name, target, sizeof(target) - 1);
       if (n <= 0) continue;
       target[n] = 0;
+      if (strcmp(target, "/dev/kfd") == 0) kfd = true;
       if (strncmp(target, "/dev/dri/renderD", 16) != 0) continue;
       std::string info = ReadSmall(base + "/fdinfo/" + f->d_name);
       std::string pdev = Field(info, "drm-pdev");
@@ -218,7 +207,43 @@ DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFi
       ph.by_bdf[pdev] += bytes;
     }
     closedir(fds);
-    if (!ph.by_bdf.empty()) holders.push_back(std::move(ph));
+    *kfd_holders += kfd;
+    if (!ph.by_bdf.empty()) holders->push_back(std::move(ph));
+  }
+}
+
+}  // namespace
+
+DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFile>& grants,
+                         const std::string& self_cgroup, const std::string& kfd_proc_dir) {
+  DriverScan out;
+  std::vector<PidHbm> holders;
+  bool opened = false;
+  if (!kfd_proc_dir.empty()) {
+    // The driver's own list of GPU processes. It names host PIDs: it is used
+    // when they are the PIDs of proc_root -- every listed process found there
+    // holds /dev/kfd open -- else (a /proc of another PID namespace, whose
+    // numbers mean other processes) the scan falls back to the full walk.
+    std::vector<std::string> pids = PidEntries(kfd_proc_dir, &opened);
+    if (opened) {
+      DriverScan kfd;
+      kfd.pid_source = "kfd";
+      size_t present = 0, kfd_holders = 0;
+      std::vector<PidHbm> h;
+      ReadPids(proc_root, pids, &kfd, &h, &present, &kfd_holders);
+      if (pids.empty() || (present > 0 && kfd_holders + kfd.fd_dirs_unreadable >= present)) {
+        out = std::move(kfd);
+        holders = std::move(h);
+      } else {
+        out.fd_entries = kfd.fd_entries;  // the wasted look counts as cost
+      }
+    }
+  }
+  if (out.pid_source != "kfd") {
+    std::vector<std::string> pids = PidEntries(proc_root, &opened);
+    if (!opened) return out;
+    size_t present = 0, kfd_holders = 0;
+    ReadPids(proc_root, pids, &out, &holders, &present, &kfd_holders);
   }
 
   // Attribution: own mapping first, then the cgroup of an attributed process

@@ -276,6 +276,10 @@ def test_kfd_pids_from_another_namespace_fall_back_to_the_full_walk(tmp_path):
     kfd = _kfd_dir(str(tmp_path / "kfd"), [900001, 900002])
     s = native.driver_scan(root, kfd_proc_dir=kfd)
     assert s["pid_source"] == "proc" and s["pids_scanned"] == 5 and len(s["procs"]) == 2
+    # host PIDs that collide with unrelated processes of this /proc (no /dev/kfd
+    # open there): not trusted either
+    s = native.driver_scan(root, kfd_proc_dir=_kfd_dir(str(tmp_path / "kfd2"), [100000, 100001]))
+    assert s["pid_source"] == "proc" and len(s["procs"]) == 2
     # no KFD directory at all (no amdgpu driver visible): the full walk too
     assert native.driver_scan(root, kfd_proc_dir=str(tmp_path / "absent"))["pid_source"] == "proc"
     # an empty KFD list is trusted: no GPU process, nothing to read

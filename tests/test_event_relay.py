@@ -158,3 +158,20 @@ def test_relay_refuses_without_a_socket(scratch):
     r = subprocess.run([harness.DAEMON, "--device-plugin-path", scratch, "--event-relay"], capture_output=True,
                        text=True, timeout=30, env=harness.Daemon(scratch, fixtures.node(1)).env)
     assert r.returncode == 1 and "--event-relay needs --health-event-socket" in r.stdout + r.stderr
+
+
+def test_doctor_asks_the_relay(scratch, tmp_path):
+    """--doctor with --health-event-socket: the relay's hello is the verdict
+    (the daemon's own container is not expected to open /dev/kfd)."""
+    import subprocess
+    from test_doctor import _doctor, _find
+    n = RelayNode(scratch)
+    try:
+        _, lines = _doctor(tmp_path, "--device-plugin-path", scratch, "--health-event-socket", n.sock, fx=n.fx)
+        line = _find(lines, "health events:")
+        assert line.startswith("ok") and "through the event relay" in line and "events=ok processors=2" in line
+    finally:
+        n.stop()
+    _, lines = _doctor(tmp_path, "--device-plugin-path", scratch, "--health-event-socket", n.sock + ".gone")
+    line = _find(lines, "health events:")
+    assert line.startswith("warn") and "not reachable" in line

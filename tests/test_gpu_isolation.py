@@ -1,0 +1,227 @@
+"""Real-MI355X checks of the round-4 isolation work (run on the GPU box).
+
+* Container device order: a process that can open only the allocated render
+  nodes (libadp_devcgroup_sim.so, the errno a container's device cgroup gives)
+  numbers its HIP devices exactly as Allocate()'s AMD_GPU_MEMORY_DEVICES lists
+  them (KFD node order), and sees nothing without them.
+* CU-slot memory units: two packed 4-unit pods own disjoint whole CU slots;
+  the first keeps its solo kernel latency next to a CU hog, with all its CUs.
+* Event relay: the daemon under a device-cgroup denial gets amdsmi event
+  notification through the relay running on real libamd_smi.
+* Driver-side HBM scan: KFD's GPU-process list finds a live HIP allocation
+  with the same bytes as the full /proc walk, reading a fraction of the fds.
+"""
+
+import json
+import os
+import re
+import subprocess
+import sys
+import time
+
+import pytest
+
+from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet, native
+
+pytestmark = pytest.mark.gpu
+
+SIM = os.path.join(BUILD_DIR, "libadp_devcgroup_sim.so")
+OUT = "gpurun_out/r4"
+
+
+def _save(name, obj):
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, name), "w") as f:
+        json.dump(obj, f, indent=1)
+
+
+@pytest.fixture(scope="module")
+def snap():
+    s = native.snapshot()
+    assert s["gpus"], "libamd_smi enumerated no GPUs"
+    return s
+
+
+@pytest.fixture(scope="module")
+def probe_exe():
+    from k8s_gpu_sharing_plugin_amd.utils import build
+    build.build_probe()
+    return build.PROBE_EXE
+
+
+def _hip_list(probe_exe, allow):
+    env = {k: v for k, v in os.environ.items() if k not in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES")}
+    env["LD_PRELOAD"] = " ".join(x for x in (env.get("LD_PRELOAD", ""), SIM) if x)
+    env["ADP_DEVCGROUP_ALLOW"] = ":".join(allow)
+    r = subprocess.run([probe_exe, "--list"], env=env, capture_output=True, text=True, timeout=60)
+    out = r.stdout.strip().splitlines()
+    try:
+        devs = json.loads(out[-1]) if out else None
+    except json.JSONDecodeError:
+        devs = None
+    return r.returncode, devs, r.stderr[-1500:]
+
+
+def test_container_hip_order_is_the_memory_device_order(scratch, snap, probe_exe):
+    """Allocate() lists a grant's devices in KFD node order; inside a
+    container (only the allocated render nodes openable) HIP device i is
+    entry i. On this 1-GPU box the list has one entry; the driver's 8-GPU run
+    records the node's three orders in the bench's topology block."""
+    bdf_of = {g["uuid"]: g["bdf"] for g in snap["gpus"]}
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, real_smi=True, args=["--resource-config", "gpu:gpu-mem-gb:-1"]).start()
+    try:
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=10).devices]
+        by_gpu = {}
+        for i in ids:
+            by_gpu.setdefault(i.split("-replica-")[0], []).append(i)
+        want = [u[:2] for u in by_gpu.values()]  # 2 units on every GPU the box shows
+        resp = c.allocate([i for w in want for i in w]).container_responses[0]
+        c.close()
+    finally:
+        assert d.stop() == 0
+        k.stop()
+    envs = dict(resp.envs)
+    order = [bdf_of[u] for u in envs["AMD_GPU_MEMORY_DEVICES"].split(",")]
+    nodes = [s.host_path for s in resp.devices]
+    rc, devs, err = _hip_list(probe_exe, nodes)
+    record = {"memory_devices": envs["AMD_GPU_MEMORY_DEVICES"], "bdf_order": order, "hip_list": devs,
+              "kfd_nodes": {g["bdf"]: g.get("kfd_node") for g in snap["gpus"]},
+              "hip_ids": {g["bdf"]: g["partitions"][0].get("hip_id") for g in snap["gpus"]}}
+    denied_rc, denied, denied_err = _hip_list(probe_exe, ["/dev/kfd"])
+    record.update({"denied_rc": denied_rc, "denied_list": denied, "denied_err": denied_err[-300:]})
+    _save("hip_order.json", record)
+    assert rc == 0 and devs, (rc, devs, err)
+    assert [x["pci"] for x in devs] == order, record
+    assert all(g.get("kfd_node") is not None for g in snap["gpus"]), record
+    # without the render node (a container not given the GPU) HIP sees none:
+    # the probe reports hipGetDeviceCount's "no ROCm-capable device"
+    assert denied_rc != 0 and "no ROCm-capable device" in str(denied), record
+
+
+def test_cu_slot_units_isolate_neighbours_with_every_cu(scratch, snap, probe_exe):
+    """--replica-cu-mask with the default unit (one CU slot + its share of
+    HBM): two packed 4-unit pods get 0:0-31 and 0:32-63 -- 32 CUs each, 4 on
+    every XCD, nothing shared and nothing idle -- and the first keeps its solo
+    kernel latency next to a CU-saturating neighbour."""
+    if snap["gpus"][0]["partitioned"]:
+        pytest.skip("box GPU is partitioned")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--resource-config", "gpu:gpu-mem-gb:-1",
+                                                     "--replica-cu-mask"]).start()
+    try:
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        free = [x.ID for x in c.watch()[0].get(timeout=10).devices]
+        assert len(free) == 32
+        grants = []
+        for _ in range(2):
+            ids = list(c.preferred(free, size=4).container_responses[0].deviceIDs)
+            for i in ids:
+                free.remove(i)
+            grants.append(dict(c.allocate(ids).container_responses[0].envs))
+        c.close()
+    finally:
+        assert d.stop() == 0
+        k.stop()
+    masks = [g["HSA_CU_MASK"] for g in grants]
+    unit = snap["gpus"][0]["vram_mib"] // 32
+    assert masks == ["0:0-31", "0:32-63"], masks
+    assert [g["AMD_GPU_MEMORY_LIMIT_MIB"] for g in grants] == [str(4 * unit)] * 2
+    base = {k_: v for k_, v in os.environ.items() if k_ != "HSA_CU_MASK"}
+    census = subprocess.run([probe_exe, "--device", "0", "--census", "--expect-cus-seen", "32"],
+                            env={**base, "HSA_CU_MASK": masks[0]}, capture_output=True, text=True, timeout=60)
+    assert census.returncode == 0, census.stdout + census.stderr[-2000:]
+    per_xcc = json.loads(census.stdout.strip().splitlines()[-1])["per_xcc"]
+
+    def latency():
+        r = subprocess.run([probe_exe, "--device", "0", "--latency", "1000"], env={**base, "HSA_CU_MASK": masks[0]},
+                           capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    solo = latency()
+    agg = subprocess.Popen([probe_exe, "--device", "0", "--aggressor", "5"], env={**base, "HSA_CU_MASK": masks[1]},
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(1.0)
+        shared = latency()
+    finally:
+        out, err = agg.communicate(timeout=60)
+    assert agg.returncode == 0, err[-2000:]
+    launches = json.loads(out.strip().splitlines()[-1])["aggressor_launches"]
+    _save("cu_slot_units.json", {"masks": masks, "unit_mib": unit, "census_per_xcc": per_xcc, "solo": solo,
+                                 "with_neighbour": shared, "aggressor_launches": launches})
+    assert per_xcc == [4] * 8
+    assert launches > 100
+    assert shared["p50_us"] < 1.5 * solo["p50_us"], (solo, shared)
+
+
+def test_event_relay_on_real_amdsmi(scratch, snap, tmp_path):
+    """The relay registers real amdsmi event notification; the daemon, denied
+    /dev/kfd and the render nodes like an unprivileged pod, runs with events on
+    through it."""
+    sock = str(tmp_path / "events.sock")
+    rdir = scratch + "-relay"
+    os.makedirs(rdir, exist_ok=True)
+    relay = harness.Daemon(rdir, real_smi=True, args=["--event-relay", "--health-event-socket", sock]).start()
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = None
+    try:
+        relay.wait_log("relaying amdsmi events on", 30)
+        env = {"LD_PRELOAD": " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), SIM) if x)}
+        d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--health-event-socket", sock],
+                           env=env).start()
+        k.wait_registration(30)
+        log = d.wait_log("health monitor watching", 30)
+        _save("event_relay.json", {"relay_log": relay.log()[-3000:], "daemon_log": log[-4000:]})
+        assert "event notification registered on" in relay.log(), relay.log()[-2000:]
+        assert "events on through the relay" in log, log[-3000:]
+        assert "device access: Operation not permitted: /dev/kfd" in log  # the daemon itself is denied
+    finally:
+        if d:
+            assert d.stop() == 0
+        k.stop()
+        assert relay.stop() == 0
+
+
+def test_driver_scan_reads_the_gpu_processes_kfd_lists(tmp_path):
+    """A HIP process holding 1 GiB: the scan through KFD's process list finds
+    it with the same bytes as the full /proc walk, reading only GPU processes."""
+    code = r'''
+import ctypes, sys
+lib = ctypes.CDLL("libamdhip64.so")
+p = ctypes.c_void_p()
+rc = lib.hipMalloc(ctypes.byref(p), ctypes.c_size_t(1 << 30))
+lib.hipMemset(p, 1, ctypes.c_size_t(1 << 30)); lib.hipDeviceSynchronize()
+print("holding", rc, flush=True)
+sys.stdin.read()
+'''
+    p = subprocess.Popen([sys.executable, "-c", code], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        line = p.stdout.readline().split()
+        assert line[:2] == ["holding", "0"], (line, p.stderr.read()[-2000:] if p.poll() is not None else "")
+        kfd_dir = "/sys/class/kfd/kfd/proc"
+        listed = sorted(int(x) for x in os.listdir(kfd_dir) if x.isdigit()) if os.path.isdir(kfd_dir) else []
+        fast = native.driver_scan("/proc", kfd_proc_dir=kfd_dir)
+        full = native.driver_scan("/proc")
+        mine = lambda s: sum(x["bytes"] for x in s["procs"] if x["pid"] == p.pid)  # noqa: E731
+        _save("driver_scan_real.json", {"kfd_listed": listed, "child": p.pid,
+                                        "kfd": {k_: fast[k_] for k_ in ("pid_source", "pids_scanned", "fd_entries",
+                                                                        "scan_us", "total")},
+                                        "full": {k_: full[k_] for k_ in ("pid_source", "pids_scanned", "fd_entries",
+                                                                         "scan_us", "total")},
+                                        "child_bytes": {"kfd": mine(fast), "full": mine(full)}})
+        assert listed, "KFD lists no GPU process"
+        if p.pid in listed:  # this /proc is the host PID namespace's: KFD's list is used
+            assert fast["pid_source"] == "kfd" and fast["pids_scanned"] == len(listed)
+            assert fast["fd_entries"] <= full["fd_entries"]
+        else:  # a PID namespace of its own (KFD names host PIDs): the scan falls back to the walk
+            assert fast["pid_source"] == "proc"
+        assert mine(fast) >= 1 << 30 and mine(fast) == mine(full)
+    finally:
+        p.stdin.close()
+        p.wait(timeout=30)

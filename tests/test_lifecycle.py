@@ -627,3 +627,36 @@ def test_unlink_then_bind_takeover_stands_by(scratch):
     assert os.stat(path).st_ino == ino
     other.close()
     k.stop()
+
+
+def test_sigterm_during_the_socket_recheck_exits_at_once(scratch):
+    """A deleted plugin socket is looked at again from a one-shot timer, not a
+    sleep inside the event loop: signals and kubelet events are handled in the
+    meantime. With the re-check window widened to 5 s, SIGTERM right after the
+    delete still exits at once (the old usleep held the loop for the window)."""
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, env={"ADP_DEBUG_SOCKET_RECHECK_MS": "5000"}).start()
+    k.wait_registration()
+    os.unlink(os.path.join(scratch, "amd-gpu.sock"))
+    time.sleep(0.2)  # the delete event is read and the re-check armed
+    t = time.monotonic()
+    assert d.stop() == 0
+    assert time.monotonic() - t < 2.0
+    assert "was removed, restarting" not in d.log()  # the re-check never ran
+    k.stop()
+
+
+def test_socket_recheck_window_reregisters_after_it(scratch):
+    """The deleted socket stays deleted through the window: the daemon
+    re-registers once the timer fires."""
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, env={"ADP_DEBUG_SOCKET_RECHECK_MS": "300"}).start()
+    k.wait_registration()
+    os.unlink(os.path.join(scratch, "amd-gpu.sock"))
+    t = time.monotonic()
+    d.wait_log("was removed, restarting", timeout=5)
+    assert time.monotonic() - t >= 0.25
+    k.wait_registration()
+    assert os.path.exists(os.path.join(scratch, "amd-gpu.sock"))
+    assert d.stop() == 0
+    k.stop()

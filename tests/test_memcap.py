@@ -282,6 +282,23 @@ def test_stream_ordered_pools_never_hold_memory_past_the_cap():
     assert (out["info end"]["free_mib"], out["info end"]["total_mib"]) == (100, 100)
 
 
+@pytest.mark.parametrize("delay_us", ["0", "50"])
+def test_pool_trim_racing_stream_ordered_allocations_never_passes_the_cap(delay_us):
+    """Advisor round 3: ReconcilePools read a pool's reserve without the lock,
+    then subtracted a pool_live that another thread's hipMallocAsync had grown
+    meanwhile -- giving back bytes the pool still held, so later allocations
+    passed the grant (the pre-fix shim let the mock device reach 110-120 MiB
+    under a 100 MiB cap in 2 of 5 runs of this check). Now the reserve is
+    applied only when no stream-ordered allocation or free moved in between."""
+    for _ in range(5):
+        out, _ = _run({"LD_PRELOAD": PRELOAD, "AMD_GPU_MEMORY_LIMIT_MIB": "100",
+                       "HIP_MOCK_POOL_ATTR_DELAY_US": delay_us}, "poolrace")
+        r = out["poolrace"]
+        assert r["max_physical_mib"] <= 100.0, r
+        assert r["async_ok"] > 1000 and r["sync_ok"] > 500, r  # the trims still give memory back
+        assert (out["poolrace info"]["free_mib"], out["poolrace info"]["total_mib"]) == (100, 100)
+
+
 def test_without_the_shim_a_pool_holds_past_the_cap():
     """The same sequence uncapped: the pool's reserve plus the next hipMalloc
     is what the shim has to bound (80 + 50 here)."""
