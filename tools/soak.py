@@ -1,7 +1,7 @@
 """Soak test: the daemon under continuous pod churn, periodic SIGHUP restarts,
 kubelet restarts and metric scrapes; samples its RSS, open fds and threads.
 
-  python tools/soak.py [--seconds 300] [--clients 4] [--real] [--enforce] [--out soak.json]
+  python tools/soak.py [--seconds 300] [--clients 4] [--real] [--enforce] [--holders N] [--out soak.json]
 
 Prints one progress line per sample (every 10 s) and a final JSON summary with
 pods served, restarts, and first/last/max RSS/fds/threads. Exit code 1 if the
@@ -45,7 +45,21 @@ def main():
     ap.add_argument("--max-rss-growth-mib", type=int, default=16)
     ap.add_argument("--enforce", action="store_true",
                     help="replicas with HBM shares enforced by the HBM-cap shim (re-installed on every restart)")
+    ap.add_argument("--holders", type=int, default=0,
+                    help="(--real) HIP processes holding 256 MiB each during the soak: GPU processes for the "
+                         "driver-side scan to find")
     a = ap.parse_args()
+    holders = []
+    if a.real and a.holders:
+        code = ("import ctypes, sys\nlib = ctypes.CDLL('libamdhip64.so')\np = ctypes.c_void_p()\n"
+                "rc = lib.hipMalloc(ctypes.byref(p), ctypes.c_size_t(256 << 20))\n"
+                "lib.hipMemset(p, 1, ctypes.c_size_t(256 << 20)); lib.hipDeviceSynchronize()\n"
+                "print('holding', rc, flush=True)\nsys.stdin.read()\n")
+        for _ in range(a.holders):
+            h = subprocess.Popen([sys.executable, "-c", code], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                 stderr=subprocess.DEVNULL, text=True)
+            h.stdout.readline()
+            holders.append(h)
     d = harness.scratch_dir("adpsoak")
     ksock = os.path.join(d, "kubelet.sock")
     kub = harness.NativeKubelet(ksock).start()
@@ -66,6 +80,7 @@ def main():
         env["DP_DRIVER_HBM_POLL_MS"] = "100"
     dm = harness.Daemon(d, None if a.real else fixtures.node(8), args=args, real_smi=a.real, env=env).start()
     driver_polls = None
+    scans = []  # (source, processes, descriptors, seconds) of the last scan, per scrape
     samples, pods, hups, kubelet_restarts, scrapes = [], 0, 0, 0, 0
     ok = True
     t_end = time.time() + a.seconds
@@ -101,9 +116,19 @@ def main():
                 reg = kub.wait(lambda e: e.get("event") == "register", 30)
             sock = os.path.join(d, reg["endpoint"])
             with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
+                scan = {}
                 for line in r.read().decode().splitlines():
                     if line.startswith("amdgpu_dp_driver_hbm_polls_total "):
                         driver_polls = int(line.split()[1])
+                    elif line.startswith("amdgpu_dp_driver_hbm_scan_processes{"):
+                        scan["source"] = line.split('source="')[1].split('"')[0]
+                        scan["processes"] = int(line.split()[-1])
+                    elif line.startswith("amdgpu_dp_driver_hbm_scan_descriptors "):
+                        scan["descriptors"] = int(line.split()[-1])
+                    elif line.startswith("amdgpu_dp_driver_hbm_scan_seconds "):
+                        scan["ms"] = float(line.split()[-1]) * 1e3
+                if scan.get("ms"):
+                    scans.append(scan)
             scrapes += 1
             if time.time() >= next_sample:
                 s = proc_stats(dm.proc.pid)
@@ -114,6 +139,9 @@ def main():
     finally:
         code = dm.stop()
         kub.stop()
+        for h in holders:
+            h.stdin.close()
+            h.wait(timeout=30)
     if code not in (0, None):
         ok = False
     warm = samples[min(2, len(samples) - 1)] if samples else {}
@@ -126,8 +154,15 @@ def main():
         "rss_mib_max": max((s["rss_mib"] for s in samples), default=None),
         "fds_after_warmup": warm.get("fds"), "fds_last": last.get("fds"),
         "threads_after_warmup": warm.get("threads"), "threads_last": last.get("threads"),
-        "exit_code": code, "driver_hbm_polls": driver_polls,
+        "exit_code": code, "driver_hbm_polls": driver_polls, "holders": len(holders),
     }
+    if scans:
+        ms = sorted(s["ms"] for s in scans)
+        summary["driver_scan"] = {
+            "scrapes": len(scans), "sources": sorted({s.get("source", "?") for s in scans}),
+            "processes_max": max(s.get("processes", 0) for s in scans),
+            "descriptors_max": max(s.get("descriptors", 0) for s in scans),
+            "ms_p50": round(ms[len(ms) // 2], 3), "ms_max": round(ms[-1], 3)}
     if samples and last["rss_mib"] - warm["rss_mib"] > a.max_rss_growth_mib:
         ok = False
     if samples and (last["fds"] > warm["fds"] + 4 or last["threads"] > warm["threads"] + 2):
