@@ -80,7 +80,9 @@ tsan-e2e:
 	ADP_BUILD_DIR=$(CURDIR)/build/tsan TSAN_OPTIONS=log_path=$(CURDIR)/build/tsan-logs/daemon \
 	  $(PY) -m pytest -q -p no:cacheprovider tests/test_e2e_mock.py tests/test_health.py \
 	  tests/test_metrics.py tests/test_lifecycle.py tests/test_robustness.py tests/test_h2_native.py \
-	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py tests/test_preferred.py -k "not additional_ids and not classification and not bruteforce"
+	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py tests/test_preferred.py \
+	  tests/test_event_relay.py tests/test_policy_units.py tests/test_hip_order.py \
+	  -k "not additional_ids and not classification and not bruteforce and not snapshot_reports and not scan_reads_only and not another_namespace and not without_client_id"
 	@if ls build/tsan-logs/* >/dev/null 2>&1; then cat build/tsan-logs/*; exit 1; fi
 
 # The daemon under ASan/UBSan/LSan, driven by the same end-to-end suites.
@@ -89,7 +91,7 @@ tsan-e2e:
 # protobuf codec, the config front end, grant accounting files + /metrics, the
 # driver-side /proc scan (native/fuzz/). FUZZ_SECONDS per target, in parallel;
 # corpora grow in build/fuzz/corpus/<target>; a crash leaves build/fuzz/crash-*.
-FUZZ_TARGETS ?= plugin h2 h2_diff proto config grantfile procscan
+FUZZ_TARGETS ?= plugin h2 h2_diff proto config grantfile procscan relay
 FUZZ_SECONDS ?= 60
 CLANGXX      ?= /opt/rocm/lib/llvm/bin/clang++
 fuzz:
@@ -107,11 +109,13 @@ asan-e2e:
 	cmake -S native -B build/asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DADP_SANITIZE=ON >/dev/null
 	ninja -C build/asan -j$(JOBS) amdgpu-device-plugin amdgpu-dp-kubelet amdsmi_mock
 	rm -rf build/asan-logs && mkdir -p build/asan-logs
-	ADP_BUILD_DIR=$(CURDIR)/build/asan ASAN_OPTIONS=log_path=$(CURDIR)/build/asan-logs/daemon:detect_leaks=1 \
+	ADP_BUILD_DIR=$(CURDIR)/build/asan ASAN_OPTIONS=log_path=$(CURDIR)/build/asan-logs/daemon:detect_leaks=1:verify_asan_link_order=0 \
 	  UBSAN_OPTIONS=print_stacktrace=1:log_path=$(CURDIR)/build/asan-logs/ubsan \
 	  $(PY) -m pytest -q -p no:cacheprovider tests/test_e2e_mock.py tests/test_health.py \
 	  tests/test_metrics.py tests/test_lifecycle.py tests/test_robustness.py tests/test_h2_native.py \
-	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py tests/test_preferred.py -k "not additional_ids and not classification and not bruteforce"
+	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py tests/test_preferred.py \
+	  tests/test_event_relay.py tests/test_policy_units.py tests/test_hip_order.py \
+	  -k "not additional_ids and not classification and not bruteforce and not snapshot_reports and not scan_reads_only and not another_namespace and not without_client_id"
 	@if ls build/asan-logs/* >/dev/null 2>&1; then cat build/asan-logs/*; exit 1; fi
 
 # Line coverage of native/src from the unit, stress and CPU end-to-end suites.

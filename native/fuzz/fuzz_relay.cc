@@ -1,0 +1,62 @@
+// Coverage-guided fuzzing (libFuzzer) of the event-relay wire lines
+// (health/relay.cc): the daemon parses whatever arrives on its relay socket.
+// Checks: no crash; an accepted event line re-formatted from its fields parses
+// back to the same fields (message newlines folded to spaces); a hello's
+// verdict is exactly "events=ok" present.
+#include <fuzzer/FuzzedDataProvider.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+
+#include "common/log.h"
+#include "health/relay.h"
+
+using namespace adp;
+
+namespace {
+[[noreturn]] void Fail(const char* what) {
+  fprintf(stderr, "invariant violated: %s\n", what);
+  abort();
+}
+}  // namespace
+
+extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
+  static bool quiet = (SetLogLevel(LogLevel::kError), true);
+  (void)quiet;
+  std::string line(reinterpret_cast<const char*>(data), size);
+  health::RelayLine r = health::ParseRelayLine(line);
+  if (r.kind == "event") {
+    if (r.bdf.find(' ') != std::string::npos) Fail("bdf with a space");
+    smi::ProcessorInfo p;
+    p.kfd_node = r.node;
+    p.bdf = r.bdf == "-" ? "" : r.bdf;
+    p.partition_id = r.part;
+    health::RelayLine back = health::ParseRelayLine(health::FormatRelayEvent(p, r.type, r.message));
+    std::string folded = r.message;
+    for (char& c : folded)
+      if (c == '\n' || c == '\r') c = ' ';
+    while (!folded.empty() && (folded.back() == '\n' || folded.back() == '\r' || folded.back() == ' ')) folded.pop_back();
+    std::string got = back.message;
+    while (!got.empty() && got.back() == ' ') got.pop_back();
+    if (back.kind != "event" || back.node != r.node || back.part != r.part || back.type != r.type) Fail("round trip");
+    if (!r.bdf.empty() && r.bdf != "-" && back.bdf != r.bdf) Fail("bdf round trip");
+    if (got != folded) Fail("message round trip");
+  } else if (r.kind == "hello") {
+    // ok iff the first "events=" token is exactly "events=ok"
+    std::string first;
+    std::string body = line;
+    while (!body.empty() && (body.back() == '\n' || body.back() == '\r')) body.pop_back();
+    for (size_t b = 0; b <= body.size() && first.empty();) {
+      size_t e = body.find(' ', b);
+      if (e == std::string::npos) e = body.size();
+      std::string tok = body.substr(b, e - b);
+      if (tok.size() >= 7 && tok.compare(0, 7, "events=") == 0) first = tok;
+      b = e + 1;
+    }
+    if (r.events_ok != (first == "events=ok")) Fail("hello verdict");
+  } else if (!r.kind.empty()) {
+    Fail("unknown kind");
+  }
+  return 0;
+}

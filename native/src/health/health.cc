@@ -427,6 +427,7 @@ void Monitor::RelayConnect() {
     return;
   }
   relay_buf_.clear();
+  relay_synced_ = false;
   events_reason_ = "waiting for the event relay's hello";
 }
 
@@ -450,7 +451,10 @@ void Monitor::RelayWait(int ms, std::vector<smi::Event>* out) {
   while ((nl = relay_buf_.find('\n')) != std::string::npos) {
     RelayLine l = ParseRelayLine(std::string_view(relay_buf_).substr(0, nl));
     relay_buf_.erase(0, nl + 1);
-    if (l.kind == "hello") {
+    if (l.kind == "hello" && !l.after_reinit && !relay_synced_) {
+      // The connect hello predates the re-enumeration this monitor asked for.
+    } else if (l.kind == "hello") {
+      relay_synced_ = true;
       bool was = events_ok_;
       events_ok_ = l.events_ok;
       events_reason_ = l.events_ok ? "" : "relay: " + l.reason;

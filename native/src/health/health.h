@@ -198,6 +198,7 @@ class Monitor {
   // partial input line, and when a connection was last tried.
   int relay_fd_ = -1;
   std::string relay_buf_;
+  bool relay_synced_ = false;  // the relay answered this connection's "reinit"
   int64_t relay_tried_ms_ = -1000000;
   void RelayConnect();
   void RelayClose(const std::string& why);

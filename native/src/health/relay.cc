@@ -69,6 +69,7 @@ RelayLine ParseRelayLine(std::string_view line) {
   if (line.rfind("hello ", 0) == 0) {
     r.kind = "hello";
     r.events_ok = Kv(line, "events") == "ok";
+    r.after_reinit = line.rfind("hello v1 reinit ", 0) == 0;
     size_t at = line.find(" reason=");
     if (at != std::string_view::npos) r.reason = std::string(line.substr(at + 8));
     return r;
@@ -225,7 +226,9 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
       }
     }
     bool do_reinit = false;
-    for (size_t i = 0; i < clients.size(); ++i) {
+    // Only the clients polled above (accept may have appended new ones).
+    const size_t polled = pfds.size() - 2;
+    for (size_t i = 0; i < polled; ++i) {
       auto& c = clients[i];
       if (c.fd < 0 || !(pfds[2 + i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
       char buf[256];
@@ -253,8 +256,11 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     if (do_reinit) {
       LOG_INFO(kComp, "re-enumerating (a daemon asked)");
       enumerate_and_register(true);
+      // Marked, so a daemon tells the state after its own request from the
+      // hello every connection gets first (sent before the request was read).
+      std::string fresh = "hello v1 reinit " + events_state + "\n";
       for (auto& c : clients)
-        if (!SendAll(c.fd, hello())) {
+        if (!SendAll(c.fd, fresh)) {
           close(c.fd);
           c.fd = -1;
         }

@@ -11,12 +11,15 @@
 // kubelet input -- one line per client, "reinit", is all it reads.
 //
 // Wire protocol (text lines over SOCK_STREAM):
-//   relay -> daemon  "hello v1 events=ok processors=<n>"
-//                    "hello v1 events=off reason=<text>"     (registration failed)
+//   relay -> daemon  "hello v1 events=ok processors=<n>"         (on connect)
+//                    "hello v1 events=off reason=<text>"       (registration failed)
+//                    "hello v1 reinit events=ok processors=<n>" (after a "reinit")
 //                    "event node=<kfd node|-> bdf=<bdf> part=<partition id> type=<t> <message>"
 //   daemon -> relay  "reinit"   re-enumerate (amdsmi_shut_down + init) and register
-//                               again, then a new hello (a new daemon generation,
-//                               e.g. after a re-partition)
+//                               again, then a "reinit" hello to every client (a new
+//                               daemon generation, e.g. after a re-partition). A
+//                               daemon takes its event state from that hello only:
+//                               the connect hello predates the re-registration.
 #pragma once
 
 #include <string>
@@ -30,6 +33,7 @@ namespace adp::health {
 struct RelayLine {
   std::string kind;
   bool events_ok = false;
+  bool after_reinit = false;  // hello sent after a re-enumeration a daemon asked for
   std::string reason;      // hello with events=off
   uint32_t node = 0xffffffffu;  // KFD topology node of the processor ("-" = unreported)
   std::string bdf;

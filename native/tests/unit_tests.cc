@@ -198,7 +198,9 @@ static void TestRelayLines() {
   r = health::ParseRelayLine(health::FormatRelayEvent(p, 4, ""));
   CHECK(r.kind == "event" && r.node == 0xffffffffu && r.type == 4 && r.message.empty());
   r = health::ParseRelayLine("hello v1 events=ok processors=8");
-  CHECK(r.kind == "hello" && r.events_ok);
+  CHECK(r.kind == "hello" && r.events_ok && !r.after_reinit);
+  r = health::ParseRelayLine("hello v1 reinit events=ok processors=8");
+  CHECK(r.kind == "hello" && r.events_ok && r.after_reinit);
   r = health::ParseRelayLine("hello v1 events=off reason=NO_PERM: denied");
   CHECK(r.kind == "hello" && !r.events_ok && r.reason == "NO_PERM: denied");
   for (const char* bad : {"", "event", "event node=x bdf=a part=0 type=3", "event node=1 bdf=a part=0",
