@@ -220,6 +220,45 @@ def _device_order(snap, rank_bdfs):
     return out
 
 
+def _container_view(snap):
+    """HIP's numbering as a container sees it, on real GPUs: a process that may
+    open only some render nodes (libadp_devcgroup_sim.so returns EPERM for the
+    others, as a container's device cgroup does) lists its HIP devices. For
+    every served GPU together, and for the last and first GPU requested in
+    reverse order, the listed PCI addresses must come in KFD-node order -- the
+    order the plugin gives every per-device container list in. Reported, never
+    fatal."""
+    import subprocess
+    from .. import BUILD_DIR
+    from ..utils.build import PROBE_EXE
+    sim = os.path.join(BUILD_DIR, "libadp_devcgroup_sim.so")
+    gpus = snap.get("gpus") or []
+    if not gpus or any(g.get("kfd_node") is None for g in gpus) or not os.path.exists(PROBE_EXE):
+        return {"skipped": "no KFD nodes or probe"}
+    render = {g["bdf"]: [p["render"] for p in g["partitions"] if p.get("render")] for g in gpus}
+    kfd = [g["bdf"] for g in sorted(gpus, key=lambda g: g["kfd_node"])]
+
+    def hip_list(bdfs):
+        env = {k: v for k, v in os.environ.items() if k not in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                                                                  "CUDA_VISIBLE_DEVICES")}
+        env["LD_PRELOAD"] = " ".join(x for x in (env.get("LD_PRELOAD", ""), sim) if x)
+        env["ADP_DEVCGROUP_ALLOW"] = ":".join(["/dev/kfd"] + [r for b in bdfs for r in render[b]])
+        r = subprocess.run([PROBE_EXE, "--list"], env=env, capture_output=True, text=True, timeout=120)
+        devs = json.loads(r.stdout.strip().splitlines()[-1])
+        return [d["pci"] for d in devs] if isinstance(devs, list) else devs
+
+    cases = [kfd] + ([[kfd[-1], kfd[0]]] if len(kfd) >= 2 else [])
+    out = {"cases": []}
+    try:
+        for req in cases:
+            want = [b for b in kfd if b in req]
+            out["cases"].append({"granted": req, "kfd_order": want, "hip": hip_list(req)})
+        out["hip_order_is_kfd_order"] = all(c["hip"] == c["kfd_order"] for c in out["cases"])
+    except Exception as e:  # diagnostic only
+        out["error"] = str(e)
+    return out
+
+
 def _topology(snap, rank_bdfs):
     """The node block of the JSON: what GetPreferredAllocation scores against."""
     if not snap:
@@ -324,6 +363,7 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
         dist.all_gather_object(rank_bdfs, my_bdf)
     daemon = kub = None
     info = {}
+    info_snap = {}
     try:
         if rank == 0:
             d = harness.scratch_dir("adpbench")
@@ -346,6 +386,7 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
                            (config not in POD_SIZE or e.get("resource", "").endswith("/gpu")), 20)
             devs = kub.wait(lambda e: e.get("event") == "devices" and e.get("resource") == reg["resource"], 20)
             snap = _node_snapshot(real, fx, served)
+            info_snap = snap
             bdf_of = _bdf_map(snap)
             sock = os.path.join(d, reg["endpoint"])
             info = {"socket": sock, "resource": reg["resource"],
@@ -508,6 +549,8 @@ def run(gpus=1, steps=20, warmup=2, pods_per_step=100, config="spx-none", force_
             # The node the daemon served, and a k-GPU pod's placement on it.
             result["topology"] = info.get("topology")
             result["preferred_k"] = info.get("preferred_k")
+            if real and probe and isinstance(result["topology"], dict) and "device_order" in result["topology"]:
+                result["topology"]["device_order"]["container_view"] = _container_view(info_snap)
             probes = [s.get("probe") for s in everyone if s.get("probe")]
             if probes:
                 result["probe"] = probes

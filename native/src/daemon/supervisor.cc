@@ -361,6 +361,30 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
   for (const auto& g : s.gpus) parts += g.partitions.size();
   d.Line("ok", "enumeration: " + std::to_string(s.gpus.size()) + " GPU(s), " + std::to_string(parts) +
                    " compute partition(s), " + s.gpus[0].compute_mode + "/" + s.gpus[0].memory_mode);
+  {
+    // How a container numbers its GPUs: KFD topology-node order (what every
+    // per-device list Allocate() returns follows), not necessarily amdsmi's.
+    std::vector<std::pair<uint32_t, int>> nodes;
+    bool known = true;
+    for (const auto& g : s.gpus) {
+      known = known && g.kfd_node != inventory::kNoKfdNode;
+      nodes.emplace_back(g.kfd_node, g.node_index);
+    }
+    std::sort(nodes.begin(), nodes.end());
+    std::string order;
+    bool differs = false;
+    for (size_t i = 0; i < nodes.size(); ++i) {
+      order += (i ? "," : "") + std::to_string(nodes[i].second);
+      differs = differs || nodes[i].second != s.gpus[i].node_index;
+    }
+    if (!known)
+      d.Line("warn", "device order: amdsmi reports no KFD topology node for some GPU -- per-device container lists "
+                     "(HSA_CU_MASK, AMD_GPU_MEMORY_*) assume HIP numbers GPUs in amdsmi order");
+    else
+      d.Line("ok", "device order: containers number GPUs in KFD-node order (amdsmi indices " + order + ")" +
+                       (differs ? ", which differs from amdsmi's order: per-device container lists follow KFD order"
+                                : ""));
+  }
   auto specs = strategy::BuildPluginSpecs(s, v.partition, v.rc, f.resource_prefix);
   if (!specs.ok()) {
     d.Line("FAIL", "partition strategy: " + specs.status().message());

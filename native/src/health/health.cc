@@ -314,9 +314,9 @@ Status Monitor::Start() {
     // Privilege separation: the relay holds the registration; this process
     // needs no /dev/kfd. It asks the relay to re-enumerate (a new generation
     // may follow a re-partition) and takes its hello as the event state.
+    // The monitor thread reads its answer: the supervisor is not held up here.
     RelayConnect();
-    if (relay_fd_ >= 0) RelayWait(1000, nullptr);
-    if (!events_ok_)
+    if (relay_fd_ < 0)
       LOG_WARN(kComp, "events via relay %s: %s; polling meanwhile, reconnecting every second",
                cfg_.event_relay.c_str(), events_reason_.c_str());
   } else {
@@ -372,7 +372,7 @@ Status Monitor::Start() {
     }
   }
   LOG_INFO(kComp, "health monitor watching %zu GPU(s) (events %s, poll every %d ms)", snap_->gpus.size(),
-           events_ok_ ? "on" : "off", cfg_.poll_interval_ms);
+           events_ok_ ? "on" : relay_fd_ >= 0 ? "through the relay, once it answers" : "off", cfg_.poll_interval_ms);
   if (!events_ok_ && cfg_.poll_interval_ms == 0 && cfg_.event_relay.empty()) return Status::Ok();
   stop_.store(false);
   if (wake_fd_ < 0) wake_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);

@@ -151,3 +151,19 @@ def test_doctor_reports_memory_unit_cu_slots(tmp_path, unit_args, level, says):
     assert line and line.split()[0] == level and "amd.com/gpu-mem-gb" in line and says in line, lines
     _, lines = _doctor(tmp_path, *args)
     assert _find(lines, "CU shares:") is None
+
+
+def test_doctor_reports_the_container_device_order(tmp_path):
+    """KFD-node order is how a container numbers its GPUs; the doctor says it
+    and whether it differs from amdsmi's enumeration order on this node."""
+    fx = fixtures.node(3)
+    _, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), fx=fx)
+    line = _find(lines, "device order:")
+    assert line.startswith("ok") and "amdsmi indices 0,1,2)" in line and "differs" not in line, line
+    fx["gpus"][0]["kfd_node"] = 40
+    _, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), fx=fx)
+    line = _find(lines, "device order:")
+    assert "amdsmi indices 1,2,0" in line and "differs from amdsmi's order" in line, line
+    fx["gpus"][1]["kfd_node"] = None
+    _, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), fx=fx)
+    assert _find(lines, "device order:").startswith("warn")
