@@ -175,7 +175,8 @@ def test_event_relay_on_real_amdsmi(scratch, snap, tmp_path):
         d = harness.Daemon(scratch, real_smi=True, args=["--devices", "0", "--health-event-socket", sock],
                            env=env).start()
         k.wait_registration(30)
-        log = d.wait_log("health monitor watching", 30)
+        d.wait_log("health monitor watching", 30)
+        log = d.wait_log("events on through the relay", 30)
         _save("event_relay.json", {"relay_log": relay.log()[-3000:], "daemon_log": log[-4000:]})
         assert "event notification registered on" in relay.log(), relay.log()[-2000:]
         assert "events on through the relay" in log, log[-3000:]
@@ -225,3 +226,86 @@ sys.stdin.read()
     finally:
         p.stdin.close()
         p.wait(timeout=30)
+
+
+def _userns_mounts_ok():
+    try:
+        return subprocess.run(["unshare", "-rm", "sh", "-c", "mount --rbind /dev /mnt && true"], capture_output=True,
+                              timeout=20).returncode == 0
+    except (OSError, subprocess.TimeoutExpired):
+        return False
+
+
+def test_images_on_the_real_gpu(scratch, snap, tmp_path):
+    """The assembled DaemonSet image (tests/test_image_rootfs.py) on the
+    MI355X: its own libamd_smi enumerates the GPU and its daemon allocates it
+    to a kubelet; the validation image's HIP runtime runs the probe's
+    checksummed HBM copy. With user+mount namespaces the images run chrooted
+    with the host's /dev, /sys and /proc bound in (as the chart mounts them);
+    without them (this pool's boxes) the image's own loader runs them with
+    only the image's library directories, and LD_DEBUG=files shows every
+    shared object came from the image."""
+    from k8s_gpu_sharing_plugin_amd.utils import image
+    binds = ("/dev", "/sys", "/proc")
+    chroot = _userns_mounts_ok()
+
+    def cmd(rootfs, argv):
+        return image.chroot_cmd(rootfs, argv, binds) if chroot else image.loader_cmd(rootfs, argv)
+    env = {k: v for k, v in os.environ.items() if k not in ("LD_PRELOAD", "LD_LIBRARY_PATH", "AMD_SMI_LIB")}
+    dbg = dict(env, LD_DEBUG="files")
+    rt = str(tmp_path / "runtime")
+    image.build_rootfs(rt)
+    rep = subprocess.run(cmd(rt, ["/usr/bin/amdgpu-device-plugin", "--smi-report"]), capture_output=True,
+                         text=True, timeout=120, env=dbg)
+    report = json.loads(rep.stdout[rep.stdout.index("{"):]) if rep.returncode == 0 and "{" in rep.stdout else {}
+    daemon_libs = image.loaded_files(rep.stderr)
+    pdir = os.path.join(rt, "var/lib/kubelet/device-plugins") if chroot else scratch
+    os.makedirs(pdir, exist_ok=True)
+    k = kubelet.StubKubelet(os.path.join(pdir, "kubelet.sock")).start()
+    if chroot:
+        dm = image.image_daemon(rt, ["--devices", "0"], binds=binds)
+    else:
+        dm = harness.Daemon(scratch, real_smi=True, args=["--devices", "0"])
+        dm.env = dict(env, ADP_LOG_LEVEL="info")
+        dm._log = open(dm.log_path, "w")
+        dm.proc = subprocess.Popen(cmd(rt, ["/usr/bin/amdgpu-device-plugin", "--device-plugin-path", scratch,
+                                            "--devices", "0"]), env=dm.env, stdout=dm._log,
+                                   stderr=subprocess.STDOUT)
+    try:
+        reg = k.wait_registration(60)
+        c = kubelet.PluginClient(os.path.join(pdir, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=20).devices]
+        specs = [s.container_path for s in c.allocate(ids[:1]).container_responses[0].devices]
+        maps = open(f"/proc/{dm.proc.pid}/maps").read() if dm.proc.poll() is None else ""
+        c.close()
+    finally:
+        code = dm.stop()
+        k.stop()
+    smi_mapped = sorted({ln.split()[-1] for ln in maps.splitlines() if "libamd_smi" in ln})
+    val = str(tmp_path / "validation")
+    image.build_rootfs(val, stage="validation")
+    probe = subprocess.run(cmd(val, ["/usr/bin/amdgpu-dp-probe", "--device", "0", "--bytes", str(64 << 20),
+                                     "--iters", "2"]), capture_output=True, text=True, timeout=180, env=dbg)
+    result = json.loads(probe.stdout.strip().splitlines()[-1]) if probe.stdout.strip() else {}
+    probe_libs = image.loaded_files(probe.stderr)
+    # Libraries the environment preloads into every process (outside any
+    # image) show up in a bare `--list` of the image's loader as well.
+    base = subprocess.run(image.loader_cmd(rt, ["/usr/bin/amdgpu-device-plugin"])[:-1] + ["--list"] +
+                          image.loader_cmd(rt, ["/usr/bin/amdgpu-device-plugin"])[-1:],
+                          capture_output=True, text=True, timeout=60, env=dbg)
+    preloaded = {f for f in image.loaded_files(base.stderr) if not f.startswith(rt)}
+    outside = [f for f in daemon_libs + probe_libs if not f.startswith((rt, val)) and f not in preloaded]
+    _save("images_on_gpu.json", {"mode": "chroot" if chroot else "image loader", "smi_report_rc": rep.returncode,
+                                 "enumeration": report.get("enumeration"), "daemon_libs": daemon_libs,
+                                 "daemon_libamd_smi_mapped": smi_mapped, "advertised": ids, "device_specs": specs,
+                                 "daemon_exit": code, "probe": result, "probe_libs": probe_libs,
+                                 "loaded_from_outside_the_images": outside,
+                                 "probe_stderr_tail": [ln for ln in probe.stderr.splitlines()
+                                                       if "file=" not in ln][-20:]})
+    assert rep.returncode == 0 and report.get("enumeration") == "ok", rep.stderr[-2000:]
+    assert ids == [snap["gpus"][0]["uuid"]] and "/dev/kfd" in specs
+    assert specs[-1] == snap["gpus"][0]["partitions"][0]["render"]
+    assert code == 0
+    assert smi_mapped and all(p.startswith(rt) for p in smi_mapped), smi_mapped
+    assert probe.returncode == 0 and result.get("checksum_ok"), result
+    assert not outside, outside  # every shared object came from the images

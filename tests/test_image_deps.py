@@ -17,67 +17,24 @@ deployments/container/Dockerfile.ubuntu:15-55, which needs only the Go binary.
 import glob
 import os
 import re
-import shlex
 import subprocess
 
 import pytest
 
 from k8s_gpu_sharing_plugin_amd import DAEMON, PROBE_BIN
+from k8s_gpu_sharing_plugin_amd.utils import image
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ROCM_LIB = "/opt/rocm/lib"
-
-# Libraries every base image has (glibc + the C++ runtime apt/microdnf use).
-BASE = {
-    "ubuntu": {"libc.so.6", "libm.so.6", "ld-linux-x86-64.so.2", "libpthread.so.0", "libdl.so.2", "librt.so.1",
-               "libgcc_s.so.1", "libstdc++.so.6", "libz.so.1", "libzstd.so.1"},
-    "ubi9": {"libc.so.6", "libm.so.6", "ld-linux-x86-64.so.2", "libpthread.so.0", "libdl.so.2", "librt.so.1",
-             "libgcc_s.so.1", "libz.so.1", "libzstd.so.1"},
-}
-# soname -> package that installs it, per distribution.
-PACKAGES = {
-    "ubuntu": {"libnghttp2.so.14": "libnghttp2-14", "libdrm.so.2": "libdrm2", "libdrm_amdgpu.so.1": "libdrm-amdgpu1",
-               "libyaml-0.so.2": "libyaml-0-2", "libelf.so.1": "libelf1", "libnuma.so.1": "libnuma1",
-               "libz.so.1": "zlib1g", "libzstd.so.1": "libzstd1", "libstdc++.so.6": "libstdc++6"},
-    "ubi9": {"libnghttp2.so.14": "libnghttp2", "libdrm.so.2": "libdrm", "libdrm_amdgpu.so.1": "libdrm",
-             "libyaml-0.so.2": "libyaml", "libelf.so.1": "elfutils-libelf", "libnuma.so.1": "numactl-libs",
-             "libstdc++.so.6": "libstdc++"},
-}
+# The Dockerfile model shared with the rootfs assembly (tests/test_image_rootfs.py).
+BASE, PACKAGES, BUILT, stages = image.BASE, image.PACKAGES, image.BUILT, image.stages
 # Libraries the daemon itself dlopens (native/src/smi/smi.cc, native/src/daemon/yaml.cc).
 DAEMON_DLOPENS = {"libamd_smi.so.26", "libyaml-0.so.2"}
-# The build stage's outputs, as built in this tree.
-BUILT = {"/build/amdgpu-device-plugin": DAEMON, "/build/amdgpu-dp-probe": PROBE_BIN,
-         "/build/libadp_memcap.so": os.path.join(os.path.dirname(DAEMON), "libadp_memcap.so")}
-
-
-def stages(path):
-    """[(name, base image, [instruction lines])] of a Dockerfile (continuations joined)."""
-    text = open(path).read().replace("\\\n", " ")
-    out = []
-    for line in text.splitlines():
-        line = line.strip()
-        if not line or line.startswith("#"):
-            continue
-        m = re.match(r"FROM\s+(\S+)(?:\s+AS\s+(\S+))?", line, re.I)
-        if m:
-            out.append((m.group(2) or "", m.group(1), []))
-        elif out:
-            out[-1][2].append(line)
-    return out
 
 
 def stage_contents(lines):
-    pkgs, copies = set(), []
-    for line in lines:
-        if line.startswith("RUN"):
-            for cmd in re.split(r"&&|;", line[3:]):
-                words = shlex.split(cmd)
-                if words[:2] in (["apt-get", "install"], ["microdnf", "install"]):
-                    pkgs |= {w for w in words[2:] if not w.startswith("-")}
-        elif line.startswith("COPY") and "--from=build" in line:
-            args = [a for a in shlex.split(line)[1:] if not a.startswith("--")]
-            copies += args[:-1]
-    return pkgs, copies
+    pkgs, copies, _, _ = image.stage_contents(lines)
+    return pkgs, [src for sources, _ in copies for src in sources]
 
 
 def sonames(path):
