@@ -4,7 +4,7 @@ JOBS       ?= 8
 PY         ?= python3
 GPURUN     ?= /usr/local/graft/bin/gpurun
 
-.PHONY: all build probe test test-native test-gpu bench asan tsan tsan-e2e asan-e2e fuzz coverage lint image clean
+.PHONY: all build probe test test-native test-gpu bench asan tsan tsan-e2e asan-e2e fuzz coverage lint image image-rootfs clean
 
 # Containerised targets (reference Makefile:44-74): `make docker-<target>` runs
 # `make <target>` in the development image built from docker/Dockerfile.devel.
@@ -133,6 +133,12 @@ lint:
 
 image:
 	$(MAKE) -f deployments/container/Makefile build-ubuntu
+
+# Without a container engine: assemble the runtime/validation stages of
+# Dockerfile.ubuntu as root filesystems and run the daemon in them (chrooted,
+# unprivileged user namespace), against a stub kubelet.
+image-rootfs: build
+	$(PY) -m pytest -q tests/test_image_rootfs.py tests/test_image_deps.py
 
 clean:
 	rm -rf build
