@@ -17,7 +17,8 @@ from ..models import fixtures
 
 class Daemon:
     def __init__(self, plugin_dir: str, fixture: dict = None, args=(), env=None, real_smi=False,
-                 event_fifo: str = None, state_dir: str = None, nofile: int = None):
+                 event_fifo: str = None, state_dir: str = None, nofile: int = None, launch=None,
+                 log_path: str = None):
         self.plugin_dir = plugin_dir
         self.args = list(args)
         self.env = dict(os.environ)
@@ -34,13 +35,19 @@ class Daemon:
         else:
             self.env.pop("AMD_SMI_LIB", None)
         self.env.update(env or {})
-        self.log_path = plugin_dir + ".daemon.log"
+        self.log_path = log_path or plugin_dir + ".daemon.log"
         self.proc = None
         self.nofile = nofile  # RLIMIT_NOFILE for the daemon (descriptor exhaustion tests)
+        # argv -> argv: how the daemon binary is started (e.g. inside an
+        # assembled container image, utils/image.py); the result must exec the
+        # daemon in place so signals reach it.
+        self.launch = launch
 
     def start(self):
         self._log = open(self.log_path, "w")
         argv = [DAEMON, "--device-plugin-path", self.plugin_dir, *self.args]
+        if self.launch:
+            argv = self.launch(argv)
         if self.nofile:
             # The limit is set by a shell that then execs the daemon (same pid).
             # A preexec_fn would run Python between fork and exec, which can

@@ -193,15 +193,16 @@ def unresolved(rootfs, files):
     return out
 
 
-def image_daemon(rootfs, args=(), env=None, fixture=None, binds=(), log_path=None):
-    """The daemon of an assembled runtime image, as its ENTRYPOINT runs it
-    (chrooted, root of a user namespace). With `fixture` the amdsmi mock is
-    copied into the image's /tmp and loaded (CPU); with `binds` of /dev and /sys
-    it uses the image's real libamd_smi (GPU box). Returns a started
-    harness.Daemon whose process is the daemon itself (unshare and chroot exec)."""
+def image_daemon(rootfs, args=(), env=None, fixture=None, binds=(), plugin_dir="/var/lib/kubelet/device-plugins",
+                 loader=False, log_path=None):
+    """The daemon of an assembled runtime image, as its ENTRYPOINT runs it.
+    Chrooted (root of a user namespace; `binds` of /dev and /sys for real GPUs)
+    or, with `loader`, through the image's own dynamic loader (hosts without
+    user namespaces; `plugin_dir` is then a host path). With `fixture` the
+    amdsmi mock is copied into the image's /tmp and loaded (CPU). Returns a
+    started harness.Daemon whose process is the daemon itself."""
     import tempfile
     from .. import MOCK_LIB
-    from ..models import fixtures
     from . import harness
     e = {k: v for k, v in os.environ.items() if k not in ("LD_PRELOAD", "LD_LIBRARY_PATH", "AMD_SMI_LIB")}
     e.setdefault("ADP_LOG_LEVEL", "info")
@@ -209,19 +210,18 @@ def image_daemon(rootfs, args=(), env=None, fixture=None, binds=(), log_path=Non
         shutil.copy2(MOCK_LIB, os.path.join(rootfs, "tmp", "libamdsmi_mock.so"))
         with open(os.path.join(rootfs, "tmp", "fixture.json"), "w") as f:
             json.dump(fixture, f)
-        e.update({"AMD_SMI_LIB": "/tmp/libamdsmi_mock.so", "AMDSMI_MOCK_FIXTURE": "/tmp/fixture.json"})
+        mock = "/tmp/libamdsmi_mock.so" if not loader else os.path.join(rootfs, "tmp", "libamdsmi_mock.so")
+        fx = "/tmp/fixture.json" if not loader else os.path.join(rootfs, "tmp", "fixture.json")
+        e.update({"AMD_SMI_LIB": mock, "AMDSMI_MOCK_FIXTURE": fx})
     e.update(env or {})
-    d = harness.Daemon.__new__(harness.Daemon)
-    d.plugin_dir = "/var/lib/kubelet/device-plugins"
-    d.args = list(args)
+
+    def launch(argv):  # [DAEMON, "--device-plugin-path", dir, *args] -> the image's entrypoint
+        inner = ["/usr/bin/amdgpu-device-plugin", *argv[1:]]
+        return loader_cmd(rootfs, inner) if loader else chroot_cmd(rootfs, inner, binds)
+    d = harness.Daemon(plugin_dir, real_smi=True, args=args, launch=launch,
+                       log_path=log_path or tempfile.mktemp(prefix="adp-image-", suffix=".log"))
     d.env = e
-    d.log_path = log_path or tempfile.mktemp(prefix="adp-image-", suffix=".log")
-    d.nofile = None
-    d._log = open(d.log_path, "w")
-    d.proc = subprocess.Popen(chroot_cmd(rootfs, ["/usr/bin/amdgpu-device-plugin", "--device-plugin-path",
-                                                  d.plugin_dir, *d.args], binds),
-                              env=e, stdout=d._log, stderr=subprocess.STDOUT)
-    return d
+    return d.start()
 
 
 def loader_cmd(rootfs, argv):

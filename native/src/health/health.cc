@@ -373,7 +373,7 @@ Status Monitor::Start() {
   }
   LOG_INFO(kComp, "health monitor watching %zu GPU(s) (events %s, poll every %d ms)", snap_->gpus.size(),
            events_ok_ ? "on" : relay_fd_ >= 0 ? "through the relay, once it answers" : "off", cfg_.poll_interval_ms);
-  if (!events_ok_ && cfg_.poll_interval_ms == 0 && cfg_.event_relay.empty()) return Status::Ok();
+  if (!events_ok_ && cfg_.poll_interval_ms == 0 && (cfg_.event_relay.empty() || !cfg_.events)) return Status::Ok();
   stop_.store(false);
   if (wake_fd_ < 0) wake_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   thread_ = std::thread([this] { Run(); });

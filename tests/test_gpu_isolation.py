@@ -262,15 +262,8 @@ def test_images_on_the_real_gpu(scratch, snap, tmp_path):
     pdir = os.path.join(rt, "var/lib/kubelet/device-plugins") if chroot else scratch
     os.makedirs(pdir, exist_ok=True)
     k = kubelet.StubKubelet(os.path.join(pdir, "kubelet.sock")).start()
-    if chroot:
-        dm = image.image_daemon(rt, ["--devices", "0"], binds=binds)
-    else:
-        dm = harness.Daemon(scratch, real_smi=True, args=["--devices", "0"])
-        dm.env = dict(env, ADP_LOG_LEVEL="info")
-        dm._log = open(dm.log_path, "w")
-        dm.proc = subprocess.Popen(cmd(rt, ["/usr/bin/amdgpu-device-plugin", "--device-plugin-path", scratch,
-                                            "--devices", "0"]), env=dm.env, stdout=dm._log,
-                                   stderr=subprocess.STDOUT)
+    dm = image.image_daemon(rt, ["--devices", "0"], binds=binds, loader=not chroot,
+                            plugin_dir="/var/lib/kubelet/device-plugins" if chroot else scratch)
     try:
         reg = k.wait_registration(60)
         c = kubelet.PluginClient(os.path.join(pdir, reg.endpoint))
