@@ -2,7 +2,9 @@
 // (health/relay.cc): the daemon parses whatever arrives on its relay socket.
 // Checks: no crash; an accepted event line re-formatted from its fields parses
 // back to the same fields (message newlines folded to spaces); a hello's
-// verdict is exactly "events=ok" present.
+// verdict is exactly "events=ok" present; an accepted scan reply (the relay's
+// answer to "scan", memcap/driver_usage.h) re-serialises to the bytes it was
+// parsed from, and its sums match its rows.
 #include <fuzzer/FuzzedDataProvider.h>
 
 #include <cstdio>
@@ -11,6 +13,7 @@
 
 #include "common/log.h"
 #include "health/relay.h"
+#include "memcap/driver_usage.h"
 
 using namespace adp;
 
@@ -57,6 +60,16 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     if (r.events_ok != (first == "events=ok")) Fail("hello verdict");
   } else if (!r.kind.empty()) {
     Fail("unknown kind");
+  }
+  memcap::DriverScan s;
+  size_t used = 0;
+  if (memcap::ParseScan(line, &s, &used)) {
+    if (used > line.size()) Fail("scan consumed past the input");
+    if (memcap::SerializeScan(s) != line.substr(0, used)) Fail("scan round trip");
+    uint64_t sum = 0, total = 0;
+    for (const auto& p : s.procs) sum += p.bytes;
+    for (const auto& [bdf, b] : s.total) total += b;
+    if (sum != total) Fail("scan totals");
   }
   return 0;
 }

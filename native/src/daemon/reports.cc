@@ -24,6 +24,7 @@
 #include "health/health.h"
 #include "health/relay.h"
 #include "inventory/inventory.h"
+#include "memcap/driver_usage.h"
 #include "memcap/usage.h"
 #include "plugin/plugin.h"
 #include "smi/smi.h"
@@ -335,7 +336,24 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
     std::string src = MemcapSource(f);
     if (src.empty()) d.Line("FAIL", "--enforce-memory-units: libadp_memcap.so not found (--memcap-lib)");
     else d.Line("ok", "HBM-cap shim " + src);
-    if (!f.metrics_addr.empty() && f.driver_hbm_poll_ms > 0) {
+    if (!f.metrics_addr.empty() && f.driver_hbm_poll_ms > 0 && !f.health_event_socket.empty()) {
+      // The scan runs in the event relay (its privilege, its --host-proc).
+      int fd = health::ConnectRelay(f.health_event_socket);
+      if (fd >= 0) fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) & ~O_NONBLOCK);
+      auto scan = fd < 0 ? Result<memcap::DriverScan>(Unavailable("not reachable"))
+                         : memcap::RemoteScan(fd, "", memcap::SelfCgroup(), 10000);
+      if (fd >= 0) close(fd);
+      if (!scan.ok())
+        d.Line("warn", "driver-side HBM check: the event relay at " + f.health_event_socket + " ran no scan (" +
+                           scan.status().ToString() + ") -- start the relay container (--event-relay)");
+      else if (scan->fd_dirs_unreadable == 0)
+        d.Line("ok", "driver-side HBM check: the event relay reads " + std::to_string(scan->pids_scanned) +
+                         " processes (" + scan->pid_source + " list)");
+      else
+        d.Line("warn", "driver-side HBM check: " + std::to_string(scan->fd_dirs_unreadable) + " of " +
+                           std::to_string(scan->pids_scanned) + " processes not readable by the event relay -- "
+                           "run it privileged, with the host's /proc at --host-proc");
+    } else if (!f.metrics_addr.empty() && f.driver_hbm_poll_ms > 0) {
       memcap::DriverScan scan = memcap::ScanDriverHbm(f.host_proc, {}, memcap::SelfCgroup());
       if (scan.fd_dirs_unreadable == 0)
         d.Line("ok", "driver-side HBM check: " + std::to_string(scan.pids_scanned) + " processes readable under " +

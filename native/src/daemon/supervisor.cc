@@ -211,7 +211,9 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     DoctorReport d;
     return Doctor(lib->get(), v, cfg, d);
   }
-  if (cfg.flags.event_relay) return health::RunEventRelay(lib->get(), cfg.flags.health_event_socket, sfd, cfg.flags.driver_root);
+  if (cfg.flags.event_relay) return health::RunEventRelay(lib->get(), cfg.flags.health_event_socket, sfd,
+                                                      {cfg.flags.driver_root, cfg.flags.host_proc,
+                                                       cfg.flags.kfd_proc_dir});
 
   std::string kubelet_sock =
       v.popts.kubelet_socket.empty() ? PathJoin(v.popts.plugin_dir, "kubelet.sock") : v.popts.kubelet_socket;
@@ -416,6 +418,10 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
                    "# HELP amdgpu_dp_driver_hbm_scan_seconds Wall time of the last driver-side scan.\n"
                    "# TYPE amdgpu_dp_driver_hbm_scan_seconds gauge\n"
                    "amdgpu_dp_driver_hbm_scan_seconds " + std::to_string(dsnap->last_scan_ns / 1e9) + "\n"
+                   "# HELP amdgpu_dp_driver_hbm_scan_failures_total Driver-side scans the event relay could not "
+                   "run (the previous scan stays in effect).\n"
+                   "# TYPE amdgpu_dp_driver_hbm_scan_failures_total counter\n"
+                   "amdgpu_dp_driver_hbm_scan_failures_total " + std::to_string(dsnap->scan_failures) + "\n"
                    "# HELP amdgpu_dp_hbm_over_grant_events_total Transitions of any grant to over its HBM by the "
                    "driver's count.\n"
                    "# TYPE amdgpu_dp_hbm_over_grant_events_total counter\n"
@@ -581,6 +587,9 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
       memcap::DriverHbmMonitor::Options dopt;
       dopt.proc_root = cfg.flags.host_proc;
       dopt.kfd_proc_dir = cfg.flags.kfd_proc_dir;
+      // With an event relay the scan runs there (it holds the privilege to
+      // read other containers' descriptors; this daemon then needs none).
+      dopt.relay_socket = cfg.flags.health_event_socket;
       dopt.usage_dir = v.popts.memcap_usage_dir;
       dopt.poll_ms = static_cast<int>(std::min<uint64_t>(cfg.flags.driver_hbm_poll_ms, 3600000));
       dopt.slack_bytes = cfg.flags.driver_hbm_slack_mib << 20;

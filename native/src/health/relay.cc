@@ -11,12 +11,17 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "common/log.h"
 #include "common/strings.h"
 #include "inventory/inventory.h"
+#include "memcap/driver_usage.h"
 
 namespace adp::health {
 namespace {
@@ -60,6 +65,74 @@ bool SendAll(int fd, const std::string& s) {
   }
   return true;
 }
+
+// Scans run on their own thread: a walk of every /proc/<pid>/fd can take
+// seconds on a busy node, and events must not wait for it. Requests beyond a
+// few queued ones are refused (the connection closes; the daemon retries on
+// its next poll).
+class ScanWorker {
+ public:
+  explicit ScanWorker(const RelayOptions& o) : opts_(o), thread_([this] { Run(); }) {}
+  ~ScanWorker() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    thread_.join();
+    for (auto& r : queue_) close(r.fd);
+  }
+  // Takes ownership of `fd`.
+  void Submit(int fd, std::string usage_dir, std::string cgroup) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (queue_.size() >= 4) {
+      LOG_WARN(kComp, "scan request refused: %zu already queued", queue_.size());
+      close(fd);
+      return;
+    }
+    queue_.push_back({fd, std::move(usage_dir), std::move(cgroup)});
+    cv_.notify_one();
+  }
+
+ private:
+  struct Request {
+    int fd;
+    std::string usage_dir, cgroup;
+  };
+  void Run() {
+    for (;;) {
+      Request r;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
+        if (stop_) return;
+        r = std::move(queue_.front());
+        queue_.pop_front();
+      }
+      memcap::DriverScan s = memcap::ScanDriverHbm(opts_.proc_root, memcap::ListGrantFiles(r.usage_dir), r.cgroup,
+                                                   opts_.kfd_proc_dir);
+      if (!logged_) {
+        logged_ = true;
+        LOG_INFO(kComp, "first HBM scan for a daemon: %zu process(es) from %s, %zu descriptor(s), %zu unreadable",
+                 s.pids_scanned, s.pid_source == "kfd" ? opts_.kfd_proc_dir.c_str() : opts_.proc_root.c_str(),
+                 s.fd_entries, s.fd_dirs_unreadable);
+      }
+      // The reply is written blocking, bounded: a daemon that stops reading loses it.
+      fcntl(r.fd, F_SETFL, fcntl(r.fd, F_GETFL) & ~O_NONBLOCK);
+      timeval tv{5, 0};
+      setsockopt(r.fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+      SendAll(r.fd, memcap::SerializeScan(s));
+      close(r.fd);
+    }
+  }
+  RelayOptions opts_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Request> queue_;
+  bool stop_ = false;
+  bool logged_ = false;
+  std::thread thread_;
+};
 
 }  // namespace
 
@@ -118,7 +191,8 @@ int ConnectRelay(const std::string& socket_path) {
   return fd;
 }
 
-int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_fd, const std::string& driver_root) {
+int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_fd, const RelayOptions& opts) {
+  const std::string& driver_root = opts.driver_root;
   sockaddr_un addr{};
   if (socket_path.empty() || socket_path.size() >= sizeof(addr.sun_path)) {
     LOG_ERROR(kComp, "--event-relay needs --health-event-socket (a path shorter than %zu bytes)",
@@ -179,6 +253,7 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     std::string in;
   };
   std::vector<Client> clients;
+  ScanWorker scans(opts);
   auto hello = [&]() { return "hello v1 " + events_state + "\n"; };
   int exit_code = 0;
   bool quit = false;
@@ -246,8 +321,20 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
         continue;
       }
       size_t nl;
-      while ((nl = c.in.find('\n')) != std::string::npos) {
-        if (c.in.compare(0, nl, "reinit") == 0) do_reinit = true;
+      while (c.fd >= 0 && (nl = c.in.find('\n')) != std::string::npos) {
+        std::string_view line(c.in.data(), nl);
+        if (line == "reinit") do_reinit = true;
+        if (line.rfind("scan\t", 0) == 0) {
+          // "scan\t<usage dir>\t<cgroup>": the connection becomes the scan's.
+          size_t tab = line.find('\t', 5);
+          if (tab == std::string_view::npos) {
+            close(c.fd);
+          } else {
+            scans.Submit(c.fd, std::string(line.substr(5, tab - 5)), std::string(line.substr(tab + 1)));
+          }
+          c.fd = -1;
+          break;
+        }
         c.in.erase(0, nl + 1);
       }
     }

@@ -20,6 +20,13 @@
 //                               daemon generation, e.g. after a re-partition). A
 //                               daemon takes its event state from that hello only:
 //                               the connect hello predates the re-registration.
+//                    "scan\t<usage dir>\t<daemon cgroup>"
+//                               one driver-side HBM scan (memcap/driver_usage.h) of
+//                               the relay's --host-proc: the reply is SerializeScan's
+//                               text, then the relay closes that connection (it gets
+//                               no events). Reading other containers' /proc/<pid>/fd
+//                               needs CAP_SYS_PTRACE; with the scan here the daemon
+//                               needs no capability at all.
 #pragma once
 
 #include <string>
@@ -48,8 +55,13 @@ std::string FormatRelayEvent(const smi::ProcessorInfo& p, uint32_t type, const s
 // passes their signalfd): binds `socket_path` (mode 0600), registers events on
 // every amdsmi processor and forwards them to every connected daemon. Returns
 // the process exit code.
-int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_fd,
-                  const std::string& driver_root = "/");
+// `proc_root` / `kfd_proc_dir`: where scans read processes (ScanDriverHbm).
+struct RelayOptions {
+  std::string driver_root = "/";
+  std::string proc_root = "/proc";
+  std::string kfd_proc_dir = "/sys/class/kfd/kfd/proc";
+};
+int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_fd, const RelayOptions& opts = {});
 
 // Daemon side: connects to the relay (non-blocking), -1 when not reachable.
 int ConnectRelay(const std::string& socket_path);

@@ -5,10 +5,13 @@
 #include <fcntl.h>
 #include <poll.h>
 #include <sys/eventfd.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/sysmacros.h>
+#include <sys/un.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -266,15 +269,135 @@ DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFi
         p.via_cgroup = true;
       }
     }
-    out.total[p.bdf] += p.bytes;
+  }
+  Aggregate(&out);
+  return out;
+}
+
+void Aggregate(DriverScan* s) {
+  s->total.clear();
+  s->unattributed.clear();
+  s->by_grant.clear();
+  s->grant_procs.clear();
+  for (const auto& p : s->procs) {
+    s->total[p.bdf] += p.bytes;
     if (p.grant.empty()) {
-      out.unattributed[p.bdf] += p.bytes;
+      s->unattributed[p.bdf] += p.bytes;
     } else {
-      out.by_grant[{p.grant, p.bdf}] += p.bytes;
-      if (p.bytes) ++out.grant_procs[{p.grant, p.bdf}];
+      s->by_grant[{p.grant, p.bdf}] += p.bytes;
+      if (p.bytes) ++s->grant_procs[{p.grant, p.bdf}];
     }
   }
+}
+
+namespace {
+
+// Fields are tab separated; none may hold a tab or a newline (a cgroup path or
+// BDF with one is rewritten: those come from /proc, not from the daemon).
+std::string Clean(std::string v) {
+  for (char& c : v)
+    if (c == '\t' || c == '\n' || c == '\r') c = ' ';
+  return v;
+}
+
+std::vector<std::string_view> Fields(std::string_view line) {
+  std::vector<std::string_view> f;
+  for (size_t b = 0; b <= line.size();) {
+    size_t e = line.find('\t', b);
+    if (e == std::string_view::npos) e = line.size();
+    f.push_back(line.substr(b, e - b));
+    b = e + 1;
+  }
+  return f;
+}
+
+bool ToU64(std::string_view v, uint64_t* out) {
+  if (v.empty() || v.size() > 20) return false;
+  uint64_t n = 0;
+  for (char c : v) {
+    if (c < '0' || c > '9') return false;
+    uint64_t d = static_cast<uint64_t>(c - '0');
+    if (n > (UINT64_MAX - d) / 10) return false;
+    n = n * 10 + d;
+  }
+  *out = n;
+  return true;
+}
+
+}  // namespace
+
+std::string SerializeScan(const DriverScan& s) {
+  std::string out = "scan\t" + Clean(s.pid_source) + "\t" + std::to_string(s.pids_scanned) + "\t" +
+                    std::to_string(s.fd_entries) + "\t" + std::to_string(s.fd_dirs_unreadable) + "\t" +
+                    std::to_string(s.procs.size()) + "\n";
+  for (const auto& p : s.procs)
+    out += "p\t" + std::to_string(p.pid) + "\t" + Clean(p.bdf) + "\t" + std::to_string(p.bytes) + "\t" +
+           Clean(p.grant) + "\t" + (p.via_cgroup ? "1" : "0") + "\t" + Clean(p.cgroup) + "\n";
   return out;
+}
+
+bool ParseScan(std::string_view text, DriverScan* out, size_t* consumed) {
+  // A header, then exactly as many process lines as it announces.
+  size_t nl = text.find('\n');
+  if (nl == std::string_view::npos) return false;
+  auto h = Fields(text.substr(0, nl));
+  uint64_t pids = 0, fds = 0, unreadable = 0, n = 0;
+  if (h.size() != 6 || h[0] != "scan" || !ToU64(h[2], &pids) || !ToU64(h[3], &fds) ||
+      !ToU64(h[4], &unreadable) || !ToU64(h[5], &n) || n > 1000000)
+    return false;
+  DriverScan s;
+  s.pid_source = std::string(h[1]);
+  s.pids_scanned = pids;
+  s.fd_entries = fds;
+  s.fd_dirs_unreadable = unreadable;
+  size_t pos = nl + 1;
+  for (uint64_t i = 0; i < n; ++i) {
+    size_t e = text.find('\n', pos);
+    if (e == std::string_view::npos) return false;
+    auto f = Fields(text.substr(pos, e - pos));
+    uint64_t pid = 0, bytes = 0;
+    if (f.size() != 7 || f[0] != "p" || !ToU64(f[1], &pid) || pid > INT32_MAX || !ToU64(f[3], &bytes) ||
+        (f[5] != "0" && f[5] != "1"))
+      return false;
+    s.procs.push_back({static_cast<int>(pid), std::string(f[2]), bytes, std::string(f[6]), std::string(f[4]),
+                       f[5] == "1"});
+    pos = e + 1;
+  }
+  Aggregate(&s);
+  *out = std::move(s);
+  if (consumed) *consumed = pos;
+  return true;
+}
+
+Result<DriverScan> RemoteScan(int fd, const std::string& usage_dir, const std::string& self_cgroup, int timeout_ms) {
+  if (usage_dir.find_first_of("\t\n") != std::string::npos || self_cgroup.find_first_of("\t\n") != std::string::npos)
+    return InvalidArgument("usage directory or cgroup with a tab or newline");
+  std::string req = "scan\t" + usage_dir + "\t" + self_cgroup + "\n";
+  if (send(fd, req.data(), req.size(), MSG_NOSIGNAL) != static_cast<ssize_t>(req.size()))
+    return Unavailable(std::string("event relay: ") + strerror(errno));
+  std::string in;
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  for (;;) {
+    // The relay greets every connection ("hello v1 ..."): lines before the reply are skipped.
+    for (size_t nl; in.compare(0, 5, "scan\t") != 0 && (nl = in.find('\n')) != std::string::npos;)
+      in.erase(0, nl + 1);
+    DriverScan s;
+    if (ParseScan(in, &s, nullptr)) return s;
+    if (in.size() > (64u << 20)) return Internal("event relay: scan reply too large");
+    int left = static_cast<int>(
+        std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count());
+    if (left <= 0) return Unavailable("event relay: no scan reply in time");
+    pollfd p{fd, POLLIN, 0};
+    if (poll(&p, 1, left) <= 0) continue;
+    char buf[65536];
+    ssize_t n = recv(fd, buf, sizeof(buf), 0);
+    if (n == 0) return Unavailable("event relay closed the connection");
+    if (n < 0) {
+      if (errno == EINTR || errno == EAGAIN) continue;
+      return Unavailable(std::string("event relay: ") + strerror(errno));
+    }
+    in.append(buf, static_cast<size_t>(n));
+  }
 }
 
 DriverHbmMonitor::DriverHbmMonitor(Options opts, GrantFn grants)
@@ -284,9 +407,47 @@ DriverHbmMonitor::DriverHbmMonitor(Options opts, GrantFn grants)
 
 DriverHbmMonitor::~DriverHbmMonitor() { Stop(); }
 
+namespace {
+
+int ConnectUnix(const std::string& path) {
+  sockaddr_un addr{};
+  if (path.empty() || path.size() >= sizeof(addr.sun_path)) return -1;
+  int fd = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) return -1;
+  addr.sun_family = AF_UNIX;
+  memcpy(addr.sun_path, path.c_str(), path.size());
+  if (connect(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0) {
+    close(fd);
+    return -1;
+  }
+  return fd;
+}
+
+}  // namespace
+
 void DriverHbmMonitor::PollOnce() {
   auto t0 = std::chrono::steady_clock::now();
-  DriverScan scan = ScanDriverHbm(opts_.proc_root, ListGrantFiles(opts_.usage_dir), self_cgroup_, opts_.kfd_proc_dir);
+  DriverScan scan;
+  if (!opts_.relay_socket.empty()) {
+    // A poll that cannot reach the relay keeps the previous scan and grant states.
+    int fd = ConnectUnix(opts_.relay_socket);
+    Result<DriverScan> r = fd < 0 ? Result<DriverScan>(Unavailable("event relay " + opts_.relay_socket + ": " +
+                                                                   strerror(errno)))
+                                  : RemoteScan(fd, opts_.usage_dir, self_cgroup_, std::max(opts_.poll_ms, 30000));
+    if (fd >= 0) close(fd);
+    if (!r.ok()) {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (snap_.scan_error.empty())
+        LOG_WARN(kComp, "driver-side scan through the relay failed: %s", r.status().ToString().c_str());
+      snap_.scan_error = r.status().ToString();
+      snap_.remote = true;
+      ++snap_.scan_failures;
+      return;
+    }
+    scan = std::move(*r);
+  } else {
+    scan = ScanDriverHbm(opts_.proc_root, ListGrantFiles(opts_.usage_dir), self_cgroup_, opts_.kfd_proc_dir);
+  }
   uint64_t scan_ns = static_cast<uint64_t>(
       std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
   auto granted = grants_ ? grants_() : std::map<std::string, std::map<std::string, uint64_t>>{};
@@ -321,8 +482,14 @@ void DriverHbmMonitor::PollOnce() {
              scan.fd_dirs_unreadable, scan.pids_scanned);
   if (snap_.polls == 0)
     LOG_INFO(kComp, "first scan: %zu candidate process(es) from %s, %zu descriptor(s), %.2f ms",
-             scan.pids_scanned, scan.pid_source == "kfd" ? opts_.kfd_proc_dir.c_str() : opts_.proc_root.c_str(),
+             scan.pids_scanned,
+             !opts_.relay_socket.empty() ? (scan.pid_source + " list, through the event relay").c_str()
+             : scan.pid_source == "kfd"  ? opts_.kfd_proc_dir.c_str()
+                                         : opts_.proc_root.c_str(),
              scan.fd_entries, scan_ns / 1e6);
+  if (!snap_.scan_error.empty()) LOG_INFO(kComp, "driver-side scan through the relay works again");
+  snap_.scan_error.clear();
+  snap_.remote = !opts_.relay_socket.empty();
   snap_.scan = std::move(scan);
   snap_.grants = std::move(states);
   snap_.last_scan_ns = scan_ns;
@@ -347,7 +514,9 @@ void DriverHbmMonitor::Start() {
     }
   });
   LOG_INFO(kComp, "checking HBM grants against the driver every %d ms (%s, runtime allowance %.0f MiB/process)",
-           opts_.poll_ms, opts_.proc_root.c_str(), opts_.slack_bytes / 1048576.0);
+           opts_.poll_ms,
+           opts_.relay_socket.empty() ? opts_.proc_root.c_str() : ("scans by the event relay at " + opts_.relay_socket).c_str(),
+           opts_.slack_bytes / 1048576.0);
 }
 
 void DriverHbmMonitor::Stop() {

@@ -31,10 +31,13 @@
 #include <functional>
 #include <map>
 #include <mutex>
+#include <string_view>
 #include <string>
 #include <thread>
 #include <utility>
 #include <vector>
+
+#include "common/status.h"
 
 namespace adp::memcap {
 
@@ -86,6 +89,21 @@ DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFi
 // The cgroup line of the calling process ("" if unreadable).
 std::string SelfCgroup();
 
+// Recomputes a scan's per-GPU and per-grant sums from its process rows.
+void Aggregate(DriverScan* s);
+
+// The scan as the event relay sends it (health/relay.h): a header line
+// "scan\t<pid source>\t<pids>\t<fds>\t<unreadable>\t<n>" and n lines
+// "p\t<pid>\t<bdf>\t<bytes>\t<grant>\t<via cgroup 0|1>\t<cgroup>".
+std::string SerializeScan(const DriverScan& s);
+// Parses one complete reply at the start of `text` (false: incomplete or
+// malformed); `consumed` gets its length.
+bool ParseScan(std::string_view text, DriverScan* out, size_t* consumed);
+// Asks the event relay connected on `fd` for a scan (the relay holds the
+// privilege to read other containers' /proc/<pid>/fd): usage_dir and the
+// daemon's own cgroup as the relay should use them.
+Result<DriverScan> RemoteScan(int fd, const std::string& usage_dir, const std::string& self_cgroup, int timeout_ms);
+
 // Polls ScanDriverHbm and checks every grant against the driver: a grant is
 // over when its processes hold more on a GPU than granted there plus `slack`
 // per process (the HIP runtime's own allocations -- code objects, queues,
@@ -97,6 +115,9 @@ class DriverHbmMonitor {
     std::string proc_root = "/proc";
     std::string kfd_proc_dir = "/sys/class/kfd/kfd/proc";  // "" = always walk every process
     std::string usage_dir;
+    // Non-empty: the event relay's socket; scans run there (RemoteScan), with
+    // the relay's own /proc and KFD list, and proc_root/kfd_proc_dir are unused.
+    std::string relay_socket;
     int poll_ms = 10000;
     uint64_t slack_bytes = 512ull << 20;
   };
@@ -118,6 +139,9 @@ class DriverHbmMonitor {
     uint64_t slack_bytes = 0;
     uint64_t last_scan_ns = 0;   // wall time of the last scan
     uint64_t scan_ns_total = 0;  // all scans
+    uint64_t scan_failures = 0;  // relay scans that failed (the previous scan stays)
+    std::string scan_error;      // the last failure's reason, "" once a scan succeeds again
+    bool remote = false;         // scans run in the event relay
   };
 
   DriverHbmMonitor(Options opts, GrantFn grants);

@@ -32,6 +32,7 @@
 #include "grpc/server_conn.h"
 #include "health/health.h"
 #include "health/relay.h"
+#include "memcap/driver_usage.h"
 #include "memcap/usage.h"
 #include "metrics/metrics.h"
 #include "plugin/plugin.h"
@@ -207,6 +208,29 @@ static void TestRelayLines() {
                           "event node=1 bdf=a part=-1 type=3", "event node=4294967295 bdf=a part=0 type=3",
                           "bogus line", "event node=1 bdf=a part=0 type=99999999999"})
     CHECK(health::ParseRelayLine(bad).kind.empty());
+
+  // the relay's scan reply
+  memcap::DriverScan scan;
+  scan.pid_source = "kfd";
+  scan.pids_scanned = 3;
+  scan.fd_entries = 7;
+  scan.procs = {{11, "0000:0c:00.0", 3u << 20, "0::/pod/a", "k1", false},
+                {12, "0000:0c:00.0", 5u << 20, "0::/pod/a\tx", "k1", true},
+                {13, "0000:0d:00.0", 1u << 20, "0::/", "", false}};
+  memcap::Aggregate(&scan);
+  std::string text = memcap::SerializeScan(scan);
+  memcap::DriverScan back;
+  size_t used = 0;
+  CHECK(memcap::ParseScan(text + "trailing", &back, &used) && used == text.size());
+  CHECK(back.pid_source == "kfd" && back.pids_scanned == 3 && back.fd_entries == 7 && back.procs.size() == 3);
+  CHECK(back.procs[1].cgroup == "0::/pod/a x" && back.procs[1].via_cgroup && back.procs[1].pid == 12);
+  CHECK((back.by_grant[{"k1", "0000:0c:00.0"}] == 8u << 20) && back.unattributed["0000:0d:00.0"] == 1u << 20);
+  CHECK((back.grant_procs[{"k1", "0000:0c:00.0"}] == 2));
+  CHECK(!memcap::ParseScan(text.substr(0, text.size() - 1), &back, &used));  // incomplete
+  for (const char* bad : {"scan\tproc\t1\t1\t0\t1\np\tx\tb\t1\tk\t0\tc\n",
+                          "scan\tproc\t1\t1\t0\n", "scan\tproc\t1\t1\t0\t1\np\t1\tb\t1\tk\t2\tc\n",
+                          "scan\tproc\t1\t1\t0\t99999999999999999999999\n"})
+    CHECK(!memcap::ParseScan(bad, &back, &used));
 }
 
 static void TestProto() {

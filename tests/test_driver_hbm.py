@@ -327,3 +327,63 @@ def test_daemon_scan_uses_the_kfd_list(scratch, tmp_path):
     finally:
         d.stop()
         k.stop()
+
+
+def test_scan_runs_in_the_event_relay(scratch, tmp_path):
+    """With --health-event-socket the daemon asks the event relay for each scan:
+    the relay (the pod's privileged container) reads the processes, the daemon
+    -- here pointed at a /proc that does not exist -- needs no privilege to read
+    other containers' descriptors. Over-grant detection is the same; a relay
+    that goes away leaves the last scan in effect and counts the failures."""
+    import signal
+    proc = FakeProc(str(tmp_path / "proc"))
+    kfd = _kfd_dir(str(tmp_path / "kfd"), [])
+    sock = os.path.join(scratch + ".relay", "events.sock")
+    os.makedirs(os.path.dirname(sock))
+    fx = dict(fixtures.node(2), events_open_kfd=True)
+    relay = harness.Daemon(scratch + "-relay", fx, args=[
+        "--event-relay", "--health-event-socket", sock, "--host-proc", proc.root, "--kfd-proc-dir", ""]).start()
+    relay.wait_log("relaying amdsmi events on")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fx, args=[
+        "--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack",
+        "--enforce-memory-units", "--memcap-lib", SHIM, "--host-proc", str(tmp_path / "nosuch"),
+        "--kfd-proc-dir", kfd, "--health-event-socket", sock, "--driver-hbm-poll-ms", "50",
+        "--driver-hbm-slack-mib", "100"]).start()
+    try:
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics")).group(1))
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        resp = c.allocate(ids[:3]).container_responses[0]
+        c.close()
+        host = [m.host_path for m in resp.mounts if m.container_path == "/run/amdgpu-dp/memcap"][0]
+        key = os.path.basename(host).split(".")[0]
+        ctr = "0::/kubepods/pod-r/ctr"
+        proc.process(601, ctr, vram_mib=1000, maps_file=host)
+        proc.process(602, ctr, vram_mib=2500)  # bypasses the shim
+        s = _scrape_after_poll(port, _polls(port) + 2)
+        lab = dict(allocation=key, bdf=BDF0)
+        assert _value(s, "amdgpu_dp_container_hbm_driver_bytes", **lab) == 3500 * MIB
+        assert _value(s, "amdgpu_dp_container_hbm_over_grant", **lab) == 1
+        assert _value(s, "amdgpu_dp_driver_hbm_scan_processes", source="proc") == 2
+        assert _value(s, "amdgpu_dp_driver_hbm_scan_failures_total") == 0
+        assert "scans by the event relay at " + sock in d.log()
+        assert "through the event relay" in d.wait_log("first scan:")
+        assert "first HBM scan for a daemon" in relay.wait_log("first HBM scan for a daemon")
+        # the daemon's health connection is unaffected by the scan connections
+        assert "events on through the relay" in d.wait_log("events on through the relay")
+        relay.signal(signal.SIGTERM)
+        relay.proc.wait(timeout=10)
+        d.wait_log("driver-side scan through the relay failed")
+        deadline = time.time() + 5
+        while _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_driver_hbm_scan_failures_total") < 2:
+            assert time.time() < deadline
+            time.sleep(0.05)
+        s = _parse(_get(port, "/metrics")[1])
+        assert _value(s, "amdgpu_dp_container_hbm_over_grant", **lab) == 1  # the last scan stays
+    finally:
+        d.stop()
+        k.stop()
+        if relay.proc.poll() is None:
+            relay.stop()

@@ -170,8 +170,18 @@ def test_doctor_asks_the_relay(scratch, tmp_path):
         _, lines = _doctor(tmp_path, "--device-plugin-path", scratch, "--health-event-socket", n.sock, fx=n.fx)
         line = _find(lines, "health events:")
         assert line.startswith("ok") and "through the event relay" in line and "events=ok processors=2" in line
+        # enforced grants: the driver-side scan is the relay's too
+        enforced = ("--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units", "--metrics-addr",
+                    "127.0.0.1:0", "--memcap-lib", os.path.join(BUILD_DIR, "libadp_memcap.so"))
+        _, lines = _doctor(tmp_path, "--device-plugin-path", scratch, "--health-event-socket", n.sock, *enforced,
+                           fx=n.fx)
+        line = _find(lines, "driver-side HBM check")
+        assert line.startswith("ok") and "the event relay reads" in line, lines
     finally:
         n.stop()
     _, lines = _doctor(tmp_path, "--device-plugin-path", scratch, "--health-event-socket", n.sock + ".gone")
     line = _find(lines, "health events:")
     assert line.startswith("warn") and "not reachable" in line
+    _, lines = _doctor(tmp_path, "--device-plugin-path", scratch, "--health-event-socket", n.sock + ".gone", *enforced)
+    line = _find(lines, "driver-side HBM check")
+    assert line.startswith("warn") and "ran no scan" in line and "--event-relay" in line, lines

@@ -130,24 +130,40 @@ def test_max_retired_pages_renders_zero_as_off(value, rendered):
 
 def test_driver_hbm_check_mounts_the_hosts_proc():
     """enforceMemoryUnits + metrics: the driver-side grant check reads the
-    host's processes through a read-only hostPath /proc at /host/proc."""
+    host's processes through a read-only hostPath /proc at /host/proc -- in the
+    event relay (the pod's privileged container), so the daemon keeps no
+    capability at all; without the relay the daemon reads them itself and gets
+    CAP_SYS_PTRACE for it."""
     ds = daemonset({"enforceMemoryUnits": True, "metrics": {"enabled": True}})
     check_consistent(ds)
     e = env(ds)
-    assert e["DP_HOST_PROC"] == "/host/proc" and e["DP_DRIVER_HBM_POLL_MS"] == "10000"
-    assert e["DP_DRIVER_HBM_SLACK_MIB"] == "512"
-    (m,) = [m for m in container(ds)["volumeMounts"] if m["name"] == "host-proc"]
-    assert m == {"name": "host-proc", "mountPath": "/host/proc", "readOnly": True}
+    assert e["DP_DRIVER_HBM_POLL_MS"] == "10000" and e["DP_DRIVER_HBM_SLACK_MIB"] == "512"
+    assert "DP_HOST_PROC" not in e and e["DP_HEALTH_EVENT_SOCKET"]
+    assert container(ds)["securityContext"] == {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}}
+    assert "host-proc" not in {m["name"] for m in container(ds)["volumeMounts"]}
+    r = relay(ds)
+    assert {x["name"]: x["value"] for x in r["env"]}["DP_HOST_PROC"] == "/host/proc"
+    mounts = {m["name"]: m for m in r["volumeMounts"]}
+    assert mounts["host-proc"] == {"name": "host-proc", "mountPath": "/host/proc", "readOnly": True}
+    # the grants' accounting files, at the path the daemon names them by
+    assert mounts["device-plugin"] == {"name": "device-plugin", "mountPath": "/var/lib/kubelet/device-plugins",
+                                       "readOnly": True}
     vols = {v["name"]: v for v in ds["spec"]["template"]["spec"]["volumes"]}
     assert vols["host-proc"]["hostPath"]["path"] == "/proc"
-    # reading other containers' /proc/<pid>/fd needs CAP_SYS_PTRACE: that and nothing else
-    assert container(ds)["securityContext"]["capabilities"] == {"drop": ["ALL"], "add": ["SYS_PTRACE"]}
+    # without the relay (health events off) the daemon scans: CAP_SYS_PTRACE and nothing else
+    solo = daemonset({"enforceMemoryUnits": True, "metrics": {"enabled": True}, "healthEvents": False})
+    check_consistent(solo)
+    assert relay(solo) is None and env(solo)["DP_HOST_PROC"] == "/host/proc"
+    (m,) = [m for m in container(solo)["volumeMounts"] if m["name"] == "host-proc"]
+    assert m == {"name": "host-proc", "mountPath": "/host/proc", "readOnly": True}
+    assert container(solo)["securityContext"]["capabilities"] == {"drop": ["ALL"], "add": ["SYS_PTRACE"]}
     for vals in ({"enforceMemoryUnits": True}, {"metrics": {"enabled": True}},
                  {"enforceMemoryUnits": True, "metrics": {"enabled": True}, "driverHbmCheck": {"enabled": False}}):
         off = daemonset(vals)
         assert env(off)["DP_DRIVER_HBM_POLL_MS"] == "0" and "DP_HOST_PROC" not in env(off)
         assert "host-proc" not in {v["name"] for v in off["spec"]["template"]["spec"]["volumes"]}
         assert container(off)["securityContext"]["capabilities"] == {"drop": ["ALL"]}
+        assert "DP_HOST_PROC" not in {x["name"] for x in relay(off)["env"]}
 
 
 def test_loop_affinity_value():
