@@ -338,11 +338,11 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
     else d.Line("ok", "HBM-cap shim " + src);
     if (!f.metrics_addr.empty() && f.driver_hbm_poll_ms > 0 && !f.health_event_socket.empty()) {
       // The scan runs in the event relay (its privilege, its --host-proc).
-      int fd = health::ConnectRelay(f.health_event_socket);
-      if (fd >= 0) fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) & ~O_NONBLOCK);
-      auto scan = fd < 0 ? Result<memcap::DriverScan>(Unavailable("not reachable"))
-                         : memcap::RemoteScan(fd, "", memcap::SelfCgroup(), 10000);
-      if (fd >= 0) close(fd);
+      int rfd = health::ConnectRelay(f.health_event_socket);
+      if (rfd >= 0) fcntl(rfd, F_SETFL, fcntl(rfd, F_GETFL) & ~O_NONBLOCK);
+      auto scan = rfd < 0 ? Result<memcap::DriverScan>(Unavailable("not reachable"))
+                          : memcap::RemoteScan(rfd, "", memcap::SelfCgroup(), 10000);
+      if (rfd >= 0) close(rfd);
       if (!scan.ok())
         d.Line("warn", "driver-side HBM check: the event relay at " + f.health_event_socket + " ran no scan (" +
                            scan.status().ToString() + ") -- start the relay container (--event-relay)");
