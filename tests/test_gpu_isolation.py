@@ -9,7 +9,9 @@
 * Event relay: the daemon under a device-cgroup denial gets amdsmi event
   notification through the relay running on real libamd_smi.
 * Driver-side HBM scan: KFD's GPU-process list finds a live HIP allocation
-  with the same bytes as the full /proc walk, reading a fraction of the fds.
+  with the same bytes as the full /proc walk, reading a fraction of the fds;
+  run by the event relay for a daemon that may read no other process, it
+  reports the same allocation on /metrics.
 """
 
 import json
@@ -188,10 +190,7 @@ def test_event_relay_on_real_amdsmi(scratch, snap, tmp_path):
         assert relay.stop() == 0
 
 
-def test_driver_scan_reads_the_gpu_processes_kfd_lists(tmp_path):
-    """A HIP process holding 1 GiB: the scan through KFD's process list finds
-    it with the same bytes as the full /proc walk, reading only GPU processes."""
-    code = r'''
+_HOLDER = r'''
 import ctypes, sys
 lib = ctypes.CDLL("libamdhip64.so")
 p = ctypes.c_void_p()
@@ -200,11 +199,25 @@ lib.hipMemset(p, 1, ctypes.c_size_t(1 << 30)); lib.hipDeviceSynchronize()
 print("holding", rc, flush=True)
 sys.stdin.read()
 '''
-    p = subprocess.Popen([sys.executable, "-c", code], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+
+
+def _hold_1gib():
+    """A child process holding 1 GiB of HBM until its stdin closes."""
+    p = subprocess.Popen([sys.executable, "-c", _HOLDER], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                          stderr=subprocess.PIPE, text=True)
+    line = p.stdout.readline().split()
+    if line[:2] != ["holding", "0"]:
+        p.stdin.close()
+        p.wait(timeout=30)
+        raise AssertionError((line, p.stderr.read()[-2000:]))
+    return p
+
+
+def test_driver_scan_reads_the_gpu_processes_kfd_lists(tmp_path):
+    """A HIP process holding 1 GiB: the scan through KFD's process list finds
+    it with the same bytes as the full /proc walk, reading only GPU processes."""
+    p = _hold_1gib()
     try:
-        line = p.stdout.readline().split()
-        assert line[:2] == ["holding", "0"], (line, p.stderr.read()[-2000:] if p.poll() is not None else "")
         kfd_dir = "/sys/class/kfd/kfd/proc"
         listed = sorted(int(x) for x in os.listdir(kfd_dir) if x.isdigit()) if os.path.isdir(kfd_dir) else []
         fast = native.driver_scan("/proc", kfd_proc_dir=kfd_dir)
@@ -226,6 +239,55 @@ sys.stdin.read()
     finally:
         p.stdin.close()
         p.wait(timeout=30)
+
+
+def test_driver_scan_through_the_relay(scratch, snap, tmp_path):
+    """The chart's layout: the relay (real libamd_smi, the host's /proc) runs
+    the driver-side scans; the daemon is denied the GPU device nodes and given
+    a --host-proc that does not exist, so every byte it reports came through
+    the relay. A HIP process holding 1 GiB shows on /metrics."""
+    from test_metrics import _get, _parse, _value
+    sock = str(tmp_path / "events.sock")
+    rdir = scratch + "-relay"
+    os.makedirs(rdir, exist_ok=True)
+    relay = harness.Daemon(rdir, real_smi=True, args=["--event-relay", "--health-event-socket", sock]).start()
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = None
+    holder = None
+    try:
+        relay.wait_log("relaying amdsmi events on", 30)
+        holder = _hold_1gib()
+        env = {"LD_PRELOAD": " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), SIM) if x)}
+        d = harness.Daemon(scratch, real_smi=True, env=env, args=[
+            "--devices", "0", "--health-event-socket", sock, "--metrics-addr", "127.0.0.1:0",
+            "--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units", "--host-proc",
+            str(tmp_path / "nosuch"), "--driver-hbm-poll-ms", "200"]).start()
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics", 30)).group(1))
+        k.wait_registration(30)
+        bdf = snap["gpus"][0]["bdf"]
+        deadline = time.time() + 30
+        while True:
+            m = _parse(_get(port, "/metrics")[1])
+            held = _value(m, "amdgpu_dp_gpu_hbm_driver_bytes", bdf=bdf)
+            if (held or 0) >= 1 << 30 or time.time() > deadline:
+                break
+            time.sleep(0.2)
+        record = {"gpu_driver_bytes": held, "scan_failures": _value(m, "amdgpu_dp_driver_hbm_scan_failures_total"),
+                  "scan_seconds": _value(m, "amdgpu_dp_driver_hbm_scan_seconds"),
+                  "daemon_log": [ln for ln in d.log().splitlines() if "driver-hbm" in ln][:4],
+                  "relay_log": [ln for ln in relay.log().splitlines() if "scan" in ln][:4]}
+        _save("driver_scan_relay.json", record)
+        assert (held or 0) >= 1 << 30, record
+        assert record["scan_failures"] == 0, record
+        assert "first HBM scan for a daemon" in relay.log()
+    finally:
+        if holder:
+            holder.stdin.close()
+            holder.wait(timeout=30)
+        if d:
+            assert d.stop() == 0
+        k.stop()
+        assert relay.stop() == 0
 
 
 def _userns_mounts_ok():
