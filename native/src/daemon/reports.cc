@@ -341,7 +341,8 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
       int rfd = health::ConnectRelay(f.health_event_socket);
       if (rfd >= 0) fcntl(rfd, F_SETFL, fcntl(rfd, F_GETFL) & ~O_NONBLOCK);
       auto scan = rfd < 0 ? Result<memcap::DriverScan>(Unavailable("not reachable"))
-                          : memcap::RemoteScan(rfd, "", memcap::SelfCgroup(), 10000);
+                          : memcap::RemoteScan(rfd, PathJoin(f.plugin_dir, "amdgpu-dp/usage"), memcap::SelfCgroup(),
+                                               10000);
       if (rfd >= 0) close(rfd);
       if (!scan.ok())
         d.Line("warn", "driver-side HBM check: the event relay at " + f.health_event_socket + " ran no scan (" +

@@ -327,7 +327,10 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
         if (line.rfind("scan\t", 0) == 0) {
           // "scan\t<usage dir>\t<cgroup>": the connection becomes the scan's.
           size_t tab = line.find('\t', 5);
-          if (tab == std::string_view::npos) {
+          std::string_view dir = tab == std::string_view::npos ? std::string_view() : line.substr(5, tab - 5);
+          // An absolute directory without "..": the relay stats its entries, nothing more.
+          if (dir.empty() || dir[0] != '/' || dir.find("/..") != std::string_view::npos) {
+            LOG_WARN(kComp, "malformed scan request dropped");
             close(c.fd);
           } else {
             scans.Submit(c.fd, std::string(line.substr(5, tab - 5)), std::string(line.substr(tab + 1)));

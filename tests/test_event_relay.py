@@ -185,3 +185,41 @@ def test_doctor_asks_the_relay(scratch, tmp_path):
     _, lines = _doctor(tmp_path, "--device-plugin-path", scratch, "--health-event-socket", n.sock + ".gone", *enforced)
     line = _find(lines, "driver-side HBM check")
     assert line.startswith("warn") and "ran no scan" in line and "--event-relay" in line, lines
+
+
+def test_relay_answers_scan_requests_and_drops_malformed_ones(scratch, tmp_path):
+    """The relay's second request: one driver-side scan per connection, the
+    reply in SerializeScan's lines, then the connection closes. A request whose
+    directory is relative or climbs out ("..") is dropped unanswered."""
+    import socket as so
+    sock = str(tmp_path / "events.sock")
+    fx = dict(fixtures.node(1), events_open_kfd=True)
+    relay = harness.Daemon(scratch + "-relay", fx, args=["--event-relay", "--health-event-socket", sock,
+                                                         "--host-proc", str(tmp_path / "proc")]).start()
+    os.makedirs(str(tmp_path / "proc"))
+
+    def ask(line):
+        c = so.socket(so.AF_UNIX, so.SOCK_STREAM)
+        c.settimeout(10)
+        c.connect(sock)
+        c.sendall(line.encode())
+        data = b""
+        while True:
+            chunk = c.recv(65536)
+            if not chunk:
+                break
+            data += chunk
+        c.close()
+        return data.decode()
+    try:
+        relay.wait_log("relaying amdsmi events on")
+        out = ask(f"scan\t{tmp_path}/usage\t0::/\n")
+        lines = out.splitlines()
+        assert lines[0].startswith("hello v1 ") and lines[1].split("\t")[:2] == ["scan", "proc"], out
+        assert lines[1].split("\t")[-1] == "0" and len(lines) == 2  # an empty /proc: no process rows
+        for bad in ("scan\trelative/dir\tx\n", f"scan\t{tmp_path}/../etc\tx\n", "scan\tnotab\n"):
+            out = ask(bad)
+            assert "scan\t" not in out, (bad, out)
+        assert relay.log().count("malformed scan request dropped") == 3
+    finally:
+        relay.stop()
