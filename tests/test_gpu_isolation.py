@@ -246,7 +246,7 @@ def test_driver_scan_through_the_relay(scratch, snap, tmp_path):
     the driver-side scans; the daemon is denied the GPU device nodes and given
     a --host-proc that does not exist, so every byte it reports came through
     the relay. A HIP process holding 1 GiB shows on /metrics."""
-    from test_metrics import _get, _parse, _value
+    from test_metrics import _get, _parse
     sock = str(tmp_path / "events.sock")
     rdir = scratch + "-relay"
     os.makedirs(rdir, exist_ok=True)
@@ -260,20 +260,29 @@ def test_driver_scan_through_the_relay(scratch, snap, tmp_path):
         env = {"LD_PRELOAD": " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), SIM) if x)}
         d = harness.Daemon(scratch, real_smi=True, env=env, args=[
             "--devices", "0", "--health-event-socket", sock, "--metrics-addr", "127.0.0.1:0",
-            "--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units", "--host-proc",
+            "--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units", "--memcap-lib",
+            os.path.join(BUILD_DIR, "libadp_memcap.so"), "--host-proc",
             str(tmp_path / "nosuch"), "--driver-hbm-poll-ms", "200"]).start()
         port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics", 30)).group(1))
         k.wait_registration(30)
         bdf = snap["gpus"][0]["bdf"]
+        def get(samples, name, **labels):  # None until the first scan has run
+            want = set(labels.items())
+            hits = [v for (n, ls), v in samples.items() if n == name and want <= set(ls)]
+            return hits[0] if len(hits) == 1 else None
         deadline = time.time() + 30
         while True:
-            m = _parse(_get(port, "/metrics")[1])
-            held = _value(m, "amdgpu_dp_gpu_hbm_driver_bytes", bdf=bdf)
+            text = _get(port, "/metrics")[1]
+            m = _parse(text)
+            held = get(m, "amdgpu_dp_gpu_hbm_driver_bytes", bdf=bdf)
             if (held or 0) >= 1 << 30 or time.time() > deadline:
                 break
             time.sleep(0.2)
-        record = {"gpu_driver_bytes": held, "scan_failures": _value(m, "amdgpu_dp_driver_hbm_scan_failures_total"),
-                  "scan_seconds": _value(m, "amdgpu_dp_driver_hbm_scan_seconds"),
+        record = {"gpu_driver_bytes": held, "scan_failures": get(m, "amdgpu_dp_driver_hbm_scan_failures_total"),
+                  "scan_processes": {str(dict(ls)): v for (n, ls), v in m.items()
+                                     if n == "amdgpu_dp_driver_hbm_scan_processes"},
+                  "scan_seconds": get(m, "amdgpu_dp_driver_hbm_scan_seconds"),
+                  "driver_metric_lines": [ln for ln in text.splitlines() if "driver" in ln and not ln.startswith("#")],
                   "daemon_log": [ln for ln in d.log().splitlines() if "driver-hbm" in ln][:4],
                   "relay_log": [ln for ln in relay.log().splitlines() if "scan" in ln][:4]}
         _save("driver_scan_relay.json", record)
