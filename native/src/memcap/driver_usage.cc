@@ -476,20 +476,21 @@ void DriverHbmMonitor::PollOnce() {
     }
     st.over_transitions = transitions_[kb];
   }
+  const bool remote = !opts_.relay_socket.empty();
   if (snap_.polls == 0 && scan.fd_dirs_unreadable)
-    LOG_WARN(kComp, "%zu of %zu processes' file descriptors are not readable: HBM they hold is not seen (run the "
-             "plugin privileged, with the host's PID namespace or /proc at --host-proc)",
-             scan.fd_dirs_unreadable, scan.pids_scanned);
-  if (snap_.polls == 0)
-    LOG_INFO(kComp, "first scan: %zu candidate process(es) from %s, %zu descriptor(s), %.2f ms",
-             scan.pids_scanned,
-             !opts_.relay_socket.empty() ? (scan.pid_source + " list, through the event relay").c_str()
-             : scan.pid_source == "kfd"  ? opts_.kfd_proc_dir.c_str()
-                                         : opts_.proc_root.c_str(),
-             scan.fd_entries, scan_ns / 1e6);
+    LOG_WARN(kComp, "%zu of %zu processes' file descriptors are not readable: HBM they hold is not seen (run %s "
+             "privileged, with the host's PID namespace or /proc at --host-proc)",
+             scan.fd_dirs_unreadable, scan.pids_scanned, remote ? "the event relay" : "the plugin");
+  if (snap_.polls == 0) {
+    std::string from = remote                      ? "the event relay's " + scan.pid_source + " list"
+                       : scan.pid_source == "kfd" ? opts_.kfd_proc_dir
+                                                  : opts_.proc_root;
+    LOG_INFO(kComp, "first scan: %zu candidate process(es) from %s, %zu descriptor(s), %.2f ms", scan.pids_scanned,
+             from.c_str(), scan.fd_entries, scan_ns / 1e6);
+  }
   if (!snap_.scan_error.empty()) LOG_INFO(kComp, "driver-side scan through the relay works again");
   snap_.scan_error.clear();
-  snap_.remote = !opts_.relay_socket.empty();
+  snap_.remote = remote;
   snap_.scan = std::move(scan);
   snap_.grants = std::move(states);
   snap_.last_scan_ns = scan_ns;

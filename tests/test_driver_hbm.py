@@ -369,7 +369,7 @@ def test_scan_runs_in_the_event_relay(scratch, tmp_path):
         assert _value(s, "amdgpu_dp_driver_hbm_scan_processes", source="proc") == 2
         assert _value(s, "amdgpu_dp_driver_hbm_scan_failures_total") == 0
         assert "scans by the event relay at " + sock in d.log()
-        assert "through the event relay" in d.wait_log("first scan:")
+        assert "from the event relay's proc list" in d.wait_log("first scan:")
         assert "first HBM scan for a daemon" in relay.wait_log("first HBM scan for a daemon")
         # the daemon's health connection is unaffected by the scan connections
         assert "events on through the relay" in d.wait_log("events on through the relay")
