@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -245,7 +246,50 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     if (st.ok()) LOG_INFO(kComp, "event notification registered on %zu processor(s)", procs.size());
     else LOG_ERROR(kComp, "event notification unavailable: %s", st.ToString().c_str());
   };
+  // The amdsmi wait blocks (≤100 ms slices), so it runs on a thread of its
+  // own and hands formatted lines to the main loop through a pipe: the main
+  // loop sleeps in poll() on sockets, signals and that pipe, and answers a
+  // daemon's request at once. Re-enumeration stops the thread first (it reads
+  // `procs`, which only the main thread changes, and only then).
+  int pipefd[2];
+  if (pipe2(pipefd, O_CLOEXEC | O_NONBLOCK) != 0) {
+    LOG_ERROR(kComp, "pipe: %s", strerror(errno));
+    close(lfd);
+    return 1;
+  }
+  std::atomic<bool> waiter_stop{false};
+  std::thread waiter;
+  auto start_waiter = [&] {
+    if (!registered) return;
+    waiter_stop.store(false);
+    waiter = std::thread([&] {
+      std::vector<smi::Event> events;
+      while (!waiter_stop.load()) {
+        events.clear();
+        if (Status st = lib->EventsWait(100, &events); !st.ok()) {
+          LOG_WARN(kComp, "event wait failed: %s", st.ToString().c_str());
+          usleep(100000);
+          continue;
+        }
+        for (const auto& e : events) {
+          const smi::ProcessorInfo* p = nullptr;
+          for (const auto& q : procs)
+            if (q.handle == e.handle) p = &q;
+          if (!p) continue;
+          std::string line = FormatRelayEvent(*p, e.type, e.message);
+          if (write(pipefd[1], line.data(), line.size()) != static_cast<ssize_t>(line.size()))
+            LOG_WARN(kComp, "event dropped (relay loop behind): %s", OneLine(line).c_str());
+        }
+      }
+    });
+  };
+  auto stop_waiter = [&] {
+    if (!waiter.joinable()) return;
+    waiter_stop.store(true);
+    waiter.join();
+  };
   enumerate_and_register(false);
+  start_waiter();
   LOG_INFO(kComp, "relaying amdsmi events on %s", socket_path.c_str());
 
   struct Client {
@@ -257,33 +301,27 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
   auto hello = [&]() { return "hello v1 " + events_state + "\n"; };
   int exit_code = 0;
   bool quit = false;
-  std::vector<smi::Event> events;
+  std::string pending;  // event bytes read from the pipe, up to the last full line
   while (!quit) {
-    // The amdsmi wait is the relay's clock: at most 100 ms, then sockets and signals.
-    events.clear();
-    if (registered) {
-      if (Status st = lib->EventsWait(100, &events); !st.ok()) {
-        LOG_WARN(kComp, "event wait failed: %s", st.ToString().c_str());
-        usleep(100000);
+    std::vector<pollfd> pfds = {{signal_fd, POLLIN, 0}, {lfd, POLLIN, 0}, {pipefd[0], POLLIN, 0}};
+    for (const auto& c : clients) pfds.push_back({c.fd, POLLIN, 0});
+    if (poll(pfds.data(), pfds.size(), -1) < 0 && errno != EINTR) break;
+    if (pfds[2].revents & POLLIN) {
+      char buf[4096];
+      ssize_t n;
+      while ((n = read(pipefd[0], buf, sizeof(buf))) > 0) pending.append(buf, static_cast<size_t>(n));
+      size_t cut = pending.rfind('\n');
+      if (cut != std::string::npos) {
+        std::string lines = pending.substr(0, cut + 1);
+        pending.erase(0, cut + 1);
+        LOG_INFO(kComp, "%s", OneLine(lines).c_str());
+        for (auto& c : clients)
+          if (c.fd >= 0 && !SendAll(c.fd, lines)) {
+            close(c.fd);
+            c.fd = -1;
+          }
       }
     }
-    for (const auto& e : events) {
-      const smi::ProcessorInfo* p = nullptr;
-      for (const auto& q : procs)
-        if (q.handle == e.handle) p = &q;
-      if (!p) continue;
-      std::string line = FormatRelayEvent(*p, e.type, e.message);
-      LOG_INFO(kComp, "%s", OneLine(line).c_str());
-      for (auto& c : clients)
-        if (c.fd >= 0 && !SendAll(c.fd, line)) {
-          close(c.fd);
-          c.fd = -1;
-        }
-    }
-    std::vector<pollfd> pfds = {{signal_fd, POLLIN, 0}, {lfd, POLLIN, 0}};
-    for (const auto& c : clients) pfds.push_back({c.fd, POLLIN, 0});
-    int wait = registered ? 0 : 100;  // without events, poll is the clock
-    if (poll(pfds.data(), pfds.size(), wait) < 0 && errno != EINTR) break;
     if (pfds[0].revents & POLLIN) {
       signalfd_siginfo si;
       while (read(signal_fd, &si, sizeof(si)) == sizeof(si))
@@ -302,10 +340,11 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     }
     bool do_reinit = false;
     // Only the clients polled above (accept may have appended new ones).
-    const size_t polled = pfds.size() - 2;
+    constexpr size_t kFixed = 3;  // signals, listener, event pipe
+    const size_t polled = pfds.size() - kFixed;
     for (size_t i = 0; i < polled; ++i) {
       auto& c = clients[i];
-      if (c.fd < 0 || !(pfds[2 + i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+      if (c.fd < 0 || !(pfds[kFixed + i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
       char buf[256];
       ssize_t n = recv(c.fd, buf, sizeof(buf), 0);
       if (n <= 0) {
@@ -345,7 +384,9 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
                   clients.end());
     if (do_reinit) {
       LOG_INFO(kComp, "re-enumerating (a daemon asked)");
+      stop_waiter();
       enumerate_and_register(true);
+      start_waiter();
       // Marked, so a daemon tells the state after its own request from the
       // hello every connection gets first (sent before the request was read).
       std::string fresh = "hello v1 reinit " + events_state + "\n";
@@ -356,9 +397,12 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
         }
     }
   }
+  stop_waiter();
   if (!handles.empty() && registered) lib->EventsStop(handles);
   for (auto& c : clients)
     if (c.fd >= 0) close(c.fd);
+  close(pipefd[0]);
+  close(pipefd[1]);
   close(lfd);
   unlink(socket_path.c_str());
   LOG_INFO(kComp, "event relay stopped");

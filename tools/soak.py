@@ -1,11 +1,15 @@
 """Soak test: the daemon under continuous pod churn, periodic SIGHUP restarts,
 kubelet restarts and metric scrapes; samples its RSS, open fds and threads.
 
-  python tools/soak.py [--seconds 300] [--clients 4] [--real] [--enforce] [--holders N] [--out soak.json]
+  python tools/soak.py [--seconds 300] [--clients 4] [--real] [--enforce] [--holders N] [--relay]
+                       [--out soak.json]
 
 Prints one progress line per sample (every 10 s) and a final JSON summary with
 pods served, restarts, and first/last/max RSS/fds/threads. Exit code 1 if the
 daemon died, RSS grew by more than --max-rss-growth-mib, or fds/threads leaked.
+With --relay an event relay (--event-relay) runs next to the daemon, which
+takes its health events -- and, with --enforce, its driver-side scans -- from
+it; the relay's RSS/fds/threads are sampled and checked the same way.
 """
 
 import argparse
@@ -48,6 +52,8 @@ def main():
     ap.add_argument("--holders", type=int, default=0,
                     help="(--real) HIP processes holding 256 MiB each during the soak: GPU processes for the "
                          "driver-side scan to find")
+    ap.add_argument("--relay", action="store_true",
+                    help="events and driver-side scans through an event relay process (the chart's layout)")
     a = ap.parse_args()
     holders = []
     if a.real and a.holders:
@@ -78,7 +84,20 @@ def main():
     env = {"ADP_LOG_LEVEL": "warn", "DP_HEALTH_POLL_MS": "200"}
     if a.enforce:  # grant accounting files per pod, and the driver-side /proc scan every 100 ms
         env["DP_DRIVER_HBM_POLL_MS"] = "100"
-    dm = harness.Daemon(d, None if a.real else fixtures.node(8), args=args, real_smi=a.real, env=env).start()
+    fx = None if a.real else dict(fixtures.node(8), events_open_kfd=True)
+    relay = None
+    if a.relay:
+        esock = os.path.join(d + ".relay", "events.sock")
+        os.makedirs(os.path.dirname(esock), exist_ok=True)
+        relay = harness.Daemon(d + ".relay", fx, args=["--event-relay", "--health-event-socket", esock],
+                               real_smi=a.real, env={"ADP_LOG_LEVEL": "warn"}).start()
+        deadline = time.time() + 30
+        while not os.path.exists(esock):
+            assert time.time() < deadline and relay.proc.poll() is None, relay.log()[-2000:]
+            time.sleep(0.05)
+        args += ["--health-event-socket", esock]
+    dm = harness.Daemon(d, fx, args=args, real_smi=a.real, env=env).start()
+    relay_samples = []
     driver_polls = None
     scans = []  # (source, processes, descriptors, seconds) of the last scan, per scrape
     samples, pods, hups, kubelet_restarts, scrapes = [], 0, 0, 0, 0
@@ -134,11 +153,20 @@ def main():
                 s = proc_stats(dm.proc.pid)
                 s.update({"t": round(a.seconds - (t_end - time.time()), 1), "pods": pods})
                 samples.append(s)
+                if relay:
+                    r_ = proc_stats(relay.proc.pid)
+                    relay_samples.append(r_)
+                    s = dict(s, relay=r_)
                 print(json.dumps(s), flush=True)
                 next_sample = time.time() + 10
+            if relay and relay.proc.poll() is not None:
+                ok = False
+                print("relay died", flush=True)
+                break
     finally:
         code = dm.stop()
         kub.stop()
+        relay_code = relay.stop() if relay and relay.proc.poll() is None else (relay.proc.returncode if relay else None)
         for h in holders:
             h.stdin.close()
             h.wait(timeout=30)
@@ -167,6 +195,18 @@ def main():
         ok = False
     if samples and (last["fds"] > warm["fds"] + 4 or last["threads"] > warm["threads"] + 2):
         ok = False
+    if relay:
+        rw = relay_samples[min(2, len(relay_samples) - 1)] if relay_samples else {}
+        rl = relay_samples[-1] if relay_samples else {}
+        summary["relay"] = {"exit_code": relay_code, "rss_mib_after_warmup": rw.get("rss_mib"),
+                            "rss_mib_last": rl.get("rss_mib"), "fds_after_warmup": rw.get("fds"),
+                            "fds_last": rl.get("fds"), "threads_after_warmup": rw.get("threads"),
+                            "threads_last": rl.get("threads")}
+        if relay_code not in (0, None):
+            ok = False
+        if relay_samples and (rl["rss_mib"] - rw["rss_mib"] > a.max_rss_growth_mib or rl["fds"] > rw["fds"] + 4
+                              or rl["threads"] > rw["threads"] + 2):
+            ok = False
     summary["ok"] = ok
     print(json.dumps(summary), flush=True)
     if a.out:
