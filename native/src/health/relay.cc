@@ -335,7 +335,8 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
           continue;
         }
         clients.push_back({cfd, ""});
-        LOG_INFO(kComp, "daemon connected (%zu client(s))", clients.size());
+        // (a scan connection every poll: not worth an info line each)
+        LOG_DEBUG(kComp, "connection accepted (%zu client(s))", clients.size());
       }
     }
     bool do_reinit = false;
@@ -362,7 +363,10 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
       size_t nl;
       while (c.fd >= 0 && (nl = c.in.find('\n')) != std::string::npos) {
         std::string_view line(c.in.data(), nl);
-        if (line == "reinit") do_reinit = true;
+        if (line == "reinit") {
+          do_reinit = true;
+          LOG_INFO(kComp, "daemon connected for events");
+        }
         if (line.rfind("scan\t", 0) == 0) {
           // "scan\t<usage dir>\t<cgroup>": the connection becomes the scan's.
           size_t tab = line.find('\t', 5);

@@ -96,7 +96,7 @@ def test_reset_events_travel_through_the_relay(scratch):
         n.d.wait_log("VMFAULT(1) on GPU 0")
         rlog = n.relay.log()
         assert "event notification registered on 2 processor(s)" in rlog
-        assert "daemon connected" in rlog and "re-enumerating (a daemon asked)" in rlog
+        assert "daemon connected for events" in rlog and "re-enumerating (a daemon asked)" in rlog
     finally:
         n.stop()
 
