@@ -369,7 +369,8 @@ bool ParseScan(std::string_view text, DriverScan* out, size_t* consumed) {
   return true;
 }
 
-Result<DriverScan> RemoteScan(int fd, const std::string& usage_dir, const std::string& self_cgroup, int timeout_ms) {
+Result<DriverScan> RemoteScan(int fd, const std::string& usage_dir, const std::string& self_cgroup, int timeout_ms,
+                              int cancel_fd) {
   if (usage_dir.find_first_of("\t\n") != std::string::npos || self_cgroup.find_first_of("\t\n") != std::string::npos)
     return InvalidArgument("usage directory or cgroup with a tab or newline");
   std::string req = "scan\t" + usage_dir + "\t" + self_cgroup + "\n";
@@ -387,8 +388,9 @@ Result<DriverScan> RemoteScan(int fd, const std::string& usage_dir, const std::s
     int left = static_cast<int>(
         std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count());
     if (left <= 0) return Unavailable("event relay: no scan reply in time");
-    pollfd p{fd, POLLIN, 0};
-    if (poll(&p, 1, left) <= 0) continue;
+    pollfd p[2] = {{fd, POLLIN, 0}, {cancel_fd, POLLIN, 0}};
+    if (poll(p, cancel_fd >= 0 ? 2 : 1, left) <= 0) continue;
+    if (cancel_fd >= 0 && (p[1].revents & POLLIN)) return Unavailable("scan cancelled");
     char buf[65536];
     ssize_t n = recv(fd, buf, sizeof(buf), 0);
     if (n == 0) return Unavailable("event relay closed the connection");
@@ -433,9 +435,11 @@ void DriverHbmMonitor::PollOnce() {
     int fd = ConnectUnix(opts_.relay_socket);
     Result<DriverScan> r = fd < 0 ? Result<DriverScan>(Unavailable("event relay " + opts_.relay_socket + ": " +
                                                                    strerror(errno)))
-                                  : RemoteScan(fd, opts_.usage_dir, self_cgroup_, std::max(opts_.poll_ms, 30000));
+                                  : RemoteScan(fd, opts_.usage_dir, self_cgroup_, std::max(opts_.poll_ms, 30000),
+                                               wake_fd_);
     if (fd >= 0) close(fd);
     if (!r.ok()) {
+      if (stop_.load()) return;  // cancelled by Stop()
       std::lock_guard<std::mutex> lk(mu_);
       if (snap_.scan_error.empty())
         LOG_WARN(kComp, "driver-side scan through the relay failed: %s", r.status().ToString().c_str());

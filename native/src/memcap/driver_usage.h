@@ -101,8 +101,10 @@ std::string SerializeScan(const DriverScan& s);
 bool ParseScan(std::string_view text, DriverScan* out, size_t* consumed);
 // Asks the event relay connected on `fd` for a scan (the relay holds the
 // privilege to read other containers' /proc/<pid>/fd): usage_dir and the
-// daemon's own cgroup as the relay should use them.
-Result<DriverScan> RemoteScan(int fd, const std::string& usage_dir, const std::string& self_cgroup, int timeout_ms);
+// daemon's own cgroup as the relay should use them. A readable `cancel_fd`
+// (>= 0) ends the wait early (the monitor's stop).
+Result<DriverScan> RemoteScan(int fd, const std::string& usage_dir, const std::string& self_cgroup, int timeout_ms,
+                              int cancel_fd = -1);
 
 // Polls ScanDriverHbm and checks every grant against the driver: a grant is
 // over when its processes hold more on a GPU than granted there plus `slack`

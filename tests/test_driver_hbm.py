@@ -387,3 +387,49 @@ def test_scan_runs_in_the_event_relay(scratch, tmp_path):
         k.stop()
         if relay.proc.poll() is None:
             relay.stop()
+
+
+def test_a_relay_that_never_answers_does_not_hold_up_shutdown(scratch, tmp_path):
+    """A relay that greets and then never answers a scan: the poll waits (the
+    scan is counted as failed only at its deadline), and stopping the daemon
+    cancels the wait instead of sitting out the 30 s scan timeout."""
+    import socket as so
+    import threading
+    path = os.path.join(scratch + ".mute", "events.sock")
+    os.makedirs(os.path.dirname(path))
+    srv = so.socket(so.AF_UNIX, so.SOCK_STREAM)
+    srv.bind(path)
+    srv.listen(8)
+    conns = []
+
+    def serve():
+        while True:
+            try:
+                c, _ = srv.accept()
+            except OSError:
+                return
+            c.sendall(b"hello v1 events=ok processors=1\n")
+            conns.append(c)  # read nothing, answer nothing
+    threading.Thread(target=serve, daemon=True).start()
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(1), args=[
+        "--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units",
+        "--memcap-lib", SHIM, "--health-event-socket", path, "--driver-hbm-poll-ms", "50"]).start()
+    try:
+        d.wait_log("scans by the event relay at")
+        k.wait_registration()
+        deadline = time.time() + 10
+        while len(conns) < 2:  # the health monitor's connection and a scan's
+            assert time.time() < deadline
+            time.sleep(0.05)
+        t0 = time.time()
+        assert d.stop() == 0
+        assert time.time() - t0 < 10
+        assert "driver-side scan through the relay failed" not in d.log()
+    finally:
+        if d.proc.poll() is None:
+            d.stop()
+        k.stop()
+        srv.close()
+        for c in conns:
+            c.close()
