@@ -32,7 +32,8 @@
 //                     amdsmi_get_gpu_kfd_info reports node_id unsupported)
 //               } ] }
 // Runtime injection:
-//   event FIFO lines: "<gpu>[:<partition>] <event-type> [message]"
+//   event FIFO lines: "<gpu>[:<partition>] <event-type> [message]",
+//                     "hang <ms>" (that event wait then returns only after <ms>)
 //   state_dir files:  gpu<i>.ecc (uncorrectable count; not a number = query fails),
 //                     gpu<i>.dead (device gone),
 //                     gpu<i>.partition ("CPX NPS2": live partition-mode override),
@@ -685,8 +686,9 @@ amdsmi_status_t amdsmi_get_gpu_event_notification(int timeout_ms, uint32_t* num,
   }
   pollfd pfd{fd, POLLIN, 0};
   int r = poll(&pfd, 1, timeout_ms);
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::unique_lock<std::mutex> lk(g_mu);
   if (!g) return AMDSMI_STATUS_INIT_ERROR;
+  int hang_ms = 0;
   if (r > 0) {
     char buf[4096];
     ssize_t n;
@@ -701,6 +703,10 @@ amdsmi_status_t amdsmi_get_gpu_event_notification(int timeout_ms, uint32_t* num,
     std::string target;
     int type = 0;
     if (!(ls >> target >> type)) continue;
+    if (target == "hang") {  // fault injection: "hang <ms>" -- this wait does not return for that long
+      hang_ms = type;
+      continue;
+    }
     std::string msg;
     std::getline(ls, msg);
     int gpu = atoi(target.c_str());
@@ -719,6 +725,10 @@ amdsmi_status_t amdsmi_get_gpu_event_notification(int timeout_ms, uint32_t* num,
     ++got;
   }
   *num = got;
+  if (hang_ms > 0) {
+    lk.unlock();
+    usleep(static_cast<useconds_t>(hang_ms) * 1000);
+  }
   return got ? AMDSMI_STATUS_SUCCESS : AMDSMI_STATUS_NO_DATA;
 }
 

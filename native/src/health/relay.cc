@@ -12,6 +12,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -258,15 +260,24 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     return 1;
   }
   std::atomic<bool> waiter_stop{false};
+  std::atomic<int64_t> beat_ms{0};  // the waiter's last sign of life (steady clock)
+  auto now_ms = [] {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  };
   std::thread waiter;
   auto start_waiter = [&] {
     if (!registered) return;
     waiter_stop.store(false);
+    beat_ms.store(now_ms());
     waiter = std::thread([&] {
       std::vector<smi::Event> events;
       while (!waiter_stop.load()) {
         events.clear();
-        if (Status st = lib->EventsWait(100, &events); !st.ok()) {
+        beat_ms.store(now_ms());
+        Status st = lib->EventsWait(100, &events);
+        beat_ms.store(now_ms());
+        if (!st.ok()) {
           LOG_WARN(kComp, "event wait failed: %s", st.ToString().c_str());
           usleep(100000);
           continue;
@@ -302,10 +313,42 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
   int exit_code = 0;
   bool quit = false;
   std::string pending;  // event bytes read from the pipe, up to the last full line
+  // Watchdog: an amdsmi wait that has not returned for kStuckMs means events
+  // are not being delivered; the daemons are told (a "reinit" hello with
+  // events=off, so they poll) and told again when the wait returns.
+  const int64_t kStuckMs = [] {
+    const char* e = getenv("ADP_RELAY_STUCK_MS");
+    return e && atoll(e) > 0 ? static_cast<int64_t>(atoll(e)) : int64_t{10000};
+  }();
+  bool stuck = false;
+  std::string state_before_stuck;
+  auto broadcast = [&](const std::string& line) {
+    for (auto& c : clients)
+      if (c.fd >= 0 && !SendAll(c.fd, line)) {
+        close(c.fd);
+        c.fd = -1;
+      }
+  };
   while (!quit) {
     std::vector<pollfd> pfds = {{signal_fd, POLLIN, 0}, {lfd, POLLIN, 0}, {pipefd[0], POLLIN, 0}};
     for (const auto& c : clients) pfds.push_back({c.fd, POLLIN, 0});
-    if (poll(pfds.data(), pfds.size(), -1) < 0 && errno != EINTR) break;
+    int timeout = waiter.joinable() ? static_cast<int>(std::min<int64_t>(1000, kStuckMs / 2 + 1)) : -1;
+    if (poll(pfds.data(), pfds.size(), timeout) < 0 && errno != EINTR) break;
+    if (waiter.joinable()) {
+      int64_t silent = now_ms() - beat_ms.load();
+      if (!stuck && silent > kStuckMs) {
+        stuck = true;
+        state_before_stuck = events_state;
+        events_state = "events=off reason=the amdsmi event wait has not returned for " + std::to_string(silent) + " ms";
+        LOG_ERROR(kComp, "%s: daemons fall back to polling", events_state.c_str());
+        broadcast("hello v1 reinit " + events_state + "\n");
+      } else if (stuck && silent <= kStuckMs) {
+        stuck = false;
+        events_state = state_before_stuck;
+        LOG_INFO(kComp, "the amdsmi event wait returned again: events back on");
+        broadcast("hello v1 reinit " + events_state + "\n");
+      }
+    }
     if (pfds[2].revents & POLLIN) {
       char buf[4096];
       ssize_t n;
@@ -315,11 +358,7 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
         std::string lines = pending.substr(0, cut + 1);
         pending.erase(0, cut + 1);
         LOG_INFO(kComp, "%s", OneLine(lines).c_str());
-        for (auto& c : clients)
-          if (c.fd >= 0 && !SendAll(c.fd, lines)) {
-            close(c.fd);
-            c.fd = -1;
-          }
+        broadcast(lines);
       }
     }
     if (pfds[0].revents & POLLIN) {
@@ -387,22 +426,29 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     clients.erase(std::remove_if(clients.begin(), clients.end(), [](const Client& c) { return c.fd < 0; }),
                   clients.end());
     if (do_reinit) {
-      LOG_INFO(kComp, "re-enumerating (a daemon asked)");
-      stop_waiter();
-      enumerate_and_register(true);
-      start_waiter();
+      if (stuck) {
+        // amdsmi cannot be re-initialised under a wait that does not return:
+        // the daemon gets the current (events off) state instead.
+        LOG_WARN(kComp, "re-enumeration a daemon asked for skipped: the event wait is stuck");
+      } else {
+        LOG_INFO(kComp, "re-enumerating (a daemon asked)");
+        stop_waiter();
+        enumerate_and_register(true);
+        start_waiter();
+      }
       // Marked, so a daemon tells the state after its own request from the
       // hello every connection gets first (sent before the request was read).
-      std::string fresh = "hello v1 reinit " + events_state + "\n";
-      for (auto& c : clients)
-        if (!SendAll(c.fd, fresh)) {
-          close(c.fd);
-          c.fd = -1;
-        }
+      broadcast("hello v1 reinit " + events_state + "\n");
     }
   }
-  stop_waiter();
-  if (!handles.empty() && registered) lib->EventsStop(handles);
+  if (stuck) {
+    // Joining would wait on the stuck call; the process is about to exit.
+    LOG_WARN(kComp, "exiting with the event wait still stuck");
+    waiter.detach();
+  } else {
+    stop_waiter();
+    if (!handles.empty() && registered) lib->EventsStop(handles);
+  }
   for (auto& c : clients)
     if (c.fd >= 0) close(c.fd);
   close(pipefd[0]);

@@ -14,6 +14,9 @@
 //   relay -> daemon  "hello v1 events=ok processors=<n>"         (on connect)
 //                    "hello v1 events=off reason=<text>"       (registration failed)
 //                    "hello v1 reinit events=ok processors=<n>" (after a "reinit")
+//                    "hello v1 reinit events=off reason=..."   (watchdog: the amdsmi
+//                                 wait has not returned for ADP_RELAY_STUCK_MS,
+//                                 default 10 s; "events=ok" again once it does)
 //                    "event node=<kfd node|-> bdf=<bdf> part=<partition id> type=<t> <message>"
 //   daemon -> relay  "reinit"   re-enumerate (amdsmi_shut_down + init) and register
 //                               again, then a "reinit" hello to every client (a new

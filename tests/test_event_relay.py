@@ -223,3 +223,30 @@ def test_relay_answers_scan_requests_and_drops_malformed_ones(scratch, tmp_path)
         assert relay.log().count("malformed scan request dropped") == 3
     finally:
         relay.stop()
+
+
+def test_a_stuck_event_wait_turns_events_off_until_it_returns(scratch):
+    """Watchdog: an amdsmi event wait that does not return (the mock's "hang")
+    for ADP_RELAY_STUCK_MS is reported to the daemon as events off -- it polls
+    -- and, once the wait returns, as events on again; events then flow."""
+    n = RelayNode(scratch, relay_env={"ADP_RELAY_STUCK_MS": "300"})
+    try:
+        n.d.wait_log("events on through the relay")
+        n.inject("hang 1500")
+        log = n.d.wait_log("has not returned for")
+        line = [ln for ln in log.splitlines() if "has not returned for" in ln][0]
+        assert "event relay reports" in line and "polling only" in line, line
+        deadline = time.time() + 5
+        while _value(n.metrics(), "amdgpu_dp_health_events_enabled") != 0:
+            assert time.time() < deadline
+            time.sleep(0.05)
+        assert "daemons fall back to polling" in n.relay.wait_log("daemons fall back to polling")
+        n.relay.wait_log("the amdsmi event wait returned again", timeout=10)
+        deadline = time.time() + 5
+        while _value(n.metrics(), "amdgpu_dp_health_events_enabled") != 1:
+            assert time.time() < deadline
+            time.sleep(0.05)
+        n.inject("1 3 mode1 reset")
+        assert n.health() == ["Healthy", "Unhealthy"]
+    finally:
+        n.stop()
