@@ -301,6 +301,12 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   if (!cfg.flags.metrics_addr.empty() && !cfg.flags.pod_resources_socket.empty())
     pod_lister = std::make_unique<podresources::CachedLister>(cfg.flags.pod_resources_socket,
                                                               std::chrono::milliseconds(2000));
+  // (env only: how long the health loop may go without an iteration before /healthz fails)
+  const int64_t stall_ms = [] {
+    const char* e = getenv("ADP_HEALTH_STALL_MS");
+    return e && atoll(e) > 0 ? static_cast<int64_t>(atoll(e)) : int64_t{60000};
+  }();
+  std::atomic<bool> stall_logged{false};
   if (!cfg.flags.metrics_addr.empty()) {
     std::string smi_version = (*lib)->Version();
     http = std::make_unique<metrics::HttpServer>(
@@ -317,6 +323,10 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
               "# HELP amdgpu_dp_health_events_enabled 1 if amdsmi event notification is registered (-1 not started).\n"
               "# TYPE amdgpu_dp_health_events_enabled gauge\n"
               "amdgpu_dp_health_events_enabled " + std::to_string(health_counters.events_enabled.load()) + "\n"
+              "# HELP amdgpu_dp_health_loop_age_seconds Time since the health monitor loop last iterated (0 when "
+              "none runs; /healthz fails past ADP_HEALTH_STALL_MS).\n"
+              "# TYPE amdgpu_dp_health_loop_age_seconds gauge\n"
+              "amdgpu_dp_health_loop_age_seconds " + std::to_string(health_counters.HealthLoopAgeMs() / 1e3) + "\n"
               "# HELP amdgpu_dp_health_polls_total Health polls (liveness + uncorrectable ECC) run.\n"
               "# TYPE amdgpu_dp_health_polls_total counter\n"
               "amdgpu_dp_health_polls_total " + std::to_string(health_counters.polls.load()) + "\n"
@@ -445,8 +455,17 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
                                            have_grants ? &grant_files : nullptr);
           return out;
         },
-        [&] {
+        [&, stall_ms] {
           if (!serving.load()) return false;
+          // A health loop stuck in a call that never returns (an amdsmi event
+          // wait or query) stops advancing: the liveness probe restarts us.
+          if (int64_t age = health_counters.HealthLoopAgeMs(); age > stall_ms) {
+            if (!stall_logged.exchange(true))
+              LOG_ERROR(kComp, "the health monitor has not advanced for %lld ms: /healthz fails",
+                        static_cast<long long>(age));
+            return false;
+          }
+          stall_logged.store(false);
           std::lock_guard<std::mutex> lk(plugins_mu);
           for (auto& p : plugins)
             if (p->device_count() > 0 && !p->running()) return false;

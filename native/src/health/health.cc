@@ -612,11 +612,17 @@ void Monitor::Update(int gpu, uint32_t set, uint32_t clear, const std::string& r
   }
 }
 
+int64_t HealthCounters::HealthLoopAgeMs() const {
+  int64_t beat = loop_beat_ms.load();
+  return beat == 0 ? 0 : std::max<int64_t>(0, NowMs() - beat);
+}
+
 void Monitor::Run() {
   using Clock = std::chrono::steady_clock;
   auto next_poll = Clock::now() + std::chrono::milliseconds(cfg_.poll_interval_ms);
   std::vector<smi::Event> events;
   while (!stop_.load()) {
+    counters_->loop_beat_ms.store(NowMs());
     int slice = 100;  // bounded so Stop() (SIGHUP, config, re-partition, exit) is prompt; the reference waits 5000 ms
     if (cfg_.wait_ms > 0 && cfg_.wait_ms < slice) slice = cfg_.wait_ms;
     if (cfg_.poll_interval_ms > 0) {  // wake for the next poll, not a slice later
@@ -682,6 +688,7 @@ void Monitor::Run() {
       next_poll = Clock::now() + std::chrono::milliseconds(cfg_.poll_interval_ms);
     }
   }
+  counters_->loop_beat_ms.store(0);
 }
 
 }  // namespace adp::health

@@ -107,6 +107,12 @@ struct HealthCounters {
   std::atomic<uint64_t> events_received{0};
   std::atomic<uint64_t> retired_reads_ok{0};
   std::atomic<uint64_t> retired_read_errors{0};
+  // Steady-clock ms of the monitor loop's last iteration (0 = no monitor
+  // running): a wait or amdsmi query that never returns stops it advancing,
+  // which /healthz reports (HealthLoopAgeMs).
+  std::atomic<int64_t> loop_beat_ms{0};
+  // How long the running monitor loop has not iterated (0 when none runs).
+  int64_t HealthLoopAgeMs() const;
   // Last retired-page count per GPU (by PCI address), for /metrics.
   void SetRetiredPages(const std::string& bdf, uint32_t n);
   std::map<std::string, uint32_t> RetiredPages() const;

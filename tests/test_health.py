@@ -236,3 +236,31 @@ def test_events_counted_per_gpu_and_type_on_metrics(node):
             break
         time.sleep(0.05)
     assert got == want, body[-2000:]
+
+
+def test_healthz_fails_while_the_health_loop_is_stuck(scratch):
+    """A health monitor stuck in a call that does not return (here the mock's
+    event wait, "hang") stops its loop: /healthz answers 503 -- the liveness
+    probe restarts the daemon -- and 200 again once the loop moves.
+    amdgpu_dp_health_loop_age_seconds shows the age."""
+    import re
+    from test_metrics import _get, _parse, _value
+    n = Node(scratch, dict(fixtures.node(1), events_open_kfd=True), args=["--metrics-addr", "127.0.0.1:0"],
+             env={"ADP_HEALTH_STALL_MS": "400", "DP_HEALTH_POLL_MS": "100"})
+    try:
+        port = int(re.search(r"on port (\d+)", n.d.wait_log("serving /metrics")).group(1))
+        assert _get(port, "/healthz")[0] == 200
+        assert _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_health_loop_age_seconds") < 0.4
+        n.inject("hang 2000")
+        deadline = time.time() + 3
+        while _get(port, "/healthz")[0] != 503:
+            assert time.time() < deadline
+            time.sleep(0.05)
+        assert _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_health_loop_age_seconds") > 0.4
+        assert "the health monitor has not advanced for" in n.d.log()
+        deadline = time.time() + 5
+        while _get(port, "/healthz")[0] != 200:
+            assert time.time() < deadline
+            time.sleep(0.05)
+    finally:
+        n.close()
