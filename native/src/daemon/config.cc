@@ -129,6 +129,10 @@ const std::vector<FlagDef>& Table() {
        "print, as JSON, the status of every amdsmi query the plugin uses and whether each device node "
        "opens (what this container's privileges and device cgroup allow) and exit",
        [](Flags& f) -> void* { return &f.smi_report; }},
+      {"relay-ping", "ADP_RELAY_PING", "", Kind::kBool,
+       "liveness check of the event relay at --health-event-socket (the relay container's probe): exit 0 "
+       "when it greets within 5 s with a working event wait, 1 otherwise; loads no amdsmi",
+       [](Flags& f) -> void* { return &f.relay_ping; }},
       {"doctor", "ADP_DOCTOR", "", Kind::kBool,
        "check what this deployment needs on this node -- amdsmi, enumeration, resources, device-node "
        "access, health events, ECC, the kubelet socket, the plugin directory, the HBM-cap shim, the host "

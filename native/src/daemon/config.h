@@ -49,6 +49,7 @@ struct Flags {
   bool dry_run = false;
   bool list_grants = false;
   bool smi_report = false;       // print every amdsmi query's status + device-node access, exit
+  bool relay_ping = false;       // liveness check of the event relay at --health-event-socket, exit
   bool doctor = false;           // check what a deployment needs on this node, say what to change, exit
   bool health_events = true;     // register amdsmi event notification (needs /dev/kfd access)
   std::string health_event_socket;  // events from the relay at this socket ("" = in-process)

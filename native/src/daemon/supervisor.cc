@@ -173,6 +173,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   LOG_INFO(kComp, "running with resource config: %s", v.rc.ToJson().c_str());
 
   if (cfg.flags.list_grants) return ListGrants(PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage"));
+  if (cfg.flags.relay_ping) return health::PingRelay(cfg.flags.health_event_socket, 5000);
 
   // Signals are consumed through a signalfd; block them before any thread starts.
   sigset_t sigs;

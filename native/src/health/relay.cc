@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -192,6 +193,36 @@ int ConnectRelay(const std::string& socket_path) {
   }
   fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK);
   return fd;
+}
+
+int PingRelay(const std::string& socket_path, int timeout_ms) {
+  int fd = ConnectRelay(socket_path);
+  if (fd < 0) {
+    printf("event relay at %s not reachable: %s\n", socket_path.c_str(), strerror(errno));
+    return 1;
+  }
+  std::string in;
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  size_t nl;
+  while ((nl = in.find('\n')) == std::string::npos) {
+    int left = static_cast<int>(
+        std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count());
+    pollfd p{fd, POLLIN, 0};
+    if (left <= 0 || poll(&p, 1, left) <= 0) break;
+    char buf[512];
+    ssize_t n = recv(fd, buf, sizeof(buf), 0);
+    if (n <= 0) break;
+    in.append(buf, static_cast<size_t>(n));
+  }
+  close(fd);
+  if (nl == std::string::npos) {
+    printf("event relay at %s did not greet within %d ms\n", socket_path.c_str(), timeout_ms);
+    return 1;
+  }
+  RelayLine l = ParseRelayLine(std::string_view(in).substr(0, nl));
+  printf("%s\n", in.substr(0, nl).c_str());
+  if (l.kind != "hello") return 1;
+  return l.reason.find("has not returned") != std::string::npos ? 1 : 0;
 }
 
 int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_fd, const RelayOptions& opts) {

@@ -69,4 +69,10 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
 // Daemon side: connects to the relay (non-blocking), -1 when not reachable.
 int ConnectRelay(const std::string& socket_path);
 
+// Liveness probe of a relay (--relay-ping): 0 when it greets within
+// `timeout_ms` and its event wait is not stuck (events off for another reason
+// -- no /dev/kfd -- is alive: restarting would not help), else 1. Prints the
+// greeting or what went wrong.
+int PingRelay(const std::string& socket_path, int timeout_ms);
+
 }  // namespace adp::health

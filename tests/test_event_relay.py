@@ -250,3 +250,43 @@ def test_a_stuck_event_wait_turns_events_off_until_it_returns(scratch):
         assert n.health() == ["Healthy", "Unhealthy"]
     finally:
         n.stop()
+
+
+def test_relay_ping_is_the_relays_liveness(scratch, tmp_path):
+    """--relay-ping (the relay container's exec liveness probe): 0 for a relay
+    that greets -- events off for a lasting reason included, a restart would
+    not fix that -- 1 for no relay, a relay that never greets, and a relay
+    whose amdsmi event wait is stuck."""
+    import socket as so
+    import subprocess
+
+    def ping(sock):
+        r = subprocess.run([harness.DAEMON, "--relay-ping", "--health-event-socket", sock], capture_output=True,
+                           text=True, timeout=30)
+        return r.returncode, r.stdout
+    assert ping(str(tmp_path / "none.sock"))[0] == 1
+    mute = so.socket(so.AF_UNIX, so.SOCK_STREAM)
+    mute.bind(str(tmp_path / "mute.sock"))
+    mute.listen(1)
+    try:
+        rc, out = ping(str(tmp_path / "mute.sock"))
+        assert rc == 1 and "did not greet" in out
+    finally:
+        mute.close()
+    n = RelayNode(scratch, relay_env={"ADP_RELAY_STUCK_MS": "300"})
+    try:
+        rc, out = ping(n.sock)
+        assert rc == 0 and out.startswith("hello v1 events=ok"), out
+        n.inject("hang 2000")
+        n.relay.wait_log("daemons fall back to polling")
+        rc, out = ping(n.sock)
+        assert rc == 1 and "has not returned" in out, out
+    finally:
+        n.stop()
+    os.makedirs(scratch + "b")
+    denied = RelayNode(scratch + "b", relay_env={"LD_PRELOAD": _preload(SIM)})
+    try:
+        rc, out = ping(denied.sock)
+        assert rc == 0 and "events=off" in out, out
+    finally:
+        denied.stop()

@@ -94,7 +94,11 @@ def test_defaults_render_a_valid_daemonset():
     r = relay(ds)
     assert r["securityContext"] == {"privileged": True}
     assert r["args"] == ["--event-relay", "--health-event-socket", "/run/amdgpu-dp-events/events.sock"]
-    assert not r.get("ports") and "livenessProbe" not in r  # no network-facing input
+    assert not r.get("ports")  # no network-facing input
+    # its liveness: the relay greets on its socket and its event wait is not stuck
+    assert r["livenessProbe"]["exec"]["command"] == ["/usr/bin/amdgpu-device-plugin", "--relay-ping",
+                                                     "--health-event-socket",
+                                                     "/run/amdgpu-dp-events/events.sock"]
     shared = {m["name"]: m["mountPath"] for m in r["volumeMounts"]}
     assert shared["event-socket"] == "/run/amdgpu-dp-events"
     assert {m["name"]: m["mountPath"] for m in container(ds)["volumeMounts"]}["event-socket"] == "/run/amdgpu-dp-events"
