@@ -179,7 +179,11 @@ def test_event_relay_on_real_amdsmi(scratch, snap, tmp_path):
         k.wait_registration(30)
         d.wait_log("health monitor watching", 30)
         log = d.wait_log("events on through the relay", 30)
-        _save("event_relay.json", {"relay_log": relay.log()[-3000:], "daemon_log": log[-4000:]})
+        ping = subprocess.run([harness.DAEMON, "--relay-ping", "--health-event-socket", sock], capture_output=True,
+                              text=True, timeout=30)
+        _save("event_relay.json", {"relay_log": relay.log()[-3000:], "daemon_log": log[-4000:],
+                                   "relay_ping": {"rc": ping.returncode, "out": ping.stdout}})
+        assert ping.returncode == 0 and ping.stdout.startswith("hello v1 events=ok"), ping.stdout + ping.stderr
         assert "event notification registered on" in relay.log(), relay.log()[-2000:]
         assert "events on through the relay" in log, log[-3000:]
         assert "device access: Operation not permitted: /dev/kfd" in log  # the daemon itself is denied
