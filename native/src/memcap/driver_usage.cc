@@ -311,8 +311,9 @@ std::vector<std::string_view> Fields(std::string_view line) {
   return f;
 }
 
+// Canonical decimal only (no sign, no leading zero): what std::to_string writes.
 bool ToU64(std::string_view v, uint64_t* out) {
-  if (v.empty() || v.size() > 20) return false;
+  if (v.empty() || v.size() > 20 || (v.size() > 1 && v[0] == '0')) return false;
   uint64_t n = 0;
   for (char c : v) {
     if (c < '0' || c > '9') return false;
@@ -340,6 +341,8 @@ bool ParseScan(std::string_view text, DriverScan* out, size_t* consumed) {
   // A header, then exactly as many process lines as it announces.
   size_t nl = text.find('\n');
   if (nl == std::string_view::npos) return false;
+  // (SerializeScan never writes a carriage return: a reply holding one is not its)
+  if (text.substr(0, nl).find('\r') != std::string_view::npos) return false;
   auto h = Fields(text.substr(0, nl));
   uint64_t pids = 0, fds = 0, unreadable = 0, n = 0;
   if (h.size() != 6 || h[0] != "scan" || !ToU64(h[2], &pids) || !ToU64(h[3], &fds) ||
@@ -353,7 +356,7 @@ bool ParseScan(std::string_view text, DriverScan* out, size_t* consumed) {
   size_t pos = nl + 1;
   for (uint64_t i = 0; i < n; ++i) {
     size_t e = text.find('\n', pos);
-    if (e == std::string_view::npos) return false;
+    if (e == std::string_view::npos || text.substr(pos, e - pos).find('\r') != std::string_view::npos) return false;
     auto f = Fields(text.substr(pos, e - pos));
     uint64_t pid = 0, bytes = 0;
     if (f.size() != 7 || f[0] != "p" || !ToU64(f[1], &pid) || pid > INT32_MAX || !ToU64(f[3], &bytes) ||
