@@ -24,7 +24,7 @@ def lib() -> ctypes.CDLL:
     so = ctypes.CDLL(CAPI_LIB)
     for name in ("adp_prioritize", "adp_strip_replicas", "adp_parse_additional_ids",
                  "adp_parse_resource_config", "adp_best_effort", "adp_snapshot", "adp_plugin_specs",
-                 "adp_driver_scan"):
+                 "adp_driver_scan", "adp_kfd_topology_cus"):
         fn = getattr(so, name)
         fn.argtypes = [ctypes.c_char_p]
         fn.restype = ctypes.c_void_p
@@ -74,6 +74,11 @@ def driver_scan(proc_root, kfd_proc_dir="", usage_dir="", self_cgroup=""):
                                             "usage_dir": usage_dir, "self_cgroup": self_cgroup}))
 
 
+def kfd_topology_cus(topology_dir, node):
+    """CUs of a KFD topology node (inventory::KfdTopologyCus), 0 when unreadable."""
+    return _check(_call("adp_kfd_topology_cus", {"dir": topology_dir, "node": int(node)}))["cus"]
+
+
 def strip_replicas(ids):
     return _call("adp_strip_replicas", list(ids))
 
@@ -95,8 +100,10 @@ def best_effort(parent, scores, available, required, size):
                                       "required": required, "size": size})
 
 
-def snapshot(lib_path: str = "", devices=None, include_card_nodes=False):
+def snapshot(lib_path: str = "", devices=None, include_card_nodes=False, sysfs_root=None):
     req = {"lib": lib_path, "include_card_nodes": include_card_nodes}
+    if sysfs_root is not None:
+        req["sysfs_root"] = sysfs_root
     if devices is not None:
         req["devices"] = list(devices)
     return _check(_call("adp_snapshot", req))

@@ -30,6 +30,8 @@
 //                     is kfd_node + p): the order ROCr/HIP number the GPUs in, which
 //                     need not be amdsmi's enumeration order ("kfd_node": null =
 //                     amdsmi_get_gpu_kfd_info reports node_id unsupported)
+//                 "render_denied": true,        asic_info and vram_info fail (FILE_ERROR), as
+//                     with the render node denied by a device cgroup
 //               } ] }
 // Runtime injection:
 //   event FIFO lines: "<gpu>[:<partition>] <event-type> [message]",
@@ -87,6 +89,7 @@ struct MockProc {
   bool report_numa_ranges = true;
   int links_down = 0;
   int64_t kfd_node = 0;         // -1: node_id not reported
+  bool render_denied = false;   // asic_info / vram_info fail as without render-node access
   bool evt_init = false;
   uint64_t evt_mask = 0;
 };
@@ -233,6 +236,7 @@ bool Load() {
       mp->cmode = cmode;
       mp->mmode = mmode;
       mp->links_down = jg.value("xgmi_links_down", 0);
+      mp->render_denied = jg.value("render_denied", false);
       if (jg.count("kfd_node") && jg["kfd_node"].is_null()) mp->kfd_node = -1;
       else mp->kfd_node = jg.value("kfd_node", static_cast<int64_t>(2 + gi * 8)) + p;
       mg.procs.push_back(mp.get());
@@ -408,6 +412,7 @@ amdsmi_status_t amdsmi_get_gpu_topo_numa_affinity(amdsmi_processor_handle h, int
 amdsmi_status_t amdsmi_get_gpu_vram_info(amdsmi_processor_handle h, amdsmi_vram_info_t* info) {
   GET_PROC(h);
   memset(info, 0, sizeof(*info));
+  if (p->render_denied) return AMDSMI_STATUS_FILE_ERROR;  // libdrm could not open the render node
   info->vram_type = AMDSMI_VRAM_TYPE_HBM3E;
   CopyStr(info->vram_vendor, sizeof(info->vram_vendor), "MOCK");
   info->vram_size = p->vram_mib;
@@ -542,6 +547,7 @@ amdsmi_status_t amdsmi_get_gpu_kfd_info(amdsmi_processor_handle h, amdsmi_kfd_in
 amdsmi_status_t amdsmi_get_gpu_asic_info(amdsmi_processor_handle h, amdsmi_asic_info_t* info) {
   GET_PROC(h);
   memset(info, 0, sizeof(*info));
+  if (p->render_denied) return AMDSMI_STATUS_FILE_ERROR;
   CopyStr(info->market_name, sizeof(info->market_name), p->market);
   CopyStr(info->asic_serial, sizeof(info->asic_serial), p->serial);
   info->vendor_id = 0x1002;

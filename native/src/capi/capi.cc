@@ -182,6 +182,14 @@ char* adp_best_effort(const char* in) {
 
 // Loads libamd_smi (path "" = default search), enumerates, returns the snapshot.
 // {"lib": "...", "devices": [0, 1] | ["0000:0c:00.0", "<uuid>", ...]} (as --devices)
+// {"dir", "node"} -> {"cus": n}: inventory::KfdTopologyCus.
+char* adp_kfd_topology_cus(const char* in) {
+  return Guard([&] {
+    json j = json::parse(in);
+    return Dup(json{{"cus", adp::inventory::KfdTopologyCus(j.value("dir", std::string()), j.value("node", 0u))}}.dump());
+  });
+}
+
 char* adp_snapshot(const char* in) {
   return Guard([&] {
     json j = json::parse(in);
@@ -194,6 +202,7 @@ char* adp_snapshot(const char* in) {
         else opt.only_ids.push_back(d.get<std::string>());
       }
     opt.include_card_nodes = j.value("include_card_nodes", false);
+    opt.sysfs_root = j.value("sysfs_root", opt.sysfs_root);
     auto snap = adp::inventory::BuildSnapshot(lib->get(), opt);
     if (!snap.ok()) return Err(snap.status().ToString());
     return Dup(SnapshotJson(**snap).dump());

@@ -168,6 +168,11 @@ const std::vector<FlagDef>& Table() {
        "KFD's list of GPU processes (host PIDs) for the driver-side HBM check: only those processes' "
        "descriptors are read, not every process's (empty = always walk every process under --host-proc)",
        [](Flags& f) -> void* { return &f.kfd_proc_dir; }},
+      {"sysfs-root", "DP_SYSFS_ROOT", "sysfsRoot", Kind::kString,
+       "where sysfs is mounted: without the render node (an unprivileged pod's device cgroup denies it) "
+       "amdsmi's asic_info fails, and the CU count comes from <root>/class/kfd/kfd/topology and the product "
+       "name from <root>/bus/pci/devices/<bdf>/product_name, both readable unprivileged (empty = neither)",
+       [](Flags& f) -> void* { return &f.sysfs_root; }},
       {"cdi-spec-dir", "CDI_SPEC_DIR", "cdiSpecDir", Kind::kString,
        "directory for the generated CDI spec (cdi-annotations / cdi-cri strategies)",
        [](Flags& f) -> void* { return &f.cdi_spec_dir; }},

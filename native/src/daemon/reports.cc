@@ -183,6 +183,14 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
   for (const auto& g : s.gpus) parts += g.partitions.size();
   d.Line("ok", "enumeration: " + std::to_string(s.gpus.size()) + " GPU(s), " + std::to_string(parts) +
                    " compute partition(s), " + s.gpus[0].compute_mode + "/" + s.gpus[0].memory_mode);
+  if (s.cus_unknown)
+    d.Line(f.replica_cu_mask ? "FAIL" : "warn",
+           "CU counts: unknown on " + std::to_string(s.cus_unknown) + " processor(s) -- amdsmi's asic_info needs the "
+           "render node and KFD topology (under --sysfs-root " + f.sysfs_root + ") is not readable" +
+           (f.replica_cu_mask ? ", so --replica-cu-mask cuts no CU shares" : ""));
+  else if (s.cus_from_topology)
+    d.Line("ok", "CU counts: from KFD topology on " + std::to_string(s.cus_from_topology) +
+                     " processor(s) (asic_info needs the render node, which this container may not open)");
   {
     // How a container numbers its GPUs: KFD topology-node order (what every
     // per-device list Allocate() returns follows), not necessarily amdsmi's.

@@ -96,6 +96,7 @@ Result<Validated> Validate(const Config& cfg) {
                            (f.memcap_lib.empty() ? std::string("next to the binary or in /usr/lib/amdgpu-device-plugin")
                                                  : f.memcap_lib) + "); set --memcap-lib");
   v.bopts.driver_root = f.driver_root;
+  v.bopts.sysfs_root = f.sysfs_root;
   v.bopts.include_card_nodes = f.include_card_nodes;
   std::string devs = Trim(f.devices);
   if (!devs.empty() && devs != "all") {

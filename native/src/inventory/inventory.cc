@@ -95,10 +95,87 @@ int Snapshot::GpuOfHandle(int h) const {
   return -1;
 }
 
+uint32_t KfdTopologyCus(const std::string& topology_dir, uint32_t node) {
+  std::string path = topology_dir + "/" + std::to_string(node) + "/properties";
+  int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return 0;
+  std::string text;
+  char buf[4096];
+  ssize_t n;
+  while ((n = read(fd, buf, sizeof(buf))) > 0 && text.size() < 65536) text.append(buf, static_cast<size_t>(n));
+  close(fd);
+  uint64_t simds = 0, per_cu = 0;
+  for (size_t b = 0; b < text.size();) {
+    size_t e = text.find('\n', b);
+    if (e == std::string::npos) e = text.size();
+    std::string line = text.substr(b, e - b);
+    b = e + 1;
+    size_t sp = line.find(' ');
+    if (sp == std::string::npos) continue;
+    std::string key = line.substr(0, sp);
+    auto v = ParseUint(Trim(line.substr(sp + 1)));
+    if (!v) continue;
+    if (key == "simd_count") simds = *v;
+    else if (key == "simd_per_cu") per_cu = *v;
+  }
+  if (simds == 0 || per_cu == 0 || simds % per_cu != 0 || simds / per_cu > 0xffffu) return 0;
+  return static_cast<uint32_t>(simds / per_cu);
+}
+
+std::string PciProductName(const std::string& sysfs_root, const std::string& bdf) {
+  // Compute partitions report their own function numbers; the board is function 0.
+  size_t dot = bdf.rfind('.');
+  if (dot == std::string::npos || bdf.find('/') != std::string::npos) return "";
+  std::string path = sysfs_root + "/bus/pci/devices/" + bdf.substr(0, dot) + ".0/product_name";
+  int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return "";
+  char buf[256];
+  ssize_t n = read(fd, buf, sizeof(buf) - 1);
+  close(fd);
+  if (n <= 0) return "";
+  std::string v = Trim(std::string_view(buf, static_cast<size_t>(n)));
+  for (char c : v)
+    if (static_cast<unsigned char>(c) < 0x20) return "";  // not a name
+  return v;
+}
+
 Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo> procs,
                                                   const BuildOptions& opt) {
   auto snap = std::make_shared<Snapshot>();
   snap->procs = std::move(procs);
+  // Without the render node asic_info fails and the CU count (what CU shares
+  // are cut from) is unknown; KFD's topology has it, readable unprivileged.
+  // The board's FRU product name (PCI sysfs) names the model where asic_info
+  // says "AMD Radeon Graphics" -- and answers without the render node too.
+  if (!opt.sysfs_root.empty()) {
+    const std::string topo = opt.sysfs_root + "/class/kfd/kfd/topology/nodes";
+    size_t filled = 0, missing = 0, named = 0;
+    for (auto& p : snap->procs) {
+      std::string product = PciProductName(opt.sysfs_root, p.bdf);
+      if (!product.empty() && product != p.market_name) {
+        p.market_name = product;
+        ++named;
+      }
+      if (p.num_cu != 0) continue;
+      uint32_t cus = p.kfd_node == kNoKfdNode ? 0 : KfdTopologyCus(topo, p.kfd_node);
+      if (cus) {
+        p.num_cu = cus;
+        ++filled;
+      } else {
+        ++missing;
+      }
+    }
+    snap->cus_from_topology = filled;
+    snap->cus_unknown = missing;
+    if (filled)
+      LOG_INFO(kComp, "CU counts of %zu processor(s) from KFD topology (%s): amdsmi's asic_info did not answer",
+               filled, topo.c_str());
+    if (named)
+      LOG_INFO(kComp, "product names of %zu processor(s) from PCI sysfs (the board's FRU name)", named);
+    if (missing)
+      LOG_WARN(kComp, "CU count of %zu processor(s) unknown (asic_info and KFD topology): no CU shares on them",
+               missing);
+  }
   // Group handles into physical GPUs. Compute partitions of one GPU report the
   // same ASIC serial; without one, group by PCI domain:bus:device (partitions
   // differ only in the function number); last resort, the UUID.

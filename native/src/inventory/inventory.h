@@ -102,6 +102,10 @@ struct Snapshot {
   std::vector<int> gpu_link_types;    // raw smi::LinkType, -1 = query failed
   std::string smi_path;
   std::string smi_version;
+  // Processors whose CU count came from KFD topology (asic_info unanswered),
+  // and those whose count stayed unknown.
+  size_t cus_from_topology = 0;
+  size_t cus_unknown = 0;
 
   LinkClass Link(int a, int b) const { return gpu_links[a * gpus.size() + b]; }
   uint64_t Hops(int a, int b) const { return gpu_hops[a * gpus.size() + b]; }
@@ -140,7 +144,19 @@ struct BuildOptions {
   // ... or by GPU UUID / PCI address ("0000:0c:00.0", function ignored).
   std::vector<std::string> only_ids;
   bool include_card_nodes = false;
+  // sysfs, for what amdsmi's asic_info gives only with the render node (which
+  // an unprivileged pod's device cgroup denies): the CU count from KFD's
+  // topology (class/kfd/kfd/topology/nodes/<node>/properties) and the board's
+  // product name (bus/pci/devices/<bdf>/product_name, the FRU name: "AMD
+  // Instinct MI355 OAM" where asic_info says "AMD Radeon Graphics"). "" = neither.
+  std::string sysfs_root = "/sys";
 };
+
+// CUs of KFD topology node `node` (simd_count / simd_per_cu of its properties
+// file), 0 when unreadable.
+uint32_t KfdTopologyCus(const std::string& topology_dir, uint32_t node);
+// <sysfs root>/bus/pci/devices/<bdf, function 0>/product_name, "" when absent.
+std::string PciProductName(const std::string& sysfs_root, const std::string& bdf);
 
 // Builds a snapshot from the loaded library (one enumeration + link queries).
 Result<std::shared_ptr<const Snapshot>> BuildSnapshot(smi::Library* lib, const BuildOptions& opt);

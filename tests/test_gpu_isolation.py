@@ -377,3 +377,46 @@ def test_images_on_the_real_gpu(scratch, snap, tmp_path):
     assert smi_mapped and all(p.startswith(rt) for p in smi_mapped), smi_mapped
     assert probe.returncode == 0 and result.get("checksum_ok"), result
     assert not outside, outside  # every shared object came from the images
+
+
+def test_kfd_topology_cus_match_asic_info(snap, tmp_path):
+    """The CU-count fallback on real hardware: KFD topology gives every GPU the
+    CU count asic_info does, and a daemon denied the render nodes (the chart's
+    drop-ALL container, through the device-cgroup simulator) still cuts 32
+    CU-slot units per SPX GPU."""
+    topo = "/sys/class/kfd/kfd/topology/nodes"
+    rows = []
+    for g in snap["gpus"]:
+        for p in g["partitions"]:
+            node = p.get("kfd_node")
+            rows.append({"bdf": g["bdf"], "partition": p.get("partition_id"), "kfd_node": node,
+                         "asic_info_cus": p.get("cus"),
+                         "topology_cus": native.kfd_topology_cus(topo, node) if node is not None else None})
+    # what else the node exposes without the render node (a market-name source, if any)
+    extra = {}
+    for g in snap["gpus"]:
+        for path in (f"/sys/bus/pci/devices/{g['bdf']}/product_name",
+                     f"{topo}/{g['partitions'][0].get('kfd_node')}/name"):
+            try:
+                with open(path) as f:
+                    extra[path] = f.read().strip()
+            except OSError as e:
+                extra[path] = f"unreadable: {e.strerror}"
+    env = {"LD_PRELOAD": " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), SIM) if x)}
+    r = subprocess.run([harness.DAEMON, "--device-plugin-path", str(tmp_path), "--dry-run", "--replica-cu-mask",
+                        "--resource-config", "gpu:gpu-mem-gb:-1"], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, **env))
+    dry = json.loads(r.stdout) if r.returncode == 0 else {"rc": r.returncode}
+    log = [ln for ln in r.stderr.splitlines() if "KFD topology" in ln or "CU" in ln]
+    _save("kfd_topology.json", {"rows": rows, "sysfs": extra, "denied_dry_run": dry, "denied_log": log})
+    assert all(x["topology_cus"] == x["asic_info_cus"] and x["topology_cus"] for x in rows), rows
+    assert r.returncode == 0, r.stderr[-2000:]
+    spx = [g for g in dry["gpus"] if g["partitions"] == 1]
+    assert all(g["cus"] == 256 for g in spx), dry["gpus"]
+    if spx and len(spx) == len(dry["gpus"]):
+        assert dry["resources"][0]["allocatable"] == 32 * len(spx), dry["resources"]
+    assert any("from KFD topology" in ln for ln in log), log
+    # the board's FRU name labels the node even without the render node
+    fru = [v for k, v in extra.items() if k.endswith("product_name") and not v.startswith("unreadable")]
+    if fru and fru[0]:
+        assert dry["labels"]["amd.com/gpu.product"] == "-".join(fru[0].split()), dry["labels"]
