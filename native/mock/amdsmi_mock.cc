@@ -35,7 +35,8 @@
 //               } ] }
 // Runtime injection:
 //   event FIFO lines: "<gpu>[:<partition>] <event-type> [message]",
-//                     "hang <ms>" (that event wait then returns only after <ms>)
+//                     "hang <ms>" (that event wait then returns only after <ms>),
+//                     "fail <n>" (the next n event waits fail)
 //   state_dir files:  gpu<i>.ecc (uncorrectable count; not a number = query fails),
 //                     gpu<i>.dead (device gone),
 //                     gpu<i>.partition ("CPX NPS2": live partition-mode override),
@@ -110,6 +111,7 @@ struct State {
   std::string event_fifo, state_dir;
   int fifo_fd = -1;
   std::string fifo_buf;
+  int fail_waits = 0;  // "fail <n>": the next n event waits fail
   std::vector<std::unique_ptr<MockProc>> procs;
   std::vector<MockGpu> gpus;
 };
@@ -690,6 +692,13 @@ amdsmi_status_t amdsmi_get_gpu_event_notification(int timeout_ms, uint32_t* num,
     *num = 0;
     return AMDSMI_STATUS_NO_DATA;
   }
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g && g->fail_waits > 0) {
+      --g->fail_waits;
+      return AMDSMI_STATUS_API_FAILED;
+    }
+  }
   pollfd pfd{fd, POLLIN, 0};
   int r = poll(&pfd, 1, timeout_ms);
   std::unique_lock<std::mutex> lk(g_mu);
@@ -711,6 +720,10 @@ amdsmi_status_t amdsmi_get_gpu_event_notification(int timeout_ms, uint32_t* num,
     if (!(ls >> target >> type)) continue;
     if (target == "hang") {  // fault injection: "hang <ms>" -- this wait does not return for that long
       hang_ms = type;
+      continue;
+    }
+    if (target == "fail") {  // "fail <n>": the next n waits return AMDSMI_STATUS_API_FAILED
+      g->fail_waits = type;
       continue;
     }
     std::string msg;

@@ -222,7 +222,10 @@ int PingRelay(const std::string& socket_path, int timeout_ms) {
   RelayLine l = ParseRelayLine(std::string_view(in).substr(0, nl));
   printf("%s\n", in.substr(0, nl).c_str());
   if (l.kind != "hello") return 1;
-  return l.reason.find("has not returned") != std::string::npos ? 1 : 0;
+  // a hung or failing event wait: a restart (amdsmi initialised afresh) is the fix
+  return l.reason.find("has not returned") != std::string::npos || l.reason.find("has failed for") != std::string::npos
+             ? 1
+             : 0;
 }
 
 int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_fd, const RelayOptions& opts) {
@@ -292,6 +295,7 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
   }
   std::atomic<bool> waiter_stop{false};
   std::atomic<int64_t> beat_ms{0};  // the waiter's last sign of life (steady clock)
+  std::atomic<int> wait_failures{0};  // consecutive failed waits
   auto now_ms = [] {
     return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
@@ -309,10 +313,13 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
         Status st = lib->EventsWait(100, &events);
         beat_ms.store(now_ms());
         if (!st.ok()) {
-          LOG_WARN(kComp, "event wait failed: %s", st.ToString().c_str());
+          int n = wait_failures.fetch_add(1) + 1;
+          if (n == 1 || n % 600 == 0)  // the first, then one a minute
+            LOG_WARN(kComp, "event wait failed (%d in a row): %s", n, st.ToString().c_str());
           usleep(100000);
           continue;
         }
+        wait_failures.store(0);
         for (const auto& e : events) {
           const smi::ProcessorInfo* p = nullptr;
           for (const auto& q : procs)
@@ -367,13 +374,19 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     if (poll(pfds.data(), pfds.size(), timeout) < 0 && errno != EINTR) break;
     if (waiter.joinable()) {
       int64_t silent = now_ms() - beat_ms.load();
-      if (!stuck && silent > kStuckMs) {
+      // A wait that keeps failing delivers no more events than one that hangs.
+      int64_t failing_ms = static_cast<int64_t>(wait_failures.load()) * 100;
+      if (!stuck && (silent > kStuckMs || failing_ms > kStuckMs)) {
         stuck = true;
         state_before_stuck = events_state;
-        events_state = "events=off reason=the amdsmi event wait has not returned for " + std::to_string(silent) + " ms";
+        events_state = silent > kStuckMs
+                           ? "events=off reason=the amdsmi event wait has not returned for " + std::to_string(silent) +
+                                 " ms"
+                           : "events=off reason=the amdsmi event wait has failed for " + std::to_string(failing_ms) +
+                                 " ms";
         LOG_ERROR(kComp, "%s: daemons fall back to polling", events_state.c_str());
         broadcast("hello v1 reinit " + events_state + "\n");
-      } else if (stuck && silent <= kStuckMs) {
+      } else if (stuck && silent <= kStuckMs && failing_ms <= kStuckMs) {
         stuck = false;
         events_state = state_before_stuck;
         LOG_INFO(kComp, "the amdsmi event wait returned again: events back on");
@@ -456,8 +469,9 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     }
     clients.erase(std::remove_if(clients.begin(), clients.end(), [](const Client& c) { return c.fd < 0; }),
                   clients.end());
+    const bool hung = waiter.joinable() && now_ms() - beat_ms.load() > kStuckMs;
     if (do_reinit) {
-      if (stuck) {
+      if (hung) {
         // amdsmi cannot be re-initialised under a wait that does not return:
         // the daemon gets the current (events off) state instead.
         LOG_WARN(kComp, "re-enumeration a daemon asked for skipped: the event wait is stuck");
@@ -472,8 +486,8 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
       broadcast("hello v1 reinit " + events_state + "\n");
     }
   }
-  if (stuck) {
-    // Joining would wait on the stuck call; the process is about to exit.
+  if (waiter.joinable() && now_ms() - beat_ms.load() > kStuckMs) {
+    // Joining would wait on the hung call; the process is about to exit.
     LOG_WARN(kComp, "exiting with the event wait still stuck");
     waiter.detach();
   } else {

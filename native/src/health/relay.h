@@ -15,8 +15,9 @@
 //                    "hello v1 events=off reason=<text>"       (registration failed)
 //                    "hello v1 reinit events=ok processors=<n>" (after a "reinit")
 //                    "hello v1 reinit events=off reason=..."   (watchdog: the amdsmi
-//                                 wait has not returned for ADP_RELAY_STUCK_MS,
-//                                 default 10 s; "events=ok" again once it does)
+//                                 wait has not returned, or has kept failing, for
+//                                 ADP_RELAY_STUCK_MS, default 10 s; "events=ok"
+//                                 again once waits succeed)
 //                    "event node=<kfd node|-> bdf=<bdf> part=<partition id> type=<t> <message>"
 //   daemon -> relay  "reinit"   re-enumerate (amdsmi_shut_down + init) and register
 //                               again, then a "reinit" hello to every client (a new

@@ -290,3 +290,32 @@ def test_relay_ping_is_the_relays_liveness(scratch, tmp_path):
         assert rc == 0 and "events=off" in out, out
     finally:
         denied.stop()
+
+
+def test_a_failing_event_wait_turns_events_off_too(scratch):
+    """An event wait that keeps failing (after a GPU reset amdsmi may answer
+    every wait with an error) delivers no events either: after
+    ADP_RELAY_STUCK_MS of failures the daemon is told events are off, the relay
+    ping fails (a restart re-initialises amdsmi), and a daemon's reinit is
+    still served; once the waits succeed, events are on again."""
+    import subprocess
+    n = RelayNode(scratch, relay_env={"ADP_RELAY_STUCK_MS": "500"})
+    try:
+        n.d.wait_log("events on through the relay")
+        n.inject("fail 30")  # ~3 s of failed waits (the relay retries every 100 ms)
+        n.relay.wait_log("the amdsmi event wait has failed for")
+        deadline = time.time() + 5
+        while _value(n.metrics(), "amdgpu_dp_health_events_enabled") != 0:
+            assert time.time() < deadline
+            time.sleep(0.05)
+        r = subprocess.run([harness.DAEMON, "--relay-ping", "--health-event-socket", n.sock], capture_output=True,
+                           text=True, timeout=30)
+        assert r.returncode == 1 and "has failed for" in r.stdout, r.stdout
+        n.relay.wait_log("the amdsmi event wait returned again", timeout=10)
+        deadline = time.time() + 5
+        while _value(n.metrics(), "amdgpu_dp_health_events_enabled") != 1:
+            assert time.time() < deadline
+            time.sleep(0.05)
+        assert "event wait failed (1 in a row)" in n.relay.log()
+    finally:
+        n.stop()
