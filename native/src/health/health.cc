@@ -72,6 +72,10 @@ HealthConfig HealthConfig::FromEnv() {
     if (n && *n >= -1) c.max_retired_pages = *n;
     else LOG_WARN(kComp, "ignoring DP_MAX_RETIRED_PAGES=%s (want -1, 0 or a page count)", v);
   }
+  if (const char* v = std::getenv("ADP_EVENT_FAIL_MS"); v && *v) {
+    auto n = ParseInt(v);
+    if (n && *n > 0 && *n < 86400000) c.event_fail_ms = static_cast<int>(*n);
+  }
   return c;
 }
 
@@ -641,8 +645,26 @@ void Monitor::Run() {
       events.clear();
       Status st = lib_->EventsWait(slice, &events);
       if (!st.ok()) {
-        LOG_WARN(kComp, "event wait failed: %s", st.ToString().c_str());
+        if (wait_failures_++ == 0) wait_failing_since_ms_ = NowMs();
+        if (wait_failures_ == 1 || wait_failures_ % 600 == 0)  // the first, then about one a minute
+          LOG_WARN(kComp, "event wait failed (%llu in a row): %s", static_cast<unsigned long long>(wait_failures_),
+                   st.ToString().c_str());
+        // Waits that keep failing deliver no events: say so (the metric, the
+        // relay-less equivalent of the relay's watchdog) and keep trying.
+        if (!events_failing_ && NowMs() - wait_failing_since_ms_ > cfg_.event_fail_ms) {
+          events_failing_ = true;
+          counters_->events_enabled.store(0);
+          LOG_ERROR(kComp, "amdsmi event waits have failed for %lld ms: events off, polling only until they succeed",
+                    static_cast<long long>(NowMs() - wait_failing_since_ms_));
+        }
         Sleep(slice);
+      } else if (wait_failures_) {
+        wait_failures_ = 0;
+        if (events_failing_) {
+          events_failing_ = false;
+          counters_->events_enabled.store(1);
+          LOG_INFO(kComp, "amdsmi event waits succeed again: events on");
+        }
       }
     } else {
       events.clear();

@@ -65,6 +65,10 @@ struct HealthConfig {
   // -1 = the driver's own threshold when amdsmi can read it (root), else off;
   // 0 = off; N = N pages.
   int64_t max_retired_pages = -1;
+  // In-process events: how long amdsmi event waits may keep failing before
+  // events count as off (ADP_EVENT_FAIL_MS; the event relay's watchdog is
+  // ADP_RELAY_STUCK_MS).
+  int event_fail_ms = 10000;
   // amdsmi event notification (--health-events); off = polling only.
   bool events = true;
   // Where /dev/kfd is (--driver-root): why event registration failed.
@@ -206,6 +210,11 @@ class Monitor {
   std::string relay_buf_;
   bool relay_synced_ = false;  // the relay answered this connection's "reinit"
   int64_t relay_tried_ms_ = -1000000;
+  // In-process event waits that keep failing: since when, how many, and
+  // whether events are reported off because of it.
+  int64_t wait_failing_since_ms_ = 0;
+  uint64_t wait_failures_ = 0;
+  bool events_failing_ = false;
   void RelayConnect();
   void RelayClose(const std::string& why);
   // Reads relay lines for up to `ms`: hellos update events_ok_, events are

@@ -264,3 +264,33 @@ def test_healthz_fails_while_the_health_loop_is_stuck(scratch):
             time.sleep(0.05)
     finally:
         n.close()
+
+
+def test_failing_event_waits_report_events_off_until_they_succeed(scratch):
+    """In-process events: amdsmi event waits that keep failing (the mock's
+    "fail <n>") deliver nothing, so after ADP_EVENT_FAIL_MS the daemon reports
+    events off (amdgpu_dp_health_events_enabled 0) and logs it once, not every
+    100 ms; when waits succeed again events are on and reset events work."""
+    import re
+    from test_metrics import _get, _parse, _value
+    n = Node(scratch, dict(fixtures.node(2), events_open_kfd=True), args=["--metrics-addr", "127.0.0.1:0"],
+             env={"ADP_EVENT_FAIL_MS": "300"})
+    try:
+        port = int(re.search(r"on port (\d+)", n.d.wait_log("serving /metrics")).group(1))
+
+        def enabled():
+            return _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_health_events_enabled")
+        assert enabled() == 1
+        n.inject("fail 20")
+        deadline = time.time() + 5
+        while enabled() != 0:
+            assert time.time() < deadline
+            time.sleep(0.05)
+        assert "events off, polling only until they succeed" in n.d.log()
+        n.d.wait_log("amdsmi event waits succeed again: events on", timeout=10)
+        assert enabled() == 1
+        assert n.d.log().count("event wait failed (") == 1  # rate-limited
+        n.inject("1 3 mode1 reset")
+        assert [x.health for x in n.next().devices] == ["Healthy", "Unhealthy"]
+    finally:
+        n.close()
