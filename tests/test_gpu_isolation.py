@@ -246,10 +246,16 @@ def test_driver_scan_reads_the_gpu_processes_kfd_lists(tmp_path):
 
 
 def test_driver_scan_through_the_relay(scratch, snap, tmp_path):
-    """The chart's layout: the relay (real libamd_smi, the host's /proc) runs
-    the driver-side scans; the daemon is denied the GPU device nodes and given
-    a --host-proc that does not exist, so every byte it reports came through
-    the relay. A HIP process holding 1 GiB shows on /metrics."""
+    """The chart's layout, every feature at once: the daemon is denied the GPU
+    device nodes (an unprivileged pod's device cgroup, through the simulator)
+    and given a --host-proc that does not exist; the relay (real libamd_smi,
+    the host's /proc) holds the events and runs the driver-side scans.
+    - a HIP process holding 1 GiB shows on /metrics (the relay's scan);
+    - health events are on through the relay;
+    - --replica-cu-mask still cuts CU-slot units (CU counts from KFD topology):
+      a 4-unit pod gets HSA_CU_MASK 0:0-31 and 4 slots' HBM;
+    - the node label names the product (the board's PCI product_name);
+    - /healthz answers 200."""
     from test_metrics import _get, _parse
     sock = str(tmp_path / "events.sock")
     rdir = scratch + "-relay"
@@ -266,9 +272,20 @@ def test_driver_scan_through_the_relay(scratch, snap, tmp_path):
             "--devices", "0", "--health-event-socket", sock, "--metrics-addr", "127.0.0.1:0",
             "--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units", "--memcap-lib",
             os.path.join(BUILD_DIR, "libadp_memcap.so"), "--host-proc",
-            str(tmp_path / "nosuch"), "--driver-hbm-poll-ms", "200"]).start()
+            str(tmp_path / "nosuch"), "--driver-hbm-poll-ms", "200", "--replica-cu-mask",
+            "--node-labels-file", str(tmp_path / "labels")]).start()
         port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics", 30)).group(1))
-        k.wait_registration(30)
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        free = [x.ID for x in c.watch()[0].get(timeout=10).devices]
+        pod = list(c.preferred(free, size=4).container_responses[0].deviceIDs)
+        envs = dict(c.allocate(pod).container_responses[0].envs)
+        c.close()
+        layout = {"units": len(free), "hsa_cu_mask": envs.get("HSA_CU_MASK"),
+                  "limit_mib": envs.get("AMD_GPU_MEMORY_LIMIT_MIB"),
+                  "labels": open(str(tmp_path / "labels")).read().splitlines(),
+                  "healthz": _get(port, "/healthz")[0],
+                  "events": "events on through the relay" in d.wait_log("events on through the relay", 30)}
         bdf = snap["gpus"][0]["bdf"]
         def get(samples, name, **labels):  # None until the first scan has run
             want = set(labels.items())
@@ -287,12 +304,19 @@ def test_driver_scan_through_the_relay(scratch, snap, tmp_path):
                                      if n == "amdgpu_dp_driver_hbm_scan_processes"},
                   "scan_seconds": get(m, "amdgpu_dp_driver_hbm_scan_seconds"),
                   "driver_metric_lines": [ln for ln in text.splitlines() if "driver" in ln and not ln.startswith("#")],
-                  "daemon_log": [ln for ln in d.log().splitlines() if "driver-hbm" in ln][:4],
-                  "relay_log": [ln for ln in relay.log().splitlines() if "scan" in ln][:4]}
+                  "daemon_log": [ln for ln in d.log().splitlines() if "driver-hbm" in ln or "inventory" in ln][:8],
+                  "relay_log": [ln for ln in relay.log().splitlines() if "scan" in ln][:4], "layout": layout}
         _save("driver_scan_relay.json", record)
         assert (held or 0) >= 1 << 30, record
         assert record["scan_failures"] == 0, record
         assert "first HBM scan for a daemon" in relay.log()
+        if not snap["gpus"][0]["partitioned"]:
+            unit = snap["gpus"][0]["vram_mib"] // 32
+            assert layout["units"] == 32 and layout["hsa_cu_mask"] == "0:0-31", layout
+            assert layout["limit_mib"] == str(4 * unit), layout
+        assert layout["healthz"] == 200 and layout["events"], layout
+        product = [ln for ln in layout["labels"] if ln.startswith("amd.com/gpu.product=")]
+        assert product and product[0] != "amd.com/gpu.product=", layout["labels"]
     finally:
         if holder:
             holder.stdin.close()
