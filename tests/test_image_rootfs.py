@@ -70,6 +70,11 @@ def test_entrypoint_runs_in_the_image(rootfs):
                        capture_output=True, text=True, timeout=60)
     out = r.stdout + r.stderr
     assert "cannot open shared object" not in out and "libamd_smi" in out, out[-2000:]
+    # the event relay's liveness probe (the chart's exec command) runs in the image and loads no amdsmi
+    r = subprocess.run(image.chroot_cmd(d, ["/usr/bin/amdgpu-device-plugin", "--relay-ping", "--health-event-socket",
+                                            "/run/amdgpu-dp-events/events.sock"]),
+                       capture_output=True, text=True, timeout=30)
+    assert r.returncode == 1 and "not reachable" in r.stdout and "loading amdsmi" not in r.stderr, r.stdout + r.stderr
 
 
 def test_image_serves_a_kubelet(rootfs):
