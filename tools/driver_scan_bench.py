@@ -7,6 +7,10 @@ Times the scan reading only KFD's processes against the full walk of every
 process, for several N, and checks both attribute the same HBM.
 
   python tools/driver_scan_bench.py --others 1000,10000 --fds 100 --out profiles/r4/driver_scan/scan_cost.json
+
+--relay also times the same scans asked of an event relay (--event-relay on the
+mock, the chart's layout): connect, greeting, request, the serialized reply,
+close -- what one poll of a daemon with --health-event-socket costs.
 """
 
 import argparse
@@ -50,6 +54,43 @@ def build(root, others, fds):
             os.symlink(f"socket:[{n * fds + fd}]" if fd % 2 else "/var/log/app.log", os.path.join(fd_dir, str(fd)))
 
 
+def relay_scan(sock):
+    """One scan through the relay's socket, as memcap::RemoteScan asks it: (us, reply header)."""
+    import socket
+    t = time.perf_counter()
+    c = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    c.connect(sock)
+    c.sendall(b"scan\t/nonexistent/usage\t0::/bench\n")
+    data = b""
+    while True:
+        chunk = c.recv(1 << 16)
+        if not chunk:
+            break
+        data += chunk
+    c.close()
+    us = (time.perf_counter() - t) * 1e6
+    header = next(ln for ln in data.decode().splitlines() if ln.startswith("scan\t")).split("\t")
+    return us, {"source": header[1], "pids": int(header[2]), "fds": int(header[3]), "rows": int(header[5]),
+                "reply_bytes": len(data)}
+
+
+def timed_relay(proc, kfd, reps, tmp):
+    from k8s_gpu_sharing_plugin_amd.models import fixtures
+    from k8s_gpu_sharing_plugin_amd.utils import harness
+    sock = os.path.join(tmp, "relay.sock")
+    r = harness.Daemon(os.path.join(tmp, "relay"), fixtures.node(1), env={"ADP_LOG_LEVEL": "warn"}, args=[
+        "--event-relay", "--health-event-socket", sock, "--host-proc", proc, "--kfd-proc-dir", kfd]).start()
+    try:
+        deadline = time.time() + 30
+        while not os.path.exists(sock):
+            assert time.time() < deadline, r.log()[-2000:]
+            time.sleep(0.02)
+        runs = [relay_scan(sock) for _ in range(reps)]
+    finally:
+        r.stop()
+    return runs[-1][1], statistics.median(u for u, _ in runs)
+
+
 def timed(proc, kfd, reps):
     runs = [native.driver_scan(proc, kfd_proc_dir=kfd) for _ in range(reps)]
     return runs[-1], statistics.median(r["scan_us"] for r in runs)
@@ -61,6 +102,7 @@ def main():
     ap.add_argument("--fds", type=int, default=100)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default="")
+    ap.add_argument("--relay", action="store_true", help="also time the scans through an event relay")
     a = ap.parse_args()
     rows = []
     for others in [int(x) for x in a.others.split(",")]:
@@ -79,11 +121,17 @@ def main():
                    "full_walk": {"pids": full["pids_scanned"], "fds": full["fd_entries"],
                                  "scan_us_p50": round(full_us, 1)},
                    "same_attribution": same, "hbm_total": fast["total"], "build_s": round(built_s, 1)}
+            if a.relay:
+                rk, rk_us = timed_relay(proc, kfd, a.reps, root)
+                rf, rf_us = timed_relay(proc, "", max(1, a.reps // 2), root)
+                row["relay"] = {"kfd": dict(rk, round_trip_us_p50=round(rk_us, 1)),
+                                "full_walk": dict(rf, round_trip_us_p50=round(rf_us, 1))}
             rows.append(row)
             print(json.dumps(row), flush=True)
         finally:
             shutil.rmtree(root, ignore_errors=True)
-    out = {"what": "memcap::ScanDriverHbm on a synthetic /proc (tmpfs), KFD GPU-process list vs full walk",
+    out = {"what": "memcap::ScanDriverHbm on a synthetic /proc (tmpfs), KFD GPU-process list vs full walk"
+                   + (", in process and through an event relay (round trip: connect to close)" if a.relay else ""),
            "host": os.uname().nodename, "rows": rows}
     if a.out:
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
