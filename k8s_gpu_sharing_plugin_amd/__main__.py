@@ -151,6 +151,21 @@ def _status(args) -> int:
               f"{int(one('amdgpu_dp_allocatable')):>11} {'yes' if one('amdgpu_dp_registered') else 'no':>10} "
               f"{int(one('amdgpu_dp_rpc_total', {'method': 'Allocate'})):>9} "
               f"{int(one('amdgpu_dp_rpc_total', {'method': 'GetPreferredAllocation'})):>9} {resid:>21}")
+    def scalar(name):
+        got = by(name)
+        return got[0][1] if got else None
+    ev = scalar("amdgpu_dp_health_events_enabled")
+    age = scalar("amdgpu_dp_health_loop_age_seconds")
+    line = "health: events " + {1: "on", 0: "off (polling)", -1: "not started", None: "?"}.get(
+        None if ev is None else int(ev), "?")
+    if age is not None:
+        line += f", monitor loop {age:.1f} s ago"
+    polls = scalar("amdgpu_dp_driver_hbm_polls_total")
+    if polls is not None:
+        failures = scalar("amdgpu_dp_driver_hbm_scan_failures_total") or 0
+        secs = scalar("amdgpu_dp_driver_hbm_scan_seconds") or 0
+        line += f"; driver-side scans {int(polls)} (last {secs * 1e3:.2f} ms, {int(failures)} failed)"
+    print(line)
     bad = [ls for ls, v in by("amdgpu_dp_device_healthy") if v == 0]
     for ls in bad:
         print(f"UNHEALTHY {ls.get('resource')} {ls.get('device')} (index {ls.get('index')})")

@@ -503,6 +503,8 @@ def test_status_cli_reads_metrics(served):
     cols = line.split()
     assert cols[1:5] == ["2", "2", "6", "yes"] and int(cols[5]) == 3, line
     assert re.search(r"\d+\.\d / \d+\.\d$", line), line  # residency p50 / p99 at 100 ns (from /stats)
+    health = next(ln for ln in r.stdout.splitlines() if ln.startswith("health: "))
+    assert re.match(r"health: events (on|off \(polling\)), monitor loop \d+\.\d s ago", health), health
     fd = os.open(fifo, os.O_WRONLY | os.O_NONBLOCK)
     os.write(fd, b"1 3 pre-reset\n")
     os.close(fd)
