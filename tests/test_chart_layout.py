@@ -110,3 +110,24 @@ def test_the_default_pod_with_an_unprivileged_plugin(scratch, tmp_path):
         d.stop()
         k.stop()
         relay.stop()
+
+
+def test_doctor_in_the_plugin_container(scratch, tmp_path):
+    """--doctor run where the chart runs the plugin (denied device nodes, the
+    relay next to it): the denial is the expected state, not a warning."""
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import DAEMON, MOCK_LIB
+    from test_doctor import _find
+    from test_event_relay import RelayNode
+    n = RelayNode(scratch)
+    try:
+        env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB, LD_PRELOAD=_preload(SIM),
+                   AMDSMI_MOCK_FIXTURE=fixtures.write(n.fx, str(tmp_path / "fx")))
+        r = subprocess.run([DAEMON, "--doctor", "--device-plugin-path", scratch, "--health-event-socket", n.sock],
+                           capture_output=True, text=True, timeout=60, env=env)
+        lines = r.stdout.splitlines()
+        line = _find(lines, "device nodes:")
+        assert line.startswith("ok") and "as expected for the unprivileged plugin" in line, lines
+        assert _find(lines, "health events:").startswith("ok")
+    finally:
+        n.stop()
