@@ -146,6 +146,22 @@ int SmiReport(smi::Library* lib, const Validated& v, const Config& cfg) {
              std::to_string(access[i].err) + ", \"error\": \"" + (access[i].err ? strerror(access[i].err) : "") +
              "\"}";
   }
+  // What sysfs answers without the render node: KFD topology CUs and the
+  // board's PCI product name, per processor (the fallbacks for asic_info).
+  out += "], \"sysfs\": [";
+  if (snap.ok() && !cfg.flags.sysfs_root.empty()) {
+    const std::string topo = cfg.flags.sysfs_root + "/class/kfd/kfd/topology/nodes";
+    bool first = true;
+    for (const auto& p : (*snap)->procs) {
+      out += std::string(first ? "" : ", ") + "{\"bdf\": \"" + JsonEscape(p.bdf) + "\", \"kfd_node\": " +
+             (p.kfd_node == inventory::kNoKfdNode ? std::string("null") : std::to_string(p.kfd_node)) +
+             ", \"topology_cus\": " +
+             std::to_string(p.kfd_node == inventory::kNoKfdNode ? 0 : inventory::KfdTopologyCus(topo, p.kfd_node)) +
+             ", \"pci_product_name\": \"" + JsonEscape(inventory::PciProductName(cfg.flags.sysfs_root, p.bdf)) +
+             "\"}";
+      first = false;
+    }
+  }
   out += "], \"enumeration\": \"" + std::string(snap.ok() ? "ok" : JsonEscape(snap.status().ToString())) + "\"}";
   printf("%s\n", out.c_str());
   fflush(stdout);

@@ -118,3 +118,18 @@ def test_doctor_names_the_cu_count_source(tmp_path):
     assert rc == 1 and line.startswith("FAIL") and "no CU shares" in line, lines
     _, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), fx=fixtures.node(1))
     assert _find(lines, "CU counts:") is None  # asic_info answered: nothing to say
+
+
+def test_smi_report_lists_the_sysfs_fallbacks(tmp_path):
+    sysfs = _topology(str(tmp_path / "sys"), {2: 256})
+    fx = fixtures.node(1)
+    d = os.path.join(sysfs, "bus/pci/devices", fx["gpus"][0]["bdf"])
+    os.makedirs(d)
+    with open(os.path.join(d, "product_name"), "w") as f:
+        f.write("AMD Instinct MI355 OAM\n")
+    env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB, AMDSMI_MOCK_FIXTURE=fixtures.write(fx, str(tmp_path / "fx")))
+    r = subprocess.run([harness.DAEMON, "--device-plugin-path", str(tmp_path), "--smi-report", "--sysfs-root", sysfs],
+                       capture_output=True, text=True, timeout=60, env=env)
+    rep = json.loads(r.stdout)
+    assert rep["sysfs"] == [{"bdf": fx["gpus"][0]["bdf"], "kfd_node": 2, "topology_cus": 256,
+                             "pci_product_name": "AMD Instinct MI355 OAM"}], rep["sysfs"]
