@@ -79,6 +79,9 @@ def test_the_default_pod_with_an_unprivileged_plugin(scratch, tmp_path):
         assert "CU counts of 2 processor(s) from KFD topology" in log
         # a process of this pod's container holding more than its 4 slots' HBM (around the shim)
         host = [m.host_path for m in r.mounts if m.container_path == "/run/amdgpu-dp/memcap"][0]
+        deadline = time.time() + 5
+        while not os.path.isfile(host) and time.time() < deadline:  # written just after Allocate() answers
+            time.sleep(0.01)
         key = os.path.basename(host).split(".")[0]
         proc.process(701, "0::/kubepods/pod-x/ctr", vram_mib=1000, maps_file=host)
         proc.process(702, "0::/kubepods/pod-x/ctr", vram_mib=4 * unit)

@@ -358,6 +358,9 @@ def test_scan_runs_in_the_event_relay(scratch, tmp_path):
         resp = c.allocate(ids[:3]).container_responses[0]
         c.close()
         host = [m.host_path for m in resp.mounts if m.container_path == "/run/amdgpu-dp/memcap"][0]
+        deadline = time.time() + 5
+        while not os.path.isfile(host) and time.time() < deadline:  # written just after Allocate() answers
+            time.sleep(0.01)
         key = os.path.basename(host).split(".")[0]
         ctr = "0::/kubepods/pod-r/ctr"
         proc.process(601, ctr, vram_mib=1000, maps_file=host)
