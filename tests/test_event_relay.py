@@ -319,3 +319,41 @@ def test_a_failing_event_wait_turns_events_off_too(scratch):
         assert "event wait failed (1 in a row)" in n.relay.log()
     finally:
         n.stop()
+
+
+def test_relay_keeps_no_descriptor_per_scan(scratch, tmp_path):
+    """Hundreds of scan connections (one per daemon poll in production), some
+    dropped before the reply: the relay's open descriptors and threads do not
+    grow."""
+    import socket as so
+    sock = str(tmp_path / "events.sock")
+    fx = dict(fixtures.node(1), events_open_kfd=True)
+    os.makedirs(str(tmp_path / "proc"))
+    relay = harness.Daemon(scratch + "-relay", fx, args=["--event-relay", "--health-event-socket", sock,
+                                                         "--host-proc", str(tmp_path / "proc")]).start()
+
+    def counts():
+        pid = relay.proc.pid
+        threads = int([ln for ln in open(f"/proc/{pid}/status") if ln.startswith("Threads:")][0].split()[1])
+        return len(os.listdir(f"/proc/{pid}/fd")), threads
+
+    def scan(read_reply):
+        c = so.socket(so.AF_UNIX, so.SOCK_STREAM)
+        c.settimeout(10)
+        c.connect(sock)
+        c.sendall(f"scan\t{tmp_path}/usage\t0::/x\n".encode())
+        if read_reply:
+            while c.recv(65536):
+                pass
+        c.close()
+    try:
+        relay.wait_log("relaying amdsmi events on")
+        scan(True)
+        before = counts()
+        for i in range(400):
+            scan(i % 4 != 0)  # every 4th client hangs up without reading
+        time.sleep(0.3)
+        after = counts()
+        assert after[0] <= before[0] + 2 and after[1] == before[1], (before, after)
+    finally:
+        relay.stop()
