@@ -168,6 +168,11 @@ const std::vector<FlagDef>& Table() {
        "KFD's list of GPU processes (host PIDs) for the driver-side HBM check: only those processes' "
        "descriptors are read, not every process's (empty = always walk every process under --host-proc)",
        [](Flags& f) -> void* { return &f.kfd_proc_dir; }},
+      {"drain-file", "DP_DRAIN_FILE", "drainFile", Kind::kString,
+       "operator drain list: every GPU named in this file (PCI address, UUID, partition UUID or node index; "
+       "whitespace or comma separated, '#' comments) is advertised Unhealthy until it is removed from the file "
+       "(read when the health monitor starts and at every poll; a reset does not clear it; empty = off)",
+       [](Flags& f) -> void* { return &f.drain_file; }},
       {"sysfs-root", "DP_SYSFS_ROOT", "sysfsRoot", Kind::kString,
        "where sysfs is mounted: without the render node (an unprivileged pod's device cgroup denies it) "
        "amdsmi's asic_info fails, and the CU count comes from <root>/class/kfd/kfd/topology and the product "

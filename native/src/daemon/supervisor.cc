@@ -294,8 +294,9 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   // Driver-side check of enforced HBM grants (--driver-hbm-poll-ms): started
   // with the first generation that enforces grants into an accounting dir.
   std::unique_ptr<memcap::DriverHbmMonitor> driver_hbm;
-  std::mutex access_mu;  // node_access: written by restart, read by /metrics
+  std::mutex access_mu;  // node_access, metrics_gpus: written by restart, read by /metrics
   std::vector<inventory::NodeAccess> node_access;
+  std::vector<std::pair<std::string, std::string>> metrics_gpus;  // (ledger key, bdf) of the served GPUs
   const std::string usage_dir = PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage");  // startup-only flag
   std::unique_ptr<metrics::HttpServer> http;
   std::unique_ptr<podresources::CachedLister> pod_lister;
@@ -346,6 +347,21 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
               std::to_string(health_counters.retired_read_errors.load()) + "\n";
           {
             std::lock_guard<std::mutex> lk(access_mu);
+            // Why a GPU is Unhealthy, one series per failure cause (the ledger's bits).
+            static const std::pair<uint32_t, const char*> kCauses[] = {
+                {health::kFailEcc, "ecc"},           {health::kFailUnresponsive, "unresponsive"},
+                {health::kFailResetPending, "reset_pending"}, {health::kFailEvent, "event"},
+                {health::kFailRetiredPages, "retired_pages"}, {health::kFailDrained, "drained"}};
+            if (!metrics_gpus.empty())
+              out += "# HELP amdgpu_dp_gpu_failure 1 while the GPU is Unhealthy for this cause (drained: the "
+                     "operator's drain file, not a fault).\n"
+                     "# TYPE amdgpu_dp_gpu_failure gauge\n";
+            for (const auto& [key, bdf] : metrics_gpus) {
+              uint32_t bits = ledger.Get(key).fail;
+              for (const auto& [bit, cause] : kCauses)
+                out += "amdgpu_dp_gpu_failure{bdf=\"" + metrics::LabelValue(bdf) + "\",cause=\"" + cause + "\"} " +
+                       ((bits & bit) ? "1" : "0") + "\n";
+            }
             if (!node_access.empty())
               out += "# HELP amdgpu_dp_device_node_openable 1 if the plugin can open the device node (0: denied, "
                      "e.g. by the container's device cgroup).\n"
@@ -583,6 +599,8 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
       else LOG_WARN(kComp, "device access: %s", what.c_str());
       std::lock_guard<std::mutex> lk(access_mu);
       node_access = std::move(access);
+      metrics_gpus.clear();
+      for (const auto& g : (*snap)->gpus) metrics_gpus.emplace_back(health::Ledger::KeyOf(g), g.bdf);
     }
     auto specs = strategy::BuildPluginSpecs(**snap, v.partition, v.rc, cfg.flags.resource_prefix);
     if (!specs.ok()) {
@@ -627,6 +645,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     }
     health::HealthConfig hcfg = health::HealthConfig::FromEnv();
     hcfg.events = cfg.flags.health_events;
+    hcfg.drain_file = cfg.flags.drain_file;
     hcfg.driver_root = cfg.flags.driver_root;
     hcfg.event_relay = cfg.flags.health_event_socket;
     publish_plugins(*snap, *specs, !hcfg.disabled);

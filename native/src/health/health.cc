@@ -1,5 +1,6 @@
 #include "health/health.h"
 
+#include <fcntl.h>
 #include <poll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -12,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <set>
 #include <sstream>
 
 #include "common/log.h"
@@ -375,6 +377,7 @@ Status Monitor::Start() {
       Notify(g.index, false, r.reason);
     }
   }
+  if (!cfg_.drain_file.empty()) ApplyDrain();  // at once, not a poll interval later
   LOG_INFO(kComp, "health monitor watching %zu GPU(s) (events %s, poll every %d ms)", snap_->gpus.size(),
            events_ok_ ? "on" : relay_fd_ >= 0 ? "through the relay, once it answers" : "off", cfg_.poll_interval_ms);
   if (!events_ok_ && cfg_.poll_interval_ms == 0 && (cfg_.event_relay.empty() || !cfg_.events)) return Status::Ok();
@@ -483,8 +486,45 @@ void Monitor::RelayWait(int ms, std::vector<smi::Event>* out) {
   if (closed) RelayClose("the event relay closed the connection");
 }
 
+void Monitor::ApplyDrain() {
+  std::string text;
+  int fd = open(cfg_.drain_file.c_str(), O_RDONLY | O_CLOEXEC | O_NONBLOCK);
+  if (fd >= 0) {
+    char buf[4096];
+    ssize_t n;
+    while ((n = read(fd, buf, sizeof(buf))) > 0 && text.size() < 65536) text.append(buf, static_cast<size_t>(n));
+    close(fd);
+  }  // absent or unreadable: nothing drained
+  std::set<std::string> names;
+  for (size_t b = 0; b < text.size();) {
+    size_t e = text.find('\n', b);
+    if (e == std::string::npos) e = text.size();
+    std::string line = text.substr(b, e - b);
+    b = e + 1;
+    if (size_t hash = line.find('#'); hash != std::string::npos) line.resize(hash);
+    for (char& c : line)
+      if (c == ',' || c == '\t' || c == '\r') c = ' ';
+    for (size_t p = 0; p < line.size();) {
+      size_t q = line.find(' ', p);
+      if (q == std::string::npos) q = line.size();
+      if (q > p) names.insert(line.substr(p, q - p));
+      p = q + 1;
+    }
+  }
+  for (const auto& g : snap_->gpus) {
+    bool drained = names.count(g.uuid) || names.count(g.bdf) || names.count(std::to_string(g.node_index));
+    // a PCI address without the function, and partition UUIDs, name the GPU too
+    if (!drained && g.bdf.size() > 2) drained = names.count(g.bdf.substr(0, g.bdf.rfind('.')));
+    for (const auto& p : g.partitions) drained = drained || names.count(p.uuid);
+    bool was = fail_[g.index] & kFailDrained;
+    if (drained && !was) Update(g.index, kFailDrained, 0, "drained by the operator (" + cfg_.drain_file + ")");
+    if (!drained && was) Update(g.index, 0, kFailDrained, "removed from the drain file");
+  }
+}
+
 void Monitor::PollOnce() {
   uint64_t poll = counters_->polls.fetch_add(1) + 1;
+  if (!cfg_.drain_file.empty()) ApplyDrain();
   size_t answered = 0, ecc_ok = 0, retired_ok = 0;
   std::string counts;
   for (const auto& g : snap_->gpus) {
@@ -699,7 +739,7 @@ void Monitor::Run() {
             ledger_->Put(keys_[gpu], r);
           }
           if (fail_[gpu] == 0) Notify(gpu, true, why);  // keep the reference's idempotent notify
-          Update(gpu, 0, ~0u, why);
+          Update(gpu, 0, ~static_cast<uint32_t>(kFailDrained), why);  // a drain outlives a reset
         } else {
           Update(gpu, e.type == smi::kEvtGpuPreReset ? kFailResetPending : kFailEvent, 0, why);
         }

@@ -76,6 +76,10 @@ struct HealthConfig {
   // --health-event-socket: events come from the privileged relay (relay.h) at
   // this Unix socket instead of an in-process amdsmi registration ("" = in-process).
   std::string event_relay;
+  // Operator drain list (--drain-file): GPUs named in it (PCI address, UUID,
+  // partition UUID or node index; one or more per line, '#' comments) are
+  // advertised Unhealthy until removed. Read at every poll.
+  std::string drain_file;
   static HealthConfig FromEnv();
   static HealthConfig FromValues(const char* disable_value, const char* poll_ms_value);
 };
@@ -89,6 +93,7 @@ enum FailBits : uint32_t {
   kFailResetPending = 1u << 2,  // GPU_PRE_RESET without a GPU_POST_RESET yet
   kFailEvent = 1u << 3,         // any other non-ignored amdsmi event
   kFailRetiredPages = 1u << 4,  // retired HBM pages reached the threshold
+  kFailDrained = 1u << 5,       // listed in the operator's drain file (not a fault; cleared by removal only)
 };
 
 struct GpuRecord {
@@ -197,6 +202,8 @@ class Monitor {
   // Sets/clears failure bits of a GPU, records them in the ledger and notifies
   // listeners when the GPU's overall health flips.
   void Update(int gpu, uint32_t set, uint32_t clear, const std::string& reason);
+  // Applies the drain file to every GPU (PollOnce).
+  void ApplyDrain();
 
   smi::Library* lib_;
   std::shared_ptr<const inventory::Snapshot> snap_;

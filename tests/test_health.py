@@ -294,3 +294,49 @@ def test_failing_event_waits_report_events_off_until_they_succeed(scratch):
         assert [x.health for x in n.next().devices] == ["Healthy", "Unhealthy"]
     finally:
         n.close()
+
+
+def test_operator_drain_file(scratch, tmp_path):
+    """--drain-file: a GPU named in it (PCI address, UUID, node index; '#'
+    comments) is advertised Unhealthy -- every replica of it -- until removed;
+    a GPU_POST_RESET does not undo a drain."""
+    import queue
+    drain = tmp_path / "drain"
+    fx = dict(fixtures.node(2), events_open_kfd=True)
+    n = Node(scratch, fx, args=["--resource-config", "gpu:sharedgpu:2", "--drain-file", str(drain),
+                                "--metrics-addr", "127.0.0.1:0"], env={"DP_HEALTH_POLL_MS": "100"})
+    try:
+        last = [x.health for x in n.first.devices]
+
+        def until(want, timeout=5):
+            nonlocal last
+            deadline = time.time() + timeout
+            while last != want and time.time() < deadline:
+                try:
+                    last = [x.health for x in n.q.get(timeout=0.2).devices]
+                except queue.Empty:
+                    pass
+            return last
+        drain.write_text(f"# maintenance\n{fx['gpus'][1]['bdf']}  # bad fan\n")
+        assert until(["Healthy", "Healthy", "Unhealthy", "Unhealthy"]) == ["Healthy", "Healthy", "Unhealthy",
+                                                                          "Unhealthy"]
+        assert "drained by the operator" in n.d.wait_log("drained by the operator")
+        import re
+        from test_metrics import _get, _parse, _value
+        port = int(re.search(r"on port (\d+)", n.d.log()).group(1))
+        m = _parse(_get(port, "/metrics")[1])
+        bdf1 = fx["gpus"][1]["bdf"]
+        assert _value(m, "amdgpu_dp_gpu_failure", bdf=bdf1, cause="drained") == 1
+        assert _value(m, "amdgpu_dp_gpu_failure", bdf=bdf1, cause="ecc") == 0
+        assert _value(m, "amdgpu_dp_gpu_failure", bdf=fx["gpus"][0]["bdf"], cause="drained") == 0
+        n.inject("1 4 reset done")  # a post-reset clears faults, not a drain
+        n.d.wait_log("GPU_POST_RESET")
+        time.sleep(0.4)
+        assert until(["Healthy"] * 4, timeout=0.5) == ["Healthy", "Healthy", "Unhealthy", "Unhealthy"]
+        drain.write_text("0\n")  # node index 0 instead
+        assert until(["Unhealthy", "Unhealthy", "Healthy", "Healthy"]) == ["Unhealthy", "Unhealthy", "Healthy",
+                                                                          "Healthy"]
+        drain.unlink()
+        assert until(["Healthy"] * 4) == ["Healthy"] * 4
+    finally:
+        n.close()

@@ -82,6 +82,7 @@ def test_defaults_render_a_valid_daemonset():
     assert e["AUTO_REPLICA_UNIT"] == "auto"
     # health state on by default: env + hostPath volume
     assert e["DP_HEALTH_STATE_FILE"] == "/var/lib/amdgpu-device-plugin/health.state"
+    assert e["DP_DRAIN_FILE"] == "/var/lib/amdgpu-device-plugin/drain"
     vol = {v["name"]: v for v in ds["spec"]["template"]["spec"]["volumes"]}["health-state"]
     assert vol["hostPath"] == {"path": "/var/lib/amdgpu-device-plugin", "type": "DirectoryOrCreate"}
     assert container(ds)["image"] == "amdgpu-device-plugin:0.1.0"
@@ -303,7 +304,7 @@ def test_prometheus_operator_objects():
     assert sm["spec"]["selector"]["matchLabels"].items() <= svc["metadata"]["labels"].items()
     assert sm["spec"]["endpoints"] == [{"port": "metrics", "path": "/metrics", "interval": "30s"}]
     rules = rule["spec"]["groups"][0]["rules"]
-    assert len(rules) == 11 and all(r["alert"].startswith("AmdGpu") for r in rules)
+    assert len(rules) == 12 and all(r["alert"].startswith("AmdGpu") for r in rules)
     over = [r for r in rules if r["alert"] == "AmdGpuContainerOverHbmGrant"][0]
     assert "amdgpu_dp_container_hbm_over_grant" in over["expr"] and over["labels"]["severity"] == "critical"
     assert "> 0.9" in [r for r in rules if r["alert"] == "AmdGpuContainerNearHbmGrant"][0]["expr"]
