@@ -303,6 +303,8 @@ void Monitor::Notify(int gpu, bool healthy, const std::string& reason) {
 Status Monitor::Start() {
   if (cfg_.disabled) {
     LOG_INFO(kComp, "health checks disabled by DP_DISABLE_HEALTHCHECKS");
+    if (!cfg_.drain_file.empty())
+      LOG_WARN(kComp, "--drain-file %s is not applied: health checks are disabled", cfg_.drain_file.c_str());
     return Status::Ok();
   }
   // Only the handles of GPUs in this snapshot are watched.
