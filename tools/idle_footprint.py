@@ -7,7 +7,11 @@ driver-side HBM check) registered with a stub kubelet, left idle for
 switches per second (all threads: every wake-up the daemon causes), RSS,
 threads and fds, from /proc.
 
-  python tools/idle_footprint.py [--real] [--enforce] [--seconds 60] [--scrape-s 15]
+  python tools/idle_footprint.py [--real] [--enforce] [--relay] [--seconds 60] [--scrape-s 15]
+
+--relay: the chart's layout -- an event relay process next to the daemon, which
+takes its events (and, with --enforce, its driver-side scans) from it; the
+relay's own CPU, wake-ups and RSS are reported under "relay".
 
 Prints one JSON object.
 """
@@ -66,6 +70,7 @@ def main(argv=None):
     ap.add_argument("--seconds", type=float, default=60)
     ap.add_argument("--scrape-s", type=float, default=15)
     ap.add_argument("--settle-s", type=float, default=3, help="idle time before measuring (start-up excluded)")
+    ap.add_argument("--relay", action="store_true", help="events and scans through an event relay process")
     a = ap.parse_args(argv)
     d = harness.scratch_dir("adpidle")
     kub = harness.NativeKubelet(os.path.join(d, "kubelet.sock")).start()
@@ -79,15 +84,29 @@ def main(argv=None):
         from k8s_gpu_sharing_plugin_amd import BUILD_DIR
         args += ["--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units",
                  "--memcap-lib", os.path.join(BUILD_DIR, "libadp_memcap.so")]
+    fx = None if a.real else dict(fixtures.node(8), events_open_kfd=True)
+    relay = None
+    if a.relay:
+        esock = os.path.join(d + ".relay", "events.sock")
+        os.makedirs(os.path.dirname(esock), exist_ok=True)
+        relay = harness.Daemon(d + ".relay", fx, args=["--event-relay", "--health-event-socket", esock],
+                               real_smi=a.real, env={"ADP_LOG_LEVEL": "warn"}).start()
+        deadline = time.time() + 30
+        while not os.path.exists(esock):
+            if time.time() > deadline or relay.proc.poll() is not None:
+                raise SystemExit("the relay never listened:\n" + relay.log()[-3000:])
+            time.sleep(0.05)
+        args += ["--health-event-socket", esock]
     # production defaults: no DP_HEALTH_POLL_MS / DP_DRIVER_HBM_POLL_MS overrides
-    dm = harness.Daemon(d, None if a.real else fixtures.node(8), args=args, real_smi=a.real,
-                        env={"ADP_LOG_LEVEL": "warn"}).start()
+    dm = harness.Daemon(d, fx, args=args, real_smi=a.real, env={"ADP_LOG_LEVEL": "warn"}).start()
     try:
         if kub.wait(lambda e: e.get("event") == "devices", 30) is None:
             raise SystemExit("the daemon never delivered a device list:\n" + dm.log()[-3000:])
         time.sleep(a.settle_s)
         pid = dm.proc.pid
+        rpid = relay.proc.pid if relay else None
         c0, s0_, t0 = cpu_seconds(pid), context_switches(pid), time.monotonic()
+        rc0, rs0 = (cpu_seconds(rpid), context_switches(rpid)) if rpid else (0, 0)
         scrapes, next_scrape, t_end = 0, t0, t0 + a.seconds
         while time.monotonic() < t_end:
             if time.monotonic() >= next_scrape:
@@ -103,9 +122,16 @@ def main(argv=None):
                "cpu_pct_of_a_core": round((c1 - c0) * 100 / dt, 3),
                "context_switches_per_s": round((s1 - s0_) / dt, 1), **proc_stats(pid),
                "daemon_alive": dm.proc.poll() is None}
+        if rpid:
+            rc1, rs1 = cpu_seconds(rpid), context_switches(rpid)
+            res["relay"] = {"cpu_pct_of_a_core": round((rc1 - rc0) * 100 / dt, 3),
+                            "context_switches_per_s": round((rs1 - rs0) / dt, 1), **proc_stats(rpid),
+                            "alive": relay.proc.poll() is None}
     finally:
         code = dm.stop()
         kub.stop()
+        if relay and relay.proc.poll() is None:
+            relay.stop()
     res["daemon_exit"] = code
     print(json.dumps(res), flush=True)
     return 0 if res["daemon_alive"] and code in (0, None) else 1
