@@ -164,7 +164,9 @@ step_idle() {
   local secs=${IDLE_SECONDS:-60}
   timeout -k 10 $((secs + 90)) python tools/idle_footprint.py --real --seconds $secs > $out/idle.json 2> $out/idle.err || die IDLE $out/idle.err
   timeout -k 10 $((secs + 90)) python tools/idle_footprint.py --real --enforce --seconds $secs > $out/idle_enforce.json 2> $out/idle_enforce.err || die "IDLE (enforce)" $out/idle_enforce.err
-  cat $out/idle.json $out/idle_enforce.json
+  # the chart's layout: events and scans through the event relay
+  timeout -k 10 $((secs + 90)) python tools/idle_footprint.py --real --enforce --relay --seconds $secs > $out/idle_relay.json 2> $out/idle_relay.err || die "IDLE (relay)" $out/idle_relay.err
+  cat $out/idle.json $out/idle_enforce.json $out/idle_relay.json
 }
 step_driver() {
   timeout -k 10 180 python tools/probe_driver_usage.py > $out/driver_usage.json 2> $out/driver_usage.err || die DRIVER $out/driver_usage.err
