@@ -293,6 +293,18 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     close(lfd);
     return 1;
   }
+  // Watchdog: an amdsmi wait that has not returned for kStuckMs means events
+  // are not being delivered; the daemons are told (a "reinit" hello with
+  // events=off, so they poll) and told again when the wait returns.
+  const int64_t kStuckMs = [] {
+    const char* e = getenv("ADP_RELAY_STUCK_MS");
+    return e && atoll(e) > 0 ? static_cast<int64_t>(atoll(e)) : int64_t{10000};
+  }();
+  // The wait's slice (an event ends the wait at once): short, because
+  // re-enumeration -- every daemon (re)start asks for one -- must wait for the
+  // slice to end before it can stop the waiter; and well under the watchdog's
+  // threshold. Idle, that is ~10 wake-ups/s at 0.02% of a core (profiles/r4/idle/).
+  const int wait_slice_ms = static_cast<int>(std::max<int64_t>(10, std::min<int64_t>(100, kStuckMs / 4)));
   std::atomic<bool> waiter_stop{false};
   std::atomic<int64_t> beat_ms{0};  // the waiter's last sign of life (steady clock)
   std::atomic<int> wait_failures{0};  // consecutive failed waits
@@ -310,7 +322,7 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
       while (!waiter_stop.load()) {
         events.clear();
         beat_ms.store(now_ms());
-        Status st = lib->EventsWait(100, &events);
+        Status st = lib->EventsWait(wait_slice_ms, &events);
         beat_ms.store(now_ms());
         if (!st.ok()) {
           int n = wait_failures.fetch_add(1) + 1;
@@ -351,13 +363,7 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
   int exit_code = 0;
   bool quit = false;
   std::string pending;  // event bytes read from the pipe, up to the last full line
-  // Watchdog: an amdsmi wait that has not returned for kStuckMs means events
-  // are not being delivered; the daemons are told (a "reinit" hello with
-  // events=off, so they poll) and told again when the wait returns.
-  const int64_t kStuckMs = [] {
-    const char* e = getenv("ADP_RELAY_STUCK_MS");
-    return e && atoll(e) > 0 ? static_cast<int64_t>(atoll(e)) : int64_t{10000};
-  }();
+
   bool stuck = false;
   std::string state_before_stuck;
   auto broadcast = [&](const std::string& line) {
