@@ -134,3 +134,65 @@ def test_doctor_in_the_plugin_container(scratch, tmp_path):
         assert _find(lines, "health events:").startswith("ok")
     finally:
         n.stop()
+
+
+def _writes(log):
+    try:
+        lines = open(log).read().splitlines()
+    except OSError:
+        return []
+    return [ln.split(" ", 1) for ln in lines if " " in ln]
+
+
+def test_every_write_lands_on_a_mounted_volume(scratch, tmp_path):
+    """readOnlyRootFilesystem: every filesystem write the plugin and the relay
+    attempt (logged by libadp_devcgroup_sim.so's ADP_FS_WRITE_LOG: opens for
+    writing, mkdir, rename, unlink, socket binds) falls on a volume the chart
+    mounts writable -- the kubelet's plugin directory, the health-state
+    hostPath (health state, drain file), the NFD features directory, the event
+    socket's emptyDir, /dev -- never on the container's own filesystem."""
+    fx = dict(fixtures.node(2), events_open_kfd=True)
+    plugin_dir = scratch  # /var/lib/kubelet/device-plugins
+    state_dir = str(tmp_path / "state")  # /var/lib/amdgpu-device-plugin
+    nfd_dir = str(tmp_path / "nfd")  # /etc/nfd-features
+    sock_dir = scratch + ".events"  # /run/amdgpu-dp-events
+    for d in (state_dir, nfd_dir, sock_dir):
+        os.makedirs(d)
+    sock = os.path.join(sock_dir, "events.sock")
+    dlog, rlog = str(tmp_path / "daemon.writes"), str(tmp_path / "relay.writes")
+    proc = FakeProc(str(tmp_path / "proc"))
+    relay = harness.Daemon(scratch + "-relay", fx, env={"LD_PRELOAD": _preload(SIM), "ADP_DEVCGROUP_ALLOW": "/dev",
+                                                        "ADP_FS_WRITE_LOG": rlog}, args=[
+        "--event-relay", "--health-event-socket", sock, "--host-proc", proc.root, "--kfd-proc-dir", ""]).start()
+    relay.wait_log("relaying amdsmi events on")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fx, env={"LD_PRELOAD": _preload(SIM), "ADP_FS_WRITE_LOG": dlog,
+                                         "DP_HEALTH_POLL_MS": "100"}, args=[
+        "--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units", "--memcap-lib",
+        os.path.join(BUILD_DIR, "libadp_memcap.so"), "--metrics-addr", "127.0.0.1:0",
+        "--health-event-socket", sock, "--host-proc", str(tmp_path / "nosuch"), "--driver-hbm-poll-ms", "50",
+        "--health-state-file", os.path.join(state_dir, "health.state"),
+        "--drain-file", os.path.join(state_dir, "drain"), "--node-labels-file", os.path.join(nfd_dir, "amd-gpu")])
+    d.start()
+    try:
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        for i in range(3):
+            c.allocate(ids[i * 4:i * 4 + 4])
+        c.close()
+        d.wait_log("events on through the relay")
+        with open(os.path.join(state_dir, "drain"), "w") as f:
+            f.write(fx["gpus"][1]["bdf"] + "\n")
+        d.wait_log("drained by the operator")
+        os.kill(d.proc.pid, __import__("signal").SIGHUP)  # a restart re-creates sockets and files
+        d.wait_log("registered device plugin", timeout=10)
+    finally:
+        d.stop()
+        k.stop()
+        relay.stop()
+    allowed = [plugin_dir, state_dir, nfd_dir, sock_dir, "/dev/"]
+    bad = {who: sorted({p for _, p in _writes(log) if not any(p.startswith(a) for a in allowed)})
+           for who, log in (("daemon", dlog), ("relay", rlog))}
+    assert _writes(dlog) and _writes(rlog), "the write log recorded nothing"
+    assert bad == {"daemon": [], "relay": []}, bad

@@ -444,3 +444,56 @@ def test_kfd_topology_cus_match_asic_info(snap, tmp_path):
     fru = [v for k, v in extra.items() if k.endswith("product_name") and not v.startswith("unreadable")]
     if fru and fru[0]:
         assert dry["labels"]["amd.com/gpu.product"] == "-".join(fru[0].split()), dry["labels"]
+
+
+def test_every_write_lands_on_a_mounted_volume_on_real_amdsmi(scratch, snap, tmp_path):
+    """The chart's layout on real libamd_smi with every filesystem write logged
+    (libadp_devcgroup_sim.so, ADP_FS_WRITE_LOG): the plugin (denied the device
+    nodes) and the relay (allowed /dev) write only to the volumes the chart
+    mounts writable -- what readOnlyRootFilesystem needs, including whatever
+    libamd_smi itself writes."""
+    from test_chart_layout import _writes
+    plugin_dir = scratch
+    state_dir, nfd_dir, sock_dir = str(tmp_path / "state"), str(tmp_path / "nfd"), scratch + ".events"
+    for d in (state_dir, nfd_dir, sock_dir):
+        os.makedirs(d)
+    sock = os.path.join(sock_dir, "events.sock")
+    dlog, rlog = str(tmp_path / "daemon.writes"), str(tmp_path / "relay.writes")
+    pre = " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), SIM) if x)
+    relay = harness.Daemon(scratch + "-relay", real_smi=True, args=["--event-relay", "--health-event-socket", sock],
+                           env={"LD_PRELOAD": pre, "ADP_DEVCGROUP_ALLOW": "/dev", "ADP_FS_WRITE_LOG": rlog}).start()
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = None
+    try:
+        relay.wait_log("relaying amdsmi events on", 30)
+        d = harness.Daemon(scratch, real_smi=True, env={"LD_PRELOAD": pre, "ADP_FS_WRITE_LOG": dlog,
+                                                        "DP_HEALTH_POLL_MS": "200"}, args=[
+            "--devices", "0", "--resource-config", "gpu:gpu-mem-gb:-1", "--replica-cu-mask",
+            "--enforce-memory-units", "--memcap-lib", os.path.join(BUILD_DIR, "libadp_memcap.so"),
+            "--metrics-addr", "127.0.0.1:0", "--health-event-socket", sock, "--driver-hbm-poll-ms", "200",
+            "--health-state-file", os.path.join(state_dir, "health.state"),
+            "--drain-file", os.path.join(state_dir, "drain"),
+            "--node-labels-file", os.path.join(nfd_dir, "amd-gpu")]).start()
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=10).devices]
+        c.allocate(ids[:4])
+        c.close()
+        d.wait_log("events on through the relay", 30)
+        d.wait_log("health poll #1", 30)
+        time.sleep(1.0)  # a few health polls and relay scans
+    finally:
+        if d:
+            assert d.stop() == 0
+        k.stop()
+        assert relay.stop() == 0
+    allowed = [plugin_dir, state_dir, nfd_dir, sock_dir, "/dev/"]
+    summary = {}
+    for who, log in (("daemon", dlog), ("relay", rlog)):
+        w = _writes(log)
+        summary[who] = {"writes": len(w), "calls": sorted({c for c, _ in w}),
+                        "outside_mounts": sorted({p for _, p in w if not any(p.startswith(a) for a in allowed)}),
+                        "dev": sorted({p for _, p in w if p.startswith("/dev/")})}
+    _save("fs_writes.json", summary)
+    assert summary["daemon"]["writes"] and summary["relay"]["writes"], summary
+    assert not summary["daemon"]["outside_mounts"] and not summary["relay"]["outside_mounts"], summary
