@@ -150,13 +150,15 @@ def test_every_write_lands_on_a_mounted_volume(scratch, tmp_path):
     writing, mkdir, rename, unlink, socket binds) falls on a volume the chart
     mounts writable -- the kubelet's plugin directory, the health-state
     hostPath (health state, drain file), the NFD features directory, the event
-    socket's emptyDir, /dev -- never on the container's own filesystem."""
+    socket's emptyDir, /var/run/cdi (CDI list strategies), /dev -- never on the
+    container's own filesystem."""
     fx = dict(fixtures.node(2), events_open_kfd=True)
     plugin_dir = scratch  # /var/lib/kubelet/device-plugins
     state_dir = str(tmp_path / "state")  # /var/lib/amdgpu-device-plugin
     nfd_dir = str(tmp_path / "nfd")  # /etc/nfd-features
     sock_dir = scratch + ".events"  # /run/amdgpu-dp-events
-    for d in (state_dir, nfd_dir, sock_dir):
+    cdi_dir = str(tmp_path / "cdi")  # /var/run/cdi (mounted with a CDI list strategy)
+    for d in (state_dir, nfd_dir, sock_dir, cdi_dir):
         os.makedirs(d)
     sock = os.path.join(sock_dir, "events.sock")
     dlog, rlog = str(tmp_path / "daemon.writes"), str(tmp_path / "relay.writes")
@@ -172,7 +174,8 @@ def test_every_write_lands_on_a_mounted_volume(scratch, tmp_path):
         os.path.join(BUILD_DIR, "libadp_memcap.so"), "--metrics-addr", "127.0.0.1:0",
         "--health-event-socket", sock, "--host-proc", str(tmp_path / "nosuch"), "--driver-hbm-poll-ms", "50",
         "--health-state-file", os.path.join(state_dir, "health.state"),
-        "--drain-file", os.path.join(state_dir, "drain"), "--node-labels-file", os.path.join(nfd_dir, "amd-gpu")])
+        "--drain-file", os.path.join(state_dir, "drain"), "--node-labels-file", os.path.join(nfd_dir, "amd-gpu"),
+        "--device-list-strategy", "cdi-annotations", "--cdi-spec-dir", cdi_dir])
     d.start()
     try:
         reg = k.wait_registration()
@@ -191,7 +194,8 @@ def test_every_write_lands_on_a_mounted_volume(scratch, tmp_path):
         d.stop()
         k.stop()
         relay.stop()
-    allowed = [plugin_dir, state_dir, nfd_dir, sock_dir, "/dev/"]
+    allowed = [plugin_dir, state_dir, nfd_dir, sock_dir, cdi_dir, "/dev/"]
+    assert any(p.startswith(cdi_dir) for _, p in _writes(dlog))  # the CDI spec was written, there
     bad = {who: sorted({p for _, p in _writes(log) if not any(p.startswith(a) for a in allowed)})
            for who, log in (("daemon", dlog), ("relay", rlog))}
     assert _writes(dlog) and _writes(rlog), "the write log recorded nothing"

@@ -73,15 +73,16 @@ def test_static_manifests():
             assert doc["spec"]["selector"]["matchLabels"] == doc["spec"]["template"]["metadata"]["labels"]
         if "cpumanager" in path:
             assert c["securityContext"] == {"privileged": True}
-        else:  # the plugin container itself never runs privileged
+        else:  # the plugin container itself never runs privileged, and writes only to its volumes
             assert c["securityContext"]["capabilities"]["drop"] == ["ALL"], path
+            assert c["securityContext"]["readOnlyRootFilesystem"] is True, path
         vols = {v["name"] for v in spec["volumes"]}
         for ctr in spec["containers"]:
             assert {m["name"] for m in ctr["volumeMounts"]} <= vols, (path, ctr["name"])
         if "health-events" in path:
             # privilege separation: only the relay is privileged, and the two share the socket dir
             (relay,) = [x for x in spec["containers"] if x["name"] == "event-relay"]
-            assert relay["securityContext"] == {"privileged": True}
+            assert relay["securityContext"] == {"privileged": True, "readOnlyRootFilesystem": True}
             assert relay["args"] == ["--event-relay", "--health-event-socket", "/run/amdgpu-dp-events/events.sock"]
             assert {e["name"]: e["value"] for e in c["env"]}["DP_HEALTH_EVENT_SOCKET"] == \
                 "/run/amdgpu-dp-events/events.sock"

@@ -91,9 +91,11 @@ def test_defaults_render_a_valid_daemonset():
     assert e["DP_HEALTH_EVENTS"] == "true"
     assert e["DP_HEALTH_EVENT_SOCKET"] == "/run/amdgpu-dp-events/events.sock"
     sc = container(ds)["securityContext"]
-    assert sc == {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}}, sc
+    assert sc == {"allowPrivilegeEscalation": False, "readOnlyRootFilesystem": True,
+                  "capabilities": {"drop": ["ALL"]}}, sc
     r = relay(ds)
-    assert r["securityContext"] == {"privileged": True}
+    # both write only to mounted volumes (tests/test_chart_layout.py, on real amdsmi too)
+    assert r["securityContext"] == {"privileged": True, "readOnlyRootFilesystem": True}
     assert r["args"] == ["--event-relay", "--health-event-socket", "/run/amdgpu-dp-events/events.sock"]
     assert not r.get("ports")  # no network-facing input
     # its liveness: the relay greets on its socket and its event wait is not stuck
@@ -144,7 +146,8 @@ def test_driver_hbm_check_mounts_the_hosts_proc():
     e = env(ds)
     assert e["DP_DRIVER_HBM_POLL_MS"] == "10000" and e["DP_DRIVER_HBM_SLACK_MIB"] == "512"
     assert "DP_HOST_PROC" not in e and e["DP_HEALTH_EVENT_SOCKET"]
-    assert container(ds)["securityContext"] == {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}}
+    assert container(ds)["securityContext"] == {"allowPrivilegeEscalation": False, "readOnlyRootFilesystem": True,
+                                                "capabilities": {"drop": ["ALL"]}}
     assert "host-proc" not in {m["name"] for m in container(ds)["volumeMounts"]}
     r = relay(ds)
     assert {x["name"]: x["value"] for x in r["env"]}["DP_HOST_PROC"] == "/host/proc"
@@ -348,3 +351,20 @@ def test_grafana_dashboard_configmap():
     assert not helm_render.render({"metrics": {"enabled": True}})["grafana-dashboard.yaml"].strip()
     assert not helm_render.render({"metrics": {"enabled": False, "grafanaDashboard": {"enabled": True}}})[
         "grafana-dashboard.yaml"].strip()
+
+
+@pytest.mark.parametrize("strategy,mounted", [("envvar", False), ("volume-mounts", False),
+                                               ("cdi-annotations", True), ("cdi-cri", True)])
+def test_cdi_strategies_write_the_spec_where_the_runtime_reads_it(strategy, mounted):
+    """The CDI list strategies make the daemon write a CDI spec (--cdi-spec-dir,
+    /var/run/cdi): the chart mounts the host's /var/run/cdi there, so the
+    container runtime sees it -- and the read-only root filesystem is never
+    written."""
+    ds = daemonset({"deviceListStrategy": strategy})
+    check_consistent(ds)
+    mounts = {m["name"]: m for m in container(ds)["volumeMounts"]}
+    vols = {v["name"]: v for v in ds["spec"]["template"]["spec"]["volumes"]}
+    assert ("cdi-specs" in mounts) == mounted
+    if mounted:
+        assert mounts["cdi-specs"]["mountPath"] == "/var/run/cdi"
+        assert vols["cdi-specs"]["hostPath"] == {"path": "/var/run/cdi", "type": "DirectoryOrCreate"}

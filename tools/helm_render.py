@@ -191,6 +191,8 @@ class Renderer:
             "trunc": lambda n, s: gostr(s)[:n],
             "trimSuffix": lambda suf, s: gostr(s)[:-len(suf)] if suf and gostr(s).endswith(suf) else gostr(s),
             "contains": lambda sub, s: gostr(sub) in gostr(s),
+            "hasPrefix": lambda pre, s: gostr(s).startswith(gostr(pre)),
+            "toString": lambda v: gostr(v),
             "printf": _printf,
             "toYaml": _to_yaml,
             "nindent": lambda n, s: "\n" + "\n".join((" " * n + ln) if ln else ln for ln in gostr(s).split("\n")),
