@@ -166,6 +166,12 @@ def _status(args) -> int:
         secs = scalar("amdgpu_dp_driver_hbm_scan_seconds") or 0
         line += f"; driver-side scans {int(polls)} (last {secs * 1e3:.2f} ms, {int(failures)} failed)"
     print(line)
+    causes = {}
+    for ls, v in by("amdgpu_dp_gpu_failure"):
+        if v:
+            causes.setdefault(ls.get("bdf"), []).append(ls.get("cause"))
+    for bdf, cs in sorted(causes.items()):
+        print(f"GPU {bdf}: " + ", ".join(sorted(cs)))
     bad = [ls for ls, v in by("amdgpu_dp_device_healthy") if v == 0]
     for ls in bad:
         print(f"UNHEALTHY {ls.get('resource')} {ls.get('device')} (index {ls.get('index')})")

@@ -329,6 +329,11 @@ def test_operator_drain_file(scratch, tmp_path):
         assert _value(m, "amdgpu_dp_gpu_failure", bdf=bdf1, cause="drained") == 1
         assert _value(m, "amdgpu_dp_gpu_failure", bdf=bdf1, cause="ecc") == 0
         assert _value(m, "amdgpu_dp_gpu_failure", bdf=fx["gpus"][0]["bdf"], cause="drained") == 0
+        import subprocess
+        import sys
+        st = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "status",
+                             f"http://127.0.0.1:{port}/metrics"], capture_output=True, text=True, timeout=60)
+        assert f"GPU {bdf1}: drained" in st.stdout and st.returncode == 1, st.stdout
         n.inject("1 4 reset done")  # a post-reset clears faults, not a drain
         n.d.wait_log("GPU_POST_RESET")
         time.sleep(0.4)
