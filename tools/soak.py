@@ -54,6 +54,8 @@ def main():
                          "driver-side scan to find")
     ap.add_argument("--relay", action="store_true",
                     help="events and driver-side scans through an event relay process (the chart's layout)")
+    ap.add_argument("--drain-churn", action="store_true",
+                    help="drain and undrain GPU 0 every other round through --drain-file")
     a = ap.parse_args()
     holders = []
     if a.real and a.holders:
@@ -73,8 +75,11 @@ def main():
     with socket.socket() as s0:  # a free port for the metrics endpoint
         s0.bind(("127.0.0.1", 0))
         port = s0.getsockname()[1]
+    drain = os.path.join(d + ".state", "drain")
+    os.makedirs(os.path.dirname(drain), exist_ok=True)
     args = ["--metrics-addr", f"127.0.0.1:{port}", "--resource-config", "gpu:gpu:4",
-            "--health-state-file", os.path.join(d, "health.state")]
+            "--health-state-file", os.path.join(d, "health.state"), "--drain-file", drain]
+    drains = 0
     if a.real:
         args += ["--devices", "0"]
     if a.enforce:
@@ -122,6 +127,13 @@ def main():
                 ok = False
                 print("daemon died", flush=True)
                 break
+            if a.drain_churn:  # GPU 0 in and out of service (by node index)
+                if round_no % 2:
+                    with open(drain, "w") as f:
+                        f.write("0\n")
+                    drains += 1
+                elif os.path.exists(drain):
+                    os.unlink(drain)
             # every 5th round: SIGHUP (full restart); every 7th: kubelet restart
             if round_no % 5 == 0:
                 mark = len(kub.events)
@@ -182,7 +194,7 @@ def main():
         "rss_mib_max": max((s["rss_mib"] for s in samples), default=None),
         "fds_after_warmup": warm.get("fds"), "fds_last": last.get("fds"),
         "threads_after_warmup": warm.get("threads"), "threads_last": last.get("threads"),
-        "exit_code": code, "driver_hbm_polls": driver_polls, "holders": len(holders),
+        "exit_code": code, "driver_hbm_polls": driver_polls, "holders": len(holders), "drains": drains,
     }
     if scans:
         ms = sorted(s["ms"] for s in scans)
