@@ -120,6 +120,11 @@ class ScanWorker {
         LOG_INFO(kComp, "first HBM scan for a daemon: %zu process(es) from %s, %zu descriptor(s), %zu unreadable",
                  s.pids_scanned, s.pid_source == "kfd" ? opts_.kfd_proc_dir.c_str() : opts_.proc_root.c_str(),
                  s.fd_entries, s.fd_dirs_unreadable);
+        // A node has hundreds of processes; a handful means this /proc is the
+        // relay container's own PID namespace, where no pod's process is seen.
+        if (s.pid_source == "proc" && s.pids_scanned < 5)
+          LOG_WARN(kComp, "only %zu process(es) under %s: is the host's /proc mounted there (--host-proc)? Other "
+                   "pods' HBM is not seen", s.pids_scanned, opts_.proc_root.c_str());
       }
       // The reply is written blocking, bounded: a daemon that stops reading loses it.
       fcntl(r.fd, F_SETFL, fcntl(r.fd, F_GETFL) & ~O_NONBLOCK);

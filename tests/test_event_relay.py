@@ -221,6 +221,8 @@ def test_relay_answers_scan_requests_and_drops_malformed_ones(scratch, tmp_path)
             out = ask(bad)
             assert "scan\t" not in out, (bad, out)
         assert relay.log().count("malformed scan request dropped") == 3
+        # an empty /proc (the relay's own PID namespace, not the host's): said once
+        assert relay.log().count("is the host's /proc mounted there (--host-proc)?") == 1
     finally:
         relay.stop()
 
