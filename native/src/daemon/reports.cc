@@ -382,6 +382,9 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
       if (!scan.ok())
         d.Line("warn", "driver-side HBM check: the event relay at " + f.health_event_socket + " ran no scan (" +
                            scan.status().ToString() + ") -- start the relay container (--event-relay)");
+      else if (scan->pid_source == "proc" && scan->pids_scanned < 5)
+        d.Line("warn", "driver-side HBM check: the event relay sees only " + std::to_string(scan->pids_scanned) +
+                           " process(es) -- mount the host's /proc into it and point its --host-proc there");
       else if (scan->fd_dirs_unreadable == 0)
         d.Line("ok", "driver-side HBM check: the event relay reads " + std::to_string(scan->pids_scanned) +
                          " processes (" + scan->pid_source + " list)");
