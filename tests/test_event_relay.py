@@ -359,3 +359,45 @@ def test_relay_keeps_no_descriptor_per_scan(scratch, tmp_path):
         assert after[0] <= before[0] + 2 and after[1] == before[1], (before, after)
     finally:
         relay.stop()
+
+
+def test_partition_events_through_the_relay(scratch):
+    """CPX: each compute partition is its own amdsmi processor and KFD node.
+    A reset event of one partition, relayed by KFD node, marks its GPU -- all
+    of that GPU's partitions (a reset is device-wide), partitionStrategy single
+    -- Unhealthy, and none of the other GPU's."""
+    fifo = os.path.join(scratch + ".fixture", "events")
+    os.makedirs(os.path.dirname(fifo))
+    os.mkfifo(fifo)
+    sock = os.path.join(scratch + ".fixture", "events.sock")
+    fx = dict(fixtures.node(2, ["CPX", "CPX"], memory="NPS2"), events_open_kfd=True)
+    relay = harness.Daemon(scratch + "-relay", fx, args=["--event-relay", "--health-event-socket", sock],
+                           event_fifo=fifo).start()
+    relay.wait_log("relaying amdsmi events on")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fx, args=["--partition-strategy", "single", "--health-event-socket", sock],
+                       env={"LD_PRELOAD": _preload(SIM)}).start()
+    try:
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        q, call = c.watch()
+        first = q.get(timeout=5)
+        assert len(first.devices) == 16
+        d.wait_log("events on through the relay")
+        assert "event notification registered on 16 processor(s)" in relay.log()
+        fd = os.open(fifo, os.O_WRONLY | os.O_NONBLOCK)
+        os.write(fd, b"1:3 3 partition reset\n")
+        os.close(fd)
+        law = q.get(timeout=5)
+        bdf1 = fx["gpus"][1]["bdf"][:-1]  # partitions report their own function numbers
+        sick = sorted(x.ID for x in law.devices if x.health == "Unhealthy")
+        assert len(sick) == 8, [x.health for x in law.devices]
+        assert "event node=13 " in relay.log()  # KFD node 2 + 8*1 + partition 3
+        d.wait_log("GPU_PRE_RESET")
+        assert bdf1 in d.log()
+        call.cancel()
+        c.close()
+    finally:
+        d.stop()
+        k.stop()
+        relay.stop()
