@@ -162,7 +162,8 @@ const std::vector<FlagDef>& Table() {
        [](Flags& f) -> void* { return &f.driver_hbm_slack_mib; }},
       {"host-proc", "DP_HOST_PROC", "hostProc", Kind::kString,
        "the /proc of the PID namespace the pods run in, for the driver-side HBM check: /proc with hostPID, "
-       "else a hostPath mount of the host's /proc",
+       "else a hostPath mount of the host's /proc (with --health-event-socket the event relay runs the scans, "
+       "with its own --host-proc)",
        [](Flags& f) -> void* { return &f.host_proc; }},
       {"kfd-proc-dir", "DP_KFD_PROC_DIR", "kfdProcDir", Kind::kString,
        "KFD's list of GPU processes (host PIDs) for the driver-side HBM check: only those processes' "
