@@ -169,11 +169,12 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     return 1;
   }
   Validated v = std::move(*validated);
+  // The relay's liveness probe runs every 30 s: no config dump, no amdsmi.
+  if (cfg.flags.relay_ping) return health::PingRelay(cfg.flags.health_event_socket, 5000);
   LOG_INFO(kComp, "running with config:\n%s", cfg.ToJson().c_str());
   LOG_INFO(kComp, "running with resource config: %s", v.rc.ToJson().c_str());
 
   if (cfg.flags.list_grants) return ListGrants(PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage"));
-  if (cfg.flags.relay_ping) return health::PingRelay(cfg.flags.health_event_socket, 5000);
 
   // Signals are consumed through a signalfd; block them before any thread starts.
   sigset_t sigs;
