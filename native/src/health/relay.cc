@@ -424,6 +424,16 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     if (pfds[1].revents & POLLIN) {
       int cfd;
       while ((cfd = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK)) >= 0) {
+        // Only this relay's own uid (the plugin container runs as the same
+        // root) -- the socket's mode says so already; the kernel's peer
+        // credentials make sure.
+        ucred cred{};
+        socklen_t clen = sizeof(cred);
+        if (getsockopt(cfd, SOL_SOCKET, SO_PEERCRED, &cred, &clen) != 0 || cred.uid != geteuid()) {
+          LOG_WARN(kComp, "connection from uid %u refused", static_cast<unsigned>(cred.uid));
+          close(cfd);
+          continue;
+        }
         if (!SendAll(cfd, hello())) {
           close(cfd);
           continue;

@@ -56,7 +56,8 @@ RelayLine ParseRelayLine(std::string_view line);
 std::string FormatRelayEvent(const smi::ProcessorInfo& p, uint32_t type, const std::string& message);
 
 // Runs the relay until SIGTERM/SIGINT/SIGQUIT (the caller blocked them and
-// passes their signalfd): binds `socket_path` (mode 0600), registers events on
+// passes their signalfd): binds `socket_path` (owner-only; connections from
+// another uid are refused by their SO_PEERCRED too), registers events on
 // every amdsmi processor and forwards them to every connected daemon. Returns
 // the process exit code.
 // `proc_root` / `kfd_proc_dir`: where scans read processes (ScanDriverHbm).

@@ -401,3 +401,35 @@ def test_partition_events_through_the_relay(scratch):
         d.stop()
         k.stop()
         relay.stop()
+
+
+def test_relay_refuses_other_uids(scratch, tmp_path):
+    """The socket is its owner's only; behind that the relay checks the peer's
+    credentials (SO_PEERCRED) and closes connections from another uid, even if
+    the socket file was made world-writable."""
+    import subprocess
+    import sys
+    if os.geteuid() != 0:
+        import pytest
+        pytest.skip("needs root to connect as another uid")
+    import shutil
+    import tempfile
+    sdir = tempfile.mkdtemp(prefix="adp-uid-", dir="/tmp")  # traversable by another uid
+    os.chmod(sdir, 0o755)
+    sock = os.path.join(sdir, "events.sock")
+    fx = dict(fixtures.node(1), events_open_kfd=True)
+    relay = harness.Daemon(scratch + "-relay", fx, args=["--event-relay", "--health-event-socket", sock]).start()
+    try:
+        relay.wait_log("relaying amdsmi events on")
+        assert os.stat(sock).st_mode & 0o077 == 0  # owner only
+        os.chmod(sock, 0o666)
+        code = ("import socket, sys\n"
+                "c = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM); c.settimeout(5); c.connect(sys.argv[1])\n"
+                "print(repr(c.recv(100)))\n")
+        r = subprocess.run([sys.executable, "-c", code, sock], capture_output=True, text=True, timeout=30,
+                           preexec_fn=lambda: os.setuid(65534))
+        assert r.stdout.strip() == "b''", r.stdout + r.stderr  # closed without a greeting
+        assert "connection from uid 65534 refused" in relay.wait_log("refused")
+    finally:
+        relay.stop()
+        shutil.rmtree(sdir, ignore_errors=True)
