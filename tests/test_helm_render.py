@@ -368,3 +368,23 @@ def test_cdi_strategies_write_the_spec_where_the_runtime_reads_it(strategy, moun
     if mounted:
         assert mounts["cdi-specs"]["mountPath"] == "/var/run/cdi"
         assert vols["cdi-specs"]["hostPath"] == {"path": "/var/run/cdi", "type": "DirectoryOrCreate"}
+
+
+def test_metrics_network_policy():
+    """metrics.networkPolicy: only the listed peers reach the metrics port (the
+    endpoints are unauthenticated); off by default and without metrics."""
+    out = helm_render.render({"metrics": {"enabled": True, "networkPolicy": {"enabled": True}}})
+    (np,) = [d for d in yaml.safe_load_all(out["networkpolicy.yaml"]) if d]
+    assert np["kind"] == "NetworkPolicy" and np["spec"]["policyTypes"] == ["Ingress"]
+    ds = daemonset({"metrics": {"enabled": True}})
+    assert np["spec"]["podSelector"]["matchLabels"].items() <= ds["spec"]["template"]["metadata"]["labels"].items()
+    (rule,) = np["spec"]["ingress"]
+    assert rule["ports"] == [{"port": 9400, "protocol": "TCP"}]
+    assert rule["from"] == [{"namespaceSelector": {"matchLabels": {"kubernetes.io/metadata.name": "monitoring"}}}]
+    custom = helm_render.render({"metrics": {"enabled": True, "port": 9500, "networkPolicy": {
+        "enabled": True, "from": [{"podSelector": {"matchLabels": {"app": "prometheus"}}}]}}})
+    (np2,) = [d for d in yaml.safe_load_all(custom["networkpolicy.yaml"]) if d]
+    assert np2["spec"]["ingress"][0] == {"ports": [{"port": 9500, "protocol": "TCP"}],
+                                         "from": [{"podSelector": {"matchLabels": {"app": "prometheus"}}}]}
+    for vals in ({}, {"metrics": {"enabled": True}}, {"metrics": {"enabled": False, "networkPolicy": {"enabled": True}}}):
+        assert not helm_render.render(vals)["networkpolicy.yaml"].strip()
