@@ -169,6 +169,14 @@ const std::vector<FlagDef>& Table() {
        "KFD's list of GPU processes (host PIDs) for the driver-side HBM check: only those processes' "
        "descriptors are read, not every process's (empty = always walk every process under --host-proc)",
        [](Flags& f) -> void* { return &f.kfd_proc_dir; }},
+      {"drain", "ADP_DRAIN", "", Kind::kString,
+       "add these GPUs (PCI addresses, UUIDs or node indices, comma separated; checked against this node's "
+       "GPUs) to --drain-file, print the drain list and exit: from the plugin pod, `amdgpu-device-plugin --drain "
+       "0000:0c:00.0` takes a GPU out of service at the next health poll",
+       [](Flags& f) -> void* { return &f.drain; }},
+      {"undrain", "ADP_UNDRAIN", "", Kind::kString,
+       "remove these GPUs from --drain-file (every line naming them), print the drain list and exit",
+       [](Flags& f) -> void* { return &f.undrain; }},
       {"drain-file", "DP_DRAIN_FILE", "drainFile", Kind::kString,
        "operator drain list: every GPU named in this file (PCI address, UUID, partition UUID or node index; "
        "whitespace or comma separated, '#' comments) is advertised Unhealthy until it is removed from the file "

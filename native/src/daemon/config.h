@@ -59,7 +59,8 @@ struct Flags {
   std::string host_proc = "/proc";      // the host's /proc (hostPID, or a hostPath mount)
   std::string kfd_proc_dir = "/sys/class/kfd/kfd/proc";  // GPU processes by host PID ("" = walk all)
   std::string sysfs_root = "/sys";
-  std::string drain_file;  // operator drain list: GPUs named in it are advertised Unhealthy  // KFD topology (CU counts) and PCI product names without the render node
+  std::string drain_file;  // operator drain list: GPUs named in it are advertised Unhealthy
+  std::string drain, undrain;  // one-shot: add / remove GPUs in the drain file, then exit  // KFD topology (CU counts) and PCI product names without the render node
   uint64_t server_threads = 0;  // 0 -> plugin::DefaultServerThreads()
   std::string metrics_addr;     // "" = no metrics endpoint
   std::string node_labels_file; // "" = no NFD feature file

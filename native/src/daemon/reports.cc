@@ -10,6 +10,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <fstream>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -416,6 +417,80 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
            budget < 2.0 ? "off (under 2 CPUs)" : "on");
   d.Line("ok", b);
   return d.Finish();
+}
+
+int DrainCommand(smi::Library* lib, const Validated& v, const Config& cfg) {
+  const Flags& f = cfg.flags;
+  if (f.drain_file.empty()) {
+    fprintf(stderr, "--drain/--undrain need --drain-file (DP_DRAIN_FILE)\n");
+    return 1;
+  }
+  auto snap = inventory::BuildSnapshot(lib, v.bopts);
+  if (!snap.ok()) {
+    fprintf(stderr, "enumeration failed: %s\n", snap.status().ToString().c_str());
+    return 1;
+  }
+  // Every name a GPU answers to in the drain file (health::Monitor::ApplyDrain).
+  auto names_of = [](const inventory::PhysicalGpu& g) {
+    std::set<std::string> n = {g.uuid, g.bdf, std::to_string(g.node_index)};
+    if (g.bdf.rfind('.') != std::string::npos) n.insert(g.bdf.substr(0, g.bdf.rfind('.')));
+    for (const auto& p : g.partitions) n.insert(p.uuid);
+    return n;
+  };
+  auto resolve = [&](const std::string& list, std::vector<const inventory::PhysicalGpu*>* out) -> bool {
+    for (const auto& id : Split(list, ',')) {
+      std::string t = Trim(id);
+      if (t.empty()) continue;
+      const inventory::PhysicalGpu* hit = nullptr;
+      for (const auto& g : (*snap)->gpus)
+        if (names_of(g).count(t)) hit = &g;
+      if (!hit) {
+        fprintf(stderr, "no GPU of this node is named %s\n", t.c_str());
+        return false;
+      }
+      out->push_back(hit);
+    }
+    return true;
+  };
+  std::vector<const inventory::PhysicalGpu*> add, remove;
+  if (!resolve(f.drain, &add) || !resolve(f.undrain, &remove)) return 1;
+
+  std::vector<std::string> lines;
+  {
+    std::ifstream in(f.drain_file);
+    for (std::string line; std::getline(in, line);) lines.push_back(line);
+  }
+  auto names_line = [&](const std::string& line, const inventory::PhysicalGpu* g) {
+    std::string body = line.substr(0, line.find('#'));
+    for (char& c : body)
+      if (c == ',' || c == '\t' || c == '\r') c = ' ';
+    auto n = names_of(*g);
+    for (const auto& tok : Split(body, ' '))
+      if (!tok.empty() && n.count(tok)) return true;
+    return false;
+  };
+  for (const auto* g : remove)
+    lines.erase(std::remove_if(lines.begin(), lines.end(), [&](const std::string& l) { return names_line(l, g); }),
+                lines.end());
+  for (const auto* g : add) {
+    bool listed = false;
+    for (const auto& l : lines) listed = listed || names_line(l, g);
+    if (!listed) lines.push_back(g->bdf + "  # " + g->uuid);
+  }
+  std::string body;
+  for (const auto& l : lines) body += l + "\n";
+  std::string tmp = f.drain_file + ".tmp." + std::to_string(getpid());
+  int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  bool ok = fd >= 0 && write(fd, body.data(), body.size()) == static_cast<ssize_t>(body.size());
+  if (fd >= 0) close(fd);
+  if (!ok || rename(tmp.c_str(), f.drain_file.c_str()) != 0) {
+    fprintf(stderr, "cannot write %s: %s\n", f.drain_file.c_str(), strerror(errno));
+    unlink(tmp.c_str());
+    return 1;
+  }
+  printf("%s", body.c_str());
+  fflush(stdout);
+  return 0;
 }
 
 }  // namespace adp::daemon

@@ -26,5 +26,7 @@ struct DoctorReport {
   int Finish();
 };
 int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorReport& d);
+// --drain / --undrain: edits --drain-file (atomically) and prints it.
+int DrainCommand(smi::Library* lib, const Validated& v, const Config& cfg);
 
 }  // namespace adp::daemon

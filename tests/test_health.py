@@ -345,3 +345,48 @@ def test_operator_drain_file(scratch, tmp_path):
         assert until(["Healthy"] * 4) == ["Healthy"] * 4
     finally:
         n.close()
+
+
+def test_drain_and_undrain_commands(scratch, tmp_path):
+    """`amdgpu-device-plugin --drain <id>` / `--undrain <id>` (run in the
+    plugin pod, DP_DRAIN_FILE set) edit the drain file -- IDs checked against
+    this node's GPUs -- and the running daemon applies it at its next poll."""
+    import queue
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import DAEMON, MOCK_LIB
+    drain = tmp_path / "drain"
+    fx = dict(fixtures.node(2), events_open_kfd=True)
+    n = Node(scratch, fx, args=["--drain-file", str(drain)], env={"DP_HEALTH_POLL_MS": "100"})
+    env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB, AMDSMI_MOCK_FIXTURE=fixtures.write(fx, str(tmp_path / "fx")),
+               DP_DRAIN_FILE=str(drain))
+
+    def cli(*args):
+        r = subprocess.run([DAEMON, "--device-plugin-path", str(tmp_path), *args], capture_output=True, text=True,
+                           timeout=60, env=env)
+        return r.returncode, r.stdout, r.stderr
+
+    last = [x.health for x in n.first.devices]
+
+    def until(want, timeout=5):
+        nonlocal last
+        deadline = time.time() + timeout
+        while last != want and time.time() < deadline:
+            try:
+                last = [x.health for x in n.q.get(timeout=0.2).devices]
+            except queue.Empty:
+                pass
+        return last
+    try:
+        bdf1, uuid1 = fx["gpus"][1]["bdf"], fx["gpus"][1]["uuid"]
+        rc, out, _ = cli("--drain", bdf1)
+        assert rc == 0 and out.startswith(bdf1) and uuid1 in out, out
+        assert until(["Healthy", "Unhealthy"]) == ["Healthy", "Unhealthy"]
+        rc, out, _ = cli("--drain", uuid1)  # already listed under another name: unchanged
+        assert rc == 0 and out.count("\n") == 1
+        rc, _, err = cli("--drain", "0000:99:00.0")
+        assert rc == 1 and "no GPU of this node is named 0000:99:00.0" in err
+        rc, out, _ = cli("--undrain", "1")  # by node index
+        assert rc == 0 and out == ""
+        assert until(["Healthy", "Healthy"]) == ["Healthy", "Healthy"]
+    finally:
+        n.close()
