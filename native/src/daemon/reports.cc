@@ -430,20 +430,13 @@ int DrainCommand(smi::Library* lib, const Validated& v, const Config& cfg) {
     fprintf(stderr, "enumeration failed: %s\n", snap.status().ToString().c_str());
     return 1;
   }
-  // Every name a GPU answers to in the drain file (health::Monitor::ApplyDrain).
-  auto names_of = [](const inventory::PhysicalGpu& g) {
-    std::set<std::string> n = {g.uuid, g.bdf, std::to_string(g.node_index)};
-    if (g.bdf.rfind('.') != std::string::npos) n.insert(g.bdf.substr(0, g.bdf.rfind('.')));
-    for (const auto& p : g.partitions) n.insert(p.uuid);
-    return n;
-  };
   auto resolve = [&](const std::string& list, std::vector<const inventory::PhysicalGpu*>* out) -> bool {
     for (const auto& id : Split(list, ',')) {
       std::string t = Trim(id);
       if (t.empty()) continue;
       const inventory::PhysicalGpu* hit = nullptr;
       for (const auto& g : (*snap)->gpus)
-        if (names_of(g).count(t)) hit = &g;
+        if (health::DrainNames(g).count(t)) hit = &g;
       if (!hit) {
         fprintf(stderr, "no GPU of this node is named %s\n", t.c_str());
         return false;
@@ -461,12 +454,9 @@ int DrainCommand(smi::Library* lib, const Validated& v, const Config& cfg) {
     for (std::string line; std::getline(in, line);) lines.push_back(line);
   }
   auto names_line = [&](const std::string& line, const inventory::PhysicalGpu* g) {
-    std::string body = line.substr(0, line.find('#'));
-    for (char& c : body)
-      if (c == ',' || c == '\t' || c == '\r') c = ' ';
-    auto n = names_of(*g);
-    for (const auto& tok : Split(body, ' '))
-      if (!tok.empty() && n.count(tok)) return true;
+    auto tokens = health::DrainTokens(line);
+    for (const auto& n : health::DrainNames(*g))
+      if (tokens.count(n)) return true;
     return false;
   };
   for (const auto* g : remove)

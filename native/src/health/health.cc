@@ -488,20 +488,12 @@ void Monitor::RelayWait(int ms, std::vector<smi::Event>* out) {
   if (closed) RelayClose("the event relay closed the connection");
 }
 
-void Monitor::ApplyDrain() {
-  std::string text;
-  int fd = open(cfg_.drain_file.c_str(), O_RDONLY | O_CLOEXEC | O_NONBLOCK);
-  if (fd >= 0) {
-    char buf[4096];
-    ssize_t n;
-    while ((n = read(fd, buf, sizeof(buf))) > 0 && text.size() < 65536) text.append(buf, static_cast<size_t>(n));
-    close(fd);
-  }  // absent or unreadable: nothing drained
+std::set<std::string> DrainTokens(std::string_view text) {
   std::set<std::string> names;
   for (size_t b = 0; b < text.size();) {
     size_t e = text.find('\n', b);
-    if (e == std::string::npos) e = text.size();
-    std::string line = text.substr(b, e - b);
+    if (e == std::string_view::npos) e = text.size();
+    std::string line(text.substr(b, e - b));
     b = e + 1;
     if (size_t hash = line.find('#'); hash != std::string::npos) line.resize(hash);
     for (char& c : line)
@@ -513,11 +505,30 @@ void Monitor::ApplyDrain() {
       p = q + 1;
     }
   }
+  return names;
+}
+
+std::set<std::string> DrainNames(const inventory::PhysicalGpu& g) {
+  std::set<std::string> n = {g.uuid, g.bdf, std::to_string(g.node_index)};
+  if (size_t dot = g.bdf.rfind('.'); dot != std::string::npos) n.insert(g.bdf.substr(0, dot));
+  for (const auto& p : g.partitions) n.insert(p.uuid);
+  n.erase("");
+  return n;
+}
+
+void Monitor::ApplyDrain() {
+  std::string text;
+  int fd = open(cfg_.drain_file.c_str(), O_RDONLY | O_CLOEXEC | O_NONBLOCK);
+  if (fd >= 0) {
+    char buf[4096];
+    ssize_t n;
+    while ((n = read(fd, buf, sizeof(buf))) > 0 && text.size() < 65536) text.append(buf, static_cast<size_t>(n));
+    close(fd);
+  }  // absent or unreadable: nothing drained
+  const std::set<std::string> names = DrainTokens(text);
   for (const auto& g : snap_->gpus) {
-    bool drained = names.count(g.uuid) || names.count(g.bdf) || names.count(std::to_string(g.node_index));
-    // a PCI address without the function, and partition UUIDs, name the GPU too
-    if (!drained && g.bdf.size() > 2) drained = names.count(g.bdf.substr(0, g.bdf.rfind('.')));
-    for (const auto& p : g.partitions) drained = drained || names.count(p.uuid);
+    bool drained = false;
+    for (const auto& n : DrainNames(g)) drained = drained || names.count(n);
     bool was = fail_[g.index] & kFailDrained;
     if (drained && !was) Update(g.index, kFailDrained, 0, "drained by the operator (" + cfg_.drain_file + ")");
     if (!drained && was) Update(g.index, 0, kFailDrained, "removed from the drain file");

@@ -176,6 +176,13 @@ class Ledger {
   std::string path_;
 };
 
+// The drain file's syntax (--drain-file), shared by the monitor and the
+// --drain / --undrain commands: the names in `text` (whitespace or comma
+// separated, '#' starts a comment), and the names a GPU answers to there (its
+// UUID, PCI address with or without the function, node index, partition UUIDs).
+std::set<std::string> DrainTokens(std::string_view text);
+std::set<std::string> DrainNames(const inventory::PhysicalGpu& g);
+
 class Monitor {
  public:
   // `ledger` / `counters` may be null: the Monitor then keeps its own.

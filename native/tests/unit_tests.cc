@@ -233,6 +233,22 @@ static void TestRelayLines() {
     CHECK(!memcap::ParseScan(bad, &back, &used));
 }
 
+static void TestDrainSyntax() {
+  g_case = "drain-syntax";
+  auto t = health::DrainTokens("# maintenance\n0000:0c:00.0  # fan\r\nGPU-a,GPU-b\t3\n\n#0000:0d:00.0\n");
+  CHECK((t == std::set<std::string>{"0000:0c:00.0", "GPU-a", "GPU-b", "3"}));
+  inventory::PhysicalGpu g;
+  g.uuid = "GPU-a";
+  g.bdf = "0000:0c:00.0";
+  g.node_index = 3;
+  inventory::Partition p;
+  p.uuid = "GPU-a-p1";
+  g.partitions.push_back(p);
+  auto n = health::DrainNames(g);
+  CHECK((n == std::set<std::string>{"GPU-a", "0000:0c:00.0", "0000:0c:00", "3", "GPU-a-p1"}));
+  CHECK(health::DrainTokens("").empty() && health::DrainTokens("# only a comment").empty());
+}
+
 static void TestProto() {
   g_case = "proto";
   pb::AllocateResponse r;
@@ -1113,6 +1129,7 @@ int main() {
   TestAdditionalIds();
   TestResourceConfig();
   TestRelayLines();
+  TestDrainSyntax();
   TestProto();
   TestTopology();
   TestHierarchicalMatchesOracle();
