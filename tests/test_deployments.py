@@ -72,7 +72,7 @@ def test_static_manifests():
             assert doc["apiVersion"] == "apps/v1"
             assert doc["spec"]["selector"]["matchLabels"] == doc["spec"]["template"]["metadata"]["labels"]
         if "cpumanager" in path:
-            assert c["securityContext"] == {"privileged": True}
+            assert c["securityContext"] == {"privileged": True, "readOnlyRootFilesystem": True}
         else:  # the plugin container itself never runs privileged, and writes only to its volumes
             assert c["securityContext"]["capabilities"]["drop"] == ["ALL"], path
             assert c["securityContext"]["readOnlyRootFilesystem"] is True, path

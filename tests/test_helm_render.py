@@ -125,7 +125,7 @@ def test_health_events_off_runs_unprivileged():
     custom = {"runAsUser": 0, "capabilities": {"add": ["SYS_ADMIN"]}}
     assert container(daemonset({"securityContext": custom}))["securityContext"] == custom
     compat = daemonset({"compatWithCPUManager": True})
-    assert container(compat)["securityContext"] == {"privileged": True}
+    assert container(compat)["securityContext"] == {"privileged": True, "readOnlyRootFilesystem": True}
     assert relay(compat) is None and "DP_HEALTH_EVENT_SOCKET" not in env(compat)  # events in-process
 
 
