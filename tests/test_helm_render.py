@@ -233,7 +233,7 @@ def test_reference_value_names_win():
     e = env(ds)
     assert e["PARTITION_STRATEGY"] == "mixed" and e["DRIVER_ROOT"] == "/run/amd"
     assert e["PASS_DEVICE_SPECS"] == "true"  # compat mode always passes device specs
-    assert container(ds)["securityContext"] == {"privileged": True}
+    assert container(ds)["securityContext"] == {"privileged": True, "readOnlyRootFilesystem": True}
 
 
 def test_legacy_api_and_overrides():
