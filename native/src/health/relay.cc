@@ -245,7 +245,7 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
   addr.sun_family = AF_UNIX;
   memcpy(addr.sun_path, socket_path.c_str(), socket_path.size());
   unlink(socket_path.c_str());
-  mode_t old = umask(0077);  // 0600: only the daemon's uid (root, same pod) may connect
+  mode_t old = umask(0077);  // owner-only: only the daemon's uid (root, same pod) may connect
   int rc = lfd < 0 ? -1 : bind(lfd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr));
   umask(old);
   if (rc != 0 || listen(lfd, 8) != 0) {
@@ -321,6 +321,7 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
   auto start_waiter = [&] {
     if (!registered) return;
     waiter_stop.store(false);
+    wait_failures.store(0);  // a fresh registration: earlier failures say nothing about it
     beat_ms.store(now_ms());
     waiter = std::thread([&] {
       std::vector<smi::Event> events;
