@@ -444,8 +444,14 @@ void DriverHbmMonitor::PollOnce() {
     if (!r.ok()) {
       if (stop_.load()) return;  // cancelled by Stop()
       std::lock_guard<std::mutex> lk(mu_);
-      if (snap_.scan_error.empty())
+      // The pod's two containers start together: a relay not listening yet is
+      // expected for the first polls, a warning only after that.
+      if (snap_.polls == 0 && snap_.scan_failures < 5) {
+        if (snap_.scan_failures == 0)
+          LOG_INFO(kComp, "driver-side scan: waiting for the event relay (%s)", r.status().ToString().c_str());
+      } else if (snap_.scan_error.empty()) {
         LOG_WARN(kComp, "driver-side scan through the relay failed: %s", r.status().ToString().c_str());
+      }
       snap_.scan_error = r.status().ToString();
       snap_.remote = true;
       ++snap_.scan_failures;
@@ -495,7 +501,9 @@ void DriverHbmMonitor::PollOnce() {
     LOG_INFO(kComp, "first scan: %zu candidate process(es) from %s, %zu descriptor(s), %.2f ms", scan.pids_scanned,
              from.c_str(), scan.fd_entries, scan_ns / 1e6);
   }
-  if (!snap_.scan_error.empty()) LOG_INFO(kComp, "driver-side scan through the relay works again");
+  if (!snap_.scan_error.empty())
+    LOG_INFO(kComp, "%s", snap_.polls == 0 ? "driver-side scan: the event relay answers"
+                                           : "driver-side scan through the relay works again");
   snap_.scan_error.clear();
   snap_.remote = remote;
   snap_.scan = std::move(scan);
