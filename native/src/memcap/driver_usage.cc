@@ -446,10 +446,11 @@ void DriverHbmMonitor::PollOnce() {
       std::lock_guard<std::mutex> lk(mu_);
       // The pod's two containers start together: a relay not listening yet is
       // expected for the first polls, a warning only after that.
-      if (snap_.polls == 0 && snap_.scan_failures < 5) {
+      constexpr uint64_t kStartupGrace = 5;  // failed polls before a relay that never answered is a warning
+      if (snap_.polls == 0 && snap_.scan_failures < kStartupGrace) {
         if (snap_.scan_failures == 0)
           LOG_INFO(kComp, "driver-side scan: waiting for the event relay (%s)", r.status().ToString().c_str());
-      } else if (snap_.scan_error.empty()) {
+      } else if (snap_.polls == 0 ? snap_.scan_failures == kStartupGrace : snap_.scan_error.empty()) {
         LOG_WARN(kComp, "driver-side scan through the relay failed: %s", r.status().ToString().c_str());
       }
       snap_.scan_error = r.status().ToString();

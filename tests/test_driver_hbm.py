@@ -436,3 +436,52 @@ def test_a_relay_that_never_answers_does_not_hold_up_shutdown(scratch, tmp_path)
         srv.close()
         for c in conns:
             c.close()
+
+
+def test_a_malformed_relay_reply_counts_as_a_failed_scan(scratch, tmp_path):
+    """A relay answering a scan with something ParseScan rejects (then closing)
+    leaves the previous state and counts a failure; nothing of the reply is
+    taken."""
+    import socket as so
+    import threading
+    path = os.path.join(scratch + ".bad", "events.sock")
+    os.makedirs(os.path.dirname(path))
+    srv = so.socket(so.AF_UNIX, so.SOCK_STREAM)
+    srv.bind(path)
+    srv.listen(8)
+
+    def serve():
+        while True:
+            try:
+                c, _ = srv.accept()
+            except OSError:
+                return
+            c.sendall(b"hello v1 events=ok processors=1\n")
+            c.settimeout(2)
+            try:
+                req = c.recv(4096)
+            except OSError:
+                req = b""
+            if req.startswith(b"scan\t"):
+                c.sendall(b"scan\tproc\t1\t1\t0\t1\np\tNOTAPID\t0000:0c:00.0\t1\tk\t0\tc\n")
+                c.close()
+            # (the health monitor's connection stays open, silent)
+    threading.Thread(target=serve, daemon=True).start()
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(1), args=[
+        "--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units",
+        "--memcap-lib", SHIM, "--health-event-socket", path, "--driver-hbm-poll-ms", "50"]).start()
+    try:
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics")).group(1))
+        k.wait_registration()
+        deadline = time.time() + 10
+        while _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_driver_hbm_scan_failures_total") < 6:
+            assert time.time() < deadline
+            time.sleep(0.05)
+        s = _parse(_get(port, "/metrics")[1])
+        assert _value(s, "amdgpu_dp_driver_hbm_polls_total") == 0  # nothing accepted
+        assert "closed the connection" in d.wait_log("driver-side scan through the relay failed")
+    finally:
+        d.stop()
+        k.stop()
+        srv.close()
