@@ -485,3 +485,29 @@ def test_a_malformed_relay_reply_counts_as_a_failed_scan(scratch, tmp_path):
         d.stop()
         k.stop()
         srv.close()
+
+
+def test_a_relay_that_starts_after_the_plugin_is_waited_for(scratch, tmp_path):
+    """The pod's two containers start together: polls before the relay listens
+    are a wait (info), not a failure warning; the first answer says so."""
+    proc = FakeProc(str(tmp_path / "proc"))
+    sock = os.path.join(scratch + ".late", "events.sock")
+    os.makedirs(os.path.dirname(sock))
+    fx = dict(fixtures.node(1), events_open_kfd=True)
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fx, args=[
+        "--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:gpu-mem-gb:-1", "--enforce-memory-units",
+        "--memcap-lib", SHIM, "--health-event-socket", sock, "--driver-hbm-poll-ms", "100"]).start()
+    relay = None
+    try:
+        d.wait_log("driver-side scan: waiting for the event relay")
+        time.sleep(0.25)  # two or three polls without a relay: inside the grace
+        relay = harness.Daemon(scratch + "-relay", fx, args=[
+            "--event-relay", "--health-event-socket", sock, "--host-proc", proc.root, "--kfd-proc-dir", ""]).start()
+        d.wait_log("driver-side scan: the event relay answers", timeout=10)
+        assert "driver-side scan through the relay failed" not in d.log()
+    finally:
+        d.stop()
+        k.stop()
+        if relay:
+            relay.stop()
