@@ -199,6 +199,8 @@ step_curve() {
 }
 step_soak() {
   local secs=${SOAK_SECONDS:-180}
+  # one gpurun call may run 1200 s in all: leave room for the box set-up and the summary
+  if [ "$secs" -gt 1000 ]; then echo "SOAK_SECONDS=$secs does not fit one call; using 1000"; secs=1000; fi
   timeout -k 10 $((secs + 220)) python -u tools/soak.py --seconds $secs --real ${SOAK_ARGS:-} --out $out/soak.json > $out/soak.log 2>&1 || die SOAK $out/soak.log
   tail -1 $out/soak.log
 }
