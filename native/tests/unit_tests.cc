@@ -233,6 +233,43 @@ static void TestRelayLines() {
     CHECK(!memcap::ParseScan(bad, &back, &used));
 }
 
+static void TestRemoteScan() {
+  g_case = "remote-scan";
+  memcap::DriverScan scan;
+  scan.pid_source = "kfd";
+  scan.pids_scanned = 1;
+  scan.procs = {{42, "0000:0c:00.0", 7u << 20, "0::/pod/a", "k", false}};
+  memcap::Aggregate(&scan);
+  int sv[2];
+  CHECK(socketpair(AF_UNIX, SOCK_STREAM, 0, sv) == 0);
+  // the relay's greeting, then (after the request) the reply in two pieces
+  std::thread relay([&] {
+    std::string hello = "hello v1 events=ok processors=1\n";
+    CHECK(write(sv[1], hello.data(), hello.size()) == static_cast<ssize_t>(hello.size()));
+    char req[512];
+    ssize_t n = read(sv[1], req, sizeof(req));
+    CHECK(n > 0 && std::string(req, static_cast<size_t>(n)) == "scan\t/usage\t0::/self\n");
+    std::string reply = memcap::SerializeScan(scan);
+    CHECK(write(sv[1], reply.data(), 7) == 7);
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    CHECK(write(sv[1], reply.data() + 7, reply.size() - 7) == static_cast<ssize_t>(reply.size() - 7));
+  });
+  auto r = memcap::RemoteScan(sv[0], "/usage", "0::/self", 5000);
+  relay.join();
+  CHECK(r.ok() && r->pid_source == "kfd" && r->procs.size() == 1 && r->procs[0].pid == 42);
+  CHECK((r->by_grant[{"k", "0000:0c:00.0"}] == 7u << 20));
+  close(sv[1]);
+  // a closed connection before a full reply is an error, not a partial scan
+  r = memcap::RemoteScan(sv[0], "/usage", "0::/self", 5000);
+  CHECK(!r.ok());
+  close(sv[0]);
+  // a tab in the directory never reaches the wire
+  CHECK(socketpair(AF_UNIX, SOCK_STREAM, 0, sv) == 0);
+  CHECK(!memcap::RemoteScan(sv[0], "/us\tage", "c", 100).ok());
+  close(sv[0]);
+  close(sv[1]);
+}
+
 static void TestDrainSyntax() {
   g_case = "drain-syntax";
   auto t = health::DrainTokens("# maintenance\n0000:0c:00.0  # fan\r\nGPU-a,GPU-b\t3\n\n#0000:0d:00.0\n");
@@ -1130,6 +1167,7 @@ int main() {
   TestResourceConfig();
   TestRelayLines();
   TestDrainSyntax();
+  TestRemoteScan();
   TestProto();
   TestTopology();
   TestHierarchicalMatchesOracle();
