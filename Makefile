@@ -99,7 +99,7 @@ fuzz:
 	  -DCMAKE_CXX_COMPILER=$(CLANGXX) -DCMAKE_C_COMPILER=$(dir $(CLANGXX))clang >/dev/null
 	ninja -C build/fuzz -j$(JOBS) $(addprefix fuzz_,$(FUZZ_TARGETS))
 	$(PY) tools/gen_fuzz_seeds.py build/fuzz/corpus/h2 build/fuzz/corpus/h2_diff
-	cd build/fuzz && for t in $(FUZZ_TARGETS); do mkdir -p corpus/$$t; \
+	cd build/fuzz && rm -f fuzz_*.failed && for t in $(FUZZ_TARGETS); do mkdir -p corpus/$$t; \
 	  ( ./fuzz_$$t -max_total_time=$(FUZZ_SECONDS) -rss_limit_mb=2048 -print_final_stats=1 corpus/$$t \
 	    > fuzz_$$t.log 2>&1 || echo "fuzz_$$t FAILED (build/fuzz/fuzz_$$t.log)" > fuzz_$$t.failed ) & done; wait; \
 	  for t in $(FUZZ_TARGETS); do grep -h "DONE" fuzz_$$t.log | sed "s/^/$$t /"; done; \

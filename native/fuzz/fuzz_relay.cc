@@ -2,7 +2,7 @@
 // (health/relay.cc): the daemon parses whatever arrives on its relay socket.
 // Checks: no crash; an accepted event line re-formatted from its fields parses
 // back to the same fields (message newlines folded to spaces); a hello's
-// verdict is exactly "events=ok" present; an accepted scan reply (the relay's
+// verdict is exactly "events=ok" present before its reason; an accepted scan reply (the relay's
 // answer to "scan", memcap/driver_usage.h) re-serialises to the bytes it was
 // parsed from, and its sums match its rows.
 #include <fuzzer/FuzzedDataProvider.h>
@@ -46,10 +46,12 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     if (!r.bdf.empty() && r.bdf != "-" && back.bdf != r.bdf) Fail("bdf round trip");
     if (got != folded) Fail("message round trip");
   } else if (r.kind == "hello") {
-    // ok iff the first "events=" token is exactly "events=ok"
+    // ok iff the first "events=" token before the free-text reason is exactly "events=ok"
     std::string first;
     std::string body = line;
     while (!body.empty() && (body.back() == '\n' || body.back() == '\r')) body.pop_back();
+    if (size_t at = body.find(" reason="); at != std::string::npos) body.resize(at);
+    if (r.gap < -1 || r.gap > 1) Fail("gap");
     for (size_t b = 0; b <= body.size() && first.empty();) {
       size_t e = body.find(' ', b);
       if (e == std::string::npos) e = body.size();

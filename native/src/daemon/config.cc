@@ -182,6 +182,11 @@ const std::vector<FlagDef>& Table() {
        "whitespace or comma separated, '#' comments) is advertised Unhealthy until it is removed from the file "
        "(read when the health monitor starts and at every poll; a reset does not clear it; empty = off)",
        [](Flags& f) -> void* { return &f.drain_file; }},
+      {"reset-recovery-hold-ms", "DP_RESET_RECOVERY_HOLD_MS", "resetRecoveryHoldMs", Kind::kUint,
+       "a GPU waiting for GPU_POST_RESET across an event gap (events lost: relay restarted or re-registered, "
+       "events off, a new in-process registration) is back in service once amdsmi has answered every health "
+       "poll for this long with no new GPU_PRE_RESET (0 = only the event brings it back)",
+       [](Flags& f) -> void* { return &f.reset_recovery_hold_ms; }, true},
       {"sysfs-root", "DP_SYSFS_ROOT", "sysfsRoot", Kind::kString,
        "where sysfs is mounted: without the render node (an unprivileged pod's device cgroup denies it) "
        "amdsmi's asic_info fails, and the CU count comes from <root>/class/kfd/kfd/topology and the product "

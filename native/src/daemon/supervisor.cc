@@ -1,5 +1,6 @@
 #include "daemon/supervisor.h"
 
+#include "daemon/daemon_metrics.h"
 #include "daemon/reports.h"
 #include "daemon/validate.h"
 
@@ -159,21 +160,633 @@ void ArmTimer(int tfd, int ms) {
   timerfd_settime(tfd, 0, &its, nullptr);
 }
 
+// One daemon: the running generation (node snapshot, plugins, health
+// monitor), the state that outlives generations (health ledger and counters,
+// the driver-side HBM check, /metrics), and the epoll loop that restarts,
+// re-registers or stops them (main.go:205-326).
+class Supervisor {
+ public:
+  Supervisor(Config cfg, Validated v, std::function<Result<Config>()> reload, smi::Library* lib, int sfd)
+      : cfg_(std::move(cfg)), v_(std::move(v)), reload_(std::move(reload)), lib_(lib), sfd_(sfd),
+        ledger_(cfg_.flags.health_state_file),
+        usage_dir_(PathJoin(cfg_.flags.plugin_dir, "amdgpu-dp/usage")) {}
+  ~Supervisor() {
+    for (int fd : {ep_, ifd_, tfd_, efd_, lfd_, rfd_})
+      if (fd >= 0) close(fd);
+  }
+
+  int Run() {
+    if (Status st = SetupWatches(); !st.ok()) {
+      LOG_ERROR(kComp, "%s", st.message().c_str());
+      return 1;
+    }
+    if (Status st = StartHttp(); !st.ok()) {
+      LOG_ERROR(kComp, "%s", st.ToString().c_str());
+      return 1;
+    }
+    Restart();
+    while (!quit_) {
+      epoll_event events[8];
+      int n = epoll_wait(ep_, events, 8, -1);
+      if (n < 0) {
+        if (errno == EINTR) continue;
+        LOG_ERROR(kComp, "epoll_wait: %s", strerror(errno));
+        exit_code_ = 1;
+        break;
+      }
+      bool do_restart = false;
+      bool do_reregister = false;  // a lighter restart: see Reregister
+      for (int i = 0; i < n && !quit_; ++i) {
+        int fd = events[i].data.fd;
+        uint64_t x;
+        if (fd == tfd_) {
+          Drain(tfd_, &x);
+          do_restart = true;
+        } else if (fd == rfd_) {
+          Drain(rfd_, &x);
+          OnSocketRecheck(&do_reregister);
+        } else if (fd == efd_) {
+          Drain(efd_, &x);
+          LOG_ERROR(kComp, "a gRPC server exhausted its crash budget; exiting");
+          exit_code_ = 1;
+          quit_ = true;
+        } else if (fd == lfd_) {
+          Drain(lfd_, &x);
+          LOG_INFO(kComp, "partition layout changed, re-enumerating");
+          reinit_ = true;
+          do_restart = true;
+        } else if (fd == ifd_) {
+          OnInotify(&do_restart, &do_reregister);
+        } else if (fd == sfd_) {
+          OnSignals(&do_restart);
+        }
+      }
+      if (do_restart && !quit_) Restart();
+      else if (do_reregister && !quit_) Reregister();
+    }
+    StopAll();
+    if (driver_hbm_) driver_hbm_->Stop();
+    if (http_) http_->Stop();
+    // Grant files of containers allocated just before the signal: the runtime mounts them next.
+    if (!v_.popts.memcap_usage_dir.empty() && !memcap::Flush(2000))
+      LOG_WARN(kComp, "grant accounting files still being written at exit");
+    // Labels describe a node this daemon is serving; do not leave them behind.
+    if (!cfg_.flags.node_labels_file.empty()) unlink(cfg_.flags.node_labels_file.c_str());
+    return exit_code_;
+  }
+
+ private:
+  static void Drain(int fd, uint64_t* x) {
+    ssize_t r = read(fd, x, sizeof(*x));
+    (void)r;
+  }
+
+  // inotify on the kubelet socket's directory (and the plugin directory, and
+  // the config file's), timers and eventfds, all in one epoll set.
+  Status SetupWatches() {
+    kubelet_sock_ = v_.popts.kubelet_socket.empty() ? PathJoin(v_.popts.plugin_dir, "kubelet.sock")
+                                                    : v_.popts.kubelet_socket;
+    std::string watch_dir = kubelet_sock_.substr(0, kubelet_sock_.rfind('/'));
+    if (watch_dir.empty()) watch_dir = "/";
+    kubelet_name_ = BaseName(kubelet_sock_);
+    LOG_INFO(kComp, "starting FS watcher on %s", watch_dir.c_str());
+    ifd_ = inotify_init1(IN_NONBLOCK | IN_CLOEXEC);
+    if (ifd_ < 0 || inotify_add_watch(ifd_, watch_dir.c_str(), IN_CREATE | IN_MOVED_TO | IN_DELETE) < 0)
+      return Internal("failed to create FS watcher on " + watch_dir + ": " + strerror(errno));
+    if (PathJoin(v_.popts.plugin_dir, "") != PathJoin(watch_dir, ""))
+      inotify_add_watch(ifd_, v_.popts.plugin_dir.c_str(), IN_DELETE);
+    // Config file: watch its directory (editors and ConfigMap updates replace the
+    // file rather than writing it in place).
+    if (reload_ && !cfg_.config_file.empty()) {
+      std::string dir = cfg_.config_file.substr(0, cfg_.config_file.rfind('/') + 1);
+      if (dir.empty()) dir = ".";
+      config_name_ = BaseName(cfg_.config_file);
+      config_wd_ = inotify_add_watch(ifd_, dir.c_str(), IN_CLOSE_WRITE | IN_MOVED_TO | IN_CREATE);
+      if (config_wd_ < 0)
+        LOG_WARN(kComp, "cannot watch config file %s: %s", cfg_.config_file.c_str(), strerror(errno));
+    }
+    tfd_ = timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC | TFD_NONBLOCK);  // retry backoff
+    efd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);  // a gRPC server exhausted its crash budget
+    lfd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);  // health monitor: partition layout changed
+    // One-shot: look again at plugin sockets deleted from under us (recheck_sockets_).
+    rfd_ = timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC | TFD_NONBLOCK);
+    ep_ = epoll_create1(EPOLL_CLOEXEC);
+    for (int fd : {sfd_, ifd_, tfd_, efd_, lfd_, rfd_}) {
+      epoll_event ev{};
+      ev.events = EPOLLIN;
+      ev.data.fd = fd;
+      epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &ev);
+    }
+    return Status::Ok();
+  }
+
+  Status StartHttp() {
+    if (cfg_.flags.metrics_addr.empty()) return Status::Ok();
+    if (!cfg_.flags.pod_resources_socket.empty())
+      pod_lister_ = std::make_unique<podresources::CachedLister>(cfg_.flags.pod_resources_socket,
+                                                                 std::chrono::milliseconds(2000));
+    smi_version_ = lib_->Version();
+    // (env only: how long the health loop may go without an iteration before /healthz fails)
+    if (const char* e = getenv("ADP_HEALTH_STALL_MS"); e && atoll(e) > 0) stall_ms_ = atoll(e);
+    http_ = std::make_unique<metrics::HttpServer>([this] { return MetricsText(); }, [this] { return Healthy(); },
+                                                  [this] { return StatsJson(); });
+    return http_->Start(cfg_.flags.metrics_addr);
+  }
+
+  // GET /metrics: the daemon's families, then the plugins'.
+  std::string MetricsText() {
+    DaemonMetricsInput in;
+    in.smi_version = smi_version_;
+    in.restarts = restarts_.load();
+    in.health = &health_counters_;
+    {
+      std::lock_guard<std::mutex> lk(access_mu_);
+      in.node_access = node_access_;
+      for (const auto& [key, bdf] : metrics_gpus_) {
+        uint32_t fail = ledger_.Get(key).fail;
+        bool gap = (fail & health::kFailResetPending) && ledger_.Gap(key, nullptr);
+        in.gpus.push_back({bdf, fail, gap});
+      }
+    }
+    // Ask the kubelet who holds which device (cached; outside the plugins lock).
+    Result<std::vector<podresources::Assignment>> assigned = Unavailable("off");
+    if (pod_lister_) {
+      assigned = pod_lister_->Get();
+      in.pod_resources_up = assigned.ok() ? 1 : 0;
+    }
+    // Grant accounting files: read (and old ones collected) here, before the
+    // plugins lock the health listener also takes -- a slow filesystem must
+    // not hold up health verdicts.
+    std::vector<memcap::Usage> grant_files;
+    bool have_grants = false;
+    struct stat st;
+    if (stat(usage_dir_.c_str(), &st) == 0 && S_ISDIR(st.st_mode)) {
+      have_grants = true;
+      grant_files = memcap::ReadAll(usage_dir_);
+      std::set<std::string> live;
+      if (assigned.ok()) {
+        std::map<std::tuple<std::string, std::string, std::string, std::string>, std::vector<std::string_view>> ctrs;
+        for (const auto& a : *assigned) ctrs[{a.ns, a.pod, a.container, a.resource}].push_back(a.device_id);
+        for (const auto& [k, ids] : ctrs) live.insert(memcap::AllocationKey(ids));
+      }
+      memcap::Collect(usage_dir_, assigned.ok() ? &live : nullptr, 120, 4096);
+    }
+    std::unique_ptr<memcap::DriverHbmMonitor::Snapshot> dsnap;
+    if (driver_hbm_) dsnap = std::make_unique<memcap::DriverHbmMonitor::Snapshot>(driver_hbm_->Get());
+    in.driver_hbm = dsnap.get();
+    std::string out;
+    AppendDaemonMetrics(in, &out);
+    std::lock_guard<std::mutex> lk(plugins_mu_);
+    std::vector<const plugin::Plugin*> ps;
+    for (auto& p : plugins_)
+      if (p->device_count() > 0) ps.push_back(p.get());
+    plugin::Plugin::AppendPrometheus(ps, &out, assigned.ok() ? &*assigned : nullptr, dsnap.get(),
+                                     have_grants ? &grant_files : nullptr);
+    return out;
+  }
+
+  // GET /healthz
+  bool Healthy() {
+    if (!serving_.load()) return false;
+    // A health loop stuck in a call that never returns (an amdsmi event wait
+    // or query) stops advancing: the liveness probe restarts us.
+    if (int64_t age = health_counters_.HealthLoopAgeMs(); age > stall_ms_) {
+      if (!stall_logged_.exchange(true))
+        LOG_ERROR(kComp, "the health monitor has not advanced for %lld ms: /healthz fails", static_cast<long long>(age));
+      return false;
+    }
+    stall_logged_.store(false);
+    std::lock_guard<std::mutex> lk(plugins_mu_);
+    for (auto& p : plugins_)
+      if (p->device_count() > 0 && !p->running()) return false;
+    return true;
+  }
+
+  // GET /stats: what SIGUSR1 logs, as one JSON document
+  std::string StatsJson() {
+    std::string out = "{\"plugins\": [";
+    {
+      std::lock_guard<std::mutex> lk(plugins_mu_);
+      for (size_t i = 0; i < plugins_.size(); ++i) out += (i ? ", " : "") + plugins_[i]->StatsJson();
+    }
+    return out + "], \"health\": " + health_counters_.Json() + ", \"restarts\": " + std::to_string(restarts_.load()) +
+           "}\n";
+  }
+
+  void StopAll() {
+    serving_.store(false);
+    if (monitor_) monitor_->Stop();
+    monitor_.reset();
+    for (auto& p : plugins_) p->Stop();
+    std::lock_guard<std::mutex> lk(plugins_mu_);
+    plugins_.clear();
+  }
+
+  void ScheduleRetry(const char* why) {
+    LOG_WARN(kComp, "%s; retrying in %d ms", why, backoff_ms_);
+    ArmTimer(tfd_, backoff_ms_);
+    backoff_ms_ = std::min(kMaxBackoffMs, backoff_ms_ * 2);
+  }
+
+  // Starts (serves + registers) every plugin with devices; the number started,
+  // or -1 after scheduling a retry because the kubelet could not be reached.
+  int StartPlugins() {
+    int started = 0;
+    const int efd = efd_;
+    for (auto& p : plugins_) {
+      if (p->device_count() == 0) continue;
+      Status st = p->Start([efd] {
+        uint64_t one = 1;
+        ssize_t w = write(efd, &one, sizeof(one));
+        (void)w;
+      });
+      if (!st.ok()) {
+        LOG_ERROR(kComp, "could not contact kubelet, retrying (is the device-plugin feature "
+                         "enabled and is %s present?)", kubelet_sock_.c_str());
+        ScheduleRetry("plugin start failed");
+        return -1;
+      }
+      ++started;
+    }
+    backoff_ms_ = 1000;
+    serving_.store(true);
+    return started;
+  }
+
+  // Creates this generation's plugins and applies the failures recorded by
+  // earlier generations, in ONE critical section with the health listener
+  // (plugins_mu_): the monitor writes the ledger before it notifies, so a
+  // verdict that changes concurrently is either in the ledger read here or
+  // notified to the new plugins afterwards -- a GPU_POST_RESET racing a
+  // re-registration can never leave a recovered GPU advertised Unhealthy.
+  void PublishPlugins(const std::shared_ptr<const inventory::Snapshot>& snap,
+                      const std::vector<strategy::PluginSpec>& specs, bool apply_ledger) {
+    static const int reregister_delay_ms = [] {  // test hook: widens the window the lock closes
+      const char* e = getenv("ADP_DEBUG_PUBLISH_DELAY_MS");
+      return e ? atoi(e) : 0;
+    }();
+    std::lock_guard<std::mutex> lk(plugins_mu_);
+    for (const auto& s : specs) plugins_.push_back(std::make_unique<plugin::Plugin>(snap, s, v_.popts));
+    WarnSharedDeviceLists(plugins_);
+    if (!apply_ledger) return;
+    auto failed = ledger_.Failed(*snap);
+    if (reregister_delay_ms > 0) usleep(static_cast<useconds_t>(reregister_delay_ms) * 1000);
+    for (const auto& [gpu, why] : failed) {
+      LOG_WARN(kComp, "GPU %s is unhealthy since an earlier plugin generation: %s", snap->gpus[gpu].bdf.c_str(),
+               why.c_str());
+      for (auto& p : plugins_) p->SetGpuHealth(gpu, false, why);
+    }
+  }
+
+  // Where the HBM-cap shim, its preload list and the grant accounting files
+  // go this generation (--enforce-memory-units).
+  void InstallMemcapFiles() {
+    const Flags& f = cfg_.flags;
+    v_.popts.memcap_host_path = f.enforce_memory_units ? InstallMemcap(f) : "";
+    v_.popts.memcap_preload_list =
+        !v_.popts.memcap_host_path.empty() && f.memcap_ld_so_preload ? InstallPreloadList(f) : "";
+    v_.popts.memcap_usage_dir =
+        !v_.popts.memcap_host_path.empty() && f.container_hbm_metrics && !f.metrics_addr.empty() ? usage_dir_ : "";
+  }
+
+  // Driver-side check of enforced HBM grants (--driver-hbm-poll-ms): started
+  // with the first generation that enforces grants into an accounting dir.
+  void StartDriverHbm() {
+    if (driver_hbm_ || v_.popts.memcap_usage_dir.empty() || cfg_.flags.driver_hbm_poll_ms == 0) return;
+    memcap::DriverHbmMonitor::Options dopt;
+    dopt.proc_root = cfg_.flags.host_proc;
+    dopt.kfd_proc_dir = cfg_.flags.kfd_proc_dir;
+    // With an event relay the scan runs there (it holds the privilege to
+    // read other containers' descriptors; this daemon then needs none).
+    dopt.relay_socket = cfg_.flags.health_event_socket;
+    dopt.usage_dir = v_.popts.memcap_usage_dir;
+    dopt.poll_ms = static_cast<int>(std::min<uint64_t>(cfg_.flags.driver_hbm_poll_ms, 3600000));
+    dopt.slack_bytes = cfg_.flags.driver_hbm_slack_mib << 20;
+    std::string dir = v_.popts.memcap_usage_dir;
+    driver_hbm_ = std::make_unique<memcap::DriverHbmMonitor>(dopt, [this, dir] {
+      // The accounting files are read before taking the lock the health
+      // listener needs (as /metrics does): only ID lookups run under it.
+      std::vector<memcap::Usage> files = memcap::ReadAll(dir);
+      std::lock_guard<std::mutex> lk(plugins_mu_);
+      std::vector<const plugin::Plugin*> ps;
+      for (auto& p : plugins_) ps.push_back(p.get());
+      return plugin::Plugin::GrantedByKey(ps, files);
+    });
+    driver_hbm_->Start();
+  }
+
+  health::HealthConfig HealthConfigNow() const {
+    health::HealthConfig h = health::HealthConfig::FromEnv();
+    h.events = cfg_.flags.health_events;
+    h.drain_file = cfg_.flags.drain_file;
+    h.driver_root = cfg_.flags.driver_root;
+    h.event_relay = cfg_.flags.health_event_socket;
+    h.reset_recovery_hold_ms = static_cast<int64_t>(std::min<uint64_t>(cfg_.flags.reset_recovery_hold_ms, 86400000));
+    return h;
+  }
+
+  void StartMonitor(const std::shared_ptr<const inventory::Snapshot>& snap, const health::HealthConfig& hcfg) {
+    monitor_ = std::make_unique<health::Monitor>(lib_, snap, hcfg, &ledger_, &health_counters_);
+    const int lfd = lfd_;
+    monitor_->SetLayoutListener([lfd](const std::string&) {
+      uint64_t one = 1;
+      ssize_t w = write(lfd, &one, sizeof(one));
+      (void)w;
+    });
+    // Verdicts go to whichever plugins are serving (re-registration replaces them).
+    monitor_->AddListener([this](int gpu, bool ok, const std::string& why) {
+      std::lock_guard<std::mutex> lk(plugins_mu_);
+      for (auto& p : plugins_) p->SetGpuHealth(gpu, ok, why);
+    });
+    Status hs = monitor_->Start();
+    if (!hs.ok()) LOG_WARN(kComp, "health monitor: %s", hs.ToString().c_str());
+  }
+
+  // A new generation: re-enumerate (after amdsmi re-init when asked), rebuild
+  // the plugins from the strategy, start them and a new health monitor.
+  void Restart() {
+    StopAll();
+    ArmTimer(tfd_, 0);  // disarm
+    ArmTimer(rfd_, 0);
+    recheck_sockets_.clear();
+    if (reinit_) {
+      Status rs = lib_->Reinit();
+      if (!rs.ok()) {
+        LOG_ERROR(kComp, "amdsmi re-initialisation failed: %s", rs.ToString().c_str());
+        ScheduleRetry("amdsmi re-init failed");
+        return;
+      }
+      reinit_ = false;
+      LOG_INFO(kComp, "amdsmi re-initialised");
+    }
+    LOG_INFO(kComp, "retrieving plugins");
+    auto snap = inventory::BuildSnapshot(lib_, v_.bopts);
+    if (!snap.ok()) {
+      LOG_ERROR(kComp, "device enumeration failed: %s", snap.status().ToString().c_str());
+      reinit_ = true;
+      ScheduleRetry("enumeration failed");
+      return;
+    }
+    if (!cfg_.flags.node_labels_file.empty()) WriteLabels(cfg_.flags.node_labels_file, **snap);
+    {
+      auto access = inventory::ProbeDeviceAccess(**snap, cfg_.flags.driver_root);
+      std::string what = inventory::DescribeAccess(access);
+      if (what == "ok") LOG_INFO(kComp, "device access: %zu node(s) openable", access.size());
+      else LOG_WARN(kComp, "device access: %s", what.c_str());
+      std::lock_guard<std::mutex> lk(access_mu_);
+      node_access_ = std::move(access);
+      metrics_gpus_.clear();
+      for (const auto& g : (*snap)->gpus) metrics_gpus_.emplace_back(health::Ledger::KeyOf(g), g.bdf);
+    }
+    auto specs = strategy::BuildPluginSpecs(**snap, v_.partition, v_.rc, cfg_.flags.resource_prefix);
+    if (!specs.ok()) {
+      LOG_ERROR(kComp, "error creating partition strategy: %s", specs.status().message().c_str());
+      exit_code_ = 1;
+      quit_ = true;
+      return;
+    }
+    restarts_.fetch_add(1);
+    cur_snap_ = *snap;
+    cur_specs_ = *specs;
+    for (const auto& g : cur_snap_->gpus) health_counters_.SetVramTotal(g.bdf, g.vram_mib << 20);
+    InstallMemcapFiles();
+    StartDriverHbm();
+    health::HealthConfig hcfg = HealthConfigNow();
+    PublishPlugins(*snap, *specs, !hcfg.disabled);
+    int started = StartPlugins();
+    if (started < 0) return;
+    if (started == 0) LOG_INFO(kComp, "no devices found; waiting indefinitely");
+    StartMonitor(*snap, hcfg);
+  }
+
+  // Kubelet restarted (or our socket vanished): same devices, same health
+  // monitor; only the plugins are replaced and register again.
+  void Reregister() {
+    if (!monitor_ || !cur_snap_) {
+      Restart();
+      return;
+    }
+    serving_.store(false);
+    ArmTimer(tfd_, 0);
+    ArmTimer(rfd_, 0);
+    recheck_sockets_.clear();
+    for (auto& p : plugins_) p->Stop();
+    {
+      std::lock_guard<std::mutex> lk(plugins_mu_);
+      plugins_.clear();
+    }
+    restarts_.fetch_add(1);
+    LOG_INFO(kComp, "re-registering plugins (devices and health monitor unchanged)");
+    if (cfg_.flags.enforce_memory_units) v_.popts.memcap_host_path = InstallMemcap(cfg_.flags);
+    if (!v_.popts.memcap_preload_list.empty()) v_.popts.memcap_preload_list = InstallPreloadList(cfg_.flags);
+    PublishPlugins(cur_snap_, cur_specs_, !health::HealthConfig::FromEnv().disabled);
+    StartPlugins();
+  }
+
+  // Re-reads flags/env/file; on success adopts the new config (startup-bound
+  // settings excepted). Returns false when the new config is invalid.
+  bool ReloadConfig(const char* why) {
+    if (!reload_) return true;
+    auto next = reload_();
+    if (!next.ok()) {
+      LOG_ERROR(kComp, "%s: config not reloaded: %s", why, next.status().message().c_str());
+      return false;
+    }
+    for (const auto& w : next->warnings) LOG_WARN(kComp, "%s: %s", why, w.c_str());
+    auto nv = Validate(*next);
+    if (!nv.ok()) {
+      LOG_ERROR(kComp, "%s: config not reloaded: %s", why, nv.status().message().c_str());
+      return false;
+    }
+    const Flags& was = cfg_.flags;
+    const Flags& now = next->flags;
+    if (now.amdsmi_lib != was.amdsmi_lib || now.metrics_addr != was.metrics_addr ||
+        now.pod_resources_socket != was.pod_resources_socket || now.node_labels_file != was.node_labels_file ||
+        now.plugin_dir != was.plugin_dir || now.kubelet_socket != was.kubelet_socket ||
+        now.health_state_file != was.health_state_file)
+      LOG_WARN(kComp, "%s: amdsmiLib, metricsAddr, podResourcesSocket, nodeLabelsFile, devicePluginPath, "
+                      "kubeletSocket and healthStateFile apply at startup only", why);
+    std::string old_json = cfg_.ToJson();
+    Config merged = *next;
+    merged.flags.amdsmi_lib = was.amdsmi_lib;
+    merged.flags.metrics_addr = was.metrics_addr;
+    merged.flags.pod_resources_socket = was.pod_resources_socket;
+    merged.flags.node_labels_file = was.node_labels_file;
+    merged.flags.plugin_dir = was.plugin_dir;
+    merged.flags.kubelet_socket = was.kubelet_socket;
+    merged.flags.health_state_file = was.health_state_file;
+    auto mv = Validate(merged);
+    if (!mv.ok()) return false;
+    if (merged.ToJson() != old_json) {
+      cfg_ = std::move(merged);
+      v_ = std::move(*mv);
+      LOG_INFO(kComp, "%s: reloaded config:\n%s", why, cfg_.ToJson().c_str());
+      LOG_INFO(kComp, "running with resource config: %s", v_.rc.ToJson().c_str());
+    }
+    return true;
+  }
+
+  void StandBy(const plugin::Plugin& pl) {
+    // Another instance (a rollout with maxSurge) unlinked ours and bound the
+    // path: binding it back would start a tug of war. The kubelet now talks to
+    // that instance; this one stands by until the kubelet restarts or the file
+    // disappears again.
+    LOG_WARN(kComp, "inotify: %s now belongs to another process; '%s' stands by", pl.socket_path().c_str(),
+             pl.resource_name().c_str());
+  }
+
+  void OnSocketRecheck(bool* do_reregister) {
+    for (auto& pl : plugins_) {
+      if (!recheck_sockets_.count(pl->socket_path()) || !pl->running()) continue;
+      struct stat st;
+      if (stat(pl->socket_path().c_str(), &st) != 0) {
+        LOG_WARN(kComp, "inotify: %s was removed, restarting", pl->socket_path().c_str());
+        *do_reregister = true;
+      } else if (!pl->owns_socket()) {
+        StandBy(*pl);
+      }
+    }
+    recheck_sockets_.clear();
+  }
+
+  void OnInotify(bool* do_restart, bool* do_reregister) {
+    static const int kSocketRecheckMs = [] {  // test hook: widens the window (default 20 ms)
+      const char* e = getenv("ADP_DEBUG_SOCKET_RECHECK_MS");
+      return e && atoi(e) > 0 ? atoi(e) : 20;
+    }();
+    char buf[4096] __attribute__((aligned(__alignof__(inotify_event))));
+    ssize_t len;
+    while ((len = read(ifd_, buf, sizeof(buf))) > 0) {
+      for (char* p = buf; p < buf + len;) {
+        auto* e = reinterpret_cast<inotify_event*>(p);
+        p += sizeof(inotify_event) + e->len;
+        if (config_wd_ >= 0 && e->wd == config_wd_ && e->len &&
+            (config_name_ == e->name || std::string(e->name) == "..data")) {
+          LOG_INFO(kComp, "inotify: config file %s changed", cfg_.config_file.c_str());
+          std::string before = cfg_.ToJson();
+          if (ReloadConfig("config file changed") && cfg_.ToJson() != before) {
+            reinit_ = true;
+            *do_restart = true;
+          }
+          continue;
+        }
+        if (e->len && kubelet_name_ == e->name && (e->mask & (IN_CREATE | IN_MOVED_TO))) {
+          LOG_INFO(kComp, "inotify: %s created, restarting", kubelet_sock_.c_str());
+          backoff_ms_ = 1000;
+          *do_reregister = true;
+        }
+        // One of our own sockets removed from under us (not by our own Stop():
+        // those are re-created before this event is read, so stat finds them).
+        if (!e->len || !(e->mask & IN_DELETE)) continue;
+        // The HBM-cap shim's directory wiped (a kubelet cleaning its plugin
+        // directory): put it back for the next memory-unit pod.
+        if (!v_.popts.memcap_host_path.empty() && std::string(e->name) == "amdgpu-dp") {
+          LOG_WARN(kComp, "inotify: %s was removed; reinstalling", v_.popts.memcap_host_path.c_str());
+          InstallMemcap(cfg_.flags);
+          if (!v_.popts.memcap_preload_list.empty()) InstallPreloadList(cfg_.flags);
+          for (auto& pl : plugins_)
+            if (Status gs = pl->InstallGrantFiles(); !gs.ok()) LOG_ERROR(kComp, "%s", gs.ToString().c_str());
+        }
+        for (auto& pl : plugins_) {
+          struct stat st;
+          if (!pl->running() || BaseName(pl->socket_path()) != e->name) continue;
+          if (stat(pl->socket_path().c_str(), &st) != 0) {
+            // Another instance unlinks the path and binds it microseconds
+            // later: look again after a moment (rfd_) before taking it back
+            // -- without sleeping here, so signals and kubelet events are
+            // not held up meanwhile.
+            recheck_sockets_.insert(pl->socket_path());
+            ArmTimer(rfd_, kSocketRecheckMs);
+          } else if (!pl->owns_socket()) {
+            StandBy(*pl);
+          }
+        }
+      }
+    }
+  }
+
+  void OnSignals(bool* do_restart) {
+    signalfd_siginfo si;
+    while (read(sfd_, &si, sizeof(si)) == sizeof(si)) {
+      if (si.ssi_signo == SIGHUP) {
+        LOG_INFO(kComp, "received SIGHUP, restarting");
+        ReloadConfig("SIGHUP");
+        // The monitor is stopped first so it cannot write the old verdicts back.
+        if (monitor_) monitor_->Stop();
+        ledger_.Reload();
+        reinit_ = true;
+        *do_restart = true;
+      } else if (si.ssi_signo == SIGUSR1) {
+        // Explicitly requested: printed whatever the log level.
+        for (auto& p : plugins_) Logf(LogLevel::kInfo, kComp, "stats: %s", p->StatsJson().c_str());
+        Logf(LogLevel::kInfo, kComp, "health: %s", health_counters_.Json().c_str());
+      } else {
+        LOG_INFO(kComp, "received signal %s, shutting down", strsignal(static_cast<int>(si.ssi_signo)));
+        quit_ = true;
+      }
+    }
+  }
+
+  Config cfg_;  // replaced on a successful reload
+  Validated v_;
+  std::function<Result<Config>()> reload_;
+  smi::Library* lib_;
+  const int sfd_;
+  int ep_ = -1, ifd_ = -1, tfd_ = -1, efd_ = -1, lfd_ = -1, rfd_ = -1;
+  std::string kubelet_sock_, kubelet_name_;
+  int config_wd_ = -1;
+  std::string config_name_;
+  // Plugin sockets found deleted, looked at again when rfd_ fires.
+  std::set<std::string> recheck_sockets_;
+
+  std::vector<std::unique_ptr<plugin::Plugin>> plugins_;
+  // The metrics thread reads plugins_; the vector is only changed under this
+  // lock (plugin objects themselves are safe to read while they start/stop).
+  std::mutex plugins_mu_;
+  std::atomic<uint64_t> restarts_{0};
+  std::atomic<bool> serving_{false};
+  std::unique_ptr<health::Monitor> monitor_;
+  // Health verdicts outlive every plugin generation (and, with a state file,
+  // the process): a restart must not re-advertise a failed GPU as Healthy.
+  health::Ledger ledger_;
+  health::HealthCounters health_counters_;
+  int backoff_ms_ = 1000;
+  int exit_code_ = 0;
+  bool quit_ = false;
+  // Re-initialise amdsmi before the next enumeration (SIGHUP, a detected
+  // re-partition, or a retry): a re-partitioned GPU gets new processor handles.
+  bool reinit_ = false;
+  // The running generation's node snapshot and plugin specs: a kubelet restart
+  // re-registers the same plugins without re-enumerating or restarting the
+  // health monitor (whose amdsmi event wait cannot be interrupted).
+  std::shared_ptr<const inventory::Snapshot> cur_snap_;
+  std::vector<strategy::PluginSpec> cur_specs_;
+  std::unique_ptr<memcap::DriverHbmMonitor> driver_hbm_;
+  std::mutex access_mu_;  // node_access_, metrics_gpus_: written by Restart, read by /metrics
+  std::vector<inventory::NodeAccess> node_access_;
+  std::vector<std::pair<std::string, std::string>> metrics_gpus_;  // (ledger key, bdf) of the served GPUs
+  const std::string usage_dir_;  // grant accounting files (the plugin directory is a startup-only flag)
+  std::string smi_version_;
+  std::unique_ptr<metrics::HttpServer> http_;
+  std::unique_ptr<podresources::CachedLister> pod_lister_;
+  int64_t stall_ms_ = 60000;
+  std::atomic<bool> stall_logged_{false};
+};
+
 }  // namespace
 
 int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload) {
-  Config cfg = startup_cfg;  // replaced on a successful reload
-  auto validated = Validate(cfg);
+  auto validated = Validate(startup_cfg);
   if (!validated.ok()) {
     LOG_ERROR(kComp, "unable to validate flags: %s", validated.status().message().c_str());
     return 1;
   }
   Validated v = std::move(*validated);
+  const Config& cfg = startup_cfg;
   // The relay's liveness probe runs every 30 s: no config dump, no amdsmi.
   if (cfg.flags.relay_ping) return health::PingRelay(cfg.flags.health_event_socket, 5000);
   LOG_INFO(kComp, "running with config:\n%s", cfg.ToJson().c_str());
   LOG_INFO(kComp, "running with resource config: %s", v.rc.ToJson().c_str());
-
   if (cfg.flags.list_grants) return ListGrants(PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage"));
 
   // Signals are consumed through a signalfd; block them before any thread starts.
@@ -202,8 +815,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
       signalfd_siginfo si;
       pollfd p{sfd, POLLIN, 0};
       poll(&p, 1, -1);
-      if (read(sfd, &si, sizeof(si)) == sizeof(si) && si.ssi_signo != SIGHUP && si.ssi_signo != SIGUSR1)
-        return 0;
+      if (read(sfd, &si, sizeof(si)) == sizeof(si) && si.ssi_signo != SIGHUP && si.ssi_signo != SIGUSR1) return 0;
     }
   }
   LOG_INFO(kComp, "amdsmi %s loaded from %s", (*lib)->Version().c_str(), (*lib)->path().c_str());
@@ -214,665 +826,17 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     return Doctor(lib->get(), v, cfg, d);
   }
   if (!cfg.flags.drain.empty() || !cfg.flags.undrain.empty()) return DrainCommand(lib->get(), v, cfg);
-  if (cfg.flags.event_relay) return health::RunEventRelay(lib->get(), cfg.flags.health_event_socket, sfd,
-                                                      {cfg.flags.driver_root, cfg.flags.host_proc,
-                                                       cfg.flags.kfd_proc_dir});
-
-  std::string kubelet_sock =
-      v.popts.kubelet_socket.empty() ? PathJoin(v.popts.plugin_dir, "kubelet.sock") : v.popts.kubelet_socket;
-  std::string watch_dir = kubelet_sock.substr(0, kubelet_sock.rfind('/'));
-  if (watch_dir.empty()) watch_dir = "/";
-  std::string kubelet_name = BaseName(kubelet_sock);
-  LOG_INFO(kComp, "starting FS watcher on %s", watch_dir.c_str());
-  int ifd = inotify_init1(IN_NONBLOCK | IN_CLOEXEC);
-  if (ifd < 0 || inotify_add_watch(ifd, watch_dir.c_str(), IN_CREATE | IN_MOVED_TO | IN_DELETE) < 0) {
-    LOG_ERROR(kComp, "failed to create FS watcher on %s: %s", watch_dir.c_str(), strerror(errno));
-    return 1;
+  if (cfg.flags.event_relay)
+    return health::RunEventRelay(lib->get(), cfg.flags.health_event_socket, sfd,
+                                 {cfg.flags.driver_root, cfg.flags.host_proc, cfg.flags.kfd_proc_dir});
+  int rc;
+  {
+    Supervisor s(cfg, std::move(v), std::move(reload), lib->get(), sfd);
+    rc = s.Run();
   }
-  if (PathJoin(v.popts.plugin_dir, "") != PathJoin(watch_dir, ""))
-    inotify_add_watch(ifd, v.popts.plugin_dir.c_str(), IN_DELETE);
-  // Config file: watch its directory (editors and ConfigMap updates replace the
-  // file rather than writing it in place).
-  int config_wd = -1;
-  std::string config_name;
-  if (reload && !cfg.config_file.empty()) {
-    std::string dir = cfg.config_file.substr(0, cfg.config_file.rfind('/') + 1);
-    if (dir.empty()) dir = ".";
-    config_name = BaseName(cfg.config_file);
-    config_wd = inotify_add_watch(ifd, dir.c_str(), IN_CLOSE_WRITE | IN_MOVED_TO | IN_CREATE);
-    if (config_wd < 0) LOG_WARN(kComp, "cannot watch config file %s: %s", cfg.config_file.c_str(), strerror(errno));
-  }
-  int tfd = timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC | TFD_NONBLOCK);
-  int efd = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
-  int lfd = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);  // health monitor: partition layout changed
-  // One-shot: look again at plugin sockets deleted from under us (recheck_sockets).
-  int rfd = timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC | TFD_NONBLOCK);
-  int ep = epoll_create1(EPOLL_CLOEXEC);
-  for (int fd : {sfd, ifd, tfd, efd, lfd, rfd}) {
-    epoll_event ev{};
-    ev.events = EPOLLIN;
-    ev.data.fd = fd;
-    epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev);
-  }
-  // Plugin sockets found deleted, looked at again when rfd fires.
-  std::set<std::string> recheck_sockets;
-  const int kSocketRecheckMs = [] {  // test hook: widens the window (default 20 ms)
-    const char* e = getenv("ADP_DEBUG_SOCKET_RECHECK_MS");
-    return e && atoi(e) > 0 ? atoi(e) : 20;
-  }();
-  auto stand_by = [](const plugin::Plugin& pl) {
-    // Another instance (a rollout with maxSurge) unlinked ours and bound the
-    // path: binding it back would start a tug of war. The kubelet now talks to
-    // that instance; this one stands by until the kubelet restarts or the file
-    // disappears again.
-    LOG_WARN(kComp, "inotify: %s now belongs to another process; '%s' stands by", pl.socket_path().c_str(),
-             pl.resource_name().c_str());
-  };
-
-
-  std::vector<std::unique_ptr<plugin::Plugin>> plugins;
-  // The metrics thread reads `plugins`; the vector is only changed under this
-  // lock (plugin objects themselves are safe to read while they start/stop).
-  std::mutex plugins_mu;
-  std::atomic<uint64_t> restarts{0};
-  std::atomic<bool> serving{false};
-  std::unique_ptr<health::Monitor> monitor;
-  // Health verdicts outlive every plugin generation (and, with a state file,
-  // the process): a restart must not re-advertise a failed GPU as Healthy.
-  health::Ledger ledger(cfg.flags.health_state_file);
-  health::HealthCounters health_counters;
-  int backoff_ms = 1000;
-  int exit_code = 0;
-  bool quit = false;
-  // Re-initialise amdsmi before the next enumeration (SIGHUP, a detected
-  // re-partition, or a retry): a re-partitioned GPU gets new processor handles.
-  bool reinit = false;
-  // The running generation's node snapshot and plugin specs: a kubelet restart
-  // re-registers the same plugins without re-enumerating or restarting the
-  // health monitor (whose amdsmi event wait cannot be interrupted).
-  std::shared_ptr<const inventory::Snapshot> cur_snap;
-  std::vector<strategy::PluginSpec> cur_specs;
-
-  // Driver-side check of enforced HBM grants (--driver-hbm-poll-ms): started
-  // with the first generation that enforces grants into an accounting dir.
-  std::unique_ptr<memcap::DriverHbmMonitor> driver_hbm;
-  std::mutex access_mu;  // node_access, metrics_gpus: written by restart, read by /metrics
-  std::vector<inventory::NodeAccess> node_access;
-  std::vector<std::pair<std::string, std::string>> metrics_gpus;  // (ledger key, bdf) of the served GPUs
-  const std::string usage_dir = PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage");  // startup-only flag
-  std::unique_ptr<metrics::HttpServer> http;
-  std::unique_ptr<podresources::CachedLister> pod_lister;
-  if (!cfg.flags.metrics_addr.empty() && !cfg.flags.pod_resources_socket.empty())
-    pod_lister = std::make_unique<podresources::CachedLister>(cfg.flags.pod_resources_socket,
-                                                              std::chrono::milliseconds(2000));
-  // (env only: how long the health loop may go without an iteration before /healthz fails)
-  const int64_t stall_ms = [] {
-    const char* e = getenv("ADP_HEALTH_STALL_MS");
-    return e && atoll(e) > 0 ? static_cast<int64_t>(atoll(e)) : int64_t{60000};
-  }();
-  std::atomic<bool> stall_logged{false};
-  if (!cfg.flags.metrics_addr.empty()) {
-    std::string smi_version = (*lib)->Version();
-    http = std::make_unique<metrics::HttpServer>(
-        [&, smi_version] {
-          std::string out =
-              "# HELP amdgpu_dp_build_info Plugin and amdsmi versions.\n"
-              "# TYPE amdgpu_dp_build_info gauge\n"
-              "amdgpu_dp_build_info{version=\"" ADP_VERSION "\",amdsmi=\"" +
-              metrics::LabelValue(smi_version) +
-              "\"} 1\n"
-              "# HELP amdgpu_dp_restarts_total Plugin (re)starts: kubelet restart, SIGHUP, retries.\n"
-              "# TYPE amdgpu_dp_restarts_total counter\n"
-              "amdgpu_dp_restarts_total " + std::to_string(restarts.load()) + "\n"
-              "# HELP amdgpu_dp_health_events_enabled 1 if amdsmi event notification is registered (-1 not started).\n"
-              "# TYPE amdgpu_dp_health_events_enabled gauge\n"
-              "amdgpu_dp_health_events_enabled " + std::to_string(health_counters.events_enabled.load()) + "\n"
-              "# HELP amdgpu_dp_health_loop_age_seconds Time since the health monitor loop last iterated (0 when "
-              "none runs; /healthz fails past ADP_HEALTH_STALL_MS).\n"
-              "# TYPE amdgpu_dp_health_loop_age_seconds gauge\n"
-              "amdgpu_dp_health_loop_age_seconds " + std::to_string(health_counters.HealthLoopAgeMs() / 1e3) + "\n"
-              "# HELP amdgpu_dp_health_polls_total Health polls (liveness + uncorrectable ECC) run.\n"
-              "# TYPE amdgpu_dp_health_polls_total counter\n"
-              "amdgpu_dp_health_polls_total " + std::to_string(health_counters.polls.load()) + "\n"
-              "# HELP amdgpu_dp_health_ecc_reads_total Uncorrectable-ECC reads by result.\n"
-              "# TYPE amdgpu_dp_health_ecc_reads_total counter\n"
-              "amdgpu_dp_health_ecc_reads_total{result=\"ok\"} " + std::to_string(health_counters.ecc_reads_ok.load()) + "\n"
-              "amdgpu_dp_health_ecc_reads_total{result=\"error\"} " + std::to_string(health_counters.ecc_read_errors.load()) + "\n"
-              "# HELP amdgpu_dp_health_events_total amdsmi events received.\n"
-              "# TYPE amdgpu_dp_health_events_total counter\n"
-              "amdgpu_dp_health_events_total " + std::to_string(health_counters.events_received.load()) + "\n"
-              "# HELP amdgpu_dp_health_retired_page_reads_total Retired-HBM-page reads by result.\n"
-              "# TYPE amdgpu_dp_health_retired_page_reads_total counter\n"
-              "amdgpu_dp_health_retired_page_reads_total{result=\"ok\"} " +
-              std::to_string(health_counters.retired_reads_ok.load()) + "\n"
-              "amdgpu_dp_health_retired_page_reads_total{result=\"error\"} " +
-              std::to_string(health_counters.retired_read_errors.load()) + "\n";
-          {
-            std::lock_guard<std::mutex> lk(access_mu);
-            // Why a GPU is Unhealthy, one series per failure cause (the ledger's bits).
-            static const std::pair<uint32_t, const char*> kCauses[] = {
-                {health::kFailEcc, "ecc"},           {health::kFailUnresponsive, "unresponsive"},
-                {health::kFailResetPending, "reset_pending"}, {health::kFailEvent, "event"},
-                {health::kFailRetiredPages, "retired_pages"}, {health::kFailDrained, "drained"}};
-            if (!metrics_gpus.empty())
-              out += "# HELP amdgpu_dp_gpu_failure 1 while the GPU is Unhealthy for this cause (drained: the "
-                     "operator's drain file, not a fault).\n"
-                     "# TYPE amdgpu_dp_gpu_failure gauge\n";
-            for (const auto& [key, bdf] : metrics_gpus) {
-              uint32_t bits = ledger.Get(key).fail;
-              for (const auto& [bit, cause] : kCauses)
-                out += "amdgpu_dp_gpu_failure{bdf=\"" + metrics::LabelValue(bdf) + "\",cause=\"" + cause + "\"} " +
-                       ((bits & bit) ? "1" : "0") + "\n";
-            }
-            if (!node_access.empty())
-              out += "# HELP amdgpu_dp_device_node_openable 1 if the plugin can open the device node (0: denied, "
-                     "e.g. by the container's device cgroup).\n"
-                     "# TYPE amdgpu_dp_device_node_openable gauge\n";
-            for (const auto& a : node_access)
-              out += "amdgpu_dp_device_node_openable{node=\"" + metrics::LabelValue(a.path) + "\"} " +
-                     (a.err ? "0" : "1") + "\n";
-          }
-          if (auto events = health_counters.EventCounts(); !events.empty()) {
-            out += "# HELP amdgpu_dp_gpu_events_total amdsmi events per GPU and type, ignored ones included "
-                   "(VMFAULT: an application's GPU page fault; THERMAL_THROTTLE; GPU_PRE_RESET / GPU_POST_RESET).\n"
-                   "# TYPE amdgpu_dp_gpu_events_total counter\n";
-            for (const auto& [k, n] : events)
-              out += "amdgpu_dp_gpu_events_total{bdf=\"" + metrics::LabelValue(k.first) + "\",type=\"" +
-                     metrics::LabelValue(k.second) + "\"} " + std::to_string(n) + "\n";
-          }
-          if (auto retired = health_counters.RetiredPages(); !retired.empty()) {
-            out += "# HELP amdgpu_dp_retired_pages HBM pages the driver retired (last health poll).\n"
-                   "# TYPE amdgpu_dp_retired_pages gauge\n";
-            for (const auto& [bdf, n] : retired)
-              out += "amdgpu_dp_retired_pages{bdf=\"" + metrics::LabelValue(bdf) + "\"} " + std::to_string(n) + "\n";
-          }
-          if (auto total = health_counters.VramTotal(); !total.empty()) {
-            out += "# HELP amdgpu_dp_gpu_hbm_total_bytes HBM of the GPU.\n"
-                   "# TYPE amdgpu_dp_gpu_hbm_total_bytes gauge\n";
-            for (const auto& [bdf, n] : total)
-              out += "amdgpu_dp_gpu_hbm_total_bytes{bdf=\"" + metrics::LabelValue(bdf) + "\"} " + std::to_string(n) + "\n";
-          }
-          if (auto used = health_counters.VramUsed(); !used.empty()) {
-            out += "# HELP amdgpu_dp_gpu_hbm_used_bytes HBM in use on the GPU, all processes (last health poll).\n"
-                   "# TYPE amdgpu_dp_gpu_hbm_used_bytes gauge\n";
-            for (const auto& [bdf, n] : used)
-              out += "amdgpu_dp_gpu_hbm_used_bytes{bdf=\"" + metrics::LabelValue(bdf) + "\"} " + std::to_string(n) + "\n";
-          }
-          // Ask the kubelet who holds which device (cached; outside the plugins lock).
-          Result<std::vector<podresources::Assignment>> assigned = Unavailable("off");
-          if (pod_lister) {
-            assigned = pod_lister->Get();
-            out += "# HELP amdgpu_dp_pod_resources_up 1 if the kubelet PodResources API answered.\n"
-                   "# TYPE amdgpu_dp_pod_resources_up gauge\n"
-                   "amdgpu_dp_pod_resources_up " + std::string(assigned.ok() ? "1" : "0") + "\n";
-          }
-          // Grant accounting files: read (and old ones collected) here, before
-          // the plugins lock the health listener also takes -- a slow
-          // filesystem must not hold up health verdicts.
-          std::vector<memcap::Usage> grant_files;
-          bool have_grants = false;
-          {
-            struct stat st;
-            if (stat(usage_dir.c_str(), &st) == 0 && S_ISDIR(st.st_mode)) {
-              have_grants = true;
-              grant_files = memcap::ReadAll(usage_dir);
-              std::set<std::string> live;
-              if (assigned.ok()) {
-                std::map<std::tuple<std::string, std::string, std::string, std::string>,
-                         std::vector<std::string_view>> ctrs;
-                for (const auto& a : *assigned) ctrs[{a.ns, a.pod, a.container, a.resource}].push_back(a.device_id);
-                for (const auto& [k, ids] : ctrs) live.insert(memcap::AllocationKey(ids));
-              }
-              memcap::Collect(usage_dir, assigned.ok() ? &live : nullptr, 120, 4096);
-            }
-          }
-          std::unique_ptr<memcap::DriverHbmMonitor::Snapshot> dsnap;
-          if (driver_hbm) {
-            dsnap = std::make_unique<memcap::DriverHbmMonitor::Snapshot>(driver_hbm->Get());
-            out += "# HELP amdgpu_dp_driver_hbm_polls_total Driver-side HBM scans run (DRM fdinfo of every process).\n"
-                   "# TYPE amdgpu_dp_driver_hbm_polls_total counter\n"
-                   "amdgpu_dp_driver_hbm_polls_total " + std::to_string(dsnap->polls) + "\n"
-                   "# HELP amdgpu_dp_driver_hbm_unreadable_processes Processes whose file descriptors the plugin "
-                   "may not read (their HBM is not seen).\n"
-                   "# TYPE amdgpu_dp_driver_hbm_unreadable_processes gauge\n"
-                   "amdgpu_dp_driver_hbm_unreadable_processes " + std::to_string(dsnap->scan.fd_dirs_unreadable) + "\n"
-                   "# HELP amdgpu_dp_driver_hbm_scan_processes Processes the last driver-side scan read (the GPU "
-                   "processes KFD lists, or every process without that list).\n"
-                   "# TYPE amdgpu_dp_driver_hbm_scan_processes gauge\n"
-                   "amdgpu_dp_driver_hbm_scan_processes{source=\"" + dsnap->scan.pid_source + "\"} " +
-                   std::to_string(dsnap->scan.pids_scanned) + "\n"
-                   "# HELP amdgpu_dp_driver_hbm_scan_descriptors File descriptors the last driver-side scan examined.\n"
-                   "# TYPE amdgpu_dp_driver_hbm_scan_descriptors gauge\n"
-                   "amdgpu_dp_driver_hbm_scan_descriptors " + std::to_string(dsnap->scan.fd_entries) + "\n"
-                   "# HELP amdgpu_dp_driver_hbm_scan_seconds Wall time of the last driver-side scan.\n"
-                   "# TYPE amdgpu_dp_driver_hbm_scan_seconds gauge\n"
-                   "amdgpu_dp_driver_hbm_scan_seconds " + std::to_string(dsnap->last_scan_ns / 1e9) + "\n"
-                   "# HELP amdgpu_dp_driver_hbm_scan_failures_total Driver-side scans the event relay could not "
-                   "run (the previous scan stays in effect).\n"
-                   "# TYPE amdgpu_dp_driver_hbm_scan_failures_total counter\n"
-                   "amdgpu_dp_driver_hbm_scan_failures_total " + std::to_string(dsnap->scan_failures) + "\n"
-                   "# HELP amdgpu_dp_hbm_over_grant_events_total Transitions of any grant to over its HBM by the "
-                   "driver's count.\n"
-                   "# TYPE amdgpu_dp_hbm_over_grant_events_total counter\n"
-                   "amdgpu_dp_hbm_over_grant_events_total " + std::to_string(dsnap->over_total) + "\n";
-            out += "# HELP amdgpu_dp_gpu_hbm_driver_bytes HBM every process holds on the GPU by the driver's count.\n"
-                   "# TYPE amdgpu_dp_gpu_hbm_driver_bytes gauge\n";
-            for (const auto& [bdf, n] : dsnap->scan.total)
-              out += "amdgpu_dp_gpu_hbm_driver_bytes{bdf=\"" + metrics::LabelValue(bdf) + "\"} " + std::to_string(n) + "\n";
-            out += "# HELP amdgpu_dp_gpu_hbm_unattributed_bytes HBM on the GPU held by processes outside every "
-                   "enforced grant (no grant file mapped, no grant in their cgroup).\n"
-                   "# TYPE amdgpu_dp_gpu_hbm_unattributed_bytes gauge\n";
-            for (const auto& [bdf, n] : dsnap->scan.unattributed)
-              out += "amdgpu_dp_gpu_hbm_unattributed_bytes{bdf=\"" + metrics::LabelValue(bdf) + "\"} " +
-                     std::to_string(n) + "\n";
-          }
-          std::lock_guard<std::mutex> lk(plugins_mu);
-          std::vector<const plugin::Plugin*> ps;
-          for (auto& p : plugins)
-            if (p->device_count() > 0) ps.push_back(p.get());
-          plugin::Plugin::AppendPrometheus(ps, &out, assigned.ok() ? &*assigned : nullptr, dsnap.get(),
-                                           have_grants ? &grant_files : nullptr);
-          return out;
-        },
-        [&, stall_ms] {
-          if (!serving.load()) return false;
-          // A health loop stuck in a call that never returns (an amdsmi event
-          // wait or query) stops advancing: the liveness probe restarts us.
-          if (int64_t age = health_counters.HealthLoopAgeMs(); age > stall_ms) {
-            if (!stall_logged.exchange(true))
-              LOG_ERROR(kComp, "the health monitor has not advanced for %lld ms: /healthz fails",
-                        static_cast<long long>(age));
-            return false;
-          }
-          stall_logged.store(false);
-          std::lock_guard<std::mutex> lk(plugins_mu);
-          for (auto& p : plugins)
-            if (p->device_count() > 0 && !p->running()) return false;
-          return true;
-        },
-        [&] {  // GET /stats: what SIGUSR1 logs, as one JSON document
-          std::string out = "{\"plugins\": [";
-          {
-            std::lock_guard<std::mutex> lk(plugins_mu);
-            for (size_t i = 0; i < plugins.size(); ++i) out += (i ? ", " : "") + plugins[i]->StatsJson();
-          }
-          return out + "], \"health\": " + health_counters.Json() + ", \"restarts\": " +
-                 std::to_string(restarts.load()) + "}\n";
-        });
-    Status ms = http->Start(cfg.flags.metrics_addr);
-    if (!ms.ok()) {
-      LOG_ERROR(kComp, "%s", ms.ToString().c_str());
-      return 1;
-    }
-  }
-
-  auto stop_all = [&] {
-    serving.store(false);
-    if (monitor) monitor->Stop();
-    monitor.reset();
-    for (auto& p : plugins) p->Stop();
-    std::lock_guard<std::mutex> lk(plugins_mu);
-    plugins.clear();
-  };
-
-  auto schedule_retry = [&](const char* why) {
-    LOG_WARN(kComp, "%s; retrying in %d ms", why, backoff_ms);
-    ArmTimer(tfd, backoff_ms);
-    backoff_ms = std::min(kMaxBackoffMs, backoff_ms * 2);
-  };
-
-  // Starts (serves + registers) every plugin with devices; the number started,
-  // or -1 after scheduling a retry because the kubelet could not be reached.
-  auto start_plugins = [&]() -> int {
-    int started = 0;
-    for (auto& p : plugins) {
-      if (p->device_count() == 0) continue;
-      Status st = p->Start([efd] {
-        uint64_t one = 1;
-        ssize_t w = write(efd, &one, sizeof(one));
-        (void)w;
-      });
-      if (!st.ok()) {
-        LOG_ERROR(kComp, "could not contact kubelet, retrying (is the device-plugin feature "
-                         "enabled and is %s present?)", kubelet_sock.c_str());
-        schedule_retry("plugin start failed");
-        return -1;
-      }
-      ++started;
-    }
-    backoff_ms = 1000;
-    serving.store(true);
-    return started;
-  };
-
-  // Creates this generation's plugins and applies the failures recorded by
-  // earlier generations, in ONE critical section with the health listener
-  // (plugins_mu): the monitor writes the ledger before it notifies, so a
-  // verdict that changes concurrently is either in the ledger read here or
-  // notified to the new plugins afterwards -- a GPU_POST_RESET racing a
-  // re-registration can never leave a recovered GPU advertised Unhealthy.
-  const int reregister_delay_ms = [] {  // test hook: widens the window the lock closes
-    const char* e = getenv("ADP_DEBUG_PUBLISH_DELAY_MS");
-    return e ? atoi(e) : 0;
-  }();
-  auto publish_plugins = [&](const std::shared_ptr<const inventory::Snapshot>& snap,
-                             const std::vector<strategy::PluginSpec>& specs, bool apply_ledger) {
-    std::lock_guard<std::mutex> lk(plugins_mu);
-    for (const auto& s : specs) plugins.push_back(std::make_unique<plugin::Plugin>(snap, s, v.popts));
-    WarnSharedDeviceLists(plugins);
-    if (!apply_ledger) return;
-    auto failed = ledger.Failed(*snap);
-    if (reregister_delay_ms > 0) usleep(static_cast<useconds_t>(reregister_delay_ms) * 1000);
-    for (const auto& [gpu, why] : failed) {
-      LOG_WARN(kComp, "GPU %s is unhealthy since an earlier plugin generation: %s", snap->gpus[gpu].bdf.c_str(),
-               why.c_str());
-      for (auto& p : plugins) p->SetGpuHealth(gpu, false, why);
-    }
-  };
-
-  auto restart = [&] {
-    stop_all();
-    ArmTimer(tfd, 0);  // disarm
-    ArmTimer(rfd, 0);
-    recheck_sockets.clear();
-    if (reinit) {
-      Status rs = (*lib)->Reinit();
-      if (!rs.ok()) {
-        LOG_ERROR(kComp, "amdsmi re-initialisation failed: %s", rs.ToString().c_str());
-        schedule_retry("amdsmi re-init failed");
-        return;
-      }
-      reinit = false;
-      LOG_INFO(kComp, "amdsmi re-initialised");
-    }
-    LOG_INFO(kComp, "retrieving plugins");
-    auto snap = inventory::BuildSnapshot(lib->get(), v.bopts);
-    if (!snap.ok()) {
-      LOG_ERROR(kComp, "device enumeration failed: %s", snap.status().ToString().c_str());
-      reinit = true;
-      schedule_retry("enumeration failed");
-      return;
-    }
-    if (!cfg.flags.node_labels_file.empty()) WriteLabels(cfg.flags.node_labels_file, **snap);
-    {
-      auto access = inventory::ProbeDeviceAccess(**snap, cfg.flags.driver_root);
-      std::string what = inventory::DescribeAccess(access);
-      if (what == "ok") LOG_INFO(kComp, "device access: %zu node(s) openable", access.size());
-      else LOG_WARN(kComp, "device access: %s", what.c_str());
-      std::lock_guard<std::mutex> lk(access_mu);
-      node_access = std::move(access);
-      metrics_gpus.clear();
-      for (const auto& g : (*snap)->gpus) metrics_gpus.emplace_back(health::Ledger::KeyOf(g), g.bdf);
-    }
-    auto specs = strategy::BuildPluginSpecs(**snap, v.partition, v.rc, cfg.flags.resource_prefix);
-    if (!specs.ok()) {
-      LOG_ERROR(kComp, "error creating partition strategy: %s", specs.status().message().c_str());
-      exit_code = 1;
-      quit = true;
-      return;
-    }
-    restarts.fetch_add(1);
-    cur_snap = *snap;
-    cur_specs = *specs;
-    for (const auto& g : cur_snap->gpus) health_counters.SetVramTotal(g.bdf, g.vram_mib << 20);
-    v.popts.memcap_host_path = cfg.flags.enforce_memory_units ? InstallMemcap(cfg.flags) : "";
-    v.popts.memcap_preload_list = !v.popts.memcap_host_path.empty() && cfg.flags.memcap_ld_so_preload
-                                      ? InstallPreloadList(cfg.flags)
-                                      : "";
-    v.popts.memcap_usage_dir = !v.popts.memcap_host_path.empty() && cfg.flags.container_hbm_metrics &&
-                                       !cfg.flags.metrics_addr.empty()
-                                   ? PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage")
-                                   : "";
-    if (!driver_hbm && !v.popts.memcap_usage_dir.empty() && cfg.flags.driver_hbm_poll_ms > 0) {
-      memcap::DriverHbmMonitor::Options dopt;
-      dopt.proc_root = cfg.flags.host_proc;
-      dopt.kfd_proc_dir = cfg.flags.kfd_proc_dir;
-      // With an event relay the scan runs there (it holds the privilege to
-      // read other containers' descriptors; this daemon then needs none).
-      dopt.relay_socket = cfg.flags.health_event_socket;
-      dopt.usage_dir = v.popts.memcap_usage_dir;
-      dopt.poll_ms = static_cast<int>(std::min<uint64_t>(cfg.flags.driver_hbm_poll_ms, 3600000));
-      dopt.slack_bytes = cfg.flags.driver_hbm_slack_mib << 20;
-      std::string dir = v.popts.memcap_usage_dir;
-      driver_hbm = std::make_unique<memcap::DriverHbmMonitor>(dopt, [&plugins, &plugins_mu, dir] {
-        // The accounting files are read before taking the lock the health
-        // listener needs (as /metrics does): only ID lookups run under it.
-        std::vector<memcap::Usage> files = memcap::ReadAll(dir);
-        std::lock_guard<std::mutex> lk(plugins_mu);
-        std::vector<const plugin::Plugin*> ps;
-        for (auto& p : plugins) ps.push_back(p.get());
-        return plugin::Plugin::GrantedByKey(ps, files);
-      });
-      driver_hbm->Start();
-    }
-    health::HealthConfig hcfg = health::HealthConfig::FromEnv();
-    hcfg.events = cfg.flags.health_events;
-    hcfg.drain_file = cfg.flags.drain_file;
-    hcfg.driver_root = cfg.flags.driver_root;
-    hcfg.event_relay = cfg.flags.health_event_socket;
-    publish_plugins(*snap, *specs, !hcfg.disabled);
-    int started = start_plugins();
-    if (started < 0) return;
-    if (started == 0) LOG_INFO(kComp, "no devices found; waiting indefinitely");
-    monitor = std::make_unique<health::Monitor>(lib->get(), *snap, hcfg, &ledger, &health_counters);
-    monitor->SetLayoutListener([lfd](const std::string&) {
-      uint64_t one = 1;
-      ssize_t w = write(lfd, &one, sizeof(one));
-      (void)w;
-    });
-    // Verdicts go to whichever plugins are serving (re-registration replaces them).
-    monitor->AddListener([&plugins, &plugins_mu](int gpu, bool ok, const std::string& why) {
-      std::lock_guard<std::mutex> lk(plugins_mu);
-      for (auto& p : plugins) p->SetGpuHealth(gpu, ok, why);
-    });
-    Status hs = monitor->Start();
-    if (!hs.ok()) LOG_WARN(kComp, "health monitor: %s", hs.ToString().c_str());
-  };
-
-  // Kubelet restarted (or our socket vanished): same devices, same health
-  // monitor; only the plugins are replaced and register again.
-  auto reregister = [&] {
-    if (!monitor || !cur_snap) {
-      restart();
-      return;
-    }
-    serving.store(false);
-    ArmTimer(tfd, 0);
-    ArmTimer(rfd, 0);
-    recheck_sockets.clear();
-    for (auto& p : plugins) p->Stop();
-    {
-      std::lock_guard<std::mutex> lk(plugins_mu);
-      plugins.clear();
-    }
-    restarts.fetch_add(1);
-    LOG_INFO(kComp, "re-registering plugins (devices and health monitor unchanged)");
-    if (cfg.flags.enforce_memory_units) v.popts.memcap_host_path = InstallMemcap(cfg.flags);
-    if (!v.popts.memcap_preload_list.empty()) v.popts.memcap_preload_list = InstallPreloadList(cfg.flags);
-    publish_plugins(cur_snap, cur_specs, !health::HealthConfig::FromEnv().disabled);
-    start_plugins();
-  };
-
-  // Re-reads flags/env/file; on success adopts the new config (startup-bound
-  // settings excepted). Returns false when the new config is invalid.
-  auto reload_config = [&](const char* why) -> bool {
-    if (!reload) return true;
-    auto next = reload();
-    if (!next.ok()) {
-      LOG_ERROR(kComp, "%s: config not reloaded: %s", why, next.status().message().c_str());
-      return false;
-    }
-    for (const auto& w : next->warnings) LOG_WARN(kComp, "%s: %s", why, w.c_str());
-    auto nv = Validate(*next);
-    if (!nv.ok()) {
-      LOG_ERROR(kComp, "%s: config not reloaded: %s", why, nv.status().message().c_str());
-      return false;
-    }
-    const Flags& was = cfg.flags;
-    const Flags& now = next->flags;
-    if (now.amdsmi_lib != was.amdsmi_lib || now.metrics_addr != was.metrics_addr ||
-        now.pod_resources_socket != was.pod_resources_socket || now.node_labels_file != was.node_labels_file ||
-        now.plugin_dir != was.plugin_dir || now.kubelet_socket != was.kubelet_socket ||
-        now.health_state_file != was.health_state_file)
-      LOG_WARN(kComp, "%s: amdsmiLib, metricsAddr, podResourcesSocket, nodeLabelsFile, devicePluginPath, "
-                      "kubeletSocket and healthStateFile apply at startup only", why);
-    std::string old_json = cfg.ToJson();
-    Config merged = *next;
-    merged.flags.amdsmi_lib = was.amdsmi_lib;
-    merged.flags.metrics_addr = was.metrics_addr;
-    merged.flags.pod_resources_socket = was.pod_resources_socket;
-    merged.flags.node_labels_file = was.node_labels_file;
-    merged.flags.plugin_dir = was.plugin_dir;
-    merged.flags.kubelet_socket = was.kubelet_socket;
-    merged.flags.health_state_file = was.health_state_file;
-    auto mv = Validate(merged);
-    if (!mv.ok()) return false;
-    if (merged.ToJson() != old_json) {
-      cfg = std::move(merged);
-      v = std::move(*mv);
-      LOG_INFO(kComp, "%s: reloaded config:\n%s", why, cfg.ToJson().c_str());
-      LOG_INFO(kComp, "running with resource config: %s", v.rc.ToJson().c_str());
-    }
-    return true;
-  };
-
-  restart();
-  while (!quit) {
-    epoll_event events[8];
-    int n = epoll_wait(ep, events, 8, -1);
-    if (n < 0) {
-      if (errno == EINTR) continue;
-      LOG_ERROR(kComp, "epoll_wait: %s", strerror(errno));
-      exit_code = 1;
-      break;
-    }
-    bool do_restart = false;
-    bool do_reregister = false;  // a lighter restart: see reregister
-    for (int i = 0; i < n && !quit; ++i) {
-      int fd = events[i].data.fd;
-      if (fd == tfd) {
-        uint64_t exp;
-        ssize_t r = read(tfd, &exp, sizeof(exp));
-        (void)r;
-        do_restart = true;
-      } else if (fd == rfd) {
-        uint64_t exp;
-        ssize_t r = read(rfd, &exp, sizeof(exp));
-        (void)r;
-        for (auto& pl : plugins) {
-          if (!recheck_sockets.count(pl->socket_path()) || !pl->running()) continue;
-          struct stat st;
-          if (stat(pl->socket_path().c_str(), &st) != 0) {
-            LOG_WARN(kComp, "inotify: %s was removed, restarting", pl->socket_path().c_str());
-            do_reregister = true;
-          } else if (!pl->owns_socket()) {
-            stand_by(*pl);
-          }
-        }
-        recheck_sockets.clear();
-      } else if (fd == efd) {
-        uint64_t x;
-        ssize_t r = read(efd, &x, sizeof(x));
-        (void)r;
-        LOG_ERROR(kComp, "a gRPC server exhausted its crash budget; exiting");
-        exit_code = 1;
-        quit = true;
-      } else if (fd == lfd) {
-        uint64_t x;
-        ssize_t r = read(lfd, &x, sizeof(x));
-        (void)r;
-        LOG_INFO(kComp, "partition layout changed, re-enumerating");
-        reinit = true;
-        do_restart = true;
-      } else if (fd == ifd) {
-        char buf[4096] __attribute__((aligned(__alignof__(inotify_event))));
-        ssize_t len;
-        while ((len = read(ifd, buf, sizeof(buf))) > 0) {
-          for (char* p = buf; p < buf + len;) {
-            auto* e = reinterpret_cast<inotify_event*>(p);
-            if (config_wd >= 0 && e->wd == config_wd && e->len &&
-                (config_name == e->name || std::string(e->name) == "..data")) {
-              LOG_INFO(kComp, "inotify: config file %s changed", cfg.config_file.c_str());
-              std::string before = cfg.ToJson();
-              if (reload_config("config file changed") && cfg.ToJson() != before) {
-                reinit = true;
-                do_restart = true;
-              }
-              p += sizeof(inotify_event) + e->len;
-              continue;
-            }
-            if (e->len && kubelet_name == e->name && (e->mask & (IN_CREATE | IN_MOVED_TO))) {
-              LOG_INFO(kComp, "inotify: %s created, restarting", kubelet_sock.c_str());
-              backoff_ms = 1000;
-              do_reregister = true;
-            }
-            // One of our own sockets removed from under us (not by our own Stop():
-            // those are re-created before this event is read, so stat finds them).
-            if (e->len && (e->mask & IN_DELETE)) {
-              // The HBM-cap shim's directory wiped (a kubelet cleaning its
-              // plugin directory): put it back for the next memory-unit pod.
-              if (!v.popts.memcap_host_path.empty() && std::string(e->name) == "amdgpu-dp") {
-                LOG_WARN(kComp, "inotify: %s was removed; reinstalling", v.popts.memcap_host_path.c_str());
-                InstallMemcap(cfg.flags);
-                if (!v.popts.memcap_preload_list.empty()) InstallPreloadList(cfg.flags);
-                for (auto& pl : plugins)
-                  if (Status gs = pl->InstallGrantFiles(); !gs.ok())
-                    LOG_ERROR(kComp, "%s", gs.ToString().c_str());
-              }
-              for (auto& pl : plugins) {
-                struct stat st;
-                if (!pl->running() || BaseName(pl->socket_path()) != e->name) continue;
-                if (stat(pl->socket_path().c_str(), &st) != 0) {
-                  // Another instance unlinks the path and binds it microseconds
-                  // later: look again after a moment (rfd) before taking it back
-                  // -- without sleeping here, so signals and kubelet events
-                  // are not held up meanwhile.
-                  recheck_sockets.insert(pl->socket_path());
-                  ArmTimer(rfd, kSocketRecheckMs);
-                } else if (!pl->owns_socket()) {
-                  stand_by(*pl);
-                }
-              }
-            }
-            p += sizeof(inotify_event) + e->len;
-          }
-        }
-      } else if (fd == sfd) {
-        signalfd_siginfo si;
-        while (read(sfd, &si, sizeof(si)) == sizeof(si)) {
-          if (si.ssi_signo == SIGHUP) {
-            LOG_INFO(kComp, "received SIGHUP, restarting");
-            reload_config("SIGHUP");
-            // The monitor is stopped first so it cannot write the old verdicts back.
-            if (monitor) monitor->Stop();
-            ledger.Reload();
-            reinit = true;
-            do_restart = true;
-          } else if (si.ssi_signo == SIGUSR1) {
-            // Explicitly requested: printed whatever the log level.
-            for (auto& p : plugins) Logf(LogLevel::kInfo, kComp, "stats: %s", p->StatsJson().c_str());
-            Logf(LogLevel::kInfo, kComp, "health: %s", health_counters.Json().c_str());
-          } else {
-            LOG_INFO(kComp, "received signal %s, shutting down", strsignal(static_cast<int>(si.ssi_signo)));
-            quit = true;
-          }
-        }
-      }
-    }
-    if (do_restart && !quit) restart();
-    else if (do_reregister && !quit) reregister();
-  }
-  stop_all();
-  if (driver_hbm) driver_hbm->Stop();
-  if (http) http->Stop();
-  // Grant files of containers allocated just before the signal: the runtime mounts them next.
-  if (!v.popts.memcap_usage_dir.empty() && !memcap::Flush(2000))
-    LOG_WARN(kComp, "grant accounting files still being written at exit");
-  // Labels describe a node this daemon is serving; do not leave them behind.
-  if (!cfg.flags.node_labels_file.empty()) unlink(cfg.flags.node_labels_file.c_str());
-  for (int fd : {ep, sfd, ifd, tfd, efd, lfd, rfd}) close(fd);
-  LOG_INFO(kComp, "shutdown complete (exit %d)", exit_code);
-  return exit_code;
+  close(sfd);
+  LOG_INFO(kComp, "shutdown complete (exit %d)", rc);
+  return rc;
 }
 
 }  // namespace adp::daemon

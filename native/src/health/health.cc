@@ -121,6 +121,31 @@ std::map<std::pair<std::string, std::string>, uint64_t> HealthCounters::EventCou
   return events_;
 }
 
+void HealthCounters::CountRecovered(const std::string& bdf) {
+  std::lock_guard<std::mutex> lk(mu_);
+  ++recovered_[bdf];
+}
+
+std::map<std::string, uint64_t> HealthCounters::Recovered() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return recovered_;
+}
+
+HealthCounters::RelayCursor HealthCounters::GetRelayCursor() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return cursor_;
+}
+
+void HealthCounters::SetRelayCursor(const RelayCursor& c) {
+  std::lock_guard<std::mutex> lk(mu_);
+  cursor_ = c;
+}
+
+void HealthCounters::AdvanceRelaySeq(uint64_t seq) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (cursor_.valid && seq > cursor_.seq) cursor_.seq = seq;
+}
+
 int Monitor::Classify(const HealthConfig& cfg, uint32_t type) {
   if (cfg.ignored.count(type)) return 0;
   if (type == smi::kEvtGpuPostReset) return +1;
@@ -252,6 +277,53 @@ void Ledger::SaveLocked() const {
   }
 }
 
+bool Ledger::MarkGap(const std::string& key, const std::string& why, bool tentative, int64_t now_ms) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = gaps_.find(key);
+  if (it == gaps_.end()) {
+    gaps_[key] = GapMark{now_ms, why, tentative, 0};
+    return true;
+  }
+  if (it->second.tentative && !tentative) {  // confirmed: the relay could not replay what was missed
+    it->second.tentative = false;
+    it->second.why = why;
+    return true;
+  }
+  return false;
+}
+
+std::vector<std::string> Ledger::CancelTentativeGaps() {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<std::string> out;
+  for (auto it = gaps_.begin(); it != gaps_.end();) {
+    if (it->second.tentative) {
+      out.push_back(it->first);
+      it = gaps_.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  return out;
+}
+
+void Ledger::ClearGap(const std::string& key) {
+  std::lock_guard<std::mutex> lk(mu_);
+  gaps_.erase(key);
+}
+
+bool Ledger::Gap(const std::string& key, GapMark* out) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = gaps_.find(key);
+  if (it == gaps_.end()) return false;
+  if (out) *out = it->second;
+  return true;
+}
+
+void Ledger::SetResponsiveSince(const std::string& key, int64_t ms) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (auto it = gaps_.find(key); it != gaps_.end()) it->second.responsive_since_ms = ms;
+}
+
 std::vector<std::pair<int, std::string>> Ledger::Failed(const inventory::Snapshot& snap) const {
   std::vector<std::pair<int, std::string>> out;
   std::lock_guard<std::mutex> lk(mu_);
@@ -263,18 +335,21 @@ std::vector<std::pair<int, std::string>> Ledger::Failed(const inventory::Snapsho
 }
 
 std::string HealthCounters::Json() const {
-  char buf[400];
+  char buf[512];
   int e = events_enabled.load();
+  uint64_t recovered = 0;
+  for (const auto& [_, n] : Recovered()) recovered += n;
   snprintf(buf, sizeof(buf),
            "{\"events\": \"%s\", \"polls\": %llu, \"responsive\": %llu, \"ecc_reads_ok\": %llu, "
            "\"ecc_read_errors\": %llu, \"events_received\": %llu, \"retired_reads_ok\": %llu, "
-           "\"retired_read_errors\": %llu}",
+           "\"retired_read_errors\": %llu, \"event_gaps\": %llu, \"recovered_without_event\": %llu}",
            e < 0 ? "not started" : e ? "on" : "off", static_cast<unsigned long long>(polls.load()),
            static_cast<unsigned long long>(responsive.load()), static_cast<unsigned long long>(ecc_reads_ok.load()),
            static_cast<unsigned long long>(ecc_read_errors.load()),
            static_cast<unsigned long long>(events_received.load()),
            static_cast<unsigned long long>(retired_reads_ok.load()),
-           static_cast<unsigned long long>(retired_read_errors.load()));
+           static_cast<unsigned long long>(retired_read_errors.load()),
+           static_cast<unsigned long long>(event_gaps.load()), static_cast<unsigned long long>(recovered));
   return buf;
 }
 
@@ -290,6 +365,7 @@ Monitor::Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> s
   fail_.assign(n, 0);
   link_change_polls_.assign(n, 0);
   retired_threshold_.assign(n, 0);
+  fingerprint_ = ProcessorFingerprint(snap_->procs);
 }
 
 Monitor::~Monitor() { Stop(); }
@@ -379,6 +455,16 @@ Status Monitor::Start() {
       Notify(g.index, false, r.reason);
     }
   }
+  // GPUs still waiting for GPU_POST_RESET from an earlier generation (or
+  // process): a new in-process registration cannot receive what was sent
+  // before it existed; events off receive nothing. In relay mode the relay's
+  // answer to this generation's reinit says whether anything was missed.
+  if (!events_ok_ && (!cfg_.events || cfg_.event_relay.empty()))
+    MarkGap("events off: " + events_reason_, false);
+  else if (cfg_.event_relay.empty())
+    MarkGap("amdsmi event registration renewed by a new monitor generation", false);
+  else if (relay_fd_ < 0)
+    MarkGap(events_reason_, true);
   if (!cfg_.drain_file.empty()) ApplyDrain();  // at once, not a poll interval later
   LOG_INFO(kComp, "health monitor watching %zu GPU(s) (events %s, poll every %d ms)", snap_->gpus.size(),
            events_ok_ ? "on" : relay_fd_ >= 0 ? "through the relay, once it answers" : "off", cfg_.poll_interval_ms);
@@ -430,8 +516,14 @@ void Monitor::RelayConnect() {
     events_reason_ = "event relay " + cfg_.event_relay + " not reachable (" + strerror(errno) + ")";
     return;
   }
-  static const char kReinit[] = "reinit\n";
-  if (send(relay_fd_, kReinit, sizeof(kReinit) - 1, MSG_NOSIGNAL) != static_cast<ssize_t>(sizeof(kReinit) - 1)) {
+  // Our processors (the relay re-enumerates only if they differ from its
+  // registration) and where we are in its event stream (it replays what this
+  // daemon missed since, e.g. across a SIGHUP).
+  HealthCounters::RelayCursor cur = counters_->GetRelayCursor();
+  std::string req = "reinit fp=" + fingerprint_ + " since=" +
+                    (cur.valid ? cur.relay + ":" + std::to_string(cur.seq) + ":" + std::to_string(cur.gen)
+                               : std::string("-")) + "\n";
+  if (send(relay_fd_, req.data(), req.size(), MSG_NOSIGNAL) != static_cast<ssize_t>(req.size())) {
     RelayClose("cannot write to the event relay");
     return;
   }
@@ -447,9 +539,11 @@ void Monitor::RelayClose(const std::string& why) {
   events_ok_ = false;
   events_reason_ = why;
   counters_->events_enabled.store(0);
+  // Events sent meanwhile are replayed if the relay comes back holding them.
+  MarkGap("event relay: " + why, true);
 }
 
-void Monitor::RelayWait(int ms, std::vector<smi::Event>* out) {
+void Monitor::RelayWait(int ms) {
   pollfd p[2] = {{relay_fd_, POLLIN, 0}, {wake_fd_, POLLIN, 0}};
   if (poll(p, wake_fd_ >= 0 ? 2 : 1, ms) <= 0 || !(p[0].revents & (POLLIN | POLLHUP | POLLERR))) return;
   char buf[4096];
@@ -470,14 +564,27 @@ void Monitor::RelayWait(int ms, std::vector<smi::Event>* out) {
       counters_->events_enabled.store(events_ok_ ? 1 : 0);
       if (events_ok_ && !was) LOG_INFO(kComp, "events on through the relay at %s", cfg_.event_relay.c_str());
       if (!events_ok_) LOG_WARN(kComp, "event relay reports %s; using polling only", events_reason_.c_str());
-    } else if (l.kind == "event" && out) {
+      if (!l.relay.empty()) counters_->SetRelayCursor({true, l.relay, l.seq, l.gen});
+      if (!events_ok_) {
+        MarkGap("the event relay reports events off (" + l.reason + ")", false);
+      } else if (l.gap != 0) {
+        MarkGap(l.gap == 1 ? "the event relay renewed its registration or no longer holds the events missed"
+                           : "the event relay cannot replay missed events (an older relay)",
+                false);
+      } else {
+        for (const auto& key : ledger_->CancelTentativeGaps())
+          LOG_INFO(kComp, "GPU %s: the event relay replayed what was missed; waiting for GPU_POST_RESET again",
+                   key.c_str());
+      }
+    } else if (l.kind == "event") {
+      counters_->AdvanceRelaySeq(l.seq);
       // The relay's processor -> this snapshot's handle: by KFD node when both
       // know it, else by PCI address and partition.
       for (const auto& pr : snap_->procs) {
         bool hit = l.node != 0xffffffffu && pr.kfd_node != 0xffffffffu ? pr.kfd_node == l.node
                                                                        : pr.bdf == l.bdf && pr.partition_id == l.part;
         if (!hit) continue;
-        out->push_back({pr.handle, l.type, l.message});
+        HandleEvent({pr.handle, l.type, l.message});  // in order with the hellos around it
         break;
       }
     } else if (l.kind.empty()) {
@@ -580,6 +687,7 @@ void Monitor::PollOnce() {
     } else if (alive && (fail & kFailUnresponsive)) {
       Update(g.index, 0, kFailUnresponsive, "device responding again");
     }
+    CheckGapRecovery(g.index, alive);
     if (!alive) continue;
     ++answered;
     counters_->responsive.fetch_add(1);
@@ -652,6 +760,54 @@ void Monitor::PollOnce() {
   }
 }
 
+void Monitor::MarkGap(const std::string& why, bool tentative) {
+  if (!tentative) counters_->event_gaps.fetch_add(1);
+  const int64_t now = NowMs();
+  for (const auto& g : snap_->gpus) {
+    if (!(fail_[g.index] & kFailResetPending)) continue;
+    if (!ledger_->MarkGap(keys_[g.index], why, tentative, now)) continue;
+    if (cfg_.reset_recovery_hold_ms > 0)
+      LOG_WARN(kComp, "GPU %s waits for GPU_POST_RESET across an event gap (%s): back in service once amdsmi has "
+               "answered every poll for %lld s, unless a GPU_PRE_RESET arrives%s", g.bdf.c_str(), why.c_str(),
+               static_cast<long long>(cfg_.reset_recovery_hold_ms / 1000),
+               tentative ? " or the relay replays what was missed" : "");
+    else
+      LOG_WARN(kComp, "GPU %s waits for GPU_POST_RESET across an event gap (%s); --reset-recovery-hold-ms=0: only "
+               "the event (or the operator) brings it back", g.bdf.c_str(), why.c_str());
+  }
+}
+
+void Monitor::CheckGapRecovery(int gpu, bool alive) {
+  const std::string& key = keys_[gpu];
+  GapMark m;
+  if (!ledger_->Gap(key, &m)) return;
+  if (!(fail_[gpu] & kFailResetPending)) {  // the event came after all, or the operator cleared it
+    ledger_->ClearGap(key);
+    return;
+  }
+  const int64_t now = NowMs();
+  if (!alive) {
+    ledger_->SetResponsiveSince(key, 0);
+    return;
+  }
+  if (m.responsive_since_ms == 0) {
+    m.responsive_since_ms = now;
+    ledger_->SetResponsiveSince(key, now);
+  }
+  if (cfg_.reset_recovery_hold_ms <= 0) return;
+  const int64_t from = std::max(m.since_ms, m.responsive_since_ms);
+  if (now - from < cfg_.reset_recovery_hold_ms) return;
+  const auto& g = snap_->gpus[gpu];
+  char held[32];
+  snprintf(held, sizeof(held), "%.1f", static_cast<double>(now - from) / 1000.0);
+  std::string why = "no GPU_POST_RESET after an event gap (" + m.why + "); amdsmi answered every poll for " + held +
+                    " s";
+  LOG_WARN(kComp, "GPU %s recovered without GPU_POST_RESET: %s", g.bdf.c_str(), why.c_str());
+  counters_->CountRecovered(g.bdf);
+  ledger_->ClearGap(key);
+  Update(gpu, 0, kFailResetPending, why);
+}
+
 void Monitor::Update(int gpu, uint32_t set, uint32_t clear, const std::string& reason) {
   uint32_t before = fail_[gpu];
   uint32_t after = (before | set) & ~clear;
@@ -674,6 +830,43 @@ int64_t HealthCounters::HealthLoopAgeMs() const {
   return beat == 0 ? 0 : std::max<int64_t>(0, NowMs() - beat);
 }
 
+void Monitor::HandleEvent(const smi::Event& e) {
+  counters_->events_received.fetch_add(1);
+  int gpu = -1;
+  for (size_t i = 0; i < snap_->procs.size(); ++i)
+    if (snap_->procs[i].handle == e.handle) gpu = snap_->GpuOfHandle(static_cast<int>(i));
+  int verdict = Classify(cfg_, e.type);
+  LOG_INFO(kComp, "event %s(%u) on GPU %d: %s%s", EventName(e.type), e.type, gpu,
+           e.message.c_str(), verdict == 0 ? " (ignored)" : "");
+  if (gpu >= 0) {
+    const char* name = EventName(e.type);
+    counters_->CountEvent(snap_->gpus[gpu].bdf,
+                          strcmp(name, "EVENT") ? std::string(name) : "EVENT_" + std::to_string(e.type));
+  }
+  if (gpu < 0 || verdict == 0) return;
+  std::string why = std::string(EventName(e.type)) + ": " + e.message;
+  if (verdict > 0) {
+    // A completed reset clears every failure, poll-detected ones included,
+    // and the ECC count after the reset is the new baseline.
+    void* h = snap_->procs[snap_->gpus[gpu].partitions.front().handle].handle;
+    auto ecc = lib_->UncorrectableErrors(h);
+    if (ecc.ok()) {
+      ecc_baseline_[gpu] = *ecc;
+      GpuRecord r = ledger_->Get(keys_[gpu]);
+      r.has_baseline = true;
+      r.ecc_baseline = r.ecc_seen = *ecc;
+      ledger_->Put(keys_[gpu], r);
+    }
+    if (fail_[gpu] == 0) Notify(gpu, true, why);  // keep the reference's idempotent notify
+    Update(gpu, 0, ~static_cast<uint32_t>(kFailDrained), why);  // a drain outlives a reset
+    ledger_->ClearGap(keys_[gpu]);
+  } else {
+    Update(gpu, e.type == smi::kEvtGpuPreReset ? kFailResetPending : kFailEvent, 0, why);
+    // A new reset: only a gap after it lets polling end the wait.
+    if (e.type == smi::kEvtGpuPreReset) ledger_->ClearGap(keys_[gpu]);
+  }
+}
+
 void Monitor::Run() {
   using Clock = std::chrono::steady_clock;
   auto next_poll = Clock::now() + std::chrono::milliseconds(cfg_.poll_interval_ms);
@@ -692,7 +885,7 @@ void Monitor::Run() {
         RelayConnect();
         if (relay_fd_ >= 0) LOG_INFO(kComp, "connected to the event relay at %s", cfg_.event_relay.c_str());
       }
-      if (relay_fd_ >= 0) RelayWait(slice, &events);
+      if (relay_fd_ >= 0) RelayWait(slice);
       else Sleep(slice);
     } else if (events_ok_) {
       events.clear();
@@ -709,6 +902,7 @@ void Monitor::Run() {
           counters_->events_enabled.store(0);
           LOG_ERROR(kComp, "amdsmi event waits have failed for %lld ms: events off, polling only until they succeed",
                     static_cast<long long>(NowMs() - wait_failing_since_ms_));
+          MarkGap("amdsmi event waits failing", false);
         }
         Sleep(slice);
       } else if (wait_failures_) {
@@ -723,41 +917,7 @@ void Monitor::Run() {
       events.clear();
       Sleep(slice);
     }
-    {
-      for (const auto& e : events) {
-        counters_->events_received.fetch_add(1);
-        int gpu = -1;
-        for (size_t i = 0; i < snap_->procs.size(); ++i)
-          if (snap_->procs[i].handle == e.handle) gpu = snap_->GpuOfHandle(static_cast<int>(i));
-        int verdict = Classify(cfg_, e.type);
-        LOG_INFO(kComp, "event %s(%u) on GPU %d: %s%s", EventName(e.type), e.type, gpu,
-                 e.message.c_str(), verdict == 0 ? " (ignored)" : "");
-        if (gpu >= 0) {
-          const char* name = EventName(e.type);
-          counters_->CountEvent(snap_->gpus[gpu].bdf,
-                                strcmp(name, "EVENT") ? std::string(name) : "EVENT_" + std::to_string(e.type));
-        }
-        if (gpu < 0 || verdict == 0) continue;
-        std::string why = std::string(EventName(e.type)) + ": " + e.message;
-        if (verdict > 0) {
-          // A completed reset clears every failure, poll-detected ones included,
-          // and the ECC count after the reset is the new baseline.
-          void* h = snap_->procs[snap_->gpus[gpu].partitions.front().handle].handle;
-          auto ecc = lib_->UncorrectableErrors(h);
-          if (ecc.ok()) {
-            ecc_baseline_[gpu] = *ecc;
-            GpuRecord r = ledger_->Get(keys_[gpu]);
-            r.has_baseline = true;
-            r.ecc_baseline = r.ecc_seen = *ecc;
-            ledger_->Put(keys_[gpu], r);
-          }
-          if (fail_[gpu] == 0) Notify(gpu, true, why);  // keep the reference's idempotent notify
-          Update(gpu, 0, ~static_cast<uint32_t>(kFailDrained), why);  // a drain outlives a reset
-        } else {
-          Update(gpu, e.type == smi::kEvtGpuPreReset ? kFailResetPending : kFailEvent, 0, why);
-        }
-      }
-    }
+    for (const auto& e : events) HandleEvent(e);
     if (cfg_.poll_interval_ms > 0 && Clock::now() >= next_poll) {
       PollOnce();
       next_poll = Clock::now() + std::chrono::milliseconds(cfg_.poll_interval_ms);

@@ -34,6 +34,18 @@
 // GPU_POST_RESET event (or a device that answers again, for "unresponsive")
 // clears a failure. The reference keeps Device health only for one
 // ListAndWatch lifetime (server.go:95-116,251-265) and never recovers it.
+//
+// Event gaps: a GPU_POST_RESET that nobody was registered to receive is lost
+// for good, and a GPU whose GPU_PRE_RESET was seen would stay Unhealthy. The
+// monitor therefore records every stretch in which events may have been missed
+// -- a new in-process registration (each monitor generation), event waits that
+// keep failing, events off, the relay disconnected, or a relay that says it
+// re-registered or could not replay what this daemon missed (relay.h) -- on
+// each GPU that is waiting for its GPU_POST_RESET. Such a GPU gets a polled
+// recovery check: once amdsmi has answered at every poll for
+// --reset-recovery-hold-ms since the gap, with no new GPU_PRE_RESET, it is back
+// in service (logged, amdgpu_dp_gpu_recovered_without_event_total). A GPU with
+// no gap since its GPU_PRE_RESET keeps waiting for the event.
 #pragma once
 
 #include <atomic>
@@ -80,6 +92,10 @@ struct HealthConfig {
   // partition UUID or node index; one or more per line, '#' comments) are
   // advertised Unhealthy until removed. Read at every poll.
   std::string drain_file;
+  // A GPU waiting for GPU_POST_RESET across an event gap is back in service
+  // once amdsmi has answered at every poll for this long (--reset-recovery-hold-ms;
+  // 0 = never without the event).
+  int64_t reset_recovery_hold_ms = 120000;
   static HealthConfig FromEnv();
   static HealthConfig FromValues(const char* disable_value, const char* poll_ms_value);
 };
@@ -136,6 +152,24 @@ struct HealthCounters {
   // worth watching.
   void CountEvent(const std::string& bdf, const std::string& type);
   std::map<std::pair<std::string, std::string>, uint64_t> EventCounts() const;
+  // Event gaps the monitor recorded (any GPU waiting for GPU_POST_RESET or not).
+  std::atomic<uint64_t> event_gaps{0};
+  // GPUs put back in service by the polled check after an event gap, per PCI address.
+  void CountRecovered(const std::string& bdf);
+  std::map<std::string, uint64_t> Recovered() const;
+  // Where this daemon is in the relay's event stream, across monitor
+  // generations: the relay instance, the last event sequence number handled
+  // and the relay's registration generation (relay.h). Not valid until a relay
+  // has answered a reinit; a new process starts without one.
+  struct RelayCursor {
+    bool valid = false;
+    std::string relay;
+    uint64_t seq = 0;
+    uint64_t gen = 0;
+  };
+  RelayCursor GetRelayCursor() const;
+  void SetRelayCursor(const RelayCursor& c);
+  void AdvanceRelaySeq(uint64_t seq);
   std::string Json() const;
 
  private:
@@ -143,6 +177,19 @@ struct HealthCounters {
   std::map<std::string, uint32_t> retired_;
   std::map<std::string, uint64_t> vram_used_, vram_total_;
   std::map<std::pair<std::string, std::string>, uint64_t> events_;
+  std::map<std::string, uint64_t> recovered_;
+  RelayCursor cursor_;
+};
+
+// An event gap recorded on a GPU waiting for GPU_POST_RESET (Ledger, in memory
+// only: a new process starts a gap of its own).
+struct GapMark {
+  int64_t since_ms = 0;  // steady clock
+  std::string why;
+  // The relay connection dropped: confirmed if the relay cannot replay what
+  // was missed, dropped if it can.
+  bool tentative = false;
+  int64_t responsive_since_ms = 0;  // first poll of the current run of answered polls (0 = none yet)
 };
 
 // Per-GPU health verdicts shared by all Monitor generations of a daemon.
@@ -169,10 +216,19 @@ class Ledger {
   static std::string Serialize(const std::map<std::string, GpuRecord>& m);
   static std::map<std::string, GpuRecord> Parse(const std::string& body);
 
+  // Event gaps (GapMark). MarkGap returns true when it created a mark or
+  // confirmed a tentative one (worth a log line).
+  bool MarkGap(const std::string& key, const std::string& why, bool tentative, int64_t now_ms);
+  std::vector<std::string> CancelTentativeGaps();
+  void ClearGap(const std::string& key);
+  bool Gap(const std::string& key, GapMark* out) const;
+  void SetResponsiveSince(const std::string& key, int64_t ms);
+
  private:
   void SaveLocked() const;
   mutable std::mutex mu_;
   std::map<std::string, GpuRecord> recs_;
+  std::map<std::string, GapMark> gaps_;
   std::string path_;
 };
 
@@ -211,6 +267,10 @@ class Monitor {
   void Update(int gpu, uint32_t set, uint32_t clear, const std::string& reason);
   // Applies the drain file to every GPU (PollOnce).
   void ApplyDrain();
+  // Records an event gap on every GPU waiting for GPU_POST_RESET.
+  void MarkGap(const std::string& why, bool tentative);
+  // The polled recovery check of a GPU waiting across a gap (PollOnce).
+  void CheckGapRecovery(int gpu, bool alive);
 
   smi::Library* lib_;
   std::shared_ptr<const inventory::Snapshot> snap_;
@@ -224,6 +284,7 @@ class Monitor {
   std::string relay_buf_;
   bool relay_synced_ = false;  // the relay answered this connection's "reinit"
   int64_t relay_tried_ms_ = -1000000;
+  std::string fingerprint_;  // ProcessorFingerprint of the snapshot, sent with "reinit"
   // In-process event waits that keep failing: since when, how many, and
   // whether events are reported off because of it.
   int64_t wait_failing_since_ms_ = 0;
@@ -231,9 +292,11 @@ class Monitor {
   bool events_failing_ = false;
   void RelayConnect();
   void RelayClose(const std::string& why);
-  // Reads relay lines for up to `ms`: hellos update events_ok_, events are
-  // mapped to this snapshot's handles and appended.
-  void RelayWait(int ms, std::vector<smi::Event>* out);
+  // Reads relay lines for up to `ms`: hellos update events_ok_ and the event
+  // gaps, events are mapped to this snapshot's handles and handled, in order.
+  void RelayWait(int ms);
+  // One amdsmi event (in-process or relayed): counts it and updates health.
+  void HandleEvent(const smi::Event& e);
   std::thread thread_;
   std::atomic<bool> stop_{false};
   std::function<void(const std::string&)> layout_listener_;

@@ -44,6 +44,11 @@ std::string OneLine(std::string s) {
   return s;
 }
 
+int64_t NowMs() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 // Value of "key=value" (up to the next space) in `line`, "" if absent.
 std::string_view Kv(std::string_view line, std::string_view key, size_t* end = nullptr) {
   for (size_t b = 0; b < line.size();) {
@@ -68,6 +73,18 @@ bool SendAll(int fd, const std::string& s) {
     off += static_cast<size_t>(n);
   }
   return true;
+}
+
+// 16 hex digits from /dev/urandom (time and PID if it cannot be read).
+std::string RandomId() {
+  uint64_t v = 0;
+  int fd = open("/dev/urandom", O_RDONLY | O_CLOEXEC);
+  if (fd < 0 || read(fd, &v, sizeof(v)) != static_cast<ssize_t>(sizeof(v)))
+    v = static_cast<uint64_t>(NowMs()) * 0x9e3779b97f4a7c15ull ^ static_cast<uint64_t>(getpid());
+  if (fd >= 0) close(fd);
+  char buf[17];
+  snprintf(buf, sizeof(buf), "%016llx", static_cast<unsigned long long>(v));
+  return buf;
 }
 
 // Scans run on their own thread: a walk of every /proc/<pid>/fd can take
@@ -143,6 +160,226 @@ class ScanWorker {
   std::thread thread_;
 };
 
+// The amdsmi side of the relay: the processors, their event registration, the
+// thread that waits for events (writing each as a line to `event_fd`), and
+// the registrar thread that renews the registration when a daemon's view of
+// the processors differs from it. None of it runs on the poll loop: a
+// re-enumeration (amdsmi shut_down + init) takes as long as the driver makes
+// it, and greetings, scans and event forwarding do not wait for it. Renewals
+// end with a "done <client> <renewed 0|1>" line on `done_fd`.
+class Registration {
+ public:
+  struct State {
+    bool ok = false;
+    std::string reason;     // events off: why
+    size_t processors = 0;
+    uint64_t gen = 0;       // renewals so far (each one a stretch without a registration)
+    std::string fp;         // ProcessorFingerprint of the registered processors ("" = none)
+    int64_t renew_ms = 0;   // how long the last renewal took
+  };
+
+  Registration(smi::Library* lib, std::string driver_root, int event_fd, int done_fd, int64_t stuck_ms)
+      : lib_(lib), driver_root_(std::move(driver_root)), event_fd_(event_fd), done_fd_(done_fd), stuck_ms_(stuck_ms),
+        // The wait's slice (an event ends the wait at once): short, because a
+        // renewal must wait for the slice to end before it can stop the waiter;
+        // and well under the watchdog's threshold. Idle, that is ~10 wake-ups/s
+        // at 0.02% of a core (profiles/r4/idle/).
+        slice_ms_(static_cast<int>(std::max<int64_t>(10, std::min<int64_t>(100, stuck_ms / 4)))) {}
+
+  State Get() const {
+    std::lock_guard<std::mutex> lk(mu_);
+    return state_;
+  }
+  bool running() const { return running_.load(); }
+  // How long the running waiter has been inside one amdsmi wait.
+  int64_t SilentMs() const { return running_.load() ? NowMs() - beat_ms_.load() : 0; }
+  // How long waits have kept failing (each failure is followed by 100 ms of rest).
+  int64_t FailingMs() const { return running_.load() ? static_cast<int64_t>(wait_failures_.load()) * 100 : 0; }
+  bool Hung() const { return SilentMs() > stuck_ms_; }
+
+  // Enumerates (after amdsmi shut_down + init when `reinit`), registers every
+  // processor and starts the waiter. Called on the caller's thread once before
+  // StartRegistrar(), then only by the registrar.
+  void Renew(bool reinit) {
+    const int64_t t0 = NowMs();
+    StopWaiter();
+    if (registered_) lib_->EventsStop(handles_);
+    registered_ = false;
+    handles_.clear();
+    procs_.clear();
+    State s = Get();
+    ++s.gen;
+    s.ok = false;
+    s.processors = 0;
+    s.fp.clear();
+    Status st = reinit ? lib_->Reinit() : Status::Ok();
+    if (!st.ok()) {
+      s.reason = "amdsmi re-initialisation failed: " + OneLine(st.ToString());
+    } else if (auto en = lib_->Enumerate(); !en.ok()) {
+      s.reason = "enumeration failed: " + OneLine(en.status().ToString());
+    } else {
+      procs_ = std::move(*en);
+      for (const auto& p : procs_) handles_.push_back(p.handle);
+      s.processors = procs_.size();
+      s.fp = ProcessorFingerprint(procs_);
+      st = lib_->EventsInit(handles_, RelayMask());
+      registered_ = st.ok();
+      s.ok = st.ok();
+      s.reason.clear();
+      if (!st.ok()) {
+        s.reason = OneLine(st.ToString());
+        if (inventory::KfdAccessErrno(driver_root_) == EPERM)
+          s.reason += "; /dev/kfd not openable (EPERM) in the relay's container: run the relay privileged";
+      }
+    }
+    s.renew_ms = NowMs() - t0;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      state_ = s;
+    }
+    if (s.ok)
+      LOG_INFO(kComp, "event notification registered on %zu processor(s) (generation %llu, %s%lld ms)", s.processors,
+               static_cast<unsigned long long>(s.gen), reinit ? "amdsmi re-initialised, " : "",
+               static_cast<long long>(s.renew_ms));
+    else if (s.processors)
+      LOG_ERROR(kComp, "event notification unavailable: %s", s.reason.c_str());
+    else
+      LOG_ERROR(kComp, "events=off reason=%s", s.reason.c_str());
+    StartWaiter();
+  }
+
+  // Starts the registrar thread, which serves Request().
+  void StartRegistrar() {
+    registrar_ = std::thread([this] { RegistrarLoop(); });
+  }
+  // A daemon (client `id`) subscribed with its fingerprint ("" = none given).
+  void Request(uint64_t id, std::string fp) {
+    std::lock_guard<std::mutex> lk(req_mu_);
+    requests_.push_back({id, std::move(fp)});
+    req_cv_.notify_one();
+  }
+
+  // Ends the registrar (after the renewal it may be in) and the registration.
+  // Returns false when the waiter is stuck in amdsmi: it is left running and
+  // this object must outlive it (the process is about to exit).
+  bool Shutdown() {
+    {
+      std::lock_guard<std::mutex> lk(req_mu_);
+      req_stop_ = true;
+    }
+    req_cv_.notify_all();
+    if (registrar_.joinable()) registrar_.join();
+    if (Hung()) {
+      LOG_WARN(kComp, "exiting with the event wait still stuck");
+      waiter_.detach();
+      return false;
+    }
+    StopWaiter();
+    if (registered_) lib_->EventsStop(handles_);
+    registered_ = false;
+    return true;
+  }
+
+ private:
+  void RegistrarLoop() {
+    for (;;) {
+      std::pair<uint64_t, std::string> r;
+      {
+        std::unique_lock<std::mutex> lk(req_mu_);
+        req_cv_.wait(lk, [&] { return req_stop_ || !requests_.empty(); });
+        if (req_stop_) return;
+        r = std::move(requests_.front());
+        requests_.pop_front();
+      }
+      State cur = Get();
+      bool renewed = false;
+      if (Hung()) {
+        // amdsmi cannot be re-initialised under a wait that does not return:
+        // the daemon gets the current (events off) state instead.
+        LOG_WARN(kComp, "re-enumeration a daemon asked for skipped: the event wait is stuck");
+      } else if (r.second.empty() || r.second != cur.fp || !cur.ok || wait_failures_.load() > 0) {
+        LOG_INFO(kComp, "re-enumerating (a daemon asked: %s)",
+                 r.second.empty()        ? "no processor fingerprint given"
+                 : r.second != cur.fp    ? ("its processors " + r.second + " differ from the registration's " +
+                                         (cur.fp.empty() ? std::string("(none)") : cur.fp)).c_str()
+                 : !cur.ok               ? "events are off"
+                                         : "the event wait is failing");
+        Renew(true);
+        renewed = true;
+      } else {
+        LOG_INFO(kComp, "registration kept (a daemon's processors match it: %s, generation %llu)", cur.fp.c_str(),
+                 static_cast<unsigned long long>(cur.gen));
+      }
+      std::string line = "done " + std::to_string(r.first) + (renewed ? " 1\n" : " 0\n");
+      if (write(done_fd_, line.data(), line.size()) != static_cast<ssize_t>(line.size()))
+        LOG_WARN(kComp, "renewal result not delivered to the poll loop");
+    }
+  }
+
+  void StartWaiter() {
+    if (!registered_) return;
+    wait_failures_.store(0);  // a fresh registration: earlier failures say nothing about it
+    beat_ms_.store(NowMs());
+    waiter_stop_.store(false);
+    running_.store(true);
+    waiter_ = std::thread([this] {
+      std::vector<smi::Event> events;
+      while (!waiter_stop_.load()) {
+        events.clear();
+        beat_ms_.store(NowMs());
+        Status st = lib_->EventsWait(slice_ms_, &events);
+        beat_ms_.store(NowMs());
+        if (!st.ok()) {
+          int n = wait_failures_.fetch_add(1) + 1;
+          if (n == 1 || n % 600 == 0)  // the first, then one a minute
+            LOG_WARN(kComp, "event wait failed (%d in a row): %s", n, st.ToString().c_str());
+          usleep(100000);
+          continue;
+        }
+        wait_failures_.store(0);
+        for (const auto& e : events) {
+          const smi::ProcessorInfo* p = nullptr;
+          for (const auto& q : procs_)
+            if (q.handle == e.handle) p = &q;
+          if (!p) continue;
+          std::string line = FormatRelayEvent(*p, e.type, e.message);
+          if (write(event_fd_, line.data(), line.size()) != static_cast<ssize_t>(line.size()))
+            LOG_WARN(kComp, "event dropped (relay loop behind): %s", OneLine(line).c_str());
+        }
+      }
+    });
+  }
+  void StopWaiter() {
+    if (!waiter_.joinable()) return;
+    waiter_stop_.store(true);
+    waiter_.join();
+    running_.store(false);
+  }
+
+  smi::Library* lib_;
+  const std::string driver_root_;
+  const int event_fd_, done_fd_;
+  const int64_t stuck_ms_;
+  const int slice_ms_;
+  // Owned by whichever thread runs Renew (never two at once); the waiter
+  // reads procs_ and only runs while they do not change.
+  std::vector<smi::ProcessorInfo> procs_;
+  std::vector<void*> handles_;
+  bool registered_ = false;
+  std::thread waiter_;
+  std::atomic<bool> waiter_stop_{false};
+  std::atomic<bool> running_{false};
+  std::atomic<int64_t> beat_ms_{0};    // the waiter's last sign of life
+  std::atomic<int> wait_failures_{0};  // consecutive failed waits
+  mutable std::mutex mu_;
+  State state_;
+  std::thread registrar_;
+  std::mutex req_mu_;
+  std::condition_variable req_cv_;
+  std::deque<std::pair<uint64_t, std::string>> requests_;
+  bool req_stop_ = false;
+};
+
 }  // namespace
 
 RelayLine ParseRelayLine(std::string_view line) {
@@ -150,14 +387,22 @@ RelayLine ParseRelayLine(std::string_view line) {
   while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.remove_suffix(1);
   if (line.rfind("hello ", 0) == 0) {
     r.kind = "hello";
-    r.events_ok = Kv(line, "events") == "ok";
-    r.after_reinit = line.rfind("hello v1 reinit ", 0) == 0;
     size_t at = line.find(" reason=");
     if (at != std::string_view::npos) r.reason = std::string(line.substr(at + 8));
+    std::string_view head = line.substr(0, at);  // key=value tokens never come from the reason
+    r.events_ok = Kv(head, "events") == "ok";
+    r.after_reinit = line.rfind("hello v1 reinit ", 0) == 0;
+    r.relay = std::string(Kv(head, "relay"));
+    if (auto v = ParseUint(std::string(Kv(head, "gen")))) r.gen = *v;
+    if (auto v = ParseUint(std::string(Kv(head, "seq")))) r.seq = *v;
+    std::string_view gap = Kv(head, "gap");
+    r.gap = gap == "0" ? 0 : gap == "1" ? 1 : -1;
     return r;
   }
   if (line.rfind("event ", 0) != 0) return r;
   size_t end = 0, last = 0;
+  std::string_view seq = Kv(line, "seq", &end);
+  if (!seq.empty()) last = std::max(last, end);
   std::string_view node = Kv(line, "node", &end);
   last = std::max(last, end);
   r.bdf = std::string(Kv(line, "bdf", &end));
@@ -167,6 +412,11 @@ RelayLine ParseRelayLine(std::string_view line) {
   auto type = ParseUint(std::string(Kv(line, "type", &end)));
   last = std::max(last, end);
   if (!part || !type || *type > 0xffffffffu || *part > 0xffffffffu) return r;
+  if (!seq.empty()) {
+    auto s = ParseUint(std::string(seq));
+    if (!s) return r;
+    r.seq = *s;
+  }
   if (node != "-") {
     auto n = ParseUint(std::string(node));
     if (!n || *n >= 0xffffffffu) return r;
@@ -183,6 +433,23 @@ std::string FormatRelayEvent(const smi::ProcessorInfo& p, uint32_t type, const s
   return "event node=" + (p.kfd_node == 0xffffffffu ? std::string("-") : std::to_string(p.kfd_node)) +
          " bdf=" + (p.bdf.empty() ? std::string("-") : p.bdf) + " part=" + std::to_string(p.partition_id) +
          " type=" + std::to_string(type) + " " + OneLine(message) + "\n";
+}
+
+std::string ProcessorFingerprint(const std::vector<smi::ProcessorInfo>& procs) {
+  std::vector<std::string> keys;
+  keys.reserve(procs.size());
+  for (const auto& p : procs)
+    keys.push_back(p.bdf + "/" + std::to_string(p.partition_id) + "/" + std::to_string(p.kfd_node) + "/" +
+                   p.compute_partition + "/" + p.memory_partition);
+  std::sort(keys.begin(), keys.end());
+  uint64_t h = 0xcbf29ce484222325ull;  // FNV-1a
+  for (const auto& k : keys) {
+    for (unsigned char c : k) h = (h ^ c) * 0x100000001b3ull;
+    h = (h ^ ';') * 0x100000001b3ull;
+  }
+  char buf[17];
+  snprintf(buf, sizeof(buf), "%016llx", static_cast<unsigned long long>(h));
+  return buf;
 }
 
 int ConnectRelay(const std::string& socket_path) {
@@ -234,7 +501,6 @@ int PingRelay(const std::string& socket_path, int timeout_ms) {
 }
 
 int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_fd, const RelayOptions& opts) {
-  const std::string& driver_root = opts.driver_root;
   sockaddr_un addr{};
   if (socket_path.empty() || socket_path.size() >= sizeof(addr.sun_path)) {
     LOG_ERROR(kComp, "--event-relay needs --health-event-socket (a path shorter than %zu bytes)",
@@ -253,168 +519,168 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     if (lfd >= 0) close(lfd);
     return 1;
   }
-
-  std::vector<smi::ProcessorInfo> procs;
-  std::vector<void*> handles;
-  std::string events_state;  // the hello line's tail
-  bool registered = false;   // event notification is registered on `handles`
-  auto enumerate_and_register = [&](bool reinit) {
-    if (registered) lib->EventsStop(handles);
-    registered = false;
-    handles.clear();
-    procs.clear();
-    if (reinit) {
-      if (Status st = lib->Reinit(); !st.ok()) {
-        events_state = "events=off reason=amdsmi re-initialisation failed: " + OneLine(st.ToString());
-        LOG_ERROR(kComp, "%s", events_state.c_str());
-        return;
-      }
-    }
-    auto en = lib->Enumerate();
-    if (!en.ok()) {
-      events_state = "events=off reason=enumeration failed: " + OneLine(en.status().ToString());
-      LOG_ERROR(kComp, "%s", events_state.c_str());
-      return;
-    }
-    procs = std::move(*en);
-    for (const auto& p : procs) handles.push_back(p.handle);
-    Status st = lib->EventsInit(handles, RelayMask());
-    registered = st.ok();
-    std::string why = st.ok() ? "" : OneLine(st.ToString());
-    if (int kerr = st.ok() ? 0 : inventory::KfdAccessErrno(driver_root); kerr == EPERM)
-      why += "; /dev/kfd not openable (EPERM) in the relay's container: run the relay privileged";
-    events_state = st.ok() ? "events=ok processors=" + std::to_string(procs.size()) : "events=off reason=" + why;
-    if (st.ok()) LOG_INFO(kComp, "event notification registered on %zu processor(s)", procs.size());
-    else LOG_ERROR(kComp, "event notification unavailable: %s", st.ToString().c_str());
-  };
-  // The amdsmi wait blocks (≤100 ms slices), so it runs on a thread of its
-  // own and hands formatted lines to the main loop through a pipe: the main
-  // loop sleeps in poll() on sockets, signals and that pipe, and answers a
-  // daemon's request at once. Re-enumeration stops the thread first (it reads
-  // `procs`, which only the main thread changes, and only then).
-  int pipefd[2];
-  if (pipe2(pipefd, O_CLOEXEC | O_NONBLOCK) != 0) {
+  // The waiter hands formatted event lines to this loop through one pipe, the
+  // registrar its renewal results through another: this loop sleeps in poll()
+  // on sockets, signals and those pipes, and answers a daemon at once.
+  int ev_pipe[2], done_pipe[2];
+  if (pipe2(ev_pipe, O_CLOEXEC | O_NONBLOCK) != 0) {
     LOG_ERROR(kComp, "pipe: %s", strerror(errno));
     close(lfd);
     return 1;
   }
-  // Watchdog: an amdsmi wait that has not returned for kStuckMs means events
-  // are not being delivered; the daemons are told (a "reinit" hello with
-  // events=off, so they poll) and told again when the wait returns.
+  if (pipe2(done_pipe, O_CLOEXEC | O_NONBLOCK) != 0) {
+    LOG_ERROR(kComp, "pipe: %s", strerror(errno));
+    close(ev_pipe[0]);
+    close(ev_pipe[1]);
+    close(lfd);
+    return 1;
+  }
+  // Watchdog: an amdsmi wait that has not returned (or has kept failing) for
+  // kStuckMs means events are not being delivered; the daemons are told (a
+  // "reinit" hello with events=off, so they poll) and told again when the wait
+  // returns.
   const int64_t kStuckMs = [] {
     const char* e = getenv("ADP_RELAY_STUCK_MS");
     return e && atoll(e) > 0 ? static_cast<int64_t>(atoll(e)) : int64_t{10000};
   }();
-  // The wait's slice (an event ends the wait at once): short, because
-  // re-enumeration -- every daemon (re)start asks for one -- must wait for the
-  // slice to end before it can stop the waiter; and well under the watchdog's
-  // threshold. Idle, that is ~10 wake-ups/s at 0.02% of a core (profiles/r4/idle/).
-  const int wait_slice_ms = static_cast<int>(std::max<int64_t>(10, std::min<int64_t>(100, kStuckMs / 4)));
-  std::atomic<bool> waiter_stop{false};
-  std::atomic<int64_t> beat_ms{0};  // the waiter's last sign of life (steady clock)
-  std::atomic<int> wait_failures{0};  // consecutive failed waits
-  auto now_ms = [] {
-    return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
-        .count();
-  };
-  std::thread waiter;
-  auto start_waiter = [&] {
-    if (!registered) return;
-    waiter_stop.store(false);
-    wait_failures.store(0);  // a fresh registration: earlier failures say nothing about it
-    beat_ms.store(now_ms());
-    waiter = std::thread([&] {
-      std::vector<smi::Event> events;
-      while (!waiter_stop.load()) {
-        events.clear();
-        beat_ms.store(now_ms());
-        Status st = lib->EventsWait(wait_slice_ms, &events);
-        beat_ms.store(now_ms());
-        if (!st.ok()) {
-          int n = wait_failures.fetch_add(1) + 1;
-          if (n == 1 || n % 600 == 0)  // the first, then one a minute
-            LOG_WARN(kComp, "event wait failed (%d in a row): %s", n, st.ToString().c_str());
-          usleep(100000);
-          continue;
-        }
-        wait_failures.store(0);
-        for (const auto& e : events) {
-          const smi::ProcessorInfo* p = nullptr;
-          for (const auto& q : procs)
-            if (q.handle == e.handle) p = &q;
-          if (!p) continue;
-          std::string line = FormatRelayEvent(*p, e.type, e.message);
-          if (write(pipefd[1], line.data(), line.size()) != static_cast<ssize_t>(line.size()))
-            LOG_WARN(kComp, "event dropped (relay loop behind): %s", OneLine(line).c_str());
-        }
-      }
-    });
-  };
-  auto stop_waiter = [&] {
-    if (!waiter.joinable()) return;
-    waiter_stop.store(true);
-    waiter.join();
-  };
-  enumerate_and_register(false);
-  start_waiter();
-  LOG_INFO(kComp, "relaying amdsmi events on %s", socket_path.c_str());
+  const std::string relay_id = RandomId();
+  // Heap-held: a waiter stuck in amdsmi at exit keeps using it (Shutdown).
+  auto* reg = new Registration(lib, opts.driver_root, ev_pipe[1], done_pipe[1], kStuckMs);
+  reg->Renew(false);
+  reg->StartRegistrar();
+  LOG_INFO(kComp, "relaying amdsmi events on %s (relay %s)", socket_path.c_str(), relay_id.c_str());
 
   struct Client {
     int fd;
     std::string in;
+    uint64_t id;
+    bool subscribed = false;  // sent its reinit: gets events and reinit hellos
+    int gap = 1;              // what its reinit hello says, unless the registration is renewed
   };
   std::vector<Client> clients;
+  uint64_t next_id = 1;
   ScanWorker scans(opts);
-  auto hello = [&]() { return "hello v1 " + events_state + "\n"; };
+  // The last kRelayRingSize events forwarded, for daemons that reconnect.
+  std::deque<std::pair<uint64_t, std::string>> ring;
+  uint64_t seq = 0;
+  bool stuck = false;
+  std::string stuck_reason;
+  auto hello = [&](bool reinit, int gap) {
+    Registration::State s = reg->Get();
+    bool ok = s.ok && !stuck;
+    std::string h = std::string("hello v1 ") + (reinit ? "reinit " : "") +
+                    (ok ? "events=ok processors=" + std::to_string(s.processors) : std::string("events=off")) +
+                    " relay=" + relay_id + " gen=" + std::to_string(s.gen) + " seq=" + std::to_string(seq);
+    if (gap >= 0) h += " gap=" + std::to_string(gap);
+    if (!ok) h += " reason=" + (stuck ? stuck_reason : s.reason);
+    return h + "\n";
+  };
+  auto send_to = [](Client& c, const std::string& s) {
+    if (c.fd >= 0 && !SendAll(c.fd, s)) {
+      close(c.fd);
+      c.fd = -1;
+    }
+  };
+  auto broadcast = [&](const std::string& s) {
+    for (auto& c : clients)
+      if (c.subscribed) send_to(c, s);
+  };
+  // "reinit fp=<fp> since=<relay>:<seq>:<gen>": replay what the daemon missed,
+  // decide whether it can have missed anything, and pass the fingerprint on.
+  auto subscribe = [&](Client& c, std::string_view line) {
+    std::string fp(Kv(line, "fp"));
+    auto since = Split(Kv(line, "since"), ':');
+    int gap = 1;
+    if (since.size() == 3 && since[0] == relay_id) {
+      auto s = ParseUint(since[1]);
+      auto g = ParseUint(since[2]);
+      if (s && g && *s <= seq) {
+        bool held = *s == seq || (!ring.empty() && ring.front().first <= *s + 1);
+        std::string replay;
+        size_t n = 0;
+        for (const auto& [q, l] : ring)
+          if (q > *s) {
+            replay += l;
+            ++n;
+          }
+        if (n) {
+          LOG_INFO(kComp, "replaying %zu event(s) after #%llu to a reconnected daemon%s", n,
+                   static_cast<unsigned long long>(*s), held ? "" : " (older ones are no longer held)");
+          send_to(c, replay);
+        }
+        gap = held && *g == reg->Get().gen ? 0 : 1;
+      }
+    }
+    c.subscribed = true;
+    c.gap = gap;
+    LOG_INFO(kComp, "daemon connected for events (%s)",
+             since.size() == 3 ? (gap ? "it may have missed events" : "nothing missed") : "a new daemon");
+    reg->Request(c.id, std::move(fp));
+  };
   int exit_code = 0;
   bool quit = false;
-  std::string pending;  // event bytes read from the pipe, up to the last full line
+  std::string pending, done_pending;  // bytes read from the pipes, up to the last full line
 
-  bool stuck = false;
-  std::string state_before_stuck;
-  auto broadcast = [&](const std::string& line) {
-    for (auto& c : clients)
-      if (c.fd >= 0 && !SendAll(c.fd, line)) {
-        close(c.fd);
-        c.fd = -1;
-      }
-  };
   while (!quit) {
-    std::vector<pollfd> pfds = {{signal_fd, POLLIN, 0}, {lfd, POLLIN, 0}, {pipefd[0], POLLIN, 0}};
+    std::vector<pollfd> pfds = {
+        {signal_fd, POLLIN, 0}, {lfd, POLLIN, 0}, {ev_pipe[0], POLLIN, 0}, {done_pipe[0], POLLIN, 0}};
+    constexpr size_t kFixed = 4;  // signals, listener, event pipe, renewal pipe
     for (const auto& c : clients) pfds.push_back({c.fd, POLLIN, 0});
-    int timeout = waiter.joinable() ? static_cast<int>(std::min<int64_t>(1000, kStuckMs / 2 + 1)) : -1;
+    int timeout = static_cast<int>(std::min<int64_t>(1000, kStuckMs / 2 + 1));
     if (poll(pfds.data(), pfds.size(), timeout) < 0 && errno != EINTR) break;
-    if (waiter.joinable()) {
-      int64_t silent = now_ms() - beat_ms.load();
+    if (reg->running()) {
+      int64_t silent = reg->SilentMs();
       // A wait that keeps failing delivers no more events than one that hangs.
-      int64_t failing_ms = static_cast<int64_t>(wait_failures.load()) * 100;
+      int64_t failing_ms = reg->FailingMs();
       if (!stuck && (silent > kStuckMs || failing_ms > kStuckMs)) {
         stuck = true;
-        state_before_stuck = events_state;
-        events_state = silent > kStuckMs
-                           ? "events=off reason=the amdsmi event wait has not returned for " + std::to_string(silent) +
-                                 " ms"
-                           : "events=off reason=the amdsmi event wait has failed for " + std::to_string(failing_ms) +
-                                 " ms";
-        LOG_ERROR(kComp, "%s: daemons fall back to polling", events_state.c_str());
-        broadcast("hello v1 reinit " + events_state + "\n");
+        stuck_reason = silent > kStuckMs
+                           ? "the amdsmi event wait has not returned for " + std::to_string(silent) + " ms"
+                           : "the amdsmi event wait has failed for " + std::to_string(failing_ms) + " ms";
+        LOG_ERROR(kComp, "events=off reason=%s: daemons fall back to polling", stuck_reason.c_str());
+        broadcast(hello(true, 1));
       } else if (stuck && silent <= kStuckMs && failing_ms <= kStuckMs) {
         stuck = false;
-        events_state = state_before_stuck;
         LOG_INFO(kComp, "the amdsmi event wait returned again: events back on");
-        broadcast("hello v1 reinit " + events_state + "\n");
+        broadcast(hello(true, 1));
       }
     }
     if (pfds[2].revents & POLLIN) {
       char buf[4096];
       ssize_t n;
-      while ((n = read(pipefd[0], buf, sizeof(buf))) > 0) pending.append(buf, static_cast<size_t>(n));
-      size_t cut = pending.rfind('\n');
-      if (cut != std::string::npos) {
-        std::string lines = pending.substr(0, cut + 1);
-        pending.erase(0, cut + 1);
-        LOG_INFO(kComp, "%s", OneLine(lines).c_str());
-        broadcast(lines);
+      while ((n = read(ev_pipe[0], buf, sizeof(buf))) > 0) pending.append(buf, static_cast<size_t>(n));
+      std::string out;
+      size_t nl;
+      while ((nl = pending.find('\n')) != std::string::npos) {
+        // "event node=..." -> "event seq=<n> node=...", held for replays
+        std::string line = "event seq=" + std::to_string(++seq) + pending.substr(5, nl - 4);
+        pending.erase(0, nl + 1);
+        ring.emplace_back(seq, line);
+        if (ring.size() > kRelayRingSize) ring.pop_front();
+        out += line;
+      }
+      if (!out.empty()) {
+        LOG_INFO(kComp, "%s", OneLine(out).c_str());
+        broadcast(out);
+      }
+    }
+    if (pfds[3].revents & POLLIN) {
+      char buf[512];
+      ssize_t n;
+      while ((n = read(done_pipe[0], buf, sizeof(buf))) > 0) done_pending.append(buf, static_cast<size_t>(n));
+      size_t nl;
+      while ((nl = done_pending.find('\n')) != std::string::npos) {
+        auto f = Split(std::string_view(done_pending).substr(0, nl), ' ');
+        done_pending.erase(0, nl + 1);
+        if (f.size() != 3) continue;
+        if (f[2] == "1") {
+          // Renewed: every subscribed daemon went without a registration meanwhile.
+          broadcast(hello(true, 1));
+        } else {
+          auto id = ParseUint(f[1]);
+          for (auto& c : clients)
+            if (id && c.id == *id) send_to(c, hello(true, c.gap));
+        }
       }
     }
     if (pfds[0].revents & POLLIN) {
@@ -422,31 +688,7 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
       while (read(signal_fd, &si, sizeof(si)) == sizeof(si))
         if (si.ssi_signo != SIGHUP && si.ssi_signo != SIGUSR1) quit = true;
     }
-    if (pfds[1].revents & POLLIN) {
-      int cfd;
-      while ((cfd = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK)) >= 0) {
-        // Only this relay's own uid (the plugin container runs as the same
-        // root) -- the socket's mode says so already; the kernel's peer
-        // credentials make sure.
-        ucred cred{};
-        socklen_t clen = sizeof(cred);
-        if (getsockopt(cfd, SOL_SOCKET, SO_PEERCRED, &cred, &clen) != 0 || cred.uid != geteuid()) {
-          LOG_WARN(kComp, "connection from uid %u refused", static_cast<unsigned>(cred.uid));
-          close(cfd);
-          continue;
-        }
-        if (!SendAll(cfd, hello())) {
-          close(cfd);
-          continue;
-        }
-        clients.push_back({cfd, ""});
-        // (a scan connection every poll: not worth an info line each)
-        LOG_DEBUG(kComp, "connection accepted (%zu client(s))", clients.size());
-      }
-    }
-    bool do_reinit = false;
-    // Only the clients polled above (accept may have appended new ones).
-    constexpr size_t kFixed = 3;  // signals, listener, event pipe
+    // Only the clients polled above (accept below appends new ones).
     const size_t polled = pfds.size() - kFixed;
     for (size_t i = 0; i < polled; ++i) {
       auto& c = clients[i];
@@ -468,10 +710,7 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
       size_t nl;
       while (c.fd >= 0 && (nl = c.in.find('\n')) != std::string::npos) {
         std::string_view line(c.in.data(), nl);
-        if (line == "reinit") {
-          do_reinit = true;
-          LOG_INFO(kComp, "daemon connected for events");
-        }
+        if (line == "reinit" || line.rfind("reinit ", 0) == 0) subscribe(c, line);
         if (line.rfind("scan\t", 0) == 0) {
           // "scan\t<usage dir>\t<cgroup>": the connection becomes the scan's.
           size_t tab = line.find('\t', 5);
@@ -489,38 +728,39 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
         c.in.erase(0, nl + 1);
       }
     }
+    if (pfds[1].revents & POLLIN) {
+      int cfd;
+      while ((cfd = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK)) >= 0) {
+        // Only this relay's own uid (the plugin container runs as the same
+        // root) -- the socket's mode says so already; the kernel's peer
+        // credentials make sure.
+        ucred cred{};
+        socklen_t clen = sizeof(cred);
+        if (getsockopt(cfd, SOL_SOCKET, SO_PEERCRED, &cred, &clen) != 0 || cred.uid != geteuid()) {
+          LOG_WARN(kComp, "connection from uid %u refused", static_cast<unsigned>(cred.uid));
+          close(cfd);
+          continue;
+        }
+        if (!SendAll(cfd, hello(false, -1))) {
+          close(cfd);
+          continue;
+        }
+        clients.push_back({cfd, "", next_id++});
+        // (a scan connection every poll: not worth an info line each)
+        LOG_DEBUG(kComp, "connection accepted (%zu client(s))", clients.size());
+      }
+    }
     clients.erase(std::remove_if(clients.begin(), clients.end(), [](const Client& c) { return c.fd < 0; }),
                   clients.end());
-    const bool hung = waiter.joinable() && now_ms() - beat_ms.load() > kStuckMs;
-    if (do_reinit) {
-      if (hung) {
-        // amdsmi cannot be re-initialised under a wait that does not return:
-        // the daemon gets the current (events off) state instead.
-        LOG_WARN(kComp, "re-enumeration a daemon asked for skipped: the event wait is stuck");
-      } else {
-        LOG_INFO(kComp, "re-enumerating (a daemon asked)");
-        stop_waiter();
-        enumerate_and_register(true);
-        start_waiter();
-      }
-      // Marked, so a daemon tells the state after its own request from the
-      // hello every connection gets first (sent before the request was read).
-      broadcast("hello v1 reinit " + events_state + "\n");
-    }
   }
-  if (waiter.joinable() && now_ms() - beat_ms.load() > kStuckMs) {
-    // Joining would wait on the hung call; the process is about to exit.
-    LOG_WARN(kComp, "exiting with the event wait still stuck");
-    waiter.detach();
-  } else {
-    stop_waiter();
-    if (!handles.empty() && registered) lib->EventsStop(handles);
-  }
+  if (reg->Shutdown()) {
+    delete reg;
+    close(ev_pipe[1]);
+    close(done_pipe[1]);
+  }  // else a waiter stuck in amdsmi still holds it and the pipe's write end; the process exits next
   for (auto& c : clients)
     if (c.fd >= 0) close(c.fd);
-  close(pipefd[0]);
-  close(pipefd[1]);
-  close(lfd);
+  for (int fd : {ev_pipe[0], done_pipe[0], lfd}) close(fd);
   unlink(socket_path.c_str());
   LOG_INFO(kComp, "event relay stopped");
   return exit_code;

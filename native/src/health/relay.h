@@ -8,37 +8,68 @@
 // monitoring needs it, else drop-ALL
 // (/root/reference/deployments/helm/nvidia-device-plugin/templates/daemonset.yml:80-93);
 // here only the relay container is privileged, and it parses no network or
-// kubelet input -- one line per client, "reinit", is all it reads.
+// kubelet input -- one line per client, "reinit" or "scan", is all it reads.
+//
+// A GPU_POST_RESET nobody is registered for is lost for good (a GPU waiting
+// for it stays out of service, health.h), so the relay is built not to lose
+// events itself:
+//  * every forwarded event carries a sequence number and the relay keeps the
+//    last kRelayRingSize of them; a daemon that reconnects (a new monitor
+//    generation: SIGHUP, config reload, kubelet restart, re-partition) names
+//    the last one it handled and gets the ones it missed replayed;
+//  * a daemon's reinit re-enumerates amdsmi only when the daemon's view of the
+//    processors (ProcessorFingerprint) differs from the relay's registration --
+//    a re-partition -- or the event wait is failing; otherwise the registration,
+//    and the kernel's event queue behind it, is kept;
+//  * re-enumeration (amdsmi shut_down + init) runs on a thread of its own: the
+//    poll loop keeps greeting, scanning and forwarding meanwhile.
+// What cannot be replayed is reported as a gap ("gap=1"), and the daemon
+// falls back to its polled recovery check for GPUs waiting across it.
 //
 // Wire protocol (text lines over SOCK_STREAM):
-//   relay -> daemon  "hello v1 events=ok processors=<n>"         (on connect)
-//                    "hello v1 events=off reason=<text>"       (registration failed)
-//                    "hello v1 reinit events=ok processors=<n>" (after a "reinit")
-//                    "hello v1 reinit events=off reason=..."   (watchdog: the amdsmi
-//                                 wait has not returned, or has kept failing, for
-//                                 ADP_RELAY_STUCK_MS, default 10 s; "events=ok"
-//                                 again once waits succeed)
-//                    "event node=<kfd node|-> bdf=<bdf> part=<partition id> type=<t> <message>"
-//   daemon -> relay  "reinit"   re-enumerate (amdsmi_shut_down + init) and register
-//                               again, then a "reinit" hello to every client (a new
-//                               daemon generation, e.g. after a re-partition). A
-//                               daemon takes its event state from that hello only:
-//                               the connect hello predates the re-registration.
+//   relay -> daemon  "hello v1 events=ok processors=<n> relay=<id> gen=<g> seq=<s>"   (on connect)
+//                    "hello v1 events=off relay=<id> gen=<g> seq=<s> reason=<text>"
+//                    "hello v1 reinit events=ok processors=<n> relay=<id> gen=<g> seq=<s> gap=<0|1>"
+//                          the answer to a reinit (to every subscribed client when
+//                          the registration was renewed, gap=1 then), and the
+//                          watchdog's "events=off ... reason=the amdsmi event wait
+//                          has not returned / has failed for <ms> ms" when the wait
+//                          hangs or keeps failing for ADP_RELAY_STUCK_MS (default
+//                          10 s), "events=ok" again once waits succeed
+//                    "event seq=<n> node=<kfd node|-> bdf=<bdf> part=<partition id> type=<t> <message>"
+//                          relay: a random ID of this relay process; gen: its
+//                          registration generation (+1 on each re-registration);
+//                          seq: the last event sequence number it forwarded
+//   daemon -> relay  "reinit fp=<fingerprint> since=<relay>:<seq>:<gen>|-"
+//                          subscribe to events: replays the events after <seq>
+//                          that were forwarded while this daemon was away (when
+//                          <relay> is this relay and they are still held),
+//                          re-enumerates only if <fingerprint> differs from the
+//                          registration's (or the wait fails), then answers with a
+//                          reinit hello; gap=0 when nothing can have been missed
+//                          since <seq>. A bare "reinit" (older daemons) always
+//                          re-enumerates and is answered gap=1. A daemon takes its
+//                          event state from that hello only: the connect hello
+//                          predates its request.
 //                    "scan\t<usage dir>\t<daemon cgroup>"
-//                               one driver-side HBM scan (memcap/driver_usage.h) of
-//                               the relay's --host-proc: the reply is SerializeScan's
-//                               text, then the relay closes that connection (it gets
-//                               no events). Reading other containers' /proc/<pid>/fd
-//                               needs CAP_SYS_PTRACE; with the scan here the daemon
-//                               needs no capability at all.
+//                          one driver-side HBM scan (memcap/driver_usage.h) of
+//                          the relay's --host-proc: the reply is SerializeScan's
+//                          text, then the relay closes that connection (it gets
+//                          no events). Reading other containers' /proc/<pid>/fd
+//                          needs CAP_SYS_PTRACE; with the scan here the daemon
+//                          needs no capability at all.
 #pragma once
 
+#include <cstdint>
 #include <string>
 #include <string_view>
+#include <vector>
 
 #include "smi/smi.h"
 
 namespace adp::health {
+
+constexpr size_t kRelayRingSize = 1024;
 
 // One parsed relay line (ParseRelayLine). kind: "hello", "event" or "" (malformed).
 struct RelayLine {
@@ -46,6 +77,10 @@ struct RelayLine {
   bool events_ok = false;
   bool after_reinit = false;  // hello sent after a re-enumeration a daemon asked for
   std::string reason;      // hello with events=off
+  std::string relay;       // hello: the relay's instance ID ("" = an older relay)
+  uint64_t gen = 0;        // hello: registration generation
+  uint64_t seq = 0;        // hello: last event forwarded; event: its sequence number (0 = none)
+  int gap = -1;            // reinit hello: 0 nothing missed, 1 events may have been missed, -1 not said
   uint32_t node = 0xffffffffu;  // KFD topology node of the processor ("-" = unreported)
   std::string bdf;
   uint32_t part = 0;
@@ -53,7 +88,14 @@ struct RelayLine {
   std::string message;
 };
 RelayLine ParseRelayLine(std::string_view line);
+// Without the sequence number (the relay's waiter thread; the poll loop numbers the lines).
 std::string FormatRelayEvent(const smi::ProcessorInfo& p, uint32_t type, const std::string& message);
+
+// 16 hex digits identifying a processor layout: every processor's PCI address,
+// partition ID, KFD node and partition modes, order-independent. Daemon and
+// relay compute it from their own enumerations; equal means the relay's event
+// registration covers the daemon's processors.
+std::string ProcessorFingerprint(const std::vector<smi::ProcessorInfo>& procs);
 
 // Runs the relay until SIGTERM/SIGINT/SIGQUIT (the caller blocked them and
 // passes their signalfd): binds `socket_path` (owner-only; connections from

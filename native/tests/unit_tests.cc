@@ -184,6 +184,32 @@ static void TestResourceConfig() {
   CHECK(std::string(alloc::ReplicaPolicyName(alloc::ReplicaPolicy::kAuto)) == "auto");
 }
 
+static void TestLedgerGaps() {
+  g_case = "ledger-gaps";
+  health::Ledger l;
+  health::GapMark m;
+  CHECK(!l.Gap("a", &m));
+  CHECK(l.MarkGap("a", "relay dropped", true, 100));     // new: worth a log line
+  CHECK(!l.MarkGap("a", "relay dropped", true, 200));    // again: not
+  CHECK(l.Gap("a", &m) && m.tentative && m.since_ms == 100);
+  CHECK(l.MarkGap("a", "relay renewed", false, 300));    // confirmed: logged, keeps its start
+  CHECK(l.Gap("a", &m) && !m.tentative && m.since_ms == 100 && m.why == "relay renewed");
+  CHECK(!l.MarkGap("a", "other", true, 400));            // a confirmed mark never goes back to tentative
+  CHECK(l.MarkGap("b", "relay dropped", true, 500));
+  l.SetResponsiveSince("b", 600);
+  CHECK(l.Gap("b", &m) && m.responsive_since_ms == 600);
+  auto cancelled = l.CancelTentativeGaps();              // the relay replayed what b missed
+  CHECK(cancelled.size() == 1 && cancelled[0] == "b" && !l.Gap("b", nullptr) && l.Gap("a", nullptr));
+  l.ClearGap("a");
+  CHECK(!l.Gap("a", nullptr));
+  // gaps are not part of the state file
+  health::GpuRecord r;
+  r.fail = health::kFailResetPending;
+  l.Put("c", r);
+  l.MarkGap("c", "x", false, 1);
+  CHECK(health::Ledger::Serialize(l.All()) == "adp-health v1\nc\t-\t0\t4\t\n");
+}
+
 static void TestRelayLines() {
   g_case = "relay-lines";
   smi::ProcessorInfo p;
@@ -206,8 +232,37 @@ static void TestRelayLines() {
   CHECK(r.kind == "hello" && !r.events_ok && r.reason == "NO_PERM: denied");
   for (const char* bad : {"", "event", "event node=x bdf=a part=0 type=3", "event node=1 bdf=a part=0",
                           "event node=1 bdf=a part=-1 type=3", "event node=4294967295 bdf=a part=0 type=3",
-                          "bogus line", "event node=1 bdf=a part=0 type=99999999999"})
+                          "bogus line", "event node=1 bdf=a part=0 type=99999999999",
+                          "event seq=x node=1 bdf=a part=0 type=3"})
     CHECK(health::ParseRelayLine(bad).kind.empty());
+  // sequence numbers, the relay's cursor fields and gap
+  r = health::ParseRelayLine("event seq=42 node=10 bdf=0000:0c:00.1 part=1 type=4 reset done");
+  CHECK(r.kind == "event" && r.seq == 42 && r.node == 10 && r.type == 4 && r.message == "reset done");
+  r = health::ParseRelayLine("hello v1 reinit events=ok processors=8 relay=00ff00ff00ff00ff gen=3 seq=17 gap=0");
+  CHECK(r.kind == "hello" && r.after_reinit && r.events_ok && r.relay == "00ff00ff00ff00ff" && r.gen == 3 &&
+        r.seq == 17 && r.gap == 0);
+  // keys inside the reason are not the hello's
+  r = health::ParseRelayLine("hello v1 reinit events=off relay=ab gen=2 seq=5 gap=1 reason=x gap=0 events=ok");
+  CHECK(!r.events_ok && r.gap == 1 && r.reason == "x gap=0 events=ok" && r.seq == 5);
+  r = health::ParseRelayLine("hello v1 events=ok processors=8");  // an older relay: no gap said
+  CHECK(r.gap == -1 && r.relay.empty());
+
+  // processor fingerprints: order-independent, sensitive to every field
+  smi::ProcessorInfo q = p;
+  q.bdf = "0000:0d:00.0";
+  q.kfd_node = 11;
+  std::string fp = health::ProcessorFingerprint({p, q});
+  CHECK(fp.size() == 16 && fp == health::ProcessorFingerprint({q, p}));
+  CHECK(fp != health::ProcessorFingerprint({p}));
+  smi::ProcessorInfo q2 = q;
+  q2.compute_partition = "CPX";
+  CHECK(fp != health::ProcessorFingerprint({p, q2}));
+  q2 = q;
+  q2.kfd_node = 12;
+  CHECK(fp != health::ProcessorFingerprint({p, q2}));
+  q2 = q;
+  q2.partition_id = 2;
+  CHECK(fp != health::ProcessorFingerprint({p, q2}));
 
   // the relay's scan reply
   memcap::DriverScan scan;
@@ -1166,6 +1221,7 @@ int main() {
   TestAdditionalIds();
   TestResourceConfig();
   TestRelayLines();
+  TestLedgerGaps();
   TestDrainSyntax();
   TestRemoteScan();
   TestProto();

@@ -32,7 +32,7 @@ def _preload(*libs):
 
 
 class RelayNode:
-    def __init__(self, scratch, relay_env=None):
+    def __init__(self, scratch, relay_env=None, daemon_args=(), daemon_env=None):
         self.scratch = scratch
         self.fifo = os.path.join(scratch + ".fixture", "events")
         os.makedirs(scratch + ".fixture", exist_ok=True)
@@ -44,8 +44,9 @@ class RelayNode:
         self.start_relay()
         self.k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
         self.d = harness.Daemon(scratch, self.fx, args=["--health-event-socket", self.sock,
-                                                        "--metrics-addr", "127.0.0.1:0"],
-                                env={"LD_PRELOAD": _preload(SIM), "DP_HEALTH_POLL_MS": "200"}).start()
+                                                        "--metrics-addr", "127.0.0.1:0", *daemon_args],
+                                env={"LD_PRELOAD": _preload(SIM), "DP_HEALTH_POLL_MS": "200",
+                                     **(daemon_env or {})}).start()
         self.port = int(re.search(r"on port (\d+)", self.d.wait_log("serving /metrics")).group(1))
         reg = self.k.wait_registration()
         self.c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
@@ -68,6 +69,26 @@ class RelayNode:
     def health(self, timeout=5):
         law = self.q.get(timeout=timeout)
         return [x.health for x in law.devices]
+
+    def rewatch(self, timeout=15):
+        """Follow the plugin's next registration (a SIGHUP restarts it); the
+        first ListAndWatch of the new generation."""
+        self.call.cancel()
+        self.c.close()
+        reg = self.k.wait_registration(timeout)
+        self.c = kubelet.PluginClient(os.path.join(self.scratch, reg.endpoint))
+        self.q, self.call = self.c.watch()
+        return self.health()
+
+    def wait_health(self, want, timeout=10):
+        deadline = time.time() + timeout
+        while True:
+            h = self.health(timeout=max(0.05, deadline - time.time()))
+            if h == want:
+                return h
+
+    def bdf(self, gpu):
+        return self.fx["gpus"][gpu]["bdf"]
 
     def metrics(self):
         return _parse(_get(self.port, "/metrics")[1])
@@ -96,7 +117,9 @@ def test_reset_events_travel_through_the_relay(scratch):
         n.d.wait_log("VMFAULT(1) on GPU 0")
         rlog = n.relay.log()
         assert "event notification registered on 2 processor(s)" in rlog
-        assert "daemon connected for events" in rlog and "re-enumerating (a daemon asked)" in rlog
+        assert "daemon connected for events (a new daemon)" in rlog
+        # The daemon's processors match the relay's registration: kept, not re-enumerated.
+        assert "registration kept (a daemon's processors match it" in rlog and "re-enumerating" not in rlog
     finally:
         n.stop()
 
@@ -392,7 +415,7 @@ def test_partition_events_through_the_relay(scratch):
         bdf1 = fx["gpus"][1]["bdf"][:-1]  # partitions report their own function numbers
         sick = sorted(x.ID for x in law.devices if x.health == "Unhealthy")
         assert len(sick) == 8, [x.health for x in law.devices]
-        assert "event node=13 " in relay.log()  # KFD node 2 + 8*1 + partition 3
+        assert " node=13 " in relay.log()  # KFD node 2 + 8*1 + partition 3
         d.wait_log("GPU_PRE_RESET")
         assert bdf1 in d.log()
         call.cancel()
@@ -433,3 +456,144 @@ def test_relay_refuses_other_uids(scratch, tmp_path):
     finally:
         relay.stop()
         shutil.rmtree(sdir, ignore_errors=True)
+
+
+# --- event gaps: a GPU_POST_RESET nobody received ----------------------------------
+
+
+def _series(metrics, name, bdf):
+    for (n, labels), v in metrics.items():
+        if n == name and dict(labels).get("bdf") == bdf:
+            return v
+    return None
+
+
+def test_relay_killed_between_pre_and_post_reset_recovers_by_polling(scratch):
+    """GPU_PRE_RESET arrives, then the relay dies (SIGKILL) and the reset
+    completes while nobody is registered: the GPU_POST_RESET is lost. The new
+    relay cannot replay it (another relay instance), so the daemon records an
+    event gap on the waiting GPU; once amdsmi has answered every poll for
+    --reset-recovery-hold-ms it is Healthy again, logged and counted. The other
+    GPU never changes."""
+    n = RelayNode(scratch, daemon_args=["--reset-recovery-hold-ms", "2500"])
+    try:
+        n.d.wait_log("events on through the relay")
+        n.inject("1 3 mode1 reset")
+        assert n.health() == ["Healthy", "Unhealthy"]
+        t_kill = time.time()
+        n.relay.proc.kill()
+        n.relay.proc.wait(timeout=10)
+        n.d.wait_log("event relay: the event relay closed the connection")
+        n.start_relay()  # (the reset's POST happened in between: nobody received it)
+        n.d.wait_log("renewed its registration or no longer holds the events missed", timeout=10)
+        log = n.d.wait_log("waits for GPU_POST_RESET across an event gap")
+        assert n.bdf(1) in log
+        m = n.metrics()
+        assert _series(m, "amdgpu_dp_gpu_awaiting_polled_recovery", n.bdf(1)) == 1
+        assert _series(m, "amdgpu_dp_gpu_awaiting_polled_recovery", n.bdf(0)) == 0
+        assert n.wait_health(["Healthy", "Healthy"], timeout=15) == ["Healthy", "Healthy"]
+        assert time.time() - t_kill >= 2.4  # not before the hold
+        line = [ln for ln in n.d.log().splitlines() if "recovered without GPU_POST_RESET" in ln]
+        assert len(line) == 1 and n.bdf(1) in line[0] and "amdsmi answered every poll for" in line[0], line
+        m = n.metrics()
+        assert _series(m, "amdgpu_dp_gpu_recovered_without_event_total", n.bdf(1)) == 1
+        assert _series(m, "amdgpu_dp_gpu_recovered_without_event_total", n.bdf(0)) == 0
+        assert _series(m, "amdgpu_dp_gpu_awaiting_polled_recovery", n.bdf(1)) == 0
+        assert _value(m, "amdgpu_dp_health_event_gaps_total") >= 1
+        # events flow through the new relay as before
+        n.inject("0 3 reset")
+        assert n.health() == ["Unhealthy", "Healthy"]
+    finally:
+        n.stop()
+
+
+def test_events_missed_across_a_sighup_are_replayed(scratch):
+    """The daemon's SIGHUP closes its relay connection for a moment (a new
+    monitor generation); a GPU_POST_RESET relayed meanwhile is replayed to the
+    new connection, so the GPU is Healthy at once -- not after the polled
+    hold, which is set out of reach here -- and the relay kept its registration
+    (the daemon's processors match it)."""
+    n = RelayNode(scratch, daemon_args=["--reset-recovery-hold-ms", "600000"],
+                  daemon_env={"ADP_DEBUG_PUBLISH_DELAY_MS": "800"})
+    try:
+        n.d.wait_log("events on through the relay")
+        n.inject("1 3 mode1 reset")
+        assert n.health() == ["Healthy", "Unhealthy"]
+        n.d.signal(signal.SIGHUP)
+        n.d.wait_log("retrieving plugins", count=2)  # the old monitor is stopped: nobody subscribed
+        n.inject("1 4 reset done")
+        n.relay.wait_log(" type=4 ")  # relayed while the daemon was away
+        first = n.rewatch()
+        if first != ["Healthy", "Healthy"]:
+            n.wait_health(["Healthy", "Healthy"], timeout=5)
+        rlog = n.relay.wait_log("replaying 1 event(s)")
+        assert "daemon connected for events (nothing missed)" in rlog
+        assert "re-enumerating" not in rlog and rlog.count("registration kept") == 2
+        assert "recovered without GPU_POST_RESET" not in n.d.log()
+        assert "across an event gap" not in n.d.log()
+    finally:
+        n.stop()
+
+
+def test_a_pre_reset_without_a_gap_keeps_waiting(scratch):
+    """No gap since GPU_PRE_RESET (SIGHUPs only: the relay replays what the
+    daemon missed and says nothing was lost): the GPU waits for its
+    GPU_POST_RESET however long amdsmi answers -- today's rule -- and the event
+    still ends the wait."""
+    n = RelayNode(scratch, daemon_args=["--reset-recovery-hold-ms", "500"])
+    try:
+        n.d.wait_log("events on through the relay")
+        n.inject("0 3 pre-reset")
+        assert n.health() == ["Unhealthy", "Healthy"]
+        for i in range(2):
+            n.d.signal(signal.SIGHUP)
+            assert n.rewatch() == ["Unhealthy", "Healthy"]
+        n.relay.wait_log("daemon connected for events (nothing missed)", count=2)
+        time.sleep(2.0)  # four times the hold, ten polls
+        assert "recovered without GPU_POST_RESET" not in n.d.log()
+        assert n.q.empty() or all(h[0] == "Unhealthy" for h in [n.health(0.1)])
+        n.inject("0 4 post-reset")
+        n.wait_health(["Healthy", "Healthy"])
+    finally:
+        n.stop()
+
+
+def test_sighup_storm_with_interleaved_resets_leaves_no_gpu_stuck(scratch):
+    """SIGHUPs back to back with GPU_PRE_RESET / GPU_POST_RESET pairs injected
+    at every point of the restart -- before, during and after the daemon's
+    reconnection -- and one relay restart in the middle: every GPU ends
+    Healthy, by the events themselves (the polled hold is out of reach), and
+    the relay never re-enumerated for a daemon whose processors it had."""
+    import random
+    rnd = random.Random(5)
+    n = RelayNode(scratch, daemon_args=["--reset-recovery-hold-ms", "600000"])
+    try:
+        n.d.wait_log("events on through the relay")
+        for i in range(16):
+            gpu = i % 2
+            n.inject(f"{gpu} 3 storm pre {i}")
+            n.d.signal(signal.SIGHUP)
+            time.sleep(rnd.uniform(0, 0.25))
+            if i == 8:
+                # a relay restart between PRE and POST, the POST after it: received
+                n.relay.signal(signal.SIGTERM)
+                n.relay.proc.wait(timeout=10)
+                n.start_relay()
+                n.d.wait_log("connected to the event relay", count=1, timeout=10)
+            n.inject(f"{gpu} 4 storm post {i}")
+            time.sleep(rnd.uniform(0, 0.25))
+        deadline = time.time() + 20
+        h = n.rewatch()
+        while h != ["Healthy", "Healthy"]:
+            assert time.time() < deadline, (h, n.d.log()[-4000:])
+            try:
+                h = n.health(timeout=1)
+            except Exception:
+                h = n.rewatch()
+        dlog = n.d.log()
+        assert dlog.count("received SIGHUP") == 16
+        assert "recovered without GPU_POST_RESET" not in dlog
+        rlog = n.relay.log()
+        assert "re-enumerating" not in rlog, rlog
+    finally:
+        n.stop()

@@ -436,3 +436,59 @@ def test_retired_pages_default_to_the_drivers_threshold(mk, readable):
     else:
         time.sleep(0.5)
         assert "retired HBM pages" not in n.d.log()
+
+
+def test_in_process_regeneration_is_an_event_gap(mk):
+    """Without the relay, every monitor generation registers amdsmi events
+    afresh: a GPU_POST_RESET sent between the old registration and the new one
+    reached nobody. A GPU waiting for it across that gap goes back in service
+    once amdsmi has answered every poll for --reset-recovery-hold-ms."""
+    n = mk(args=["--reset-recovery-hold-ms", "1000"])
+    ids = sorted(n.start())
+    n.inject("0 3 pre-reset")
+    n.wait_health(lambda h: h[ids[0]] == "Unhealthy")
+    time.sleep(1.5)  # no gap yet: the hold does not run
+    assert "recovered without GPU_POST_RESET" not in n.d.log()
+    n.d.signal(signal.SIGHUP)
+    assert n.first_law() == {ids[0]: "Unhealthy", ids[1]: "Healthy"}
+    log = n.d.wait_log("waits for GPU_POST_RESET across an event gap")
+    assert "registration renewed by a new monitor generation" in log
+    n.wait_health(lambda h: h[ids[0]] == "Healthy", timeout=10)
+    assert n.d.log().count("recovered without GPU_POST_RESET") == 1
+
+
+def test_hold_zero_keeps_the_strict_rule(mk):
+    """--reset-recovery-hold-ms=0: only the event brings the GPU back, gap or not."""
+    n = mk(args=["--reset-recovery-hold-ms", "0"])
+    ids = sorted(n.start())
+    n.inject("0 3 pre-reset")
+    n.wait_health(lambda h: h[ids[0]] == "Unhealthy")
+    n.d.signal(signal.SIGHUP)
+    assert n.first_law() == {ids[0]: "Unhealthy", ids[1]: "Healthy"}
+    assert "only the event (or the operator) brings it back" in n.d.wait_log("across an event gap")
+    time.sleep(1.0)
+    assert "recovered without" not in n.d.log()
+    n.inject("0 4 post-reset")
+    n.wait_health(lambda h: h[ids[0]] == "Healthy")
+
+
+def test_failing_event_waits_are_a_gap(mk):
+    """In-process event waits that keep failing (ADP_EVENT_FAIL_MS) deliver no
+    GPU_POST_RESET either: a GPU waiting across them is recovered by polling;
+    a new GPU_PRE_RESET afterwards starts a fresh wait that only a new gap (or
+    the event) ends."""
+    n = mk(args=["--reset-recovery-hold-ms", "800"], env={"ADP_EVENT_FAIL_MS": "300"})
+    ids = sorted(n.start())
+    n.inject("1 3 pre-reset")
+    n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+    n.inject("fail 20")  # ~2 s of failed waits
+    n.d.wait_log("amdsmi event waits have failed for")
+    n.wait_health(lambda h: h[ids[1]] == "Healthy", timeout=10)
+    assert "event gap (amdsmi event waits failing)" in n.d.log()
+    n.d.wait_log("amdsmi event waits succeed again", timeout=10)
+    n.inject("1 3 pre-reset again")
+    n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+    time.sleep(1.6)  # twice the hold: no gap since this PRE_RESET
+    assert n.d.log().count("recovered without GPU_POST_RESET") == 1
+    n.inject("1 4 post-reset")
+    n.wait_health(lambda h: h[ids[1]] == "Healthy")
