@@ -214,7 +214,8 @@ const std::vector<FlagDef>& Table() {
        [](Flags& f) -> void* { return &f.loop_affinity; }},
       {"node-labels-file", "DP_NODE_LABELS_FILE", "nodeLabelsFile", Kind::kString,
        "write node-feature labels (amd.com/gpu.product, .count, .memory-mib, partition modes, "
-       "interconnect) to this file for node-feature-discovery's local source (empty = off)",
+       "interconnect; amd.com/<resource>.memory-unit and .memory-unit-mib for memory-unit resources) to this "
+       "file for node-feature-discovery's local source (empty = off)",
        [](Flags& f) -> void* { return &f.node_labels_file; }},
       {"pod-resources-socket", "DP_POD_RESOURCES_SOCKET", "podResourcesSocket", Kind::kString,
        "kubelet PodResources socket; with --metrics-addr, per-device allocations and "

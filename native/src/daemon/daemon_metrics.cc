@@ -111,6 +111,14 @@ void AppendDaemonMetrics(const DaemonMetricsInput& in, std::string* out) {
     Family(out, "amdgpu_dp_gpu_hbm_used_bytes", "gauge", "HBM in use on the GPU, all processes (last health poll).");
     for (const auto& [bdf, n] : used) Sample(out, "amdgpu_dp_gpu_hbm_used_bytes", Bdf(bdf), Num(n));
   }
+  if (!in.layout_changes_live.empty()) {
+    Family(out, "amdgpu_dp_replica_layout_changes_with_live_allocations_total", "counter",
+           "Plugin restarts that changed what a replicated resource's IDs mean (memory unit, replica count) while "
+           "running pods held some of them (kubelet PodResources).");
+    for (const auto& [res, n] : in.layout_changes_live)
+      Sample(out, "amdgpu_dp_replica_layout_changes_with_live_allocations_total",
+             "resource=\"" + metrics::LabelValue(res) + "\"", Num(n));
+  }
   if (in.pod_resources_up >= 0) {
     Family(out, "amdgpu_dp_pod_resources_up", "gauge", "1 if the kubelet PodResources API answered.");
     Sample(out, "amdgpu_dp_pod_resources_up", "", in.pod_resources_up ? "1" : "0");

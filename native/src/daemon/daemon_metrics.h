@@ -11,6 +11,7 @@
 #pragma once
 
 #include <cstdint>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -35,6 +36,8 @@ struct DaemonMetricsInput {
   std::vector<inventory::NodeAccess> node_access;
   int pod_resources_up = -1;  // -1: no PodResources socket configured
   const memcap::DriverHbmMonitor::Snapshot* driver_hbm = nullptr;  // null: the check is off
+  // Per resource: restarts that changed what its IDs mean while running pods held some.
+  std::map<std::string, uint64_t> layout_changes_live;
 };
 
 void AppendDaemonMetrics(const DaemonMetricsInput& in, std::string* out);

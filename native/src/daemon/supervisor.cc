@@ -114,10 +114,13 @@ std::string InstallPreloadList(const Flags& f) {
   return path;
 }
 
-// Atomically replaces `path` with one `key=value` line per label.
-void WriteLabels(const std::string& path, const inventory::Snapshot& snap) {
+// Atomically replaces `path` with one `key=value` line per label: the node's
+// (inventory::NodeLabels) and `extra` (the served resources').
+void WriteLabels(const std::string& path, const inventory::Snapshot& snap,
+                 const std::vector<std::pair<std::string, std::string>>& extra) {
   std::string body;
   for (const auto& [k, v] : inventory::NodeLabels(snap)) body += k + "=" + v + "\n";
+  for (const auto& [k, v] : extra) body += k + "=" + v + "\n";
   std::string tmp = path + ".tmp";
   FILE* f = fopen(tmp.c_str(), "w");
   bool ok = f && fwrite(body.data(), 1, body.size(), f) == body.size();
@@ -302,6 +305,7 @@ class Supervisor {
     {
       std::lock_guard<std::mutex> lk(access_mu_);
       in.node_access = node_access_;
+      in.layout_changes_live = layout_changes_live_;
       for (const auto& [key, bdf] : metrics_gpus_) {
         uint32_t fail = ledger_.Get(key).fail;
         bool gap = (fail & health::kFailResetPending) && ledger_.Gap(key, nullptr);
@@ -527,7 +531,6 @@ class Supervisor {
       ScheduleRetry("enumeration failed");
       return;
     }
-    if (!cfg_.flags.node_labels_file.empty()) WriteLabels(cfg_.flags.node_labels_file, **snap);
     {
       auto access = inventory::ProbeDeviceAccess(**snap, cfg_.flags.driver_root);
       std::string what = inventory::DescribeAccess(access);
@@ -553,10 +556,105 @@ class Supervisor {
     StartDriverHbm();
     health::HealthConfig hcfg = HealthConfigNow();
     PublishPlugins(*snap, *specs, !hcfg.disabled);
+    if (!cfg_.flags.node_labels_file.empty()) WriteLabels(cfg_.flags.node_labels_file, **snap, ResourceLabels());
+    CheckReplicaLayouts();
     int started = StartPlugins();
     if (started < 0) return;
     if (started == 0) LOG_INFO(kComp, "no devices found; waiting indefinitely");
     StartMonitor(*snap, hcfg);
+  }
+
+  // Per memory-unit resource: what one unit is, where pod authors (and
+  // schedulers) can read it -- amd.com/<resource>.memory-unit-mib and
+  // .memory-unit (cu-slot or mib).
+  std::vector<std::pair<std::string, std::string>> ResourceLabels() {
+    std::vector<std::pair<std::string, std::string>> out;
+    std::lock_guard<std::mutex> lk(plugins_mu_);
+    for (const auto& p : plugins_) {
+      if (!p->memory_units() || p->device_count() == 0) continue;
+      const std::string key = p->resource_name();  // "<prefix>/<name>"
+      out.emplace_back(key + ".memory-unit", p->memory_unit_kind());
+      if (p->memory_unit_mib()) out.emplace_back(key + ".memory-unit-mib", std::to_string(p->memory_unit_mib()));
+      else out.emplace_back(key + ".memory-unit-mib", "mixed");
+    }
+    return out;
+  }
+
+  // What each replicated resource's IDs mean (Plugin::ReplicaLayout), kept
+  // across generations and -- in <plugin dir>/amdgpu-dp/replica-layout --
+  // across processes. A resource whose layout changes (autoReplicaUnit,
+  // replicaCuMask, a resourceConfig replica count, a re-partition) while the
+  // kubelet says running containers hold its IDs: those IDs now mean other
+  // devices or other amounts of HBM than the containers were given, and the
+  // node can be over-committed until they end. Logged as an error and counted.
+  void CheckReplicaLayouts() {
+    std::map<std::string, std::string> now;
+    {
+      std::lock_guard<std::mutex> lk(plugins_mu_);
+      for (const auto& p : plugins_)
+        if (p->device_count() > 0) now[p->resource_name()] = p->ReplicaLayout();
+    }
+    const std::string path = PathJoin(cfg_.flags.plugin_dir, "amdgpu-dp/replica-layout");
+    if (!layouts_loaded_) {
+      layouts_loaded_ = true;
+      if (FILE* f = fopen(path.c_str(), "r")) {
+        char line[8192];
+        while (fgets(line, sizeof(line), f)) {
+          std::string l(line);
+          while (!l.empty() && l.back() == '\n') l.pop_back();
+          size_t tab = l.find('\t');
+          if (tab != std::string::npos) layouts_[l.substr(0, tab)] = l.substr(tab + 1);
+        }
+        fclose(f);
+      }
+    }
+    std::vector<std::string> changed;
+    for (const auto& [res, before] : layouts_) {
+      auto it = now.find(res);
+      if (it != now.end() && it->second != before) changed.push_back(res);
+    }
+    layouts_ = now;
+    std::string body;
+    for (const auto& [res, lay] : now) body += res + "\t" + lay + "\n";
+    mkdir(PathJoin(cfg_.flags.plugin_dir, "amdgpu-dp").c_str(), 0755);
+    std::string tmp = path + ".tmp";
+    if (FILE* f = fopen(tmp.c_str(), "w")) {
+      bool ok = fwrite(body.data(), 1, body.size(), f) == body.size();
+      ok = (fclose(f) == 0) && ok;
+      if (!ok || rename(tmp.c_str(), path.c_str()) != 0) unlink(tmp.c_str());
+    }
+    if (changed.empty()) return;
+    Result<std::vector<podresources::Assignment>> live = Unavailable("no --pod-resources-socket");
+    if (!cfg_.flags.pod_resources_socket.empty()) live = podresources::List(cfg_.flags.pod_resources_socket, 1000);
+    for (const auto& res : changed) {
+      const std::string& after = now[res];
+      if (!live.ok()) {
+        LOG_WARN(kComp, "'%s': what its IDs mean changed (now: %s); whether running containers hold some is unknown "
+                 "(kubelet PodResources: %s)", res.c_str(), after.c_str(), live.status().ToString().c_str());
+        continue;
+      }
+      size_t held = 0, pods = 0;
+      std::set<std::string> seen;
+      for (const auto& a : *live)
+        if (a.resource == res) {
+          ++held;
+          if (seen.insert(a.ns + "/" + a.pod).second) ++pods;
+        }
+      if (held == 0) {
+        LOG_INFO(kComp, "'%s': what its IDs mean changed (now: %s); no running container holds any", res.c_str(),
+                 after.c_str());
+        continue;
+      }
+      {
+        std::lock_guard<std::mutex> lk(access_mu_);
+        ++layout_changes_live_[res];
+      }
+      LOG_ERROR(kComp, "'%s': what its IDs mean changed while %zu of them are held by %zu running pod(s) (now: %s): "
+                "those pods keep what they were given, new pods are granted by the new layout, and the node can be "
+                "over-committed until the old pods end. Drain the node before changing autoReplicaUnit, "
+                "replicaCuMask or a resourceConfig replica count (amdgpu_dp_stale_allocated_ids counts their IDs "
+                "that no longer exist)", res.c_str(), held, pods, after.c_str());
+    }
   }
 
   // Kubelet restarted (or our socket vanished): same devices, same health
@@ -765,6 +863,9 @@ class Supervisor {
   std::mutex access_mu_;  // node_access_, metrics_gpus_: written by Restart, read by /metrics
   std::vector<inventory::NodeAccess> node_access_;
   std::vector<std::pair<std::string, std::string>> metrics_gpus_;  // (ledger key, bdf) of the served GPUs
+  std::map<std::string, uint64_t> layout_changes_live_;  // per resource (CheckReplicaLayouts)
+  std::map<std::string, std::string> layouts_;  // resource -> Plugin::ReplicaLayout of the running generation
+  bool layouts_loaded_ = false;
   const std::string usage_dir_;  // grant accounting files (the plugin directory is a startup-only flag)
   std::string smi_version_;
   std::unique_ptr<metrics::HttpServer> http_;

@@ -570,7 +570,8 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     bool ok = s.ok && !stuck;
     std::string h = std::string("hello v1 ") + (reinit ? "reinit " : "") +
                     (ok ? "events=ok processors=" + std::to_string(s.processors) : std::string("events=off")) +
-                    " relay=" + relay_id + " gen=" + std::to_string(s.gen) + " seq=" + std::to_string(seq);
+                    " relay=" + relay_id + " gen=" + std::to_string(s.gen) + " seq=" + std::to_string(seq) +
+                    " fp=" + (s.fp.empty() ? std::string("-") : s.fp) + " renew_ms=" + std::to_string(s.renew_ms);
     if (gap >= 0) h += " gap=" + std::to_string(gap);
     if (!ok) h += " reason=" + (stuck ? stuck_reason : s.reason);
     return h + "\n";

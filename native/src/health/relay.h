@@ -39,7 +39,10 @@
 //                    "event seq=<n> node=<kfd node|-> bdf=<bdf> part=<partition id> type=<t> <message>"
 //                          relay: a random ID of this relay process; gen: its
 //                          registration generation (+1 on each re-registration);
-//                          seq: the last event sequence number it forwarded
+//                          seq: the last event sequence number it forwarded;
+//                          every hello also carries fp=<the registration's
+//                          ProcessorFingerprint> and renew_ms=<how long its last
+//                          renewal took>
 //   daemon -> relay  "reinit fp=<fingerprint> since=<relay>:<seq>:<gen>|-"
 //                          subscribe to events: replays the events after <seq>
 //                          that were forwarded while this daemon was away (when

@@ -272,6 +272,7 @@ void Plugin::BuildUnits() {
     pb::PutLen(&u.mount_bytes, 2, mb);
     units_.push_back(std::move(u));
   }
+  if (memory_units_) CheckMemoryUnitName();
   if (replicated_)
     LOG_INFO(kComp, "'%s': preferred allocation %s replicas (%s)", spec_.resource_name.c_str(),
              replica_policy_ == alloc::ReplicaPolicy::kPack ? "packs" : "spreads",
@@ -284,8 +285,14 @@ void Plugin::BuildUnits() {
     unit_by_id_[u.id] = static_cast<int>(i);
     unit_index_by_id_[u.id] = static_cast<int>(i);  // view into units_[i].id (never modified)
     if (replicated_) {
-      LOG_INFO(kComp, "replicating device %s (%s, %llu MiB) %u times", u.id.c_str(), u.index.c_str(),
-               static_cast<unsigned long long>(u.vram_mib), u.replicas);
+      if (memory_units_)
+        LOG_INFO(kComp, "replicating device %s (%s, %llu MiB) %u times: '%s' units of %llu MiB (%s)", u.id.c_str(),
+                 u.index.c_str(), static_cast<unsigned long long>(u.vram_mib), u.replicas,
+                 spec_.resource_name.c_str(), static_cast<unsigned long long>(u.grant_mib),
+                 UnitIsCuSlot(u) ? "cu-slot" : "mib");
+      else
+        LOG_INFO(kComp, "replicating device %s (%s, %llu MiB) %u times", u.id.c_str(), u.index.c_str(),
+                 static_cast<unsigned long long>(u.vram_mib), u.replicas);
       for (unsigned r = 0; r < u.replicas; ++r) {
         advertised_.push_back(alloc::ReplicaId(u.id, r));
         advertised_unit_.push_back(static_cast<int>(i));
@@ -338,6 +345,49 @@ void Plugin::BuildUnits() {
               "client accepts; the kubelet will not see these devices. Lower the replica count (resource-config) "
               "or raise the memory unit (--auto-replica-unit-mib)", spec_.resource_name.c_str(),
               law_bytes_size_.load(), advertised_.size());
+}
+
+bool Plugin::UnitIsCuSlot(const Unit& u) const {
+  return memory_units_ && opts_.cu_slot_units && u.grant_mib != opts_.auto_replica_unit_mib;
+}
+
+// A resource named for gigabytes whose unit is not about one: with CU-slot
+// units (--replica-cu-mask, --auto-replica-unit auto) one "gpu-mem-gb" is
+// ~9 GiB on an MI355X, and a pod asking for 16 of them gets half the GPU.
+void Plugin::CheckMemoryUnitName() {
+  uint64_t common = units_.empty() ? 0 : units_[0].grant_mib;
+  bool cu_slot = !units_.empty() && UnitIsCuSlot(units_[0]);
+  for (const auto& u : units_) {
+    if (u.grant_mib != common) common = 0;
+    cu_slot = cu_slot && UnitIsCuSlot(u);
+  }
+  memory_unit_mib_ = common;
+  memory_unit_kind_ = cu_slot ? "cu-slot" : "mib";
+  std::string name = ToLower(spec_.resource_name);
+  size_t slash = name.rfind('/');
+  if (slash != std::string::npos) name = name.substr(slash + 1);
+  const bool says_gb = name.find("gb") != std::string::npos || name.find("gib") != std::string::npos ||
+                       name.find("mem") != std::string::npos;
+  uint64_t lo = units_.empty() ? 0 : units_[0].grant_mib, hi = lo;
+  for (const auto& u : units_) {
+    lo = std::min(lo, u.grant_mib);
+    hi = std::max(hi, u.grant_mib);
+  }
+  if (says_gb && (lo < 900 || hi > 1100))
+    LOG_WARN(kComp, "'%s' is named for gigabytes but one unit is %llu%s MiB (%s units%s): a pod requesting N of it "
+             "gets N x that. Name it for what it is (e.g. resourceConfig gpu:gpu-slot:-1) or use 1 GiB units "
+             "(--auto-replica-unit mib). The node label amd.com/%s.memory-unit-mib says the size",
+             spec_.resource_name.c_str(), static_cast<unsigned long long>(lo),
+             hi != lo ? (".." + std::to_string(hi)).c_str() : "", memory_unit_kind_,
+             cu_slot ? ": one CU on every XCD each, --replica-cu-mask" : "", name.c_str());
+}
+
+std::string Plugin::ReplicaLayout() const {
+  if (!replicated_) return "";
+  std::string out = memory_units_ ? std::string("memory-units ") + memory_unit_kind_ : std::string("time-slice");
+  for (const auto& u : units_)
+    out += " " + u.id + "=" + std::to_string(u.replicas) + "x" + std::to_string(u.grant_mib) + "MiB";
+  return out;
 }
 
 void Plugin::RebuildListAndWatch() {

@@ -226,6 +226,17 @@ class Plugin {
     return false;
   }
   bool grants_hbm() const { return hbm_grants_; }
+  // Memory-unit resources (replicas -1): what one unit is -- "cu-slot" (a CU on
+  // every XCD and its share of the HBM) or "mib" -- and its size in MiB when
+  // every device has the same (0 when they differ or this is not a memory-unit
+  // resource). Published as node labels and amdgpu_dp_memory_unit_mib.
+  bool memory_units() const { return memory_units_; }
+  const char* memory_unit_kind() const { return memory_unit_kind_; }
+  uint64_t memory_unit_mib() const { return memory_unit_mib_; }
+  // Replicated resources: what their IDs mean -- the kind and size of a unit
+  // and every device's replica count -- as one comparable line ("" when the
+  // resource is not replicated). A change while pods hold the IDs re-means them.
+  std::string ReplicaLayout() const;
   // GetPreferredAllocation's replica policy for this resource (never kAuto).
   alloc::ReplicaPolicy replica_policy() const { return replica_policy_; }
   const std::vector<Unit>& units() const { return units_; }
@@ -311,7 +322,11 @@ class Plugin {
   strategy::PluginSpec spec_;
   PluginOptions opts_;
   bool replicated_ = false;
+  bool UnitIsCuSlot(const Unit& u) const;
+  void CheckMemoryUnitName();
   bool memory_units_ = false;  // auto replicas: one ID per auto_replica_unit_mib of HBM
+  const char* memory_unit_kind_ = "";
+  uint64_t memory_unit_mib_ = 0;
   bool hbm_grants_ = false;    // Allocate() reports (and may enforce) HBM per replica: memory units or HBM shares
   bool hip_order_known_ = true;
   alloc::ReplicaPolicy replica_policy_ = alloc::ReplicaPolicy::kSpread;  // resolved for this resource  // units are in KFD-node (HIP) order; false: amdsmi order, nodes unreported

@@ -120,6 +120,22 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
   for (auto* p : plugins) gauge("amdgpu_dp_allocatable", res(p), static_cast<double>(p->advertised_.size()));
   family("amdgpu_dp_healthy_devices", "gauge", "Physical devices currently advertised Healthy.");
   for (auto* p : plugins) gauge("amdgpu_dp_healthy_devices", res(p), static_cast<double>(p->healthy_count()));
+  {
+    bool any = false;
+    for (auto* p : plugins) any = any || p->memory_units_;
+    if (any) {
+      family("amdgpu_dp_memory_unit_mib", "gauge",
+             "HBM one unit of a memory-unit resource (replicas -1) grants, per device: a pod requesting N units "
+             "gets N times this (kind: cu-slot, a CU on every XCD and its share of the HBM, or mib).");
+      for (auto* p : plugins) {
+        if (!p->memory_units_) continue;
+        for (const auto& u : p->units_)
+          gauge("amdgpu_dp_memory_unit_mib",
+                res(p) + ",device=\"" + LabelValue(u.id) + "\",kind=\"" + (p->UnitIsCuSlot(u) ? "cu-slot" : "mib") + "\"",
+                static_cast<double>(u.grant_mib));
+      }
+    }
+  }
   family("amdgpu_dp_registered", "gauge", "1 while the plugin is serving and registered with the kubelet.");
   for (auto* p : plugins) gauge("amdgpu_dp_registered", res(p), p->registered() ? 1 : 0);
   family("amdgpu_dp_device_healthy", "gauge", "Per-device health (1 Healthy, 0 Unhealthy).");
@@ -178,6 +194,9 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
     struct Use { std::vector<uint64_t> ids; std::vector<std::set<std::string>> pods; };
     std::map<std::tuple<const Plugin*, int, std::string, std::string, std::string>, uint64_t> per_pod;
     std::vector<Use> uses(plugins.size());
+    // IDs the kubelet says running containers hold that this plugin no longer
+    // advertises: the replica count or memory unit changed under them.
+    std::vector<uint64_t> stale(plugins.size(), 0);
     for (size_t i = 0; i < plugins.size(); ++i) {
       uses[i].ids.assign(plugins[i]->units_.size(), 0);
       uses[i].pods.resize(plugins[i]->units_.size());
@@ -187,7 +206,10 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
         const Plugin* p = plugins[i];
         if (a.resource != p->spec_.resource_name) continue;
         auto it = p->advertised_index_.find(a.device_id);
-        if (it == p->advertised_index_.end()) continue;
+        if (it == p->advertised_index_.end()) {
+          ++stale[i];
+          continue;
+        }
         ++uses[i].ids[it->second];
         uses[i].pods[it->second].insert(a.ns + "/" + a.pod);
         ++per_pod[{p, it->second, a.ns, a.pod, a.container}];
@@ -202,6 +224,11 @@ void Plugin::AppendPrometheus(const std::vector<const Plugin*>& plugins, std::st
       for (size_t u = 0; u < uses[i].ids.size(); ++u)
         gauge("amdgpu_dp_device_allocated_ids", dev(plugins[i], static_cast<int>(u)),
               static_cast<double>(uses[i].ids[u]));
+    family("amdgpu_dp_stale_allocated_ids", "gauge",
+           "IDs of this resource that running containers hold (kubelet PodResources) but the plugin no longer "
+           "advertises: the replica count or memory unit changed while they ran, so the node can be over-committed.");
+    for (size_t i = 0; i < plugins.size(); ++i)
+      gauge("amdgpu_dp_stale_allocated_ids", res(plugins[i]), static_cast<double>(stale[i]));
     family("amdgpu_dp_device_pods", "gauge", "Distinct pods sharing the device.");
     for (size_t i = 0; i < plugins.size(); ++i)
       for (size_t u = 0; u < uses[i].pods.size(); ++u)

@@ -388,3 +388,20 @@ def test_metrics_network_policy():
                                          "from": [{"podSelector": {"matchLabels": {"app": "prometheus"}}}]}
     for vals in ({}, {"metrics": {"enabled": True}}, {"metrics": {"enabled": False, "networkPolicy": {"enabled": True}}}):
         assert not helm_render.render(vals)["networkpolicy.yaml"].strip()
+
+
+@pytest.mark.parametrize("values,want", [
+    ({}, "gpu:gpu-mem-gb:-1"),                                           # MiB units: the name is right
+    ({"replicaCuMask": True}, "gpu:gpu-slot:-1"),                        # auto -> CU slots: renamed
+    ({"autoReplicaUnit": "cu-slot"}, "gpu:gpu-slot:-1"),
+    ({"replicaCuMask": True, "autoReplicaUnit": "mib"}, "gpu:gpu-mem-gb:-1"),
+    ({"replicaCuMask": True, "resourceConfig": "gpu:mem-slots:-1"}, "gpu:mem-slots:-1"),  # the user's own name
+])
+def test_cu_slot_units_do_not_keep_a_gigabyte_name(values, want):
+    """A memory unit that is a CU slot (~9 GiB on an MI355X) under the default
+    resource name gpu-mem-gb would let a pod asking for 16 "GB" take half the
+    GPU: with CU-slot units the chart's default renders as gpu-slot instead;
+    MiB units and a name the user chose are left alone."""
+    ds = daemonset(values)
+    check_consistent(ds)
+    assert env(ds)["RESOURCE_CONFIG"] == want

@@ -132,7 +132,6 @@ def main():
             rt, ln = c.reinit("reinit")
             renew_rt.append(rt)
             renew_ms.append(float(kv(ln, "renew_ms")))
-            assert kv(ln, "events") == "ok" or not real or True
         last = ln
         fp = kv(last, "fp")
         for _ in range(a.rounds):
