@@ -82,7 +82,7 @@ def test_bench_two_ranks_gloo():
     assert res["server_residency"]["all_calls"]["samples"] > 0
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_bench_multi_gpu_without_launcher(n):
     """`python bench.py --gpus N` starts its N ranks itself (the driver's 1-GPU
     invocation, N > 1): one process group of N ranks, the daemon serving
@@ -107,6 +107,14 @@ def test_bench_multi_gpu_without_launcher(n):
     for p in res["per_rank"]:
         assert p["admitted_bdfs"] == [p["rank_bdf"]] and p["allocate"]["n"] == 40
     assert sorted(p["rank_bdf"] for p in res["per_rank"]) == sorted(topo["served_bdfs"])
+    # container lists follow KFD order; on the node model HIP order is the same
+    order = topo["device_order"]
+    assert order["hip_order"] == topo["rank_bdfs"] and order["hip_order_is_kfd_order"] is True
+    assert sorted(order["kfd_order"]) == sorted(topo["served_bdfs"])
+    # a k=4 pod on the 8-GPU mesh stays on one NUMA node (GPUs 0-3 and 4-7 share one each)
+    numa = {g["bdf"]: g["numa"] for g in topo["gpus"]}
+    if n >= 4:
+        assert len({numa[b] for b in pk["bdfs"]}) == 1, (pk, numa)
 
 
 def test_bench_serves_the_ranks_gpus_not_amdsmi_order():
@@ -168,3 +176,34 @@ def test_bench_one_rank_under_torchrun_uses_a_process_group():
     assert r.returncode == 0, r.stderr[-4000:]
     res = _last_json(r.stdout)
     assert res["rccl_world"] == 1 and res["backend"] == "gloo"
+
+
+@pytest.mark.parametrize("config,advertised", [("timeslice4", 32), ("cpx-single", 64)])
+def test_bench_eight_ranks_advertise_the_baseline_counts(config, advertised):
+    """BASELINE configs 3 and 4 at N=8 -- the path the driver's 8-GPU scaling run
+    takes: 8 ranks (gloo here, RCCL there), one daemon serving all 8 GPUs.
+    Time-slice sharing advertises 4 replicas x 8 GPUs = 32; CPX with
+    partitionStrategy=single advertises 8 partitions x 8 GPUs = 64. Every rank
+    admits pods on its own GPU only, and a k=4 pod's preferred placement stays
+    on one GPU's partitions (CPX) or one NUMA node (SPX)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--steps", "2", "--warmup", "1", "--mock",
+                        "--pods-per-step", "20", "--config", config],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = _last_json(r.stdout)
+    assert res["n_gpus"] == 8 and res["rccl_world"] == 8
+    assert res["allocatable"] == advertised and res["advertised"] == advertised
+    assert res["value"] > 0 and res["allocate_p99_us"] >= res["value"]
+    per = res["per_rank"]
+    assert sorted(p["rank"] for p in per) == list(range(8))
+    assert all(p["rank_devices"] == advertised // 8 for p in per)
+    assert all(p["admitted_bdfs"] == [p["rank_bdf"]] for p in per)
+    topo = res["topology"]
+    pk = res["preferred_k"]
+    assert pk["k"] == 4 and pk["available"] == advertised
+    numa = {g["bdf"]: g["numa"] for g in topo["gpus"]}
+    if config == "cpx-single":
+        assert len(set(pk["bdfs"])) == 1  # four partitions of one GPU
+    else:
+        assert len(set(pk["bdfs"])) == 4 and len({numa[b] for b in pk["bdfs"]}) == 1

@@ -94,8 +94,9 @@ def main():
     if a.relay:
         esock = os.path.join(d + ".relay", "events.sock")
         os.makedirs(os.path.dirname(esock), exist_ok=True)
+        # (info: its per-connection decisions -- registration kept or renewed -- are counted below)
         relay = harness.Daemon(d + ".relay", fx, args=["--event-relay", "--health-event-socket", esock],
-                               real_smi=a.real, env={"ADP_LOG_LEVEL": "warn"}).start()
+                               real_smi=a.real, env={"ADP_LOG_LEVEL": "info"}).start()
         deadline = time.time() + 30
         while not os.path.exists(esock):
             assert time.time() < deadline and relay.proc.poll() is None, relay.log()[-2000:]
@@ -210,7 +211,12 @@ def main():
     if relay:
         rw = relay_samples[min(2, len(relay_samples) - 1)] if relay_samples else {}
         rl = relay_samples[-1] if relay_samples else {}
+        rlog = relay.log()
         summary["relay"] = {"exit_code": relay_code, "rss_mib_after_warmup": rw.get("rss_mib"),
+                            "daemon_connections": rlog.count("daemon connected for events"),
+                            "registration_kept": rlog.count("registration kept"),
+                            "registration_renewed": rlog.count("re-enumerating"),
+                            "nothing_missed": rlog.count("nothing missed"),
                             "rss_mib_last": rl.get("rss_mib"), "fds_after_warmup": rw.get("fds"),
                             "fds_last": rl.get("fds"), "threads_after_warmup": rw.get("threads"),
                             "threads_last": rl.get("threads")}
