@@ -411,28 +411,35 @@ void Plugin::AppendMemcapUsage(const std::vector<const Plugin*>& plugins, const 
   for (const auto& r : rows) Sample(out, "amdgpu_dp_container_hbm_processes", r.labels, uint64_t{r.u.processes});
   if (!driver) return;
 
-  // Driver-side truth, per GPU of the grant (partitions of one GPU share its PCI address).
-  Family(out, "amdgpu_dp_container_hbm_driver_bytes", "gauge",
-         "HBM the container's processes hold on the GPU by the driver's count (DRM fdinfo), whatever path "
-         "allocated it.");
-  Family(out, "amdgpu_dp_container_hbm_over_grant", "gauge",
-         "1 while the driver counts more HBM for the container on the GPU than granted (+ the runtime allowance "
-         "per process).");
-  Family(out, "amdgpu_dp_container_hbm_over_grant_total", "counter",
-         "Times the container went over its grant on the GPU by the driver's count.");
+  // Driver-side truth, per GPU of the grant (partitions of one GPU share its
+  // PCI address). Each family's samples form one group: a scrape that
+  // interleaves families is refused by strict parsers.
+  struct DriverRow {
+    std::string labels;
+    memcap::DriverHbmMonitor::GrantState st;
+  };
+  std::vector<DriverRow> drows;
   for (const auto& r : rows) {
     std::set<std::string> bdfs;
     for (int u : r.units) bdfs.insert(r.p->snap_->gpus[r.p->units_[u].gpu].bdf);
     for (const auto& bdf : bdfs) {
-      auto it = driver->grants.find({r.u.key, bdf});
-      memcap::DriverHbmMonitor::GrantState st;
-      if (it != driver->grants.end()) st = it->second;
-      std::string labels = r.labels + ",bdf=\"" + LabelValue(bdf) + "\"";
-      Sample(out, "amdgpu_dp_container_hbm_driver_bytes", labels, st.driver_bytes);
-      Sample(out, "amdgpu_dp_container_hbm_over_grant", labels, uint64_t{st.over ? 1u : 0u});
-      Sample(out, "amdgpu_dp_container_hbm_over_grant_total", labels, st.over_transitions);
+      DriverRow d{r.labels + ",bdf=\"" + LabelValue(bdf) + "\"", {}};
+      if (auto it = driver->grants.find({r.u.key, bdf}); it != driver->grants.end()) d.st = it->second;
+      drows.push_back(std::move(d));
     }
   }
+  Family(out, "amdgpu_dp_container_hbm_driver_bytes", "gauge",
+         "HBM the container's processes hold on the GPU by the driver's count (DRM fdinfo), whatever path "
+         "allocated it.");
+  for (const auto& d : drows) Sample(out, "amdgpu_dp_container_hbm_driver_bytes", d.labels, d.st.driver_bytes);
+  Family(out, "amdgpu_dp_container_hbm_over_grant", "gauge",
+         "1 while the driver counts more HBM for the container on the GPU than granted (+ the runtime allowance "
+         "per process).");
+  for (const auto& d : drows)
+    Sample(out, "amdgpu_dp_container_hbm_over_grant", d.labels, uint64_t{d.st.over ? 1u : 0u});
+  Family(out, "amdgpu_dp_container_hbm_over_grant_total", "counter",
+         "Times the container went over its grant on the GPU by the driver's count.");
+  for (const auto& d : drows) Sample(out, "amdgpu_dp_container_hbm_over_grant_total", d.labels, d.st.over_transitions);
 }
 
 }  // namespace adp::plugin
