@@ -7,6 +7,7 @@
 // parsed from, and its sums match its rows.
 #include <fuzzer/FuzzedDataProvider.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -67,7 +68,11 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
   size_t used = 0;
   if (memcap::ParseScan(line, &s, &used)) {
     if (used > line.size()) Fail("scan consumed past the input");
-    if (memcap::SerializeScan(s) != line.substr(0, used)) Fail("scan round trip");
+    // (a previous-version header without the render-only field reads as 0)
+    std::string expect = line.substr(0, used);
+    size_t nl = expect.find('\n');
+    if (std::count(expect.begin(), expect.begin() + nl, '\t') == 5) expect.insert(nl, "\t0");
+    if (memcap::SerializeScan(s) != expect) Fail("scan round trip");
     uint64_t sum = 0, total = 0;
     for (const auto& p : s.procs) sum += p.bytes;
     for (const auto& [bdf, b] : s.total) total += b;

@@ -135,6 +135,10 @@ void AppendDaemonMetrics(const DaemonMetricsInput& in, std::string* out) {
            "that list).");
     Sample(out, "amdgpu_dp_driver_hbm_scan_processes", "source=\"" + metrics::LabelValue(d->scan.pid_source) + "\"",
            Num(d->scan.pids_scanned));
+    Family(out, "amdgpu_dp_driver_hbm_render_only_processes", "gauge",
+           "Processes holding HBM through a render node without /dev/kfd (in no KFD process list), as the last "
+           "full walk of every process found them (ADP_DRIVER_FULL_WALK_MS); they are read on every scan.");
+    Sample(out, "amdgpu_dp_driver_hbm_render_only_processes", "", Num(d->render_only));
     Family(out, "amdgpu_dp_driver_hbm_scan_descriptors", "gauge", "File descriptors the last driver-side scan examined.");
     Sample(out, "amdgpu_dp_driver_hbm_scan_descriptors", "", Num(d->scan.fd_entries));
     Family(out, "amdgpu_dp_driver_hbm_scan_seconds", "gauge", "Wall time of the last driver-side scan.");

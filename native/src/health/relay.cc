@@ -93,7 +93,9 @@ std::string RandomId() {
 // its next poll).
 class ScanWorker {
  public:
-  explicit ScanWorker(const RelayOptions& o) : opts_(o), thread_([this] { Run(); }) {}
+  explicit ScanWorker(const RelayOptions& o) : opts_(o), thread_([this] { Run(); }) {
+    state_.full_walk_ms = memcap::FullWalkMsFromEnv();
+  }
   ~ScanWorker() {
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -130,8 +132,16 @@ class ScanWorker {
         r = std::move(queue_.front());
         queue_.pop_front();
       }
+      // One ScanState for every daemon's requests: the periodic full walk and
+      // the render-only holders it found are the node's, not a connection's.
       memcap::DriverScan s = memcap::ScanDriverHbm(opts_.proc_root, memcap::ListGrantFiles(r.usage_dir), r.cgroup,
-                                                   opts_.kfd_proc_dir);
+                                                   opts_.kfd_proc_dir, &state_);
+      if (s.pid_source == "proc" && s.render_only && !render_only_logged_) {
+        render_only_logged_ = true;
+        LOG_WARN(kComp, "%zu process(es) hold HBM through a render node without /dev/kfd (not in KFD's process "
+                 "list): read on every scan from now on, and a full walk every %lld ms finds new ones",
+                 s.render_only, static_cast<long long>(state_.full_walk_ms));
+      }
       if (!logged_) {
         logged_ = true;
         LOG_INFO(kComp, "first HBM scan for a daemon: %zu process(es) from %s, %zu descriptor(s), %zu unreadable",
@@ -157,6 +167,8 @@ class ScanWorker {
   std::deque<Request> queue_;
   bool stop_ = false;
   bool logged_ = false;
+  bool render_only_logged_ = false;
+  memcap::ScanState state_;  // only the scan thread touches it
   std::thread thread_;
 };
 

@@ -153,6 +153,7 @@ namespace {
 struct PidHbm {
   int pid;
   std::map<std::string, uint64_t> by_bdf;
+  bool kfd = false;  // also holds /dev/kfd open
 };
 
 // Reads the descriptors of `pids`: render-node fds with DRM fdinfo become
@@ -176,7 +177,7 @@ void ReadPids(const std::string& proc_root, const std::vector<std::string>& pids
       continue;
     }
     ++*present;
-    PidHbm ph{atoi(pid.c_str()), {}};
+    PidHbm ph{atoi(pid.c_str()), {}, false};
     bool kfd = false;
     int fdd = dirfd(fds);
     while (dirent* f = readdir(fds)) {
@@ -211,18 +212,34 @@ void ReadPids(const std::string& proc_root, const std::vector<std::string>& pids
     }
     closedir(fds);
     *kfd_holders += kfd;
+    ph.kfd = kfd;
     if (!ph.by_bdf.empty()) holders->push_back(std::move(ph));
   }
 }
 
 }  // namespace
 
+int64_t FullWalkMsFromEnv() {
+  const char* e = getenv("ADP_DRIVER_FULL_WALK_MS");
+  if (e && *e) {
+    char* end = nullptr;
+    long long v = strtoll(e, &end, 10);
+    if (end && *end == 0 && v >= 0) return v;
+  }
+  return 60000;
+}
+
 DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFile>& grants,
-                         const std::string& self_cgroup, const std::string& kfd_proc_dir) {
+                         const std::string& self_cgroup, const std::string& kfd_proc_dir, ScanState* state) {
   DriverScan out;
   std::vector<PidHbm> holders;
   bool opened = false;
-  if (!kfd_proc_dir.empty()) {
+  const int64_t now = std::chrono::duration_cast<std::chrono::milliseconds>(
+                          std::chrono::steady_clock::now().time_since_epoch()).count();
+  // A full walk: the first scan, then one every full_walk_ms (ScanState).
+  const bool walk_all = state && (state->last_full_ms < 0 ||
+                                  (state->full_walk_ms > 0 && now - state->last_full_ms >= state->full_walk_ms));
+  if (!kfd_proc_dir.empty() && !walk_all) {
     // The driver's own list of GPU processes. It names host PIDs: it is used
     // when they are the PIDs of proc_root -- every listed process found there
     // holds /dev/kfd open -- else (a /proc of another PID namespace, whose
@@ -235,6 +252,16 @@ DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFi
       std::vector<PidHbm> h;
       ReadPids(proc_root, pids, &kfd, &h, &present, &kfd_holders);
       if (pids.empty() || (present > 0 && kfd_holders + kfd.fd_dirs_unreadable >= present)) {
+        // ... plus the render-only holders the last full walk found (not in
+        // KFD's list, still read every scan).
+        if (state && !state->render_only_pids.empty()) {
+          std::set<std::string> listed(pids.begin(), pids.end());
+          std::vector<std::string> extra;
+          for (const auto& pid : state->render_only_pids)
+            if (!listed.count(pid)) extra.push_back(pid);
+          size_t p2 = 0, k2 = 0;
+          ReadPids(proc_root, extra, &kfd, &h, &p2, &k2);
+        }
         out = std::move(kfd);
         holders = std::move(h);
       } else {
@@ -247,6 +274,21 @@ DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFi
     if (!opened) return out;
     size_t present = 0, kfd_holders = 0;
     ReadPids(proc_root, pids, &out, &holders, &present, &kfd_holders);
+    if (state) {
+      state->last_full_ms = now;
+      ++state->full_walks;
+      state->render_only_pids.clear();
+      for (const auto& h : holders) {
+        uint64_t bytes = 0;
+        for (const auto& [_, b] : h.by_bdf) bytes += b;
+        if (!h.kfd && bytes) state->render_only_pids.push_back(std::to_string(h.pid));
+      }
+    }
+  }
+  for (const auto& h : holders) {
+    uint64_t bytes = 0;
+    for (const auto& [_, b] : h.by_bdf) bytes += b;
+    out.render_only += !h.kfd && bytes;
   }
 
   // Attribution: own mapping first, then the cgroup of an attributed process
@@ -330,38 +372,54 @@ bool ToU64(std::string_view v, uint64_t* out) {
 std::string SerializeScan(const DriverScan& s) {
   std::string out = "scan\t" + Clean(s.pid_source) + "\t" + std::to_string(s.pids_scanned) + "\t" +
                     std::to_string(s.fd_entries) + "\t" + std::to_string(s.fd_dirs_unreadable) + "\t" +
-                    std::to_string(s.procs.size()) + "\n";
+                    std::to_string(s.procs.size()) + "\t" + std::to_string(s.render_only) + "\n";
   for (const auto& p : s.procs)
     out += "p\t" + std::to_string(p.pid) + "\t" + Clean(p.bdf) + "\t" + std::to_string(p.bytes) + "\t" +
            Clean(p.grant) + "\t" + (p.via_cgroup ? "1" : "0") + "\t" + Clean(p.cgroup) + "\n";
   return out;
 }
 
-bool ParseScan(std::string_view text, DriverScan* out, size_t* consumed) {
-  // A header, then exactly as many process lines as it announces.
+ParseResult ParseScanReply(std::string_view text, DriverScan* out, size_t* consumed) {
+  // A header, then exactly as many process lines as it announces. Until a
+  // line is complete it can only be judged as far as it goes: "scan\t" and a
+  // run of digits can still become a reply, "scab" or a letter in a number
+  // cannot -- a reply that is not one fails at once instead of at the timeout.
+  constexpr std::string_view kHead = "scan\t";
   size_t nl = text.find('\n');
-  if (nl == std::string_view::npos) return false;
+  if (nl == std::string_view::npos) {
+    size_t n = std::min(text.size(), kHead.size());
+    if (text.substr(0, n) != kHead.substr(0, n)) return ParseResult::kMalformed;
+    return text.find('\r') != std::string_view::npos || text.size() > 4096 ? ParseResult::kMalformed
+                                                                             : ParseResult::kIncomplete;
+  }
   // (SerializeScan never writes a carriage return: a reply holding one is not its)
-  if (text.substr(0, nl).find('\r') != std::string_view::npos) return false;
+  if (text.substr(0, nl).find('\r') != std::string_view::npos) return ParseResult::kMalformed;
   auto h = Fields(text.substr(0, nl));
-  uint64_t pids = 0, fds = 0, unreadable = 0, n = 0;
-  if (h.size() != 6 || h[0] != "scan" || !ToU64(h[2], &pids) || !ToU64(h[3], &fds) ||
-      !ToU64(h[4], &unreadable) || !ToU64(h[5], &n) || n > 1000000)
-    return false;
+  uint64_t pids = 0, fds = 0, unreadable = 0, n = 0, render_only = 0;
+  if ((h.size() != 6 && h.size() != 7) || h[0] != "scan" || !ToU64(h[2], &pids) || !ToU64(h[3], &fds) ||
+      !ToU64(h[4], &unreadable) || !ToU64(h[5], &n) || n > 1000000 || (h.size() == 7 && !ToU64(h[6], &render_only)))
+    return ParseResult::kMalformed;
   DriverScan s;
   s.pid_source = std::string(h[1]);
   s.pids_scanned = pids;
   s.fd_entries = fds;
   s.fd_dirs_unreadable = unreadable;
+  s.render_only = render_only;
   size_t pos = nl + 1;
   for (uint64_t i = 0; i < n; ++i) {
     size_t e = text.find('\n', pos);
-    if (e == std::string_view::npos || text.substr(pos, e - pos).find('\r') != std::string_view::npos) return false;
+    if (e == std::string_view::npos) {
+      std::string_view part = text.substr(pos);
+      if (part.find('\r') != std::string_view::npos || (!part.empty() && part[0] != 'p'))
+        return ParseResult::kMalformed;
+      return ParseResult::kIncomplete;
+    }
+    if (text.substr(pos, e - pos).find('\r') != std::string_view::npos) return ParseResult::kMalformed;
     auto f = Fields(text.substr(pos, e - pos));
     uint64_t pid = 0, bytes = 0;
     if (f.size() != 7 || f[0] != "p" || !ToU64(f[1], &pid) || pid > INT32_MAX || !ToU64(f[3], &bytes) ||
         (f[5] != "0" && f[5] != "1"))
-      return false;
+      return ParseResult::kMalformed;
     s.procs.push_back({static_cast<int>(pid), std::string(f[2]), bytes, std::string(f[6]), std::string(f[4]),
                        f[5] == "1"});
     pos = e + 1;
@@ -369,7 +427,11 @@ bool ParseScan(std::string_view text, DriverScan* out, size_t* consumed) {
   Aggregate(&s);
   *out = std::move(s);
   if (consumed) *consumed = pos;
-  return true;
+  return ParseResult::kOk;
+}
+
+bool ParseScan(std::string_view text, DriverScan* out, size_t* consumed) {
+  return ParseScanReply(text, out, consumed) == ParseResult::kOk;
 }
 
 Result<DriverScan> RemoteScan(int fd, const std::string& usage_dir, const std::string& self_cgroup, int timeout_ms,
@@ -386,7 +448,11 @@ Result<DriverScan> RemoteScan(int fd, const std::string& usage_dir, const std::s
     for (size_t nl; in.compare(0, 5, "scan\t") != 0 && (nl = in.find('\n')) != std::string::npos;)
       in.erase(0, nl + 1);
     DriverScan s;
-    if (ParseScan(in, &s, nullptr)) return s;
+    if (in.compare(0, 5, "scan\t") == 0) {  // (a partial line before it may still be a greeting)
+      ParseResult pr = ParseScanReply(in, &s, nullptr);
+      if (pr == ParseResult::kOk) return s;
+      if (pr == ParseResult::kMalformed) return Internal("event relay: malformed scan reply");
+    }
     if (in.size() > (64u << 20)) return Internal("event relay: scan reply too large");
     int left = static_cast<int>(
         std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count());
@@ -408,6 +474,7 @@ Result<DriverScan> RemoteScan(int fd, const std::string& usage_dir, const std::s
 DriverHbmMonitor::DriverHbmMonitor(Options opts, GrantFn grants)
     : opts_(std::move(opts)), grants_(std::move(grants)), self_cgroup_(SelfCgroup()) {
   snap_.slack_bytes = opts_.slack_bytes;
+  scan_state_.full_walk_ms = FullWalkMsFromEnv();
 }
 
 DriverHbmMonitor::~DriverHbmMonitor() { Stop(); }
@@ -460,7 +527,8 @@ void DriverHbmMonitor::PollOnce() {
     }
     scan = std::move(*r);
   } else {
-    scan = ScanDriverHbm(opts_.proc_root, ListGrantFiles(opts_.usage_dir), self_cgroup_, opts_.kfd_proc_dir);
+    scan = ScanDriverHbm(opts_.proc_root, ListGrantFiles(opts_.usage_dir), self_cgroup_, opts_.kfd_proc_dir,
+                         &scan_state_);
   }
   uint64_t scan_ns = static_cast<uint64_t>(
       std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
@@ -506,6 +574,16 @@ void DriverHbmMonitor::PollOnce() {
     LOG_INFO(kComp, "%s", snap_.polls == 0 ? "driver-side scan: the event relay answers"
                                            : "driver-side scan through the relay works again");
   snap_.scan_error.clear();
+  if (scan.pid_source == "proc") {
+    snap_.render_only = scan.render_only;
+    if (scan.render_only && !snap_.render_only_logged) {
+      snap_.render_only_logged = true;
+      LOG_WARN(kComp, "%zu process(es) hold HBM through a render node without /dev/kfd (not in KFD's process list): "
+               "read on every scan from now on, and a full walk every %lld ms finds new ones",
+               scan.render_only, static_cast<long long>(scan_state_.full_walk_ms));
+    }
+  }
+  snap_.full_walks = remote ? snap_.full_walks : scan_state_.full_walks;
   snap_.remote = remote;
   snap_.scan = std::move(scan);
   snap_.grants = std::move(states);

@@ -63,7 +63,27 @@ struct DriverScan {
   // Where the candidate PIDs came from: "kfd" (the driver's list of GPU
   // processes, /sys/class/kfd/kfd/proc) or "proc" (every process).
   std::string pid_source = "proc";
+  // Processes holding VRAM through a render node without /dev/kfd open (Mesa,
+  // Vulkan, VA-API, a child that inherited the fd, raw amdgpu GEM ioctls): in
+  // no KFD list, so only a full walk finds them (ScanState).
+  size_t render_only = 0;
 };
+
+// What one scanner carries from scan to scan. KFD lists only the processes
+// that opened /dev/kfd; a render-node-only VRAM holder is in no such list and
+// the fast path alone would never see it -- a bypass of the in-process cap.
+// So the first scan, and one every `full_walk_ms`, walks every process; the
+// render-only holders it finds are read on every fast-path scan in between
+// (their bytes do not vanish and reappear), and a new one is found within
+// `full_walk_ms`.
+struct ScanState {
+  int64_t full_walk_ms = 60000;  // 0: only the first scan walks everything
+  int64_t last_full_ms = -1;     // steady clock of the last full walk (-1: none yet)
+  std::vector<std::string> render_only_pids;
+  uint64_t full_walks = 0;
+};
+// ADP_DRIVER_FULL_WALK_MS, else 60000.
+int64_t FullWalkMsFromEnv();
 
 // A grant's accounting file as the daemon sees it: processes that mapped it
 // show the same device and inode in /proc/<pid>/maps.
@@ -83,8 +103,11 @@ uint64_t ParseFdinfoSize(const std::string& value);
 // read, so the cost follows the GPU processes, not every descriptor on the
 // node; the full walk remains when that directory is absent or none of its
 // PIDs is under `proc_root` (a /proc of another PID namespace).
+// `state` (may be null: then the KFD list alone, as before) makes the fast
+// path periodic full walks plus the render-only holders they found.
 DriverScan ScanDriverHbm(const std::string& proc_root, const std::vector<GrantFile>& grants,
-                         const std::string& self_cgroup, const std::string& kfd_proc_dir = "");
+                         const std::string& self_cgroup, const std::string& kfd_proc_dir = "",
+                         ScanState* state = nullptr);
 
 // The cgroup line of the calling process ("" if unreadable).
 std::string SelfCgroup();
@@ -93,11 +116,16 @@ std::string SelfCgroup();
 void Aggregate(DriverScan* s);
 
 // The scan as the event relay sends it (health/relay.h): a header line
-// "scan\t<pid source>\t<pids>\t<fds>\t<unreadable>\t<n>" and n lines
+// "scan\t<pid source>\t<pids>\t<fds>\t<unreadable>\t<n>\t<render only>" and n lines
 // "p\t<pid>\t<bdf>\t<bytes>\t<grant>\t<via cgroup 0|1>\t<cgroup>".
 std::string SerializeScan(const DriverScan& s);
-// Parses one complete reply at the start of `text` (false: incomplete or
-// malformed); `consumed` gets its length.
+// Parses one complete reply at the start of `text`; `consumed` gets its length.
+// kIncomplete: a prefix of a reply (wait for more bytes); kMalformed: no reply
+// can start this way (fail at once). A relay of the previous version (no
+// render-only field) is read too.
+enum class ParseResult { kOk, kIncomplete, kMalformed };
+ParseResult ParseScanReply(std::string_view text, DriverScan* out, size_t* consumed);
+// ParseScanReply == kOk.
 bool ParseScan(std::string_view text, DriverScan* out, size_t* consumed);
 // Asks the event relay connected on `fd` for a scan (the relay holds the
 // privilege to read other containers' /proc/<pid>/fd): usage_dir and the
@@ -144,6 +172,9 @@ class DriverHbmMonitor {
     uint64_t scan_failures = 0;  // relay scans that failed (the previous scan stays)
     std::string scan_error;      // the last failure's reason, "" once a scan succeeds again
     bool remote = false;         // scans run in the event relay
+    size_t render_only = 0;      // render-node-only VRAM holders at the last full walk
+    bool render_only_logged = false;
+    uint64_t full_walks = 0;     // scans that walked every process (local scans)
   };
 
   DriverHbmMonitor(Options opts, GrantFn grants);
@@ -160,6 +191,7 @@ class DriverHbmMonitor {
   mutable std::mutex mu_;
   Snapshot snap_;
   std::map<std::pair<std::string, std::string>, uint64_t> transitions_;
+  ScanState scan_state_;  // local scans (the relay keeps its own)
   std::atomic<bool> stop_{false};
   int wake_fd_ = -1;
   std::thread thread_;

@@ -286,6 +286,19 @@ static void TestRelayLines() {
                           "scan\tproc\t1\t1\t0\n", "scan\tproc\t1\t1\t0\t1\np\t1\tb\t1\tk\t2\tc\n",
                           "scan\tproc\t1\t1\t0\t99999999999999999999999\n"})
     CHECK(!memcap::ParseScan(bad, &back, &used));
+
+  // incomplete vs malformed: a prefix of a reply waits, anything else fails at once
+  using PR = memcap::ParseResult;
+  for (std::string part : {std::string(""), std::string("sc"), std::string("scan\t"), std::string("scan\tproc\t1"),
+                           text.substr(0, text.size() - 1), text.substr(0, text.find('\n') + 2)})
+    CHECK(memcap::ParseScanReply(part, &back, &used) == PR::kIncomplete);
+  for (const char* bad : {"scab", "hello v1", "scan\tproc\t1\r", "scan\tproc\t1\t1\t0\t1\nq",
+                          "scan\tproc\t1\t1\t0\t1\np\tx\tb\t1\tk\t0\tc\n", "scan\tproc\t1\t1\t0\t1\t-3\n"})
+    CHECK(memcap::ParseScanReply(bad, &back, &used) == PR::kMalformed);
+  // the render-only count travels; a relay of the previous version (6 header fields) is read too
+  scan.render_only = 2;
+  CHECK(memcap::ParseScanReply(memcap::SerializeScan(scan), &back, &used) == PR::kOk && back.render_only == 2);
+  CHECK(memcap::ParseScanReply("scan\tproc\t1\t1\t0\t0\n", &back, &used) == PR::kOk && back.render_only == 0);
 }
 
 static void TestRemoteScan() {

@@ -40,7 +40,7 @@ class FakeProc:
         os.makedirs(root, exist_ok=True)
 
     def process(self, pid, cgroup, vram_mib=None, client=None, maps_file=None, bdf=BDF0, extra_fds=(),
-                maps_dev=None, maps_path="/run/amdgpu-dp/memcap"):
+                maps_dev=None, maps_path="/run/amdgpu-dp/memcap", kfd=True):
         base = os.path.join(self.root, str(pid))
         os.makedirs(os.path.join(base, "fd"), exist_ok=True)
         os.makedirs(os.path.join(base, "fdinfo"), exist_ok=True)
@@ -54,10 +54,10 @@ class FakeProc:
         with open(os.path.join(base, "maps"), "w") as f:
             f.write(maps)
         fd = os.path.join(base, "fd", "3")
-        if not os.path.lexists(fd):
+        if kfd and not os.path.lexists(fd):
             os.symlink("/dev/kfd", fd)  # the KFD fd carries no memory stats
-        with open(os.path.join(base, "fdinfo", "3"), "w") as f:
-            f.write("pos:\t0\n")
+            with open(os.path.join(base, "fdinfo", "3"), "w") as f:
+                f.write("pos:\t0\n")
         if vram_mib is not None:
             self.render(pid, 7, vram_mib, client if client is not None else pid * 10, bdf)
         for n, target in extra_fds:
@@ -323,7 +323,8 @@ def test_daemon_scan_uses_the_kfd_list(scratch, tmp_path):
         assert _value(s, "amdgpu_dp_driver_hbm_scan_processes", source="kfd") == 2
         assert _value(s, "amdgpu_dp_driver_hbm_scan_descriptors") == 4
         assert _value(s, "amdgpu_dp_driver_hbm_scan_seconds") >= 0
-        assert "first scan: 2 candidate process(es) from " + kfd in d.log()
+        # the first scan walks every process (render-only holders are in no KFD list), the next ones KFD's
+        assert "first scan: 52 candidate process(es) from " + proc.root in d.log()
     finally:
         d.stop()
         k.stop()
@@ -480,7 +481,8 @@ def test_a_malformed_relay_reply_counts_as_a_failed_scan(scratch, tmp_path):
             time.sleep(0.05)
         s = _parse(_get(port, "/metrics")[1])
         assert _value(s, "amdgpu_dp_driver_hbm_polls_total") == 0  # nothing accepted
-        assert "closed the connection" in d.wait_log("driver-side scan through the relay failed")
+        # judged malformed at once, not after the scan timeout
+        assert "malformed scan reply" in d.wait_log("driver-side scan through the relay failed")
     finally:
         d.stop()
         k.stop()
@@ -511,3 +513,74 @@ def test_a_relay_that_starts_after_the_plugin_is_waited_for(scratch, tmp_path):
         k.stop()
         if relay:
             relay.stop()
+
+
+def test_a_render_only_holder_is_found_by_the_periodic_full_walk(scratch, tmp_path):
+    """Advisor round 4: with KFD's process list the scan read only processes
+    that opened /dev/kfd, so one holding HBM through a render node alone (Mesa,
+    Vulkan, VA-API, a child that inherited the fd, raw amdgpu ioctls) was
+    invisible -- a way around the grant. The first scan and one every
+    ADP_DRIVER_FULL_WALK_MS walk every process; the render-only holders they
+    find are read on every fast scan in between, so the grant's driver count
+    does not flap; a new one is found within the walk period."""
+    proc = FakeProc(str(tmp_path / "proc"))
+    kfd_dir = str(tmp_path / "kfd")
+    os.makedirs(kfd_dir)
+    for pid in range(8000, 8040):  # bystanders, not GPU processes
+        proc.process(pid, "0::/system.slice/x", kfd=False)
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(2), args=[
+        "--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:gpu-mem-gb:-1", "--replica-policy", "pack",
+        "--enforce-memory-units", "--memcap-lib", SHIM, "--host-proc", proc.root, "--kfd-proc-dir", kfd_dir,
+        "--driver-hbm-poll-ms", "50", "--driver-hbm-slack-mib", "100"],
+        env={"ADP_DRIVER_FULL_WALK_MS": "600"}).start()
+    try:
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics")).group(1))
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        resp = c.allocate(ids[:3]).container_responses[0]  # 3000 MiB on GPU 0
+        c.close()
+        host = [m.host_path for m in resp.mounts if m.container_path == "/run/amdgpu-dp/memcap"][0]
+        deadline = time.time() + 5
+        while not os.path.isfile(host) and time.time() < deadline:
+            time.sleep(0.01)
+        key = os.path.basename(host).split(".")[0]
+        ctr = "0::/kubepods/pod-v/ctr"
+        proc.process(701, ctr, vram_mib=1000, maps_file=host)           # the HIP process, KFD lists it
+        _kfd_dir(kfd_dir, [701])
+        proc.process(702, ctr, vram_mib=2500, kfd=False)                # Vulkan in the same container
+        lab = dict(allocation=key, bdf=BDF0)
+        # fast scans see the KFD process only ...
+        s = _scrape_after_poll(port, _polls(port) + 2)
+        first = _value(s, "amdgpu_dp_container_hbm_driver_bytes", **lab)
+        # ... until the next full walk (<= 600 ms) finds the render-only holder
+        deadline = time.time() + 5
+        while _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_container_hbm_driver_bytes", **lab) < 3500 * MIB:
+            assert time.time() < deadline, d.log()[-2000:]
+            time.sleep(0.05)
+        assert first in (1000 * MIB, 3500 * MIB)
+        # from then on every scan -- fast ones included -- counts it: no flapping
+        bytes_seen, fast_procs = set(), set()
+        polls0 = _polls(port)
+        while _polls(port) < polls0 + 20:
+            s = _parse(_get(port, "/metrics")[1])
+            bytes_seen.add(_value(s, "amdgpu_dp_container_hbm_driver_bytes", **lab))
+            fast_procs |= {v for (n, ls), v in s.items()
+                           if n == "amdgpu_dp_driver_hbm_scan_processes" and dict(ls).get("source") == "kfd"}
+            time.sleep(0.02)
+        assert bytes_seen == {3500 * MIB}, bytes_seen
+        assert fast_procs == {2}  # fast scans read KFD's process and the carried render-only one
+        assert _value(s, "amdgpu_dp_container_hbm_over_grant", **lab) == 1
+        assert _value(s, "amdgpu_dp_hbm_over_grant_events_total") == 1  # one transition, not one per walk
+        assert _value(s, "amdgpu_dp_driver_hbm_render_only_processes") == 1
+        assert "hold HBM through a render node without /dev/kfd" in d.log()
+        # a second render-only holder appears: found by the next walk
+        proc.process(703, ctr, vram_mib=300, kfd=False)
+        deadline = time.time() + 5
+        while _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_container_hbm_driver_bytes", **lab) < 3800 * MIB:
+            assert time.time() < deadline
+            time.sleep(0.05)
+    finally:
+        d.stop()
+        k.stop()
