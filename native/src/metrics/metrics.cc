@@ -206,7 +206,7 @@ HttpServer::HttpServer(Render render, Healthy healthy, Render stats)
 
 HttpServer::~HttpServer() { Stop(); }
 
-Status HttpServer::Start(const std::string& addr) {
+Status HttpServer::Listen(const std::string& addr) {
   std::string host, port = addr;
   size_t colon = addr.rfind(':');
   if (colon != std::string::npos) {
@@ -223,29 +223,46 @@ Status HttpServer::Start(const std::string& addr) {
   int rc = getaddrinfo(host.empty() ? nullptr : host.c_str(), port.c_str(), &hints, &res);
   if (rc != 0) return InvalidArgument("invalid --metrics-addr '" + addr + "': " + gai_strerror(rc));
   Status st = Unavailable("no usable address for " + addr);
-  for (addrinfo* ai = res; ai; ai = ai->ai_next) {
+  bool bound = false;
+  for (addrinfo* ai = res; ai && !bound; ai = ai->ai_next) {
     int fd = socket(ai->ai_family, ai->ai_socktype | SOCK_CLOEXEC | SOCK_NONBLOCK, ai->ai_protocol);
     if (fd < 0) continue;
     int one = 1;
     setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
     if (bind(fd, ai->ai_addr, ai->ai_addrlen) == 0 && listen(fd, 16) == 0) {
-      listen_fd_ = fd;
-      sockaddr_storage ss{};
-      socklen_t len = sizeof(ss);
-      getsockname(fd, reinterpret_cast<sockaddr*>(&ss), &len);
-      port_ = ntohs(ss.ss_family == AF_INET6 ? reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port
-                                             : reinterpret_cast<sockaddr_in*>(&ss)->sin_port);
+      if (listen_fds_.empty()) {
+        sockaddr_storage ss{};
+        socklen_t len = sizeof(ss);
+        getsockname(fd, reinterpret_cast<sockaddr*>(&ss), &len);
+        port_ = ntohs(ss.ss_family == AF_INET6 ? reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port
+                                               : reinterpret_cast<sockaddr_in*>(&ss)->sin_port);
+      }
+      listen_fds_.push_back(fd);
+      bound = true;
       break;
     }
     st = Unavailable("metrics listen on " + addr + ": " + strerror(errno));
     close(fd);
   }
   freeaddrinfo(res);
-  if (listen_fd_ < 0) return st;
+  return bound ? Status::Ok() : st;
+}
+
+Status HttpServer::Start(const std::string& addr) {
+  for (const auto& one : Split(addr, ',')) {
+    std::string a = Trim(one);
+    if (a.empty()) continue;
+    if (Status st = Listen(a); !st.ok()) {
+      for (int fd : listen_fds_) close(fd);
+      listen_fds_.clear();
+      return st;
+    }
+  }
+  if (listen_fds_.empty()) return InvalidArgument("invalid --metrics-addr '" + addr + "'");
   stop_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   spare_fd_ = open("/dev/null", O_RDONLY | O_CLOEXEC);
   thread_ = std::thread([this] { Run(); });
-  LOG_INFO(kComp, "serving /metrics and /healthz on port %d (and /stats)", port_);
+  LOG_INFO(kComp, "serving /metrics and /healthz on port %d (and /stats) at %s", port_, addr.c_str());
   return Status::Ok();
 }
 
@@ -256,10 +273,11 @@ void HttpServer::Stop() {
     (void)w;
     thread_.join();
   }
-  if (listen_fd_ >= 0) close(listen_fd_);
+  for (int fd : listen_fds_) close(fd);
+  listen_fds_.clear();
   if (stop_fd_ >= 0) close(stop_fd_);
   if (spare_fd_ >= 0) close(spare_fd_);
-  listen_fd_ = stop_fd_ = spare_fd_ = -1;
+  stop_fd_ = spare_fd_ = -1;
 }
 
 // Connections are served concurrently from one poll loop, each with a 2 s
@@ -286,7 +304,9 @@ void HttpServer::Run() {
   while (true) {
     p.clear();
     p.push_back({stop_fd_, POLLIN, 0});
-    p.push_back({cs.size() < kMaxClients ? listen_fd_ : -1, POLLIN, 0});  // full: leave them in the backlog
+    for (int lfd : listen_fds_)
+      p.push_back({cs.size() < kMaxClients ? lfd : -1, POLLIN, 0});  // full: leave them in the backlog
+    const size_t fixed = 1 + listen_fds_.size();
     int timeout = -1;
     auto now = Clock::now();
     for (const auto& c : cs) {
@@ -300,11 +320,11 @@ void HttpServer::Run() {
       break;
     }
     if (p[0].revents) break;
-    // Clients first (their pollfds follow the two fixed entries, in order).
+    // Clients first (their pollfds follow the fixed entries, in order).
     now = Clock::now();
     for (size_t i = cs.size(); i-- > 0;) {
       Client& c = cs[i];
-      short re = p[2 + i].revents;
+      short re = p[fixed + i].revents;
       bool done = false;
       if (re && !c.responding) {
         char buf[2048];
@@ -325,9 +345,11 @@ void HttpServer::Run() {
       }
       if (done || now >= c.deadline) drop(i);
     }
-    if (p[1].revents) {
+    for (size_t l = 0; l < listen_fds_.size(); ++l) {
+      if (!p[1 + l].revents) continue;
+      const int listen_fd = listen_fds_[l];
       while (cs.size() < kMaxClients) {
-        int fd = accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK);
+        int fd = accept4(listen_fd, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK);
         if (fd >= 0) {
           cs.push_back({fd, Clock::now() + std::chrono::seconds(2), {}, {}, 0, false});
           continue;
@@ -335,7 +357,7 @@ void HttpServer::Run() {
         if (errno == EINTR) continue;
         if ((errno == EMFILE || errno == ENFILE) && spare_fd_ >= 0) {
           close(spare_fd_);
-          int shed = accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
+          int shed = accept4(listen_fd, nullptr, nullptr, SOCK_CLOEXEC);
           if (shed >= 0) close(shed);
           spare_fd_ = open("/dev/null", O_RDONLY | O_CLOEXEC);
           if (shed >= 0) continue;

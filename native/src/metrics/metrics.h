@@ -113,7 +113,10 @@ class HttpServer {
   // tools that would otherwise parse the log.
   HttpServer(Render render, Healthy healthy, Render stats = nullptr);
   ~HttpServer();
-  // addr: "host:port", ":port" (all interfaces) or "port". Port 0 picks a free port.
+  // addr: "host:port", ":port" (all interfaces) or "port", or several of them
+  // comma separated (e.g. the pod IP and loopback: kubectl port-forward and
+  // in-pod tools dial 127.0.0.1). Port 0 picks a free port. port() is the
+  // first address's.
   Status Start(const std::string& addr);
   void Stop();
   int port() const { return port_; }
@@ -124,7 +127,8 @@ class HttpServer {
   Render render_;
   Healthy healthy_;
   Render stats_;
-  int listen_fd_ = -1;
+  Status Listen(const std::string& addr);
+  std::vector<int> listen_fds_;
   int stop_fd_ = -1;
   int spare_fd_ = -1;  // reserve descriptor: shed connections at EMFILE instead of spinning
   int port_ = 0;

@@ -210,7 +210,8 @@ def test_metrics_and_node_feature_labels():
     check_consistent(ds)
     c = container(ds)
     # bound to the pod's own IP (downward API), not every interface
-    assert env(ds)["DP_METRICS_ADDR"] == "$(POD_IP):9500" and env(ds)["DP_NODE_LABELS_FILE"]
+    # the pod IP for Prometheus, loopback for kubectl port-forward and in-pod tools
+    assert env(ds)["DP_METRICS_ADDR"] == "$(POD_IP):9500,127.0.0.1:9500" and env(ds)["DP_NODE_LABELS_FILE"]
     pod_ip = [e for e in c["env"] if e["name"] == "POD_IP"][0]
     assert pod_ip["valueFrom"] == {"fieldRef": {"fieldPath": "status.podIP"}}
     names = [e["name"] for e in c["env"]]

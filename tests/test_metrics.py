@@ -535,3 +535,31 @@ def test_stats_endpoint_is_json(served):
     assert sum(n for _, n in p["residency_100ns"]) >= 4 and p["residency_p50_us"] > 0
     assert st["health"]["events"] in ("on", "off", "not started") and st["restarts"] >= 1
     call.cancel()
+
+
+def test_metrics_listens_on_every_address_given(scratch):
+    """--metrics-addr takes a comma-separated list (the chart: the pod IP for
+    Prometheus and loopback for kubectl port-forward and in-pod tools, which
+    dial 127.0.0.1): every address answers; one that cannot be bound fails the
+    start instead of serving half."""
+    import socket
+    import subprocess
+    import urllib.request
+    with socket.socket() as s0:
+        s0.bind(("127.0.0.1", 0))
+        port = s0.getsockname()[1]
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(1), args=[
+        "--metrics-addr", f"127.0.0.2:{port}, 127.0.0.1:{port}"]).start()
+    try:
+        assert f"on port {port} (and /stats) at 127.0.0.2:{port}" in d.wait_log("serving /metrics")
+        for host in ("127.0.0.1", "127.0.0.2"):
+            with urllib.request.urlopen(f"http://{host}:{port}/metrics", timeout=5) as r:
+                assert b"amdgpu_dp_build_info" in r.read()
+    finally:
+        d.stop()
+        k.stop()
+    r = subprocess.run([harness.DAEMON, "--device-plugin-path", scratch, "--metrics-addr",
+                        f"127.0.0.1:{port},not-an-address:x"], capture_output=True, text=True, timeout=30,
+                       env=harness.Daemon(scratch, fixtures.node(1)).env)
+    assert r.returncode == 1 and "invalid --metrics-addr 'not-an-address:x'" in r.stdout + r.stderr
