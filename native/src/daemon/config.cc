@@ -175,7 +175,8 @@ const std::vector<FlagDef>& Table() {
        "0000:0c:00.0` takes a GPU out of service at the next health poll",
        [](Flags& f) -> void* { return &f.drain; }},
       {"undrain", "ADP_UNDRAIN", "", Kind::kString,
-       "remove these GPUs from --drain-file (every line naming them), print the drain list and exit",
+       "remove these GPUs from --drain-file (their names only: other GPUs named on the same line, and its "
+       "comment, stay), print the drain list and exit",
        [](Flags& f) -> void* { return &f.undrain; }},
       {"drain-file", "DP_DRAIN_FILE", "drainFile", Kind::kString,
        "operator drain list: every GPU named in this file (PCI address, UUID, partition UUID or node index; "

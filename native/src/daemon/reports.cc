@@ -459,9 +459,23 @@ int DrainCommand(smi::Library* lib, const Validated& v, const Config& cfg) {
       if (tokens.count(n)) return true;
     return false;
   };
-  for (const auto* g : remove)
-    lines.erase(std::remove_if(lines.begin(), lines.end(), [&](const std::string& l) { return names_line(l, g); }),
-                lines.end());
+  // Only this GPU's names leave a line; other GPUs named with it stay drained.
+  for (const auto* g : remove) {
+    const std::set<std::string> names = health::DrainNames(*g);
+    std::vector<std::string> next;
+    for (const auto& l : lines) {
+      if (!names_line(l, g)) {
+        next.push_back(l);
+        continue;
+      }
+      std::string rest = health::RemoveDrainNames(l, names);
+      if (!rest.empty()) {
+        fprintf(stderr, "kept on the same line: %s\n", rest.c_str());
+        next.push_back(rest);
+      }
+    }
+    lines = std::move(next);
+  }
   for (const auto* g : add) {
     bool listed = false;
     for (const auto& l : lines) listed = listed || names_line(l, g);

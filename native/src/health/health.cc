@@ -615,6 +615,33 @@ std::set<std::string> DrainTokens(std::string_view text) {
   return names;
 }
 
+std::string RemoveDrainNames(std::string_view line, const std::set<std::string>& names) {
+  std::string_view body = line, comment;
+  if (size_t hash = line.find('#'); hash != std::string_view::npos) {
+    body = line.substr(0, hash);
+    comment = line.substr(hash);
+  }
+  bool commas = body.find(',') != std::string_view::npos;
+  std::vector<std::string> keep;
+  bool removed = false;
+  for (size_t p = 0; p < body.size();) {
+    size_t q = body.find_first_of(" \t,\r", p);
+    if (q == std::string_view::npos) q = body.size();
+    if (q > p) {
+      std::string tok(body.substr(p, q - p));
+      if (names.count(tok)) removed = true;
+      else keep.push_back(std::move(tok));
+    }
+    p = q + 1;
+  }
+  if (!removed) return std::string(line);
+  if (keep.empty()) return "";
+  std::string out;
+  for (const auto& t : keep) out += (out.empty() ? "" : commas ? "," : " ") + t;
+  if (!comment.empty()) out += "  " + std::string(comment);
+  return out;
+}
+
 std::set<std::string> DrainNames(const inventory::PhysicalGpu& g) {
   std::set<std::string> n = {g.uuid, g.bdf, std::to_string(g.node_index)};
   if (size_t dot = g.bdf.rfind('.'); dot != std::string::npos) n.insert(g.bdf.substr(0, dot));

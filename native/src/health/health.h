@@ -238,6 +238,10 @@ class Ledger {
 // UUID, PCI address with or without the function, node index, partition UUIDs).
 std::set<std::string> DrainTokens(std::string_view text);
 std::set<std::string> DrainNames(const inventory::PhysicalGpu& g);
+// One drain-file line without the tokens in `names`: the other names on it and
+// its comment stay (a line "0,1 # maintenance" undrained of GPU 0 becomes
+// "1 # maintenance"). "" when no name is left on it (the line goes).
+std::string RemoveDrainNames(std::string_view line, const std::set<std::string>& names);
 
 class Monitor {
  public:

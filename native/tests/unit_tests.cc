@@ -210,6 +210,17 @@ static void TestLedgerGaps() {
   CHECK(health::Ledger::Serialize(l.All()) == "adp-health v1\nc\t-\t0\t4\t\n");
 }
 
+static void TestRemoveDrainNames() {
+  g_case = "remove-drain-names";
+  std::set<std::string> g0 = {"0000:0c:00.0", "0000:0c:00", "0", "GPU-a"};
+  CHECK(health::RemoveDrainNames("0000:0c:00.0  # GPU-a", g0).empty());  // our own line goes
+  CHECK(health::RemoveDrainNames("0,1 # maintenance", g0) == "1  # maintenance");
+  CHECK(health::RemoveDrainNames("GPU-a GPU-b\tGPU-c", g0) == "GPU-b GPU-c");
+  CHECK(health::RemoveDrainNames("# 0 is mentioned only in a comment", g0) == "# 0 is mentioned only in a comment");
+  CHECK(health::RemoveDrainNames("1,2", g0) == "1,2");  // untouched: byte for byte
+  CHECK(health::RemoveDrainNames("0000:0c:00,0000:0c:00.0", g0).empty());
+}
+
 static void TestRelayLines() {
   g_case = "relay-lines";
   smi::ProcessorInfo p;
@@ -1235,6 +1246,7 @@ int main() {
   TestResourceConfig();
   TestRelayLines();
   TestLedgerGaps();
+  TestRemoveDrainNames();
   TestDrainSyntax();
   TestRemoteScan();
   TestProto();

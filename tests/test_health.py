@@ -388,5 +388,13 @@ def test_drain_and_undrain_commands(scratch, tmp_path):
         rc, out, _ = cli("--undrain", "1")  # by node index
         assert rc == 0 and out == ""
         assert until(["Healthy", "Healthy"]) == ["Healthy", "Healthy"]
+        # a hand-written line draining both GPUs: undraining one keeps the other and the comment
+        bdf0 = fx["gpus"][0]["bdf"]
+        drain.write_text(f"# planned work\n{bdf0},{uuid1}  # rack 4 maintenance\n")
+        assert until(["Unhealthy", "Unhealthy"]) == ["Unhealthy", "Unhealthy"]
+        rc, out, err = cli("--undrain", bdf1)
+        assert rc == 0 and out == f"# planned work\n{bdf0}  # rack 4 maintenance\n", out
+        assert "kept on the same line" in err
+        assert until(["Unhealthy", "Healthy"]) == ["Unhealthy", "Healthy"]
     finally:
         n.close()
