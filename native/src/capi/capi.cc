@@ -114,7 +114,7 @@ char* adp_prioritize(const char* in) {
 }
 
 // One driver-side HBM scan: {"proc_root", "kfd_proc_dir", "usage_dir", "self_cgroup"} ->
-// {pid_source, pids_scanned, fd_entries, fd_dirs_unreadable, scan_us, procs: [{pid, bdf, bytes, grant}],
+// {pid_source, pids_scanned, fd_entries, fd_dirs_unreadable, render_only, scan_us, procs: [{pid, bdf, bytes, grant}],
 //  total: {bdf: bytes}, unattributed: {bdf: bytes}}
 char* adp_driver_scan(const char* in) {
   return Guard([&] {
@@ -128,7 +128,8 @@ char* adp_driver_scan(const char* in) {
     for (const auto& p : s.procs)
       procs.push_back({{"pid", p.pid}, {"bdf", p.bdf}, {"bytes", p.bytes}, {"grant", p.grant}});
     return Dup(json{{"pid_source", s.pid_source}, {"pids_scanned", s.pids_scanned}, {"fd_entries", s.fd_entries},
-                    {"fd_dirs_unreadable", s.fd_dirs_unreadable}, {"scan_us", us}, {"procs", procs},
+                    {"fd_dirs_unreadable", s.fd_dirs_unreadable}, {"render_only", s.render_only},
+                    {"scan_us", us}, {"procs", procs},
                     {"total", s.total}, {"unattributed", s.unattributed}}
                    .dump());
   });

@@ -497,3 +497,61 @@ def test_every_write_lands_on_a_mounted_volume_on_real_amdsmi(scratch, snap, tmp
     _save("fs_writes.json", summary)
     assert summary["daemon"]["writes"] and summary["relay"]["writes"], summary
     assert not summary["daemon"]["outside_mounts"] and not summary["relay"]["outside_mounts"], summary
+
+
+_RENDER_HOLDER = r'''
+import ctypes, glob, os, sys
+drm = ctypes.CDLL("libdrm_amdgpu.so.1")
+class Req(ctypes.Structure):
+    _fields_ = [("alloc_size", ctypes.c_uint64), ("phys_alignment", ctypes.c_uint64),
+                ("preferred_heap", ctypes.c_uint32), ("flags", ctypes.c_uint64)]
+dev, node = ctypes.c_void_p(), None
+for path in sorted(glob.glob("/dev/dri/renderD*")):
+    try:
+        fd = os.open(path, os.O_RDWR)
+    except OSError:
+        continue
+    major, minor = ctypes.c_uint32(), ctypes.c_uint32()
+    if drm.amdgpu_device_initialize(fd, ctypes.byref(major), ctypes.byref(minor), ctypes.byref(dev)) == 0:
+        node = path
+        break
+    os.close(fd)
+size = int(sys.argv[1]) << 20
+bo, ptr = ctypes.c_void_p(), ctypes.c_void_p()
+# AMDGPU_GEM_DOMAIN_VRAM, AMDGPU_GEM_CREATE_CPU_ACCESS_REQUIRED
+rc = drm.amdgpu_bo_alloc(dev, ctypes.byref(Req(size, 4096, 4, 1)), ctypes.byref(bo)) if node else -1
+rc_map = drm.amdgpu_bo_cpu_map(bo, ctypes.byref(ptr)) if rc == 0 else -1
+if rc_map == 0:
+    ctypes.memset(ptr, 1, size)
+print("holding", rc, rc_map, node, flush=True)
+sys.stdin.read()
+'''
+
+
+def test_render_only_vram_holder_is_seen_by_a_full_walk(snap):
+    """Advisor round 4, on the MI355X: a process that allocates VRAM through
+    libdrm_amdgpu on a render node -- no /dev/kfd open, so in no KFD process
+    list -- holds HBM the driver counts in its DRM fdinfo. The full walk finds
+    it and counts it render-only; the plugin's periodic full walk
+    (ADP_DRIVER_FULL_WALK_MS) exists for exactly this holder."""
+    mib = 256
+    p = subprocess.Popen([sys.executable, "-c", _RENDER_HOLDER, str(mib)], stdin=subprocess.PIPE,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        line = p.stdout.readline().split()
+        assert line[:3] == ["holding", "0", "0"], (line, p.stderr.read()[-2000:] if p.poll() is not None else "")
+        links = [os.readlink(f"/proc/{p.pid}/fd/{f}") for f in os.listdir(f"/proc/{p.pid}/fd")]
+        assert "/dev/kfd" not in links and any(t.startswith("/dev/dri/renderD") for t in links), links
+        full = native.driver_scan("/proc")
+        rows = [r for r in full["procs"] if r["pid"] == p.pid]
+        kfd = native.driver_scan("/proc", kfd_proc_dir="/sys/class/kfd/kfd/proc")
+        _save("render_only_holder.json", {
+            "holder": {"pid": p.pid, "render_node": line[3], "bo_mib": mib, "fds": sorted(set(links))},
+            "full_walk": {"rows": rows, "render_only": full["render_only"], "pids_scanned": full["pids_scanned"]},
+            "kfd_list_scan": {"pid_source": kfd["pid_source"], "pids_scanned": kfd["pids_scanned"],
+                              "holder_rows": [r for r in kfd["procs"] if r["pid"] == p.pid]}})
+        assert rows and sum(r["bytes"] for r in rows) >= mib << 20, rows
+        assert full["render_only"] >= 1
+    finally:
+        p.stdin.close()
+        p.wait(timeout=30)
