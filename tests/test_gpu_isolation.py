@@ -187,6 +187,16 @@ def test_event_relay_on_real_amdsmi(scratch, snap, tmp_path):
         assert "event notification registered on" in relay.log(), relay.log()[-2000:]
         assert "events on through the relay" in log, log[-3000:]
         assert "device access: Operation not permitted: /dev/kfd" in log  # the daemon itself is denied
+        # The daemon's view of the processors (denied the device nodes) matches
+        # the relay's on real amdsmi: its restarts keep the registration, and
+        # the relay says nothing was missed.
+        import signal
+        for i in range(2):
+            d.signal(signal.SIGHUP)
+            d.wait_log("events on through the relay", 30, count=i + 2)
+        rlog = relay.wait_log("nothing missed", 30, count=2)
+        _save("event_relay_restarts.json", {"relay_log": rlog[-4000:]})
+        assert rlog.count("registration kept") == 3 and "re-enumerating" not in rlog, rlog[-3000:]
     finally:
         if d:
             assert d.stop() == 0
