@@ -172,7 +172,12 @@ class Supervisor {
   Supervisor(Config cfg, Validated v, std::function<Result<Config>()> reload, smi::Library* lib, int sfd)
       : cfg_(std::move(cfg)), v_(std::move(v)), reload_(std::move(reload)), lib_(lib), sfd_(sfd),
         ledger_(cfg_.flags.health_state_file),
-        usage_dir_(PathJoin(cfg_.flags.plugin_dir, "amdgpu-dp/usage")) {}
+        usage_dir_(PathJoin(cfg_.flags.plugin_dir, "amdgpu-dp/usage")) {
+    // Where this daemon is in the event relay's stream survives the container
+    // with the verdicts it goes with (health.h HealthCounters::PersistRelayCursor).
+    if (!cfg_.flags.health_state_file.empty() && !cfg_.flags.health_event_socket.empty())
+      health_counters_.PersistRelayCursor(cfg_.flags.health_state_file + ".relay");
+  }
   ~Supervisor() {
     for (int fd : {ep_, ifd_, tfd_, efd_, lfd_, rfd_})
       if (fd >= 0) close(fd);

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <optional>
 #include <set>
 #include <sstream>
 
@@ -23,6 +24,11 @@
 namespace adp::health {
 namespace {
 constexpr const char* kComp = "health";
+
+int64_t NowMsSteady() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
 
 const char* EventName(uint32_t t) {
   switch (t) {
@@ -139,11 +145,55 @@ HealthCounters::RelayCursor HealthCounters::GetRelayCursor() const {
 void HealthCounters::SetRelayCursor(const RelayCursor& c) {
   std::lock_guard<std::mutex> lk(mu_);
   cursor_ = c;
+  cursor_dirty_ = true;
+  SaveCursorLocked();
 }
 
 void HealthCounters::AdvanceRelaySeq(uint64_t seq) {
   std::lock_guard<std::mutex> lk(mu_);
-  if (cursor_.valid && seq > cursor_.seq) cursor_.seq = seq;
+  if (!cursor_.valid || seq <= cursor_.seq) return;
+  cursor_.seq = seq;
+  cursor_dirty_ = true;
+  if (NowMsSteady() - cursor_saved_ms_ >= 1000) SaveCursorLocked();
+}
+
+void HealthCounters::PersistRelayCursor(const std::string& path) {
+  std::lock_guard<std::mutex> lk(mu_);
+  cursor_path_ = path;
+  std::ifstream in(path);
+  std::string header, line;
+  if (!in || !std::getline(in, header) || Trim(header) != "adp-relay-cursor v1" || !std::getline(in, line)) return;
+  auto f = Split(line, '\t');
+  auto seq = f.size() == 3 ? ParseUint(f[1]) : std::nullopt;
+  auto gen = f.size() == 3 ? ParseUint(f[2]) : std::nullopt;
+  if (!seq || !gen || f[0].empty()) {
+    LOG_WARN(kComp, "relay cursor %s: malformed; the relay will report a gap", path.c_str());
+    return;
+  }
+  cursor_ = {true, f[0], *seq, *gen};
+  LOG_INFO(kComp, "relay cursor %s: relay %s, event #%llu, generation %llu", path.c_str(), f[0].c_str(),
+           static_cast<unsigned long long>(*seq), static_cast<unsigned long long>(*gen));
+}
+
+void HealthCounters::FlushRelayCursor() {
+  std::lock_guard<std::mutex> lk(mu_);
+  SaveCursorLocked();
+}
+
+void HealthCounters::SaveCursorLocked() {
+  if (cursor_path_.empty() || !cursor_dirty_ || !cursor_.valid) return;
+  cursor_saved_ms_ = NowMsSteady();
+  cursor_dirty_ = false;
+  std::string body = "adp-relay-cursor v1\n" + cursor_.relay + "\t" + std::to_string(cursor_.seq) + "\t" +
+                     std::to_string(cursor_.gen) + "\n";
+  std::string tmp = cursor_path_ + ".tmp";
+  FILE* f = fopen(tmp.c_str(), "w");
+  bool ok = f && fwrite(body.data(), 1, body.size(), f) == body.size();
+  if (f) ok = (fclose(f) == 0) && ok;
+  if (!ok || rename(tmp.c_str(), cursor_path_.c_str()) != 0) {
+    LOG_WARN(kComp, "cannot write relay cursor %s: %s", cursor_path_.c_str(), strerror(errno));
+    unlink(tmp.c_str());
+  }
 }
 
 int Monitor::Classify(const HealthConfig& cfg, uint32_t type) {
@@ -496,6 +546,7 @@ void Monitor::Stop() {
     close(relay_fd_);
     relay_fd_ = -1;
     events_ok_ = false;
+    counters_->FlushRelayCursor();
   } else if (events_ok_) {
     lib_->EventsStop(handles_);
     events_ok_ = false;

@@ -170,6 +170,14 @@ struct HealthCounters {
   RelayCursor GetRelayCursor() const;
   void SetRelayCursor(const RelayCursor& c);
   void AdvanceRelaySeq(uint64_t seq);
+  // With --health-state-file the cursor also outlives the process (<state>.relay):
+  // a restarted plugin container resumes the relay's stream where it left it,
+  // and the relay replays what it missed instead of reporting a gap. Loaded
+  // here; written on every hello, at most once a second for events, and by
+  // FlushRelayCursor (monitor stop). A cursor that lags only replays events
+  // already handled, which re-applies them in order.
+  void PersistRelayCursor(const std::string& path);
+  void FlushRelayCursor();
   std::string Json() const;
 
  private:
@@ -179,6 +187,10 @@ struct HealthCounters {
   std::map<std::pair<std::string, std::string>, uint64_t> events_;
   std::map<std::string, uint64_t> recovered_;
   RelayCursor cursor_;
+  std::string cursor_path_;
+  int64_t cursor_saved_ms_ = 0;
+  bool cursor_dirty_ = false;
+  void SaveCursorLocked();
 };
 
 // An event gap recorded on a GPU waiting for GPU_POST_RESET (Ledger, in memory

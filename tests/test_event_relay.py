@@ -597,3 +597,37 @@ def test_sighup_storm_with_interleaved_resets_leaves_no_gpu_stuck(scratch):
         assert "re-enumerating" not in rlog, rlog
     finally:
         n.stop()
+
+
+def test_a_restarted_plugin_container_resumes_the_relays_stream(scratch):
+    """With --health-state-file the daemon's place in the relay's event stream
+    (<state>.relay) outlives the process: a plugin container restarted between
+    a GPU's PRE_RESET and POST_RESET gets the POST_RESET replayed by the relay
+    -- which kept running and held it -- and the GPU is Healthy at once, not
+    after the polled hold (set out of reach). Without the file the new process
+    starts a gap (tested above)."""
+    state = os.path.join(scratch + ".fixture", "health.state")
+    n = RelayNode(scratch, daemon_args=["--health-state-file", state, "--reset-recovery-hold-ms", "600000"])
+    try:
+        n.d.wait_log("events on through the relay")
+        n.inject("1 3 mode1 reset")
+        assert n.health() == ["Healthy", "Unhealthy"]
+        n.call.cancel()
+        n.c.close()
+        assert n.d.stop() == 0
+        assert open(state + ".relay").read().startswith("adp-relay-cursor v1\n")
+        n.inject("1 4 reset done")  # while no daemon is connected: the relay holds it
+        n.relay.wait_log(" type=4 ")
+        n.d = harness.Daemon(scratch, n.fx, args=["--health-event-socket", n.sock, "--health-state-file", state,
+                                                  "--reset-recovery-hold-ms", "600000"],
+                             env={"LD_PRELOAD": _preload(SIM), "DP_HEALTH_POLL_MS": "200"}).start()
+        first = n.rewatch()
+        assert first[1] == "Unhealthy" or first == ["Healthy", "Healthy"]  # the ledger's verdict, then the replay
+        if first != ["Healthy", "Healthy"]:
+            n.wait_health(["Healthy", "Healthy"], timeout=5)
+        assert "relay cursor " + state + ".relay: relay " in n.d.log()
+        rlog = n.relay.wait_log("replaying 1 event(s)")
+        assert rlog.count("daemon connected for events (nothing missed)") == 1
+        assert "across an event gap" not in n.d.log()
+    finally:
+        n.stop()
