@@ -492,3 +492,39 @@ def test_failing_event_waits_are_a_gap(mk):
     assert n.d.log().count("recovered without GPU_POST_RESET") == 1
     n.inject("1 4 post-reset")
     n.wait_health(lambda h: h[ids[1]] == "Healthy")
+
+
+def test_in_process_sighup_storm_with_resets_leaves_no_gpu_stuck(mk):
+    """SIGHUPs back to back with PRE/POST pairs injected around them, and every
+    third POST_RESET dropped (as a real registration gap would lose it): every
+    GPU ends Healthy -- by the event when it arrives, by the polled check
+    across the gaps when it does not."""
+    import random
+    rnd = random.Random(11)
+    n = mk(args=["--reset-recovery-hold-ms", "800"])
+    ids = sorted(n.start())
+    for i in range(12):
+        gpu = i % 2
+        n.inject(f"{gpu} 3 storm pre {i}")
+        n.d.signal(signal.SIGHUP)
+        time.sleep(rnd.uniform(0, 0.2))
+        if i % 3 != 2:  # 2, 5, 8, 11 lost -- the last one too
+            n.inject(f"{gpu} 4 storm post {i}")
+        time.sleep(rnd.uniform(0, 0.2))
+    deadline = time.monotonic() + 20
+    h = None
+    while True:
+        try:
+            h = n.first_law(timeout=2)
+        except Exception:
+            pass
+        if h == {ids[0]: "Healthy", ids[1]: "Healthy"}:
+            break
+        assert time.monotonic() < deadline, (h, n.d.log()[-3000:])
+        try:
+            h = n.wait_health(lambda x: x == {ids[0]: "Healthy", ids[1]: "Healthy"}, timeout=3)
+            break
+        except Exception:
+            continue
+    assert n.d.log().count("received SIGHUP") == 12
+    assert "recovered without GPU_POST_RESET" in n.d.log()  # GPU 1's last reset: only polling ended it
