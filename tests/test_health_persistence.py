@@ -506,11 +506,17 @@ def test_in_process_sighup_storm_with_resets_leaves_no_gpu_stuck(mk):
     for i in range(12):
         gpu = i % 2
         n.inject(f"{gpu} 3 storm pre {i}")
+        if i % 3 == 2:
+            # the mock's FIFO would hand an unread PRE_RESET to the next
+            # registration, after the gap (real amdsmi loses it): the reset
+            # whose POST is lost is one seen before the gap
+            n.d.wait_log(f"storm pre {i}")
         n.d.signal(signal.SIGHUP)
         time.sleep(rnd.uniform(0, 0.2))
         if i % 3 != 2:  # 2, 5, 8, 11 lost -- the last one too
             n.inject(f"{gpu} 4 storm post {i}")
         time.sleep(rnd.uniform(0, 0.2))
+    n.d.wait_log("storm pre 11")
     deadline = time.monotonic() + 20
     h = None
     while True:
