@@ -494,6 +494,19 @@ def test_failing_event_waits_are_a_gap(mk):
     n.wait_health(lambda h: h[ids[1]] == "Healthy")
 
 
+def _settled(d, timeout=30):
+    """Waits until the daemon's last SIGHUP has been followed by a running
+    health monitor (SIGHUPs sent while one is pending coalesce, so counting
+    them does not work)."""
+    deadline = time.monotonic() + timeout
+    while True:
+        log = d.log()
+        if log.rfind("health monitor watching") > log.rfind("received SIGHUP"):
+            return
+        assert time.monotonic() < deadline, log[-3000:]
+        time.sleep(0.05)
+
+
 def test_in_process_sighup_storm_with_resets_leaves_no_gpu_stuck(mk):
     """SIGHUPs back to back with PRE/POST pairs injected around them, and every
     third POST_RESET dropped (as a real registration gap would lose it): every
@@ -505,19 +518,21 @@ def test_in_process_sighup_storm_with_resets_leaves_no_gpu_stuck(mk):
     ids = sorted(n.start())
     for i in range(12):
         gpu = i % 2
-        n.inject(f"{gpu} 3 storm pre {i}")
         if i % 3 == 2:
-            # the mock's FIFO would hand an unread PRE_RESET to the next
-            # registration, after the gap (real amdsmi loses it): the reset
-            # whose POST is lost is one seen before the gap
-            n.d.wait_log(f"storm pre {i}")
+            # The reset whose POST is lost must be one seen before the gap: a
+            # PRE_RESET written during a restart may be lost with the mock's
+            # event FIFO (as real amdsmi loses it) or read after it.
+            _settled(n.d)
+            n.inject(f"{gpu} 3 storm pre {i}")
+            n.d.wait_log(f"storm pre {i}", timeout=30)
+        else:
+            n.inject(f"{gpu} 3 storm pre {i}")
         n.d.signal(signal.SIGHUP)
         time.sleep(rnd.uniform(0, 0.2))
         if i % 3 != 2:  # 2, 5, 8, 11 lost -- the last one too
             n.inject(f"{gpu} 4 storm post {i}")
         time.sleep(rnd.uniform(0, 0.2))
-    n.d.wait_log("storm pre 11")
-    deadline = time.monotonic() + 20
+    deadline = time.monotonic() + 30
     h = None
     while True:
         try:
@@ -532,5 +547,5 @@ def test_in_process_sighup_storm_with_resets_leaves_no_gpu_stuck(mk):
             break
         except Exception:
             continue
-    assert n.d.log().count("received SIGHUP") == 12
+    assert n.d.log().count("received SIGHUP") >= 4  # (signals sent while one is pending coalesce)
     assert "recovered without GPU_POST_RESET" in n.d.log()  # GPU 1's last reset: only polling ended it
