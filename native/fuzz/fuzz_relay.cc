@@ -1,5 +1,7 @@
 // Coverage-guided fuzzing (libFuzzer) of the event-relay wire lines
-// (health/relay.cc): the daemon parses whatever arrives on its relay socket.
+// (health/relay.cc): the daemon parses whatever arrives on its relay socket,
+// and the privileged relay parses the daemon's request lines (a scan's
+// directory is only accepted absolute and without "..").
 // Checks: no crash; an accepted event line re-formatted from its fields parses
 // back to the same fields (message newlines folded to spaces); a hello's
 // verdict is exactly "events=ok" present before its reason; an accepted scan reply (the relay's
@@ -63,6 +65,19 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     if (r.events_ok != (first == "events=ok")) Fail("hello verdict");
   } else if (!r.kind.empty()) {
     Fail("unknown kind");
+  }
+  // The privileged side: the relay's reading of a daemon's request line.
+  health::RelayRequest q = health::ParseRelayRequest(line);
+  if (q.kind == "reinit") {
+    if (!q.fp.empty() && q.fp.size() != 16) Fail("fingerprint shape");
+    if (q.has_since && (q.since_relay.empty() || q.since_relay.size() > 32)) Fail("cursor shape");
+    if (!q.usage_dir.empty() || q.malformed) Fail("reinit with scan fields");
+  } else if (q.kind == "scan") {
+    if (!q.malformed && (q.usage_dir.empty() || q.usage_dir[0] != '/' ||
+                         q.usage_dir.find("/..") != std::string::npos || q.usage_dir.find('\t') != std::string::npos))
+      Fail("scan directory accepted");
+  } else if (!q.kind.empty()) {
+    Fail("unknown request kind");
   }
   memcap::DriverScan s;
   size_t used = 0;

@@ -441,6 +441,49 @@ RelayLine ParseRelayLine(std::string_view line) {
   return r;
 }
 
+RelayRequest ParseRelayRequest(std::string_view line) {
+  RelayRequest r;
+  while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.remove_suffix(1);
+  auto hex = [](std::string_view v, size_t min, size_t max) {
+    if (v.size() < min || v.size() > max) return false;
+    for (char c : v)
+      if (!((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f'))) return false;
+    return true;
+  };
+  if (line == "reinit" || line.rfind("reinit ", 0) == 0) {
+    r.kind = "reinit";
+    std::string_view fp = Kv(line, "fp");
+    if (hex(fp, 16, 16)) r.fp = std::string(fp);
+    auto since = Split(Kv(line, "since"), ':');
+    if (since.size() == 3 && hex(since[0], 1, 32)) {
+      auto seq = ParseUint(since[1]);
+      auto gen = ParseUint(since[2]);
+      if (seq && gen) {
+        r.has_since = true;
+        r.since_relay = since[0];
+        r.since_seq = *seq;
+        r.since_gen = *gen;
+      }
+    }
+    return r;
+  }
+  if (line.rfind("scan\t", 0) == 0) {
+    // "scan\t<usage dir>\t<cgroup>": an absolute directory without "..": the
+    // relay stats its entries, nothing more.
+    r.kind = "scan";
+    size_t tab = line.find('\t', 5);
+    if (tab == std::string_view::npos) {
+      r.malformed = true;
+      return r;
+    }
+    std::string_view dir = line.substr(5, tab - 5);
+    r.usage_dir = std::string(dir);
+    r.cgroup = std::string(line.substr(tab + 1));
+    r.malformed = dir.empty() || dir[0] != '/' || dir.find("/..") != std::string_view::npos;
+  }
+  return r;
+}
+
 std::string FormatRelayEvent(const smi::ProcessorInfo& p, uint32_t type, const std::string& message) {
   return "event node=" + (p.kfd_node == 0xffffffffu ? std::string("-") : std::to_string(p.kfd_node)) +
          " bdf=" + (p.bdf.empty() ? std::string("-") : p.bdf) + " part=" + std::to_string(p.partition_id) +
@@ -600,35 +643,30 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
   };
   // "reinit fp=<fp> since=<relay>:<seq>:<gen>": replay what the daemon missed,
   // decide whether it can have missed anything, and pass the fingerprint on.
-  auto subscribe = [&](Client& c, std::string_view line) {
-    std::string fp(Kv(line, "fp"));
-    auto since = Split(Kv(line, "since"), ':');
+  auto subscribe = [&](Client& c, RelayRequest& rq) {
     int gap = 1;
-    if (since.size() == 3 && since[0] == relay_id) {
-      auto s = ParseUint(since[1]);
-      auto g = ParseUint(since[2]);
-      if (s && g && *s <= seq) {
-        bool held = *s == seq || (!ring.empty() && ring.front().first <= *s + 1);
-        std::string replay;
-        size_t n = 0;
-        for (const auto& [q, l] : ring)
-          if (q > *s) {
-            replay += l;
-            ++n;
-          }
-        if (n) {
-          LOG_INFO(kComp, "replaying %zu event(s) after #%llu to a reconnected daemon%s", n,
-                   static_cast<unsigned long long>(*s), held ? "" : " (older ones are no longer held)");
-          send_to(c, replay);
+    if (rq.has_since && rq.since_relay == relay_id && rq.since_seq <= seq) {
+      const uint64_t s = rq.since_seq;
+      bool held = s == seq || (!ring.empty() && ring.front().first <= s + 1);
+      std::string replay;
+      size_t n = 0;
+      for (const auto& [q, l] : ring)
+        if (q > s) {
+          replay += l;
+          ++n;
         }
-        gap = held && *g == reg->Get().gen ? 0 : 1;
+      if (n) {
+        LOG_INFO(kComp, "replaying %zu event(s) after #%llu to a reconnected daemon%s", n,
+                 static_cast<unsigned long long>(s), held ? "" : " (older ones are no longer held)");
+        send_to(c, replay);
       }
+      gap = held && rq.since_gen == reg->Get().gen ? 0 : 1;
     }
     c.subscribed = true;
     c.gap = gap;
     LOG_INFO(kComp, "daemon connected for events (%s)",
-             since.size() == 3 ? (gap ? "it may have missed events" : "nothing missed") : "a new daemon");
-    reg->Request(c.id, std::move(fp));
+             rq.has_since ? (gap ? "it may have missed events" : "nothing missed") : "a new daemon");
+    reg->Request(c.id, std::move(rq.fp));
   };
   int exit_code = 0;
   bool quit = false;
@@ -722,18 +760,15 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
       }
       size_t nl;
       while (c.fd >= 0 && (nl = c.in.find('\n')) != std::string::npos) {
-        std::string_view line(c.in.data(), nl);
-        if (line == "reinit" || line.rfind("reinit ", 0) == 0) subscribe(c, line);
-        if (line.rfind("scan\t", 0) == 0) {
-          // "scan\t<usage dir>\t<cgroup>": the connection becomes the scan's.
-          size_t tab = line.find('\t', 5);
-          std::string_view dir = tab == std::string_view::npos ? std::string_view() : line.substr(5, tab - 5);
-          // An absolute directory without "..": the relay stats its entries, nothing more.
-          if (dir.empty() || dir[0] != '/' || dir.find("/..") != std::string_view::npos) {
+        RelayRequest rq = ParseRelayRequest(std::string_view(c.in.data(), nl));
+        if (rq.kind == "reinit") subscribe(c, rq);
+        if (rq.kind == "scan") {
+          // The connection becomes the scan's.
+          if (rq.malformed) {
             LOG_WARN(kComp, "malformed scan request dropped");
             close(c.fd);
           } else {
-            scans.Submit(c.fd, std::string(line.substr(5, tab - 5)), std::string(line.substr(tab + 1)));
+            scans.Submit(c.fd, std::move(rq.usage_dir), std::move(rq.cgroup));
           }
           c.fd = -1;
           break;

@@ -91,6 +91,18 @@ struct RelayLine {
   std::string message;
 };
 RelayLine ParseRelayLine(std::string_view line);
+// One daemon -> relay request line, as the (privileged) relay reads it.
+// kind: "reinit", "scan" or "" (anything else: ignored).
+struct RelayRequest {
+  std::string kind;
+  std::string fp;                 // reinit: 16 hex digits, "" when absent or not that shape
+  bool has_since = false;         // reinit: a well-formed cursor was given
+  std::string since_relay;        // (hex, at most 32 characters)
+  uint64_t since_seq = 0, since_gen = 0;
+  std::string usage_dir, cgroup;  // scan
+  bool malformed = false;         // a scan the relay drops: the directory is relative or climbs ("..")
+};
+RelayRequest ParseRelayRequest(std::string_view line);
 // Without the sequence number (the relay's waiter thread; the poll loop numbers the lines).
 std::string FormatRelayEvent(const smi::ProcessorInfo& p, uint32_t type, const std::string& message);
 

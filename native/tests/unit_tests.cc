@@ -258,6 +258,24 @@ static void TestRelayLines() {
   r = health::ParseRelayLine("hello v1 events=ok processors=8");  // an older relay: no gap said
   CHECK(r.gap == -1 && r.relay.empty());
 
+  // the relay's reading of a daemon's requests
+  auto rq = health::ParseRelayRequest("reinit fp=0123456789abcdef since=00ff00ff00ff00ff:17:3\n");
+  CHECK(rq.kind == "reinit" && rq.fp == "0123456789abcdef" && rq.has_since && rq.since_relay == "00ff00ff00ff00ff" &&
+        rq.since_seq == 17 && rq.since_gen == 3);
+  rq = health::ParseRelayRequest("reinit");
+  CHECK(rq.kind == "reinit" && rq.fp.empty() && !rq.has_since);
+  rq = health::ParseRelayRequest("reinit fp=XYZ since=-");
+  CHECK(rq.kind == "reinit" && rq.fp.empty() && !rq.has_since);
+  rq = health::ParseRelayRequest("reinit since=zz:1:2");  // not a relay ID
+  CHECK(!rq.has_since);
+  rq = health::ParseRelayRequest("reinitx");
+  CHECK(rq.kind.empty());
+  rq = health::ParseRelayRequest("scan\t/var/lib/kubelet/device-plugins/amdgpu-dp/usage\t0::/kubepods/x");
+  CHECK(rq.kind == "scan" && !rq.malformed && rq.usage_dir == "/var/lib/kubelet/device-plugins/amdgpu-dp/usage" &&
+        rq.cgroup == "0::/kubepods/x");
+  for (const char* bad : {"scan\trelative\tx", "scan\t/a/../etc\tx", "scan\tnotab", "scan\t\tx"})
+    CHECK(health::ParseRelayRequest(bad).kind == "scan" && health::ParseRelayRequest(bad).malformed);
+
   // processor fingerprints: order-independent, sensitive to every field
   smi::ProcessorInfo q = p;
   q.bdf = "0000:0d:00.0";
