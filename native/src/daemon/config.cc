@@ -188,6 +188,13 @@ const std::vector<FlagDef>& Table() {
        "events off, a new in-process registration) is back in service once amdsmi has answered every health "
        "poll for this long with no new GPU_PRE_RESET (0 = only the event brings it back)",
        [](Flags& f) -> void* { return &f.reset_recovery_hold_ms; }, true},
+      {"reset-flap-limit", "DP_RESET_FLAP_LIMIT", "resetFlapLimit", Kind::kUint,
+       "a GPU that sees this many GPU_PRE_RESETs within --reset-flap-window-ms is kept Unhealthy (cause "
+       "\"flapping\"), its GPU_POST_RESETs notwithstanding, until a whole window passes without one (0 = off)",
+       [](Flags& f) -> void* { return &f.reset_flap_limit; }, true},
+      {"reset-flap-window-ms", "DP_RESET_FLAP_WINDOW_MS", "resetFlapWindowMs", Kind::kUint,
+       "the window of --reset-flap-limit, and the quiet time that ends a quarantine",
+       [](Flags& f) -> void* { return &f.reset_flap_window_ms; }},
       {"sysfs-root", "DP_SYSFS_ROOT", "sysfsRoot", Kind::kString,
        "where sysfs is mounted: without the render node (an unprivileged pod's device cgroup denies it) "
        "amdsmi's asic_info fails, and the CU count comes from <root>/class/kfd/kfd/topology and the product "

@@ -64,7 +64,8 @@ void AppendDaemonMetrics(const DaemonMetricsInput& in, std::string* out) {
     static const std::pair<uint32_t, const char*> kCauses[] = {
         {health::kFailEcc, "ecc"},           {health::kFailUnresponsive, "unresponsive"},
         {health::kFailResetPending, "reset_pending"}, {health::kFailEvent, "event"},
-        {health::kFailRetiredPages, "retired_pages"}, {health::kFailDrained, "drained"}};
+        {health::kFailRetiredPages, "retired_pages"}, {health::kFailDrained, "drained"},
+        {health::kFailFlapping, "flapping"}};
     Family(out, "amdgpu_dp_gpu_failure", "gauge",
            "1 while the GPU is Unhealthy for this cause (drained: the operator's drain file, not a fault).");
     for (const auto& g : in.gpus)

@@ -491,6 +491,8 @@ class Supervisor {
     h.driver_root = cfg_.flags.driver_root;
     h.event_relay = cfg_.flags.health_event_socket;
     h.reset_recovery_hold_ms = static_cast<int64_t>(std::min<uint64_t>(cfg_.flags.reset_recovery_hold_ms, 86400000));
+    h.reset_flap_limit = static_cast<int>(std::min<uint64_t>(cfg_.flags.reset_flap_limit, 1000));
+    h.reset_flap_window_ms = static_cast<int64_t>(std::min<uint64_t>(cfg_.flags.reset_flap_window_ms, 86400000));
     return h;
   }
 

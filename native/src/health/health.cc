@@ -285,7 +285,7 @@ std::map<std::string, GpuRecord> Ledger::Parse(const std::string& body) {
     }
     r.ecc_seen = *seen;
     r.fail = static_cast<uint32_t>(*fail) &
-             (kFailEcc | kFailUnresponsive | kFailResetPending | kFailEvent | kFailRetiredPages);
+             (kFailEcc | kFailUnresponsive | kFailResetPending | kFailEvent | kFailRetiredPages | kFailFlapping);
     if (f.size() > 4) r.reason = f[4];
     out[f[0]] = std::move(r);
   }
@@ -367,6 +367,21 @@ bool Ledger::Gap(const std::string& key, GapMark* out) const {
   if (it == gaps_.end()) return false;
   if (out) *out = it->second;
   return true;
+}
+
+int Ledger::RecordReset(const std::string& key, int64_t now_ms, int64_t window_ms) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto& v = resets_[key];
+  v.push_back(now_ms);
+  v.erase(std::remove_if(v.begin(), v.end(), [&](int64_t t) { return now_ms - t >= window_ms; }), v.end());
+  return static_cast<int>(v.size());
+}
+
+int64_t Ledger::LastReset(const std::string& key, int64_t now_ms) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto& v = resets_[key];
+  if (v.empty()) v.push_back(now_ms);
+  return v.back();
 }
 
 void Ledger::SetResponsiveSince(const std::string& key, int64_t ms) {
@@ -766,6 +781,16 @@ void Monitor::PollOnce() {
       Update(g.index, 0, kFailUnresponsive, "device responding again");
     }
     CheckGapRecovery(g.index, alive);
+    if (fail & kFailFlapping) {
+      // Quarantine ends after a whole window without a GPU_PRE_RESET (or with
+      // damping turned off).
+      const int64_t now = NowMs();
+      const int64_t quiet = now - ledger_->LastReset(keys_[g.index], now);
+      if (cfg_.reset_flap_limit <= 0 || quiet >= cfg_.reset_flap_window_ms)
+        Update(g.index, 0, kFailFlapping,
+               cfg_.reset_flap_limit <= 0 ? "reset-flap damping off"
+                                          : "no reset for " + std::to_string(quiet / 1000) + " s: quarantine over");
+    }
     if (!alive) continue;
     ++answered;
     counters_->responsive.fetch_add(1);
@@ -936,12 +961,24 @@ void Monitor::HandleEvent(const smi::Event& e) {
       ledger_->Put(keys_[gpu], r);
     }
     if (fail_[gpu] == 0) Notify(gpu, true, why);  // keep the reference's idempotent notify
-    Update(gpu, 0, ~static_cast<uint32_t>(kFailDrained), why);  // a drain outlives a reset
+    // A drain outlives a reset, and so does a flapping GPU's quarantine.
+    Update(gpu, 0, ~static_cast<uint32_t>(kFailDrained | kFailFlapping), why);
     ledger_->ClearGap(keys_[gpu]);
   } else {
     Update(gpu, e.type == smi::kEvtGpuPreReset ? kFailResetPending : kFailEvent, 0, why);
-    // A new reset: only a gap after it lets polling end the wait.
-    if (e.type == smi::kEvtGpuPreReset) ledger_->ClearGap(keys_[gpu]);
+    if (e.type == smi::kEvtGpuPreReset) {
+      // A new reset: only a gap after it lets polling end the wait.
+      ledger_->ClearGap(keys_[gpu]);
+      if (cfg_.reset_flap_limit > 0) {
+        int n = ledger_->RecordReset(keys_[gpu], NowMs(), cfg_.reset_flap_window_ms);
+        if (n >= cfg_.reset_flap_limit && !(fail_[gpu] & kFailFlapping)) {
+          std::string w = std::to_string(cfg_.reset_flap_window_ms / 1000);
+          LOG_WARN(kComp, "GPU %s reset %d times within %s s: quarantined until %s s pass without a reset",
+                   snap_->gpus[gpu].bdf.c_str(), n, w.c_str(), w.c_str());
+          Update(gpu, kFailFlapping, 0, std::to_string(n) + " resets within " + w + " s (flapping)");
+        }
+      }
+    }
   }
 }
 

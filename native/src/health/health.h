@@ -96,6 +96,12 @@ struct HealthConfig {
   // once amdsmi has answered at every poll for this long (--reset-recovery-hold-ms;
   // 0 = never without the event).
   int64_t reset_recovery_hold_ms = 120000;
+  // Reset-flap damping (--reset-flap-limit / --reset-flap-window-ms): a GPU
+  // that sees this many GPU_PRE_RESETs within the window is kept out of
+  // service -- its GPU_POST_RESETs notwithstanding -- until a whole window
+  // passes without one. 0 = off.
+  int reset_flap_limit = 3;
+  int64_t reset_flap_window_ms = 600000;
   static HealthConfig FromEnv();
   static HealthConfig FromValues(const char* disable_value, const char* poll_ms_value);
 };
@@ -110,6 +116,7 @@ enum FailBits : uint32_t {
   kFailEvent = 1u << 3,         // any other non-ignored amdsmi event
   kFailRetiredPages = 1u << 4,  // retired HBM pages reached the threshold
   kFailDrained = 1u << 5,       // listed in the operator's drain file (not a fault; cleared by removal only)
+  kFailFlapping = 1u << 6,      // reset too often: quarantined until a quiet window passes (a POST_RESET does not clear it)
 };
 
 struct GpuRecord {
@@ -235,12 +242,19 @@ class Ledger {
   void ClearGap(const std::string& key);
   bool Gap(const std::string& key, GapMark* out) const;
   void SetResponsiveSince(const std::string& key, int64_t ms);
+  // Reset history for flap damping (in memory; steady clock): records a
+  // GPU_PRE_RESET at `now_ms` and returns how many fall within `window_ms`.
+  int RecordReset(const std::string& key, int64_t now_ms, int64_t window_ms);
+  // The last recorded reset (0 = none known; then `now_ms` is recorded, so a
+  // quarantine loaded from the state file lasts one more window).
+  int64_t LastReset(const std::string& key, int64_t now_ms);
 
  private:
   void SaveLocked() const;
   mutable std::mutex mu_;
   std::map<std::string, GpuRecord> recs_;
   std::map<std::string, GapMark> gaps_;
+  std::map<std::string, std::vector<int64_t>> resets_;
   std::string path_;
 };
 

@@ -566,7 +566,7 @@ def test_sighup_storm_with_interleaved_resets_leaves_no_gpu_stuck(scratch):
     the relay never re-enumerated for a daemon whose processors it had."""
     import random
     rnd = random.Random(5)
-    n = RelayNode(scratch, daemon_args=["--reset-recovery-hold-ms", "600000"])
+    n = RelayNode(scratch, daemon_args=["--reset-recovery-hold-ms", "600000", "--reset-flap-limit", "0"])
     try:
         n.d.wait_log("events on through the relay")
         for i in range(16):

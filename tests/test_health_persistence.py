@@ -179,7 +179,7 @@ def test_post_reset_racing_a_reregistration_leaves_the_gpu_healthy(mk):
     critical section with the health listener, so the GPU ends Healthy every
     time. ADP_DEBUG_PUBLISH_DELAY_MS holds that section open between the
     ledger read and the apply -- the window in which the reset lands."""
-    n = mk(env={"ADP_DEBUG_PUBLISH_DELAY_MS": "300"})
+    n = mk(env={"ADP_DEBUG_PUBLISH_DELAY_MS": "300"}, args=["--reset-flap-limit", "0"])  # 4 resets in a row
     ids = sorted(n.start())
     for _ in range(4):
         n.inject("1 3 pre-reset")
@@ -514,7 +514,7 @@ def test_in_process_sighup_storm_with_resets_leaves_no_gpu_stuck(mk):
     across the gaps when it does not."""
     import random
     rnd = random.Random(11)
-    n = mk(args=["--reset-recovery-hold-ms", "800"])
+    n = mk(args=["--reset-recovery-hold-ms", "800", "--reset-flap-limit", "0"])  # (6 resets per GPU)
     ids = sorted(n.start())
     for i in range(12):
         gpu = i % 2
@@ -549,3 +549,37 @@ def test_in_process_sighup_storm_with_resets_leaves_no_gpu_stuck(mk):
             continue
     assert n.d.log().count("received SIGHUP") >= 4  # (signals sent while one is pending coalesce)
     assert "recovered without GPU_POST_RESET" in n.d.log()  # GPU 1's last reset: only polling ended it
+
+
+def test_a_flapping_gpu_is_quarantined_until_a_quiet_window(mk):
+    """--reset-flap-limit 3 within --reset-flap-window-ms: the third
+    GPU_PRE_RESET in the window keeps the GPU out of service (cause
+    "flapping"); its GPU_POST_RESET no longer brings it back, a SIGHUP does not
+    either; once a whole window passes without a reset it is Healthy again. The
+    other GPU is untouched, and two resets stay under the limit."""
+    n = mk(args=["--reset-flap-limit", "3", "--reset-flap-window-ms", "2500", "--metrics-addr", "127.0.0.1:0"])
+    ids = sorted(n.start())
+    for i in range(2):
+        n.inject(f"1 3 pre {i}")
+        n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+        n.inject(f"1 4 post {i}")
+        n.wait_health(lambda h: h[ids[1]] == "Healthy")
+    n.inject("1 3 pre 2")
+    n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+    t_last = time.monotonic()
+    assert "reset 3 times within 2 s: quarantined" in n.d.wait_log("quarantined")
+    n.inject("1 4 post 2")
+    n.d.wait_log("post 2")
+    time.sleep(0.3)
+    assert n.q.empty() or all(health(n.q.get_nowait())[ids[1]] == "Unhealthy" for _ in range(n.q.qsize()))
+    port = int(__import__("re").search(r"on port (\d+)", n.d.log()).group(1))
+    from test_metrics import _get, _parse, _value
+    bdf1 = n.fx["gpus"][1]["bdf"]
+    s = _parse(_get(port, "/metrics")[1])
+    assert _value(s, "amdgpu_dp_gpu_failure", bdf=bdf1, cause="flapping") == 1
+    assert _value(s, "amdgpu_dp_gpu_failure", bdf=bdf1, cause="reset_pending") == 0
+    n.d.signal(signal.SIGHUP)  # the quarantine outlives a restart
+    assert n.first_law() == {ids[0]: "Healthy", ids[1]: "Unhealthy"}
+    n.wait_health(lambda h: h[ids[1]] == "Healthy", timeout=10)
+    assert time.monotonic() - t_last >= 2.4
+    assert "quarantine over" in n.d.log()
