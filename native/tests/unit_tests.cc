@@ -208,6 +208,15 @@ static void TestLedgerGaps() {
   l.Put("c", r);
   l.MarkGap("c", "x", false, 1);
   CHECK(health::Ledger::Serialize(l.All()) == "adp-health v1\nc\t-\t0\t4\t\n");
+  // reset history for flap damping: a sliding window
+  CHECK(l.RecordReset("d", 1000, 500) == 1);
+  CHECK(l.RecordReset("d", 1200, 500) == 2);
+  CHECK(l.RecordReset("d", 1600, 500) == 2);  // 1000 fell out of the window
+  CHECK(l.LastReset("d", 9999) == 1600);
+  CHECK(l.LastReset("e", 5000) == 5000);      // none known: now (a loaded quarantine lasts a window)
+  // the flapping bit survives the state file; drained never does (the drain file is its source)
+  auto parsed = health::Ledger::Parse("adp-health v1\nf\t-\t0\t96\tx\n");
+  CHECK(parsed["f"].fail == health::kFailFlapping);
 }
 
 static void TestRemoveDrainNames() {
