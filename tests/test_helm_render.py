@@ -406,3 +406,17 @@ def test_cu_slot_units_do_not_keep_a_gigabyte_name(values, want):
     ds = daemonset(values)
     check_consistent(ds)
     assert env(ds)["RESOURCE_CONFIG"] == want
+
+
+@pytest.mark.parametrize("values,hold,limit,window", [
+    ({}, "120000", "3", "600000"),
+    ({"resetRecoveryHoldMs": 0, "resetFlap": {"limit": 0, "windowMs": 60000}}, "0", "0", "60000"),
+])
+def test_reset_recovery_and_flap_values(values, hold, limit, window):
+    """The event-gap hold and the reset-flap damping reach the daemon; 0 (off)
+    survives the template (no `default` turning it back on)."""
+    ds = daemonset(values)
+    check_consistent(ds)
+    e = env(ds)
+    assert (e["DP_RESET_RECOVERY_HOLD_MS"], e["DP_RESET_FLAP_LIMIT"], e["DP_RESET_FLAP_WINDOW_MS"]) == \
+        (hold, limit, window)
