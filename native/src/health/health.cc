@@ -102,6 +102,11 @@ void HealthCounters::SetVramUsed(const std::string& bdf, uint64_t bytes) {
   vram_used_[bdf] = bytes;
 }
 
+bool HealthCounters::HasVramUsed(const std::string& bdf) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return vram_used_.count(bdf) != 0;
+}
+
 std::map<std::string, uint64_t> HealthCounters::VramUsed() const {
   std::lock_guard<std::mutex> lk(mu_);
   return vram_used_;
@@ -780,7 +785,13 @@ void Monitor::PollOnce() {
     } else if (alive && (fail & kFailUnresponsive)) {
       Update(g.index, 0, kFailUnresponsive, "device responding again");
     }
-    CheckGapRecovery(g.index, alive);
+    // The polled recovery wants the driver answering about the device's memory
+    // too (it fails while a reset is under way), not just the UUID amdsmi
+    // keeps; on a platform where that query never works, liveness alone.
+    Result<uint64_t> used = alive ? lib_->VramUsed(h) : Result<uint64_t>(Unavailable("not responding"));
+    if (used.ok()) counters_->SetVramUsed(g.bdf, *used);
+    // (the counters outlive monitor generations: "ever readable" does too)
+    CheckGapRecovery(g.index, alive && (used.ok() || !counters_->HasVramUsed(g.bdf)));
     if (fail & kFailFlapping) {
       // Quarantine ends after a whole window without a GPU_PRE_RESET (or with
       // damping turned off).
@@ -811,7 +822,6 @@ void Monitor::PollOnce() {
     } else {
       counters_->retired_read_errors.fetch_add(1);
     }
-    if (auto used = lib_->VramUsed(h); used.ok()) counters_->SetVramUsed(g.bdf, *used);
     auto ecc = lib_->UncorrectableErrors(h);
     if (!ecc.ok()) {
       counters_->ecc_read_errors.fetch_add(1);

@@ -43,7 +43,9 @@
 // re-registered or could not replay what this daemon missed (relay.h) -- on
 // each GPU that is waiting for its GPU_POST_RESET. Such a GPU gets a polled
 // recovery check: once amdsmi has answered at every poll for
-// --reset-recovery-hold-ms since the gap, with no new GPU_PRE_RESET, it is back
+// --reset-recovery-hold-ms since the gap -- liveness and the device's VRAM
+// usage, which the driver does not report mid-reset -- with no new
+// GPU_PRE_RESET, it is back
 // in service (logged, amdgpu_dp_gpu_recovered_without_event_total). A GPU with
 // no gap since its GPU_PRE_RESET keeps waiting for the event.
 #pragma once
@@ -151,6 +153,7 @@ struct HealthCounters {
   // Last HBM-in-use reading per GPU (bytes, all processes), for /metrics.
   void SetVramUsed(const std::string& bdf, uint64_t bytes);
   std::map<std::string, uint64_t> VramUsed() const;
+  bool HasVramUsed(const std::string& bdf) const;  // readable at least once (any generation)
   // HBM of each GPU (bytes, from the snapshot; set by the supervisor), next to VramUsed().
   void SetVramTotal(const std::string& bdf, uint64_t bytes);
   std::map<std::string, uint64_t> VramTotal() const;
