@@ -442,6 +442,21 @@ amdsmi_status_t amdsmi_get_gpu_memory_usage(amdsmi_processor_handle h, amdsmi_me
   return AMDSMI_STATUS_SUCCESS;
 }
 
+// state_dir/gpu<i>.activity: the graphics activity in percent, or anything
+// else for the driver's refusal while the GPU is in reset (AMDSMI_STATUS_BUSY).
+amdsmi_status_t amdsmi_get_gpu_activity(amdsmi_processor_handle h, amdsmi_engine_usage_t* info) {
+  GET_PROC(h);
+  if (!info) return AMDSMI_STATUS_INVAL;
+  memset(info, 0, sizeof(*info));
+  if (!g->state_dir.empty()) {
+    std::ifstream f(g->state_dir + "/gpu" + std::to_string(p->gpu) + ".activity");
+    uint32_t pct = 0;
+    if (f.is_open() && !(f >> pct)) return AMDSMI_STATUS_BUSY;
+    info->gfx_activity = pct;
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
 // state_dir/gpu<i>.partition ("CPX NPS2") overrides the fixture's modes: an
 // operator re-partitioning the GPU behind the daemon's back.
 static bool PartitionOverride(const MockProc* p, std::string* cmode, std::string* mmode) {

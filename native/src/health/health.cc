@@ -102,6 +102,16 @@ void HealthCounters::SetVramUsed(const std::string& bdf, uint64_t bytes) {
   vram_used_[bdf] = bytes;
 }
 
+void HealthCounters::MarkQueryOk(const std::string& bdf, const std::string& query) {
+  std::lock_guard<std::mutex> lk(mu_);
+  queries_ok_.insert({bdf, query});
+}
+
+bool HealthCounters::QueryEverOk(const std::string& bdf, const std::string& query) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return queries_ok_.count({bdf, query}) != 0;
+}
+
 bool HealthCounters::HasVramUsed(const std::string& bdf) const {
   std::lock_guard<std::mutex> lk(mu_);
   return vram_used_.count(bdf) != 0;
@@ -790,8 +800,19 @@ void Monitor::PollOnce() {
     // keeps; on a platform where that query never works, liveness alone.
     Result<uint64_t> used = alive ? lib_->VramUsed(h) : Result<uint64_t>(Unavailable("not responding"));
     if (used.ok()) counters_->SetVramUsed(g.bdf, *used);
+    // The SMU's metrics (graphics activity) are refused while the GPU is in
+    // reset, which makes them the better sign that a reset is over; asked only
+    // of a GPU waiting across a gap.
+    bool activity_ok = true;
+    if (alive && (fail & kFailResetPending) && ledger_->Gap(keys_[g.index], nullptr)) {
+      auto act = lib_->Activity(h);
+      if (act.ok()) counters_->MarkQueryOk(g.bdf, "activity");
+      activity_ok = act.ok() || !counters_->QueryEverOk(g.bdf, "activity");
+    } else if (alive && poll == 1) {
+      if (lib_->Activity(h).ok()) counters_->MarkQueryOk(g.bdf, "activity");  // learn whether it works here
+    }
     // (the counters outlive monitor generations: "ever readable" does too)
-    CheckGapRecovery(g.index, alive && (used.ok() || !counters_->HasVramUsed(g.bdf)));
+    CheckGapRecovery(g.index, alive && activity_ok && (used.ok() || !counters_->HasVramUsed(g.bdf)));
     if (fail & kFailFlapping) {
       // Quarantine ends after a whole window without a GPU_PRE_RESET (or with
       // damping turned off).

@@ -43,8 +43,8 @@
 // re-registered or could not replay what this daemon missed (relay.h) -- on
 // each GPU that is waiting for its GPU_POST_RESET. Such a GPU gets a polled
 // recovery check: once amdsmi has answered at every poll for
-// --reset-recovery-hold-ms since the gap -- liveness and the device's VRAM
-// usage, which the driver does not report mid-reset -- with no new
+// --reset-recovery-hold-ms since the gap -- liveness, the device's VRAM usage
+// and the SMU's activity metrics, which the driver refuses mid-reset -- with no new
 // GPU_PRE_RESET, it is back
 // in service (logged, amdgpu_dp_gpu_recovered_without_event_total). A GPU with
 // no gap since its GPU_PRE_RESET keeps waiting for the event.
@@ -154,6 +154,9 @@ struct HealthCounters {
   void SetVramUsed(const std::string& bdf, uint64_t bytes);
   std::map<std::string, uint64_t> VramUsed() const;
   bool HasVramUsed(const std::string& bdf) const;  // readable at least once (any generation)
+  // Other amdsmi queries that have answered at least once for a GPU (any generation).
+  void MarkQueryOk(const std::string& bdf, const std::string& query);
+  bool QueryEverOk(const std::string& bdf, const std::string& query) const;
   // HBM of each GPU (bytes, from the snapshot; set by the supervisor), next to VramUsed().
   void SetVramTotal(const std::string& bdf, uint64_t bytes);
   std::map<std::string, uint64_t> VramTotal() const;
@@ -196,6 +199,7 @@ struct HealthCounters {
   std::map<std::string, uint64_t> vram_used_, vram_total_;
   std::map<std::pair<std::string, std::string>, uint64_t> events_;
   std::map<std::string, uint64_t> recovered_;
+  std::set<std::pair<std::string, std::string>> queries_ok_;
   RelayCursor cursor_;
   std::string cursor_path_;
   int64_t cursor_saved_ms_ = 0;

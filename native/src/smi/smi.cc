@@ -31,6 +31,7 @@ struct Library::Fns {
   decltype(&amdsmi_get_gpu_vram_info) vram_info = nullptr;
   decltype(&amdsmi_get_gpu_memory_total) memory_total = nullptr;
   decltype(&amdsmi_get_gpu_memory_usage) memory_usage = nullptr;
+  decltype(&amdsmi_get_gpu_activity) activity = nullptr;
   decltype(&amdsmi_get_gpu_compute_partition) compute_partition = nullptr;
   decltype(&amdsmi_get_gpu_memory_partition) memory_partition = nullptr;
   decltype(&amdsmi_get_gpu_kfd_info) kfd_info = nullptr;
@@ -116,6 +117,7 @@ Result<std::unique_ptr<Library>> Library::Open(const std::string& path,
   Resolve(dl, "amdsmi_get_gpu_vram_info", &f->vram_info);
   Resolve(dl, "amdsmi_get_gpu_memory_total", &f->memory_total);
   Resolve(dl, "amdsmi_get_gpu_memory_usage", &f->memory_usage);
+  Resolve(dl, "amdsmi_get_gpu_activity", &f->activity);
   Resolve(dl, "amdsmi_get_gpu_compute_partition", &f->compute_partition);
   Resolve(dl, "amdsmi_get_gpu_memory_partition", &f->memory_partition);
   Resolve(dl, "amdsmi_get_gpu_kfd_info", &f->kfd_info);
@@ -392,6 +394,14 @@ Result<uint64_t> Library::VramUsed(void* h) {
   return used;
 }
 
+Result<uint32_t> Library::Activity(void* h) {
+  if (!f_->activity) return NotSupported("activity query not present");
+  amdsmi_engine_usage_t u{};
+  amdsmi_status_t st = f_->activity(h, &u);
+  if (st != AMDSMI_STATUS_SUCCESS) return Unavailable("activity query failed (" + std::to_string(st) + ")");
+  return u.gfx_activity;
+}
+
 Result<uint32_t> Library::RetiredPageThreshold(void* h) {
   if (!f_->bad_page_threshold) return NotSupported("bad page threshold query not present");
   uint32_t t = 0;
@@ -498,6 +508,8 @@ std::string Library::QueryReport() {
     else add("vram_info", kMissing);
     if (f_->memory_usage) { uint64_t u = 0; int st = f_->memory_usage(h, AMDSMI_MEM_TYPE_VRAM, &u); add("memory_usage", st, st == 0 ? std::to_string(u) : ""); }
     else add("memory_usage", kMissing);
+    if (f_->activity) { amdsmi_engine_usage_t u{}; int st = f_->activity(h, &u); add("activity", st, st == 0 ? std::to_string(u.gfx_activity) : ""); }
+    else add("activity", kMissing);
     if (f_->compute_partition) { char b[64] = {0}; int st = f_->compute_partition(h, b, sizeof(b) - 1); add("compute_partition", st, st == 0 ? q(b) : ""); }
     else add("compute_partition", kMissing);
     if (f_->memory_partition) { char b[64] = {0}; int st = f_->memory_partition(h, b, sizeof(b) - 1); add("memory_partition", st, st == 0 ? q(b) : ""); }

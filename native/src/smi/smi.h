@@ -122,6 +122,9 @@ class Library {
   Result<uint32_t> RetiredPageThreshold(void* h);
   // HBM in use on the device (bytes, every process: amdsmi_get_gpu_memory_usage).
   Result<uint64_t> VramUsed(void* h);
+  // Graphics-engine activity in percent (amdsmi_get_gpu_activity: the SMU's
+  // gpu_metrics, which the driver does not serve while the GPU is in reset).
+  Result<uint32_t> Activity(void* h);
   bool Responsive(void* h);
   // Processes with memory on the device and their VRAM (driver accounting).
   Result<std::vector<GpuProcess>> ProcessList(void* h);

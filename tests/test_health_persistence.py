@@ -585,27 +585,29 @@ def test_a_flapping_gpu_is_quarantined_until_a_quiet_window(mk):
     assert "quarantine over" in n.d.log()
 
 
-def test_polled_recovery_waits_for_the_driver_to_report_the_devices_memory(mk):
+@pytest.mark.parametrize("query,busy,ok", [("vram_used", "busy", "100"), ("activity", "in-reset", "7")])
+def test_polled_recovery_waits_for_the_driver_to_report_the_devices_memory(mk, query, busy, ok):
     """The polled recovery after an event gap needs more than amdsmi's cached
     UUID: the driver must report the device's VRAM usage too -- it does not
     while a reset is under way. Here the mock's VRAM query fails after the gap:
     the GPU stays out until it answers, then comes back once the hold has
-    passed from there."""
+    passed from there. The same for the SMU's activity metrics (the driver
+    refuses them while the GPU is in reset)."""
     n = mk(args=["--reset-recovery-hold-ms", "600"])
     ids = sorted(n.start())
     n.d.wait_log("health poll #1")  # VRAM usage read at least once
     n.inject("1 3 pre-reset")
     n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
-    vram = os.path.join(n.state, "gpu1.vram_used")
+    vram = os.path.join(n.state, f"gpu1.{query}")
     with open(vram, "w") as f:
-        f.write("busy\n")  # the driver does not answer about the device's memory
+        f.write(busy + "\n")  # the driver does not answer about the device
     n.d.signal(signal.SIGHUP)  # an in-process registration gap
     assert n.first_law() == {ids[0]: "Healthy", ids[1]: "Unhealthy"}
     n.d.wait_log("across an event gap")
     time.sleep(1.5)  # more than twice the hold
     assert "recovered without GPU_POST_RESET" not in n.d.log()
     with open(vram, "w") as f:
-        f.write("100\n")
+        f.write(ok + "\n")
     t0 = time.monotonic()
     n.wait_health(lambda h: h[ids[1]] == "Healthy", timeout=10)
     assert time.monotonic() - t0 >= 0.5
