@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--holders", type=int, default=0,
                     help="(--real) HIP processes holding 256 MiB each during the soak: GPU processes for the "
                          "driver-side scan to find")
+    ap.add_argument("--relay-restart-every", type=int, default=0,
+                    help="with --relay: stop the relay every N rounds (SIGTERM and SIGKILL in turn) and start a new "
+                         "one -- amdsmi registered afresh each time, the daemon reconnecting across the gap")
     ap.add_argument("--relay", action="store_true",
                     help="events and driver-side scans through an event relay process (the chart's layout)")
     ap.add_argument("--drain-churn", action="store_true",
@@ -95,8 +98,12 @@ def main():
         esock = os.path.join(d + ".relay", "events.sock")
         os.makedirs(os.path.dirname(esock), exist_ok=True)
         # (info: its per-connection decisions -- registration kept or renewed -- are counted below)
-        relay = harness.Daemon(d + ".relay", fx, args=["--event-relay", "--health-event-socket", esock],
-                               real_smi=a.real, env={"ADP_LOG_LEVEL": "info"}).start()
+        def start_relay(n):
+            return harness.Daemon(d + f".relay{n}" if n else d + ".relay", fx,
+                                  args=["--event-relay", "--health-event-socket", esock],
+                                  real_smi=a.real, env={"ADP_LOG_LEVEL": "info"},
+                                  log_path=(d + f".relay{n}.log") if n else None).start()
+        relay = start_relay(0)
         deadline = time.time() + 30
         while not os.path.exists(esock):
             assert time.time() < deadline and relay.proc.poll() is None, relay.log()[-2000:]
@@ -107,6 +114,7 @@ def main():
     driver_polls = None
     scans = []  # (source, processes, descriptors, seconds) of the last scan, per scrape
     samples, pods, hups, kubelet_restarts, scrapes = [], 0, 0, 0, 0
+    relay_restarts, relay_logs = 0, []
     ok = True
     t_end = time.time() + a.seconds
     next_sample = time.time()
@@ -141,6 +149,17 @@ def main():
                 dm.signal(signal.SIGHUP)
                 hups += 1
                 reg = kub.wait(lambda e: e.get("event") == "register", 30, since=mark)
+            if relay and a.relay_restart_every and round_no % a.relay_restart_every == 0:
+                relay_logs.append(relay.log())
+                if relay_restarts % 2:
+                    relay.proc.kill()
+                    relay.proc.wait(timeout=30)
+                else:
+                    relay.stop()
+                relay_restarts += 1
+                os.makedirs(d + f".relay{relay_restarts}", exist_ok=True)
+                relay = start_relay(relay_restarts)
+                relay_samples = []  # a new process: its own baseline
             if round_no % 7 == 0:
                 kub.stop()
                 kub = harness.NativeKubelet(ksock).start()
@@ -211,8 +230,10 @@ def main():
     if relay:
         rw = relay_samples[min(2, len(relay_samples) - 1)] if relay_samples else {}
         rl = relay_samples[-1] if relay_samples else {}
-        rlog = relay.log()
+        rlog = "".join(relay_logs) + relay.log()
         summary["relay"] = {"exit_code": relay_code, "rss_mib_after_warmup": rw.get("rss_mib"),
+                            "restarts": relay_restarts,
+                            "registrations": rlog.count("event notification registered on"),
                             "daemon_connections": rlog.count("daemon connected for events"),
                             "registration_kept": rlog.count("registration kept"),
                             "registration_renewed": rlog.count("re-enumerating"),
