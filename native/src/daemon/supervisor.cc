@@ -623,14 +623,9 @@ class Supervisor {
     layouts_ = now;
     std::string body;
     for (const auto& [res, lay] : now) body += res + "\t" + lay + "\n";
-    mkdir(PathJoin(cfg_.flags.plugin_dir, "amdgpu-dp").c_str(), 0755);
-    std::string tmp = path + ".tmp";
-    if (FILE* f = fopen(tmp.c_str(), "w")) {
-      bool ok = fwrite(body.data(), 1, body.size(), f) == body.size();
-      ok = (fclose(f) == 0) && ok;
-      if (!ok || rename(tmp.c_str(), path.c_str()) != 0) unlink(tmp.c_str());
-    }
+    if (body != layouts_written_) WriteLayoutFile(path, body);  // (each restart would rewrite it otherwise)
     if (changed.empty()) return;
+
     Result<std::vector<podresources::Assignment>> live = Unavailable("no --pod-resources-socket");
     if (!cfg_.flags.pod_resources_socket.empty()) live = podresources::List(cfg_.flags.pod_resources_socket, 1000);
     for (const auto& res : changed) {
@@ -662,6 +657,19 @@ class Supervisor {
                 "replicaCuMask or a resourceConfig replica count (amdgpu_dp_stale_allocated_ids counts their IDs "
                 "that no longer exist)", res.c_str(), held, pods, after.c_str());
     }
+  }
+
+  void WriteLayoutFile(const std::string& path, const std::string& body) {
+    mkdir(PathJoin(cfg_.flags.plugin_dir, "amdgpu-dp").c_str(), 0755);
+    std::string tmp = path + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "w");
+    bool ok = f && fwrite(body.data(), 1, body.size(), f) == body.size();
+    if (f) ok = (fclose(f) == 0) && ok;
+    if (!ok || rename(tmp.c_str(), path.c_str()) != 0) {
+      unlink(tmp.c_str());
+      return;
+    }
+    layouts_written_ = body;
   }
 
   // Kubelet restarted (or our socket vanished): same devices, same health
@@ -783,6 +791,8 @@ class Supervisor {
         // One of our own sockets removed from under us (not by our own Stop():
         // those are re-created before this event is read, so stat finds them).
         if (!e->len || !(e->mask & IN_DELETE)) continue;
+        // (the replica-layout file went with it: written again at the next restart)
+        if (std::string(e->name) == "amdgpu-dp") layouts_written_.clear();
         // The HBM-cap shim's directory wiped (a kubelet cleaning its plugin
         // directory): put it back for the next memory-unit pod.
         if (!v_.popts.memcap_host_path.empty() && std::string(e->name) == "amdgpu-dp") {
@@ -873,6 +883,7 @@ class Supervisor {
   std::map<std::string, uint64_t> layout_changes_live_;  // per resource (CheckReplicaLayouts)
   std::map<std::string, std::string> layouts_;  // resource -> Plugin::ReplicaLayout of the running generation
   bool layouts_loaded_ = false;
+  std::string layouts_written_;  // the replica-layout file's body as last written
   const std::string usage_dir_;  // grant accounting files (the plugin directory is a startup-only flag)
   std::string smi_version_;
   std::unique_ptr<metrics::HttpServer> http_;
