@@ -62,6 +62,13 @@ def test_preferred_allocation_is_always_offered(served, args):
     assert opts.get_preferred_allocation_available is True and opts.pre_start_required is False
     got = list(s.c.preferred(s.ids, (), 2).container_responses[0].deviceIDs)
     assert len(got) == 2 and set(got) <= set(s.ids)
+    if "none" not in args:
+        # partitions of one GPU together: the advertised list holds each GPU's 8
+        # CPX partitions in a row (unit order)
+        gpu_of = {i: n // 8 for n, i in enumerate(s.ids[:16])}
+        for k in (2, 8):
+            got = list(s.c.preferred(s.ids[:16], (), k).container_responses[0].deviceIDs)
+            assert len({gpu_of[i] for i in got}) == 1, (k, got)
 
 
 def test_prestart_is_required_only_when_asked(served):
