@@ -210,8 +210,7 @@ class Registration {
   bool Hung() const { return SilentMs() > stuck_ms_; }
 
   // Enumerates (after amdsmi shut_down + init when `reinit`), registers every
-  // processor and starts the waiter. Called on the caller's thread once before
-  // StartRegistrar(), then only by the registrar.
+  // processor and starts the waiter. Only the registrar thread calls it.
   void Renew(bool reinit) {
     const int64_t t0 = NowMs();
     StopWaiter();
@@ -260,9 +259,18 @@ class Registration {
     StartWaiter();
   }
 
-  // Starts the registrar thread, which serves Request().
+  // Starts the registrar thread: the first registration, then Request()s.
+  // The poll loop runs meanwhile -- a scan or a greeting does not wait for
+  // amdsmi (~100 ms on the MI355X); a daemon's reinit is answered after it.
   void StartRegistrar() {
-    registrar_ = std::thread([this] { RegistrarLoop(); });
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      state_.reason = "registering event notification";
+    }
+    registrar_ = std::thread([this] {
+      Renew(false);
+      RegistrarLoop();
+    });
   }
   // A daemon (client `id`) subscribed with its fingerprint ("" = none given).
   void Request(uint64_t id, std::string fp) {
@@ -601,7 +609,6 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
   const std::string relay_id = RandomId();
   // Heap-held: a waiter stuck in amdsmi at exit keeps using it (Shutdown).
   auto* reg = new Registration(lib, opts.driver_root, ev_pipe[1], done_pipe[1], kStuckMs);
-  reg->Renew(false);
   reg->StartRegistrar();
   LOG_INFO(kComp, "relaying amdsmi events on %s (relay %s)", socket_path.c_str(), relay_id.c_str());
 
