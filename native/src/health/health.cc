@@ -12,10 +12,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
-#include <fstream>
-#include <optional>
 #include <set>
-#include <sstream>
 
 #include "common/log.h"
 #include "common/strings.h"
@@ -25,7 +22,7 @@ namespace adp::health {
 namespace {
 constexpr const char* kComp = "health";
 
-int64_t NowMsSteady() {
+int64_t NowMs() {
   return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
 }
@@ -87,350 +84,10 @@ HealthConfig HealthConfig::FromEnv() {
   return c;
 }
 
-void HealthCounters::SetRetiredPages(const std::string& bdf, uint32_t n) {
-  std::lock_guard<std::mutex> lk(mu_);
-  retired_[bdf] = n;
-}
-
-std::map<std::string, uint32_t> HealthCounters::RetiredPages() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return retired_;
-}
-
-void HealthCounters::SetVramUsed(const std::string& bdf, uint64_t bytes) {
-  std::lock_guard<std::mutex> lk(mu_);
-  vram_used_[bdf] = bytes;
-}
-
-void HealthCounters::MarkQueryOk(const std::string& bdf, const std::string& query) {
-  std::lock_guard<std::mutex> lk(mu_);
-  queries_ok_.insert({bdf, query});
-}
-
-bool HealthCounters::QueryEverOk(const std::string& bdf, const std::string& query) const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return queries_ok_.count({bdf, query}) != 0;
-}
-
-bool HealthCounters::HasVramUsed(const std::string& bdf) const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return vram_used_.count(bdf) != 0;
-}
-
-std::map<std::string, uint64_t> HealthCounters::VramUsed() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return vram_used_;
-}
-
-void HealthCounters::SetVramTotal(const std::string& bdf, uint64_t bytes) {
-  std::lock_guard<std::mutex> lk(mu_);
-  vram_total_[bdf] = bytes;
-}
-
-std::map<std::string, uint64_t> HealthCounters::VramTotal() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return vram_total_;
-}
-
-void HealthCounters::CountEvent(const std::string& bdf, const std::string& type) {
-  std::lock_guard<std::mutex> lk(mu_);
-  ++events_[{bdf, type}];
-}
-
-std::map<std::pair<std::string, std::string>, uint64_t> HealthCounters::EventCounts() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return events_;
-}
-
-void HealthCounters::CountRecovered(const std::string& bdf) {
-  std::lock_guard<std::mutex> lk(mu_);
-  ++recovered_[bdf];
-}
-
-std::map<std::string, uint64_t> HealthCounters::Recovered() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return recovered_;
-}
-
-HealthCounters::RelayCursor HealthCounters::GetRelayCursor() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return cursor_;
-}
-
-void HealthCounters::SetRelayCursor(const RelayCursor& c) {
-  std::lock_guard<std::mutex> lk(mu_);
-  cursor_ = c;
-  cursor_dirty_ = true;
-  SaveCursorLocked();
-}
-
-void HealthCounters::AdvanceRelaySeq(uint64_t seq) {
-  std::lock_guard<std::mutex> lk(mu_);
-  if (!cursor_.valid || seq <= cursor_.seq) return;
-  cursor_.seq = seq;
-  cursor_dirty_ = true;
-  if (NowMsSteady() - cursor_saved_ms_ >= 1000) SaveCursorLocked();
-}
-
-void HealthCounters::PersistRelayCursor(const std::string& path) {
-  std::lock_guard<std::mutex> lk(mu_);
-  cursor_path_ = path;
-  std::ifstream in(path);
-  std::string header, line;
-  if (!in || !std::getline(in, header) || Trim(header) != "adp-relay-cursor v1" || !std::getline(in, line)) return;
-  auto f = Split(line, '\t');
-  auto seq = f.size() == 3 ? ParseUint(f[1]) : std::nullopt;
-  auto gen = f.size() == 3 ? ParseUint(f[2]) : std::nullopt;
-  if (!seq || !gen || f[0].empty()) {
-    LOG_WARN(kComp, "relay cursor %s: malformed; the relay will report a gap", path.c_str());
-    return;
-  }
-  cursor_ = {true, f[0], *seq, *gen};
-  LOG_INFO(kComp, "relay cursor %s: relay %s, event #%llu, generation %llu", path.c_str(), f[0].c_str(),
-           static_cast<unsigned long long>(*seq), static_cast<unsigned long long>(*gen));
-}
-
-void HealthCounters::FlushRelayCursor() {
-  std::lock_guard<std::mutex> lk(mu_);
-  SaveCursorLocked();
-}
-
-void HealthCounters::SaveCursorLocked() {
-  if (cursor_path_.empty() || !cursor_dirty_ || !cursor_.valid) return;
-  cursor_saved_ms_ = NowMsSteady();
-  cursor_dirty_ = false;
-  std::string body = "adp-relay-cursor v1\n" + cursor_.relay + "\t" + std::to_string(cursor_.seq) + "\t" +
-                     std::to_string(cursor_.gen) + "\n";
-  std::string tmp = cursor_path_ + ".tmp";
-  FILE* f = fopen(tmp.c_str(), "w");
-  bool ok = f && fwrite(body.data(), 1, body.size(), f) == body.size();
-  if (f) ok = (fclose(f) == 0) && ok;
-  if (!ok || rename(tmp.c_str(), cursor_path_.c_str()) != 0) {
-    LOG_WARN(kComp, "cannot write relay cursor %s: %s", cursor_path_.c_str(), strerror(errno));
-    unlink(tmp.c_str());
-  }
-}
-
 int Monitor::Classify(const HealthConfig& cfg, uint32_t type) {
   if (cfg.ignored.count(type)) return 0;
   if (type == smi::kEvtGpuPostReset) return +1;
   return -1;
-}
-
-Ledger::Ledger(std::string path) : path_(std::move(path)) {
-  if (path_.empty()) return;
-  std::ifstream in(path_);
-  if (!in) {
-    if (errno != ENOENT)
-      LOG_WARN(kComp, "cannot read health state %s: %s; starting empty", path_.c_str(), strerror(errno));
-    return;
-  }
-  std::stringstream ss;
-  ss << in.rdbuf();
-  recs_ = Parse(ss.str());
-  size_t failed = 0;
-  for (const auto& [_, r] : recs_) failed += r.fail != 0;
-  LOG_INFO(kComp, "health state %s: %zu GPU record(s), %zu unhealthy", path_.c_str(), recs_.size(), failed);
-}
-
-void Ledger::Reload() {
-  if (path_.empty()) return;
-  std::ifstream in(path_);
-  std::map<std::string, GpuRecord> next;
-  if (in) {
-    std::stringstream ss;
-    ss << in.rdbuf();
-    next = Parse(ss.str());
-  } else if (errno != ENOENT) {
-    LOG_WARN(kComp, "cannot re-read health state %s: %s; keeping the current state", path_.c_str(), strerror(errno));
-    return;
-  }
-  std::lock_guard<std::mutex> lk(mu_);
-  for (const auto& [k, r] : recs_)
-    if (r.fail && (!next.count(k) || !next[k].fail))
-      LOG_INFO(kComp, "health state %s: GPU %s cleared by the operator (was: %s)", path_.c_str(), k.c_str(),
-               r.reason.c_str());
-  recs_ = std::move(next);
-}
-
-std::string Ledger::Serialize(const std::map<std::string, GpuRecord>& m) {
-  std::string out = "adp-health v1\n";
-  for (const auto& [k, r] : m) {
-    std::string reason = r.reason;
-    for (auto& c : reason)
-      if (c == '\t' || c == '\n' || c == '\r') c = ' ';
-    out += k + "\t" + (r.has_baseline ? std::to_string(r.ecc_baseline) : "-") + "\t" +
-           std::to_string(r.ecc_seen) + "\t" + std::to_string(r.fail) + "\t" + reason + "\n";
-  }
-  return out;
-}
-
-std::map<std::string, GpuRecord> Ledger::Parse(const std::string& body) {
-  std::map<std::string, GpuRecord> out;
-  std::istringstream in(body);
-  std::string line;
-  bool header = false;
-  while (std::getline(in, line)) {
-    if (!header) {
-      if (Trim(line) != "adp-health v1") {
-        LOG_WARN(kComp, "health state: unknown format '%s'; ignored", line.c_str());
-        return {};
-      }
-      header = true;
-      continue;
-    }
-    if (Trim(line).empty()) continue;
-    auto f = Split(line, '\t');
-    if (f.size() < 4 || f[0].empty()) {
-      LOG_WARN(kComp, "health state: malformed line '%s' skipped", line.c_str());
-      continue;
-    }
-    GpuRecord r;
-    auto seen = ParseUint(f[2]);
-    auto fail = ParseUint(f[3]);
-    if (f[1] != "-") {
-      auto b = ParseUint(f[1]);
-      if (!b) { LOG_WARN(kComp, "health state: malformed line '%s' skipped", line.c_str()); continue; }
-      r.has_baseline = true;
-      r.ecc_baseline = *b;
-    }
-    if (!seen || !fail) {
-      LOG_WARN(kComp, "health state: malformed line '%s' skipped", line.c_str());
-      continue;
-    }
-    r.ecc_seen = *seen;
-    r.fail = static_cast<uint32_t>(*fail) &
-             (kFailEcc | kFailUnresponsive | kFailResetPending | kFailEvent | kFailRetiredPages | kFailFlapping);
-    if (f.size() > 4) r.reason = f[4];
-    out[f[0]] = std::move(r);
-  }
-  return out;
-}
-
-GpuRecord Ledger::Get(const std::string& key) const {
-  std::lock_guard<std::mutex> lk(mu_);
-  auto it = recs_.find(key);
-  return it == recs_.end() ? GpuRecord{} : it->second;
-}
-
-std::map<std::string, GpuRecord> Ledger::All() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return recs_;
-}
-
-void Ledger::Put(const std::string& key, const GpuRecord& r) {
-  std::lock_guard<std::mutex> lk(mu_);
-  auto it = recs_.find(key);
-  if (it != recs_.end() && it->second.has_baseline == r.has_baseline && it->second.ecc_baseline == r.ecc_baseline &&
-      it->second.ecc_seen == r.ecc_seen && it->second.fail == r.fail && it->second.reason == r.reason)
-    return;
-  recs_[key] = r;
-  SaveLocked();
-}
-
-void Ledger::SaveLocked() const {
-  if (path_.empty()) return;
-  std::string body = Serialize(recs_);
-  std::string tmp = path_ + ".tmp";
-  FILE* f = fopen(tmp.c_str(), "w");
-  bool ok = f && fwrite(body.data(), 1, body.size(), f) == body.size();
-  if (f) ok = (fflush(f) == 0) && (fsync(fileno(f)) == 0) && ok;
-  if (f) ok = (fclose(f) == 0) && ok;
-  if (!ok || rename(tmp.c_str(), path_.c_str()) != 0) {
-    LOG_WARN(kComp, "cannot write health state %s: %s", path_.c_str(), strerror(errno));
-    unlink(tmp.c_str());
-  }
-}
-
-bool Ledger::MarkGap(const std::string& key, const std::string& why, bool tentative, int64_t now_ms) {
-  std::lock_guard<std::mutex> lk(mu_);
-  auto it = gaps_.find(key);
-  if (it == gaps_.end()) {
-    gaps_[key] = GapMark{now_ms, why, tentative, 0};
-    return true;
-  }
-  if (it->second.tentative && !tentative) {  // confirmed: the relay could not replay what was missed
-    it->second.tentative = false;
-    it->second.why = why;
-    return true;
-  }
-  return false;
-}
-
-std::vector<std::string> Ledger::CancelTentativeGaps() {
-  std::lock_guard<std::mutex> lk(mu_);
-  std::vector<std::string> out;
-  for (auto it = gaps_.begin(); it != gaps_.end();) {
-    if (it->second.tentative) {
-      out.push_back(it->first);
-      it = gaps_.erase(it);
-    } else {
-      ++it;
-    }
-  }
-  return out;
-}
-
-void Ledger::ClearGap(const std::string& key) {
-  std::lock_guard<std::mutex> lk(mu_);
-  gaps_.erase(key);
-}
-
-bool Ledger::Gap(const std::string& key, GapMark* out) const {
-  std::lock_guard<std::mutex> lk(mu_);
-  auto it = gaps_.find(key);
-  if (it == gaps_.end()) return false;
-  if (out) *out = it->second;
-  return true;
-}
-
-int Ledger::RecordReset(const std::string& key, int64_t now_ms, int64_t window_ms) {
-  std::lock_guard<std::mutex> lk(mu_);
-  auto& v = resets_[key];
-  v.push_back(now_ms);
-  v.erase(std::remove_if(v.begin(), v.end(), [&](int64_t t) { return now_ms - t >= window_ms; }), v.end());
-  return static_cast<int>(v.size());
-}
-
-int64_t Ledger::LastReset(const std::string& key, int64_t now_ms) {
-  std::lock_guard<std::mutex> lk(mu_);
-  auto& v = resets_[key];
-  if (v.empty()) v.push_back(now_ms);
-  return v.back();
-}
-
-void Ledger::SetResponsiveSince(const std::string& key, int64_t ms) {
-  std::lock_guard<std::mutex> lk(mu_);
-  if (auto it = gaps_.find(key); it != gaps_.end()) it->second.responsive_since_ms = ms;
-}
-
-std::vector<std::pair<int, std::string>> Ledger::Failed(const inventory::Snapshot& snap) const {
-  std::vector<std::pair<int, std::string>> out;
-  std::lock_guard<std::mutex> lk(mu_);
-  for (const auto& g : snap.gpus) {
-    auto it = recs_.find(KeyOf(g));
-    if (it != recs_.end() && it->second.fail) out.emplace_back(g.index, it->second.reason);
-  }
-  return out;
-}
-
-std::string HealthCounters::Json() const {
-  char buf[512];
-  int e = events_enabled.load();
-  uint64_t recovered = 0;
-  for (const auto& [_, n] : Recovered()) recovered += n;
-  snprintf(buf, sizeof(buf),
-           "{\"events\": \"%s\", \"polls\": %llu, \"responsive\": %llu, \"ecc_reads_ok\": %llu, "
-           "\"ecc_read_errors\": %llu, \"events_received\": %llu, \"retired_reads_ok\": %llu, "
-           "\"retired_read_errors\": %llu, \"event_gaps\": %llu, \"recovered_without_event\": %llu}",
-           e < 0 ? "not started" : e ? "on" : "off", static_cast<unsigned long long>(polls.load()),
-           static_cast<unsigned long long>(responsive.load()), static_cast<unsigned long long>(ecc_reads_ok.load()),
-           static_cast<unsigned long long>(ecc_read_errors.load()),
-           static_cast<unsigned long long>(events_received.load()),
-           static_cast<unsigned long long>(retired_reads_ok.load()),
-           static_cast<unsigned long long>(retired_read_errors.load()),
-           static_cast<unsigned long long>(event_gaps.load()), static_cast<unsigned long long>(recovered));
-  return buf;
 }
 
 Monitor::Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> snap, HealthConfig cfg,
@@ -583,12 +240,6 @@ void Monitor::Stop() {
   }
 }
 
-namespace {
-int64_t NowMs() {
-  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
-      .count();
-}
-}  // namespace
 
 void Monitor::RelayConnect() {
   relay_tried_ms_ = NowMs();
@@ -674,61 +325,6 @@ void Monitor::RelayWait(int ms) {
   }
   if (relay_buf_.size() > 65536) relay_buf_.clear();
   if (closed) RelayClose("the event relay closed the connection");
-}
-
-std::set<std::string> DrainTokens(std::string_view text) {
-  std::set<std::string> names;
-  for (size_t b = 0; b < text.size();) {
-    size_t e = text.find('\n', b);
-    if (e == std::string_view::npos) e = text.size();
-    std::string line(text.substr(b, e - b));
-    b = e + 1;
-    if (size_t hash = line.find('#'); hash != std::string::npos) line.resize(hash);
-    for (char& c : line)
-      if (c == ',' || c == '\t' || c == '\r') c = ' ';
-    for (size_t p = 0; p < line.size();) {
-      size_t q = line.find(' ', p);
-      if (q == std::string::npos) q = line.size();
-      if (q > p) names.insert(line.substr(p, q - p));
-      p = q + 1;
-    }
-  }
-  return names;
-}
-
-std::string RemoveDrainNames(std::string_view line, const std::set<std::string>& names) {
-  std::string_view body = line, comment;
-  if (size_t hash = line.find('#'); hash != std::string_view::npos) {
-    body = line.substr(0, hash);
-    comment = line.substr(hash);
-  }
-  bool commas = body.find(',') != std::string_view::npos;
-  std::vector<std::string> keep;
-  bool removed = false;
-  for (size_t p = 0; p < body.size();) {
-    size_t q = body.find_first_of(" \t,\r", p);
-    if (q == std::string_view::npos) q = body.size();
-    if (q > p) {
-      std::string tok(body.substr(p, q - p));
-      if (names.count(tok)) removed = true;
-      else keep.push_back(std::move(tok));
-    }
-    p = q + 1;
-  }
-  if (!removed) return std::string(line);
-  if (keep.empty()) return "";
-  std::string out;
-  for (const auto& t : keep) out += (out.empty() ? "" : commas ? "," : " ") + t;
-  if (!comment.empty()) out += "  " + std::string(comment);
-  return out;
-}
-
-std::set<std::string> DrainNames(const inventory::PhysicalGpu& g) {
-  std::set<std::string> n = {g.uuid, g.bdf, std::to_string(g.node_index)};
-  if (size_t dot = g.bdf.rfind('.'); dot != std::string::npos) n.insert(g.bdf.substr(0, dot));
-  for (const auto& p : g.partitions) n.insert(p.uuid);
-  n.erase("");
-  return n;
 }
 
 void Monitor::ApplyDrain() {
@@ -957,11 +553,6 @@ void Monitor::Update(int gpu, uint32_t set, uint32_t clear, const std::string& r
     LOG_INFO(kComp, "GPU %s stays unhealthy (%s; failure bits %u -> %u)", snap_->gpus[gpu].bdf.c_str(),
              reason.c_str(), before, after);
   }
-}
-
-int64_t HealthCounters::HealthLoopAgeMs() const {
-  int64_t beat = loop_beat_ms.load();
-  return beat == 0 ? 0 : std::max<int64_t>(0, NowMs() - beat);
 }
 
 void Monitor::HandleEvent(const smi::Event& e) {
