@@ -485,8 +485,8 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
   // addresses are the same ID (distinct IDs counted without comparing strings).
   std::vector<const std::pair<const std::string_view, int>*> entries;
   std::vector<std::pair<int, uint32_t>> shares;  // (unit, replica) of CU-partitioned units
-  std::string c, joined, cu_mask, mem_mib, mem_frac, mem_devs;
-  std::vector<uint64_t> grant_bytes;
+  std::string c, joined, cu_mask;
+  MemoryGrant grant;
   for (const auto& ids : containers) {
     us.clear();
     shares.clear();
@@ -519,120 +519,11 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       for (const auto* e : entries) ++units_per[e->second];
     }
     us.erase(std::unique(us.begin(), us.end()), us.end());
-    if (unhealthy_units_.load(std::memory_order_relaxed) != 0) {
-      // A kubelet racing a health transition (or holding a stale device list)
-      // can name a device that is Unhealthy right now.
-      auto law = CurrentLaw();
-      for (int u : us) {
-        if (law->healthy[u]) continue;
-        stats_.unhealthy_allocations.Add(1);
-        if (opts_.reject_unhealthy)
-          return FailedPrecondition("allocation request for '" + spec_.resource_name + "': device " +
-                                    units_[u].id + " is Unhealthy");
-        if (warned_law_[u].exchange(law->version, std::memory_order_relaxed) != law->version)
-          LOG_WARN(kComp, "allocate '%s': device %s is Unhealthy (allocated anyway; --reject-unhealthy refuses)",
-                   spec_.resource_name.c_str(), units_[u].id.c_str());
-      }
-    }
-    // Memory-unit resources (replicas = -1): tell the container how much HBM it
-    // was granted on each device so frameworks can cap themselves (e.g.
-    // torch.cuda.set_per_process_memory_fraction). Listed in enumeration order
-    // -- the order HIP numbers the container's devices and HSA_CU_MASK uses --
-    // whatever order the ID strategy gives AMD_VISIBLE_DEVICES. The reference
-    // hands out memory units without telling the workload.
-    mem_mib.clear();
-    mem_frac.clear();
-    mem_devs.clear();
-    grant_bytes.clear();
-    if (hbm_grants_) {
-      char buf[32];
-      for (size_t i = 0; i < us.size(); ++i) {
-        const Unit& u = units_[us[i]];
-        uint64_t granted = static_cast<uint64_t>(units_per[us[i]]) * u.grant_mib;
-        if (i) { mem_mib += ','; mem_frac += ','; mem_devs += ','; }
-        mem_devs += u.visible_id;
-        mem_mib += std::to_string(granted);
-        grant_bytes.push_back(granted << 20);
-        // Under the HBM-cap shim the device reports the grant as its memory, so
-        // the grant is all of what the workload sees.
-        double frac = !memcap_bytes_.empty() ? 1.0 : u.vram_mib ? std::min(1.0, double(granted) / u.vram_mib) : 0.0;
-        snprintf(buf, sizeof(buf), "%.4f", frac);
-        mem_frac += buf;
-      }
-    }
+    if (unhealthy_units_.load(std::memory_order_relaxed) != 0) ADP_RETURN_IF_ERROR(CheckAllocatedHealth(us));
+    grant.Clear();
+    if (hbm_grants_) BuildMemoryGrant(us, units_per, &grant);
     cu_mask.clear();
-    if (!shares.empty()) {
-      // HSA_CU_MASK="<agent>:<first>-<last>,...;...": agents are numbered in the
-      // container in KFD-node order (= unit order, us is sorted by unit), and
-      // devices without an entry keep all their CUs. Adjacent replica shares merge.
-      // By unit, then by where the replica's range starts (memory-unit ranges
-      // follow the IDs' lexicographic order, not the replica number).
-      std::sort(shares.begin(), shares.end(), [&](const auto& a, const auto& b) {
-        if (a.first != b.first) return a.first < b.first;
-        const auto& ra = units_[a.first].replica_cus[a.second];
-        const auto& rb = units_[b.first].replica_cus[b.second];
-        return ra != rb ? ra < rb : a.second < b.second;
-      });
-      shares.erase(std::unique(shares.begin(), shares.end()), shares.end());
-      size_t k = 0;
-      for (size_t ord = 0; ord < us.size(); ++ord) {
-        while (k < shares.size() && shares[k].first < us[ord]) ++k;
-        if (k == shares.size() || shares[k].first != us[ord]) continue;
-        const Unit& unit = units_[us[ord]];
-        const auto& ranges = unit.replica_cus;
-        size_t end = k;
-        while (end < shares.size() && shares[end].first == us[ord]) ++end;
-        // Shares are sorted by range and distinct; memory units share slots, so a
-        // run of equal ranges is the units of one slot this container holds.
-        auto run_end = [&](size_t g) {
-          size_t h = g + 1;
-          while (h < end && ranges[shares[h].second] == ranges[shares[g].second]) ++h;
-          return h;
-        };
-        auto filled = [&](size_t g, size_t h) {
-          return h - g == unit.slot_units[ranges[shares[g].second].first / unit.xcds];
-        };
-        // --memory-unit-cu-slots whole: keep only the slots whose units are all
-        // this container's, so no neighbour runs on them. A container filling no
-        // slot keeps its partial ones (it needs some CUs) and is counted.
-        bool whole_only = false;
-        if (!unit.slot_units.empty()) {
-          for (size_t g = k; g < end && !whole_only;) {
-            size_t h = run_end(g);
-            whole_only = filled(g, h);
-            g = h;
-          }
-          if (!whole_only) stats_.partial_cu_slot_allocations.Add(1);
-        }
-        if (!cu_mask.empty()) cu_mask += ';';
-        cu_mask += std::to_string(ord);
-        char sep = ':';
-        bool open = false;
-        uint32_t lo = 0, hi = 0;
-        auto emit = [&] {
-          cu_mask += sep;
-          cu_mask += std::to_string(lo) + "-" + std::to_string(hi);
-          sep = ',';
-        };
-        for (size_t g = k; g < end;) {
-          size_t h = run_end(g);
-          const auto& rg = ranges[shares[g].second];
-          bool keep = !whole_only || filled(g, h);
-          g = h;
-          if (!keep) continue;
-          if (open && rg.first <= hi + 1) {  // equal and adjacent ranges merge
-            hi = std::max(hi, rg.second);
-            continue;
-          }
-          if (open) emit();
-          lo = rg.first;
-          hi = rg.second;
-          open = true;
-        }
-        if (open) emit();
-        k = end;
-      }
-    }
+    if (!shares.empty()) BuildCuMask(us, &shares, &cu_mask);
     if (opts_.id_strategy == DeviceIdStrategy::kUuid)
       std::sort(us.begin(), us.end(), [&](int a, int b) { return units_[a].id < units_[b].id; });
 
@@ -642,56 +533,14 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
       if (i) joined += ',';
       joined += units_[us[i]].visible_id;
     }
-    switch (opts_.list_strategy) {
-      case DeviceListStrategy::kEnvvar:
-        pb::PutMapEntry(&c, 1, opts_.envvar, joined);
-        break;
-      case DeviceListStrategy::kVolumeMounts:
-        pb::PutMapEntry(&c, 1, opts_.envvar, kVolumeMountRoot);
-        for (int u : us) c += units_[u].mount_bytes;
-        break;
-      case DeviceListStrategy::kCdiAnnotations: {
-        if (us.empty()) break;
-        std::string names;
-        for (size_t i = 0; i < us.size(); ++i) {
-          if (i) names += ',';
-          names += std::string(kCdiVendorClass) + "=" + units_[us[i]].visible_id;
-        }
-        pb::PutMapEntry(&c, 4, "cdi.k8s.io/amd-gpu-device-plugin_" + units_[us[0]].visible_id, names);
-        break;
-      }
-      case DeviceListStrategy::kCdiCri:
-        for (int u : us) {
-          std::string n;
-          pb::PutStr(&n, 1, std::string(kCdiVendorClass) + "=" + units_[u].visible_id);
-          pb::PutLen(&c, 5, n);
-        }
-        break;
-    }
-    if (!mem_mib.empty()) {
-      pb::PutMapEntry(&c, 1, kMemoryLimitEnv, mem_mib);
-      pb::PutMapEntry(&c, 1, kMemoryFractionEnv, mem_frac);
-      pb::PutMapEntry(&c, 1, kMemoryDevicesEnv, mem_devs);
+    AppendDeviceList(us, joined, &c);
+    if (!grant.mib.empty()) {
+      pb::PutMapEntry(&c, 1, kMemoryLimitEnv, grant.mib);
+      pb::PutMapEntry(&c, 1, kMemoryFractionEnv, grant.frac);
+      pb::PutMapEntry(&c, 1, kMemoryDevicesEnv, grant.devs);
       c += memcap_bytes_;  // the container enforces the grant (empty unless --enforce-memory-units)
-      if (!memcap_bytes_.empty()) {
-        // The grant itself, read-only: the shim's caps (the env can only lower them).
-        // Encoded in place (a Mount: container path, host path, read-only).
-        static thread_local std::string gm, cpath, hpath;
-        for (size_t i = 0; i < grant_bytes.size(); ++i) {
-          char num[24];
-          cpath.assign(adp_memcap::kGrantDir).push_back('/');
-          cpath.append(num, static_cast<size_t>(std::to_chars(num, num + sizeof(num), i).ptr - num));
-          hpath.assign(grant_dir_prefix_);
-          hpath.append(num, static_cast<size_t>(std::to_chars(num, num + sizeof(num), grant_bytes[i] >> 20).ptr - num));
-          hpath.append(".mib");
-          gm.clear();
-          pb::PutStr(&gm, 1, cpath);
-          pb::PutStr(&gm, 2, hpath);
-          pb::PutBool(&gm, 3, true);
-          pb::PutLen(&c, 2, gm);
-        }
-      }
-      if (!memcap_bytes_.empty() && !opts_.memcap_usage_dir.empty()) AddUsageFile(ids, grant_bytes, &c);
+      if (!memcap_bytes_.empty()) AppendGrantMounts(grant.bytes, &c);
+      if (!memcap_bytes_.empty() && !opts_.memcap_usage_dir.empty()) AddUsageFile(ids, grant.bytes, &c);
     }
     if (!cu_mask.empty()) pb::PutMapEntry(&c, 1, kCuMaskEnv, cu_mask);
     if (opts_.pass_device_specs) {
@@ -708,6 +557,172 @@ Status Plugin::HandleAllocate(std::string_view req, std::string* resp) {
   stats_.allocate_ns_total.Add(dt);
   stats_.allocate_ns_max.Observe(dt);
   return Status::Ok();
+}
+
+// A kubelet racing a health transition (or holding a stale device list) can
+// name a device that is Unhealthy right now.
+Status Plugin::CheckAllocatedHealth(const std::vector<int>& us) {
+  auto law = CurrentLaw();
+  for (int u : us) {
+    if (law->healthy[u]) continue;
+    stats_.unhealthy_allocations.Add(1);
+    if (opts_.reject_unhealthy)
+      return FailedPrecondition("allocation request for '" + spec_.resource_name + "': device " + units_[u].id +
+                                " is Unhealthy");
+    if (warned_law_[u].exchange(law->version, std::memory_order_relaxed) != law->version)
+      LOG_WARN(kComp, "allocate '%s': device %s is Unhealthy (allocated anyway; --reject-unhealthy refuses)",
+               spec_.resource_name.c_str(), units_[u].id.c_str());
+  }
+  return Status::Ok();
+}
+
+// Memory-unit resources (replicas = -1): tell the container how much HBM it
+// was granted on each device so frameworks can cap themselves (e.g.
+// torch.cuda.set_per_process_memory_fraction). Listed in enumeration order
+// (us sorted by unit) -- the order HIP numbers the container's devices and
+// HSA_CU_MASK uses -- whatever order the ID strategy gives AMD_VISIBLE_DEVICES.
+// The reference hands out memory units without telling the workload.
+void Plugin::BuildMemoryGrant(const std::vector<int>& us, const std::vector<int>& units_per,
+                              MemoryGrant* g) const {
+  char buf[32];
+  for (size_t i = 0; i < us.size(); ++i) {
+    const Unit& u = units_[us[i]];
+    uint64_t granted = static_cast<uint64_t>(units_per[us[i]]) * u.grant_mib;
+    if (i) { g->mib += ','; g->frac += ','; g->devs += ','; }
+    g->devs += u.visible_id;
+    g->mib += std::to_string(granted);
+    g->bytes.push_back(granted << 20);
+    // Under the HBM-cap shim the device reports the grant as its memory, so
+    // the grant is all of what the workload sees.
+    double frac = !memcap_bytes_.empty() ? 1.0 : u.vram_mib ? std::min(1.0, double(granted) / u.vram_mib) : 0.0;
+    snprintf(buf, sizeof(buf), "%.4f", frac);
+    g->frac += buf;
+  }
+}
+
+// HSA_CU_MASK="<agent>:<first>-<last>,...;...": agents are numbered in the
+// container in KFD-node order (= unit order, us is sorted by unit), and
+// devices without an entry keep all their CUs. Adjacent replica shares merge.
+void Plugin::BuildCuMask(const std::vector<int>& us, std::vector<std::pair<int, uint32_t>>* shares_in,
+                         std::string* cu_mask) {
+  auto& shares = *shares_in;
+  // By unit, then by where the replica's range starts (memory-unit ranges
+  // follow the IDs' lexicographic order, not the replica number).
+  std::sort(shares.begin(), shares.end(), [&](const auto& a, const auto& b) {
+    if (a.first != b.first) return a.first < b.first;
+    const auto& ra = units_[a.first].replica_cus[a.second];
+    const auto& rb = units_[b.first].replica_cus[b.second];
+    return ra != rb ? ra < rb : a.second < b.second;
+  });
+  shares.erase(std::unique(shares.begin(), shares.end()), shares.end());
+  size_t k = 0;
+  for (size_t ord = 0; ord < us.size(); ++ord) {
+    while (k < shares.size() && shares[k].first < us[ord]) ++k;
+    if (k == shares.size() || shares[k].first != us[ord]) continue;
+    const Unit& unit = units_[us[ord]];
+    const auto& ranges = unit.replica_cus;
+    size_t end = k;
+    while (end < shares.size() && shares[end].first == us[ord]) ++end;
+    // Shares are sorted by range and distinct; memory units share slots, so a
+    // run of equal ranges is the units of one slot this container holds.
+    auto run_end = [&](size_t g) {
+      size_t h = g + 1;
+      while (h < end && ranges[shares[h].second] == ranges[shares[g].second]) ++h;
+      return h;
+    };
+    auto filled = [&](size_t g, size_t h) {
+      return h - g == unit.slot_units[ranges[shares[g].second].first / unit.xcds];
+    };
+    // --memory-unit-cu-slots whole: keep only the slots whose units are all
+    // this container's, so no neighbour runs on them. A container filling no
+    // slot keeps its partial ones (it needs some CUs) and is counted.
+    bool whole_only = false;
+    if (!unit.slot_units.empty()) {
+      for (size_t g = k; g < end && !whole_only;) {
+        size_t h = run_end(g);
+        whole_only = filled(g, h);
+        g = h;
+      }
+      if (!whole_only) stats_.partial_cu_slot_allocations.Add(1);
+    }
+    if (!cu_mask->empty()) *cu_mask += ';';
+    *cu_mask += std::to_string(ord);
+    char sep = ':';
+    bool open = false;
+    uint32_t lo = 0, hi = 0;
+    auto emit = [&] {
+      *cu_mask += sep;
+      *cu_mask += std::to_string(lo) + "-" + std::to_string(hi);
+      sep = ',';
+    };
+    for (size_t g = k; g < end;) {
+      size_t h = run_end(g);
+      const auto& rg = ranges[shares[g].second];
+      bool keep = !whole_only || filled(g, h);
+      g = h;
+      if (!keep) continue;
+      if (open && rg.first <= hi + 1) {  // equal and adjacent ranges merge
+        hi = std::max(hi, rg.second);
+        continue;
+      }
+      if (open) emit();
+      lo = rg.first;
+      hi = rg.second;
+      open = true;
+    }
+    if (open) emit();
+    k = end;
+  }
+}
+
+// The device list in the --device-list-strategy's form (server.go:338-346, apiEnvs/apiMounts at
+// server.go:423-441; the CDI forms are this plugin's own).
+void Plugin::AppendDeviceList(const std::vector<int>& us, const std::string& joined, std::string* c) const {
+  switch (opts_.list_strategy) {
+    case DeviceListStrategy::kEnvvar:
+      pb::PutMapEntry(c, 1, opts_.envvar, joined);
+      break;
+    case DeviceListStrategy::kVolumeMounts:
+      pb::PutMapEntry(c, 1, opts_.envvar, kVolumeMountRoot);
+      for (int u : us) *c += units_[u].mount_bytes;
+      break;
+    case DeviceListStrategy::kCdiAnnotations: {
+      if (us.empty()) break;
+      std::string names;
+      for (size_t i = 0; i < us.size(); ++i) {
+        if (i) names += ',';
+        names += std::string(kCdiVendorClass) + "=" + units_[us[i]].visible_id;
+      }
+      pb::PutMapEntry(c, 4, "cdi.k8s.io/amd-gpu-device-plugin_" + units_[us[0]].visible_id, names);
+      break;
+    }
+    case DeviceListStrategy::kCdiCri:
+      for (int u : us) {
+        std::string n;
+        pb::PutStr(&n, 1, std::string(kCdiVendorClass) + "=" + units_[u].visible_id);
+        pb::PutLen(c, 5, n);
+      }
+      break;
+  }
+}
+
+// The grant itself, read-only: the shim's caps (the env can only lower them).
+// Encoded in place (a Mount: container path, host path, read-only).
+void Plugin::AppendGrantMounts(const std::vector<uint64_t>& grant_bytes, std::string* c) const {
+  static thread_local std::string gm, cpath, hpath;
+  for (size_t i = 0; i < grant_bytes.size(); ++i) {
+    char num[24];
+    cpath.assign(adp_memcap::kGrantDir).push_back('/');
+    cpath.append(num, static_cast<size_t>(std::to_chars(num, num + sizeof(num), i).ptr - num));
+    hpath.assign(grant_dir_prefix_);
+    hpath.append(num, static_cast<size_t>(std::to_chars(num, num + sizeof(num), grant_bytes[i] >> 20).ptr - num));
+    hpath.append(".mib");
+    gm.clear();
+    pb::PutStr(&gm, 1, cpath);
+    pb::PutStr(&gm, 2, hpath);
+    pb::PutBool(&gm, 3, true);
+    pb::PutLen(c, 2, gm);
+  }
 }
 
 // The grant's accounting file (memcap/usage.h), mounted read-write where the

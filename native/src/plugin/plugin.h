@@ -300,6 +300,17 @@ class Plugin {
                                 const std::vector<memcap::Usage>* grant_files);
   void AddUsageFile(const std::vector<std::string_view>& ids, const std::vector<uint64_t>& grant_bytes,
                     std::string* c);
+  // Allocate's pieces, per container (HandleAllocate).
+  struct MemoryGrant {
+    std::string mib, frac, devs;   // the AMD_GPU_MEMORY_* env values
+    std::vector<uint64_t> bytes;   // per device, in enumeration order
+    void Clear() { mib.clear(); frac.clear(); devs.clear(); bytes.clear(); }
+  };
+  Status CheckAllocatedHealth(const std::vector<int>& us);
+  void BuildMemoryGrant(const std::vector<int>& us, const std::vector<int>& units_per, MemoryGrant* g) const;
+  void BuildCuMask(const std::vector<int>& us, std::vector<std::pair<int, uint32_t>>* shares, std::string* cu_mask);
+  void AppendDeviceList(const std::vector<int>& us, const std::string& joined, std::string* c) const;
+  void AppendGrantMounts(const std::vector<uint64_t>& grant_bytes, std::string* c) const;
 
  public:
   // With the shim: writes every grant file this plugin's Allocate() can mount
