@@ -203,75 +203,7 @@ void Plugin::BuildUnits() {
                     : memory_units_                                     ? alloc::ReplicaPolicy::kPack
                                                                         : alloc::ReplicaPolicy::kSpread;
   hbm_grants_ = memory_units_ || (opts_.replica_hbm_share && replicated_);
-  for (const auto& ref : spec_.devices) {
-    const auto& g = snap_->gpus[ref.gpu];
-    Unit u;
-    u.gpu = ref.gpu;
-    if (ref.partition < 0) {
-      u.id = g.uuid;
-      u.index = std::to_string(g.node_index);
-      u.numa = g.numa;
-      u.vram_mib = g.vram_mib;
-      for (const auto& p : g.partitions) {
-        if (!p.render_path.empty()) u.paths.push_back(p.render_path);
-        if (!p.card_path.empty()) u.paths.push_back(p.card_path);
-        u.handles.push_back(p.handle);
-      }
-    } else {
-      const auto& p = g.partitions[ref.partition];
-      u.id = p.uuid;
-      u.index = std::to_string(g.node_index) + ":" + std::to_string(ref.partition);
-      u.numa = p.numa >= 0 ? p.numa : g.numa;
-      u.vram_mib = p.vram_mib;
-      if (!p.render_path.empty()) u.paths.push_back(p.render_path);
-      if (!p.card_path.empty()) u.paths.push_back(p.card_path);
-      u.handles.push_back(p.handle);
-    }
-    // Auto replicas: one per `auto_replica_unit_mib` of this device's own memory
-    // (server.go:100-103; per-partition memory fixes B4). At least one.
-    u.replicas = v.auto_replicas
-                     ? static_cast<unsigned>(std::max<uint64_t>(1, u.vram_mib / opts_.auto_replica_unit_mib))
-                     : std::max(1u, v.replicas);
-    if (hbm_grants_) u.grant_mib = memory_units_ ? opts_.auto_replica_unit_mib : u.vram_mib / u.replicas;
-    u.cus = ref.partition < 0 ? g.cus : g.partitions[ref.partition].cus;
-    u.xcds = ref.partition < 0 ? g.xcds : g.partitions[ref.partition].xcds;
-    if (memory_units_ && opts_.cu_slot_units) {
-      // One unit = one CU slot (one CU on every XCD) and that slot's share of
-      // the HBM: 32 units of 9,215 MiB on an SPX MI355X. Every grant is then a
-      // whole number of slots -- no slot is shared, none left idle.
-      const uint32_t per = u.xcds && u.cus % u.xcds == 0 ? u.cus / u.xcds : 0;
-      if (per >= 2 && u.vram_mib / per > 0) {
-        u.replicas = per;
-        u.grant_mib = u.vram_mib / per;
-      } else {
-        LOG_WARN(kComp, "device %s: %u CUs over %u XCDs give no CU slots; its memory units are %llu MiB",
-                 u.id.c_str(), u.cus, u.xcds, static_cast<unsigned long long>(opts_.auto_replica_unit_mib));
-      }
-    }
-    if (opts_.replica_cu_mask && replicated_) {
-      u.replica_cus = memory_units_ ? MemoryUnitCuRanges(u.cus, u.xcds, u.replicas)
-                                    : ReplicaCuRanges(u.cus, u.xcds, u.replicas);
-      if (memory_units_ && opts_.whole_cu_slots && !u.replica_cus.empty()) {
-        u.slot_units.assign(u.cus / u.xcds, 0);
-        for (const auto& rg : u.replica_cus) ++u.slot_units[rg.first / u.xcds];
-      }
-      if (u.replica_cus.empty() && u.replicas > 1)
-        LOG_WARN(kComp, "device %s: %u CUs over %u XCDs cannot be split into %u CU shares; its replicas "
-                 "share all CUs", u.id.c_str(), u.cus, u.xcds, u.replicas);
-    }
-    u.visible_id = opts_.id_strategy == DeviceIdStrategy::kIndex ? u.index : u.id;
-    for (const auto& path : u.paths) {
-      pb::DeviceSpec ds{path, PathJoin(opts_.driver_root, path), "rw"};
-      std::string b;
-      pb::Encode(ds, &b);
-      pb::PutLen(&u.spec_bytes, 3, b);
-    }
-    pb::Mount m{PathJoin(kVolumeMountRoot, u.visible_id), kVolumeMountHostPath, false};
-    std::string mb;
-    pb::Encode(m, &mb);
-    pb::PutLen(&u.mount_bytes, 2, mb);
-    units_.push_back(std::move(u));
-  }
+  for (const auto& ref : spec_.devices) units_.push_back(MakeUnit(ref));
   if (memory_units_) CheckMemoryUnitName();
   if (replicated_)
     LOG_INFO(kComp, "'%s': preferred allocation %s replicas (%s)", spec_.resource_name.c_str(),
@@ -280,6 +212,107 @@ void Plugin::BuildUnits() {
              : opts_.replica_policy != alloc::ReplicaPolicy::kAuto ? "--replica-policy"
              : memory_units_                                     ? "auto: memory units"
                                                                  : "auto: time-slice replicas");
+  BuildAdvertised();
+  if (hbm_grants_ && !opts_.memcap_host_path.empty()) BuildMemcapBytes();
+  pb::DeviceSpec kfd{"/dev/kfd", PathJoin(opts_.driver_root, "/dev/kfd"), "rw"};
+  std::string kb;
+  pb::Encode(kfd, &kb);
+  pb::PutLen(&kfd_spec_bytes_, 3, kb);
+  graph_ = alloc::DeviceGraph(*snap_, spec_.devices);
+  if (!replicated_ && units_.size() <= 8) {
+    // Anonymous zero pages: only the pages of entries actually used get memory.
+    void* p = mmap(nullptr, kBestEffortCacheBytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p != MAP_FAILED) best_effort_cache_.reset(static_cast<std::atomic<uint16_t>*>(p));
+  }
+  healthy_.assign(units_.size(), 1);
+  warned_law_.reset(new std::atomic<uint64_t>[units_.size()]());
+  RebuildListAndWatch();
+  // grpc-go clients -- the kubelet's device manager dials without raising it --
+  // refuse messages above 4 MiB, so a larger device list never reaches the
+  // kubelet and the resource stays at 0 allocatable.
+  constexpr size_t kKubeletMaxRecv = 4u << 20;
+  if (law_bytes_size_.load() + 5 > kKubeletMaxRecv)
+    LOG_ERROR(kComp, "'%s': the ListAndWatch device list is %zu bytes (%zu IDs), above the 4 MiB a kubelet's gRPC "
+              "client accepts; the kubelet will not see these devices. Lower the replica count (resource-config) "
+              "or raise the memory unit (--auto-replica-unit-mib)", spec_.resource_name.c_str(),
+              law_bytes_size_.load(), advertised_.size());
+}
+
+// One advertised device (a whole GPU or a partition) with everything Allocate
+// hands out for it encoded once.
+Unit Plugin::MakeUnit(const alloc::DeviceRef& ref) const {
+  const auto& v = spec_.variant;
+  const auto& g = snap_->gpus[ref.gpu];
+  Unit u;
+  u.gpu = ref.gpu;
+  if (ref.partition < 0) {
+    u.id = g.uuid;
+    u.index = std::to_string(g.node_index);
+    u.numa = g.numa;
+    u.vram_mib = g.vram_mib;
+    for (const auto& p : g.partitions) {
+      if (!p.render_path.empty()) u.paths.push_back(p.render_path);
+      if (!p.card_path.empty()) u.paths.push_back(p.card_path);
+      u.handles.push_back(p.handle);
+    }
+  } else {
+    const auto& p = g.partitions[ref.partition];
+    u.id = p.uuid;
+    u.index = std::to_string(g.node_index) + ":" + std::to_string(ref.partition);
+    u.numa = p.numa >= 0 ? p.numa : g.numa;
+    u.vram_mib = p.vram_mib;
+    if (!p.render_path.empty()) u.paths.push_back(p.render_path);
+    if (!p.card_path.empty()) u.paths.push_back(p.card_path);
+    u.handles.push_back(p.handle);
+  }
+  // Auto replicas: one per `auto_replica_unit_mib` of this device's own memory
+  // (server.go:100-103; per-partition memory fixes B4). At least one.
+  u.replicas = v.auto_replicas
+                   ? static_cast<unsigned>(std::max<uint64_t>(1, u.vram_mib / opts_.auto_replica_unit_mib))
+                   : std::max(1u, v.replicas);
+  if (hbm_grants_) u.grant_mib = memory_units_ ? opts_.auto_replica_unit_mib : u.vram_mib / u.replicas;
+  u.cus = ref.partition < 0 ? g.cus : g.partitions[ref.partition].cus;
+  u.xcds = ref.partition < 0 ? g.xcds : g.partitions[ref.partition].xcds;
+  if (memory_units_ && opts_.cu_slot_units) {
+    // One unit = one CU slot (one CU on every XCD) and that slot's share of
+    // the HBM: 32 units of 9,215 MiB on an SPX MI355X. Every grant is then a
+    // whole number of slots -- no slot is shared, none left idle.
+    const uint32_t per = u.xcds && u.cus % u.xcds == 0 ? u.cus / u.xcds : 0;
+    if (per >= 2 && u.vram_mib / per > 0) {
+      u.replicas = per;
+      u.grant_mib = u.vram_mib / per;
+    } else {
+      LOG_WARN(kComp, "device %s: %u CUs over %u XCDs give no CU slots; its memory units are %llu MiB",
+               u.id.c_str(), u.cus, u.xcds, static_cast<unsigned long long>(opts_.auto_replica_unit_mib));
+    }
+  }
+  if (opts_.replica_cu_mask && replicated_) {
+    u.replica_cus = memory_units_ ? MemoryUnitCuRanges(u.cus, u.xcds, u.replicas)
+                                  : ReplicaCuRanges(u.cus, u.xcds, u.replicas);
+    if (memory_units_ && opts_.whole_cu_slots && !u.replica_cus.empty()) {
+      u.slot_units.assign(u.cus / u.xcds, 0);
+      for (const auto& rg : u.replica_cus) ++u.slot_units[rg.first / u.xcds];
+    }
+    if (u.replica_cus.empty() && u.replicas > 1)
+      LOG_WARN(kComp, "device %s: %u CUs over %u XCDs cannot be split into %u CU shares; its replicas "
+               "share all CUs", u.id.c_str(), u.cus, u.xcds, u.replicas);
+  }
+  u.visible_id = opts_.id_strategy == DeviceIdStrategy::kIndex ? u.index : u.id;
+  for (const auto& path : u.paths) {
+    pb::DeviceSpec ds{path, PathJoin(opts_.driver_root, path), "rw"};
+    std::string b;
+    pb::Encode(ds, &b);
+    pb::PutLen(&u.spec_bytes, 3, b);
+  }
+  pb::Mount m{PathJoin(kVolumeMountRoot, u.visible_id), kVolumeMountHostPath, false};
+  std::string mb;
+  pb::Encode(m, &mb);
+  pb::PutLen(&u.mount_bytes, 2, mb);
+  return u;
+}
+
+// The advertised IDs: one per device, or its replicas' IDs (replicas.cc).
+void Plugin::BuildAdvertised() {
   for (size_t i = 0; i < units_.size(); ++i) {
     const auto& u = units_[i];
     unit_by_id_[u.id] = static_cast<int>(i);
@@ -308,43 +341,24 @@ void Plugin::BuildUnits() {
       LOG_WARN(kComp, "device ID '%s' exceeds 63 characters", advertised_[i].c_str());
     advertised_index_[advertised_[i]] = advertised_unit_[i];
   }
-  if (hbm_grants_ && !opts_.memcap_host_path.empty()) {
-    grant_dir_prefix_ = GrantDir();
-    if (grant_dir_prefix_.empty() || grant_dir_prefix_.back() != '/') grant_dir_prefix_ += '/';
-    pb::PutMapEntry(&memcap_bytes_, 1, "LD_PRELOAD", kMemcapContainerPath);
-    pb::Mount m{kMemcapContainerPath, opts_.memcap_host_path, true};
-    std::string mb;
-    pb::Encode(m, &mb);
-    pb::PutLen(&memcap_bytes_, 2, mb);
-    if (!opts_.memcap_preload_list.empty()) {
-      pb::Mount pl{"/etc/ld.so.preload", opts_.memcap_preload_list, true};
-      std::string pb_;
-      pb::Encode(pl, &pb_);
-      pb::PutLen(&memcap_bytes_, 2, pb_);
-    }
+}
+
+// What every memory-unit container of an --enforce-memory-units plugin gets:
+// the HBM-cap shim, preloaded (and pinned by /etc/ld.so.preload if asked).
+void Plugin::BuildMemcapBytes() {
+  grant_dir_prefix_ = GrantDir();
+  if (grant_dir_prefix_.empty() || grant_dir_prefix_.back() != '/') grant_dir_prefix_ += '/';
+  pb::PutMapEntry(&memcap_bytes_, 1, "LD_PRELOAD", kMemcapContainerPath);
+  pb::Mount m{kMemcapContainerPath, opts_.memcap_host_path, true};
+  std::string mb;
+  pb::Encode(m, &mb);
+  pb::PutLen(&memcap_bytes_, 2, mb);
+  if (!opts_.memcap_preload_list.empty()) {
+    pb::Mount pl{"/etc/ld.so.preload", opts_.memcap_preload_list, true};
+    std::string pb_;
+    pb::Encode(pl, &pb_);
+    pb::PutLen(&memcap_bytes_, 2, pb_);
   }
-  pb::DeviceSpec kfd{"/dev/kfd", PathJoin(opts_.driver_root, "/dev/kfd"), "rw"};
-  std::string kb;
-  pb::Encode(kfd, &kb);
-  pb::PutLen(&kfd_spec_bytes_, 3, kb);
-  graph_ = alloc::DeviceGraph(*snap_, spec_.devices);
-  if (!replicated_ && units_.size() <= 8) {
-    // Anonymous zero pages: only the pages of entries actually used get memory.
-    void* p = mmap(nullptr, kBestEffortCacheBytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (p != MAP_FAILED) best_effort_cache_.reset(static_cast<std::atomic<uint16_t>*>(p));
-  }
-  healthy_.assign(units_.size(), 1);
-  warned_law_.reset(new std::atomic<uint64_t>[units_.size()]());
-  RebuildListAndWatch();
-  // grpc-go clients -- the kubelet's device manager dials without raising it --
-  // refuse messages above 4 MiB, so a larger device list never reaches the
-  // kubelet and the resource stays at 0 allocatable.
-  constexpr size_t kKubeletMaxRecv = 4u << 20;
-  if (law_bytes_size_.load() + 5 > kKubeletMaxRecv)
-    LOG_ERROR(kComp, "'%s': the ListAndWatch device list is %zu bytes (%zu IDs), above the 4 MiB a kubelet's gRPC "
-              "client accepts; the kubelet will not see these devices. Lower the replica count (resource-config) "
-              "or raise the memory unit (--auto-replica-unit-mib)", spec_.resource_name.c_str(),
-              law_bytes_size_.load(), advertised_.size());
 }
 
 bool Plugin::UnitIsCuSlot(const Unit& u) const {

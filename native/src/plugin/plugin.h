@@ -288,6 +288,9 @@ class Plugin {
 
  private:
   void BuildUnits();
+  Unit MakeUnit(const alloc::DeviceRef& ref) const;
+  void BuildAdvertised();
+  void BuildMemcapBytes();
   Status PreferredImpl(std::string_view req, std::string* resp);
   std::vector<int> CachedBestEffort(const std::vector<int>& avail, const std::vector<int>& must, int size);
   void RebuildListAndWatch();
