@@ -1,0 +1,152 @@
+"""Real-MI355X check of the polled recovery across an event gap (round 5).
+
+A GPU whose GPU_POST_RESET was lost in an event gap comes back once amdsmi
+has answered every health poll -- liveness, VRAM usage and the SMU's activity
+metrics where they ever answered -- for --reset-recovery-hold-ms. On the mock
+(tests/test_health_persistence.py) the queries answer what the fixture says;
+here real libamd_smi answers them, in the three layouts a plugin runs in:
+
+* in-process: the plugin holds its own event registration (a new one per
+  monitor generation cannot receive what was sent before it: a gap);
+* denied: the plugin's device cgroup denies /dev/kfd and the render nodes
+  (libadp_devcgroup_sim.so), events are off (a gap) and the polled queries
+  are what an unprivileged pod can still ask;
+* relay: the chart's layout -- denied as above, events through the event
+  relay, which cannot replay what a fresh daemon missed (a gap).
+
+The GPU's earlier PRE_RESET is seeded in --health-state-file, as a plugin
+container restarted in the middle of a reset finds it. The same scenario runs
+on the amdsmi mock on CPU (in-process and relay layouts) so its mechanics stay
+pinned without a GPU. Parity: the reference never brings a GPU back
+(server.go:259, FIXME).
+"""
+
+import json
+import os
+import re
+import time
+
+import pytest
+
+from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+from k8s_gpu_sharing_plugin_amd.models import fixtures
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
+
+SIM = os.path.join(BUILD_DIR, "libadp_devcgroup_sim.so")
+OUT = "gpurun_out/r5"
+RESET_PENDING = 1 << 2  # health::kFailResetPending
+HOLD_MS = 2000
+
+
+@pytest.fixture(scope="module")
+def real_snap():
+    from k8s_gpu_sharing_plugin_amd.utils import native
+    s = native.snapshot()
+    assert s["gpus"], "libamd_smi enumerated no GPUs"
+    return s
+
+
+def _health(resp):
+    return {x.ID: x.health for x in resp.devices}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["in-process", "denied", "relay"])
+def test_reset_pending_gpu_recovers_by_polling_on_real_amdsmi(scratch, real_snap, tmp_path, layout):
+    rec = _scenario(scratch, tmp_path, layout, real_snap["gpus"][0], None)
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, f"polled_recovery_{layout}.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+
+
+@pytest.mark.parametrize("layout", ["in-process", "relay"])
+def test_reset_pending_gpu_recovers_by_polling_on_the_mock(scratch, tmp_path, layout):
+    fx = fixtures.node(1)
+    _scenario(scratch, tmp_path, layout, fx["gpus"][0], fx)
+
+
+def _scenario(scratch, tmp_path, layout, g, fixture):
+    """Seed GPU g reset-pending, start the plugin in `layout`, and check that
+    polling (and nothing else) brings it back after HOLD_MS; returns the record."""
+    from test_metrics import _get, _parse
+    from test_metrics_exposition import check_exposition
+    real = fixture is None
+    key = g["uuid"] or g["bdf"]
+    state = tmp_path / "health.state"
+    state.write_text(f"adp-health v1\n{key}\t-\t0\t{RESET_PENDING}\tGPU_PRE_RESET: seeded by the test\n")
+    env = {"DP_HEALTH_POLL_MS": "200"}
+    if layout != "in-process" and real:  # the mock opens no device node
+        env["LD_PRELOAD"] = " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), SIM) if x)
+    relay = None
+    sock = str(tmp_path / "events.sock")
+    if layout == "relay":
+        rdir = scratch + "-relay"
+        os.makedirs(rdir, exist_ok=True)
+        relay = harness.Daemon(rdir, fixture, real_smi=real,
+                               args=["--event-relay", "--health-event-socket", sock]).start()
+        relay.wait_log("relaying amdsmi events on", 30)
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = None
+    c = None
+    try:
+        args = ["--devices", "0", "--health-state-file", str(state), "--metrics-addr", "127.0.0.1:0",
+                "--reset-recovery-hold-ms", str(HOLD_MS)]
+        if relay:
+            args += ["--health-event-socket", sock]
+        t0 = time.monotonic()
+        d = harness.Daemon(scratch, fixture, real_smi=real, args=args, env=env).start()
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics", 30)).group(1))
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        q, call = c.watch()
+        first = _health(q.get(timeout=10))
+        d.wait_log("waits for GPU_POST_RESET across an event gap", 30)
+        text_waiting = _get(port, "/metrics")[1]
+        check_exposition(text_waiting)  # real amdsmi's values (product names, ...) parse too
+        waiting = _parse(text_waiting)
+        log = d.wait_log("recovered without GPU_POST_RESET", 30)
+        t_recovered = time.monotonic() - t0
+        deadline = time.monotonic() + 10
+        law = first
+        while any(h != "Healthy" for h in law.values()) and time.monotonic() < deadline:
+            law = _health(q.get(timeout=max(0.05, deadline - time.monotonic())))
+        call.cancel()
+        text = _get(port, "/metrics")[1]
+        families = check_exposition(text)
+        m = _parse(text)
+
+        def get(samples, name, **labels):
+            want = set(labels.items())
+            hits = [v for (n, ls), v in samples.items() if n == name and want <= set(ls)]
+            return hits[0] if len(hits) == 1 else None
+        lines = [ln for ln in log.splitlines()
+                 if any(s in ln for s in ("event gap", "recovered without", "events off", "stays unhealthy",
+                                          "events on", "health poll #1", "relay"))]
+        record = {
+            "layout": layout, "bdf": g["bdf"], "hold_ms": HOLD_MS,
+            "first_law": first, "law_after": law, "seconds_to_recovery_from_start": round(t_recovered, 2),
+            "awaiting_before": get(waiting, "amdgpu_dp_gpu_awaiting_polled_recovery", bdf=g["bdf"]),
+            "awaiting_after": get(m, "amdgpu_dp_gpu_awaiting_polled_recovery", bdf=g["bdf"]),
+            "recovered_total": get(m, "amdgpu_dp_gpu_recovered_without_event_total", bdf=g["bdf"]),
+            "event_gaps_total": get(m, "amdgpu_dp_health_event_gaps_total"),
+            "hbm_used_bytes": get(m, "amdgpu_dp_gpu_hbm_used_bytes", bdf=g["bdf"]),
+            "state_after": state.read_text().splitlines(),
+            "metric_families": len(families),
+            "log": lines[-20:],
+        }
+        assert all(h == "Unhealthy" for h in first.values()), record
+        assert record["awaiting_before"] == 1 and record["awaiting_after"] == 0, record
+        assert all(h == "Healthy" for h in law.values()), record
+        assert record["recovered_total"] == 1 and record["event_gaps_total"] >= 1, record
+        assert t_recovered >= HOLD_MS / 1000, record
+        assert "waits for GPU_POST_RESET across an event gap" in log, record
+        assert all(ln.split("\t")[3] == "0" for ln in record["state_after"][1:]), record
+        return record
+    finally:
+        if c:
+            c.close()
+        if d:
+            assert d.stop() == 0
+        k.stop()
+        if relay:
+            assert relay.stop() == 0
