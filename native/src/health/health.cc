@@ -261,6 +261,9 @@ void Monitor::RelayConnect() {
   }
   relay_buf_.clear();
   relay_synced_ = false;
+  relay_cursor_sent_ = cur.valid;
+  relay_connected_ms_ = NowMs();
+  relay_overdue_ = false;
   events_reason_ = "waiting for the event relay's hello";
 }
 
@@ -300,8 +303,9 @@ void Monitor::RelayWait(int ms) {
       if (!events_ok_) {
         MarkGap("the event relay reports events off (" + l.reason + ")", false);
       } else if (l.gap != 0) {
-        MarkGap(l.gap == 1 ? "the event relay renewed its registration or no longer holds the events missed"
-                           : "the event relay cannot replay missed events (an older relay)",
+        MarkGap(l.gap != 1             ? "the event relay cannot replay missed events (an older relay)"
+                : !relay_cursor_sent_ ? "a first connection to the event relay: what was sent before it is unknown"
+                                      : "the event relay renewed its registration or no longer holds the events missed",
                 false);
       } else {
         for (const auto& key : ledger_->CancelTentativeGaps())
@@ -624,6 +628,15 @@ void Monitor::Run() {
       }
       if (relay_fd_ >= 0) RelayWait(slice);
       else Sleep(slice);
+      // A relay that accepted the reinit but never answers it (its registrar
+      // stuck in amdsmi): events cannot be trusted to arrive.
+      if (relay_fd_ >= 0 && !relay_synced_ && !relay_overdue_ &&
+          NowMs() - relay_connected_ms_ > cfg_.event_fail_ms) {
+        relay_overdue_ = true;
+        LOG_WARN(kComp, "the event relay has not answered this daemon's reinit for %d ms; polling only until it does",
+                 cfg_.event_fail_ms);
+        MarkGap("the event relay did not answer", false);
+      }
     } else if (events_ok_) {
       events.clear();
       Status st = lib_->EventsWait(slice, &events);

@@ -320,6 +320,9 @@ class Monitor {
   int relay_fd_ = -1;
   std::string relay_buf_;
   bool relay_synced_ = false;  // the relay answered this connection's "reinit"
+  bool relay_cursor_sent_ = false;  // the reinit named where this daemon was in the relay's events
+  int64_t relay_connected_ms_ = 0;  // when this connection's reinit was sent
+  bool relay_overdue_ = false;      // no answer for event_fail_ms: counted as a gap
   int64_t relay_tried_ms_ = -1000000;
   std::string fingerprint_;  // ProcessorFingerprint of the snapshot, sent with "reinit"
   // In-process event waits that keep failing: since when, how many, and

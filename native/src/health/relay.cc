@@ -270,6 +270,9 @@ class Registration {
     registrar_ = std::thread([this] {
       Renew(false);
       RegistrarLoop();
+      std::lock_guard<std::mutex> lk(req_mu_);
+      registrar_exited_ = true;
+      req_cv_.notify_all();
     });
   }
   // A daemon (client `id`) subscribed with its fingerprint ("" = none given).
@@ -283,11 +286,22 @@ class Registration {
   // Returns false when the waiter is stuck in amdsmi: it is left running and
   // this object must outlive it (the process is about to exit).
   bool Shutdown() {
+    bool exited;
     {
-      std::lock_guard<std::mutex> lk(req_mu_);
+      std::unique_lock<std::mutex> lk(req_mu_);
       req_stop_ = true;
+      req_cv_.notify_all();
+      // A renewal stopping a waiter that is stuck in amdsmi never ends: exit
+      // without it rather than hang the container's shutdown.
+      exited = !registrar_.joinable() ||
+               req_cv_.wait_for(lk, std::chrono::milliseconds(stuck_ms_ + slice_ms_ + 1000),
+                                [&] { return registrar_exited_; });
     }
-    req_cv_.notify_all();
+    if (!exited) {
+      LOG_WARN(kComp, "exiting with a registration renewal stuck in amdsmi");
+      registrar_.detach();
+      return false;
+    }
     if (registrar_.joinable()) registrar_.join();
     if (Hung()) {
       LOG_WARN(kComp, "exiting with the event wait still stuck");
@@ -398,6 +412,7 @@ class Registration {
   std::condition_variable req_cv_;
   std::deque<std::pair<uint64_t, std::string>> requests_;
   bool req_stop_ = false;
+  bool registrar_exited_ = false;
 };
 
 }  // namespace
@@ -673,6 +688,9 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     c.gap = gap;
     LOG_INFO(kComp, "daemon connected for events (%s)",
              rq.has_since ? (gap ? "it may have missed events" : "nothing missed") : "a new daemon");
+    // The watchdog's events=off stands whatever the registrar answers (and a
+    // registrar renewing under a stuck wait may never answer): say so now.
+    if (stuck) send_to(c, hello(true, 1));
     reg->Request(c.id, std::move(rq.fp));
   };
   int exit_code = 0;

@@ -631,3 +631,81 @@ def test_a_restarted_plugin_container_resumes_the_relays_stream(scratch):
         assert "across an event gap" not in n.d.log()
     finally:
         n.stop()
+
+
+def test_relay_exits_with_a_renewal_stuck_in_amdsmi(scratch):
+    """A daemon's reinit starts a renewal just as the amdsmi event wait hangs:
+    the renewal waits for the waiter, which does not return. SIGTERM then ends
+    the relay after its watchdog's threshold (plus a second), not when amdsmi
+    lets go: a container that would not stop is killed by the kubelet only
+    after the grace period, with the node's events off all that time."""
+    import socket
+    n = RelayNode(scratch, relay_env={"ADP_RELAY_STUCK_MS": "1500"})
+    try:
+        n.d.wait_log("events on through the relay")
+        n.inject("hang 8000")
+        time.sleep(0.3)  # the waiter has taken the hang
+        c = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        c.settimeout(5)
+        c.connect(n.sock)
+        assert c.recv(4096).startswith(b"hello v1 ")
+        c.sendall(b"reinit fp=0000000000000000\n")  # processors the registration does not have
+        n.relay.wait_log("re-enumerating (a daemon asked")
+        t0 = time.time()
+        n.relay.signal(signal.SIGTERM)
+        rc = n.relay.proc.wait(timeout=10)
+        took = time.time() - t0
+        c.close()
+        assert rc == 0, rc
+        log = n.relay.log()
+        assert "exiting with a registration renewal stuck in amdsmi" in log, log[-3000:]
+        assert took < 5.0, took  # 1.5 s watchdog + 1 s, not the 8 s hang
+    finally:
+        n.stop()
+
+
+def test_a_relay_that_never_answers_the_reinit_is_a_gap(scratch, tmp_path):
+    """A relay that greets but never answers the daemon's reinit (its
+    registrar stuck): after ADP_EVENT_FAIL_MS the daemon polls, records an
+    event gap, and a GPU that was waiting for GPU_POST_RESET recovers by the
+    polled check."""
+    import socket
+    import threading
+    sock = str(tmp_path / "mute.sock")
+    srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    srv.bind(sock)
+    srv.listen(4)
+    conns = []
+    stop = threading.Event()
+
+    def serve():
+        srv.settimeout(0.2)
+        while not stop.is_set():
+            try:
+                conn, _ = srv.accept()
+            except OSError:
+                continue
+            conn.sendall(b"hello v1 events=ok processors=2 relay=00ab gen=1 seq=0 fp=- renew_ms=1\n")
+            conns.append(conn)  # read nothing, answer nothing
+    t = threading.Thread(target=serve, daemon=True)
+    t.start()
+    fx = fixtures.node(2)
+    state = tmp_path / "health.state"
+    state.write_text(f"adp-health v1\n{fx['gpus'][1]['uuid']}\t-\t0\t4\tGPU_PRE_RESET: seeded\n")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fx, args=["--health-event-socket", sock, "--health-state-file", str(state),
+                                          "--reset-recovery-hold-ms", "500"],
+                       env={"DP_HEALTH_POLL_MS": "100", "ADP_EVENT_FAIL_MS": "700"}).start()
+    try:
+        log = d.wait_log("has not answered this daemon's reinit for 700 ms")
+        assert "events on through the relay" not in log
+        log = d.wait_log("recovered without GPU_POST_RESET", timeout=10)
+        assert "no GPU_POST_RESET after an event gap (the event relay did not answer)" in log, log[-3000:]
+    finally:
+        d.stop()
+        k.stop()
+        stop.set()
+        t.join(5)
+        for c in conns:
+            c.close()
+        srv.close()

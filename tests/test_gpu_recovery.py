@@ -140,6 +140,8 @@ def _scenario(scratch, tmp_path, layout, g, fixture):
         assert record["recovered_total"] == 1 and record["event_gaps_total"] >= 1, record
         assert t_recovered >= HOLD_MS / 1000, record
         assert "waits for GPU_POST_RESET across an event gap" in log, record
+        if layout == "relay":  # a fresh daemon: no cursor, so nothing says what it missed
+            assert "a first connection to the event relay" in log, record
         assert all(ln.split("\t")[3] == "0" for ln in record["state_after"][1:]), record
         return record
     finally:
