@@ -270,9 +270,7 @@ class Registration {
     registrar_ = std::thread([this] {
       Renew(false);
       RegistrarLoop();
-      std::lock_guard<std::mutex> lk(req_mu_);
-      registrar_exited_ = true;
-      req_cv_.notify_all();
+      registrar_exited_.store(true);
     });
   }
   // A daemon (client `id`) subscribed with its fingerprint ("" = none given).
@@ -286,18 +284,17 @@ class Registration {
   // Returns false when the waiter is stuck in amdsmi: it is left running and
   // this object must outlive it (the process is about to exit).
   bool Shutdown() {
-    bool exited;
     {
-      std::unique_lock<std::mutex> lk(req_mu_);
+      std::lock_guard<std::mutex> lk(req_mu_);
       req_stop_ = true;
-      req_cv_.notify_all();
-      // A renewal stopping a waiter that is stuck in amdsmi never ends: exit
-      // without it rather than hang the container's shutdown.
-      exited = !registrar_.joinable() ||
-               req_cv_.wait_for(lk, std::chrono::milliseconds(stuck_ms_ + slice_ms_ + 1000),
-                                [&] { return registrar_exited_; });
     }
-    if (!exited) {
+    req_cv_.notify_all();
+    // A renewal stopping a waiter that is stuck in amdsmi never ends: exit
+    // without it rather than hang the container's shutdown. (Polled: no timed
+    // condition-variable wait, which this toolchain's TSan cannot follow.)
+    const int64_t deadline = NowMs() + stuck_ms_ + slice_ms_ + 1000;
+    while (registrar_.joinable() && !registrar_exited_.load() && NowMs() < deadline) usleep(10000);
+    if (registrar_.joinable() && !registrar_exited_.load()) {
       LOG_WARN(kComp, "exiting with a registration renewal stuck in amdsmi");
       registrar_.detach();
       return false;
@@ -412,8 +409,12 @@ class Registration {
   std::condition_variable req_cv_;
   std::deque<std::pair<uint64_t, std::string>> requests_;
   bool req_stop_ = false;
-  bool registrar_exited_ = false;
+  std::atomic<bool> registrar_exited_{false};
 };
+
+// A Registration a stuck thread still uses at exit: deliberately kept, and
+// reachable (not a leak to LeakSanitizer).
+Registration* volatile g_abandoned = nullptr;
 
 }  // namespace
 
@@ -830,7 +831,11 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     delete reg;
     close(ev_pipe[1]);
     close(done_pipe[1]);
-  }  // else a waiter stuck in amdsmi still holds it and the pipe's write end; the process exits next
+  } else {
+    // A thread stuck in amdsmi still uses it and the pipes' write ends; the
+    // process exits next.
+    g_abandoned = reg;
+  }
   for (auto& c : clients)
     if (c.fd >= 0) close(c.fd);
   for (int fd : {ev_pipe[0], done_pipe[0], lfd}) close(fd);
