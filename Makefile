@@ -78,7 +78,7 @@ tsan-e2e:
 	ninja -C build/tsan -j$(JOBS) amdgpu-device-plugin amdgpu-dp-kubelet amdsmi_mock
 	rm -rf build/tsan-logs && mkdir -p build/tsan-logs
 	ADP_BUILD_DIR=$(CURDIR)/build/tsan TSAN_OPTIONS=log_path=$(CURDIR)/build/tsan-logs/daemon \
-	  $(PY) -m pytest -q -p no:cacheprovider tests/test_e2e_mock.py tests/test_health.py \
+	  $(PY) -m pytest -q -p no:cacheprovider -m "not gpu" tests/test_e2e_mock.py tests/test_health.py \
 	  tests/test_metrics.py tests/test_lifecycle.py tests/test_robustness.py tests/test_h2_native.py \
 	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py tests/test_preferred.py \
 	  tests/test_event_relay.py tests/test_policy_units.py tests/test_hip_order.py tests/test_kfd_topology.py tests/test_chart_layout.py \
@@ -112,7 +112,7 @@ asan-e2e:
 	rm -rf build/asan-logs && mkdir -p build/asan-logs
 	ADP_BUILD_DIR=$(CURDIR)/build/asan ASAN_OPTIONS=log_path=$(CURDIR)/build/asan-logs/daemon:detect_leaks=1:verify_asan_link_order=0 \
 	  UBSAN_OPTIONS=print_stacktrace=1:log_path=$(CURDIR)/build/asan-logs/ubsan \
-	  $(PY) -m pytest -q -p no:cacheprovider tests/test_e2e_mock.py tests/test_health.py \
+	  $(PY) -m pytest -q -p no:cacheprovider -m "not gpu" tests/test_e2e_mock.py tests/test_health.py \
 	  tests/test_metrics.py tests/test_lifecycle.py tests/test_robustness.py tests/test_h2_native.py \
 	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py tests/test_preferred.py \
 	  tests/test_event_relay.py tests/test_policy_units.py tests/test_hip_order.py tests/test_kfd_topology.py tests/test_chart_layout.py \
