@@ -18,8 +18,12 @@ runs `amdgpu-device-plugin --list-grants` (the accounting files of
 --enforce-memory-units with /metrics under <device-plugin dir>/amdgpu-dp/usage)
 and prints a table; `doctor` runs `amdgpu-device-plugin --doctor` (exit 1 on a
 failure); `status` reads a running daemon's /metrics (default
-http://127.0.0.1:9400/metrics) and prints its resources, device health, RPC
-counts with the loops' residency, and the containers' HBM against their grants.
+http://127.0.0.1:9400/metrics) and prints its resources, device health (why a
+GPU is out of service, whether it awaits the polled recovery after an event
+gap), what one memory unit is, RPC counts with the loops' residency, and the
+containers' HBM against their grants; exit 1 on an Unhealthy device, a
+container over its grant, or IDs running pods hold that are no longer
+advertised.
 """
 
 import json
@@ -165,13 +169,34 @@ def _status(args) -> int:
         failures = scalar("amdgpu_dp_driver_hbm_scan_failures_total") or 0
         secs = scalar("amdgpu_dp_driver_hbm_scan_seconds") or 0
         line += f"; driver-side scans {int(polls)} (last {secs * 1e3:.2f} ms, {int(failures)} failed)"
+    gaps = scalar("amdgpu_dp_health_event_gaps_total")
+    if gaps:
+        line += f"; {int(gaps)} event gap(s)"
+    recovered = sum(v for _, v in by("amdgpu_dp_gpu_recovered_without_event_total"))
+    if recovered:
+        line += f", {int(recovered)} GPU(s) recovered without GPU_POST_RESET"
     print(line)
+    # memory-unit resources: what one unit is (a pod asking for N gets N x this)
+    units = {}
+    for ls, v in by("amdgpu_dp_memory_unit_mib"):
+        units.setdefault(ls.get("resource"), set()).add((int(v), ls.get("kind")))
+    for res, us in sorted(units.items()):
+        sizes = sorted(us)
+        size = (f"{sizes[0][0]} MiB" if len(sizes) == 1 else
+                f"{sizes[0][0]}..{sizes[-1][0]} MiB")
+        print(f"{res}: one unit = {size} ({', '.join(sorted({k for _, k in sizes}))})")
+    stale = [(ls.get("resource"), v) for ls, v in by("amdgpu_dp_stale_allocated_ids") if v]
+    for res, v in stale:
+        print(f"STALE {res}: {int(v)} ID(s) running pods hold are no longer advertised (the layout changed "
+              "under them: drain the node)")
+    awaiting = {ls.get("bdf") for ls, v in by("amdgpu_dp_gpu_awaiting_polled_recovery") if v}
     causes = {}
     for ls, v in by("amdgpu_dp_gpu_failure"):
         if v:
             causes.setdefault(ls.get("bdf"), []).append(ls.get("cause"))
     for bdf, cs in sorted(causes.items()):
-        print(f"GPU {bdf}: " + ", ".join(sorted(cs)))
+        print(f"GPU {bdf}: " + ", ".join(sorted(cs)) +
+              (" (awaiting polled recovery after an event gap)" if bdf in awaiting else ""))
     bad = [ls for ls, v in by("amdgpu_dp_device_healthy") if v == 0]
     for ls in bad:
         print(f"UNHEALTHY {ls.get('resource')} {ls.get('device')} (index {ls.get('index')})")
@@ -188,7 +213,7 @@ def _status(args) -> int:
     over = [ls for ls, v in by("amdgpu_dp_container_hbm_over_grant") if v]
     for ls in over:
         print(f"OVER GRANT {ls.get('namespace')}/{ls.get('pod')}/{ls.get('container')} on {ls.get('bdf')}")
-    return 1 if bad or over else 0
+    return 1 if bad or over or stale else 0
 
 
 def main(argv=None) -> int:

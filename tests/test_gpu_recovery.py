@@ -24,6 +24,8 @@ pinned without a GPU. Parity: the reference never brings a GPU back
 import json
 import os
 import re
+import subprocess
+import sys
 import time
 
 import pytest
@@ -104,6 +106,8 @@ def _scenario(scratch, tmp_path, layout, g, fixture):
         text_waiting = _get(port, "/metrics")[1]
         check_exposition(text_waiting)  # real amdsmi's values (product names, ...) parse too
         waiting = _parse(text_waiting)
+        st = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "status",
+                             f"http://127.0.0.1:{port}/metrics"], capture_output=True, text=True, timeout=60)
         log = d.wait_log("recovered without GPU_POST_RESET", 30)
         t_recovered = time.monotonic() - t0
         deadline = time.monotonic() + 10
@@ -136,6 +140,9 @@ def _scenario(scratch, tmp_path, layout, g, fixture):
         }
         assert all(h == "Unhealthy" for h in first.values()), record
         assert record["awaiting_before"] == 1 and record["awaiting_after"] == 0, record
+        # the status CLI names the cause and the pending recovery, and fails
+        assert st.returncode == 1, st.stdout + st.stderr
+        assert f"GPU {g['bdf']}: reset_pending (awaiting polled recovery after an event gap)" in st.stdout, st.stdout
         assert all(h == "Healthy" for h in law.values()), record
         assert record["recovered_total"] == 1 and record["event_gaps_total"] >= 1, record
         assert t_recovered >= HOLD_MS / 1000, record

@@ -18,6 +18,8 @@ these checks; the chart default it is compared with is
 
 import os
 import re
+import subprocess
+import sys
 import time
 
 from k8s_gpu_sharing_plugin_amd.models import fixtures
@@ -125,6 +127,12 @@ def test_changing_the_unit_under_live_grants_is_an_error(scratch):
         s = _parse(_get(port, "/metrics")[1])
         assert _value(s, "amdgpu_dp_replica_layout_changes_with_live_allocations_total", resource=res) == 1
         assert _value(s, "amdgpu_dp_stale_allocated_ids", resource=res) == 2  # replicas 100, 101 are gone
+        # the status CLI says so, with what one unit now is, and fails
+        st = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "status",
+                             f"http://127.0.0.1:{port}/metrics"], capture_output=True, text=True, timeout=60)
+        assert st.returncode == 1, st.stdout + st.stderr
+        assert f"STALE {res}: 2 ID(s) running pods hold are no longer advertised" in st.stdout, st.stdout
+        assert re.search(rf"^{res}: one unit = \d+ MiB \(cu-slot\)$", st.stdout, re.M), st.stdout
         # no pod holds IDs any more: a change back is only noted
         pr.payload = _list_response([])
         _config(cfg, "mib")
