@@ -24,7 +24,7 @@ import subprocess
 import pytest
 
 from k8s_gpu_sharing_plugin_amd.models import fixtures
-from k8s_gpu_sharing_plugin_amd.utils import harness, image, kubelet
+from k8s_gpu_sharing_plugin_amd.utils import image, kubelet
 
 
 def _can_unshare():

@@ -7,7 +7,7 @@ allocated again, 2 GiB more past a 4000 MiB grant are refused, and 200 rounds
 of 512 MiB allocate/free all succeed. One JSON line; run with the shim
 preloaded and a grant (tests/test_gpu.py::test_memcap_with_pytorch_allocator_configs).
 """
-import json, os, sys, torch
+import json, os, torch
 torch.cuda.init()
 res = {"backend": torch.cuda.get_allocator_backend(), "conf": os.environ.get("PYTORCH_CUDA_ALLOC_CONF", "")}
 free, total = torch.cuda.mem_get_info()
