@@ -27,6 +27,12 @@ int64_t NowMs() {
       .count();
 }
 
+// For what is persisted (the reset history): a steady clock restarts with the node.
+int64_t WallMs() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
 const char* EventName(uint32_t t) {
   switch (t) {
     case 1: return "VMFAULT";
@@ -416,7 +422,7 @@ void Monitor::PollOnce() {
     if (fail & kFailFlapping) {
       // Quarantine ends after a whole window without a GPU_PRE_RESET (or with
       // damping turned off).
-      const int64_t now = NowMs();
+      const int64_t now = WallMs();
       const int64_t quiet = now - ledger_->LastReset(keys_[g.index], now);
       if (cfg_.reset_flap_limit <= 0 || quiet >= cfg_.reset_flap_window_ms)
         Update(g.index, 0, kFailFlapping,
@@ -596,7 +602,7 @@ void Monitor::HandleEvent(const smi::Event& e) {
       // A new reset: only a gap after it lets polling end the wait.
       ledger_->ClearGap(keys_[gpu]);
       if (cfg_.reset_flap_limit > 0) {
-        int n = ledger_->RecordReset(keys_[gpu], NowMs(), cfg_.reset_flap_window_ms);
+        int n = ledger_->RecordReset(keys_[gpu], WallMs(), cfg_.reset_flap_window_ms);
         if (n >= cfg_.reset_flap_limit && !(fail_[gpu] & kFailFlapping)) {
           std::string w = std::to_string(cfg_.reset_flap_window_ms / 1000);
           LOG_WARN(kComp, "GPU %s reset %d times within %s s: quarantined until %s s pass without a reset",

@@ -127,6 +127,10 @@ struct GpuRecord {
   uint64_t ecc_seen = 0;      // highest count observed since; a lower count means a counter reset
   uint32_t fail = 0;
   std::string reason;  // last failure reason (empty when healthy)
+  // GPU_PRE_RESETs within the flap window (wall clock, ms since the epoch):
+  // kept with the verdict, so a plugin container restart does not reset the
+  // count or shorten a quarantine.
+  std::vector<int64_t> resets;
 };
 
 // Liveness of the health machinery itself, shared by all Monitor generations
@@ -238,7 +242,8 @@ class Ledger {
   void Reload();
   // File format, exposed for tests: "adp-health v1" header, then one
   // tab-separated line per GPU: key, ecc baseline ("-" = none), highest ECC
-  // count seen, fail bits, reason.
+  // count seen, fail bits, reason, and -- when there are any -- the recent
+  // resets as "resets=<ms>,<ms>,..." (a field older versions ignore).
   static std::string Serialize(const std::map<std::string, GpuRecord>& m);
   static std::map<std::string, GpuRecord> Parse(const std::string& body);
 
@@ -249,11 +254,12 @@ class Ledger {
   void ClearGap(const std::string& key);
   bool Gap(const std::string& key, GapMark* out) const;
   void SetResponsiveSince(const std::string& key, int64_t ms);
-  // Reset history for flap damping (in memory; steady clock): records a
-  // GPU_PRE_RESET at `now_ms` and returns how many fall within `window_ms`.
+  // Reset history for flap damping (GpuRecord::resets; wall clock, so it
+  // survives a restart): records a GPU_PRE_RESET at `now_ms` and returns how
+  // many fall within `window_ms`.
   int RecordReset(const std::string& key, int64_t now_ms, int64_t window_ms);
-  // The last recorded reset (0 = none known; then `now_ms` is recorded, so a
-  // quarantine loaded from the state file lasts one more window).
+  // The last recorded reset (none known, e.g. a state file from an older
+  // version: `now_ms` is recorded, so its quarantine lasts one more window).
   int64_t LastReset(const std::string& key, int64_t now_ms);
 
  private:
@@ -261,7 +267,6 @@ class Ledger {
   mutable std::mutex mu_;
   std::map<std::string, GpuRecord> recs_;
   std::map<std::string, GapMark> gaps_;
-  std::map<std::string, std::vector<int64_t>> resets_;
   std::string path_;
 };
 

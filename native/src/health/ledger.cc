@@ -63,7 +63,12 @@ std::string Ledger::Serialize(const std::map<std::string, GpuRecord>& m) {
     for (auto& c : reason)
       if (c == '\t' || c == '\n' || c == '\r') c = ' ';
     out += k + "\t" + (r.has_baseline ? std::to_string(r.ecc_baseline) : "-") + "\t" +
-           std::to_string(r.ecc_seen) + "\t" + std::to_string(r.fail) + "\t" + reason + "\n";
+           std::to_string(r.ecc_seen) + "\t" + std::to_string(r.fail) + "\t" + reason;
+    if (!r.resets.empty()) {
+      out += "\tresets=";
+      for (size_t i = 0; i < r.resets.size(); ++i) out += (i ? "," : "") + std::to_string(r.resets[i]);
+    }
+    out += "\n";
   }
   return out;
 }
@@ -105,6 +110,17 @@ std::map<std::string, GpuRecord> Ledger::Parse(const std::string& body) {
     r.fail = static_cast<uint32_t>(*fail) &
              (kFailEcc | kFailUnresponsive | kFailResetPending | kFailEvent | kFailRetiredPages | kFailFlapping);
     if (f.size() > 4) r.reason = f[4];
+    if (f.size() > 5 && f[5].rfind("resets=", 0) == 0) {
+      for (const auto& t : Split(std::string_view(f[5]).substr(7), ',')) {
+        auto v = ParseUint(t);
+        if (!v || r.resets.size() >= 64) {
+          LOG_WARN(kComp, "health state: reset history of %s malformed; ignored", f[0].c_str());
+          r.resets.clear();
+          break;
+        }
+        r.resets.push_back(static_cast<int64_t>(*v));
+      }
+    }
     out[f[0]] = std::move(r);
   }
   return out;
@@ -127,7 +143,11 @@ void Ledger::Put(const std::string& key, const GpuRecord& r) {
   if (it != recs_.end() && it->second.has_baseline == r.has_baseline && it->second.ecc_baseline == r.ecc_baseline &&
       it->second.ecc_seen == r.ecc_seen && it->second.fail == r.fail && it->second.reason == r.reason)
     return;
+  // The reset history is the ledger's own (RecordReset): a record read
+  // earlier does not roll it back.
+  std::vector<int64_t> resets = it != recs_.end() ? std::move(it->second.resets) : std::vector<int64_t>{};
   recs_[key] = r;
+  recs_[key].resets = std::move(resets);
   SaveLocked();
 }
 
@@ -189,17 +209,21 @@ bool Ledger::Gap(const std::string& key, GapMark* out) const {
 
 int Ledger::RecordReset(const std::string& key, int64_t now_ms, int64_t window_ms) {
   std::lock_guard<std::mutex> lk(mu_);
-  auto& v = resets_[key];
+  auto& v = recs_[key].resets;
   v.push_back(now_ms);
   v.erase(std::remove_if(v.begin(), v.end(), [&](int64_t t) { return now_ms - t >= window_ms; }), v.end());
+  SaveLocked();
   return static_cast<int>(v.size());
 }
 
 int64_t Ledger::LastReset(const std::string& key, int64_t now_ms) {
   std::lock_guard<std::mutex> lk(mu_);
-  auto& v = resets_[key];
-  if (v.empty()) v.push_back(now_ms);
-  return v.back();
+  auto& v = recs_[key].resets;
+  if (v.empty()) {
+    v.push_back(now_ms);
+    SaveLocked();
+  }
+  return *std::max_element(v.begin(), v.end());
 }
 
 void Ledger::SetResponsiveSince(const std::string& key, int64_t ms) {

@@ -217,6 +217,19 @@ static void TestLedgerGaps() {
   // the flapping bit survives the state file; drained never does (the drain file is its source)
   auto parsed = health::Ledger::Parse("adp-health v1\nf\t-\t0\t96\tx\n");
   CHECK(parsed["f"].fail == health::kFailFlapping);
+  // the reset history is written with the verdicts and read back; a record
+  // Put() from an earlier Get() does not roll it back
+  health::GpuRecord before = l.Get("d");
+  l.Put("d", before);
+  CHECK(l.Get("d").resets == std::vector<int64_t>({1200, 1600}));
+  std::string body = health::Ledger::Serialize(l.All());
+  CHECK(body.find("\nd\t-\t0\t0\t\tresets=1200,1600\n") != std::string::npos);
+  auto back = health::Ledger::Parse(body);
+  CHECK(back["d"].resets == std::vector<int64_t>({1200, 1600}) && back["c"].resets.empty());
+  // an older file (no field) and a malformed field: no history, the line kept
+  CHECK(health::Ledger::Parse("adp-health v1\ng\t-\t0\t64\tx\tresets=1,y\n")["g"].fail == health::kFailFlapping);
+  CHECK(health::Ledger::Parse("adp-health v1\ng\t-\t0\t64\tx\tresets=1,y\n")["g"].resets.empty());
+  CHECK(health::Ledger::Parse("adp-health v1\ng\t-\t0\t64\tx\tfuture=1\n")["g"].resets.empty());
 }
 
 static void TestRemoveDrainNames() {

@@ -585,6 +585,39 @@ def test_a_flapping_gpu_is_quarantined_until_a_quiet_window(mk):
     assert "quarantine over" in n.d.log()
 
 
+def test_the_reset_history_survives_a_container_restart(mk):
+    """With --health-state-file the resets counted for flap damping are kept
+    with the verdicts (wall clock): two resets, a plugin container restart,
+    and the third reset within the window quarantines the GPU -- a restart
+    neither resets the count nor ends a quarantine early."""
+    import tempfile
+    state = os.path.join(tempfile.mkdtemp(prefix="adp-flap-"), "health.state")
+
+    def make():
+        return mk(args=["--reset-flap-limit", "3", "--reset-flap-window-ms", "60000", "--health-state-file", state])
+    n = make()
+    ids = sorted(n.start())
+    for i in range(2):
+        n.inject(f"1 3 pre {i}")
+        n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+        n.inject(f"1 4 post {i}")
+        n.wait_health(lambda h: h[ids[1]] == "Healthy")
+    line = [ln for ln in open(state).read().splitlines() if ln.startswith(n.fx["gpus"][1]["uuid"])][0]
+    assert len(line.split("\t")[5].split("=")[1].split(",")) == 2, line
+    assert n.close() == 0
+    n = make()  # a new process, the same state file
+    assert n.start() == {ids[0]: "Healthy", ids[1]: "Healthy"}
+    n.inject("1 3 pre 2")
+    assert "reset 3 times within 60 s: quarantined" in n.d.wait_log("quarantined")
+    n.inject("1 4 post 2")
+    n.d.wait_log("post 2")
+    assert n.close() == 0
+    n = make()  # and the quarantine itself outlives the next restart
+    assert n.start() == {ids[0]: "Healthy", ids[1]: "Unhealthy"}
+    time.sleep(0.5)
+    assert "quarantine over" not in n.d.log()
+
+
 @pytest.mark.parametrize("query,busy,ok", [("vram_used", "busy", "100"), ("activity", "in-reset", "7")])
 def test_polled_recovery_waits_for_the_driver_to_report_the_devices_memory(mk, query, busy, ok):
     """The polled recovery after an event gap needs more than amdsmi's cached
