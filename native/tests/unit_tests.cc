@@ -1272,8 +1272,55 @@ void TestMemcapUsage() {
   rmdir(root);
 }
 
+static void TestStringHelpers() {
+  g_case = "strings";
+  CHECK(Split("a,,b", ',') == std::vector<std::string>({"a", "", "b"}));
+  CHECK(Split("", ',') == std::vector<std::string>({""}));
+  CHECK(SplitOn("a::b::", "::") == std::vector<std::string>({"a", "b", ""}));
+  CHECK(SplitOn("abc", "") == std::vector<std::string>({"abc"}));
+  CHECK(Trim(" \t x y \n") == "x y" && Trim("   ").empty());
+  CHECK(Join({"a", "b", "c"}, ", ") == "a, b, c" && Join({}, ",").empty());
+  CHECK(ToLower("MiXeD-1") == "mixed-1");
+  CHECK(StartsWith("abc", "ab") && !StartsWith("a", "ab") && EndsWith("abc", "bc") && !EndsWith("c", "bc"));
+  CHECK(ParseInt("-42") == -42 && !ParseInt("") && !ParseInt(" 1") && !ParseInt("1x") &&
+        !ParseInt("99999999999999999999"));
+  CHECK(ParseUint("18446744073709551615") == UINT64_MAX && !ParseUint("18446744073709551616") &&
+        !ParseUint("-1") && !ParseUint("+1") && !ParseUint(""));
+  CHECK(ParseBool(" Yes ") == true && ParseBool("off") == false && ParseBool("t") == true && !ParseBool("maybe"));
+  CHECK(JsonEscape("a\"b\\c\nd\re\tf") == "a\\\"b\\\\c\\nd\\re\\tf");
+  CHECK(JsonEscape(std::string("\x01z", 2)) == "\\u0001z");
+  CHECK(PathJoin("/a/", "/b//c/") == "/a/b/c" && PathJoin("", "x") == "x" && PathJoin("/", "") == "/");
+  CHECK(BaseName("/a/b/") == "b" && BaseName("c") == "c" && BaseName("/").empty());  // "/": no file name
+}
+
+static void TestGrpcCommon() {
+  g_case = "grpc-common";
+  using adp::grpc::FromGrpcCode;
+  using adp::grpc::ToGrpcCode;
+  // every status code maps to its gRPC code and back (kNotSupported is
+  // UNIMPLEMENTED on the wire)
+  for (Code c : {Code::kOk, Code::kInvalidArgument, Code::kNotFound, Code::kAlreadyExists,
+                 Code::kFailedPrecondition, Code::kUnavailable, Code::kUnimplemented, Code::kInternal,
+                 Code::kDeadlineExceeded, Code::kPermissionDenied})
+    CHECK(FromGrpcCode(ToGrpcCode(c)) == c);
+  CHECK(ToGrpcCode(Code::kNotSupported) == adp::grpc::kGrpcUnimplemented);
+  CHECK(FromGrpcCode(adp::grpc::kGrpcResourceExhausted) == Code::kInternal);  // codes we never send
+  std::string framed;
+  adp::grpc::FrameMessage(std::string(300, 'x'), &framed);
+  CHECK(framed.size() == 305 && framed[0] == 0 && framed[3] == 1 && static_cast<unsigned char>(framed[4]) == 44);
+  // grpc-message percent-encoding: printable ASCII but '%' passes; round trip
+  std::string msg = "100% done\n\xc3\xa9";
+  std::string enc = adp::grpc::PercentEncode(msg);
+  CHECK(enc == "100%25 done%0A%C3%A9");
+  CHECK(adp::grpc::PercentDecode(enc) == msg);
+  CHECK(adp::grpc::PercentDecode("%4") == "%4" && adp::grpc::PercentDecode("%zz") == "%zz" &&
+        adp::grpc::PercentDecode("a%41") == "aA");
+}
+
 int main() {
   TestLongLogLine();
+  TestStringHelpers();
+  TestGrpcCommon();
   TestYaml();
   TestConfigFuzz();
   TestReplicaCuRanges();
