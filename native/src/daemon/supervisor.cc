@@ -313,7 +313,8 @@ class Supervisor {
       in.layout_changes_live = layout_changes_live_;
       for (const auto& [key, bdf] : metrics_gpus_) {
         uint32_t fail = ledger_.Get(key).fail;
-        bool gap = (fail & health::kFailResetPending) && ledger_.Gap(key, nullptr);
+        health::GapMark m;
+        bool gap = (fail & health::kFailResetPending) && ledger_.Gap(key, &m) && !m.tentative;
         in.gpus.push_back({bdf, fail, gap});
       }
     }

@@ -252,8 +252,11 @@ void Monitor::RelayConnect() {
   relay_fd_ = ConnectRelay(cfg_.event_relay);
   if (relay_fd_ < 0) {
     events_reason_ = "event relay " + cfg_.event_relay + " not reachable (" + strerror(errno) + ")";
+    if (relay_lost_ms_ == 0) relay_lost_ms_ = NowMs();
     return;
   }
+  relay_lost_ms_ = 0;
+  relay_lost_confirmed_ = false;
   // Our processors (the relay re-enumerates only if they differ from its
   // registration) and where we are in its event stream (it replays what this
   // daemon missed since, e.g. across a SIGHUP).
@@ -280,6 +283,8 @@ void Monitor::RelayClose(const std::string& why) {
   events_ok_ = false;
   events_reason_ = why;
   counters_->events_enabled.store(0);
+  relay_lost_ms_ = NowMs();
+  relay_lost_confirmed_ = false;
   // Events sent meanwhile are replayed if the relay comes back holding them.
   MarkGap("event relay: " + why, true);
 }
@@ -506,11 +511,14 @@ void Monitor::MarkGap(const std::string& why, bool tentative) {
   for (const auto& g : snap_->gpus) {
     if (!(fail_[g.index] & kFailResetPending)) continue;
     if (!ledger_->MarkGap(keys_[g.index], why, tentative, now)) continue;
-    if (cfg_.reset_recovery_hold_ms > 0)
+    if (cfg_.reset_recovery_hold_ms > 0 && tentative)
+      LOG_WARN(kComp, "GPU %s waits for GPU_POST_RESET; events may have been missed (%s): unless the event relay "
+               "replays them, it is back in service once amdsmi has answered every poll for %g s",
+               g.bdf.c_str(), why.c_str(), static_cast<double>(cfg_.reset_recovery_hold_ms) / 1000.0);
+    else if (cfg_.reset_recovery_hold_ms > 0)
       LOG_WARN(kComp, "GPU %s waits for GPU_POST_RESET across an event gap (%s): back in service once amdsmi has "
-               "answered every poll for %lld s, unless a GPU_PRE_RESET arrives%s", g.bdf.c_str(), why.c_str(),
-               static_cast<long long>(cfg_.reset_recovery_hold_ms / 1000),
-               tentative ? " or the relay replays what was missed" : "");
+               "answered every poll for %g s, unless a GPU_PRE_RESET arrives", g.bdf.c_str(), why.c_str(),
+               static_cast<double>(cfg_.reset_recovery_hold_ms) / 1000.0);
     else
       LOG_WARN(kComp, "GPU %s waits for GPU_POST_RESET across an event gap (%s); --reset-recovery-hold-ms=0: only "
                "the event (or the operator) brings it back", g.bdf.c_str(), why.c_str());
@@ -534,7 +542,9 @@ void Monitor::CheckGapRecovery(int gpu, bool alive) {
     m.responsive_since_ms = now;
     ledger_->SetResponsiveSince(key, now);
   }
-  if (cfg_.reset_recovery_hold_ms <= 0) return;
+  // A tentative gap (the relay connection dropped) may be replayed whole:
+  // only a confirmed one lets polling end the wait.
+  if (cfg_.reset_recovery_hold_ms <= 0 || m.tentative) return;
   const int64_t from = std::max(m.since_ms, m.responsive_since_ms);
   if (now - from < cfg_.reset_recovery_hold_ms) return;
   const auto& g = snap_->gpus[gpu];
@@ -642,6 +652,14 @@ void Monitor::Run() {
         LOG_WARN(kComp, "the event relay has not answered this daemon's reinit for %d ms; polling only until it does",
                  cfg_.event_fail_ms);
         MarkGap("the event relay did not answer", false);
+      }
+      // A relay away for good cannot replay anything: the tentative gap holds.
+      if (relay_fd_ < 0 && relay_lost_ms_ != 0 && !relay_lost_confirmed_ &&
+          NowMs() - relay_lost_ms_ > cfg_.event_fail_ms) {
+        relay_lost_confirmed_ = true;
+        char secs[32];
+        snprintf(secs, sizeof(secs), "%g", cfg_.event_fail_ms / 1000.0);
+        MarkGap(std::string("the event relay has been unreachable for ") + secs + " s", false);
       }
     } else if (events_ok_) {
       events.clear();

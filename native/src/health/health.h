@@ -328,6 +328,10 @@ class Monitor {
   bool relay_cursor_sent_ = false;  // the reinit named where this daemon was in the relay's events
   int64_t relay_connected_ms_ = 0;  // when this connection's reinit was sent
   bool relay_overdue_ = false;      // no answer for event_fail_ms: counted as a gap
+  // Since when the relay has been out of reach (0 = connected): a tentative
+  // gap is confirmed once that lasts event_fail_ms.
+  int64_t relay_lost_ms_ = 0;
+  bool relay_lost_confirmed_ = false;
   int64_t relay_tried_ms_ = -1000000;
   std::string fingerprint_;  // ProcessorFingerprint of the snapshot, sent with "reinit"
   // In-process event waits that keep failing: since when, how many, and

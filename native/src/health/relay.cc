@@ -694,6 +694,10 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     if (stuck) send_to(c, hello(true, 1));
     reg->Request(c.id, std::move(rq.fp));
   };
+  const std::string drop_on = [] {
+    const char* e = getenv("ADP_DEBUG_RELAY_DROP_ON");
+    return std::string(e ? e : "");
+  }();
   int exit_code = 0;
   bool quit = false;
   std::string pending, done_pending;  // bytes read from the pipes, up to the last full line
@@ -738,7 +742,18 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
       }
       if (!out.empty()) {
         LOG_INFO(kComp, "%s", OneLine(out).c_str());
-        broadcast(out);
+        if (!drop_on.empty() && out.find(drop_on) != std::string::npos) {
+          // Tests: what a daemon whose socket buffer is full sees -- dropped,
+          // the events it missed held in the ring for its reconnection.
+          for (auto& c : clients)
+            if (c.subscribed && c.fd >= 0) {
+              close(c.fd);
+              c.fd = -1;
+            }
+          LOG_WARN(kComp, "every daemon connection dropped (ADP_DEBUG_RELAY_DROP_ON)");
+        } else {
+          broadcast(out);
+        }
       }
     }
     if (pfds[3].revents & POLLIN) {

@@ -709,3 +709,63 @@ def test_a_relay_that_never_answers_the_reinit_is_a_gap(scratch, tmp_path):
         for c in conns:
             c.close()
         srv.close()
+
+
+def test_a_dropped_connection_is_a_tentative_gap_the_replay_cancels(scratch):
+    """The relay drops a daemon whose socket buffer is full (here: on cue,
+    ADP_DEBUG_RELAY_DROP_ON). The GPU waiting for GPU_POST_RESET gets a
+    *tentative* gap: the daemon reconnects with its cursor, the relay replays
+    what it missed and says nothing was lost, and the mark is cancelled -- so
+    polling does not return the GPU (the hold passes several times over), and
+    the POST_RESET replayed or sent later does. A POST_RESET the drop itself
+    swallowed arrives by the replay."""
+    n = RelayNode(scratch, relay_env={"ADP_DEBUG_RELAY_DROP_ON": "dropme"},
+                  daemon_args=["--reset-recovery-hold-ms", "500"])
+    try:
+        n.d.wait_log("events on through the relay")
+        n.inject("1 3 pre-reset")
+        assert n.health() == ["Healthy", "Unhealthy"]
+        # a VMFAULT on GPU 0 whose delivery drops the connection
+        n.inject("0 1 fault dropme")
+        n.d.wait_log("event relay: the event relay closed the connection")
+        log = n.d.wait_log("the event relay replayed what was missed; waiting for GPU_POST_RESET again", timeout=10)
+        assert n.bdf(1) in log
+        assert "VMFAULT(1) on GPU 0" in n.d.wait_log("VMFAULT(1) on GPU 0")  # replayed
+        time.sleep(1.5)  # three holds: no polled recovery without a real gap
+        assert "recovered without GPU_POST_RESET" not in n.d.log()
+        assert _series(n.metrics(), "amdgpu_dp_gpu_awaiting_polled_recovery", n.bdf(1)) == 0
+        # the POST_RESET whose delivery drops the connection arrives by the replay
+        n.inject("1 4 reset done dropme")
+        n.d.wait_log("event relay: the event relay closed the connection", count=2)
+        n.wait_health(["Healthy", "Healthy"], timeout=10)
+        rlog = n.relay.log()
+        assert rlog.count("daemon connected for events (nothing missed)") == 2, rlog[-3000:]
+        assert "recovered without GPU_POST_RESET" not in n.d.log()
+    finally:
+        n.stop()
+
+
+def test_a_relay_gone_for_good_confirms_the_gap(scratch):
+    """The relay dies and does not come back: the tentative gap of the GPU
+    waiting for GPU_POST_RESET is confirmed after ADP_EVENT_FAIL_MS without a
+    relay, and the polled recovery returns the GPU. Before that, nothing
+    returns it (a relay that came back could still replay the event)."""
+    n = RelayNode(scratch, daemon_args=["--reset-recovery-hold-ms", "300"],
+                  daemon_env={"ADP_EVENT_FAIL_MS": "1500"})
+    try:
+        n.d.wait_log("events on through the relay")
+        n.inject("1 3 pre-reset")
+        assert n.health() == ["Healthy", "Unhealthy"]
+        t0 = time.time()
+        n.relay.proc.kill()
+        n.relay.proc.wait(timeout=10)
+        log = n.d.wait_log("events may have been missed")
+        assert n.bdf(1) in log
+        assert _series(n.metrics(), "amdgpu_dp_gpu_awaiting_polled_recovery", n.bdf(1)) == 0  # tentative
+        log = n.d.wait_log("the event relay has been unreachable for 1.5 s", timeout=10)
+        n.wait_health(["Healthy", "Healthy"], timeout=10)
+        assert time.time() - t0 >= 1.5
+        line = [ln for ln in n.d.log().splitlines() if "recovered without GPU_POST_RESET" in ln]
+        assert len(line) == 1 and "unreachable" in line[0], line
+    finally:
+        n.stop()
