@@ -178,6 +178,13 @@ const std::vector<FlagDef>& Table() {
        "remove these GPUs from --drain-file (their names only: other GPUs named on the same line, and its "
        "comment, stay), print the drain list and exit",
        [](Flags& f) -> void* { return &f.undrain; }},
+      {"return-to-service", "ADP_RETURN_TO_SERVICE", "", Kind::kString,
+       "return these GPUs (named as for --drain) to service and exit: the running daemon clears what its health "
+       "monitor holds against them -- a GPU_PRE_RESET without its GPU_POST_RESET, a flapping quarantine and its "
+       "reset count, an ECC verdict (re-baselined at the current count), an event -- at its next poll, as if their "
+       "lines were deleted from --health-state-file. A drain stays (--undrain); a failure still present (no "
+       "answer, retired pages) comes back at that poll. The request is written next to --drain-file",
+       [](Flags& f) -> void* { return &f.return_to_service; }},
       {"drain-file", "DP_DRAIN_FILE", "drainFile", Kind::kString,
        "operator drain list: every GPU named in this file (PCI address, UUID, partition UUID or node index; "
        "whitespace or comma separated, '#' comments) is advertised Unhealthy until it is removed from the file "

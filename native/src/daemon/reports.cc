@@ -422,7 +422,7 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
 int DrainCommand(smi::Library* lib, const Validated& v, const Config& cfg) {
   const Flags& f = cfg.flags;
   if (f.drain_file.empty()) {
-    fprintf(stderr, "--drain/--undrain need --drain-file (DP_DRAIN_FILE)\n");
+    fprintf(stderr, "--drain/--undrain/--return-to-service need --drain-file (DP_DRAIN_FILE)\n");
     return 1;
   }
   auto snap = inventory::BuildSnapshot(lib, v.bopts);
@@ -445,8 +445,38 @@ int DrainCommand(smi::Library* lib, const Validated& v, const Config& cfg) {
     }
     return true;
   };
-  std::vector<const inventory::PhysicalGpu*> add, remove;
-  if (!resolve(f.drain, &add) || !resolve(f.undrain, &remove)) return 1;
+  std::vector<const inventory::PhysicalGpu*> add, remove, back;
+  if (!resolve(f.drain, &add) || !resolve(f.undrain, &remove) || !resolve(f.return_to_service, &back)) return 1;
+  if (!back.empty()) {
+    // A request, not an edit of the state file the daemon keeps writing: the
+    // monitor takes the file (rename) at its next poll and clears the GPUs.
+    const std::string req = f.drain_file + ".return";
+    std::string body;
+    {
+      std::ifstream in(req);
+      for (std::string line; std::getline(in, line);) body += line + "\n";
+    }
+    const std::set<std::string> listed = health::DrainTokens(body);
+    for (const auto* g : back) {
+      bool already = false;
+      for (const auto& n : health::DrainNames(*g)) already = already || listed.count(n);
+      if (!already) body += g->bdf + "  # " + g->uuid + "\n";
+    }
+    std::string tmp = req + ".tmp." + std::to_string(getpid());
+    int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    bool ok = fd >= 0 && write(fd, body.data(), body.size()) == static_cast<ssize_t>(body.size());
+    if (fd >= 0) close(fd);
+    if (!ok || rename(tmp.c_str(), req.c_str()) != 0) {
+      fprintf(stderr, "cannot write %s: %s\n", req.c_str(), strerror(errno));
+      unlink(tmp.c_str());
+      return 1;
+    }
+    for (const auto* g : back)
+      printf("%s (%s): back in service at the daemon's next health poll (request in %s)\n", g->bdf.c_str(),
+             g->uuid.c_str(), req.c_str());
+    fflush(stdout);
+    if (add.empty() && remove.empty()) return 0;
+  }
 
   std::vector<std::string> lines;
   {

@@ -27,6 +27,8 @@ struct DoctorReport {
 };
 int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorReport& d);
 // --drain / --undrain: edits --drain-file (atomically) and prints it.
+// --return-to-service: adds the GPUs to the request file next to it
+// (<drain file>.return), which the running daemon's monitor consumes.
 int DrainCommand(smi::Library* lib, const Validated& v, const Config& cfg);
 
 }  // namespace adp::daemon

@@ -945,7 +945,8 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     DoctorReport d;
     return Doctor(lib->get(), v, cfg, d);
   }
-  if (!cfg.flags.drain.empty() || !cfg.flags.undrain.empty()) return DrainCommand(lib->get(), v, cfg);
+  if (!cfg.flags.drain.empty() || !cfg.flags.undrain.empty() || !cfg.flags.return_to_service.empty())
+    return DrainCommand(lib->get(), v, cfg);
   if (cfg.flags.event_relay)
     return health::RunEventRelay(lib->get(), cfg.flags.health_event_socket, sfd,
                                  {cfg.flags.driver_root, cfg.flags.host_proc, cfg.flags.kfd_proc_dir});

@@ -361,9 +361,55 @@ void Monitor::ApplyDrain() {
   }
 }
 
+void Monitor::ApplyReturnRequests() {
+  // Taken by rename first: a request written meanwhile is a new file, read at
+  // the next poll, never lost to our unlink.
+  const std::string req = cfg_.drain_file + ".return", taken = req + ".taken";
+  if (rename(req.c_str(), taken.c_str()) != 0) return;  // none
+  std::string text;
+  int fd = open(taken.c_str(), O_RDONLY | O_CLOEXEC | O_NONBLOCK);
+  if (fd >= 0) {
+    char buf[4096];
+    ssize_t n;
+    while ((n = read(fd, buf, sizeof(buf))) > 0 && text.size() < 65536) text.append(buf, static_cast<size_t>(n));
+    close(fd);
+  }
+  unlink(taken.c_str());
+  const std::set<std::string> names = DrainTokens(text);
+  for (const auto& g : snap_->gpus) {
+    bool named = false;
+    for (const auto& n : DrainNames(g)) named = named || names.count(n);
+    if (!named) continue;
+    const std::string& key = keys_[g.index];
+    // As if the GPU's line were deleted from the state file: the current ECC
+    // count is the new baseline, no reset history, no gap.
+    GpuRecord r = ledger_->Get(key);
+    const std::string was = r.reason;
+    auto ecc = lib_->UncorrectableErrors(snap_->procs[g.partitions.front().handle].handle);
+    if (ecc.ok()) {
+      ecc_baseline_[g.index] = *ecc;
+      r.has_baseline = true;
+      r.ecc_baseline = r.ecc_seen = *ecc;
+      ledger_->Put(key, r);
+    }
+    ledger_->ClearGap(key);
+    ledger_->ClearResets(key);
+    if (!(fail_[g.index] & ~kFailDrained)) {
+      LOG_INFO(kComp, "GPU %s: return-to-service asked: %s", g.bdf.c_str(),
+               fail_[g.index] ? "drained -- the drain file keeps it out (--undrain)" : "nothing held against it");
+      continue;
+    }
+    LOG_WARN(kComp, "GPU %s returned to service by the operator (was: %s)", g.bdf.c_str(), was.c_str());
+    Update(g.index, 0, ~static_cast<uint32_t>(kFailDrained), "returned to service by the operator");
+  }
+}
+
 void Monitor::PollOnce() {
   uint64_t poll = counters_->polls.fetch_add(1) + 1;
-  if (!cfg_.drain_file.empty()) ApplyDrain();
+  if (!cfg_.drain_file.empty()) {
+    ApplyDrain();
+    ApplyReturnRequests();
+  }
   size_t answered = 0, ecc_ok = 0, retired_ok = 0;
   std::string counts;
   for (const auto& g : snap_->gpus) {

@@ -261,6 +261,7 @@ class Ledger {
   // The last recorded reset (none known, e.g. a state file from an older
   // version: `now_ms` is recorded, so its quarantine lasts one more window).
   int64_t LastReset(const std::string& key, int64_t now_ms);
+  void ClearResets(const std::string& key);
 
  private:
   void SaveLocked() const;
@@ -309,6 +310,9 @@ class Monitor {
   void Update(int gpu, uint32_t set, uint32_t clear, const std::string& reason);
   // Applies the drain file to every GPU (PollOnce).
   void ApplyDrain();
+  // Consumes the operator's return-to-service request (<drain file>.return,
+  // --return-to-service): clears every failure but a drain of the GPUs named.
+  void ApplyReturnRequests();
   // Records an event gap on every GPU waiting for GPU_POST_RESET.
   void MarkGap(const std::string& why, bool tentative);
   // The polled recovery check of a GPU waiting across a gap (PollOnce).

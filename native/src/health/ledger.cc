@@ -226,6 +226,14 @@ int64_t Ledger::LastReset(const std::string& key, int64_t now_ms) {
   return *std::max_element(v.begin(), v.end());
 }
 
+void Ledger::ClearResets(const std::string& key) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = recs_.find(key);
+  if (it == recs_.end() || it->second.resets.empty()) return;
+  it->second.resets.clear();
+  SaveLocked();
+}
+
 void Ledger::SetResponsiveSince(const std::string& key, int64_t ms) {
   std::lock_guard<std::mutex> lk(mu_);
   if (auto it = gaps_.find(key); it != gaps_.end()) it->second.responsive_since_ms = ms;

@@ -226,6 +226,8 @@ static void TestLedgerGaps() {
   CHECK(body.find("\nd\t-\t0\t0\t\tresets=1200,1600\n") != std::string::npos);
   auto back = health::Ledger::Parse(body);
   CHECK(back["d"].resets == std::vector<int64_t>({1200, 1600}) && back["c"].resets.empty());
+  l.ClearResets("d");  // --return-to-service
+  CHECK(l.Get("d").resets.empty() && l.RecordReset("d", 1700, 500) == 1);
   // an older file (no field) and a malformed field: no history, the line kept
   CHECK(health::Ledger::Parse("adp-health v1\ng\t-\t0\t64\tx\tresets=1,y\n")["g"].fail == health::kFailFlapping);
   CHECK(health::Ledger::Parse("adp-health v1\ng\t-\t0\t64\tx\tresets=1,y\n")["g"].resets.empty());

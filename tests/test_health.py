@@ -398,3 +398,86 @@ def test_drain_and_undrain_commands(scratch, tmp_path):
         assert until(["Unhealthy", "Healthy"]) == ["Unhealthy", "Healthy"]
     finally:
         n.close()
+
+
+def test_return_to_service_command(scratch, tmp_path):
+    """`amdgpu-device-plugin --return-to-service <id>` (in the plugin pod,
+    DP_DRAIN_FILE set): the running daemon clears what it holds against the
+    GPU at its next poll -- a reset that never completed, a flapping
+    quarantine, an ECC verdict (re-baselined at the current count) -- as if
+    its line were deleted from the state file, without a restart. A drain
+    stays (that is --undrain's); a name that is no GPU of the node fails."""
+    import queue
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import DAEMON, MOCK_LIB
+    drain = tmp_path / "drain"
+    state = tmp_path / "health.state"
+    fx = dict(fixtures.node(2), events_open_kfd=True)
+    n = Node(scratch, fx, args=["--drain-file", str(drain), "--health-state-file", str(state),
+                                "--reset-recovery-hold-ms", "0", "--reset-flap-limit", "2"],
+             env={"DP_HEALTH_POLL_MS": "100"})
+    env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB, AMDSMI_MOCK_FIXTURE=fixtures.write(fx, str(tmp_path / "fx")),
+               DP_DRAIN_FILE=str(drain))
+
+    def cli(*args):
+        r = subprocess.run([DAEMON, "--device-plugin-path", str(tmp_path), *args], capture_output=True, text=True,
+                           timeout=60, env=env)
+        return r.returncode, r.stdout, r.stderr
+
+    last = [x.health for x in n.first.devices]
+
+    def until(want, timeout=5):
+        nonlocal last
+        deadline = time.time() + timeout
+        while last != want and time.time() < deadline:
+            try:
+                last = [x.health for x in n.q.get(timeout=0.2).devices]
+            except queue.Empty:
+                pass
+        return last
+    try:
+        bdf0, bdf1 = fx["gpus"][0]["bdf"], fx["gpus"][1]["bdf"]
+        n.d.wait_log("health poll #1")
+        # GPU 1: a reset that never completes (no gap, no polled recovery)
+        n.inject("1 3 pre-reset")
+        assert until(["Healthy", "Unhealthy"]) == ["Healthy", "Unhealthy"]
+        rc, out, err = cli("--return-to-service", bdf1)
+        assert rc == 0 and bdf1 in out, out + err
+        assert until(["Healthy", "Healthy"]) == ["Healthy", "Healthy"]
+        log = n.d.wait_log("returned to service by the operator")
+        assert f"GPU {bdf1} returned to service by the operator (was: GPU_PRE_RESET" in log, log[-3000:]
+        assert not os.path.exists(str(drain) + ".return")  # the request is consumed
+        assert "\t4\t" not in state.read_text()
+        # GPU 0: ECC over its baseline, and two resets (the flap limit): both cleared, the count too
+        with open(os.path.join(n.state, "gpu0.ecc"), "w") as f:
+            f.write("5\n")
+        n.d.wait_log("uncorrectable ECC errors rose to 5")
+        n.inject("0 3 pre a")
+        n.inject("0 4 post a")
+        n.inject("0 3 pre b")
+        n.d.wait_log("quarantined")
+        time.sleep(0.3)
+        while not n.q.empty():  # (the POST between the resets sent a Healthy list too)
+            last = [x.health for x in n.q.get_nowait().devices]
+        assert last == ["Unhealthy", "Healthy"], last
+        rc, _, _ = cli("--return-to-service", "0")  # by node index
+        assert rc == 0
+        assert until(["Healthy", "Healthy"]) == ["Healthy", "Healthy"]
+        time.sleep(0.5)  # ECC re-baselined at 5: no new verdict
+        while not n.q.empty():
+            last = [x.health for x in n.q.get_nowait().devices]
+            assert last == ["Healthy", "Healthy"], last
+        assert "resets=" not in [ln for ln in state.read_text().splitlines() if ln.startswith(fx["gpus"][0]["uuid"])][0]
+        n.inject("0 3 pre c")  # one reset after the return: under the limit again
+        n.d.wait_log("pre c")
+        assert n.d.log().count("quarantined") == 1
+        # a drain stays drained
+        assert cli("--drain", bdf1)[0] == 0
+        assert until(["Unhealthy", "Unhealthy"]) == ["Unhealthy", "Unhealthy"]
+        assert cli("--return-to-service", bdf1)[0] == 0
+        n.d.wait_log(f"GPU {bdf1}: return-to-service asked: drained")
+        assert last[1] == "Unhealthy"
+        rc, _, err = cli("--return-to-service", "0000:99:00.0")
+        assert rc == 1 and "no GPU of this node is named 0000:99:00.0" in err
+    finally:
+        n.close()
