@@ -159,3 +159,62 @@ def _scenario(scratch, tmp_path, layout, g, fixture):
         k.stop()
         if relay:
             assert relay.stop() == 0
+
+
+@pytest.mark.gpu
+def test_return_to_service_on_real_amdsmi(scratch, real_snap, tmp_path):
+    """The operator's way back, in the chart's unprivileged plugin container
+    (device nodes denied): a GPU seeded reset-pending, with no polled recovery
+    (--reset-recovery-hold-ms 0), stays out until `--return-to-service <bdf>`
+    -- the command names the GPU against real amdsmi's enumeration -- and the
+    running daemon returns it at its next poll."""
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import DAEMON
+    g = real_snap["gpus"][0]
+    key = g["uuid"] or g["bdf"]
+    state = tmp_path / "health.state"
+    drain = tmp_path / "drain"
+    state.write_text(f"adp-health v1\n{key}\t-\t0\t{RESET_PENDING}\tGPU_PRE_RESET: seeded by the test\n")
+    env = {"DP_HEALTH_POLL_MS": "200",
+           "LD_PRELOAD": " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), SIM) if x)}
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = None
+    c = None
+    try:
+        d = harness.Daemon(scratch, None, real_smi=True, env=env, args=[
+            "--devices", "0", "--health-state-file", str(state), "--drain-file", str(drain),
+            "--reset-recovery-hold-ms", "0"]).start()
+        reg = k.wait_registration(30)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        q, call = c.watch()
+        first = _health(q.get(timeout=10))
+        d.wait_log("health poll #1", 30)
+        time.sleep(1.0)  # five polls: nothing returns it
+        assert "returned to service" not in d.log()
+        cmd_env = dict(os.environ, DP_DRAIN_FILE=str(drain), LD_PRELOAD=env["LD_PRELOAD"])
+        cmd_env.pop("AMD_SMI_LIB", None)
+        r = subprocess.run([DAEMON, "--device-plugin-path", scratch, "--return-to-service", g["bdf"]],
+                           capture_output=True, text=True, timeout=60, env=cmd_env)
+        log = d.wait_log("returned to service by the operator", 30)
+        deadline = time.monotonic() + 10
+        law = first
+        while any(h != "Healthy" for h in law.values()) and time.monotonic() < deadline:
+            law = _health(q.get(timeout=max(0.05, deadline - time.monotonic())))
+        call.cancel()
+        record = {"first_law": first, "law_after": law, "command": {"rc": r.returncode, "out": r.stdout,
+                                                                    "err": r.stderr[-2000:]},
+                  "log": [ln for ln in log.splitlines() if "return" in ln or "stays unhealthy" in ln][-6:],
+                  "state_after": state.read_text().splitlines()}
+        os.makedirs(OUT, exist_ok=True)
+        with open(os.path.join(OUT, "return_to_service.json"), "w") as f:
+            json.dump(record, f, indent=1)
+        assert all(h == "Unhealthy" for h in first.values()), record
+        assert r.returncode == 0 and g["bdf"] in r.stdout, record
+        assert all(h == "Healthy" for h in law.values()), record
+        assert all(ln.split("\t")[3] == "0" for ln in record["state_after"][1:]), record
+    finally:
+        if c:
+            c.close()
+        if d:
+            assert d.stop() == 0
+        k.stop()
