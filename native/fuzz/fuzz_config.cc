@@ -5,14 +5,19 @@
 // (LoadConfig with an injected environment, no config file). Operators write
 // these, but a DaemonSet's values come from templating and typos: anything
 // must be either accepted or refused with a message, never crash. A
-// resource-config that parses must name valid resources only.
+// resource-config that parses must name valid resources only. Also the two
+// files operators edit by hand next to the daemon: the health state file
+// (what parses must survive a write and a re-read unchanged) and a drain-file
+// line (undraining names removes exactly those names).
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 
 #include "common/log.h"
 #include "daemon/config.h"
 #include "daemon/yaml.h"
+#include "health/health.h"
 #include "strategy/strategy.h"
 
 using namespace adp;
@@ -22,7 +27,44 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
   static bool quiet = (SetLogLevel(LogLevel::kError), true);
   (void)quiet;
   std::string body(reinterpret_cast<const char*>(data + 1), size - 1);
-  switch (data[0] % 4) {
+  switch (data[0] % 6) {
+    case 4: {
+      auto recs = health::Ledger::Parse(body);
+      auto again = health::Ledger::Parse(health::Ledger::Serialize(recs));
+      bool same = again.size() == recs.size();
+      for (const auto& [k, r] : recs) {
+        auto it = again.find(k);
+        same = same && it != again.end() && it->second.fail == r.fail && it->second.reason == r.reason &&
+               it->second.has_baseline == r.has_baseline && it->second.ecc_baseline == r.ecc_baseline &&
+               it->second.ecc_seen == r.ecc_seen && it->second.resets == r.resets;
+      }
+      if (!same) {
+        fprintf(stderr, "invariant violated: the health state does not survive a write and a re-read\n");
+        abort();
+      }
+      break;
+    }
+    case 5: {
+      // "<line>\n<names, comma separated>"
+      size_t nl = body.find('\n');
+      if (nl == std::string::npos) return 0;
+      std::string line = body.substr(0, nl);
+      if (line.find('\r') != std::string::npos) return 0;
+      std::set<std::string> names = health::DrainTokens(body.substr(nl + 1));
+      std::string rest = health::RemoveDrainNames(line, names);
+      auto before = health::DrainTokens(line), after = health::DrainTokens(rest);
+      for (const auto& t : before)
+        if (names.count(t) == after.count(t)) {  // a name removed stays; any other stays
+          fprintf(stderr, "invariant violated: '%s' after undraining from '%s'\n", t.c_str(), line.c_str());
+          abort();
+        }
+      for (const auto& t : after)
+        if (!before.count(t)) {
+          fprintf(stderr, "invariant violated: '%s' appeared undraining '%s'\n", t.c_str(), line.c_str());
+          abort();
+        }
+      break;
+    }
     case 0: (void)daemon::ParseConfigFile(body); break;
     case 1: (void)yaml::ParseSubset(body); break;
     case 2: {

@@ -79,6 +79,7 @@ std::map<std::string, GpuRecord> Ledger::Parse(const std::string& body) {
   std::string line;
   bool header = false;
   while (std::getline(in, line)) {
+    if (!line.empty() && line.back() == '\r') line.pop_back();  // CRLF (a file edited elsewhere)
     if (!header) {
       if (Trim(line) != "adp-health v1") {
         LOG_WARN(kComp, "health state: unknown format '%s'; ignored", line.c_str());
@@ -110,6 +111,8 @@ std::map<std::string, GpuRecord> Ledger::Parse(const std::string& body) {
     r.fail = static_cast<uint32_t>(*fail) &
              (kFailEcc | kFailUnresponsive | kFailResetPending | kFailEvent | kFailRetiredPages | kFailFlapping);
     if (f.size() > 4) r.reason = f[4];
+    for (auto& c : r.reason)
+      if (c == '\r') c = ' ';  // as Serialize writes it
     if (f.size() > 5 && f[5].rfind("resets=", 0) == 0) {
       for (const auto& t : Split(std::string_view(f[5]).substr(7), ',')) {
         auto v = ParseUint(t);

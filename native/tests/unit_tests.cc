@@ -226,6 +226,9 @@ static void TestLedgerGaps() {
   CHECK(body.find("\nd\t-\t0\t0\t\tresets=1200,1600\n") != std::string::npos);
   auto back = health::Ledger::Parse(body);
   CHECK(back["d"].resets == std::vector<int64_t>({1200, 1600}) && back["c"].resets.empty());
+  // CRLF line endings (a file edited on another system) read as LF
+  auto crlf = health::Ledger::Parse("adp-health v1\r\nh\t-\t0\t4\twhy\tresets=5,6\r\n");
+  CHECK(crlf["h"].fail == 4 && crlf["h"].reason == "why" && crlf["h"].resets == std::vector<int64_t>({5, 6}));
   l.ClearResets("d");  // --return-to-service
   CHECK(l.Get("d").resets.empty() && l.RecordReset("d", 1700, 500) == 1);
   // an older file (no field) and a malformed field: no history, the line kept
