@@ -905,6 +905,10 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
   const Config& cfg = startup_cfg;
   // The relay's liveness probe runs every 30 s: no config dump, no amdsmi.
   if (cfg.flags.relay_ping) return health::PingRelay(cfg.flags.health_event_socket, 5000);
+  // An operator's command (kubectl exec): its printed answer, not the startup log.
+  const bool operator_command =
+      !cfg.flags.drain.empty() || !cfg.flags.undrain.empty() || !cfg.flags.return_to_service.empty();
+  if (operator_command && !getenv("ADP_LOG_LEVEL")) SetLogLevel(LogLevel::kWarn);
   LOG_INFO(kComp, "running with config:\n%s", cfg.ToJson().c_str());
   LOG_INFO(kComp, "running with resource config: %s", v.rc.ToJson().c_str());
   if (cfg.flags.list_grants) return ListGrants(PathJoin(cfg.flags.plugin_dir, "amdgpu-dp/usage"));
@@ -945,8 +949,7 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     DoctorReport d;
     return Doctor(lib->get(), v, cfg, d);
   }
-  if (!cfg.flags.drain.empty() || !cfg.flags.undrain.empty() || !cfg.flags.return_to_service.empty())
-    return DrainCommand(lib->get(), v, cfg);
+  if (operator_command) return DrainCommand(lib->get(), v, cfg);
   if (cfg.flags.event_relay)
     return health::RunEventRelay(lib->get(), cfg.flags.health_event_socket, sfd,
                                  {cfg.flags.driver_root, cfg.flags.host_proc, cfg.flags.kfd_proc_dir});
