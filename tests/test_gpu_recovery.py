@@ -15,7 +15,8 @@ here real libamd_smi answers them, in the three layouts a plugin runs in:
   relay, which cannot replay what a fresh daemon missed (a gap).
 
 The GPU's earlier PRE_RESET is seeded in --health-state-file, as a plugin
-container restarted in the middle of a reset finds it. The same scenario runs
+container restarted in the middle of a reset finds it. Also the operator's way
+back without any gap (--return-to-service) in the unprivileged layout. The same scenario runs
 on the amdsmi mock on CPU (in-process and relay layouts) so its mechanics stay
 pinned without a GPU. Parity: the reference never brings a GPU back
 (server.go:259, FIXME).
