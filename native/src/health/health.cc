@@ -365,7 +365,13 @@ void Monitor::ApplyReturnRequests() {
   // Taken by rename first: a request written meanwhile is a new file, read at
   // the next poll, never lost to our unlink.
   const std::string req = cfg_.drain_file + ".return", taken = req + ".taken";
-  if (rename(req.c_str(), taken.c_str()) != 0) return;  // none
+  if (rename(req.c_str(), taken.c_str()) != 0) {
+    if (errno != ENOENT && !return_request_warned_) {  // e.g. a read-only directory: say so once
+      return_request_warned_ = true;
+      LOG_WARN(kComp, "cannot take the return-to-service request %s: %s", req.c_str(), strerror(errno));
+    }
+    return;
+  }
   std::string text;
   int fd = open(taken.c_str(), O_RDONLY | O_CLOEXEC | O_NONBLOCK);
   if (fd >= 0) {

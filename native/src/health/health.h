@@ -336,6 +336,7 @@ class Monitor {
   // gap is confirmed once that lasts event_fail_ms.
   int64_t relay_lost_ms_ = 0;
   bool relay_lost_confirmed_ = false;
+  bool return_request_warned_ = false;
   int64_t relay_tried_ms_ = -1000000;
   std::string fingerprint_;  // ProcessorFingerprint of the snapshot, sent with "reinit"
   // In-process event waits that keep failing: since when, how many, and
