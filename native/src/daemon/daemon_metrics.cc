@@ -58,6 +58,25 @@ void AppendDaemonMetrics(const DaemonMetricsInput& in, std::string* out) {
          "registration or could not replay what this daemon missed; events off; event waits failing; a new "
          "in-process registration.");
   Sample(out, "amdgpu_dp_health_event_gaps_total", "", Num(h.event_gaps.load()));
+  if (h.relay_connected.load() >= 0) {
+    // Relay mode: which relay this daemon follows and where it is in its stream.
+    Family(out, "amdgpu_dp_event_relay_connected", "gauge", "1 while the daemon is connected to the event relay.");
+    Sample(out, "amdgpu_dp_event_relay_connected", "", std::to_string(h.relay_connected.load()));
+    Family(out, "amdgpu_dp_event_relay_disconnects_total", "counter",
+           "Connections to the event relay that broke: the relay restarted, or dropped this daemon when it fell "
+           "behind (events it held are replayed on reconnection).");
+    Sample(out, "amdgpu_dp_event_relay_disconnects_total", "", Num(h.relay_disconnects.load()));
+    auto cur = h.GetRelayCursor();
+    if (cur.valid) {
+      Family(out, "amdgpu_dp_event_relay_info", "gauge",
+             "The event relay instance this daemon follows (relay: its random ID, new at every relay start), "
+             "with the relay's registration generation (renewals so far) as the value.");
+      Sample(out, "amdgpu_dp_event_relay_info", "relay=\"" + metrics::LabelValue(cur.relay) + "\"", Num(cur.gen));
+      Family(out, "amdgpu_dp_event_relay_last_event_seq", "gauge",
+             "Number of the last event this daemon received from the relay (the relay's count).");
+      Sample(out, "amdgpu_dp_event_relay_last_event_seq", "", Num(cur.seq));
+    }
+  }
 
   if (!in.gpus.empty()) {
     // Why a GPU is Unhealthy, one series per failure cause (the ledger's bits).

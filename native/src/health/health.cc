@@ -253,10 +253,12 @@ void Monitor::RelayConnect() {
   if (relay_fd_ < 0) {
     events_reason_ = "event relay " + cfg_.event_relay + " not reachable (" + strerror(errno) + ")";
     if (relay_lost_ms_ == 0) relay_lost_ms_ = NowMs();
+    counters_->relay_connected.store(0);
     return;
   }
   relay_lost_ms_ = 0;
   relay_lost_confirmed_ = false;
+  counters_->relay_connected.store(1);
   // Our processors (the relay re-enumerates only if they differ from its
   // registration) and where we are in its event stream (it replays what this
   // daemon missed since, e.g. across a SIGHUP).
@@ -277,7 +279,11 @@ void Monitor::RelayConnect() {
 }
 
 void Monitor::RelayClose(const std::string& why) {
-  if (relay_fd_ >= 0) close(relay_fd_);
+  if (relay_fd_ >= 0) {
+    close(relay_fd_);
+    counters_->relay_disconnects.fetch_add(1);
+  }
+  counters_->relay_connected.store(0);
   relay_fd_ = -1;
   if (events_ok_) LOG_WARN(kComp, "event relay: %s; polling only until it is back", why.c_str());
   events_ok_ = false;

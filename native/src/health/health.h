@@ -171,6 +171,10 @@ struct HealthCounters {
   std::map<std::pair<std::string, std::string>, uint64_t> EventCounts() const;
   // Event gaps the monitor recorded (any GPU waiting for GPU_POST_RESET or not).
   std::atomic<uint64_t> event_gaps{0};
+  // Relay mode: connections to the event relay that broke (it restarted, or
+  // dropped a daemon that fell behind), and whether one is up now.
+  std::atomic<uint64_t> relay_disconnects{0};
+  std::atomic<int> relay_connected{-1};  // -1: not in relay mode
   // GPUs put back in service by the polled check after an event gap, per PCI address.
   void CountRecovered(const std::string& bdf);
   std::map<std::string, uint64_t> Recovered() const;

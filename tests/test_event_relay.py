@@ -128,10 +128,18 @@ def test_daemon_reconnects_when_the_relay_restarts(scratch):
     n = RelayNode(scratch)
     try:
         n.d.wait_log("events on through the relay")
+        m = n.metrics()
+        assert _value(m, "amdgpu_dp_event_relay_connected") == 1
+        assert _value(m, "amdgpu_dp_event_relay_disconnects_total") == 0
+        first_relay = [dict(ls)["relay"] for (name, ls) in m if name == "amdgpu_dp_event_relay_info"]
+        assert len(first_relay) == 1 and len(first_relay[0]) == 16, m
         n.relay.signal(signal.SIGTERM)
         n.relay.proc.wait(timeout=10)
         n.d.wait_log("event relay: the event relay closed the connection; polling only")
-        assert _value(n.metrics(), "amdgpu_dp_health_events_enabled") == 0
+        m = n.metrics()
+        assert _value(m, "amdgpu_dp_health_events_enabled") == 0
+        assert _value(m, "amdgpu_dp_event_relay_connected") == 0
+        assert _value(m, "amdgpu_dp_event_relay_disconnects_total") == 1
         n.start_relay()
         n.d.wait_log("connected to the event relay", timeout=10)
         deadline = time.time() + 10
@@ -140,6 +148,10 @@ def test_daemon_reconnects_when_the_relay_restarts(scratch):
             time.sleep(0.1)
         n.inject("0 3 reset")
         assert n.health() == ["Unhealthy", "Healthy"]
+        m = n.metrics()
+        relays = [dict(ls)["relay"] for (name, ls) in m if name == "amdgpu_dp_event_relay_info"]
+        assert len(relays) == 1 and relays != first_relay  # a new relay instance
+        assert _value(m, "amdgpu_dp_event_relay_last_event_seq") == 1
     finally:
         n.stop()
 
