@@ -169,6 +169,11 @@ def _status(args) -> int:
         failures = scalar("amdgpu_dp_driver_hbm_scan_failures_total") or 0
         secs = scalar("amdgpu_dp_driver_hbm_scan_seconds") or 0
         line += f"; driver-side scans {int(polls)} (last {secs * 1e3:.2f} ms, {int(failures)} failed)"
+    relay = scalar("amdgpu_dp_event_relay_connected")
+    if relay is not None:
+        lost = int(scalar("amdgpu_dp_event_relay_disconnects_total") or 0)
+        line += "; event relay " + ("connected" if relay == 1 else "NOT connected") + (
+            f" ({lost} connection(s) lost)" if lost else "")
     gaps = scalar("amdgpu_dp_health_event_gaps_total")
     if gaps:
         line += f"; {int(gaps)} event gap(s)"

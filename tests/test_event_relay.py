@@ -148,6 +148,11 @@ def test_daemon_reconnects_when_the_relay_restarts(scratch):
             time.sleep(0.1)
         n.inject("0 3 reset")
         assert n.health() == ["Unhealthy", "Healthy"]
+        import subprocess
+        import sys
+        st = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "status",
+                             f"http://127.0.0.1:{n.port}/metrics"], capture_output=True, text=True, timeout=60)
+        assert "event relay connected (1 connection(s) lost)" in st.stdout, st.stdout
         m = n.metrics()
         relays = [dict(ls)["relay"] for (name, ls) in m if name == "amdgpu_dp_event_relay_info"]
         assert len(relays) == 1 and relays != first_relay  # a new relay instance
