@@ -475,6 +475,19 @@ int DrainCommand(smi::Library* lib, const Validated& v, const Config& cfg) {
       printf("%s (%s): back in service at the daemon's next health poll (request in %s)\n", g->bdf.c_str(),
              g->uuid.c_str(), req.c_str());
     fflush(stdout);
+    // Wait (a little) for the daemon to take it: two poll intervals, 2..30 s.
+    const health::HealthConfig hc = health::HealthConfig::FromEnv();
+    const int wait_ms = hc.disabled || hc.poll_interval_ms <= 0
+                            ? 0
+                            : std::min(30000, std::max(2000, 2 * hc.poll_interval_ms));
+    struct stat st;
+    for (int waited = 0; waited < wait_ms && stat(req.c_str(), &st) == 0; waited += 50) usleep(50000);
+    if (stat(req.c_str(), &st) == 0)
+      fprintf(stderr, "the request is still waiting after %d ms: is the plugin running here with health checks on "
+              "(DP_DISABLE_HEALTHCHECKS unset, DP_HEALTH_POLL_MS > 0) and this --drain-file? It stays queued.\n",
+              wait_ms);
+    else
+      printf("taken by the running daemon\n");
     if (add.empty() && remove.empty()) return 0;
   }
 

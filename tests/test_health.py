@@ -417,7 +417,7 @@ def test_return_to_service_command(scratch, tmp_path):
                                 "--reset-recovery-hold-ms", "0", "--reset-flap-limit", "2"],
              env={"DP_HEALTH_POLL_MS": "100"})
     env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB, AMDSMI_MOCK_FIXTURE=fixtures.write(fx, str(tmp_path / "fx")),
-               DP_DRAIN_FILE=str(drain))
+               DP_DRAIN_FILE=str(drain), DP_HEALTH_POLL_MS="100")
 
     def cli(*args):
         r = subprocess.run([DAEMON, "--device-plugin-path", str(tmp_path), *args], capture_output=True, text=True,
@@ -442,7 +442,7 @@ def test_return_to_service_command(scratch, tmp_path):
         n.inject("1 3 pre-reset")
         assert until(["Healthy", "Unhealthy"]) == ["Healthy", "Unhealthy"]
         rc, out, err = cli("--return-to-service", bdf1)
-        assert rc == 0 and bdf1 in out, out + err
+        assert rc == 0 and bdf1 in out and "taken by the running daemon" in out, out + err
         assert until(["Healthy", "Healthy"]) == ["Healthy", "Healthy"]
         log = n.d.wait_log("returned to service by the operator")
         assert f"GPU {bdf1} returned to service by the operator (was: GPU_PRE_RESET" in log, log[-3000:]
@@ -481,3 +481,21 @@ def test_return_to_service_command(scratch, tmp_path):
         assert rc == 1 and "no GPU of this node is named 0000:99:00.0" in err
     finally:
         n.close()
+
+
+def test_return_to_service_without_a_daemon_says_so(tmp_path):
+    """No daemon takes the request (none running, or health checks off): the
+    command says so after two poll intervals (at least 2 s) and leaves the
+    request queued for the next daemon."""
+    import subprocess
+    from k8s_gpu_sharing_plugin_amd import DAEMON, MOCK_LIB
+    fx = fixtures.node(2)
+    drain = tmp_path / "drain"
+    env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB, AMDSMI_MOCK_FIXTURE=fixtures.write(fx, str(tmp_path / "fx")),
+               DP_DRAIN_FILE=str(drain), DP_HEALTH_POLL_MS="100")
+    t0 = time.time()
+    r = subprocess.run([DAEMON, "--device-plugin-path", str(tmp_path), "--return-to-service", "0"],
+                       capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0 and "the request is still waiting after 2000 ms" in r.stderr, r.stdout + r.stderr
+    assert 2.0 <= time.time() - t0 < 20
+    assert fx["gpus"][0]["bdf"] in open(str(drain) + ".return").read()
