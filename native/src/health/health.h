@@ -39,15 +39,19 @@
 // for good, and a GPU whose GPU_PRE_RESET was seen would stay Unhealthy. The
 // monitor therefore records every stretch in which events may have been missed
 // -- a new in-process registration (each monitor generation), event waits that
-// keep failing, events off, the relay disconnected, or a relay that says it
-// re-registered or could not replay what this daemon missed (relay.h) -- on
-// each GPU that is waiting for its GPU_POST_RESET. Such a GPU gets a polled
+// keep failing, events off, a relay that says it re-registered or could not
+// replay what this daemon missed (relay.h), a first connection, or a reinit
+// it leaves unanswered -- on each GPU that is waiting for its GPU_POST_RESET.
+// A dropped relay connection is a tentative gap: the relay's replay on
+// reconnection cancels it, and it is confirmed when the relay cannot replay or
+// stays away for event_fail_ms. A GPU with a confirmed gap gets a polled
 // recovery check: once amdsmi has answered at every poll for
 // --reset-recovery-hold-ms since the gap -- liveness, the device's VRAM usage
-// and the SMU's activity metrics, which the driver refuses mid-reset -- with no new
-// GPU_PRE_RESET, it is back
-// in service (logged, amdgpu_dp_gpu_recovered_without_event_total). A GPU with
-// no gap since its GPU_PRE_RESET keeps waiting for the event.
+// and the SMU's activity metrics, which the driver refuses mid-reset -- with no
+// new GPU_PRE_RESET, it is back in service (logged,
+// amdgpu_dp_gpu_recovered_without_event_total). A GPU with no gap since its
+// GPU_PRE_RESET keeps waiting for the event -- or for the operator
+// (--return-to-service, ApplyReturnRequests).
 #pragma once
 
 #include <atomic>
