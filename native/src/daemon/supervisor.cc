@@ -621,9 +621,11 @@ class Supervisor {
       auto it = now.find(res);
       if (it != now.end() && it->second != before) changed.push_back(res);
     }
-    layouts_ = now;
+    // A resource absent this time (no device left, a config without it) keeps
+    // its last layout: if it comes back changed, that is still a change.
+    for (const auto& [res, lay] : now) layouts_[res] = lay;
     std::string body;
-    for (const auto& [res, lay] : now) body += res + "\t" + lay + "\n";
+    for (const auto& [res, lay] : layouts_) body += res + "\t" + lay + "\n";
     if (body != layouts_written_) WriteLayoutFile(path, body);  // (each restart would rewrite it otherwise)
     if (changed.empty()) return;
 

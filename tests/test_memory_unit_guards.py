@@ -149,3 +149,43 @@ def test_changing_the_unit_under_live_grants_is_an_error(scratch):
         d.stop()
         k.stop()
         pr.stop()
+
+
+def test_a_resource_absent_for_a_while_keeps_its_layout(scratch):
+    """A memory-unit resource leaves the config (the node serves another
+    resource meanwhile) and comes back with another unit while a pod still
+    holds its old IDs: still a change under live grants -- the last layout
+    seen is kept while the resource is absent."""
+    pr_sock = os.path.join(scratch + ".fixture", "pod-resources.sock")
+    os.makedirs(os.path.dirname(pr_sock), exist_ok=True)
+    pr = PodResourcesStub(pr_sock)
+    cfg = os.path.join(scratch + ".fixture", "config.yaml")
+
+    def write(rc, unit):
+        tmp = cfg + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(f"version: v1\nflags:\n  resourceConfig: {rc}\n  replicaCuMask: true\n"
+                    f"  autoReplicaUnit: {unit}\n")
+        os.rename(tmp, cfg)
+    write("gpu:gpu-mem-gb:-1", "mib")
+    k, d, port = _start(scratch, ["--config-file", cfg], pr_sock=pr_sock)
+    try:
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        c.close()
+        res = "amd.com/gpu-mem-gb"
+        pr.payload = _list_response([("ml", "train", "main", res, [ids[0], ids[200]])])
+        write("gpu:sharedgpu:4", "mib")  # the memory-unit resource is gone for now
+        d.wait_log("'amd.com/sharedgpu': preferred allocation")
+        layout = open(os.path.join(scratch, "amdgpu-dp", "replica-layout")).read()
+        assert layout.count("amd.com/gpu-mem-gb\tmemory-units mib") == 1, layout  # remembered
+        write("gpu:gpu-mem-gb:-1", "cu-slot")  # back, with another unit, the pod still running
+        log = d.wait_log("what its IDs mean changed while")
+        assert "'amd.com/gpu-mem-gb'" in [ln for ln in log.splitlines() if "what its IDs mean changed while" in ln][0]
+        s = _parse(_get(port, "/metrics")[1])
+        assert _value(s, "amdgpu_dp_replica_layout_changes_with_live_allocations_total", resource=res) == 1
+    finally:
+        d.stop()
+        k.stop()
+        pr.stop()
