@@ -254,8 +254,10 @@ void Monitor::RelayConnect() {
     events_reason_ = "event relay " + cfg_.event_relay + " not reachable (" + strerror(errno) + ")";
     if (relay_lost_ms_ == 0) relay_lost_ms_ = NowMs();
     counters_->relay_connected.store(0);
+    relay_retry_ms_ = std::min(1000, relay_retry_ms_ * 2);
     return;
   }
+  relay_retry_ms_ = 100;
   relay_lost_ms_ = 0;
   relay_lost_confirmed_ = false;
   counters_->relay_connected.store(1);
@@ -291,6 +293,7 @@ void Monitor::RelayClose(const std::string& why) {
   counters_->events_enabled.store(0);
   relay_lost_ms_ = NowMs();
   relay_lost_confirmed_ = false;
+  relay_tried_ms_ = relay_lost_ms_;  // the next try in relay_retry_ms_
   // Events sent meanwhile are replayed if the relay comes back holding them.
   MarkGap("event relay: " + why, true);
 }
@@ -696,7 +699,7 @@ void Monitor::Run() {
     }
     if (!cfg_.event_relay.empty() && cfg_.events) {
       events.clear();
-      if (relay_fd_ < 0 && NowMs() - relay_tried_ms_ >= 1000) {
+      if (relay_fd_ < 0 && NowMs() - relay_tried_ms_ >= relay_retry_ms_) {
         RelayConnect();
         if (relay_fd_ >= 0) LOG_INFO(kComp, "connected to the event relay at %s", cfg_.event_relay.c_str());
       }

@@ -346,6 +346,10 @@ class Monitor {
   bool relay_lost_confirmed_ = false;
   bool return_request_warned_ = false;
   int64_t relay_tried_ms_ = -1000000;
+  // Reconnection backoff: 100 ms after a drop (a relay restart takes about that
+  // long, and events it holds meanwhile die with it if it restarts again),
+  // doubling to 1 s while the relay stays away.
+  int relay_retry_ms_ = 100;
   std::string fingerprint_;  // ProcessorFingerprint of the snapshot, sent with "reinit"
   // In-process event waits that keep failing: since when, how many, and
   // whether events are reported off because of it.

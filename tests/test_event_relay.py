@@ -786,3 +786,83 @@ def test_a_relay_gone_for_good_confirms_the_gap(scratch):
         assert len(line) == 1 and "unreachable" in line[0], line
     finally:
         n.stop()
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("seed", [int(s) for s in os.environ.get("ADP_CHAOS_SEEDS", "11,12,13").split(",")])
+def test_chaos_of_resets_restarts_and_drops_leaves_no_gpu_stuck(scratch, seed):
+    """A seeded random mix of everything that can come between a GPU_PRE_RESET
+    and its GPU_POST_RESET: daemon SIGHUPs, the relay dropping the daemon (its
+    buffer full: ADP_DEBUG_RELAY_DROP_ON), the relay restarted (SIGTERM or
+    SIGKILL), events in between. Every POST_RESET is sent while a relay runs;
+    it reaches the daemon directly or by the relay's replay -- unless the relay
+    holding it restarts before the daemon is back, which the daemon sees as an
+    event gap (a new relay): then the polled check returns the GPU. Either
+    way no GPU stays out of service, and a polled return only ever follows a
+    confirmed gap on that GPU."""
+    import random
+    rnd = random.Random(seed)
+    n = RelayNode(scratch, relay_env={"ADP_DEBUG_RELAY_DROP_ON": "dropme"},
+                  daemon_args=["--reset-recovery-hold-ms", "1500", "--reset-flap-limit", "0"])
+    try:
+        n.d.wait_log("events on through the relay")
+        pending = set()
+        for i in range(24):
+            op = rnd.choice(["pre", "post", "post", "sighup", "drop", "restart", "vm"])
+            gpu = rnd.randrange(2)
+            if op == "pre":
+                n.inject(f"{gpu} 3 chaos pre {i}")
+                pending.add(gpu)
+            elif op == "post" and pending:
+                g = rnd.choice(sorted(pending))
+                n.inject(f"{g} 4 chaos post {i}" + (" dropme" if rnd.random() < 0.5 else ""))
+                pending.discard(g)
+            elif op == "sighup":
+                n.d.signal(signal.SIGHUP)
+            elif op == "drop":
+                n.inject(f"{gpu} 1 chaos vm dropme {i}")
+            elif op == "restart":
+                if rnd.random() < 0.5:
+                    n.relay.signal(signal.SIGTERM)
+                else:
+                    n.relay.proc.kill()
+                n.relay.proc.wait(timeout=10)
+                n.start_relay()
+            elif op == "vm":
+                n.inject(f"{gpu} 1 chaos vm {i}")
+            time.sleep(rnd.uniform(0, 0.15))
+        for g in sorted(pending):
+            n.inject(f"{g} 4 chaos final post {g}")
+        # The plugin's socket name never changes: watch it afresh until the
+        # node is Healthy (a SIGHUP may restart the plugin under a watch).
+        endpoint = os.path.join(scratch, n.k.wait_registration(10).endpoint)
+        deadline = time.time() + 20
+        h = None
+        while h != ["Healthy", "Healthy"]:
+            if time.time() >= deadline and os.environ.get("ADP_CHAOS_DUMP"):
+                open(os.environ["ADP_CHAOS_DUMP"] + ".daemon", "w").write(n.d.log())
+                import glob
+                with open(os.environ["ADP_CHAOS_DUMP"] + ".relays", "w") as f:
+                    for r in sorted(glob.glob(scratch + "-relay*.daemon.log")):
+                        f.write(f"==== {r}\n" + open(r).read())
+            assert time.time() < deadline, (seed, h, n.d.log()[-5000:])
+            try:
+                c = kubelet.PluginClient(endpoint)
+                q, call = c.watch()
+                try:
+                    while h != ["Healthy", "Healthy"] and time.time() < deadline:
+                        h = [x.health for x in q.get(timeout=1).devices]
+                finally:
+                    call.cancel()
+                    c.close()
+            except Exception:
+                time.sleep(0.2)
+        log = n.d.log().splitlines()
+        for i, ln in enumerate(log):
+            if "recovered without GPU_POST_RESET" in ln:
+                bdf = ln.split("GPU ")[1].split(" ")[0]
+                assert any(f"GPU {bdf} waits for GPU_POST_RESET across an event gap" in p for p in log[:i]), ln
+    finally:
+        n.stop()
