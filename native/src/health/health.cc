@@ -144,7 +144,7 @@ Status Monitor::Start() {
     // The monitor thread reads its answer: the supervisor is not held up here.
     RelayConnect();
     if (relay_fd_ < 0)
-      LOG_WARN(kComp, "events via relay %s: %s; polling meanwhile, reconnecting every second",
+      LOG_WARN(kComp, "events via relay %s: %s; polling meanwhile, reconnecting (every second at most)",
                cfg_.event_relay.c_str(), events_reason_.c_str());
   } else {
     Status st = lib_->EventsInit(handles_, mask);
