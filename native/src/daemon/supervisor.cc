@@ -518,6 +518,12 @@ class Supervisor {
   // the plugins from the strategy, start them and a new health monitor.
   void Restart() {
     StopAll();
+    if (standby_) {
+      // Back from standing by: the instance that served meanwhile wrote the
+      // verdicts; start from its file.
+      standby_ = false;
+      ledger_.Reload();
+    }
     ArmTimer(tfd_, 0);  // disarm
     ArmTimer(rfd_, 0);
     recheck_sockets_.clear();
@@ -749,6 +755,18 @@ class Supervisor {
     // disappears again.
     LOG_WARN(kComp, "inotify: %s now belongs to another process; '%s' stands by", pl.socket_path().c_str(),
              pl.resource_name().c_str());
+    // No plugin of this instance serves any more: its health monitor pauses.
+    // The serving instance owns the verdicts now -- the state file both would
+    // write, the operator's return-to-service requests both would take.
+    for (const auto& p : plugins_)
+      if (p->running() && p->owns_socket()) return;
+    if (monitor_) {
+      LOG_WARN(kComp, "no plugin of this instance serves: its health monitor pauses (the serving instance keeps "
+               "the health verdicts)");
+      monitor_->Stop();
+      monitor_.reset();
+      standby_ = true;
+    }
   }
 
   void OnSocketRecheck(bool* do_reregister) {
@@ -864,6 +882,7 @@ class Supervisor {
   std::atomic<uint64_t> restarts_{0};
   std::atomic<bool> serving_{false};
   std::unique_ptr<health::Monitor> monitor_;
+  bool standby_ = false;  // another instance took every socket: the monitor is paused
   // Health verdicts outlive every plugin generation (and, with a state file,
   // the process): a restart must not re-advertise a failed GPU as Healthy.
   health::Ledger ledger_;

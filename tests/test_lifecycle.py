@@ -660,3 +660,47 @@ def test_socket_recheck_window_reregisters_after_it(scratch):
     assert os.path.exists(os.path.join(scratch, "amd-gpu.sock"))
     assert d.stop() == 0
     k.stop()
+
+
+def test_a_standing_by_instance_pauses_its_health_monitor(scratch, tmp_path):
+    """Once another instance serves every socket, this one's health monitor
+    pauses: the serving instance owns the verdicts -- the state file both
+    would write, and the operator's return-to-service requests, which the
+    standing-by one must not take. When the kubelet restarts (the socket
+    disappears), it serves again with a monitor reading the other instance's
+    verdicts from the state file."""
+    drain = tmp_path / "drain"
+    state = tmp_path / "health.state"
+    fx = fixtures.node(2)
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, fx, args=["--drain-file", str(drain), "--health-state-file", str(state)],
+                       env={"DP_HEALTH_POLL_MS": "100"}).start()
+    try:
+        k.wait_registration()
+        d.wait_log("health poll #1")
+        path = os.path.join(scratch, "amd-gpu.sock")
+        d.signal(signal.SIGSTOP)
+        try:
+            os.unlink(path)
+            other = _foreign_socket(path)
+        finally:
+            d.signal(signal.SIGCONT)
+        d.wait_log("its health monitor pauses")
+        req = str(drain) + ".return"
+        with open(req, "w") as f:
+            f.write(fx["gpus"][0]["bdf"] + "\n")
+        time.sleep(0.6)  # six polls of a running monitor
+        assert os.path.exists(req), "the standing-by instance took the request"
+        # the other instance's verdicts, as it writes them
+        state.write_text(f"adp-health v1\n{fx['gpus'][1]['uuid']}\t-\t0\t4\tGPU_PRE_RESET: seen by the other\n")
+        os.unlink(req)
+        other.close()
+        os.unlink(path)  # the other instance is gone; the kubelet restarts
+        k.stop()
+        k = kubelet.StubKubelet(sock(scratch)).start()
+        k.wait_registration(15)
+        log = d.wait_log("stays unhealthy from an earlier generation")
+        assert "GPU_PRE_RESET: seen by the other" in log
+    finally:
+        d.stop()
+        k.stop()
