@@ -409,7 +409,15 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
     if (access(dir.empty() ? "/" : dir.c_str(), W_OK) == 0) d.Line("ok", "health state file " + f.health_state_file);
     else d.Line("warn", "health state file " + f.health_state_file + ": directory not writable -- verdicts will "
                         "not outlive a container restart");
+    // What it holds against this node's GPUs now (the operator's next question).
+    health::Ledger ledger(f.health_state_file);
+    for (const auto& [gpu, reason] : ledger.Failed(s))
+      d.Line("warn", "GPU " + s.gpus[gpu].bdf + " is out of service by the state file: " + reason +
+                         " -- once repaired, --return-to-service " + s.gpus[gpu].bdf);
   }
+  if (!f.drain_file.empty() && access((f.drain_file + ".return").c_str(), F_OK) == 0)
+    d.Line("warn", "a return-to-service request is waiting in " + f.drain_file + ".return: no running daemon "
+                   "with health checks has taken it");
   double budget = plugin::CpuBudget();
   char b[160];
   snprintf(b, sizeof(b), "CPU budget %.2f CPUs: %d gRPC loop(s) per socket, busy-poll %s", budget,

@@ -167,3 +167,24 @@ def test_doctor_reports_the_container_device_order(tmp_path):
     fx["gpus"][1]["kfd_node"] = None
     _, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), fx=fx)
     assert _find(lines, "device order:").startswith("warn")
+
+
+def test_verdicts_in_the_state_file_and_a_waiting_request_are_named(tmp_path):
+    """The operator's next question after "why is this GPU out": --doctor names
+    each GPU the state file keeps out of service, with the reason and the way
+    back, and a return-to-service request nobody took."""
+    fx = fixtures.node(2)
+    d = tmp_path / "dp"
+    d.mkdir()
+    state = tmp_path / "health.state"
+    state.write_text(f"adp-health v1\n{fx['gpus'][1]['uuid']}\t-\t0\t4\tGPU_PRE_RESET: mode1 reset\n")
+    drain = tmp_path / "drain"
+    (tmp_path / "drain.return").write_text("0\n")
+    rc, lines = _doctor(tmp_path, "--device-plugin-path", str(d), "--health-state-file", str(state),
+                        "--drain-file", str(drain), fx=fx)
+    bdf1 = fx["gpus"][1]["bdf"]
+    line = _find(lines, f"GPU {bdf1} is out of service by the state file")
+    assert line and line.startswith("warn") and "GPU_PRE_RESET: mode1 reset" in line, lines
+    assert f"--return-to-service {bdf1}" in line
+    assert _find(lines, f"GPU {fx['gpus'][0]['bdf']} is out of service") is None
+    assert _find(lines, "a return-to-service request is waiting"), lines
