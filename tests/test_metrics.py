@@ -535,6 +535,14 @@ def test_stats_endpoint_is_json(served):
     assert sum(n for _, n in p["residency_100ns"]) >= 4 and p["residency_p50_us"] > 0
     assert st["health"]["events"] in ("on", "off", "not started") and st["restarts"] >= 1
     call.cancel()
+    # only GET: a scraper that POSTs is told so, and an unknown path is a 404
+    req = urllib.request.Request(f"http://127.0.0.1:{port}/metrics", data=b"x", method="POST")
+    try:
+        urllib.request.urlopen(req, timeout=5)
+        raise AssertionError("POST accepted")
+    except urllib.error.HTTPError as e:
+        assert e.code == 405 and e.read() == b"only GET\n"
+    assert _get(port, "/nosuch")[0] == 404
 
 
 def test_metrics_listens_on_every_address_given(scratch):
