@@ -691,11 +691,24 @@ void Monitor::Run() {
   std::vector<smi::Event> events;
   while (!stop_.load()) {
     counters_->loop_beat_ms.store(NowMs());
-    int slice = 100;  // bounded so Stop() (SIGHUP, config, re-partition, exit) is prompt; the reference waits 5000 ms
-    if (cfg_.wait_ms > 0 && cfg_.wait_ms < slice) slice = cfg_.wait_ms;
+    // An amdsmi event wait cannot be interrupted: bounded so Stop() (SIGHUP,
+    // config, re-partition, exit) is prompt -- the reference waits 5000 ms.
+    // Every other wait here also ends on the wake eventfd, so it sleeps until
+    // the next thing due (a poll, a relay reconnection or deadline): an idle
+    // daemon wakes a few times a second at most, not ten.
+    const bool in_process_wait = events_ok_ && (cfg_.event_relay.empty() || !cfg_.events);
+    int slice = in_process_wait ? 100 : 5000;
+    if (in_process_wait && cfg_.wait_ms > 0 && cfg_.wait_ms < slice) slice = cfg_.wait_ms;
     if (cfg_.poll_interval_ms > 0) {  // wake for the next poll, not a slice later
       auto until = std::chrono::duration_cast<std::chrono::milliseconds>(next_poll - Clock::now()).count();
       slice = static_cast<int>(std::max<long long>(1, std::min<long long>(slice, until)));
+    }
+    if (!cfg_.event_relay.empty() && cfg_.events) {
+      const int64_t now = NowMs();
+      auto due = [&](int64_t at) { slice = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(slice, at - now))); };
+      if (relay_fd_ < 0) due(relay_tried_ms_ + relay_retry_ms_);
+      if (relay_fd_ >= 0 && !relay_synced_ && !relay_overdue_) due(relay_connected_ms_ + cfg_.event_fail_ms + 1);
+      if (relay_fd_ < 0 && relay_lost_ms_ != 0 && !relay_lost_confirmed_) due(relay_lost_ms_ + cfg_.event_fail_ms + 1);
     }
     if (!cfg_.event_relay.empty() && cfg_.events) {
       events.clear();
