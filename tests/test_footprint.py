@@ -26,6 +26,19 @@ def test_idle_daemon_sleeps(enforce, capsys):
     assert res["threads"] < 20 and res["rss_mib"] < 64, res
 
 
+def test_idle_daemon_behind_the_relay_sleeps_between_polls(capsys):
+    """The chart's layout: events come from the relay, so the monitor waits on
+    sockets the wake eventfd interrupts, not in amdsmi, and sleeps until its
+    next poll -- a few wake-ups a second (the relay's own waiter keeps its
+    100 ms slices)."""
+    args = ["--seconds", "4", "--scrape-s", "1", "--settle-s", "1", "--relay"]
+    assert idle_footprint.main(args) == 0
+    import json
+    res = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert res["daemon_alive"] and res["relay"]["alive"], res
+    assert res["context_switches_per_s"] < 10, res  # ~3/s idle (was ~12/s with 100 ms slices)
+
+
 def test_health_event_reaches_the_kubelet_fast(capsys):
     """tools/health_latency.py: a GPU_PRE_RESET on one of 8 GPUs reaches the
     kubelet as an Unhealthy device list, and GPU_POST_RESET as Healthy, within
