@@ -114,6 +114,7 @@ def main():
     driver_polls = None
     scans = []  # (source, processes, descriptors, seconds) of the last scan, per scrape
     samples, pods, hups, kubelet_restarts, scrapes = [], 0, 0, 0, 0
+    daemon_counts = {}  # the daemon's own relay counters, last scrape
     relay_restarts, relay_logs = 0, []
     ok = True
     t_end = time.time() + a.seconds
@@ -178,6 +179,9 @@ def main():
                         scan["descriptors"] = int(line.split()[-1])
                     elif line.startswith("amdgpu_dp_driver_hbm_scan_seconds "):
                         scan["ms"] = float(line.split()[-1]) * 1e3
+                    elif line.startswith(("amdgpu_dp_event_relay_disconnects_total ",
+                                          "amdgpu_dp_health_event_gaps_total ")):
+                        daemon_counts[line.split()[0]] = int(float(line.split()[1]))
                 if scan.get("ms"):
                     scans.append(scan)
             scrapes += 1
@@ -238,6 +242,11 @@ def main():
                             "registration_kept": rlog.count("registration kept"),
                             "registration_renewed": rlog.count("re-enumerating"),
                             "nothing_missed": rlog.count("nothing missed"),
+                            # the daemon's side: connections lost (one per relay restart, plus
+                            # any drop) and event gaps it recorded
+                            "daemon_relay_disconnects": daemon_counts.get(
+                                "amdgpu_dp_event_relay_disconnects_total"),
+                            "daemon_event_gaps": daemon_counts.get("amdgpu_dp_health_event_gaps_total"),
                             "rss_mib_last": rl.get("rss_mib"), "fds_after_warmup": rw.get("fds"),
                             "fds_last": rl.get("fds"), "threads_after_warmup": rw.get("threads"),
                             "threads_last": rl.get("threads")}
