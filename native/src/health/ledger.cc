@@ -18,19 +18,36 @@
 namespace adp::health {
 namespace {
 constexpr const char* kComp = "health";
+// A node's verdicts take a few hundred bytes a GPU: anything past this is not
+// a state file this daemon wrote, and is not read whole into memory.
+constexpr size_t kMaxStateBytes = 1 << 20;
+
+// The state file's text (at most kMaxStateBytes); false when it cannot be read
+// (errno says why; ENOENT: there is none yet).
+bool ReadState(const std::string& path, std::string* out) {
+  std::ifstream in(path, std::ios::binary);
+  if (!in) return false;
+  out->resize(kMaxStateBytes);
+  in.read(out->data(), static_cast<std::streamsize>(kMaxStateBytes));
+  out->resize(static_cast<size_t>(in.gcount()));
+  if (out->size() == kMaxStateBytes && in.peek() != std::ifstream::traits_type::eof()) {
+    LOG_WARN(kComp, "health state %s is larger than %zu bytes: only its start is read", path.c_str(),
+             kMaxStateBytes);
+    if (size_t nl = out->rfind('\n'); nl != std::string::npos) out->resize(nl + 1);  // whole lines only
+  }
+  return true;
+}
 }  // namespace
 
 Ledger::Ledger(std::string path) : path_(std::move(path)) {
   if (path_.empty()) return;
-  std::ifstream in(path_);
-  if (!in) {
+  std::string body;
+  if (!ReadState(path_, &body)) {
     if (errno != ENOENT)
       LOG_WARN(kComp, "cannot read health state %s: %s; starting empty", path_.c_str(), strerror(errno));
     return;
   }
-  std::stringstream ss;
-  ss << in.rdbuf();
-  recs_ = Parse(ss.str());
+  recs_ = Parse(body);
   size_t failed = 0;
   for (const auto& [_, r] : recs_) failed += r.fail != 0;
   LOG_INFO(kComp, "health state %s: %zu GPU record(s), %zu unhealthy", path_.c_str(), recs_.size(), failed);
@@ -38,12 +55,10 @@ Ledger::Ledger(std::string path) : path_(std::move(path)) {
 
 void Ledger::Reload() {
   if (path_.empty()) return;
-  std::ifstream in(path_);
+  std::string body;
   std::map<std::string, GpuRecord> next;
-  if (in) {
-    std::stringstream ss;
-    ss << in.rdbuf();
-    next = Parse(ss.str());
+  if (ReadState(path_, &body)) {
+    next = Parse(body);
   } else if (errno != ENOENT) {
     LOG_WARN(kComp, "cannot re-read health state %s: %s; keeping the current state", path_.c_str(), strerror(errno));
     return;

@@ -229,6 +229,17 @@ static void TestLedgerGaps() {
   // CRLF line endings (a file edited on another system) read as LF
   auto crlf = health::Ledger::Parse("adp-health v1\r\nh\t-\t0\t4\twhy\tresets=5,6\r\n");
   CHECK(crlf["h"].fail == 4 && crlf["h"].reason == "why" && crlf["h"].resets == std::vector<int64_t>({5, 6}));
+  {
+    // a state file far larger than any node's: its start is read, no more
+    char tmpl[] = "/tmp/adp-ledger-XXXXXX";
+    int fd = mkstemp(tmpl);
+    std::string big = "adp-health v1\nbig\t-\t0\t4\tr\n" + std::string(3u << 20, '#') + "\ntail\t-\t0\t4\tr\n";
+    CHECK(fd >= 0 && write(fd, big.data(), big.size()) == static_cast<ssize_t>(big.size()));
+    close(fd);
+    health::Ledger lb(tmpl);
+    CHECK(lb.Get("big").fail == 4 && lb.All().count("tail") == 0);
+    unlink(tmpl);
+  }
   l.ClearResets("d");  // --return-to-service
   CHECK(l.Get("d").resets.empty() && l.RecordReset("d", 1700, 500) == 1);
   // an older file (no field) and a malformed field: no history, the line kept
