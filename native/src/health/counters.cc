@@ -111,9 +111,16 @@ void HealthCounters::AdvanceRelaySeq(uint64_t seq) {
 void HealthCounters::PersistRelayCursor(const std::string& path) {
   std::lock_guard<std::mutex> lk(mu_);
   cursor_path_ = path;
-  std::ifstream in(path);
-  std::string header, line;
-  if (!in || !std::getline(in, header) || Trim(header) != "adp-relay-cursor v1" || !std::getline(in, line)) return;
+  // Two short lines; at most 4 KiB of whatever is there is looked at.
+  std::ifstream in(path, std::ios::binary);
+  if (!in) return;
+  std::string body(4096, '\0');
+  in.read(body.data(), static_cast<std::streamsize>(body.size()));
+  body.resize(static_cast<size_t>(in.gcount()));
+  auto lines = Split(body, '\n');
+  if (lines.size() < 2 || Trim(lines[0]) != "adp-relay-cursor v1") return;
+  std::string line = lines[1];
+  if (!line.empty() && line.back() == '\r') line.pop_back();
   auto f = Split(line, '\t');
   auto seq = f.size() == 3 ? ParseUint(f[1]) : std::nullopt;
   auto gen = f.size() == 3 ? ParseUint(f[2]) : std::nullopt;

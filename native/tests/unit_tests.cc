@@ -240,6 +240,27 @@ static void TestLedgerGaps() {
     CHECK(lb.Get("big").fail == 4 && lb.All().count("tail") == 0);
     unlink(tmpl);
   }
+  {
+    // the relay cursor file: read back (CRLF too); malformed = no cursor (the relay reports a gap)
+    char tmpl[] = "/tmp/adp-cursor-XXXXXX";
+    int fd = mkstemp(tmpl);
+    close(fd);
+    auto cursor_from = [&](const std::string& body) {
+      FILE* f = fopen(tmpl, "w");
+      fputs(body.c_str(), f);
+      fclose(f);
+      health::HealthCounters hc;
+      hc.PersistRelayCursor(tmpl);
+      return hc.GetRelayCursor();
+    };
+    auto c1 = cursor_from("adp-relay-cursor v1\nab12\t7\t3\n");
+    CHECK(c1.valid && c1.relay == "ab12" && c1.seq == 7 && c1.gen == 3);
+    CHECK(cursor_from("adp-relay-cursor v1\r\nab12\t7\t3\r\n").valid);
+    CHECK(!cursor_from("adp-relay-cursor v1\nab12\t7\n").valid);
+    CHECK(!cursor_from("something else\nab12\t7\t3\n").valid);
+    CHECK(!cursor_from("adp-relay-cursor v1\n" + std::string(10000, 'x') + "\t1\t1\n").valid);
+    unlink(tmpl);
+  }
   l.ClearResets("d");  // --return-to-service
   CHECK(l.Get("d").resets.empty() && l.RecordReset("d", 1700, 500) == 1);
   // an older file (no field) and a malformed field: no history, the line kept
