@@ -1,5 +1,5 @@
 // Coverage-guided fuzzing (libFuzzer) of the event-relay wire lines
-// (health/relay.cc): the daemon parses whatever arrives on its relay socket,
+// (health/relay_protocol.cc): the daemon parses whatever arrives on its relay socket,
 // and the privileged relay parses the daemon's request lines (a scan's
 // directory is only accepted absolute and without "..").
 // Checks: no crash; an accepted event line re-formatted from its fields parses
