@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <optional>
 #include <set>
 
 #include "common/log.h"
@@ -429,131 +430,15 @@ void Monitor::PollOnce() {
   std::string counts;
   for (const auto& g : snap_->gpus) {
     void* h = snap_->procs[g.partitions.front().handle].handle;
-    if (layout_listener_ && !layout_changed_) {
-      auto [compute, memory] = lib_->PartitionModes(h);
-      for (auto& c : compute) c = static_cast<char>(toupper(static_cast<unsigned char>(c)));
-      for (auto& c : memory) c = static_cast<char>(toupper(static_cast<unsigned char>(c)));
-      bool changed = (!compute.empty() && compute != g.reported_compute) ||
-                     (!memory.empty() && memory != g.reported_memory);
-      if (changed) {
-        layout_changed_ = true;
-        std::string why = "GPU " + g.bdf + " partition mode changed " + g.reported_compute + "/" +
-                          g.reported_memory + " -> " + compute + "/" + memory;
-        LOG_WARN(kComp, "%s", why.c_str());
-        layout_listener_(why);
-        return;  // handles are about to be re-created; no health verdicts from them
-      }
-      // xGMI links that went down (or came back) change the topology scores
-      // GetPreferredAllocation uses; re-enumerate once the new count has held for
-      // two consecutive polls (a flapping link does not cause restart storms).
-      int down = lib_->XgmiLinksDown(h);
-      if (down != g.xgmi_links_down) {
-        if (++link_change_polls_[g.index] >= 2) {
-          layout_changed_ = true;
-          std::string why = "GPU " + g.bdf + " xGMI links down " + std::to_string(g.xgmi_links_down) +
-                            " -> " + std::to_string(down);
-          LOG_WARN(kComp, "%s", why.c_str());
-          layout_listener_(why);
-          return;
-        }
-      } else {
-        link_change_polls_[g.index] = 0;
-      }
-    }
-    bool alive = lib_->Responsive(h);
-    uint32_t& fail = fail_[g.index];
-    if (!alive && !(fail & kFailUnresponsive)) {
-      Update(g.index, kFailUnresponsive, 0, "device not responding to amdsmi");
-    } else if (alive && (fail & kFailUnresponsive)) {
-      Update(g.index, 0, kFailUnresponsive, "device responding again");
-    }
-    // The polled recovery wants the driver answering about the device's memory
-    // too (it fails while a reset is under way), not just the UUID amdsmi
-    // keeps; on a platform where that query never works, liveness alone.
-    Result<uint64_t> used = alive ? lib_->VramUsed(h) : Result<uint64_t>(Unavailable("not responding"));
-    if (used.ok()) counters_->SetVramUsed(g.bdf, *used);
-    // The SMU's metrics (graphics activity) are refused while the GPU is in
-    // reset, which makes them the better sign that a reset is over; asked only
-    // of a GPU waiting across a gap.
-    bool activity_ok = true;
-    if (alive && (fail & kFailResetPending) && ledger_->Gap(keys_[g.index], nullptr)) {
-      auto act = lib_->Activity(h);
-      if (act.ok()) counters_->MarkQueryOk(g.bdf, "activity");
-      activity_ok = act.ok() || !counters_->QueryEverOk(g.bdf, "activity");
-    } else if (alive && poll == 1) {
-      if (lib_->Activity(h).ok()) counters_->MarkQueryOk(g.bdf, "activity");  // learn whether it works here
-    }
-    // (the counters outlive monitor generations: "ever readable" does too)
-    CheckGapRecovery(g.index, alive && activity_ok && (used.ok() || !counters_->HasVramUsed(g.bdf)));
-    if (fail & kFailFlapping) {
-      // Quarantine ends after a whole window without a GPU_PRE_RESET (or with
-      // damping turned off).
-      const int64_t now = WallMs();
-      const int64_t quiet = now - ledger_->LastReset(keys_[g.index], now);
-      if (cfg_.reset_flap_limit <= 0 || quiet >= cfg_.reset_flap_window_ms)
-        Update(g.index, 0, kFailFlapping,
-               cfg_.reset_flap_limit <= 0 ? "reset-flap damping off"
-                                          : "no reset for " + std::to_string(quiet / 1000) + " s: quarantine over");
-    }
-    if (!alive) continue;
+    if (layout_listener_ && !layout_changed_ && PollLayout(g, h))
+      return;  // handles are about to be re-created; no health verdicts from them
+    if (!PollLiveness(g, h, poll)) continue;
     ++answered;
     counters_->responsive.fetch_add(1);
-    // Retired HBM pages: the driver takes a page out of service after an
-    // uncorrectable error in it; past the threshold the GPU is not trusted
-    // with new work (the reference has no such check).
-    if (auto bp = lib_->RetiredPages(h); bp.ok()) {
-      ++retired_ok;
-      counters_->retired_reads_ok.fetch_add(1);
-      counters_->SetRetiredPages(g.bdf, *bp);
-      uint32_t thr = retired_threshold_[g.index];
-      if (thr && *bp >= thr && !(fail & kFailRetiredPages)) {
-        Update(g.index, kFailRetiredPages, 0,
-               std::to_string(*bp) + " retired HBM pages (threshold " + std::to_string(thr) + ")");
-      } else if ((fail & kFailRetiredPages) && (!thr || *bp < thr)) {
-        Update(g.index, 0, kFailRetiredPages, "retired HBM pages below the threshold");
-      }
-    } else {
-      counters_->retired_read_errors.fetch_add(1);
-    }
-    auto ecc = lib_->UncorrectableErrors(h);
-    if (!ecc.ok()) {
-      counters_->ecc_read_errors.fetch_add(1);
-      if (poll == 1)
-        LOG_WARN(kComp, "GPU %s: uncorrectable ECC count unreadable (%s); ECC polling is off for it",
-                 g.bdf.c_str(), ecc.status().ToString().c_str());
-      continue;
-    }
-    ++ecc_ok;
-    counters_->ecc_reads_ok.fetch_add(1);
-    counts += (counts.empty() ? "" : ",") + std::to_string(*ecc);
-    GpuRecord r = ledger_->Get(keys_[g.index]);
-    if (!r.has_baseline) {  // unreadable when the monitor started: the first read is the baseline
-      r.has_baseline = true;
-      r.ecc_baseline = r.ecc_seen = *ecc;
-      ecc_baseline_[g.index] = *ecc;
-      ledger_->Put(keys_[g.index], r);
-      continue;
-    }
-    if (*ecc < r.ecc_seen) {
-      // The driver reset its RAS counters (GPU reset / driver reload): the
-      // errors that failed the GPU are gone with the state they described.
-      LOG_INFO(kComp, "GPU %s: uncorrectable ECC count fell %llu -> %llu (counters reset); re-baselined",
-               g.bdf.c_str(), static_cast<unsigned long long>(r.ecc_seen), static_cast<unsigned long long>(*ecc));
-      ecc_baseline_[g.index] = *ecc;
-      r.has_baseline = true;
-      r.ecc_baseline = r.ecc_seen = *ecc;
-      ledger_->Put(keys_[g.index], r);
-      if (fail & kFailEcc) Update(g.index, 0, kFailEcc, "uncorrectable ECC counters reset");
-      continue;
-    }
-    if (*ecc > r.ecc_seen) {
-      r.ecc_seen = *ecc;
-      ledger_->Put(keys_[g.index], r);
-    }
-    if (*ecc > ecc_baseline_[g.index] && !(fail & kFailEcc)) {
-      Update(g.index, kFailEcc, 0,
-             "uncorrectable ECC errors rose to " + std::to_string(*ecc) + " (baseline " +
-                 std::to_string(ecc_baseline_[g.index]) + ")");
+    retired_ok += PollRetiredPages(g, h);
+    if (auto ecc = PollEcc(g, h, poll)) {
+      ++ecc_ok;
+      counts += (counts.empty() ? "" : ",") + std::to_string(*ecc);
     }
   }
   if (poll == 1) {
@@ -564,6 +449,131 @@ void Monitor::PollOnce() {
              counts.c_str(), retired_ok, thresholds, events_ok_ ? "on" : "off", events_ok_ ? "" : ": ",
              events_reason_.c_str());
   }
+}
+
+bool Monitor::PollLayout(const inventory::PhysicalGpu& g, void* h) {
+  auto [compute, memory] = lib_->PartitionModes(h);
+  for (auto& c : compute) c = static_cast<char>(toupper(static_cast<unsigned char>(c)));
+  for (auto& c : memory) c = static_cast<char>(toupper(static_cast<unsigned char>(c)));
+  std::string why;
+  if ((!compute.empty() && compute != g.reported_compute) || (!memory.empty() && memory != g.reported_memory)) {
+    why = "GPU " + g.bdf + " partition mode changed " + g.reported_compute + "/" + g.reported_memory + " -> " +
+          compute + "/" + memory;
+  } else {
+    // xGMI links that went down (or came back) change the topology scores
+    // GetPreferredAllocation uses; re-enumerate once the new count has held for
+    // two consecutive polls (a flapping link does not cause restart storms).
+    int down = lib_->XgmiLinksDown(h);
+    if (down == g.xgmi_links_down) {
+      link_change_polls_[g.index] = 0;
+      return false;
+    }
+    if (++link_change_polls_[g.index] < 2) return false;
+    why = "GPU " + g.bdf + " xGMI links down " + std::to_string(g.xgmi_links_down) + " -> " + std::to_string(down);
+  }
+  layout_changed_ = true;
+  LOG_WARN(kComp, "%s", why.c_str());
+  layout_listener_(why);
+  return true;
+}
+
+bool Monitor::PollLiveness(const inventory::PhysicalGpu& g, void* h, uint64_t poll) {
+  const bool alive = lib_->Responsive(h);
+  if (!alive && !(fail_[g.index] & kFailUnresponsive))
+    Update(g.index, kFailUnresponsive, 0, "device not responding to amdsmi");
+  else if (alive && (fail_[g.index] & kFailUnresponsive))
+    Update(g.index, 0, kFailUnresponsive, "device responding again");
+  // The polled recovery wants the driver answering about the device's memory
+  // too (it fails while a reset is under way), not just the UUID amdsmi
+  // keeps; on a platform where that query never works, liveness alone.
+  Result<uint64_t> used = alive ? lib_->VramUsed(h) : Result<uint64_t>(Unavailable("not responding"));
+  if (used.ok()) counters_->SetVramUsed(g.bdf, *used);
+  // The SMU's metrics (graphics activity) are refused while the GPU is in
+  // reset, which makes them the better sign that a reset is over; asked only
+  // of a GPU waiting across a gap.
+  bool activity_ok = true;
+  if (alive && (fail_[g.index] & kFailResetPending) && ledger_->Gap(keys_[g.index], nullptr)) {
+    auto act = lib_->Activity(h);
+    if (act.ok()) counters_->MarkQueryOk(g.bdf, "activity");
+    activity_ok = act.ok() || !counters_->QueryEverOk(g.bdf, "activity");
+  } else if (alive && poll == 1) {
+    if (lib_->Activity(h).ok()) counters_->MarkQueryOk(g.bdf, "activity");  // learn whether it works here
+  }
+  // (the counters outlive monitor generations: "ever readable" does too)
+  CheckGapRecovery(g.index, alive && activity_ok && (used.ok() || !counters_->HasVramUsed(g.bdf)));
+  if (fail_[g.index] & kFailFlapping) {
+    // Quarantine ends after a whole window without a GPU_PRE_RESET (or with
+    // damping turned off).
+    const int64_t now = WallMs();
+    const int64_t quiet = now - ledger_->LastReset(keys_[g.index], now);
+    if (cfg_.reset_flap_limit <= 0 || quiet >= cfg_.reset_flap_window_ms)
+      Update(g.index, 0, kFailFlapping,
+             cfg_.reset_flap_limit <= 0 ? "reset-flap damping off"
+                                        : "no reset for " + std::to_string(quiet / 1000) + " s: quarantine over");
+  }
+  return alive;
+}
+
+// Retired HBM pages: the driver takes a page out of service after an
+// uncorrectable error in it; past the threshold the GPU is not trusted with
+// new work (the reference has no such check).
+bool Monitor::PollRetiredPages(const inventory::PhysicalGpu& g, void* h) {
+  auto bp = lib_->RetiredPages(h);
+  if (!bp.ok()) {
+    counters_->retired_read_errors.fetch_add(1);
+    return false;
+  }
+  counters_->retired_reads_ok.fetch_add(1);
+  counters_->SetRetiredPages(g.bdf, *bp);
+  const uint32_t thr = retired_threshold_[g.index];
+  const bool failed = fail_[g.index] & kFailRetiredPages;
+  if (thr && *bp >= thr && !failed)
+    Update(g.index, kFailRetiredPages, 0,
+           std::to_string(*bp) + " retired HBM pages (threshold " + std::to_string(thr) + ")");
+  else if (failed && (!thr || *bp < thr))
+    Update(g.index, 0, kFailRetiredPages, "retired HBM pages below the threshold");
+  return true;
+}
+
+std::optional<uint64_t> Monitor::PollEcc(const inventory::PhysicalGpu& g, void* h, uint64_t poll) {
+  auto ecc = lib_->UncorrectableErrors(h);
+  if (!ecc.ok()) {
+    counters_->ecc_read_errors.fetch_add(1);
+    if (poll == 1)
+      LOG_WARN(kComp, "GPU %s: uncorrectable ECC count unreadable (%s); ECC polling is off for it", g.bdf.c_str(),
+               ecc.status().ToString().c_str());
+    return std::nullopt;
+  }
+  counters_->ecc_reads_ok.fetch_add(1);
+  GpuRecord r = ledger_->Get(keys_[g.index]);
+  if (!r.has_baseline) {  // unreadable when the monitor started: the first read is the baseline
+    r.has_baseline = true;
+    r.ecc_baseline = r.ecc_seen = *ecc;
+    ecc_baseline_[g.index] = *ecc;
+    ledger_->Put(keys_[g.index], r);
+    return *ecc;
+  }
+  if (*ecc < r.ecc_seen) {
+    // The driver reset its RAS counters (GPU reset / driver reload): the
+    // errors that failed the GPU are gone with the state they described.
+    LOG_INFO(kComp, "GPU %s: uncorrectable ECC count fell %llu -> %llu (counters reset); re-baselined",
+             g.bdf.c_str(), static_cast<unsigned long long>(r.ecc_seen), static_cast<unsigned long long>(*ecc));
+    ecc_baseline_[g.index] = *ecc;
+    r.has_baseline = true;
+    r.ecc_baseline = r.ecc_seen = *ecc;
+    ledger_->Put(keys_[g.index], r);
+    if (fail_[g.index] & kFailEcc) Update(g.index, 0, kFailEcc, "uncorrectable ECC counters reset");
+    return *ecc;
+  }
+  if (*ecc > r.ecc_seen) {
+    r.ecc_seen = *ecc;
+    ledger_->Put(keys_[g.index], r);
+  }
+  if (*ecc > ecc_baseline_[g.index] && !(fail_[g.index] & kFailEcc))
+    Update(g.index, kFailEcc, 0,
+           "uncorrectable ECC errors rose to " + std::to_string(*ecc) + " (baseline " +
+               std::to_string(ecc_baseline_[g.index]) + ")");
+  return *ecc;
 }
 
 void Monitor::MarkGap(const std::string& why, bool tentative) {

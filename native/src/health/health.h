@@ -60,6 +60,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <optional>
 #include <set>
 #include <string>
 #include <string_view>
@@ -313,6 +314,15 @@ class Monitor {
   void Run();
   void Notify(int gpu, bool healthy, const std::string& reason);
   void PollOnce();
+  // PollOnce's parts, per GPU (h: its first processor's handle). PollLayout:
+  // true when the partition modes or xGMI links changed (the supervisor
+  // re-enumerates); PollLiveness: whether amdsmi answers (and the polled
+  // recovery and the end of a quarantine); PollRetiredPages: whether readable;
+  // PollEcc: the uncorrectable count when readable.
+  bool PollLayout(const inventory::PhysicalGpu& g, void* h);
+  bool PollLiveness(const inventory::PhysicalGpu& g, void* h, uint64_t poll);
+  bool PollRetiredPages(const inventory::PhysicalGpu& g, void* h);
+  std::optional<uint64_t> PollEcc(const inventory::PhysicalGpu& g, void* h, uint64_t poll);
   // Sets/clears failure bits of a GPU, records them in the ledger and notifies
   // listeners when the GPU's overall health flips.
   void Update(int gpu, uint32_t set, uint32_t clear, const std::string& reason);
