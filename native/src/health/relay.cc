@@ -404,58 +404,91 @@ class Registration {
 // reachable (not a leak to LeakSanitizer).
 Registration* volatile g_abandoned = nullptr;
 
-}  // namespace
+// The relay's socket server: one poll() loop over the signals, the listening
+// socket, the two pipes (event lines from the waiter, renewal results from
+// the registrar) and the connected daemons. It answers a daemon at once;
+// nothing it does waits for amdsmi.
+class RelayServer {
+ public:
+  RelayServer(smi::Library* lib, const RelayOptions& opts)
+      : lib_(lib), opts_(opts), stuck_ms_(EnvMs("ADP_RELAY_STUCK_MS", 10000)), relay_id_(RandomId()),
+        drop_on_(Env("ADP_DEBUG_RELAY_DROP_ON")), scans_(opts) {}
+  ~RelayServer() {
+    for (auto& c : clients_)
+      if (c.fd >= 0) close(c.fd);
+    for (int fd : {ev_pipe_[0], done_pipe_[0], lfd_})
+      if (fd >= 0) close(fd);
+  }
 
+  // Binds the socket (owner-only) and starts the registration; false: logged.
+  bool Open(const std::string& socket_path) {
+    sockaddr_un addr{};
+    socket_path_ = socket_path;
+    lfd_ = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
+    addr.sun_family = AF_UNIX;
+    memcpy(addr.sun_path, socket_path.c_str(), socket_path.size());
+    unlink(socket_path.c_str());
+    mode_t old = umask(0077);  // owner-only: only the daemon's uid (root, same pod) may connect
+    int rc = lfd_ < 0 ? -1 : bind(lfd_, reinterpret_cast<sockaddr*>(&addr), sizeof(addr));
+    umask(old);
+    if (rc != 0 || listen(lfd_, 8) != 0) {
+      LOG_ERROR(kComp, "cannot listen on %s: %s", socket_path.c_str(), strerror(errno));
+      return false;
+    }
+    if (pipe2(ev_pipe_, O_CLOEXEC | O_NONBLOCK) != 0 || pipe2(done_pipe_, O_CLOEXEC | O_NONBLOCK) != 0) {
+      LOG_ERROR(kComp, "pipe: %s", strerror(errno));
+      for (int* p : {ev_pipe_, done_pipe_})
+        for (int i : {0, 1})
+          if (p[i] >= 0) close(p[i]), p[i] = -1;
+      return false;
+    }
+    // Heap-held: a waiter stuck in amdsmi at exit keeps using it (Shutdown).
+    reg_ = new Registration(lib_, opts_.driver_root, ev_pipe_[1], done_pipe_[1], stuck_ms_);
+    reg_->StartRegistrar();
+    LOG_INFO(kComp, "relaying amdsmi events on %s (relay %s)", socket_path.c_str(), relay_id_.c_str());
+    return true;
+  }
 
-int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_fd, const RelayOptions& opts) {
-  sockaddr_un addr{};
-  if (socket_path.empty() || socket_path.size() >= sizeof(addr.sun_path)) {
-    LOG_ERROR(kComp, "--event-relay needs --health-event-socket (a path shorter than %zu bytes)",
-              sizeof(addr.sun_path));
-    return 1;
+  // Serves until a terminating signal; then ends the registration.
+  int Run(int signal_fd) {
+    bool quit = false;
+    while (!quit) {
+      std::vector<pollfd> pfds = {
+          {signal_fd, POLLIN, 0}, {lfd_, POLLIN, 0}, {ev_pipe_[0], POLLIN, 0}, {done_pipe_[0], POLLIN, 0}};
+      constexpr size_t kFixed = 4;  // signals, listener, event pipe, renewal pipe
+      for (const auto& c : clients_) pfds.push_back({c.fd, POLLIN, 0});
+      int timeout = static_cast<int>(std::min<int64_t>(1000, stuck_ms_ / 2 + 1));
+      if (poll(pfds.data(), pfds.size(), timeout) < 0 && errno != EINTR) break;
+      Watchdog();
+      if (pfds[2].revents & POLLIN) OnEvents();
+      if (pfds[3].revents & POLLIN) OnRenewals();
+      if (pfds[0].revents & POLLIN) {
+        signalfd_siginfo si;
+        while (read(signal_fd, &si, sizeof(si)) == sizeof(si))
+          if (si.ssi_signo != SIGHUP && si.ssi_signo != SIGUSR1) quit = true;
+      }
+      // Only the clients polled above (accept below appends new ones).
+      for (size_t i = 0; i + kFixed < pfds.size(); ++i)
+        if (clients_[i].fd >= 0 && (pfds[kFixed + i].revents & (POLLIN | POLLHUP | POLLERR))) OnClient(clients_[i]);
+      if (pfds[1].revents & POLLIN) Accept();
+      clients_.erase(std::remove_if(clients_.begin(), clients_.end(), [](const Client& c) { return c.fd < 0; }),
+                     clients_.end());
+    }
+    if (reg_->Shutdown()) {
+      delete reg_;
+      close(ev_pipe_[1]);
+      close(done_pipe_[1]);
+    } else {
+      // A thread stuck in amdsmi still uses it and the pipes' write ends; the
+      // process exits next.
+      g_abandoned = reg_;
+    }
+    unlink(socket_path_.c_str());
+    LOG_INFO(kComp, "event relay stopped");
+    return 0;
   }
-  int lfd = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
-  addr.sun_family = AF_UNIX;
-  memcpy(addr.sun_path, socket_path.c_str(), socket_path.size());
-  unlink(socket_path.c_str());
-  mode_t old = umask(0077);  // owner-only: only the daemon's uid (root, same pod) may connect
-  int rc = lfd < 0 ? -1 : bind(lfd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr));
-  umask(old);
-  if (rc != 0 || listen(lfd, 8) != 0) {
-    LOG_ERROR(kComp, "cannot listen on %s: %s", socket_path.c_str(), strerror(errno));
-    if (lfd >= 0) close(lfd);
-    return 1;
-  }
-  // The waiter hands formatted event lines to this loop through one pipe, the
-  // registrar its renewal results through another: this loop sleeps in poll()
-  // on sockets, signals and those pipes, and answers a daemon at once.
-  int ev_pipe[2], done_pipe[2];
-  if (pipe2(ev_pipe, O_CLOEXEC | O_NONBLOCK) != 0) {
-    LOG_ERROR(kComp, "pipe: %s", strerror(errno));
-    close(lfd);
-    return 1;
-  }
-  if (pipe2(done_pipe, O_CLOEXEC | O_NONBLOCK) != 0) {
-    LOG_ERROR(kComp, "pipe: %s", strerror(errno));
-    close(ev_pipe[0]);
-    close(ev_pipe[1]);
-    close(lfd);
-    return 1;
-  }
-  // Watchdog: an amdsmi wait that has not returned (or has kept failing) for
-  // kStuckMs means events are not being delivered; the daemons are told (a
-  // "reinit" hello with events=off, so they poll) and told again when the wait
-  // returns.
-  const int64_t kStuckMs = [] {
-    const char* e = getenv("ADP_RELAY_STUCK_MS");
-    return e && atoll(e) > 0 ? static_cast<int64_t>(atoll(e)) : int64_t{10000};
-  }();
-  const std::string relay_id = RandomId();
-  // Heap-held: a waiter stuck in amdsmi at exit keeps using it (Shutdown).
-  auto* reg = new Registration(lib, opts.driver_root, ev_pipe[1], done_pipe[1], kStuckMs);
-  reg->StartRegistrar();
-  LOG_INFO(kComp, "relaying amdsmi events on %s (relay %s)", socket_path.c_str(), relay_id.c_str());
 
+ private:
   struct Client {
     int fd;
     std::string in;
@@ -463,45 +496,123 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
     bool subscribed = false;  // sent its reinit: gets events and reinit hellos
     int gap = 1;              // what its reinit hello says, unless the registration is renewed
   };
-  std::vector<Client> clients;
-  uint64_t next_id = 1;
-  ScanWorker scans(opts);
-  // The last kRelayRingSize events forwarded, for daemons that reconnect.
-  std::deque<std::pair<uint64_t, std::string>> ring;
-  uint64_t seq = 0;
-  bool stuck = false;
-  std::string stuck_reason;
-  auto hello = [&](bool reinit, int gap) {
-    Registration::State s = reg->Get();
-    bool ok = s.ok && !stuck;
+
+  static std::string Env(const char* name) {
+    const char* e = getenv(name);
+    return e ? e : "";
+  }
+  static int64_t EnvMs(const char* name, int64_t dflt) {
+    const char* e = getenv(name);
+    return e && atoll(e) > 0 ? static_cast<int64_t>(atoll(e)) : dflt;
+  }
+
+  std::string Hello(bool reinit, int gap) const {
+    Registration::State s = reg_->Get();
+    bool ok = s.ok && !stuck_;
     std::string h = std::string("hello v1 ") + (reinit ? "reinit " : "") +
                     (ok ? "events=ok processors=" + std::to_string(s.processors) : std::string("events=off")) +
-                    " relay=" + relay_id + " gen=" + std::to_string(s.gen) + " seq=" + std::to_string(seq) +
+                    " relay=" + relay_id_ + " gen=" + std::to_string(s.gen) + " seq=" + std::to_string(seq_) +
                     " fp=" + (s.fp.empty() ? std::string("-") : s.fp) + " renew_ms=" + std::to_string(s.renew_ms);
     if (gap >= 0) h += " gap=" + std::to_string(gap);
-    if (!ok) h += " reason=" + (stuck ? stuck_reason : s.reason);
+    if (!ok) h += " reason=" + (stuck_ ? stuck_reason_ : s.reason);
     return h + "\n";
-  };
-  auto send_to = [](Client& c, const std::string& s) {
+  }
+  static void SendTo(Client& c, const std::string& s) {
     if (c.fd >= 0 && !SendAll(c.fd, s)) {
       close(c.fd);
       c.fd = -1;
     }
-  };
-  auto broadcast = [&](const std::string& s) {
-    for (auto& c : clients)
-      if (c.subscribed) send_to(c, s);
-  };
+  }
+  void Broadcast(const std::string& s) {
+    for (auto& c : clients_)
+      if (c.subscribed) SendTo(c, s);
+  }
+
+  // Watchdog: an amdsmi wait that has not returned (or has kept failing) for
+  // stuck_ms_ means events are not being delivered; the daemons are told (a
+  // "reinit" hello with events=off, so they poll) and told again when the
+  // wait returns.
+  void Watchdog() {
+    if (!reg_->running()) return;
+    int64_t silent = reg_->SilentMs();
+    // A wait that keeps failing delivers no more events than one that hangs.
+    int64_t failing_ms = reg_->FailingMs();
+    if (!stuck_ && (silent > stuck_ms_ || failing_ms > stuck_ms_)) {
+      stuck_ = true;
+      stuck_reason_ = silent > stuck_ms_
+                          ? "the amdsmi event wait has not returned for " + std::to_string(silent) + " ms"
+                          : "the amdsmi event wait has failed for " + std::to_string(failing_ms) + " ms";
+      LOG_ERROR(kComp, "events=off reason=%s: daemons fall back to polling", stuck_reason_.c_str());
+      Broadcast(Hello(true, 1));
+    } else if (stuck_ && silent <= stuck_ms_ && failing_ms <= stuck_ms_) {
+      stuck_ = false;
+      LOG_INFO(kComp, "the amdsmi event wait returned again: events back on");
+      Broadcast(Hello(true, 1));
+    }
+  }
+
+  // Event lines from the waiter: numbered, held for replays, forwarded.
+  void OnEvents() {
+    char buf[4096];
+    ssize_t n;
+    while ((n = read(ev_pipe_[0], buf, sizeof(buf))) > 0) pending_.append(buf, static_cast<size_t>(n));
+    std::string out;
+    size_t nl;
+    while ((nl = pending_.find('\n')) != std::string::npos) {
+      // "event node=..." -> "event seq=<n> node=...", held for replays
+      std::string line = "event seq=" + std::to_string(++seq_) + pending_.substr(5, nl - 4);
+      pending_.erase(0, nl + 1);
+      ring_.emplace_back(seq_, line);
+      if (ring_.size() > kRelayRingSize) ring_.pop_front();
+      out += line;
+    }
+    if (out.empty()) return;
+    LOG_INFO(kComp, "%s", OneLine(out).c_str());
+    if (!drop_on_.empty() && out.find(drop_on_) != std::string::npos) {
+      // Tests: what a daemon whose socket buffer is full sees -- dropped,
+      // the events it missed held in the ring for its reconnection.
+      for (auto& c : clients_)
+        if (c.subscribed && c.fd >= 0) {
+          close(c.fd);
+          c.fd = -1;
+        }
+      LOG_WARN(kComp, "every daemon connection dropped (ADP_DEBUG_RELAY_DROP_ON)");
+      return;
+    }
+    Broadcast(out);
+  }
+
+  // "done <client> <renewed 0|1>" from the registrar.
+  void OnRenewals() {
+    char buf[512];
+    ssize_t n;
+    while ((n = read(done_pipe_[0], buf, sizeof(buf))) > 0) done_pending_.append(buf, static_cast<size_t>(n));
+    size_t nl;
+    while ((nl = done_pending_.find('\n')) != std::string::npos) {
+      auto f = Split(std::string_view(done_pending_).substr(0, nl), ' ');
+      done_pending_.erase(0, nl + 1);
+      if (f.size() != 3) continue;
+      if (f[2] == "1") {
+        // Renewed: every subscribed daemon went without a registration meanwhile.
+        Broadcast(Hello(true, 1));
+      } else {
+        auto id = ParseUint(f[1]);
+        for (auto& c : clients_)
+          if (id && c.id == *id) SendTo(c, Hello(true, c.gap));
+      }
+    }
+  }
+
   // "reinit fp=<fp> since=<relay>:<seq>:<gen>": replay what the daemon missed,
   // decide whether it can have missed anything, and pass the fingerprint on.
-  auto subscribe = [&](Client& c, RelayRequest& rq) {
+  void Subscribe(Client& c, RelayRequest& rq) {
     int gap = 1;
-    if (rq.has_since && rq.since_relay == relay_id && rq.since_seq <= seq) {
+    if (rq.has_since && rq.since_relay == relay_id_ && rq.since_seq <= seq_) {
       const uint64_t s = rq.since_seq;
-      bool held = s == seq || (!ring.empty() && ring.front().first <= s + 1);
+      bool held = s == seq_ || (!ring_.empty() && ring_.front().first <= s + 1);
       std::string replay;
       size_t n = 0;
-      for (const auto& [q, l] : ring)
+      for (const auto& [q, l] : ring_)
         if (q > s) {
           replay += l;
           ++n;
@@ -509,9 +620,9 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
       if (n) {
         LOG_INFO(kComp, "replaying %zu event(s) after #%llu to a reconnected daemon%s", n,
                  static_cast<unsigned long long>(s), held ? "" : " (older ones are no longer held)");
-        send_to(c, replay);
+        SendTo(c, replay);
       }
-      gap = held && rq.since_gen == reg->Get().gen ? 0 : 1;
+      gap = held && rq.since_gen == reg_->Get().gen ? 0 : 1;
     }
     c.subscribed = true;
     c.gap = gap;
@@ -519,172 +630,100 @@ int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_
              rq.has_since ? (gap ? "it may have missed events" : "nothing missed") : "a new daemon");
     // The watchdog's events=off stands whatever the registrar answers (and a
     // registrar renewing under a stuck wait may never answer): say so now.
-    if (stuck) send_to(c, hello(true, 1));
-    reg->Request(c.id, std::move(rq.fp));
-  };
-  const std::string drop_on = [] {
-    const char* e = getenv("ADP_DEBUG_RELAY_DROP_ON");
-    return std::string(e ? e : "");
-  }();
-  int exit_code = 0;
-  bool quit = false;
-  std::string pending, done_pending;  // bytes read from the pipes, up to the last full line
+    if (stuck_) SendTo(c, Hello(true, 1));
+    reg_->Request(c.id, std::move(rq.fp));
+  }
 
-  while (!quit) {
-    std::vector<pollfd> pfds = {
-        {signal_fd, POLLIN, 0}, {lfd, POLLIN, 0}, {ev_pipe[0], POLLIN, 0}, {done_pipe[0], POLLIN, 0}};
-    constexpr size_t kFixed = 4;  // signals, listener, event pipe, renewal pipe
-    for (const auto& c : clients) pfds.push_back({c.fd, POLLIN, 0});
-    int timeout = static_cast<int>(std::min<int64_t>(1000, kStuckMs / 2 + 1));
-    if (poll(pfds.data(), pfds.size(), timeout) < 0 && errno != EINTR) break;
-    if (reg->running()) {
-      int64_t silent = reg->SilentMs();
-      // A wait that keeps failing delivers no more events than one that hangs.
-      int64_t failing_ms = reg->FailingMs();
-      if (!stuck && (silent > kStuckMs || failing_ms > kStuckMs)) {
-        stuck = true;
-        stuck_reason = silent > kStuckMs
-                           ? "the amdsmi event wait has not returned for " + std::to_string(silent) + " ms"
-                           : "the amdsmi event wait has failed for " + std::to_string(failing_ms) + " ms";
-        LOG_ERROR(kComp, "events=off reason=%s: daemons fall back to polling", stuck_reason.c_str());
-        broadcast(hello(true, 1));
-      } else if (stuck && silent <= kStuckMs && failing_ms <= kStuckMs) {
-        stuck = false;
-        LOG_INFO(kComp, "the amdsmi event wait returned again: events back on");
-        broadcast(hello(true, 1));
-      }
+  // A daemon's request lines: a reinit subscribes it; a scan takes the
+  // connection over.
+  void OnClient(Client& c) {
+    char buf[256];
+    ssize_t n = recv(c.fd, buf, sizeof(buf), 0);
+    if (n <= 0) {
+      if (n < 0 && (errno == EAGAIN || errno == EINTR)) return;
+      close(c.fd);
+      c.fd = -1;
+      return;
     }
-    if (pfds[2].revents & POLLIN) {
-      char buf[4096];
-      ssize_t n;
-      while ((n = read(ev_pipe[0], buf, sizeof(buf))) > 0) pending.append(buf, static_cast<size_t>(n));
-      std::string out;
-      size_t nl;
-      while ((nl = pending.find('\n')) != std::string::npos) {
-        // "event node=..." -> "event seq=<n> node=...", held for replays
-        std::string line = "event seq=" + std::to_string(++seq) + pending.substr(5, nl - 4);
-        pending.erase(0, nl + 1);
-        ring.emplace_back(seq, line);
-        if (ring.size() > kRelayRingSize) ring.pop_front();
-        out += line;
-      }
-      if (!out.empty()) {
-        LOG_INFO(kComp, "%s", OneLine(out).c_str());
-        if (!drop_on.empty() && out.find(drop_on) != std::string::npos) {
-          // Tests: what a daemon whose socket buffer is full sees -- dropped,
-          // the events it missed held in the ring for its reconnection.
-          for (auto& c : clients)
-            if (c.subscribed && c.fd >= 0) {
-              close(c.fd);
-              c.fd = -1;
-            }
-          LOG_WARN(kComp, "every daemon connection dropped (ADP_DEBUG_RELAY_DROP_ON)");
+    c.in.append(buf, static_cast<size_t>(n));
+    if (c.in.size() > 4096) {  // nothing legitimate is that long
+      close(c.fd);
+      c.fd = -1;
+      return;
+    }
+    size_t nl;
+    while (c.fd >= 0 && (nl = c.in.find('\n')) != std::string::npos) {
+      RelayRequest rq = ParseRelayRequest(std::string_view(c.in.data(), nl));
+      if (rq.kind == "reinit") Subscribe(c, rq);
+      if (rq.kind == "scan") {
+        // The connection becomes the scan's.
+        if (rq.malformed) {
+          LOG_WARN(kComp, "malformed scan request dropped");
+          close(c.fd);
         } else {
-          broadcast(out);
+          scans_.Submit(c.fd, std::move(rq.usage_dir), std::move(rq.cgroup));
         }
-      }
-    }
-    if (pfds[3].revents & POLLIN) {
-      char buf[512];
-      ssize_t n;
-      while ((n = read(done_pipe[0], buf, sizeof(buf))) > 0) done_pending.append(buf, static_cast<size_t>(n));
-      size_t nl;
-      while ((nl = done_pending.find('\n')) != std::string::npos) {
-        auto f = Split(std::string_view(done_pending).substr(0, nl), ' ');
-        done_pending.erase(0, nl + 1);
-        if (f.size() != 3) continue;
-        if (f[2] == "1") {
-          // Renewed: every subscribed daemon went without a registration meanwhile.
-          broadcast(hello(true, 1));
-        } else {
-          auto id = ParseUint(f[1]);
-          for (auto& c : clients)
-            if (id && c.id == *id) send_to(c, hello(true, c.gap));
-        }
-      }
-    }
-    if (pfds[0].revents & POLLIN) {
-      signalfd_siginfo si;
-      while (read(signal_fd, &si, sizeof(si)) == sizeof(si))
-        if (si.ssi_signo != SIGHUP && si.ssi_signo != SIGUSR1) quit = true;
-    }
-    // Only the clients polled above (accept below appends new ones).
-    const size_t polled = pfds.size() - kFixed;
-    for (size_t i = 0; i < polled; ++i) {
-      auto& c = clients[i];
-      if (c.fd < 0 || !(pfds[kFixed + i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
-      char buf[256];
-      ssize_t n = recv(c.fd, buf, sizeof(buf), 0);
-      if (n <= 0) {
-        if (n < 0 && (errno == EAGAIN || errno == EINTR)) continue;
-        close(c.fd);
         c.fd = -1;
+        return;
+      }
+      c.in.erase(0, nl + 1);
+    }
+  }
+
+  void Accept() {
+    int cfd;
+    while ((cfd = accept4(lfd_, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK)) >= 0) {
+      // Only this relay's own uid (the plugin container runs as the same
+      // root) -- the socket's mode says so already; the kernel's peer
+      // credentials make sure.
+      ucred cred{};
+      socklen_t clen = sizeof(cred);
+      if (getsockopt(cfd, SOL_SOCKET, SO_PEERCRED, &cred, &clen) != 0 || cred.uid != geteuid()) {
+        LOG_WARN(kComp, "connection from uid %u refused", static_cast<unsigned>(cred.uid));
+        close(cfd);
         continue;
       }
-      c.in.append(buf, static_cast<size_t>(n));
-      if (c.in.size() > 4096) {  // nothing legitimate is that long
-        close(c.fd);
-        c.fd = -1;
+      if (!SendAll(cfd, Hello(false, -1))) {
+        close(cfd);
         continue;
       }
-      size_t nl;
-      while (c.fd >= 0 && (nl = c.in.find('\n')) != std::string::npos) {
-        RelayRequest rq = ParseRelayRequest(std::string_view(c.in.data(), nl));
-        if (rq.kind == "reinit") subscribe(c, rq);
-        if (rq.kind == "scan") {
-          // The connection becomes the scan's.
-          if (rq.malformed) {
-            LOG_WARN(kComp, "malformed scan request dropped");
-            close(c.fd);
-          } else {
-            scans.Submit(c.fd, std::move(rq.usage_dir), std::move(rq.cgroup));
-          }
-          c.fd = -1;
-          break;
-        }
-        c.in.erase(0, nl + 1);
-      }
+      clients_.push_back({cfd, "", next_id_++});
+      // (a scan connection every poll: not worth an info line each)
+      LOG_DEBUG(kComp, "connection accepted (%zu client(s))", clients_.size());
     }
-    if (pfds[1].revents & POLLIN) {
-      int cfd;
-      while ((cfd = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK)) >= 0) {
-        // Only this relay's own uid (the plugin container runs as the same
-        // root) -- the socket's mode says so already; the kernel's peer
-        // credentials make sure.
-        ucred cred{};
-        socklen_t clen = sizeof(cred);
-        if (getsockopt(cfd, SOL_SOCKET, SO_PEERCRED, &cred, &clen) != 0 || cred.uid != geteuid()) {
-          LOG_WARN(kComp, "connection from uid %u refused", static_cast<unsigned>(cred.uid));
-          close(cfd);
-          continue;
-        }
-        if (!SendAll(cfd, hello(false, -1))) {
-          close(cfd);
-          continue;
-        }
-        clients.push_back({cfd, "", next_id++});
-        // (a scan connection every poll: not worth an info line each)
-        LOG_DEBUG(kComp, "connection accepted (%zu client(s))", clients.size());
-      }
-    }
-    clients.erase(std::remove_if(clients.begin(), clients.end(), [](const Client& c) { return c.fd < 0; }),
-                  clients.end());
   }
-  if (reg->Shutdown()) {
-    delete reg;
-    close(ev_pipe[1]);
-    close(done_pipe[1]);
-  } else {
-    // A thread stuck in amdsmi still uses it and the pipes' write ends; the
-    // process exits next.
-    g_abandoned = reg;
+
+  smi::Library* lib_;
+  const RelayOptions opts_;
+  const int64_t stuck_ms_;
+  const std::string relay_id_;
+  const std::string drop_on_;  // test hook (ADP_DEBUG_RELAY_DROP_ON)
+  std::string socket_path_;
+  int lfd_ = -1;
+  int ev_pipe_[2] = {-1, -1}, done_pipe_[2] = {-1, -1};
+  Registration* reg_ = nullptr;
+  ScanWorker scans_;
+  std::vector<Client> clients_;
+  uint64_t next_id_ = 1;
+  // The last kRelayRingSize events forwarded, for daemons that reconnect.
+  std::deque<std::pair<uint64_t, std::string>> ring_;
+  uint64_t seq_ = 0;
+  bool stuck_ = false;
+  std::string stuck_reason_;
+  std::string pending_, done_pending_;  // bytes read from the pipes, up to the last full line
+};
+
+}  // namespace
+
+int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_fd, const RelayOptions& opts) {
+  if (socket_path.empty() || socket_path.size() >= sizeof(sockaddr_un{}.sun_path)) {
+    LOG_ERROR(kComp, "--event-relay needs --health-event-socket (a path shorter than %zu bytes)",
+              sizeof(sockaddr_un{}.sun_path));
+    return 1;
   }
-  for (auto& c : clients)
-    if (c.fd >= 0) close(c.fd);
-  for (int fd : {ev_pipe[0], done_pipe[0], lfd}) close(fd);
-  unlink(socket_path.c_str());
-  LOG_INFO(kComp, "event relay stopped");
-  return exit_code;
+  RelayServer server(lib, opts);
+  if (!server.Open(socket_path)) return 1;
+  return server.Run(signal_fd);
 }
 
 }  // namespace adp::health
