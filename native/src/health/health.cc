@@ -165,8 +165,31 @@ Status Monitor::Start() {
     }
   }
   counters_->events_enabled.store(events_ok_ ? 1 : 0);
-  // The ECC baseline is the one recorded at the first observation of the GPU,
-  // not the current count: errors that accrued across a restart still count.
+  LoadVerdicts();
+  // GPUs still waiting for GPU_POST_RESET from an earlier generation (or
+  // process): a new in-process registration cannot receive what was sent
+  // before it existed; events off receive nothing. In relay mode the relay's
+  // answer to this generation's reinit says whether anything was missed.
+  if (!events_ok_ && (!cfg_.events || cfg_.event_relay.empty()))
+    MarkGap("events off: " + events_reason_, false);
+  else if (cfg_.event_relay.empty())
+    MarkGap("amdsmi event registration renewed by a new monitor generation", false);
+  else if (relay_fd_ < 0)
+    MarkGap(events_reason_, true);
+  if (!cfg_.drain_file.empty()) ApplyDrain();  // at once, not a poll interval later
+  LOG_INFO(kComp, "health monitor watching %zu GPU(s) (events %s, poll every %d ms)", snap_->gpus.size(),
+           events_ok_ ? "on" : relay_fd_ >= 0 ? "through the relay, once it answers" : "off", cfg_.poll_interval_ms);
+  if (!events_ok_ && cfg_.poll_interval_ms == 0 && (cfg_.event_relay.empty() || !cfg_.events)) return Status::Ok();
+  stop_.store(false);
+  if (wake_fd_ < 0) wake_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  thread_ = std::thread([this] { Run(); });
+  return Status::Ok();
+}
+
+// Each GPU's verdict and ECC baseline from the ledger: the baseline is the
+// one recorded at the first observation of the GPU, not the current count, so
+// errors that accrued across a restart still count.
+void Monitor::LoadVerdicts() {
   for (const auto& g : snap_->gpus) {
     void* h = snap_->procs[g.partitions.front().handle].handle;
     auto ecc = lib_->UncorrectableErrors(h);
@@ -199,24 +222,6 @@ Status Monitor::Start() {
       Notify(g.index, false, r.reason);
     }
   }
-  // GPUs still waiting for GPU_POST_RESET from an earlier generation (or
-  // process): a new in-process registration cannot receive what was sent
-  // before it existed; events off receive nothing. In relay mode the relay's
-  // answer to this generation's reinit says whether anything was missed.
-  if (!events_ok_ && (!cfg_.events || cfg_.event_relay.empty()))
-    MarkGap("events off: " + events_reason_, false);
-  else if (cfg_.event_relay.empty())
-    MarkGap("amdsmi event registration renewed by a new monitor generation", false);
-  else if (relay_fd_ < 0)
-    MarkGap(events_reason_, true);
-  if (!cfg_.drain_file.empty()) ApplyDrain();  // at once, not a poll interval later
-  LOG_INFO(kComp, "health monitor watching %zu GPU(s) (events %s, poll every %d ms)", snap_->gpus.size(),
-           events_ok_ ? "on" : relay_fd_ >= 0 ? "through the relay, once it answers" : "off", cfg_.poll_interval_ms);
-  if (!events_ok_ && cfg_.poll_interval_ms == 0 && (cfg_.event_relay.empty() || !cfg_.events)) return Status::Ok();
-  stop_.store(false);
-  if (wake_fd_ < 0) wake_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
-  thread_ = std::thread([this] { Run(); });
-  return Status::Ok();
 }
 
 void Monitor::Sleep(int ms) {

@@ -314,6 +314,7 @@ class Monitor {
   void Run();
   void Notify(int gpu, bool healthy, const std::string& reason);
   void PollOnce();
+  void LoadVerdicts();  // Start(): the verdicts, ECC baselines and retired-page thresholds of the GPUs
   // PollOnce's parts, per GPU (h: its first processor's handle). PollLayout:
   // true when the partition modes or xGMI links changed (the supervisor
   // re-enumerates); PollLiveness: whether amdsmi answers (and the polled
