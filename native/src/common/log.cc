@@ -68,7 +68,17 @@ const char* LevelName(LogLevel l) {
 
 void SetLogLevel(LogLevel l) { g_level.store(static_cast<int>(l)); }
 LogLevel GetLogLevel() { return static_cast<LogLevel>(g_level.load()); }
-bool LogEnabled(LogLevel l) { return static_cast<int>(l) >= g_level.load(std::memory_order_relaxed); }
+namespace {
+thread_local int t_quiet = 0;
+}  // namespace
+
+QuietLogs::QuietLogs() { ++t_quiet; }
+QuietLogs::~QuietLogs() { --t_quiet; }
+
+bool LogEnabled(LogLevel l) {
+  if (t_quiet > 0 && l < LogLevel::kError) return false;
+  return static_cast<int>(l) >= g_level.load(std::memory_order_relaxed);
+}
 
 void Logf(LogLevel l, const char* component, const char* fmt, ...) {
   // Most lines fit the stack buffer; longer ones (SIGUSR1 stats with a

@@ -20,6 +20,16 @@ bool LogEnabled(LogLevel l);
 void Logf(LogLevel l, const char* component, const char* fmt, ...)
     __attribute__((format(printf, 3, 4)));
 
+// While one lives, this thread logs errors only (e.g. objects built just to
+// look at what they would do; other threads log as before).
+class QuietLogs {
+ public:
+  QuietLogs();
+  ~QuietLogs();
+  QuietLogs(const QuietLogs&) = delete;
+  QuietLogs& operator=(const QuietLogs&) = delete;
+};
+
 }  // namespace adp
 
 #define ADP_LOG(level, comp, ...)                                  \

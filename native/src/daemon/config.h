@@ -63,6 +63,7 @@ struct Flags {
   uint64_t reset_recovery_hold_ms = 120000;  // polled recovery of a GPU_POST_RESET lost in an event gap (0 = off)
   uint64_t reset_flap_limit = 3;             // resets within the window that quarantine a GPU (0 = off)
   uint64_t reset_flap_window_ms = 600000;
+  bool defer_layout_changes = false;  // keep serving the old layout while pods hold IDs it would re-mean
   std::string drain, undrain;  // one-shot: add / remove GPUs in the drain file, then exit
   std::string return_to_service;  // one-shot: ask the running daemon to clear GPUs' verdicts, then exit
   uint64_t server_threads = 0;  // 0 -> plugin::DefaultServerThreads()

@@ -139,6 +139,13 @@ void AppendDaemonMetrics(const DaemonMetricsInput& in, std::string* out) {
       Sample(out, "amdgpu_dp_replica_layout_changes_with_live_allocations_total",
              "resource=\"" + metrics::LabelValue(res) + "\"", Num(n));
   }
+  if (!in.deferred_layouts.empty()) {
+    Family(out, "amdgpu_dp_deferred_layout_change", "gauge",
+           "1 while a config change that would re-mean this resource's IDs waits for the running pods holding "
+           "some (--defer-layout-changes).");
+    for (const auto& res : in.deferred_layouts)
+      Sample(out, "amdgpu_dp_deferred_layout_change", "resource=\"" + metrics::LabelValue(res) + "\"", "1");
+  }
   if (in.pod_resources_up >= 0) {
     Family(out, "amdgpu_dp_pod_resources_up", "gauge", "1 if the kubelet PodResources API answered.");
     Sample(out, "amdgpu_dp_pod_resources_up", "", in.pod_resources_up ? "1" : "0");

@@ -38,6 +38,8 @@ struct DaemonMetricsInput {
   const memcap::DriverHbmMonitor::Snapshot* driver_hbm = nullptr;  // null: the check is off
   // Per resource: restarts that changed what its IDs mean while running pods held some.
   std::map<std::string, uint64_t> layout_changes_live;
+  // --defer-layout-changes: resources whose config change waits for running pods.
+  std::vector<std::string> deferred_layouts;
 };
 
 void AppendDaemonMetrics(const DaemonMetricsInput& in, std::string* out);

@@ -179,7 +179,7 @@ class Supervisor {
       health_counters_.PersistRelayCursor(cfg_.flags.health_state_file + ".relay");
   }
   ~Supervisor() {
-    for (int fd : {ep_, ifd_, tfd_, efd_, lfd_, rfd_})
+    for (int fd : {ep_, ifd_, tfd_, efd_, lfd_, rfd_, dfd_})
       if (fd >= 0) close(fd);
   }
 
@@ -213,6 +213,10 @@ class Supervisor {
         } else if (fd == rfd_) {
           Drain(rfd_, &x);
           OnSocketRecheck(&do_reregister);
+        } else if (fd == dfd_) {
+          Drain(dfd_, &x);
+          const std::string before = cfg_.ToJson();
+          if (ReloadConfig("deferred config change") && cfg_.ToJson() != before) do_restart = true;
         } else if (fd == efd_) {
           Drain(efd_, &x);
           LOG_ERROR(kComp, "a gRPC server exhausted its crash budget; exiting");
@@ -278,8 +282,10 @@ class Supervisor {
     lfd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);  // health monitor: partition layout changed
     // One-shot: look again at plugin sockets deleted from under us (recheck_sockets_).
     rfd_ = timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC | TFD_NONBLOCK);
+    // One-shot: look again at a config change deferred for live grants.
+    dfd_ = timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC | TFD_NONBLOCK);
     ep_ = epoll_create1(EPOLL_CLOEXEC);
-    for (int fd : {sfd_, ifd_, tfd_, efd_, lfd_, rfd_}) {
+    for (int fd : {sfd_, ifd_, tfd_, efd_, lfd_, rfd_, dfd_}) {
       epoll_event ev{};
       ev.events = EPOLLIN;
       ev.data.fd = fd;
@@ -311,6 +317,7 @@ class Supervisor {
       std::lock_guard<std::mutex> lk(access_mu_);
       in.node_access = node_access_;
       in.layout_changes_live = layout_changes_live_;
+      in.deferred_layouts.assign(deferred_layouts_.begin(), deferred_layouts_.end());
       for (const auto& [key, bdf] : metrics_gpus_) {
         uint32_t fail = ledger_.Get(key).fail;
         health::GapMark m;
@@ -739,12 +746,83 @@ class Supervisor {
     merged.flags.health_state_file = was.health_state_file;
     auto mv = Validate(merged);
     if (!mv.ok()) return false;
-    if (merged.ToJson() != old_json) {
+    if (merged.ToJson() == old_json) {
+      ForgetDeferral();  // (an edit undone while deferred)
+      return true;
+    }
+    if (merged.flags.defer_layout_changes && DeferLayoutChange(merged, *mv, why)) return false;
+    ForgetDeferral();
+    {
       cfg_ = std::move(merged);
       v_ = std::move(*mv);
       LOG_INFO(kComp, "%s: reloaded config:\n%s", why, cfg_.ToJson().c_str());
       LOG_INFO(kComp, "running with resource config: %s", v_.rc.ToJson().c_str());
     }
+    return true;
+  }
+
+  void ForgetDeferral() {
+    ArmTimer(dfd_, 0);
+    std::lock_guard<std::mutex> lk(access_mu_);
+    deferred_layouts_.clear();
+  }
+
+  // --defer-layout-changes: true (and the timer armed) when `next` would change
+  // what a resource's IDs mean while running pods hold some of them. The
+  // layouts are those of plugins built from the current devices, not started.
+  bool DeferLayoutChange(const Config& next, const Validated& nv, const char* why) {
+    static const int recheck_ms = [] {  // test hook (default: every 30 s)
+      const char* e = getenv("ADP_DEFER_RECHECK_MS");
+      return e && atoi(e) > 0 ? atoi(e) : 30000;
+    }();
+    if (!cur_snap_) return false;
+    auto specs = strategy::BuildPluginSpecs(*cur_snap_, nv.partition, nv.rc, next.flags.resource_prefix);
+    if (!specs.ok()) return false;  // the restart says why
+    plugin::PluginOptions po = nv.popts;
+    po.quiet = true;
+    std::map<std::string, std::string> after, now;
+    for (const auto& sp : *specs) {
+      plugin::Plugin p(cur_snap_, sp, po);
+      if (p.device_count() > 0) after[p.resource_name()] = p.ReplicaLayout();
+    }
+    {
+      std::lock_guard<std::mutex> lk(plugins_mu_);
+      for (const auto& p : plugins_)
+        if (p->device_count() > 0) now[p->resource_name()] = p->ReplicaLayout();
+    }
+    std::set<std::string> changed;  // IDs that would mean something else, or vanish
+    for (const auto& [res, lay] : now) {
+      auto it = after.find(res);
+      if (!lay.empty() && (it == after.end() || it->second != lay)) changed.insert(res);
+    }
+    if (changed.empty()) return false;
+    if (cfg_.flags.pod_resources_socket.empty()) {
+      LOG_WARN(kComp, "%s: --defer-layout-changes needs the kubelet's PodResources socket; applying", why);
+      return false;
+    }
+    auto live = podresources::List(cfg_.flags.pod_resources_socket, 1000);
+    if (!live.ok()) {
+      LOG_WARN(kComp, "%s: whether running pods hold IDs of the resources this change re-means is unknown (%s); "
+               "applying", why, live.status().ToString().c_str());
+      return false;
+    }
+    std::set<std::string> held;
+    for (const auto& a : *live)
+      if (changed.count(a.resource)) held.insert(a.resource);
+    if (held.empty()) return false;
+    std::string names;
+    for (const auto& r : held) names += (names.empty() ? "'" : ", '") + r + "'";
+    bool first;
+    {
+      std::lock_guard<std::mutex> lk(access_mu_);
+      first = deferred_layouts_ != held;
+      deferred_layouts_ = held;
+    }
+    if (first)
+      LOG_WARN(kComp, "%s: config change deferred: running pods hold IDs of %s, which it would re-mean; the "
+               "current layout is served until they end (looked at every %d s; --defer-layout-changes)", why,
+               names.c_str(), recheck_ms / 1000);
+    ArmTimer(dfd_, recheck_ms);
     return true;
   }
 
@@ -903,6 +981,10 @@ class Supervisor {
   std::vector<inventory::NodeAccess> node_access_;
   std::vector<std::pair<std::string, std::string>> metrics_gpus_;  // (ledger key, bdf) of the served GPUs
   std::map<std::string, uint64_t> layout_changes_live_;  // per resource (CheckReplicaLayouts)
+  // --defer-layout-changes: resources whose layout change waits for the pods
+  // holding their IDs (under access_mu_), and the timer that looks again.
+  std::set<std::string> deferred_layouts_;
+  int dfd_ = -1;
   std::map<std::string, std::string> layouts_;  // resource -> Plugin::ReplicaLayout of the running generation
   bool layouts_loaded_ = false;
   std::string layouts_written_;  // the replica-layout file's body as last written

@@ -131,7 +131,12 @@ Plugin::Plugin(std::shared_ptr<const inventory::Snapshot> snap, strategy::Plugin
                PluginOptions opts)
     : snap_(std::move(snap)), spec_(std::move(spec)), opts_(std::move(opts)) {
   if (opts_.kubelet_socket.empty()) opts_.kubelet_socket = PathJoin(opts_.plugin_dir, "kubelet.sock");
-  BuildUnits();
+  if (opts_.quiet) {
+    QuietLogs q;
+    BuildUnits();
+  } else {
+    BuildUnits();
+  }
 }
 
 Plugin::~Plugin() { Stop(); }

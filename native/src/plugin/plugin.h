@@ -97,6 +97,8 @@ struct PluginOptions {
   bool cu_slot_units = false;
   int dial_timeout_ms = 5000;             // server.go:208,219
   bool register_with_kubelet = true;
+  // Built only to see what it would advertise (Plugin::ReplicaLayout): no log lines.
+  bool quiet = false;
   bool trace = false;                     // log every RPC with its handler time
   std::string cdi_spec_dir = "/var/run/cdi";  // where cdi-* strategies write the CDI spec
   int server_threads = 0;                 // gRPC loops; <=0 -> DefaultServerThreads()

@@ -420,3 +420,18 @@ def test_reset_recovery_and_flap_values(values, hold, limit, window):
     e = env(ds)
     assert (e["DP_RESET_RECOVERY_HOLD_MS"], e["DP_RESET_FLAP_LIMIT"], e["DP_RESET_FLAP_WINDOW_MS"]) == \
         (hold, limit, window)
+
+
+def test_defer_layout_changes_value_mounts_pod_resources():
+    """deferLayoutChanges reaches the daemon and mounts the kubelet's
+    PodResources socket (which IDs running pods hold) even without metrics."""
+    e = env(daemonset())
+    assert e["DP_DEFER_LAYOUT_CHANGES"] == "false"
+    ds = daemonset({"deferLayoutChanges": True})
+    check_consistent(ds)
+    assert env(ds)["DP_DEFER_LAYOUT_CHANGES"] == "true"
+    mounts = {m["name"]: m for m in container(ds)["volumeMounts"]}
+    assert mounts["pod-resources"]["readOnly"] is True
+    assert any(v["name"] == "pod-resources" for v in ds["spec"]["template"]["spec"]["volumes"])
+    ds0 = daemonset()
+    assert "pod-resources" not in {m["name"] for m in container(ds0)["volumeMounts"]}

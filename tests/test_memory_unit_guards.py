@@ -189,3 +189,50 @@ def test_a_resource_absent_for_a_while_keeps_its_layout(scratch):
         d.stop()
         k.stop()
         pr.stop()
+
+
+def test_a_layout_change_under_live_grants_can_wait_for_the_pods(scratch):
+    """--defer-layout-changes: a config change that would re-mean IDs running
+    pods hold does not apply while they run -- the current layout keeps being
+    served (amdgpu_dp_deferred_layout_change says so) -- and applies by itself
+    once they are gone, with no over-commit in between."""
+    pr_sock = os.path.join(scratch + ".fixture", "pod-resources.sock")
+    os.makedirs(os.path.dirname(pr_sock), exist_ok=True)
+    pr = PodResourcesStub(pr_sock)
+    cfg = os.path.join(scratch + ".fixture", "config.yaml")
+    _config(cfg, "mib")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(2), args=[
+        "--config-file", cfg, "--metrics-addr", "127.0.0.1:0", "--pod-resources-socket", pr_sock,
+        "--defer-layout-changes"], env={"ADP_DEFER_RECHECK_MS": "300"}).start()
+    port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics")).group(1))
+    try:
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        c.close()
+        res = "amd.com/gpu-mem-gb"
+        pr.payload = _list_response([("ml", "train", "main", res, [ids[0], ids[100]])])
+        _config(cfg, "auto")  # -> CU slots: what the held IDs mean would change
+        log = d.wait_log("config change deferred")
+        assert f"running pods hold IDs of '{res}'" in log
+        time.sleep(1.0)  # three rechecks: still deferred, still the old layout
+        assert "what its IDs mean changed while" not in d.log() and d.log().count("config change deferred") == 1
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        assert len(c.watch()[0].get(timeout=5).devices) == len(ids)
+        c.close()
+        s = _parse(_get(port, "/metrics")[1])
+        assert _value(s, "amdgpu_dp_deferred_layout_change", resource=res) == 1
+        pr.payload = _list_response([])  # the pod ended
+        reg = k.wait_registration(15)  # the change applied: the plugin restarts with it
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        assert len(c.watch()[0].get(timeout=5).devices) == 64  # 32 CU slots per GPU
+        c.close()
+        assert "deferred config change: reloaded config" in d.log()
+        assert "what its IDs mean changed while" not in d.log()
+        s = _parse(_get(port, "/metrics")[1])
+        assert not [v for (n, ls), v in s.items() if n == "amdgpu_dp_deferred_layout_change"]
+    finally:
+        d.stop()
+        k.stop()
+        pr.stop()
