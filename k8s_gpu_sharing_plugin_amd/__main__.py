@@ -190,6 +190,9 @@ def _status(args) -> int:
         size = (f"{sizes[0][0]} MiB" if len(sizes) == 1 else
                 f"{sizes[0][0]}..{sizes[-1][0]} MiB")
         print(f"{res}: one unit = {size} ({', '.join(sorted({k for _, k in sizes}))})")
+    for ls, v in by("amdgpu_dp_deferred_layout_change"):
+        if v:
+            print(f"DEFERRED {ls.get('resource')}: a config change waits for the running pods holding its IDs")
     stale = [(ls.get("resource"), v) for ls, v in by("amdgpu_dp_stale_allocated_ids") if v]
     for res, v in stale:
         print(f"STALE {res}: {int(v)} ID(s) running pods hold are no longer advertised (the layout changed "

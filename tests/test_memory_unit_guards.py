@@ -223,6 +223,9 @@ def test_a_layout_change_under_live_grants_can_wait_for_the_pods(scratch):
         c.close()
         s = _parse(_get(port, "/metrics")[1])
         assert _value(s, "amdgpu_dp_deferred_layout_change", resource=res) == 1
+        st = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "status",
+                             f"http://127.0.0.1:{port}/metrics"], capture_output=True, text=True, timeout=60)
+        assert f"DEFERRED {res}: a config change waits" in st.stdout, st.stdout
         pr.payload = _list_response([])  # the pod ended
         reg = k.wait_registration(15)  # the change applied: the plugin restarts with it
         c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
