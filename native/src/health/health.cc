@@ -45,6 +45,18 @@ const char* EventName(uint32_t t) {
 }
 }  // namespace
 
+std::string DescribeFailures(uint32_t bits) {
+  static const std::pair<uint32_t, const char*> kNames[] = {
+      {kFailResetPending, "waiting for GPU_POST_RESET"}, {kFailFlapping, "resetting too often"},
+      {kFailEcc, "uncorrectable ECC errors"},            {kFailRetiredPages, "retired HBM pages"},
+      {kFailUnresponsive, "not responding"},             {kFailEvent, "an amdsmi event"},
+      {kFailDrained, "drained by the operator"}};
+  std::string out;
+  for (const auto& [bit, name] : kNames)
+    if (bits & bit) out += (out.empty() ? "" : ", ") + std::string(name);
+  return out;
+}
+
 std::vector<uint64_t> ParseAdditionalIds(std::string_view input) {
   std::vector<uint64_t> out;
   if (input.empty()) return out;
@@ -642,6 +654,7 @@ void Monitor::Update(int gpu, uint32_t set, uint32_t clear, const std::string& r
   r.fail = after;
   if (!after) r.reason.clear();
   else if (set & ~before) r.reason = reason;
+  else if (clear & before) r.reason = "still: " + DescribeFailures(after);  // the old reason may be the cleared one
   ledger_->Put(keys_[gpu], r);
   if ((before == 0) != (after == 0)) {
     Notify(gpu, after == 0, reason);

@@ -74,6 +74,8 @@ namespace adp::health {
 
 // getAdditionalXids semantics: split on ',', trim, keep valid unsigned values in order.
 std::vector<uint64_t> ParseAdditionalIds(std::string_view input);
+// What failure bits (FailBits) hold a GPU out, in words: "drained by the operator, ...".
+std::string DescribeFailures(uint32_t bits);
 
 struct HealthConfig {
   bool disabled = false;

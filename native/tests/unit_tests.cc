@@ -261,6 +261,10 @@ static void TestLedgerGaps() {
     CHECK(!cursor_from("adp-relay-cursor v1\n" + std::string(10000, 'x') + "\t1\t1\n").valid);
     unlink(tmpl);
   }
+  CHECK(health::DescribeFailures(health::kFailDrained) == "drained by the operator");
+  CHECK(health::DescribeFailures(health::kFailEcc | health::kFailResetPending) ==
+        "waiting for GPU_POST_RESET, uncorrectable ECC errors");
+  CHECK(health::DescribeFailures(0).empty());
   l.ClearResets("d");  // --return-to-service
   CHECK(l.Get("d").resets.empty() && l.RecordReset("d", 1700, 500) == 1);
   // an older file (no field) and a malformed field: no history, the line kept
