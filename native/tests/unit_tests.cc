@@ -245,9 +245,9 @@ static void TestLedgerGaps() {
     char tmpl[] = "/tmp/adp-cursor-XXXXXX";
     int fd = mkstemp(tmpl);
     close(fd);
-    auto cursor_from = [&](const std::string& body) {
+    auto cursor_from = [&](const std::string& text) {
       FILE* f = fopen(tmpl, "w");
-      fputs(body.c_str(), f);
+      fputs(text.c_str(), f);
       fclose(f);
       health::HealthCounters hc;
       hc.PersistRelayCursor(tmpl);
