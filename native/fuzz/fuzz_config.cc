@@ -36,7 +36,7 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         auto it = again.find(k);
         same = same && it != again.end() && it->second.fail == r.fail && it->second.reason == r.reason &&
                it->second.has_baseline == r.has_baseline && it->second.ecc_baseline == r.ecc_baseline &&
-               it->second.ecc_seen == r.ecc_seen && it->second.resets == r.resets;
+               it->second.ecc_seen == r.ecc_seen && it->second.resets == r.resets && it->second.gap == r.gap;
       }
       if (!same) {
         fprintf(stderr, "invariant violated: the health state does not survive a write and a re-read\n");

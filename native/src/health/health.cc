@@ -178,6 +178,16 @@ Status Monitor::Start() {
   }
   counters_->events_enabled.store(events_ok_ ? 1 : 0);
   LoadVerdicts();
+  // A confirmed gap from before this process (the state file): this process's
+  // own link to the events may miss nothing, and the wait still has to end.
+  for (const auto& g : snap_->gpus) {
+    const std::string gap = ledger_->Get(keys_[g.index]).gap;
+    if (gap.empty() || !(fail_[g.index] & kFailResetPending)) continue;
+    if (ledger_->MarkGap(keys_[g.index], gap, false, NowMs()))
+      LOG_WARN(kComp, "GPU %s waits for GPU_POST_RESET across an event gap from before this process (%s): back in "
+               "service once amdsmi has answered every poll for %g s", g.bdf.c_str(), gap.c_str(),
+               static_cast<double>(cfg_.reset_recovery_hold_ms) / 1000.0);
+  }
   // GPUs still waiting for GPU_POST_RESET from an earlier generation (or
   // process): a new in-process registration cannot receive what was sent
   // before it existed; events off receive nothing. In relay mode the relay's

@@ -138,6 +138,10 @@ struct GpuRecord {
   // kept with the verdict, so a plugin container restart does not reset the
   // count or shorten a quarantine.
   std::vector<int64_t> resets;
+  // A confirmed event gap this GPU is waiting across (why; "" = none): kept
+  // with the verdict, so a process started after it -- whose own connection
+  // to the relay may miss nothing -- still lets the polled check end the wait.
+  std::string gap;
 };
 
 // Liveness of the health machinery itself, shared by all Monitor generations
@@ -254,7 +258,8 @@ class Ledger {
   // File format, exposed for tests: "adp-health v1" header, then one
   // tab-separated line per GPU: key, ecc baseline ("-" = none), highest ECC
   // count seen, fail bits, reason, and -- when there are any -- the recent
-  // resets as "resets=<ms>,<ms>,..." (a field older versions ignore).
+  // resets as "resets=<ms>,<ms>,..." and a confirmed event gap as "gap=<why>"
+  // (fields older versions ignore).
   static std::string Serialize(const std::map<std::string, GpuRecord>& m);
   static std::map<std::string, GpuRecord> Parse(const std::string& body);
 

@@ -83,6 +83,12 @@ std::string Ledger::Serialize(const std::map<std::string, GpuRecord>& m) {
       out += "\tresets=";
       for (size_t i = 0; i < r.resets.size(); ++i) out += (i ? "," : "") + std::to_string(r.resets[i]);
     }
+    if (!r.gap.empty()) {
+      std::string gap = r.gap;
+      for (auto& c : gap)
+        if (c == '\t' || c == '\n' || c == '\r') c = ' ';
+      out += "\tgap=" + gap;
+    }
     out += "\n";
   }
   return out;
@@ -128,15 +134,20 @@ std::map<std::string, GpuRecord> Ledger::Parse(const std::string& body) {
     if (f.size() > 4) r.reason = f[4];
     for (auto& c : r.reason)
       if (c == '\r') c = ' ';  // as Serialize writes it
-    if (f.size() > 5 && f[5].rfind("resets=", 0) == 0) {
-      for (const auto& t : Split(std::string_view(f[5]).substr(7), ',')) {
-        auto v = ParseUint(t);
-        if (!v || r.resets.size() >= 64) {
-          LOG_WARN(kComp, "health state: reset history of %s malformed; ignored", f[0].c_str());
-          r.resets.clear();
-          break;
+    // Extension fields ("name=value"), each at most once; unknown ones ignored.
+    for (size_t i = 5; i < f.size(); ++i) {
+      if (f[i].rfind("resets=", 0) == 0 && r.resets.empty()) {
+        for (const auto& t : Split(std::string_view(f[i]).substr(7), ',')) {
+          auto v = ParseUint(t);
+          if (!v || r.resets.size() >= 64) {
+            LOG_WARN(kComp, "health state: reset history of %s malformed; ignored", f[0].c_str());
+            r.resets.clear();
+            break;
+          }
+          r.resets.push_back(static_cast<int64_t>(*v));
         }
-        r.resets.push_back(static_cast<int64_t>(*v));
+      } else if (f[i].rfind("gap=", 0) == 0 && r.gap.empty() && f[i].size() > 4) {
+        r.gap = f[i].substr(4);
       }
     }
     out[f[0]] = std::move(r);
@@ -161,11 +172,13 @@ void Ledger::Put(const std::string& key, const GpuRecord& r) {
   if (it != recs_.end() && it->second.has_baseline == r.has_baseline && it->second.ecc_baseline == r.ecc_baseline &&
       it->second.ecc_seen == r.ecc_seen && it->second.fail == r.fail && it->second.reason == r.reason)
     return;
-  // The reset history is the ledger's own (RecordReset): a record read
-  // earlier does not roll it back.
+  // The reset history and the gap are the ledger's own (RecordReset,
+  // MarkGap): a record read earlier does not roll them back.
   std::vector<int64_t> resets = it != recs_.end() ? std::move(it->second.resets) : std::vector<int64_t>{};
+  std::string gap = it != recs_.end() ? std::move(it->second.gap) : std::string();
   recs_[key] = r;
   recs_[key].resets = std::move(resets);
+  recs_[key].gap = std::move(gap);
   SaveLocked();
 }
 
@@ -186,16 +199,20 @@ void Ledger::SaveLocked() const {
 bool Ledger::MarkGap(const std::string& key, const std::string& why, bool tentative, int64_t now_ms) {
   std::lock_guard<std::mutex> lk(mu_);
   auto it = gaps_.find(key);
+  bool marked = false;
   if (it == gaps_.end()) {
     gaps_[key] = GapMark{now_ms, why, tentative, 0};
-    return true;
-  }
-  if (it->second.tentative && !tentative) {  // confirmed: the relay could not replay what was missed
+    marked = true;
+  } else if (it->second.tentative && !tentative) {  // confirmed: the relay could not replay what was missed
     it->second.tentative = false;
     it->second.why = why;
-    return true;
+    marked = true;
   }
-  return false;
+  if (auto r = recs_.find(key); marked && !tentative && r != recs_.end()) {
+    r->second.gap = why;  // a confirmed gap outlives this process (GpuRecord::gap)
+    SaveLocked();
+  }
+  return marked;
 }
 
 std::vector<std::string> Ledger::CancelTentativeGaps() {
@@ -215,6 +232,10 @@ std::vector<std::string> Ledger::CancelTentativeGaps() {
 void Ledger::ClearGap(const std::string& key) {
   std::lock_guard<std::mutex> lk(mu_);
   gaps_.erase(key);
+  if (auto it = recs_.find(key); it != recs_.end() && !it->second.gap.empty()) {
+    it->second.gap.clear();
+    SaveLocked();
+  }
 }
 
 bool Ledger::Gap(const std::string& key, GapMark* out) const {

@@ -202,11 +202,13 @@ static void TestLedgerGaps() {
   CHECK(cancelled.size() == 1 && cancelled[0] == "b" && !l.Gap("b", nullptr) && l.Gap("a", nullptr));
   l.ClearGap("a");
   CHECK(!l.Gap("a", nullptr));
-  // gaps are not part of the state file
+  // a confirmed gap is part of the state file (a tentative one is not)
   health::GpuRecord r;
   r.fail = health::kFailResetPending;
   l.Put("c", r);
   l.MarkGap("c", "x", false, 1);
+  CHECK(health::Ledger::Serialize(l.All()) == "adp-health v1\nc\t-\t0\t4\t\tgap=x\n");
+  l.ClearGap("c");
   CHECK(health::Ledger::Serialize(l.All()) == "adp-health v1\nc\t-\t0\t4\t\n");
   // reset history for flap damping: a sliding window
   CHECK(l.RecordReset("d", 1000, 500) == 1);
@@ -260,6 +262,26 @@ static void TestLedgerGaps() {
     CHECK(!cursor_from("something else\nab12\t7\t3\n").valid);
     CHECK(!cursor_from("adp-relay-cursor v1\n" + std::string(10000, 'x') + "\t1\t1\n").valid);
     unlink(tmpl);
+  }
+  {
+    // a confirmed gap is written with the verdict (a tentative one is not),
+    // survives Put() of an earlier record, and goes with ClearGap
+    health::Ledger lg;
+    health::GpuRecord rp;
+    rp.fail = health::kFailResetPending;
+    lg.Put("p", rp);
+    lg.MarkGap("p", "the relay restarted", true, 5);
+    CHECK(lg.Get("p").gap.empty());
+    lg.MarkGap("p", "the relay restarted", false, 6);  // confirmed
+    CHECK(lg.Get("p").gap == "the relay restarted");
+    lg.Put("p", rp);
+    std::string body = health::Ledger::Serialize(lg.All());
+    CHECK(body.find("\tgap=the relay restarted\n") != std::string::npos);
+    CHECK(health::Ledger::Parse(body)["p"].gap == "the relay restarted");
+    CHECK(health::Ledger::Parse("adp-health v1\nq\t-\t0\t4\tr\tgap=x\tresets=1,2\n")["q"].resets.size() == 2);
+    CHECK(health::Ledger::Parse("adp-health v1\nq\t-\t0\t4\tr\tgap=x\tresets=1,2\n")["q"].gap == "x");
+    lg.ClearGap("p");
+    CHECK(lg.Get("p").gap.empty() && !lg.Gap("p", nullptr));
   }
   CHECK(health::DescribeFailures(health::kFailDrained) == "drained by the operator");
   CHECK(health::DescribeFailures(health::kFailEcc | health::kFailResetPending) ==

@@ -866,3 +866,42 @@ def test_chaos_of_resets_restarts_and_drops_leaves_no_gpu_stuck(scratch, seed):
                 assert any(f"GPU {bdf} waits for GPU_POST_RESET across an event gap" in p for p in log[:i]), ln
     finally:
         n.stop()
+
+
+def test_a_gap_confirmed_before_a_container_restart_still_ends_the_wait(scratch):
+    """GPU_PRE_RESET, then the relay restarts mid-reset (its POST_RESET is
+    lost: a confirmed gap), then the plugin container restarts before the
+    polled hold has passed. The new process connects to the same relay with its
+    cursor and misses nothing from there on -- but the gap is in the state file,
+    so the polled check still returns the GPU (without it, the GPU would wait
+    for a POST_RESET that will never come)."""
+    state = os.path.join(scratch + ".fixture", "health.state")
+    args = ["--health-state-file", state, "--reset-recovery-hold-ms", "1500"]
+    n = RelayNode(scratch, daemon_args=args)
+    try:
+        n.d.wait_log("events on through the relay")
+        n.inject("1 3 mode1 reset")
+        assert n.health() == ["Healthy", "Unhealthy"]
+        n.relay.proc.kill()
+        n.relay.proc.wait(timeout=10)
+        n.start_relay()
+        n.d.wait_log("waits for GPU_POST_RESET across an event gap")
+        line = [ln for ln in open(state).read().splitlines() if ln.startswith(n.fx["gpus"][1]["uuid"])][0]
+        assert "\tgap=" in line, line
+        n.call.cancel()
+        n.c.close()
+        assert n.d.stop() == 0  # before the hold has passed
+        assert "recovered without GPU_POST_RESET" not in n.d.log()
+        n.d = harness.Daemon(scratch, n.fx, args=["--health-event-socket", n.sock, *args],
+                             env={"LD_PRELOAD": _preload(SIM), "DP_HEALTH_POLL_MS": "200"}).start()
+        first = n.rewatch()
+        assert first == ["Healthy", "Unhealthy"], first
+        log = n.d.wait_log("across an event gap from before this process")
+        assert n.bdf(1) in log
+        n.relay.wait_log("daemon connected for events (nothing missed)")  # its own link missed nothing
+        assert n.wait_health(["Healthy", "Healthy"], timeout=10) == ["Healthy", "Healthy"]
+        assert "recovered without GPU_POST_RESET" in n.d.log()
+        line = [ln for ln in open(state).read().splitlines() if ln.startswith(n.fx["gpus"][1]["uuid"])][0]
+        assert "gap=" not in line and line.split("\t")[3] == "0", line
+    finally:
+        n.stop()
