@@ -411,9 +411,12 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
                         "not outlive a container restart");
     // What it holds against this node's GPUs now (the operator's next question).
     health::Ledger ledger(f.health_state_file);
-    for (const auto& [gpu, reason] : ledger.Failed(s))
+    for (const auto& [gpu, reason] : ledger.Failed(s)) {
+      const std::string gap = ledger.Get(health::Ledger::KeyOf(s.gpus[gpu])).gap;
       d.Line("warn", "GPU " + s.gpus[gpu].bdf + " is out of service by the state file: " + reason +
+                         (gap.empty() ? "" : " (after an event gap -- " + gap + " -- the polled check returns it)") +
                          " -- once repaired, --return-to-service " + s.gpus[gpu].bdf);
+    }
   }
   if (!f.drain_file.empty() && access((f.drain_file + ".return").c_str(), F_OK) == 0)
     d.Line("warn", "a return-to-service request is waiting in " + f.drain_file + ".return: no running daemon "

@@ -177,7 +177,8 @@ def test_verdicts_in_the_state_file_and_a_waiting_request_are_named(tmp_path):
     d = tmp_path / "dp"
     d.mkdir()
     state = tmp_path / "health.state"
-    state.write_text(f"adp-health v1\n{fx['gpus'][1]['uuid']}\t-\t0\t4\tGPU_PRE_RESET: mode1 reset\n")
+    state.write_text(f"adp-health v1\n{fx['gpus'][1]['uuid']}\t-\t0\t4\tGPU_PRE_RESET: mode1 reset"
+                     "\tgap=the event relay restarted\n")
     drain = tmp_path / "drain"
     (tmp_path / "drain.return").write_text("0\n")
     rc, lines = _doctor(tmp_path, "--device-plugin-path", str(d), "--health-state-file", str(state),
@@ -186,5 +187,6 @@ def test_verdicts_in_the_state_file_and_a_waiting_request_are_named(tmp_path):
     line = _find(lines, f"GPU {bdf1} is out of service by the state file")
     assert line and line.startswith("warn") and "GPU_PRE_RESET: mode1 reset" in line, lines
     assert f"--return-to-service {bdf1}" in line
+    assert "after an event gap -- the event relay restarted -- the polled check returns it" in line
     assert _find(lines, f"GPU {fx['gpus'][0]['bdf']} is out of service") is None
     assert _find(lines, "a return-to-service request is waiting"), lines
