@@ -839,11 +839,11 @@ class Supervisor {
     for (const auto& p : plugins_)
       if (p->running() && p->owns_socket()) return;
     if (monitor_) {
-      LOG_WARN(kComp, "no plugin of this instance serves: its health monitor pauses (the serving instance keeps "
-               "the health verdicts)");
-      monitor_->Stop();
+      monitor_->Stop();  // (its last poll may still be running: the log line follows it)
       monitor_.reset();
       standby_ = true;
+      LOG_WARN(kComp, "no plugin of this instance serves: its health monitor pauses (the serving instance keeps "
+               "the health verdicts)");
     }
   }
 

@@ -690,7 +690,7 @@ def test_a_standing_by_instance_pauses_its_health_monitor(scratch, tmp_path):
         with open(req, "w") as f:
             f.write(fx["gpus"][0]["bdf"] + "\n")
         time.sleep(0.6)  # six polls of a running monitor
-        assert os.path.exists(req), "the standing-by instance took the request"
+        assert os.path.exists(req), "the standing-by instance took the request:\n" + d.log()[-3000:]
         # the other instance's verdicts, as it writes them
         state.write_text(f"adp-health v1\n{fx['gpus'][1]['uuid']}\t-\t0\t4\tGPU_PRE_RESET: seen by the other\n")
         os.unlink(req)
