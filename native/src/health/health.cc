@@ -216,6 +216,7 @@ void Monitor::LoadVerdicts() {
     void* h = snap_->procs[g.partitions.front().handle].handle;
     auto ecc = lib_->UncorrectableErrors(h);
     GpuRecord r = ledger_->Get(keys_[g.index]);
+    const uint32_t was = r.fail;
     if (!r.has_baseline && ecc.ok()) {
       r.has_baseline = true;
       r.ecc_baseline = r.ecc_seen = *ecc;
@@ -226,7 +227,7 @@ void Monitor::LoadVerdicts() {
       r.ecc_baseline = r.ecc_seen = *ecc;
       if (r.fail & kFailEcc) {
         r.fail &= ~kFailEcc;
-        if (!r.fail) r.reason.clear();
+        r.reason = r.fail ? "still: " + DescribeFailures(r.fail) : "";
       }
     }
     ecc_baseline_[g.index] = r.ecc_baseline;
@@ -242,6 +243,12 @@ void Monitor::LoadVerdicts() {
     if (r.fail) {
       LOG_WARN(kComp, "GPU %s stays unhealthy from an earlier generation: %s", g.bdf.c_str(), r.reason.c_str());
       Notify(g.index, false, r.reason);
+    } else if (was) {
+      // The plugins applied the ledger's verdict before this monitor started
+      // (Supervisor::PublishPlugins); no poll would change it back.
+      LOG_INFO(kComp, "GPU %s healthy again: uncorrectable ECC counters reset since an earlier generation",
+               g.bdf.c_str());
+      Notify(g.index, true, "uncorrectable ECC counters reset");
     }
   }
 }

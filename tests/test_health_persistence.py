@@ -246,6 +246,37 @@ def test_state_file_survives_daemon_restart(mk, scratch):
     assert "counters reset" in n.d.log()
 
 
+def test_ecc_counters_reset_while_the_daemon_was_down(mk, scratch):
+    """A GPU reset (or driver reload) while the container was down clears the
+    RAS counters: the ECC failure the state file holds is gone with them. The
+    monitor re-baselines at its start and the plugins (which applied the state
+    file's verdicts before it started) advertise the GPU Healthy again -- no
+    poll has to run for that (a poll finds nothing to change: the count it
+    reads is the new baseline)."""
+    state_file = os.path.join(scratch + ".fixture", "health.state")
+    n = mk(args=["--health-state-file", state_file])
+    ids = sorted(n.start())
+    n.set_ecc(1, 7)
+    n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+    assert n.stop_daemon() == 0
+    n.set_ecc(1, 2)
+    n.env["DP_HEALTH_POLL_MS"] = "60000"  # the monitor's start alone, no poll
+    first = n.start()
+    if first[ids[1]] != "Healthy":  # the state file's verdict, published before the monitor started
+        n.wait_health(lambda h: h[ids[1]] == "Healthy")
+    assert "uncorrectable ECC count 2 below the 7 seen before (counters reset); re-baselined" in n.d.log()
+    assert "stays unhealthy from an earlier generation" not in n.d.log()
+    assert "\t2\t2\t0\t\n" in open(state_file).read()  # healthy, baseline 2, no reason
+    assert "healthy again: uncorrectable ECC counters reset" in n.d.log()
+    # The new baseline is the count read at start: errors after it fail the GPU again.
+    assert n.stop_daemon() == 0
+    n.set_ecc(1, 3)
+    n.env["DP_HEALTH_POLL_MS"] = "100"
+    n.start()
+    n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+    assert "rose to 3 (baseline 2)" in n.d.log()
+
+
 def test_ecc_baseline_is_the_first_observation(mk, scratch):
     """Errors that accrue while the daemon is down still fail the GPU when it
     comes back (the baseline is not re-taken at each start)."""
