@@ -42,7 +42,8 @@
 //                     gpu<i>.partition ("CPX NPS2": live partition-mode override),
 //                     gpu<i>.xgmi_down (number of xGMI links reported down),
 //                     gpu<i>.badpages (retired HBM pages; not a number = query fails),
-//                     gpu<i>.badpage_threshold (absent = the query needs root, as unprivileged)
+//                     gpu<i>.badpage_threshold (absent = the query needs root, as unprivileged),
+//                     enumerate_fail (amdsmi_get_socket_handles answers BUSY)
 //   amdsmi_shut_down + amdsmi_init re-reads the fixture (re-enumeration after a
 //   re-partition).
 #include <amd_smi/amdsmi.h>
@@ -340,6 +341,9 @@ amdsmi_status_t amdsmi_get_socket_handles(uint32_t* count, amdsmi_socket_handle*
   std::lock_guard<std::mutex> lk(g_mu);
   CountCall();
   if (!g || !count) return AMDSMI_STATUS_INVAL;
+  // state_dir/enumerate_fail: enumeration refused (a driver mid-reload).
+  if (!g->state_dir.empty() && access((g->state_dir + "/enumerate_fail").c_str(), F_OK) == 0)
+    return AMDSMI_STATUS_BUSY;
   uint32_t n = static_cast<uint32_t>(g->gpus.size());
   if (!out) { *count = n; return AMDSMI_STATUS_SUCCESS; }
   uint32_t m = *count < n ? *count : n;

@@ -306,6 +306,47 @@ def test_repartition_is_detected_and_reenumerated(scratch):
         k.stop()
 
 
+@pytest.mark.parametrize("what", ["enumeration", "amdsmi re-init"])
+def test_failure_on_restart_is_retried_with_backoff(scratch, what):
+    """amdsmi refuses to enumerate, or to initialise again, at a SIGHUP (a
+    driver mid-reload): the daemon re-initialises amdsmi and tries again on a
+    doubling timer, and serves the same devices once amdsmi works again (the
+    reference exits and relies on the pod's restart)."""
+    fixture_dir = scratch + ".fixture"
+    state = os.path.join(fixture_dir, "state")
+    os.makedirs(state, exist_ok=True)
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(2), state_dir=state).start()
+    fx = fixtures.node(2)
+    fx["state_dir"] = state
+    try:
+        first = k.wait_registration()
+        fail = os.path.join(state, "enumerate_fail")
+        if what == "enumeration":
+            open(fail, "w").close()
+        else:
+            fixtures.write(dict(fx, init_status=34), fixture_dir)  # DRIVER_NOT_LOADED
+        d.signal(signal.SIGHUP)
+        d.wait_log(what + " failed; retrying in 1000 ms", timeout=10)
+        d.wait_log(what + " failed; retrying in 2000 ms", timeout=10)  # the timer's retry, failing again
+        if what == "enumeration":
+            os.unlink(fail)
+        else:
+            fixtures.write(fx, fixture_dir)
+        reg = k.wait_registration(10)
+        assert reg.resource_name == first.resource_name and reg.endpoint == first.endpoint
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        assert len(c.watch()[0].get(timeout=5).devices) == 2
+        c.close()
+        log = d.log()
+        assert log.count("device enumeration failed" if what == "enumeration"
+                         else "amdsmi re-initialisation failed") == 2
+        assert "amdsmi re-initialised" in log
+    finally:
+        assert d.stop() == 0
+        k.stop()
+
+
 def _cpu_seconds(pid):
     with open(f"/proc/{pid}/stat") as f:
         fields = f.read().rsplit(")", 1)[1].split()
