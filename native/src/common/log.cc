@@ -67,7 +67,6 @@ const char* LevelName(LogLevel l) {
 }  // namespace
 
 void SetLogLevel(LogLevel l) { g_level.store(static_cast<int>(l)); }
-LogLevel GetLogLevel() { return static_cast<LogLevel>(g_level.load()); }
 namespace {
 thread_local int t_quiet = 0;
 }  // namespace

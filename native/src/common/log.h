@@ -15,7 +15,6 @@ namespace adp {
 enum class LogLevel { kDebug = 0, kInfo = 1, kWarn = 2, kError = 3 };
 
 void SetLogLevel(LogLevel l);
-LogLevel GetLogLevel();
 bool LogEnabled(LogLevel l);
 void Logf(LogLevel l, const char* component, const char* fmt, ...)
     __attribute__((format(printf, 3, 4)));

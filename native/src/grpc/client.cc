@@ -120,7 +120,6 @@ Channel::~Channel() {
   if (fd_ >= 0) close(fd_);
 }
 
-bool Channel::alive() const { return !dead_ && fd_ >= 0; }
 
 Result<std::unique_ptr<Channel>> Channel::Dial(const std::string& uds_path, int timeout_ms) {
   std::unique_ptr<Channel> ch(new Channel());

@@ -213,7 +213,6 @@ class Channel {
   Status Recv(int32_t stream_id, std::string* message, int timeout_ms);
   // Processes pending input without blocking (or up to timeout_ms).
   Status Pump(int timeout_ms);
-  bool alive() const;
 
   // Client frame pattern of the kubelet's grpc-go transport (BDP estimation on,
   // the default for a kubelet dial): a PING with an 8-byte payload after the

@@ -82,12 +82,6 @@ std::string PhysicalGpu::PartitionProfile() const {
          "gb";
 }
 
-std::vector<int> Snapshot::HandlesOf(int gpu) const {
-  std::vector<int> out;
-  for (const auto& p : gpus[gpu].partitions) out.push_back(p.handle);
-  return out;
-}
-
 int Snapshot::GpuOfHandle(int h) const {
   for (const auto& g : gpus)
     for (const auto& p : g.partitions)

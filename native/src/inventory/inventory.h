@@ -109,8 +109,6 @@ struct Snapshot {
 
   LinkClass Link(int a, int b) const { return gpu_links[a * gpus.size() + b]; }
   uint64_t Hops(int a, int b) const { return gpu_hops[a * gpus.size() + b]; }
-  // amdsmi handle indices belonging to physical GPU `gpu`.
-  std::vector<int> HandlesOf(int gpu) const;
   // Physical GPU that owns amdsmi handle index `h` (-1 if none).
   int GpuOfHandle(int h) const;
 };

@@ -118,13 +118,6 @@ void Histogram::AppendPrometheus(const std::string& name, const std::string& lab
   *out += name + "_sum{" + labels + "} " + num + "\n" + name + "_count{" + labels + "} " + std::to_string(cum) + "\n";
 }
 
-void Histogram::Reset() {
-  for (auto& s : shards_) {
-    for (auto& b : s.buckets) b.store(0, std::memory_order_relaxed);
-    s.sum_ns.store(0, std::memory_order_relaxed);
-  }
-}
-
 FineHistogram::FineHistogram() : shards_(new Shard[kShards]) {}
 
 void FineHistogram::Observe(uint64_t ns) {

@@ -61,7 +61,6 @@ class Histogram {
   double QuantileUs(double q) const;
   // Appends `name_bucket{labels,le=..}`, `name_sum`, `name_count` lines.
   void AppendPrometheus(const std::string& name, const std::string& labels, std::string* out) const;
-  void Reset();
 
  private:
   struct alignas(64) Shard {

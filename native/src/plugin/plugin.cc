@@ -47,16 +47,6 @@ bool ParseDeviceIdStrategy(std::string_view s, DeviceIdStrategy* out) {
   return false;
 }
 
-const char* DeviceListStrategyName(DeviceListStrategy s) {
-  switch (s) {
-    case DeviceListStrategy::kEnvvar: return "envvar";
-    case DeviceListStrategy::kVolumeMounts: return "volume-mounts";
-    case DeviceListStrategy::kCdiAnnotations: return "cdi-annotations";
-    case DeviceListStrategy::kCdiCri: return "cdi-cri";
-  }
-  return "?";
-}
-
 std::vector<std::pair<uint32_t, uint32_t>> ReplicaCuRanges(uint32_t cus, uint32_t xcds, unsigned replicas) {
   std::vector<std::pair<uint32_t, uint32_t>> out;
   if (replicas < 2 || cus == 0 || xcds == 0 || cus % xcds != 0) return out;
@@ -121,10 +111,6 @@ double CpuBudget() {
 int DefaultServerThreads() {
   double budget = CpuBudget();
   return static_cast<int>(std::clamp(std::ceil(budget), 1.0, 8.0));
-}
-
-const char* DeviceIdStrategyName(DeviceIdStrategy s) {
-  return s == DeviceIdStrategy::kIndex ? "index" : "uuid";
 }
 
 Plugin::Plugin(std::shared_ptr<const inventory::Snapshot> snap, strategy::PluginSpec spec,
@@ -612,14 +598,6 @@ bool Plugin::ApplyHealth(const std::vector<int>& us, bool healthy, const std::st
   }
   if (changed) RebuildListAndWatch();
   return changed;
-}
-
-void Plugin::SetHandleHealth(int handle, bool healthy, const std::string& reason) {
-  std::vector<int> us;
-  for (size_t i = 0; i < units_.size(); ++i)
-    for (int h : units_[i].handles)
-      if (h == handle) us.push_back(static_cast<int>(i));
-  PostHealth(std::move(us), healthy, reason);
 }
 
 void Plugin::SetGpuHealth(int gpu, bool healthy, const std::string& reason) {

@@ -52,8 +52,6 @@ enum class DeviceListStrategy { kEnvvar, kVolumeMounts, kCdiAnnotations, kCdiCri
 enum class DeviceIdStrategy { kUuid, kIndex };
 bool ParseDeviceListStrategy(std::string_view s, DeviceListStrategy* out);
 bool ParseDeviceIdStrategy(std::string_view s, DeviceIdStrategy* out);
-const char* DeviceListStrategyName(DeviceListStrategy s);
-const char* DeviceIdStrategyName(DeviceIdStrategy s);
 
 inline constexpr const char* kDefaultPluginDir = "/var/lib/kubelet/device-plugins/";
 inline constexpr const char* kVisibleDevicesEnv = "AMD_VISIBLE_DEVICES";
@@ -255,9 +253,8 @@ class Plugin {
   // once another process has bound the same path).
   bool owns_socket() const;
 
-  // Thread-safe. Marks every device that contains amdsmi handle `handle`.
-  void SetHandleHealth(int handle, bool healthy, const std::string& reason);
-  // Thread-safe. Marks every device of physical GPU `gpu`.
+  // Thread-safe. Marks every device of physical GPU `gpu` (health is per GPU:
+  // a reset or an ECC failure takes all of its partitions).
   void SetGpuHealth(int gpu, bool healthy, const std::string& reason);
 
   const RpcStats& stats() const { return stats_; }

@@ -437,30 +437,6 @@ Status Library::Reinit() {
   return Status::Ok();
 }
 
-Result<std::vector<GpuProcess>> Library::ProcessList(void* h) {
-  if (!f_->process_list) return NotSupported("process list query not present");
-  std::vector<amdsmi_proc_info_t> buf(16);
-  for (int attempt = 0; attempt < 4; ++attempt) {
-    uint32_t n = static_cast<uint32_t>(buf.size());
-    amdsmi_status_t st = f_->process_list(h, &n, buf.data());
-    if (st == AMDSMI_STATUS_OUT_OF_RESOURCES && n > buf.size()) {  // more processes than room: grow, retry
-      buf.resize(n + 8);
-      continue;
-    }
-    if (st != AMDSMI_STATUS_SUCCESS) return Unavailable("process list query failed (" + std::to_string(st) + ")");
-    std::vector<GpuProcess> out;
-    for (uint32_t i = 0; i < n && i < buf.size(); ++i) {
-      GpuProcess g;
-      g.pid = buf[i].pid;
-      g.vram_bytes = buf[i].memory_usage.vram_mem;
-      g.name.assign(buf[i].name, strnlen(buf[i].name, sizeof(buf[i].name)));
-      out.push_back(std::move(g));
-    }
-    return out;
-  }
-  return Unavailable("process list kept growing");
-}
-
 std::string Library::QueryReport() {
   std::string out = "{\"amdsmi\": \"" + Version() + "\", \"path\": \"" + path_ + "\", \"processors\": [";
   uint32_t nsock = 0;

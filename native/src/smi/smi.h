@@ -80,14 +80,6 @@ struct Event {
   std::string message;
 };
 
-// One process holding memory on a GPU, as the driver accounts it
-// (amdsmi_get_gpu_process_list). `pid` is in the host's PID namespace.
-struct GpuProcess {
-  uint32_t pid = 0;
-  uint64_t vram_bytes = 0;
-  std::string name;
-};
-
 class Library {
  public:
   ~Library();
@@ -126,8 +118,6 @@ class Library {
   // gpu_metrics, which the driver does not serve while the GPU is in reset).
   Result<uint32_t> Activity(void* h);
   bool Responsive(void* h);
-  // Processes with memory on the device and their VRAM (driver accounting).
-  Result<std::vector<GpuProcess>> ProcessList(void* h);
 
   // Every query the plugin uses, run once per processor, with its amdsmi
   // status: what works in this container (device cgroup, privileges) and what

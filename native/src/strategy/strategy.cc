@@ -86,15 +86,6 @@ bool ParsePartitionStrategy(std::string_view s, PartitionStrategy* out) {
   return false;
 }
 
-const char* PartitionStrategyName(PartitionStrategy s) {
-  switch (s) {
-    case PartitionStrategy::kNone: return "none";
-    case PartitionStrategy::kSingle: return "single";
-    case PartitionStrategy::kMixed: return "mixed";
-  }
-  return "?";
-}
-
 std::string PartitionInvalidReason(const inventory::PhysicalGpu& g) {
   if (!g.partitioned()) return "not partitioned";
   // Memory partitions (NPSn) must split evenly over compute partitions: NPS4

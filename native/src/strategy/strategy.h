@@ -56,7 +56,6 @@ bool ValidResourceName(std::string_view name);
 
 enum class PartitionStrategy { kNone, kSingle, kMixed };
 bool ParsePartitionStrategy(std::string_view s, PartitionStrategy* out);
-const char* PartitionStrategyName(PartitionStrategy s);
 
 struct PluginSpec {
   std::string original;       // "gpu" or a partition profile such as "cpx-1xcd.36gb"

@@ -275,9 +275,9 @@ static void TestLedgerGaps() {
     lg.MarkGap("p", "the relay restarted", false, 6);  // confirmed
     CHECK(lg.Get("p").gap == "the relay restarted");
     lg.Put("p", rp);
-    std::string body = health::Ledger::Serialize(lg.All());
-    CHECK(body.find("\tgap=the relay restarted\n") != std::string::npos);
-    CHECK(health::Ledger::Parse(body)["p"].gap == "the relay restarted");
+    std::string persisted = health::Ledger::Serialize(lg.All());
+    CHECK(persisted.find("\tgap=the relay restarted\n") != std::string::npos);
+    CHECK(health::Ledger::Parse(persisted)["p"].gap == "the relay restarted");
     CHECK(health::Ledger::Parse("adp-health v1\nq\t-\t0\t4\tr\tgap=x\tresets=1,2\n")["q"].resets.size() == 2);
     CHECK(health::Ledger::Parse("adp-health v1\nq\t-\t0\t4\tr\tgap=x\tresets=1,2\n")["q"].gap == "x");
     lg.ClearGap("p");
