@@ -196,6 +196,9 @@ class Registration {
   // How long waits have kept failing (each failure is followed by 100 ms of rest).
   int64_t FailingMs() const { return running_.load() ? static_cast<int64_t>(wait_failures_.load()) * 100 : 0; }
   bool Hung() const { return SilentMs() > stuck_ms_; }
+  // Events the waiter could not hand to the poll loop (its pipe full) since
+  // the last call: they are in no daemon's stream and in no replay.
+  uint64_t TakeDropped() { return dropped_.exchange(0); }
 
   // Enumerates (after amdsmi shut_down + init when `reinit`), registers every
   // processor and starts the waiter. Only the registrar thread calls it.
@@ -362,8 +365,11 @@ class Registration {
             if (q.handle == e.handle) p = &q;
           if (!p) continue;
           std::string line = FormatRelayEvent(*p, e.type, e.message);
-          if (write(event_fd_, line.data(), line.size()) != static_cast<ssize_t>(line.size()))
-            LOG_WARN(kComp, "event dropped (relay loop behind): %s", OneLine(line).c_str());
+          const bool refused = !drop_event_.empty() && line.find(drop_event_) != std::string::npos;  // test hook
+          if (refused || write(event_fd_, line.data(), line.size()) != static_cast<ssize_t>(line.size())) {
+            LOG_ERROR(kComp, "event dropped (relay loop behind): %s", OneLine(line).c_str());
+            dropped_.fetch_add(1);  // the poll loop tells the daemons (within a second)
+          }
         }
       }
     });
@@ -390,6 +396,11 @@ class Registration {
   std::atomic<bool> running_{false};
   std::atomic<int64_t> beat_ms_{0};    // the waiter's last sign of life
   std::atomic<int> wait_failures_{0};  // consecutive failed waits
+  std::atomic<uint64_t> dropped_{0};    // events the pipe refused (TakeDropped)
+  const std::string drop_event_ = [] {  // test hook: refuse event lines containing it
+    const char* e = getenv("ADP_DEBUG_RELAY_REFUSE_EVENT");
+    return std::string(e ? e : "");
+  }();
   mutable std::mutex mu_;
   State state_;
   std::thread registrar_;
@@ -461,6 +472,7 @@ class RelayServer {
       if (poll(pfds.data(), pfds.size(), timeout) < 0 && errno != EINTR) break;
       Watchdog();
       if (pfds[2].revents & POLLIN) OnEvents();
+      OnDropped();
       if (pfds[3].revents & POLLIN) OnRenewals();
       if (pfds[0].revents & POLLIN) {
         signalfd_siginfo si;
@@ -582,6 +594,20 @@ class RelayServer {
     Broadcast(out);
   }
 
+  // Events the waiter dropped are in no daemon's stream and no replay: every
+  // subscribed daemon is told it may have missed events (a confirmed gap: it
+  // polls its waiting GPUs back), and so is one that reconnects later with a
+  // cursor from before the loss.
+  void OnDropped() {
+    const uint64_t n = reg_->TakeDropped();
+    if (!n) return;
+    lost_ = true;
+    lost_seq_ = seq_;
+    LOG_ERROR(kComp, "%llu event(s) lost after #%llu: daemons are told they may have missed events",
+              static_cast<unsigned long long>(n), static_cast<unsigned long long>(seq_));
+    Broadcast(Hello(true, 1));
+  }
+
   // "done <client> <renewed 0|1>" from the registrar.
   void OnRenewals() {
     char buf[512];
@@ -610,6 +636,7 @@ class RelayServer {
     if (rq.has_since && rq.since_relay == relay_id_ && rq.since_seq <= seq_) {
       const uint64_t s = rq.since_seq;
       bool held = s == seq_ || (!ring_.empty() && ring_.front().first <= s + 1);
+      if (lost_ && s <= lost_seq_) held = false;  // it was away when events were lost
       std::string replay;
       size_t n = 0;
       for (const auto& [q, l] : ring_)
@@ -708,6 +735,8 @@ class RelayServer {
   // The last kRelayRingSize events forwarded, for daemons that reconnect.
   std::deque<std::pair<uint64_t, std::string>> ring_;
   uint64_t seq_ = 0;
+  bool lost_ = false;      // events were dropped (OnDropped) ...
+  uint64_t lost_seq_ = 0;  // ... after this one: a cursor at or before it missed them
   bool stuck_ = false;
   std::string stuck_reason_;
   std::string pending_, done_pending_;  // bytes read from the pipes, up to the last full line

@@ -762,6 +762,46 @@ def test_a_dropped_connection_is_a_tentative_gap_the_replay_cancels(scratch):
         n.stop()
 
 
+def test_an_event_the_relay_itself_dropped_is_a_confirmed_gap(scratch):
+    """The relay's waiter cannot hand an event to its poll loop (the pipe
+    between them full; here on cue, ADP_DEBUG_RELAY_REFUSE_EVENT): the event is
+    in no daemon's stream and in no replay. The relay tells every daemon it may
+    have missed events, and the GPU waiting for that GPU_POST_RESET comes back
+    by the polled recovery instead of staying Unhealthy. Events after the loss
+    are delivered as before."""
+    n = RelayNode(scratch, relay_env={"ADP_DEBUG_RELAY_REFUSE_EVENT": "lostme"},
+                  daemon_args=["--reset-recovery-hold-ms", "500"])
+    try:
+        n.d.wait_log("events on through the relay")
+        n.inject("1 3 pre-reset")
+        assert n.health() == ["Healthy", "Unhealthy"]
+        n.inject("1 4 reset done lostme")
+        rlog = n.relay.wait_log("event(s) lost after #1: daemons are told they may have missed events")
+        assert "event dropped (relay loop behind)" in rlog
+        log = n.d.wait_log("across an event gap", timeout=10)
+        assert n.bdf(1) in log
+        n.wait_health(["Healthy", "Healthy"], timeout=10)
+        line = [ln for ln in n.d.log().splitlines() if "recovered without GPU_POST_RESET" in ln]
+        assert len(line) == 1 and n.bdf(1) in line[0], line
+        assert "GPU_POST_RESET(4)" not in n.d.log()  # it never arrived
+        # A daemon reconnecting with a cursor at the loss may have missed it ...
+        n.d.signal(signal.SIGHUP)
+        assert n.rewatch() == ["Healthy", "Healthy"]
+        n.relay.wait_log("daemon connected for events (it may have missed events)")
+        n.d.wait_log("events on through the relay", count=2)
+        # ... one whose cursor is past it has not; events flow as before.
+        n.inject("0 3 pre-reset")
+        n.wait_health(["Unhealthy", "Healthy"], timeout=10)
+        n.d.signal(signal.SIGHUP)
+        assert n.rewatch() == ["Unhealthy", "Healthy"]
+        n.relay.wait_log("daemon connected for events (nothing missed)")
+        n.d.wait_log("events on through the relay", count=3)
+        n.inject("0 4 reset done")
+        n.wait_health(["Healthy", "Healthy"], timeout=10)
+    finally:
+        n.stop()
+
+
 def test_a_relay_gone_for_good_confirms_the_gap(scratch):
     """The relay dies and does not come back: the tentative gap of the GPU
     waiting for GPU_POST_RESET is confirmed after ADP_EVENT_FAIL_MS without a
