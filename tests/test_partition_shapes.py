@@ -118,3 +118,18 @@ def test_spx_is_never_rejected_by_the_model_table(scratch):
     r = dry_run(scratch, fx)
     rep = json.loads(r.stdout)
     assert [g["vram_mib"] for g in rep["gpus"]] == [100000, 294896]
+
+
+@pytest.mark.parametrize("reported", ["", "SPX"])
+def test_partition_mode_from_the_handle_count(scratch, reported):
+    """A driver that reports no compute partition mode (and no accelerator
+    partition profile), or one that says SPX while listing 4 handles: the mode
+    is taken from the handle count (4 -> QPX), and names and sizes follow."""
+    fx = fixtures.node(1, "QPX")
+    fx["gpus"][0].update(compute_partition=reported, report_profile=False, partitions=4)
+    r = dry_run(scratch, fx, "--partition-strategy", "mixed")
+    assert r.returncode == 0, r.stderr
+    rep = json.loads(r.stdout)
+    assert rep["gpus"][0]["mode"] == "QPX/NPS1" and rep["gpus"][0]["profile"] == "qpx-2xcd.72gb"
+    assert {x["resource"]: x["allocatable"] for x in rep["resources"]} == {"amd.com/qpx-2xcd.72gb": 4}
+    assert ("reports SPX but has 4 handles; treating as QPX" in r.stderr) == (reported == "SPX")
