@@ -835,16 +835,17 @@ import pytest  # noqa: E402
 def test_chaos_of_resets_restarts_and_drops_leaves_no_gpu_stuck(scratch, seed):
     """A seeded random mix of everything that can come between a GPU_PRE_RESET
     and its GPU_POST_RESET: daemon SIGHUPs, the relay dropping the daemon (its
-    buffer full: ADP_DEBUG_RELAY_DROP_ON), the relay restarted (SIGTERM or
-    SIGKILL), events in between. Every POST_RESET is sent while a relay runs;
+    buffer full: ADP_DEBUG_RELAY_DROP_ON), a POST_RESET the relay itself loses
+    (ADP_DEBUG_RELAY_REFUSE_EVENT), the relay restarted (SIGTERM or SIGKILL),
+    events in between. Every POST_RESET is sent while a relay runs;
     it reaches the daemon directly or by the relay's replay -- unless the relay
-    holding it restarts before the daemon is back, which the daemon sees as an
-    event gap (a new relay): then the polled check returns the GPU. Either
+    lost it, or the relay holding it restarts before the daemon is back; the
+    daemon sees either as an event gap: then the polled check returns the GPU. Either
     way no GPU stays out of service, and a polled return only ever follows a
     confirmed gap on that GPU."""
     import random
     rnd = random.Random(seed)
-    n = RelayNode(scratch, relay_env={"ADP_DEBUG_RELAY_DROP_ON": "dropme"},
+    n = RelayNode(scratch, relay_env={"ADP_DEBUG_RELAY_DROP_ON": "dropme", "ADP_DEBUG_RELAY_REFUSE_EVENT": "lostme"},
                   daemon_args=["--reset-recovery-hold-ms", "1500", "--reset-flap-limit", "0"])
     try:
         n.d.wait_log("events on through the relay")
@@ -857,7 +858,9 @@ def test_chaos_of_resets_restarts_and_drops_leaves_no_gpu_stuck(scratch, seed):
                 pending.add(gpu)
             elif op == "post" and pending:
                 g = rnd.choice(sorted(pending))
-                n.inject(f"{g} 4 chaos post {i}" + (" dropme" if rnd.random() < 0.5 else ""))
+                # dropme: the relay drops the daemon (the replay brings it);
+                # lostme: the relay's own waiter drops it (a confirmed gap)
+                n.inject(f"{g} 4 chaos post {i}" + rnd.choice(["", "", " dropme", " dropme", " lostme"]))
                 pending.discard(g)
             elif op == "sighup":
                 n.d.signal(signal.SIGHUP)
