@@ -140,6 +140,7 @@ image:
 # Dockerfile.ubuntu as root filesystems and run the daemon in them (chrooted,
 # unprivileged user namespace), against a stub kubelet.
 image-rootfs: build
+	$(PY) -c "from k8s_gpu_sharing_plugin_amd.utils import build; build.build_image_tree()"
 	$(PY) -m pytest -q tests/test_image_rootfs.py tests/test_image_deps.py
 
 clean:

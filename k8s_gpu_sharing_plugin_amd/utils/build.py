@@ -26,15 +26,27 @@ def _run(cmd, **kw):
 
 
 def build_native(jobs: int = 8, build_type: str = "Release", build_dir: str = BUILD_DIR,
-                 extra_cmake=None) -> str:
-    """Configure (once) and build every native target. Returns the build dir."""
+                 extra_cmake=None, targets=None) -> str:
+    """Configure (once) and build every native target (or `targets`). Returns the build dir."""
     generator = ["-G", "Ninja"] if shutil.which("ninja") else []
     if not os.path.exists(os.path.join(build_dir, "CMakeCache.txt")):
         os.makedirs(build_dir, exist_ok=True)
         _run(["cmake", "-S", NATIVE_SRC, "-B", build_dir, f"-DCMAKE_BUILD_TYPE={build_type}",
               *generator, *(extra_cmake or [])])
-    _run(["cmake", "--build", build_dir, "--", f"-j{jobs}"])
+    _run(["cmake", "--build", build_dir, *(["--target", *targets] if targets else []), "--", f"-j{jobs}"])
     return build_dir
+
+
+# What the image stages build (deployments/container/Dockerfile.*): the daemon
+# and the shim, with the fault-injection hooks compiled out.
+IMAGE_BUILD_DIR = os.path.join(REPO_ROOT, "build", "image")
+IMAGE_CMAKE = ["-DADP_TEST_HOOKS=OFF"]
+IMAGE_TARGETS = ["amdgpu-device-plugin", "adp_memcap"]
+
+
+def build_image_tree(jobs: int = 8) -> str:
+    """build/image: the image stages' cmake line and targets (ADP_TEST_HOOKS=OFF)."""
+    return build_native(jobs, build_dir=IMAGE_BUILD_DIR, extra_cmake=IMAGE_CMAKE, targets=IMAGE_TARGETS)
 
 
 PROBE_MAIN = os.path.join(NATIVE_SRC, "probe", "probe_main.cpp")
@@ -89,6 +101,7 @@ def build_descriptor() -> str:
 
 def build_all(probe: bool = True) -> None:
     build_native()
+    build_image_tree()
     build_descriptor()
     if probe:
         build_probe()

@@ -46,9 +46,19 @@ PACKAGES = {
              "libyaml-0.so.2": "libyaml", "libelf.so.1": "elfutils-libelf", "libnuma.so.1": "numactl-libs",
              "libstdc++.so.6": "libstdc++"},
 }
-# The build stage's outputs, as built in this tree.
-BUILT = {"/build/amdgpu-device-plugin": DAEMON, "/build/amdgpu-dp-probe": PROBE_BIN,
-         "/build/libadp_memcap.so": os.path.join(os.path.dirname(DAEMON), "libadp_memcap.so")}
+# The build stage's outputs, as built in this tree: the daemon and the shim of
+# build/image (the stage's cmake line: ADP_TEST_HOOKS=OFF), the probe.
+IMAGE_DIR = os.path.join(REPO_ROOT, "build", "image")
+IMAGE_DAEMON = os.path.join(IMAGE_DIR, "amdgpu-device-plugin")
+BUILT = {"/build/amdgpu-device-plugin": IMAGE_DAEMON, "/build/amdgpu-dp-probe": PROBE_BIN,
+         "/build/libadp_memcap.so": os.path.join(IMAGE_DIR, "libadp_memcap.so")}
+
+
+def ensure_image_tree():
+    """build/image, built here on first use (it travels to the GPU box built)."""
+    if not all(os.path.exists(BUILT[k]) for k in ("/build/amdgpu-device-plugin", "/build/libadp_memcap.so")):
+        from . import build
+        build.build_image_tree()
 
 
 def dockerfile(dist="ubuntu"):
@@ -118,6 +128,7 @@ def build_rootfs(dest, dist="ubuntu", stage="runtime"):
     Only ubuntu stages can be assembled from this host."""
     if dist != "ubuntu":
         raise ValueError("only the ubuntu stages can be assembled on this (Ubuntu 22.04) host")
+    ensure_image_tree()
     (name, base, lines), = [s for s in stages(dockerfile(dist)) if s[0] == stage]
     pkgs, copies, ldconf, entry = stage_contents(lines)
     if os.path.exists(dest):

@@ -10,6 +10,8 @@
 // Fixture: $AMDSMI_MOCK_FIXTURE (JSON). Schema (all keys optional except gpus):
 //   { "init_status": 0, "events_supported": true, "lib_version": [26,2,1],
 //     "events_open_kfd": false,  event registration opens /dev/kfd (EPERM -> NO_PERM)
+//     "evt_init_fail_on": [1],   amdsmi_init_gpu_event_notification fails (API_FAILED) on
+//                                these processors (global enumeration index)
 //     "event_fifo": "<path>", "state_dir": "<path>", "topology": "xgmi"|"pcie",
 //     "numa_bw_penalty": false,
 //     "gpus": [ { "uuid": "...", "bdf": "0000:0c:00.0", "numa": 0, "vram_mib": 294896,
@@ -35,6 +37,9 @@
 //               } ] }
 // Runtime injection:
 //   event FIFO lines: "<gpu>[:<partition>] <event-type> [message]",
+//                     "foreign <event-type> [message]" (on a processor handle
+//                     that was never enumerated: amdsmi's handles not being
+//                     the ones it handed out),
 //                     "hang <ms>" (that event wait then returns only after <ms>),
 //                     "fail <n>" (the next n event waits fail)
 //   state_dir files:  gpu<i>.ecc (uncorrectable count; not a number = query fails),
@@ -46,6 +51,12 @@
 //                     enumerate_fail (amdsmi_get_socket_handles answers BUSY)
 //   amdsmi_shut_down + amdsmi_init re-reads the fixture (re-enumeration after a
 //   re-partition).
+// Registration accounting (tests of the rollback of a partial registration):
+//   $AMDSMI_MOCK_EVT_FILE, when set, holds "live=<n> double_init=<n>
+//   leaked_at_shutdown=<n> inits=<n> stops=<n>" after every change: live
+//   registrations, inits of a handle already registered (the real library
+//   would leak its KFD event file), handles still registered at
+//   amdsmi_shut_down.
 #include <amd_smi/amdsmi.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -113,6 +124,7 @@ struct State {
   int fifo_fd = -1;
   std::string fifo_buf;
   int fail_waits = 0;  // "fail <n>": the next n event waits fail
+  std::vector<int> evt_init_fail_on;  // global processor indices whose registration fails
   std::vector<std::unique_ptr<MockProc>> procs;
   std::vector<MockGpu> gpus;
 };
@@ -168,6 +180,8 @@ bool Load() {
   g->state_dir = j.value("state_dir", std::string());
   if (const char* e = getenv("AMDSMI_MOCK_EVENT_FIFO")) g->event_fifo = e;
   if (const char* e = getenv("AMDSMI_MOCK_STATE_DIR")) g->state_dir = e;
+  if (j.count("evt_init_fail_on"))
+    for (const auto& v : j["evt_init_fail_on"]) g->evt_init_fail_on.push_back(v.get<int>());
   if (j.count("lib_version")) {
     for (int i = 0; i < 3; ++i) g->ver[i] = j["lib_version"][i].get<uint32_t>();
   }
@@ -280,6 +294,32 @@ void CountCall() {
   fclose(fp);
 }
 
+// Event registration accounting (outlives amdsmi_shut_down: process-wide).
+struct EvtStats {
+  long live = 0, double_init = 0, leaked_at_shutdown = 0, inits = 0, stops = 0;
+} g_evt;
+void WriteEvtStats() {
+  const char* f = getenv("AMDSMI_MOCK_EVT_FILE");
+  if (!f) return;
+  FILE* fp = fopen(f, "w");
+  if (!fp) return;
+  fprintf(fp, "live=%ld double_init=%ld leaked_at_shutdown=%ld inits=%ld stops=%ld\n", g_evt.live,
+          g_evt.double_init, g_evt.leaked_at_shutdown, g_evt.inits, g_evt.stops);
+  fclose(fp);
+}
+void ForgetRegistrations() {  // amdsmi_shut_down: handles still registered were never stopped
+  if (!g) return;
+  for (auto& p : g->procs)
+    if (p->evt_init) {
+      ++g_evt.leaked_at_shutdown;
+      --g_evt.live;
+    }
+  WriteEvtStats();
+}
+
+// A processor handle amdsmi never enumerated ("foreign" FIFO lines).
+char g_foreign_handle;
+
 #define GET_PROC(h)                                   \
   std::lock_guard<std::mutex> lk(g_mu);               \
   CountCall();                                        \
@@ -312,6 +352,7 @@ amdsmi_status_t amdsmi_init(uint64_t) {
 
 amdsmi_status_t amdsmi_shut_down(void) {
   std::lock_guard<std::mutex> lk(g_mu);
+  ForgetRegistrations();
   if (g) {
     if (g->fifo_fd >= 0) close(g->fifo_fd);
     delete g;
@@ -677,7 +718,16 @@ amdsmi_status_t amdsmi_init_gpu_event_notification(amdsmi_processor_handle h) {
     if (fd < 0 && errno == EPERM) return AMDSMI_STATUS_NO_PERM;
     if (fd >= 0) close(fd);
   }
+  size_t index = 0;
+  while (index < g->procs.size() && g->procs[index].get() != p) ++index;
+  if (std::find(g->evt_init_fail_on.begin(), g->evt_init_fail_on.end(), static_cast<int>(index)) !=
+      g->evt_init_fail_on.end())
+    return AMDSMI_STATUS_API_FAILED;
+  ++g_evt.inits;
+  if (p->evt_init) ++g_evt.double_init;
+  else ++g_evt.live;
   p->evt_init = true;
+  WriteEvtStats();
   if (g->fifo_fd < 0 && !g->event_fifo.empty()) {
     // O_RDWR keeps a writer open so poll() blocks instead of reporting HUP.
     g->fifo_fd = open(g->event_fifo.c_str(), O_RDWR | O_NONBLOCK | O_CLOEXEC);
@@ -694,7 +744,10 @@ amdsmi_status_t amdsmi_set_gpu_event_notification_mask(amdsmi_processor_handle h
 
 amdsmi_status_t amdsmi_stop_gpu_event_notification(amdsmi_processor_handle h) {
   GET_PROC(h);
+  ++g_evt.stops;
+  if (p->evt_init) --g_evt.live;
   p->evt_init = false;
+  WriteEvtStats();
   return AMDSMI_STATUS_SUCCESS;
 }
 
@@ -747,6 +800,17 @@ amdsmi_status_t amdsmi_get_gpu_event_notification(int timeout_ms, uint32_t* num,
     }
     std::string msg;
     std::getline(ls, msg);
+    if (target == "foreign") {  // a handle amdsmi never enumerated, while anything is registered
+      bool any = false;
+      for (auto& p : g->procs) any = any || p->evt_init;
+      if (!any) continue;
+      memset(&data[got], 0, sizeof(data[got]));
+      data[got].processor_handle = &g_foreign_handle;
+      data[got].event = static_cast<amdsmi_evt_notification_type_t>(type);
+      CopyStr(data[got].message, sizeof(data[got].message), msg.empty() ? "mock event" : msg);
+      ++got;
+      continue;
+    }
     int gpu = atoi(target.c_str());
     int part = 0;
     size_t colon = target.find(':');

@@ -147,6 +147,12 @@ const std::vector<FlagDef>& Table() {
        "registering them in this process, which then needs no /dev/kfd access (privilege separation: "
        "only the relay runs privileged; empty = register in-process)",
        [](Flags& f) -> void* { return &f.health_event_socket; }},
+      {"health-event-extra-types", "DP_HEALTH_EVENT_EXTRA_TYPES", "healthEventExtraTypes", Kind::kString,
+       "amdsmi event types to register on top of GPU_PRE_RESET/POST_RESET, VMFAULT and THERMAL_THROTTLE, by number "
+       "or name, comma separated (e.g. '12,13' = KFD PROCESS_START/PROCESS_END, which every HIP process causes): "
+       "counted per GPU in amdgpu_dp_gpu_events_total, never a health verdict; the event relay registers its own "
+       "(empty = none)",
+       [](Flags& f) -> void* { return &f.health_event_extra_types; }},
       {"event-relay", "DP_EVENT_RELAY", "", Kind::kBool,
        "run as the event relay: register amdsmi event notification (needs /dev/kfd) and forward every "
        "event to daemons connecting to --health-event-socket; nothing else (no kubelet, no network)",

@@ -53,6 +53,7 @@ struct Flags {
   bool doctor = false;           // check what a deployment needs on this node, say what to change, exit
   bool health_events = true;     // register amdsmi event notification (needs /dev/kfd access)
   std::string health_event_socket;  // events from the relay at this socket ("" = in-process)
+  std::string health_event_extra_types;  // amdsmi event types registered on top, counted only
   bool event_relay = false;         // run as that relay
   uint64_t driver_hbm_poll_ms = 10000;  // driver-side check of enforced grants (0 = off)
   uint64_t driver_hbm_slack_mib = 512;  // HIP runtime allowance per process in that check

@@ -58,6 +58,17 @@ void AppendDaemonMetrics(const DaemonMetricsInput& in, std::string* out) {
          "registration or could not replay what this daemon missed; events off; event waits failing; a new "
          "in-process registration.");
   Sample(out, "amdgpu_dp_health_event_gaps_total", "", Num(h.event_gaps.load()));
+  {
+    // Always exported (GPU_PRE_RESET at least, 0): an alert on it needs the series.
+    Family(out, "amdgpu_dp_unmatched_events_total", "counter",
+           "amdsmi events on a processor that matches no GPU of this node (a handle amdsmi never enumerated, or "
+           "one the event relay could not place), by type. An unmatched GPU_PRE_RESET holds every GPU until the "
+           "polled check or the operator returns it.");
+    auto unmatched = h.Unmatched();
+    unmatched.emplace("GPU_PRE_RESET", 0);
+    for (const auto& [type, n] : unmatched)
+      Sample(out, "amdgpu_dp_unmatched_events_total", "type=\"" + metrics::LabelValue(type) + "\"", Num(n));
+  }
   if (h.relay_connected.load() >= 0) {
     // Relay mode: which relay this daemon follows and where it is in its stream.
     Family(out, "amdgpu_dp_event_relay_connected", "gauge", "1 while the daemon is connected to the event relay.");
@@ -114,7 +125,7 @@ void AppendDaemonMetrics(const DaemonMetricsInput& in, std::string* out) {
   if (auto events = h.EventCounts(); !events.empty()) {
     Family(out, "amdgpu_dp_gpu_events_total", "counter",
            "amdsmi events per GPU and type, ignored ones included (VMFAULT: an application's GPU page fault; "
-           "THERMAL_THROTTLE; GPU_PRE_RESET / GPU_POST_RESET).");
+           "THERMAL_THROTTLE; GPU_PRE_RESET / GPU_POST_RESET; --health-event-extra-types such as PROCESS_START).");
     for (const auto& [k, n] : events)
       Sample(out, "amdgpu_dp_gpu_events_total", Bdf(k.first) + ",type=\"" + metrics::LabelValue(k.second) + "\"",
              Num(n));

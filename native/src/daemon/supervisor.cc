@@ -51,6 +51,18 @@ namespace {
 constexpr const char* kComp = "daemon";
 constexpr int kMaxBackoffMs = 30000;
 
+// A fault-injection delay from the environment: only in builds with
+// ADP_TEST_HOOKS (the development tree); shipped binaries read nothing.
+int TestHookMs(const char* name, int dflt) {
+#ifdef ADP_TEST_HOOKS
+  const char* e = getenv(name);
+  return e && atoi(e) > 0 ? atoi(e) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
+}
+
 // --enforce-memory-units: copies the shim into <plugin dir>/amdgpu-dp/ -- a
 // host path the container runtime can bind-mount into pods (the kubelet wipes
 // the directory when it restarts; every plugin (re)start installs it again) --
@@ -438,10 +450,8 @@ class Supervisor {
   // re-registration can never leave a recovered GPU advertised Unhealthy.
   void PublishPlugins(const std::shared_ptr<const inventory::Snapshot>& snap,
                       const std::vector<strategy::PluginSpec>& specs, bool apply_ledger) {
-    static const int reregister_delay_ms = [] {  // test hook: widens the window the lock closes
-      const char* e = getenv("ADP_DEBUG_PUBLISH_DELAY_MS");
-      return e ? atoi(e) : 0;
-    }();
+    // Test hook (ADP_TEST_HOOKS builds only): widens the window the lock closes.
+    static const int reregister_delay_ms = TestHookMs("ADP_DEBUG_PUBLISH_DELAY_MS", 0);
     std::lock_guard<std::mutex> lk(plugins_mu_);
     for (const auto& s : specs) plugins_.push_back(std::make_unique<plugin::Plugin>(snap, s, v_.popts));
     WarnSharedDeviceLists(plugins_);
@@ -498,6 +508,7 @@ class Supervisor {
     h.drain_file = cfg_.flags.drain_file;
     h.driver_root = cfg_.flags.driver_root;
     h.event_relay = cfg_.flags.health_event_socket;
+    h.extra_types = v_.extra_event_types;
     h.reset_recovery_hold_ms = static_cast<int64_t>(std::min<uint64_t>(cfg_.flags.reset_recovery_hold_ms, 86400000));
     h.reset_flap_limit = static_cast<int>(std::min<uint64_t>(cfg_.flags.reset_flap_limit, 1000));
     h.reset_flap_window_ms = static_cast<int64_t>(std::min<uint64_t>(cfg_.flags.reset_flap_window_ms, 86400000));
@@ -790,10 +801,13 @@ class Supervisor {
       for (const auto& p : plugins_)
         if (p->device_count() > 0) now[p->resource_name()] = p->ReplicaLayout();
     }
-    std::set<std::string> changed;  // IDs that would mean something else, or vanish
+    // IDs that would mean something else, or vanish -- as CheckReplicaLayouts
+    // counts it: a whole-GPU resource ("" layout) turned into replicas or
+    // memory units re-means the exclusive IDs running pods hold just as well.
+    std::set<std::string> changed;
     for (const auto& [res, lay] : now) {
       auto it = after.find(res);
-      if (!lay.empty() && (it == after.end() || it->second != lay)) changed.insert(res);
+      if (it == after.end() || it->second != lay) changed.insert(res);
     }
     if (changed.empty()) return false;
     if (cfg_.flags.pod_resources_socket.empty()) {
@@ -862,10 +876,8 @@ class Supervisor {
   }
 
   void OnInotify(bool* do_restart, bool* do_reregister) {
-    static const int kSocketRecheckMs = [] {  // test hook: widens the window (default 20 ms)
-      const char* e = getenv("ADP_DEBUG_SOCKET_RECHECK_MS");
-      return e && atoi(e) > 0 ? atoi(e) : 20;
-    }();
+    // Test hook (ADP_TEST_HOOKS builds only): widens the window (default 20 ms).
+    static const int kSocketRecheckMs = TestHookMs("ADP_DEBUG_SOCKET_RECHECK_MS", 20);
     char buf[4096] __attribute__((aligned(__alignof__(inotify_event))));
     ssize_t len;
     while ((len = read(ifd_, buf, sizeof(buf))) > 0) {
@@ -1053,9 +1065,11 @@ int RunDaemon(const Config& startup_cfg, std::function<Result<Config>()> reload)
     return Doctor(lib->get(), v, cfg, d);
   }
   if (operator_command) return DrainCommand(lib->get(), v, cfg);
-  if (cfg.flags.event_relay)
-    return health::RunEventRelay(lib->get(), cfg.flags.health_event_socket, sfd,
-                                 {cfg.flags.driver_root, cfg.flags.host_proc, cfg.flags.kfd_proc_dir});
+  if (cfg.flags.event_relay) {
+    health::RelayOptions ro{cfg.flags.driver_root, cfg.flags.host_proc, cfg.flags.kfd_proc_dir};
+    for (uint32_t t : v.extra_event_types) ro.extra_mask |= smi::EventMask(t);
+    return health::RunEventRelay(lib->get(), cfg.flags.health_event_socket, sfd, ro);
+  }
   int rc;
   {
     Supervisor s(cfg, std::move(v), std::move(reload), lib->get(), sfd);

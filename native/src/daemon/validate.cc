@@ -95,6 +95,9 @@ Result<Validated> Validate(const Config& cfg) {
     return InvalidArgument("--enforce-memory-units: libadp_memcap.so not found (" +
                            (f.memcap_lib.empty() ? std::string("next to the binary or in /usr/lib/amdgpu-device-plugin")
                                                  : f.memcap_lib) + "); set --memcap-lib");
+  auto extra = health::ParseEventTypes(f.health_event_extra_types);
+  if (!extra.ok()) return InvalidArgument("invalid --health-event-extra-types option: " + extra.status().message());
+  v.extra_event_types = std::move(*extra);
   v.bopts.driver_root = f.driver_root;
   v.bopts.sysfs_root = f.sysfs_root;
   v.bopts.include_card_nodes = f.include_card_nodes;

@@ -4,6 +4,8 @@
 // (validateFlags + setup).
 #pragma once
 
+#include <set>
+
 #include <string>
 
 #include "common/status.h"
@@ -19,6 +21,7 @@ struct Validated {
   plugin::PluginOptions popts;
   strategy::ResourceConfig rc;
   inventory::BuildOptions bopts;
+  std::set<uint32_t> extra_event_types;  // --health-event-extra-types
 };
 
 Result<Validated> Validate(const Config& cfg);

@@ -78,6 +78,16 @@ std::map<std::pair<std::string, std::string>, uint64_t> HealthCounters::EventCou
   return events_;
 }
 
+void HealthCounters::CountUnmatched(const std::string& type) {
+  std::lock_guard<std::mutex> lk(mu_);
+  ++unmatched_[type];
+}
+
+std::map<std::string, uint64_t> HealthCounters::Unmatched() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return unmatched_;
+}
+
 void HealthCounters::CountRecovered(const std::string& bdf) {
   std::lock_guard<std::mutex> lk(mu_);
   ++recovered_[bdf];

@@ -22,28 +22,25 @@
 namespace adp::health {
 namespace {
 constexpr const char* kComp = "health";
+// Housekeeping period when liveness polls are off (DP_HEALTH_POLL_MS=0).
+constexpr int kHousekeepingMs = 1000;
+}  // namespace
 
-int64_t NowMs() {
+int64_t Clock::SteadyMs() const {
   return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
 }
 
 // For what is persisted (the reset history): a steady clock restarts with the node.
-int64_t WallMs() {
+int64_t Clock::WallMs() const {
   return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch())
       .count();
 }
 
-const char* EventName(uint32_t t) {
-  switch (t) {
-    case 1: return "VMFAULT";
-    case 2: return "THERMAL_THROTTLE";
-    case 3: return "GPU_PRE_RESET";
-    case 4: return "GPU_POST_RESET";
-    default: return "EVENT";
-  }
+const Clock* Clock::System() {
+  static const Clock c;
+  return &c;
 }
-}  // namespace
 
 std::string DescribeFailures(uint32_t bits) {
   static const std::pair<uint32_t, const char*> kNames[] = {
@@ -71,6 +68,34 @@ std::vector<uint64_t> ParseAdditionalIds(std::string_view input) {
     out.push_back(*v);
   }
   return out;
+}
+
+Result<std::set<uint32_t>> ParseEventTypes(std::string_view input) {
+  std::set<uint32_t> out;
+  for (const auto& part : Split(input, ',')) {
+    std::string t = Trim(part);
+    if (t.empty()) continue;
+    std::optional<uint64_t> v = ParseUint(t);
+    if (!v) {
+      std::string up = t;
+      for (auto& c : up) c = static_cast<char>(toupper(static_cast<unsigned char>(c)));
+      if (up.rfind("AMDSMI_EVT_NOTIF_", 0) == 0) up = up.substr(17);
+      for (uint32_t i = 1; i <= smi::kEvtLast && !v; ++i)
+        if (smi::EventTypeName(i) == up) v = i;
+    }
+    if (!v || *v < 1 || *v > smi::kEvtLast)
+      return InvalidArgument("unknown amdsmi event type '" + t + "' (1.." + std::to_string(smi::kEvtLast) +
+                             " or a name such as PROCESS_START)");
+    out.insert(static_cast<uint32_t>(*v));
+  }
+  return out;
+}
+
+uint64_t HealthConfig::EventMask() const {
+  uint64_t mask = smi::EventMask(smi::kEvtGpuPreReset) | smi::EventMask(smi::kEvtGpuPostReset) |
+                  smi::EventMask(smi::kEvtVmFault) | smi::EventMask(smi::kEvtThermalThrottle);
+  for (uint32_t t : extra_types) mask |= smi::EventMask(t);
+  return mask;
 }
 
 HealthConfig HealthConfig::FromValues(const char* disable_value, const char* poll_ms_value) {
@@ -106,7 +131,11 @@ HealthConfig HealthConfig::FromEnv() {
 int Monitor::Classify(const HealthConfig& cfg, uint32_t type) {
   if (cfg.ignored.count(type)) return 0;
   if (type == smi::kEvtGpuPostReset) return +1;
-  return -1;
+  if (type >= smi::kEvtVmFault && type <= smi::kEvtGpuPreReset) return -1;
+  // KFD's informational events (5..13: migration, page faults, queue
+  // eviction, process start/end), registered only by --health-event-extra-types:
+  // counted, never a verdict.
+  return 0;
 }
 
 Monitor::Monitor(smi::Library* lib, std::shared_ptr<const inventory::Snapshot> snap, HealthConfig cfg,
@@ -144,8 +173,7 @@ Status Monitor::Start() {
   for (const auto& g : snap_->gpus)
     for (const auto& p : g.partitions) watched.push_back(snap_->procs[p.handle].handle);
   handles_ = watched;
-  uint64_t mask = smi::EventMask(smi::kEvtGpuPreReset) | smi::EventMask(smi::kEvtGpuPostReset) |
-                  smi::EventMask(smi::kEvtVmFault) | smi::EventMask(smi::kEvtThermalThrottle);
+  const uint64_t mask = cfg_.EventMask();
   if (!cfg_.events) {
     events_ok_ = false;
     events_reason_ = "off by configuration (--health-events=false)";
@@ -183,7 +211,7 @@ Status Monitor::Start() {
   for (const auto& g : snap_->gpus) {
     const std::string gap = ledger_->Get(keys_[g.index]).gap;
     if (gap.empty() || !(fail_[g.index] & kFailResetPending)) continue;
-    if (ledger_->MarkGap(keys_[g.index], gap, false, NowMs()))
+    if (ledger_->MarkGap(keys_[g.index], gap, false, SteadyNow()))
       LOG_WARN(kComp, "GPU %s waits for GPU_POST_RESET across an event gap from before this process (%s): back in "
                "service once amdsmi has answered every poll for %g s", g.bdf.c_str(), gap.c_str(),
                static_cast<double>(cfg_.reset_recovery_hold_ms) / 1000.0);
@@ -201,7 +229,13 @@ Status Monitor::Start() {
   if (!cfg_.drain_file.empty()) ApplyDrain();  // at once, not a poll interval later
   LOG_INFO(kComp, "health monitor watching %zu GPU(s) (events %s, poll every %d ms)", snap_->gpus.size(),
            events_ok_ ? "on" : relay_fd_ >= 0 ? "through the relay, once it answers" : "off", cfg_.poll_interval_ms);
-  if (!events_ok_ && cfg_.poll_interval_ms == 0 && (cfg_.event_relay.empty() || !cfg_.events)) return Status::Ok();
+  if (cfg_.poll_interval_ms == 0 && cfg_.reset_recovery_hold_ms > 0)
+    LOG_WARN(kComp, "DP_HEALTH_POLL_MS=0: no liveness polls, so a GPU waiting for GPU_POST_RESET across an event gap "
+             "is not brought back by --reset-recovery-hold-ms (only the event or --return-to-service does); "
+             "quarantines, drains and return-to-service requests are still applied every %d ms", kHousekeepingMs);
+  // The thread runs even without events and polls: quarantines end, drains
+  // and return-to-service requests apply (Housekeeping).
+  if (!cfg_.run_thread) return Status::Ok();
   stop_.store(false);
   if (wake_fd_ < 0) wake_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   thread_ = std::thread([this] { Run(); });
@@ -275,7 +309,9 @@ void Monitor::Stop() {
     relay_fd_ = -1;
     events_ok_ = false;
     counters_->FlushRelayCursor();
-  } else if (events_ok_) {
+  } else if (cfg_.event_relay.empty() && lib_) {
+    // Whatever is registered, events on or not (the library undoes a partial
+    // registration itself, and stops only what it holds).
     lib_->EventsStop(handles_);
     events_ok_ = false;
   }
@@ -283,11 +319,11 @@ void Monitor::Stop() {
 
 
 void Monitor::RelayConnect() {
-  relay_tried_ms_ = NowMs();
+  relay_tried_ms_ = SteadyNow();
   relay_fd_ = ConnectRelay(cfg_.event_relay);
   if (relay_fd_ < 0) {
     events_reason_ = "event relay " + cfg_.event_relay + " not reachable (" + strerror(errno) + ")";
-    if (relay_lost_ms_ == 0) relay_lost_ms_ = NowMs();
+    if (relay_lost_ms_ == 0) relay_lost_ms_ = SteadyNow();
     counters_->relay_connected.store(0);
     relay_retry_ms_ = std::min(1000, relay_retry_ms_ * 2);
     return;
@@ -310,7 +346,7 @@ void Monitor::RelayConnect() {
   relay_buf_.clear();
   relay_synced_ = false;
   relay_cursor_sent_ = cur.valid;
-  relay_connected_ms_ = NowMs();
+  relay_connected_ms_ = SteadyNow();
   relay_overdue_ = false;
   events_reason_ = "waiting for the event relay's hello";
 }
@@ -326,7 +362,7 @@ void Monitor::RelayClose(const std::string& why) {
   events_ok_ = false;
   events_reason_ = why;
   counters_->events_enabled.store(0);
-  relay_lost_ms_ = NowMs();
+  relay_lost_ms_ = SteadyNow();
   relay_lost_confirmed_ = false;
   relay_tried_ms_ = relay_lost_ms_;  // the next try in relay_retry_ms_
   // Events sent meanwhile are replayed if the relay comes back holding them.
@@ -344,46 +380,65 @@ void Monitor::RelayWait(int ms) {
   while ((nl = relay_buf_.find('\n')) != std::string::npos) {
     RelayLine l = ParseRelayLine(std::string_view(relay_buf_).substr(0, nl));
     relay_buf_.erase(0, nl + 1);
-    if (l.kind == "hello" && !l.after_reinit && !relay_synced_) {
-      // The connect hello predates the re-enumeration this monitor asked for.
-    } else if (l.kind == "hello") {
-      relay_synced_ = true;
-      bool was = events_ok_;
-      events_ok_ = l.events_ok;
-      events_reason_ = l.events_ok ? "" : "relay: " + l.reason;
-      counters_->events_enabled.store(events_ok_ ? 1 : 0);
-      if (events_ok_ && !was) LOG_INFO(kComp, "events on through the relay at %s", cfg_.event_relay.c_str());
-      if (!events_ok_) LOG_WARN(kComp, "event relay reports %s; using polling only", events_reason_.c_str());
-      if (!l.relay.empty()) counters_->SetRelayCursor({true, l.relay, l.seq, l.gen});
-      if (!events_ok_) {
-        MarkGap("the event relay reports events off (" + l.reason + ")", false);
-      } else if (l.gap != 0) {
-        MarkGap(l.gap != 1             ? "the event relay cannot replay missed events (an older relay)"
-                : !relay_cursor_sent_ ? "a first connection to the event relay: what was sent before it is unknown"
-                                      : "the event relay renewed its registration or no longer holds the events missed",
-                false);
-      } else {
-        for (const auto& key : ledger_->CancelTentativeGaps())
-          LOG_INFO(kComp, "GPU %s: the event relay replayed what was missed; waiting for GPU_POST_RESET again",
-                   key.c_str());
-      }
-    } else if (l.kind == "event") {
-      counters_->AdvanceRelaySeq(l.seq);
-      // The relay's processor -> this snapshot's handle: by KFD node when both
-      // know it, else by PCI address and partition.
-      for (const auto& pr : snap_->procs) {
-        bool hit = l.node != 0xffffffffu && pr.kfd_node != 0xffffffffu ? pr.kfd_node == l.node
-                                                                       : pr.bdf == l.bdf && pr.partition_id == l.part;
-        if (!hit) continue;
-        HandleEvent({pr.handle, l.type, l.message});  // in order with the hellos around it
-        break;
-      }
-    } else if (l.kind.empty()) {
-      LOG_WARN(kComp, "event relay: malformed line ignored");
-    }
+    HandleRelayLine(l);
   }
   if (relay_buf_.size() > 65536) relay_buf_.clear();
   if (closed) RelayClose("the event relay closed the connection");
+}
+
+void Monitor::HandleRelayLine(const RelayLine& l) {
+  if (l.kind == "hello" && !l.after_reinit && !relay_synced_) {
+    // The connect hello predates the re-enumeration this monitor asked for.
+  } else if (l.kind == "hello") {
+    relay_synced_ = true;
+    bool was = events_ok_;
+    events_ok_ = l.events_ok;
+    events_reason_ = l.events_ok ? "" : "relay: " + l.reason;
+    counters_->events_enabled.store(events_ok_ ? 1 : 0);
+    if (events_ok_ && !was) LOG_INFO(kComp, "events on through the relay at %s", cfg_.event_relay.c_str());
+    if (!events_ok_) LOG_WARN(kComp, "event relay reports %s; using polling only", events_reason_.c_str());
+    if (!l.relay.empty()) counters_->SetRelayCursor({true, l.relay, l.seq, l.gen});
+    if (!events_ok_) {
+      MarkGap("the event relay reports events off (" + l.reason + ")", false);
+    } else if (l.gap != 0) {
+      MarkGap(l.gap != 1             ? "the event relay cannot replay missed events (an older relay)"
+              : !relay_cursor_sent_ ? "a first connection to the event relay: what was sent before it is unknown"
+                                    : "the event relay renewed its registration or no longer holds the events missed",
+              false);
+    } else {
+      for (const auto& key : ledger_->CancelTentativeGaps())
+        LOG_INFO(kComp, "GPU %s: the event relay replayed what was missed; waiting for GPU_POST_RESET again",
+                 key.c_str());
+    }
+  } else if (l.kind == "event") {
+    counters_->AdvanceRelaySeq(l.seq);
+    // The relay's processor -> this snapshot's handle: by KFD node when both
+    // know it, else by PCI address and partition. "node=- bdf=-": the relay
+    // could not place it either (amdsmi named a processor it never enumerated).
+    void* handle = nullptr;
+    const bool placed = l.node != 0xffffffffu || (!l.bdf.empty() && l.bdf != "-");
+    for (const auto& pr : snap_->procs) {
+      bool hit = l.node != 0xffffffffu && pr.kfd_node != 0xffffffffu ? pr.kfd_node == l.node
+                                                                     : pr.bdf == l.bdf && pr.partition_id == l.part;
+      if (placed && hit) {
+        handle = pr.handle;
+        break;
+      }
+    }
+    std::string unplaced;
+    if (!handle && placed)
+      unplaced = "the relay's processor (node " + (l.node == 0xffffffffu ? std::string("-") : std::to_string(l.node)) +
+                 ", " + l.bdf + " partition " + std::to_string(l.part) + ") is none of this daemon's";
+    else if (!handle)
+      unplaced = "the event relay could not place it either";
+    // In order with the hellos around it; a replayed event is known by its
+    // relay and sequence number.
+    const HealthCounters::RelayCursor cur = counters_->GetRelayCursor();
+    HandleEvent({handle, l.type, l.message}, unplaced,
+                cur.valid && l.seq ? cur.relay + ":" + std::to_string(l.seq) : std::string());
+  } else if (l.kind.empty()) {
+    LOG_WARN(kComp, "event relay: malformed line ignored");
+  }
 }
 
 void Monitor::ApplyDrain() {
@@ -454,12 +509,29 @@ void Monitor::ApplyReturnRequests() {
   }
 }
 
-void Monitor::PollOnce() {
-  uint64_t poll = counters_->polls.fetch_add(1) + 1;
+void Monitor::Housekeeping() {
   if (!cfg_.drain_file.empty()) {
     ApplyDrain();
     ApplyReturnRequests();
   }
+  for (const auto& g : snap_->gpus) EndQuarantine(g.index);
+}
+
+void Monitor::EndQuarantine(int gpu) {
+  if (!(fail_[gpu] & kFailFlapping)) return;
+  // Quarantine ends after a whole window without a GPU_PRE_RESET (or with
+  // damping turned off).
+  const int64_t now = clock_->WallMs();
+  const int64_t quiet = now - ledger_->LastReset(keys_[gpu], now);
+  if (cfg_.reset_flap_limit <= 0 || quiet >= cfg_.reset_flap_window_ms)
+    Update(gpu, 0, kFailFlapping,
+           cfg_.reset_flap_limit <= 0 ? "reset-flap damping off"
+                                      : "no reset for " + std::to_string(quiet / 1000) + " s: quarantine over");
+}
+
+void Monitor::PollOnce() {
+  uint64_t poll = counters_->polls.fetch_add(1) + 1;
+  Housekeeping();
   size_t answered = 0, ecc_ok = 0, retired_ok = 0;
   std::string counts;
   for (const auto& g : snap_->gpus) {
@@ -535,16 +607,6 @@ bool Monitor::PollLiveness(const inventory::PhysicalGpu& g, void* h, uint64_t po
   }
   // (the counters outlive monitor generations: "ever readable" does too)
   CheckGapRecovery(g.index, alive && activity_ok && (used.ok() || !counters_->HasVramUsed(g.bdf)));
-  if (fail_[g.index] & kFailFlapping) {
-    // Quarantine ends after a whole window without a GPU_PRE_RESET (or with
-    // damping turned off).
-    const int64_t now = WallMs();
-    const int64_t quiet = now - ledger_->LastReset(keys_[g.index], now);
-    if (cfg_.reset_flap_limit <= 0 || quiet >= cfg_.reset_flap_window_ms)
-      Update(g.index, 0, kFailFlapping,
-             cfg_.reset_flap_limit <= 0 ? "reset-flap damping off"
-                                        : "no reset for " + std::to_string(quiet / 1000) + " s: quarantine over");
-  }
   return alive;
 }
 
@@ -612,7 +674,7 @@ std::optional<uint64_t> Monitor::PollEcc(const inventory::PhysicalGpu& g, void* 
 
 void Monitor::MarkGap(const std::string& why, bool tentative) {
   if (!tentative) counters_->event_gaps.fetch_add(1);
-  const int64_t now = NowMs();
+  const int64_t now = SteadyNow();
   for (const auto& g : snap_->gpus) {
     if (!(fail_[g.index] & kFailResetPending)) continue;
     if (!ledger_->MarkGap(keys_[g.index], why, tentative, now)) continue;
@@ -638,7 +700,7 @@ void Monitor::CheckGapRecovery(int gpu, bool alive) {
     ledger_->ClearGap(key);
     return;
   }
-  const int64_t now = NowMs();
+  const int64_t now = SteadyNow();
   if (!alive) {
     ledger_->SetResponsiveSince(key, 0);
     return;
@@ -681,21 +743,37 @@ void Monitor::Update(int gpu, uint32_t set, uint32_t clear, const std::string& r
   }
 }
 
-void Monitor::HandleEvent(const smi::Event& e) {
+void Monitor::HandleEvent(const smi::Event& e, const std::string& unplaced, const std::string& event_id) {
   counters_->events_received.fetch_add(1);
-  int gpu = -1;
-  for (size_t i = 0; i < snap_->procs.size(); ++i)
-    if (snap_->procs[i].handle == e.handle) gpu = snap_->GpuOfHandle(static_cast<int>(i));
-  int verdict = Classify(cfg_, e.type);
-  LOG_INFO(kComp, "event %s(%u) on GPU %d: %s%s", EventName(e.type), e.type, gpu,
-           e.message.c_str(), verdict == 0 ? " (ignored)" : "");
-  if (gpu >= 0) {
-    const char* name = EventName(e.type);
-    counters_->CountEvent(snap_->gpus[gpu].bdf,
-                          strcmp(name, "EVENT") ? std::string(name) : "EVENT_" + std::to_string(e.type));
+  int proc = -1;
+  if (e.handle)
+    for (size_t i = 0; i < snap_->procs.size(); ++i)
+      if (snap_->procs[i].handle == e.handle) proc = static_cast<int>(i);
+  const int gpu = proc >= 0 ? snap_->GpuOfHandle(proc) : -1;
+  const int verdict = Classify(cfg_, e.type);
+  const std::string name = smi::EventTypeName(e.type);
+  if (proc >= 0 && gpu < 0) {
+    // A GPU of the node this daemon does not serve (--devices): the relay
+    // forwards every GPU's events.
+    LOG_DEBUG(kComp, "event %s(%u) on %s, which this daemon does not serve", name.c_str(), e.type,
+              snap_->procs[proc].bdf.c_str());
+    return;
   }
-  if (gpu < 0 || verdict == 0) return;
-  std::string why = std::string(EventName(e.type)) + ": " + e.message;
+  if (gpu < 0) {
+    HandleUnmatched(e, verdict, unplaced.empty() ? "amdsmi named a processor handle it never enumerated" : unplaced);
+    return;
+  }
+  const std::string& bdf = snap_->gpus[gpu].bdf;
+  // KFD's informational events come with every HIP process: not worth a line each.
+  if (e.type > smi::kEvtGpuPostReset && verdict == 0)
+    LOG_DEBUG(kComp, "event %s(%u) on GPU %d (%s): %s (counted)", name.c_str(), e.type, gpu, bdf.c_str(),
+              e.message.c_str());
+  else
+    LOG_INFO(kComp, "event %s(%u) on GPU %d (%s): %s%s", name.c_str(), e.type, gpu, bdf.c_str(), e.message.c_str(),
+             verdict == 0 ? " (ignored)" : "");
+  counters_->CountEvent(bdf, name);
+  if (verdict == 0) return;
+  std::string why = name + ": " + e.message;
   if (verdict > 0) {
     // A completed reset clears every failure, poll-detected ones included,
     // and the ECC count after the reset is the new baseline.
@@ -718,11 +796,11 @@ void Monitor::HandleEvent(const smi::Event& e) {
       // A new reset: only a gap after it lets polling end the wait.
       ledger_->ClearGap(keys_[gpu]);
       if (cfg_.reset_flap_limit > 0) {
-        int n = ledger_->RecordReset(keys_[gpu], WallMs(), cfg_.reset_flap_window_ms);
+        int n = ledger_->RecordReset(keys_[gpu], clock_->WallMs(), cfg_.reset_flap_window_ms, event_id);
         if (n >= cfg_.reset_flap_limit && !(fail_[gpu] & kFailFlapping)) {
           std::string w = std::to_string(cfg_.reset_flap_window_ms / 1000);
           LOG_WARN(kComp, "GPU %s reset %d times within %s s: quarantined until %s s pass without a reset",
-                   snap_->gpus[gpu].bdf.c_str(), n, w.c_str(), w.c_str());
+                   bdf.c_str(), n, w.c_str(), w.c_str());
           Update(gpu, kFailFlapping, 0, std::to_string(n) + " resets within " + w + " s (flapping)");
         }
       }
@@ -730,12 +808,88 @@ void Monitor::HandleEvent(const smi::Event& e) {
   }
 }
 
+void Monitor::HandleUnmatched(const smi::Event& e, int verdict, const std::string& why) {
+  const std::string name = smi::EventTypeName(e.type);
+  counters_->CountUnmatched(name);
+  const bool reset = e.type == smi::kEvtGpuPreReset && verdict < 0;
+  // Logged every time for a reset; otherwise the first ten, then every thousandth.
+  if (reset || ++unmatched_seen_ <= 10 || unmatched_seen_ % 1000 == 0)
+    LOG_ERROR(kComp, "event %s(%u) on a processor that matches no GPU of this node (%s): %s%s", name.c_str(), e.type,
+              why.c_str(), e.message.c_str(),
+              reset ? "; every GPU is held until the polled check (--reset-recovery-hold-ms) or the operator returns it"
+                    : "; counted in amdgpu_dp_unmatched_events_total");
+  if (!reset) return;
+  // The reference's rule for an event that names no device: every device goes
+  // Unhealthy (nvidia.go:244-251). Here every GPU waits for a GPU_POST_RESET,
+  // which cannot be placed either: each gets a confirmed event gap too, so the
+  // polled recovery check brings it back after the hold. A GPU already waiting
+  // for its own GPU_POST_RESET keeps waiting for that (no gap is added to it).
+  const std::string reason = "GPU_PRE_RESET on an unknown processor (" + why + "): " + e.message;
+  const int64_t now = SteadyNow();
+  counters_->event_gaps.fetch_add(1);
+  for (const auto& g : snap_->gpus) {
+    const bool waiting = fail_[g.index] & kFailResetPending;
+    Update(g.index, kFailResetPending, 0, reason);
+    if (!waiting) ledger_->MarkGap(keys_[g.index], "a GPU_PRE_RESET that could not be placed", false, now);
+  }
+}
+
+void Monitor::InProcessWait(int ms, std::vector<smi::Event>* events) {
+  events->clear();
+  Status st = lib_->EventsWait(ms, events);
+  if (!st.ok()) {
+    if (wait_failures_++ == 0) wait_failing_since_ms_ = SteadyNow();
+    if (wait_failures_ == 1 || wait_failures_ % 600 == 0)  // the first, then about one a minute
+      LOG_WARN(kComp, "event wait failed (%llu in a row): %s", static_cast<unsigned long long>(wait_failures_),
+               st.ToString().c_str());
+    // Waits that keep failing deliver no events: say so (the metric, the
+    // relay-less equivalent of the relay's watchdog) and keep trying.
+    if (!events_failing_ && SteadyNow() - wait_failing_since_ms_ > cfg_.event_fail_ms) {
+      events_failing_ = true;
+      counters_->events_enabled.store(0);
+      LOG_ERROR(kComp, "amdsmi event waits have failed for %lld ms: events off, polling only until they succeed",
+                static_cast<long long>(SteadyNow() - wait_failing_since_ms_));
+      MarkGap("amdsmi event waits failing", false);
+    }
+    if (ms > 0) Sleep(ms);
+  } else if (wait_failures_) {
+    wait_failures_ = 0;
+    if (events_failing_) {
+      events_failing_ = false;
+      counters_->events_enabled.store(1);
+      LOG_INFO(kComp, "amdsmi event waits succeed again: events on");
+    }
+  }
+  for (const auto& e : *events) HandleEvent(e);
+}
+
+void Monitor::RelayDeadlines() {
+  // A relay that accepted the reinit but never answers it (its registrar
+  // stuck in amdsmi): events cannot be trusted to arrive.
+  if (relay_fd_ >= 0 && !relay_synced_ && !relay_overdue_ && SteadyNow() - relay_connected_ms_ > cfg_.event_fail_ms) {
+    relay_overdue_ = true;
+    LOG_WARN(kComp, "the event relay has not answered this daemon's reinit for %d ms; polling only until it does",
+             cfg_.event_fail_ms);
+    MarkGap("the event relay did not answer", false);
+  }
+  // A relay away for good cannot replay anything: the tentative gap holds.
+  if (relay_fd_ < 0 && relay_lost_ms_ != 0 && !relay_lost_confirmed_ &&
+      SteadyNow() - relay_lost_ms_ > cfg_.event_fail_ms) {
+    relay_lost_confirmed_ = true;
+    char secs[32];
+    snprintf(secs, sizeof(secs), "%g", cfg_.event_fail_ms / 1000.0);
+    MarkGap(std::string("the event relay has been unreachable for ") + secs + " s", false);
+  }
+}
+
 void Monitor::Run() {
-  using Clock = std::chrono::steady_clock;
-  auto next_poll = Clock::now() + std::chrono::milliseconds(cfg_.poll_interval_ms);
+  using SteadyClock = std::chrono::steady_clock;
+  // Polls, or -- with polls off -- the housekeeping they include.
+  const int period = cfg_.poll_interval_ms > 0 ? cfg_.poll_interval_ms : kHousekeepingMs;
+  auto next_poll = SteadyClock::now() + std::chrono::milliseconds(period);
   std::vector<smi::Event> events;
   while (!stop_.load()) {
-    counters_->loop_beat_ms.store(NowMs());
+    counters_->loop_beat_ms.store(Clock::System()->SteadyMs());  // /healthz compares it with the real clock
     // An amdsmi event wait cannot be interrupted: bounded so Stop() (SIGHUP,
     // config, re-partition, exit) is prompt -- the reference waits 5000 ms.
     // Every other wait here also ends on the wake eventfd, so it sleeps until
@@ -744,76 +898,32 @@ void Monitor::Run() {
     const bool in_process_wait = events_ok_ && (cfg_.event_relay.empty() || !cfg_.events);
     int slice = in_process_wait ? 100 : 5000;
     if (in_process_wait && cfg_.wait_ms > 0 && cfg_.wait_ms < slice) slice = cfg_.wait_ms;
-    if (cfg_.poll_interval_ms > 0) {  // wake for the next poll, not a slice later
-      auto until = std::chrono::duration_cast<std::chrono::milliseconds>(next_poll - Clock::now()).count();
+    {  // wake for the next poll, not a slice later
+      auto until = std::chrono::duration_cast<std::chrono::milliseconds>(next_poll - SteadyClock::now()).count();
       slice = static_cast<int>(std::max<long long>(1, std::min<long long>(slice, until)));
     }
     if (!cfg_.event_relay.empty() && cfg_.events) {
-      const int64_t now = NowMs();
+      const int64_t now = SteadyNow();
       auto due = [&](int64_t at) { slice = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(slice, at - now))); };
       if (relay_fd_ < 0) due(relay_tried_ms_ + relay_retry_ms_);
       if (relay_fd_ >= 0 && !relay_synced_ && !relay_overdue_) due(relay_connected_ms_ + cfg_.event_fail_ms + 1);
       if (relay_fd_ < 0 && relay_lost_ms_ != 0 && !relay_lost_confirmed_) due(relay_lost_ms_ + cfg_.event_fail_ms + 1);
-    }
-    if (!cfg_.event_relay.empty() && cfg_.events) {
-      events.clear();
-      if (relay_fd_ < 0 && NowMs() - relay_tried_ms_ >= relay_retry_ms_) {
+      if (relay_fd_ < 0 && SteadyNow() - relay_tried_ms_ >= relay_retry_ms_) {
         RelayConnect();
         if (relay_fd_ >= 0) LOG_INFO(kComp, "connected to the event relay at %s", cfg_.event_relay.c_str());
       }
       if (relay_fd_ >= 0) RelayWait(slice);
       else Sleep(slice);
-      // A relay that accepted the reinit but never answers it (its registrar
-      // stuck in amdsmi): events cannot be trusted to arrive.
-      if (relay_fd_ >= 0 && !relay_synced_ && !relay_overdue_ &&
-          NowMs() - relay_connected_ms_ > cfg_.event_fail_ms) {
-        relay_overdue_ = true;
-        LOG_WARN(kComp, "the event relay has not answered this daemon's reinit for %d ms; polling only until it does",
-                 cfg_.event_fail_ms);
-        MarkGap("the event relay did not answer", false);
-      }
-      // A relay away for good cannot replay anything: the tentative gap holds.
-      if (relay_fd_ < 0 && relay_lost_ms_ != 0 && !relay_lost_confirmed_ &&
-          NowMs() - relay_lost_ms_ > cfg_.event_fail_ms) {
-        relay_lost_confirmed_ = true;
-        char secs[32];
-        snprintf(secs, sizeof(secs), "%g", cfg_.event_fail_ms / 1000.0);
-        MarkGap(std::string("the event relay has been unreachable for ") + secs + " s", false);
-      }
+      RelayDeadlines();
     } else if (events_ok_) {
-      events.clear();
-      Status st = lib_->EventsWait(slice, &events);
-      if (!st.ok()) {
-        if (wait_failures_++ == 0) wait_failing_since_ms_ = NowMs();
-        if (wait_failures_ == 1 || wait_failures_ % 600 == 0)  // the first, then about one a minute
-          LOG_WARN(kComp, "event wait failed (%llu in a row): %s", static_cast<unsigned long long>(wait_failures_),
-                   st.ToString().c_str());
-        // Waits that keep failing deliver no events: say so (the metric, the
-        // relay-less equivalent of the relay's watchdog) and keep trying.
-        if (!events_failing_ && NowMs() - wait_failing_since_ms_ > cfg_.event_fail_ms) {
-          events_failing_ = true;
-          counters_->events_enabled.store(0);
-          LOG_ERROR(kComp, "amdsmi event waits have failed for %lld ms: events off, polling only until they succeed",
-                    static_cast<long long>(NowMs() - wait_failing_since_ms_));
-          MarkGap("amdsmi event waits failing", false);
-        }
-        Sleep(slice);
-      } else if (wait_failures_) {
-        wait_failures_ = 0;
-        if (events_failing_) {
-          events_failing_ = false;
-          counters_->events_enabled.store(1);
-          LOG_INFO(kComp, "amdsmi event waits succeed again: events on");
-        }
-      }
+      InProcessWait(slice, &events);
     } else {
-      events.clear();
       Sleep(slice);
     }
-    for (const auto& e : events) HandleEvent(e);
-    if (cfg_.poll_interval_ms > 0 && Clock::now() >= next_poll) {
-      PollOnce();
-      next_poll = Clock::now() + std::chrono::milliseconds(cfg_.poll_interval_ms);
+    if (SteadyClock::now() >= next_poll) {
+      if (cfg_.poll_interval_ms > 0) PollOnce();
+      else Housekeeping();
+      next_poll = SteadyClock::now() + std::chrono::milliseconds(period);
     }
   }
   counters_->loop_beat_ms.store(0);

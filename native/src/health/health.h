@@ -74,6 +74,9 @@ namespace adp::health {
 
 // getAdditionalXids semantics: split on ',', trim, keep valid unsigned values in order.
 std::vector<uint64_t> ParseAdditionalIds(std::string_view input);
+// --health-event-extra-types: comma-separated amdsmi event type numbers
+// (1..13) or names ("PROCESS_START"); an error names the first bad entry.
+Result<std::set<uint32_t>> ParseEventTypes(std::string_view input);
 // What failure bits (FailBits) hold a GPU out, in words: "drained by the operator, ...".
 std::string DescribeFailures(uint32_t bits);
 
@@ -92,6 +95,12 @@ struct HealthConfig {
   int event_fail_ms = 10000;
   // amdsmi event notification (--health-events); off = polling only.
   bool events = true;
+  // --health-event-extra-types: amdsmi event types registered on top of the
+  // four the monitor acts on (e.g. 12,13 = KFD PROCESS_START / PROCESS_END,
+  // which any HIP process causes): counted per GPU, never a health verdict.
+  std::set<uint32_t> extra_types;
+  // The registration mask: GPU_PRE/POST_RESET, VMFAULT, THERMAL_THROTTLE and the extra types.
+  uint64_t EventMask() const;
   // Where /dev/kfd is (--driver-root): why event registration failed.
   std::string driver_root = "/";
   // --health-event-socket: events come from the privileged relay (relay.h) at
@@ -111,6 +120,9 @@ struct HealthConfig {
   // passes without one. 0 = off.
   int reset_flap_limit = 3;
   int64_t reset_flap_window_ms = 600000;
+  // Tests (native/tests/health_model.cc): Start() starts no thread; the
+  // harness steps the monitor itself.
+  bool run_thread = true;
   static HealthConfig FromEnv();
   static HealthConfig FromValues(const char* disable_value, const char* poll_ms_value);
 };
@@ -142,6 +154,20 @@ struct GpuRecord {
   // with the verdict, so a process started after it -- whose own connection
   // to the relay may miss nothing -- still lets the polled check end the wait.
   std::string gap;
+  // The relayed GPU_PRE_RESET last counted in `resets` ("<relay>:<seq>"; ""
+  // = none or in-process): a replay of it after a restart -- the persisted
+  // relay cursor lags by up to a second -- is not counted twice.
+  std::string last_reset_event;
+};
+
+// The monitor's time (a test harness drives a fake one): steady for holds,
+// gaps and deadlines; wall for what is persisted (the reset history).
+class Clock {
+ public:
+  virtual ~Clock() = default;
+  virtual int64_t SteadyMs() const;
+  virtual int64_t WallMs() const;
+  static const Clock* System();
 };
 
 // Liveness of the health machinery itself, shared by all Monitor generations
@@ -180,6 +206,10 @@ struct HealthCounters {
   // worth watching.
   void CountEvent(const std::string& bdf, const std::string& type);
   std::map<std::pair<std::string, std::string>, uint64_t> EventCounts() const;
+  // Events on a processor that matches no enumerated one (amdsmi handed back
+  // a handle it never enumerated, or the relay could not place it), by type.
+  void CountUnmatched(const std::string& type);
+  std::map<std::string, uint64_t> Unmatched() const;
   // Event gaps the monitor recorded (any GPU waiting for GPU_POST_RESET or not).
   std::atomic<uint64_t> event_gaps{0};
   // Relay mode: connections to the event relay that broke (it restarted, or
@@ -217,7 +247,7 @@ struct HealthCounters {
   std::map<std::string, uint32_t> retired_;
   std::map<std::string, uint64_t> vram_used_, vram_total_;
   std::map<std::pair<std::string, std::string>, uint64_t> events_;
-  std::map<std::string, uint64_t> recovered_;
+  std::map<std::string, uint64_t> recovered_, unmatched_;
   std::set<std::pair<std::string, std::string>> queries_ok_;
   RelayCursor cursor_;
   std::string cursor_path_;
@@ -272,8 +302,12 @@ class Ledger {
   void SetResponsiveSince(const std::string& key, int64_t ms);
   // Reset history for flap damping (GpuRecord::resets; wall clock, so it
   // survives a restart): records a GPU_PRE_RESET at `now_ms` and returns how
-  // many fall within `window_ms`.
-  int RecordReset(const std::string& key, int64_t now_ms, int64_t window_ms);
+  // many fall within `window_ms`. `event_id` ("<relay>:<seq>" of a relayed
+  // event, "" otherwise): an event of the same relay at or before the last one
+  // recorded is a replay, not recorded again. At most kMaxResetHistory are
+  // kept (the newest): the count only has to reach the limit.
+  static constexpr size_t kMaxResetHistory = 64;
+  int RecordReset(const std::string& key, int64_t now_ms, int64_t window_ms, const std::string& event_id = "");
   // The last recorded reset (none known, e.g. a state file from an older
   // version: `now_ms` is recorded, so its quarantine lasts one more window).
   int64_t LastReset(const std::string& key, int64_t now_ms);
@@ -298,6 +332,8 @@ std::set<std::string> DrainNames(const inventory::PhysicalGpu& g);
 // "1 # maintenance"). "" when no name is left on it (the line goes).
 std::string RemoveDrainNames(std::string_view line, const std::set<std::string>& names);
 
+struct RelayLine;  // relay.h
+
 class Monitor {
  public:
   // `ledger` / `counters` may be null: the Monitor then keeps its own.
@@ -312,15 +348,23 @@ class Monitor {
   Status Start();
   void Stop();
   bool events_enabled() const { return events_ok_.load(); }
+  // Before Start(): where the monitor reads the time (tests; default the system's).
+  void SetClock(const Clock* c) { clock_ = c; }
 
   // Decision function, exposed for tests: how an event changes a GPU's health.
   // Returns +1 (healthy), -1 (unhealthy), 0 (no change).
   static int Classify(const HealthConfig& cfg, uint32_t event_type);
 
  private:
+  friend class MonitorTestPeer;  // native/tests/health_model.cc steps a monitor without its thread
   void Run();
   void Notify(int gpu, bool healthy, const std::string& reason);
   void PollOnce();
+  // What must run whether or not polls do (DP_HEALTH_POLL_MS=0): the drain
+  // file, return-to-service requests and the end of reset-flap quarantines.
+  // Part of every poll, and on a timer of its own when polling is off.
+  void Housekeeping();
+  void EndQuarantine(int gpu);
   void LoadVerdicts();  // Start(): the verdicts, ECC baselines and retired-page thresholds of the GPUs
   // PollOnce's parts, per GPU (h: its first processor's handle). PollLayout:
   // true when the partition modes or xGMI links changed (the supervisor
@@ -379,8 +423,22 @@ class Monitor {
   // Reads relay lines for up to `ms`: hellos update events_ok_ and the event
   // gaps, events are mapped to this snapshot's handles and handled, in order.
   void RelayWait(int ms);
+  void HandleRelayLine(const RelayLine& l);
+  // The relay's deadlines: an unanswered reinit, a relay away for event_fail_ms.
+  void RelayDeadlines();
+  // One in-process amdsmi event wait of up to `ms` (its failures tracked as a
+  // gap once they last event_fail_ms), and the events it returned.
+  void InProcessWait(int ms, std::vector<smi::Event>* events);
   // One amdsmi event (in-process or relayed): counts it and updates health.
-  void HandleEvent(const smi::Event& e);
+  // A null/unknown handle is an unmatched event (`unplaced`: what the relay
+  // said about it); `event_id`: "<relay>:<seq>" of a relayed event.
+  void HandleEvent(const smi::Event& e, const std::string& unplaced = "", const std::string& event_id = "");
+  // An event on no enumerated processor: ERROR + amdgpu_dp_unmatched_events_total;
+  // a GPU_PRE_RESET holds every GPU (reference nvidia.go:244-251).
+  void HandleUnmatched(const smi::Event& e, int verdict, const std::string& why);
+  uint64_t unmatched_seen_ = 0;  // log rate limit
+  const Clock* clock_ = Clock::System();
+  int64_t SteadyNow() const { return clock_->SteadyMs(); }
   std::thread thread_;
   std::atomic<bool> stop_{false};
   std::function<void(const std::string&)> layout_listener_;

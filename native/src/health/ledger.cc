@@ -89,6 +89,8 @@ std::string Ledger::Serialize(const std::map<std::string, GpuRecord>& m) {
         if (c == '\t' || c == '\n' || c == '\r') c = ' ';
       out += "\tgap=" + gap;
     }
+    if (!r.last_reset_event.empty() && r.last_reset_event.find_first_of("\t\n\r ") == std::string::npos)
+      out += "\treset_event=" + r.last_reset_event;
     out += "\n";
   }
   return out;
@@ -139,13 +141,18 @@ std::map<std::string, GpuRecord> Ledger::Parse(const std::string& body) {
       if (f[i].rfind("resets=", 0) == 0 && r.resets.empty()) {
         for (const auto& t : Split(std::string_view(f[i]).substr(7), ',')) {
           auto v = ParseUint(t);
-          if (!v || r.resets.size() >= 64) {
+          if (!v) {
             LOG_WARN(kComp, "health state: reset history of %s malformed; ignored", f[0].c_str());
             r.resets.clear();
             break;
           }
           r.resets.push_back(static_cast<int64_t>(*v));
         }
+        // A longer history (an older version kept every one): the newest count.
+        std::sort(r.resets.begin(), r.resets.end());
+        if (r.resets.size() > kMaxResetHistory) r.resets.erase(r.resets.begin(), r.resets.end() - kMaxResetHistory);
+      } else if (f[i].rfind("reset_event=", 0) == 0 && r.last_reset_event.empty() && f[i].size() > 12) {
+        r.last_reset_event = f[i].substr(12);
       } else if (f[i].rfind("gap=", 0) == 0 && r.gap.empty() && f[i].size() > 4) {
         r.gap = f[i].substr(4);
       }
@@ -176,9 +183,11 @@ void Ledger::Put(const std::string& key, const GpuRecord& r) {
   // MarkGap): a record read earlier does not roll them back.
   std::vector<int64_t> resets = it != recs_.end() ? std::move(it->second.resets) : std::vector<int64_t>{};
   std::string gap = it != recs_.end() ? std::move(it->second.gap) : std::string();
+  std::string last_event = it != recs_.end() ? std::move(it->second.last_reset_event) : std::string();
   recs_[key] = r;
   recs_[key].resets = std::move(resets);
   recs_[key].gap = std::move(gap);
+  recs_[key].last_reset_event = std::move(last_event);
   SaveLocked();
 }
 
@@ -246,13 +255,41 @@ bool Ledger::Gap(const std::string& key, GapMark* out) const {
   return true;
 }
 
-int Ledger::RecordReset(const std::string& key, int64_t now_ms, int64_t window_ms) {
+namespace {
+// "<relay>:<seq>" -> (relay, seq); false when not that shape.
+bool SplitEventId(const std::string& id, std::string* relay, uint64_t* seq) {
+  size_t colon = id.rfind(':');
+  if (colon == std::string::npos || colon == 0) return false;
+  auto v = ParseUint(id.substr(colon + 1));
+  if (!v) return false;
+  *relay = id.substr(0, colon);
+  *seq = *v;
+  return true;
+}
+}  // namespace
+
+int Ledger::RecordReset(const std::string& key, int64_t now_ms, int64_t window_ms, const std::string& event_id) {
   std::lock_guard<std::mutex> lk(mu_);
-  auto& v = recs_[key].resets;
+  GpuRecord& r = recs_[key];
+  auto& v = r.resets;
+  auto in_window = [&] {
+    v.erase(std::remove_if(v.begin(), v.end(), [&](int64_t t) { return now_ms - t >= window_ms; }), v.end());
+    return static_cast<int>(v.size());
+  };
+  std::string relay, last_relay;
+  uint64_t seq = 0, last_seq = 0;
+  if (SplitEventId(event_id, &relay, &seq) && SplitEventId(r.last_reset_event, &last_relay, &last_seq) &&
+      relay == last_relay && seq <= last_seq) {
+    LOG_INFO(kComp, "GPU %s: GPU_PRE_RESET #%llu replayed by the event relay was counted before; not counted again",
+             key.c_str(), static_cast<unsigned long long>(seq));
+    return in_window();
+  }
   v.push_back(now_ms);
-  v.erase(std::remove_if(v.begin(), v.end(), [&](int64_t t) { return now_ms - t >= window_ms; }), v.end());
+  if (v.size() > kMaxResetHistory) v.erase(v.begin(), v.end() - kMaxResetHistory);  // the newest
+  if (!event_id.empty()) r.last_reset_event = event_id;
+  const int n = in_window();
   SaveLocked();
-  return static_cast<int>(v.size());
+  return n;
 }
 
 int64_t Ledger::LastReset(const std::string& key, int64_t now_ms) {

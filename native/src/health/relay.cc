@@ -35,10 +35,11 @@ namespace {
 
 constexpr const char* kComp = "event-relay";
 
-// Every event type the daemon classifies (health.cc Classify).
-uint64_t RelayMask() {
+// Every event type the daemon classifies (health.cc Classify), and the
+// relay's --health-event-extra-types.
+uint64_t RelayMask(uint64_t extra) {
   return smi::EventMask(smi::kEvtGpuPreReset) | smi::EventMask(smi::kEvtGpuPostReset) |
-         smi::EventMask(smi::kEvtVmFault) | smi::EventMask(smi::kEvtThermalThrottle);
+         smi::EventMask(smi::kEvtVmFault) | smi::EventMask(smi::kEvtThermalThrottle) | extra;
 }
 
 std::string OneLine(std::string s) {
@@ -178,8 +179,9 @@ class Registration {
     int64_t renew_ms = 0;   // how long the last renewal took
   };
 
-  Registration(smi::Library* lib, std::string driver_root, int event_fd, int done_fd, int64_t stuck_ms)
-      : lib_(lib), driver_root_(std::move(driver_root)), event_fd_(event_fd), done_fd_(done_fd), stuck_ms_(stuck_ms),
+  Registration(smi::Library* lib, std::string driver_root, uint64_t mask, int event_fd, int done_fd, int64_t stuck_ms)
+      : lib_(lib), driver_root_(std::move(driver_root)), mask_(mask), event_fd_(event_fd), done_fd_(done_fd),
+        stuck_ms_(stuck_ms),
         // The wait's slice (an event ends the wait at once): short, because a
         // renewal must wait for the slice to end before it can stop the waiter;
         // and well under the watchdog's threshold. Idle, that is ~10 wake-ups/s
@@ -205,7 +207,9 @@ class Registration {
   void Renew(bool reinit) {
     const int64_t t0 = NowMs();
     StopWaiter();
-    if (registered_) lib_->EventsStop(handles_);
+    // Every registration the library holds, whether the last renewal
+    // completed or not (it undoes a partial one itself).
+    lib_->EventsStopAll();
     registered_ = false;
     handles_.clear();
     procs_.clear();
@@ -224,7 +228,7 @@ class Registration {
       for (const auto& p : procs_) handles_.push_back(p.handle);
       s.processors = procs_.size();
       s.fp = ProcessorFingerprint(procs_);
-      st = lib_->EventsInit(handles_, RelayMask());
+      st = lib_->EventsInit(handles_, mask_);
       registered_ = st.ok();
       s.ok = st.ok();
       s.reason.clear();
@@ -297,7 +301,7 @@ class Registration {
       return false;
     }
     StopWaiter();
-    if (registered_) lib_->EventsStop(handles_);
+    lib_->EventsStopAll();
     registered_ = false;
     return true;
   }
@@ -363,9 +367,20 @@ class Registration {
           const smi::ProcessorInfo* p = nullptr;
           for (const auto& q : procs_)
             if (q.handle == e.handle) p = &q;
-          if (!p) continue;
-          std::string line = FormatRelayEvent(*p, e.type, e.message);
-          const bool refused = !drop_event_.empty() && line.find(drop_event_) != std::string::npos;  // test hook
+          if (!p) {
+            // A handle amdsmi never enumerated: forwarded unplaced ("node=-
+            // bdf=-"), and each daemon applies its rule for those (a
+            // GPU_PRE_RESET holds every GPU); never dropped silently.
+            const uint64_t n = unmatched_.fetch_add(1) + 1;
+            if (e.type == smi::kEvtGpuPreReset || n <= 10 || n % 1000 == 0)
+              LOG_ERROR(kComp, "event %s(%u) on a processor handle amdsmi did not enumerate (%llu so far): forwarded "
+                        "unplaced", smi::EventTypeName(e.type).c_str(), e.type, static_cast<unsigned long long>(n));
+          }
+          std::string line = p ? FormatRelayEvent(*p, e.type, e.message) : FormatUnplacedRelayEvent(e.type, e.message);
+          bool refused = false;
+#ifdef ADP_TEST_HOOKS
+          refused = !drop_event_.empty() && line.find(drop_event_) != std::string::npos;
+#endif
           if (refused || write(event_fd_, line.data(), line.size()) != static_cast<ssize_t>(line.size())) {
             LOG_ERROR(kComp, "event dropped (relay loop behind): %s", OneLine(line).c_str());
             dropped_.fetch_add(1);  // the poll loop tells the daemons (within a second)
@@ -383,6 +398,7 @@ class Registration {
 
   smi::Library* lib_;
   const std::string driver_root_;
+  const uint64_t mask_;
   const int event_fd_, done_fd_;
   const int64_t stuck_ms_;
   const int slice_ms_;
@@ -397,10 +413,13 @@ class Registration {
   std::atomic<int64_t> beat_ms_{0};    // the waiter's last sign of life
   std::atomic<int> wait_failures_{0};  // consecutive failed waits
   std::atomic<uint64_t> dropped_{0};    // events the pipe refused (TakeDropped)
+  std::atomic<uint64_t> unmatched_{0};  // events on handles amdsmi never enumerated
+#ifdef ADP_TEST_HOOKS
   const std::string drop_event_ = [] {  // test hook: refuse event lines containing it
     const char* e = getenv("ADP_DEBUG_RELAY_REFUSE_EVENT");
     return std::string(e ? e : "");
   }();
+#endif
   mutable std::mutex mu_;
   State state_;
   std::thread registrar_;
@@ -423,7 +442,10 @@ class RelayServer {
  public:
   RelayServer(smi::Library* lib, const RelayOptions& opts)
       : lib_(lib), opts_(opts), stuck_ms_(EnvMs("ADP_RELAY_STUCK_MS", 10000)), relay_id_(RandomId()),
-        drop_on_(Env("ADP_DEBUG_RELAY_DROP_ON")), scans_(opts) {}
+#ifdef ADP_TEST_HOOKS
+        drop_on_(Env("ADP_DEBUG_RELAY_DROP_ON")),
+#endif
+        scans_(opts) {}
   ~RelayServer() {
     for (auto& c : clients_)
       if (c.fd >= 0) close(c.fd);
@@ -454,7 +476,7 @@ class RelayServer {
       return false;
     }
     // Heap-held: a waiter stuck in amdsmi at exit keeps using it (Shutdown).
-    reg_ = new Registration(lib_, opts_.driver_root, ev_pipe_[1], done_pipe_[1], stuck_ms_);
+    reg_ = new Registration(lib_, opts_.driver_root, RelayMask(opts_.extra_mask), ev_pipe_[1], done_pipe_[1], stuck_ms_);
     reg_->StartRegistrar();
     LOG_INFO(kComp, "relaying amdsmi events on %s (relay %s)", socket_path.c_str(), relay_id_.c_str());
     return true;
@@ -580,6 +602,7 @@ class RelayServer {
     }
     if (out.empty()) return;
     LOG_INFO(kComp, "%s", OneLine(out).c_str());
+#ifdef ADP_TEST_HOOKS
     if (!drop_on_.empty() && out.find(drop_on_) != std::string::npos) {
       // Tests: what a daemon whose socket buffer is full sees -- dropped,
       // the events it missed held in the ring for its reconnection.
@@ -591,6 +614,7 @@ class RelayServer {
       LOG_WARN(kComp, "every daemon connection dropped (ADP_DEBUG_RELAY_DROP_ON)");
       return;
     }
+#endif
     Broadcast(out);
   }
 
@@ -724,7 +748,9 @@ class RelayServer {
   const RelayOptions opts_;
   const int64_t stuck_ms_;
   const std::string relay_id_;
+#ifdef ADP_TEST_HOOKS
   const std::string drop_on_;  // test hook (ADP_DEBUG_RELAY_DROP_ON)
+#endif
   std::string socket_path_;
   int lfd_ = -1;
   int ev_pipe_[2] = {-1, -1}, done_pipe_[2] = {-1, -1};

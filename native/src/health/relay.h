@@ -37,6 +37,9 @@
 //                          hangs or keeps failing for ADP_RELAY_STUCK_MS (default
 //                          10 s), "events=ok" again once waits succeed
 //                    "event seq=<n> node=<kfd node|-> bdf=<bdf> part=<partition id> type=<t> <message>"
+//                          ("node=- bdf=-": on a handle amdsmi never enumerated --
+//                          forwarded all the same, the daemon applies its rule for
+//                          an event it cannot place)
 //                          relay: a random ID of this relay process; gen: its
 //                          registration generation (+1 on each re-registration);
 //                          seq: the last event sequence number it forwarded;
@@ -105,6 +108,8 @@ struct RelayRequest {
 RelayRequest ParseRelayRequest(std::string_view line);
 // Without the sequence number (the relay's waiter thread; the poll loop numbers the lines).
 std::string FormatRelayEvent(const smi::ProcessorInfo& p, uint32_t type, const std::string& message);
+// An event on a handle amdsmi never enumerated: "event node=- bdf=- part=0 type=<t> <message>".
+std::string FormatUnplacedRelayEvent(uint32_t type, const std::string& message);
 
 // 16 hex digits identifying a processor layout: every processor's PCI address,
 // partition ID, KFD node and partition modes, order-independent. Daemon and
@@ -122,6 +127,8 @@ struct RelayOptions {
   std::string driver_root = "/";
   std::string proc_root = "/proc";
   std::string kfd_proc_dir = "/sys/class/kfd/kfd/proc";
+  // --health-event-extra-types of the relay: registered too, forwarded like the rest.
+  uint64_t extra_mask = 0;
 };
 int RunEventRelay(smi::Library* lib, const std::string& socket_path, int signal_fd, const RelayOptions& opts = {});
 

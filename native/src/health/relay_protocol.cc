@@ -139,6 +139,10 @@ std::string FormatRelayEvent(const smi::ProcessorInfo& p, uint32_t type, const s
          " type=" + std::to_string(type) + " " + OneLine(message) + "\n";
 }
 
+std::string FormatUnplacedRelayEvent(uint32_t type, const std::string& message) {
+  return "event node=- bdf=- part=0 type=" + std::to_string(type) + " " + OneLine(message) + "\n";
+}
+
 std::string ProcessorFingerprint(const std::vector<smi::ProcessorInfo>& procs) {
   std::vector<std::string> keys;
   keys.reserve(procs.size());

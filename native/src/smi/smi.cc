@@ -76,7 +76,18 @@ std::string FormatBdf(uint64_t bdf_id) {
 
 uint64_t EventMask(uint32_t event_type) { return AMDSMI_EVENT_MASK_FROM_INDEX(event_type); }
 
+std::string EventTypeName(uint32_t type) {
+  static const char* const kNames[] = {
+      "NONE",           "VMFAULT",       "THERMAL_THROTTLE", "GPU_PRE_RESET", "GPU_POST_RESET",
+      "MIGRATE_START",  "MIGRATE_END",   "PAGE_FAULT_START", "PAGE_FAULT_END", "QUEUE_EVICTION",
+      "QUEUE_RESTORE",  "UNMAP_FROM_GPU", "PROCESS_START",   "PROCESS_END"};
+  static_assert(sizeof(kNames) / sizeof(kNames[0]) == AMDSMI_EVT_NOTIF_LAST + 1, "amdsmi event types changed");
+  if (type >= 1 && type <= AMDSMI_EVT_NOTIF_LAST) return kNames[type];
+  return "EVENT_" + std::to_string(type);
+}
+
 Library::~Library() {
+  if (f_) EventsStopAll();
   if (initialized_ && f_ && f_->shut_down) f_->shut_down();
   if (dl_) dlclose(dl_);
 }
@@ -336,15 +347,37 @@ int Library::XgmiLinksDown(void* h) {
 Status Library::EventsInit(const std::vector<void*>& handles, uint64_t mask) {
   if (!f_->evt_init || !f_->evt_mask || !f_->evt_get)
     return NotSupported("event notification API not present");
-  for (void* h : handles) {
-    amdsmi_status_t st = f_->evt_init(h);
-    if (st != AMDSMI_STATUS_SUCCESS)
-      return Status(st == AMDSMI_STATUS_NOT_SUPPORTED ? Code::kNotSupported : Code::kUnavailable,
-                    "amdsmi_init_gpu_event_notification failed (" + std::to_string(st) + ")");
+  std::lock_guard<std::mutex> lk(evt_mu_);
+  std::vector<void*> fresh;  // registered by this call: undone if a later handle fails
+  auto rollback = [&](size_t failed_at, const Status& why) {
+    if (!fresh.empty() && !f_->evt_stop)
+      LOG_WARN(kComp, "%zu event registration(s) cannot be undone: amdsmi_stop_gpu_event_notification missing",
+               fresh.size());
+    else if (!fresh.empty())
+      LOG_WARN(kComp, "event registration failed on processor %zu of %zu: undoing the %zu made before it", failed_at,
+               handles.size(), fresh.size());
+    if (f_->evt_stop)
+      for (void* r : fresh) f_->evt_stop(r);
+    return why;
+  };
+  for (size_t i = 0; i < handles.size(); ++i) {
+    void* h = handles[i];
+    const bool live = std::find(evt_live_.begin(), evt_live_.end(), h) != evt_live_.end();
+    amdsmi_status_t st = AMDSMI_STATUS_SUCCESS;
+    if (!live) {
+      st = f_->evt_init(h);
+      if (st != AMDSMI_STATUS_SUCCESS)
+        return rollback(i, Status(st == AMDSMI_STATUS_NOT_SUPPORTED ? Code::kNotSupported : Code::kUnavailable,
+                                  "amdsmi_init_gpu_event_notification failed (" + std::to_string(st) + ") on processor " +
+                                      std::to_string(i)));
+      fresh.push_back(h);  // initialised: stopped again if anything below fails
+    }
     st = f_->evt_mask(h, mask);
     if (st != AMDSMI_STATUS_SUCCESS)
-      return Unavailable("amdsmi_set_gpu_event_notification_mask failed (" + std::to_string(st) + ")");
+      return rollback(i, Unavailable("amdsmi_set_gpu_event_notification_mask failed (" + std::to_string(st) +
+                                     ") on processor " + std::to_string(i)));
   }
+  evt_live_.insert(evt_live_.end(), fresh.begin(), fresh.end());
   return Status::Ok();
 }
 
@@ -366,8 +399,25 @@ Status Library::EventsWait(int timeout_ms, std::vector<Event>* out) {
 }
 
 void Library::EventsStop(const std::vector<void*>& handles) {
-  if (!f_->evt_stop) return;
-  for (void* h : handles) f_->evt_stop(h);
+  std::lock_guard<std::mutex> lk(evt_mu_);
+  for (void* h : handles) {
+    auto it = std::find(evt_live_.begin(), evt_live_.end(), h);
+    if (it == evt_live_.end()) continue;
+    if (f_->evt_stop) f_->evt_stop(h);
+    evt_live_.erase(it);
+  }
+}
+
+void Library::EventsStopAll() {
+  std::lock_guard<std::mutex> lk(evt_mu_);
+  if (f_->evt_stop)
+    for (void* h : evt_live_) f_->evt_stop(h);
+  evt_live_.clear();
+}
+
+size_t Library::EventsRegistered() const {
+  std::lock_guard<std::mutex> lk(evt_mu_);
+  return evt_live_.size();
 }
 
 Result<uint64_t> Library::UncorrectableErrors(void* h) {
@@ -425,6 +475,7 @@ std::pair<std::string, std::string> Library::PartitionModes(void* h) {
 }
 
 Status Library::Reinit() {
+  EventsStopAll();  // the handles die with the shut-down; their registrations must not outlive them unstopped
   if (initialized_) f_->shut_down();
   initialized_ = false;
   amdsmi_status_t st = f_->init(AMDSMI_INIT_AMD_GPUS);
@@ -519,7 +570,14 @@ std::string Library::QueryReport() {
       int st = f_->process_list(h, &n, buf.data());
       add("process_list", st, st == 0 ? std::to_string(n) : "");
     } else add("process_list", kMissing);
-    if (f_->evt_init && f_->evt_mask && f_->evt_stop) {
+    bool live;
+    {
+      std::lock_guard<std::mutex> lk(evt_mu_);
+      live = std::find(evt_live_.begin(), evt_live_.end(), h) != evt_live_.end();
+    }
+    if (live) {
+      add("event_notification_init", 0, "\"registered by this process\"");  // not re-registered: no double init
+    } else if (f_->evt_init && f_->evt_mask && f_->evt_stop) {
       int st = f_->evt_init(h);
       add("event_notification_init", st);
       if (st == 0) {

@@ -17,6 +17,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -72,7 +73,16 @@ enum EventType : uint32_t {  // amdsmi_evt_notification_type_t values
   kEvtThermalThrottle = 2,
   kEvtGpuPreReset = 3,
   kEvtGpuPostReset = 4,
+  // 5..13: KFD's informational events (migration, page faults, queue
+  // eviction/restore, unmap, process start/end) -- never a device failure.
+  kEvtProcessStart = 12,
+  kEvtProcessEnd = 13,
+  kEvtLast = 13,
 };
+
+// "GPU_PRE_RESET", "PROCESS_START", ... (amdsmi's names without the
+// AMDSMI_EVT_NOTIF_ prefix); "EVENT_<n>" for a type amdsmi does not define.
+std::string EventTypeName(uint32_t type);
 
 struct Event {
   void* handle = nullptr;
@@ -100,11 +110,21 @@ class Library {
   // Number of xGMI links reported down (0 when unsupported).
   int XgmiLinksDown(void* h);
 
-  // Event notification (health). Init registers `mask` on each handle.
+  // Event notification (health). Init registers `mask` on each handle, all or
+  // nothing: when one handle's registration fails, the handles it had already
+  // registered are stopped again before it returns, so a failed init leaves no
+  // registration behind (a reload re-registering them would otherwise leak
+  // the kernel's event file of each). A handle already registered by an
+  // earlier EventsInit only gets the new mask.
   Status EventsInit(const std::vector<void*>& handles, uint64_t mask);
   // Waits up to timeout_ms; appends received events.
   Status EventsWait(int timeout_ms, std::vector<Event>* out);
+  // Stops the registrations among `handles` (the others: nothing to stop).
   void EventsStop(const std::vector<void*>& handles);
+  // Stops every registration this Library holds (before a Reinit).
+  void EventsStopAll();
+  // Registrations held (tests; /metrics).
+  size_t EventsRegistered() const;
 
   // RAS polling (fallback health when events are unavailable).
   Result<uint64_t> UncorrectableErrors(void* h);
@@ -141,6 +161,8 @@ class Library {
   std::unique_ptr<Fns> f_;
   std::string path_;
   bool initialized_ = false;
+  mutable std::mutex evt_mu_;
+  std::vector<void*> evt_live_;  // handles with a live event registration
 };
 
 std::string FormatBdf(uint64_t bdf_id);

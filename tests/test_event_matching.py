@@ -1,0 +1,237 @@
+"""Events that name no known processor, opt-in extra event types, and the
+rollback of a partial event registration (round-6 review items 1 and 3).
+
+* Unmatched events. The reference makes every device Unhealthy when an event
+  names no device (/root/reference/cmd/nvidia-device-plugin/nvidia.go:244-251).
+  Here an event on a processor handle amdsmi never enumerated -- in-process,
+  or one the event relay could not place ("node=- bdf=-") -- is logged as an
+  ERROR and counted in amdgpu_dp_unmatched_events_total{type}; an unmatched
+  GPU_PRE_RESET holds every GPU (reset pending, with a confirmed event gap, so
+  the polled check brings each back after --reset-recovery-hold-ms). The mock
+  delivers such events with FIFO lines "foreign <type>".
+* --health-event-extra-types: KFD's informational events (PROCESS_START = 12,
+  PROCESS_END = 13, ...) registered on top, counted per GPU and never a verdict.
+* A registration that fails on one processor is undone on the ones before it
+  (smi.cc EventsInit), and every stop releases whatever was registered: across
+  SIGHUPs the mock's live registration count returns to what is expected and
+  no handle is registered twice (reference nvidia.go:210-226 deletes its
+  event set whatever happened).
+"""
+
+import os
+import re
+import signal
+import subprocess
+import time
+
+import pytest
+
+from k8s_gpu_sharing_plugin_amd import DAEMON, MOCK_LIB
+from k8s_gpu_sharing_plugin_amd.models import fixtures
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet, native
+
+from test_event_relay import RelayNode
+from test_health import Node
+from test_metrics import _get, _parse
+
+
+def _samples(port, name):
+    m = _parse(_get(port, "/metrics")[1])
+    return {tuple(sorted(ls)): v for (n, ls), v in m.items() if n == name}
+
+
+def _wait_samples(port, name, want, timeout=5.0):
+    deadline = time.monotonic() + timeout
+    while True:
+        got = _samples(port, name)
+        if all(got.get(k) == v for k, v in want.items()) or time.monotonic() > deadline:
+            return got
+        time.sleep(0.05)
+
+
+def _port(d):
+    return int(re.search(r"on port (\d+)", d.wait_log("serving /metrics")).group(1))
+
+
+def test_event_types_parse_and_classify():
+    c = native.health_config("", "")
+    assert all(c["verdicts"][str(t)] == 0 for t in range(5, 14)), c  # KFD's informational events: no verdict
+    assert c["verdicts"]["3"] == -1 and c["verdicts"]["4"] == 1
+
+
+@pytest.mark.parametrize("value", ["99", "0", "PROCESS_BEGIN", "12,x"])
+def test_unknown_extra_event_type_is_refused(scratch, value):
+    env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB,
+               AMDSMI_MOCK_FIXTURE=fixtures.write(fixtures.node(1), scratch + ".fixture"))
+    r = subprocess.run([DAEMON, "--device-plugin-path", scratch, "--health-event-extra-types", value],
+                       capture_output=True, text=True, timeout=30, env=env)
+    assert r.returncode == 1 and "invalid --health-event-extra-types option" in r.stdout + r.stderr, r
+
+
+def test_extra_event_types_are_counted_never_a_verdict(scratch):
+    n = Node(scratch, fixtures.node(2), args=["--metrics-addr", "127.0.0.1:0",
+                                              "--health-event-extra-types", "12, process_end"])
+    try:
+        port = _port(n.d)
+        bdf = [g["bdf"] for g in fixtures.node(2)["gpus"]]
+        for line in ("0 12 4d2 python3", "0 13 4d2 python3", "1 12 4d3 probe", "1 5 migrate (not registered)"):
+            n.inject(line)
+        want = {(("bdf", bdf[0]), ("type", "PROCESS_START")): 1, (("bdf", bdf[0]), ("type", "PROCESS_END")): 1,
+                (("bdf", bdf[1]), ("type", "PROCESS_START")): 1}
+        got = _wait_samples(port, "amdgpu_dp_gpu_events_total", want)
+        assert got == want, got  # MIGRATE_START (5) was not registered: the mock filters it, as amdsmi does
+        time.sleep(0.3)
+        assert n.q.empty()  # no health transition
+        assert "events off" not in n.d.log()
+    finally:
+        n.close()
+
+
+@pytest.mark.parametrize("layout", ["in-process", "relay"])
+def test_unmatched_pre_reset_holds_every_gpu_until_polled_recovery(scratch, layout):
+    hold = ["--reset-recovery-hold-ms", "600"]
+    if layout == "relay":
+        n = RelayNode(scratch, daemon_args=hold)
+        d, relay = n.d, n.relay
+        d.wait_log("events on through the relay")
+        port = n.port
+        health = n.health
+    else:
+        n = Node(scratch, fixtures.node(2), args=["--metrics-addr", "127.0.0.1:0", *hold],
+                 env={"DP_HEALTH_POLL_MS": "100"})
+        d, relay = n.d, None
+        port = _port(d)
+
+        def health(timeout=5):
+            return [x.health for x in n.next(timeout).devices]
+    try:
+        n.inject("foreign 1 a VM fault on a handle nobody enumerated")
+        n.inject("foreign 3 reset of a processor amdsmi never named")
+        deadline = time.monotonic() + 10
+        h = health()
+        while h != ["Unhealthy", "Unhealthy"]:
+            h = health(max(0.05, deadline - time.monotonic()))
+        log = d.wait_log("GPU_PRE_RESET(3) on a processor that matches no GPU of this node")
+        assert "every GPU is held until the polled check" in log
+        got = _wait_samples(port, "amdgpu_dp_unmatched_events_total",
+                            {(("type", "GPU_PRE_RESET"),): 1, (("type", "VMFAULT"),): 1})
+        assert got == {(("type", "GPU_PRE_RESET"),): 1, (("type", "VMFAULT"),): 1}, got
+        if relay is not None:
+            rlog = relay.wait_log("forwarded unplaced")
+            assert "processor handle amdsmi did not enumerate" in rlog
+            assert "the event relay could not place it either" in log
+        else:
+            assert "amdsmi named a processor handle it never enumerated" in log
+        # back after the hold, by the polled check (no GPU_POST_RESET can be placed)
+        deadline = time.monotonic() + 10
+        while h != ["Healthy", "Healthy"]:
+            h = health(max(0.05, deadline - time.monotonic()))
+        rec = _samples(port, "amdgpu_dp_gpu_recovered_without_event_total")
+        assert sorted(rec.values()) == [1, 1], rec
+        assert d.log().count("recovered without GPU_POST_RESET") == 2
+    finally:
+        (n.stop if layout == "relay" else n.close)()
+
+
+def test_unmatched_post_reset_and_ignored_types_change_nothing(scratch):
+    n = Node(scratch, fixtures.node(2), args=["--metrics-addr", "127.0.0.1:0"])
+    try:
+        port = _port(n.d)
+        for line in ("foreign 4 post", "foreign 2 thermal", "foreign 12 not registered anywhere"):
+            n.inject(line)
+        want = {(("type", "GPU_POST_RESET"),): 1, (("type", "THERMAL_THROTTLE"),): 1,
+                (("type", "PROCESS_START"),): 1, (("type", "GPU_PRE_RESET"),): 0}
+        got = _wait_samples(port, "amdgpu_dp_unmatched_events_total", want)
+        assert got == want, got
+        time.sleep(0.3)
+        assert n.q.empty()
+        assert n.d.log().count("matches no GPU of this node") == 3
+    finally:
+        n.close()
+
+
+def test_relay_event_on_a_gpu_this_daemon_does_not_serve_is_not_unmatched(scratch):
+    n = RelayNode(scratch, daemon_args=["--devices", "0"])
+    try:
+        n.d.wait_log("events on through the relay")
+        n.inject("1 3 reset of the GPU another daemon serves")
+        n.inject("0 1 fault here")  # in order after it: once this is seen, the other was handled
+        n.d.wait_log("VMFAULT(1) on GPU 0")
+        assert _samples(n.port, "amdgpu_dp_unmatched_events_total") == {(("type", "GPU_PRE_RESET"),): 0}
+        time.sleep(0.2)
+        assert n.q.empty()
+    finally:
+        n.stop()
+
+
+def _evt(path):
+    text = open(path).read() if os.path.exists(path) else ""
+    return {k: int(v) for k, v in re.findall(r"(\w+)=(\d+)", text)}
+
+
+@pytest.mark.parametrize("fail_on", [None, [1]])
+def test_event_registration_is_never_leaked_across_reloads(scratch, tmp_path, fail_on):
+    """GPU 1's registration fails (fail_on=[1]): the one made on GPU 0 is undone,
+    events are off (polling), and every SIGHUP generation starts from zero live
+    registrations -- nothing registered twice, nothing left at shutdown. Without
+    the fault, each generation holds exactly one registration per processor."""
+    fx = fixtures.node(2)
+    if fail_on:
+        fx["evt_init_fail_on"] = fail_on
+    evt = str(tmp_path / "evt")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fx, env={"AMDSMI_MOCK_EVT_FILE": evt, "DP_HEALTH_POLL_MS": "100"}).start()
+    try:
+        k.wait_registration()
+        d.wait_log("health monitor watching")
+        want_live = 0 if fail_on else 2
+        for gen in range(1, 5):
+            if gen > 1:
+                d.signal(signal.SIGHUP)
+                d.wait_log("health monitor watching", count=gen, timeout=15)
+            s = _evt(evt)
+            assert s["live"] == want_live and s["double_init"] == 0 and s["leaked_at_shutdown"] == 0, (gen, s)
+        log = d.log()
+        if fail_on:
+            assert log.count("undoing the 1 made before it") == 4, log[-3000:]
+            assert "events off: amdsmi event notification unavailable" in log
+    finally:
+        assert d.stop() == 0
+        k.stop()
+    s = _evt(evt)
+    assert s["live"] == 0 and s["double_init"] == 0 and s["leaked_at_shutdown"] == 0, s
+    assert s["stops"] >= s["inits"], s
+
+
+def test_relay_never_leaks_a_registration_across_renewals(scratch, tmp_path):
+    """The relay's renewals (a daemon with a different processor view, or
+    events off) stop whatever the last one registered, complete or not."""
+    fx = dict(fixtures.node(2), evt_init_fail_on=[1])
+    evt = str(tmp_path / "evt")
+    sock = os.path.join(scratch + ".fixture", "events.sock")
+    os.makedirs(scratch + ".fixture", exist_ok=True)
+    rdir = scratch + "-relay"
+    os.makedirs(rdir, exist_ok=True)
+    relay = harness.Daemon(rdir, fx, args=["--event-relay", "--health-event-socket", sock],
+                           env={"AMDSMI_MOCK_EVT_FILE": evt}).start()
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = None
+    try:
+        relay.wait_log("event notification unavailable")
+        d = harness.Daemon(scratch, fx, args=["--health-event-socket", sock],
+                           env={"DP_HEALTH_POLL_MS": "100"}).start()
+        k.wait_registration()
+        for gen in range(1, 4):
+            if gen > 1:
+                d.signal(signal.SIGHUP)
+            relay.wait_log("re-enumerating (a daemon asked: events are off)", count=gen, timeout=15)
+            relay.wait_log("event notification unavailable", count=gen + 1, timeout=15)
+            s = _evt(evt)
+            assert s["live"] == 0 and s["double_init"] == 0 and s["leaked_at_shutdown"] == 0, (gen, s)
+    finally:
+        if d:
+            d.stop()
+        k.stop()
+        assert relay.stop() == 0
+    s = _evt(evt)
+    assert s["live"] == 0 and s["double_init"] == 0 and s["leaked_at_shutdown"] == 0, s

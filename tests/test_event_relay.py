@@ -32,8 +32,9 @@ def _preload(*libs):
 
 
 class RelayNode:
-    def __init__(self, scratch, relay_env=None, daemon_args=(), daemon_env=None):
+    def __init__(self, scratch, relay_env=None, daemon_args=(), daemon_env=None, relay_launch=None):
         self.scratch = scratch
+        self.relay_launch = relay_launch  # argv -> argv for the relay process (e.g. another build's binary)
         self.fifo = os.path.join(scratch + ".fixture", "events")
         os.makedirs(scratch + ".fixture", exist_ok=True)
         os.mkfifo(self.fifo)
@@ -58,7 +59,7 @@ class RelayNode:
         rdir = self.scratch + f"-relay{n}"
         os.makedirs(rdir, exist_ok=True)
         self.relay = harness.Daemon(rdir, self.fx, args=["--event-relay", "--health-event-socket", self.sock],
-                                    env=self.relay_env, event_fifo=self.fifo).start()
+                                    env=self.relay_env, event_fifo=self.fifo, launch=self.relay_launch).start()
         self.relay.wait_log("relaying amdsmi events on")
 
     def inject(self, line):

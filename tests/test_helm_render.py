@@ -308,7 +308,7 @@ def test_prometheus_operator_objects():
     assert sm["spec"]["selector"]["matchLabels"].items() <= svc["metadata"]["labels"].items()
     assert sm["spec"]["endpoints"] == [{"port": "metrics", "path": "/metrics", "interval": "30s"}]
     rules = rule["spec"]["groups"][0]["rules"]
-    assert len(rules) == 18 and all(r["alert"].startswith("AmdGpu") for r in rules)
+    assert len(rules) == 19 and all(r["alert"].startswith("AmdGpu") for r in rules)
     over = [r for r in rules if r["alert"] == "AmdGpuContainerOverHbmGrant"][0]
     assert "amdgpu_dp_container_hbm_over_grant" in over["expr"] and over["labels"]["severity"] == "critical"
     assert "> 0.9" in [r for r in rules if r["alert"] == "AmdGpuContainerNearHbmGrant"][0]["expr"]

@@ -61,6 +61,7 @@ def runtime_stages():
 def test_runtime_stage_provides_every_needed_library(dist, name, base, lines):
     if not (os.path.exists(DAEMON) and os.path.exists(PROBE_BIN)):
         pytest.skip("native artefacts not built")
+    image.ensure_image_tree()
     pkgs, copies = stage_contents(lines)
     shipped, copied_names = [], set()
     for src in copies:
@@ -79,7 +80,7 @@ def test_runtime_stage_provides_every_needed_library(dist, name, base, lines):
     for f in shipped:
         for so in sonames(f):
             need.setdefault(so, set()).add(os.path.basename(f))
-        if f == DAEMON:
+        if os.path.basename(f) == "amdgpu-device-plugin":
             for so in DAEMON_DLOPENS:
                 need.setdefault(so, set()).add("amdgpu-device-plugin (dlopen)")
         elif f.startswith(ROCM_LIB):

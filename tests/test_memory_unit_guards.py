@@ -239,3 +239,52 @@ def test_a_layout_change_under_live_grants_can_wait_for_the_pods(scratch):
         d.stop()
         k.stop()
         pr.stop()
+
+
+def test_a_whole_gpu_resource_turned_into_replicas_waits_for_its_pods(scratch):
+    """--defer-layout-changes, from a whole-GPU resource (no replicas, an empty
+    layout) to time-slice replicas while a pod holds one GPU exclusively: the
+    same GPU would be shared by new pods -- a re-meaning, deferred like any
+    other (round-5 advice: an empty layout becoming non-empty is a change)."""
+    pr_sock = os.path.join(scratch + ".fixture", "pod-resources.sock")
+    os.makedirs(os.path.dirname(pr_sock), exist_ok=True)
+    pr = PodResourcesStub(pr_sock)
+    cfg = os.path.join(scratch + ".fixture", "config.yaml")
+
+    def write(rc):
+        tmp = cfg + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(f"version: v1\nflags:\n  resourceConfig: {rc}\n")
+        os.rename(tmp, cfg)
+    write("gpu:gpu:1")
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(2), args=[
+        "--config-file", cfg, "--metrics-addr", "127.0.0.1:0", "--pod-resources-socket", pr_sock,
+        "--defer-layout-changes"], env={"ADP_DEFER_RECHECK_MS": "300"}).start()
+    port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics")).group(1))
+    try:
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        c.close()
+        assert len(ids) == 2 and not any("-replica-" in i for i in ids)
+        res = "amd.com/gpu"
+        pr.payload = _list_response([("ml", "train", "main", res, [ids[0]])])
+        write("gpu:gpu:4")  # the held GPU would become 4 replicas, 3 of them for new pods
+        log = d.wait_log("config change deferred")
+        assert f"running pods hold IDs of '{res}'" in log
+        time.sleep(0.8)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        assert [x.ID for x in c.watch()[0].get(timeout=5).devices] == ids  # still whole GPUs
+        c.close()
+        assert _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_deferred_layout_change", resource=res) == 1
+        pr.payload = _list_response([])  # the pod ended
+        reg = k.wait_registration(15)
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        assert len(c.watch()[0].get(timeout=5).devices) == 8
+        c.close()
+        assert "what its IDs mean changed while" not in d.log()
+    finally:
+        d.stop()
+        k.stop()
+        pr.stop()

@@ -10,6 +10,9 @@
 #                shipped without build/; normally built on the CPU side)
 #   tests        pytest -m gpu (thread-method timeouts, so a hang names its test)
 #   smoke        __graft_entry__.smoke()
+#   events       real amdsmi events (KFD PROCESS_START/END from the HIP probe):
+#                raw, in-process and through the relay (tests/test_gpu_events.py);
+#                records in gpurun_out/r6/
 #   bench        the driver-shaped headline run (python bench.py, defaults)
 #   configs      bench for the three real-hardware configs (spx-none,
 #                timeslice4, auto-mem), 50 steps each
@@ -60,6 +63,11 @@ step_tests() {
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
     -p no:cacheprovider > $out/pytest_gpu.log 2>&1 || die "GPU TESTS" $out/pytest_gpu.log
   tail -2 $out/pytest_gpu.log
+}
+step_events() {
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_events.py -m gpu -v -rs --timeout 180 --timeout-method thread \
+    -p no:cacheprovider > $out/pytest_events.log 2>&1 || die EVENTS $out/pytest_events.log
+  tail -4 $out/pytest_events.log
 }
 step_smoke() {
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.json 2> $out/smoke.err || die SMOKE $out/smoke.err
