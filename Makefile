@@ -31,8 +31,12 @@ build:
 probe:
 	$(PY) -c "from k8s_gpu_sharing_plugin_amd.utils import build; build.build_probe()"
 
+# Unit tests, then the bounded model check of the health state machine: every
+# sequence of up to HEALTH_MODEL_DEPTH steps over its 16 events, both layouts.
+HEALTH_MODEL_DEPTH ?= 6
 test-native: build
 	$(BUILD)/adp_unit_tests
+	$(BUILD)/adp_health_model --depth $(HEALTH_MODEL_DEPTH)
 
 test: build
 	$(PY) -m pytest tests -q -m "not gpu"

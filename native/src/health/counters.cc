@@ -115,7 +115,7 @@ void HealthCounters::AdvanceRelaySeq(uint64_t seq) {
   if (!cursor_.valid || seq <= cursor_.seq) return;
   cursor_.seq = seq;
   cursor_dirty_ = true;
-  if (NowMs() - cursor_saved_ms_ >= 1000) SaveCursorLocked();
+  if (clock_->SteadyMs() - cursor_saved_ms_ >= 1000) SaveCursorLocked();
 }
 
 void HealthCounters::PersistRelayCursor(const std::string& path) {
@@ -150,7 +150,7 @@ void HealthCounters::FlushRelayCursor() {
 
 void HealthCounters::SaveCursorLocked() {
   if (cursor_path_.empty() || !cursor_dirty_ || !cursor_.valid) return;
-  cursor_saved_ms_ = NowMs();
+  cursor_saved_ms_ = clock_->SteadyMs();
   cursor_dirty_ = false;
   std::string body = "adp-relay-cursor v1\n" + cursor_.relay + "\t" + std::to_string(cursor_.seq) + "\t" +
                      std::to_string(cursor_.gen) + "\n";

@@ -304,12 +304,14 @@ void Monitor::Stop() {
     close(wake_fd_);
     wake_fd_ = -1;
   }
-  if (relay_fd_ >= 0) {
-    close(relay_fd_);
+  if (!cfg_.event_relay.empty()) {
+    // Connected or not: where this daemon is in the relay's stream goes to
+    // the state file, so a restart is not replayed what it already handled.
+    if (relay_fd_ >= 0) close(relay_fd_);
     relay_fd_ = -1;
     events_ok_ = false;
     counters_->FlushRelayCursor();
-  } else if (cfg_.event_relay.empty() && lib_) {
+  } else if (lib_) {
     // Whatever is registered, events on or not (the library undoes a partial
     // registration itself, and stops only what it holds).
     lib_->EventsStop(handles_);
@@ -320,14 +322,20 @@ void Monitor::Stop() {
 
 void Monitor::RelayConnect() {
   relay_tried_ms_ = SteadyNow();
-  relay_fd_ = ConnectRelay(cfg_.event_relay);
-  if (relay_fd_ < 0) {
+  int fd = ConnectRelay(cfg_.event_relay);
+  if (fd < 0) {
     events_reason_ = "event relay " + cfg_.event_relay + " not reachable (" + strerror(errno) + ")";
     if (relay_lost_ms_ == 0) relay_lost_ms_ = SteadyNow();
     counters_->relay_connected.store(0);
     relay_retry_ms_ = std::min(1000, relay_retry_ms_ * 2);
     return;
   }
+  RelayAttach(fd);
+}
+
+void Monitor::RelayAttach(int fd) {
+  relay_fd_ = fd;
+  relay_tried_ms_ = SteadyNow();
   relay_retry_ms_ = 100;
   relay_lost_ms_ = 0;
   relay_lost_confirmed_ = false;
@@ -436,6 +444,11 @@ void Monitor::HandleRelayLine(const RelayLine& l) {
     const HealthCounters::RelayCursor cur = counters_->GetRelayCursor();
     HandleEvent({handle, l.type, l.message}, unplaced,
                 cur.valid && l.seq ? cur.relay + ":" + std::to_string(l.seq) : std::string());
+    // An event that changed a verdict is saved as handled at once (others at
+    // most once a second): a restart replaying a GPU_PRE_RESET the operator
+    // has since returned, or a GPU_POST_RESET older than an ECC verdict,
+    // would undo what came after it.
+    if (Classify(cfg_, l.type) != 0) counters_->FlushRelayCursor();
   } else if (l.kind.empty()) {
     LOG_WARN(kComp, "event relay: malformed line ignored");
   }

@@ -235,12 +235,17 @@ struct HealthCounters {
   // With --health-state-file the cursor also outlives the process (<state>.relay):
   // a restarted plugin container resumes the relay's stream where it left it,
   // and the relay replays what it missed instead of reporting a gap. Loaded
-  // here; written on every hello, at most once a second for events, and by
-  // FlushRelayCursor (monitor stop). A cursor that lags only replays events
-  // already handled, which re-applies them in order.
+  // here; written on every hello, at once after an event that changed a
+  // verdict (GPU_PRE/POST_RESET), at most once a second for the others, and
+  // by FlushRelayCursor (monitor stop, connected or not). A replay of events
+  // already handled would re-apply them out of turn -- a GPU_PRE_RESET the
+  // operator has since returned would hold the GPU again, a GPU_POST_RESET
+  // would erase a later ECC verdict (found by native/tests/health_model.cc).
   void PersistRelayCursor(const std::string& path);
   void FlushRelayCursor();
   std::string Json() const;
+  // Where the cursor's save throttle reads the time (tests; default the system's).
+  void SetClock(const Clock* c) { clock_ = c; }
 
  private:
   mutable std::mutex mu_;
@@ -253,6 +258,7 @@ struct HealthCounters {
   std::string cursor_path_;
   int64_t cursor_saved_ms_ = 0;
   bool cursor_dirty_ = false;
+  const Clock* clock_ = Clock::System();
   void SaveCursorLocked();
 };
 
@@ -419,6 +425,9 @@ class Monitor {
   uint64_t wait_failures_ = 0;
   bool events_failing_ = false;
   void RelayConnect();
+  // A connection to the relay (non-blocking socket) is this monitor's: asks
+  // for the events it missed (the "reinit" line) and waits for the answer.
+  void RelayAttach(int fd);
   void RelayClose(const std::string& why);
   // Reads relay lines for up to `ms`: hellos update events_ok_ and the event
   // gaps, events are mapped to this snapshot's handles and handled, in order.

@@ -86,6 +86,8 @@ std::string EventTypeName(uint32_t type) {
   return "EVENT_" + std::to_string(type);
 }
 
+Library::Library() = default;
+
 Library::~Library() {
   if (f_) EventsStopAll();
   if (initialized_ && f_ && f_->shut_down) f_->shut_down();

@@ -90,9 +90,11 @@ struct Event {
   std::string message;
 };
 
+// Every query is virtual: a test harness (native/tests/health_model.cc)
+// subclasses it with a scripted fake instead of a dlopen'ed library.
 class Library {
  public:
-  ~Library();
+  virtual ~Library();
   Library(const Library&) = delete;
   Library& operator=(const Library&) = delete;
 
@@ -105,10 +107,10 @@ class Library {
   const std::string& path() const { return path_; }
   std::string Version() const;
 
-  Result<std::vector<ProcessorInfo>> Enumerate();
+  virtual Result<std::vector<ProcessorInfo>> Enumerate();
   Link GetLink(void* src, void* dst);
   // Number of xGMI links reported down (0 when unsupported).
-  int XgmiLinksDown(void* h);
+  virtual int XgmiLinksDown(void* h);
 
   // Event notification (health). Init registers `mask` on each handle, all or
   // nothing: when one handle's registration fails, the handles it had already
@@ -116,28 +118,28 @@ class Library {
   // registration behind (a reload re-registering them would otherwise leak
   // the kernel's event file of each). A handle already registered by an
   // earlier EventsInit only gets the new mask.
-  Status EventsInit(const std::vector<void*>& handles, uint64_t mask);
+  virtual Status EventsInit(const std::vector<void*>& handles, uint64_t mask);
   // Waits up to timeout_ms; appends received events.
-  Status EventsWait(int timeout_ms, std::vector<Event>* out);
+  virtual Status EventsWait(int timeout_ms, std::vector<Event>* out);
   // Stops the registrations among `handles` (the others: nothing to stop).
-  void EventsStop(const std::vector<void*>& handles);
+  virtual void EventsStop(const std::vector<void*>& handles);
   // Stops every registration this Library holds (before a Reinit).
-  void EventsStopAll();
+  virtual void EventsStopAll();
   // Registrations held (tests; /metrics).
   size_t EventsRegistered() const;
 
   // RAS polling (fallback health when events are unavailable).
-  Result<uint64_t> UncorrectableErrors(void* h);
+  virtual Result<uint64_t> UncorrectableErrors(void* h);
   // HBM pages the driver retired after uncorrectable errors, and the count at
   // which the driver itself gives up on the GPU (needs root on current drivers).
-  Result<uint32_t> RetiredPages(void* h);
-  Result<uint32_t> RetiredPageThreshold(void* h);
+  virtual Result<uint32_t> RetiredPages(void* h);
+  virtual Result<uint32_t> RetiredPageThreshold(void* h);
   // HBM in use on the device (bytes, every process: amdsmi_get_gpu_memory_usage).
-  Result<uint64_t> VramUsed(void* h);
+  virtual Result<uint64_t> VramUsed(void* h);
   // Graphics-engine activity in percent (amdsmi_get_gpu_activity: the SMU's
   // gpu_metrics, which the driver does not serve while the GPU is in reset).
-  Result<uint32_t> Activity(void* h);
-  bool Responsive(void* h);
+  virtual Result<uint32_t> Activity(void* h);
+  virtual bool Responsive(void* h);
 
   // Every query the plugin uses, run once per processor, with its amdsmi
   // status: what works in this container (device cgroup, privileges) and what
@@ -146,15 +148,17 @@ class Library {
 
   // Current compute/memory partition mode of a processor, e.g. {"CPX", "NPS2"}
   // (empty strings when the query is unavailable).
-  std::pair<std::string, std::string> PartitionModes(void* h);
+  virtual std::pair<std::string, std::string> PartitionModes(void* h);
 
   // amdsmi_shut_down + amdsmi_init: picks up a changed partition layout (the
   // driver re-creates processors when a GPU is re-partitioned). Invalidates all
   // handles; callers must have stopped every user of the old ones.
-  Status Reinit();
+  virtual Status Reinit();
+
+ protected:
+  Library();  // (out of line: Fns is incomplete here)
 
  private:
-  Library() = default;
   void ReadPartitionProfile(void* h, ProcessorInfo* p);
   struct Fns;
   void* dl_ = nullptr;

@@ -184,6 +184,33 @@ static void TestResourceConfig() {
   CHECK(std::string(alloc::ReplicaPolicyName(alloc::ReplicaPolicy::kAuto)) == "auto");
 }
 
+// Round-5 advice: the reset history is capped at the newest 64 (recording and
+// parsing), and a relayed GPU_PRE_RESET replayed after a restart is not
+// counted twice (keyed by "<relay>:<seq>").
+static void TestLedgerResetHistory() {
+  g_case = "ledger-reset-history";
+  health::Ledger l;
+  CHECK(l.RecordReset("g", 1000, 10000, "aa:5") == 1);
+  CHECK(l.RecordReset("g", 1100, 10000, "aa:5") == 1);  // the same event, replayed
+  CHECK(l.RecordReset("g", 1200, 10000, "aa:4") == 1);  // an older one of that relay: replayed too
+  CHECK(l.RecordReset("g", 1300, 10000, "bb:1") == 2);  // another relay instance: a new reset
+  CHECK(l.RecordReset("g", 1400, 10000, "") == 3);      // in-process: no identity, always new
+  CHECK(l.Get("g").last_reset_event == "bb:1");
+  for (int i = 0; i < 100; ++i) l.RecordReset("h", 5000 + i, 1000000);
+  auto h = l.Get("h").resets;
+  CHECK(h.size() == health::Ledger::kMaxResetHistory);
+  CHECK(!h.empty() && h.front() == 5000 + 100 - 64 && h.back() == 5099);  // the newest kept
+  // A file from an older version with 100 entries: the newest 64, not none.
+  std::string body = "adp-health v1\nk\t0\t0\t4\tflapping\tresets=";
+  for (int i = 0; i < 100; ++i) body += (i ? "," : "") + std::to_string(7000 + i);
+  body += "\treset_event=cc:9\n";
+  auto m = health::Ledger::Parse(body);
+  CHECK(m.count("k") && m["k"].resets.size() == 64 && m["k"].resets.front() == 7036 && m["k"].resets.back() == 7099);
+  CHECK(m["k"].last_reset_event == "cc:9");
+  auto back = health::Ledger::Parse(health::Ledger::Serialize(m));
+  CHECK(back["k"].resets == m["k"].resets && back["k"].last_reset_event == "cc:9");
+}
+
 static void TestLedgerGaps() {
   g_case = "ledger-gaps";
   health::Ledger l;
@@ -1396,6 +1423,7 @@ int main() {
   TestResourceConfig();
   TestRelayLines();
   TestLedgerGaps();
+  TestLedgerResetHistory();
   TestRemoveDrainNames();
   TestDrainSyntax();
   TestRemoteScan();

@@ -13,7 +13,15 @@
 // every event: type, message, and whether its handle is one amdsmi enumerated
 // -- the pointer identity the daemon's in-process matching relies on.
 //
-// usage: amdgpu-dp-event-probe [--lib <libamd_smi.so>] [--types 12,13] [--wait-ms 8000]
+// --self-hip: after registering, this process itself opens the GPU through
+// HIP (dlopen'ed libamdhip64: hipInit, hipMalloc, hipFree) -- KFD delivers an
+// unprivileged client only the per-process events of its own process, so this
+// is how the decoding and the handle identity are seen on a box without root.
+//
+// usage: amdgpu-dp-event-probe [--lib <libamd_smi.so>] [--types 12,13] [--wait-ms 8000] [--self-hip]
+#include <dlfcn.h>
+#include <unistd.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -31,10 +39,13 @@ using namespace adp;
 int main(int argc, char** argv) {
   std::string lib_path, types = "12,13";
   int wait_ms = 8000;
-  for (int i = 1; i + 1 < argc; i += 2) {
-    if (!strcmp(argv[i], "--lib")) lib_path = argv[i + 1];
-    else if (!strcmp(argv[i], "--types")) types = argv[i + 1];
-    else if (!strcmp(argv[i], "--wait-ms")) wait_ms = atoi(argv[i + 1]);
+  bool self_hip = false;
+  for (int i = 1; i < argc; ++i) {
+    if (!strcmp(argv[i], "--self-hip")) self_hip = true;
+    else if (i + 1 >= argc) break;
+    else if (!strcmp(argv[i], "--lib")) lib_path = argv[++i];
+    else if (!strcmp(argv[i], "--types")) types = argv[++i];
+    else if (!strcmp(argv[i], "--wait-ms")) wait_ms = atoi(argv[++i]);
   }
   auto extra = health::ParseEventTypes(types);
   if (!extra.ok()) {
@@ -58,6 +69,33 @@ int main(int argc, char** argv) {
   Status reg = (*lib)->EventsInit(handles, hc.EventMask());
   printf("%s\n", reg.ok() ? "registered" : "registration failed");
   fflush(stdout);
+
+  // This process opens the GPU itself (KFD process creation, VM acquire,
+  // a queue): what KFD reports to its own registration.
+  std::string hip = "\"not asked\"";
+  if (self_hip && reg.ok()) {
+    void* dl = dlopen("libamdhip64.so", RTLD_NOW | RTLD_LOCAL);
+    if (!dl) dl = dlopen("/opt/rocm/lib/libamdhip64.so", RTLD_NOW | RTLD_LOCAL);
+    if (!dl) {
+      hip = "\"" + JsonEscape(std::string("dlopen: ") + dlerror()) + "\"";
+    } else {
+      auto init = reinterpret_cast<int (*)(unsigned)>(dlsym(dl, "hipInit"));
+      auto set = reinterpret_cast<int (*)(int)>(dlsym(dl, "hipSetDevice"));
+      auto alloc = reinterpret_cast<int (*)(void**, size_t)>(dlsym(dl, "hipMalloc"));
+      auto free_ = reinterpret_cast<int (*)(void*)>(dlsym(dl, "hipFree"));
+      auto sync = reinterpret_cast<int (*)()>(dlsym(dl, "hipDeviceSynchronize"));
+      int a = -1, b = -1, c = -1, d = -1, e = -1;
+      void* p = nullptr;
+      if (init && set && alloc && free_ && sync) {  // each step only after the one before succeeded
+        if ((a = init(0)) == 0 && (b = set(0)) == 0 && (c = alloc(&p, 64 << 20)) == 0 && (d = sync()) == 0)
+          e = free_(p);
+      }
+      hip = "{\"pid\": " + std::to_string(getpid()) + ", \"hipInit\": " + std::to_string(a) +
+            ", \"hipSetDevice\": " + std::to_string(b) + ", \"hipMalloc\": " + std::to_string(c) +
+            ", \"hipDeviceSynchronize\": " + std::to_string(d) + ", \"hipFree\": " + std::to_string(e) + "}";
+      // (not dlclose'd: the HIP runtime stays until exit)
+    }
+  }
 
   std::map<std::string, int> wait_status;  // status text -> waits
   std::string events;
@@ -85,7 +123,8 @@ int main(int argc, char** argv) {
   }
   (*lib)->EventsStop(handles);
 
-  std::string out = "{\"amdsmi\": \"" + (*lib)->Version() + "\", \"mask\": " + std::to_string(hc.EventMask()) +
+  std::string out = "{\"amdsmi\": \"" + (*lib)->Version() + "\", \"pid\": " + std::to_string(getpid()) +
+                    ", \"self_hip\": " + hip + ", \"mask\": " + std::to_string(hc.EventMask()) +
                     ", \"registration\": \"" + JsonEscape(reg.ok() ? "ok" : reg.ToString()) + "\", \"processors\": [";
   for (size_t i = 0; i < procs->size(); ++i) {
     const auto& p = (*procs)[i];

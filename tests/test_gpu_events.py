@@ -11,7 +11,11 @@ never change health. A HIP program (the probe) run while the daemon watches
 makes real events flow through each layout:
 
 * raw: amdgpu-dp-event-probe -- smi::Library alone, the wait statuses and
-  whether each event's handle is one amdsmi enumerated;
+  whether each event's handle is one amdsmi enumerated -- while another
+  process runs HIP, and while the registering process runs HIP itself
+  (--self-hip: KFD hands an unprivileged registration only its own
+  process's per-process events; round 6's first box session found none from
+  another process);
 * in-process: the daemon's own registration;
 * relay: the chart's layout -- the daemon denied /dev/kfd and the render nodes
   (libadp_devcgroup_sim.so), the events registered by the event relay and
@@ -84,6 +88,31 @@ def raw(hip_program):
     rec["first_line"], rec["stderr"] = first, err[-2000:]
     _record("raw_events.json", rec)
     return rec
+
+
+@pytest.fixture(scope="module")
+def raw_self():
+    """The registering process opens the GPU itself (every KFD type registered)."""
+    r = subprocess.run([EVENT_PROBE, "--types", "5,6,7,8,9,10,11,12,13", "--wait-ms", "4000", "--self-hip"],
+                       capture_output=True, text=True, timeout=120)
+    lines = r.stdout.strip().splitlines()
+    rec = json.loads(lines[-1]) if lines and lines[-1].startswith("{") else {"error": r.stdout + r.stderr}
+    rec["rc"], rec["first_line"], rec["stderr"] = r.returncode, lines[0] if lines else "", r.stderr[-2000:]
+    _record("raw_events_self.json", rec)
+    return rec
+
+
+def test_raw_events_of_its_own_process_name_enumerated_processors(raw_self, real_snap):
+    """Decoding and handle identity on real amdsmi: events KFD reports about the
+    registering process itself carry a handle amdsmi enumerated (the daemon's
+    in-process matching is by that pointer) and the box GPU's PCI address."""
+    assert raw_self["rc"] == 0 and raw_self["registration"] == "ok", raw_self
+    assert raw_self["self_hip"]["hipInit"] == 0 and raw_self["self_hip"]["hipMalloc"] == 0, raw_self
+    assert raw_self["unmatched"] == 0, raw_self
+    if raw_self["events_total"] == 0:
+        pytest.skip(f"no KFD event even about this process; waits: {raw_self['waits']}")
+    bdf = real_snap["gpus"][0]["bdf"]
+    assert all(e["bdf"] == bdf and e["processor"] >= 0 for e in raw_self["events"]), raw_self
 
 
 def test_raw_amdsmi_events_name_enumerated_processors(raw, real_snap):

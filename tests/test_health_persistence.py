@@ -675,3 +675,39 @@ def test_polled_recovery_waits_for_the_driver_to_report_the_devices_memory(mk, q
     t0 = time.monotonic()
     n.wait_health(lambda h: h[ids[1]] == "Healthy", timeout=10)
     assert time.monotonic() - t0 >= 0.5
+
+
+def test_quarantine_and_operator_requests_apply_with_polling_off(mk, tmp_path):
+    """DP_HEALTH_POLL_MS=0 turns liveness polling off, not the rest (round-5
+    advice): a reset-flap quarantine still ends after a quiet window, and drains
+    and return-to-service requests still apply, on the monitor's 1 s timer --
+    before, all three ran only inside a poll, and a flapping GPU stayed out for
+    good."""
+    drain = str(tmp_path / "drain")
+    n = mk(args=["--reset-flap-limit", "2", "--reset-flap-window-ms", "1500", "--drain-file", drain],
+           env={"DP_HEALTH_POLL_MS": "0"})
+    ids = sorted(n.start())
+    assert "DP_HEALTH_POLL_MS=0: no liveness polls" in n.d.log()
+    n.inject("1 3 pre 0")
+    n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+    n.inject("1 4 post 0")
+    n.wait_health(lambda h: h[ids[1]] == "Healthy")
+    n.inject("1 3 pre 1")
+    n.wait_health(lambda h: h[ids[1]] == "Unhealthy")
+    t_last = time.monotonic()
+    n.inject("1 4 post 1")
+    n.d.wait_log("quarantined")
+    n.wait_health(lambda h: h[ids[1]] == "Healthy", timeout=8)  # no poll runs: the timer ended it
+    assert time.monotonic() - t_last >= 1.4
+    assert "quarantine over" in n.d.log()
+    with open(drain, "w") as f:
+        f.write(n.fx["gpus"][0]["bdf"] + "\n")
+    n.wait_health(lambda h: h[ids[0]] == "Unhealthy", timeout=5)
+    open(drain, "w").close()
+    n.wait_health(lambda h: h[ids[0]] == "Healthy", timeout=5)
+    n.inject("0 3 pre 2")  # a reset that never completes ...
+    n.wait_health(lambda h: h[ids[0]] == "Unhealthy")
+    with open(drain + ".return", "w") as f:  # ... and the operator's way back
+        f.write(n.fx["gpus"][0]["bdf"] + "\n")
+    n.wait_health(lambda h: h[ids[0]] == "Healthy", timeout=5)
+    assert "returned to service by the operator" in n.d.log()

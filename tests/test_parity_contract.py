@@ -13,6 +13,7 @@ import os
 import grpc
 import pytest
 
+from k8s_gpu_sharing_plugin_amd import REPO_ROOT
 from k8s_gpu_sharing_plugin_amd.models import fixtures
 from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
 
@@ -170,3 +171,50 @@ def test_unhealthy_allocation_is_counted_not_silent(scratch):
     finally:
         d.stop()
         k.stop()
+
+
+def _chart_pod(values=None):
+    import sys
+    import yaml
+    sys.path.insert(0, os.path.join(REPO_ROOT, "tools"))
+    import helm_render
+    out = helm_render.render(values or {})
+    ds = [d for d in yaml.safe_load_all(out["daemonset.yaml"]) if d and d.get("kind") == "DaemonSet"][0]
+    spec = ds["spec"]["template"]["spec"]
+    containers = spec.get("initContainers", []) + spec["containers"]
+    host_paths = {v["name"]: v["hostPath"]["path"] for v in spec["volumes"] if v.get("hostPath")}
+    return containers, host_paths, helm_render.render_notes(values or {})
+
+
+def test_default_install_security_posture_is_the_documented_deviation():
+    """docs/PARITY.md rows "Privileged container by default" and "Writable host
+    directory by default": the reference's default install is one drop-ALL
+    container with one hostPath, the kubelet's device-plugin directory
+    (/root/reference/deployments/helm/nvidia-device-plugin/templates/daemonset.yml:80-104).
+    Here the default is exactly one privileged container -- the event relay --
+    and the plugin container drops everything; the host paths are the ones
+    listed, /var/lib/amdgpu-device-plugin the only one beyond the kubelet's that
+    is written. The install notes say so, with the opt-outs; with both opt-outs
+    nothing is privileged and nothing of the host is written but the kubelet's
+    directory."""
+    containers, host_paths, notes = _chart_pod()
+    privileged = [c["name"] for c in containers if (c.get("securityContext") or {}).get("privileged")]
+    assert privileged == ["event-relay"], privileged
+    plugin = [c for c in containers if c["name"] != "event-relay"]
+    assert len(plugin) == 1 and plugin[0]["securityContext"]["capabilities"] == {"drop": ["ALL"]}
+    assert plugin[0]["securityContext"]["allowPrivilegeEscalation"] is False
+    assert host_paths == {"device-plugin": "/var/lib/kubelet/device-plugins", "sys": "/sys", "dev": "/dev",
+                          "health-state": "/var/lib/amdgpu-device-plugin"}, host_paths
+    writable = {m["name"] for c in containers for m in c.get("volumeMounts", [])
+                if m["name"] in host_paths and not m.get("readOnly")}
+    assert writable == {"device-plugin", "dev", "health-state"}, writable
+    assert '"event-relay" container runs privileged' in notes and "healthEvents=false" in notes
+    assert "/var/lib/amdgpu-device-plugin is mounted writable" in notes and "healthState.enabled=false" in notes
+    parity = open(os.path.join(REPO_ROOT, "docs", "PARITY.md")).read()
+    assert "| Privileged container by default |" in parity and "| Writable host directory by default |" in parity
+
+    containers, host_paths, notes = _chart_pod({"healthEvents": False, "healthState": {"enabled": False}})
+    assert not [c for c in containers if (c.get("securityContext") or {}).get("privileged")]
+    assert [c["name"] for c in containers] == ["amdgpu-device-plugin"]
+    assert host_paths == {"device-plugin": "/var/lib/kubelet/device-plugins", "sys": "/sys", "dev": "/dev"}
+    assert "privileged" not in notes

@@ -305,7 +305,7 @@ def merge(dst, src):
     return dst
 
 
-def render(values_override=None, release="amdgpu", chart_dir=CHART):
+def render(values_override=None, release="amdgpu", chart_dir=CHART, notes=False):
     """Renders every template of the chart; returns {template file: text}."""
     with open(os.path.join(chart_dir, "values.yaml")) as f:
         values = yaml.safe_load(f)
@@ -331,7 +331,14 @@ def render(values_override=None, release="amdgpu", chart_dir=CHART):
     for name, nodes in parsed.items():  # defines first (helpers)
         if name.startswith("_"):
             r.render_nodes(nodes, r.root, {})
-    return {name: r.render_nodes(nodes, r.root, {}) for name, nodes in parsed.items() if not name.startswith("_")}
+    # NOTES.txt is what helm prints after an install, not a manifest (render_notes).
+    return {name: r.render_nodes(nodes, r.root, {}) for name, nodes in parsed.items()
+            if not name.startswith("_") and (notes or name != "NOTES.txt")}
+
+
+def render_notes(values_override=None, release="amdgpu", chart_dir=CHART):
+    """The text `helm install` prints (templates/NOTES.txt)."""
+    return render(values_override, release, chart_dir, notes=True)["NOTES.txt"]
 
 
 def _set(values, assignment):
