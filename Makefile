@@ -51,9 +51,10 @@ bench: build
 # Sanitizer builds of the native unit + stress tests (host code only).
 asan:
 	cmake -S native -B build/asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DADP_SANITIZE=ON >/dev/null
-	ninja -C build/asan -j$(JOBS) adp_unit_tests adp_stress amdsmi_mock adp_memcap adp_memcap_check
+	ninja -C build/asan -j$(JOBS) adp_unit_tests adp_stress adp_health_model amdsmi_mock adp_memcap adp_memcap_check
 	ASAN_OPTIONS=detect_leaks=1 build/asan/adp_unit_tests
 	build/asan/adp_stress
+	ASAN_OPTIONS=detect_leaks=1 build/asan/adp_health_model --depth 4
 	LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $(CURDIR)/build/asan/libadp_memcap.so" ASAN_OPTIONS=detect_leaks=0 \
 	  AMD_GPU_MEMORY_LIMIT_MIB=100,50 ADP_MEMCAP_KEY=make-asan-$$$$ build/asan/adp_memcap_check
 	LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $(CURDIR)/build/asan/libadp_memcap.so" ASAN_OPTIONS=detect_leaks=0 \

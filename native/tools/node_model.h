@@ -1,6 +1,8 @@
 // A synthetic MI355X node snapshot (no amdsmi): `gpus` GPUs of `parts` compute
 // partitions each, fully connected by xGMI, NUMA 0 for the first four GPUs and
 // 1 for the rest. Shared by the handler microbenchmark and the fuzz targets.
+// `kfd`: the KFD topology nodes (the order HIP numbers a container's devices):
+// 0 unreported, 1 in amdsmi's enumeration order, 2 in the reverse order.
 #pragma once
 
 #include <cstdio>
@@ -11,7 +13,7 @@
 
 namespace adp::testing {
 
-inline std::shared_ptr<const inventory::Snapshot> NodeModel(int gpus, int parts) {
+inline std::shared_ptr<const inventory::Snapshot> NodeModel(int gpus, int parts, int kfd = 0) {
   std::vector<smi::ProcessorInfo> procs;
   for (int g = 0; g < gpus; ++g) {
     for (int p = 0; p < parts; ++p) {
@@ -28,10 +30,14 @@ inline std::shared_ptr<const inventory::Snapshot> NodeModel(int gpus, int parts)
       pi.partition_id = p;
       pi.num_cu = 256 / parts;
       pi.xcd_count = 8 / parts;
+      if (kfd == 1) pi.kfd_node = static_cast<uint32_t>(2 + g * parts + p);
+      if (kfd == 2) pi.kfd_node = static_cast<uint32_t>(2 + (gpus - 1 - g) * parts + p);
       procs.push_back(pi);
     }
   }
-  auto s = inventory::GroupProcessors(procs, {});
+  inventory::BuildOptions opt;
+  opt.sysfs_root = "";  // nothing of this machine's /sys
+  auto s = inventory::GroupProcessors(procs, opt);
   auto& snap = *s;
   size_t n = snap->gpus.size();
   for (size_t a = 0; a < n; ++a)
