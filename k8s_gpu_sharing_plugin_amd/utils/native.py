@@ -164,3 +164,58 @@ class ChurnClient:
 def proto_roundtrip(msg_type: str, data: bytes) -> bytes:
     res = _check(_take(lib().adp_proto_roundtrip(msg_type.encode(), data, len(data))))
     return bytes.fromhex(res["hex"])
+
+
+def _open(fn_name: str, cfg: dict):
+    so = lib()
+    fn = getattr(so, fn_name)
+    fn.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+    fn.restype = ctypes.c_void_p
+    err = ctypes.c_void_p()
+    h = fn(json.dumps(cfg).encode(), ctypes.byref(err))
+    if not h:
+        msg = ctypes.string_at(err.value).decode() if err.value else "unknown error"
+        if err.value:
+            so.adp_free(err.value)
+        raise NativeError(msg)
+    return h
+
+
+class HostedMonitor:
+    """The daemon's health monitor (health::Monitor) running in this process,
+    on the real libamd_smi by default: KFD hands an unprivileged registration
+    only its own process's per-process events, so a test that then opens the
+    GPU from this same process sees real events reach the monitor."""
+
+    def __init__(self, lib_path: str = "", devices=(0,), extra_types: str = "", poll_ms: int = 200):
+        self._h = _open("adp_monitor_open", {"lib": lib_path, "devices": list(devices),
+                                              "extra_types": extra_types, "poll_ms": poll_ms})
+        so = lib()
+        so.adp_monitor_state.argtypes = [ctypes.c_void_p]
+        so.adp_monitor_state.restype = ctypes.c_void_p
+        so.adp_monitor_close.argtypes = [ctypes.c_void_p]
+
+    def state(self) -> dict:
+        return _check(_take(lib().adp_monitor_state(self._h)))
+
+    def close(self) -> None:
+        if self._h:
+            lib().adp_monitor_close(self._h)
+            self._h = None
+
+
+class HostedRelay:
+    """The event relay (health::RunEventRelay) serving `socket_path` from a
+    thread of this process (see HostedMonitor for why)."""
+
+    def __init__(self, socket_path: str, lib_path: str = "", extra_types: str = ""):
+        self._h = _open("adp_relay_open", {"lib": lib_path, "socket": socket_path, "extra_types": extra_types})
+        lib().adp_relay_close.argtypes = [ctypes.c_void_p]
+        lib().adp_relay_close.restype = ctypes.c_int
+
+    def close(self) -> int:
+        rc = 0
+        if self._h:
+            rc = lib().adp_relay_close(self._h)
+            self._h = None
+        return rc

@@ -6,6 +6,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <json.hpp>
+#include <memory>
+#include <mutex>
 #include <string>
 
 #include "alloc/replicas.h"
@@ -321,3 +323,168 @@ void adp_bench_reset(void* h) { static_cast<adp::bench::ChurnClient*>(h)->ResetS
 void adp_bench_close(void* h) { delete static_cast<adp::bench::ChurnClient*>(h); }
 
 }  // extern "C"
+
+// ---- the health monitor and the event relay, hosted in the calling process ----
+// KFD hands an unprivileged event registration only the per-process events of
+// its own process (PROCESS_START and the like; resets are device-wide), so to
+// see real events flow through the monitor or the relay on a box without root
+// the process that registers must be the one that then opens the GPU: a
+// Python process hosting them here and running HIP (tests/test_gpu_events.py,
+// utils/hosted_events.py).
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/signalfd.h>
+#include <unistd.h>
+
+#include <thread>
+
+#include "health/relay.h"
+
+namespace {
+
+struct HostedMonitor {
+  std::unique_ptr<adp::smi::Library> lib;
+  std::shared_ptr<const adp::inventory::Snapshot> snap;
+  adp::health::HealthCounters counters;
+  adp::health::Ledger ledger;
+  std::unique_ptr<adp::health::Monitor> mon;
+  std::mutex mu;
+  std::vector<std::pair<int, bool>> transitions;  // (gpu, healthy) notified
+};
+
+struct HostedRelay {
+  std::unique_ptr<adp::smi::Library> lib;
+  int sig[2] = {-1, -1};  // what RunEventRelay reads as its signalfd
+  std::thread thread;
+  int rc = -1;
+};
+
+adp::Result<std::unique_ptr<adp::smi::Library>> OpenLib(const json& j) {
+  return adp::smi::Library::Open(j.value("lib", std::string()));
+}
+
+}  // namespace
+
+extern "C" {
+
+// {"lib", "devices": [0], "extra_types": "12,13", "poll_ms": 200} -> handle (null: *err says why)
+void* adp_monitor_open(const char* in, char** err) {
+  try {
+    json j = json::parse(in);
+    auto lib = OpenLib(j);
+    if (!lib.ok()) {
+      *err = Dup(lib.status().ToString());
+      return nullptr;
+    }
+    adp::inventory::BuildOptions opt;
+    if (j.count("devices")) opt.only_gpus = j["devices"].get<std::vector<int>>();
+    auto snap = adp::inventory::BuildSnapshot(lib->get(), opt);
+    if (!snap.ok()) {
+      *err = Dup(snap.status().ToString());
+      return nullptr;
+    }
+    auto extra = adp::health::ParseEventTypes(j.value("extra_types", std::string()));
+    if (!extra.ok()) {
+      *err = Dup(extra.status().ToString());
+      return nullptr;
+    }
+    auto h = std::make_unique<HostedMonitor>();
+    h->lib = std::move(*lib);
+    h->snap = *snap;
+    adp::health::HealthConfig c;
+    c.poll_interval_ms = j.value("poll_ms", 200);
+    c.extra_types = *extra;
+    h->mon = std::make_unique<adp::health::Monitor>(h->lib.get(), h->snap, c, &h->ledger, &h->counters);
+    HostedMonitor* raw = h.get();
+    h->mon->AddListener([raw](int gpu, bool ok, const std::string&) {
+      std::lock_guard<std::mutex> lk(raw->mu);
+      raw->transitions.emplace_back(gpu, ok);
+    });
+    adp::Status st = h->mon->Start();
+    if (!st.ok()) {
+      *err = Dup(st.ToString());
+      return nullptr;
+    }
+    return h.release();
+  } catch (const std::exception& e) {
+    *err = Dup(e.what());
+    return nullptr;
+  }
+}
+
+// -> {"events_enabled", "events": [{"bdf", "type", "n"}], "unmatched": {type: n}, "transitions": [[gpu, ok]],
+//     "registrations": n, "gpus": [bdf]}
+char* adp_monitor_state(void* hp) {
+  return Guard([&] {
+    auto* h = static_cast<HostedMonitor*>(hp);
+    json events = json::array();
+    for (const auto& [k, n] : h->counters.EventCounts()) events.push_back({{"bdf", k.first}, {"type", k.second}, {"n", n}});
+    json tr = json::array();
+    {
+      std::lock_guard<std::mutex> lk(h->mu);
+      for (const auto& [g, ok] : h->transitions) tr.push_back({g, ok});
+    }
+    json gpus = json::array();
+    for (const auto& g : h->snap->gpus) gpus.push_back(g.bdf);
+    return Dup(json{{"events_enabled", h->counters.events_enabled.load()}, {"events", events},
+                    {"unmatched", h->counters.Unmatched()}, {"transitions", tr},
+                    {"registrations", h->lib->EventsRegistered()}, {"gpus", gpus}}
+                   .dump());
+  });
+}
+
+void adp_monitor_close(void* hp) {
+  auto* h = static_cast<HostedMonitor*>(hp);
+  h->mon->Stop();
+  delete h;
+}
+
+// {"lib", "socket", "extra_types": "12,13"} -> handle (null: *err says why); the relay serves on a thread.
+void* adp_relay_open(const char* in, char** err) {
+  try {
+    json j = json::parse(in);
+    auto lib = OpenLib(j);
+    if (!lib.ok()) {
+      *err = Dup(lib.status().ToString());
+      return nullptr;
+    }
+    auto extra = adp::health::ParseEventTypes(j.value("extra_types", std::string()));
+    if (!extra.ok()) {
+      *err = Dup(extra.status().ToString());
+      return nullptr;
+    }
+    auto h = std::make_unique<HostedRelay>();
+    h->lib = std::move(*lib);
+    if (pipe2(h->sig, O_CLOEXEC | O_NONBLOCK) != 0) {
+      *err = Dup("pipe failed");
+      return nullptr;
+    }
+    adp::health::RelayOptions ro;
+    for (uint32_t t : *extra) ro.extra_mask |= adp::smi::EventMask(t);
+    std::string sock = j.value("socket", std::string());
+    HostedRelay* raw = h.get();
+    h->thread = std::thread([raw, sock, ro] { raw->rc = adp::health::RunEventRelay(raw->lib.get(), sock, raw->sig[0], ro); });
+    return h.release();
+  } catch (const std::exception& e) {
+    *err = Dup(e.what());
+    return nullptr;
+  }
+}
+
+// Stops the relay (as SIGTERM would) and returns its exit code.
+int adp_relay_close(void* hp) {
+  auto* h = static_cast<HostedRelay*>(hp);
+  signalfd_siginfo si{};
+  si.ssi_signo = SIGTERM;
+  ssize_t w = write(h->sig[1], &si, sizeof(si));
+  (void)w;
+  h->thread.join();
+  int rc = h->rc;
+  close(h->sig[0]);
+  close(h->sig[1]);
+  delete h;
+  return rc;
+}
+
+}  // extern "C"
+

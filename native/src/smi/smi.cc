@@ -91,7 +91,9 @@ Library::Library() = default;
 Library::~Library() {
   if (f_) EventsStopAll();
   if (initialized_ && f_ && f_->shut_down) f_->shut_down();
-  if (dl_) dlclose(dl_);
+  // Not dlclose'd: a library's thread-local destructors and atexit handlers
+  // may still point into it (the process either exits next or, in the GPU
+  // tests, goes on to load the HIP runtime, which crashed on an unmapped mock).
 }
 
 Result<std::unique_ptr<Library>> Library::Open(const std::string& path,

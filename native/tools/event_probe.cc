@@ -116,7 +116,7 @@ int main(int argc, char** argv) {
       char head[160];
       snprintf(head, sizeof(head), "{\"ms\": %lld, \"type\": %u, \"name\": \"%s\", \"processor\": %d",
                static_cast<long long>(elapsed()), e.type, smi::EventTypeName(e.type).c_str(), idx);
-      events += std::string(n_events++ ? ",\n   " : "") + head + ", \"bdf\": \"" +
+      events += std::string(n_events++ ? ", " : "") + head + ", \"bdf\": \"" +
                 (idx >= 0 ? (*procs)[idx].bdf : std::string("?")) + "\", \"message\": \"" + JsonEscape(e.message) +
                 "\"}";
     }

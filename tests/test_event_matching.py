@@ -235,3 +235,52 @@ def test_relay_never_leaks_a_registration_across_renewals(scratch, tmp_path):
         assert relay.stop() == 0
     s = _evt(evt)
     assert s["live"] == 0 and s["double_init"] == 0 and s["leaked_at_shutdown"] == 0, s
+
+
+def test_hosted_monitor_and_relay_on_the_mock(scratch, tmp_path):
+    """The C API's hosted monitor and relay (what the GPU tests run next to HIP,
+    utils/hosted_events.py) on the mock: an event reaches the hosted monitor's
+    counters, and the hosted relay forwards one to a real daemon."""
+    fifo = str(tmp_path / "events")
+    os.mkfifo(fifo)
+    fx = dict(fixtures.node(2), event_fifo=fifo)
+    fxpath = fixtures.write(fx, scratch + ".fixture")
+    old = {k: os.environ.get(k) for k in ("AMD_SMI_LIB", "AMDSMI_MOCK_FIXTURE")}
+    os.environ["AMD_SMI_LIB"], os.environ["AMDSMI_MOCK_FIXTURE"] = MOCK_LIB, fxpath
+    try:
+        m = native.HostedMonitor(extra_types="12,13", devices=(0, 1))
+        try:
+            fd = os.open(fifo, os.O_WRONLY | os.O_NONBLOCK)
+            os.write(fd, b"1 12 4d2 python3\n")
+            os.close(fd)
+            deadline = time.monotonic() + 5
+            st = m.state()
+            while not st["events"] and time.monotonic() < deadline:
+                time.sleep(0.05)
+                st = m.state()
+            assert st["events"] == [{"bdf": fx["gpus"][1]["bdf"], "type": "PROCESS_START", "n": 1}], st
+            assert st["events_enabled"] == 1 and st["registrations"] == 2 and st["transitions"] == [], st
+        finally:
+            m.close()
+        sock = str(tmp_path / "relay.sock")
+        r = native.HostedRelay(sock, extra_types="12")
+        k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+        d = harness.Daemon(scratch, fx, args=["--health-event-socket", sock, "--metrics-addr", "127.0.0.1:0"]).start()
+        try:
+            port = _port(d)
+            d.wait_log("events on through the relay")
+            fd = os.open(fifo, os.O_WRONLY | os.O_NONBLOCK)
+            os.write(fd, b"0 12 4d3 probe\n")
+            os.close(fd)
+            want = {(("bdf", fx["gpus"][0]["bdf"]), ("type", "PROCESS_START")): 1}
+            assert _wait_samples(port, "amdgpu_dp_gpu_events_total", want) == want
+        finally:
+            d.stop()
+            k.stop()
+            assert r.close() == 0
+    finally:
+        for key, v in old.items():
+            if v is None:
+                os.environ.pop(key, None)
+            else:
+                os.environ[key] = v

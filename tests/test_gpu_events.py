@@ -4,22 +4,22 @@ Five rounds proved only that event registration succeeds on the box: every
 step after it -- decoding amdsmi_evt_notification_data_t, matching the event's
 processor handle to an enumerated one, the relay's line and the daemon's
 KFD-node / PCI-address mapping -- had run against the mock alone, which hands
-back the very handle it was given. KFD reports a PROCESS_START (12) and a
-PROCESS_END (13) event for every process that opens a GPU, no privilege
-needed; registered as --health-event-extra-types they are counted per GPU and
-never change health. A HIP program (the probe) run while the daemon watches
-makes real events flow through each layout:
+back the very handle it was given. KFD reports a PROCESS_START (12) when a process opens a GPU, and
+PROCESS_END (13); registered as --health-event-extra-types they are counted
+per GPU and never change health. KFD hands an unprivileged registration only
+its OWN process's per-process events (measured here, round 6: a HIP program
+next to the registration delivers nothing, the registering process opening
+the GPU itself delivers its PROCESS_START). So:
 
 * raw: amdgpu-dp-event-probe -- smi::Library alone, the wait statuses and
   whether each event's handle is one amdsmi enumerated -- while another
-  process runs HIP, and while the registering process runs HIP itself
-  (--self-hip: KFD hands an unprivileged registration only its own
-  process's per-process events; round 6's first box session found none from
-  another process);
-* in-process: the daemon's own registration;
-* relay: the chart's layout -- the daemon denied /dev/kfd and the render nodes
-  (libadp_devcgroup_sim.so), the events registered by the event relay and
-  forwarded as "event seq=N node=<kfd node> bdf=<pci> ...".
+  process runs HIP (nothing arrives; recorded), and with --self-hip;
+* in-process monitor: health::Monitor hosted by a helper process
+  (utils/hosted_events.py over libadp_capi) that then opens the GPU;
+* relay: the chart's layout -- the event relay hosted the same way, the real
+  daemon denied /dev/kfd and the render nodes (libadp_devcgroup_sim.so),
+  the event forwarded as "event seq=N node=<kfd node> bdf=<pci> ..." and
+  mapped by the daemon to the box GPU.
 
 Every record goes to gpurun_out/r6/ (copied into profiles/r6/). If this
 kernel emits no such event the raw record says so with amdsmi's own wait
@@ -31,6 +31,7 @@ import json
 import os
 import re
 import subprocess
+import sys
 import time
 
 import pytest
@@ -84,7 +85,7 @@ def raw(hip_program):
         time.sleep(0.3)
         _run_hip(hip_program)
     out, err = p.communicate(timeout=60)
-    rec = json.loads(out.strip().splitlines()[-1])
+    rec = json.loads(out.strip().splitlines()[-1])  # (one line)
     rec["first_line"], rec["stderr"] = first, err[-2000:]
     _record("raw_events.json", rec)
     return rec
@@ -120,10 +121,11 @@ def test_raw_amdsmi_events_name_enumerated_processors(raw, real_snap):
     assert raw["registration"] == "ok", raw
     assert raw["unmatched"] == 0, raw  # every event's handle is one amdsmi enumerated
     if raw["events_total"] == 0:
-        pytest.skip(f"no PROCESS_START/END event from this kernel; waits: {raw['waits']}")
+        pytest.skip(f"no event about another process reached this registration; waits: {raw['waits']}")
+    # Whatever KFD lets through about another process (round 6 saw its
+    # PROCESS_END, not its PROCESS_START) names the box GPU.
     bdf = real_snap["gpus"][0]["bdf"]
-    names = {(e["name"], e["bdf"]) for e in raw["events"]}
-    assert ("PROCESS_START", bdf) in names, raw
+    assert all(e["bdf"] == bdf and e["processor"] >= 0 for e in raw["events"]), raw
 
 
 def _wait_metric(port, name, labels, at_least=1, timeout=10.0):
@@ -137,72 +139,106 @@ def _wait_metric(port, name, labels, at_least=1, timeout=10.0):
         time.sleep(0.1)
 
 
-@pytest.mark.parametrize("layout", ["in-process", "relay"])
-def test_daemon_counts_real_events_on_the_box_gpu(scratch, real_snap, hip_program, raw, tmp_path, layout):
-    if raw["events_total"] == 0:
-        pytest.skip("this kernel emits no PROCESS_START/END (raw_events.json)")
+HELPER = [sys.executable, "-m", "k8s_gpu_sharing_plugin_amd.utils.hosted_events"]
+
+
+def test_real_event_reaches_the_in_process_monitor(raw_self, real_snap):
+    """The daemon's in-process monitor (health::Monitor on the real libamd_smi,
+    --health-event-extra-types 12,13), hosted by a helper process that then
+    opens the GPU itself: KFD's PROCESS_START reaches it, its handle is matched
+    to the box GPU by pointer identity, it is counted per GPU
+    (amdgpu_dp_gpu_events_total's source) and changes no health."""
+    if raw_self.get("events_total", 0) == 0:
+        pytest.skip("no KFD event even about the registering process (raw_events_self.json)")
+    r = subprocess.run(HELPER + ["monitor"], capture_output=True, text=True, timeout=120)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    rec = json.loads(lines[-1]) if lines else {"error": r.stdout[-2000:] + r.stderr[-2000:]}
+    rec["rc"] = r.returncode
+    rec["log"] = [ln for ln in r.stderr.splitlines() if "event" in ln or "health" in ln][-12:]
+    _record("hosted_monitor_events.json", rec)
+    bdf = real_snap["gpus"][0]["bdf"]
+    assert r.returncode == 0 and rec["hip"]["hipInit"] == 0 and rec["hip"]["hipMalloc"] == 0, rec
+    after = rec["after"]
+    assert after["events_enabled"] == 1 and after["registrations"] >= 1, rec
+    counted = {(e["bdf"], e["type"]): e["n"] for e in after["events"]}
+    assert counted.get((bdf, "PROCESS_START"), 0) >= 1, rec
+    assert not after["unmatched"], rec  # the handle amdsmi handed back is one it enumerated
+    assert after["transitions"] == [], rec  # counted, never a verdict
+
+
+def test_real_event_travels_through_the_relay_to_the_daemon(scratch, raw_self, real_snap, tmp_path):
+    """The chart's layout with a real event: the event relay (hosted by a helper
+    process that then opens the GPU) registers on the real libamd_smi and
+    forwards KFD's PROCESS_START as "event seq=N node=<KFD node> bdf=<PCI
+    address> ..."; the daemon -- denied /dev/kfd and the render nodes, like an
+    unprivileged pod -- maps it by KFD node to the box GPU and counts it."""
+    if raw_self.get("events_total", 0) == 0:
+        pytest.skip("no KFD event even about the registering process (raw_events_self.json)")
+    from test_metrics import _get, _parse
     g = real_snap["gpus"][0]
-    env = {"DP_HEALTH_POLL_MS": "200"}
-    relay = None
+    part0 = g["partitions"][0]
     sock = str(tmp_path / "events.sock")
-    if layout == "relay":
-        env["LD_PRELOAD"] = " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), SIM) if x)
-        rdir = scratch + "-relay"
-        os.makedirs(rdir, exist_ok=True)
-        relay = harness.Daemon(rdir, None, real_smi=True,
-                               args=["--event-relay", "--health-event-socket", sock,
-                                     "--health-event-extra-types", TYPES]).start()
-        relay.wait_log("event notification registered on", 30)
+    relay_log = open(tmp_path / "relay.log", "w")
+    helper = subprocess.Popen(HELPER + ["relay", sock], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                              stderr=relay_log, text=True)
     k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
-    d = c = None
+    d = None
+    rec = {"bdf": g["bdf"], "kfd_node": part0.get("kfd_node")}
     try:
-        args = ["--devices", "0", "--metrics-addr", "127.0.0.1:0", "--health-event-extra-types", TYPES]
-        if relay:
-            args += ["--health-event-socket", sock]
-        d = harness.Daemon(scratch, None, real_smi=True, args=args, env=env).start()
+        assert helper.stdout.readline().strip() == "ready"
+        env = {"DP_HEALTH_POLL_MS": "200",
+               "LD_PRELOAD": " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), SIM) if x)}
+        d = harness.Daemon(scratch, None, real_smi=True, env=env, args=[
+            "--devices", "0", "--metrics-addr", "127.0.0.1:0", "--health-event-socket", sock,
+            "--health-event-extra-types", TYPES]).start()
         port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics", 30)).group(1))
         reg = k.wait_registration(30)
         c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
         q, call = c.watch()
         first = {x.ID: x.health for x in q.get(timeout=10).devices}
-        d.wait_log("events on through the relay" if relay else "health monitor watching", 30)
-        _run_hip(hip_program)
+        d.wait_log("events on through the relay", 30)
+        helper.stdin.write("go\n")
+        helper.stdin.flush()
+        assert helper.stdout.readline().strip() == "opened"
+        rec["hip"] = json.loads(helper.stdout.readline())["hip"]
         m, started = _wait_metric(port, "amdgpu_dp_gpu_events_total", {"bdf": g["bdf"], "type": "PROCESS_START"})
-        m, ended = _wait_metric(port, "amdgpu_dp_gpu_events_total", {"bdf": g["bdf"], "type": "PROCESS_END"})
         time.sleep(0.5)
         transitions = []
         while not q.empty():
             transitions.append({x.ID: x.health for x in q.get().devices})
         call.cancel()
-        unmatched = {dict(ls)["type"]: v for (n, ls), v in m.items() if n == "amdgpu_dp_unmatched_events_total"}
-        events = {dict(ls)["bdf"] + " " + dict(ls)["type"]: v for (n, ls), v in m.items()
-                  if n == "amdgpu_dp_gpu_events_total"}
-        rlines = []
-        if relay:
-            rlines = [ln for ln in relay.log().splitlines() if "event seq=" in ln][-10:]
-        part0 = g["partitions"][0]
-        rec = {"layout": layout, "bdf": g["bdf"], "kfd_node": part0.get("kfd_node"), "first_law": first,
-               "transitions": transitions, "events_total": events, "unmatched": unmatched,
-               "relay_event_lines": rlines,
-               "daemon_log": [ln for ln in d.log().splitlines() if "event" in ln][-15:]}
-        _record(f"daemon_events_{layout}.json", rec)
-        assert started and started >= 1, rec
-        assert ended and ended >= 1, rec
-        assert all(v == 0 for v in unmatched.values()), rec
-        assert transitions == [] and all(h == "Healthy" for h in first.values()), rec
-        if relay:
-            # the relay's line carries the box GPU's KFD node and PCI address
-            want = re.compile(r"event seq=\d+ node=(\d+|-) bdf=" + re.escape(g["bdf"]) + r" part=\d+ type=12 ")
-            hits = [want.search(ln) for ln in rlines]
-            assert any(hits), rec
-            node = next(h.group(1) for h in hits if h)
-            if part0.get("kfd_node") is not None:
-                assert node == str(part0["kfd_node"]), rec
+        c.close()
+        m = _parse(_get(port, "/metrics")[1])
+        rec.update({"first_law": first, "transitions": transitions, "process_start_counted": started,
+                    "unmatched": {dict(ls)["type"]: v for (n, ls), v in m.items()
+                                  if n == "amdgpu_dp_unmatched_events_total"},
+                    "daemon_log": [ln for ln in d.log().splitlines() if "relay" in ln or "event" in ln][-12:]})
     finally:
-        if c:
-            c.close()
+        if helper.poll() is None:
+            try:
+                helper.stdin.write("done\n")
+                helper.stdin.flush()
+            except OSError:
+                pass
+        try:
+            rec["helper_rc"] = helper.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            helper.kill()
+            rec["helper_rc"] = "killed"
+        relay_log.close()
+        rec["relay_event_lines"] = [ln for ln in open(tmp_path / "relay.log").read().splitlines()
+                                    if "event seq=" in ln][-6:]
+        _record("relay_daemon_events.json", rec)
         if d:
             assert d.stop() == 0
         k.stop()
-        if relay:
-            assert relay.stop() == 0
+    assert rec["hip"]["hipInit"] == 0, rec
+    assert started and started >= 1, rec
+    assert all(v == 0 for v in rec["unmatched"].values()), rec
+    assert rec["transitions"] == [] and all(h == "Healthy" for h in rec["first_law"].values()), rec
+    want = re.compile(r"event seq=\d+ node=(\d+|-) bdf=" + re.escape(g["bdf"]) + r" part=\d+ type=12 ")
+    hits = [want.search(ln) for ln in rec["relay_event_lines"]]
+    assert any(hits), rec
+    if part0.get("kfd_node") is not None:
+        assert next(h.group(1) for h in hits if h) == str(part0["kfd_node"]), rec
+    assert rec["helper_rc"] == 0, rec
