@@ -32,11 +32,14 @@ probe:
 	$(PY) -c "from k8s_gpu_sharing_plugin_amd.utils import build; build.build_probe()"
 
 # Unit tests, then the bounded model check of the health state machine: every
-# sequence of up to HEALTH_MODEL_DEPTH steps over its 16 events, both layouts.
+# sequence of up to HEALTH_MODEL_DEPTH steps over its 16 events, both layouts,
+# then up to HEALTH_MODEL_EXT_DEPTH steps over the extended 22/23 events.
 HEALTH_MODEL_DEPTH ?= 6
+HEALTH_MODEL_EXT_DEPTH ?= 5
 test-native: build
 	$(BUILD)/adp_unit_tests
 	$(BUILD)/adp_health_model --depth $(HEALTH_MODEL_DEPTH)
+	$(BUILD)/adp_health_model --extended --depth $(HEALTH_MODEL_EXT_DEPTH)
 
 test: build
 	$(PY) -m pytest tests -q -m "not gpu"
@@ -88,7 +91,8 @@ tsan-e2e:
 	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py tests/test_preferred.py \
 	  tests/test_event_relay.py tests/test_policy_units.py tests/test_hip_order.py tests/test_kfd_topology.py tests/test_chart_layout.py \
 	  tests/test_memory_unit_guards.py tests/test_parity_contract.py tests/test_metrics_exposition.py tests/test_gpu_recovery.py \
-	  -k "not additional_ids and not classification and not bruteforce and not snapshot_reports and not scan_reads_only and not another_namespace and not without_client_id and not partitions_read and not parser_edge"
+	  tests/test_event_matching.py \
+	  -k "not additional_ids and not classification and not bruteforce and not snapshot_reports and not scan_reads_only and not another_namespace and not without_client_id and not partitions_read and not parser_edge and not hosted and not event_types_parse"
 	@if ls build/tsan-logs/* >/dev/null 2>&1; then cat build/tsan-logs/*; exit 1; fi
 
 # The daemon under ASan/UBSan/LSan, driven by the same end-to-end suites.
@@ -122,7 +126,8 @@ asan-e2e:
 	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py tests/test_preferred.py \
 	  tests/test_event_relay.py tests/test_policy_units.py tests/test_hip_order.py tests/test_kfd_topology.py tests/test_chart_layout.py \
 	  tests/test_memory_unit_guards.py tests/test_parity_contract.py tests/test_metrics_exposition.py tests/test_gpu_recovery.py \
-	  -k "not additional_ids and not classification and not bruteforce and not snapshot_reports and not scan_reads_only and not another_namespace and not without_client_id and not partitions_read and not parser_edge"
+	  tests/test_event_matching.py \
+	  -k "not additional_ids and not classification and not bruteforce and not snapshot_reports and not scan_reads_only and not another_namespace and not without_client_id and not partitions_read and not parser_edge and not hosted and not event_types_parse"
 	@if ls build/asan-logs/* >/dev/null 2>&1; then cat build/asan-logs/*; exit 1; fi
 
 # Line coverage of native/src from the unit, stress and CPU end-to-end suites.

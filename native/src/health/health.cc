@@ -649,7 +649,7 @@ std::optional<uint64_t> Monitor::PollEcc(const inventory::PhysicalGpu& g, void* 
   if (!ecc.ok()) {
     counters_->ecc_read_errors.fetch_add(1);
     if (poll == 1)
-      LOG_WARN(kComp, "GPU %s: uncorrectable ECC count unreadable (%s); ECC polling is off for it", g.bdf.c_str(),
+      LOG_WARN(kComp, "GPU %s: uncorrectable ECC count unreadable (%s); read again every poll", g.bdf.c_str(),
                ecc.status().ToString().c_str());
     return std::nullopt;
   }

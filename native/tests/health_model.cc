@@ -1,5 +1,6 @@
 // Bounded exhaustive model check of the health state machine (round-6 review
 // item 2). Run: build/native/adp_health_model [--depth N] [--mode in-process|relay|both]
+//   [--extended] [--replay STEP,STEP,...]
 //
 // The reference's whole health loop is ~120 lines (nvidia.go:181-269,
 // server.go:251-265): a device goes Unhealthy on an Xid and never comes back.
@@ -30,6 +31,17 @@
 //   DRAIN UNDRAIN RETURN      the operator's drain file / --return-to-service for GPU 0
 //   CLOCK_HOLD                --reset-recovery-hold-ms (+1) pass
 //
+// --extended adds (22 symbols in-process, 23 with the relay):
+//   PRE1 POST1                an amdsmi event on GPU 1, which then resets too
+//   UNPLACED                  relay: a GPU_PRE_RESET the relay could not place
+//                             (node=- bdf=-); in-process: a GPU_POST_RESET on an
+//                             unknown handle (counted, no verdict)
+//   RELAY_RENEW               relay: the relay renews its registration (events
+//                             keep flowing); in-process: one failing wait
+//   RELAY_STUCK               relay only: the watchdog turns events off and on
+//   HALF_HOLD                 half of --reset-recovery-hold-ms passes
+//   ECC_UNREADABLE            GPU 0's ECC count turns unreadable / readable again
+//
 // against a small reference model of what the monitor must believe, given the
 // events it was delivered. Invariants checked after every step:
 //   I1  what the plugins advertise (the listener) = the monitor's failure bits
@@ -43,13 +55,15 @@
 //       poll, a hold, and another poll is back (lookahead run per state);
 //   I4  the state file re-read (Ledger::Parse) equals the ledger in memory;
 //   I5  drained exactly while the drain file names the GPU;
-//   I6  GPU 1 (never the target) stays healthy, but for an unplaceable reset;
-//   I7  a reset-flap quarantine begins only with a delivered GPU_PRE_RESET and
+//   I6  GPU 1 (never the target) stays healthy, but for an unplaceable reset
+//       (--extended: it may wait for its own GPU_POST_RESET and be quarantined);
+//   I7  (per GPU) a reset-flap quarantine begins only with a delivered GPU_PRE_RESET and
 //       ends only after a quiet window (or the operator), and does end then;
-//   I8  the reset history never counts more resets than distinct
+//   I8  (per GPU) the reset history never counts more resets than distinct
 //       GPU_PRE_RESETs were delivered (relay replays counted once);
 //   I9  the ECC verdict = the count rose above the baseline of the first
-//       observation / the last completed reset / counter reset / operator.
+//       observation / the last completed reset / counter reset / operator,
+//       whenever the count could be read.
 // States are deduplicated by a canonical hash (times relative to the clock,
 // clamped past every threshold), so each distinct state is expanded once per
 // remaining depth: every sequence up to --depth is covered. Each node is
@@ -138,11 +152,30 @@ namespace {
 
 enum Sym : int {
   A_PRE, A_POST, A_VMFAULT, A_POLL_OK, A_POLL_FAIL, A_ECC_UP, A_ECC_RESET, A_RELAY_DROP, A_RELAY_RESTART, A_LOST_EVENT, A_SIGHUP,
-  A_RESTART, A_DRAIN, A_UNDRAIN, A_RETURN, A_CLOCK_HOLD, kSymbols
+  A_RESTART, A_DRAIN, A_UNDRAIN, A_RETURN, A_CLOCK_HOLD, kBaseSymbols,
+  // --extended: GPU 1 resets too; an unplaceable GPU_PRE_RESET from the relay
+  // (in-process: an unplaceable GPU_POST_RESET); the relay renewing its
+  // registration (in-process: one failing wait); the relay's watchdog turning
+  // events off and on again (relay only); half a hold passing; GPU 0's ECC
+  // count becoming unreadable and readable again.
+  A_PRE1 = kBaseSymbols, A_POST1, A_UNPLACED, A_RELAY_RENEW, A_RELAY_STUCK, A_HALF_HOLD, A_ECC_UNREADABLE, kSymbols
 };
-const char* kSymNames[] = {"PRE",        "POST",          "VMFAULT",    "POLL_OK", "POLL_FAIL", "ECC_UP",
-                           "ECC_RESET",  "RELAY_DROP",    "RELAY_RESTART", "LOST_EVENT", "SIGHUP", "RESTART",
-                           "DRAIN",      "UNDRAIN",       "RETURN",     "CLOCK_HOLD"};
+const char* kSymNames[] = {"PRE",         "POST",          "VMFAULT",      "POLL_OK",     "POLL_FAIL",
+                           "ECC_UP",      "ECC_RESET",     "RELAY_DROP",   "RELAY_RESTART", "LOST_EVENT",
+                           "SIGHUP",      "RESTART",       "DRAIN",        "UNDRAIN",     "RETURN",
+                           "CLOCK_HOLD",  "PRE1",          "POST1",        "UNPLACED",    "RELAY_RENEW",
+                           "RELAY_STUCK", "HALF_HOLD",     "ECC_UNREADABLE"};
+static_assert(sizeof(kSymNames) / sizeof(kSymNames[0]) == kSymbols, "symbol names");
+
+bool g_extended = false;  // --extended: set before the workers fork
+
+// The symbols explored in a layout.
+std::vector<int> Alphabet(bool relay, bool extended) {
+  std::vector<int> a;
+  for (int s = 0; s < (extended ? static_cast<int>(kSymbols) : static_cast<int>(kBaseSymbols)); ++s)
+    if (relay || s != A_RELAY_STUCK) a.push_back(s);
+  return a;
+}
 
 constexpr int64_t kHoldMs = 1000, kWindowMs = 2500, kEventFailMs = 500, kPollMs = 200;
 constexpr int kFlapLimit = 2;
@@ -170,6 +203,7 @@ class FakeSmi : public smi::Library {
   char handle[2] = {0, 0};
   char foreign = 0;  // a handle amdsmi never enumerated
   bool waits_failing = false;
+  bool ecc_ok = true;  // GPU 0's uncorrectable count readable
   std::set<void*> registered;
   std::deque<smi::Event> queue;        // events the kernel holds for the registration
   std::vector<smi::Event> delivered;   // what EventsWait handed out (for the model)
@@ -204,6 +238,7 @@ class FakeSmi : public smi::Library {
   Result<uint64_t> UncorrectableErrors(void* h) override {
     int i = Index(h);
     if (i < 0 || !gpu[i].alive) return Unavailable("not answering");
+    if (i == 0 && !ecc_ok) return Unavailable("ecc query failed");
     return gpu[i].ecc;
   }
   Result<uint32_t> RetiredPages(void* h) override {
@@ -284,6 +319,7 @@ struct RelayModel {
   std::vector<std::pair<uint64_t, std::string>> ring;
   bool lost = false;
   uint64_t lost_seq = 0;
+  bool stuck = false;  // the watchdog says the amdsmi event wait hangs: events=off
   int fd = -1;  // the daemon's connection (relay side), -1: none
   std::string Id() const {
     char b[8];
@@ -291,9 +327,11 @@ struct RelayModel {
     return b;
   }
   std::string Hello(bool reinit, int gap) const {
-    std::string h = std::string("hello v1 ") + (reinit ? "reinit " : "") + "events=ok processors=2 relay=" + Id() +
+    std::string h = std::string("hello v1 ") + (reinit ? "reinit " : "") +
+                    (stuck ? std::string("events=off") : std::string("events=ok processors=2")) + " relay=" + Id() +
                     " gen=" + std::to_string(gen) + " seq=" + std::to_string(seq) + " fp=- renew_ms=0";
     if (gap >= 0) h += " gap=" + std::to_string(gap);
+    if (stuck) h += " reason=the amdsmi event wait has not returned for 10001 ms";
     return h + "\n";
   }
   void Send(const std::string& s) {
@@ -313,7 +351,7 @@ struct Model {
   bool pending[2] = {false, false};      // a delivered GPU_PRE_RESET awaits its GPU_POST_RESET
   bool gap_since_pre[2] = {false, false};  // the monitor recorded a confirmed gap since it
   bool drained = false;
-  std::set<std::string> pre_ids;         // distinct GPU_PRE_RESETs delivered since the operator's last return
+  std::set<std::string> pre_ids[2];      // distinct GPU_PRE_RESETs delivered since the operator's last return
   bool has_baseline = false;
   uint64_t baseline = 0, seen = 0;       // GPU 0's ECC reference
 };
@@ -364,7 +402,7 @@ class World {
     Before before = Observe();
     smi_.delivered.clear();
     sent_.clear();
-    pres_delivered_ = 0;
+    pres_delivered_[0] = pres_delivered_[1] = 0;
     bool housekept = false, polled = false;
     const bool in_proc = !relay_mode_;
     switch (sym) {
@@ -449,10 +487,55 @@ class World {
         MonitorTestPeer::Housekeeping(*mon_);
         housekept = true;
         break;
-      case A_CLOCK_HOLD:
-        clock_.Advance(kHoldMs + 1);
+      case A_CLOCK_HOLD: case A_HALF_HOLD:
+        clock_.Advance(sym == A_CLOCK_HOLD ? kHoldMs + 1 : kHoldMs / 2);
         if (relay_mode_) MonitorTestPeer::Deadlines(*mon_);
         TimePasses();
+        break;
+      case A_PRE1: case A_POST1:
+        if (in_proc) {
+          smi_.Raise(&smi_.handle[1], sym == A_PRE1 ? 3 : 4);
+          MonitorTestPeer::Wait(*mon_);
+        } else {
+          Emit(sym == A_PRE1 ? 3 : 4, 1);
+        }
+        break;
+      case A_UNPLACED:
+        if (in_proc) {
+          smi_.Raise(&smi_.foreign, 4);  // (the unplaceable PRE is LOST_EVENT here)
+          MonitorTestPeer::Wait(*mon_);
+        } else {
+          Emit(3, -1);  // "node=- bdf=-"
+        }
+        break;
+      case A_RELAY_RENEW:
+        if (in_proc) {  // one wait fails, the next succeeds: no gap
+          const bool was = smi_.waits_failing;
+          smi_.waits_failing = true;
+          MonitorTestPeer::Wait(*mon_);
+          smi_.waits_failing = was;
+          MonitorTestPeer::Wait(*mon_);
+        } else {  // relay.cc OnRenewals "1": every subscribed daemon went without a registration
+          ++relay_.gen;
+          if (relay_.fd >= 0) {
+            relay_.Send(relay_.Hello(true, 1));
+            MonitorTestPeer::RelayRead(*mon_);
+          }
+        }
+        break;
+      case A_RELAY_STUCK:  // relay.cc Watchdog: events off (and on again), told to every daemon
+        relay_.stuck = !relay_.stuck;
+        if (relay_.fd >= 0) {
+          relay_.Send(relay_.Hello(true, 1));
+          MonitorTestPeer::RelayRead(*mon_);
+        }
+        break;
+      case A_ECC_UNREADABLE:
+        smi_.ecc_ok = !smi_.ecc_ok;
+        clock_.Advance(kPollMs);
+        TimePasses();
+        MonitorTestPeer::Poll(*mon_);
+        polled = housekept = true;
         break;
     }
     Settle();
@@ -480,8 +563,9 @@ class World {
       k += std::string("|m") + (model_.pending[g] ? "P" : "p") + (model_.gap_since_pre[g] ? "G" : "g");
     }
     k += "|smi:" + std::to_string(smi_.gpu[0].alive) + "/" + std::to_string(smi_.gpu[0].ecc) + "/" +
-         std::to_string(smi_.waits_failing) + "/q" + std::to_string(smi_.queue.size()) + "/r" +
-         std::to_string(smi_.registered.size());
+         std::to_string(smi_.ecc_ok) + "/" + std::to_string(smi_.waits_failing) + "/r" +
+         std::to_string(smi_.registered.size()) + "/q";
+    for (const auto& e : smi_.queue) k += std::to_string(smi_.Index(e.handle)) + ":" + std::to_string(e.type) + ",";
     k += "|model:" + std::to_string(model_.drained) + "/" +
          std::to_string(model_.has_baseline) + "/" + std::to_string(model_.baseline) + "/" +
          std::to_string(model_.seen);
@@ -500,7 +584,8 @@ class World {
         return "lag" + std::to_string(relay_.seq - c.seq) + (c.gen == relay_.gen ? "" : "g") +
                (relay_.lost && c.seq <= relay_.lost_seq ? "L" : "");
       };
-      k += "|relay:" + std::to_string(relay_.fd >= 0) + "/mem:" + cursor(cur) + "/file:" + cursor(fc);
+      k += "|relay:" + std::to_string(relay_.fd >= 0) + (relay_.stuck ? "S" : "s") + "/mem:" + cursor(cur) +
+           "/file:" + cursor(fc);
       // The events either cursor could still have replayed, and whether the
       // daemon already had each.
       uint64_t base = UINT64_MAX;
@@ -508,12 +593,13 @@ class World {
         if (c->valid && c->relay == relay_.Id()) base = std::min(base, c->seq);
       for (const auto& [q, l] : relay_.ring)
         if (q > base || (base == UINT64_MAX && relay_.fd < 0 && false))
-          k += std::to_string(TypeOf(l)) + (delivered_ids_.count(relay_.Id() + ":" + std::to_string(q)) ? "d" : "n");
+          k += std::to_string(GpuOf(l)) + ":" + std::to_string(TypeOf(l)) +
+               (delivered_ids_.count(relay_.Id() + ":" + std::to_string(q)) ? "d" : "n");
     }
-    {
+    for (int g = 0; g < 2; ++g) {
       // resets recorded vs distinct resets delivered (I8), clamped
-      const size_t rs = ledger_->Get(key_[0]).resets.size();
-      k += "|i8:" + std::to_string(std::min<size_t>(3, model_.pre_ids.size() - std::min(rs, model_.pre_ids.size())));
+      const size_t rs = ledger_->Get(key_[g]).resets.size(), ids = model_.pre_ids[g].size();
+      k += "|i8:" + std::to_string(std::min<size_t>(3, ids - std::min(rs, ids)));
     }
     return k;
   }
@@ -533,8 +619,10 @@ class World {
     int gpus = 0;
     for (int g = 0; g < 2; ++g) {
       health::GapMark m;
-      if ((MonitorTestPeer::Fail(*mon_, g) & health::kFailResetPending) && ledger_->Gap(key_[g], &m) && !m.tentative)
-        gpus |= 1 << g;
+      // a confirmed gap in the ledger, or one the model knows there must be
+      // (an unplaceable GPU_PRE_RESET)
+      const bool gap = (ledger_->Gap(key_[g], &m) && !m.tentative) || (model_.pending[g] && model_.gap_since_pre[g]);
+      if ((MonitorTestPeer::Fail(*mon_, g) & health::kFailResetPending) && gap) gpus |= 1 << g;
     }
     return gpus;
   }
@@ -548,7 +636,7 @@ class World {
  private:
   struct Before {
     uint32_t fail[2];
-    std::vector<int64_t> resets0;
+    std::vector<int64_t> resets[2];
     bool gap_confirmed[2];
     health::GapMark gap[2];
     uint64_t recovered[2];
@@ -562,8 +650,8 @@ class World {
       s.fail[g] = ledger_->Get(key_[g]).fail | (mon_ ? MonitorTestPeer::Fail(*mon_, g) & health::kFailDrained : 0);
       s.gap_confirmed[g] = ledger_->Gap(key_[g], &s.gap[g]) && !s.gap[g].tentative;
       s.recovered[g] = rec.count(kBdf[g]) ? rec[kBdf[g]] : 0;
+      s.resets[g] = ledger_->Get(key_[g]).resets;
     }
-    s.resets0 = ledger_->Get(key_[0]).resets;
     s.steady = clock_.steady;
     s.wall = clock_.wall;
     return s;
@@ -616,11 +704,12 @@ class World {
       for (const auto& [q, l] : relay_.ring)
         if (q > rq.since_seq) {
           replay += l;
-          sent_.emplace_back(relay_.Id() + ":" + std::to_string(q), TypeOf(l));
+          sent_.push_back({relay_.Id() + ":" + std::to_string(q), TypeOf(l), GpuOf(l)});
         }
       relay_.Send(replay);
       gap = held && rq.since_gen == relay_.gen ? 0 : 1;
     }
+    if (relay_.stuck) relay_.Send(relay_.Hello(true, 1));
     relay_.Send(relay_.Hello(true, gap));
     MonitorTestPeer::RelayRead(*mon_);
   }
@@ -629,13 +718,16 @@ class World {
     if (relay_mode_) relay_.Close();
   }
 
-  void Emit(uint32_t type) {
+  // An event line of GPU `gpu` (-1: unplaceable, "node=- bdf=-").
+  void Emit(uint32_t type, int gpu = 0) {
     const uint64_t seq = ++relay_.seq;
-    std::string line = "event seq=" + std::to_string(seq) + " node=2 bdf=" + kBdf[0] +
-                       " part=0 type=" + std::to_string(type) + " fake\n";
+    std::string where = gpu < 0 ? std::string("node=- bdf=-")
+                                : "node=" + std::to_string(2 + 8 * gpu) + " bdf=" + kBdf[gpu];
+    std::string line = "event seq=" + std::to_string(seq) + " " + where + " part=0 type=" + std::to_string(type) +
+                       " fake\n";
     relay_.ring.emplace_back(seq, line);
     if (relay_.fd >= 0) {
-      sent_.emplace_back(relay_.Id() + ":" + std::to_string(seq), type);
+      sent_.push_back({relay_.Id() + ":" + std::to_string(seq), type, gpu});
       relay_.Send(line);
       MonitorTestPeer::RelayRead(*mon_);
     }
@@ -658,13 +750,18 @@ class World {
   static uint32_t TypeOf(const std::string& line) {
     return static_cast<uint32_t>(std::stoul(line.substr(line.find("type=") + 5)));
   }
+  static int GpuOf(const std::string& line) {
+    return line.find(std::string("bdf=") + kBdf[1]) != std::string::npos ? 1
+           : line.find("bdf=-") != std::string::npos                    ? -1
+                                                                         : 0;
+  }
 
   // Everything the monitor was handed this step, into the model, in order
   // (the relay's lines are read as soon as they are written).
   void Settle() {
     if (relay_mode_) {
-      for (const auto& [id, type] : sent_) Deliver(0, type, id);
-      for (const auto& [id, type] : sent_) delivered_ids_.insert(id);
+      for (const auto& e : sent_) Deliver(e.gpu, e.type, e.id);
+      for (const auto& e : sent_) delivered_ids_.insert(e.id);
     } else {
       for (const auto& e : smi_.delivered) {
         int g = smi_.Index(e.handle);
@@ -684,16 +781,16 @@ class World {
       // A replayed event the daemon already handled is no new reset.
       if (replayed_.count(id)) return;
       replayed_.insert(id);
-      ++pres_delivered_;
+      ++pres_delivered_[g];
       model_.pending[g] = true;
       model_.gap_since_pre[g] = false;
-      model_.pre_ids.insert(id);
+      model_.pre_ids[g].insert(id);
     } else if (type == 4) {
       if (replayed_.count(id)) return;
       replayed_.insert(id);
       model_.pending[g] = false;
       model_.gap_since_pre[g] = false;
-      if (smi_.gpu[g].alive && g == 0) {
+      if (smi_.gpu[g].alive && g == 0 && smi_.ecc_ok) {
         model_.has_baseline = true;
         model_.baseline = model_.seen = smi_.gpu[0].ecc;
       }
@@ -713,15 +810,15 @@ class World {
     }
     if (sym == A_RETURN) {
       for (int g = 0; g < 1; ++g) model_.pending[g] = model_.gap_since_pre[g] = false;
-      model_.pre_ids.clear();
-      if (smi_.gpu[0].alive) {
+      model_.pre_ids[0].clear();
+      if (smi_.gpu[0].alive && smi_.ecc_ok) {
         model_.has_baseline = true;
         model_.baseline = model_.seen = smi_.gpu[0].ecc;
       }
     }
     if (sym == A_DRAIN) model_.drained = true;
     if (sym == A_UNDRAIN) model_.drained = false;
-    if ((polled || sym == A_SIGHUP || sym == A_RESTART) && smi_.gpu[0].alive) {
+    if ((polled || sym == A_SIGHUP || sym == A_RESTART) && smi_.gpu[0].alive && smi_.ecc_ok) {
       const uint64_t c = smi_.gpu[0].ecc;
       if (!model_.has_baseline) {
         model_.has_baseline = true;
@@ -784,31 +881,38 @@ class World {
     if (model_.drained != static_cast<bool>(f0 & health::kFailDrained))
       fail(std::string("I5: drain file ") + (model_.drained ? "names" : "does not name") + " GPU 0, bits " +
            std::to_string(f0));
-    // I6
-    if ((f1 & ~health::kFailResetPending) != 0)
-      fail("I6: bystander GPU 1 has failure bits " + std::to_string(f1));
-    // I7
-    const bool flap = f0 & health::kFailFlapping, was_flap = before.fail[0] & health::kFailFlapping;
-    int64_t last = before.resets0.empty() ? INT64_MIN : *std::max_element(before.resets0.begin(), before.resets0.end());
-    if (flap && !was_flap) {
-      if (pres_delivered_ == 0) fail("I7: quarantine began without a new GPU_PRE_RESET delivered");
-      int in_window = 0;
-      for (int64_t t : ledger_->Get(key_[0]).resets) in_window += clock_.wall - t < kWindowMs;
-      if (in_window < kFlapLimit) fail("I7: quarantined with " + std::to_string(in_window) + " resets in the window");
+    // I6: the bystander GPU 1 (in --extended it resets too, so it may wait
+    // for a GPU_POST_RESET and be quarantined)
+    const uint32_t allowed1 = health::kFailResetPending | (g_extended ? uint32_t{health::kFailFlapping} : 0u);
+    if ((f1 & ~allowed1) != 0) fail("I6: bystander GPU 1 has failure bits " + std::to_string(f1));
+    // I7, per GPU
+    for (int g = 0; g < 2; ++g) {
+      const std::string G = "I7: GPU " + std::to_string(g) + " ";
+      const uint32_t f = MonitorTestPeer::Fail(*mon_, g);
+      const std::vector<int64_t>& was = before.resets[g];
+      const bool flap = f & health::kFailFlapping, was_flap = before.fail[g] & health::kFailFlapping;
+      const bool returned = sym == A_RETURN && g == 0;
+      const int64_t last = was.empty() ? INT64_MIN : *std::max_element(was.begin(), was.end());
+      const std::vector<int64_t> now = ledger_->Get(key_[g]).resets;
+      if (flap && !was_flap) {
+        if (pres_delivered_[g] == 0) fail(G + "quarantine began without a new GPU_PRE_RESET delivered");
+        int in_window = 0;
+        for (int64_t t : now) in_window += clock_.wall - t < kWindowMs;
+        if (in_window < kFlapLimit) fail(G + "quarantined with " + std::to_string(in_window) + " resets in the window");
+      }
+      if (!flap && was_flap && !returned && !was.empty() && clock_.wall - last < kWindowMs)
+        fail(G + "quarantine ended " + std::to_string(clock_.wall - last) + " ms after the last reset");
+      if (flap && housekept && !returned && !was.empty()) {
+        const int64_t last_now = now.empty() ? INT64_MIN : *std::max_element(now.begin(), now.end());
+        if (clock_.wall - last_now >= kWindowMs) fail(G + "still quarantined after a quiet window");
+      }
+      // I8
+      if (now.size() > model_.pre_ids[g].size())
+        fail("I8: GPU " + std::to_string(g) + " " + std::to_string(now.size()) + " resets recorded for " +
+             std::to_string(model_.pre_ids[g].size()) + " distinct GPU_PRE_RESETs");
     }
-    if (!flap && was_flap && sym != A_RETURN && !before.resets0.empty() && clock_.wall - last < kWindowMs)
-      fail("I7: quarantine ended " + std::to_string(clock_.wall - last) + " ms after the last reset");
-    if (flap && housekept && sym != A_RETURN && !before.resets0.empty()) {
-      std::vector<int64_t> now = ledger_->Get(key_[0]).resets;
-      int64_t last_now = now.empty() ? INT64_MIN : *std::max_element(now.begin(), now.end());
-      if (clock_.wall - last_now >= kWindowMs) fail("I7: still quarantined after a quiet window");
-    }
-    // I8
-    if (ledger_->Get(key_[0]).resets.size() > model_.pre_ids.size())
-      fail("I8: " + std::to_string(ledger_->Get(key_[0]).resets.size()) + " resets recorded for " +
-           std::to_string(model_.pre_ids.size()) + " distinct GPU_PRE_RESETs");
     // I9 (after a poll that read the count)
-    if (polled && smi_.gpu[0].alive && model_.has_baseline &&
+    if (polled && smi_.gpu[0].alive && smi_.ecc_ok && model_.has_baseline &&
         static_cast<bool>(f0 & health::kFailEcc) != (smi_.gpu[0].ecc > model_.baseline))
       fail("I9: ECC verdict " + std::to_string(static_cast<bool>(f0 & health::kFailEcc)) + " for count " +
            std::to_string(smi_.gpu[0].ecc) + " against baseline " + std::to_string(model_.baseline));
@@ -829,10 +933,15 @@ class World {
   int lfd_ = -1;
   RelayModel relay_;
   Model model_;
-  std::vector<std::pair<std::string, uint32_t>> sent_;  // relay event lines written this step ("<relay>:<seq>", type)
+  struct Sent {
+    std::string id;  // "<relay>:<seq>"
+    uint32_t type;
+    int gpu;         // -1: unplaceable
+  };
+  std::vector<Sent> sent_;  // relay event lines written this step
   std::set<std::string> delivered_ids_;  // every relay event the daemon was sent
   std::set<std::string> replayed_;
-  int pres_delivered_ = 0;  // new GPU_PRE_RESETs this step
+  int pres_delivered_[2] = {0, 0};  // new GPU_PRE_RESETs this step
   uint64_t local_events_ = 0;
 };
 
@@ -944,7 +1053,7 @@ void Expand(bool relay, const std::string& dir, int depth, const std::vector<int
   while (!stack.empty()) {
     std::vector<int> seq = std::move(stack.back());
     stack.pop_back();
-    for (int s = 0; s < kSymbols; ++s) {
+    for (int s : Alphabet(relay, g_extended)) {
       std::vector<int> next = seq;
       next.push_back(s);
       if (Visit(relay, dir, depth, next, sh)) stack.push_back(std::move(next));
@@ -964,6 +1073,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--jobs") && i + 1 < argc) jobs = std::max(1, atoi(argv[++i]));
     else if (!strcmp(argv[i], "--mode") && i + 1 < argc) mode = argv[++i];
     else if (!strcmp(argv[i], "--replay") && i + 1 < argc) replay = Split(argv[++i], ',');
+    else if (!strcmp(argv[i], "--extended")) g_extended = true;
   }
   SetLogLevel(getenv("ADP_LOG_LEVEL") ? LogLevel::kInfo : LogLevel::kError);
   setvbuf(stdout, nullptr, _IOLBF, 0);
@@ -991,9 +1101,18 @@ int main(int argc, char** argv) {
   new (sh) Shared();
   if (!replay.empty()) {  // one sequence, logged: --replay PRE,SIGHUP,...
     std::vector<int> seq;
-    for (const auto& n : replay)
+    for (const auto& n : replay) {
+      int sym = -1;
       for (int s = 0; s < kSymbols; ++s)
-        if (n == kSymNames[s]) seq.push_back(s);
+        if (n == kSymNames[s]) sym = s;
+      if (sym < 0) {
+        fprintf(stderr, "unknown step '%s'\n", n.c_str());
+        rmdir(dir.c_str());
+        return 2;
+      }
+      if (sym >= kBaseSymbols) g_extended = true;  // a step of the extended alphabet: its invariants
+      seq.push_back(sym);
+    }
     for (bool relay : modes) {
       std::string v = Replay(relay, dir, seq, nullptr, nullptr, sh);
       printf("%s: %s\n", relay ? "relay" : "in-process", v.empty() ? "ok" : v.c_str());
@@ -1005,9 +1124,9 @@ int main(int argc, char** argv) {
     // pull from a shared counter, each expanding its subtree depth first.
     std::vector<std::pair<bool, std::vector<int>>> tasks;
     for (bool relay : modes)
-      for (int s = 0; s < kSymbols; ++s)
+      for (int s : Alphabet(relay, g_extended))
         if (Visit(relay, dir, depth, {s}, sh))
-          for (int s2 = 0; s2 < kSymbols; ++s2) tasks.push_back({relay, {s, s2}});
+          for (int s2 : Alphabet(relay, g_extended)) tasks.push_back({relay, {s, s2}});
     std::vector<pid_t> kids;
     for (int j = 0; j < jobs; ++j) {
       pid_t pid = fork();
@@ -1035,13 +1154,18 @@ int main(int argc, char** argv) {
       }
     }
     double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    double all = 0, n = 1;
-    for (int i = 0; i < depth; ++i) all += (n *= kSymbols);
-    all *= static_cast<double>(modes.size());
-    printf("health model: %s, depth %d, %d symbols, %d workers: all %.0f sequences of 1..%d steps covered by %llu "
+    double all = 0;
+    std::string sizes;
+    for (bool relay : modes) {
+      const size_t k = Alphabet(relay, g_extended).size();
+      double n = 1;
+      for (int i = 0; i < depth; ++i) all += (n *= static_cast<double>(k));
+      sizes += (sizes.empty() ? "" : "/") + std::to_string(k);
+    }
+    printf("health model: %s%s, depth %d, %s symbols, %d workers: all %.0f sequences of 1..%d steps covered by %llu "
            "distinct states (%llu transitions, %llu pruned as seen, %llu liveness probes, %llu monitor steps) in "
            "%.1f s: %llu violation(s)\n",
-           mode.c_str(), depth, kSymbols, jobs, all, depth, static_cast<unsigned long long>(sh->distinct.load()),
+           mode.c_str(), g_extended ? " (extended)" : "", depth, sizes.c_str(), jobs, all, depth, static_cast<unsigned long long>(sh->distinct.load()),
            static_cast<unsigned long long>(sh->transitions.load()), static_cast<unsigned long long>(sh->pruned.load()),
            static_cast<unsigned long long>(sh->probes.load()), static_cast<unsigned long long>(sh->steps.load()), secs,
            static_cast<unsigned long long>(sh->violations.load()));

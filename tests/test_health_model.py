@@ -30,6 +30,33 @@ def test_every_sequence_of_five_steps_keeps_the_invariants():
     assert int(m.group(2)) > 5000 and int(m.group(3)) == 0, r.stdout
 
 
+def test_extended_alphabet_every_sequence_of_four_steps():
+    """--extended adds GPU 1's resets, an unplaceable GPU_PRE_RESET, the relay
+    renewing its registration (in-process: one failing wait), the relay's
+    watchdog turning events off and on (relay only), half a hold, and GPU 0's
+    ECC count turning unreadable and back. `make test-native` runs depth 5."""
+    r = subprocess.run([MODEL, "--extended", "--depth", "4", "--jobs", "4"], capture_output=True, text=True,
+                       timeout=600)
+    m = re.search(r"\(extended\), depth 4, 22/23 symbols.* all (\d+) sequences of 1\.\.4 steps covered by (\d+) "
+                  r"distinct states .* (\d+) violation", r.stdout)
+    assert r.returncode == 0 and m, r.stdout[-3000:]
+    assert int(m.group(1)) == sum(22 ** i + 23 ** i for i in range(1, 5))
+    assert int(m.group(2)) > 10000 and int(m.group(3)) == 0, r.stdout
+
+
+@pytest.mark.parametrize("seq", [
+    # an unplaceable GPU_PRE_RESET holds both GPUs; the polled check returns them
+    "UNPLACED,POLL_OK,CLOCK_HOLD,POLL_OK",
+    # GPU 1 quarantined by its own resets while GPU 0 is untouched; the quiet window ends it
+    "PRE1,POST1,PRE1,POST1,CLOCK_HOLD,CLOCK_HOLD,CLOCK_HOLD",
+    # an ECC rise while the count could not be read is seen once it can
+    "ECC_UNREADABLE,ECC_UP,POLL_OK,ECC_UNREADABLE,POLL_OK",
+])
+def test_extended_replays(seq):
+    r = subprocess.run([MODEL, "--replay", seq], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.count(": ok") == 2, r.stdout + r.stderr
+
+
 # Found by the model check in round 6 (relay layout): a plugin container
 # restarted while its relay connection was down kept a relay cursor up to a
 # second old, and the relay's replay re-applied what had been handled:
