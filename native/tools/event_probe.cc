@@ -18,7 +18,15 @@
 // unprivileged client only the per-process events of its own process, so this
 // is how the decoding and the handle identity are seen on a box without root.
 //
+// --cycles N: first N generations of what a SIGHUP does to the daemon's
+// registration (EventsInit on every processor, then EventsStopAll), each
+// status recorded, before the registration that waits -- whether the real
+// library takes a registration again after a stop, in one process (review
+// item 3; the rollback itself is exercised on the mock, which can fail one
+// processor's init).
+//
 // usage: amdgpu-dp-event-probe [--lib <libamd_smi.so>] [--types 12,13] [--wait-ms 8000] [--self-hip]
+//                              [--cycles N]
 #include <dlfcn.h>
 #include <unistd.h>
 
@@ -38,7 +46,7 @@ using namespace adp;
 
 int main(int argc, char** argv) {
   std::string lib_path, types = "12,13";
-  int wait_ms = 8000;
+  int wait_ms = 8000, cycles = 0;
   bool self_hip = false;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--self-hip")) self_hip = true;
@@ -46,6 +54,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--lib")) lib_path = argv[++i];
     else if (!strcmp(argv[i], "--types")) types = argv[++i];
     else if (!strcmp(argv[i], "--wait-ms")) wait_ms = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--cycles")) cycles = atoi(argv[++i]);
   }
   auto extra = health::ParseEventTypes(types);
   if (!extra.ok()) {
@@ -66,6 +75,15 @@ int main(int argc, char** argv) {
   hc.extra_types = *extra;
   std::vector<void*> handles;
   for (const auto& p : *procs) handles.push_back(p.handle);
+  std::string gens;
+  for (int c = 0; c < cycles; ++c) {
+    Status st = (*lib)->EventsInit(handles, hc.EventMask());
+    const size_t live = (*lib)->EventsRegistered();
+    (*lib)->EventsStopAll();
+    gens += std::string(c ? ", " : "") + "{\"init\": \"" + JsonEscape(st.ok() ? "ok" : st.ToString()) +
+            "\", \"registered\": " + std::to_string(live) +
+            ", \"after_stop\": " + std::to_string((*lib)->EventsRegistered()) + "}";
+  }
   Status reg = (*lib)->EventsInit(handles, hc.EventMask());
   printf("%s\n", reg.ok() ? "registered" : "registration failed");
   fflush(stdout);
@@ -125,7 +143,8 @@ int main(int argc, char** argv) {
 
   std::string out = "{\"amdsmi\": \"" + (*lib)->Version() + "\", \"pid\": " + std::to_string(getpid()) +
                     ", \"self_hip\": " + hip + ", \"mask\": " + std::to_string(hc.EventMask()) +
-                    ", \"registration\": \"" + JsonEscape(reg.ok() ? "ok" : reg.ToString()) + "\", \"processors\": [";
+                    ", \"cycles\": [" + gens + "], \"registration\": \"" +
+                    JsonEscape(reg.ok() ? "ok" : reg.ToString()) + "\", \"processors\": [";
   for (size_t i = 0; i < procs->size(); ++i) {
     const auto& p = (*procs)[i];
     out += std::string(i ? ", " : "") + "{\"bdf\": \"" + p.bdf + "\", \"kfd_node\": " +

@@ -203,6 +203,36 @@ def test_event_registration_is_never_leaked_across_reloads(scratch, tmp_path, fa
     assert s["stops"] >= s["inits"], s
 
 
+@pytest.mark.parametrize("fail_on", [None, [1]])
+def test_event_probe_cycles_register_and_stop_everything(scratch, tmp_path, fail_on):
+    """amdgpu-dp-event-probe --cycles N (what the GPU test runs on the real
+    library): N generations of EventsInit + EventsStopAll, then the waiting
+    registration. On the mock each generation holds one registration per
+    processor and none after its stop; with GPU 1's init failing, none at all."""
+    from k8s_gpu_sharing_plugin_amd import binary
+    import json
+    fx = fixtures.node(2)
+    if fail_on:
+        fx["evt_init_fail_on"] = fail_on
+    evt = str(tmp_path / "evt")
+    env = dict(os.environ, AMD_SMI_LIB=MOCK_LIB, AMDSMI_MOCK_FIXTURE=fixtures.write(fx, scratch + ".fixture"),
+               AMDSMI_MOCK_EVT_FILE=evt)
+    r = subprocess.run([binary("amdgpu-dp-event-probe"), "--lib", MOCK_LIB, "--cycles", "3", "--wait-ms", "300"],
+                       capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(rec["cycles"]) == 3, rec
+    for c in rec["cycles"]:
+        assert c["after_stop"] == 0, rec
+        if fail_on:
+            assert c["init"] != "ok" and c["registered"] == 0, rec
+        else:
+            assert c["init"] == "ok" and c["registered"] == 2, rec
+    assert (rec["registration"] == "ok") == (not fail_on), rec
+    s = _evt(evt)
+    assert s["live"] == 0 and s["double_init"] == 0 and s["leaked_at_shutdown"] == 0, s
+
+
 def test_relay_never_leaks_a_registration_across_renewals(scratch, tmp_path):
     """The relay's renewals (a daemon with a different processor view, or
     events off) stop whatever the last one registered, complete or not."""

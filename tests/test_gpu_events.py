@@ -128,6 +128,28 @@ def test_raw_amdsmi_events_name_enumerated_processors(raw, real_snap):
     assert all(e["bdf"] == bdf and e["processor"] >= 0 for e in raw["events"]), raw
 
 
+def test_real_amdsmi_takes_a_registration_again_after_a_stop(raw_self, real_snap):
+    """Review item 3 on the real library: what a SIGHUP does to the daemon's
+    registration (EventsInit on every processor, then EventsStopAll), three
+    generations in one process, then the registration that waits -- each init
+    succeeds, each stop leaves none live, and the last registration still gets
+    the process's own PROCESS_START (the rollback of a partial registration is
+    exercised on the mock: a real GPU's init cannot be made to fail)."""
+    r = subprocess.run([EVENT_PROBE, "--types", TYPES, "--wait-ms", "4000", "--self-hip", "--cycles", "3"],
+                       capture_output=True, text=True, timeout=120)
+    lines = r.stdout.strip().splitlines()
+    rec = json.loads(lines[-1]) if lines and lines[-1].startswith("{") else {"error": r.stdout + r.stderr}
+    rec["rc"], rec["stderr"] = r.returncode, r.stderr[-2000:]
+    _record("raw_events_cycles.json", rec)
+    n = len(real_snap["gpus"])
+    assert rec["rc"] == 0 and len(rec["cycles"]) == 3, rec
+    assert all(c["init"] == "ok" and c["registered"] >= n and c["after_stop"] == 0 for c in rec["cycles"]), rec
+    assert rec["registration"] == "ok" and rec["unmatched"] == 0, rec
+    if raw_self.get("events_total", 0) == 0:
+        pytest.skip("no KFD event even about the registering process (raw_events_self.json)")
+    assert any(e["name"] == "PROCESS_START" for e in rec["events"]), rec
+
+
 def _wait_metric(port, name, labels, at_least=1, timeout=10.0):
     from test_metrics import _get, _parse
     deadline = time.monotonic() + timeout
