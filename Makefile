@@ -83,7 +83,7 @@ tsan:
 # the C API into Python are skipped: a TSan .so cannot be dlopen'ed there).
 tsan-e2e:
 	cmake -S native -B build/tsan -G Ninja -DCMAKE_BUILD_TYPE=RelWithDebInfo -DADP_TSAN=ON >/dev/null
-	ninja -C build/tsan -j$(JOBS) amdgpu-device-plugin amdgpu-dp-kubelet amdsmi_mock
+	ninja -C build/tsan -j$(JOBS) amdgpu-device-plugin amdgpu-dp-kubelet amdsmi_mock amdgpu-dp-event-probe
 	rm -rf build/tsan-logs && mkdir -p build/tsan-logs
 	ADP_BUILD_DIR=$(CURDIR)/build/tsan TSAN_OPTIONS=log_path=$(CURDIR)/build/tsan-logs/daemon \
 	  $(PY) -m pytest -q -p no:cacheprovider -m "not gpu" tests/test_e2e_mock.py tests/test_health.py \
@@ -117,7 +117,7 @@ fuzz:
 
 asan-e2e:
 	cmake -S native -B build/asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DADP_SANITIZE=ON >/dev/null
-	ninja -C build/asan -j$(JOBS) amdgpu-device-plugin amdgpu-dp-kubelet amdsmi_mock
+	ninja -C build/asan -j$(JOBS) amdgpu-device-plugin amdgpu-dp-kubelet amdsmi_mock amdgpu-dp-event-probe
 	rm -rf build/asan-logs && mkdir -p build/asan-logs
 	ADP_BUILD_DIR=$(CURDIR)/build/asan ASAN_OPTIONS=log_path=$(CURDIR)/build/asan-logs/daemon:detect_leaks=1:verify_asan_link_order=0 \
 	  UBSAN_OPTIONS=print_stacktrace=1:log_path=$(CURDIR)/build/asan-logs/ubsan \

@@ -195,6 +195,7 @@ class Builder {
             if (ek == k) {
               ev2 = std::move(val);  // last one wins, as in the JSON the reference builds
               replaced = true;
+              break;  // keys are unique in out->map
             }
           if (!replaced) out->map.emplace_back(std::move(k), std::move(val));
         }

@@ -56,7 +56,12 @@ int main(int argc, char** argv) {
        alloc::ReplicaPolicy::kPack, 1, true, true},
   };
   char scratch[] = "/tmp/adp-microbench-XXXXXX";
-  std::string usage_dir = std::string(mkdtemp(scratch)) + "/usage";
+  const char* root = mkdtemp(scratch);
+  if (!root) {
+    perror("mkdtemp");
+    return 2;
+  }
+  std::string usage_dir = std::string(root) + "/usage";
   printf("{");
   bool first = true;
   for (const auto& c : cases) {
