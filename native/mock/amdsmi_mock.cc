@@ -799,7 +799,7 @@ amdsmi_status_t amdsmi_get_gpu_event_notification(int timeout_ms, uint32_t* num,
       continue;
     }
     std::string msg;
-    std::getline(ls, msg);
+    std::getline(ls >> std::ws, msg);  // (the separator is not part of the message)
     if (target == "foreign") {  // a handle amdsmi never enumerated, while anything is registered
       bool any = false;
       for (auto& p : g->procs) any = any || p->evt_init;

@@ -362,6 +362,8 @@ Status Library::EventsInit(const std::vector<void*>& handles, uint64_t mask) {
                handles.size(), fresh.size());
     if (f_->evt_stop)
       for (void* r : fresh) f_->evt_stop(r);
+    else  // still registered: remembered, so the next call does not initialise them twice
+      evt_live_.insert(evt_live_.end(), fresh.begin(), fresh.end());
     return why;
   };
   for (size_t i = 0; i < handles.size(); ++i) {

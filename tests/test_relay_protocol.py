@@ -1,0 +1,236 @@
+"""The event relay's replay contract, spoken to the real relay by a raw client.
+
+A daemon that (re)connects sends "reinit fp=<fp> since=<relay>:<seq>:<gen>"
+with the cursor of the last event it handled. The relay (relay.cc Subscribe)
+replays every event it still holds after that cursor, then answers with a
+"hello v1 reinit ... gap=<0|1>": gap=0 only when nothing can have been missed --
+the same relay instance, the same registration generation, a cursor it has not
+passed beyond its ring (kRelayRingSize = 1024 events) and no event lost after
+it. The daemon-level tests (test_event_relay.py) and the model checker
+(native/tests/health_model.cc, whose relay is a model of Subscribe with a ring
+that never overflows) cover what the daemon does with the answer; these pin the
+relay's side of the wire exactly, fence posts included: ring overflow, a lost
+event, a cursor from another relay / generation / the future, a malformed or
+over-long request, an unplaceable event's line.
+
+Reference: the reference has no relay -- its plugin registers NVML events
+itself (/root/reference/cmd/nvidia-device-plugin/nvidia.go:181-269).
+"""
+
+import os
+import re
+import socket
+import time
+
+import pytest
+
+from k8s_gpu_sharing_plugin_amd.models import fixtures
+from k8s_gpu_sharing_plugin_amd.utils import harness
+
+RING = 1024  # kRelayRingSize (native/src/health/relay.h)
+HELLO = re.compile(r"hello v1 (reinit )?(events=\S+)(?: processors=(\d+))? relay=(\w+) gen=(\d+) seq=(\d+) fp=(\S+)"
+                   r" renew_ms=\d+(?: gap=(\d))?")
+EVENT = re.compile(r"event seq=(\d+) node=(\S+) bdf=(\S+) part=(\d+) type=(\d+) ?(.*)")
+
+
+class Relay:
+    """The relay alone (no daemon) on the mock, events injected through its FIFO."""
+
+    def __init__(self, scratch, env=None):
+        fdir = scratch + ".fixture"
+        os.makedirs(fdir, exist_ok=True)
+        self.fifo = os.path.join(fdir, "events")
+        os.mkfifo(self.fifo)
+        self.sock = os.path.join(fdir, "events.sock")
+        self.fx = dict(fixtures.node(2), events_open_kfd=True)
+        self.d = harness.Daemon(scratch, self.fx, args=["--event-relay", "--health-event-socket", self.sock],
+                                env=env, event_fifo=self.fifo).start()
+        self.d.wait_log("event notification registered on")
+        self.clients = []
+
+    def inject(self, lines):
+        fd = os.open(self.fifo, os.O_WRONLY | os.O_NONBLOCK)
+        try:
+            os.write(fd, "".join(ln + "\n" for ln in lines).encode())
+        finally:
+            os.close(fd)
+
+    def events(self, n, prefix="e"):
+        """n events (GPU 0 / GPU 1 alternating, a VM fault: no verdict anywhere),
+        in chunks the relay's pipes keep up with; waits until all are numbered."""
+        seq0, log0 = self.hello()["seq"], len(self.d.log())
+        for i in range(0, n, 100):
+            self.inject([f"{(i + j) % 2} 1 {prefix}{i + j}" for j in range(min(100, n - i))])
+            deadline = time.time() + 10
+            while self.hello()["seq"] < seq0 + min(n, i + 100):
+                assert time.time() < deadline, self.d.log()[-3000:]
+                time.sleep(0.02)
+        assert "lost after" not in self.d.log()[log0:]
+
+    def connect(self):
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.settimeout(10)
+        s.connect(self.sock)
+        self.clients.append(s)
+        return s, s.makefile("r", encoding="utf-8", newline="\n")
+
+    def hello(self):
+        """The greeting a fresh connection gets: relay id, generation, last seq."""
+        s, f = self.connect()
+        m = HELLO.fullmatch(f.readline().rstrip("\n"))
+        s.close()
+        self.clients.remove(s)
+        assert m and not m.group(1), m
+        return {"events": m.group(2), "relay": m.group(4), "gen": int(m.group(5)), "seq": int(m.group(6))}
+
+    def subscribe(self, since=None, raw=None):
+        """Sends a reinit; returns (replayed event lines, the reinit hello's
+        fields) -- everything up to and including the registrar's answer."""
+        s, f = self.connect()
+        greeting = f.readline()
+        g = HELLO.fullmatch(greeting.rstrip("\n"))
+        assert g, greeting
+        # The daemon's processor fingerprint, as it would send it (the
+        # registration's: no renewal, so the generation stays).
+        fp = g.group(7)
+        line = (raw if raw is not None else "reinit fp={fp}" + (f" since={since}" if since else "")).format(fp=fp)
+        s.sendall((line + "\n").encode())
+        replay = []
+        while True:
+            ln = f.readline().rstrip("\n")
+            assert ln, "connection closed before the reinit hello"
+            m = HELLO.fullmatch(ln)
+            if m and m.group(1):
+                return replay, {"events": m.group(2), "gen": int(m.group(5)), "seq": int(m.group(6)),
+                                "gap": int(m.group(8)) if m.group(8) is not None else None}
+            replay.append(ln)
+
+    def stop(self):
+        for s in self.clients:
+            s.close()
+        assert self.d.stop() == 0
+
+
+@pytest.fixture
+def relay(scratch):
+    r = Relay(scratch)
+    yield r
+    r.stop()
+
+
+def _seqs(lines):
+    out = []
+    for ln in lines:
+        m = EVENT.fullmatch(ln)
+        assert m, ln
+        out.append(int(m.group(1)))
+    return out
+
+
+def test_replay_is_exactly_what_follows_the_cursor(relay):
+    relay.events(5)
+    h = relay.hello()
+    assert h["seq"] == 5 and h["events"] == "events=ok"
+    cur = lambda seq, gen=h["gen"], rid=h["relay"]: f"{rid}:{seq}:{gen}"  # noqa: E731
+    for since, want in [(0, [1, 2, 3, 4, 5]), (2, [3, 4, 5]), (4, [5]), (5, [])]:
+        replay, r = relay.subscribe(cur(since))
+        assert _seqs(replay) == want and r["gap"] == 0 and r["seq"] == 5, (since, replay, r)
+    # every replayed line is the line a live subscriber got, byte for byte
+    s, f = relay.connect()
+    fp = HELLO.fullmatch(f.readline().rstrip("\n")).group(7)
+    s.sendall(f"reinit fp={fp}\n".encode())
+    while not f.readline().startswith("hello v1 reinit"):
+        pass
+    relay.events(2, prefix="live")
+    live = [f.readline().rstrip("\n") for _ in range(2)]
+    replay, r = relay.subscribe(cur(5))
+    assert replay == live and _seqs(live) == [6, 7] and r["gap"] == 0, (live, replay)
+    assert EVENT.fullmatch(live[0]).group(3) == relay.fx["gpus"][0]["bdf"]
+    assert EVENT.fullmatch(live[1]).group(3) == relay.fx["gpus"][1]["bdf"]
+
+
+def test_a_cursor_the_relay_cannot_vouch_for_is_a_gap(relay):
+    relay.events(3)
+    h = relay.hello()
+    other = "f" * len(h["relay"]) if h["relay"] != "f" * len(h["relay"]) else "e" * len(h["relay"])
+    cases = {
+        "no cursor (a new daemon)": (None, [], 1),
+        "another relay instance": (f"{other}:2:{h['gen']}", [], 1),
+        "another registration generation: replayed, yet a gap": (f"{h['relay']}:1:{h['gen'] + 1}", [2, 3], 1),
+        "a cursor from the future": (f"{h['relay']}:9:{h['gen']}", [], 1),
+    }
+    for what, (since, want, gap) in cases.items():
+        replay, r = relay.subscribe(since)
+        assert _seqs(replay) == want and r["gap"] == gap, (what, replay, r)
+
+
+@pytest.mark.parametrize("line", [
+    "reinit fp={fp} since=zz:1:1",   # relay id not hex
+    "reinit fp={fp} since=abc:x:1",  # seq not a number
+    "reinit fp={fp} since=abc:1",    # two fields
+    "reinit fp={fp} since=",         # empty
+])
+def test_a_malformed_cursor_is_no_cursor(relay, line):
+    relay.events(2)
+    replay, r = relay.subscribe(raw=line)
+    assert replay == [] and r["gap"] == 1, (line, replay, r)
+
+
+def test_an_overlong_request_closes_the_connection(relay):
+    s, f = relay.connect()
+    f.readline()
+    s.sendall(b"reinit " + b"x" * 5000)  # no newline, past the relay's 4096-byte bound
+    try:
+        assert f.readline() == ""  # closed, nothing more sent
+    except ConnectionResetError:  # closed with the request unread
+        pass
+    assert relay.hello()["events"] == "events=ok"  # the relay goes on
+
+
+def test_ring_overflow_fence_post(relay):
+    """The ring holds the last 1024 events: a cursor whose next event is still
+    held is replayed without a gap; one event further back is a gap (the
+    replay is still everything held)."""
+    n = RING + 6
+    relay.events(n)
+    h = relay.hello()
+    assert h["seq"] == n
+    first_held = n - RING + 1  # 7
+    for since, gap in [(first_held - 1, 0), (first_held - 2, 1), (0, 1), (n - 1, 0)]:
+        replay, r = relay.subscribe(f"{h['relay']}:{since}:{h['gen']}")
+        want = list(range(max(since, first_held - 1) + 1, n + 1))
+        assert _seqs(replay) == want and r["gap"] == gap, (since, len(replay), r)
+
+
+def test_an_event_the_relay_lost_is_a_gap_for_every_cursor_before_it(scratch):
+    """An event the relay could not number (its loop behind: here the test
+    hook refuses it) is in no stream and no replay: a cursor at or before the
+    loss is answered gap=1, a cursor past it gap=0."""
+    r = Relay(scratch, env={"ADP_DEBUG_RELAY_REFUSE_EVENT": "refuseme"})
+    try:
+        r.events(3)
+        r.inject(["0 1 refuseme"])
+        r.d.wait_log("lost after #3")
+        r.events(2)
+        h = r.hello()
+        assert h["seq"] == 5
+        for since, want, gap in [(2, [3, 4, 5], 1), (3, [4, 5], 1), (4, [5], 0), (5, [], 0)]:
+            replay, a = r.subscribe(f"{h['relay']}:{since}:{h['gen']}")
+            assert _seqs(replay) == want and a["gap"] == gap, (since, replay, a)
+    finally:
+        r.stop()
+
+
+def test_an_unplaceable_event_is_numbered_and_replayed_unplaced(relay):
+    relay.events(1)
+    relay.inject(["foreign 3 from nowhere"])
+    relay.d.wait_log("forwarded unplaced")
+    deadline = time.time() + 5
+    while relay.hello()["seq"] < 2:
+        assert time.time() < deadline
+        time.sleep(0.02)
+    h = relay.hello()
+    replay, r = relay.subscribe(f"{h['relay']}:1:{h['gen']}")
+    assert len(replay) == 1 and r["gap"] == 0, replay
+    m = EVENT.fullmatch(replay[0])
+    assert m.group(1, 2, 3, 5, 6) == ("2", "-", "-", "3", "from nowhere"), replay
