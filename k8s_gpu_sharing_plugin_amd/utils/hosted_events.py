@@ -27,7 +27,9 @@ from . import native
 
 
 def open_gpu() -> dict:
-    """hipInit, hipSetDevice(0), hipMalloc, hipDeviceSynchronize, hipFree in this process."""
+    """hipInit, hipSetDevice(0), hipMalloc, hipDeviceSynchronize, hipFree in this
+    process; `hipInit_wall` is hipInit's [start, end] on the wall clock the
+    daemon's and the relay's log lines carry (KFD's PROCESS_START comes from it)."""
     for name in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
         try:
             hip = ctypes.CDLL(name)
@@ -36,7 +38,9 @@ def open_gpu() -> dict:
             hip = None
     if hip is None:
         return {"error": "libamdhip64.so not found"}
+    t = time.time()
     out = {"hipInit": hip.hipInit(0)}
+    out["hipInit_wall"] = [t, time.time()]
     if out["hipInit"] == 0:
         out["hipSetDevice"] = hip.hipSetDevice(0)
         p = ctypes.c_void_p()

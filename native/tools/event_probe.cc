@@ -17,6 +17,10 @@
 // HIP (dlopen'ed libamdhip64: hipInit, hipMalloc, hipFree) -- KFD delivers an
 // unprivileged client only the per-process events of its own process, so this
 // is how the decoding and the handle identity are seen on a box without root.
+// The waits run on their own thread meanwhile, and every HIP step's start and
+// end are recorded on the events' clock (ms since registration): an event's
+// "ms" minus hipInit's start is KFD -> amdsmi -> this process's delivery
+// latency.
 //
 // --cycles N: first N generations of what a SIGHUP does to the daemon's
 // registration (EventsInit on every processor, then EventsStopAll), each
@@ -30,12 +34,14 @@
 #include <dlfcn.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common/strings.h"
@@ -88,10 +94,45 @@ int main(int argc, char** argv) {
   printf("%s\n", reg.ok() ? "registered" : "registration failed");
   fflush(stdout);
 
+  std::map<std::string, int> wait_status;  // status text -> waits
+  std::string events;
+  size_t n_events = 0, unmatched = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto elapsed = [&] {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+  };
+  auto elapsed_us = [&] {
+    return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+  };
+  // The waits, on their own thread (amdsmi's wait returns as soon as KFD
+  // queues an event), while the main thread opens the GPU.
+  std::thread waiter([&] {
+    while (reg.ok() && elapsed() < wait_ms) {
+      std::vector<smi::Event> got;
+      Status st = (*lib)->EventsWait(200, &got);
+      const long long at_us = elapsed_us();
+      ++wait_status[st.ok() ? (got.empty() ? "ok (no data)" : "ok") : st.ToString()];
+      for (const auto& e : got) {
+        int idx = -1;
+        for (size_t i = 0; i < procs->size(); ++i)
+          if ((*procs)[i].handle == e.handle) idx = static_cast<int>(i);
+        unmatched += idx < 0;
+        char head[200];
+        snprintf(head, sizeof(head),
+                 "{\"ms\": %lld, \"us\": %lld, \"type\": %u, \"name\": \"%s\", \"processor\": %d", at_us / 1000,
+                 at_us, e.type, smi::EventTypeName(e.type).c_str(), idx);
+        events += std::string(n_events++ ? ", " : "") + head + ", \"bdf\": \"" +
+                  (idx >= 0 ? (*procs)[idx].bdf : std::string("?")) + "\", \"message\": \"" + JsonEscape(e.message) +
+                  "\"}";
+      }
+    }
+  });
+
   // This process opens the GPU itself (KFD process creation, VM acquire,
   // a queue): what KFD reports to its own registration.
   std::string hip = "\"not asked\"";
   if (self_hip && reg.ok()) {
+    usleep(300000);  // the waiter is inside a wait by then
     void* dl = dlopen("libamdhip64.so", RTLD_NOW | RTLD_LOCAL);
     if (!dl) dl = dlopen("/opt/rocm/lib/libamdhip64.so", RTLD_NOW | RTLD_LOCAL);
     if (!dl) {
@@ -104,41 +145,29 @@ int main(int argc, char** argv) {
       auto sync = reinterpret_cast<int (*)()>(dlsym(dl, "hipDeviceSynchronize"));
       int a = -1, b = -1, c = -1, d = -1, e = -1;
       void* p = nullptr;
+      std::string steps;  // "name": [start_us, end_us] on the events' clock
+      auto timed = [&](const char* name, auto&& fn) {
+        const long long s0 = elapsed_us();
+        int rc = fn();
+        steps += std::string(steps.empty() ? "" : ", ") + "\"" + name + "\": [" + std::to_string(s0) + ", " +
+                 std::to_string(elapsed_us()) + "]";
+        return rc;
+      };
       if (init && set && alloc && free_ && sync) {  // each step only after the one before succeeded
-        if ((a = init(0)) == 0 && (b = set(0)) == 0 && (c = alloc(&p, 64 << 20)) == 0 && (d = sync()) == 0)
-          e = free_(p);
+        if ((a = timed("hipInit", [&] { return init(0); })) == 0 &&
+            (b = timed("hipSetDevice", [&] { return set(0); })) == 0 &&
+            (c = timed("hipMalloc", [&] { return alloc(&p, 64 << 20); })) == 0 &&
+            (d = timed("hipDeviceSynchronize", [&] { return sync(); })) == 0)
+          e = timed("hipFree", [&] { return free_(p); });
       }
       hip = "{\"pid\": " + std::to_string(getpid()) + ", \"hipInit\": " + std::to_string(a) +
             ", \"hipSetDevice\": " + std::to_string(b) + ", \"hipMalloc\": " + std::to_string(c) +
-            ", \"hipDeviceSynchronize\": " + std::to_string(d) + ", \"hipFree\": " + std::to_string(e) + "}";
+            ", \"hipDeviceSynchronize\": " + std::to_string(d) + ", \"hipFree\": " + std::to_string(e) +
+            ", \"steps_us\": {" + steps + "}}";
       // (not dlclose'd: the HIP runtime stays until exit)
     }
   }
-
-  std::map<std::string, int> wait_status;  // status text -> waits
-  std::string events;
-  size_t n_events = 0, unmatched = 0;
-  auto t0 = std::chrono::steady_clock::now();
-  auto elapsed = [&] {
-    return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
-  };
-  while (reg.ok() && elapsed() < wait_ms) {
-    std::vector<smi::Event> got;
-    Status st = (*lib)->EventsWait(200, &got);
-    ++wait_status[st.ok() ? (got.empty() ? "ok (no data)" : "ok") : st.ToString()];
-    for (const auto& e : got) {
-      int idx = -1;
-      for (size_t i = 0; i < procs->size(); ++i)
-        if ((*procs)[i].handle == e.handle) idx = static_cast<int>(i);
-      unmatched += idx < 0;
-      char head[160];
-      snprintf(head, sizeof(head), "{\"ms\": %lld, \"type\": %u, \"name\": \"%s\", \"processor\": %d",
-               static_cast<long long>(elapsed()), e.type, smi::EventTypeName(e.type).c_str(), idx);
-      events += std::string(n_events++ ? ", " : "") + head + ", \"bdf\": \"" +
-                (idx >= 0 ? (*procs)[idx].bdf : std::string("?")) + "\", \"message\": \"" + JsonEscape(e.message) +
-                "\"}";
-    }
-  }
+  waiter.join();
   (*lib)->EventsStop(handles);
 
   std::string out = "{\"amdsmi\": \"" + (*lib)->Version() + "\", \"pid\": " + std::to_string(getpid()) +

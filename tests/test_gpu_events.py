@@ -99,6 +99,16 @@ def raw_self():
     lines = r.stdout.strip().splitlines()
     rec = json.loads(lines[-1]) if lines and lines[-1].startswith("{") else {"error": r.stdout + r.stderr}
     rec["rc"], rec["first_line"], rec["stderr"] = r.returncode, lines[0] if lines else "", r.stderr[-2000:]
+    # Delivery latency: the process's PROCESS_START as amdsmi's wait returned
+    # it, after hipInit started (the waits run on their own thread meanwhile).
+    try:
+        t_init = rec["self_hip"]["steps_us"]["hipInit"]
+        starts = [e["us"] for e in rec["events"] if e["name"] == "PROCESS_START"]
+        if starts:
+            rec["process_start_latency_us"] = {"after_hipInit_start": starts[0] - t_init[0],
+                                               "after_hipInit_end": starts[0] - t_init[1]}
+    except (KeyError, TypeError):
+        pass
     _record("raw_events_self.json", rec)
     return rec
 
@@ -114,6 +124,15 @@ def test_raw_events_of_its_own_process_name_enumerated_processors(raw_self, real
         pytest.skip(f"no KFD event even about this process; waits: {raw_self['waits']}")
     bdf = real_snap["gpus"][0]["bdf"]
     assert all(e["bdf"] == bdf and e["processor"] >= 0 for e in raw_self["events"]), raw_self
+    lat = raw_self.get("process_start_latency_us")
+    if lat is not None:  # an event cannot precede what causes it
+        assert lat["after_hipInit_start"] >= 0, raw_self
+
+
+def _log_time(line):
+    """The wall-clock time of a daemon / relay log line ("2026-...Z ...")."""
+    from datetime import datetime, timezone
+    return datetime.strptime(line.split()[0], "%Y-%m-%dT%H:%M:%S.%fZ").replace(tzinfo=timezone.utc).timestamp()
 
 
 def test_raw_amdsmi_events_name_enumerated_processors(raw, real_snap):
@@ -172,11 +191,16 @@ def test_real_event_reaches_the_in_process_monitor(raw_self, real_snap):
     (amdgpu_dp_gpu_events_total's source) and changes no health."""
     if raw_self.get("events_total", 0) == 0:
         pytest.skip("no KFD event even about the registering process (raw_events_self.json)")
-    r = subprocess.run(HELPER + ["monitor"], capture_output=True, text=True, timeout=120)
+    r = subprocess.run(HELPER + ["monitor"], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, ADP_LOG_LEVEL="debug"))
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     rec = json.loads(lines[-1]) if lines else {"error": r.stdout[-2000:] + r.stderr[-2000:]}
     rec["rc"] = r.returncode
     rec["log"] = [ln for ln in r.stderr.splitlines() if "event" in ln or "health" in ln][-12:]
+    counted = [ln for ln in r.stderr.splitlines() if "event PROCESS_START(12) on GPU" in ln]
+    if counted and "hip" in rec and "hipInit_wall" in rec["hip"]:
+        # KFD -> amdsmi -> the monitor's handler, on the wall clock
+        rec["process_start_latency_ms"] = round((_log_time(counted[0]) - rec["hip"]["hipInit_wall"][0]) * 1e3, 3)
     _record("hosted_monitor_events.json", rec)
     bdf = real_snap["gpus"][0]["bdf"]
     assert r.returncode == 0 and rec["hip"]["hipInit"] == 0 and rec["hip"]["hipMalloc"] == 0, rec
@@ -208,7 +232,7 @@ def test_real_event_travels_through_the_relay_to_the_daemon(scratch, raw_self, r
     rec = {"bdf": g["bdf"], "kfd_node": part0.get("kfd_node")}
     try:
         assert helper.stdout.readline().strip() == "ready"
-        env = {"DP_HEALTH_POLL_MS": "200",
+        env = {"DP_HEALTH_POLL_MS": "200", "ADP_LOG_LEVEL": "debug",
                "LD_PRELOAD": " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), SIM) if x)}
         d = harness.Daemon(scratch, None, real_smi=True, env=env, args=[
             "--devices", "0", "--metrics-addr", "127.0.0.1:0", "--health-event-socket", sock,
@@ -250,6 +274,17 @@ def test_real_event_travels_through_the_relay_to_the_daemon(scratch, raw_self, r
         relay_log.close()
         rec["relay_event_lines"] = [ln for ln in open(tmp_path / "relay.log").read().splitlines()
                                     if "event seq=" in ln][-6:]
+        # KFD -> relay (its line numbered) -> daemon (counted), on the wall clock
+        try:
+            t0 = rec["hip"]["hipInit_wall"][0]
+            relay_t = next(_log_time(ln) for ln in rec["relay_event_lines"] if " type=12 " in ln)
+            daemon_t = next(_log_time(ln) for ln in (d.log().splitlines() if d else [])
+                            if "event PROCESS_START(12) on GPU" in ln)
+            rec["process_start_latency_ms"] = {"kfd_to_relay": round((relay_t - t0) * 1e3, 3),
+                                               "relay_to_daemon": round((daemon_t - relay_t) * 1e3, 3),
+                                               "total": round((daemon_t - t0) * 1e3, 3)}
+        except (KeyError, StopIteration, ValueError):
+            pass
         _record("relay_daemon_events.json", rec)
         if d:
             assert d.stop() == 0
