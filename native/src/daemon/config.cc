@@ -572,6 +572,26 @@ std::string Config::ToJson() const {
   return out + "\n  }\n}";
 }
 
+std::vector<FlagInfo> FlagTable() {
+  std::vector<FlagInfo> out;
+  for (const auto& d : Table()) {
+    FlagInfo fi;
+    fi.name = d.name;
+    fi.env = d.env;
+    fi.file_key = d.file_key;
+    fi.kind = d.kind == Kind::kBool ? 'b' : d.kind == Kind::kUint ? 'u' : 's';
+    fi.allow_zero = d.allow_zero;
+    for (const auto& a : Aliases())
+      if (fi.name == a.canonical) {
+        fi.alias_name = a.name;
+        fi.alias_env = a.env;
+        fi.alias_file_key = a.file_key;
+      }
+    out.push_back(std::move(fi));
+  }
+  return out;
+}
+
 std::string UsageText() {
   std::string s =
       "amdgpu-device-plugin: Kubernetes device plugin for AMD Instinct MI355X GPUs\n\n"

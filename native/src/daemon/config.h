@@ -121,4 +121,16 @@ Result<ConfigFile> ParseConfigFile(const std::string& body);
 
 std::string UsageText();
 
+// Every setting and where it can come from (tests, docs): its command-line
+// name, environment variable and config-file key ("" = none), its type
+// ('s' string, 'b' bool, 'u' unsigned; `allow_zero`: 0 is a value), and the
+// compatibility alias of each kind, if any.
+struct FlagInfo {
+  std::string name, env, file_key;
+  char kind = 's';
+  bool allow_zero = false;
+  std::string alias_name, alias_env, alias_file_key;
+};
+std::vector<FlagInfo> FlagTable();
+
 }  // namespace adp::daemon

@@ -9,6 +9,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <atomic>
 #include <cstdio>
@@ -21,6 +22,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <json.hpp>
 
 #include "alloc/replicas.h"
 #include "alloc/topology.h"
@@ -759,6 +762,102 @@ static void TestConfig() {
   CHECK(!daemon::LoadConfig(2, bad, &env).ok());
 }
 
+// Precedence, property-tested over every setting: each one randomly given on
+// the command line, in the environment and in the config file, each by its
+// canonical name and by its compatibility alias where it has one; the value
+// that wins is the highest source's -- command line > environment > file >
+// default, the canonical name before the alias at each level (config.cc
+// LoadConfig; the reference's order, main.go:62-130 + config.go:30-144, with
+// its quirk fixed: a `false` in the file turns a default-on flag off).
+static void TestConfigPrecedenceProperty() {
+  g_case = "config precedence";
+  const std::vector<daemon::FlagInfo> flags = daemon::FlagTable();
+  CHECK(flags.size() > 50);
+  std::mt19937_64 rng(20261018);
+  char path[] = "/tmp/adp-precedence-XXXXXX";
+  int fd = mkstemp(path);
+  CHECK(fd >= 0);
+  if (fd < 0) return;
+  close(fd);
+  const daemon::Config defaults;
+  const nlohmann::json dflt = nlohmann::json::parse(defaults.ToJson())["flags"];
+  int from_level[7] = {0};
+  for (int trial = 0; trial < 300; ++trial) {
+    std::vector<std::string> args = {"x", "--config-file", path};
+    std::map<std::string, std::string> env;
+    std::string file = "version: v1\nflags:\n";
+    std::vector<nlohmann::json> want(flags.size());
+    std::vector<int> won(flags.size(), 6);
+    for (size_t i = 0; i < flags.size(); ++i) {
+      const daemon::FlagInfo& f = flags[i];
+      const std::string names[6] = {f.name, f.alias_name, f.env, f.alias_env, f.file_key, f.alias_file_key};
+      const std::string key = f.file_key.empty() ? f.name : f.file_key;
+      want[i] = dflt[key];
+      for (int src = 0; src < 6; ++src) {
+        if (names[src].empty() || rng() % 3 != 0) continue;
+        // A value of the setting's type: JSON (what ToJson shows) + its text.
+        nlohmann::json v;
+        std::string text;
+        if (f.kind == 'b') {
+          v = static_cast<bool>(rng() % 2);
+          text = v.get<bool>() ? "true" : "false";
+        } else if (f.kind == 'u') {
+          uint64_t n = (f.allow_zero ? 0 : 1) + rng() % 5000;
+          v = n;
+          text = std::to_string(n);
+        } else {
+          text = rng() % 4 == 0 ? std::to_string(1000 + rng() % 9000)  // a number where a string belongs
+                                : "v" + std::to_string(trial) + "-" + std::to_string(i) + "-" + std::to_string(src);
+          v = text;
+        }
+        if (src <= 1) {
+          if (f.kind == 'b' && text == "true" && rng() % 2) args.push_back("--" + names[src]);  // bare bool
+          else if (rng() % 2) args.push_back("--" + names[src] + "=" + text);
+          else if (f.kind != 'b') args.insert(args.end(), {"--" + names[src], text});
+          else args.push_back("--" + names[src] + "=" + text);
+        } else if (src <= 3) {
+          env[names[src]] = text;
+        } else {
+          // Plain or quoted: a quoted "true" / "12" is accepted for a bool / integer too.
+          const bool quote = f.kind == 's' ? !std::all_of(text.begin(), text.end(), ::isdigit) || rng() % 2
+                                           : rng() % 3 == 0;
+          file += "  " + names[src] + ": " + (quote ? "'" + text + "'" : text) + "\n";
+        }
+        if (src < won[i]) {
+          won[i] = src;
+          want[i] = v;
+        }
+      }
+    }
+    FILE* out = fopen(path, "w");
+    CHECK(out != nullptr);
+    if (!out) break;
+    fputs(file.c_str(), out);
+    fclose(out);
+    std::vector<const char*> argv;
+    for (const auto& a : args) argv.push_back(a.c_str());
+    auto c = daemon::LoadConfig(static_cast<int>(argv.size()), argv.data(), &env);
+    CHECK(c.ok());
+    if (!c.ok()) {
+      fprintf(stderr, "trial %d: %s\n", trial, c.status().ToString().c_str());
+      continue;
+    }
+    const nlohmann::json got = nlohmann::json::parse(c->ToJson())["flags"];
+    for (size_t i = 0; i < flags.size(); ++i) {
+      const std::string key = flags[i].file_key.empty() ? flags[i].name : flags[i].file_key;
+      ++from_level[won[i]];
+      if (got[key] != want[i]) {
+        CHECK(got[key] == want[i]);
+        fprintf(stderr, "trial %d: %s = %s, want %s (from source %d)\n", trial, key.c_str(), got[key].dump().c_str(),
+                want[i].dump().c_str(), won[i]);
+      }
+    }
+  }
+  unlink(path);
+  // Every level decided some settings (the aliases are few: fewer wins there).
+  for (int l = 0; l < 7; ++l) CHECK(from_level[l] > 0);
+}
+
 static void TestGrpcLoopback(bool native_http2) {
   g_case = native_http2 ? "grpc" : "grpc/nghttp2";
   std::string dir = "/tmp/adp-unit-" + std::to_string(getpid());
@@ -1431,6 +1530,7 @@ int main() {
   TestTopology();
   TestHierarchicalMatchesOracle();
   TestConfig();
+  TestConfigPrecedenceProperty();
   TestGrpcLoopback(true);
   TestGrpcLoopback(false);
   TestH2Fuzz();
