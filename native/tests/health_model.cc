@@ -1141,7 +1141,11 @@ int main(int argc, char** argv) {
                               "drain", "drain.return", "drain.return.taken", "relay.sock"})
           unlink((wdir + "/" + f).c_str());
         rmdir(wdir.c_str());
+#ifdef ADP_COVERAGE
+        exit(0);  // gcov writes this worker's counts at exit
+#else
         _exit(0);
+#endif
       }
       if (pid > 0) kids.push_back(pid);
     }

@@ -3,8 +3,8 @@ end-to-end pytest suites (the reference's `make coverage` = go test -coverprofil
 
   python tools/coverage.py [--build build/cov] [--out coverage.txt]
 
-Builds an --coverage tree, runs adp_unit_tests, adp_stress and the CPU pytest
-suites against it (ADP_BUILD_DIR), then runs gcov on every object of adp_core
+Builds an --coverage tree, runs adp_unit_tests, adp_stress, the health model
+check (extended alphabet, depth 4) and the CPU pytest suites against it (ADP_BUILD_DIR), then runs gcov on every object of adp_core
 and prints per-file and total line coverage of native/src.
 """
 import argparse
@@ -38,6 +38,9 @@ def main():
             os.unlink(gcda)
         run([os.path.join(b, "adp_unit_tests")], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         run([os.path.join(b, "adp_stress")], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        # the health model check (its workers are forked: their counts merge into the same .gcda files)
+        run([os.path.join(b, "adp_health_model"), "--extended", "--depth", "4", "--jobs", "4"],
+            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         env = dict(os.environ, ADP_BUILD_DIR=b)
         subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "not gpu", "-p", "no:cacheprovider",
                         os.path.join(ROOT, "tests")], cwd=ROOT, env=env, check=True)
