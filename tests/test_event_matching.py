@@ -164,6 +164,30 @@ def test_relay_event_on_a_gpu_this_daemon_does_not_serve_is_not_unmatched(scratc
         n.stop()
 
 
+def test_relay_event_on_a_processor_the_daemon_does_not_know_is_unmatched(scratch):
+    """The relay places an event (KFD node, PCI address) on a GPU that is in no
+    enumeration of the daemon's (here the relay sees a third GPU): the daemon
+    cannot place it -- an ERROR and a counter, and a GPU_PRE_RESET holds every
+    GPU it serves until the polled check, as for an unplaceable one."""
+    n = RelayNode(scratch, relay_gpus=3, daemon_args=["--reset-recovery-hold-ms", "600"])
+    try:
+        n.d.wait_log("events on through the relay")
+        third = fixtures.node(3)["gpus"][2]["bdf"]
+        n.inject("2 3 reset of a GPU only the relay knows")
+        deadline = time.monotonic() + 10
+        h = n.health()
+        while h != ["Unhealthy", "Unhealthy"]:
+            h = n.health(max(0.05, deadline - time.monotonic()))
+        log = n.d.wait_log("GPU_PRE_RESET(3) on a processor that matches no GPU of this node")
+        assert "the relay's processor (node " in log and f"{third} partition 0) is none of this daemon's" in log
+        assert _samples(n.port, "amdgpu_dp_unmatched_events_total") == {(("type", "GPU_PRE_RESET"),): 1}
+        deadline = time.monotonic() + 10
+        while h != ["Healthy", "Healthy"]:  # no GPU_POST_RESET can be placed: the polled check
+            h = n.health(max(0.05, deadline - time.monotonic()))
+    finally:
+        n.stop()
+
+
 def _evt(path):
     text = open(path).read() if os.path.exists(path) else ""
     return {k: int(v) for k, v in re.findall(r"(\w+)=(\d+)", text)}

@@ -32,7 +32,7 @@ def _preload(*libs):
 
 
 class RelayNode:
-    def __init__(self, scratch, relay_env=None, daemon_args=(), daemon_env=None, relay_launch=None):
+    def __init__(self, scratch, relay_env=None, daemon_args=(), daemon_env=None, relay_launch=None, relay_gpus=None):
         self.scratch = scratch
         self.relay_launch = relay_launch  # argv -> argv for the relay process (e.g. another build's binary)
         self.fifo = os.path.join(scratch + ".fixture", "events")
@@ -40,6 +40,8 @@ class RelayNode:
         os.mkfifo(self.fifo)
         self.sock = os.path.join(scratch + ".fixture", "events.sock")
         self.fx = dict(fixtures.node(2), events_open_kfd=True)
+        # The relay may see more GPUs than the daemon does (their views disagree).
+        self.relay_fx = dict(fixtures.node(relay_gpus), events_open_kfd=True) if relay_gpus else self.fx
         self.relay_env = relay_env
         self.relay = None
         self.start_relay()
@@ -58,7 +60,7 @@ class RelayNode:
         n = 0 if self.relay is None else len(self.relay.log()) + 1
         rdir = self.scratch + f"-relay{n}"
         os.makedirs(rdir, exist_ok=True)
-        self.relay = harness.Daemon(rdir, self.fx, args=["--event-relay", "--health-event-socket", self.sock],
+        self.relay = harness.Daemon(rdir, self.relay_fx, args=["--event-relay", "--health-event-socket", self.sock],
                                     env=self.relay_env, event_fifo=self.fifo, launch=self.relay_launch).start()
         self.relay.wait_log("relaying amdsmi events on")
 

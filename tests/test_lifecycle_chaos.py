@@ -1,0 +1,196 @@
+"""Seeded random lifecycles: everything that restarts or re-registers the
+plugins, interleaved, against one running daemon.
+
+Each step is one of: SIGHUP, or three at once; the kubelet restarting (its
+socket re-created), or going away for a few steps; the plugin's own socket
+deleted; a config-file edit (resource renamed and/or replica count changed,
+applied live), or a broken one (ignored: the running config stays, across a
+SIGHUP too); GPU 1 drained or undrained by the operator's drain file; SIGUSR1.
+After every step (the kubelet's absence aside) the daemon must come back
+to the expected state on its own: registered with the current kubelet for the
+expected resource, and that resource's ListAndWatch listing 2 GPUs x R
+replicas with exactly GPU 1's replicas Unhealthy while it is drained. At the
+end its descriptors and threads are where they started and SIGTERM exits 0
+with its sockets removed. The single triggers are pinned one by one in
+test_lifecycle.py; this is their interleavings (the reference restarts on
+kubelet.sock re-creation and SIGHUP only: main.go:283-326).
+"""
+
+import os
+import queue
+import random
+import signal
+import time
+
+import pytest
+
+from k8s_gpu_sharing_plugin_amd.models import fixtures
+from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
+
+SEEDS = [int(s) for s in os.environ.get("ADP_LIFECYCLE_SEEDS", "1,2,3").split(",")]
+STEPS = int(os.environ.get("ADP_LIFECYCLE_STEPS", "12"))
+
+
+def _count(pid, what):
+    if what == "fds":
+        return len(os.listdir(f"/proc/{pid}/fd"))
+    return len(os.listdir(f"/proc/{pid}/task"))
+
+
+class Life:
+    def __init__(self, scratch, tmp_path):
+        self.scratch = scratch
+        self.ksock = os.path.join(scratch, "kubelet.sock")
+        self.fx = fixtures.node(2)
+        self.cfg = str(tmp_path / "config.yaml")
+        self.drain = str(tmp_path / "drain")
+        self.replicas, self.name, self.drained = 2, "sharedgpu", False
+        self.write_config()
+        self.k = kubelet.StubKubelet(self.ksock).start()
+        self.d = harness.Daemon(scratch, self.fx, args=["--config-file", self.cfg, "--drain-file", self.drain],
+                                env={"DP_HEALTH_POLL_MS": "100"}).start()
+        self.reg = None
+        self.history = []
+        self.kubelet_down = False
+
+    def write_config(self):
+        tmp = self.cfg + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(f"version: v1\nflags:\n  resourceConfig: gpu:{self.name}:{self.replicas}\n")
+        os.rename(tmp, self.cfg)
+
+    def step(self, rnd):
+        what = rnd.choice(["sighup", "storm", "kubelet", "kubelet-away", "socket", "config", "config", "broken",
+                           "drain", "usr1"])
+        if self.kubelet_down and what in ("kubelet", "kubelet-away"):
+            what = "kubelet-back"
+        if what == "sighup":
+            self.d.signal(signal.SIGHUP)
+        elif what == "storm":
+            for _ in range(3):
+                self.d.signal(signal.SIGHUP)
+        elif what == "kubelet-away":
+            self.k.stop()
+            if os.path.exists(self.ksock):
+                os.unlink(self.ksock)
+            self.kubelet_down = True
+            self.reg = None
+        elif what == "kubelet-back":
+            self.k = kubelet.StubKubelet(self.ksock).start()
+            self.kubelet_down = False
+            self.reg = None
+        elif what == "usr1":
+            self.d.signal(signal.SIGUSR1)
+        elif what == "broken":
+            # A valid edit replaced at once by a broken one may never be read
+            # (then the daemon rightly keeps what it ran): the valid one is
+            # let settle first.
+            if self.history and self.history[-1].startswith("config"):
+                self.settle()
+            with open(self.cfg + ".tmp", "w") as f:
+                f.write("version: v2\n")
+            os.rename(self.cfg + ".tmp", self.cfg)
+        elif what == "kubelet":
+            self.k.stop()
+            if os.path.exists(self.ksock):
+                os.unlink(self.ksock)
+            self.k = kubelet.StubKubelet(self.ksock).start()
+            self.reg = None  # the new kubelet knows no plugin yet
+        elif what == "socket":
+            if self.reg is not None:
+                try:
+                    os.unlink(os.path.join(self.scratch, self.reg.endpoint))
+                except FileNotFoundError:
+                    pass
+        elif what == "config":
+            self.replicas = rnd.choice([1, 2, 3])
+            self.name = rnd.choice(["sharedgpu", "timeshared"])
+            self.write_config()
+            what += f" gpu:{self.name}:{self.replicas}"
+        elif what == "drain":
+            self.drained = not self.drained
+            with open(self.drain + ".tmp", "w") as f:
+                f.write(f"{self.fx['gpus'][1]['bdf']}\n" if self.drained else "# none\n")
+            os.rename(self.drain + ".tmp", self.drain)
+            what += " on" if self.drained else " off"
+        self.history.append(what)
+
+    def step_kubelet_back(self):
+        self.k = kubelet.StubKubelet(self.ksock).start()
+        self.kubelet_down = False
+        self.reg = None
+        self.history.append("kubelet-back")
+
+    def settle(self, timeout=20.0):
+        """Until the kubelet's latest registration is the expected resource and
+        its ListAndWatch shows the expected devices and health."""
+        if self.kubelet_down:  # nothing to register with: alive, that is all
+            time.sleep(0.3)
+            assert self.d.proc.poll() is None, (self.history, self.d.log()[-4000:])
+            return
+        want_name = f"amd.com/{self.name}"
+        want = (2 * self.replicas, self.replicas if self.drained else 0)
+        deadline = time.monotonic() + timeout
+        seen = None
+        while True:
+            assert self.d.proc.poll() is None, (self.history, self.d.log()[-4000:])
+            try:
+                while True:
+                    self.reg = self.k.registrations.get_nowait()
+            except queue.Empty:
+                pass
+            if self.reg is not None and self.reg.resource_name == want_name:
+                c = kubelet.PluginClient(os.path.join(self.scratch, self.reg.endpoint))
+                try:
+                    q, call = c.watch()
+                    first = q.get(timeout=2)
+                    call.cancel()
+                    if hasattr(first, "devices"):
+                        # ... and no other resource's socket left behind (a renamed one is gone)
+                        socks = sorted(e for e in os.listdir(self.scratch)
+                                       if e.endswith(".sock") and e != "kubelet.sock")
+                        seen = (len(first.devices), sum(x.health != "Healthy" for x in first.devices), socks)
+                        if seen == want + ([self.reg.endpoint],):
+                            return
+                    else:  # the endpoint is being restarted: the call failed
+                        seen = repr(first)[:200]
+                except queue.Empty:
+                    seen = "no ListAndWatch answer"
+                finally:
+                    c.close()
+            else:
+                seen = self.reg.resource_name if self.reg is not None else "no registration"
+            assert time.monotonic() < deadline, (self.history, want_name, want, seen, self.d.log()[-4000:])
+            time.sleep(0.1)
+
+    def close(self):
+        rc = self.d.stop()
+        if not self.kubelet_down:
+            self.k.stop()
+        return rc
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_interleaved_restarts_reloads_and_drains_settle(scratch, tmp_path, seed):
+    rnd = random.Random(seed)
+    life = Life(scratch, tmp_path)
+    try:
+        life.settle()
+        pid = life.d.proc.pid
+        fds0, threads0 = _count(pid, "fds"), _count(pid, "threads")
+        for _ in range(STEPS):
+            life.step(rnd)
+            if rnd.random() < 0.3:  # sometimes a second trigger before the first settled
+                life.step(rnd)
+            life.settle()
+        if life.kubelet_down:
+            life.step_kubelet_back()
+            life.settle()
+        fds, threads = _count(pid, "fds"), _count(pid, "threads")
+        # (a restart may be mid-way: a few descriptors of slack, none per step)
+        assert fds <= fds0 + 6 and threads <= threads0 + 2, (fds0, fds, threads0, threads, life.history)
+        endpoints = [e for e in os.listdir(scratch) if e.endswith(".sock") and e != "kubelet.sock"]
+    finally:
+        rc = life.close()
+    assert rc == 0, life.d.log()[-3000:]
+    assert all(not os.path.exists(os.path.join(scratch, e)) for e in endpoints), endpoints
