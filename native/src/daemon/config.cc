@@ -202,8 +202,9 @@ const std::vector<FlagDef>& Table() {
        "poll for this long with no new GPU_PRE_RESET (0 = only the event brings it back)",
        [](Flags& f) -> void* { return &f.reset_recovery_hold_ms; }, true},
       {"reset-flap-limit", "DP_RESET_FLAP_LIMIT", "resetFlapLimit", Kind::kUint,
-       "a GPU that sees this many GPU_PRE_RESETs within --reset-flap-window-ms is kept Unhealthy (cause "
-       "\"flapping\"), its GPU_POST_RESETs notwithstanding, until a whole window passes without one (0 = off)",
+       "a GPU that resets this many times within --reset-flap-window-ms is kept Unhealthy (cause "
+       "\"flapping\"), its GPU_POST_RESETs notwithstanding, until a whole window passes without a reset (0 = off; "
+       "a reset counts once, however many partitions report its GPU_PRE_RESET)",
        [](Flags& f) -> void* { return &f.reset_flap_limit; }, true},
       {"defer-layout-changes", "DP_DEFER_LAYOUT_CHANGES", "deferLayoutChanges", Kind::kBool,
        "a live config change (config file, SIGHUP) that would change what a replicated resource's IDs mean "

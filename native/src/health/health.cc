@@ -804,11 +804,17 @@ void Monitor::HandleEvent(const smi::Event& e, const std::string& unplaced, cons
     Update(gpu, 0, ~static_cast<uint32_t>(kFailDrained | kFailFlapping), why);
     ledger_->ClearGap(keys_[gpu]);
   } else {
+    // KFD reports a reset on every KFD node of the GPU -- each compute
+    // partition (DPX/QPX/CPX) -- so one reset is a GPU_PRE_RESET per partition,
+    // then a GPU_POST_RESET per partition. Only the first, the one that finds
+    // the GPU not waiting yet, starts a reset; the others belong to it.
+    const bool same_reset = e.type == smi::kEvtGpuPreReset && (fail_[gpu] & kFailResetPending);
     Update(gpu, e.type == smi::kEvtGpuPreReset ? kFailResetPending : kFailEvent, 0, why);
     if (e.type == smi::kEvtGpuPreReset) {
-      // A new reset: only a gap after it lets polling end the wait.
+      // Only a gap after it lets polling end the wait (the GPU_POST_RESETs come
+      // after every partition's GPU_PRE_RESET: one seen now is not missed yet).
       ledger_->ClearGap(keys_[gpu]);
-      if (cfg_.reset_flap_limit > 0) {
+      if (cfg_.reset_flap_limit > 0 && !same_reset) {
         int n = ledger_->RecordReset(keys_[gpu], clock_->WallMs(), cfg_.reset_flap_window_ms, event_id);
         if (n >= cfg_.reset_flap_limit && !(fail_[gpu] & kFailFlapping)) {
           std::string w = std::to_string(cfg_.reset_flap_window_ms / 1000);

@@ -59,11 +59,15 @@
 //       (--extended: it may wait for its own GPU_POST_RESET and be quarantined);
 //   I7  (per GPU) a reset-flap quarantine begins only with a delivered GPU_PRE_RESET and
 //       ends only after a quiet window (or the operator), and does end then;
-//   I8  (per GPU) the reset history never counts more resets than distinct
-//       GPU_PRE_RESETs were delivered (relay replays counted once);
+//   I8  (per GPU) the reset history never counts more resets than were
+//       delivered: a GPU_PRE_RESET that finds the GPU already waiting is the
+//       same reset (every partition of a GPU reports it), and a relay replay
+//       counts once;
 //   I9  the ECC verdict = the count rose above the baseline of the first
 //       observation / the last completed reset / counter reset / operator,
-//       whenever the count could be read.
+//       whenever the count could be read;
+//   I10 (per GPU) a new reset that makes --reset-flap-limit resets within the
+//       window quarantines the GPU.
 // States are deduplicated by a canonical hash (times relative to the clock,
 // clamped past every threshold), so each distinct state is expanded once per
 // remaining depth: every sequence up to --depth is covered. Each node is
@@ -351,7 +355,11 @@ struct Model {
   bool pending[2] = {false, false};      // a delivered GPU_PRE_RESET awaits its GPU_POST_RESET
   bool gap_since_pre[2] = {false, false};  // the monitor recorded a confirmed gap since it
   bool drained = false;
-  std::set<std::string> pre_ids[2];      // distinct GPU_PRE_RESETs delivered since the operator's last return
+  // Resets since the operator's last return: the GPU_PRE_RESETs that found the
+  // GPU not waiting (on a partitioned GPU every partition reports the same
+  // reset: one per KFD node), with the time each was delivered.
+  std::set<std::string> pre_ids[2];
+  std::vector<int64_t> pre_times[2];
   bool has_baseline = false;
   uint64_t baseline = 0, seen = 0;       // GPU 0's ECC reference
 };
@@ -561,6 +569,7 @@ class World {
              rels(m.responsive_since_ms);
       k += std::string("|h") + (healthy_[g] ? "1" : "0");
       k += std::string("|m") + (model_.pending[g] ? "P" : "p") + (model_.gap_since_pre[g] ? "G" : "g");
+      for (int64_t t : model_.pre_times[g]) k += "," + std::to_string(std::min<int64_t>(clock_.wall - t, kWindowMs));
     }
     k += "|smi:" + std::to_string(smi_.gpu[0].alive) + "/" + std::to_string(smi_.gpu[0].ecc) + "/" +
          std::to_string(smi_.ecc_ok) + "/" + std::to_string(smi_.waits_failing) + "/r" +
@@ -781,10 +790,13 @@ class World {
       // A replayed event the daemon already handled is no new reset.
       if (replayed_.count(id)) return;
       replayed_.insert(id);
-      ++pres_delivered_[g];
+      if (!model_.pending[g]) {  // a new reset (not another partition's report of the one pending)
+        ++pres_delivered_[g];
+        model_.pre_ids[g].insert(id);
+        model_.pre_times[g].push_back(clock_.wall);
+      }
       model_.pending[g] = true;
       model_.gap_since_pre[g] = false;
-      model_.pre_ids[g].insert(id);
     } else if (type == 4) {
       if (replayed_.count(id)) return;
       replayed_.insert(id);
@@ -811,6 +823,7 @@ class World {
     if (sym == A_RETURN) {
       for (int g = 0; g < 1; ++g) model_.pending[g] = model_.gap_since_pre[g] = false;
       model_.pre_ids[0].clear();
+      model_.pre_times[0].clear();
       if (smi_.gpu[0].alive && smi_.ecc_ok) {
         model_.has_baseline = true;
         model_.baseline = model_.seen = smi_.gpu[0].ecc;
@@ -909,7 +922,17 @@ class World {
       // I8
       if (now.size() > model_.pre_ids[g].size())
         fail("I8: GPU " + std::to_string(g) + " " + std::to_string(now.size()) + " resets recorded for " +
-             std::to_string(model_.pre_ids[g].size()) + " distinct GPU_PRE_RESETs");
+             std::to_string(model_.pre_ids[g].size()) + " resets delivered");
+      // I10: a new reset that makes --reset-flap-limit resets within the window
+      // quarantines the GPU (counted with a step's worth of slack: the monitor
+      // timestamps an event when it handles it, within the step).
+      if (pres_delivered_[g] > 0) {
+        int recent = 0;
+        for (int64_t t : model_.pre_times[g]) recent += clock_.wall - t < kWindowMs - kHoldMs - 100;
+        if (recent >= kFlapLimit && !flap)
+          fail("I10: GPU " + std::to_string(g) + " had " + std::to_string(recent) +
+               " resets within the window and is not quarantined");
+      }
     }
     // I9 (after a poll that read the count)
     if (polled && smi_.gpu[0].alive && smi_.ecc_ok && model_.has_baseline &&

@@ -188,6 +188,52 @@ def test_relay_event_on_a_processor_the_daemon_does_not_know_is_unmatched(scratc
         n.stop()
 
 
+@pytest.mark.parametrize("layout", ["in-process", "relay"])
+def test_one_reset_of_a_partitioned_gpu_is_one_reset(scratch, layout):
+    """KFD reports a GPU reset on every KFD node of the GPU: on a CPX MI355X
+    that is 8 GPU_PRE_RESETs, then 8 GPU_POST_RESETs, for one reset. Counted
+    per event, one reset quarantined the GPU for a whole flap window (found by
+    the health model check once its I8 counted resets, not events). It is one
+    reset: the GPU is back after its POST_RESETs, and it takes
+    --reset-flap-limit such resets to quarantine it."""
+    cpx = fixtures.node(2, modes="CPX")
+    args = ["--partition-strategy", "single", "--reset-flap-limit", "2", "--metrics-addr", "127.0.0.1:0"]
+    if layout == "relay":
+        n = RelayNode(scratch, fx=cpx, daemon_args=args)
+        n.d.wait_log("events on through the relay")
+        q, stop = n.q, n.stop
+    else:
+        n = Node(scratch, cpx, args=args, env={"DP_HEALTH_POLL_MS": "100"})
+        q, stop = n.q, n.close
+
+    def unhealthy(timeout=5):
+        return sum(d.health != "Healthy" for d in q.get(timeout=timeout).devices)
+    try:
+        for rnd in range(2):
+            for p in range(8):
+                n.inject(f"0:{p} 3 reset {rnd} pre on partition {p}")
+            while unhealthy() != 8:
+                pass
+            for p in range(8):
+                n.inject(f"0:{p} 4 reset {rnd} post on partition {p}")
+            if rnd == 0:
+                while unhealthy() != 0:  # one reset: back in service
+                    pass
+                assert "quarantined" not in n.d.log()
+        # the second reset reaches --reset-flap-limit 2: its POST_RESETs do not bring it back
+        assert "GPU 0000:0c:00.0 reset 2 times within" in n.d.wait_log("reset 2 times within")
+        n.d.wait_log("reset 1 post on partition 7")
+        time.sleep(0.3)
+        last = None
+        while not q.empty():
+            last = q.get_nowait()
+        assert last is None or sum(d.health != "Healthy" for d in last.devices) == 8
+        assert _samples(n.port if layout == "relay" else _port(n.d), "amdgpu_dp_gpu_failure") \
+            .get((("bdf", "0000:0c:00.0"), ("cause", "flapping"))) == 1
+    finally:
+        stop()
+
+
 def _evt(path):
     text = open(path).read() if os.path.exists(path) else ""
     return {k: int(v) for k, v in re.findall(r"(\w+)=(\d+)", text)}

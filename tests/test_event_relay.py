@@ -32,14 +32,15 @@ def _preload(*libs):
 
 
 class RelayNode:
-    def __init__(self, scratch, relay_env=None, daemon_args=(), daemon_env=None, relay_launch=None, relay_gpus=None):
+    def __init__(self, scratch, relay_env=None, daemon_args=(), daemon_env=None, relay_launch=None, relay_gpus=None,
+                 fx=None):
         self.scratch = scratch
         self.relay_launch = relay_launch  # argv -> argv for the relay process (e.g. another build's binary)
         self.fifo = os.path.join(scratch + ".fixture", "events")
         os.makedirs(scratch + ".fixture", exist_ok=True)
         os.mkfifo(self.fifo)
         self.sock = os.path.join(scratch + ".fixture", "events.sock")
-        self.fx = dict(fixtures.node(2), events_open_kfd=True)
+        self.fx = dict(fx or fixtures.node(2), events_open_kfd=True)
         # The relay may see more GPUs than the daemon does (their views disagree).
         self.relay_fx = dict(fixtures.node(relay_gpus), events_open_kfd=True) if relay_gpus else self.fx
         self.relay_env = relay_env
