@@ -33,7 +33,7 @@ probe:
 
 # Unit tests, then the bounded model check of the health state machine: every
 # sequence of up to HEALTH_MODEL_DEPTH steps over its 16 events, both layouts,
-# then up to HEALTH_MODEL_EXT_DEPTH steps over the extended 22/23 events.
+# then up to HEALTH_MODEL_EXT_DEPTH steps over the extended 24/25 events.
 HEALTH_MODEL_DEPTH ?= 6
 HEALTH_MODEL_EXT_DEPTH ?= 5
 test-native: build

@@ -31,7 +31,7 @@
 //   DRAIN UNDRAIN RETURN      the operator's drain file / --return-to-service for GPU 0
 //   CLOCK_HOLD                --reset-recovery-hold-ms (+1) pass
 //
-// --extended adds (22 symbols in-process, 23 with the relay):
+// --extended adds (24 symbols in-process, 25 with the relay):
 //   PRE1 POST1                an amdsmi event on GPU 1, which then resets too
 //   UNPLACED                  relay: a GPU_PRE_RESET the relay could not place
 //                             (node=- bdf=-); in-process: a GPU_POST_RESET on an
@@ -41,6 +41,9 @@
 //   RELAY_STUCK               relay only: the watchdog turns events off and on
 //   HALF_HOLD                 half of --reset-recovery-hold-ms passes
 //   ECC_UNREADABLE            GPU 0's ECC count turns unreadable / readable again
+//   PRE_P1 POST_P1            the event reported by GPU 0's second compute
+//                             partition (GPU 0 is DPX; KFD reports a reset on
+//                             every KFD node of the GPU)
 //
 // against a small reference model of what the monitor must believe, given the
 // events it was delivered. Invariants checked after every step:
@@ -161,14 +164,17 @@ enum Sym : int {
   // (in-process: an unplaceable GPU_POST_RESET); the relay renewing its
   // registration (in-process: one failing wait); the relay's watchdog turning
   // events off and on again (relay only); half a hold passing; GPU 0's ECC
-  // count becoming unreadable and readable again.
-  A_PRE1 = kBaseSymbols, A_POST1, A_UNPLACED, A_RELAY_RENEW, A_RELAY_STUCK, A_HALF_HOLD, A_ECC_UNREADABLE, kSymbols
+  // count becoming unreadable and readable again; a reset event reported by
+  // GPU 0's second compute partition (GPU 0 is DPX: KFD reports a reset on
+  // each of its nodes).
+  A_PRE1 = kBaseSymbols, A_POST1, A_UNPLACED, A_RELAY_RENEW, A_RELAY_STUCK, A_HALF_HOLD, A_ECC_UNREADABLE,
+  A_PRE_P1, A_POST_P1, kSymbols
 };
 const char* kSymNames[] = {"PRE",         "POST",          "VMFAULT",      "POLL_OK",     "POLL_FAIL",
                            "ECC_UP",      "ECC_RESET",     "RELAY_DROP",   "RELAY_RESTART", "LOST_EVENT",
                            "SIGHUP",      "RESTART",       "DRAIN",        "UNDRAIN",     "RETURN",
                            "CLOCK_HOLD",  "PRE1",          "POST1",        "UNPLACED",    "RELAY_RENEW",
-                           "RELAY_STUCK", "HALF_HOLD",     "ECC_UNREADABLE"};
+                           "RELAY_STUCK", "HALF_HOLD",     "ECC_UNREADABLE", "PRE_P1",      "POST_P1"};
 static_assert(sizeof(kSymNames) / sizeof(kSymNames[0]) == kSymbols, "symbol names");
 
 bool g_extended = false;  // --extended: set before the workers fork
@@ -204,7 +210,7 @@ class FakeSmi : public smi::Library {
     uint64_t ecc = 0;
   };
   Gpu gpu[2];
-  char handle[2] = {0, 0};
+  char handle[3] = {0, 0, 0};  // GPU 0 partition 0, GPU 1, GPU 0 partition 1
   char foreign = 0;  // a handle amdsmi never enumerated
   bool waits_failing = false;
   bool ecc_ok = true;  // GPU 0's uncorrectable count readable
@@ -212,7 +218,7 @@ class FakeSmi : public smi::Library {
   std::deque<smi::Event> queue;        // events the kernel holds for the registration
   std::vector<smi::Event> delivered;   // what EventsWait handed out (for the model)
 
-  int Index(void* h) const { return h == &handle[0] ? 0 : h == &handle[1] ? 1 : -1; }
+  int Index(void* h) const { return h == &handle[0] || h == &handle[2] ? 0 : h == &handle[1] ? 1 : -1; }
   Status EventsInit(const std::vector<void*>& hs, uint64_t) override {
     for (void* h : hs) registered.insert(h);
     return Status::Ok();
@@ -271,23 +277,26 @@ class FakeSmi : public smi::Library {
 };
 
 std::shared_ptr<const inventory::Snapshot> MakeSnapshot(FakeSmi* smi) {
-  std::vector<smi::ProcessorInfo> procs(2);
-  for (int i = 0; i < 2; ++i) {
+  // GPU 0 in DPX (two compute partitions, KFD nodes 2 and 3), GPU 1 in SPX.
+  std::vector<smi::ProcessorInfo> procs(3);
+  for (int i = 0; i < 3; ++i) {
+    const int gpu = i == 2 ? 1 : 0, part = i == 1 ? 1 : 0;
     auto& p = procs[i];
-    p.handle = &smi->handle[i];
-    p.uuid = "75a3000" + std::to_string(i) + "-0000-1000-80c0-bf9907890000";
-    p.bdf = kBdf[i];
-    p.bdf_id = (i == 0 ? 0x0cull : 0x2cull) << 8;
-    p.render_minor = 128 + 8 * i;
+    p.handle = &smi->handle[i == 0 ? 0 : i == 1 ? 2 : 1];
+    p.uuid = "75a3000" + std::to_string(gpu) + "-0000-1000-80c0-bf990789000" + std::to_string(part);
+    p.bdf = std::string(kBdf[gpu]).substr(0, 11) + std::to_string(part);
+    p.bdf_id = ((gpu == 0 ? 0x0cull : 0x2cull) << 8) | static_cast<uint64_t>(part);
+    p.render_minor = 128 + 8 * gpu + part;
     p.numa_node = 0;
-    p.vram_mib = 294896;
-    p.compute_partition = "SPX";
+    p.vram_mib = gpu == 0 ? 294896 / 2 : 294896;
+    p.compute_partition = gpu == 0 ? "DPX" : "SPX";
     p.memory_partition = "NPS1";
-    p.kfd_node = 2 + 8 * i;
-    p.num_cu = 256;
-    p.xcd_count = 8;
+    p.partition_id = static_cast<uint32_t>(part);
+    p.kfd_node = 2 + 8 * gpu + part;
+    p.num_cu = gpu == 0 ? 128 : 256;
+    p.xcd_count = gpu == 0 ? 4 : 8;
     p.market_name = "AMD Instinct MI355X";
-    p.asic_serial = "0x09C0BF990789730" + std::to_string(i);
+    p.asic_serial = "0x09C0BF990789730" + std::to_string(gpu);
   }
   inventory::BuildOptions o;
   o.sysfs_root = "";
@@ -506,6 +515,14 @@ class World {
           MonitorTestPeer::Wait(*mon_);
         } else {
           Emit(sym == A_PRE1 ? 3 : 4, 1);
+        }
+        break;
+      case A_PRE_P1: case A_POST_P1:
+        if (in_proc) {
+          smi_.Raise(&smi_.handle[2], sym == A_PRE_P1 ? 3 : 4);
+          MonitorTestPeer::Wait(*mon_);
+        } else {
+          Emit(sym == A_PRE_P1 ? 3 : 4, 0, 1);
         }
         break;
       case A_UNPLACED:
@@ -727,13 +744,14 @@ class World {
     if (relay_mode_) relay_.Close();
   }
 
-  // An event line of GPU `gpu` (-1: unplaceable, "node=- bdf=-").
-  void Emit(uint32_t type, int gpu = 0) {
+  // An event line of GPU `gpu`'s partition `part` (-1: unplaceable, "node=- bdf=-").
+  void Emit(uint32_t type, int gpu = 0, int part = 0) {
     const uint64_t seq = ++relay_.seq;
     std::string where = gpu < 0 ? std::string("node=- bdf=-")
-                                : "node=" + std::to_string(2 + 8 * gpu) + " bdf=" + kBdf[gpu];
-    std::string line = "event seq=" + std::to_string(seq) + " " + where + " part=0 type=" + std::to_string(type) +
-                       " fake\n";
+                                : "node=" + std::to_string(2 + 8 * gpu + part) + " bdf=" +
+                                      std::string(kBdf[gpu]).substr(0, 11) + std::to_string(part);
+    std::string line = "event seq=" + std::to_string(seq) + " " + where + " part=" + std::to_string(part) +
+                       " type=" + std::to_string(type) + " fake\n";
     relay_.ring.emplace_back(seq, line);
     if (relay_.fd >= 0) {
       sent_.push_back({relay_.Id() + ":" + std::to_string(seq), type, gpu});

@@ -33,14 +33,15 @@ def test_every_sequence_of_five_steps_keeps_the_invariants():
 def test_extended_alphabet_every_sequence_of_four_steps():
     """--extended adds GPU 1's resets, an unplaceable GPU_PRE_RESET, the relay
     renewing its registration (in-process: one failing wait), the relay's
-    watchdog turning events off and on (relay only), half a hold, and GPU 0's
-    ECC count turning unreadable and back. `make test-native` runs depth 5."""
+    watchdog turning events off and on (relay only), half a hold, GPU 0's
+    ECC count turning unreadable and back, and reset events reported by GPU 0's
+    second compute partition (GPU 0 is DPX). `make test-native` runs depth 5."""
     r = subprocess.run([MODEL, "--extended", "--depth", "4", "--jobs", "4"], capture_output=True, text=True,
                        timeout=600)
-    m = re.search(r"\(extended\), depth 4, 22/23 symbols.* all (\d+) sequences of 1\.\.4 steps covered by (\d+) "
+    m = re.search(r"\(extended\), depth 4, 24/25 symbols.* all (\d+) sequences of 1\.\.4 steps covered by (\d+) "
                   r"distinct states .* (\d+) violation", r.stdout)
     assert r.returncode == 0 and m, r.stdout[-3000:]
-    assert int(m.group(1)) == sum(22 ** i + 23 ** i for i in range(1, 5))
+    assert int(m.group(1)) == sum(24 ** i + 25 ** i for i in range(1, 5))
     assert int(m.group(2)) > 10000 and int(m.group(3)) == 0, r.stdout
 
 
