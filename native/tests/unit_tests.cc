@@ -495,6 +495,11 @@ static void TestDrainSyntax() {
   g.partitions.push_back(p);
   auto n = health::DrainNames(g);
   CHECK((n == std::set<std::string>{"GPU-a", "0000:0c:00.0", "0000:0c:00", "3", "GPU-a-p1"}));
+  p.uuid = "GPU-a-p2";
+  g.partitions.push_back(p);  // two partitions: the second one's PCI function names the GPU too
+  n = health::DrainNames(g);
+  CHECK((n == std::set<std::string>{"GPU-a", "0000:0c:00.0", "0000:0c:00", "0000:0c:00.1", "3", "GPU-a-p1",
+                                    "GPU-a-p2"}));
   CHECK(health::DrainTokens("").empty() && health::DrainTokens("# only a comment").empty());
 }
 

@@ -347,6 +347,30 @@ def test_operator_drain_file(scratch, tmp_path):
         n.close()
 
 
+def test_a_partition_pci_function_drains_its_gpu(scratch, tmp_path):
+    """On a CPX node amd-smi lists each compute partition with its own PCI
+    function (0000:2c:00.0 .. .7): naming any of them in the drain file drains
+    the whole GPU -- all 8 partitions -- as a reset holds it."""
+    import queue
+    drain = tmp_path / "drain"
+    fx = fixtures.node(2, modes="CPX")
+    n = Node(scratch, fx, args=["--partition-strategy", "single", "--drain-file", str(drain)],
+             env={"DP_HEALTH_POLL_MS": "100"})
+    try:
+        drain.write_text(fx["gpus"][1]["bdf"][:-1] + "3  # a partition of GPU 1\n")
+        deadline = time.time() + 5
+        bad = 0
+        while bad != 8 and time.time() < deadline:
+            try:
+                bad = sum(x.health != "Healthy" for x in n.q.get(timeout=0.2).devices)
+            except queue.Empty:
+                pass
+        assert bad == 8
+        assert "drained by the operator" in n.d.log()
+    finally:
+        n.close()
+
+
 def test_drain_and_undrain_commands(scratch, tmp_path):
     """`amdgpu-device-plugin --drain <id>` / `--undrain <id>` (run in the
     plugin pod, DP_DRAIN_FILE set) edit the drain file -- IDs checked against
