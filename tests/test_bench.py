@@ -48,8 +48,11 @@ def test_bench_single_process_contract():
     # was busy during the timed region (its 300 pods = 600 calls)
     pl = res["placement"]
     assert pl["relation"] in ("same-core", "same-l3", "other-l3") and pl["client_cpus"], pl
-    busy = [b for _, b in pl["loops_during_timed"] if b > 0]
-    assert len(busy) == 1 and busy[0] >= 300, pl
+    # (another loop may wake a few times meanwhile: a health broadcast to the
+    # ListAndWatch stream it serves)
+    busy = [b for _, b in pl["loops_during_timed"] if b >= 300]
+    idle = [b for _, b in pl["loops_during_timed"] if b < 300]
+    assert len(busy) == 1 and all(b <= 10 for b in idle), pl
     # the daemon's own share of each client's latency (read -> reply handed to
     # send()): one sample per call, the timed 300 pods being 600 calls
     sr = res["server_residency"]
