@@ -45,8 +45,12 @@ class Relay:
         self.fx = dict(fixtures.node(2), events_open_kfd=True)
         self.d = harness.Daemon(scratch, self.fx, args=["--event-relay", "--health-event-socket", self.sock],
                                 env=env, event_fifo=self.fifo).start()
-        self.d.wait_log("event notification registered on")
         self.clients = []
+        try:
+            self.d.wait_log("event notification registered on")
+        except BaseException:
+            self.d.stop()
+            raise
 
     def inject(self, lines):
         fd = os.open(self.fifo, os.O_WRONLY | os.O_NONBLOCK)
@@ -234,3 +238,66 @@ def test_an_unplaceable_event_is_numbered_and_replayed_unplaced(relay):
     assert len(replay) == 1 and r["gap"] == 0, replay
     m = EVENT.fullmatch(replay[0])
     assert m.group(1, 2, 3, 5, 6) == ("2", "-", "-", "3", "from nowhere"), replay
+
+
+class SubscribeModel:
+    """relay.cc Subscribe in a few lines: what a cursor is replayed and
+    whether nothing can have been missed."""
+
+    def __init__(self, relay_id, gen):
+        self.id, self.gen, self.seq, self.ring = relay_id, gen, 0, []
+        self.lost, self.lost_seq = False, 0
+
+    def event(self):
+        self.seq += 1
+        self.ring = (self.ring + [self.seq])[-RING:]
+
+    def lose(self):
+        self.lost, self.lost_seq = True, self.seq
+
+    def subscribe(self, rid, seq, gen):
+        if rid != self.id or seq > self.seq:
+            return [], 1
+        held = seq == self.seq or (bool(self.ring) and self.ring[0] <= seq + 1)
+        if self.lost and seq <= self.lost_seq:
+            held = False
+        return [q for q in self.ring if q > seq], 0 if held and gen == self.gen else 1
+
+
+@pytest.mark.parametrize("seed", [int(x) for x in os.environ.get("ADP_RELAY_SEEDS", "1,2,3,4").split(",")])
+def test_random_histories_match_the_subscribe_model(scratch, seed):
+    """Seeded random histories -- events, events the relay loses, daemons
+    reconnecting with cursors of this relay or another, this generation or
+    another, behind, current or from the future -- answered by the real relay
+    exactly as the model of its Subscribe says (the model the health model
+    check's relay follows)."""
+    import random
+    rnd = random.Random(seed)
+    r = Relay(scratch, env={"ADP_DEBUG_RELAY_REFUSE_EVENT": "refuseme"})
+    try:
+        h = r.hello()
+        m = SubscribeModel(h["relay"], h["gen"])
+        other = "0" * len(h["relay"]) if h["relay"] != "0" * len(h["relay"]) else "1" * len(h["relay"])
+        losses = 0
+        for step in range(30):
+            what = rnd.random()
+            if what < 0.35:
+                k = rnd.randint(1, 4)
+                r.events(k, prefix=f"s{step}-")
+                for _ in range(k):
+                    m.event()
+            elif what < 0.45:
+                losses += 1
+                r.inject([f"{rnd.randint(0, 1)} 1 refuseme {step}"])
+                r.d.wait_log("lost after", count=losses)
+                m.lose()
+            else:
+                rid = h["relay"] if rnd.random() < 0.85 else other
+                seq = rnd.randint(0, m.seq + 2)
+                gen = h["gen"] if rnd.random() < 0.85 else h["gen"] + 1
+                replay, a = r.subscribe(f"{rid}:{seq}:{gen}")
+                want = m.subscribe(rid, seq, gen)
+                assert (_seqs(replay), a["gap"]) == want, (step, rid == h["relay"], seq, gen, m.seq, m.lost_seq)
+        assert r.hello()["seq"] == m.seq
+    finally:
+        r.stop()
