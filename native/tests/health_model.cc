@@ -992,7 +992,7 @@ class World {
 struct Shared {
   std::atomic<uint64_t> next_task{0};
   std::atomic<uint64_t> distinct{0}, transitions{0}, pruned{0}, probes{0}, steps{0}, violations{0}, printed{0};
-  static constexpr size_t kSlots = size_t{1} << 22;
+  static constexpr size_t kSlots = size_t{1} << 24;  // 128 MiB: ~5x the states of extended depth 7
   std::atomic<uint64_t> table[kSlots];
 };
 
@@ -1011,7 +1011,12 @@ bool Claim(Shared* sh, const std::string& key, int remaining, bool* fresh) {
   uint64_t tag = h & ~uint64_t{0xff};
   if (!tag) tag = 0x100;
   const uint64_t want = tag | static_cast<uint64_t>(remaining + 1);
+  size_t probes = 0;
   for (size_t i = (h >> 8) & (Shared::kSlots - 1);; i = (i + 1) & (Shared::kSlots - 1)) {
+    if (++probes > Shared::kSlots) {
+      fprintf(stderr, "health model: the state table is full (%zu slots)\n", Shared::kSlots);
+      abort();
+    }
     uint64_t e = sh->table[i].load();
     while (true) {
       if (e == 0) {
