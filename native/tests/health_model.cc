@@ -618,7 +618,7 @@ class World {
       for (const auto* c : {&cur, &fc})
         if (c->valid && c->relay == relay_.Id()) base = std::min(base, c->seq);
       for (const auto& [q, l] : relay_.ring)
-        if (q > base || (base == UINT64_MAX && relay_.fd < 0 && false))
+        if (q > base)
           k += std::to_string(GpuOf(l)) + ":" + std::to_string(TypeOf(l)) +
                (delivered_ids_.count(relay_.Id() + ":" + std::to_string(q)) ? "d" : "n");
     }
