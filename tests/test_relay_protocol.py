@@ -29,7 +29,7 @@ from k8s_gpu_sharing_plugin_amd.utils import harness
 
 RING = 1024  # kRelayRingSize (native/src/health/relay.h)
 HELLO = re.compile(r"hello v1 (reinit )?(events=\S+)(?: processors=(\d+))? relay=(\w+) gen=(\d+) seq=(\d+) fp=(\S+)"
-                   r" renew_ms=\d+(?: gap=(\d))?")
+                   r" renew_ms=\d+(?: gap=(\d))?(?: reason=(.*))?")
 EVENT = re.compile(r"event seq=(\d+) node=(\S+) bdf=(\S+) part=(\d+) type=(\d+) ?(.*)")
 
 
@@ -39,12 +39,14 @@ class Relay:
     def __init__(self, scratch, env=None):
         fdir = scratch + ".fixture"
         os.makedirs(fdir, exist_ok=True)
+        self.state = os.path.join(fdir, "state")  # the mock's runtime knobs
+        os.makedirs(self.state, exist_ok=True)
         self.fifo = os.path.join(fdir, "events")
         os.mkfifo(self.fifo)
         self.sock = os.path.join(fdir, "events.sock")
         self.fx = dict(fixtures.node(2), events_open_kfd=True)
         self.d = harness.Daemon(scratch, self.fx, args=["--event-relay", "--health-event-socket", self.sock],
-                                env=env, event_fifo=self.fifo).start()
+                                env=env, event_fifo=self.fifo, state_dir=self.state).start()
         self.clients = []
         try:
             self.d.wait_log("event notification registered on")
@@ -106,7 +108,7 @@ class Relay:
             m = HELLO.fullmatch(ln)
             if m and m.group(1):
                 return replay, {"events": m.group(2), "gen": int(m.group(5)), "seq": int(m.group(6)),
-                                "gap": int(m.group(8)) if m.group(8) is not None else None}
+                                "gap": int(m.group(8)) if m.group(8) is not None else None, "reason": m.group(9)}
             replay.append(ln)
 
     def stop(self):
@@ -301,3 +303,26 @@ def test_random_histories_match_the_subscribe_model(scratch, seed):
         assert r.hello()["seq"] == m.seq
     finally:
         r.stop()
+
+
+def test_a_failed_renewal_is_events_off_until_one_succeeds(relay):
+    """A daemon whose processors differ from the registration makes the relay
+    renew it; when amdsmi cannot enumerate then, every daemon is told events
+    are off (with why) in a new generation -- and the next daemon that
+    subscribes while they are off makes the relay try again."""
+    relay.events(2)
+    h = relay.hello()
+    open(os.path.join(relay.state, "enumerate_fail"), "w").close()
+    replay, r = relay.subscribe(raw="reinit fp=0123456789abcdef since=%s:2:%d" % (h["relay"], h["gen"]))
+    assert r["events"] == "events=off" and r["gen"] == h["gen"] + 1 and r["gap"] == 1, r
+    assert "enumeration failed" in r["reason"], r
+    assert _seqs(replay) == [], replay
+    assert "enumeration failed" in relay.d.wait_log("enumeration failed")
+    g = relay.hello()
+    assert g["events"] == "events=off" and g["gen"] == h["gen"] + 1
+    os.unlink(os.path.join(relay.state, "enumerate_fail"))
+    replay, r = relay.subscribe(f"{h['relay']}:2:{g['gen']}")  # its own fingerprint: still renewed (events off)
+    assert r["events"] == "events=ok" and r["gen"] == g["gen"] + 1 and r["gap"] == 1, r
+    relay.events(1)
+    replay, r = relay.subscribe(f"{h['relay']}:2:{r['gen']}")
+    assert _seqs(replay) == [3] and r["gap"] == 0, (replay, r)
