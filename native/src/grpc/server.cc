@@ -798,6 +798,13 @@ void Server::CloseConn(Loop& l, int fd) {
 }
 
 Status Server::RunLoop(Loop& l) {
+#ifdef ADP_TEST_HOOKS
+  // Tests: loop 0 fails every time it starts -- the crash budget end to end
+  // (the reference exits after more than 5 crashes within an hour,
+  // server.go:191-203). Compiled out of image builds.
+  static const bool crash_hook = getenv("ADP_DEBUG_GRPC_LOOP_CRASH") != nullptr;
+  if (crash_hook && l.index == 0) return Internal("ADP_DEBUG_GRPC_LOOP_CRASH");
+#endif
   epoll_event events[64];
   // Adaptive busy-poll: after serving a request, keep polling without sleeping
   // for busy_poll_us_ so the kubelet's follow-up call (Allocate after

@@ -108,6 +108,31 @@ def test_waits_for_kubelet_with_backoff(scratch):
     k.stop()
 
 
+def test_grpc_crash_budget_is_fatal(scratch):
+    """A plugin's gRPC server that keeps crashing (test hook: its first loop
+    fails each time it starts) is restarted, and after more than 5 crashes in
+    an hour the daemon exits 1 -- the reference's crash budget
+    (server.go:191-203), left to the DaemonSet's restart."""
+    if not _hooks_compiled():
+        pytest.skip("this build has no test hooks (-DADP_TEST_HOOKS=OFF)")
+    k = kubelet.StubKubelet(sock(scratch)).start()
+    d = harness.Daemon(scratch, env={"ADP_DEBUG_GRPC_LOOP_CRASH": "1"}).start()
+    try:
+        assert d.proc.wait(20) == 1
+        log = d.log()
+        assert log.count("crashed: INTERNAL: ADP_DEBUG_GRPC_LOOP_CRASH") == 7, log[-3000:]
+        assert "has repeatedly crashed recently; giving up" in log
+        assert "exhausted its crash budget; exiting" in log
+    finally:
+        d.stop()
+        k.stop()
+
+
+def _hooks_compiled():
+    from k8s_gpu_sharing_plugin_amd import DAEMON
+    return b"ADP_DEBUG_GRPC_LOOP_CRASH" in open(DAEMON, "rb").read()
+
+
 def test_rejected_registration_retries(scratch):
     k = kubelet.StubKubelet(sock(scratch), reject_with="nope").start()
     d = harness.Daemon(scratch).start()
