@@ -210,8 +210,9 @@ const std::vector<FlagDef>& Table() {
        "a live config change (config file, SIGHUP) that would change what a replicated resource's IDs mean "
        "(memory unit, replica count, CU masks) while running pods hold some of them (kubelet PodResources) "
        "waits: the current layout keeps being served, amdgpu_dp_deferred_layout_change says so, and the "
-       "change applies once no pod holds those IDs (looked at every 30 s). Off: it applies at once and the "
-       "node may be over-committed until those pods end",
+       "change applies once no pod holds those IDs (looked at every 30 s); a change is applied, with a "
+       "warning, when PodResources cannot say (no --pod-resources-socket, or it does not answer). Off: it "
+       "applies at once and the node may be over-committed until those pods end",
        [](Flags& f) -> void* { return &f.defer_layout_changes; }},
       {"reset-flap-window-ms", "DP_RESET_FLAP_WINDOW_MS", "resetFlapWindowMs", Kind::kUint,
        "the window of --reset-flap-limit, and the quiet time that ends a quarantine",

@@ -22,6 +22,8 @@ import subprocess
 import sys
 import time
 
+import pytest
+
 from k8s_gpu_sharing_plugin_amd.models import fixtures
 from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
 
@@ -288,3 +290,40 @@ def test_a_whole_gpu_resource_turned_into_replicas_waits_for_its_pods(scratch):
         d.stop()
         k.stop()
         pr.stop()
+
+
+@pytest.mark.parametrize("socket", ["none", "unreachable"])
+def test_a_deferral_that_cannot_know_applies_and_says_so(scratch, socket):
+    """--defer-layout-changes can only wait for pods the kubelet's PodResources
+    API names: without its socket, or with one that does not answer, a change
+    that re-means IDs applies (a config change is never blocked on an unknown)
+    with a warning saying why."""
+    cfg = os.path.join(scratch + ".fixture", "config.yaml")
+    os.makedirs(os.path.dirname(cfg), exist_ok=True)
+
+    def write(rc):
+        with open(cfg + ".tmp", "w") as f:
+            f.write(f"version: v1\nflags:\n  resourceConfig: {rc}\n")
+        os.rename(cfg + ".tmp", cfg)
+    write("gpu:gpu:2")
+    args = ["--config-file", cfg, "--defer-layout-changes"]
+    if socket == "none":
+        args += ["--pod-resources-socket="]  # (its default is the kubelet's path)
+    else:
+        args += ["--pod-resources-socket", os.path.join(scratch + ".fixture", "nobody-listens.sock")]
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(2), args=args).start()
+    try:
+        reg = k.wait_registration()
+        write("gpu:gpu:3")
+        reg = k.wait_registration(15)  # applied
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        assert len(c.watch()[0].get(timeout=5).devices) == 6
+        c.close()
+        want = ("--defer-layout-changes needs the kubelet's PodResources socket; applying" if socket == "none"
+                else "whether running pods hold IDs of the resources this change re-means is unknown")
+        assert want in d.wait_log(want)
+        assert "config change deferred" not in d.log()
+    finally:
+        d.stop()
+        k.stop()
