@@ -190,3 +190,34 @@ def test_verdicts_in_the_state_file_and_a_waiting_request_are_named(tmp_path):
     assert "after an event gap -- the event relay restarted -- the polled check returns it" in line
     assert _find(lines, f"GPU {fx['gpus'][0]['bdf']} is out of service") is None
     assert _find(lines, "a return-to-service request is waiting"), lines
+
+
+def _state_fx(tmp_path, **files):
+    """A 2-GPU node whose mock reads runtime knobs from a state directory."""
+    state = tmp_path / "state"
+    state.mkdir(exist_ok=True)
+    for name, body in files.items():
+        (state / name).write_text(body)
+    return dict(fixtures.node(2), state_dir=str(state))
+
+
+def test_enumeration_failure_is_a_failure_with_a_hint(tmp_path):
+    rc, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), fx=_state_fx(tmp_path, enumerate_fail=""))
+    line = _find(lines, "enumeration")
+    assert rc == 1 and line.startswith("FAIL") and "amdgpu driver loaded" in line, lines
+
+
+@pytest.mark.parametrize("args,fx_extra,says", [
+    (["--health-events=false"], {}, "health events: off by configuration -- resets are seen by polling only"),
+    ([], {"events_supported": False}, "health events: "),
+])
+def test_health_events_off_is_a_warning_that_says_why(tmp_path, args, fx_extra, says):
+    rc, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), *args, fx=dict(fixtures.node(2), **fx_extra))
+    line = _find(lines, says)
+    assert rc == 0 and line and line.startswith("warn"), lines
+
+
+def test_ecc_unreadable_on_some_gpus_is_a_warning(tmp_path):
+    rc, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), fx=_state_fx(tmp_path, **{"gpu1.ecc": "x"}))
+    line = _find(lines, "uncorrectable ECC readable on 1 of 2 GPU(s)")
+    assert rc == 0 and line and line.startswith("warn") and "not detected on the others" in line, lines
