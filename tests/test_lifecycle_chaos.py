@@ -5,7 +5,9 @@ Each step is one of: SIGHUP, or three at once; the kubelet restarting (its
 socket re-created), or going away for a few steps; the plugin's own socket
 deleted; a config-file edit (resource renamed and/or replica count changed,
 applied live), or a broken one (ignored: the running config stays, across a
-SIGHUP too); GPU 1 drained or undrained by the operator's drain file; SIGUSR1.
+SIGHUP too); GPU 1 drained or undrained by the operator's drain file; SIGUSR1;
+in the chart's layout also the event relay stopped or killed and started
+again (events must be back on through it at every settle).
 After every step (the kubelet's absence aside) the daemon must come back
 to the expected state on its own: registered with the current kubelet for the
 expected resource, and that resource's ListAndWatch listing 2 GPUs x R
@@ -28,6 +30,7 @@ from k8s_gpu_sharing_plugin_amd.models import fixtures
 from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
 
 SEEDS = [int(s) for s in os.environ.get("ADP_LIFECYCLE_SEEDS", "1,2,3").split(",")]
+RELAY_SEEDS = [int(s) for s in os.environ.get("ADP_LIFECYCLE_RELAY_SEEDS", "1,2").split(",")]
 STEPS = int(os.environ.get("ADP_LIFECYCLE_STEPS", "12"))
 
 
@@ -38,7 +41,7 @@ def _count(pid, what):
 
 
 class Life:
-    def __init__(self, scratch, tmp_path):
+    def __init__(self, scratch, tmp_path, relay=False):
         self.scratch = scratch
         self.ksock = os.path.join(scratch, "kubelet.sock")
         self.fx = fixtures.node(2)
@@ -47,11 +50,39 @@ class Life:
         self.replicas, self.name, self.drained = 2, "sharedgpu", False
         self.write_config()
         self.k = kubelet.StubKubelet(self.ksock).start()
-        self.d = harness.Daemon(scratch, self.fx, args=["--config-file", self.cfg, "--drain-file", self.drain],
-                                env={"DP_HEALTH_POLL_MS": "100"}).start()
+        args = ["--config-file", self.cfg, "--drain-file", self.drain]
+        env = {"DP_HEALTH_POLL_MS": "100"}
+        self.relay, self.relays = None, 0
+        if relay:
+            # the chart's layout: events through the relay, the daemon denied
+            # /dev/kfd and the render nodes like an unprivileged pod
+            from k8s_gpu_sharing_plugin_amd import BUILD_DIR
+            self.fx = dict(self.fx, events_open_kfd=True)
+            self.rsock = str(tmp_path / "events.sock")
+            self.start_relay()
+            sim = os.path.join(BUILD_DIR, "libadp_devcgroup_sim.so")
+            args += ["--health-event-socket", self.rsock, "--metrics-addr", "127.0.0.1:0"]
+            env["LD_PRELOAD"] = " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), sim) if x)
+        self.d = harness.Daemon(scratch, self.fx, args=args, env=env).start()
         self.reg = None
         self.history = []
         self.kubelet_down = False
+
+    def start_relay(self):
+        self.relays += 1
+        rdir = f"{self.scratch}-relay{self.relays}"
+        os.makedirs(rdir, exist_ok=True)
+        self.relay = harness.Daemon(rdir, self.fx, args=["--event-relay", "--health-event-socket", self.rsock]).start()
+        self.relay.wait_log("relaying amdsmi events on")
+
+    def events_on(self):
+        import re
+        from test_metrics import _get, _parse, _value
+        port = int(re.search(r"on port (\d+)", self.d.wait_log("serving /metrics")).group(1))
+        try:
+            return _value(_parse(_get(port, "/metrics")[1]), "amdgpu_dp_health_events_enabled") == 1
+        except OSError:  # /metrics restarting with a generation
+            return False
 
     def write_config(self):
         tmp = self.cfg + ".tmp"
@@ -61,7 +92,7 @@ class Life:
 
     def step(self, rnd):
         what = rnd.choice(["sighup", "storm", "kubelet", "kubelet-away", "socket", "config", "config", "broken",
-                           "drain", "usr1"])
+                           "drain", "usr1"] + (["relay-restart", "relay-kill"] if self.relay else []))
         if self.kubelet_down and what in ("kubelet", "kubelet-away"):
             what = "kubelet-back"
         if what == "sighup":
@@ -81,6 +112,12 @@ class Life:
             self.reg = None
         elif what == "usr1":
             self.d.signal(signal.SIGUSR1)
+        elif what in ("relay-restart", "relay-kill"):
+            if what == "relay-kill":
+                self.relay.proc.kill()
+                self.relay.proc.wait()
+            self.relay.stop()
+            self.start_relay()
         elif what == "broken":
             # A valid edit replaced at once by a broken one may never be read
             # (then the daemon rightly keeps what it ran): the valid one is
@@ -151,7 +188,9 @@ class Life:
                                        if e.endswith(".sock") and e != "kubelet.sock")
                         seen = (len(first.devices), sum(x.health != "Healthy" for x in first.devices), socks)
                         if seen == want + ([self.reg.endpoint],):
-                            return
+                            if self.relay is None or self.events_on():
+                                return
+                            seen = "events not on through the relay"
                     else:  # the endpoint is being restarted: the call failed
                         seen = repr(first)[:200]
                 except queue.Empty:
@@ -167,13 +206,17 @@ class Life:
         rc = self.d.stop()
         if not self.kubelet_down:
             self.k.stop()
+        if self.relay is not None:
+            self.relay.stop()
         return rc
 
 
-@pytest.mark.parametrize("seed", SEEDS)
-def test_interleaved_restarts_reloads_and_drains_settle(scratch, tmp_path, seed):
+@pytest.mark.parametrize("seed,relay", [(s, False) for s in SEEDS] + [(s, True) for s in RELAY_SEEDS])
+def test_interleaved_restarts_reloads_and_drains_settle(scratch, tmp_path, seed, relay):
+    """(relay: the chart's layout, with the relay also stopped or killed and
+    started again, and events required back on through it at every settle)"""
     rnd = random.Random(seed)
-    life = Life(scratch, tmp_path)
+    life = Life(scratch, tmp_path, relay=relay)
     try:
         life.settle()
         pid = life.d.proc.pid
