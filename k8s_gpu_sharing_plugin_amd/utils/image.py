@@ -25,7 +25,7 @@ import shlex
 import shutil
 import subprocess
 
-from .. import DAEMON, PROBE_BIN, REPO_ROOT
+from .. import PROBE_BIN, REPO_ROOT
 
 ROCM_LIB = "/opt/rocm/lib"
 HOST_LIB = "/lib/x86_64-linux-gnu"
