@@ -190,6 +190,10 @@ def _status(args) -> int:
         size = (f"{sizes[0][0]} MiB" if len(sizes) == 1 else
                 f"{sizes[0][0]}..{sizes[-1][0]} MiB")
         print(f"{res}: one unit = {size} ({', '.join(sorted({k for _, k in sizes}))})")
+    unmatched = sorted((ls.get("type"), int(v)) for ls, v in by("amdgpu_dp_unmatched_events_total") if v)
+    if unmatched:
+        print("UNMATCHED events (amdsmi named a processor no GPU of this node is): " +
+              ", ".join(f"{t} x{n}" for t, n in unmatched))
     for ls, v in by("amdgpu_dp_deferred_layout_change"):
         if v:
             print(f"DEFERRED {ls.get('resource')}: a config change waits for the running pods holding its IDs")

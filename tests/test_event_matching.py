@@ -116,6 +116,12 @@ def test_unmatched_pre_reset_holds_every_gpu_until_polled_recovery(scratch, layo
         got = _wait_samples(port, "amdgpu_dp_unmatched_events_total",
                             {(("type", "GPU_PRE_RESET"),): 1, (("type", "VMFAULT"),): 1})
         assert got == {(("type", "GPU_PRE_RESET"),): 1, (("type", "VMFAULT"),): 1}, got
+        import subprocess
+        import sys
+        st = subprocess.run([sys.executable, "-m", "k8s_gpu_sharing_plugin_amd", "status",
+                             f"http://127.0.0.1:{port}/metrics"], capture_output=True, text=True, timeout=60)
+        assert "UNMATCHED events (amdsmi named a processor no GPU of this node is): GPU_PRE_RESET x1, VMFAULT x1" \
+            in st.stdout, st.stdout
         if relay is not None:
             rlog = relay.wait_log("forwarded unplaced")
             assert "processor handle amdsmi did not enumerate" in rlog
