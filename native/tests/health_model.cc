@@ -1,6 +1,6 @@
 // Bounded exhaustive model check of the health state machine (round-6 review
 // item 2). Run: build/native/adp_health_model [--depth N] [--mode in-process|relay|both]
-//   [--extended] [--replay STEP,STEP,...]
+//   [--extended] [--replay STEP,STEP,...] [--random WALKS --length STEPS --seed S]
 //
 // The reference's whole health loop is ~120 lines (nvidia.go:181-269,
 // server.go:251-265): a device goes Unhealthy on an Xid and never comes back.
@@ -88,6 +88,7 @@
 #include <algorithm>
 #include <atomic>
 #include <new>
+#include <random>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -1061,6 +1062,38 @@ void Report(Shared* sh, bool relay, const std::string& v) {
   if (sh->printed.fetch_add(1) < 20) printf("VIOLATION [%s] %s\n", relay ? "relay" : "in-process", v.c_str());
 }
 
+// I3: an answered poll, a hold, an answered poll -> the GPUs in `probe` back in service.
+void Lookahead(bool relay, const std::string& dir, const std::vector<int>& seq, int probe, Shared* sh) {
+  sh->probes.fetch_add(1, std::memory_order_relaxed);
+  std::vector<int> look = seq;
+  look.insert(look.end(), {A_POLL_OK, A_CLOCK_HOLD, A_POLL_OK});
+  World w(relay, dir);
+  std::string pv;
+  for (size_t i = 0; i < look.size() && pv.empty(); ++i) pv = w.Step(look[i]);
+  if (pv.empty() && (w.ResetPending() & probe))
+    pv = "I3: a reset-pending GPU with a confirmed gap is still held after POLL_OK CLOCK_HOLD POLL_OK";
+  if (!pv.empty()) Report(sh, relay, pv + " -- after " + Trace(look));
+}
+
+// --random: walks far deeper than the exhaustive bound, each checked at every
+// step and probed for liveness at its end.
+void RandomWalks(bool relay, const std::string& dir, uint64_t seed, int walks, int length, Shared* sh) {
+  std::mt19937_64 rng(seed);
+  const std::vector<int> alpha = Alphabet(relay, g_extended);
+  for (int i = 0; i < walks; ++i) {
+    std::vector<int> seq(static_cast<size_t>(length));
+    for (auto& x : seq) x = alpha[rng() % alpha.size()];
+    sh->transitions.fetch_add(1, std::memory_order_relaxed);
+    int probe = 0;
+    std::string v = Replay(relay, dir, seq, nullptr, &probe, sh);
+    if (!v.empty()) {
+      Report(sh, relay, v);
+      continue;
+    }
+    if (probe) Lookahead(relay, dir, seq, probe, sh);
+  }
+}
+
 // One node: checked, claimed, probed for liveness; true when it is to be expanded.
 bool Visit(bool relay, const std::string& dir, int depth, const std::vector<int>& seq, Shared* sh) {
   sh->transitions.fetch_add(1, std::memory_order_relaxed);
@@ -1078,18 +1111,7 @@ bool Visit(bool relay, const std::string& dir, int depth, const std::vector<int>
     return false;
   }
   if (fresh) sh->distinct.fetch_add(1, std::memory_order_relaxed);
-  if (probe) {
-    // I3: an answered poll, a hold, an answered poll -> back in service.
-    sh->probes.fetch_add(1, std::memory_order_relaxed);
-    std::vector<int> look = seq;
-    look.insert(look.end(), {A_POLL_OK, A_CLOCK_HOLD, A_POLL_OK});
-    World w(relay, dir);
-    std::string pv;
-    for (size_t i = 0; i < look.size() && pv.empty(); ++i) pv = w.Step(look[i]);
-    if (pv.empty() && (w.ResetPending() & probe))
-      pv = "I3: a reset-pending GPU with a confirmed gap is still held after POLL_OK CLOCK_HOLD POLL_OK";
-    if (!pv.empty()) Report(sh, relay, pv + " -- after " + Trace(look));
-  }
+  if (probe) Lookahead(relay, dir, seq, probe, sh);
   return remaining > 0;
 }
 
@@ -1114,12 +1136,17 @@ int main(int argc, char** argv) {
   int jobs = static_cast<int>(std::min<long>(8, std::max<long>(1, sysconf(_SC_NPROCESSORS_ONLN))));
   std::string mode = "both";
   std::vector<std::string> replay;
+  int walks = 0, length = 40;
+  uint64_t seed = 1;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--depth") && i + 1 < argc) depth = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--jobs") && i + 1 < argc) jobs = std::max(1, atoi(argv[++i]));
     else if (!strcmp(argv[i], "--mode") && i + 1 < argc) mode = argv[++i];
     else if (!strcmp(argv[i], "--replay") && i + 1 < argc) replay = Split(argv[++i], ',');
     else if (!strcmp(argv[i], "--extended")) g_extended = true;
+    else if (!strcmp(argv[i], "--random") && i + 1 < argc) walks = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--length") && i + 1 < argc) length = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--seed") && i + 1 < argc) seed = strtoull(argv[++i], nullptr, 10);
   }
   SetLogLevel(getenv("ADP_LOG_LEVEL") ? LogLevel::kInfo : LogLevel::kError);
   setvbuf(stdout, nullptr, _IOLBF, 0);
@@ -1164,6 +1191,44 @@ int main(int argc, char** argv) {
       printf("%s: %s\n", relay ? "relay" : "in-process", v.empty() ? "ok" : v.c_str());
       rc |= !v.empty();
     }
+  } else if (walks > 0) {  // --random N --length L [--seed S]
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<pid_t> kids;
+    for (int j = 0; j < jobs; ++j) {
+      pid_t pid = fork();
+      if (pid == 0) {
+        const std::string wdir = dir + "/w" + std::to_string(j);
+        mkdir(wdir.c_str(), 0700);
+        const int mine = walks / jobs + (j < walks % jobs ? 1 : 0);
+        for (size_t m = 0; m < modes.size(); ++m)
+          RandomWalks(modes[m], wdir, seed * 1000003 + static_cast<uint64_t>(j) * 17 + m, mine, length, sh);
+        for (const char* f : {"health.state", "health.state.relay", "health.state.tmp", "health.state.relay.tmp",
+                              "drain", "drain.return", "drain.return.taken", "relay.sock"})
+          unlink((wdir + "/" + f).c_str());
+        rmdir(wdir.c_str());
+#ifdef ADP_COVERAGE
+        exit(0);
+#else
+        _exit(0);
+#endif
+      }
+      if (pid > 0) kids.push_back(pid);
+    }
+    for (pid_t k : kids) {
+      int status = 0;
+      waitpid(k, &status, 0);
+      if (!WIFEXITED(status) || WEXITSTATUS(status) != 0) {
+        printf("worker %d failed (status %d)\n", static_cast<int>(k), status);
+        rc = 1;
+      }
+    }
+    double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    printf("health model: %s%s, %d random walks of %d steps per layout (seed %llu), %d workers: %llu monitor steps, "
+           "%llu liveness probes in %.1f s: %llu violation(s)\n",
+           mode.c_str(), g_extended ? " (extended)" : "", walks, length, static_cast<unsigned long long>(seed), jobs,
+           static_cast<unsigned long long>(sh->steps.load()), static_cast<unsigned long long>(sh->probes.load()), secs,
+           static_cast<unsigned long long>(sh->violations.load()));
+    rc |= sh->violations.load() != 0;
   } else {
     auto t0 = std::chrono::steady_clock::now();
     // Depth 1 here; every (first, second) pair below it is a task the workers

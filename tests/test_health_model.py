@@ -45,6 +45,17 @@ def test_extended_alphabet_every_sequence_of_four_steps():
     assert int(m.group(2)) > 10000 and int(m.group(3)) == 0, r.stdout
 
 
+def test_random_walks_far_past_the_exhaustive_bound():
+    """--random: walks of 60 steps over the extended alphabet, every step
+    checked, each probed for liveness at its end (states the depth bound never
+    reaches: quarantines over several windows, many relay generations)."""
+    r = subprocess.run([MODEL, "--extended", "--random", "400", "--length", "60", "--seed", "3", "--jobs", "4"],
+                       capture_output=True, text=True, timeout=600)
+    m = re.search(r"400 random walks of 60 steps per layout .*: (\d+) monitor steps.* (\d+) violation", r.stdout)
+    assert r.returncode == 0 and m, r.stdout[-3000:]
+    assert int(m.group(1)) == 2 * 400 * 60 and int(m.group(2)) == 0, r.stdout
+
+
 @pytest.mark.parametrize("seq", [
     # an unplaceable GPU_PRE_RESET holds both GPUs; the polled check returns them
     "UNPLACED,POLL_OK,CLOCK_HOLD,POLL_OK",
