@@ -31,6 +31,7 @@
 //
 // usage: amdgpu-dp-event-probe [--lib <libamd_smi.so>] [--types 12,13] [--wait-ms 8000] [--self-hip]
 //                              [--cycles N]
+#include <dirent.h>
 #include <dlfcn.h>
 #include <unistd.h>
 
@@ -50,9 +51,22 @@
 
 using namespace adp;
 
+namespace {
+// Open descriptors of this process (a registration amdsmi does not release
+// would keep a KFD event file open).
+int OpenFds() {
+  int n = 0;
+  if (DIR* d = opendir("/proc/self/fd")) {
+    while (readdir(d)) ++n;
+    closedir(d);
+  }
+  return n - 3;  // ".", "..", and the directory's own descriptor
+}
+}  // namespace
+
 int main(int argc, char** argv) {
   std::string lib_path, types = "12,13";
-  int wait_ms = 8000, cycles = 0;
+  int wait_ms = 8000, cycles = 0, cycles_ok = 0;
   bool self_hip = false;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--self-hip")) self_hip = true;
@@ -82,14 +96,18 @@ int main(int argc, char** argv) {
   std::vector<void*> handles;
   for (const auto& p : *procs) handles.push_back(p.handle);
   std::string gens;
+  const int fds_before = OpenFds();
   for (int c = 0; c < cycles; ++c) {
     Status st = (*lib)->EventsInit(handles, hc.EventMask());
     const size_t live = (*lib)->EventsRegistered();
     (*lib)->EventsStopAll();
+    cycles_ok += st.ok() && live == handles.size() && (*lib)->EventsRegistered() == 0;
     gens += std::string(c ? ", " : "") + "{\"init\": \"" + JsonEscape(st.ok() ? "ok" : st.ToString()) +
             "\", \"registered\": " + std::to_string(live) +
             ", \"after_stop\": " + std::to_string((*lib)->EventsRegistered()) + "}";
   }
+  const int fds_after = OpenFds();
+  if (gens.size() > 4000) gens = gens.substr(0, gens.rfind("}, {", 2000) + 1) + ", \"...\"";  // the first ones
   Status reg = (*lib)->EventsInit(handles, hc.EventMask());
   printf("%s\n", reg.ok() ? "registered" : "registration failed");
   fflush(stdout);
@@ -172,7 +190,10 @@ int main(int argc, char** argv) {
 
   std::string out = "{\"amdsmi\": \"" + (*lib)->Version() + "\", \"pid\": " + std::to_string(getpid()) +
                     ", \"self_hip\": " + hip + ", \"mask\": " + std::to_string(hc.EventMask()) +
-                    ", \"cycles\": [" + gens + "], \"registration\": \"" +
+                    ", \"cycles\": [" + gens + "], \"cycle_count\": " + std::to_string(cycles) +
+                    ", \"cycles_ok\": " + std::to_string(cycles_ok) + ", \"fds_before_cycles\": " +
+                    std::to_string(fds_before) + ", \"fds_after_cycles\": " + std::to_string(fds_after) +
+                    ", \"registration\": \"" +
                     JsonEscape(reg.ok() ? "ok" : reg.ToString()) + "\", \"processors\": [";
   for (size_t i = 0; i < procs->size(); ++i) {
     const auto& p = (*procs)[i];

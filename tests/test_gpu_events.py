@@ -129,6 +129,24 @@ def test_raw_events_of_its_own_process_name_enumerated_processors(raw_self, real
         assert lat["after_hipInit_start"] >= 0, raw_self
 
 
+def test_real_amdsmi_registration_generations_leak_nothing(real_snap):
+    """200 generations of what every SIGHUP does to an in-process monitor's
+    registration (EventsInit on every processor, EventsStopAll) on the real
+    libamd_smi, in one process: every one ok, and the process holds no more
+    descriptors after them than before -- a registration amdsmi kept would keep
+    its KFD event file open."""
+    r = subprocess.run([EVENT_PROBE, "--types", TYPES, "--wait-ms", "300", "--cycles", "200"],
+                       capture_output=True, text=True, timeout=300)
+    lines = r.stdout.strip().splitlines()
+    rec = json.loads(lines[-1]) if lines and lines[-1].startswith("{") else {"error": r.stdout + r.stderr}
+    rec["rc"], rec["stderr"] = r.returncode, r.stderr[-2000:]
+    _record("raw_events_200_generations.json", rec)
+    assert rec["rc"] == 0 and rec["cycle_count"] == 200, rec
+    assert rec["cycles_ok"] == 200, rec
+    assert rec["fds_after_cycles"] <= rec["fds_before_cycles"], rec
+    assert rec["registration"] == "ok", rec
+
+
 def _log_time(line):
     """The wall-clock time of a daemon / relay log line ("2026-...Z ...")."""
     from datetime import datetime, timezone
