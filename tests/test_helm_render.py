@@ -435,3 +435,15 @@ def test_defer_layout_changes_value_mounts_pod_resources():
     assert any(v["name"] == "pod-resources" for v in ds["spec"]["template"]["spec"]["volumes"])
     ds0 = daemonset()
     assert "pod-resources" not in {m["name"] for m in container(ds0)["volumeMounts"]}
+
+
+def test_extra_event_types_reach_both_containers():
+    """healthEventExtraTypes: the plugin counts them and the relay registers
+    them (each reads DP_HEALTH_EVENT_EXTRA_TYPES); unset by default."""
+    ds = daemonset({"healthEventExtraTypes": "12,13"})
+    assert env(ds)["DP_HEALTH_EVENT_EXTRA_TYPES"] == "12,13"
+    r = relay(ds)
+    assert {e["name"]: e.get("value") for e in r["env"]}["DP_HEALTH_EVENT_EXTRA_TYPES"] == "12,13"
+    ds = daemonset()
+    assert "DP_HEALTH_EVENT_EXTRA_TYPES" not in env(ds)
+    assert "DP_HEALTH_EVENT_EXTRA_TYPES" not in {e["name"] for e in relay(ds)["env"]}
