@@ -31,6 +31,7 @@ from k8s_gpu_sharing_plugin_amd.utils import harness, kubelet
 
 SEEDS = [int(s) for s in os.environ.get("ADP_LIFECYCLE_SEEDS", "1,2,3").split(",")]
 RELAY_SEEDS = [int(s) for s in os.environ.get("ADP_LIFECYCLE_RELAY_SEEDS", "1,2").split(",")]
+CPX_SEEDS = [int(s) for s in os.environ.get("ADP_LIFECYCLE_CPX_SEEDS", "1").split(",")]
 STEPS = int(os.environ.get("ADP_LIFECYCLE_STEPS", "12"))
 
 
@@ -41,16 +42,20 @@ def _count(pid, what):
 
 
 class Life:
-    def __init__(self, scratch, tmp_path, relay=False):
+    def __init__(self, scratch, tmp_path, relay=False, cpx=False):
         self.scratch = scratch
         self.ksock = os.path.join(scratch, "kubelet.sock")
-        self.fx = fixtures.node(2)
+        # cpx: both GPUs in CPX, every partition a device (--partition-strategy single)
+        self.fx = fixtures.node(2, modes="CPX") if cpx else fixtures.node(2)
+        self.per_gpu = 8 if cpx else 1
         self.cfg = str(tmp_path / "config.yaml")
         self.drain = str(tmp_path / "drain")
         self.replicas, self.name, self.drained = 2, "sharedgpu", False
         self.write_config()
         self.k = kubelet.StubKubelet(self.ksock).start()
         args = ["--config-file", self.cfg, "--drain-file", self.drain]
+        if cpx:
+            args += ["--partition-strategy", "single"]
         env = {"DP_HEALTH_POLL_MS": "100"}
         self.relay, self.relays = None, 0
         if relay:
@@ -166,7 +171,7 @@ class Life:
             assert self.d.proc.poll() is None, (self.history, self.d.log()[-4000:])
             return
         want_name = f"amd.com/{self.name}"
-        want = (2 * self.replicas, self.replicas if self.drained else 0)
+        want = (2 * self.per_gpu * self.replicas, self.per_gpu * self.replicas if self.drained else 0)
         deadline = time.monotonic() + timeout
         seen = None
         while True:
@@ -211,12 +216,14 @@ class Life:
         return rc
 
 
-@pytest.mark.parametrize("seed,relay", [(s, False) for s in SEEDS] + [(s, True) for s in RELAY_SEEDS])
-def test_interleaved_restarts_reloads_and_drains_settle(scratch, tmp_path, seed, relay):
+@pytest.mark.parametrize("seed,relay,cpx", [(s, False, False) for s in SEEDS] + [(s, True, False) for s in RELAY_SEEDS]
+                         + [(s, True, True) for s in CPX_SEEDS])
+def test_interleaved_restarts_reloads_and_drains_settle(scratch, tmp_path, seed, relay, cpx):
     """(relay: the chart's layout, with the relay also stopped or killed and
-    started again, and events required back on through it at every settle)"""
+    started again, and events required back on through it at every settle;
+    cpx: a node of CPX GPUs, every partition a device)"""
     rnd = random.Random(seed)
-    life = Life(scratch, tmp_path, relay=relay)
+    life = Life(scratch, tmp_path, relay=relay, cpx=cpx)
     try:
         life.settle()
         pid = life.d.proc.pid
