@@ -6,6 +6,7 @@ socket re-created), or going away for a few steps; the plugin's own socket
 deleted; a config-file edit (resource renamed and/or replica count changed,
 applied live), or a broken one (ignored: the running config stays, across a
 SIGHUP too); GPU 1 drained or undrained by the operator's drain file; SIGUSR1;
+a GPU reset (every partition's GPU_PRE_RESET, then every GPU_POST_RESET);
 in the chart's layout also the event relay stopped or killed and started
 again (events must be back on through it at every settle).
 After every step (the kubelet's absence aside) the daemon must come back
@@ -53,7 +54,14 @@ class Life:
         self.replicas, self.name, self.drained = 2, "sharedgpu", False
         self.write_config()
         self.k = kubelet.StubKubelet(self.ksock).start()
-        args = ["--config-file", self.cfg, "--drain-file", self.drain]
+        # GPU resets (every partition's GPU_PRE_RESET, then every GPU_POST_RESET)
+        # come through the mock's event FIFO; a POST lost to a restart is a gap
+        # the polled check closes within the short hold. Flap damping off: the
+        # random resets are not a flapping GPU.
+        self.fifo = str(tmp_path / "events")
+        os.mkfifo(self.fifo)
+        args = ["--config-file", self.cfg, "--drain-file", self.drain, "--reset-flap-limit", "0",
+                "--reset-recovery-hold-ms", "500"]
         if cpx:
             args += ["--partition-strategy", "single"]
         env = {"DP_HEALTH_POLL_MS": "100"}
@@ -68,7 +76,8 @@ class Life:
             sim = os.path.join(BUILD_DIR, "libadp_devcgroup_sim.so")
             args += ["--health-event-socket", self.rsock, "--metrics-addr", "127.0.0.1:0"]
             env["LD_PRELOAD"] = " ".join(x for x in (os.environ.get("LD_PRELOAD", ""), sim) if x)
-        self.d = harness.Daemon(scratch, self.fx, args=args, env=env).start()
+        self.d = harness.Daemon(scratch, self.fx, args=args, env=env,
+                                event_fifo=None if relay else self.fifo).start()
         self.reg = None
         self.history = []
         self.kubelet_down = False
@@ -77,7 +86,8 @@ class Life:
         self.relays += 1
         rdir = f"{self.scratch}-relay{self.relays}"
         os.makedirs(rdir, exist_ok=True)
-        self.relay = harness.Daemon(rdir, self.fx, args=["--event-relay", "--health-event-socket", self.rsock]).start()
+        self.relay = harness.Daemon(rdir, self.fx, args=["--event-relay", "--health-event-socket", self.rsock],
+                                    event_fifo=self.fifo).start()
         self.relay.wait_log("relaying amdsmi events on")
 
     def events_on(self):
@@ -97,7 +107,7 @@ class Life:
 
     def step(self, rnd):
         what = rnd.choice(["sighup", "storm", "kubelet", "kubelet-away", "socket", "config", "config", "broken",
-                           "drain", "usr1"] + (["relay-restart", "relay-kill"] if self.relay else []))
+                           "drain", "usr1", "reset", "reset"] + (["relay-restart", "relay-kill"] if self.relay else []))
         if self.kubelet_down and what in ("kubelet", "kubelet-away"):
             what = "kubelet-back"
         if what == "sighup":
@@ -117,6 +127,17 @@ class Life:
             self.reg = None
         elif what == "usr1":
             self.d.signal(signal.SIGUSR1)
+        elif what == "reset":
+            g = rnd.randint(0, 1)
+            parts = range(self.per_gpu)
+            lines = [f"{g}:{p} 3 chaos pre" for p in parts] + [f"{g}:{p} 4 chaos post" for p in parts]
+            try:
+                fd = os.open(self.fifo, os.O_WRONLY | os.O_NONBLOCK)
+                os.write(fd, "".join(ln + "\n" for ln in lines).encode())
+                os.close(fd)
+                what += f" gpu {g}"
+            except OSError:  # no reader right now (a restart): nothing reset
+                what += " (no reader)"
         elif what in ("relay-restart", "relay-kill"):
             if what == "relay-kill":
                 self.relay.proc.kill()
