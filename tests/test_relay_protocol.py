@@ -326,3 +326,26 @@ def test_a_failed_renewal_is_events_off_until_one_succeeds(relay):
     relay.events(1)
     replay, r = relay.subscribe(f"{h['relay']}:2:{r['gen']}")
     assert _seqs(replay) == [3] and r["gap"] == 0, (replay, r)
+
+
+def test_a_renewal_asked_for_under_a_stuck_wait_is_skipped(scratch):
+    """amdsmi cannot be re-initialised under an event wait that does not
+    return: a daemon whose processors differ from the registration, arriving
+    while the watchdog says events are off, gets the current state (events
+    off, the same generation, why) at once instead of a registrar hung behind
+    the wait -- and events come back on when the wait returns."""
+    r = Relay(scratch, env={"ADP_RELAY_STUCK_MS": "300"})
+    try:
+        h = r.hello()
+        r.inject(["hang 2500"])
+        r.d.wait_log("daemons fall back to polling")
+        t0 = time.monotonic()
+        replay, a = r.subscribe(raw="reinit fp=0123456789abcdef since=%s:0:%d" % (h["relay"], h["gen"]))
+        assert time.monotonic() - t0 < 1.5, "the answer waited for the stuck wait"
+        assert a["events"] == "events=off" and a["gen"] == h["gen"] and a["gap"] == 1, a
+        assert "has not returned" in a["reason"], a
+        assert "re-enumeration a daemon asked for skipped: the event wait is stuck" in r.d.log()
+        r.d.wait_log("the amdsmi event wait returned again", timeout=10)
+        assert r.hello()["events"] == "events=ok"
+    finally:
+        r.stop()
