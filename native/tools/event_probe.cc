@@ -68,13 +68,20 @@ int main(int argc, char** argv) {
   std::string lib_path, types = "12,13";
   int wait_ms = 8000, cycles = 0, cycles_ok = 0;
   bool self_hip = false;
+  const char* usage =
+      "usage: amdgpu-dp-event-probe [--lib <libamd_smi.so>] [--types 12,13] [--wait-ms 8000] [--self-hip] "
+      "[--cycles N]\n";
   for (int i = 1; i < argc; ++i) {
+    const bool has_value = i + 1 < argc;
     if (!strcmp(argv[i], "--self-hip")) self_hip = true;
-    else if (i + 1 >= argc) break;
-    else if (!strcmp(argv[i], "--lib")) lib_path = argv[++i];
-    else if (!strcmp(argv[i], "--types")) types = argv[++i];
-    else if (!strcmp(argv[i], "--wait-ms")) wait_ms = atoi(argv[++i]);
-    else if (!strcmp(argv[i], "--cycles")) cycles = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--lib") && has_value) lib_path = argv[++i];
+    else if (!strcmp(argv[i], "--types") && has_value) types = argv[++i];
+    else if (!strcmp(argv[i], "--wait-ms") && has_value) wait_ms = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--cycles") && has_value) cycles = atoi(argv[++i]);
+    else {
+      fputs(usage, strcmp(argv[i], "--help") ? stderr : stdout);
+      return strcmp(argv[i], "--help") ? 2 : 0;
+    }
   }
   auto extra = health::ParseEventTypes(types);
   if (!extra.ok()) {
