@@ -337,7 +337,7 @@ def test_a_renewal_asked_for_under_a_stuck_wait_is_skipped(scratch):
     r = Relay(scratch, env={"ADP_RELAY_STUCK_MS": "300"})
     try:
         h = r.hello()
-        r.inject(["hang 2500"])
+        r.inject(["hang 5000"])
         r.d.wait_log("daemons fall back to polling")
         t0 = time.monotonic()
         replay, a = r.subscribe(raw="reinit fp=0123456789abcdef since=%s:0:%d" % (h["relay"], h["gen"]))
