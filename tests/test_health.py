@@ -366,7 +366,7 @@ def test_a_partition_pci_function_drains_its_gpu(scratch, tmp_path):
             except queue.Empty:
                 pass
         assert bad == 8
-        assert "drained by the operator" in n.d.log()
+        n.d.wait_log("drained by the operator")
     finally:
         n.close()
 
