@@ -374,14 +374,15 @@ std::string RemoveDrainNames(std::string_view line, const std::set<std::string>&
 
 std::set<std::string> DrainNames(const inventory::PhysicalGpu& g) {
   std::set<std::string> n = {g.uuid, g.bdf, std::to_string(g.node_index)};
-  if (size_t dot = g.bdf.rfind('.'); dot != std::string::npos) {
-    n.insert(g.bdf.substr(0, dot));
-    // A partitioned GPU's compute partitions are PCI functions of it
-    // (0000:0c:00.0 .. .7 on a CPX MI355X, as amd-smi lists them): naming one
-    // names the GPU -- a drain holds the whole GPU, as a reset does.
-    for (size_t f = 1; f < g.partitions.size() && f < 8; ++f) n.insert(g.bdf.substr(0, dot) + "." + std::to_string(f));
+  if (size_t dot = g.bdf.rfind('.'); dot != std::string::npos) n.insert(g.bdf.substr(0, dot));
+  // A partitioned GPU's compute partitions have PCI addresses of their own
+  // (functions of the GPU's: 0000:0c:00.0 .. .7 on a CPX MI355X, as amd-smi
+  // lists them): naming one names the GPU -- a drain holds the whole GPU, as a
+  // reset does.
+  for (const auto& p : g.partitions) {
+    n.insert(p.uuid);
+    n.insert(p.bdf);
   }
-  for (const auto& p : g.partitions) n.insert(p.uuid);
   n.erase("");
   return n;
 }

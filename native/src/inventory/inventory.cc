@@ -316,6 +316,7 @@ Result<std::shared_ptr<Snapshot>> GroupProcessors(std::vector<smi::ProcessorInfo
       part.partition_id = p.partition_id;
       part.uuid = (unique || handles.size() == 1) ? p.uuid
                                                    : p.uuid + "-p" + std::to_string(p.partition_id);
+      part.bdf = p.bdf;
       part.render_path = p.render_minor ? RenderPath(p.render_minor) : "";
       if (opt.include_card_nodes && p.card_minor != 0xffffffffu) part.card_path = CardPath(p.card_minor);
       part.numa = p.numa_node;

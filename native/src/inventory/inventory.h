@@ -39,6 +39,7 @@ struct Partition {
   int handle = -1;            // index into Snapshot::procs
   uint32_t partition_id = 0;  // amdsmi kfd current_partition_id
   std::string uuid;           // stable device ID for this partition
+  std::string bdf;            // the partition's PCI address as amdsmi reports it (a function of the GPU's)
   std::string render_path;    // /dev/dri/renderD<N>
   std::string card_path;      // /dev/dri/card<N> ("" if unknown)
   int numa = -1;

@@ -496,6 +496,7 @@ static void TestDrainSyntax() {
   auto n = health::DrainNames(g);
   CHECK((n == std::set<std::string>{"GPU-a", "0000:0c:00.0", "0000:0c:00", "3", "GPU-a-p1"}));
   p.uuid = "GPU-a-p2";
+  p.bdf = "0000:0c:00.1";
   g.partitions.push_back(p);  // two partitions: the second one's PCI function names the GPU too
   n = health::DrainNames(g);
   CHECK((n == std::set<std::string>{"GPU-a", "0000:0c:00.0", "0000:0c:00", "0000:0c:00.1", "3", "GPU-a-p1",
