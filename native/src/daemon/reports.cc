@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <fstream>
+#include <iterator>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -418,9 +419,32 @@ int Doctor(smi::Library* lib, const Validated& v, const Config& cfg, DoctorRepor
                          " -- once repaired, --return-to-service " + s.gpus[gpu].bdf);
     }
   }
-  if (!f.drain_file.empty() && access((f.drain_file + ".return").c_str(), F_OK) == 0)
-    d.Line("warn", "a return-to-service request is waiting in " + f.drain_file + ".return: no running daemon "
-                   "with health checks has taken it");
+  if (!f.drain_file.empty()) {
+    // The drain list: what it takes out of service here, and names that match
+    // no GPU of this node (a typo drains nothing, silently otherwise).
+    std::ifstream in(f.drain_file);
+    std::string text((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+    std::set<std::string> names = health::DrainTokens(text), known;
+    std::vector<std::string> drained;
+    for (const auto& g : s.gpus) {
+      const std::set<std::string> own = health::DrainNames(g);
+      known.insert(own.begin(), own.end());
+      if (std::any_of(own.begin(), own.end(), [&](const std::string& n) { return names.count(n) > 0; }))
+        drained.push_back(g.bdf);
+    }
+    std::vector<std::string> unknown;
+    for (const auto& n : names)
+      if (!known.count(n)) unknown.push_back(n);
+    if (!drained.empty())
+      d.Line("warn", "drained by the operator (" + f.drain_file + "): " + Join(drained, ", ") +
+                         " -- advertised Unhealthy until --undrain");
+    if (!unknown.empty())
+      d.Line("warn", "the drain file " + f.drain_file + " names no GPU of this node as: " + Join(unknown, ", ") +
+                         " -- those entries drain nothing here (PCI address, UUID, partition UUID or node index)");
+    if (access((f.drain_file + ".return").c_str(), F_OK) == 0)
+      d.Line("warn", "a return-to-service request is waiting in " + f.drain_file + ".return: no running daemon "
+                     "with health checks has taken it");
+  }
   double budget = plugin::CpuBudget();
   char b[160];
   snprintf(b, sizeof(b), "CPU budget %.2f CPUs: %d gRPC loop(s) per socket, busy-poll %s", budget,

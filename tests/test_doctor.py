@@ -221,3 +221,19 @@ def test_ecc_unreadable_on_some_gpus_is_a_warning(tmp_path):
     rc, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), fx=_state_fx(tmp_path, **{"gpu1.ecc": "x"}))
     line = _find(lines, "uncorrectable ECC readable on 1 of 2 GPU(s)")
     assert rc == 0 and line and line.startswith("warn") and "not detected on the others" in line, lines
+
+
+def test_drain_file_entries_are_checked_against_the_node(tmp_path):
+    """--drain-file: the doctor names the GPUs the file takes out of service
+    here and the entries that match no GPU of this node (a typo drains
+    nothing); a partition's PCI function counts as its GPU."""
+    fx = fixtures.node(2, modes="CPX")
+    drain = tmp_path / "drain"
+    drain.write_text(f"{fx['gpus'][1]['bdf'][:-1]}5  # a partition of GPU 1\n0000:0c:00.9,GPU-nope  # typos\n")
+    rc, lines = _doctor(tmp_path, "--device-plugin-path", str(tmp_path), "--partition-strategy", "single",
+                        "--drain-file", str(drain), fx=fx)
+    got = _find(lines, "drained by the operator")
+    assert got and got.startswith("warn") and fx["gpus"][1]["bdf"] in got and fx["gpus"][0]["bdf"] not in got, lines
+    bad = _find(lines, "names no GPU of this node")
+    assert bad and bad.startswith("warn") and "0000:0c:00.9, GPU-nope" in bad, lines
+    assert rc == 0, lines
