@@ -268,11 +268,11 @@ class SubscribeModel:
 
 @pytest.mark.parametrize("seed", [int(x) for x in os.environ.get("ADP_RELAY_SEEDS", "1,2,3,4").split(",")])
 def test_random_histories_match_the_subscribe_model(scratch, seed):
-    """Seeded random histories -- events, events the relay loses, daemons
-    reconnecting with cursors of this relay or another, this generation or
-    another, behind, current or from the future -- answered by the real relay
-    exactly as the model of its Subscribe says (the model the health model
-    check's relay follows)."""
+    """Seeded random histories -- events, events the relay loses, renewals
+    (new generations), daemons reconnecting with cursors of this relay or
+    another, this generation or another, behind, current or from the future --
+    answered by the real relay exactly as the model of its Subscribe says (the
+    model the health model check's relay follows)."""
     import random
     rnd = random.Random(seed)
     r = Relay(scratch, env={"ADP_DEBUG_RELAY_REFUSE_EVENT": "refuseme"})
@@ -293,10 +293,19 @@ def test_random_histories_match_the_subscribe_model(scratch, seed):
                 r.inject([f"{rnd.randint(0, 1)} 1 refuseme {step}"])
                 r.d.wait_log("lost after", count=losses)
                 m.lose()
+            elif what < 0.52:
+                # a daemon whose processors differ: the relay renews its
+                # registration -- a new generation, and every subscriber is
+                # told it may have missed events (the replay is still made)
+                seq = rnd.randint(0, m.seq)
+                replay, a = r.subscribe(raw=f"reinit fp=0123456789abcdef since={h['relay']}:{seq}:{m.gen}")
+                want_replay, _ = m.subscribe(h["relay"], seq, m.gen)
+                assert _seqs(replay) == want_replay and a["gap"] == 1 and a["gen"] == m.gen + 1, (step, a)
+                m.gen += 1
             else:
                 rid = h["relay"] if rnd.random() < 0.85 else other
                 seq = rnd.randint(0, m.seq + 2)
-                gen = h["gen"] if rnd.random() < 0.85 else h["gen"] + 1
+                gen = m.gen if rnd.random() < 0.85 else rnd.choice([m.gen - 1, m.gen + 1])
                 replay, a = r.subscribe(f"{rid}:{seq}:{gen}")
                 want = m.subscribe(rid, seq, gen)
                 assert (_seqs(replay), a["gap"]) == want, (step, rid == h["relay"], seq, gen, m.seq, m.lost_seq)
