@@ -394,6 +394,12 @@ def test_relay_keeps_no_descriptor_per_scan(scratch, tmp_path):
         c.close()
     try:
         relay.wait_log("relaying amdsmi events on")
+        # the registrar registers and starts the event waiter after that line:
+        # count once all four threads (loop, registrar, waiter, scan worker) run
+        relay.wait_log("event notification registered on")
+        deadline = time.time() + 5
+        while counts()[1] < 4 and time.time() < deadline:
+            time.sleep(0.02)
         scan(True)
         before = counts()
         for i in range(400):
