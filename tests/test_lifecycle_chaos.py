@@ -247,6 +247,7 @@ def test_interleaved_restarts_reloads_and_drains_settle(scratch, tmp_path, seed,
     life = Life(scratch, tmp_path, relay=relay, cpx=cpx)
     try:
         life.settle()
+        life.d.wait_log("health monitor watching")  # (its thread starts after the registration)
         pid = life.d.proc.pid
         fds0, threads0 = _count(pid, "fds"), _count(pid, "threads")
         for _ in range(STEPS):
