@@ -75,7 +75,10 @@
 // clamped past every threshold), so each distinct state is expanded once per
 // remaining depth: every sequence up to --depth is covered. Each node is
 // rebuilt by replaying its sequence from scratch (deterministic: fake clock,
-// fake library, a relay modelled on relay.cc's Subscribe over a socketpair).
+// fake library, a relay modelled on relay.cc's Subscribe behind a real Unix
+// socket -- the contract tests/test_relay_protocol.py pins on the real relay).
+// --random instead walks N random sequences of L steps (far past the bound),
+// every step checked, each walk probed for liveness at its end.
 #include <fcntl.h>
 #include <poll.h>
 #include <sys/mman.h>
