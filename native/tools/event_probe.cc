@@ -104,11 +104,13 @@ int main(int argc, char** argv) {
   for (const auto& p : *procs) handles.push_back(p.handle);
   std::string gens;
   const int fds_before = OpenFds();
+  int fds_first = fds_before;  // after the first generation (what amdsmi keeps once is no leak)
   for (int c = 0; c < cycles; ++c) {
     Status st = (*lib)->EventsInit(handles, hc.EventMask());
     const size_t live = (*lib)->EventsRegistered();
     (*lib)->EventsStopAll();
     cycles_ok += st.ok() && live == handles.size() && (*lib)->EventsRegistered() == 0;
+    if (c == 0) fds_first = OpenFds();
     gens += std::string(c ? ", " : "") + "{\"init\": \"" + JsonEscape(st.ok() ? "ok" : st.ToString()) +
             "\", \"registered\": " + std::to_string(live) +
             ", \"after_stop\": " + std::to_string((*lib)->EventsRegistered()) + "}";
@@ -199,7 +201,8 @@ int main(int argc, char** argv) {
                     ", \"self_hip\": " + hip + ", \"mask\": " + std::to_string(hc.EventMask()) +
                     ", \"cycles\": [" + gens + "], \"cycle_count\": " + std::to_string(cycles) +
                     ", \"cycles_ok\": " + std::to_string(cycles_ok) + ", \"fds_before_cycles\": " +
-                    std::to_string(fds_before) + ", \"fds_after_cycles\": " + std::to_string(fds_after) +
+                    std::to_string(fds_before) + ", \"fds_after_first_cycle\": " + std::to_string(fds_first) +
+                    ", \"fds_after_cycles\": " + std::to_string(fds_after) +
                     ", \"registration\": \"" +
                     JsonEscape(reg.ok() ? "ok" : reg.ToString()) + "\", \"processors\": [";
   for (size_t i = 0; i < procs->size(); ++i) {

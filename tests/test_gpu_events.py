@@ -133,8 +133,8 @@ def test_real_amdsmi_registration_generations_leak_nothing(real_snap):
     """200 generations of what every SIGHUP does to an in-process monitor's
     registration (EventsInit on every processor, EventsStopAll) on the real
     libamd_smi, in one process: every one ok, and the process holds no more
-    descriptors after them than before -- a registration amdsmi kept would keep
-    its KFD event file open."""
+    descriptors after them than after the first -- a registration amdsmi kept
+    would keep its KFD event file open."""
     r = subprocess.run([EVENT_PROBE, "--types", TYPES, "--wait-ms", "300", "--cycles", "200"],
                        capture_output=True, text=True, timeout=300)
     lines = r.stdout.strip().splitlines()
@@ -143,7 +143,9 @@ def test_real_amdsmi_registration_generations_leak_nothing(real_snap):
     _record("raw_events_200_generations.json", rec)
     assert rec["rc"] == 0 and rec["cycle_count"] == 200, rec
     assert rec["cycles_ok"] == 200, rec
-    assert rec["fds_after_cycles"] <= rec["fds_before_cycles"], rec
+    # (whatever amdsmi opens once, at the first registration, is not a leak:
+    # measured from there -- round 6's box: 3 before, 3 after the first, 3 after all)
+    assert rec["fds_after_cycles"] <= rec["fds_after_first_cycle"], rec
     assert rec["registration"] == "ok", rec
 
 
