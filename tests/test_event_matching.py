@@ -306,7 +306,7 @@ def test_event_probe_cycles_register_and_stop_everything(scratch, tmp_path, fail
             assert c["init"] == "ok" and c["registered"] == 2, rec
     assert (rec["registration"] == "ok") == (not fail_on), rec
     assert rec["cycle_count"] == 3 and rec["cycles_ok"] == (0 if fail_on else 3), rec
-    assert rec["fds_after_cycles"] == rec["fds_before_cycles"], rec
+    assert rec["fds_after_cycles"] == rec["fds_after_first_cycle"] == rec["fds_before_cycles"], rec
     s = _evt(evt)
     assert s["live"] == 0 and s["double_init"] == 0 and s["leaked_at_shutdown"] == 0, s
 
