@@ -58,6 +58,7 @@ asan:
 	ASAN_OPTIONS=detect_leaks=1 build/asan/adp_unit_tests
 	build/asan/adp_stress
 	ASAN_OPTIONS=detect_leaks=1 build/asan/adp_health_model --depth 4
+	ASAN_OPTIONS=detect_leaks=1 build/asan/adp_health_model --extended --depth 3
 	LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $(CURDIR)/build/asan/libadp_memcap.so" ASAN_OPTIONS=detect_leaks=0 \
 	  AMD_GPU_MEMORY_LIMIT_MIB=100,50 ADP_MEMCAP_KEY=make-asan-$$$$ build/asan/adp_memcap_check
 	LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $(CURDIR)/build/asan/libadp_memcap.so" ASAN_OPTIONS=detect_leaks=0 \
