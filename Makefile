@@ -92,7 +92,7 @@ tsan-e2e:
 	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py tests/test_preferred.py \
 	  tests/test_event_relay.py tests/test_policy_units.py tests/test_hip_order.py tests/test_kfd_topology.py tests/test_chart_layout.py \
 	  tests/test_memory_unit_guards.py tests/test_parity_contract.py tests/test_metrics_exposition.py tests/test_gpu_recovery.py \
-	  tests/test_event_matching.py tests/test_relay_protocol.py tests/test_lifecycle_chaos.py \
+	  tests/test_event_matching.py tests/test_relay_protocol.py tests/test_lifecycle_chaos.py tests/test_relay_client.py \
 	  -k "not additional_ids and not classification and not bruteforce and not snapshot_reports and not scan_reads_only and not another_namespace and not without_client_id and not partitions_read and not parser_edge and not hosted and not event_types_parse"
 	@if ls build/tsan-logs/* >/dev/null 2>&1; then cat build/tsan-logs/*; exit 1; fi
 
@@ -127,7 +127,7 @@ asan-e2e:
 	  tests/test_health_persistence.py tests/test_h2_grpcgo.py tests/test_config.py tests/test_partition_shapes.py tests/test_driver_hbm.py tests/test_preferred.py \
 	  tests/test_event_relay.py tests/test_policy_units.py tests/test_hip_order.py tests/test_kfd_topology.py tests/test_chart_layout.py \
 	  tests/test_memory_unit_guards.py tests/test_parity_contract.py tests/test_metrics_exposition.py tests/test_gpu_recovery.py \
-	  tests/test_event_matching.py tests/test_relay_protocol.py tests/test_lifecycle_chaos.py \
+	  tests/test_event_matching.py tests/test_relay_protocol.py tests/test_lifecycle_chaos.py tests/test_relay_client.py \
 	  -k "not additional_ids and not classification and not bruteforce and not snapshot_reports and not scan_reads_only and not another_namespace and not without_client_id and not partitions_read and not parser_edge and not hosted and not event_types_parse"
 	@if ls build/asan-logs/* >/dev/null 2>&1; then cat build/asan-logs/*; exit 1; fi
 
