@@ -358,3 +358,32 @@ def test_a_renewal_asked_for_under_a_stuck_wait_is_skipped(scratch):
         assert r.hello()["events"] == "events=ok"
     finally:
         r.stop()
+
+
+def test_a_daemon_that_stops_reading_is_dropped_not_waited_for(relay):
+    """A subscriber whose socket buffer fills (it stopped reading) is dropped
+    -- never waited for: the relay keeps numbering and serving others, and
+    what the dropped one missed is in the ring for its reconnection."""
+    h = relay.hello()
+    s, f = relay.connect()
+    fp = HELLO.fullmatch(f.readline().rstrip("\n")).group(7)
+    s.sendall(f"reinit fp={fp}\n".encode())
+    while not f.readline().startswith("hello v1 reinit"):
+        pass
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)  # (and now it reads nothing)
+    relay.events(3000, prefix="y" * 50)  # ~330 KB of lines: far past what its socket holds
+    assert relay.hello()["seq"] == 3000  # the relay went on
+    # the stalled subscriber was cut: reading what was buffered ends in EOF
+    s.settimeout(10)
+    got = b""
+    while True:
+        chunk = s.recv(1 << 16)
+        if not chunk:
+            break
+        got += chunk
+    assert got.count(b"\n") < 3000, len(got)
+    # reconnecting from where it got to, it is replayed what the ring holds
+    last = max([int(m) for m in re.findall(rb"event seq=(\d+)", got)] or [0])
+    replay, a = relay.subscribe(f"{h['relay']}:{last}:{h['gen']}")
+    assert _seqs(replay) == list(range(max(last, 3000 - RING) + 1, 3001)), (last, len(replay))
+    assert a["gap"] == (0 if last >= 3000 - RING else 1), (last, a)
