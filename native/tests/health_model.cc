@@ -76,7 +76,8 @@
 // remaining depth: every sequence up to --depth is covered. Each node is
 // rebuilt by replaying its sequence from scratch (deterministic: fake clock,
 // fake library, a relay modelled on relay.cc's Subscribe behind a real Unix
-// socket -- the contract tests/test_relay_protocol.py pins on the real relay).
+// socket, its ring 3 events long so that replays overflow within the bound --
+// the contract tests/test_relay_protocol.py pins on the real relay).
 // --random instead walks N random sequences of L steps (far past the bound),
 // every step checked, each walk probed for liveness at its end.
 #include <fcntl.h>
@@ -330,6 +331,10 @@ void WriteFile(const std::string& path, const std::string& body) {
 // The relay as relay.cc serves a daemon: numbered events held in its ring,
 // the connect hello, the replay and the reinit hello of Subscribe, and the
 // loss report of OnDropped.
+// The relay keeps the last kRelayRingSize (1,024) events for replays; the model
+// keeps 3, so that sequences within the depth bound overflow it too.
+constexpr size_t kModelRing = 3;
+
 struct RelayModel {
   int instance = 1;
   uint64_t gen = 1, seq = 0;
@@ -728,7 +733,9 @@ class World {
     }
     int gap = 1;
     if (rq.has_since && rq.since_relay == relay_.Id() && rq.since_seq <= relay_.seq) {
-      bool held = true;
+      // relay.cc Subscribe: the cursor's next event still held, and none lost after it
+      bool held = rq.since_seq == relay_.seq ||
+                  (!relay_.ring.empty() && relay_.ring.front().first <= rq.since_seq + 1);
       if (relay_.lost && rq.since_seq <= relay_.lost_seq) held = false;
       std::string replay;
       for (const auto& [q, l] : relay_.ring)
@@ -757,6 +764,7 @@ class World {
     std::string line = "event seq=" + std::to_string(seq) + " " + where + " part=" + std::to_string(part) +
                        " type=" + std::to_string(type) + " fake\n";
     relay_.ring.emplace_back(seq, line);
+    if (relay_.ring.size() > kModelRing) relay_.ring.erase(relay_.ring.begin());
     if (relay_.fd >= 0) {
       sent_.push_back({relay_.Id() + ":" + std::to_string(seq), type, gpu});
       relay_.Send(line);
