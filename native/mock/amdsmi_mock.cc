@@ -764,15 +764,17 @@ amdsmi_status_t amdsmi_get_gpu_event_notification(int timeout_ms, uint32_t* num,
     *num = 0;
     return AMDSMI_STATUS_NO_DATA;
   }
+  bool queued = false;  // lines read before and not yet handed out: return at once, as the library does
   {
     std::lock_guard<std::mutex> lk(g_mu);
     if (g && g->fail_waits > 0) {
       --g->fail_waits;
       return AMDSMI_STATUS_API_FAILED;
     }
+    queued = g && g->fifo_buf.find('\n') != std::string::npos;
   }
   pollfd pfd{fd, POLLIN, 0};
-  int r = poll(&pfd, 1, timeout_ms);
+  int r = poll(&pfd, 1, queued ? 0 : timeout_ms);
   std::unique_lock<std::mutex> lk(g_mu);
   if (!g) return AMDSMI_STATUS_INIT_ERROR;
   int hang_ms = 0;

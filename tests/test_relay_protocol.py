@@ -65,12 +65,13 @@ class Relay:
         """n events (GPU 0 / GPU 1 alternating, a VM fault: no verdict anywhere),
         in chunks the relay's pipes keep up with; waits until all are numbered."""
         seq0, log0 = self.hello()["seq"], len(self.d.log())
-        for i in range(0, n, 100):
-            self.inject([f"{(i + j) % 2} 1 {prefix}{i + j}" for j in range(min(100, n - i))])
+        chunk = 200  # (~22 KB of lines: well inside the relay's 64 KiB event pipe)
+        for i in range(0, n, chunk):
+            self.inject([f"{(i + j) % 2} 1 {prefix}{i + j}" for j in range(min(chunk, n - i))])
             deadline = time.time() + 10
-            while self.hello()["seq"] < seq0 + min(n, i + 100):
+            while self.hello()["seq"] < seq0 + min(n, i + chunk):
                 assert time.time() < deadline, self.d.log()[-3000:]
-                time.sleep(0.02)
+                time.sleep(0.01)
         assert "lost after" not in self.d.log()[log0:]
 
     def connect(self):
