@@ -27,6 +27,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <algorithm>
 #include <cstring>
 #include <map>
 
@@ -65,6 +66,14 @@ constexpr size_t kMaxGrpcMessageHeader = 4096;     // grpc-message is truncated 
 // A peer that keeps sending (PINGs, SETTINGS, requests) without reading our
 // replies is cut off once this much output is queued (ENHANCE_YOUR_CALM).
 constexpr size_t kMaxQueuedOutput = 16u << 20;
+// After a connection error the peer's bytes are read and dropped until it
+// stops sending (then the GOAWAY is written and the connection closed, so it
+// can read why); a peer that keeps sending is cut off after this much
+// (otherwise the loop would read and drop for ever, never seeing EAGAIN).
+constexpr size_t kMaxDiscardAfterError = 64u << 20;
+// Bytes one readiness wake-up reads from a connection before the loop turns to
+// its other connections (epoll is level-triggered: the rest is reported again).
+constexpr size_t kReadBudgetPerWake = 1u << 20;
 // Request bytes buffered over all of a connection's open streams (each stream
 // is also capped at kMaxRequestBytes): beyond it the peer is cut off.
 constexpr size_t kMaxBufferedRequests = 64u << 20;
@@ -200,6 +209,7 @@ class H2Conn final : public ServerConn {
   bool closing_ = false;      // connection error: GOAWAY queued, close after the write
   bool peer_goaway_ = false;  // peer sent GOAWAY: finish open streams, then close
   bool aborted_ = false;      // close now, dropping queued output
+  size_t discarded_ = 0;      // bytes read and dropped since closing_ (bounded: kMaxDiscardAfterError)
   std::string rbuf_;          // incomplete frame carried over to the next read
   std::string wbuf_;
   size_t woff_ = 0;
@@ -255,10 +265,19 @@ bool H2Conn::OnReadable() {
   uint8_t buf[64 * 1024];
   ReadStarted();
   bool eof = false;
-  while (!eof) {
+  size_t budget = kReadBudgetPerWake;
+  while (!eof && !aborted_) {
     ssize_t n = read(fd_, buf, sizeof(buf));
     if (n > 0) {
-      if (closing_) continue;  // draining after a connection error
+      if (closing_) {
+        // Draining after a connection error until the peer stops sending (then
+        // the GOAWAY is written) -- but a peer that keeps sending would keep
+        // this loop here for ever (it never sees EAGAIN): cut off past a bound.
+        discarded_ += static_cast<size_t>(n);
+        if (discarded_ > kMaxDiscardAfterError) aborted_ = true;
+        continue;
+      }
+      budget -= std::min(budget, static_cast<size_t>(n));
       if (rbuf_.empty()) {
         // Common case: whole frames in this read, parsed in place.
         size_t used = Consume(buf, static_cast<size_t>(n));
@@ -268,7 +287,7 @@ bool H2Conn::OnReadable() {
         size_t used = Consume(reinterpret_cast<const uint8_t*>(rbuf_.data()), rbuf_.size());
         rbuf_.erase(0, used);
       }
-      if (static_cast<size_t>(n) < sizeof(buf)) break;
+      if (static_cast<size_t>(n) < sizeof(buf) || (budget == 0 && !closing_)) break;
       continue;
     }
     if (n == 0) {

@@ -224,6 +224,9 @@ bool Nghttp2Conn::Init() {
 bool Nghttp2Conn::OnReadable() {
   char buf[64 * 1024];
   ReadStarted();
+  // At most this much per readiness wake-up, then the loop's other
+  // connections (epoll is level-triggered: the rest is reported again).
+  size_t budget = size_t{1} << 20;
   while (true) {
     ssize_t n = read(fd_, buf, sizeof(buf));
     if (n > 0) {
@@ -232,7 +235,8 @@ bool Nghttp2Conn::OnReadable() {
         LOG_DEBUG(kComp, "nghttp2 recv error: %s", nghttp2_strerror(static_cast<int>(rv)));
         return false;
       }
-      if (static_cast<size_t>(n) < sizeof(buf)) break;
+      budget -= std::min(budget, static_cast<size_t>(n));
+      if (static_cast<size_t>(n) < sizeof(buf) || budget == 0) break;
       continue;
     }
     if (n == 0) return false;  // peer closed

@@ -361,6 +361,37 @@ def test_ping_flood_without_reading_is_cut_off(plugin):
     c2.close()
 
 
+def test_a_peer_that_keeps_sending_after_a_connection_error_is_cut_off(plugin):
+    """After a connection error the daemon drops what the peer sends until it
+    stops, then writes its GOAWAY and closes; a peer that never stops is cut
+    off after 64 MiB. Before the bound, a peer faster than the daemon kept its
+    loop reading and dropping for ever (it never saw EAGAIN) -- a TSan run,
+    where the daemon is the slower side, caught that through the PING-flood
+    test; on a fast machine the daemon usually sees EAGAIN first. Either way
+    the peer is disconnected and the daemon keeps serving others."""
+    d, path, ids = plugin()
+    s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    s.settimeout(20)
+    s.connect(path)
+    s.sendall(PREFACE + frame(SETTINGS, 0, 0) + frame(PING, 0, 1, b"onstream"))  # PING on a stream: error
+    junk = b"\x00" * (1 << 20)
+    sent = 0
+    try:
+        while sent < (256 << 20):
+            s.sendall(junk)
+            sent += len(junk)
+    except (BrokenPipeError, ConnectionResetError):
+        pass
+    s.close()
+    assert sent < (256 << 20), "the peer was never cut off"
+    assert d.proc.poll() is None
+    c2 = Conn(path)
+    c2.send(frame(HEADERS, END_HEADERS, 1, request_block("Allocate")), frame(DATA, END_STREAM, 1, allocate_msg(ids[:1])))
+    blocks, data, _ = c2.call(1)
+    assert ("grpc-status", "0") in blocks[-1][0]
+    c2.close()
+
+
 def test_buffered_request_bytes_are_capped(plugin):
     """Streams that keep sending request bytes without ever ending are cut off at
     64 MiB buffered per connection (GOAWAY ENHANCE_YOUR_CALM)."""
