@@ -381,16 +381,28 @@ void Monitor::RelayWait(int ms) {
   pollfd p[2] = {{relay_fd_, POLLIN, 0}, {wake_fd_, POLLIN, 0}};
   if (poll(p, wake_fd_ >= 0 ? 2 : 1, ms) <= 0 || !(p[0].revents & (POLLIN | POLLHUP | POLLERR))) return;
   char buf[4096];
-  ssize_t n;
-  while ((n = recv(relay_fd_, buf, sizeof(buf), 0)) > 0) relay_buf_.append(buf, static_cast<size_t>(n));
-  bool closed = n == 0 || (n < 0 && errno != EAGAIN && errno != EINTR);
-  size_t nl;
-  while ((nl = relay_buf_.find('\n')) != std::string::npos) {
-    RelayLine l = ParseRelayLine(std::string_view(relay_buf_).substr(0, nl));
-    relay_buf_.erase(0, nl + 1);
-    HandleRelayLine(l);
+  // Lines are handled as they arrive, at most 1 MiB per wake-up: a relay that
+  // kept writing (a bug) can neither hold this thread nor grow the buffer past
+  // one over-long line (64 KiB, then dropped).
+  size_t budget = size_t{1} << 20;
+  bool closed = false;
+  while (budget > 0) {
+    const ssize_t n = recv(relay_fd_, buf, sizeof(buf), 0);
+    if (n < 0 && errno == EINTR) continue;
+    if (n <= 0) {
+      closed = n == 0 || errno != EAGAIN;
+      break;
+    }
+    budget -= std::min(budget, static_cast<size_t>(n));
+    relay_buf_.append(buf, static_cast<size_t>(n));
+    size_t nl;
+    while ((nl = relay_buf_.find('\n')) != std::string::npos) {
+      RelayLine l = ParseRelayLine(std::string_view(relay_buf_).substr(0, nl));
+      relay_buf_.erase(0, nl + 1);
+      HandleRelayLine(l);
+    }
+    if (relay_buf_.size() > 65536) relay_buf_.clear();
   }
-  if (relay_buf_.size() > 65536) relay_buf_.clear();
   if (closed) RelayClose("the event relay closed the connection");
 }
 

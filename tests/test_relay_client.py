@@ -5,7 +5,8 @@ truncated write when it is killed) must not take the plugin down or poison
 its health state. A scripted relay here -- a plain Unix socket server -- greets
 the daemon, answers its reinit, then sends garbage: lines that are not
 protocol, event lines with broken fields, binary bytes, a line longer than the
-daemon's 64 KiB buffer, a connection cut in the middle of a line. The daemon
+daemon's 64 KiB buffer, 16 MiB without a newline, a connection cut in the
+middle of a line. The daemon
 keeps serving, ignores what it cannot parse, acts on the valid events after
 it, and reconnects after the cut. (The parser itself is fuzzed: fuzz_relay.)
 """
@@ -70,6 +71,9 @@ def test_a_misbehaving_relay_does_not_take_the_daemon_down(scratch, tmp_path):
                          b"event seq=2 node=99999999999 bdf=- part=0 type=3\n",
                          b"\x00\xff\xfe binary \x01\n", b"hello\n", b"x" * 70000 + b"\n"):
                 c.sendall(junk)
+            for _ in range(16):  # 16 MiB without a newline: the daemon's buffer stays bounded
+                c.sendall(b"y" * (1 << 20))
+            c.sendall(b"\n")
             # then a valid reset of GPU 0, and the connection cut mid-line
             c.sendall(f"event seq=3 node=2 bdf={bdf0} part=0 type=3 a real reset\n".encode())
             time.sleep(0.5)
