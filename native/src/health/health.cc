@@ -789,13 +789,20 @@ void Monitor::HandleEvent(const smi::Event& e, const std::string& unplaced, cons
     return;
   }
   const std::string& bdf = snap_->gpus[gpu].bdf;
-  // KFD's informational events come with every HIP process: not worth a line each.
-  if (e.type > smi::kEvtGpuPostReset && verdict == 0)
+  // KFD's informational events come with every HIP process: not worth a line
+  // each. Ignored ones (a workload's VM faults, throttling) can come in storms:
+  // the first ten of each type, then every thousandth (all are counted).
+  if (e.type > smi::kEvtGpuPostReset && verdict == 0) {
     LOG_DEBUG(kComp, "event %s(%u) on GPU %d (%s): %s (counted)", name.c_str(), e.type, gpu, bdf.c_str(),
               e.message.c_str());
-  else
-    LOG_INFO(kComp, "event %s(%u) on GPU %d (%s): %s%s", name.c_str(), e.type, gpu, bdf.c_str(), e.message.c_str(),
-             verdict == 0 ? " (ignored)" : "");
+  } else if (verdict == 0) {
+    const uint64_t n = ++ignored_seen_[e.type];
+    if (n <= 10 || n % 1000 == 0)
+      LOG_INFO(kComp, "event %s(%u) on GPU %d (%s): %s (ignored; %llu of this type so far)", name.c_str(), e.type,
+               gpu, bdf.c_str(), e.message.c_str(), static_cast<unsigned long long>(n));
+  } else {
+    LOG_INFO(kComp, "event %s(%u) on GPU %d (%s): %s", name.c_str(), e.type, gpu, bdf.c_str(), e.message.c_str());
+  }
   counters_->CountEvent(bdf, name);
   if (verdict == 0) return;
   std::string why = name + ": " + e.message;

@@ -446,6 +446,7 @@ class Monitor {
   // a GPU_PRE_RESET holds every GPU (reference nvidia.go:244-251).
   void HandleUnmatched(const smi::Event& e, int verdict, const std::string& why);
   uint64_t unmatched_seen_ = 0;  // log rate limit
+  std::map<uint32_t, uint64_t> ignored_seen_;  // ignored events per type (log rate limit)
   const Clock* clock_ = Clock::System();
   int64_t SteadyNow() const { return clock_->SteadyMs(); }
   std::thread thread_;

@@ -601,7 +601,12 @@ class RelayServer {
       out += line;
     }
     if (out.empty()) return;
-    LOG_INFO(kComp, "%s", OneLine(out).c_str());
+    // Every reset line is logged; other events (a workload's VM-fault storm,
+    // KFD's per-process events) the first hundred batches, then every
+    // thousandth -- the daemons count each.
+    const bool resets = out.find(" type=3 ") != std::string::npos || out.find(" type=4 ") != std::string::npos;
+    if (resets || ++batches_logged_ <= 100 || batches_logged_ % 1000 == 0)
+      LOG_INFO(kComp, "%s", OneLine(out).c_str());
 #ifdef ADP_TEST_HOOKS
     if (!drop_on_.empty() && out.find(drop_on_) != std::string::npos) {
       // Tests: what a daemon whose socket buffer is full sees -- dropped,
@@ -766,6 +771,7 @@ class RelayServer {
   bool stuck_ = false;
   std::string stuck_reason_;
   std::string pending_, done_pending_;  // bytes read from the pipes, up to the last full line
+  uint64_t batches_logged_ = 0;          // event batches without a reset (log rate limit)
 };
 
 }  // namespace

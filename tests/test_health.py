@@ -118,10 +118,36 @@ def test_application_events_are_ignored(node):
     n.inject("1 1 vm fault")
     n.inject("1 2 thermal")
     deadline = time.monotonic() + 5
-    while n.d.log().count("(ignored)") < 2 and time.monotonic() < deadline:
+    while n.d.log().count("(ignored; ") < 2 and time.monotonic() < deadline:
         time.sleep(0.05)
-    assert n.d.log().count("(ignored)") >= 2
+    assert n.d.log().count("(ignored; ") >= 2
     time.sleep(0.3)
+    assert n.q.empty()
+
+
+def test_a_storm_of_ignored_events_is_counted_not_logged_line_by_line(node):
+    """A workload that faults in a loop sends VM faults by the thousand: each is
+    counted (amdgpu_dp_gpu_events_total), the log gets the first ten and then
+    every thousandth, and health does not change."""
+    n = node(args=["--metrics-addr", "127.0.0.1:0"])
+    import re
+    from test_metrics import _get, _parse
+    port = int(re.search(r"on port (\d+)", n.d.wait_log("serving /metrics")).group(1))
+    for i in range(0, 2500, 250):
+        n.inject("".join(f"1 1 vm fault {i + j}\n" for j in range(250)).rstrip("\n"))
+    deadline = time.monotonic() + 15
+    total = 0
+    while time.monotonic() < deadline:
+        m = _parse(_get(port, "/metrics")[1])
+        total = sum(v for (name, ls), v in m.items()
+                    if name == "amdgpu_dp_gpu_events_total" and dict(ls).get("type") == "VMFAULT")
+        if total >= 2500:
+            break
+        time.sleep(0.1)
+    assert total == 2500, total
+    lines = [ln for ln in n.d.log().splitlines() if "VMFAULT(1)" in ln]
+    assert len(lines) == 12, len(lines)  # 1..10, 1000th, 2000th
+    assert "(ignored; 2000 of this type so far)" in lines[-1]
     assert n.q.empty()
 
 

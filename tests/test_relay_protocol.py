@@ -207,6 +207,11 @@ def test_ring_overflow_fence_post(relay):
         replay, r = relay.subscribe(f"{h['relay']}:{since}:{h['gen']}")
         want = list(range(max(since, first_held - 1) + 1, n + 1))
         assert _seqs(replay) == want and r["gap"] == gap, (since, len(replay), r)
+    # its log: the first hundred event batches, then every thousandth -- every reset line
+    logged = [ln for ln in relay.d.log().splitlines() if "I event-relay: event seq=" in ln]
+    assert len(logged) <= 101, len(logged)
+    relay.inject(["0 3 a reset"])
+    assert " type=3 a reset" in relay.d.wait_log(" type=3 a reset")
 
 
 def test_an_event_the_relay_lost_is_a_gap_for_every_cursor_before_it(scratch):
