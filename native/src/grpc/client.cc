@@ -10,6 +10,7 @@
 #include <sys/un.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <deque>
@@ -29,6 +30,8 @@ struct Channel::CallState {
   std::string req;  // framed request
   size_t req_off = 0;
   bool bad_frame = false;
+  bool too_large = false;  // a message, or the call's buffered messages, over kMaxRecvBytes
+  size_t buffered = 0;     // bytes held in msgs
 };
 
 namespace {
@@ -42,6 +45,14 @@ nghttp2_nv Nv(const char* n, const char* v) {
   nv.flags = NGHTTP2_NV_FLAG_NONE;
   return nv;
 }
+
+// What one call may hold of its peer's messages: the kubelet's own PodResources
+// client allows 16 MiB (podresources.DefaultMaxMsgSize); grpc-go's default is
+// 4 MiB. A peer that sends more fails the call instead of growing the daemon.
+constexpr size_t kMaxRecvBytes = 16u << 20;
+// What Pump() reads per call before it returns, so WaitFor() sees its deadline
+// even while a peer keeps the socket full.
+constexpr size_t kReadBudgetPerPump = 1u << 20;
 
 int64_t NowMs() {
   return std::chrono::duration_cast<std::chrono::milliseconds>(
@@ -69,21 +80,33 @@ struct ChannelCallbacks {
     else if (n == "grpc-message") c->grpc_message = PercentDecode(v);
     return 0;
   }
-  static int OnData(nghttp2_session*, uint8_t, int32_t sid, const uint8_t* data, size_t len,
+  static int OnData(nghttp2_session* s, uint8_t, int32_t sid, const uint8_t* data, size_t len,
                     void* ud) {
     auto* ch = static_cast<Channel*>(ud);
     // grpc-go's bdpEstimator.add(): the first DATA after the last ping's ACK
     // starts a new sample (written by SendBdpPing()).
     if (ch->grpc_go_ && !ch->bdp_outstanding_) ch->bdp_due_ = true;
     Channel::CallState* c = Find(ch, sid);
-    if (!c) return 0;
+    if (!c || c->too_large) return 0;
     c->buf.append(reinterpret_cast<const char*>(data), len);
     while (c->buf.size() >= 5) {
       const auto* b = reinterpret_cast<const uint8_t*>(c->buf.data());
       if (b[0] != 0) { c->bad_frame = true; c->buf.clear(); break; }
       uint32_t n = (uint32_t(b[1]) << 24) | (uint32_t(b[2]) << 16) | (uint32_t(b[3]) << 8) | b[4];
+      if (c->buffered + n > kMaxRecvBytes) {
+        // Hold nothing more of this call and cancel it: the caller gets an
+        // error, never a partial answer.
+        c->too_large = true;
+        c->closed = true;
+        c->buf.clear();
+        c->buf.shrink_to_fit();
+        c->msgs.clear();
+        nghttp2_submit_rst_stream(s, NGHTTP2_FLAG_NONE, sid, NGHTTP2_CANCEL);
+        break;
+      }
       if (c->buf.size() < 5 + static_cast<size_t>(n)) break;
       c->msgs.emplace_back(c->buf.substr(5, n));
+      c->buffered += n;
       c->buf.erase(0, 5 + static_cast<size_t>(n));
     }
     return 0;
@@ -217,13 +240,14 @@ Status Channel::Pump(int timeout_ms) {
   if (r < 0 && errno != EINTR) { dead_ = true; return Unavailable("poll failed"); }
   if (r <= 0) return Status::Ok();
   char buf[64 * 1024];
-  while (true) {
+  for (size_t budget = kReadBudgetPerPump; budget > 0;) {
     ssize_t n = read(fd_, buf, sizeof(buf));
     if (n > 0) {
       ssize_t rv = nghttp2_session_mem_recv(static_cast<nghttp2_session*>(session_),
                                             reinterpret_cast<uint8_t*>(buf), n);
       if (rv < 0) { dead_ = true; return Internal(nghttp2_strerror(static_cast<int>(rv))); }
       if (static_cast<size_t>(n) < sizeof(buf)) break;
+      budget -= std::min(budget, static_cast<size_t>(n));
       continue;
     }
     if (n == 0) { dead_ = true; break; }
@@ -295,6 +319,7 @@ Status Channel::Unary(const std::string& path, std::string_view request, std::st
     }
     return st;
   }
+  if (c->too_large) return Internal("response larger than " + std::to_string(kMaxRecvBytes) + " bytes");
   if (c->http_status != 200)
     return Unavailable("HTTP status " + std::to_string(c->http_status));
   if (c->grpc_status < 0) return Internal("missing grpc-status (stream reset code " +
@@ -319,9 +344,11 @@ Status Channel::Recv(int32_t stream_id, std::string* message, int timeout_ms) {
   if (!c->msgs.empty()) {
     *message = std::move(c->msgs.front());
     c->msgs.pop_front();
+    c->buffered -= message->size();
     return Status::Ok();
   }
-  Status end = (c->grpc_status == 0) ? NotFound("end of stream")
+  Status end = c->too_large ? Internal("stream message larger than " + std::to_string(kMaxRecvBytes) + " bytes")
+               : (c->grpc_status == 0) ? NotFound("end of stream")
                : (c->grpc_status > 0) ? Status(FromGrpcCode(c->grpc_status), c->grpc_message)
                                       : Unavailable("stream reset");
   calls_.erase(it);

@@ -255,6 +255,41 @@ class PodResourcesStub:
         self.server.stop(0)
 
 
+
+def test_pod_resources_answer_over_the_bound_fails_the_call(scratch):
+    """A PodResources answer past 16 MiB (the kubelet's own client's bound) is
+    not held: the call fails, the scrape still answers, and the next good
+    answer is used. (native/src/grpc/client.cc kMaxRecvBytes.)"""
+    pr_sock = os.path.join(scratch + ".fixture", "pod-resources.sock")
+    os.makedirs(os.path.dirname(pr_sock), exist_ok=True)
+    pr = PodResourcesStub(pr_sock)
+    k = kubelet.StubKubelet(os.path.join(scratch, "kubelet.sock")).start()
+    d = harness.Daemon(scratch, fixtures.node(2), args=[
+        "--metrics-addr", "127.0.0.1:0", "--resource-config", "gpu:sharedgpu:4",
+        "--pod-resources-socket", pr_sock]).start()
+    try:
+        port = int(re.search(r"on port (\d+)", d.wait_log("serving /metrics")).group(1))
+        reg = k.wait_registration()
+        c = kubelet.PluginClient(os.path.join(scratch, reg.endpoint))
+        ids = [x.ID for x in c.watch()[0].get(timeout=5).devices]
+        c.close()
+        pr.payload = _list_response([("ml", "huge", "main", "amd.com/sharedgpu", [ids[0], "x" * (17 << 20)])])
+        t0 = time.time()
+        s = _parse(_get(port, "/metrics")[1])
+        assert time.time() - t0 < 1.9
+        assert _value(s, "amdgpu_dp_pod_resources_up") == 0
+        assert pr.calls == 1
+        pr.payload = _list_response([("ml", "train-a", "main", "amd.com/sharedgpu", [ids[0]])])
+        s = _parse(_get(port, "/metrics")[1])
+        assert _value(s, "amdgpu_dp_pod_resources_up") == 1
+        assert _value(s, "amdgpu_dp_container_device_ids", device=ids[0].split("-replica-")[0], namespace="ml",
+                      pod="train-a") == 1
+        assert d.proc.poll() is None
+    finally:
+        pr.stop()
+        d.stop()
+        k.stop()
+
 def test_pod_resources_sharing_metrics(scratch):
     pr_sock = os.path.join(scratch + ".fixture", "pod-resources.sock")
     os.makedirs(os.path.dirname(pr_sock), exist_ok=True)
