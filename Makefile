@@ -102,14 +102,14 @@ tsan-e2e:
 # protobuf codec, the config front end, grant accounting files + /metrics, the
 # driver-side /proc scan (native/fuzz/). FUZZ_SECONDS per target, in parallel;
 # corpora grow in build/fuzz/corpus/<target>; a crash leaves build/fuzz/crash-*.
-FUZZ_TARGETS ?= plugin h2 h2_diff proto config grantfile procscan relay
+FUZZ_TARGETS ?= plugin h2 h2_diff h2_client proto config grantfile procscan relay
 FUZZ_SECONDS ?= 60
 CLANGXX      ?= /opt/rocm/lib/llvm/bin/clang++
 fuzz:
 	cmake -S native -B build/fuzz -G Ninja -DCMAKE_BUILD_TYPE=RelWithDebInfo -DADP_FUZZ=ON \
 	  -DCMAKE_CXX_COMPILER=$(CLANGXX) -DCMAKE_C_COMPILER=$(dir $(CLANGXX))clang >/dev/null
 	ninja -C build/fuzz -j$(JOBS) $(addprefix fuzz_,$(FUZZ_TARGETS))
-	$(PY) tools/gen_fuzz_seeds.py build/fuzz/corpus/h2 build/fuzz/corpus/h2_diff
+	$(PY) tools/gen_fuzz_seeds.py build/fuzz/corpus/h2 build/fuzz/corpus/h2_diff build/fuzz/corpus/h2_client
 	cd build/fuzz && rm -f fuzz_*.failed && for t in $(FUZZ_TARGETS); do mkdir -p corpus/$$t; \
 	  ( ./fuzz_$$t -max_total_time=$(FUZZ_SECONDS) -rss_limit_mb=2048 -print_final_stats=1 corpus/$$t \
 	    > fuzz_$$t.log 2>&1 || echo "fuzz_$$t FAILED (build/fuzz/fuzz_$$t.log)" > fuzz_$$t.failed ) & done; wait; \

@@ -178,7 +178,17 @@ Result<std::unique_ptr<Channel>> Channel::Dial(const std::string& uds_path, int 
       return Unavailable("connect " + uds_path + ": " + strerror(err));
     usleep(20 * 1000);
   }
+  return Start(std::move(ch), deadline, uds_path);
+}
 
+Result<std::unique_ptr<Channel>> Channel::FromFd(int fd, int timeout_ms) {
+  std::unique_ptr<Channel> ch(new Channel());
+  ch->fd_ = fd;
+  return Start(std::move(ch), NowMs() + timeout_ms, "fd " + std::to_string(fd));
+}
+
+Result<std::unique_ptr<Channel>> Channel::Start(std::unique_ptr<Channel> ch, int64_t deadline,
+                                                const std::string& peer) {
   nghttp2_session_callbacks* cbs;
   nghttp2_session_callbacks_new(&cbs);
   nghttp2_session_callbacks_set_on_header_callback(cbs, ChannelCallbacks::OnHeader);
@@ -200,7 +210,7 @@ Result<std::unique_ptr<Channel>> Channel::Dial(const std::string& uds_path, int 
   Channel* raw = ch.get();
   Status st = ch->WaitFor([raw] { return raw->got_settings_; },
                           std::max<int>(1, static_cast<int>(deadline - NowMs())));
-  if (!st.ok()) return Unavailable("HTTP/2 handshake with " + uds_path + ": " + st.message());
+  if (!st.ok()) return Unavailable("HTTP/2 handshake with " + peer + ": " + st.message());
   return ch;
 }
 
@@ -223,8 +233,14 @@ Status Channel::Flush() {
     if (w > 0) { off += static_cast<size_t>(w); continue; }
     if (w < 0 && errno == EINTR) continue;
     if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+      // A peer that takes nothing for a second is not reading at all: give up
+      // rather than hold the caller's thread for ever (no deadline reaches
+      // this loop).
       pollfd p{fd_, POLLOUT, 0};
-      poll(&p, 1, 1000);
+      if (poll(&p, 1, 1000) == 0) {
+        dead_ = true;
+        return Unavailable("peer took no bytes for 1 s");
+      }
       continue;
     }
     dead_ = true;

@@ -203,6 +203,9 @@ class Channel {
  public:
   ~Channel();
   static Result<std::unique_ptr<Channel>> Dial(const std::string& uds_path, int timeout_ms);
+  // Takes over a connected socket (non-blocking; closed with the channel) and
+  // runs the HTTP/2 handshake on it. For tests and fuzzing.
+  static Result<std::unique_ptr<Channel>> FromFd(int fd, int timeout_ms);
 
   Status Unary(const std::string& path, std::string_view request, std::string* response,
                int timeout_ms);
@@ -229,6 +232,8 @@ class Channel {
  private:
   struct CallState;
   Channel() = default;
+  static Result<std::unique_ptr<Channel>> Start(std::unique_ptr<Channel> ch, int64_t deadline_ms,
+                                                const std::string& peer);
   Status Flush();
   Status WaitFor(const std::function<bool()>& done, int timeout_ms);
   Result<int32_t> Submit(const std::string& path, std::string_view request);

@@ -15,7 +15,7 @@ import pytest
 from k8s_gpu_sharing_plugin_amd import REPO_ROOT
 
 CLANG = "/opt/rocm/lib/llvm/bin/clang++"
-TARGETS = ["plugin", "h2", "h2_diff", "proto", "config", "grantfile", "procscan", "relay"]
+TARGETS = ["plugin", "h2", "h2_diff", "h2_client", "proto", "config", "grantfile", "procscan", "relay"]
 
 
 @pytest.mark.slow

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Seed inputs for native/fuzz/fuzz_h2.cc and fuzz_h2_diff.cc: well-formed gRPC exchanges the
+"""Seed inputs for native/fuzz/fuzz_h2.cc and fuzz_h2_diff.cc (and, for a
+directory named h2_client, native/fuzz/fuzz_h2_client.cc): well-formed gRPC exchanges the
 fuzzer mutates from, so it starts inside the HTTP/2 state machine instead of
 at the frame-header checks. Written to each <dir> given (default
 build/fuzz/corpus/h2).
@@ -57,10 +58,33 @@ def seeds():
     yield "unknown_path", bytes([9]) + frame(HEADERS, END_HEADERS | END_STREAM, 1, request_headers("/t.S/Nope"))
 
 
+def client_seeds():
+    """fuzz_h2_client.cc: byte 0 = mode (even: a unary call, odd: a server
+    stream), then the server's frames after its empty SETTINGS frame."""
+    ok = lit(":status", "200") + lit("content-type", "application/grpc")
+    trailers = lit("grpc-status", "0")
+    yield "unary", (bytes([0]) + frame(SETTINGS, 1, 0) + frame(HEADERS, END_HEADERS, 1, ok) +
+                    frame(DATA, 0, 1, grpc_msg(b"pong")) + frame(HEADERS, END_HEADERS | END_STREAM, 1, trailers))
+    yield "unary_error", (bytes([0]) + frame(HEADERS, END_HEADERS | END_STREAM, 1,
+                                             ok + lit("grpc-status", "3") + lit("grpc-message", "bad%20x")))
+    msg = grpc_msg(b"split across frames")
+    yield "unary_split", (bytes([2]) + frame(HEADERS, END_HEADERS, 1, ok) + frame(DATA, 0, 1, msg[:3]) +
+                          frame(DATA, PADDED, 1, b"\x02" + msg[3:] + b"\x00\x00") +
+                          frame(HEADERS, END_HEADERS | END_STREAM, 1, trailers))
+    yield "unary_too_large", (bytes([0]) + frame(HEADERS, END_HEADERS, 1, ok) +
+                              frame(DATA, 0, 1, b"\x00\x7f\xff\xff\xff" + b"x" * 64))
+    yield "stream", (bytes([1]) + frame(HEADERS, END_HEADERS, 1, ok) +
+                     b"".join(frame(DATA, 0, 1, grpc_msg(b"m%d" % i)) for i in range(4)) +
+                     frame(HEADERS, END_HEADERS | END_STREAM, 1, trailers))
+    yield "stream_ping_goaway", (bytes([1]) + frame(PING, 0, 0, b"\x02" * 8) + frame(HEADERS, END_HEADERS, 1, ok) +
+                                 frame(DATA, 0, 1, grpc_msg(b"one")) + frame(RST, 0, 1, struct.pack(">I", 8)) +
+                                 frame(GOAWAY, 0, 0, struct.pack(">II", 1, 0)))
+
+
 def main():
     for out in sys.argv[1:] or ["build/fuzz/corpus/h2"]:
         os.makedirs(out, exist_ok=True)
-        for name, data in seeds():
+        for name, data in (client_seeds() if os.path.basename(out.rstrip("/")) == "h2_client" else seeds()):
             with open(os.path.join(out, "seed_" + name), "wb") as f:
                 f.write(data)
 
