@@ -151,12 +151,12 @@ def main():
                 hups += 1
                 reg = kub.wait(lambda e: e.get("event") == "register", 30, since=mark)
             if relay and a.relay_restart_every and round_no % a.relay_restart_every == 0:
-                relay_logs.append(relay.log())
                 if relay_restarts % 2:
                     relay.proc.kill()
                     relay.proc.wait(timeout=30)
                 else:
                     relay.stop()
+                relay_logs.append(relay.log())  # after it stopped: every line it wrote
                 relay_restarts += 1
                 os.makedirs(d + f".relay{relay_restarts}", exist_ok=True)
                 relay = start_relay(relay_restarts)
@@ -237,7 +237,10 @@ def main():
         rlog = "".join(relay_logs) + relay.log()
         summary["relay"] = {"exit_code": relay_code, "rss_mib_after_warmup": rw.get("rss_mib"),
                             "restarts": relay_restarts,
+                            "relays": relay_restarts + 1,
                             "registrations": rlog.count("event notification registered on"),
+                            "registration_failures": (rlog.count("event notification unavailable")
+                                                      + rlog.count("events=off reason")),
                             "daemon_connections": rlog.count("daemon connected for events"),
                             "registration_kept": rlog.count("registration kept"),
                             "registration_renewed": rlog.count("re-enumerating"),
@@ -250,7 +253,7 @@ def main():
                             "rss_mib_last": rl.get("rss_mib"), "fds_after_warmup": rw.get("fds"),
                             "fds_last": rl.get("fds"), "threads_after_warmup": rw.get("threads"),
                             "threads_last": rl.get("threads")}
-        if relay_code not in (0, None):
+        if relay_code not in (0, None) or summary["relay"]["registration_failures"]:
             ok = False
         if relay_samples and (rl["rss_mib"] - rw["rss_mib"] > a.max_rss_growth_mib or rl["fds"] > rw["fds"] + 4
                               or rl["threads"] > rw["threads"] + 2):
