@@ -4,7 +4,7 @@ JOBS       ?= 8
 PY         ?= python3
 GPURUN     ?= /usr/local/graft/bin/gpurun
 
-.PHONY: all build probe test test-native test-gpu bench asan tsan tsan-e2e asan-e2e fuzz coverage lint image image-rootfs clean
+.PHONY: all build probe test test-native test-gpu bench asan tsan tsan-e2e asan-e2e fuzz coverage analyze lint image image-rootfs clean
 
 # Containerised targets (reference Makefile:44-74): `make docker-<target>` runs
 # `make <target>` in the development image built from docker/Dockerfile.devel.
@@ -137,6 +137,11 @@ coverage:
 
 # -Wall -Wextra as errors over the whole native tree, Python byte-compilation,
 # and clang-format / pyflakes when the machine has them.
+# Clang static analyzer over native/src, native/mock and native/tools; fails
+# on any warning not judged harmless in tools/analyze.py (KNOWN).
+analyze:
+	$(PY) tools/analyze.py
+
 lint:
 	cmake -S native -B build/lint -G Ninja -DCMAKE_BUILD_TYPE=Release "-DCMAKE_CXX_FLAGS=-Werror -Wshadow" >/dev/null
 	ninja -C build/lint -j$(JOBS)

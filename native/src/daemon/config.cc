@@ -552,7 +552,7 @@ Result<Config> LoadConfig(int argc, const char* const* argv,
       cfg.deprecations.push_back(std::string(alias->env) + " is accepted for compatibility; use " + d.env);
     } else if (*d.file_key && file.count(file_key) && file[file_key].type != 'n') {
       st = AssignFile(d, cfg.flags, file[file_key], file_key, cfg.config_file);
-    } else if (!alias_file.empty() && file.count(alias_file) && file[alias_file].type != 'n') {
+    } else if (alias && !alias_file.empty() && file.count(alias_file) && file[alias_file].type != 'n') {
       st = AssignFile(d, cfg.flags, file[alias_file], alias_file, cfg.config_file);
       cfg.deprecations.push_back(std::string("config key ") + alias->file_key +
                                  " is accepted for compatibility; use " + d.file_key);

@@ -119,6 +119,10 @@ std::vector<GrantFile> ListGrantFiles(const std::string& usage_dir) {
   DIR* d = opendir(usage_dir.c_str());
   if (!d) return out;
   int dfd = dirfd(d);
+  if (dfd < 0) {
+    closedir(d);
+    return out;
+  }
   while (dirent* e = readdir(d)) {
     std::string name = e->d_name;
     if (name.size() != 16 + 7 || name.compare(16, 7, ".memcap") != 0) continue;
@@ -176,10 +180,14 @@ void ReadPids(const std::string& proc_root, const std::vector<std::string>& pids
       }
       continue;
     }
+    int fdd = dirfd(fds);
+    if (fdd < 0) {
+      closedir(fds);
+      continue;
+    }
     ++*present;
     PidHbm ph{atoi(pid.c_str()), {}, false};
     bool kfd = false;
-    int fdd = dirfd(fds);
     while (dirent* f = readdir(fds)) {
       if (!IsPid(f->d_name)) continue;
       ++out->fd_entries;
